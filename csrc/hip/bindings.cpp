@@ -1,0 +1,54 @@
+// pybind11 bindings of the _vodahip extension.  Tensors cross the boundary as raw device
+// pointers + HIP stream handles; shape/dtype/alignment validation happens in the Python
+// wrappers (vodascheduler_amd/ops/*.py) BEFORE anything is launched.
+#include <pybind11/pybind11.h>
+#include <pybind11/stl.h>
+
+#include "common.h"
+#include "ops.h"
+
+namespace py = pybind11;
+using namespace voda;
+
+PYBIND11_MODULE(_vodahip, m) {
+  m.doc() = "vodascheduler_amd CDNA4 (gfx950) kernels + RCCL engine";
+  m.attr("GPU_ARCH") = "gfx950";
+  m.attr("LAYERNORM_MAX_N") = kLayerNormMaxN;
+  m.attr("SOFTMAX_MAX_S") = kSoftmaxMaxS;
+
+  m.def("sgd_step", &sgd_step);
+  m.def("adam_step", &adam_step);
+  m.def("rmsprop_step", &rmsprop_step);
+  m.def("cast_scale", &cast_scale);
+  m.def("multi_tensor_copy", &multi_tensor_copy);
+  m.def("layernorm_fwd", &layernorm_fwd);
+  m.def("layernorm_bwd", &layernorm_bwd);
+  m.def("layernorm_bwd_partial_rows", &layernorm_bwd_partial_rows);
+  m.def("masked_softmax_fwd", &masked_softmax_fwd);
+  m.def("masked_softmax_bwd", &masked_softmax_bwd);
+
+  m.def("rccl_unique_id", [] { return py::bytes(rccl_unique_id()); });
+  m.def("rccl_version", &rccl_version);
+
+  py::class_<RcclComm>(m, "RcclComm")
+      .def(py::init([](py::bytes uid, int nranks, int rank, int device, double timeout_s) {
+             std::string id = uid;
+             py::gil_scoped_release nogil;
+             return new RcclComm(id, nranks, rank, device, timeout_s);
+           }),
+           py::arg("uid"), py::arg("nranks"), py::arg("rank"), py::arg("device") = -1,
+           py::arg("timeout_s") = 300.0)
+      .def("allreduce", &RcclComm::allreduce, py::call_guard<py::gil_scoped_release>())
+      .def("broadcast", &RcclComm::broadcast, py::call_guard<py::gil_scoped_release>())
+      .def("allgather", &RcclComm::allgather, py::call_guard<py::gil_scoped_release>())
+      .def("reduce_scatter", &RcclComm::reduce_scatter, py::call_guard<py::gil_scoped_release>())
+      .def("alltoall", &RcclComm::alltoall, py::call_guard<py::gil_scoped_release>())
+      .def("group_start", &RcclComm::group_start)
+      .def("group_end", &RcclComm::group_end, py::call_guard<py::gil_scoped_release>())
+      .def("async_error", &RcclComm::async_error)
+      .def("abort", &RcclComm::abort, py::call_guard<py::gil_scoped_release>())
+      .def("destroy", &RcclComm::destroy, py::call_guard<py::gil_scoped_release>())
+      .def_property_readonly("rank", &RcclComm::rank)
+      .def_property_readonly("size", &RcclComm::size)
+      .def_property_readonly("alive", &RcclComm::alive);
+}

@@ -1,0 +1,238 @@
+// LayerNorm forward / backward for CDNA4 (gfx950).
+//
+// Workload: the Transformer NMT job's encoder/decoder LayerNorms (reference
+// examples/py/tensorflow2/neural_machine_translation_with_transformer.py:203-204,257-259:
+// 10,240 rows x 256 cols) and BERT-base (rows x 768).  HBM-bound, so:
+//   * one wave64 per row, the row held in registers (N <= 64 lanes x 4 x MAXITER),
+//     8-B (bf16) / 16-B (f32) loads per lane, mean and variance by two register passes
+//     (no Welford, no re-read), butterfly reductions across the 64 lanes;
+//   * backward computes dx in the same register-resident pass and accumulates the
+//     per-column dgamma/dbeta partials in registers across the rows a block visits,
+//     then combines the 4 waves through LDS and writes ONE partial row per block;
+//     a second small kernel sums those partials per column.
+#include "common.h"
+#include "ops.h"
+
+namespace voda {
+
+template <typename WT>
+__device__ __forceinline__ float4 load_w4(const void* w, int64_t c4) {
+  return Vec4<WT>::load(reinterpret_cast<const WT*>(w), c4);
+}
+
+// MAXITER: upper bound on 256-column chunks per row (row held as MAXITER float4 per lane)
+template <typename T, typename WT, int MAXITER>
+__global__ __launch_bounds__(256) void ln_fwd_kernel(const T* __restrict__ x, const void* __restrict__ gamma,
+                                                     const void* __restrict__ beta, T* __restrict__ y,
+                                                     float* __restrict__ mean_out, float* __restrict__ rstd_out,
+                                                     int64_t M, int N, float eps) {
+  const int lane = threadIdx.x & 63;
+  const int64_t row = int64_t(blockIdx.x) * 4 + (threadIdx.x >> 6);
+  if (row >= M) return;
+  const int N4 = N >> 2;
+  const T* xr = x + row * N;
+  float4 v[MAXITER];
+  float s = 0.f;
+#pragma unroll
+  for (int it = 0; it < MAXITER; ++it) {
+    const int c4 = it * 64 + lane;
+    v[it] = c4 < N4 ? Vec4<T>::load(xr, c4) : make_float4(0.f, 0.f, 0.f, 0.f);
+    s += (v[it].x + v[it].y) + (v[it].z + v[it].w);
+  }
+  const float inv_n = 1.f / float(N);
+  const float mu = wave_sum(s) * inv_n;
+  float ss = 0.f;
+#pragma unroll
+  for (int it = 0; it < MAXITER; ++it) {
+    const int c4 = it * 64 + lane;
+    if (c4 < N4) {
+      const float a = v[it].x - mu, b = v[it].y - mu, c = v[it].z - mu, d = v[it].w - mu;
+      ss += (a * a + b * b) + (c * c + d * d);
+    }
+  }
+  const float rs = rsqrtf(wave_sum(ss) * inv_n + eps);
+  T* yr = y + row * N;
+#pragma unroll
+  for (int it = 0; it < MAXITER; ++it) {
+    const int c4 = it * 64 + lane;
+    if (c4 < N4) {
+      float4 g = gamma ? load_w4<WT>(gamma, c4) : make_float4(1.f, 1.f, 1.f, 1.f);
+      float4 b = beta ? load_w4<WT>(beta, c4) : make_float4(0.f, 0.f, 0.f, 0.f);
+      float4 o;
+      o.x = (v[it].x - mu) * rs * g.x + b.x;
+      o.y = (v[it].y - mu) * rs * g.y + b.y;
+      o.z = (v[it].z - mu) * rs * g.z + b.z;
+      o.w = (v[it].w - mu) * rs * g.w + b.w;
+      Vec4<T>::store(yr, c4, o);
+    }
+  }
+  if (lane == 0) {
+    mean_out[row] = mu;
+    rstd_out[row] = rs;
+  }
+}
+
+template <typename T, typename WT, int MAXITER>
+__global__ __launch_bounds__(256) void ln_bwd_kernel(const T* __restrict__ dy, const T* __restrict__ x,
+                                                     const float* __restrict__ mean, const float* __restrict__ rstd,
+                                                     const void* __restrict__ gamma, T* __restrict__ dx,
+                                                     float* __restrict__ part_g, float* __restrict__ part_b,
+                                                     int64_t M, int N) {
+  extern __shared__ __attribute__((aligned(16))) float lds[];  // [4][N]
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  const int N4 = N >> 2;
+  const float inv_n = 1.f / float(N);
+  float4 g[MAXITER], ag[MAXITER], ab[MAXITER];
+#pragma unroll
+  for (int it = 0; it < MAXITER; ++it) {
+    const int c4 = it * 64 + lane;
+    g[it] = (gamma && c4 < N4) ? load_w4<WT>(gamma, c4) : make_float4(1.f, 1.f, 1.f, 1.f);
+    ag[it] = make_float4(0.f, 0.f, 0.f, 0.f);
+    ab[it] = make_float4(0.f, 0.f, 0.f, 0.f);
+  }
+  for (int64_t row = int64_t(blockIdx.x) * 4 + wave; row < M; row += int64_t(gridDim.x) * 4) {
+    const float mu = mean[row], rs = rstd[row];
+    float4 xh[MAXITER], dg[MAXITER];
+    float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+    for (int it = 0; it < MAXITER; ++it) {
+      const int c4 = it * 64 + lane;
+      if (c4 < N4) {
+        float4 xv = Vec4<T>::load(x + row * N, c4);
+        float4 dv = Vec4<T>::load(dy + row * N, c4);
+        xh[it] = make_float4((xv.x - mu) * rs, (xv.y - mu) * rs, (xv.z - mu) * rs, (xv.w - mu) * rs);
+        dg[it] = make_float4(dv.x * g[it].x, dv.y * g[it].y, dv.z * g[it].z, dv.w * g[it].w);
+        ag[it].x += dv.x * xh[it].x; ag[it].y += dv.y * xh[it].y;
+        ag[it].z += dv.z * xh[it].z; ag[it].w += dv.w * xh[it].w;
+        ab[it].x += dv.x; ab[it].y += dv.y; ab[it].z += dv.z; ab[it].w += dv.w;
+        s1 += (dg[it].x * xh[it].x + dg[it].y * xh[it].y) + (dg[it].z * xh[it].z + dg[it].w * xh[it].w);
+        s2 += (dg[it].x + dg[it].y) + (dg[it].z + dg[it].w);
+      } else {
+        xh[it] = make_float4(0.f, 0.f, 0.f, 0.f);
+        dg[it] = xh[it];
+      }
+    }
+    const float c1 = wave_sum(s1) * inv_n;
+    const float c2 = wave_sum(s2) * inv_n;
+#pragma unroll
+    for (int it = 0; it < MAXITER; ++it) {
+      const int c4 = it * 64 + lane;
+      if (c4 < N4) {
+        float4 o;
+        o.x = (dg[it].x - xh[it].x * c1 - c2) * rs;
+        o.y = (dg[it].y - xh[it].y * c1 - c2) * rs;
+        o.z = (dg[it].z - xh[it].z * c1 - c2) * rs;
+        o.w = (dg[it].w - xh[it].w * c1 - c2) * rs;
+        Vec4<T>::store(dx + row * N, c4, o);
+      }
+    }
+  }
+  if (part_g == nullptr) return;  // gamma/beta gradients not requested
+  // combine the 4 waves' column partials through LDS, gamma then beta
+  for (int pass = 0; pass < 2; ++pass) {
+#pragma unroll
+    for (int it = 0; it < MAXITER; ++it) {
+      const int c4 = it * 64 + lane;
+      if (c4 < N4) reinterpret_cast<float4*>(lds + wave * N)[c4] = pass == 0 ? ag[it] : ab[it];
+    }
+    __syncthreads();
+    float* out = (pass == 0 ? part_g : part_b) + int64_t(blockIdx.x) * N;
+    for (int c = threadIdx.x; c < N; c += 256) out[c] = (lds[c] + lds[N + c]) + (lds[2 * N + c] + lds[3 * N + c]);
+    __syncthreads();
+  }
+}
+
+// Column sums of a [rows][N] fp32 partial matrix: out[c] = sum_r part[r][c] (cast to WT).
+template <typename WT>
+__global__ __launch_bounds__(256) void col_sum_kernel(const float* __restrict__ part, WT* __restrict__ out,
+                                                      int rows, int N) {
+  __shared__ float red[4][64];
+  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + tx;
+  float s = 0.f;
+  if (c < N)
+    for (int r = ty; r < rows; r += 4) s += part[int64_t(r) * N + c];
+  red[ty][tx] = s;
+  __syncthreads();
+  if (ty == 0 && c < N) Vec4<WT>::store1(out, c, (red[0][tx] + red[1][tx]) + (red[2][tx] + red[3][tx]));
+}
+
+#define LN_DISPATCH_ITER(N, ...)                                     \
+  [&] {                                                              \
+    const int _it = (N + 255) / 256;                                 \
+    if (_it <= 1) { constexpr int MI = 1; __VA_ARGS__(); }           \
+    else if (_it <= 2) { constexpr int MI = 2; __VA_ARGS__(); }      \
+    else if (_it <= 3) { constexpr int MI = 3; __VA_ARGS__(); }      \
+    else if (_it <= 4) { constexpr int MI = 4; __VA_ARGS__(); }      \
+    else if (_it <= 8) { constexpr int MI = 8; __VA_ARGS__(); }      \
+    else { constexpr int MI = 16; __VA_ARGS__(); }                   \
+  }()
+
+#define LN_DISPATCH_T(DT, WDT, ...)                                                     \
+  [&] {                                                                                 \
+    if (DT == kF32) { using T = float; using WT = float; __VA_ARGS__(); }               \
+    else if (DT == kBF16) {                                                             \
+      using T = BF16;                                                                   \
+      if (WDT == kF32) { using WT = float; __VA_ARGS__(); } else { using WT = BF16; __VA_ARGS__(); } \
+    } else {                                                                            \
+      using T = F16;                                                                    \
+      if (WDT == kF32) { using WT = float; __VA_ARGS__(); } else { using WT = F16; __VA_ARGS__(); } \
+    }                                                                                   \
+  }()
+
+void layernorm_fwd(uintptr_t x, uintptr_t gamma, uintptr_t beta, uintptr_t y, uintptr_t mean, uintptr_t rstd,
+                   int64_t M, int N, float eps, int dt, int wdt, uintptr_t stream) {
+  VODA_CHECK(N > 0 && N % 4 == 0 && N <= kLayerNormMaxN, "layernorm: N must be a multiple of 4 and <= 4096");
+  VODA_CHECK(dt != kF32 || wdt == kF32, "layernorm: fp32 input needs fp32 weights");
+  if (M == 0) return;
+  const unsigned grid = unsigned((M + 3) / 4);
+  LN_DISPATCH_T(dt, wdt, [&] {
+    LN_DISPATCH_ITER(N, [&] {
+      hipLaunchKernelGGL((ln_fwd_kernel<T, WT, MI>), dim3(grid), dim3(256), 0, as_stream(stream),
+                         reinterpret_cast<const T*>(x), reinterpret_cast<const void*>(gamma),
+                         reinterpret_cast<const void*>(beta), reinterpret_cast<T*>(y),
+                         reinterpret_cast<float*>(mean), reinterpret_cast<float*>(rstd), M, N, eps);
+    });
+  });
+  check_launch();
+}
+
+int layernorm_bwd_partial_rows(int64_t M) {
+  int64_t g = (M + 3) / 4;
+  return int(std::max<int64_t>(1, std::min<int64_t>(g, 1024)));
+}
+
+void layernorm_bwd(uintptr_t dy, uintptr_t x, uintptr_t mean, uintptr_t rstd, uintptr_t gamma, uintptr_t dx,
+                   uintptr_t dgamma, uintptr_t dbeta, uintptr_t workspace, int64_t M, int N, int dt, int wdt,
+                   uintptr_t stream) {
+  VODA_CHECK(N > 0 && N % 4 == 0 && N <= kLayerNormMaxN, "layernorm: N must be a multiple of 4 and <= 4096");
+  if (M == 0) return;
+  const int grid = layernorm_bwd_partial_rows(M);
+  float* pg = nullptr;
+  float* pb = nullptr;
+  if (dgamma != 0) {
+    VODA_CHECK(workspace != 0 && dbeta != 0, "layernorm_bwd: workspace and dbeta required");
+    pg = reinterpret_cast<float*>(workspace);
+    pb = pg + int64_t(grid) * N;
+  }
+  const size_t lds = size_t(4) * N * sizeof(float);
+  LN_DISPATCH_T(dt, wdt, [&] {
+    LN_DISPATCH_ITER(N, [&] {
+      hipLaunchKernelGGL((ln_bwd_kernel<T, WT, MI>), dim3(grid), dim3(256), pg ? lds : 0, as_stream(stream),
+                         reinterpret_cast<const T*>(dy), reinterpret_cast<const T*>(x),
+                         reinterpret_cast<const float*>(mean), reinterpret_cast<const float*>(rstd),
+                         reinterpret_cast<const void*>(gamma), reinterpret_cast<T*>(dx), pg, pb, M, N);
+    });
+    if (pg) {
+      const unsigned cg = unsigned((N + 63) / 64);
+      hipLaunchKernelGGL((col_sum_kernel<WT>), dim3(cg), dim3(256), 0, as_stream(stream), pg,
+                         reinterpret_cast<WT*>(dgamma), grid, N);
+      hipLaunchKernelGGL((col_sum_kernel<WT>), dim3(cg), dim3(256), 0, as_stream(stream), pb,
+                         reinterpret_cast<WT*>(dbeta), grid, N);
+    }
+  });
+  check_launch();
+}
+
+}  // namespace voda

@@ -1,0 +1,83 @@
+// Host-side entry points of the _vodahip extension (all launches are stream-ordered).
+#pragma once
+
+#include <cstdint>
+#include <cstring>
+#include <string>
+#include <vector>
+
+struct ncclComm;
+typedef struct ncclComm* ncclComm_t;
+
+namespace voda {
+
+constexpr int kLayerNormMaxN = 4096;
+constexpr int kSoftmaxMaxS = 2048;
+
+// ---- fused optimizers (optim.hip) ----
+void sgd_step(uintptr_t p, uintptr_t g, int g_dtype, uintptr_t mom_buf, uintptr_t p_lp, int lp_dtype, int64_t n,
+              float lr, float momentum, float dampening, float wd, bool nesterov, bool first_step, float grad_scale,
+              uintptr_t stream);
+void adam_step(uintptr_t p, uintptr_t g, int g_dtype, uintptr_t m, uintptr_t v, uintptr_t p_lp, int lp_dtype,
+               int64_t n, float lr, float beta1, float beta2, float eps, float wd, bool adamw, int64_t step,
+               float grad_scale, uintptr_t stream);
+void rmsprop_step(uintptr_t p, uintptr_t g, int g_dtype, uintptr_t sq, uintptr_t mom_buf, uintptr_t gavg,
+                  uintptr_t p_lp, int lp_dtype, int64_t n, float lr, float alpha, float eps, float wd, float momentum,
+                  bool centered, float grad_scale, uintptr_t stream);
+
+// ---- bucket pack / cast (bucket.hip) ----
+void cast_scale(uintptr_t src, int src_dt, uintptr_t dst, int dst_dt, int64_t n, float scale, uintptr_t stream);
+void multi_tensor_copy(const std::vector<uintptr_t>& srcs, const std::vector<uintptr_t>& dsts,
+                       const std::vector<int64_t>& ns, int src_dt, int dst_dt, float scale, uintptr_t stream);
+
+// ---- LayerNorm (layernorm.hip) ----
+void layernorm_fwd(uintptr_t x, uintptr_t gamma, uintptr_t beta, uintptr_t y, uintptr_t mean, uintptr_t rstd,
+                   int64_t M, int N, float eps, int dt, int wdt, uintptr_t stream);
+int layernorm_bwd_partial_rows(int64_t M);
+void layernorm_bwd(uintptr_t dy, uintptr_t x, uintptr_t mean, uintptr_t rstd, uintptr_t gamma, uintptr_t dx,
+                   uintptr_t dgamma, uintptr_t dbeta, uintptr_t workspace, int64_t M, int N, int dt, int wdt,
+                   uintptr_t stream);
+
+// ---- masked softmax (softmax.hip) ----
+void masked_softmax_fwd(uintptr_t x, uintptr_t mask, int mask_dt, uintptr_t y, int64_t B, int H, int Tq, int S,
+                        int64_t mask_bstride, int64_t mask_qstride, bool causal, float scale, int dt,
+                        uintptr_t stream);
+void masked_softmax_bwd(uintptr_t y, uintptr_t dy, uintptr_t dx, int64_t rows, int S, float scale, int dt,
+                        uintptr_t stream);
+
+// ---- RCCL engine (comm.cpp) ----
+std::string rccl_unique_id();
+int rccl_version();
+
+class RcclComm {
+ public:
+  RcclComm(const std::string& uid, int nranks, int rank, int device, double timeout_s);
+  ~RcclComm();
+  RcclComm(const RcclComm&) = delete;
+  RcclComm& operator=(const RcclComm&) = delete;
+
+  void allreduce(uintptr_t send, uintptr_t recv, int64_t count, int dtype, int op, uintptr_t stream);
+  void broadcast(uintptr_t send, uintptr_t recv, int64_t count, int dtype, int root, uintptr_t stream);
+  void allgather(uintptr_t send, uintptr_t recv, int64_t count, int dtype, uintptr_t stream);
+  void reduce_scatter(uintptr_t send, uintptr_t recv, int64_t count, int dtype, int op, uintptr_t stream);
+  void alltoall(uintptr_t send, uintptr_t recv, int64_t count, int dtype, uintptr_t stream);
+  void group_start();
+  void group_end();
+  std::string async_error() const;
+  void abort();
+  void destroy();
+  int rank() const { return rank_; }
+  int size() const { return nranks_; }
+  bool alive() const { return comm_ != nullptr && !aborted_; }
+
+ private:
+  void wait_ready(const char* what);
+  void check_live() const;
+  void finish(int r, const char* what);
+  ncclComm_t comm_ = nullptr;
+  int nranks_, rank_;
+  double timeout_s_;
+  bool aborted_ = false;
+};
+
+}  // namespace voda

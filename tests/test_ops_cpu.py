@@ -1,0 +1,88 @@
+"""CPU reference paths of the fused ops (the same flat-buffer math the HIP kernels run)."""
+import pytest
+import torch
+
+from vodascheduler_amd.ops import (FusedAdam, FusedRMSprop, FusedSGD, cast_scale_, layer_norm, make_optimizer,
+                                   masked_softmax, multi_tensor_copy_, reference_masked_softmax)
+from vodascheduler_amd.utils.flat import FlatGroup
+
+
+def _pair():
+    torch.manual_seed(0)
+    a = torch.nn.Sequential(torch.nn.Conv2d(3, 8, 3), torch.nn.Flatten(), torch.nn.Linear(8 * 6 * 6, 5))
+    b = torch.nn.Sequential(torch.nn.Conv2d(3, 8, 3), torch.nn.Flatten(), torch.nn.Linear(8 * 6 * 6, 5))
+    b.load_state_dict(a.state_dict())
+    return a, b
+
+
+def _train(m, opt, steps=4):
+    g = torch.Generator().manual_seed(3)
+    for _ in range(steps):
+        x = torch.randn(4, 3, 8, 8, generator=g)
+        opt.zero_grad()
+        m(x).square().mean().backward()
+        opt.step()
+
+
+@pytest.mark.parametrize("ours,ref,kw", [
+    (FusedSGD, torch.optim.SGD, dict(lr=0.1, momentum=0.9, weight_decay=1e-3)),
+    (FusedSGD, torch.optim.SGD, dict(lr=0.1, momentum=0.9, nesterov=True)),
+    (FusedSGD, torch.optim.SGD, dict(lr=0.1)),
+    (FusedAdam, torch.optim.Adam, dict(lr=1e-2, weight_decay=1e-3)),
+    (FusedRMSprop, torch.optim.RMSprop, dict(lr=1e-3, momentum=0.9, centered=True)),
+])
+def test_cpu_optimizers_match_torch(ours, ref, kw):
+    a, b = _pair()
+    _train(a, ref(a.parameters(), **kw))
+    _train(b, ours(b.parameters(), **kw))
+    for x, y in zip(a.parameters(), b.parameters()):
+        torch.testing.assert_close(x, y, rtol=1e-5, atol=1e-6)
+
+
+def test_flat_group_keeps_channels_last_and_views():
+    conv = torch.nn.Conv2d(4, 8, 3).to(memory_format=torch.channels_last)
+    st = conv.weight.stride()
+    fg = FlatGroup(conv.parameters())
+    assert conv.weight.stride() == st
+    assert conv.weight.data_ptr() == fg.master.data_ptr()
+    out = conv(torch.randn(2, 4, 5, 5).to(memory_format=torch.channels_last))
+    out.sum().backward()
+    assert conv.weight.grad.data_ptr() == fg.grad.data_ptr()
+    assert fg.grad.abs().sum() > 0
+    fg.zero_grad()
+    assert fg.grad.abs().sum() == 0
+
+
+def test_optimizer_state_dict_roundtrip():
+    a, b = _pair()
+    oa = make_optimizer("adam", a.parameters(), lr=1e-2)
+    _train(a, oa)
+    ob = make_optimizer("adam", b.parameters(), lr=1e-2)
+    ob.load_state_dict(oa.state_dict())
+    for x, y in zip(a.parameters(), b.parameters()):
+        torch.testing.assert_close(x, y)
+    _train(a, oa, 2)
+    _train(b, ob, 2)
+    for x, y in zip(a.parameters(), b.parameters()):
+        torch.testing.assert_close(x, y)
+
+
+def test_cpu_cast_and_multi_copy():
+    x = torch.randn(100)
+    y = torch.empty(100, dtype=torch.bfloat16)
+    cast_scale_(x, y, 0.5)
+    torch.testing.assert_close(y, (x * 0.5).bfloat16())
+    ts = [torch.randn(5), torch.randn(7)]
+    out = [torch.empty(5), torch.empty(7)]
+    multi_tensor_copy_(ts, out, 2.0)
+    torch.testing.assert_close(out[1], ts[1] * 2)
+
+
+def test_cpu_layernorm_and_softmax_reference():
+    x = torch.randn(3, 16)
+    torch.testing.assert_close(layer_norm(x), torch.nn.functional.layer_norm(x, (16,)))
+    s = torch.randn(2, 2, 4, 4)
+    y = masked_softmax(s, causal=True)
+    assert torch.allclose(y.sum(-1), torch.ones(2, 2, 4))
+    assert y[0, 0, 0, 1:].abs().max() < 1e-6
+    torch.testing.assert_close(y, reference_masked_softmax(s, None, True))

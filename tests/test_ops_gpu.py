@@ -1,0 +1,156 @@
+"""Numerics of the hand-written HIP kernels vs plain PyTorch fp32 references (MI355X)."""
+import math
+
+import pytest
+import torch
+
+from vodascheduler_amd.ops import (FusedAdam, FusedLayerNorm, FusedRMSprop, FusedSGD, cast_scale_, layer_norm,
+                                   masked_softmax, multi_tensor_copy_, reference_masked_softmax)
+from vodascheduler_amd.ops import _native
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def test_native_extension_is_loaded():
+    h = _native.hip()
+    assert h.GPU_ARCH == "gfx950"
+    assert torch.cuda.get_device_properties(0).gcnArchName.startswith("gfx950")
+
+
+def _model_pair(seed=0):
+    torch.manual_seed(seed)
+    m1 = torch.nn.Sequential(torch.nn.Linear(33, 65), torch.nn.ReLU(), torch.nn.Linear(65, 7)).to(DEV)
+    m2 = torch.nn.Sequential(torch.nn.Linear(33, 65), torch.nn.ReLU(), torch.nn.Linear(65, 7)).to(DEV)
+    m2.load_state_dict(m1.state_dict())
+    return m1, m2
+
+
+def _run(m, opt, steps=5, seed=1):
+    g = torch.Generator(device=DEV).manual_seed(seed)
+    for _ in range(steps):
+        x = torch.randn(16, 33, device=DEV, generator=g)
+        opt.zero_grad()
+        m(x).square().mean().backward()
+        opt.step()
+
+
+@pytest.mark.parametrize("kw", [dict(momentum=0.0), dict(momentum=0.9), dict(momentum=0.9, nesterov=True),
+                                dict(momentum=0.9, weight_decay=1e-2, dampening=0.1)])
+def test_fused_sgd_matches_torch(kw):
+    m1, m2 = _model_pair()
+    _run(m1, torch.optim.SGD(m1.parameters(), lr=0.1, **kw))
+    _run(m2, FusedSGD(m2.parameters(), lr=0.1, **kw))
+    for a, b in zip(m1.parameters(), m2.parameters()):
+        torch.testing.assert_close(a, b, rtol=1e-5, atol=1e-6)
+
+
+@pytest.mark.parametrize("adamw", [False, True])
+def test_fused_adam_matches_torch(adamw):
+    m1, m2 = _model_pair()
+    ref = (torch.optim.AdamW if adamw else torch.optim.Adam)(m1.parameters(), lr=1e-2, weight_decay=1e-2)
+    _run(m1, ref)
+    _run(m2, FusedAdam(m2.parameters(), lr=1e-2, weight_decay=1e-2, adamw=adamw))
+    for a, b in zip(m1.parameters(), m2.parameters()):
+        torch.testing.assert_close(a, b, rtol=1e-5, atol=1e-6)
+
+
+@pytest.mark.parametrize("kw", [dict(), dict(momentum=0.9), dict(centered=True, momentum=0.5)])
+def test_fused_rmsprop_matches_torch(kw):
+    m1, m2 = _model_pair()
+    _run(m1, torch.optim.RMSprop(m1.parameters(), lr=1e-3, **kw))
+    _run(m2, FusedRMSprop(m2.parameters(), lr=1e-3, **kw))
+    for a, b in zip(m1.parameters(), m2.parameters()):
+        torch.testing.assert_close(a, b, rtol=1e-4, atol=1e-5)
+
+
+def test_fused_sgd_bf16_weights_and_grads():
+    torch.manual_seed(0)
+    m = torch.nn.Linear(128, 64).to(DEV).to(torch.bfloat16)
+    opt = FusedSGD(m.parameters(), lr=0.05, momentum=0.9)
+    master0 = opt.flat_groups[0].master.clone()
+    x = torch.randn(8, 128, device=DEV, dtype=torch.bfloat16)
+    opt.zero_grad()
+    m(x).float().square().mean().backward()
+    g = opt.flat_groups[0].grad.float().clone()
+    opt.step()
+    expect = master0 - 0.05 * g
+    torch.testing.assert_close(opt.flat_groups[0].master, expect, rtol=1e-6, atol=1e-6)
+    # bf16 model weights are the RNE cast of the fp32 master, written by the same kernel
+    torch.testing.assert_close(opt.flat_groups[0].lowp, expect.to(torch.bfloat16), rtol=0, atol=0)
+
+
+@pytest.mark.parametrize("n", [1, 3, 4, 1000, 65537, 1 << 22])
+@pytest.mark.parametrize("sd,dd", [(torch.float32, torch.bfloat16), (torch.bfloat16, torch.float32),
+                                   (torch.float32, torch.float16), (torch.float32, torch.float32)])
+def test_cast_scale(n, sd, dd):
+    x = torch.randn(n, device=DEV).to(sd)
+    y = torch.empty(n, device=DEV, dtype=dd)
+    cast_scale_(x, y, 0.125)
+    torch.testing.assert_close(y, (x.float() * 0.125).to(dd), rtol=0, atol=0)
+
+
+def test_multi_tensor_copy_roundtrip():
+    ts = [torch.randn(s, device=DEV) for s in (1, 7, 64, 1000, 4097, 123456)] * 12  # > 64 tensors
+    flat = torch.empty(sum(t.numel() for t in ts), device=DEV, dtype=torch.bfloat16)
+    views = list(torch.split(flat, [t.numel() for t in ts]))
+    multi_tensor_copy_(ts, views, scale=0.5)
+    torch.testing.assert_close(flat, torch.cat(ts).mul(0.5).bfloat16(), rtol=0, atol=0)
+    back = [torch.empty_like(t) for t in ts]
+    multi_tensor_copy_(views, back, scale=2.0)
+    for b, t in zip(back, ts):
+        torch.testing.assert_close(b, t.bfloat16().float(), rtol=1e-2, atol=1e-2)
+
+
+@pytest.mark.parametrize("shape", [(10240, 256), (512, 768), (3, 5, 1024), (64, 4096), (7, 12)])
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+def test_layernorm_fwd_bwd(shape, dt):
+    torch.manual_seed(0)
+    n = shape[-1]
+    x = torch.randn(shape, device=DEV).mul(3).add(1).to(dt).requires_grad_()
+    w = torch.randn(n, device=DEV).requires_grad_()
+    b = torch.randn(n, device=DEV).requires_grad_()
+    y = layer_norm(x, w, b, 1e-5)
+    dy = torch.randn_like(y)
+    y.backward(dy)
+    xr = x.detach().float().requires_grad_()
+    wr = w.detach().clone().requires_grad_()
+    br = b.detach().clone().requires_grad_()
+    yr = torch.nn.functional.layer_norm(xr, (n,), wr, br, 1e-5)
+    yr.backward(dy.float())
+    tol = dict(rtol=2e-2, atol=3e-2) if dt == torch.bfloat16 else dict(rtol=1e-4, atol=1e-4)
+    torch.testing.assert_close(y.float(), yr, **tol)
+    torch.testing.assert_close(x.grad.float(), xr.grad, **tol)
+    gt = dict(rtol=2e-2, atol=2e-1) if dt == torch.bfloat16 else dict(rtol=1e-3, atol=1e-3)
+    torch.testing.assert_close(w.grad, wr.grad, **gt)
+    torch.testing.assert_close(b.grad, br.grad, **gt)
+
+
+def test_fused_layernorm_module_bf16_weights():
+    ln = FusedLayerNorm(768).to(DEV).to(torch.bfloat16)
+    x = torch.randn(4, 128, 768, device=DEV, dtype=torch.bfloat16, requires_grad=True)
+    y = ln(x)
+    y.float().sum().backward()
+    ref = torch.nn.functional.layer_norm(x.detach().float(), (768,))
+    torch.testing.assert_close(y.float(), ref, rtol=2e-2, atol=3e-2)
+    assert ln.weight.grad is not None and ln.weight.grad.dtype == torch.bfloat16
+
+
+@pytest.mark.parametrize("B,H,Tq,S", [(512, 8, 20, 20), (4, 12, 128, 128), (2, 2, 7, 512), (1, 1, 3, 2048)])
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("causal", [False, True])
+def test_masked_softmax(B, H, Tq, S, dt, causal):
+    torch.manual_seed(0)
+    x = torch.randn(B, H, Tq, S, device=DEV).mul(4).to(dt).requires_grad_()
+    mask = (torch.rand(B, 1, 1, S, device=DEV) > 0.2).float()
+    mask[..., 0] = 1
+    scale = 1 / math.sqrt(64)
+    y = masked_softmax(x, mask, causal, scale)
+    dy = torch.randn_like(y)
+    y.backward(dy)
+    xr = x.detach().float().requires_grad_()
+    yr = reference_masked_softmax(xr, mask, causal, scale)
+    yr.backward(dy.float())
+    tol = dict(rtol=2e-2, atol=1e-2) if dt == torch.bfloat16 else dict(rtol=1e-5, atol=1e-6)
+    torch.testing.assert_close(y.float(), yr, **tol)
+    torch.testing.assert_close(x.grad.float(), xr.grad, **tol)

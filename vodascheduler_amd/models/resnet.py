@@ -1,0 +1,108 @@
+"""ResNet family (ResNet-50 v1.5 bottleneck) for the elastic training workloads.
+
+Reference workload: ``applications.ResNet50(weights=None, classes=10)`` on CIFAR-10
+(reference examples/py/tensorflow2/tensorflow2_keras_cifar_elastic.py:148-151) and the
+BASELINE config "8 ResNet-50 ImageNet-shape jobs".  Convolutions/BatchNorm run on MIOpen
+through PyTorch-ROCm in channels_last bf16 (NHWC is MIOpen's fast layout on CDNA);
+random-init weights, synthetic data.
+"""
+from __future__ import annotations
+
+import torch
+from torch import nn
+
+
+class Bottleneck(nn.Module):
+    expansion = 4
+
+    def __init__(self, inplanes: int, planes: int, stride: int = 1, downsample: nn.Module | None = None):
+        super().__init__()
+        width = planes
+        self.conv1 = nn.Conv2d(inplanes, width, 1, bias=False)
+        self.bn1 = nn.BatchNorm2d(width)
+        self.conv2 = nn.Conv2d(width, width, 3, stride=stride, padding=1, bias=False)  # v1.5: stride on 3x3
+        self.bn2 = nn.BatchNorm2d(width)
+        self.conv3 = nn.Conv2d(width, planes * self.expansion, 1, bias=False)
+        self.bn3 = nn.BatchNorm2d(planes * self.expansion)
+        self.relu = nn.ReLU(inplace=True)
+        self.downsample = downsample
+
+    def forward(self, x):
+        idt = x
+        out = self.relu(self.bn1(self.conv1(x)))
+        out = self.relu(self.bn2(self.conv2(out)))
+        out = self.bn3(self.conv3(out))
+        if self.downsample is not None:
+            idt = self.downsample(x)
+        return self.relu(out + idt)
+
+
+class BasicBlock(nn.Module):
+    expansion = 1
+
+    def __init__(self, inplanes: int, planes: int, stride: int = 1, downsample: nn.Module | None = None):
+        super().__init__()
+        self.conv1 = nn.Conv2d(inplanes, planes, 3, stride=stride, padding=1, bias=False)
+        self.bn1 = nn.BatchNorm2d(planes)
+        self.conv2 = nn.Conv2d(planes, planes, 3, padding=1, bias=False)
+        self.bn2 = nn.BatchNorm2d(planes)
+        self.relu = nn.ReLU(inplace=True)
+        self.downsample = downsample
+
+    def forward(self, x):
+        idt = x if self.downsample is None else self.downsample(x)
+        out = self.relu(self.bn1(self.conv1(x)))
+        out = self.bn2(self.conv2(out))
+        return self.relu(out + idt)
+
+
+class ResNet(nn.Module):
+    def __init__(self, block, layers, num_classes: int = 1000, small_input: bool = False):
+        super().__init__()
+        self.inplanes = 64
+        if small_input:  # CIFAR-style 32x32 stem
+            self.stem = nn.Sequential(nn.Conv2d(3, 64, 3, padding=1, bias=False), nn.BatchNorm2d(64),
+                                      nn.ReLU(inplace=True))
+        else:
+            self.stem = nn.Sequential(nn.Conv2d(3, 64, 7, stride=2, padding=3, bias=False), nn.BatchNorm2d(64),
+                                      nn.ReLU(inplace=True), nn.MaxPool2d(3, stride=2, padding=1))
+        self.layer1 = self._make(block, 64, layers[0])
+        self.layer2 = self._make(block, 128, layers[1], stride=2)
+        self.layer3 = self._make(block, 256, layers[2], stride=2)
+        self.layer4 = self._make(block, 512, layers[3], stride=2)
+        self.pool = nn.AdaptiveAvgPool2d(1)
+        self.fc = nn.Linear(512 * block.expansion, num_classes)
+        for m in self.modules():
+            if isinstance(m, nn.Conv2d):
+                nn.init.kaiming_normal_(m.weight, mode="fan_out", nonlinearity="relu")
+            elif isinstance(m, nn.BatchNorm2d):
+                nn.init.ones_(m.weight)
+                nn.init.zeros_(m.bias)
+        for m in self.modules():  # zero-init last BN of each residual branch
+            if isinstance(m, Bottleneck):
+                nn.init.zeros_(m.bn3.weight)
+            elif isinstance(m, BasicBlock):
+                nn.init.zeros_(m.bn2.weight)
+
+    def _make(self, block, planes, blocks, stride=1):
+        down = None
+        if stride != 1 or self.inplanes != planes * block.expansion:
+            down = nn.Sequential(nn.Conv2d(self.inplanes, planes * block.expansion, 1, stride=stride, bias=False),
+                                 nn.BatchNorm2d(planes * block.expansion))
+        layers = [block(self.inplanes, planes, stride, down)]
+        self.inplanes = planes * block.expansion
+        layers += [block(self.inplanes, planes) for _ in range(1, blocks)]
+        return nn.Sequential(*layers)
+
+    def forward(self, x):
+        x = self.stem(x)
+        x = self.layer4(self.layer3(self.layer2(self.layer1(x))))
+        return self.fc(torch.flatten(self.pool(x), 1))
+
+
+def resnet50(num_classes: int = 1000, small_input: bool = False) -> ResNet:
+    return ResNet(Bottleneck, [3, 4, 6, 3], num_classes, small_input)
+
+
+def resnet18(num_classes: int = 1000, small_input: bool = False) -> ResNet:
+    return ResNet(BasicBlock, [2, 2, 2, 2], num_classes, small_input)

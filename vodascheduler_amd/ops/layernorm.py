@@ -1,0 +1,106 @@
+"""LayerNorm with hand-written CDNA4 forward/backward kernels (csrc/hip/layernorm.hip).
+
+``layer_norm(x, weight, bias, eps)`` normalises over the last dimension.  On GPU it runs
+the wave-per-row HIP kernels (output in the input dtype, statistics in fp32); on CPU the
+PyTorch reference ``torch.nn.functional.layer_norm`` in fp32.
+"""
+from __future__ import annotations
+
+import torch
+
+from . import _native as N
+
+MAX_N = 4096
+
+
+def _supported(x: torch.Tensor, weight: torch.Tensor | None) -> bool:
+    n = x.shape[-1]
+    if not x.is_cuda or n % 4 != 0 or n > MAX_N or x.dtype not in (torch.float32, torch.bfloat16, torch.float16):
+        return False
+    if weight is not None and weight.dtype not in (torch.float32, x.dtype):
+        return False
+    return True
+
+
+class _LayerNormFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, weight, bias, eps):
+        n = x.shape[-1]
+        xc = x.contiguous()
+        m = xc.numel() // n
+        y = torch.empty_like(xc)
+        mean = torch.empty(m, dtype=torch.float32, device=x.device)
+        rstd = torch.empty(m, dtype=torch.float32, device=x.device)
+        wdt = weight.dtype if weight is not None else (torch.float32 if x.dtype == torch.float32 else x.dtype)
+        w = weight.contiguous() if weight is not None else None
+        b = bias.to(wdt).contiguous() if bias is not None else None
+        for t, nm in ((xc, "x"), (y, "y")):
+            N.check_gpu_tensor(t, nm, align=8)
+        N.hip().layernorm_fwd(xc.data_ptr(), N.ptr(w), N.ptr(b), y.data_ptr(), mean.data_ptr(), rstd.data_ptr(),
+                              m, n, float(eps), N.dtype_code(x.dtype), N.dtype_code(wdt), N.stream_of(x))
+        ctx.save_for_backward(xc, w, mean, rstd)
+        ctx.has_bias = bias is not None
+        ctx.wdt = wdt
+        return y.view_as(x)
+
+    @staticmethod
+    def backward(ctx, dy):
+        xc, w, mean, rstd = ctx.saved_tensors
+        n = xc.shape[-1]
+        m = xc.numel() // n
+        dyc = dy.contiguous()
+        dx = torch.empty_like(xc)
+        need_w = w is not None and ctx.needs_input_grad[1]
+        need_b = ctx.has_bias and ctx.needs_input_grad[2]
+        dgamma = dbeta = ws = None
+        if need_w or need_b:
+            rows = N.hip().layernorm_bwd_partial_rows(m)
+            ws = torch.empty(2 * rows * n, dtype=torch.float32, device=xc.device)
+            dgamma = torch.empty(n, dtype=ctx.wdt, device=xc.device)
+            dbeta = torch.empty(n, dtype=ctx.wdt, device=xc.device)
+        N.hip().layernorm_bwd(dyc.data_ptr(), xc.data_ptr(), mean.data_ptr(), rstd.data_ptr(), N.ptr(w),
+                              dx.data_ptr(), N.ptr(dgamma), N.ptr(dbeta), N.ptr(ws), m, n,
+                              N.dtype_code(xc.dtype), N.dtype_code(ctx.wdt), N.stream_of(xc))
+        return (dx.view_as(dy), dgamma if need_w else None, dbeta if need_b else None, None)
+
+
+def layer_norm(x: torch.Tensor, weight: torch.Tensor | None = None, bias: torch.Tensor | None = None,
+               eps: float = 1e-5) -> torch.Tensor:
+    if x.is_cuda:
+        if not _supported(x, weight):
+            raise ValueError(f"fused layer_norm: unsupported shape/dtype {tuple(x.shape)} {x.dtype}")
+        return _LayerNormFn.apply(x, weight, bias, eps)
+    n = x.shape[-1]
+    y = torch.nn.functional.layer_norm(x.float(), (n,), None if weight is None else weight.float(),
+                                       None if bias is None else bias.float(), eps)
+    return y.to(x.dtype)
+
+
+class FusedLayerNorm(torch.nn.Module):
+    """Drop-in for ``torch.nn.LayerNorm`` over the last dimension."""
+
+    def __init__(self, normalized_shape: int, eps: float = 1e-5, elementwise_affine: bool = True,
+                 device=None, dtype=None):
+        super().__init__()
+        if isinstance(normalized_shape, (tuple, list)):
+            if len(normalized_shape) != 1:
+                raise ValueError("FusedLayerNorm normalises over the last dimension only")
+            normalized_shape = normalized_shape[0]
+        self.normalized_shape = (int(normalized_shape),)
+        self.eps = eps
+        if elementwise_affine:
+            self.weight = torch.nn.Parameter(torch.ones(normalized_shape, device=device, dtype=dtype))
+            self.bias = torch.nn.Parameter(torch.zeros(normalized_shape, device=device, dtype=dtype))
+        else:
+            self.register_parameter("weight", None)
+            self.register_parameter("bias", None)
+
+    def forward(self, x):
+        if x.is_cuda and torch.is_autocast_enabled("cuda"):
+            # keep the input dtype (bf16 out, fp32 statistics inside the kernel)
+            with torch.autocast("cuda", enabled=False):
+                return layer_norm(x, self.weight, self.bias, self.eps)
+        return layer_norm(x, self.weight, self.bias, self.eps)
+
+    def extra_repr(self):
+        return f"{self.normalized_shape}, eps={self.eps}"

@@ -1,0 +1,254 @@
+"""Fused flat-buffer optimizers: SGD(+momentum/nesterov), Adam/AdamW, RMSprop.
+
+GPU path: ONE HIP launch per parameter group per step (csrc/hip/optim.hip), reading
+param/grad/state once, optionally writing the bf16/fp16 model-weight copy in the same
+pass.  CPU path: the same math in PyTorch ops on the same flat buffers (reference used
+by the numerics tests).  Semantics follow ``torch.optim`` so the reference workloads'
+optimizers (SGD momentum 0.9 for ResNet50/VGG16, Adam for MNIST, RMSprop for
+InceptionV3/Transformer — reference examples/yaml/tensorflow2/*.yaml and SURVEY.md §2.8)
+map one-to-one.
+"""
+from __future__ import annotations
+
+import math
+
+import torch
+
+from ..utils.flat import FlatGroup
+from . import _native as N
+
+
+class _FusedFlatOptimizer(torch.optim.Optimizer):
+    """Base class: owns one :class:`FlatGroup` per param group."""
+
+    _state_names: tuple[str, ...] = ()
+
+    def __init__(self, params, defaults, grad_dtype: torch.dtype | None = None):
+        super().__init__(params, defaults)
+        self.flat_groups: list[FlatGroup] = []
+        self._flat_state: list[dict[str, torch.Tensor]] = []
+        self._steps: list[int] = []
+        for g in self.param_groups:
+            fg = FlatGroup(g["params"], flatten_params=True, grad_dtype=grad_dtype)
+            self.flat_groups.append(fg)
+            self._flat_state.append({})
+            self._steps.append(0)
+
+    # -- state buffers (allocated lazily, flat fp32) --
+    def _buf(self, gi: int, name: str) -> torch.Tensor:
+        st = self._flat_state[gi]
+        if name not in st:
+            st[name] = torch.zeros_like(self.flat_groups[gi].master)
+        return st[name]
+
+    def zero_grad(self, set_to_none: bool = False) -> None:  # grads are flat views: never None
+        for fg in self.flat_groups:
+            fg.zero_grad()
+
+    @torch.no_grad()
+    def step(self, closure=None):
+        loss = None
+        if closure is not None:
+            with torch.enable_grad():
+                loss = closure()
+        for gi, group in enumerate(self.param_groups):
+            self._steps[gi] += 1
+            fg = self.flat_groups[gi]
+            if fg.master.is_cuda:
+                self._step_gpu(gi, group, fg)
+            else:
+                self._step_cpu(gi, group, fg)
+        return loss
+
+    def _lowp_args(self, fg: FlatGroup) -> tuple[int, int]:
+        if fg.lowp is None:
+            return 0, -1
+        return fg.lowp.data_ptr(), N.dtype_code(fg.lowp.dtype)
+
+    def _check(self, fg: FlatGroup) -> None:
+        N.check_gpu_tensor(fg.master, "master")
+        N.check_gpu_tensor(fg.grad, "grad", align=8)
+        if fg.grad.numel() != fg.master.numel():
+            raise ValueError("grad/master size mismatch")
+
+    # -- checkpoint / elastic state sync --
+    def flat_state_tensors(self) -> list[torch.Tensor]:
+        """All tensors that define the optimizer+model state (for broadcast/snapshot)."""
+        out = []
+        for gi, fg in enumerate(self.flat_groups):
+            out.append(fg.master)
+            for name in self._state_names_for(gi):
+                out.append(self._buf(gi, name))
+        return out
+
+    def _state_names_for(self, gi: int) -> tuple[str, ...]:
+        return self._state_names
+
+    def state_dict(self):
+        sd = {"param_groups": [{k: v for k, v in g.items() if k != "params"} for g in self.param_groups],
+              "steps": list(self._steps), "flat": []}
+        for gi, fg in enumerate(self.flat_groups):
+            d = {"master": fg.master}
+            for name in self._state_names_for(gi):
+                d[name] = self._buf(gi, name)
+            sd["flat"].append(d)
+        return sd
+
+    @torch.no_grad()
+    def load_state_dict(self, sd):
+        if len(sd["flat"]) != len(self.flat_groups):
+            raise ValueError("param group count mismatch")
+        for g, sg in zip(self.param_groups, sd["param_groups"]):
+            g.update(sg)
+        self._steps = list(sd["steps"])
+        for gi, (fg, d) in enumerate(zip(self.flat_groups, sd["flat"])):
+            fg.master.copy_(d["master"])
+            for name in self._state_names_for(gi):
+                if name in d:
+                    self._buf(gi, name).copy_(d[name])
+            fg.sync_lowp_from_master()
+
+    def after_external_update(self) -> None:
+        """Call after master buffers were overwritten (broadcast/restore)."""
+        for fg in self.flat_groups:
+            fg.sync_lowp_from_master()
+
+
+class FusedSGD(_FusedFlatOptimizer):
+    def __init__(self, params, lr: float, momentum: float = 0.0, dampening: float = 0.0,
+                 weight_decay: float = 0.0, nesterov: bool = False, grad_scale: float = 1.0,
+                 grad_dtype: torch.dtype | None = None):
+        if nesterov and (momentum <= 0 or dampening != 0):
+            raise ValueError("Nesterov momentum requires a momentum and zero dampening")
+        super().__init__(params, dict(lr=lr, momentum=momentum, dampening=dampening,
+                                      weight_decay=weight_decay, nesterov=nesterov, grad_scale=grad_scale),
+                         grad_dtype)
+
+    def _state_names_for(self, gi):
+        return ("momentum_buffer",) if self.param_groups[gi]["momentum"] != 0 else ()
+
+    def _step_gpu(self, gi, g, fg):
+        self._check(fg)
+        mom = g["momentum"]
+        buf = self._buf(gi, "momentum_buffer") if mom != 0 else None
+        lp, lpdt = self._lowp_args(fg)
+        N.hip().sgd_step(fg.master.data_ptr(), fg.grad.data_ptr(), N.dtype_code(fg.grad.dtype), N.ptr(buf), lp, lpdt,
+                         fg.numel, float(g["lr"]), float(mom), float(g["dampening"]), float(g["weight_decay"]),
+                         bool(g["nesterov"]), self._steps[gi] == 1, float(g["grad_scale"]), N.stream_of(fg.master))
+
+    def _step_cpu(self, gi, g, fg):
+        p = fg.master
+        d = fg.grad.float() * g["grad_scale"]
+        if g["weight_decay"] != 0:
+            d = d + g["weight_decay"] * p
+        if g["momentum"] != 0:
+            buf = self._buf(gi, "momentum_buffer")
+            if self._steps[gi] == 1:
+                buf.copy_(d)
+            else:
+                buf.mul_(g["momentum"]).add_(d, alpha=1 - g["dampening"])
+            d = d + g["momentum"] * buf if g["nesterov"] else buf
+        p.add_(d, alpha=-g["lr"])
+        fg.sync_lowp_from_master()
+
+
+class FusedAdam(_FusedFlatOptimizer):
+    _state_names = ("exp_avg", "exp_avg_sq")
+
+    def __init__(self, params, lr: float = 1e-3, betas=(0.9, 0.999), eps: float = 1e-8,
+                 weight_decay: float = 0.0, adamw: bool = False, grad_scale: float = 1.0,
+                 grad_dtype: torch.dtype | None = None):
+        super().__init__(params, dict(lr=lr, betas=tuple(betas), eps=eps, weight_decay=weight_decay,
+                                      adamw=adamw, grad_scale=grad_scale), grad_dtype)
+
+    def _step_gpu(self, gi, g, fg):
+        self._check(fg)
+        m, v = self._buf(gi, "exp_avg"), self._buf(gi, "exp_avg_sq")
+        lp, lpdt = self._lowp_args(fg)
+        b1, b2 = g["betas"]
+        N.hip().adam_step(fg.master.data_ptr(), fg.grad.data_ptr(), N.dtype_code(fg.grad.dtype), m.data_ptr(),
+                          v.data_ptr(), lp, lpdt, fg.numel, float(g["lr"]), float(b1), float(b2), float(g["eps"]),
+                          float(g["weight_decay"]), bool(g["adamw"]), self._steps[gi], float(g["grad_scale"]),
+                          N.stream_of(fg.master))
+
+    def _step_cpu(self, gi, g, fg):
+        p = fg.master
+        m, v = self._buf(gi, "exp_avg"), self._buf(gi, "exp_avg_sq")
+        b1, b2 = g["betas"]
+        t = self._steps[gi]
+        d = fg.grad.float() * g["grad_scale"]
+        if g["adamw"]:
+            p.mul_(1 - g["lr"] * g["weight_decay"])
+        elif g["weight_decay"] != 0:
+            d = d + g["weight_decay"] * p
+        m.mul_(b1).add_(d, alpha=1 - b1)
+        v.mul_(b2).addcmul_(d, d, value=1 - b2)
+        bc1, bc2 = 1 - b1 ** t, 1 - b2 ** t
+        denom = (v.sqrt() / math.sqrt(bc2)).add_(g["eps"])
+        p.addcdiv_(m, denom, value=-g["lr"] / bc1)
+        fg.sync_lowp_from_master()
+
+
+class FusedAdamW(FusedAdam):
+    def __init__(self, params, lr: float = 1e-3, betas=(0.9, 0.999), eps: float = 1e-8,
+                 weight_decay: float = 1e-2, grad_scale: float = 1.0, grad_dtype: torch.dtype | None = None):
+        super().__init__(params, lr, betas, eps, weight_decay, adamw=True, grad_scale=grad_scale,
+                         grad_dtype=grad_dtype)
+
+
+class FusedRMSprop(_FusedFlatOptimizer):
+    def __init__(self, params, lr: float = 1e-2, alpha: float = 0.99, eps: float = 1e-8,
+                 weight_decay: float = 0.0, momentum: float = 0.0, centered: bool = False,
+                 grad_scale: float = 1.0, grad_dtype: torch.dtype | None = None):
+        super().__init__(params, dict(lr=lr, alpha=alpha, eps=eps, weight_decay=weight_decay,
+                                      momentum=momentum, centered=centered, grad_scale=grad_scale), grad_dtype)
+
+    def _state_names_for(self, gi):
+        g = self.param_groups[gi]
+        names = ["square_avg"]
+        if g["momentum"] > 0:
+            names.append("momentum_buffer")
+        if g["centered"]:
+            names.append("grad_avg")
+        return tuple(names)
+
+    def _step_gpu(self, gi, g, fg):
+        self._check(fg)
+        sq = self._buf(gi, "square_avg")
+        buf = self._buf(gi, "momentum_buffer") if g["momentum"] > 0 else None
+        ga = self._buf(gi, "grad_avg") if g["centered"] else None
+        lp, lpdt = self._lowp_args(fg)
+        N.hip().rmsprop_step(fg.master.data_ptr(), fg.grad.data_ptr(), N.dtype_code(fg.grad.dtype), sq.data_ptr(),
+                             N.ptr(buf), N.ptr(ga), lp, lpdt, fg.numel, float(g["lr"]), float(g["alpha"]),
+                             float(g["eps"]), float(g["weight_decay"]), float(g["momentum"]), bool(g["centered"]),
+                             float(g["grad_scale"]), N.stream_of(fg.master))
+
+    def _step_cpu(self, gi, g, fg):
+        p = fg.master
+        d = fg.grad.float() * g["grad_scale"]
+        if g["weight_decay"] != 0:
+            d = d + g["weight_decay"] * p
+        sq = self._buf(gi, "square_avg")
+        sq.mul_(g["alpha"]).addcmul_(d, d, value=1 - g["alpha"])
+        if g["centered"]:
+            ga = self._buf(gi, "grad_avg")
+            ga.mul_(g["alpha"]).add_(d, alpha=1 - g["alpha"])
+            avg = (sq - ga * ga).sqrt_().add_(g["eps"])
+        else:
+            avg = sq.sqrt().add_(g["eps"])
+        if g["momentum"] > 0:
+            buf = self._buf(gi, "momentum_buffer")
+            buf.mul_(g["momentum"]).addcdiv_(d, avg)
+            p.add_(buf, alpha=-g["lr"])
+        else:
+            p.addcdiv_(d, avg, value=-g["lr"])
+        fg.sync_lowp_from_master()
+
+
+def make_optimizer(name: str, params, **kw) -> _FusedFlatOptimizer:
+    """Factory used by the workload specs (``--optimizer SGD|Adam|AdamW|RMSprop``)."""
+    key = name.lower()
+    table = {"sgd": FusedSGD, "adam": FusedAdam, "adamw": FusedAdamW, "rmsprop": FusedRMSprop}
+    if key not in table:
+        raise ValueError(f"unknown optimizer {name!r}; expected one of {sorted(table)}")
+    return table[key](params, **kw)
