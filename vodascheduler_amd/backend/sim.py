@@ -1,0 +1,156 @@
+"""Discrete-event cluster backend: jobs progress along their scaling curves in virtual time.
+
+A job's work is ``epochs * epoch_time_1gpu`` one-GPU-seconds; on ``n`` GPUs it advances at
+``speedup(n)`` one-GPU-seconds per second.  Every start / resize / migration costs a pause
+(``resize_overhead_s`` for the elastic runtime's warm-worker path; a restart from a
+checkpoint after a halt costs ``restart_overhead_s``), so policies that churn pay for it.
+In ``oracle`` info mode the backend keeps each job's ``job_info`` record (remaining time,
+speedup table) current, which is what the metrics collector converges to on hardware.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass, field
+
+from ..common.store import JobStore, NotFound
+from ..common.types import MAX_NUM_GPU
+from ..sim.trace import PROFILES, ModelProfile, workload_of
+from .base import EV_FINISHED, HALT, MIGRATE, START, Backend, JobAction
+
+Loc = tuple[str, int]
+
+
+@dataclass
+class SimJob:
+    name: str
+    category: str
+    profile: ModelProfile
+    work: float                  # remaining one-GPU-seconds
+    total_work: float
+    epochs: int
+    n: int = 0
+    paused_until: float = 0.0
+    workers: list[Loc] = field(default_factory=list)
+    resizes: int = 0
+    migrations: int = 0
+
+    def rate(self, t: float) -> float:
+        return 0.0 if self.n == 0 or t < self.paused_until else self.profile.speedup(self.n)
+
+
+class SimBackend(Backend):
+    def __init__(self, clock, nodes: dict[str, list[int]] | None = None, store: JobStore | None = None,
+                 resize_overhead_s: float = 5.0, restart_overhead_s: float = 15.0, info_mode: str = "oracle"):
+        super().__init__()
+        self.clock = clock
+        self._nodes = nodes or {"node0": list(range(8))}
+        self.store = store
+        self.resize_overhead_s = resize_overhead_s
+        self.restart_overhead_s = restart_overhead_s
+        self.info_mode = info_mode
+        self.jobs: dict[str, SimJob] = {}
+        self.t_last = clock.now()
+        self.gpu_busy_seconds = 0.0
+        self.total_resizes = 0
+        self.total_migrations = 0
+
+    # ------------------------------------------------------------ time
+    def advance(self, t: float) -> None:
+        """Progress all jobs to time ``t`` and emit completions due by then."""
+        while True:
+            nxt = self.next_event()
+            if nxt is None or nxt > t:
+                self._progress(t)
+                break
+            self._progress(nxt)
+            for j in list(self.jobs.values()):
+                if j.n > 0 and j.work <= 1e-9:
+                    self._finish(j)
+
+    def _progress(self, t: float) -> None:
+        t0 = self.t_last
+        if t <= t0:
+            return
+        for j in self.jobs.values():
+            if j.n == 0:
+                continue
+            run_from = max(t0, j.paused_until)
+            if t > run_from:
+                j.work -= j.profile.speedup(j.n) * (t - run_from)
+            self.gpu_busy_seconds += j.n * (t - t0)
+        self.t_last = t
+
+    def next_event(self) -> float | None:
+        best = None
+        for j in self.jobs.values():
+            if j.n == 0:
+                continue
+            start = max(self.t_last, j.paused_until)
+            te = start + max(j.work, 0.0) / j.profile.speedup(j.n)
+            best = te if best is None else min(best, te)
+        return best
+
+    def _finish(self, j: SimJob) -> None:
+        j.n = 0
+        j.workers = []
+        self.jobs.pop(j.name, None)
+        self.emit(EV_FINISHED, j.name, True)
+
+    # ------------------------------------------------------------ Backend API
+    def apply(self, actions: list[JobAction]) -> None:
+        now = self.clock.now()
+        self.advance(now)
+        for a in actions:
+            name = a.job.name
+            j = self.jobs.get(name)
+            if j is None:
+                wl = workload_of(a.job.spec)
+                prof = PROFILES.get(wl["model"], ModelProfile(wl["model"], wl.get("alpha", 0.05), 0.05))
+                if "alpha" in wl:
+                    prof = ModelProfile(prof.name, float(wl["alpha"]), prof.step_time_1gpu)
+                total = float(wl["epoch_time_1gpu"]) * max(1, a.job.config.epochs)
+                j = SimJob(name, a.job.job_category, prof, total, total, a.job.config.epochs)
+                self.jobs[name] = j
+            if a.kind == HALT:
+                j.n = 0
+                j.workers = []
+                continue
+            overhead = self.restart_overhead_s if a.kind == START else self.resize_overhead_s
+            if a.kind == MIGRATE:
+                j.migrations += 1
+                self.total_migrations += 1
+            j.resizes += 1
+            self.total_resizes += 1
+            j.n = a.num_workers
+            j.workers = list(a.workers or [])
+            j.paused_until = now + overhead
+        if self.info_mode == "oracle":
+            self.publish_info()
+
+    def publish_info(self) -> None:
+        if self.store is None:
+            return
+        for j in self.jobs.values():
+            sp = {str(i): j.profile.speedup(i) for i in range(0, MAX_NUM_GPU + 2)}
+            try:
+                self.store.update_job_info(j.category, j.name, {
+                    "estimated_remainning_time_sec": max(j.work, 0.0),
+                    "speedup": sp,
+                    "efficiency": {k: (v / int(k) if int(k) else 0.0) for k, v in sp.items()},
+                })
+            except NotFound:
+                pass
+
+    def delete_job(self, job_name):
+        self.jobs.pop(job_name, None)
+
+    def nodes(self):
+        return {k: list(v) for k, v in self._nodes.items()}
+
+    def set_nodes(self, nodes: dict[str, list[int]]) -> None:
+        from .base import EV_NODES
+
+        self._nodes = {k: list(v) for k, v in nodes.items()}
+        self.emit(EV_NODES, self.nodes())
+
+    def list_running(self):
+        return {n: list(j.workers) for n, j in self.jobs.items() if j.n > 0}

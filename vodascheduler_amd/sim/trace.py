@@ -1,0 +1,141 @@
+"""Synthetic Philly-style job traces (BASELINE.json: "32-job Philly-style synthetic trace").
+
+The reference publishes no trace or numbers; this generator follows the
+published shape of the Microsoft Philly workload: Poisson arrivals, mostly small jobs
+(1-GPU dominated, power-of-two requests), heavy-tailed (log-normal) durations.  Each job
+is an MPIJob-shaped spec with the reference's launcher env knobs (NP / MIN_NP / MAX_NP /
+EPOCHS) plus a ``vodascheduler/workload`` annotation that the simulator and the GPU pool
+backend read: the model, the per-epoch time on one GPU and its scaling curve.
+"""
+from __future__ import annotations
+
+import json
+import math
+import random
+from dataclasses import dataclass
+
+from ..common.types import DEFAULT_GPU_TYPE, GPU_NAME_LABEL, GPU_RESOURCE
+
+WORKLOAD_ANNOTATION = "vodascheduler/workload"
+
+
+@dataclass
+class ModelProfile:
+    """Scaling model of a workload: speedup(n) = n / (1 + alpha * (n - 1)) (Amdahl-like
+    communication share alpha).  Defaults are calibrated from MI355X measurements where
+    available (see docs/PERFORMANCE.md)."""
+
+    name: str
+    alpha: float
+    step_time_1gpu: float  # seconds per step at the per-GPU batch on one GPU
+
+    def speedup(self, n: int) -> float:
+        if n <= 0:
+            return 0.0
+        return n / (1.0 + self.alpha * (n - 1))
+
+
+PROFILES = {
+    "resnet50": ModelProfile("resnet50", alpha=0.03, step_time_1gpu=0.043),
+    "bert-base": ModelProfile("bert-base", alpha=0.05, step_time_1gpu=0.060),
+    "vgg16": ModelProfile("vgg16", alpha=0.08, step_time_1gpu=0.030),
+    "transformer": ModelProfile("transformer", alpha=0.10, step_time_1gpu=0.020),
+    "mnist": ModelProfile("mnist", alpha=0.30, step_time_1gpu=0.004),
+}
+
+
+def speedup_table(profile: ModelProfile, max_gpu: int = 32) -> dict[str, float]:
+    return {str(i): profile.speedup(i) for i in range(0, max_gpu + 2)}
+
+
+def make_spec(name: str, model: str, np_: int, min_np: int, max_np: int, epochs: int, steps_per_epoch: int,
+              gpu_type: str = DEFAULT_GPU_TYPE, priority: int | None = None, per_gpu_batch: int | None = None,
+              epoch_time_1gpu: float | None = None) -> dict:
+    prof = PROFILES[model]
+    env = [{"name": "JOB_NAME", "value": name}, {"name": "NP", "value": str(np_)},
+           {"name": "MIN_NP", "value": str(min_np)}, {"name": "MAX_NP", "value": str(max_np)},
+           {"name": "EPOCHS", "value": str(epochs)}]
+    if priority is not None:
+        env.append({"name": "JOB_PRIORITY", "value": str(priority)})
+    wl = {"model": model, "steps_per_epoch": steps_per_epoch,
+          "epoch_time_1gpu": epoch_time_1gpu if epoch_time_1gpu is not None else steps_per_epoch * prof.step_time_1gpu,
+          "alpha": prof.alpha}
+    if per_gpu_batch is not None:
+        wl["per_gpu_batch"] = per_gpu_batch
+    cmd = (f"vodarun --min-np $(MIN_NP) --max-np $(MAX_NP) python -m vodascheduler_amd.workloads.train "
+           f"--model {model} --epochs $(EPOCHS) --steps-per-epoch {steps_per_epoch} --name $(JOB_NAME)")
+    return {
+        "apiVersion": "kubeflow.org/v1",
+        "kind": "MPIJob",
+        "metadata": {"name": name, "annotations": {WORKLOAD_ANNOTATION: json.dumps(wl)}},
+        "spec": {
+            "slotsPerWorker": 1,
+            "cleanPodPolicy": "Running",
+            "mpiReplicaSpecs": {
+                "Launcher": {"replicas": 1, "template": {"spec": {"containers": [
+                    {"name": "launcher", "image": "vodascheduler-amd:latest", "env": env,
+                     "command": ["/bin/bash", "-c"], "args": [cmd]}]}}},
+                "Worker": {"replicas": np_, "template": {"spec": {
+                    "containers": [{"name": "worker", "image": "vodascheduler-amd:latest",
+                                    "resources": {"limits": {GPU_RESOURCE: 1}}}],
+                    "nodeSelector": {GPU_NAME_LABEL: gpu_type}}}},
+            },
+        },
+    }
+
+
+def workload_of(spec: dict) -> dict:
+    ann = (spec.get("metadata", {}).get("annotations") or {}).get(WORKLOAD_ANNOTATION)
+    if not ann:
+        raise KeyError("job spec has no workload annotation")
+    return json.loads(ann)
+
+
+@dataclass
+class TraceJob:
+    submit_time: float
+    spec: dict
+
+    @property
+    def name(self) -> str:
+        return self.spec["metadata"]["name"]
+
+
+def philly_trace(n_jobs: int = 32, seed: int = 0, mean_interarrival_s: float = 30.0,
+                 mean_duration_1gpu_s: float = 600.0, max_gpus: int = 8,
+                 models: tuple[str, ...] = ("resnet50", "bert-base", "vgg16", "transformer"),
+                 elastic: bool = True, duration_scale: float = 1.0) -> list[TraceJob]:
+    """Generate ``n_jobs`` jobs.  Sizes: 1 GPU 50 %, 2 GPUs 25 %, 4 GPUs 15 %, 8 GPUs 10 %
+    (capped at ``max_gpus``); durations log-normal (sigma 1.0) around the mean GPU-time."""
+    rng = random.Random(seed)
+    sizes, weights = [1, 2, 4, 8], [0.50, 0.25, 0.15, 0.10]
+    t = 0.0
+    out = []
+    for i in range(n_jobs):
+        if i > 0:
+            t += rng.expovariate(1.0 / mean_interarrival_s)
+        np_ = min(rng.choices(sizes, weights)[0], max_gpus)
+        model = models[i % len(models)]
+        prof = PROFILES[model]
+        gpu_seconds = rng.lognormvariate(math.log(mean_duration_1gpu_s) - 0.5, 1.0) * duration_scale
+        gpu_seconds = max(gpu_seconds, 20 * prof.step_time_1gpu)
+        epochs = max(1, min(20, int(round(gpu_seconds / 60.0)) or 1))
+        steps_per_epoch = max(1, int(round(gpu_seconds / epochs / prof.step_time_1gpu)))
+        min_np = 1 if elastic else np_
+        max_np = min(max_gpus, max(np_ * 2, 2)) if elastic else np_
+        name = f"{model}-j{i:02d}"
+        out.append(TraceJob(t, make_spec(name, model, np_, min_np, max_np, epochs, steps_per_epoch)))
+    return out
+
+
+def scale_trace(trace: list[TraceJob], work_scale: float) -> list[TraceJob]:
+    """Multiply every job's work (steps per epoch) by ``work_scale`` (weak scaling over N GPUs)."""
+    out = []
+    for tj in trace:
+        spec = json.loads(json.dumps(tj.spec))
+        wl = workload_of(spec)
+        wl["steps_per_epoch"] = max(1, int(round(wl["steps_per_epoch"] * work_scale)))
+        wl["epoch_time_1gpu"] = wl["epoch_time_1gpu"] * work_scale
+        spec["metadata"]["annotations"][WORKLOAD_ANNOTATION] = json.dumps(wl)
+        out.append(TraceJob(tj.submit_time, spec))
+    return out
