@@ -1,0 +1,140 @@
+"""Small/medium convnets of the reference workloads.
+
+* ``vgg16_cifar``: ``applications.VGG16(weights=None, classes=10)`` at 32x32 (reference
+  examples/py/tensorflow2/tensorflow2_keras_cifar_elastic.py:148-151; 33,638,218 params as
+  counted in SURVEY.md §2.8: conv 14.7 M + FC 18.9 M).
+* ``KerasMnistCNN``: Conv32-Conv64-MaxPool-Dense128-Dense10 (reference
+  tensorflow2_keras_mnist_elastic.py:101-110; 1,199,882 params).
+* ``TorchMnistNet``: the PyTorch elastic example's 2-conv Net (reference
+  examples/py/pytorch/pytorch_mnist_elastic.py:80-96; 21,840 params).
+* ``inception_v3``: InceptionV3 at 75x75 for CIFAR (reference
+  tf2-keras-cifar10-inceptionv3-elastic.yaml).
+"""
+from __future__ import annotations
+
+import torch
+import torch.nn.functional as F
+from torch import nn
+
+
+def _vgg_block(cin, cout, n):
+    layers = []
+    for i in range(n):
+        layers += [nn.Conv2d(cin if i == 0 else cout, cout, 3, padding=1), nn.ReLU(inplace=True)]
+    layers.append(nn.MaxPool2d(2))
+    return layers
+
+
+class VGG16(nn.Module):
+    def __init__(self, num_classes=10, input_size=32):
+        super().__init__()
+        self.features = nn.Sequential(*_vgg_block(3, 64, 2), *_vgg_block(64, 128, 2), *_vgg_block(128, 256, 3),
+                                      *_vgg_block(256, 512, 3), *_vgg_block(512, 512, 3))
+        s = input_size // 32
+        self.classifier = nn.Sequential(nn.Flatten(), nn.Linear(512 * s * s, 4096), nn.ReLU(inplace=True),
+                                        nn.Linear(4096, 4096), nn.ReLU(inplace=True), nn.Linear(4096, num_classes))
+
+    def forward(self, x):
+        return self.classifier(self.features(x))
+
+
+def vgg16_cifar(num_classes=10):
+    return VGG16(num_classes, 32)
+
+
+class KerasMnistCNN(nn.Module):
+    def __init__(self):
+        super().__init__()
+        self.c1 = nn.Conv2d(1, 32, 3)
+        self.c2 = nn.Conv2d(32, 64, 3)
+        self.fc1 = nn.Linear(64 * 12 * 12, 128)
+        self.fc2 = nn.Linear(128, 10)
+
+    def forward(self, x):
+        x = F.relu(self.c1(x))
+        x = F.max_pool2d(F.relu(self.c2(x)), 2)
+        return self.fc2(F.relu(self.fc1(torch.flatten(x, 1))))
+
+
+class TorchMnistNet(nn.Module):
+    def __init__(self):
+        super().__init__()
+        self.conv1 = nn.Conv2d(1, 10, kernel_size=5)
+        self.conv2 = nn.Conv2d(10, 20, kernel_size=5)
+        self.fc1 = nn.Linear(320, 50)
+        self.fc2 = nn.Linear(50, 10)
+
+    def forward(self, x):
+        x = F.relu(F.max_pool2d(self.conv1(x), 2))
+        x = F.relu(F.max_pool2d(self.conv2(x), 2))
+        x = F.relu(self.fc1(x.view(-1, 320)))
+        return F.log_softmax(self.fc2(x), dim=1)
+
+
+# ----------------------------------------------------------------- InceptionV3 (compact)
+class BasicConv(nn.Module):
+    def __init__(self, cin, cout, **kw):
+        super().__init__()
+        self.conv = nn.Conv2d(cin, cout, bias=False, **kw)
+        self.bn = nn.BatchNorm2d(cout, eps=0.001)
+
+    def forward(self, x):
+        return F.relu(self.bn(self.conv(x)), inplace=True)
+
+
+class InceptionA(nn.Module):
+    def __init__(self, cin, pool):
+        super().__init__()
+        self.b1 = BasicConv(cin, 64, kernel_size=1)
+        self.b5 = nn.Sequential(BasicConv(cin, 48, kernel_size=1), BasicConv(48, 64, kernel_size=5, padding=2))
+        self.b3 = nn.Sequential(BasicConv(cin, 64, kernel_size=1), BasicConv(64, 96, kernel_size=3, padding=1),
+                                BasicConv(96, 96, kernel_size=3, padding=1))
+        self.bp = BasicConv(cin, pool, kernel_size=1)
+
+    def forward(self, x):
+        return torch.cat([self.b1(x), self.b5(x), self.b3(x), self.bp(F.avg_pool2d(x, 3, 1, 1))], 1)
+
+
+class InceptionB(nn.Module):
+    def __init__(self, cin):
+        super().__init__()
+        self.b3 = BasicConv(cin, 384, kernel_size=3, stride=2)
+        self.bd = nn.Sequential(BasicConv(cin, 64, kernel_size=1), BasicConv(64, 96, kernel_size=3, padding=1),
+                                BasicConv(96, 96, kernel_size=3, stride=2))
+
+    def forward(self, x):
+        return torch.cat([self.b3(x), self.bd(x), F.max_pool2d(x, 3, 2)], 1)
+
+
+class InceptionC(nn.Module):
+    def __init__(self, cin, c7):
+        super().__init__()
+        self.b1 = BasicConv(cin, 192, kernel_size=1)
+        self.b7 = nn.Sequential(BasicConv(cin, c7, kernel_size=1), BasicConv(c7, c7, kernel_size=(1, 7), padding=(0, 3)),
+                                BasicConv(c7, 192, kernel_size=(7, 1), padding=(3, 0)))
+        self.bd = nn.Sequential(BasicConv(cin, c7, kernel_size=1), BasicConv(c7, c7, kernel_size=(7, 1), padding=(3, 0)),
+                                BasicConv(c7, c7, kernel_size=(1, 7), padding=(0, 3)),
+                                BasicConv(c7, c7, kernel_size=(7, 1), padding=(3, 0)),
+                                BasicConv(c7, 192, kernel_size=(1, 7), padding=(0, 3)))
+        self.bp = BasicConv(cin, 192, kernel_size=1)
+
+    def forward(self, x):
+        return torch.cat([self.b1(x), self.b7(x), self.bd(x), self.bp(F.avg_pool2d(x, 3, 1, 1))], 1)
+
+
+class InceptionV3(nn.Module):
+    """InceptionV3 trunk (A/B/C stages) + head; sized for 75x75 inputs."""
+
+    def __init__(self, num_classes=10):
+        super().__init__()
+        self.stem = nn.Sequential(BasicConv(3, 32, kernel_size=3, stride=2), BasicConv(32, 32, kernel_size=3),
+                                  BasicConv(32, 64, kernel_size=3, padding=1), nn.MaxPool2d(3, 2),
+                                  BasicConv(64, 80, kernel_size=1), BasicConv(80, 192, kernel_size=3))
+        self.a = nn.Sequential(InceptionA(192, 32), InceptionA(256, 64), InceptionA(288, 64))
+        self.b = InceptionB(288)
+        self.c = nn.Sequential(InceptionC(768, 128), InceptionC(768, 160), InceptionC(768, 160), InceptionC(768, 192))
+        self.fc = nn.Linear(768, num_classes)
+
+    def forward(self, x):
+        x = self.c(self.b(self.a(self.stem(x))))
+        return self.fc(torch.flatten(F.adaptive_avg_pool2d(x, 1), 1))

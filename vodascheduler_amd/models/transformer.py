@@ -1,0 +1,75 @@
+"""Transformer NMT (eng->spa) and BERT-base.
+
+* ``TransformerNMT``: the reference's Keras example (reference
+  examples/py/tensorflow2/neural_machine_translation_with_transformer.py:89-94,191-315):
+  vocab 15000, sequence length 20, embedding 256, FFN 2048, 8 heads with key_dim 256,
+  1 encoder + 1 decoder layer, token + position embeddings, softmax head over the vocab.
+* ``BertBase``: BERT-base encoder (12 x [768, 12 heads, FFN 3072], seq 128-512) with an MLM
+  head -- the BASELINE.json "mixed ResNet-50 + BERT-base" AFS-L config.
+"""
+from __future__ import annotations
+
+import torch
+from torch import nn
+
+from ..ops.layernorm import FusedLayerNorm
+from .layers import DecoderLayer, EncoderLayer
+
+
+class PositionalEmbedding(nn.Module):
+    def __init__(self, seq_len: int, vocab: int, dim: int):
+        super().__init__()
+        self.tok = nn.Embedding(vocab, dim)
+        self.pos = nn.Embedding(seq_len, dim)
+
+    def forward(self, ids):
+        pos = torch.arange(ids.shape[1], device=ids.device)
+        return self.tok(ids) + self.pos(pos)[None]
+
+
+class TransformerNMT(nn.Module):
+    def __init__(self, vocab: int = 15000, seq_len: int = 20, d_model: int = 256, d_ff: int = 2048,
+                 heads: int = 8, key_dim: int = 256, layers: int = 1, dropout: float = 0.0):
+        super().__init__()
+        self.src_emb = PositionalEmbedding(seq_len, vocab, d_model)
+        self.tgt_emb = PositionalEmbedding(seq_len, vocab, d_model)
+        self.enc = nn.ModuleList([EncoderLayer(d_model, heads, d_ff, key_dim, dropout=dropout) for _ in range(layers)])
+        self.dec = nn.ModuleList([DecoderLayer(d_model, heads, d_ff, key_dim, dropout=dropout) for _ in range(layers)])
+        self.head = nn.Linear(d_model, vocab)
+
+    def forward(self, src, tgt):
+        src_mask = (src != 0)
+        x = self.src_emb(src)
+        for l in self.enc:
+            x = l(x, key_mask=src_mask)
+        y = self.tgt_emb(tgt)
+        for l in self.dec:
+            y = l(y, x, tgt_mask=(tgt != 0), src_mask=src_mask)
+        return self.head(y)
+
+
+class BertBase(nn.Module):
+    def __init__(self, vocab: int = 30522, seq_len: int = 128, d_model: int = 768, heads: int = 12,
+                 d_ff: int = 3072, layers: int = 12, dropout: float = 0.0):
+        super().__init__()
+        self.emb = PositionalEmbedding(seq_len, vocab, d_model)
+        self.type_emb = nn.Embedding(2, d_model)
+        self.emb_ln = FusedLayerNorm(d_model, eps=1e-12)
+        self.layers = nn.ModuleList([EncoderLayer(d_model, heads, d_ff, act="gelu", dropout=dropout, eps=1e-12)
+                                     for _ in range(layers)])
+        self.mlm_dense = nn.Linear(d_model, d_model)
+        self.mlm_ln = FusedLayerNorm(d_model, eps=1e-12)
+        self.mlm_out = nn.Linear(d_model, vocab)
+        self.mlm_out.weight = self.emb.tok.weight  # tied embeddings, as in BERT
+        self.act = nn.GELU(approximate="tanh")
+        for m in self.modules():
+            if isinstance(m, (nn.Linear, nn.Embedding)):
+                nn.init.normal_(m.weight, std=0.02)
+            if isinstance(m, nn.Linear) and m.bias is not None:
+                nn.init.zeros_(m.bias)
+
+    def forward(self, ids, attention_mask=None):
+        x = self.emb_ln(self.emb(ids) + self.type_emb.weight[0])
+        for l in self.layers:
+            x = l(x, key_mask=attention_mask)
+        return self.mlm_out(self.mlm_ln(self.act(self.mlm_dense(x))))

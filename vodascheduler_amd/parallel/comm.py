@@ -1,0 +1,244 @@
+"""Communicators for elastic data parallelism.
+
+* :class:`RcclCommunicator` -- the native engine (csrc/hip/comm.cpp): one RCCL communicator
+  per (job, membership epoch) over xGMI, non-blocking init bounded by a timeout, abortable
+  from a watchdog thread, collectives enqueued on an explicit HIP stream.
+* :class:`GlooCommunicator` -- c10d ProcessGroupGloo built directly on the job's store
+  prefix (no global default group, so a process can leave one job and join another):
+  the CPU path used by tests and the simulated-cluster config.
+
+Both expose the same surface: ``allreduce_``, ``broadcast_``, ``allgather``, ``barrier``,
+``abort``, ``destroy`` and ``rank``/``size``.  The rendezvous (unique-id exchange) goes
+through a c10d ``Store`` under a per-epoch key prefix.
+"""
+from __future__ import annotations
+
+import datetime
+import os
+import time
+
+import torch
+import torch.distributed as dist
+
+from ..ops import _native as N
+
+OPS = {"sum": 0, "avg": 1, "max": 2, "min": 3, "prod": 4}
+_GLOO_OPS = {"sum": dist.ReduceOp.SUM, "max": dist.ReduceOp.MAX, "min": dist.ReduceOp.MIN,
+             "prod": dist.ReduceOp.PRODUCT, "avg": dist.ReduceOp.SUM}
+
+
+class CommError(RuntimeError):
+    """A collective failed or was aborted (peer died / membership changed)."""
+
+
+def store_get(store: dist.Store, key: str, timeout: float) -> bytes:
+    """Blocking get with an explicit timeout (c10d get blocks up to the store timeout)."""
+    deadline = time.monotonic() + timeout
+    while True:
+        try:
+            if store.check([key]):
+                return store.get(key)
+        except RuntimeError:
+            pass
+        if time.monotonic() > deadline:
+            raise TimeoutError(f"store key {key!r} not published within {timeout:.0f}s")
+        time.sleep(0.01)
+
+
+class Communicator:
+    rank: int
+    size: int
+    device: torch.device
+
+    def allreduce_(self, t: torch.Tensor, op: str = "sum") -> torch.Tensor: ...
+    def broadcast_(self, t: torch.Tensor, root: int = 0) -> torch.Tensor: ...
+    def allgather(self, t: torch.Tensor) -> torch.Tensor: ...
+    def barrier(self) -> None: ...
+    def abort(self) -> None: ...
+    def destroy(self) -> None: ...
+
+    @property
+    def alive(self) -> bool:
+        return True
+
+
+class RcclCommunicator(Communicator):
+    def __init__(self, store: dist.Store, prefix: str, rank: int, size: int, device: torch.device,
+                 timeout: float = 300.0, stream: torch.cuda.Stream | None = None):
+        self.rank, self.size, self.device = rank, size, device
+        h = N.hip()
+        key = f"{prefix}/rccl_uid"
+        if rank == 0:
+            uid = h.rccl_unique_id()
+            store.set(key, uid)
+        else:
+            uid = store_get(store, key, timeout)
+        with torch.cuda.device(device):
+            self._c = h.RcclComm(uid, size, rank, device.index if device.index is not None else
+                                 torch.cuda.current_device(), timeout)
+        self.stream = stream
+
+    def _s(self) -> int:
+        s = self.stream if self.stream is not None else torch.cuda.current_stream(self.device)
+        return s.cuda_stream
+
+    def _chk(self, t: torch.Tensor) -> None:
+        if not t.is_cuda or not t.is_contiguous():
+            raise ValueError("RCCL collectives need contiguous GPU tensors")
+
+    def allreduce_(self, t, op="sum"):
+        self._chk(t)
+        try:
+            self._c.allreduce(t.data_ptr(), t.data_ptr(), t.numel(), N.comm_dtype_code(t.dtype), OPS[op], self._s())
+        except RuntimeError as e:
+            raise CommError(str(e)) from e
+        return t
+
+    def broadcast_(self, t, root=0):
+        self._chk(t)
+        try:
+            self._c.broadcast(t.data_ptr(), t.data_ptr(), t.numel(), N.comm_dtype_code(t.dtype), root, self._s())
+        except RuntimeError as e:
+            raise CommError(str(e)) from e
+        return t
+
+    def allgather(self, t):
+        self._chk(t)
+        out = torch.empty((self.size,) + tuple(t.shape), dtype=t.dtype, device=t.device)
+        try:
+            self._c.allgather(t.data_ptr(), out.data_ptr(), t.numel(), N.comm_dtype_code(t.dtype), self._s())
+        except RuntimeError as e:
+            raise CommError(str(e)) from e
+        return out
+
+    def group_start(self):
+        self._c.group_start()
+
+    def group_end(self):
+        self._c.group_end()
+
+    def barrier(self):
+        x = torch.ones(1, device=self.device)
+        self.allreduce_(x)
+        torch.cuda.current_stream(self.device).synchronize()
+        self.check()
+
+    def check(self) -> None:
+        err = self._c.async_error()
+        if err:
+            raise CommError(f"RCCL communicator error: {err}")
+
+    def abort(self):
+        self._c.abort()
+
+    def destroy(self):
+        self._c.destroy()
+
+    @property
+    def alive(self):
+        return self._c.alive
+
+
+class GlooCommunicator(Communicator):
+    def __init__(self, store: dist.Store, prefix: str, rank: int, size: int, timeout: float = 300.0):
+        os.environ.setdefault("GLOO_SOCKET_IFNAME", "lo")
+        self.rank, self.size, self.device = rank, size, torch.device("cpu")
+        self._pg = dist.ProcessGroupGloo(dist.PrefixStore(prefix + "/gloo", store), rank, size,
+                                         datetime.timedelta(seconds=timeout))
+        self._aborted = False
+
+    def _run(self, work):
+        try:
+            work.wait()
+        except RuntimeError as e:
+            raise CommError(str(e)) from e
+
+    def allreduce_(self, t, op="sum"):
+        if self._aborted:
+            raise CommError("communicator aborted")
+        opts = dist.AllreduceOptions()
+        opts.reduceOp = _GLOO_OPS[op]
+        self._run(self._pg.allreduce([t], opts))
+        if op == "avg":
+            t.div_(self.size)
+        return t
+
+    def broadcast_(self, t, root=0):
+        if self._aborted:
+            raise CommError("communicator aborted")
+        opts = dist.BroadcastOptions()
+        opts.rootRank = root
+        self._run(self._pg.broadcast([t], opts))
+        return t
+
+    def allgather(self, t):
+        if self._aborted:
+            raise CommError("communicator aborted")
+        outs = [torch.empty_like(t) for _ in range(self.size)]
+        self._run(self._pg.allgather([outs], [t]))
+        return torch.stack(outs)
+
+    def barrier(self):
+        self.allreduce_(torch.ones(1))
+
+    def check(self):
+        pass
+
+    def abort(self):
+        self._aborted = True
+        try:
+            self._pg.abort()
+        except Exception:
+            pass
+
+    def destroy(self):
+        try:
+            self._pg.shutdown()
+        except Exception:
+            pass
+
+    @property
+    def alive(self):
+        return not self._aborted
+
+
+class LocalCommunicator(Communicator):
+    """World of one: every collective is the identity (1-GPU jobs skip RCCL entirely)."""
+
+    def __init__(self, device: torch.device):
+        self.rank, self.size, self.device = 0, 1, device
+
+    def allreduce_(self, t, op="sum"):
+        return t
+
+    def broadcast_(self, t, root=0):
+        return t
+
+    def allgather(self, t):
+        return t.unsqueeze(0).clone()
+
+    def barrier(self):
+        pass
+
+    def check(self):
+        pass
+
+    def abort(self):
+        pass
+
+    def destroy(self):
+        pass
+
+
+def create_communicator(store: dist.Store, prefix: str, rank: int, size: int, device: torch.device,
+                        backend: str = "auto", timeout: float = 300.0,
+                        stream: torch.cuda.Stream | None = None) -> Communicator:
+    if size == 1:
+        return LocalCommunicator(device)
+    if backend == "auto":
+        backend = "rccl" if device.type == "cuda" else "gloo"
+    if backend == "rccl":
+        return RcclCommunicator(store, prefix, rank, size, device, timeout, stream)
+    if backend == "gloo":
+        return GlooCommunicator(store, prefix, rank, size, timeout)
+    raise ValueError(f"unknown comm backend {backend!r}")

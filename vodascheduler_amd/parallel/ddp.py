@@ -1,0 +1,225 @@
+"""Bucketed gradient all-reduce overlapped with backward (Horovod DistributedOptimizer
+replacement; reference hvd.DistributedOptimizer(op=hvd.Average) in
+examples/py/pytorch/pytorch_mnist_elastic.py:185-188).
+
+MI355X-first design:
+* gradients live in ONE flat buffer per parameter group (the fused optimizer's
+  ``FlatGroup``, or a grad-only one), so a bucket is a contiguous SLICE -- no fusion-buffer
+  copy on the hot path;
+* buckets cover the flat buffer back-to-front (the order gradients become ready in
+  backward) and are cut at parameter boundaries to ``bucket_cap_mb`` (default 64 MB: an
+  8-GPU ring on 7 xGMI links needs >~43 MB per collective to amortise per-step latency,
+  SURVEY.md §5.8; the first bucket is kept small so communication starts early);
+* a post-accumulate-grad hook counts ready parameters; a full bucket is enqueued on a
+  dedicated HIP stream (ordered after the producing compute via a stream wait), strictly in
+  bucket order on every rank (collective order must match across ranks);
+* averaging folds into the collective (RCCL ncclAvg) or, with ``compression='bf16'|'fp16'``
+  (Horovod's fp16 compression), into the HIP cast kernel that packs the comm buffer
+  (scale 1/N) -- halving xGMI bytes;
+* ``finalize()`` flushes buckets whose parameters got no gradient this step (zeros) and makes
+  the compute stream wait for the comm stream before the optimizer step.
+"""
+from __future__ import annotations
+
+from contextlib import contextmanager
+from dataclasses import dataclass
+
+import torch
+
+from ..ops.bucket import cast_scale_
+from ..utils.flat import FlatGroup
+from .comm import Communicator, LocalCommunicator
+
+_COMPRESS = {None: None, "none": None, "bf16": torch.bfloat16, "fp16": torch.float16}
+
+
+@dataclass
+class Bucket:
+    group: int
+    start: int           # element offset in the group's flat grad buffer
+    end: int
+    params: list[torch.nn.Parameter]
+    pending: int = 0
+    launched: bool = False
+    comm_buf: torch.Tensor | None = None
+
+    @property
+    def numel(self) -> int:
+        return self.end - self.start
+
+
+class ElasticDDP:
+    def __init__(self, model: torch.nn.Module, comm: Communicator, optimizer=None, bucket_cap_mb: float = 64.0,
+                 first_bucket_mb: float = 8.0, compression: str | None = None):
+        self.model = model
+        self.comm = comm
+        self.optimizer = optimizer
+        self.compress_dtype = _COMPRESS[compression]
+        if optimizer is not None and hasattr(optimizer, "flat_groups"):
+            self.groups: list[FlatGroup] = list(optimizer.flat_groups)
+        else:
+            params = [p for p in model.parameters() if p.requires_grad]
+            self.groups = [FlatGroup(params, flatten_params=False)]
+        self.device = self.groups[0].device
+        self.bucket_cap_mb = bucket_cap_mb
+        self.first_bucket_mb = first_bucket_mb
+        self._build_buckets()
+        self._hooks = []
+        self._sync = True
+        self._param_bucket: dict[int, Bucket] = {}
+        for b in self.buckets:
+            for p in b.params:
+                self._param_bucket[id(p)] = b
+        for g in self.groups:
+            for p in g.params:
+                if p.requires_grad:
+                    self._hooks.append(p.register_post_accumulate_grad_hook(self._on_grad))
+        self._next = 0
+        self.comm_stream = torch.cuda.Stream(self.device) if self.device.type == "cuda" else None
+        if comm is not None and hasattr(comm, "stream") and self.comm_stream is not None:
+            comm.stream = self.comm_stream
+        self._reset()
+
+    # ------------------------------------------------------------------ setup
+    def _build_buckets(self) -> None:
+        self.buckets: list[Bucket] = []
+        for gi, g in enumerate(self.groups):
+            esz = g.grad.element_size()
+            idx = list(range(len(g.params)))[::-1]  # back-to-front: backward order
+            cur: list[int] = []
+            cap = self.first_bucket_mb
+            for i in idx:
+                cur.append(i)
+                nbytes = (g.slots[cur[0]].offset + g.slots[cur[0]].numel - g.slots[i].offset) * esz
+                if nbytes >= cap * 2 ** 20:
+                    self._close(gi, cur)
+                    cur = []
+                    cap = self.bucket_cap_mb
+            if cur:
+                self._close(gi, cur)
+
+    def _close(self, gi: int, idxs: list[int]) -> None:
+        g = self.groups[gi]
+        lo = min(g.slots[i].offset for i in idxs)
+        hi_i = max(idxs, key=lambda i: g.slots[i].offset)
+        hi = g.slots[hi_i].offset + g.slots[hi_i].numel
+        # extend to the padded end so the bucket slices tile the flat buffer exactly
+        nxt = [g.slots[i].offset for i in range(len(g.params)) if g.slots[i].offset >= hi]
+        hi = min(nxt) if nxt else g.numel
+        self.buckets.append(Bucket(gi, lo, hi, [g.params[i] for i in idxs]))
+
+    def bucket_sizes_mb(self) -> list[float]:
+        return [b.numel * self.groups[b.group].grad.element_size() / 2 ** 20 for b in self.buckets]
+
+    @property
+    def world(self) -> int:
+        return 1 if self.comm is None else self.comm.size
+
+    def _reset(self) -> None:
+        self._next = 0
+        for b in self.buckets:
+            b.pending = sum(1 for p in b.params if p.requires_grad)
+            b.launched = False
+
+    # ------------------------------------------------------------------ hooks
+    def _on_grad(self, p: torch.nn.Parameter) -> None:
+        if not self._sync or self.world == 1:
+            return
+        b = self._param_bucket[id(p)]
+        b.pending -= 1
+        if b.pending == 0:
+            self._launch_ready()
+
+    def _launch_ready(self) -> None:
+        while self._next < len(self.buckets) and self.buckets[self._next].pending <= 0:
+            self._launch(self.buckets[self._next])
+            self._next += 1
+
+    def _launch(self, b: Bucket) -> None:
+        g = self.groups[b.group]
+        flat = g.grad[b.start:b.end]
+        if self.comm_stream is not None:
+            self.comm_stream.wait_stream(torch.cuda.current_stream(self.device))
+            ctx = torch.cuda.stream(self.comm_stream)
+        else:
+            ctx = _nullctx()
+        with ctx:
+            if self.compress_dtype is not None and flat.dtype != self.compress_dtype:
+                if b.comm_buf is None:
+                    b.comm_buf = torch.empty(b.numel, dtype=self.compress_dtype, device=flat.device)
+                cast_scale_(flat, b.comm_buf, 1.0 / self.world)
+                self.comm.allreduce_(b.comm_buf, "sum")
+                cast_scale_(b.comm_buf, flat, 1.0)
+            else:
+                self.comm.allreduce_(flat, "avg")
+        b.launched = True
+
+    # ------------------------------------------------------------------ API
+    def forward(self, *a, **kw):
+        return self.model(*a, **kw)
+
+    __call__ = forward
+
+    @contextmanager
+    def no_sync(self):
+        """Accumulate gradients locally (no all-reduce) inside the context."""
+        old = self._sync
+        self._sync = False
+        try:
+            yield
+        finally:
+            self._sync = old
+
+    def finalize(self) -> None:
+        """Flush remaining buckets in order and order the compute stream after them."""
+        if self.world > 1 and self._sync:
+            while self._next < len(self.buckets):
+                self._launch(self.buckets[self._next])
+                self._next += 1
+            if self.comm_stream is not None:
+                torch.cuda.current_stream(self.device).wait_stream(self.comm_stream)
+        self._reset()
+
+    def allreduce_gradients(self) -> None:
+        """Synchronous all-reduce of all gradients (no overlap); for debugging/tests."""
+        if self.world == 1:
+            return
+        for b in self.buckets:
+            b.pending = 0
+        self._launch_ready()
+        self.finalize()
+
+    def step(self) -> None:
+        self.finalize()
+        if self.optimizer is not None:
+            self.optimizer.step()
+
+    def zero_grad(self) -> None:
+        for g in self.groups:
+            g.zero_grad()
+        self._reset()
+
+    def set_communicator(self, comm: Communicator) -> None:
+        """Swap in the communicator of a new membership epoch (elastic resize)."""
+        self.comm = comm
+        if hasattr(comm, "stream") and self.comm_stream is not None:
+            comm.stream = self.comm_stream
+        self._reset()
+
+    def remove_hooks(self) -> None:
+        for h in self._hooks:
+            h.remove()
+        self._hooks = []
+
+
+@contextmanager
+def _nullctx():
+    yield
+
+
+def broadcast_tensors(comm: Communicator, tensors: list[torch.Tensor], root: int = 0) -> None:
+    """Broadcast a list of tensors from ``root`` (state sync on elastic resize)."""
+    if comm is None or isinstance(comm, LocalCommunicator) or comm.size == 1:
+        return
+    for t in tensors:
+        comm.broadcast_(t if t.is_contiguous() else t.contiguous(), root)

@@ -1,0 +1,93 @@
+"""Run a job trace end-to-end on a pool of real workers: training service -> scheduler
+(policy + Munkres placement) -> PoolBackend -> warm per-GPU workers running elastic DP.
+
+Used by ``bench.py`` (GPU pool = torchrun ranks, RCCL over xGMI) and by the CPU/gloo tests
+(BASELINE config 1: "Elastic-FIFO, 2 toy MNIST jobs on CPU/gloo, simulated 2-slot cluster").
+"""
+from __future__ import annotations
+
+import json
+import logging
+import socket
+import statistics
+import time
+
+import torch
+
+from ..allocator.allocator import ResourceAllocator
+from ..common.mq import InProcQueue
+from ..common.store import MemoryStore
+from ..common.types import DEFAULT_GPU_TYPE, JobStatus
+from ..scheduler.core import SchedulerCore
+from ..scheduler.runner import SchedulerRunner
+from ..service.service import TrainingService
+from ..sim.trace import TraceJob
+from .pool import PoolBackend, PoolWorker
+from .rendezvous import connect_store
+
+log = logging.getLogger("vodascheduler_amd.cluster")
+
+
+def free_port() -> int:
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def run_trace(store, trace: list[TraceJob], worker_locs, algorithm: str = "ElasticFIFO",
+              rate_limit_sec: float = 1.0, tick_sec: float = 1.0, train_defaults: dict | None = None,
+              timeout: float = 3600.0, gpu_type: str = DEFAULT_GPU_TYPE, progress=None) -> dict:
+    """Submit ``trace`` in real time (``submit_time`` seconds after start) and wait until every
+    job completed.  Returns JCT / makespan / resize-latency statistics."""
+    db = MemoryStore()
+    mq = InProcQueue(maxsize=10 ** 6)
+    svc = TrainingService(db, mq)
+    backend = PoolBackend(store, worker_locs, train_defaults)
+    core = SchedulerCore(gpu_type, db, ResourceAllocator(db), backend, algorithm=algorithm,
+                         rate_limit_sec=rate_limit_sec, tick_sec=tick_sec)
+    runner = SchedulerRunner(core, mq).start()
+    t0 = time.time()
+    names: list[str] = []
+    pending = sorted(trace, key=lambda tj: tj.submit_time)
+    last_report = t0
+    try:
+        while True:
+            now = time.time()
+            while pending and now - t0 >= pending[0].submit_time:
+                tj = pending.pop(0)
+                names.append(svc.create_training_job(json.dumps(tj.spec)))
+            done = runner.call(lambda: {n: j.status for n, j in core.done_jobs.items()})
+            if not pending and names and all(n in done for n in names):
+                break
+            if now - t0 > timeout:
+                raise TimeoutError(f"trace did not finish within {timeout}s ({len(done)}/{len(trace)} done)")
+            if progress is not None and now - last_report > 30:
+                last_report = now
+                progress(f"t={now - t0:.0f}s done={len(done)}/{len(trace)} running="
+                         f"{runner.call(lambda: {n: v for n, v in core.job_num_gpu.items() if v})}")
+            time.sleep(0.05)
+        t1 = time.time()
+        jobs = runner.call(lambda: {n: core.done_jobs[n].clone() for n in names})
+    finally:
+        runner.stop()
+        backend.shutdown()
+    failed = [n for n, j in jobs.items() if j.status != JobStatus.COMPLETED.value]
+    jct = {n: j.finish_timestamp - j.submit_timestamp for n, j in jobs.items()}
+    lat = sorted(r["latency_s"] for r in backend.resize_latency)
+    vals = sorted(jct.values())
+    q = lambda xs, p: xs[min(len(xs) - 1, int(p * len(xs)))] if xs else None  # noqa: E731
+    return {
+        "n_jobs": len(names), "failed": failed, "avg_jct_s": statistics.fmean(vals), "p50_jct_s": q(vals, 0.5),
+        "p95_jct_s": q(vals, 0.95), "makespan_s": max(j.finish_timestamp for j in jobs.values()) - t0,
+        "wall_s": t1 - t0, "resize_events": len(backend.events), "resize_latency_p50_s": q(lat, 0.5),
+        "resize_latency_p95_s": q(lat, 0.95), "reschedules": core.resched_count, "jct": jct,
+        "events": backend.events, "resize_latency": backend.resize_latency,
+    }
+
+
+def cpu_worker_main(host: str, port: int, wid: str, threads: int = 1) -> None:
+    """Entry point of a CPU pool worker process (tests / simulated cluster)."""
+    torch.set_num_threads(threads)
+    store = connect_store(host, port)
+    watch = connect_store(host, port)
+    PoolWorker(store, watch, wid, torch.device("cpu"), backend="gloo", timeout=120.0).serve()

@@ -1,0 +1,209 @@
+"""Warm per-GPU worker pool: the MI355X-native replacement of "MPI-Operator creates pods,
+kubelet starts containers, horovodrun discovers hosts" (SURVEY.md §3.1-3.2, §5.8 item 3).
+
+* :class:`PoolWorker` -- one long-lived process per GPU (a torchrun rank, or a process the
+  node agent started).  It keeps its HIP context, MIOpen/hipBLASLt caches and allocator pool
+  across jobs, reads job assignments from its mailbox in the store and runs them with the
+  elastic runtime; between jobs it only drops the model.
+* :class:`PoolBackend` -- the scheduler-side :class:`Backend`: turns start / scale / halt /
+  migrate actions into membership epochs (``JobRendezvous.publish``) + mailbox messages for
+  workers that join, watches job outcomes and reports completions, and measures elastic
+  resize latency (publish -> new membership synced and training).
+
+A resize therefore costs one communicator rebuild + one state broadcast, not pod creation.
+"""
+from __future__ import annotations
+
+import json
+import logging
+import threading
+import time
+from dataclasses import asdict
+
+import torch
+
+from ..backend.base import EV_FINISHED, HALT, Backend, JobAction
+from ..sim.trace import workload_of
+from ..workloads.train import TrainConfig, train_elastic
+from .elastic import ElasticContext
+from .rendezvous import JobRendezvous
+
+log = logging.getLogger("vodascheduler_amd.pool")
+
+Loc = tuple[str, int]
+
+
+def worker_id(loc: Loc) -> str:
+    return f"{loc[0]}:{loc[1]}"
+
+
+def job_train_config(job, defaults: dict | None = None) -> dict:
+    """TrainConfig (as a dict) for a job from its spec's workload annotation + env knobs."""
+    wl = workload_of(job.spec)
+    d = dict(model=wl["model"], epochs=max(1, job.config.epochs), steps_per_epoch=int(wl["steps_per_epoch"]))
+    if "per_gpu_batch" in wl:
+        d["per_gpu_batch"] = int(wl["per_gpu_batch"])
+    d.update(defaults or {})
+    return d
+
+
+class PoolBackend(Backend):
+    def __init__(self, store, worker_locs: list[Loc], train_defaults: dict | None = None,
+                 poll_interval: float = 0.05):
+        super().__init__()
+        self.store = store
+        self._lock = threading.Lock()
+        self.workers = [worker_id(l) for l in worker_locs]
+        self.node_gpus: dict[str, list[int]] = {}
+        for n, g in worker_locs:
+            self.node_gpus.setdefault(n, []).append(g)
+        self.train_defaults = dict(train_defaults or {})
+        self.members: dict[str, list[str]] = {}
+        self.active: set[str] = set()
+        self.published: dict[tuple[str, int], float] = {}
+        self.resize_latency: list[dict] = []
+        self.events: list[dict] = []
+        self._mail_n: dict[str, int] = {}
+        self._stop = threading.Event()
+        self._poll = poll_interval
+        self._mon = threading.Thread(target=self._monitor, daemon=True, name="pool-monitor")
+        self._mon.start()
+
+    # ------------------------------------------------------------------ Backend API
+    def apply(self, actions: list[JobAction]) -> None:
+        for a in actions:
+            self._apply_one(a)
+
+    def _apply_one(self, a: JobAction) -> None:
+        name = a.job.name
+        rdzv = JobRendezvous(self.store, name)
+        if a.kind == HALT:
+            new_members: list[str] = []
+        else:
+            if a.workers is None:
+                raise ValueError("PoolBackend needs placement (worker locations) for every action")
+            new_members = [worker_id(l) for l in a.workers]
+        old = self.members.get(name, [])
+        if new_members == old:
+            return
+        t = time.time()
+        e = rdzv.publish(new_members)
+        with self._lock:
+            self.members[name] = new_members
+            self.published[(name, e)] = t
+            if new_members:
+                self.active.add(name)
+            self.events.append({"t": t, "job": name, "epoch": e, "kind": a.kind, "world": len(new_members),
+                                "prev_world": len(old)})
+        cfg = job_train_config(a.job, self.train_defaults)
+        for wid in new_members:
+            if wid not in old:
+                self._mail(wid, {"job": name, "epoch": e, "cfg": cfg})
+
+    def _mail(self, wid: str, msg: dict) -> None:
+        n = self._mail_n.get(wid, 0) + 1
+        self._mail_n[wid] = n
+        self.store.set(f"pool/{wid}/msg/{n}", json.dumps(msg))
+        got = self.store.add(f"pool/{wid}/n", 1)
+        if got != n:
+            raise RuntimeError(f"mailbox counter mismatch for {wid}: {got} != {n}")
+
+    def delete_job(self, job_name: str) -> None:
+        rdzv = JobRendezvous(self.store, job_name)
+        if self.members.get(job_name):
+            rdzv.publish([])
+        rdzv.mark_done(False, "deleted")
+        with self._lock:
+            self.members.pop(job_name, None)
+            self.active.discard(job_name)
+
+    def nodes(self):
+        return {k: list(v) for k, v in self.node_gpus.items()}
+
+    def list_running(self):
+        return {j: [(m.rsplit(":", 1)[0], int(m.rsplit(":", 1)[1])) for m in mem]
+                for j, mem in self.members.items() if mem}
+
+    def shutdown(self) -> None:
+        self._stop.set()
+        self.store.set("pool/shutdown", "1")
+        self._mon.join(5)
+
+    # ------------------------------------------------------------------ monitor
+    def _monitor(self) -> None:
+        while not self._stop.is_set():
+            with self._lock:
+                jobs = list(self.active)
+                pend = [k for k in self.published if k not in {(r["job"], r["epoch"]) for r in self.resize_latency}]
+            for name in jobs:
+                out = JobRendezvous(self.store, name).outcome()
+                if out is not None:
+                    with self._lock:
+                        self.active.discard(name)
+                        self.members.pop(name, None)
+                    if out == "done":
+                        self.emit(EV_FINISHED, name, True)
+                    else:
+                        reason = JobRendezvous(self.store, name).get("failed")
+                        if reason != "deleted":
+                            self.emit(EV_FINISHED, name, False)
+            for (name, e) in pend:
+                r = JobRendezvous(self.store, name)
+                v = r.get(f"e/{e}/synced")
+                if v is not None:
+                    with self._lock:
+                        t0 = self.published[(name, e)]
+                        self.resize_latency.append({"job": name, "epoch": e, "latency_s": float(v) - t0})
+            self._stop.wait(self._poll)
+
+
+class PoolWorker:
+    """Serve job assignments on one device until ``pool/shutdown`` is set."""
+
+    def __init__(self, store, watch_store, wid: str, device: torch.device, backend: str = "auto",
+                 timeout: float = 600.0, idle_poll: float = 0.01):
+        self.store = store
+        self.watch_store = watch_store
+        self.wid = wid
+        self.device = device
+        self.backend = backend
+        self.timeout = timeout
+        self.idle_poll = idle_poll
+        self.done = 0
+        self.results: list[dict] = []
+
+    def serve(self) -> list[dict]:
+        while True:
+            n = int(self.store.add(f"pool/{self.wid}/n", 0))
+            if n > self.done:
+                self.done += 1
+                msg = json.loads(self.store.get(f"pool/{self.wid}/msg/{self.done}"))
+                self._run(msg)
+                continue
+            if self.store.check(["pool/shutdown"]):
+                return self.results
+            time.sleep(self.idle_poll)
+
+    def _run(self, msg: dict) -> None:
+        ctx = ElasticContext(self.store, msg["job"], self.wid, self.device, self.backend, self.timeout,
+                             watch_store=self.watch_store, join_epoch=int(msg["epoch"]))
+        cfg = TrainConfig(**msg["cfg"])
+        t0 = time.time()
+        try:
+            out = train_elastic(ctx, cfg)
+        except Exception as e:  # a failed job must not take the warm worker down
+            log.exception("worker %s: job %s failed", self.wid, msg["job"])
+            if ctx.rank == 0 or ctx.rank < 0:
+                ctx.rdzv.mark_done(False, f"{type(e).__name__}: {e}")
+            out = {"error": repr(e)}
+        finally:
+            ctx.stop()
+        rec = {"job": msg["job"], "wid": self.wid, "t0": t0, "t1": time.time(), "result": out,
+               "resize_log": ctx.resize_log}
+        self.results.append(rec)
+        if self.device.type == "cuda":
+            torch.cuda.synchronize(self.device)
+
+
+def train_config_dict(cfg: TrainConfig) -> dict:
+    return asdict(cfg)

@@ -41,6 +41,10 @@ PROFILES = {
     "vgg16": ModelProfile("vgg16", alpha=0.08, step_time_1gpu=0.030),
     "transformer": ModelProfile("transformer", alpha=0.10, step_time_1gpu=0.020),
     "mnist": ModelProfile("mnist", alpha=0.30, step_time_1gpu=0.004),
+    "mnist-torch": ModelProfile("mnist-torch", alpha=0.40, step_time_1gpu=0.002),
+    "resnet50-cifar": ModelProfile("resnet50-cifar", alpha=0.05, step_time_1gpu=0.020),
+    "resnet18": ModelProfile("resnet18", alpha=0.04, step_time_1gpu=0.020),
+    "inceptionv3": ModelProfile("inceptionv3", alpha=0.05, step_time_1gpu=0.030),
 }
 
 

@@ -1,0 +1,169 @@
+"""Elastic data-parallel training of a registered workload (the MI355X-native counterpart of
+the reference's Horovod elastic scripts).
+
+Per step: synthetic batch (fixed pool, real shapes) -> bf16 autocast forward/backward on
+PyTorch-ROCm (MIOpen/hipBLASLt + HIP LayerNorm/softmax kernels) -> bucketed all-reduce on
+RCCL over xGMI overlapped with backward -> fused HIP optimizer step on flat buffers.
+Elastic semantics follow the reference examples: LR = base_lr x world size on every reset
+(tensorflow2_keras_cifar_elastic.py:156,210), an epoch is a fixed number of samples split
+across the current workers (``steps_per_epoch // size``, :223), state committed every
+``commit_every`` steps, per-epoch CSV metrics + checkpoint on rank 0.
+
+Standalone (one process per GPU, launched by the local node agent):
+    python -m vodascheduler_amd.workloads.train --model resnet50 --epochs 2 --steps-per-epoch 50 \
+        --name JOB   (env: VODA_STORE=host:port, VODA_WORKER_ID, VODA_JOIN_EPOCH)
+"""
+from __future__ import annotations
+
+import argparse
+import logging
+import math
+import os
+import time
+from dataclasses import dataclass
+
+import torch
+
+from ..models import get_workload
+from ..ops.optim import make_optimizer
+from ..parallel.ddp import ElasticDDP
+from ..runtime.elastic import ElasticContext, TorchState, run
+from .metrics_logger import MetricsCSVLogger
+
+log = logging.getLogger("vodascheduler_amd.train")
+
+
+@dataclass
+class TrainConfig:
+    model: str
+    epochs: int = 1
+    steps_per_epoch: int = 10          # in single-GPU steps: epoch = steps_per_epoch * batch samples
+    per_gpu_batch: int | None = None
+    lr: float | None = None            # base LR for one worker (scaled x world)
+    commit_every: int = 1
+    amp: bool = True                   # bf16 autocast
+    compression: str | None = None     # gradient all-reduce compression: None | bf16 | fp16
+    bucket_cap_mb: float = 64.0
+    metrics_dir: str | None = None
+    checkpoint_every_epoch: bool = False
+    seed: int = 0
+    data_pool: int = 2                 # distinct synthetic batches cycled through
+
+
+def build(cfg: TrainConfig, device: torch.device):
+    w = get_workload(cfg.model)
+    torch.manual_seed(cfg.seed)  # identical init everywhere (state is broadcast anyway)
+    model = w.build().to(device)
+    if w.channels_last and device.type == "cuda":
+        model = model.to(memory_format=torch.channels_last)
+    kw = dict(w.opt_kwargs)
+    if cfg.lr is not None:
+        kw["lr"] = cfg.lr
+    opt = make_optimizer(w.optimizer, model.parameters(), **kw)
+    return w, model, opt, kw["lr"]
+
+
+def train_elastic(ctx: ElasticContext, cfg: TrainConfig) -> dict | None:
+    device = ctx.device
+    w, model, opt, base_lr = build(cfg, device)
+    bs = cfg.per_gpu_batch or w.per_gpu_batch
+    g = torch.Generator(device=device).manual_seed(cfg.seed + 1)
+    pool = []
+    for _ in range(max(1, cfg.data_pool)):
+        b = w.make_batch(bs, device, g)
+        if w.channels_last and device.type == "cuda":
+            b = tuple(t.to(memory_format=torch.channels_last) if t.dim() == 4 else t for t in b)
+        pool.append(b)
+    ddp = ElasticDDP(model, None, opt, bucket_cap_mb=cfg.bucket_cap_mb, compression=cfg.compression)
+    state = TorchState(ctx, model, opt, epoch=0, samples=0)
+    logger = MetricsCSVLogger(cfg.metrics_dir, ctx.job, cfg.epochs, bs)
+    samples_per_epoch = cfg.steps_per_epoch * bs
+    stats = {"steps": 0, "samples": 0, "train_time": 0.0, "model": cfg.model, "resizes": 0}
+
+    def on_reset():
+        stats["resizes"] += 1
+
+    state.register_reset_callbacks([on_reset])
+    amp = torch.autocast(device.type, dtype=torch.bfloat16, enabled=cfg.amp and device.type == "cuda")
+
+    @run
+    def train(state):
+        ddp.set_communicator(ctx.comm)
+        world = ctx.size
+        for gr in opt.param_groups:
+            gr["lr"] = base_lr * world
+        logger.set_params(world)
+        loss_t = None
+        while state.epoch < cfg.epochs:
+            t_ep = time.time()
+            steps = 0
+            while state.samples < samples_per_epoch:
+                batch = pool[state.step % len(pool)]
+                ddp.zero_grad()
+                with amp:
+                    loss = w.loss(model, batch)
+                loss.backward()
+                ddp.step()
+                loss_t = loss.detach()
+                state.samples += bs * world
+                state.step += 1
+                steps += 1
+                stats["steps"] += 1
+                stats["samples"] += bs * world
+                if state.step % cfg.commit_every == 0:
+                    state.commit()
+            if device.type == "cuda":
+                torch.cuda.synchronize(device)
+            ep_time = time.time() - t_ep
+            stats["train_time"] += ep_time
+            if ctx.rank == 0:
+                logger.log_epoch(state.epoch, t_ep, ep_time, steps, float(loss_t) if loss_t is not None else None,
+                                 world)
+            state.epoch += 1
+            state.samples = 0
+            state.commit()
+            if cfg.checkpoint_every_epoch and ctx.rank == 0:
+                state.save_checkpoint()
+        if device.type == "cuda":
+            torch.cuda.synchronize(device)
+        return dict(stats, final_loss=float(loss_t) if loss_t is not None else None, world=ctx.size)
+
+    try:
+        return train(state)
+    finally:
+        ddp.remove_hooks()
+
+
+def main(argv=None):
+    ap = argparse.ArgumentParser("vodascheduler_amd.workloads.train")
+    ap.add_argument("--model", required=True)
+    ap.add_argument("--name", default=os.environ.get("JOB_NAME", "job"))
+    ap.add_argument("--epochs", type=int, default=1)
+    ap.add_argument("--steps-per-epoch", type=int, default=10)
+    ap.add_argument("--batch-size", type=int, default=None)
+    ap.add_argument("--lr", type=float, default=None)
+    ap.add_argument("--commit-every", type=int, default=1)
+    ap.add_argument("--fp16-allreduce", action="store_true")
+    ap.add_argument("--compression", default=None)
+    ap.add_argument("--metrics-dir", default=os.environ.get("VODA_METRICS_DIR"))
+    ap.add_argument("--no-amp", action="store_true")
+    a = ap.parse_args(argv)
+    logging.basicConfig(level=logging.INFO)
+    from ..runtime.rendezvous import connect_store
+
+    host, port = os.environ["VODA_STORE"].rsplit(":", 1)
+    store = connect_store(host, int(port))
+    watch = connect_store(host, int(port))
+    dev = torch.device("cuda", 0) if torch.cuda.is_available() else torch.device("cpu")
+    if dev.type == "cuda":
+        torch.cuda.set_device(dev)
+    ctx = ElasticContext(store, a.name, os.environ["VODA_WORKER_ID"], dev, watch_store=watch,
+                         join_epoch=int(os.environ.get("VODA_JOIN_EPOCH", "0")))
+    cfg = TrainConfig(a.model, a.epochs, a.steps_per_epoch, a.batch_size, a.lr, a.commit_every, not a.no_amp,
+                      "fp16" if a.fp16_allreduce else a.compression, metrics_dir=a.metrics_dir)
+    out = train_elastic(ctx, cfg)
+    log.info("worker %s finished job %s: %s", ctx.worker_id, a.name, out)
+
+
+if __name__ == "__main__":
+    main()
