@@ -1,0 +1,231 @@
+#!/usr/bin/env python3
+"""Headline benchmark: avg JCT + makespan of a 32-job Philly-style trace on N MI355X GPUs,
+with elastic-resize latency (BASELINE.json metric; config "FfDL Optimizer, 32-job
+Philly-style synthetic trace, autoscale 1->8 MI355X").
+
+One process per GPU (``python -m torch.distributed.run --nproc-per-node N bench.py --gpus N``
+or plain ``python bench.py`` for N=1).  Every rank is a warm pool worker; rank 0 also runs
+the real control plane (training service -> scheduler with the chosen policy + Munkres
+placement -> PoolBackend) and submits the trace in real time.  Jobs are ResNet-50
+(ImageNet 224x224, batch 256/GPU) and BERT-base (seq 128) elastic data-parallel jobs in bf16
+(autocast) on PyTorch-ROCm, gradient all-reduce on RCCL over xGMI with bucket overlap,
+fused HIP optimizers, resized live (communicator rebuild + state broadcast).
+
+Semantics of the driver flags:
+  --steps K   mean job length in single-GPU training steps (trace scale); weak scaling:
+              every job's work is multiplied by N, so per-GPU work is fixed as N grows.
+  --warmup W  untimed warm-up steps of every model on every GPU (MIOpen/hipBLASLt caches,
+              RCCL init) before the timed trace.
+The timed region (barrier + synchronize on both sides) is the whole trace: first submission
+to last completion.  ``value`` = average JCT in seconds (lower is better); makespan, resize
+latency and aggregate throughput are reported alongside.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import threading
+import time
+
+os.environ.setdefault("GLOO_SOCKET_IFNAME", "lo")
+os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+
+from vodascheduler_amd.models import get_workload  # noqa: E402
+from vodascheduler_amd.ops import _native  # noqa: E402
+from vodascheduler_amd.ops.optim import make_optimizer  # noqa: E402
+from vodascheduler_amd.parallel.comm import RcclCommunicator  # noqa: E402
+from vodascheduler_amd.runtime.cluster import free_port, run_trace  # noqa: E402
+from vodascheduler_amd.runtime.pool import PoolWorker  # noqa: E402
+from vodascheduler_amd.runtime.rendezvous import connect_store  # noqa: E402
+from vodascheduler_amd.sim.trace import bench_trace  # noqa: E402
+
+BASELINE_METRIC = "avg JCT + makespan, 32-job trace on 1/2/4/8 MI355X; elastic-resize latency"
+MODELS = ("resnet50", "bert-base")
+BATCH = {"resnet50": 256, "bert-base": 64}
+
+
+def log(rank, *a):
+    if rank == 0:
+        print(f"[bench {time.strftime('%H:%M:%S')}]", *a, file=sys.stderr, flush=True)
+
+
+def warmup(device, steps: int):
+    """Untimed warm-up of every model in the mix on this GPU (single-GPU steps)."""
+    out = {}
+    for name in MODELS:
+        w = get_workload(name)
+        torch.manual_seed(0)
+        m = w.build().to(device)
+        if w.channels_last:
+            m = m.to(memory_format=torch.channels_last)
+        opt = make_optimizer(w.optimizer, m.parameters(), **w.opt_kwargs)
+        b = w.make_batch(BATCH[name], device, None)
+        if w.channels_last:
+            b = tuple(t.to(memory_format=torch.channels_last) if t.dim() == 4 else t for t in b)
+        t0 = None
+        for i in range(max(2, steps)):
+            if i == 1:
+                torch.cuda.synchronize(device)
+                t0 = time.perf_counter()
+            opt.zero_grad()
+            with torch.autocast("cuda", dtype=torch.bfloat16):
+                loss = w.loss(m, b)
+            loss.backward()
+            opt.step()
+        torch.cuda.synchronize(device)
+        out[name] = (time.perf_counter() - t0) / (max(2, steps) - 1) * 1e3
+        del m, opt, b
+    return out
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=30)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--jobs", type=int, default=32)
+    ap.add_argument("--algorithm", default="FfDLOptimizer")
+    ap.add_argument("--rate-limit", type=float, default=2.0)
+    ap.add_argument("--interarrival", type=float, default=0.5)
+    ap.add_argument("--commit-every", type=int, default=4)
+    ap.add_argument("--compression", default=None, choices=[None, "bf16", "fp16"])
+    ap.add_argument("--seed", type=int, default=0)
+    ap.add_argument("--out", default=None, help="also write the JSON line (+details) to this file")
+    a = ap.parse_args()
+
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != a.gpus:
+        raise SystemExit(f"--gpus {a.gpus} but WORLD_SIZE={world}")
+    device = torch.device("cuda", local)
+    torch.cuda.set_device(device)
+    _native.hip()  # the HIP extension must be present on a GPU box
+
+    if world > 1:
+        dist.init_process_group("gloo", init_method="env://", rank=rank, world_size=world)
+    port = [free_port() if rank == 0 else 0]
+    if world > 1:
+        dist.broadcast_object_list(port, src=0)
+    store = connect_store("127.0.0.1", port[0], is_master=(rank == 0))
+    watch = connect_store("127.0.0.1", port[0])
+
+    # ---------------- untimed warm-up ----------------
+    log(rank, f"warm-up: {a.warmup} steps x {MODELS} on {world} GPU(s)")
+    step_ms = warmup(device, a.warmup)
+    if world > 1:
+        comm = RcclCommunicator(store, "bench/warm", rank, world, device)
+        x = torch.ones(16 << 20, device=device)
+        comm.allreduce_(x, "sum")
+        torch.cuda.synchronize(device)
+        comm.destroy()
+        dist.barrier()
+    log(rank, f"warm-up single-GPU step ms: {step_ms}")
+
+    trace = bench_trace(a.jobs, a.steps, world, a.seed, a.interarrival, MODELS, BATCH)
+    locs = [("node0", r) for r in range(world)]
+    os.environ.setdefault("VODA_CKPT_DIR", f"/tmp/voda_ckpt_{os.getpid()}")
+    metrics_dir = f"/tmp/voda_metrics_{port[0]}"
+    defaults = {"commit_every": a.commit_every, "compression": a.compression, "metrics_dir": metrics_dir}
+
+    # ---------------- timed region ----------------
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(device)
+    t0 = time.perf_counter()
+    result: dict = {}
+    sched = None
+    if rank == 0:
+        def drive():
+            try:
+                result.update(run_trace(store, trace, locs, a.algorithm, rate_limit_sec=a.rate_limit,
+                                        tick_sec=1.0, train_defaults=defaults, timeout=3000,
+                                        progress=lambda s: log(0, s)))
+            except BaseException as e:  # never leave the pool hanging
+                result["error"] = repr(e)
+                store.set("pool/shutdown", "1")
+
+        sched = threading.Thread(target=drive, name="control-plane", daemon=True)
+        sched.start()
+    worker = PoolWorker(store, watch, f"node0:{rank}", device, backend="rccl", timeout=900)
+    recs = worker.serve()
+    if sched is not None:
+        sched.join()
+    torch.cuda.synchronize(device)
+    if world > 1:
+        dist.barrier()
+    t1 = time.perf_counter()
+
+    # ---------------- aggregate ----------------
+    my = {"steps": sum((r["result"] or {}).get("steps", 0) for r in recs if isinstance(r["result"], dict)),
+          "train_time": sum((r["result"] or {}).get("train_time", 0.0) for r in recs if isinstance(r["result"], dict)),
+          "comm_init": [x.get("comm_init_s") for r in recs for x in r["resize_log"]]}
+    allrec = [my]
+    if world > 1:
+        allrec = [None] * world
+        dist.all_gather_object(allrec, my)
+        wall = torch.tensor([t1 - t0], dtype=torch.float64)
+        dist.all_reduce(wall, op=dist.ReduceOp.MAX)
+        wall_s = float(wall.item())
+    else:
+        wall_s = t1 - t0
+    if rank == 0:
+        if "error" in result:
+            raise SystemExit(f"bench failed: {result['error']}")
+        tot_steps = sum(r["steps"] for r in allrec)
+        tot_train = sum(r["train_time"] for r in allrec)
+        samples = 0
+        for tj in trace:
+            from vodascheduler_amd.sim.trace import workload_of
+
+            wl = workload_of(tj.spec)
+            samples += wl["steps_per_epoch"] * 2 * BATCH[wl["model"]]
+        line = {
+            "metric": BASELINE_METRIC,
+            "value": round(result["avg_jct_s"], 3),
+            "unit": "s (avg JCT)",
+            "n_gpus": world,
+            "steps": a.steps,
+            "warmup": a.warmup,
+            "ms_per_step": round(tot_train / max(tot_steps, 1) * 1e3, 3),
+            "higher_is_better": False,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "bf16",
+            "data": "synthetic (random-init weights, synthetic batches of the real shapes)",
+            "config": {
+                "model": "32-job Philly-style trace: ResNet-50 (ImageNet 224, bs256/GPU) + BERT-base (seq128, bs64/GPU)",
+                "global_batch": "per job: per-GPU batch x elastic workers",
+                "seq_len": 128,
+                "parallelism": f"elastic-dp, {a.algorithm}, <= {world} GPU(s)/job, RCCL over xGMI",
+                "algorithm": a.algorithm,
+                "jobs": len(trace),
+            },
+            "makespan_s": round(result["makespan_s"], 3),
+            "p95_jct_s": round(result["p95_jct_s"], 3),
+            "wall_s": round(wall_s, 3),
+            "resize_events": result["resize_events"],
+            "resize_latency_p50_s": result["resize_latency_p50_s"],
+            "resize_latency_p95_s": result["resize_latency_p95_s"],
+            "throughput_samples_per_s": round(samples / wall_s, 1),
+            "warmup_single_gpu_step_ms": {k: round(v, 2) for k, v in step_ms.items()},
+        }
+        print(json.dumps(line), flush=True)
+        if a.out:
+            with open(a.out, "w") as f:
+                json.dump({"line": line, "jct": result["jct"], "events": result["events"],
+                           "resize_latency": result["resize_latency"], "workers": allrec}, f, indent=1)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -36,7 +36,8 @@ def free_port() -> int:
 
 def run_trace(store, trace: list[TraceJob], worker_locs, algorithm: str = "ElasticFIFO",
               rate_limit_sec: float = 1.0, tick_sec: float = 1.0, train_defaults: dict | None = None,
-              timeout: float = 3600.0, gpu_type: str = DEFAULT_GPU_TYPE, progress=None) -> dict:
+              timeout: float = 3600.0, gpu_type: str = DEFAULT_GPU_TYPE, progress=None,
+              collect_every_s: float = 2.0) -> dict:
     """Submit ``trace`` in real time (``submit_time`` seconds after start) and wait until every
     job completed.  Returns JCT / makespan / resize-latency statistics."""
     db = MemoryStore()
@@ -46,13 +47,22 @@ def run_trace(store, trace: list[TraceJob], worker_locs, algorithm: str = "Elast
     core = SchedulerCore(gpu_type, db, ResourceAllocator(db), backend, algorithm=algorithm,
                          rate_limit_sec=rate_limit_sec, tick_sec=tick_sec)
     runner = SchedulerRunner(core, mq).start()
+    collector = None
+    mdir = (train_defaults or {}).get("metrics_dir")
+    if mdir:
+        from ..collector.collector import MetricsCollector
+
+        collector = MetricsCollector(db, mdir)
     t0 = time.time()
     names: list[str] = []
     pending = sorted(trace, key=lambda tj: tj.submit_time)
-    last_report = t0
+    last_report = last_collect = t0
     try:
         while True:
             now = time.time()
+            if collector is not None and now - last_collect > collect_every_s:
+                last_collect = now
+                collector.update_info_all(list(names))
             while pending and now - t0 >= pending[0].submit_time:
                 tj = pending.pop(0)
                 names.append(svc.create_training_job(json.dumps(tj.spec)))

@@ -132,6 +132,34 @@ def philly_trace(n_jobs: int = 32, seed: int = 0, mean_interarrival_s: float = 3
     return out
 
 
+def bench_trace(n_jobs: int = 32, mean_steps: int = 30, n_gpus: int = 1, seed: int = 0,
+                mean_interarrival_s: float = 0.5, models: tuple[str, ...] = ("resnet50", "bert-base"),
+                batches: dict[str, int] | None = None, epochs: int = 2) -> list[TraceJob]:
+    """The 32-job Philly-style trace run by ``bench.py`` on real MI355X GPUs.
+
+    Weak scaling: every job's work (single-GPU steps at the per-GPU batch) is multiplied by
+    ``n_gpus``, so the per-GPU work is fixed as the pool grows.  Requests follow the Philly
+    size mix capped at ``n_gpus``; every job is elastic in ``[1, min(n_gpus, 2 x request)]``.
+    Durations are log-normal (sigma 0.8) around ``mean_steps``; arrivals are Poisson.
+    """
+    rng = random.Random(seed)
+    sizes, weights = [1, 2, 4, 8], [0.50, 0.25, 0.15, 0.10]
+    batches = batches or {}
+    t = 0.0
+    out = []
+    for i in range(n_jobs):
+        if i > 0:
+            t += rng.expovariate(1.0 / mean_interarrival_s)
+        np_ = min(rng.choices(sizes, weights)[0], n_gpus)
+        model = models[i % len(models)]
+        steps = max(2 * epochs, int(round(rng.lognormvariate(math.log(mean_steps) - 0.32, 0.8) * n_gpus)))
+        spe = max(1, steps // epochs)
+        max_np = max(np_, min(n_gpus, 2 * np_))
+        out.append(TraceJob(t, make_spec(f"{model}-j{i:02d}", model, np_, 1, max_np, epochs, spe,
+                                         per_gpu_batch=batches.get(model))))
+    return out
+
+
 def scale_trace(trace: list[TraceJob], work_scale: float) -> list[TraceJob]:
     """Multiply every job's work (steps per epoch) by ``work_scale`` (weak scaling over N GPUs)."""
     out = []
