@@ -144,18 +144,34 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const T* __restrict__ dy, c
 }
 
 // Column sums of a [rows][N] fp32 partial matrix: out[c] = sum_r part[r][c] (cast to WT).
+// 32 columns x 8 row-groups per block; every thread keeps 4 independent loads in flight
+// (rows <= 256, so <= 32 loads per thread) -- the first version (64 columns x 4 groups,
+// 1024 rows) was latency-bound at 64 us per call on BERT (rocprof, profiles/).
 template <typename WT>
 __global__ __launch_bounds__(256) void col_sum_kernel(const float* __restrict__ part, WT* __restrict__ out,
                                                       int rows, int N) {
-  __shared__ float red[4][64];
-  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
-  const int c = blockIdx.x * 64 + tx;
-  float s = 0.f;
-  if (c < N)
-    for (int r = ty; r < rows; r += 4) s += part[int64_t(r) * N + c];
-  red[ty][tx] = s;
+  __shared__ float red[8][33];
+  const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;
+  const int c = blockIdx.x * 32 + tx;
+  float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
+  if (c < N) {
+    int r = ty;
+    for (; r + 24 < rows; r += 32) {
+      s0 += part[int64_t(r) * N + c];
+      s1 += part[int64_t(r + 8) * N + c];
+      s2 += part[int64_t(r + 16) * N + c];
+      s3 += part[int64_t(r + 24) * N + c];
+    }
+    for (; r < rows; r += 8) s0 += part[int64_t(r) * N + c];
+  }
+  red[ty][tx] = (s0 + s1) + (s2 + s3);
   __syncthreads();
-  if (ty == 0 && c < N) Vec4<WT>::store1(out, c, (red[0][tx] + red[1][tx]) + (red[2][tx] + red[3][tx]));
+  if (ty == 0 && c < N) {
+    float t = 0.f;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) t += red[k][tx];
+    Vec4<WT>::store1(out, c, t);
+  }
 }
 
 #define LN_DISPATCH_ITER(N, ...)                                     \
@@ -200,7 +216,7 @@ void layernorm_fwd(uintptr_t x, uintptr_t gamma, uintptr_t beta, uintptr_t y, ui
 
 int layernorm_bwd_partial_rows(int64_t M) {
   int64_t g = (M + 3) / 4;
-  return int(std::max<int64_t>(1, std::min<int64_t>(g, 1024)));
+  return int(std::max<int64_t>(1, std::min<int64_t>(g, 256)));
 }
 
 void layernorm_bwd(uintptr_t dy, uintptr_t x, uintptr_t mean, uintptr_t rstd, uintptr_t gamma, uintptr_t dx,
@@ -225,7 +241,7 @@ void layernorm_bwd(uintptr_t dy, uintptr_t x, uintptr_t mean, uintptr_t rstd, ui
                          reinterpret_cast<const void*>(gamma), reinterpret_cast<T*>(dx), pg, pb, M, N);
     });
     if (pg) {
-      const unsigned cg = unsigned((N + 63) / 64);
+      const unsigned cg = unsigned((N + 31) / 32);
       hipLaunchKernelGGL((col_sum_kernel<WT>), dim3(cg), dim3(256), 0, as_stream(stream), pg,
                          reinterpret_cast<WT*>(dgamma), grid, N);
       hipLaunchKernelGGL((col_sum_kernel<WT>), dim3(cg), dim3(256), 0, as_stream(stream), pb,
