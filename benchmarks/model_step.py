@@ -1,0 +1,69 @@
+"""Single-GPU training-step timer for one workload of the model zoo, with the exact recipe
+the elastic trainer uses (bf16 autocast, channels_last for convnets, fused HIP optimizer).
+Meant to run standalone or under ``rocprofv3 --kernel-trace --stats`` to get the per-kernel
+breakdown of one model's step.
+
+python benchmarks/model_step.py --model bert-base --batch 64 --steps 20 --warmup 5
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from vodascheduler_amd.models import get_workload  # noqa: E402
+from vodascheduler_amd.ops import _native  # noqa: E402
+from vodascheduler_amd.ops.optim import make_optimizer  # noqa: E402
+
+
+def run(model: str, batch: int | None, steps: int, warmup: int) -> dict:
+    dev = torch.device("cuda", 0)
+    w = get_workload(model)
+    bs = batch or w.per_gpu_batch
+    torch.manual_seed(0)
+    m = w.build().to(dev)
+    if w.channels_last:
+        m = m.to(memory_format=torch.channels_last)
+    opt = make_optimizer(w.optimizer, m.parameters(), **w.opt_kwargs)
+    b = w.make_batch(bs, dev, None)
+    if w.channels_last:
+        b = tuple(t.to(memory_format=torch.channels_last) if t.dim() == 4 else t for t in b)
+
+    def step():
+        opt.zero_grad()
+        with torch.autocast("cuda", dtype=torch.bfloat16):
+            loss = w.loss(m, b)
+        loss.backward()
+        opt.step()
+        return loss
+
+    for _ in range(warmup):
+        step()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        loss = step()
+    torch.cuda.synchronize(dev)
+    dt = (time.perf_counter() - t0) / steps
+    return {"model": model, "batch": bs, "ms_per_step": round(dt * 1e3, 3),
+            "samples_per_s": round(bs / dt, 1), "loss": float(loss.detach())}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--model", default="resnet50")
+    ap.add_argument("--batch", type=int, default=None)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    a = ap.parse_args()
+    _native.hip()
+    print(json.dumps(run(a.model, a.batch, a.steps, a.warmup)), flush=True)
+
+
+if __name__ == "__main__":
+    main()

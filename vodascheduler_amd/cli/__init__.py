@@ -1,0 +1,4 @@
+"""``vodascheduler`` CLI (reference cmd/)."""
+from .main import build_parser, main
+
+__all__ = ["build_parser", "main"]

@@ -83,6 +83,9 @@ class ElasticContext:
         self._watcher: threading.Thread | None = None
         self.poll_interval = poll_interval
         self.resize_log: list[dict] = []   # timings of every (re)join, for resize-latency reports
+        # after a failed collective only a NEWER epoch can be joined: the failed one still
+        # lists the dead peer, and rebuilding its communicator would block until timeout
+        self.min_epoch = 0
 
     # ---------------------------------------------------------------- watcher
     def start_watcher(self) -> None:
@@ -122,7 +125,7 @@ class ElasticContext:
         deadline = time.monotonic() + self.timeout
         while True:
             e = self.rdzv.latest_epoch()
-            if e > 0:
+            if e > 0 and e >= self.min_epoch:
                 mem = self.rdzv.members(e)
                 if self.worker_id in mem:
                     return e
@@ -448,6 +451,7 @@ def run(func: Callable) -> Callable:
             except CommError as err:
                 log.warning("%s/%s: collective failed (%s); restoring last commit", ctx.job, ctx.worker_id, err)
                 state.restore()
+                ctx.min_epoch = ctx.epoch + 1
                 ctx.destroy_comm(abort=True)
                 reset = True
                 continue

@@ -43,6 +43,8 @@ def job_train_config(job, defaults: dict | None = None) -> dict:
     d = dict(model=wl["model"], epochs=max(1, job.config.epochs), steps_per_epoch=int(wl["steps_per_epoch"]))
     if "per_gpu_batch" in wl:
         d["per_gpu_batch"] = int(wl["per_gpu_batch"])
+    if "lr" in wl:
+        d["lr"] = float(wl["lr"])
     d.update(defaults or {})
     return d
 
@@ -53,6 +55,7 @@ class PoolBackend(Backend):
         super().__init__()
         self.store = store
         self._lock = threading.Lock()
+        self._pub_lock = threading.RLock()  # one publisher per job at a time (scheduler vs failure path)
         self.workers = [worker_id(l) for l in worker_locs]
         self.node_gpus: dict[str, list[int]] = {}
         for n, g in worker_locs:
@@ -75,6 +78,10 @@ class PoolBackend(Backend):
             self._apply_one(a)
 
     def _apply_one(self, a: JobAction) -> None:
+        with self._pub_lock:
+            self._apply_locked(a)
+
+    def _apply_locked(self, a: JobAction) -> None:
         name = a.job.name
         rdzv = JobRendezvous(self.store, name)
         if a.kind == HALT:
@@ -173,10 +180,14 @@ class PoolWorker:
         self.results: list[dict] = []
 
     def serve(self) -> list[dict]:
+        # a restarted worker resumes after the last message its predecessor took
+        # (at-most-once: a job that was running when the process died is recovered by the
+        # backend's abort epoch + migration, never replayed here)
+        self.done = int(self.store.add(f"pool/{self.wid}/done", 0))
         while True:
             n = int(self.store.add(f"pool/{self.wid}/n", 0))
             if n > self.done:
-                self.done += 1
+                self.done = int(self.store.add(f"pool/{self.wid}/done", 1))
                 msg = json.loads(self.store.get(f"pool/{self.wid}/msg/{self.done}"))
                 self._run(msg)
                 continue

@@ -89,10 +89,70 @@ def make_spec(name: str, model: str, np_: int, min_np: int, max_np: int, epochs:
 
 
 def workload_of(spec: dict) -> dict:
+    """The job's workload: the ``vodascheduler/workload`` annotation, or -- for specs written
+    for the reference (no annotation) -- what the launcher command line says: the
+    reference's example scripts take ``--model ResNet50|VGG16|InceptionV3 --dataset cifar10``
+    (examples/yaml/tensorflow2/*.yaml), the MNIST / Transformer scripts are recognised by
+    name, and ``--model <workload>`` names any workload of this framework's model zoo."""
     ann = (spec.get("metadata", {}).get("annotations") or {}).get(WORKLOAD_ANNOTATION)
-    if not ann:
-        raise KeyError("job spec has no workload annotation")
-    return json.loads(ann)
+    if ann:
+        return json.loads(ann)
+    wl = workload_from_launcher(spec)
+    if wl is None:
+        raise KeyError("job spec has no workload annotation and no recognisable launcher command")
+    return wl
+
+
+_REF_MODELS = {"resnet50": "resnet50", "vgg16": "vgg16", "inceptionv3": "inceptionv3", "resnet18": "resnet18"}
+_DATASET_SAMPLES = {"cifar10": 50000, "mnist": 60000, "imagenet": 1281167}
+
+
+def workload_from_launcher(spec: dict) -> dict | None:
+    import shlex
+
+    try:
+        cont = spec["spec"]["mpiReplicaSpecs"]["Launcher"]["template"]["spec"]["containers"][0]
+    except (KeyError, IndexError, TypeError):
+        return None
+    text = " ".join(str(x) for x in (cont.get("command") or []) + (cont.get("args") or []))
+    try:
+        toks = shlex.split(text.replace(";", " ; "))
+    except ValueError:
+        toks = text.split()
+    opts: dict[str, str] = {}
+    for i, t in enumerate(toks[:-1]):
+        if t.startswith("--"):
+            opts[t[2:].replace("_", "-")] = toks[i + 1]
+    script = " ".join(t for t in toks if t.endswith(".py") or t.startswith("vodascheduler_amd."))
+    from ..models import WORKLOADS
+
+    model = opts.get("model", "")
+    dataset = opts.get("dataset", "").lower()
+    key = model.lower().replace("_", "").replace("-", "")
+    if model in WORKLOADS:
+        name = model
+    elif key in _REF_MODELS:
+        name = _REF_MODELS[key]
+        if name == "resnet50" and dataset.startswith("cifar"):
+            name = "resnet50-cifar"
+    elif "mnist" in script:
+        name, dataset = ("mnist-torch" if "pytorch" in script else "mnist"), "mnist"
+    elif "transformer" in script:
+        name = "transformer"
+    else:
+        return None
+    w = WORKLOADS[name]
+    bs = int(opts.get("batch-size", w.per_gpu_batch))
+    if "steps-per-epoch" in opts:
+        spe = int(opts["steps-per-epoch"])
+    else:
+        spe = max(1, _DATASET_SAMPLES.get(dataset or "", 100 * bs) // bs)
+    prof = PROFILES.get(name, ModelProfile(name, 0.05, 0.05))
+    out = {"model": name, "steps_per_epoch": spe, "per_gpu_batch": bs, "alpha": prof.alpha,
+           "epoch_time_1gpu": spe * prof.step_time_1gpu}
+    if "lr" in opts:
+        out["lr"] = float(opts["lr"])
+    return out
 
 
 @dataclass
