@@ -1,0 +1,499 @@
+// Fused BatchNorm(+residual add)(+ReLU) for channels_last (NHWC) activations on CDNA4.
+//
+// The ResNet-50 / InceptionV3 / VGG jobs of the trace spend ~half of their step in
+// BatchNorm, ReLU and the residual add when those run as separate library kernels
+// (MIOpen BN fwd/bwd + elementwise ReLU / add / ReLU-backward: profiles/).  Here the
+// activation is viewed as a row-major [M = N*H*W][C] matrix and each op touches it the
+// minimum number of times:
+//
+//   forward  (train): stats pass   read x                 -> per-block partial sums
+//                     finalize     per channel: mean, invstd, running stats, a=g*invstd, b=beta-mean*a
+//                     apply pass   read x (+ residual r), write y = relu(a*x + b (+ r))
+//   backward        : reduce pass  read dy, y (ReLU mask), x -> partial sums of g and g*x
+//                     finalize     dgamma, dbeta, per-channel (a, c2, c0)
+//                     apply pass   read dy, y, x; write dx = a*g + c2*x + c0 (+ dr = g)
+//   with g = dy * (y > 0) when the forward applied ReLU (the mask comes from the saved
+//   output y, which the next convolution keeps alive anyway), and
+//   dx = a*(g - mean(g) - xhat*mean(g*xhat)) folded into per-channel constants.
+//
+// Layout / mapping: a thread owns ONE group of 8 consecutive channels (16 B of bf16) for
+// the whole kernel, so per-channel constants live in registers; a block of 256 threads
+// covers floor(256 / (C/8)) rows per iteration (one contiguous 4 KB span of memory: fully
+// coalesced dwordx4 loads), and blocks own contiguous row chunks.  C > 2048 uses grid.y
+// channel slices.  Partial sums are fp32 per block; the finalize kernels reduce them with
+// 32 row-groups per channel group and double accumulation.
+#include "common.h"
+#include "ops.h"
+
+namespace voda {
+
+namespace {
+
+constexpr int kBlock = 256;
+constexpr int kVec = 8;            // channels per thread
+constexpr int kMaxTpr = kBlock;    // channel groups per block slice (<= 2048 channels)
+
+template <typename T> struct Vec8;
+template <> struct Vec8<BF16> {
+  static __device__ __forceinline__ void load(const BF16* p, int64_t i, float (&v)[8]) {
+    uint4 u = *reinterpret_cast<const uint4*>(p + i);
+    uint32_t w[4] = {u.x, u.y, u.z, u.w};
+#pragma unroll
+    for (int k = 0; k < 4; ++k) { v[2 * k] = bf2f(w[k] & 0xffff); v[2 * k + 1] = bf2f(w[k] >> 16); }
+  }
+  static __device__ __forceinline__ void store(BF16* p, int64_t i, const float (&v)[8]) {
+    uint4 u;
+    u.x = uint32_t(f2bf(v[0])) | (uint32_t(f2bf(v[1])) << 16);
+    u.y = uint32_t(f2bf(v[2])) | (uint32_t(f2bf(v[3])) << 16);
+    u.z = uint32_t(f2bf(v[4])) | (uint32_t(f2bf(v[5])) << 16);
+    u.w = uint32_t(f2bf(v[6])) | (uint32_t(f2bf(v[7])) << 16);
+    *reinterpret_cast<uint4*>(p + i) = u;
+  }
+};
+template <> struct Vec8<F16> {
+  static __device__ __forceinline__ void load(const F16* p, int64_t i, float (&v)[8]) {
+    uint4 u = *reinterpret_cast<const uint4*>(p + i);
+    uint32_t w[4] = {u.x, u.y, u.z, u.w};
+#pragma unroll
+    for (int k = 0; k < 4; ++k) { v[2 * k] = h2f(w[k] & 0xffff); v[2 * k + 1] = h2f(w[k] >> 16); }
+  }
+  static __device__ __forceinline__ void store(F16* p, int64_t i, const float (&v)[8]) {
+    uint4 u;
+    u.x = uint32_t(f2h(v[0])) | (uint32_t(f2h(v[1])) << 16);
+    u.y = uint32_t(f2h(v[2])) | (uint32_t(f2h(v[3])) << 16);
+    u.z = uint32_t(f2h(v[4])) | (uint32_t(f2h(v[5])) << 16);
+    u.w = uint32_t(f2h(v[6])) | (uint32_t(f2h(v[7])) << 16);
+    *reinterpret_cast<uint4*>(p + i) = u;
+  }
+};
+template <> struct Vec8<float> {
+  static __device__ __forceinline__ void load(const float* p, int64_t i, float (&v)[8]) {
+    float4 a = *reinterpret_cast<const float4*>(p + i);
+    float4 b = *reinterpret_cast<const float4*>(p + i + 4);
+    v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+  }
+  static __device__ __forceinline__ void store(float* p, int64_t i, const float (&v)[8]) {
+    *reinterpret_cast<float4*>(p + i) = make_float4(v[0], v[1], v[2], v[3]);
+    *reinterpret_cast<float4*>(p + i + 4) = make_float4(v[4], v[5], v[6], v[7]);
+  }
+};
+
+// Thread -> (channel group, row offset) mapping shared by every pass.
+struct Map {
+  int tpr;        // channel groups handled by this block slice
+  int rpi;        // rows per iteration
+  int cg;         // this thread's channel group (global), valid if active
+  int rsub;       // this thread's row offset inside an iteration
+  bool active;
+};
+
+__device__ __forceinline__ Map make_map(int C) {
+  Map m;
+  const int groups = C / kVec;
+  const int slice0 = blockIdx.y * kMaxTpr;
+  m.tpr = min(groups - slice0, kMaxTpr);
+  m.rpi = kBlock / m.tpr;
+  const int t = threadIdx.x;
+  m.active = t < m.rpi * m.tpr;
+  m.cg = slice0 + (m.active ? t % m.tpr : 0);
+  m.rsub = m.active ? t / m.tpr : 0;
+  return m;
+}
+
+// Rows [r0, r1) owned by this block (contiguous chunk of iterations).
+__device__ __forceinline__ void block_rows(int64_t M, int rpi, int64_t& r0, int64_t& r1) {
+  const int64_t iters = (M + rpi - 1) / rpi;
+  const int64_t per = (iters + gridDim.x - 1) / gridDim.x;
+  r0 = int64_t(blockIdx.x) * per * rpi;
+  r1 = min<int64_t>(M, r0 + per * rpi);
+}
+
+// Block-level reduction of two 8-channel accumulators over the row offsets that share a
+// channel group; thread (rsub == 0) ends up with the block's sums.  Writes the partials.
+__device__ __forceinline__ void reduce_and_store(const Map& m, float (&s1)[8], float (&s2)[8], float* part1,
+                                                 float* part2, int C) {
+  __shared__ float red[2][kBlock][kVec + 1];
+  const int t = threadIdx.x;
+#pragma unroll
+  for (int k = 0; k < kVec; ++k) { red[0][t][k] = s1[k]; red[1][t][k] = s2[k]; }
+  __syncthreads();
+  if (m.active && m.rsub == 0) {
+    const int tl = t;  // = channel group index within the slice
+    for (int r = 1; r < m.rpi; ++r) {
+      const int o = tl + r * m.tpr;
+#pragma unroll
+      for (int k = 0; k < kVec; ++k) { s1[k] += red[0][o][k]; s2[k] += red[1][o][k]; }
+    }
+    const int64_t base = int64_t(blockIdx.x) * C + int64_t(m.cg) * kVec;
+#pragma unroll
+    for (int k = 0; k < kVec; ++k) { part1[base + k] = s1[k]; part2[base + k] = s2[k]; }
+  }
+}
+
+// ---------------------------------------------------------------- forward: statistics
+template <typename T>
+__global__ __launch_bounds__(kBlock) void bn_stats_kernel(const T* __restrict__ x, float* __restrict__ part,
+                                                          int64_t M, int C) {
+  const Map m = make_map(C);
+  int64_t r0, r1;
+  block_rows(M, m.rpi, r0, r1);
+  float s1[8] = {0, 0, 0, 0, 0, 0, 0, 0}, s2[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  if (m.active) {
+    const int64_t col = int64_t(m.cg) * kVec;
+    int64_t r = r0 + m.rsub;
+    const int64_t step = m.rpi;
+    // 4 rows in flight per thread
+    for (; r + 3 * step < r1; r += 4 * step) {
+      float v0[8], v1[8], v2[8], v3[8];
+      Vec8<T>::load(x, r * C + col, v0);
+      Vec8<T>::load(x, (r + step) * C + col, v1);
+      Vec8<T>::load(x, (r + 2 * step) * C + col, v2);
+      Vec8<T>::load(x, (r + 3 * step) * C + col, v3);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        s1[k] += (v0[k] + v1[k]) + (v2[k] + v3[k]);
+        s2[k] += (v0[k] * v0[k] + v1[k] * v1[k]) + (v2[k] * v2[k] + v3[k] * v3[k]);
+      }
+    }
+    for (; r < r1; r += step) {
+      float v[8];
+      Vec8<T>::load(x, r * C + col, v);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) { s1[k] += v[k]; s2[k] += v[k] * v[k]; }
+    }
+  }
+  reduce_and_store(m, s1, s2, part, part + int64_t(gridDim.x) * C, C);
+}
+
+// ---------------------------------------------------------------- backward: reductions
+template <typename T, bool RELU>
+__global__ __launch_bounds__(kBlock) void bn_bwd_reduce_kernel(const T* __restrict__ dy, const T* __restrict__ y,
+                                                               const T* __restrict__ x, float* __restrict__ part,
+                                                               int64_t M, int C) {
+  const Map m = make_map(C);
+  int64_t r0, r1;
+  block_rows(M, m.rpi, r0, r1);
+  float s1[8] = {0, 0, 0, 0, 0, 0, 0, 0}, s2[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  if (m.active) {
+    const int64_t col = int64_t(m.cg) * kVec;
+    const int64_t step = m.rpi;
+    int64_t r = r0 + m.rsub;
+    for (; r + step < r1; r += 2 * step) {
+      float g0[8], x0[8], g1[8], x1[8];
+      Vec8<T>::load(dy, r * C + col, g0);
+      Vec8<T>::load(x, r * C + col, x0);
+      Vec8<T>::load(dy, (r + step) * C + col, g1);
+      Vec8<T>::load(x, (r + step) * C + col, x1);
+      if constexpr (RELU) {
+        float y0[8], y1[8];
+        Vec8<T>::load(y, r * C + col, y0);
+        Vec8<T>::load(y, (r + step) * C + col, y1);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          g0[k] = y0[k] > 0.f ? g0[k] : 0.f;
+          g1[k] = y1[k] > 0.f ? g1[k] : 0.f;
+        }
+      }
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        s1[k] += g0[k] + g1[k];
+        s2[k] += g0[k] * x0[k] + g1[k] * x1[k];
+      }
+    }
+    for (; r < r1; r += step) {
+      float g[8], xv[8];
+      Vec8<T>::load(dy, r * C + col, g);
+      Vec8<T>::load(x, r * C + col, xv);
+      if constexpr (RELU) {
+        float yv[8];
+        Vec8<T>::load(y, r * C + col, yv);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) g[k] = yv[k] > 0.f ? g[k] : 0.f;
+      }
+#pragma unroll
+      for (int k = 0; k < 8; ++k) { s1[k] += g[k]; s2[k] += g[k] * xv[k]; }
+    }
+  }
+  reduce_and_store(m, s1, s2, part, part + int64_t(gridDim.x) * C, C);
+}
+
+// ---------------------------------------------------------------- finalize kernels
+// Block = 8 channels x 32 row groups; double accumulation of the per-block partials.
+constexpr int kFinCh = 8, kFinRg = 32;
+
+__device__ __forceinline__ void fin_reduce(const float* __restrict__ p1, const float* __restrict__ p2, int nb, int C,
+                                           int c, double& S1, double& S2) {
+  __shared__ double red[2][kFinRg][kFinCh + 1];
+  const int cl = threadIdx.x % kFinCh, rg = threadIdx.x / kFinCh;
+  double a = 0.0, b = 0.0;
+  if (c < C)
+    for (int r = rg; r < nb; r += kFinRg) {
+      a += double(p1[int64_t(r) * C + c]);
+      b += double(p2[int64_t(r) * C + c]);
+    }
+  red[0][rg][cl] = a;
+  red[1][rg][cl] = b;
+  __syncthreads();
+  S1 = 0.0;
+  S2 = 0.0;
+  if (rg == 0) {
+    for (int k = 0; k < kFinRg; ++k) { S1 += red[0][k][cl]; S2 += red[1][k][cl]; }
+  }
+}
+
+__global__ __launch_bounds__(kFinCh* kFinRg) void bn_fwd_finalize_kernel(
+    const float* __restrict__ part, int nb, int64_t M, int C, const float* __restrict__ gamma,
+    const float* __restrict__ beta, float* __restrict__ running_mean, float* __restrict__ running_var,
+    float* __restrict__ save_mean, float* __restrict__ save_invstd, float* __restrict__ ab, float eps,
+    float momentum) {
+  const int c = blockIdx.x * kFinCh + threadIdx.x % kFinCh;
+  double S1, S2;
+  fin_reduce(part, part + int64_t(nb) * C, nb, C, c, S1, S2);
+  if (threadIdx.x / kFinCh == 0 && c < C) {
+    const double mean = S1 / double(M);
+    double var = S2 / double(M) - mean * mean;
+    if (var < 0.0) var = 0.0;
+    const float invstd = float(1.0 / sqrt(var + double(eps)));
+    save_mean[c] = float(mean);
+    save_invstd[c] = invstd;
+    if (running_mean != nullptr) {
+      const double unbiased = M > 1 ? var * double(M) / double(M - 1) : var;
+      running_mean[c] = float((1.0 - momentum) * running_mean[c] + momentum * mean);
+      running_var[c] = float((1.0 - momentum) * running_var[c] + momentum * unbiased);
+    }
+    const float g = gamma != nullptr ? gamma[c] : 1.f;
+    const float b = beta != nullptr ? beta[c] : 0.f;
+    const float a = g * invstd;
+    ab[c] = a;
+    ab[C + c] = b - float(mean) * a;
+  }
+}
+
+__global__ __launch_bounds__(kFinCh* kFinRg) void bn_bwd_finalize_kernel(
+    const float* __restrict__ part, int nb, int64_t M, int C, const float* __restrict__ gamma,
+    const float* __restrict__ save_mean, const float* __restrict__ save_invstd, float* __restrict__ dgamma,
+    float* __restrict__ dbeta, float* __restrict__ k3) {
+  const int c = blockIdx.x * kFinCh + threadIdx.x % kFinCh;
+  double S1, S2;  // sum g, sum g*x
+  fin_reduce(part, part + int64_t(nb) * C, nb, C, c, S1, S2);
+  if (threadIdx.x / kFinCh == 0 && c < C) {
+    const double mean = save_mean[c], invstd = save_invstd[c];
+    const double db = S1;
+    const double dg = invstd * (S2 - mean * S1);
+    if (dgamma != nullptr) dgamma[c] = float(dg);
+    if (dbeta != nullptr) dbeta[c] = float(db);
+    const double g = gamma != nullptr ? gamma[c] : 1.0;
+    const double a = g * invstd;
+    const double c2 = -a * invstd * dg / double(M);
+    const double c0 = -a * db / double(M) - c2 * mean;
+    k3[c] = float(a);
+    k3[C + c] = float(c2);
+    k3[2 * C + c] = float(c0);
+  }
+}
+
+// ---------------------------------------------------------------- elementwise passes
+template <typename T, bool RES, bool RELU>
+__global__ __launch_bounds__(kBlock) void bn_apply_kernel(const T* __restrict__ x, const T* __restrict__ res,
+                                                          const float* __restrict__ ab, T* __restrict__ y,
+                                                          int64_t M, int C) {
+  const Map m = make_map(C);
+  if (!m.active) return;
+  int64_t r0, r1;
+  block_rows(M, m.rpi, r0, r1);
+  const int64_t col = int64_t(m.cg) * kVec;
+  float a[8], b[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) { a[k] = ab[col + k]; b[k] = ab[C + col + k]; }
+  const int64_t step = m.rpi;
+  int64_t r = r0 + m.rsub;
+  for (; r + step < r1; r += 2 * step) {
+    float v0[8], v1[8], q0[8], q1[8];
+    Vec8<T>::load(x, r * C + col, v0);
+    Vec8<T>::load(x, (r + step) * C + col, v1);
+    if constexpr (RES) {
+      Vec8<T>::load(res, r * C + col, q0);
+      Vec8<T>::load(res, (r + step) * C + col, q1);
+    }
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      v0[k] = fmaf(v0[k], a[k], b[k]);
+      v1[k] = fmaf(v1[k], a[k], b[k]);
+      if constexpr (RES) { v0[k] += q0[k]; v1[k] += q1[k]; }
+      if constexpr (RELU) { v0[k] = fmaxf(v0[k], 0.f); v1[k] = fmaxf(v1[k], 0.f); }
+    }
+    Vec8<T>::store(y, r * C + col, v0);
+    Vec8<T>::store(y, (r + step) * C + col, v1);
+  }
+  for (; r < r1; r += step) {
+    float v[8], q[8];
+    Vec8<T>::load(x, r * C + col, v);
+    if constexpr (RES) Vec8<T>::load(res, r * C + col, q);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      v[k] = fmaf(v[k], a[k], b[k]);
+      if constexpr (RES) v[k] += q[k];
+      if constexpr (RELU) v[k] = fmaxf(v[k], 0.f);
+    }
+    Vec8<T>::store(y, r * C + col, v);
+  }
+}
+
+template <typename T, bool RELU, bool DRES>
+__global__ __launch_bounds__(kBlock) void bn_bwd_apply_kernel(const T* __restrict__ dy, const T* __restrict__ y,
+                                                              const T* __restrict__ x, const float* __restrict__ k3,
+                                                              T* __restrict__ dx, T* __restrict__ dres, int64_t M,
+                                                              int C) {
+  const Map m = make_map(C);
+  if (!m.active) return;
+  int64_t r0, r1;
+  block_rows(M, m.rpi, r0, r1);
+  const int64_t col = int64_t(m.cg) * kVec;
+  float a[8], c2[8], c0[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) { a[k] = k3[col + k]; c2[k] = k3[C + col + k]; c0[k] = k3[2 * C + col + k]; }
+  const int64_t step = m.rpi;
+  for (int64_t r = r0 + m.rsub; r < r1; r += step) {
+    float g[8], xv[8];
+    Vec8<T>::load(dy, r * C + col, g);
+    Vec8<T>::load(x, r * C + col, xv);
+    if constexpr (RELU) {
+      float yv[8];
+      Vec8<T>::load(y, r * C + col, yv);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) g[k] = yv[k] > 0.f ? g[k] : 0.f;
+    }
+    if constexpr (DRES) Vec8<T>::store(dres, r * C + col, g);
+    float o[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) o[k] = fmaf(a[k], g[k], fmaf(c2[k], xv[k], c0[k]));
+    Vec8<T>::store(dx, r * C + col, o);
+  }
+}
+
+// ---------------------------------------------------------------- launch helpers
+struct Grid {
+  dim3 grid;
+  int nb;
+};
+
+Grid bn_grid(int64_t M, int C, int64_t cap_blocks, int iters_per_block) {
+  const int groups = C / kVec;
+  const int slices = (groups + kMaxTpr - 1) / kMaxTpr;
+  const int tpr = std::min(groups, kMaxTpr);
+  const int rpi = kBlock / tpr;
+  const int64_t iters = (M + rpi - 1) / rpi;
+  int64_t nb = (iters + iters_per_block - 1) / iters_per_block;
+  nb = std::max<int64_t>(1, std::min<int64_t>(nb, cap_blocks));
+  return {dim3(unsigned(nb), unsigned(slices)), int(nb)};
+}
+
+// partial-sum blocks: bounded so that the partial arrays stay <= 1M floats each
+Grid reduce_grid(int64_t M, int C) {
+  const int64_t cap = std::max<int64_t>(1, std::min<int64_t>(1024, (1 << 20) / C));
+  return bn_grid(M, C, cap, 8);
+}
+
+template <typename F>
+void dispatch_dt(int dt, F&& f) {
+  if (dt == kBF16) f(BF16{});
+  else if (dt == kF16) f(F16{});
+  else if (dt == kF32) f(float{});
+  else throw std::invalid_argument("batchnorm: unsupported dtype");
+}
+
+}  // namespace
+
+int64_t bn_workspace_floats(int64_t M, int C) {
+  const Grid g = reduce_grid(M, C);
+  return int64_t(2) * g.nb * C + 3 * int64_t(C);
+}
+
+void bn_fwd_train(uintptr_t x, uintptr_t residual, uintptr_t gamma, uintptr_t beta, uintptr_t running_mean,
+                  uintptr_t running_var, uintptr_t save_mean, uintptr_t save_invstd, uintptr_t y, uintptr_t workspace,
+                  int64_t M, int C, float eps, float momentum, bool relu, int dt, uintptr_t stream) {
+  VODA_CHECK(C % kVec == 0, "batchnorm: C must be a multiple of 8");
+  VODA_CHECK(M > 0, "batchnorm: empty input");
+  hipStream_t s = as_stream(stream);
+  float* ws = reinterpret_cast<float*>(workspace);
+  const Grid rg = reduce_grid(M, C);
+  float* ab = ws + int64_t(2) * rg.nb * C;
+  const Grid ag = bn_grid(M, C, 8192, 4);
+  dispatch_dt(dt, [&](auto tag) {
+    using T = decltype(tag);
+    const T* xp = reinterpret_cast<const T*>(x);
+    hipLaunchKernelGGL((bn_stats_kernel<T>), rg.grid, dim3(kBlock), 0, s, xp, ws, M, C);
+    hipLaunchKernelGGL(bn_fwd_finalize_kernel, dim3((C + kFinCh - 1) / kFinCh), dim3(kFinCh * kFinRg), 0, s, ws,
+                       rg.nb, M, C, reinterpret_cast<const float*>(gamma), reinterpret_cast<const float*>(beta),
+                       reinterpret_cast<float*>(running_mean), reinterpret_cast<float*>(running_var),
+                       reinterpret_cast<float*>(save_mean), reinterpret_cast<float*>(save_invstd), ab, eps, momentum);
+    const T* rp = reinterpret_cast<const T*>(residual);
+    T* yp = reinterpret_cast<T*>(y);
+    if (residual) {
+      if (relu) hipLaunchKernelGGL((bn_apply_kernel<T, true, true>), ag.grid, dim3(kBlock), 0, s, xp, rp, ab, yp, M, C);
+      else hipLaunchKernelGGL((bn_apply_kernel<T, true, false>), ag.grid, dim3(kBlock), 0, s, xp, rp, ab, yp, M, C);
+    } else {
+      if (relu) hipLaunchKernelGGL((bn_apply_kernel<T, false, true>), ag.grid, dim3(kBlock), 0, s, xp, rp, ab, yp, M, C);
+      else hipLaunchKernelGGL((bn_apply_kernel<T, false, false>), ag.grid, dim3(kBlock), 0, s, xp, rp, ab, yp, M, C);
+    }
+  });
+  check_launch();
+}
+
+void bn_apply(uintptr_t x, uintptr_t residual, uintptr_t ab, uintptr_t y, int64_t M, int C, bool relu, int dt,
+              uintptr_t stream) {
+  VODA_CHECK(C % kVec == 0, "batchnorm: C must be a multiple of 8");
+  hipStream_t s = as_stream(stream);
+  const Grid ag = bn_grid(M, C, 8192, 4);
+  const float* abp = reinterpret_cast<const float*>(ab);
+  dispatch_dt(dt, [&](auto tag) {
+    using T = decltype(tag);
+    const T* xp = reinterpret_cast<const T*>(x);
+    const T* rp = reinterpret_cast<const T*>(residual);
+    T* yp = reinterpret_cast<T*>(y);
+    if (residual) {
+      if (relu) hipLaunchKernelGGL((bn_apply_kernel<T, true, true>), ag.grid, dim3(kBlock), 0, s, xp, rp, abp, yp, M, C);
+      else hipLaunchKernelGGL((bn_apply_kernel<T, true, false>), ag.grid, dim3(kBlock), 0, s, xp, rp, abp, yp, M, C);
+    } else {
+      if (relu) hipLaunchKernelGGL((bn_apply_kernel<T, false, true>), ag.grid, dim3(kBlock), 0, s, xp, rp, abp, yp, M, C);
+      else hipLaunchKernelGGL((bn_apply_kernel<T, false, false>), ag.grid, dim3(kBlock), 0, s, xp, rp, abp, yp, M, C);
+    }
+  });
+  check_launch();
+}
+
+void bn_bwd(uintptr_t dy, uintptr_t y, uintptr_t x, uintptr_t save_mean, uintptr_t save_invstd, uintptr_t gamma,
+            uintptr_t dx, uintptr_t dres, uintptr_t dgamma, uintptr_t dbeta, uintptr_t workspace, int64_t M, int C,
+            bool relu, int dt, uintptr_t stream) {
+  VODA_CHECK(C % kVec == 0, "batchnorm: C must be a multiple of 8");
+  VODA_CHECK(!relu || y != 0, "batchnorm backward: ReLU mask needs the forward output");
+  hipStream_t s = as_stream(stream);
+  float* ws = reinterpret_cast<float*>(workspace);
+  const Grid rg = reduce_grid(M, C);
+  float* k3 = ws + int64_t(2) * rg.nb * C;
+  const Grid ag = bn_grid(M, C, 8192, 4);
+  dispatch_dt(dt, [&](auto tag) {
+    using T = decltype(tag);
+    const T* dyp = reinterpret_cast<const T*>(dy);
+    const T* yp = reinterpret_cast<const T*>(y);
+    const T* xp = reinterpret_cast<const T*>(x);
+    if (relu) hipLaunchKernelGGL((bn_bwd_reduce_kernel<T, true>), rg.grid, dim3(kBlock), 0, s, dyp, yp, xp, ws, M, C);
+    else hipLaunchKernelGGL((bn_bwd_reduce_kernel<T, false>), rg.grid, dim3(kBlock), 0, s, dyp, yp, xp, ws, M, C);
+    hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + kFinCh - 1) / kFinCh), dim3(kFinCh * kFinRg), 0, s, ws,
+                       rg.nb, M, C, reinterpret_cast<const float*>(gamma), reinterpret_cast<const float*>(save_mean),
+                       reinterpret_cast<const float*>(save_invstd), reinterpret_cast<float*>(dgamma),
+                       reinterpret_cast<float*>(dbeta), k3);
+    T* dxp = reinterpret_cast<T*>(dx);
+    T* drp = reinterpret_cast<T*>(dres);
+    if (relu) {
+      if (dres) hipLaunchKernelGGL((bn_bwd_apply_kernel<T, true, true>), ag.grid, dim3(kBlock), 0, s, dyp, yp, xp, k3, dxp, drp, M, C);
+      else hipLaunchKernelGGL((bn_bwd_apply_kernel<T, true, false>), ag.grid, dim3(kBlock), 0, s, dyp, yp, xp, k3, dxp, drp, M, C);
+    } else {
+      if (dres) hipLaunchKernelGGL((bn_bwd_apply_kernel<T, false, true>), ag.grid, dim3(kBlock), 0, s, dyp, yp, xp, k3, dxp, drp, M, C);
+      else hipLaunchKernelGGL((bn_bwd_apply_kernel<T, false, false>), ag.grid, dim3(kBlock), 0, s, dyp, yp, xp, k3, dxp, drp, M, C);
+    }
+  });
+  check_launch();
+}
+
+}  // namespace voda

@@ -27,6 +27,11 @@ PYBIND11_MODULE(_vodahip, m) {
   m.def("masked_softmax_fwd", &masked_softmax_fwd);
   m.def("masked_softmax_bwd", &masked_softmax_bwd);
 
+  m.def("bn_workspace_floats", &bn_workspace_floats);
+  m.def("bn_fwd_train", &bn_fwd_train);
+  m.def("bn_apply", &bn_apply);
+  m.def("bn_bwd", &bn_bwd);
+
   m.def("rccl_unique_id", [] { return py::bytes(rccl_unique_id()); });
   m.def("rccl_version", &rccl_version);
 

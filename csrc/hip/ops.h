@@ -45,6 +45,17 @@ void masked_softmax_fwd(uintptr_t x, uintptr_t mask, int mask_dt, uintptr_t y, i
 void masked_softmax_bwd(uintptr_t y, uintptr_t dy, uintptr_t dx, int64_t rows, int S, float scale, int dt,
                         uintptr_t stream);
 
+// ---- fused BatchNorm(+add)(+ReLU), channels_last [M][C] (batchnorm.hip) ----
+int64_t bn_workspace_floats(int64_t M, int C);
+void bn_fwd_train(uintptr_t x, uintptr_t residual, uintptr_t gamma, uintptr_t beta, uintptr_t running_mean,
+                  uintptr_t running_var, uintptr_t save_mean, uintptr_t save_invstd, uintptr_t y, uintptr_t workspace,
+                  int64_t M, int C, float eps, float momentum, bool relu, int dt, uintptr_t stream);
+void bn_apply(uintptr_t x, uintptr_t residual, uintptr_t ab, uintptr_t y, int64_t M, int C, bool relu, int dt,
+              uintptr_t stream);
+void bn_bwd(uintptr_t dy, uintptr_t y, uintptr_t x, uintptr_t save_mean, uintptr_t save_invstd, uintptr_t gamma,
+            uintptr_t dx, uintptr_t dres, uintptr_t dgamma, uintptr_t dbeta, uintptr_t workspace, int64_t M, int C,
+            bool relu, int dt, uintptr_t stream);
+
 // ---- RCCL engine (comm.cpp) ----
 std::string rccl_unique_id();
 int rccl_version();

@@ -1,0 +1,86 @@
+"""Fused BN(+residual)(+ReLU) HIP kernels vs an fp32 PyTorch reference (csrc/hip/batchnorm.hip)."""
+import pytest
+import torch
+import torch.nn.functional as F
+
+from vodascheduler_amd.ops.batchnorm import FusedBatchNorm2d, batch_norm_act
+
+pytestmark = pytest.mark.gpu
+
+
+def _ref(x, w, b, rm, rv, res, relu, mom, eps):
+    y = F.batch_norm(x.float(), rm, rv, w, b, True, mom, eps)
+    if res is not None:
+        y = y + res.float()
+    return F.relu(y) if relu else y
+
+
+@pytest.mark.parametrize("shape", [(8, 64, 14, 14), (4, 80, 9, 9), (2, 256, 7, 5), (3, 2048, 3, 3), (2, 4096, 2, 3),
+                                   (64, 64, 56, 56)])
+@pytest.mark.parametrize("res,relu", [(False, True), (True, True), (False, False), (True, False)])
+@pytest.mark.parametrize("dt", [torch.bfloat16, torch.float32])
+def test_bn_act_fwd_bwd(shape, res, relu, dt):
+    torch.manual_seed(0)
+    dev = "cuda"
+    C = shape[1]
+    x = (torch.randn(shape, device=dev) * 2 + 0.5).to(dt).to(memory_format=torch.channels_last).requires_grad_()
+    r = torch.randn(shape, device=dev).to(dt).to(memory_format=torch.channels_last).requires_grad_() if res else None
+    w = (torch.rand(C, device=dev) + 0.5).requires_grad_()
+    b = torch.randn(C, device=dev).requires_grad_()
+    rm, rv = torch.zeros(C, device=dev), torch.ones(C, device=dev)
+    rm2, rv2 = rm.clone(), rv.clone()
+    y = batch_norm_act(x, w, b, rm, rv, True, 0.1, 1e-5, r, relu)
+    assert y.is_contiguous(memory_format=torch.channels_last)
+    xr = x.detach().float().requires_grad_()
+    rr = r.detach().float().requires_grad_() if res else None
+    wr, br = w.detach().clone().requires_grad_(), b.detach().clone().requires_grad_()
+    yr = _ref(xr, wr, br, rm2, rv2, rr, relu, 0.1, 1e-5)
+    tol = 3e-2 if dt == torch.bfloat16 else 1e-4
+    torch.testing.assert_close(y.float(), yr, atol=tol, rtol=tol)
+    torch.testing.assert_close(rm, rm2, atol=1e-4, rtol=1e-4)
+    torch.testing.assert_close(rv, rv2, atol=1e-3, rtol=1e-3)
+    dy = torch.randn(shape, device=dev).to(dt).to(memory_format=torch.channels_last)
+    y.backward(dy)
+    yr.backward(dy.float())
+    gtol = 5e-2 if dt == torch.bfloat16 else 1e-3
+    torch.testing.assert_close(x.grad.float(), xr.grad, atol=gtol, rtol=gtol)
+    M = x.numel() // C
+    torch.testing.assert_close(w.grad, wr.grad, atol=gtol * M ** 0.5, rtol=gtol)
+    torch.testing.assert_close(b.grad, br.grad, atol=gtol * M ** 0.5, rtol=gtol)
+    if res:
+        torch.testing.assert_close(r.grad.float(), rr.grad, atol=gtol, rtol=gtol)
+
+
+def test_fused_bn_module_eval_and_autocast():
+    torch.manual_seed(0)
+    m = FusedBatchNorm2d(64, relu=True).cuda()
+    ref = torch.nn.BatchNorm2d(64).cuda()
+    ref.load_state_dict(m.state_dict())
+    x = torch.randn(4, 64, 8, 8, device="cuda").to(memory_format=torch.channels_last)
+    for _ in range(3):
+        m(x)
+        ref(x)
+    torch.testing.assert_close(m.running_mean, ref.running_mean, atol=1e-5, rtol=1e-5)
+    torch.testing.assert_close(m.running_var, ref.running_var, atol=1e-4, rtol=1e-4)
+    assert int(m.num_batches_tracked) == 3
+    m.eval()
+    ref.eval()
+    torch.testing.assert_close(m(x), F.relu(ref(x)), atol=1e-5, rtol=1e-5)
+    m.train()
+    with torch.autocast("cuda", dtype=torch.bfloat16):
+        conv = torch.nn.Conv2d(64, 64, 1).cuda().to(memory_format=torch.channels_last)
+        y = m(conv(x))
+    assert y.dtype == torch.bfloat16
+
+
+def test_resnet50_step_uses_fused_bn_kernels():
+    from vodascheduler_amd.models import resnet50
+
+    torch.manual_seed(0)
+    m = resnet50().cuda().to(memory_format=torch.channels_last)
+    x = torch.randn(4, 3, 64, 64, device="cuda").to(memory_format=torch.channels_last)
+    with torch.autocast("cuda", dtype=torch.bfloat16):
+        out = m(x)
+    out.float().sum().backward()
+    assert torch.isfinite(out.float()).all()
+    assert all(p.grad is not None and torch.isfinite(p.grad).all() for p in m.parameters())

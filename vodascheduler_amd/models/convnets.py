@@ -16,6 +16,8 @@ import torch
 import torch.nn.functional as F
 from torch import nn
 
+from ..ops.batchnorm import FusedBatchNorm2d
+
 
 def _vgg_block(cin, cout, n):
     layers = []
@@ -76,10 +78,10 @@ class BasicConv(nn.Module):
     def __init__(self, cin, cout, **kw):
         super().__init__()
         self.conv = nn.Conv2d(cin, cout, bias=False, **kw)
-        self.bn = nn.BatchNorm2d(cout, eps=0.001)
+        self.bn = FusedBatchNorm2d(cout, eps=0.001, relu=True)
 
     def forward(self, x):
-        return F.relu(self.bn(self.conv(x)), inplace=True)
+        return self.bn(self.conv(x))  # fused BN + ReLU (HIP)
 
 
 class InceptionA(nn.Module):

@@ -2,14 +2,18 @@
 
 Reference workload: ``applications.ResNet50(weights=None, classes=10)`` on CIFAR-10
 (reference examples/py/tensorflow2/tensorflow2_keras_cifar_elastic.py:148-151) and the
-BASELINE config "8 ResNet-50 ImageNet-shape jobs".  Convolutions/BatchNorm run on MIOpen
+BASELINE config "8 ResNet-50 ImageNet-shape jobs".  Convolutions run on MIOpen
 through PyTorch-ROCm in channels_last bf16 (NHWC is MIOpen's fast layout on CDNA);
-random-init weights, synthetic data.
+random-init weights, synthetic data.  Every BatchNorm is the fused HIP
+BN(+residual)(+ReLU) of ops/batchnorm.py: the bottleneck's ``relu(bn3(conv3) + identity)``
+is ONE statistics pass + ONE apply pass forward, instead of MIOpen BN + add + ReLU.
 """
 from __future__ import annotations
 
 import torch
 from torch import nn
+
+from ..ops.batchnorm import FusedBatchNorm2d
 
 
 class Bottleneck(nn.Module):
@@ -19,22 +23,18 @@ class Bottleneck(nn.Module):
         super().__init__()
         width = planes
         self.conv1 = nn.Conv2d(inplanes, width, 1, bias=False)
-        self.bn1 = nn.BatchNorm2d(width)
+        self.bn1 = FusedBatchNorm2d(width, relu=True)
         self.conv2 = nn.Conv2d(width, width, 3, stride=stride, padding=1, bias=False)  # v1.5: stride on 3x3
-        self.bn2 = nn.BatchNorm2d(width)
+        self.bn2 = FusedBatchNorm2d(width, relu=True)
         self.conv3 = nn.Conv2d(width, planes * self.expansion, 1, bias=False)
-        self.bn3 = nn.BatchNorm2d(planes * self.expansion)
-        self.relu = nn.ReLU(inplace=True)
+        self.bn3 = FusedBatchNorm2d(planes * self.expansion, relu=True)  # relu(bn3(.) + identity)
         self.downsample = downsample
 
     def forward(self, x):
-        idt = x
-        out = self.relu(self.bn1(self.conv1(x)))
-        out = self.relu(self.bn2(self.conv2(out)))
-        out = self.bn3(self.conv3(out))
-        if self.downsample is not None:
-            idt = self.downsample(x)
-        return self.relu(out + idt)
+        out = self.bn1(self.conv1(x))
+        out = self.bn2(self.conv2(out))
+        idt = x if self.downsample is None else self.downsample(x)
+        return self.bn3(self.conv3(out), idt)
 
 
 class BasicBlock(nn.Module):
@@ -43,17 +43,14 @@ class BasicBlock(nn.Module):
     def __init__(self, inplanes: int, planes: int, stride: int = 1, downsample: nn.Module | None = None):
         super().__init__()
         self.conv1 = nn.Conv2d(inplanes, planes, 3, stride=stride, padding=1, bias=False)
-        self.bn1 = nn.BatchNorm2d(planes)
+        self.bn1 = FusedBatchNorm2d(planes, relu=True)
         self.conv2 = nn.Conv2d(planes, planes, 3, padding=1, bias=False)
-        self.bn2 = nn.BatchNorm2d(planes)
-        self.relu = nn.ReLU(inplace=True)
+        self.bn2 = FusedBatchNorm2d(planes, relu=True)  # relu(bn2(.) + identity)
         self.downsample = downsample
 
     def forward(self, x):
         idt = x if self.downsample is None else self.downsample(x)
-        out = self.relu(self.bn1(self.conv1(x)))
-        out = self.bn2(self.conv2(out))
-        return self.relu(out + idt)
+        return self.bn2(self.conv2(self.bn1(self.conv1(x))), idt)
 
 
 class ResNet(nn.Module):
@@ -61,11 +58,10 @@ class ResNet(nn.Module):
         super().__init__()
         self.inplanes = 64
         if small_input:  # CIFAR-style 32x32 stem
-            self.stem = nn.Sequential(nn.Conv2d(3, 64, 3, padding=1, bias=False), nn.BatchNorm2d(64),
-                                      nn.ReLU(inplace=True))
+            self.stem = nn.Sequential(nn.Conv2d(3, 64, 3, padding=1, bias=False), FusedBatchNorm2d(64, relu=True))
         else:
-            self.stem = nn.Sequential(nn.Conv2d(3, 64, 7, stride=2, padding=3, bias=False), nn.BatchNorm2d(64),
-                                      nn.ReLU(inplace=True), nn.MaxPool2d(3, stride=2, padding=1))
+            self.stem = nn.Sequential(nn.Conv2d(3, 64, 7, stride=2, padding=3, bias=False),
+                                      FusedBatchNorm2d(64, relu=True), nn.MaxPool2d(3, stride=2, padding=1))
         self.layer1 = self._make(block, 64, layers[0])
         self.layer2 = self._make(block, 128, layers[1], stride=2)
         self.layer3 = self._make(block, 256, layers[2], stride=2)
@@ -88,7 +84,7 @@ class ResNet(nn.Module):
         down = None
         if stride != 1 or self.inplanes != planes * block.expansion:
             down = nn.Sequential(nn.Conv2d(self.inplanes, planes * block.expansion, 1, stride=stride, bias=False),
-                                 nn.BatchNorm2d(planes * block.expansion))
+                                 FusedBatchNorm2d(planes * block.expansion))
         layers = [block(self.inplanes, planes, stride, down)]
         self.inplanes = planes * block.expansion
         layers += [block(self.inplanes, planes) for _ in range(1, blocks)]

@@ -1,0 +1,135 @@
+"""Fused BatchNorm2d (+ residual add) (+ ReLU) on channels_last activations
+(csrc/hip/batchnorm.hip).
+
+``batch_norm_act(x, weight, bias, running_mean, running_var, training, momentum, eps,
+residual=None, relu=True)`` computes ``relu(bn(x) + residual)`` (either extra optional) in
+one statistics pass + one apply pass forward and one reduction pass + one apply pass
+backward, instead of MIOpen BN + separate ReLU / add / ReLU-backward kernels.  The ReLU
+mask of the backward comes from the saved output.  Statistics, running-stat updates and
+the affine parameters stay fp32; activations are bf16/fp16/fp32.
+
+GPU requirements: 4-D input in channels_last memory format (or a contiguous [M, C]
+matrix) with C % 8 == 0; anything else, and CPU tensors, use the PyTorch reference
+composition (which the GPU tests compare against).
+"""
+from __future__ import annotations
+
+import torch
+import torch.nn.functional as F
+
+from . import _native as N
+
+
+def _rows_view_ok(x: torch.Tensor) -> bool:
+    if x.dim() == 4:
+        return x.is_contiguous(memory_format=torch.channels_last)
+    return x.dim() == 2 and x.is_contiguous()
+
+
+def _supported(x, residual) -> bool:
+    if not x.is_cuda or x.dtype not in (torch.bfloat16, torch.float16, torch.float32):
+        return False
+    C = x.shape[1]
+    if C % 8 != 0 or not _rows_view_ok(x) or x.numel() == 0:
+        return False
+    if residual is not None and (residual.shape != x.shape or residual.dtype != x.dtype
+                                 or residual.stride() != x.stride()):
+        return False
+    return True
+
+
+class _BNActFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, residual, weight, bias, running_mean, running_var, momentum, eps, relu):
+        C = x.shape[1]
+        M = x.numel() // C
+        h = N.hip()
+        y = torch.empty_like(x)
+        save_mean = torch.empty(C, dtype=torch.float32, device=x.device)
+        save_invstd = torch.empty(C, dtype=torch.float32, device=x.device)
+        ws = torch.empty(h.bn_workspace_floats(M, C), dtype=torch.float32, device=x.device)
+        h.bn_fwd_train(x.data_ptr(), N.ptr(residual), N.ptr(weight), N.ptr(bias), N.ptr(running_mean),
+                       N.ptr(running_var), save_mean.data_ptr(), save_invstd.data_ptr(), y.data_ptr(),
+                       ws.data_ptr(), M, C, float(eps), float(momentum), bool(relu), N.dtype_code(x.dtype),
+                       N.stream_of(x))
+        ctx.relu = bool(relu)
+        ctx.has_res = residual is not None
+        ctx.save_for_backward(x, y if relu else None, weight, save_mean, save_invstd)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, y, weight, save_mean, save_invstd = ctx.saved_tensors
+        C = x.shape[1]
+        M = x.numel() // C
+        h = N.hip()
+        if not _rows_view_ok(dy) or dy.stride() != x.stride():
+            dy = dy.contiguous(memory_format=torch.channels_last) if dy.dim() == 4 else dy.contiguous()
+        dx = torch.empty_like(x)
+        dres = torch.empty_like(x) if ctx.has_res and ctx.needs_input_grad[1] else None
+        need_w = weight is not None and ctx.needs_input_grad[2]
+        need_b = ctx.needs_input_grad[3]
+        dw = torch.empty(C, dtype=torch.float32, device=x.device) if need_w else None
+        db = torch.empty(C, dtype=torch.float32, device=x.device) if need_b else None
+        ws = torch.empty(h.bn_workspace_floats(M, C), dtype=torch.float32, device=x.device)
+        h.bn_bwd(dy.data_ptr(), N.ptr(y), x.data_ptr(), save_mean.data_ptr(), save_invstd.data_ptr(), N.ptr(weight),
+                 dx.data_ptr(), N.ptr(dres), N.ptr(dw), N.ptr(db), ws.data_ptr(), M, C, ctx.relu,
+                 N.dtype_code(x.dtype), N.stream_of(x))
+        if dres is None and ctx.has_res and ctx.needs_input_grad[1]:
+            dres = dy
+        return dx, dres, dw, db, None, None, None, None, None
+
+
+def _reference(x, weight, bias, running_mean, running_var, training, momentum, eps, residual, relu):
+    y = F.batch_norm(x, running_mean, running_var, weight, bias, training, momentum, eps)
+    if residual is not None:
+        y = y + residual
+    return F.relu(y) if relu else y
+
+
+def batch_norm_act(x: torch.Tensor, weight: torch.Tensor | None, bias: torch.Tensor | None,
+                   running_mean: torch.Tensor | None, running_var: torch.Tensor | None, training: bool = True,
+                   momentum: float = 0.1, eps: float = 1e-5, residual: torch.Tensor | None = None,
+                   relu: bool = True) -> torch.Tensor:
+    if not _supported(x, residual):
+        return _reference(x, weight, bias, running_mean, running_var, training, momentum, eps, residual, relu)
+    if training or running_mean is None:
+        return _BNActFn.apply(x, residual, weight, bias, running_mean, running_var, momentum, eps, relu)
+    # inference: per-channel affine from the running statistics, one apply pass
+    C = x.shape[1]
+    invstd = torch.rsqrt(running_var.float() + eps)
+    a = invstd * (weight.float() if weight is not None else 1.0)
+    b = (bias.float() if bias is not None else 0.0) - running_mean.float() * a
+    ab = torch.cat([a.reshape(C), b.reshape(C)]).contiguous()
+    y = torch.empty_like(x)
+    N.hip().bn_apply(x.data_ptr(), N.ptr(residual), ab.data_ptr(), y.data_ptr(), x.numel() // C, C, bool(relu),
+                     N.dtype_code(x.dtype), N.stream_of(x))
+    return y
+
+
+class FusedBatchNorm2d(torch.nn.BatchNorm2d):
+    """``BatchNorm2d`` whose forward optionally adds a residual and applies ReLU:
+    ``forward(x, residual=None) = relu?(bn(x) + residual)``.  State dict compatible with
+    ``torch.nn.BatchNorm2d``."""
+
+    def __init__(self, num_features: int, eps: float = 1e-5, momentum: float = 0.1, relu: bool = False, **kw):
+        super().__init__(num_features, eps=eps, momentum=momentum, **kw)
+        self.relu = relu
+
+    def forward(self, x, residual=None):
+        if self.training and self.track_running_stats:
+            self.num_batches_tracked.add_(1)
+        use_batch = self.training or not self.track_running_stats
+        momentum = self.momentum if self.momentum is not None else 0.1
+        if x.is_cuda and torch.is_autocast_enabled("cuda"):
+            with torch.autocast("cuda", enabled=False):  # keep the activation dtype, fp32 stats
+                return batch_norm_act(x, self.weight, self.bias, self.running_mean if self.track_running_stats
+                                      else None, self.running_var if self.track_running_stats else None,
+                                      use_batch, momentum, self.eps, residual, self.relu)
+        return batch_norm_act(x, self.weight, self.bias,
+                              self.running_mean if self.track_running_stats else None,
+                              self.running_var if self.track_running_stats else None,
+                              use_batch, momentum, self.eps, residual, self.relu)
+
+    def extra_repr(self):
+        return super().extra_repr() + f", relu={self.relu}"
