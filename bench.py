@@ -37,7 +37,7 @@ import torch.distributed as dist  # noqa: E402
 
 sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 
-from vodascheduler_amd.models import get_workload  # noqa: E402
+from vodascheduler_amd.models import get_workload, prepare_model  # noqa: E402
 from vodascheduler_amd.ops import _native  # noqa: E402
 from vodascheduler_amd.ops.optim import make_optimizer  # noqa: E402
 from vodascheduler_amd.parallel.comm import RcclCommunicator  # noqa: E402
@@ -62,9 +62,7 @@ def warmup(device, steps: int):
     for name in MODELS:
         w = get_workload(name)
         torch.manual_seed(0)
-        m = w.build().to(device)
-        if w.channels_last:
-            m = m.to(memory_format=torch.channels_last)
+        m = prepare_model(w, device)
         opt = make_optimizer(w.optimizer, m.parameters(), **w.opt_kwargs)
         b = w.make_batch(BATCH[name], device, None)
         if w.channels_last:

@@ -16,7 +16,7 @@ import time
 import torch
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
-from vodascheduler_amd.models import get_workload  # noqa: E402
+from vodascheduler_amd.models import get_workload, prepare_model  # noqa: E402
 from vodascheduler_amd.ops import _native  # noqa: E402
 from vodascheduler_amd.ops.optim import make_optimizer  # noqa: E402
 
@@ -26,9 +26,7 @@ def run(model: str, batch: int | None, steps: int, warmup: int) -> dict:
     w = get_workload(model)
     bs = batch or w.per_gpu_batch
     torch.manual_seed(0)
-    m = w.build().to(dev)
-    if w.channels_last:
-        m = m.to(memory_format=torch.channels_last)
+    m = prepare_model(w, dev)
     opt = make_optimizer(w.optimizer, m.parameters(), **w.opt_kwargs)
     b = w.make_batch(bs, dev, None)
     if w.channels_last:

@@ -86,3 +86,35 @@ def test_cpu_layernorm_and_softmax_reference():
     assert torch.allclose(y.sum(-1), torch.ones(2, 2, 4))
     assert y[0, 0, 0, 1:].abs().max() < 1e-6
     torch.testing.assert_close(y, reference_masked_softmax(s, None, True))
+
+
+def test_fused_bn_module_cpu_matches_reference():
+    import torch.nn.functional as F
+
+    from vodascheduler_amd.ops.batchnorm import FusedBatchNorm2d
+
+    torch.manual_seed(0)
+    m = FusedBatchNorm2d(16, relu=True)
+    ref = torch.nn.BatchNorm2d(16)
+    x = torch.randn(4, 16, 5, 5)
+    r = torch.randn(4, 16, 5, 5)
+    torch.testing.assert_close(m(x, r), F.relu(ref(x) + r))
+    torch.testing.assert_close(m.running_var, ref.running_var)
+
+
+def test_optimizer_splits_param_groups_by_dtype():
+    from vodascheduler_amd.models import cast_compute_weights_
+    from vodascheduler_amd.models.transformer import BertBase
+    from vodascheduler_amd.ops.optim import FusedAdamW
+
+    m = BertBase(vocab=100, seq_len=8, d_model=32, heads=2, d_ff=64, layers=1)
+    cast_compute_weights_(m)
+    assert m.mlm_out.weight is m.emb.tok.weight and m.mlm_out.weight.dtype == torch.bfloat16
+    assert m.emb_ln.weight.dtype == torch.float32
+    opt = FusedAdamW(m.parameters(), lr=1e-3)
+    dts = sorted(str(fg.param_dtype) for fg in opt.flat_groups)
+    assert dts == ["torch.bfloat16", "torch.float32"]
+    bf = next(fg for fg in opt.flat_groups if fg.param_dtype == torch.bfloat16)
+    assert bf.master.dtype == torch.float32 and bf.lowp.dtype == torch.bfloat16 and bf.grad.dtype == torch.bfloat16
+    n = sum(p.numel() for p in {id(p): p for p in m.parameters()}.values())
+    assert sum(sum(s.numel for s in fg.slots) for fg in opt.flat_groups) == n

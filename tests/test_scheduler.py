@@ -75,6 +75,26 @@ def test_rate_limit_coalesces_requests():
     assert e.core.resched_count == 2  # nothing pending, nothing runs
 
 
+@pytest.mark.parametrize("work_conserving", [True, False])
+def test_completion_reschedules_immediately_when_work_conserving(work_conserving):
+    e = Env(gpus=2, algorithm="FIFO", rate=30)
+    e.core.work_conserving = work_conserving
+    a = e.submit("a", 2, 2, 2)
+    e.step()
+    b = e.submit("b", 2, 2, 2)
+    e.step(1)
+    assert e.core.job_num_gpu[b] == 0  # queued behind a, arrival rate-limited
+    e.core.handle_job_finished(a, True)
+    e.step(1)
+    # freed GPUs go to the waiting job at once; the reference waits out the rate limit
+    assert e.core.job_num_gpu[b] == (2 if work_conserving else 0)
+    e.step(30)
+    assert e.core.job_num_gpu[b] == 2
+    c = e.submit("c", 1, 1, 1)
+    e.step(1)
+    assert e.core.job_num_gpu[c] == 0  # arrivals are still rate-limited
+
+
 def test_finish_and_scale_actions():
     e = Env(rate=0)
     a = e.submit("a", 1, 1, 8)

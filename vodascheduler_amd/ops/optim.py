@@ -18,13 +18,30 @@ from ..utils.flat import FlatGroup
 from . import _native as N
 
 
+def _split_by_dtype(params) -> list[dict]:
+    """Param groups with one dtype each: a model whose GEMM/conv weights are stored in bf16
+    (``models.cast_compute_weights_``) and whose norm parameters stay fp32 gets one flat
+    group per dtype -- the bf16 group keeps an fp32 master + bf16 model copy + bf16 grads."""
+    params = list(params)
+    groups = params if params and isinstance(params[0], dict) else [{"params": params}]
+    out = []
+    for g in groups:
+        ps = list(g["params"])
+        by: dict[torch.dtype, list] = {}
+        for p in ps:
+            by.setdefault(p.dtype, []).append(p)
+        for dt in sorted(by, key=str):
+            out.append({**g, "params": by[dt]})
+    return out
+
+
 class _FusedFlatOptimizer(torch.optim.Optimizer):
     """Base class: owns one :class:`FlatGroup` per param group."""
 
     _state_names: tuple[str, ...] = ()
 
     def __init__(self, params, defaults, grad_dtype: torch.dtype | None = None):
-        super().__init__(params, defaults)
+        super().__init__(_split_by_dtype(params), defaults)
         self.flat_groups: list[FlatGroup] = []
         self._flat_state: list[dict[str, torch.Tensor]] = []
         self._steps: list[int] = []

@@ -48,7 +48,8 @@ class SchedulerCore:
     def __init__(self, scheduler_id: str, store: JobStore, allocator: Allocator, backend: Backend,
                  placement: PlacementManager | None = None, clock: Clock | None = None,
                  algorithm: str = DEFAULT_ALGORITHM, rate_limit_sec: float = RESCHED_RATE_LIMIT_SEC,
-                 tick_sec: float = TIME_METRICS_TICK_SEC, resume: bool = False, use_placement: bool = True):
+                 tick_sec: float = TIME_METRICS_TICK_SEC, resume: bool = False, use_placement: bool = True,
+                 work_conserving: bool = True):
         if algorithm not in ALGORITHMS:
             raise KeyError(f"Not found: algorithm {algorithm!r}")
         self.scheduler_id = scheduler_id
@@ -58,6 +59,14 @@ class SchedulerCore:
         self.clock = clock or RealClock()
         self.algorithm = algorithm
         self.rate_limit_sec = float(rate_limit_sec)
+        # Work-conserving rescheduling (documented deviation): a reschedule requested because
+        # GPUs were FREED (job completed / failed / deleted) runs immediately instead of
+        # waiting out the rate limit -- the reference rate-limits every trigger
+        # (scheduler.go:300-316), which leaves freed GPUs idle for up to ``rate_limit``
+        # seconds.  Arrivals and priority changes are still rate-limited, so bursts of
+        # submissions still coalesce into one reschedule.
+        self.work_conserving = work_conserving
+        self._urgent = False
         self.tick_sec = float(tick_sec)
         self.use_placement = use_placement
         self.placement = placement if placement is not None else (
@@ -115,7 +124,8 @@ class SchedulerCore:
     def next_wakeup(self) -> float:
         t = self.next_tick
         if self._requests:
-            t = min(t, max(self._requests[0][0], self.resched_blocked_until))
+            block = float("-inf") if self._urgent else self.resched_blocked_until
+            t = min(t, max(self._requests[0][0], block))
         return t
 
     def poll(self) -> None:
@@ -124,7 +134,9 @@ class SchedulerCore:
         while now >= self.next_tick:
             self.next_tick += self.tick_sec
             self.update_time_metrics()
-        if self._requests and now >= max(self._requests[0][0], self.resched_blocked_until):
+        block = float("-inf") if self._urgent else self.resched_blocked_until
+        if self._requests and now >= max(self._requests[0][0], block):
+            self._urgent = False
             seq_at_start = self._seq
             self.resched()
             t = self.clock.now()
@@ -274,6 +286,7 @@ class SchedulerCore:
         if running or st.done:
             self.backend.delete_job(name)
         if running:
+            self._urgent = self._urgent or self.work_conserving
             self.trigger_resched()
         self.metrics.jobs_deleted.inc()
         self._emit("deleted", job=name)
@@ -293,6 +306,7 @@ class SchedulerCore:
         self.job_workers.pop(name, None)
         (self.metrics.jobs_completed if succeeded else self.metrics.jobs_failed).inc()
         self._emit("finished", job=name, succeeded=succeeded)
+        self._urgent = self._urgent or self.work_conserving
         self.trigger_resched()
 
     # ------------------------------------------------------------------ nodes

@@ -47,6 +47,8 @@ def build_parser() -> argparse.ArgumentParser:
     ap.add_argument("--no-placement", action="store_true", help="disable the Munkres placement manager")
     ap.add_argument("--rate-limit", type=float, default=RESCHED_RATE_LIMIT_SEC)
     ap.add_argument("--tick", type=float, default=TIME_METRICS_TICK_SEC)
+    ap.add_argument("--strict-rate-limit", action="store_true",
+                    help="rate-limit reschedules triggered by job completion too (reference behaviour)")
     ap.add_argument("--store", default="memory://", help="memory:// or sqlite:///path")
     ap.add_argument("--mq", default="inproc://", help="inproc:// or sqlite:///path")
     ap.add_argument("--allocator", default=None, help="URL of a remote allocator service")
@@ -94,7 +96,7 @@ class SchedulerProcess:
         alloc = HttpAllocatorClient(a.allocator) if a.allocator else ResourceAllocator(self.store)
         self.core = SchedulerCore(a.gpu_type, self.store, alloc, self.backend, algorithm=a.algorithm,
                                   rate_limit_sec=a.rate_limit, tick_sec=a.tick, resume=a.resume,
-                                  use_placement=not a.no_placement)
+                                  use_placement=not a.no_placement, work_conserving=not a.strict_rate_limit)
         self.runner = SchedulerRunner(self.core, self.mq, queue_name=a.gpu_type)
         self.http: HttpServer | None = None
         self._collector_stop = threading.Event()

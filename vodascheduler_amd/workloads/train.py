@@ -24,7 +24,7 @@ from dataclasses import dataclass
 
 import torch
 
-from ..models import get_workload
+from ..models import get_workload, prepare_model
 from ..ops.optim import make_optimizer
 from ..parallel.ddp import ElasticDDP
 from ..runtime.elastic import ElasticContext, TorchState, run
@@ -53,9 +53,7 @@ class TrainConfig:
 def build(cfg: TrainConfig, device: torch.device):
     w = get_workload(cfg.model)
     torch.manual_seed(cfg.seed)  # identical init everywhere (state is broadcast anyway)
-    model = w.build().to(device)
-    if w.channels_last and device.type == "cuda":
-        model = model.to(memory_format=torch.channels_last)
+    model = prepare_model(w, device, cfg.amp)
     kw = dict(w.opt_kwargs)
     if cfg.lr is not None:
         kw["lr"] = cfg.lr
