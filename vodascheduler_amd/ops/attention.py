@@ -1,34 +1,30 @@
 """Scaled dot-product attention with key-padding + causal masks.
 
-Dispatch (GPU): the fused MFMA flash-attention HIP kernel (csrc/hip/attention.hip) when the
-extension provides it for the shape (bf16/fp16, supported head dim, no dropout); otherwise
-the materialised path -- scores by hipBLASLt GEMM, the hand-written masked-softmax HIP
-kernel, dropout, PV GEMM.  The reference's Transformer materialises the full
-[B, H, Tq, S] scores too (layers_tf25.py:450-461).  CPU: the same materialised math with the
-fp32 reference softmax.
+Dispatch (GPU): the fused MFMA attention HIP kernels (csrc/hip/attention.hip, ops/flash.py)
+when the shape is supported (bf16, head dim 32/64/128, Tq, Tk <= 128, no dropout);
+otherwise the materialised path -- scores by hipBLASLt GEMM, the hand-written
+masked-softmax HIP kernel, dropout, PV GEMM.  The reference's Transformer materialises
+the full [B, H, Tq, S] scores (layers_tf25.py:450-461).  CPU: the same materialised math
+with the fp32 reference softmax.
+
+Layouts: ``attention_qkvpacked`` takes the fused projection [B, T, 3, H, D] and
+``attention_q_kvpacked`` q [B, Tq, H, D] + kv [B, Tk, 2, H, D]; both return
+[B, Tq, H, D] (= the [B, Tq, H*D] input of the output projection, no copy).
 """
 from __future__ import annotations
 
 import torch
 
-from . import _native as N
+from . import flash
 from .softmax import masked_softmax
 
 
-def _flash_supported(q, k, v, key_mask, dropout_p) -> bool:
-    if not q.is_cuda or dropout_p > 0.0 or q.dtype not in (torch.bfloat16, torch.float16):
-        return False
-    try:
-        h = N.hip()
-    except RuntimeError:
-        return False
-    if not hasattr(h, "attention_supported"):
-        return False
-    B, H, Tq, D = q.shape
-    return bool(h.attention_supported(D, k.shape[2], N.dtype_code(q.dtype)))
+def _flash_ok(q: torch.Tensor, Tk: int, dropout_p: float) -> bool:
+    return dropout_p == 0.0 and q.is_cuda and flash.supported(q.shape[-1], q.shape[1], Tk, q.dtype)
 
 
 def materialized_attention(q, k, v, key_mask=None, causal=False, scale=1.0, dropout_p=0.0):
+    """q/k/v [B, H, T, D] -> [B, H, Tq, D]."""
     scores = torch.matmul(q, k.transpose(-1, -2))
     km = None
     if key_mask is not None:
@@ -39,13 +35,33 @@ def materialized_attention(q, k, v, key_mask=None, causal=False, scale=1.0, drop
     return torch.matmul(p, v)
 
 
+def attention_qkvpacked(qkv: torch.Tensor, key_mask=None, causal: bool = False, scale: float | None = None,
+                        dropout_p: float = 0.0) -> torch.Tensor:
+    """qkv [B, T, 3, H, D] -> [B, T, H, D]."""
+    D = qkv.shape[-1]
+    scale = D ** -0.5 if scale is None else scale
+    if _flash_ok(qkv[:, :, 0], qkv.shape[1], dropout_p):
+        return flash.attention_qkvpacked(qkv, key_mask, causal, scale)
+    q, k, v = (qkv[:, :, i].transpose(1, 2) for i in range(3))
+    return materialized_attention(q, k, v, key_mask, causal, scale, dropout_p).transpose(1, 2)
+
+
+def attention_q_kvpacked(q: torch.Tensor, kv: torch.Tensor, key_mask=None, causal: bool = False,
+                         scale: float | None = None, dropout_p: float = 0.0) -> torch.Tensor:
+    """q [B, Tq, H, D], kv [B, Tk, 2, H, D] -> [B, Tq, H, D]."""
+    D = q.shape[-1]
+    scale = D ** -0.5 if scale is None else scale
+    if _flash_ok(q, kv.shape[1], dropout_p):
+        return flash.attention_q_kvpacked(q, kv, key_mask, causal, scale)
+    k, v = kv[:, :, 0].transpose(1, 2), kv[:, :, 1].transpose(1, 2)
+    return materialized_attention(q.transpose(1, 2), k, v, key_mask, causal, scale, dropout_p).transpose(1, 2)
+
+
 def fused_attention(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, key_mask: torch.Tensor | None = None,
                     causal: bool = False, scale: float | None = None, dropout_p: float = 0.0) -> torch.Tensor:
-    """q: [B, H, Tq, D], k/v: [B, H, Tk, D], key_mask: [B, Tk] (nonzero = attend)."""
+    """q: [B, H, Tq, D], k/v: [B, H, Tk, D], key_mask: [B, Tk] (nonzero = attend) -> [B, H, Tq, D]."""
     if scale is None:
         scale = q.shape[-1] ** -0.5
-    if _flash_supported(q, k, v, key_mask, dropout_p):
-        from .flash import flash_attention
-
-        return flash_attention(q, k, v, key_mask, causal, scale)
+    if dropout_p == 0.0 and q.is_cuda and flash.supported(q.shape[-1], q.shape[2], k.shape[2], q.dtype):
+        return flash.flash_attention(q, k, v, key_mask, causal, scale)
     return materialized_attention(q, k, v, key_mask, causal, scale, dropout_p)
