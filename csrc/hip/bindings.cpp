@@ -32,6 +32,8 @@ PYBIND11_MODULE(_vodahip, m) {
   m.def("bn_apply", &bn_apply);
   m.def("bn_bwd", &bn_bwd);
 
+  m.def("colsum_workspace_floats", &colsum_workspace_floats);
+  m.def("colsum_accumulate", &colsum_accumulate);
   m.def("attention_supported", &attention_supported);
   m.def("attention_fwd", &attention_fwd);
   m.def("attention_bwd", &attention_bwd);

@@ -56,6 +56,11 @@ void bn_bwd(uintptr_t dy, uintptr_t y, uintptr_t x, uintptr_t save_mean, uintptr
             uintptr_t dx, uintptr_t dres, uintptr_t dgamma, uintptr_t dbeta, uintptr_t workspace, int64_t M, int C,
             bool relu, int dt, uintptr_t stream);
 
+// ---- Linear backward helpers (dense.hip) ----
+int64_t colsum_workspace_floats(int64_t M, int N);
+void colsum_accumulate(uintptr_t x, int64_t M, int N, int dt, uintptr_t out, int out_dt, bool accumulate,
+                       uintptr_t workspace, uintptr_t stream);
+
 // ---- fused MFMA attention (attention.hip) ----
 // t = 8 x (ptr, batch stride, head stride, row stride) for q, k, v, o, dout, out, dk, dv
 //     + lse ptr, delta ptr, key-mask ptr, key-mask batch stride

@@ -118,3 +118,30 @@ def test_optimizer_splits_param_groups_by_dtype():
     assert bf.master.dtype == torch.float32 and bf.lowp.dtype == torch.bfloat16 and bf.grad.dtype == torch.bfloat16
     n = sum(p.numel() for p in {id(p): p for p in m.parameters()}.values())
     assert sum(sum(s.numel for s in fg.slots) for fg in opt.flat_groups) == n
+
+
+def test_fused_linear_direct_accumulation_matches_autograd():
+    from vodascheduler_amd.ops.dense import FusedLinear
+    from vodascheduler_amd.ops.optim import FusedSGD
+
+    torch.manual_seed(0)
+    ref = torch.nn.Sequential(torch.nn.Linear(16, 32), torch.nn.GELU(), torch.nn.Linear(32, 8))
+    fused = torch.nn.Sequential(FusedLinear(16, 32), torch.nn.GELU(), FusedLinear(32, 8))
+    fused.load_state_dict(ref.state_dict())
+    opt = FusedSGD(fused.parameters(), lr=0.1)  # flat grads -> in-place accumulation path
+    ready = []
+    for p in fused.parameters():
+        p._voda_grad_ready = ready.append
+    x = torch.randn(5, 3, 16)
+    for _ in range(2):  # accumulates over two backward passes, like autograd
+        ref(x).square().sum().backward()
+        fused(x).square().sum().backward()
+    assert len(ready) == 8
+    for pr, pf in zip(ref.parameters(), fused.parameters()):
+        torch.testing.assert_close(pf.grad, pr.grad, atol=1e-5, rtol=1e-5)
+    opt.zero_grad()
+    assert all(float(p.grad.abs().sum()) == 0 for p in fused.parameters())
+    # without flat grads: ordinary autograd gradients
+    plain = FusedLinear(16, 8)
+    plain(x).sum().backward()
+    assert plain.weight.grad is not None and plain.bias.grad.shape == (8,)

@@ -154,3 +154,42 @@ def test_masked_softmax(B, H, Tq, S, dt, causal):
     tol = dict(rtol=2e-2, atol=1e-2) if dt == torch.bfloat16 else dict(rtol=1e-5, atol=1e-6)
     torch.testing.assert_close(y.float(), yr, **tol)
     torch.testing.assert_close(x.grad.float(), xr.grad, **tol)
+
+
+@pytest.mark.parametrize("M,Nc,dt,odt", [(8192, 768, torch.bfloat16, torch.bfloat16), (1000, 3072, torch.bfloat16,
+                                                                                       torch.float32),
+                                        (37, 2304, torch.float32, torch.float32), (5, 8, torch.float16, torch.float32),
+                                        (300, 4096, torch.bfloat16, torch.float32)])
+def test_colsum_accumulate(M, Nc, dt, odt):
+    from vodascheduler_amd.ops.dense import colsum_accumulate_
+
+    torch.manual_seed(0)
+    x = torch.randn(M, Nc, device="cuda").to(dt)
+    out = torch.randn(Nc, device="cuda").to(odt)
+    ref = out.float() + x.float().sum(0)
+    colsum_accumulate_(x, out)
+    tol = 2e-2 * max(1.0, M ** 0.5) if odt == torch.bfloat16 else 1e-3 * max(1.0, M ** 0.5)
+    torch.testing.assert_close(out.float(), ref, atol=tol, rtol=1e-2)
+
+
+def test_fused_linear_bf16_flat_grads_gpu():
+    from vodascheduler_amd.models import cast_compute_weights_
+    from vodascheduler_amd.ops.dense import FusedLinear
+    from vodascheduler_amd.ops.optim import FusedAdamW
+
+    torch.manual_seed(0)
+    ref = torch.nn.Linear(768, 3072).cuda()
+    m = FusedLinear(768, 3072).cuda()
+    m.load_state_dict(ref.state_dict())
+    cast_compute_weights_(m)
+    FusedAdamW(m.parameters(), lr=1e-3)
+    x = torch.randn(8, 128, 768, device="cuda")
+    with torch.autocast("cuda", dtype=torch.bfloat16):
+        y = m(x)
+        yr = ref(x)
+    g = torch.randn_like(yr.float())
+    y.float().backward(g)
+    yr.float().backward(g)
+    torch.testing.assert_close(y.float(), yr.float(), atol=5e-2, rtol=5e-2)
+    torch.testing.assert_close(m.weight.grad.float(), ref.weight.grad, atol=0.5, rtol=5e-2)
+    torch.testing.assert_close(m.bias.grad.float(), ref.bias.grad, atol=0.5, rtol=5e-2)

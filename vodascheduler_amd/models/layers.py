@@ -17,6 +17,7 @@ import torch.nn.functional as F
 from torch import nn
 
 from ..ops.attention import attention_q_kvpacked, attention_qkvpacked
+from ..ops.dense import FusedLinear
 from ..ops.layernorm import FusedLayerNorm
 
 
@@ -33,8 +34,8 @@ class MultiHeadAttention(nn.Module):
         # CUs and ran at ~190 TFLOP/s on MI355X (profiles/); the fused 2304-wide one is
         # 3x the tiles.  The fused weights are the concatenation of Keras/PyTorch's
         # separate q/k/v kernels.
-        self.qkv = nn.Linear(d_model, 3 * inner, bias=bias)
-        self.o = nn.Linear(inner, d_model, bias=bias)
+        self.qkv = FusedLinear(d_model, 3 * inner, bias=bias)
+        self.o = FusedLinear(inner, d_model, bias=bias)
         self.inner = inner
         self.dropout = dropout
 
@@ -60,8 +61,8 @@ class MultiHeadAttention(nn.Module):
 class FeedForward(nn.Module):
     def __init__(self, d_model: int, d_ff: int, act: str = "relu"):
         super().__init__()
-        self.fc1 = nn.Linear(d_model, d_ff)
-        self.fc2 = nn.Linear(d_ff, d_model)
+        self.fc1 = FusedLinear(d_model, d_ff)
+        self.fc2 = FusedLinear(d_ff, d_model)
         self.act = nn.GELU(approximate="tanh") if act == "gelu" else nn.ReLU()
 
     def forward(self, x):

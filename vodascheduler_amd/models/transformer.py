@@ -12,6 +12,7 @@ from __future__ import annotations
 import torch
 from torch import nn
 
+from ..ops.dense import FusedLinear
 from ..ops.layernorm import FusedLayerNorm
 from .layers import DecoderLayer, EncoderLayer
 
@@ -57,7 +58,7 @@ class BertBase(nn.Module):
         self.emb_ln = FusedLayerNorm(d_model, eps=1e-12)
         self.layers = nn.ModuleList([EncoderLayer(d_model, heads, d_ff, act="gelu", dropout=dropout, eps=1e-12)
                                      for _ in range(layers)])
-        self.mlm_dense = nn.Linear(d_model, d_model)
+        self.mlm_dense = FusedLinear(d_model, d_model)
         self.mlm_ln = FusedLayerNorm(d_model, eps=1e-12)
         self.mlm_out = nn.Linear(d_model, vocab)
         self.mlm_out.weight = self.emb.tok.weight  # tied embeddings, as in BERT

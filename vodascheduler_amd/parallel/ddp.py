@@ -74,6 +74,9 @@ class ElasticDDP:
             for p in g.params:
                 if p.requires_grad:
                     self._hooks.append(p.register_post_accumulate_grad_hook(self._on_grad))
+                    # layers that accumulate into the flat buffer themselves (ops/dense.py)
+                    # signal readiness through this attribute instead of autograd's hook
+                    p._voda_grad_ready = self._on_grad
         self._next = 0
         self.comm_stream = torch.cuda.Stream(self.device) if self.device.type == "cuda" else None
         if comm is not None and hasattr(comm, "stream") and self.comm_stream is not None:
@@ -210,6 +213,10 @@ class ElasticDDP:
         for h in self._hooks:
             h.remove()
         self._hooks = []
+        for g in self.groups:
+            for p in g.params:
+                if getattr(p, "_voda_grad_ready", None) == self._on_grad:
+                    p._voda_grad_ready = None
 
 
 @contextmanager

@@ -90,9 +90,11 @@ class FlatGroup:
         return torch.as_strided(flat, p.shape, p.stride(), s.offset)
 
     def attach_grads(self) -> None:
-        """(Re-)point every ``p.grad`` into the flat gradient buffer."""
+        """(Re-)point every ``p.grad`` into the flat gradient buffer.  ``_voda_flat_grad``
+        tells fused layers (ops/dense.py) they may accumulate into ``p.grad`` in place."""
         for p, s in zip(self.params, self.slots):
             p.grad = self.view(self.grad, p, s)
+            p._voda_flat_grad = True
 
     def zero_grad(self) -> None:
         self.grad.zero_()
