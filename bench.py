@@ -49,6 +49,10 @@ from vodascheduler_amd.sim.trace import bench_trace  # noqa: E402
 BASELINE_METRIC = "avg JCT + makespan, 32-job trace on 1/2/4/8 MI355X; elastic-resize latency"
 MODELS = ("resnet50", "bert-base")
 BATCH = {"resnet50": 256, "bert-base": 64}
+# --device cpu: rehearsal of the multi-rank orchestration on gloo with tiny models (tests);
+# never the headline number
+CPU_MODELS = ("mnist-torch", "mnist")
+CPU_BATCH = {"mnist-torch": 16, "mnist": 16}
 
 
 def log(rank, *a):
@@ -56,34 +60,48 @@ def log(rank, *a):
         print(f"[bench {time.strftime('%H:%M:%S')}]", *a, file=sys.stderr, flush=True)
 
 
-def warmup(device, steps: int):
-    """Untimed warm-up of every model in the mix on this GPU (single-GPU steps)."""
+def sync(device):
+    if device.type == "cuda":
+        torch.cuda.synchronize(device)
+
+
+def warmup(device, steps: int, models, batch):
+    """Untimed warm-up of every model in the mix on this device (single-GPU steps)."""
     out = {}
-    for name in MODELS:
+    for name in models:
         w = get_workload(name)
         torch.manual_seed(0)
         m = prepare_model(w, device)
         opt = make_optimizer(w.optimizer, m.parameters(), **w.opt_kwargs)
-        b = w.make_batch(BATCH[name], device, None)
-        if w.channels_last:
+        b = w.make_batch(batch[name], device, None)
+        if w.channels_last and device.type == "cuda":
             b = tuple(t.to(memory_format=torch.channels_last) if t.dim() == 4 else t for t in b)
         t0 = None
         for i in range(max(2, steps)):
             if i == 1:
-                torch.cuda.synchronize(device)
+                sync(device)
                 t0 = time.perf_counter()
             opt.zero_grad()
-            with torch.autocast("cuda", dtype=torch.bfloat16):
+            with torch.autocast(device.type, dtype=torch.bfloat16, enabled=device.type == "cuda"):
                 loss = w.loss(m, b)
             loss.backward()
             opt.step()
-        torch.cuda.synchronize(device)
+        sync(device)
         out[name] = (time.perf_counter() - t0) / (max(2, steps) - 1) * 1e3
         del m, opt, b
     return out
 
 
 def main():
+    if os.environ.get("VODA_STACKDUMP_S"):  # debugging aid: dump every thread's stack once
+        import faulthandler
+
+        faulthandler.dump_traceback_later(float(os.environ["VODA_STACKDUMP_S"]), exit=False)
+    if os.environ.get("VODA_LOG"):
+        import logging
+
+        logging.basicConfig(level=os.environ["VODA_LOG"].upper(),
+                            format=f"%(asctime)s [rank {os.environ.get('RANK', '0')}] %(name)s: %(message)s")
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=30)
@@ -96,16 +114,23 @@ def main():
     ap.add_argument("--compression", default=None, choices=[None, "bf16", "fp16"])
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--out", default=None, help="also write the JSON line (+details) to this file")
+    ap.add_argument("--device", default="cuda", choices=["cuda", "cpu"],
+                    help="cpu: rehearse the multi-rank orchestration on gloo with tiny models (tests only)")
     a = ap.parse_args()
+    models, batch = (MODELS, BATCH) if a.device == "cuda" else (CPU_MODELS, CPU_BATCH)
 
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != a.gpus:
         raise SystemExit(f"--gpus {a.gpus} but WORLD_SIZE={world}")
-    device = torch.device("cuda", local)
-    torch.cuda.set_device(device)
-    _native.hip()  # the HIP extension must be present on a GPU box
+    if a.device == "cuda":
+        device = torch.device("cuda", local)
+        torch.cuda.set_device(device)
+        _native.hip()  # the HIP extension must be present on a GPU box
+    else:
+        device = torch.device("cpu")
+        torch.set_num_threads(1)
 
     if world > 1:
         dist.init_process_group("gloo", init_method="env://", rank=rank, world_size=world)
@@ -116,18 +141,19 @@ def main():
     watch = connect_store("127.0.0.1", port[0])
 
     # ---------------- untimed warm-up ----------------
-    log(rank, f"warm-up: {a.warmup} steps x {MODELS} on {world} GPU(s)")
-    step_ms = warmup(device, a.warmup)
+    log(rank, f"warm-up: {a.warmup} steps x {models} on {world} {a.device} device(s)")
+    step_ms = warmup(device, a.warmup, models, batch)
     if world > 1:
-        comm = RcclCommunicator(store, "bench/warm", rank, world, device)
-        x = torch.ones(16 << 20, device=device)
-        comm.allreduce_(x, "sum")
-        torch.cuda.synchronize(device)
-        comm.destroy()
+        if a.device == "cuda":
+            comm = RcclCommunicator(store, "bench/warm", rank, world, device)
+            x = torch.ones(16 << 20, device=device)
+            comm.allreduce_(x, "sum")
+            torch.cuda.synchronize(device)
+            comm.destroy()
         dist.barrier()
     log(rank, f"warm-up single-GPU step ms: {step_ms}")
 
-    trace = bench_trace(a.jobs, a.steps, world, a.seed, a.interarrival, MODELS, BATCH)
+    trace = bench_trace(a.jobs, a.steps, world, a.seed, a.interarrival, models, batch)
     locs = [("node0", r) for r in range(world)]
     os.environ.setdefault("VODA_CKPT_DIR", f"/tmp/voda_ckpt_{os.getpid()}")
     metrics_dir = f"/tmp/voda_metrics_{port[0]}"
@@ -136,7 +162,7 @@ def main():
     # ---------------- timed region ----------------
     if world > 1:
         dist.barrier()
-    torch.cuda.synchronize(device)
+    sync(device)
     t0 = time.perf_counter()
     result: dict = {}
     sched = None
@@ -152,11 +178,12 @@ def main():
 
         sched = threading.Thread(target=drive, name="control-plane", daemon=True)
         sched.start()
-    worker = PoolWorker(store, watch, f"node0:{rank}", device, backend="rccl", timeout=900)
+    worker = PoolWorker(store, watch, f"node0:{rank}", device, backend="rccl" if a.device == "cuda" else "gloo",
+                        timeout=900)
     recs = worker.serve()
     if sched is not None:
         sched.join()
-    torch.cuda.synchronize(device)
+    sync(device)
     if world > 1:
         dist.barrier()
     t1 = time.perf_counter()
@@ -184,7 +211,7 @@ def main():
             from vodascheduler_amd.sim.trace import workload_of
 
             wl = workload_of(tj.spec)
-            samples += wl["steps_per_epoch"] * 2 * BATCH[wl["model"]]
+            samples += wl["steps_per_epoch"] * 2 * batch[wl["model"]]
         line = {
             "metric": BASELINE_METRIC,
             "value": round(result["avg_jct_s"], 3),
@@ -196,8 +223,9 @@ def main():
             "higher_is_better": False,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": "bf16",
-            "data": "synthetic (random-init weights, synthetic batches of the real shapes)",
+            "dtype": "bf16" if a.device == "cuda" else "fp32",
+            "data": "synthetic (random-init weights, synthetic batches of the real shapes)"
+                    + ("" if a.device == "cuda" else "; CPU/gloo orchestration rehearsal, not a benchmark"),
             "config": {
                 "model": "32-job Philly-style trace: ResNet-50 (ImageNet 224, bs256/GPU) + BERT-base (seq128, bs64/GPU)",
                 "global_batch": "per job: per-GPU batch x elastic workers",

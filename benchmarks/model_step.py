@@ -21,7 +21,7 @@ from vodascheduler_amd.ops import _native  # noqa: E402
 from vodascheduler_amd.ops.optim import make_optimizer  # noqa: E402
 
 
-def run(model: str, batch: int | None, steps: int, warmup: int) -> dict:
+def run(model: str, batch: int | None, steps: int, warmup: int, marker: bool = False) -> dict:
     dev = torch.device("cuda", 0)
     w = get_workload(model)
     bs = batch or w.per_gpu_batch
@@ -43,6 +43,9 @@ def run(model: str, batch: int | None, steps: int, warmup: int) -> dict:
     for _ in range(warmup):
         step()
     torch.cuda.synchronize(dev)
+    if marker:  # trace_window_stats.py keeps only kernels after this one
+        torch.cuda._sleep(1000)
+        torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
     for _ in range(steps):
         loss = step()
@@ -59,11 +62,12 @@ def main():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--cudnn-benchmark", action="store_true", help="MIOpen exhaustive find (benchmark mode)")
+    ap.add_argument("--profile-marker", action="store_true", help="launch a marker kernel before the timed steps")
     a = ap.parse_args()
     if a.cudnn_benchmark:
         torch.backends.cudnn.benchmark = True
     _native.hip()
-    print(json.dumps(run(a.model, a.batch, a.steps, a.warmup)), flush=True)
+    print(json.dumps(run(a.model, a.batch, a.steps, a.warmup, a.profile_marker)), flush=True)
 
 
 if __name__ == "__main__":

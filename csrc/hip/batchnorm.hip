@@ -9,11 +9,13 @@
 //   forward  (train): stats pass   read x                 -> per-block partial sums
 //                     finalize     per channel: mean, invstd, running stats, a=g*invstd, b=beta-mean*a
 //                     apply pass   read x (+ residual r), write y = relu(a*x + b (+ r))
-//   backward        : reduce pass  read dy, y (ReLU mask), x -> partial sums of g and g*x
+//   backward        : reduce pass  read dy, ReLU bit-mask, x -> partial sums of g and g*x
 //                     finalize     dgamma, dbeta, per-channel (a, c2, c0)
-//                     apply pass   read dy, y, x; write dx = a*g + c2*x + c0 (+ dr = g)
-//   with g = dy * (y > 0) when the forward applied ReLU (the mask comes from the saved
-//   output y, which the next convolution keeps alive anyway), and
+//                     apply pass   read dy, bit-mask, x; write dx = a*g + c2*x + c0 (+ dr = g)
+//   with g = dy * (y > 0) when the forward applied ReLU.  The forward apply pass writes the
+//   ReLU mask as ONE BIT per element ([M][C/8] bytes, bit k of byte (r, g) = channel 8g+k),
+//   so each backward pass reads 1/16 of the bytes it would read from the saved bf16 output
+//   (-25 % backward HBM traffic), and
 //   dx = a*(g - mean(g) - xhat*mean(g*xhat)) folded into per-channel constants.
 //
 // Layout / mapping: a thread owns ONE group of 8 consecutive channels (16 B of bf16) for
@@ -166,8 +168,14 @@ __global__ __launch_bounds__(kBlock) void bn_stats_kernel(const T* __restrict__ 
 }
 
 // ---------------------------------------------------------------- backward: reductions
+__device__ __forceinline__ void apply_mask(float (&g)[8], uint8_t mb) {
+#pragma unroll
+  for (int k = 0; k < 8; ++k) g[k] = ((mb >> k) & 1) ? g[k] : 0.f;
+}
+
 template <typename T, bool RELU>
-__global__ __launch_bounds__(kBlock) void bn_bwd_reduce_kernel(const T* __restrict__ dy, const T* __restrict__ y,
+__global__ __launch_bounds__(kBlock) void bn_bwd_reduce_kernel(const T* __restrict__ dy,
+                                                               const uint8_t* __restrict__ mask,
                                                                const T* __restrict__ x, float* __restrict__ part,
                                                                int64_t M, int C) {
   const Map m = make_map(C);
@@ -185,14 +193,9 @@ __global__ __launch_bounds__(kBlock) void bn_bwd_reduce_kernel(const T* __restri
       Vec8<T>::load(dy, (r + step) * C + col, g1);
       Vec8<T>::load(x, (r + step) * C + col, x1);
       if constexpr (RELU) {
-        float y0[8], y1[8];
-        Vec8<T>::load(y, r * C + col, y0);
-        Vec8<T>::load(y, (r + step) * C + col, y1);
-#pragma unroll
-        for (int k = 0; k < 8; ++k) {
-          g0[k] = y0[k] > 0.f ? g0[k] : 0.f;
-          g1[k] = y1[k] > 0.f ? g1[k] : 0.f;
-        }
+        const int CB = C / kVec;
+        apply_mask(g0, mask[r * CB + m.cg]);
+        apply_mask(g1, mask[(r + step) * CB + m.cg]);
       }
 #pragma unroll
       for (int k = 0; k < 8; ++k) {
@@ -204,12 +207,7 @@ __global__ __launch_bounds__(kBlock) void bn_bwd_reduce_kernel(const T* __restri
       float g[8], xv[8];
       Vec8<T>::load(dy, r * C + col, g);
       Vec8<T>::load(x, r * C + col, xv);
-      if constexpr (RELU) {
-        float yv[8];
-        Vec8<T>::load(y, r * C + col, yv);
-#pragma unroll
-        for (int k = 0; k < 8; ++k) g[k] = yv[k] > 0.f ? g[k] : 0.f;
-      }
+      if constexpr (RELU) apply_mask(g, mask[r * (C / kVec) + m.cg]);
 #pragma unroll
       for (int k = 0; k < 8; ++k) { s1[k] += g[k]; s2[k] += g[k] * xv[k]; }
     }
@@ -225,14 +223,27 @@ __device__ __forceinline__ void fin_reduce(const float* __restrict__ p1, const f
                                            int c, double& S1, double& S2) {
   __shared__ double red[2][kFinRg][kFinCh + 1];
   const int cl = threadIdx.x % kFinCh, rg = threadIdx.x / kFinCh;
-  double a = 0.0, b = 0.0;
-  if (c < C)
-    for (int r = rg; r < nb; r += kFinRg) {
-      a += double(p1[int64_t(r) * C + c]);
-      b += double(p2[int64_t(r) * C + c]);
+  // 4 independent loads per array in flight per thread (the finalize is pure L2 latency)
+  float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f, b0 = 0.f, b1 = 0.f, b2 = 0.f, b3 = 0.f;
+  if (c < C) {
+    int r = rg;
+    for (; r + 3 * kFinRg < nb; r += 4 * kFinRg) {
+      a0 += p1[int64_t(r) * C + c];
+      a1 += p1[int64_t(r + kFinRg) * C + c];
+      a2 += p1[int64_t(r + 2 * kFinRg) * C + c];
+      a3 += p1[int64_t(r + 3 * kFinRg) * C + c];
+      b0 += p2[int64_t(r) * C + c];
+      b1 += p2[int64_t(r + kFinRg) * C + c];
+      b2 += p2[int64_t(r + 2 * kFinRg) * C + c];
+      b3 += p2[int64_t(r + 3 * kFinRg) * C + c];
     }
-  red[0][rg][cl] = a;
-  red[1][rg][cl] = b;
+    for (; r < nb; r += kFinRg) {
+      a0 += p1[int64_t(r) * C + c];
+      b0 += p2[int64_t(r) * C + c];
+    }
+  }
+  red[0][rg][cl] = (double(a0) + double(a1)) + (double(a2) + double(a3));
+  red[1][rg][cl] = (double(b0) + double(b1)) + (double(b2) + double(b3));
   __syncthreads();
   S1 = 0.0;
   S2 = 0.0;
@@ -272,7 +283,7 @@ __global__ __launch_bounds__(kFinCh* kFinRg) void bn_fwd_finalize_kernel(
 __global__ __launch_bounds__(kFinCh* kFinRg) void bn_bwd_finalize_kernel(
     const float* __restrict__ part, int nb, int64_t M, int C, const float* __restrict__ gamma,
     const float* __restrict__ save_mean, const float* __restrict__ save_invstd, float* __restrict__ dgamma,
-    float* __restrict__ dbeta, float* __restrict__ k3) {
+    float* __restrict__ dbeta, float* __restrict__ k3, int accumulate) {
   const int c = blockIdx.x * kFinCh + threadIdx.x % kFinCh;
   double S1, S2;  // sum g, sum g*x
   fin_reduce(part, part + int64_t(nb) * C, nb, C, c, S1, S2);
@@ -280,8 +291,9 @@ __global__ __launch_bounds__(kFinCh* kFinRg) void bn_bwd_finalize_kernel(
     const double mean = save_mean[c], invstd = save_invstd[c];
     const double db = S1;
     const double dg = invstd * (S2 - mean * S1);
-    if (dgamma != nullptr) dgamma[c] = float(dg);
-    if (dbeta != nullptr) dbeta[c] = float(db);
+    // accumulate: add straight into the optimizer's flat fp32 gradient buffer
+    if (dgamma != nullptr) dgamma[c] = accumulate ? dgamma[c] + float(dg) : float(dg);
+    if (dbeta != nullptr) dbeta[c] = accumulate ? dbeta[c] + float(db) : float(db);
     const double g = gamma != nullptr ? gamma[c] : 1.0;
     const double a = g * invstd;
     const double c2 = -a * invstd * dg / double(M);
@@ -293,10 +305,17 @@ __global__ __launch_bounds__(kFinCh* kFinRg) void bn_bwd_finalize_kernel(
 }
 
 // ---------------------------------------------------------------- elementwise passes
+__device__ __forceinline__ uint8_t pos_bits(const float (&v)[8]) {
+  uint32_t b = 0;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) b |= (v[k] > 0.f ? 1u : 0u) << k;
+  return uint8_t(b);
+}
+
 template <typename T, bool RES, bool RELU>
 __global__ __launch_bounds__(kBlock) void bn_apply_kernel(const T* __restrict__ x, const T* __restrict__ res,
                                                           const float* __restrict__ ab, T* __restrict__ y,
-                                                          int64_t M, int C) {
+                                                          uint8_t* __restrict__ mask, int64_t M, int C) {
   const Map m = make_map(C);
   if (!m.active) return;
   int64_t r0, r1;
@@ -324,6 +343,12 @@ __global__ __launch_bounds__(kBlock) void bn_apply_kernel(const T* __restrict__ 
     }
     Vec8<T>::store(y, r * C + col, v0);
     Vec8<T>::store(y, (r + step) * C + col, v1);
+    if constexpr (RELU) {
+      if (mask != nullptr) {
+        mask[r * (C / kVec) + m.cg] = pos_bits(v0);
+        mask[(r + step) * (C / kVec) + m.cg] = pos_bits(v1);
+      }
+    }
   }
   for (; r < r1; r += step) {
     float v[8], q[8];
@@ -336,11 +361,15 @@ __global__ __launch_bounds__(kBlock) void bn_apply_kernel(const T* __restrict__ 
       if constexpr (RELU) v[k] = fmaxf(v[k], 0.f);
     }
     Vec8<T>::store(y, r * C + col, v);
+    if constexpr (RELU) {
+      if (mask != nullptr) mask[r * (C / kVec) + m.cg] = pos_bits(v);
+    }
   }
 }
 
 template <typename T, bool RELU, bool DRES>
-__global__ __launch_bounds__(kBlock) void bn_bwd_apply_kernel(const T* __restrict__ dy, const T* __restrict__ y,
+__global__ __launch_bounds__(kBlock) void bn_bwd_apply_kernel(const T* __restrict__ dy,
+                                                              const uint8_t* __restrict__ mask,
                                                               const T* __restrict__ x, const float* __restrict__ k3,
                                                               T* __restrict__ dx, T* __restrict__ dres, int64_t M,
                                                               int C) {
@@ -357,12 +386,7 @@ __global__ __launch_bounds__(kBlock) void bn_bwd_apply_kernel(const T* __restric
     float g[8], xv[8];
     Vec8<T>::load(dy, r * C + col, g);
     Vec8<T>::load(x, r * C + col, xv);
-    if constexpr (RELU) {
-      float yv[8];
-      Vec8<T>::load(y, r * C + col, yv);
-#pragma unroll
-      for (int k = 0; k < 8; ++k) g[k] = yv[k] > 0.f ? g[k] : 0.f;
-    }
+    if constexpr (RELU) apply_mask(g, mask[r * (C / kVec) + m.cg]);
     if constexpr (DRES) Vec8<T>::store(dres, r * C + col, g);
     float o[8];
 #pragma unroll
@@ -410,8 +434,9 @@ int64_t bn_workspace_floats(int64_t M, int C) {
 }
 
 void bn_fwd_train(uintptr_t x, uintptr_t residual, uintptr_t gamma, uintptr_t beta, uintptr_t running_mean,
-                  uintptr_t running_var, uintptr_t save_mean, uintptr_t save_invstd, uintptr_t y, uintptr_t workspace,
-                  int64_t M, int C, float eps, float momentum, bool relu, int dt, uintptr_t stream) {
+                  uintptr_t running_var, uintptr_t save_mean, uintptr_t save_invstd, uintptr_t y, uintptr_t mask,
+                  uintptr_t workspace, int64_t M, int C, float eps, float momentum, bool relu, int dt,
+                  uintptr_t stream) {
   VODA_CHECK(C % kVec == 0, "batchnorm: C must be a multiple of 8");
   VODA_CHECK(M > 0, "batchnorm: empty input");
   hipStream_t s = as_stream(stream);
@@ -429,12 +454,13 @@ void bn_fwd_train(uintptr_t x, uintptr_t residual, uintptr_t gamma, uintptr_t be
                        reinterpret_cast<float*>(save_mean), reinterpret_cast<float*>(save_invstd), ab, eps, momentum);
     const T* rp = reinterpret_cast<const T*>(residual);
     T* yp = reinterpret_cast<T*>(y);
+    uint8_t* mp = reinterpret_cast<uint8_t*>(mask);
     if (residual) {
-      if (relu) hipLaunchKernelGGL((bn_apply_kernel<T, true, true>), ag.grid, dim3(kBlock), 0, s, xp, rp, ab, yp, M, C);
-      else hipLaunchKernelGGL((bn_apply_kernel<T, true, false>), ag.grid, dim3(kBlock), 0, s, xp, rp, ab, yp, M, C);
+      if (relu) hipLaunchKernelGGL((bn_apply_kernel<T, true, true>), ag.grid, dim3(kBlock), 0, s, xp, rp, ab, yp, mp, M, C);
+      else hipLaunchKernelGGL((bn_apply_kernel<T, true, false>), ag.grid, dim3(kBlock), 0, s, xp, rp, ab, yp, mp, M, C);
     } else {
-      if (relu) hipLaunchKernelGGL((bn_apply_kernel<T, false, true>), ag.grid, dim3(kBlock), 0, s, xp, rp, ab, yp, M, C);
-      else hipLaunchKernelGGL((bn_apply_kernel<T, false, false>), ag.grid, dim3(kBlock), 0, s, xp, rp, ab, yp, M, C);
+      if (relu) hipLaunchKernelGGL((bn_apply_kernel<T, false, true>), ag.grid, dim3(kBlock), 0, s, xp, rp, ab, yp, mp, M, C);
+      else hipLaunchKernelGGL((bn_apply_kernel<T, false, false>), ag.grid, dim3(kBlock), 0, s, xp, rp, ab, yp, mp, M, C);
     }
   });
   check_launch();
@@ -451,22 +477,23 @@ void bn_apply(uintptr_t x, uintptr_t residual, uintptr_t ab, uintptr_t y, int64_
     const T* xp = reinterpret_cast<const T*>(x);
     const T* rp = reinterpret_cast<const T*>(residual);
     T* yp = reinterpret_cast<T*>(y);
+    uint8_t* np = nullptr;
     if (residual) {
-      if (relu) hipLaunchKernelGGL((bn_apply_kernel<T, true, true>), ag.grid, dim3(kBlock), 0, s, xp, rp, abp, yp, M, C);
-      else hipLaunchKernelGGL((bn_apply_kernel<T, true, false>), ag.grid, dim3(kBlock), 0, s, xp, rp, abp, yp, M, C);
+      if (relu) hipLaunchKernelGGL((bn_apply_kernel<T, true, true>), ag.grid, dim3(kBlock), 0, s, xp, rp, abp, yp, np, M, C);
+      else hipLaunchKernelGGL((bn_apply_kernel<T, true, false>), ag.grid, dim3(kBlock), 0, s, xp, rp, abp, yp, np, M, C);
     } else {
-      if (relu) hipLaunchKernelGGL((bn_apply_kernel<T, false, true>), ag.grid, dim3(kBlock), 0, s, xp, rp, abp, yp, M, C);
-      else hipLaunchKernelGGL((bn_apply_kernel<T, false, false>), ag.grid, dim3(kBlock), 0, s, xp, rp, abp, yp, M, C);
+      if (relu) hipLaunchKernelGGL((bn_apply_kernel<T, false, true>), ag.grid, dim3(kBlock), 0, s, xp, rp, abp, yp, np, M, C);
+      else hipLaunchKernelGGL((bn_apply_kernel<T, false, false>), ag.grid, dim3(kBlock), 0, s, xp, rp, abp, yp, np, M, C);
     }
   });
   check_launch();
 }
 
-void bn_bwd(uintptr_t dy, uintptr_t y, uintptr_t x, uintptr_t save_mean, uintptr_t save_invstd, uintptr_t gamma,
+void bn_bwd(uintptr_t dy, uintptr_t mask, uintptr_t x, uintptr_t save_mean, uintptr_t save_invstd, uintptr_t gamma,
             uintptr_t dx, uintptr_t dres, uintptr_t dgamma, uintptr_t dbeta, uintptr_t workspace, int64_t M, int C,
-            bool relu, int dt, uintptr_t stream) {
+            bool relu, bool accumulate, int dt, uintptr_t stream) {
   VODA_CHECK(C % kVec == 0, "batchnorm: C must be a multiple of 8");
-  VODA_CHECK(!relu || y != 0, "batchnorm backward: ReLU mask needs the forward output");
+  VODA_CHECK(!relu || mask != 0, "batchnorm backward: ReLU needs the forward's bit-mask");
   hipStream_t s = as_stream(stream);
   float* ws = reinterpret_cast<float*>(workspace);
   const Grid rg = reduce_grid(M, C);
@@ -475,14 +502,14 @@ void bn_bwd(uintptr_t dy, uintptr_t y, uintptr_t x, uintptr_t save_mean, uintptr
   dispatch_dt(dt, [&](auto tag) {
     using T = decltype(tag);
     const T* dyp = reinterpret_cast<const T*>(dy);
-    const T* yp = reinterpret_cast<const T*>(y);
+    const uint8_t* yp = reinterpret_cast<const uint8_t*>(mask);
     const T* xp = reinterpret_cast<const T*>(x);
     if (relu) hipLaunchKernelGGL((bn_bwd_reduce_kernel<T, true>), rg.grid, dim3(kBlock), 0, s, dyp, yp, xp, ws, M, C);
     else hipLaunchKernelGGL((bn_bwd_reduce_kernel<T, false>), rg.grid, dim3(kBlock), 0, s, dyp, yp, xp, ws, M, C);
     hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + kFinCh - 1) / kFinCh), dim3(kFinCh * kFinRg), 0, s, ws,
                        rg.nb, M, C, reinterpret_cast<const float*>(gamma), reinterpret_cast<const float*>(save_mean),
                        reinterpret_cast<const float*>(save_invstd), reinterpret_cast<float*>(dgamma),
-                       reinterpret_cast<float*>(dbeta), k3);
+                       reinterpret_cast<float*>(dbeta), k3, int(accumulate));
     T* dxp = reinterpret_cast<T*>(dx);
     T* drp = reinterpret_cast<T*>(dres);
     if (relu) {

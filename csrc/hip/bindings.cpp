@@ -32,6 +32,8 @@ PYBIND11_MODULE(_vodahip, m) {
   m.def("bn_apply", &bn_apply);
   m.def("bn_bwd", &bn_bwd);
 
+  m.def("maxpool2d_fwd", &maxpool2d_fwd);
+  m.def("maxpool2d_bwd", &maxpool2d_bwd);
   m.def("colsum_workspace_floats", &colsum_workspace_floats);
   m.def("colsum_accumulate", &colsum_accumulate);
   m.def("attention_supported", &attention_supported);
@@ -42,13 +44,14 @@ PYBIND11_MODULE(_vodahip, m) {
   m.def("rccl_version", &rccl_version);
 
   py::class_<RcclComm>(m, "RcclComm")
-      .def(py::init([](py::bytes uid, int nranks, int rank, int device, double timeout_s) {
+      .def(py::init([](py::bytes uid, int nranks, int rank, int device, double timeout_s, bool wait) {
              std::string id = uid;
              py::gil_scoped_release nogil;
-             return new RcclComm(id, nranks, rank, device, timeout_s);
+             return new RcclComm(id, nranks, rank, device, timeout_s, wait);
            }),
            py::arg("uid"), py::arg("nranks"), py::arg("rank"), py::arg("device") = -1,
-           py::arg("timeout_s") = 300.0)
+           py::arg("timeout_s") = 300.0, py::arg("wait") = true)
+      .def("poll_ready", &RcclComm::poll_ready, py::call_guard<py::gil_scoped_release>())
       .def("allreduce", &RcclComm::allreduce, py::call_guard<py::gil_scoped_release>())
       .def("broadcast", &RcclComm::broadcast, py::call_guard<py::gil_scoped_release>())
       .def("allgather", &RcclComm::allgather, py::call_guard<py::gil_scoped_release>())

@@ -63,7 +63,7 @@ int rccl_version() {
   return v;
 }
 
-RcclComm::RcclComm(const std::string& uid, int nranks, int rank, int device, double timeout_s)
+RcclComm::RcclComm(const std::string& uid, int nranks, int rank, int device, double timeout_s, bool wait)
     : nranks_(nranks), rank_(rank), timeout_s_(timeout_s) {
   VODA_CHECK(uid.size() == sizeof(ncclUniqueId), "unique id must be 128 bytes");
   VODA_CHECK(nranks >= 1 && rank >= 0 && rank < nranks, "bad rank/nranks");
@@ -74,7 +74,19 @@ RcclComm::RcclComm(const std::string& uid, int nranks, int rank, int device, dou
   cfg.blocking = 0;
   ncclResult_t r = ncclCommInitRankConfig(&comm_, nranks, id, rank, &cfg);
   if (r != ncclSuccess && r != ncclInProgress) nccl_throw(r, "ncclCommInitRankConfig");
-  wait_ready("init");
+  if (wait) wait_ready("init");
+}
+
+bool RcclComm::poll_ready() {
+  check_live();
+  ncclResult_t st = ncclSuccess;
+  ncclResult_t r = ncclCommGetAsyncError(comm_, &st);
+  if (r != ncclSuccess) nccl_throw(r, "ncclCommGetAsyncError");
+  if (st == ncclSuccess) return true;
+  if (st == ncclInProgress) return false;
+  aborted_ = true;
+  nccl_throw(st, "init");
+  return false;
 }
 
 RcclComm::~RcclComm() {

@@ -48,13 +48,20 @@ void masked_softmax_bwd(uintptr_t y, uintptr_t dy, uintptr_t dx, int64_t rows, i
 // ---- fused BatchNorm(+add)(+ReLU), channels_last [M][C] (batchnorm.hip) ----
 int64_t bn_workspace_floats(int64_t M, int C);
 void bn_fwd_train(uintptr_t x, uintptr_t residual, uintptr_t gamma, uintptr_t beta, uintptr_t running_mean,
-                  uintptr_t running_var, uintptr_t save_mean, uintptr_t save_invstd, uintptr_t y, uintptr_t workspace,
-                  int64_t M, int C, float eps, float momentum, bool relu, int dt, uintptr_t stream);
+                  uintptr_t running_var, uintptr_t save_mean, uintptr_t save_invstd, uintptr_t y, uintptr_t mask,
+                  uintptr_t workspace, int64_t M, int C, float eps, float momentum, bool relu, int dt,
+                  uintptr_t stream);
 void bn_apply(uintptr_t x, uintptr_t residual, uintptr_t ab, uintptr_t y, int64_t M, int C, bool relu, int dt,
               uintptr_t stream);
-void bn_bwd(uintptr_t dy, uintptr_t y, uintptr_t x, uintptr_t save_mean, uintptr_t save_invstd, uintptr_t gamma,
+void bn_bwd(uintptr_t dy, uintptr_t mask, uintptr_t x, uintptr_t save_mean, uintptr_t save_invstd, uintptr_t gamma,
             uintptr_t dx, uintptr_t dres, uintptr_t dgamma, uintptr_t dbeta, uintptr_t workspace, int64_t M, int C,
-            bool relu, int dt, uintptr_t stream);
+            bool relu, bool accumulate, int dt, uintptr_t stream);
+
+// ---- NHWC max pooling with argmax bytes + gather backward (pool.hip) ----
+void maxpool2d_fwd(uintptr_t x, uintptr_t y, uintptr_t idx, int N, int H, int W, int C, int Ho, int Wo, int k, int s,
+                   int p, int dt, uintptr_t stream);
+void maxpool2d_bwd(uintptr_t dy, uintptr_t idx, uintptr_t dx, int N, int H, int W, int C, int Ho, int Wo, int k, int s,
+                   int p, int dt, uintptr_t stream);
 
 // ---- Linear backward helpers (dense.hip) ----
 int64_t colsum_workspace_floats(int64_t M, int N);
@@ -76,7 +83,10 @@ int rccl_version();
 
 class RcclComm {
  public:
-  RcclComm(const std::string& uid, int nranks, int rank, int device, double timeout_s);
+  // wait=false: return right after ncclCommInitRankConfig; poll_ready() until true (lets the
+  // caller abandon an init whose membership epoch was superseded)
+  RcclComm(const std::string& uid, int nranks, int rank, int device, double timeout_s, bool wait = true);
+  bool poll_ready();
   ~RcclComm();
   RcclComm(const RcclComm&) = delete;
   RcclComm& operator=(const RcclComm&) = delete;

@@ -62,7 +62,7 @@ def test_fused_bn_module_eval_and_autocast():
         ref(x)
     torch.testing.assert_close(m.running_mean, ref.running_mean, atol=1e-5, rtol=1e-5)
     torch.testing.assert_close(m.running_var, ref.running_var, atol=1e-4, rtol=1e-4)
-    assert int(m.num_batches_tracked) == 3
+    assert int(m.state_dict()['num_batches_tracked']) == 3
     m.eval()
     ref.eval()
     torch.testing.assert_close(m(x), F.relu(ref(x)), atol=1e-5, rtol=1e-5)
@@ -84,3 +84,42 @@ def test_resnet50_step_uses_fused_bn_kernels():
     out.float().sum().backward()
     assert torch.isfinite(out.float()).all()
     assert all(p.grad is not None and torch.isfinite(p.grad).all() for p in m.parameters())
+
+
+@pytest.mark.parametrize("shape,k,s,p", [((8, 64, 112, 112), 3, 2, 1), ((4, 96, 17, 17), 3, 2, 0), ((2, 64, 32, 32), 2, 2, 0),
+                                         ((3, 8, 9, 7), 3, 1, 1)])
+@pytest.mark.parametrize("dt", [torch.bfloat16, torch.float32])
+def test_maxpool_nhwc_fwd_bwd(shape, k, s, p, dt):
+    from vodascheduler_amd.ops.pool import max_pool2d
+
+    torch.manual_seed(0)
+    x = torch.randn(shape, device="cuda").to(dt).to(memory_format=torch.channels_last).requires_grad_()
+    xr = x.detach().float().requires_grad_()
+    y = max_pool2d(x, k, s, p)
+    yr = F.max_pool2d(xr, k, s, p)
+    torch.testing.assert_close(y.float(), yr, atol=0, rtol=0)
+    dy = torch.randn_like(yr)
+    y.backward(dy.to(dt))
+    yr.backward(dy.to(dt).float())
+    torch.testing.assert_close(x.grad.float(), xr.grad, atol=1e-2 if dt == torch.bfloat16 else 1e-5, rtol=1e-2)
+
+
+def test_bn_param_grads_accumulate_into_flat_buffer():
+    from vodascheduler_amd.ops.optim import FusedSGD
+
+    torch.manual_seed(0)
+    a = FusedBatchNorm2d(64, relu=True).cuda()
+    b = FusedBatchNorm2d(64, relu=True).cuda()
+    b.load_state_dict(a.state_dict())
+    FusedSGD(b.parameters(), lr=0.1)  # b's grads live in a flat buffer -> direct accumulation
+    ready = []
+    b.weight._voda_grad_ready = ready.append
+    b.bias._voda_grad_ready = ready.append
+    x = torch.randn(8, 64, 14, 14, device="cuda").to(torch.bfloat16).to(memory_format=torch.channels_last)
+    for _ in range(2):
+        for m in (a, b):
+            xi = x.clone().requires_grad_()
+            m(xi).float().square().sum().backward()
+    assert len(ready) == 4
+    torch.testing.assert_close(b.weight.grad, a.weight.grad, atol=1e-3, rtol=1e-3)
+    torch.testing.assert_close(b.bias.grad, a.bias.grad, atol=1e-3, rtol=1e-3)

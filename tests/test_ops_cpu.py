@@ -145,3 +145,16 @@ def test_fused_linear_direct_accumulation_matches_autograd():
     plain = FusedLinear(16, 8)
     plain(x).sum().backward()
     assert plain.weight.grad is not None and plain.bias.grad.shape == (8,)
+
+
+def test_fused_bn_batches_tracked_and_state_dict():
+    from vodascheduler_amd.ops.batchnorm import FusedBatchNorm2d
+
+    m = FusedBatchNorm2d(8)
+    for _ in range(3):
+        m(torch.randn(2, 8, 3, 3))
+    assert int(m.state_dict()["num_batches_tracked"]) == 3
+    m2 = FusedBatchNorm2d(8)
+    m2.load_state_dict(m.state_dict())
+    m2(torch.randn(2, 8, 3, 3))
+    assert int(m2.state_dict()["num_batches_tracked"]) == 4

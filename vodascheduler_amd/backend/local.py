@@ -63,14 +63,16 @@ class LocalBackend(PoolBackend):
             self.healthy.discard(wid)
         with self._pub_lock:
             with self._lock:
-                affected = {j: list(m) for j, m in self.members.items() if wid in m}
+                affected = {j: list(m) for j, (_, m) in self.live.items() if wid in m}
             for job, mem in affected.items():
                 survivors = [m for m in mem if m != wid]
                 rdzv = JobRendezvous(self.store, job)
+                self.pending.pop(job, None)  # the scheduler re-places the job after EV_NODES
                 e = rdzv.publish(survivors, abort=True)
                 if not survivors:
                     rdzv.set_live_epoch(-1)  # nobody holds the state: resume from the last checkpoint
                 with self._lock:
+                    self.live[job] = (e, survivors)
                     self.members[job] = survivors
                 self.failures.append({"job": job, "worker": wid, "epoch": e, "survivors": len(survivors)})
                 log.warning("worker %s died: job %s continues on %d worker(s) (abort epoch %d)", wid, job,

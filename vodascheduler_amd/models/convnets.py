@@ -17,13 +17,14 @@ import torch.nn.functional as F
 from torch import nn
 
 from ..ops.batchnorm import FusedBatchNorm2d
+from ..ops.pool import FusedMaxPool2d, max_pool2d
 
 
 def _vgg_block(cin, cout, n):
     layers = []
     for i in range(n):
         layers += [nn.Conv2d(cin if i == 0 else cout, cout, 3, padding=1), nn.ReLU(inplace=True)]
-    layers.append(nn.MaxPool2d(2))
+    layers.append(FusedMaxPool2d(2))
     return layers
 
 
@@ -105,7 +106,7 @@ class InceptionB(nn.Module):
                                 BasicConv(96, 96, kernel_size=3, stride=2))
 
     def forward(self, x):
-        return torch.cat([self.b3(x), self.bd(x), F.max_pool2d(x, 3, 2)], 1)
+        return torch.cat([self.b3(x), self.bd(x), max_pool2d(x, 3, 2)], 1)
 
 
 class InceptionC(nn.Module):
@@ -130,7 +131,7 @@ class InceptionV3(nn.Module):
     def __init__(self, num_classes=10):
         super().__init__()
         self.stem = nn.Sequential(BasicConv(3, 32, kernel_size=3, stride=2), BasicConv(32, 32, kernel_size=3),
-                                  BasicConv(32, 64, kernel_size=3, padding=1), nn.MaxPool2d(3, 2),
+                                  BasicConv(32, 64, kernel_size=3, padding=1), FusedMaxPool2d(3, 2),
                                   BasicConv(64, 80, kernel_size=1), BasicConv(80, 192, kernel_size=3))
         self.a = nn.Sequential(InceptionA(192, 32), InceptionA(256, 64), InceptionA(288, 64))
         self.b = InceptionB(288)

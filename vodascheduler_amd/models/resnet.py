@@ -14,6 +14,7 @@ import torch
 from torch import nn
 
 from ..ops.batchnorm import FusedBatchNorm2d
+from ..ops.pool import FusedMaxPool2d
 
 
 class Bottleneck(nn.Module):
@@ -61,7 +62,7 @@ class ResNet(nn.Module):
             self.stem = nn.Sequential(nn.Conv2d(3, 64, 3, padding=1, bias=False), FusedBatchNorm2d(64, relu=True))
         else:
             self.stem = nn.Sequential(nn.Conv2d(3, 64, 7, stride=2, padding=3, bias=False),
-                                      FusedBatchNorm2d(64, relu=True), nn.MaxPool2d(3, stride=2, padding=1))
+                                      FusedBatchNorm2d(64, relu=True), FusedMaxPool2d(3, stride=2, padding=1))
         self.layer1 = self._make(block, 64, layers[0])
         self.layer2 = self._make(block, 128, layers[1], stride=2)
         self.layer3 = self._make(block, 256, layers[2], stride=2)

@@ -5,8 +5,9 @@
 residual=None, relu=True)`` computes ``relu(bn(x) + residual)`` (either extra optional) in
 one statistics pass + one apply pass forward and one reduction pass + one apply pass
 backward, instead of MIOpen BN + separate ReLU / add / ReLU-backward kernels.  The ReLU
-mask of the backward comes from the saved output.  Statistics, running-stat updates and
-the affine parameters stay fp32; activations are bf16/fp16/fp32.
+mask of the backward is a 1-bit-per-element map written by the forward apply pass.
+Statistics, running-stat updates and the affine parameters stay fp32; activations are
+bf16/fp16/fp32.
 
 GPU requirements: 4-D input in channels_last memory format (or a contiguous [M, C]
 matrix) with C % 8 == 0; anything else, and CPU tensors, use the PyTorch reference
@@ -18,6 +19,7 @@ import torch
 import torch.nn.functional as F
 
 from . import _native as N
+from .dense import _ready
 
 
 def _rows_view_ok(x: torch.Tensor) -> bool:
@@ -38,6 +40,11 @@ def _supported(x, residual) -> bool:
     return True
 
 
+def _direct_fp32(p) -> bool:
+    return (p is not None and getattr(p, "_voda_flat_grad", False) and p.grad is not None
+            and p.grad.dtype == torch.float32 and p.grad.is_contiguous())
+
+
 class _BNActFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, residual, weight, bias, running_mean, running_var, momentum, eps, relu):
@@ -48,18 +55,20 @@ class _BNActFn(torch.autograd.Function):
         save_mean = torch.empty(C, dtype=torch.float32, device=x.device)
         save_invstd = torch.empty(C, dtype=torch.float32, device=x.device)
         ws = torch.empty(h.bn_workspace_floats(M, C), dtype=torch.float32, device=x.device)
+        mask = torch.empty(M * (C // 8), dtype=torch.uint8, device=x.device) if relu else None
         h.bn_fwd_train(x.data_ptr(), N.ptr(residual), N.ptr(weight), N.ptr(bias), N.ptr(running_mean),
-                       N.ptr(running_var), save_mean.data_ptr(), save_invstd.data_ptr(), y.data_ptr(),
+                       N.ptr(running_var), save_mean.data_ptr(), save_invstd.data_ptr(), y.data_ptr(), N.ptr(mask),
                        ws.data_ptr(), M, C, float(eps), float(momentum), bool(relu), N.dtype_code(x.dtype),
                        N.stream_of(x))
         ctx.relu = bool(relu)
         ctx.has_res = residual is not None
-        ctx.save_for_backward(x, y if relu else None, weight, save_mean, save_invstd)
+        ctx.bias = bias
+        ctx.save_for_backward(x, mask, weight, save_mean, save_invstd)
         return y
 
     @staticmethod
     def backward(ctx, dy):
-        x, y, weight, save_mean, save_invstd = ctx.saved_tensors
+        x, mask, weight, save_mean, save_invstd = ctx.saved_tensors
         C = x.shape[1]
         M = x.numel() // C
         h = N.hip()
@@ -69,14 +78,25 @@ class _BNActFn(torch.autograd.Function):
         dres = torch.empty_like(x) if ctx.has_res and ctx.needs_input_grad[1] else None
         need_w = weight is not None and ctx.needs_input_grad[2]
         need_b = ctx.needs_input_grad[3]
-        dw = torch.empty(C, dtype=torch.float32, device=x.device) if need_w else None
-        db = torch.empty(C, dtype=torch.float32, device=x.device) if need_b else None
+        bias = ctx.bias
+        # fp32 gamma/beta grads go straight into the optimizer's flat grad buffer when it
+        # owns them (same contract as ops/dense.py), else into fresh tensors
+        direct = (need_w and need_b and _direct_fp32(weight) and _direct_fp32(bias))
+        if direct:
+            dw, db = weight.grad, bias.grad
+        else:
+            dw = torch.empty(C, dtype=torch.float32, device=x.device) if need_w else None
+            db = torch.empty(C, dtype=torch.float32, device=x.device) if need_b else None
         ws = torch.empty(h.bn_workspace_floats(M, C), dtype=torch.float32, device=x.device)
-        h.bn_bwd(dy.data_ptr(), N.ptr(y), x.data_ptr(), save_mean.data_ptr(), save_invstd.data_ptr(), N.ptr(weight),
-                 dx.data_ptr(), N.ptr(dres), N.ptr(dw), N.ptr(db), ws.data_ptr(), M, C, ctx.relu,
+        h.bn_bwd(dy.data_ptr(), N.ptr(mask), x.data_ptr(), save_mean.data_ptr(), save_invstd.data_ptr(), N.ptr(weight),
+                 dx.data_ptr(), N.ptr(dres), N.ptr(dw), N.ptr(db), ws.data_ptr(), M, C, ctx.relu, direct,
                  N.dtype_code(x.dtype), N.stream_of(x))
         if dres is None and ctx.has_res and ctx.needs_input_grad[1]:
             dres = dy
+        if direct:
+            _ready(weight)
+            _ready(bias)
+            return dx, dres, None, None, None, None, None, None, None
         return dx, dres, dw, db, None, None, None, None, None
 
 
@@ -116,9 +136,27 @@ class FusedBatchNorm2d(torch.nn.BatchNorm2d):
         super().__init__(num_features, eps=eps, momentum=momentum, **kw)
         self.relu = relu
 
+    def _load_from_state_dict(self, state_dict, prefix, *args, **kwargs):
+        self._pending_batches = 0
+        super()._load_from_state_dict(state_dict, prefix, *args, **kwargs)
+
+    def _save_to_state_dict(self, destination, prefix, keep_vars):
+        self.sync_batches_tracked()
+        super()._save_to_state_dict(destination, prefix, keep_vars)
+
+    def sync_batches_tracked(self) -> None:
+        """Fold the host-side step count into the ``num_batches_tracked`` buffer."""
+        n = getattr(self, "_pending_batches", 0)
+        if n and self.num_batches_tracked is not None:
+            self.num_batches_tracked.add_(n)
+            self._pending_batches = 0
+
     def forward(self, x, residual=None):
         if self.training and self.track_running_stats:
-            self.num_batches_tracked.add_(1)
+            if self.momentum is None:  # cumulative average needs the device count now
+                self.num_batches_tracked.add_(1)
+            else:  # only informational: count on the host (saves a kernel per BN per step)
+                self._pending_batches = getattr(self, "_pending_batches", 0) + 1
         use_batch = self.training or not self.track_running_stats
         momentum = self.momentum if self.momentum is not None else 0.1
         if x.is_cuda and torch.is_autocast_enabled("cuda"):

@@ -31,8 +31,9 @@ class CommError(RuntimeError):
     """A collective failed or was aborted (peer died / membership changed)."""
 
 
-def store_get(store: dist.Store, key: str, timeout: float) -> bytes:
-    """Blocking get with an explicit timeout (c10d get blocks up to the store timeout)."""
+def store_get(store: dist.Store, key: str, timeout: float, cancel=None) -> bytes:
+    """Blocking get with an explicit timeout (c10d get blocks up to the store timeout);
+    ``cancel()`` returning True abandons the wait (membership epoch superseded)."""
     deadline = time.monotonic() + timeout
     while True:
         try:
@@ -40,9 +41,25 @@ def store_get(store: dist.Store, key: str, timeout: float) -> bytes:
                 return store.get(key)
         except RuntimeError:
             pass
+        if cancel is not None and cancel():
+            raise CommError(f"superseded while waiting for {key!r}")
         if time.monotonic() > deadline:
             raise TimeoutError(f"store key {key!r} not published within {timeout:.0f}s")
         time.sleep(0.01)
+
+
+def arrival_barrier(store: dist.Store, prefix: str, size: int, timeout: float, cancel=None) -> None:
+    """Every member of an epoch announces itself before the collective bootstrap, which can
+    then never block on a member that went to a newer epoch (``cancel``) or never came."""
+    key = f"{prefix}/arrived"
+    store.add(key, 1)
+    deadline = time.monotonic() + timeout
+    while int(store.add(key, 0)) < size:
+        if cancel is not None and cancel():
+            raise CommError(f"superseded before all {size} members arrived at {prefix}")
+        if time.monotonic() > deadline:
+            raise CommError(f"only {int(store.add(key, 0))}/{size} members arrived at {prefix} within {timeout:.0f}s")
+        time.sleep(0.005)
 
 
 class Communicator:
@@ -64,18 +81,30 @@ class Communicator:
 
 class RcclCommunicator(Communicator):
     def __init__(self, store: dist.Store, prefix: str, rank: int, size: int, device: torch.device,
-                 timeout: float = 300.0, stream: torch.cuda.Stream | None = None):
+                 timeout: float = 300.0, stream: torch.cuda.Stream | None = None, cancel=None):
         self.rank, self.size, self.device = rank, size, device
         h = N.hip()
+        arrival_barrier(store, prefix, size, timeout, cancel)
         key = f"{prefix}/rccl_uid"
         if rank == 0:
             uid = h.rccl_unique_id()
             store.set(key, uid)
         else:
-            uid = store_get(store, key, timeout)
+            uid = store_get(store, key, timeout, cancel)
         with torch.cuda.device(device):
             self._c = h.RcclComm(uid, size, rank, device.index if device.index is not None else
-                                 torch.cuda.current_device(), timeout)
+                                 torch.cuda.current_device(), timeout, False)
+        deadline = time.monotonic() + timeout
+        try:
+            while not self._c.poll_ready():  # non-blocking init: abandonable, bounded
+                if cancel is not None and cancel():
+                    raise CommError("RCCL init superseded by a newer membership epoch")
+                if time.monotonic() > deadline:
+                    raise CommError(f"RCCL init timed out after {timeout:.0f}s")
+                time.sleep(0.001)
+        except Exception as e:
+            self._c.abort()
+            raise e if isinstance(e, CommError) else CommError(str(e)) from e
         self.stream = stream
 
     def _s(self) -> int:
@@ -140,9 +169,11 @@ class RcclCommunicator(Communicator):
 
 
 class GlooCommunicator(Communicator):
-    def __init__(self, store: dist.Store, prefix: str, rank: int, size: int, timeout: float = 300.0):
+    def __init__(self, store: dist.Store, prefix: str, rank: int, size: int, timeout: float = 300.0,
+                 cancel=None):
         os.environ.setdefault("GLOO_SOCKET_IFNAME", "lo")
         self.rank, self.size, self.device = rank, size, torch.device("cpu")
+        arrival_barrier(store, prefix, size, timeout, cancel)
         self._pg = dist.ProcessGroupGloo(dist.PrefixStore(prefix + "/gloo", store), rank, size,
                                          datetime.timedelta(seconds=timeout))
         self._aborted = False
@@ -232,13 +263,13 @@ class LocalCommunicator(Communicator):
 
 def create_communicator(store: dist.Store, prefix: str, rank: int, size: int, device: torch.device,
                         backend: str = "auto", timeout: float = 300.0,
-                        stream: torch.cuda.Stream | None = None) -> Communicator:
+                        stream: torch.cuda.Stream | None = None, cancel=None) -> Communicator:
     if size == 1:
         return LocalCommunicator(device)
     if backend == "auto":
         backend = "rccl" if device.type == "cuda" else "gloo"
     if backend == "rccl":
-        return RcclCommunicator(store, prefix, rank, size, device, timeout, stream)
+        return RcclCommunicator(store, prefix, rank, size, device, timeout, stream, cancel)
     if backend == "gloo":
-        return GlooCommunicator(store, prefix, rank, size, timeout)
+        return GlooCommunicator(store, prefix, rank, size, timeout, cancel)
     raise ValueError(f"unknown comm backend {backend!r}")

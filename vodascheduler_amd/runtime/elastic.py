@@ -148,10 +148,16 @@ class ElasticContext:
         self.members = self.rdzv.members(epoch)
         self.rank = self.members.index(self.worker_id)
         self.size = len(self.members)
+        log.debug("%s: %s joins epoch %d as rank %d/%d", self.job, self.worker_id, epoch, self.rank, self.size)
         self._latest_seen = max(self._latest_seen, epoch)
         self._agree_evt = None
+        # a newer epoch published before this one's bootstrap finished, or the job ending
+        # (finished by the old members before they saw this epoch), means some member will
+        # never arrive here: abandon instead of blocking until the timeout
         self.comm = create_communicator(self.rdzv.store, self.rdzv.comm_prefix(epoch), self.rank, self.size,
-                                        self.device, self.backend, self.timeout)
+                                        self.device, self.backend, self.timeout,
+                                        cancel=lambda: (self.rdzv.latest_epoch() > epoch
+                                                        or self.rdzv.outcome() is not None))
         self.resize_log.append({"epoch": epoch, "world": self.size, "comm_init_s": time.perf_counter() - t0})
 
     def destroy_comm(self, abort: bool = False) -> None:
@@ -400,6 +406,9 @@ class TorchState(State):
 
     def tensors(self):
         ts: list[torch.Tensor] = []
+        for m in self.model.modules():  # host-side counters -> buffers before they are synced
+            if hasattr(m, "sync_batches_tracked"):
+                m.sync_batches_tracked()
         opt = self.optimizer
         if opt is not None and hasattr(opt, "flat_state_tensors"):
             ts += opt.flat_state_tensors()
@@ -436,8 +445,17 @@ def run(func: Callable) -> Callable:
             if e == 0:
                 _leave(state, e)
                 return None
-            ctx.join(e)
-            state.sync()
+            try:
+                ctx.join(e)
+                state.sync()
+            except CommError as err:  # superseded / peer lost during bootstrap or sync
+                log.warning("%s/%s: epoch %d not established (%s); waiting for a newer one", ctx.job,
+                            ctx.worker_id, e, err)
+                ctx.min_epoch = e + 1
+                ctx.destroy_comm(abort=True)
+                if ctx.holds_state:
+                    state.restore()
+                continue
             ctx.resize_log[-1]["sync_s"] = time.perf_counter() - t0
             if reset:
                 state.on_reset()

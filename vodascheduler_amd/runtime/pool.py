@@ -61,7 +61,10 @@ class PoolBackend(Backend):
         for n, g in worker_locs:
             self.node_gpus.setdefault(n, []).append(g)
         self.train_defaults = dict(train_defaults or {})
-        self.members: dict[str, list[str]] = {}
+        self.members: dict[str, list[str]] = {}    # desired membership (scheduler view)
+        self.live: dict[str, tuple[int, list[str]]] = {}  # last published (epoch, members)
+        self.pending: dict[str, tuple] = {}           # membership waiting for the live epoch to sync
+        self.settle_timeout = 120.0
         self.active: set[str] = set()
         self.published: dict[tuple[str, int], float] = {}
         self.resize_latency: list[dict] = []
@@ -83,7 +86,6 @@ class PoolBackend(Backend):
 
     def _apply_locked(self, a: JobAction) -> None:
         name = a.job.name
-        rdzv = JobRendezvous(self.store, name)
         if a.kind == HALT:
             new_members: list[str] = []
         else:
@@ -94,17 +96,45 @@ class PoolBackend(Backend):
         if new_members == old:
             return
         t = time.time()
-        e = rdzv.publish(new_members)
         with self._lock:
             self.members[name] = new_members
-            self.published[(name, e)] = t
             if new_members:
                 self.active.add(name)
-            self.events.append({"t": t, "job": name, "epoch": e, "kind": a.kind, "world": len(new_members),
-                                "prev_world": len(old)})
         cfg = job_train_config(a.job, self.train_defaults)
+        # One membership change in flight per job: a new epoch is published only after every
+        # member of the previous one has joined it (rank 0 writes ``e/<n>/synced`` at the end
+        # of the collective state sync).  Publishing earlier lets two members join DIFFERENT
+        # epochs (one read the membership before the newer publish, one after) and block
+        # forever building two communicators -- reproduced on CPU/gloo with a resize right
+        # after a start.  Queued changes coalesce: only the newest membership is published.
+        self.pending[name] = (new_members, a.kind, t, cfg)
+        self._publish_if_settled(name)
+
+    def _publish_if_settled(self, name: str, force: bool = False) -> None:
+        """Publish the job's pending membership if its live epoch has synced (caller holds
+        ``_pub_lock``)."""
+        if name not in self.pending:
+            return
+        rdzv = JobRendezvous(self.store, name)
+        live_e, live_m = self.live.get(name, (0, []))
+        if live_m and not force and rdzv.get(f"e/{live_e}/synced") is None and rdzv.outcome() is None:
+            t_req = self.pending[name][2]
+            if time.time() - t_req < self.settle_timeout:
+                return  # the monitor retries
+            log.warning("job %s: epoch %d not synced after %.0fs; publishing anyway", name, live_e,
+                        self.settle_timeout)
+        new_members, kind, t, cfg = self.pending.pop(name)
+        if new_members == live_m:
+            return
+        e = rdzv.publish(new_members)
+        log.debug("publish %s epoch %d members %s (was %s)", name, e, new_members, live_m)
+        with self._lock:
+            self.live[name] = (e, list(new_members))
+            self.published[(name, e)] = t
+            self.events.append({"t": t, "t_publish": time.time(), "job": name, "epoch": e, "kind": kind,
+                                "world": len(new_members), "prev_world": len(live_m)})
         for wid in new_members:
-            if wid not in old:
+            if wid not in live_m:
                 self._mail(wid, {"job": name, "epoch": e, "cfg": cfg})
 
     def _mail(self, wid: str, msg: dict) -> None:
@@ -117,12 +147,15 @@ class PoolBackend(Backend):
 
     def delete_job(self, job_name: str) -> None:
         rdzv = JobRendezvous(self.store, job_name)
-        if self.members.get(job_name):
-            rdzv.publish([])
-        rdzv.mark_done(False, "deleted")
-        with self._lock:
-            self.members.pop(job_name, None)
-            self.active.discard(job_name)
+        with self._pub_lock:
+            self.pending.pop(job_name, None)
+            if self.live.get(job_name, (0, []))[1]:
+                e = rdzv.publish([])
+                self.live[job_name] = (e, [])
+            rdzv.mark_done(False, "deleted")
+            with self._lock:
+                self.members.pop(job_name, None)
+                self.active.discard(job_name)
 
     def nodes(self):
         return {k: list(v) for k, v in self.node_gpus.items()}
@@ -139,12 +172,21 @@ class PoolBackend(Backend):
     # ------------------------------------------------------------------ monitor
     def _monitor(self) -> None:
         while not self._stop.is_set():
+            if self.pending:
+                with self._pub_lock:
+                    for name in list(self.pending):
+                        try:
+                            self._publish_if_settled(name)
+                        except Exception:  # store hiccup: retry next round
+                            log.exception("publishing membership of %s failed", name)
             with self._lock:
                 jobs = list(self.active)
                 pend = [k for k in self.published if k not in {(r["job"], r["epoch"]) for r in self.resize_latency}]
             for name in jobs:
                 out = JobRendezvous(self.store, name).outcome()
                 if out is not None:
+                    with self._pub_lock:
+                        self.pending.pop(name, None)
                     with self._lock:
                         self.active.discard(name)
                         self.members.pop(name, None)
@@ -196,6 +238,7 @@ class PoolWorker:
             time.sleep(self.idle_poll)
 
     def _run(self, msg: dict) -> None:
+        log.debug("worker %s: mail #%d job %s epoch %s", self.wid, self.done, msg["job"], msg["epoch"])
         ctx = ElasticContext(self.store, msg["job"], self.wid, self.device, self.backend, self.timeout,
                              watch_store=self.watch_store, join_epoch=int(msg["epoch"]))
         cfg = TrainConfig(**msg["cfg"])
