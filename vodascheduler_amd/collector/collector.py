@@ -144,3 +144,30 @@ class MetricsCollector:
             except NotFound:
                 pass
         return fields
+
+
+def main(argv=None) -> int:
+    """One collector pass (the reference runs it as a CronJob every minute,
+    helm/voda-scheduler/values.yaml:104) or ``--every SECONDS`` in a loop."""
+    import argparse
+    import time
+
+    from ..common.store import open_store
+
+    ap = argparse.ArgumentParser("vodascheduler-collector")
+    ap.add_argument("--store", required=True, help="sqlite:///path (shared with the services)")
+    ap.add_argument("--metrics-dir", default=os.environ.get("VODA_METRICS_DIR", "/metrics"))
+    ap.add_argument("--every", type=float, default=0.0, help="repeat every N seconds (0 = one pass)")
+    a = ap.parse_args(argv)
+    logging.basicConfig(level=logging.INFO)
+    c = MetricsCollector(open_store(a.store), a.metrics_dir)
+    while True:
+        n = c.update_info_all()
+        log.info("updated job info of %d job(s)", n)
+        if a.every <= 0:
+            return 0
+        time.sleep(a.every)
+
+
+if __name__ == "__main__":
+    raise SystemExit(main())

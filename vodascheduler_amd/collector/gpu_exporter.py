@@ -100,3 +100,28 @@ class GpuExporter:
     def exposition(self) -> bytes:
         self.refresh()
         return generate_latest(self.registry)
+
+
+def main(argv=None) -> int:
+    """Serve ``GET /metrics`` with rocm-smi telemetry (the reference relies on an external
+    nvidia_smi_exporter, README.md:94)."""
+    import argparse
+    import logging
+
+    from ..utils.http import HttpServer, Router
+
+    ap = argparse.ArgumentParser("vodascheduler-gpu-exporter")
+    ap.add_argument("--port", type=int, default=9400)
+    a = ap.parse_args(argv)
+    logging.basicConfig(level=logging.INFO)
+    exp = GpuExporter()
+    r = Router()
+    r.add("GET", "/metrics", lambda b, q: (200, "text/plain; version=0.0.4", exp.exposition()))
+    srv = HttpServer(r, port=a.port, name="gpu-exporter")
+    logging.info("rocm-smi exporter on :%d", srv.port)
+    srv.serve_forever()
+    return 0
+
+
+if __name__ == "__main__":
+    raise SystemExit(main())

@@ -8,7 +8,8 @@ Flags mirror the reference (``-gpu``, ``-resume``, ``-algorithm``, ``-placement`
 -> ``--log-level``).  ``--allocator URL`` sends allocation requests to a remote allocator
 service over HTTP (``POST /allocation``, as the reference does); without it the allocator
 runs in-process.  Backends: ``local`` (node agent + warm per-GPU workers, the MI355X-native
-path) and ``null`` (record actions only; the virtual-time cluster lives in
+path), ``k8s`` (MPIJob CRD + pod tolerations on a Kubernetes cluster, the reference's
+deployment model) and ``null`` (record actions only; the virtual-time cluster lives in
 ``vodascheduler simulate``).  REST on :55588:
 ``GET /training``, ``PUT /algorithm``, ``PUT /ratelimit``, ``GET /metrics``.
 """
@@ -52,7 +53,13 @@ def build_parser() -> argparse.ArgumentParser:
     ap.add_argument("--store", default="memory://", help="memory:// or sqlite:///path")
     ap.add_argument("--mq", default="inproc://", help="inproc:// or sqlite:///path")
     ap.add_argument("--allocator", default=None, help="URL of a remote allocator service")
-    ap.add_argument("--backend", default="local", choices=["local", "null"])
+    ap.add_argument("--backend", default="local", choices=["local", "k8s", "null"])
+    ap.add_argument("--k8s-url", default=None, help="API server URL (default: in-cluster service account)")
+    ap.add_argument("--k8s-token", default=os.environ.get("VODA_K8S_TOKEN"))
+    ap.add_argument("--k8s-insecure", action="store_true", help="skip TLS verification of the API server")
+    ap.add_argument("--namespace", default="voda-scheduler")
+    ap.add_argument("--no-configmap-opt", action="store_true",
+                    help="do not annotate the launcher on resize (reference -configmap_opt=false)")
     ap.add_argument("--node", default=os.environ.get("VODA_NODE", "node0"))
     ap.add_argument("--gpus", default=None, help="comma-separated GPU indices (default: all)")
     ap.add_argument("--device-type", default="cuda", choices=["cuda", "cpu"],
@@ -80,7 +87,7 @@ class SchedulerProcess:
         self.agent = None
         self.tcp_store = None
         self.collector = None
-        gpus = parse_gpus(a.gpus, a.device_type)
+        gpus = parse_gpus(a.gpus, a.device_type) if a.backend != "k8s" else []
         if a.backend == "local":
             from ..agent.node_agent import NodeAgent
             from ..backend.local import LocalBackend
@@ -91,6 +98,11 @@ class SchedulerProcess:
                                    store=connect_store("127.0.0.1", a.store_port),
                                    backend="rccl" if a.device_type == "cuda" else "gloo")
             self.backend = LocalBackend(self.tcp_store, [self.agent], {"metrics_dir": a.metrics_dir})
+        elif a.backend == "k8s":
+            from ..backend.k8s import K8sBackend, K8sClient
+
+            self.backend = K8sBackend(K8sClient(a.k8s_url, a.k8s_token, insecure=a.k8s_insecure), a.gpu_type,
+                                      a.namespace, configmap_opt=not a.no_configmap_opt)
         else:
             self.backend = NullBackend({a.node: gpus})
         alloc = HttpAllocatorClient(a.allocator) if a.allocator else ResourceAllocator(self.store)
