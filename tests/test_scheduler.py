@@ -92,7 +92,16 @@ def test_completion_reschedules_immediately_when_work_conserving(work_conserving
     assert e.core.job_num_gpu[b] == 2
     c = e.submit("c", 1, 1, 1)
     e.step(1)
-    assert e.core.job_num_gpu[c] == 0  # arrivals are still rate-limited
+    assert e.core.job_num_gpu[c] == 0  # arrivals on a full cluster are still rate-limited
+
+
+def test_arrival_on_idle_gpus_starts_immediately():
+    e = Env(gpus=4, algorithm="FIFO", rate=30)
+    a = e.submit("a", 2, 2, 2)
+    e.step()
+    b = e.submit("b", 2, 2, 2)
+    e.step(1)
+    assert e.core.job_num_gpu[b] == 2  # 2 GPUs were idle: no rate-limit wait
 
 
 def test_finish_and_scale_actions():

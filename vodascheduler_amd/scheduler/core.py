@@ -60,11 +60,11 @@ class SchedulerCore:
         self.algorithm = algorithm
         self.rate_limit_sec = float(rate_limit_sec)
         # Work-conserving rescheduling (documented deviation): a reschedule requested because
-        # GPUs were FREED (job completed / failed / deleted) runs immediately instead of
-        # waiting out the rate limit -- the reference rate-limits every trigger
-        # (scheduler.go:300-316), which leaves freed GPUs idle for up to ``rate_limit``
-        # seconds.  Arrivals and priority changes are still rate-limited, so bursts of
-        # submissions still coalesce into one reschedule.
+        # GPUs were FREED (job completed / failed / deleted), or by an arrival while GPUs sit
+        # idle, runs immediately instead of waiting out the rate limit -- the reference
+        # rate-limits every trigger (scheduler.go:300-316), which leaves GPUs idle for up to
+        # ``rate_limit`` seconds.  Arrivals on a fully allocated cluster and priority changes
+        # are still rate-limited, so bursts of submissions still coalesce.
         self.work_conserving = work_conserving
         self._urgent = False
         self.tick_sec = float(tick_sec)
@@ -267,6 +267,8 @@ class SchedulerCore:
         self._persist(job)
         self.ready_jobs[name] = job
         self.job_num_gpu[name] = 0
+        if self.work_conserving and sum(self.job_num_gpu.values()) < self.total_gpus:
+            self._urgent = True  # idle GPUs: start the arrival now, nothing has to shrink
         self.trigger_resched()
         self.metrics.jobs_created.inc()
         self._emit("created", job=name)
