@@ -19,9 +19,10 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from vodascheduler_amd.models import get_workload, prepare_model  # noqa: E402
 from vodascheduler_amd.ops import _native  # noqa: E402
 from vodascheduler_amd.ops.optim import make_optimizer  # noqa: E402
+from vodascheduler_amd.runtime.stepgraph import GraphedStepper  # noqa: E402
 
 
-def run(model: str, batch: int | None, steps: int, warmup: int, marker: bool = False) -> dict:
+def run(model: str, batch: int | None, steps: int, warmup: int, marker: bool = False, graph: bool = False) -> dict:
     dev = torch.device("cuda", 0)
     w = get_workload(model)
     bs = batch or w.per_gpu_batch
@@ -32,13 +33,18 @@ def run(model: str, batch: int | None, steps: int, warmup: int, marker: bool = F
     if w.channels_last:
         b = tuple(t.to(memory_format=torch.channels_last) if t.dim() == 4 else t for t in b)
 
-    def step():
+    def step_fn(bb):
         opt.zero_grad()
-        with torch.autocast("cuda", dtype=torch.bfloat16):
-            loss = w.loss(m, b)
+        with torch.autocast("cuda", dtype=torch.bfloat16, cache_enabled=not graph):
+            loss = w.loss(m, bb)
         loss.backward()
         opt.step()
         return loss
+
+    stepper = GraphedStepper(step_fn, m, opt, warmup=2, enabled=graph)
+
+    def step():
+        return stepper(b)
 
     for _ in range(warmup):
         step()
@@ -52,7 +58,7 @@ def run(model: str, batch: int | None, steps: int, warmup: int, marker: bool = F
     torch.cuda.synchronize(dev)
     dt = (time.perf_counter() - t0) / steps
     return {"model": model, "batch": bs, "ms_per_step": round(dt * 1e3, 3),
-            "samples_per_s": round(bs / dt, 1), "loss": float(loss.detach())}
+            "samples_per_s": round(bs / dt, 1), "loss": float(loss.detach()), "graph": stepper.graph is not None}
 
 
 def main():
@@ -63,11 +69,12 @@ def main():
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--cudnn-benchmark", action="store_true", help="MIOpen exhaustive find (benchmark mode)")
     ap.add_argument("--profile-marker", action="store_true", help="launch a marker kernel before the timed steps")
+    ap.add_argument("--graph", action="store_true", help="replay the whole step as one captured hipGraph")
     a = ap.parse_args()
     if a.cudnn_benchmark:
         torch.backends.cudnn.benchmark = True
     _native.hip()
-    print(json.dumps(run(a.model, a.batch, a.steps, a.warmup, a.profile_marker)), flush=True)
+    print(json.dumps(run(a.model, a.batch, a.steps, a.warmup, a.profile_marker, a.graph)), flush=True)
 
 
 if __name__ == "__main__":

@@ -20,7 +20,7 @@ void sgd_step(uintptr_t p, uintptr_t g, int g_dtype, uintptr_t mom_buf, uintptr_
               uintptr_t stream);
 void adam_step(uintptr_t p, uintptr_t g, int g_dtype, uintptr_t m, uintptr_t v, uintptr_t p_lp, int lp_dtype,
                int64_t n, float lr, float beta1, float beta2, float eps, float wd, bool adamw, int64_t step,
-               float grad_scale, uintptr_t stream);
+               float grad_scale, uintptr_t step_ptr, uintptr_t stream);
 void rmsprop_step(uintptr_t p, uintptr_t g, int g_dtype, uintptr_t sq, uintptr_t mom_buf, uintptr_t gavg,
                   uintptr_t p_lp, int lp_dtype, int64_t n, float lr, float alpha, float eps, float wd, float momentum,
                   bool centered, float grad_scale, uintptr_t stream);

@@ -100,7 +100,15 @@ __device__ __forceinline__ void adam1(float& p, float g, float& m, float& v, con
 template <typename GT, typename LP>
 __global__ __launch_bounds__(256) void adam_kernel(float* __restrict__ p, const GT* __restrict__ g,
                                                    float* __restrict__ m, float* __restrict__ v,
-                                                   LP* __restrict__ q, int64_t n, AdamArgs a) {
+                                                   LP* __restrict__ q, int64_t n, AdamArgs a,
+                                                   const int64_t* __restrict__ dstep) {
+  if (dstep != nullptr) {
+    // step counter read on the device: the launch stays valid inside a captured hipGraph
+    // that is replayed every step (the counter is advanced by a captured add before us)
+    const float t = float(*dstep);
+    a.step_size = a.lr / (1.f - powf(a.beta1, t));
+    a.inv_sqrt_bc2 = rsqrtf(1.f - powf(a.beta2, t));
+  }
   const int64_t n4 = n >> 2;
   const int64_t stride = int64_t(gridDim.x) * blockDim.x;
   for (int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < n4; i += stride) {
@@ -232,11 +240,12 @@ void sgd_step(uintptr_t p, uintptr_t g, int g_dtype, uintptr_t mom_buf, uintptr_
 
 void adam_step(uintptr_t p, uintptr_t g, int g_dtype, uintptr_t m, uintptr_t v, uintptr_t p_lp,
                int lp_dtype, int64_t n, float lr, float beta1, float beta2, float eps, float wd,
-               bool adamw, int64_t step, float grad_scale, uintptr_t stream) {
-  VODA_CHECK(step >= 1, "adam step counter must start at 1");
+               bool adamw, int64_t step, float grad_scale, uintptr_t step_ptr, uintptr_t stream) {
+  VODA_CHECK(step >= 1 || step_ptr != 0, "adam step counter must start at 1");
   if (n == 0) return;
-  const double bc1 = 1.0 - std::pow(double(beta1), double(step));
-  const double bc2 = 1.0 - std::pow(double(beta2), double(step));
+  const double st = double(std::max<int64_t>(step, 1));
+  const double bc1 = 1.0 - std::pow(double(beta1), st);
+  const double bc2 = 1.0 - std::pow(double(beta2), st);
   AdamArgs a{lr, beta1, beta2, eps, wd, grad_scale, float(lr / bc1), float(1.0 / std::sqrt(bc2)),
              adamw ? 1 : 0};
   unsigned grid = stream_grid((n + 3) / 4);
@@ -244,7 +253,7 @@ void adam_step(uintptr_t p, uintptr_t g, int g_dtype, uintptr_t m, uintptr_t v, 
     hipLaunchKernelGGL((adam_kernel<GT, LP>), dim3(grid), dim3(256), 0, as_stream(stream),
                        reinterpret_cast<float*>(p), reinterpret_cast<const GT*>(g),
                        reinterpret_cast<float*>(m), reinterpret_cast<float*>(v),
-                       reinterpret_cast<LP*>(p_lp), n, a);
+                       reinterpret_cast<LP*>(p_lp), n, a, reinterpret_cast<const int64_t*>(step_ptr));
   });
   check_launch();
 }

@@ -1,0 +1,48 @@
+"""Whole-step hipGraph capture (runtime/stepgraph.py) trains exactly like eager mode."""
+import pytest
+import torch
+
+from vodascheduler_amd.models import get_workload, prepare_model
+from vodascheduler_amd.ops.optim import make_optimizer
+from vodascheduler_amd.runtime.stepgraph import GraphedStepper
+
+pytestmark = pytest.mark.gpu
+
+
+def _train(name, graph, steps=8, bs=16):
+    dev = torch.device("cuda", 0)
+    w = get_workload(name)
+    torch.manual_seed(0)
+    m = prepare_model(w, dev)
+    opt = make_optimizer(w.optimizer, m.parameters(), **w.opt_kwargs)
+    g = torch.Generator(device=dev).manual_seed(1)
+    batches = [w.make_batch(bs, dev, g) for _ in range(2)]
+    if w.channels_last:
+        batches = [tuple(t.to(memory_format=torch.channels_last) if t.dim() == 4 else t for t in b) for b in batches]
+
+    def step_fn(b):
+        opt.zero_grad()
+        with torch.autocast("cuda", dtype=torch.bfloat16, cache_enabled=False):
+            loss = w.loss(m, b)
+        loss.backward()
+        opt.step()
+        return loss
+
+    st = GraphedStepper(step_fn, m, opt, warmup=2, enabled=graph)
+    losses = [float(st(batches[i % 2])) for i in range(steps)]
+    torch.cuda.synchronize()
+    assert (st.graph is not None) == graph
+    return losses, torch.cat([p.detach().float().flatten() for p in m.parameters()]), opt, m
+
+
+@pytest.mark.parametrize("name", ["mnist", "mnist-torch", "resnet50-cifar"])
+def test_graph_matches_eager(name):
+    le, pe, oe, me = _train(name, False)
+    lg, pg, og, mg = _train(name, True)
+    torch.testing.assert_close(torch.tensor(lg), torch.tensor(le), atol=2e-2, rtol=2e-2)
+    torch.testing.assert_close(pg, pe, atol=2e-2, rtol=2e-2)
+    assert og._steps == oe._steps == [8] * len(oe._steps)
+    assert og._step_t.tolist() == [8] * len(oe._steps)
+    bn = [m for m in mg.modules() if hasattr(m, "sync_batches_tracked")]
+    if bn:
+        assert int(mg.state_dict()[[k for k in mg.state_dict() if k.endswith("num_batches_tracked")][0]]) == 8

@@ -50,6 +50,11 @@ class _FusedFlatOptimizer(torch.optim.Optimizer):
             self.flat_groups.append(fg)
             self._flat_state.append({})
             self._steps.append(0)
+        # Per-group step counters on the device.  They are part of the synced/checkpointed
+        # state (a rank that joins a running job must use the same Adam bias correction as
+        # the others) and are what the kernels read, so a step captured in a hipGraph stays
+        # correct on every replay.
+        self._step_t = torch.zeros(len(self.param_groups), dtype=torch.int64, device=self.flat_groups[0].device)
 
     # -- state buffers (allocated lazily, flat fp32) --
     def _buf(self, gi: int, name: str) -> torch.Tensor:
@@ -68,6 +73,7 @@ class _FusedFlatOptimizer(torch.optim.Optimizer):
         if closure is not None:
             with torch.enable_grad():
                 loss = closure()
+        self._step_t.add_(1)
         for gi, group in enumerate(self.param_groups):
             self._steps[gi] += 1
             fg = self.flat_groups[gi]
@@ -96,7 +102,16 @@ class _FusedFlatOptimizer(torch.optim.Optimizer):
             out.append(fg.master)
             for name in self._state_names_for(gi):
                 out.append(self._buf(gi, name))
+        out.append(self._step_t)
         return out
+
+    def reset_steps(self) -> None:
+        self._steps = [0] * len(self._steps)
+        self._step_t.zero_()
+
+    def advance_host_steps(self, n: int = 1) -> None:
+        """Host mirror of the device counters after ``n`` replays of a captured step."""
+        self._steps = [s + n for s in self._steps]
 
     def _state_names_for(self, gi: int) -> tuple[str, ...]:
         return self._state_names
@@ -118,6 +133,7 @@ class _FusedFlatOptimizer(torch.optim.Optimizer):
         for g, sg in zip(self.param_groups, sd["param_groups"]):
             g.update(sg)
         self._steps = list(sd["steps"])
+        self._step_t.copy_(torch.tensor(self._steps, dtype=torch.int64))
         for gi, (fg, d) in enumerate(zip(self.flat_groups, sd["flat"])):
             fg.master.copy_(d["master"])
             for name in self._state_names_for(gi):
@@ -126,9 +142,10 @@ class _FusedFlatOptimizer(torch.optim.Optimizer):
             fg.sync_lowp_from_master()
 
     def after_external_update(self) -> None:
-        """Call after master buffers were overwritten (broadcast/restore)."""
+        """Call after master buffers / step counters were overwritten (broadcast/restore)."""
         for fg in self.flat_groups:
             fg.sync_lowp_from_master()
+        self._steps = [int(x) for x in self._step_t.tolist()]
 
 
 class FusedSGD(_FusedFlatOptimizer):
@@ -186,7 +203,7 @@ class FusedAdam(_FusedFlatOptimizer):
         N.hip().adam_step(fg.master.data_ptr(), fg.grad.data_ptr(), N.dtype_code(fg.grad.dtype), m.data_ptr(),
                           v.data_ptr(), lp, lpdt, fg.numel, float(g["lr"]), float(b1), float(b2), float(g["eps"]),
                           float(g["weight_decay"]), bool(g["adamw"]), self._steps[gi], float(g["grad_scale"]),
-                          N.stream_of(fg.master))
+                          self._step_t.data_ptr() + gi * 8, N.stream_of(fg.master))
 
     def _step_cpu(self, gi, g, fg):
         p = fg.master

@@ -28,6 +28,7 @@ from ..models import get_workload, prepare_model
 from ..ops.optim import make_optimizer
 from ..parallel.ddp import ElasticDDP
 from ..runtime.elastic import ElasticContext, TorchState, run
+from ..runtime.stepgraph import GraphedStepper
 from .metrics_logger import MetricsCSVLogger
 
 log = logging.getLogger("vodascheduler_amd.train")
@@ -48,6 +49,7 @@ class TrainConfig:
     checkpoint_every_epoch: bool = False
     seed: int = 0
     data_pool: int = 2                 # distinct synthetic batches cycled through
+    graph: bool = False                # capture the whole step in a hipGraph when world == 1
 
 
 def build(cfg: TrainConfig, device: torch.device):
@@ -89,7 +91,7 @@ class _Warm:
         for t, s in zip(self._tensors(), self._init):
             t.copy_(s)
         self.opt.after_external_update()
-        self.opt._steps = [0] * len(self.opt._steps)
+        self.opt.reset_steps()
         for g in self.opt.param_groups:
             g["lr"] = self.base_lr
 
@@ -131,7 +133,16 @@ def train_elastic(ctx: ElasticContext, cfg: TrainConfig, use_cache: bool = True)
         stats["resizes"] += 1
 
     state.register_reset_callbacks([on_reset])
-    amp = torch.autocast(device.type, dtype=torch.bfloat16, enabled=cfg.amp and device.type == "cuda")
+
+    def step_fn(batch):
+        ddp.zero_grad()
+        # autocast's weight-cast cache must be off inside a captured graph
+        with torch.autocast(device.type, dtype=torch.bfloat16, enabled=cfg.amp and device.type == "cuda",
+                            cache_enabled=False):
+            loss = w.loss(model, batch)
+        loss.backward()
+        ddp.step()
+        return loss
 
     @run
     def train(state):
@@ -140,18 +151,17 @@ def train_elastic(ctx: ElasticContext, cfg: TrainConfig, use_cache: bool = True)
         for gr in opt.param_groups:
             gr["lr"] = base_lr * world
         logger.set_params(world)
+        # world 1: the whole step replays as one hipGraph (launch-bound models); collectives
+        # of world > 1 stay eager.  Re-captured after every membership change.
+        stepper = GraphedStepper(step_fn, model, opt, warmup=2,
+                                 enabled=cfg.graph and world == 1 and device.type == "cuda")
         loss_t = None
         while state.epoch < cfg.epochs:
             t_ep = time.time()
             steps = 0
             while state.samples < samples_per_epoch:
                 batch = pool[state.step % len(pool)]
-                ddp.zero_grad()
-                with amp:
-                    loss = w.loss(model, batch)
-                loss.backward()
-                ddp.step()
-                loss_t = loss.detach()
+                loss_t = stepper(batch).detach()
                 state.samples += bs * world
                 state.step += 1
                 steps += 1
