@@ -29,13 +29,13 @@ def _train(name, graph, steps=8, bs=16):
         return loss
 
     st = GraphedStepper(step_fn, m, opt, warmup=2, enabled=graph)
-    losses = [float(st(batches[i % 2])) for i in range(steps)]
+    losses = [float(st(batches[i % 2]).detach()) for i in range(steps)]
     torch.cuda.synchronize()
     assert (st.graph is not None) == graph
     return losses, torch.cat([p.detach().float().flatten() for p in m.parameters()]), opt, m
 
 
-@pytest.mark.parametrize("name", ["mnist", "mnist-torch", "resnet50-cifar"])
+@pytest.mark.parametrize("name", ["mnist", "mnist-torch"])
 def test_graph_matches_eager(name):
     le, pe, oe, me = _train(name, False)
     lg, pg, og, mg = _train(name, True)
@@ -46,3 +46,9 @@ def test_graph_matches_eager(name):
     bn = [m for m in mg.modules() if hasattr(m, "sync_batches_tracked")]
     if bn:
         assert int(mg.state_dict()[[k for k in mg.state_dict() if k.endswith("num_batches_tracked")][0]]) == 8
+
+
+def test_only_validated_workloads_are_graph_safe():
+    from vodascheduler_amd.models import WORKLOADS
+
+    assert {n for n, w in WORKLOADS.items() if w.graph_safe} == {"mnist", "mnist-torch"}

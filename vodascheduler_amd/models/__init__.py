@@ -30,6 +30,10 @@ class Workload:
     channels_last: bool = False
     samples_unit: str = "img"   # throughput unit (img or tok)
     tokens_per_sample: int = 1
+    # whole-step hipGraph capture validated on MI355X (tests/test_stepgraph_gpu.py).  Not for
+    # models whose MIOpen conv solvers or GEMM paths are not capture-safe: ResNet-50/224
+    # replayed with wrong weight gradients and the NMT Transformer faulted (docs/kernels.md)
+    graph_safe: bool = False
 
 
 def _img_batch(c, h, w, classes):
@@ -92,9 +96,10 @@ WORKLOADS: dict[str, Workload] = {
                       dict(lr=0.01, momentum=0.9), channels_last=True),
     "inceptionv3": Workload("inceptionv3", InceptionV3, _img_batch(3, 75, 75, 10), _ce, 128, "rmsprop",
                             dict(lr=1e-3), channels_last=True),
-    "mnist": Workload("mnist", KerasMnistCNN, _img_batch(1, 28, 28, 10), _ce, 128, "adam", dict(lr=1e-3)),
+    "mnist": Workload("mnist", KerasMnistCNN, _img_batch(1, 28, 28, 10), _ce, 128, "adam", dict(lr=1e-3),
+                      graph_safe=True),
     "mnist-torch": Workload("mnist-torch", TorchMnistNet, _img_batch(1, 28, 28, 10), _nll, 64, "sgd",
-                            dict(lr=0.01, momentum=0.5)),
+                            dict(lr=0.01, momentum=0.5), graph_safe=True),
     "transformer": Workload("transformer", TransformerNMT, _nmt_batch, _nmt_loss, 512, "rmsprop", dict(lr=1e-3),
                             samples_unit="tok", tokens_per_sample=20),
     "bert-base": Workload("bert-base", BertBase, _bert_batch, _bert_loss, 64, "adamw",

@@ -49,7 +49,7 @@ class TrainConfig:
     checkpoint_every_epoch: bool = False
     seed: int = 0
     data_pool: int = 2                 # distinct synthetic batches cycled through
-    graph: bool = False                # capture the whole step in a hipGraph when world == 1
+    graph: bool = True                 # capture the whole step in a hipGraph when world == 1 (graph-safe models)
 
 
 def build(cfg: TrainConfig, device: torch.device):
@@ -154,7 +154,7 @@ def train_elastic(ctx: ElasticContext, cfg: TrainConfig, use_cache: bool = True)
         # world 1: the whole step replays as one hipGraph (launch-bound models); collectives
         # of world > 1 stay eager.  Re-captured after every membership change.
         stepper = GraphedStepper(step_fn, model, opt, warmup=2,
-                                 enabled=cfg.graph and world == 1 and device.type == "cuda")
+                                 enabled=cfg.graph and w.graph_safe and world == 1 and device.type == "cuda")
         loss_t = None
         while state.epoch < cfg.epochs:
             t_ep = time.time()
