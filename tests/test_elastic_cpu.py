@@ -119,3 +119,49 @@ def test_metrics_logger_resume(tmp_path):
     lg.log_epoch(0, 0.0, 2.0, 10, 1.5, workers=2)
     lg.log_epoch(1, 2.0, 1.0, 10, 1.2, workers=4)
     assert MetricsCSVLogger(str(tmp_path), "job", 5, 32).restored_epoch() == 2
+
+
+def _cache_worker(port, rank, q):
+    import torch.distributed  # noqa: F401
+    from vodascheduler_amd.parallel.comm import COMM_CACHE, create_communicator
+    torch.set_num_threads(1)
+    store = connect_store("127.0.0.1", port)
+    members = ["w0", "w1"]
+    dev = torch.device("cpu")
+    out = []
+    for epoch in range(4):
+        if epoch == 3 and rank == 1:
+            COMM_CACHE.clear()      # e.g. a restarted worker: nobody may reuse
+        c = create_communicator(store, f"t/cache/{epoch}", rank, 2, dev, "gloo", 60, members=members)
+        t = torch.full((4,), float(rank + epoch))
+        c.allreduce_(t)
+        out.append((c.cid, float(t[0])))
+        if epoch == 1:
+            # a different member order is a different communicator
+            c2 = create_communicator(store, "t/cache/perm", rank, 2, dev, "gloo", 60, members=members[::-1])
+            assert c2.cid != c.cid
+            COMM_CACHE.put(c2)
+        COMM_CACHE.put(c)
+    q.put((rank, out, COMM_CACHE.hits, len(COMM_CACHE)))
+    COMM_CACHE.clear()
+
+
+def test_comm_cache_reuses_same_member_list():
+    port = free_port()
+    store = connect_store("127.0.0.1", port, is_master=True)  # noqa: F841
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    ps = [ctx.Process(target=_cache_worker, args=(port, r, q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    res = dict((r, (o, h, n)) for r, o, h, n in (q.get(timeout=120) for _ in ps))
+    for p in ps:
+        p.join(30)
+    for r in range(2):
+        out, hits, n = res[r]
+        cids = [c for c, _ in out]
+        assert cids[0] == cids[1] == cids[2]      # epochs 1, 2 reuse epoch 0's communicator
+        assert cids[3] != cids[0]                 # rank 1 lost its cache: rebuilt everywhere
+        assert [v for _, v in out] == [1.0, 3.0, 5.0, 7.0]
+        assert hits == 2 and n == (2 if r == 0 else 1)  # rank 1 dropped the permuted one too
+    assert res[0][0] == res[1][0]

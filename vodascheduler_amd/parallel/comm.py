@@ -14,8 +14,12 @@ through a c10d ``Store`` under a per-epoch key prefix.
 from __future__ import annotations
 
 import datetime
+import hashlib
 import os
+import threading
 import time
+import uuid
+from collections import OrderedDict
 
 import torch
 import torch.distributed as dist
@@ -81,16 +85,20 @@ class Communicator:
 
 class RcclCommunicator(Communicator):
     def __init__(self, store: dist.Store, prefix: str, rank: int, size: int, device: torch.device,
-                 timeout: float = 300.0, stream: torch.cuda.Stream | None = None, cancel=None):
+                 timeout: float = 300.0, stream: torch.cuda.Stream | None = None, cancel=None,
+                 arrived: bool = False):
         self.rank, self.size, self.device = rank, size, device
         h = N.hip()
-        arrival_barrier(store, prefix, size, timeout, cancel)
+        if not arrived:
+            arrival_barrier(store, prefix, size, timeout, cancel)
         key = f"{prefix}/rccl_uid"
         if rank == 0:
             uid = h.rccl_unique_id()
             store.set(key, uid)
         else:
             uid = store_get(store, key, timeout, cancel)
+        self.cid = hashlib.sha1(bytes(uid)).hexdigest()[:20]
+        self.cache_key = None
         with torch.cuda.device(device):
             self._c = h.RcclComm(uid, size, rank, device.index if device.index is not None else
                                  torch.cuda.current_device(), timeout, False)
@@ -170,10 +178,15 @@ class RcclCommunicator(Communicator):
 
 class GlooCommunicator(Communicator):
     def __init__(self, store: dist.Store, prefix: str, rank: int, size: int, timeout: float = 300.0,
-                 cancel=None):
+                 cancel=None, arrived: bool = False):
         os.environ.setdefault("GLOO_SOCKET_IFNAME", "lo")
         self.rank, self.size, self.device = rank, size, torch.device("cpu")
-        arrival_barrier(store, prefix, size, timeout, cancel)
+        if not arrived:
+            arrival_barrier(store, prefix, size, timeout, cancel)
+        if rank == 0:
+            store.set(f"{prefix}/gloo_cid", uuid.uuid4().hex[:20])
+        self.cid = store_get(store, f"{prefix}/gloo_cid", timeout, cancel).decode()
+        self.cache_key = None
         self._pg = dist.ProcessGroupGloo(dist.PrefixStore(prefix + "/gloo", store), rank, size,
                                          datetime.timedelta(seconds=timeout))
         self._aborted = False
@@ -263,13 +276,111 @@ class LocalCommunicator(Communicator):
 
 def create_communicator(store: dist.Store, prefix: str, rank: int, size: int, device: torch.device,
                         backend: str = "auto", timeout: float = 300.0,
-                        stream: torch.cuda.Stream | None = None, cancel=None) -> Communicator:
+                        stream: torch.cuda.Stream | None = None, cancel=None,
+                        members: list[str] | None = None) -> Communicator:
+    """New communicator for one membership epoch, or -- when ``members`` is given and every
+    member still holds an idle communicator built for exactly this ordered member list --
+    that cached one (see :class:`CommCache`)."""
     if size == 1:
         return LocalCommunicator(device)
     if backend == "auto":
         backend = "rccl" if device.type == "cuda" else "gloo"
+    if backend not in ("rccl", "gloo"):
+        raise ValueError(f"unknown comm backend {backend!r}")
+    key = (backend, tuple(members), str(device)) if members is not None else None
+    mine = COMM_CACHE.cid(key) if key is not None else ""
+    store.set(f"{prefix}/have/{rank}", mine)   # before arriving: peers read it after the barrier
+    arrival_barrier(store, prefix, size, timeout, cancel)
+    if key is not None and mine:
+        theirs = [store_get(store, f"{prefix}/have/{r}", timeout, cancel).decode() for r in range(size)]
+        if all(c == mine for c in theirs):
+            comm = COMM_CACHE.take(key)
+            if comm is not None:
+                if hasattr(comm, "stream"):
+                    comm.stream = stream
+                return comm
+    if key is not None:
+        COMM_CACHE.drop(key)
     if backend == "rccl":
-        return RcclCommunicator(store, prefix, rank, size, device, timeout, stream, cancel)
-    if backend == "gloo":
-        return GlooCommunicator(store, prefix, rank, size, timeout, cancel)
-    raise ValueError(f"unknown comm backend {backend!r}")
+        comm = RcclCommunicator(store, prefix, rank, size, device, timeout, stream, cancel, arrived=True)
+    else:
+        comm = GlooCommunicator(store, prefix, rank, size, timeout, cancel, arrived=True)
+    comm.cache_key = key
+    return comm
+
+
+class CommCache:
+    """Per-process LRU cache of IDLE communicators keyed by (backend, ordered member list,
+    device).
+
+    An RCCL communicator binds GPUs, not jobs: when a job shrinks and grows back, or the next
+    job lands on the same ordered set of GPUs, the communicator built earlier is reused
+    instead of paying another RCCL bootstrap (unique-id exchange, topology detection,
+    xGMI connection setup) -- the dominant part of an elastic resize with warm workers.
+    Reuse is agreed collectively: every member announces the id of the communicator it
+    holds for the member list; only if ALL hold the same id is it reused, otherwise a new
+    one is built (a restarted or evicted member therefore forces a rebuild, never a hang).
+    Aborted communicators are never cached."""
+
+    def __init__(self, max_entries: int = 16):
+        self.max_entries = max_entries
+        self._d: "OrderedDict[tuple, Communicator]" = OrderedDict()
+        self._lock = threading.Lock()
+        self.hits = 0
+        self.misses = 0
+
+    def cid(self, key) -> str:
+        with self._lock:
+            c = self._d.get(key)
+            return getattr(c, "cid", "") if c is not None and c.alive else ""
+
+    def take(self, key):
+        with self._lock:
+            c = self._d.pop(key, None)
+            if c is not None:
+                self.hits += 1
+            return c
+
+    def put(self, comm) -> None:
+        key = getattr(comm, "cache_key", None)
+        if key is None or not getattr(comm, "cid", "") or not comm.alive:
+            _close(comm)
+            return
+        evicted = []
+        with self._lock:
+            old = self._d.pop(key, None)
+            if old is not None and old is not comm:
+                evicted.append(old)
+            self._d[key] = comm
+            while len(self._d) > self.max_entries:
+                evicted.append(self._d.popitem(last=False)[1])
+        for c in evicted:
+            _close(c)
+
+    def drop(self, key) -> None:
+        with self._lock:
+            c = self._d.pop(key, None)
+            if c is not None:
+                self.misses += 1
+        if c is not None:
+            _close(c)
+
+    def clear(self) -> None:
+        with self._lock:
+            items = list(self._d.values())
+            self._d.clear()
+        for c in items:
+            _close(c)
+
+    def __len__(self) -> int:
+        return len(self._d)
+
+
+def _close(comm) -> None:
+    try:
+        comm.destroy() if comm.alive else comm.abort()
+    except Exception:
+        pass
+
+
+COMM_CACHE = CommCache()

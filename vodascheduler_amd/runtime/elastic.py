@@ -31,7 +31,7 @@ from typing import Any, Callable
 
 import torch
 
-from ..parallel.comm import CommError, Communicator, create_communicator
+from ..parallel.comm import COMM_CACHE, CommError, Communicator, create_communicator
 from .rendezvous import JobRendezvous, connect_store
 
 log = logging.getLogger("vodascheduler_amd.elastic")
@@ -86,6 +86,7 @@ class ElasticContext:
         # after a failed collective only a NEWER epoch can be joined: the failed one still
         # lists the dead peer, and rebuilding its communicator would block until timeout
         self.min_epoch = 0
+        self.cache_comms = os.environ.get("VODA_COMM_CACHE", "1") != "0"
 
     # ---------------------------------------------------------------- watcher
     def start_watcher(self) -> None:
@@ -157,14 +158,22 @@ class ElasticContext:
         self.comm = create_communicator(self.rdzv.store, self.rdzv.comm_prefix(epoch), self.rank, self.size,
                                         self.device, self.backend, self.timeout,
                                         cancel=lambda: (self.rdzv.latest_epoch() > epoch
-                                                        or self.rdzv.outcome() is not None))
+                                                        or self.rdzv.outcome() is not None),
+                                        members=self.members if self.cache_comms else None)
         self.resize_log.append({"epoch": epoch, "world": self.size, "comm_init_s": time.perf_counter() - t0})
 
     def destroy_comm(self, abort: bool = False) -> None:
+        """Release the epoch's communicator: back into the per-process cache when it is
+        healthy (a later epoch or job on the same ordered GPUs reuses it), else abort it."""
         if self.comm is not None:
             try:
                 if abort or not self.comm.alive:
+                    key = getattr(self.comm, "cache_key", None)
                     self.comm.abort()
+                    if key is not None:
+                        COMM_CACHE.drop(key)
+                elif getattr(self.comm, "cache_key", None) is not None:
+                    COMM_CACHE.put(self.comm)
                 else:
                     self.comm.destroy()
             except Exception:
