@@ -9,3 +9,9 @@ RCCL over xGMI and hand-written CDNA4 HIP kernels.
 """
 __version__ = "0.3.0"
 NAME = "vodascheduler_amd"
+
+from .utils.miopen_db import configure as _configure_miopen  # noqa: E402
+
+# before any process of ours runs a convolution: share MIOpen's find-db / kernel cache
+if __import__("os").environ.get("VODA_MIOPEN_DIR", "") != "off":
+    _configure_miopen()
