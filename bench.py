@@ -116,6 +116,11 @@ def main():
     ap.add_argument("--out", default=None, help="also write the JSON line (+details) to this file")
     ap.add_argument("--device", default="cuda", choices=["cuda", "cpu"],
                     help="cpu: rehearse the multi-rank orchestration on gloo with tiny models (tests only)")
+    ap.add_argument("--comm-backend", default=None, choices=[None, "rccl", "gloo"],
+                    help="data-plane collectives (default: rccl on cuda, gloo on cpu)")
+    ap.add_argument("--share-gpu", action="store_true",
+                    help="rehearsal only: every rank uses cuda:0 (needs --comm-backend gloo; "
+                         "RCCL refuses two ranks on one GPU). Never a benchmark number")
     a = ap.parse_args()
     models, batch = (MODELS, BATCH) if a.device == "cuda" else (CPU_MODELS, CPU_BATCH)
 
@@ -124,8 +129,11 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != a.gpus:
         raise SystemExit(f"--gpus {a.gpus} but WORLD_SIZE={world}")
+    comm_backend = a.comm_backend or ("rccl" if a.device == "cuda" else "gloo")
+    if a.share_gpu and comm_backend != "gloo":
+        raise SystemExit("--share-gpu needs --comm-backend gloo")
     if a.device == "cuda":
-        device = torch.device("cuda", local)
+        device = torch.device("cuda", 0 if a.share_gpu else local)
         torch.cuda.set_device(device)
         _native.hip()  # the HIP extension must be present on a GPU box
     else:
@@ -144,7 +152,7 @@ def main():
     log(rank, f"warm-up: {a.warmup} steps x {models} on {world} {a.device} device(s)")
     step_ms = warmup(device, a.warmup, models, batch)
     if world > 1:
-        if a.device == "cuda":
+        if comm_backend == "rccl":
             comm = RcclCommunicator(store, "bench/warm", rank, world, device)
             x = torch.ones(16 << 20, device=device)
             comm.allreduce_(x, "sum")
@@ -178,7 +186,7 @@ def main():
 
         sched = threading.Thread(target=drive, name="control-plane", daemon=True)
         sched.start()
-    worker = PoolWorker(store, watch, f"node0:{rank}", device, backend="rccl" if a.device == "cuda" else "gloo",
+    worker = PoolWorker(store, watch, f"node0:{rank}", device, backend=comm_backend,
                         timeout=900)
     recs = worker.serve()
     if sched is not None:
@@ -225,12 +233,14 @@ def main():
             "vs_baseline": None,
             "dtype": "bf16" if a.device == "cuda" else "fp32",
             "data": "synthetic (random-init weights, synthetic batches of the real shapes)"
-                    + ("" if a.device == "cuda" else "; CPU/gloo orchestration rehearsal, not a benchmark"),
+                    + ("" if a.device == "cuda" else "; CPU/gloo orchestration rehearsal, not a benchmark")
+                    + ("; all ranks share cuda:0 over gloo: rehearsal, not a benchmark" if a.share_gpu else ""),
             "config": {
                 "model": "32-job Philly-style trace: ResNet-50 (ImageNet 224, bs256/GPU) + BERT-base (seq128, bs64/GPU)",
                 "global_batch": "per job: per-GPU batch x elastic workers",
                 "seq_len": 128,
-                "parallelism": f"elastic-dp, {a.algorithm}, <= {world} GPU(s)/job, RCCL over xGMI",
+                "parallelism": f"elastic-dp, {a.algorithm}, <= {world} GPU(s)/job, "
+                               + ("RCCL over xGMI" if comm_backend == "rccl" else "gloo"),
                 "algorithm": a.algorithm,
                 "jobs": len(trace),
             },

@@ -21,6 +21,7 @@ PYBIND11_MODULE(_vodahip, m) {
   m.def("rmsprop_step", &rmsprop_step);
   m.def("cast_scale", &cast_scale);
   m.def("multi_tensor_copy", &multi_tensor_copy);
+  m.def("adasum_combine", &adasum_combine);
   m.def("layernorm_fwd", &layernorm_fwd);
   m.def("layernorm_bwd", &layernorm_bwd);
   m.def("layernorm_bwd_partial_rows", &layernorm_bwd_partial_rows);

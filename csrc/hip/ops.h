@@ -30,6 +30,10 @@ void cast_scale(uintptr_t src, int src_dt, uintptr_t dst, int dst_dt, int64_t n,
 void multi_tensor_copy(const std::vector<uintptr_t>& srcs, const std::vector<uintptr_t>& dsts,
                        const std::vector<int64_t>& ns, int src_dt, int dst_dt, float scale, uintptr_t stream);
 
+// ---- Adasum segmented pairwise combine (adasum.hip) ----
+void adasum_combine(uintptr_t a, uintptr_t b, uintptr_t out, int dt, uintptr_t meta, int64_t nblk, int64_t nseg,
+                    uintptr_t partials, uintptr_t stream);
+
 // ---- LayerNorm (layernorm.hip) ----
 void layernorm_fwd(uintptr_t x, uintptr_t gamma, uintptr_t beta, uintptr_t y, uintptr_t mean, uintptr_t rstd,
                    int64_t M, int N, float eps, int dt, int wdt, uintptr_t stream);

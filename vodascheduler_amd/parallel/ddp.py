@@ -16,6 +16,9 @@ MI355X-first design:
 * averaging folds into the collective (RCCL ncclAvg) or, with ``compression='bf16'|'fp16'``
   (Horovod's fp16 compression), into the HIP cast kernel that packs the comm buffer
   (scale 1/N) -- halving xGMI bytes;
+* ``reduction='adasum'`` (Horovod ``op=hvd.Adasum``, pytorch_mnist_elastic.py:188) instead
+  all-gathers the bucket and runs the deterministic per-parameter Adasum tree of
+  ``ops/adasum.py`` on every rank (HIP segmented combine kernels);
 * ``finalize()`` flushes buckets whose parameters got no gradient this step (zeros) and makes
   the compute stream wait for the comm stream before the optimizer step.
 """
@@ -26,6 +29,7 @@ from dataclasses import dataclass
 
 import torch
 
+from ..ops.adasum import AdasumPlan, adasum_tree_
 from ..ops.bucket import cast_scale_
 from ..utils.flat import FlatGroup
 from .comm import Communicator, LocalCommunicator
@@ -42,6 +46,8 @@ class Bucket:
     pending: int = 0
     launched: bool = False
     comm_buf: torch.Tensor | None = None
+    segments: list[tuple[int, int]] | None = None   # per-parameter ranges, relative to start
+    plan: AdasumPlan | None = None
 
     @property
     def numel(self) -> int:
@@ -50,8 +56,11 @@ class Bucket:
 
 class ElasticDDP:
     def __init__(self, model: torch.nn.Module, comm: Communicator, optimizer=None, bucket_cap_mb: float = 64.0,
-                 first_bucket_mb: float = 8.0, compression: str | None = None):
+                 first_bucket_mb: float = 8.0, compression: str | None = None, reduction: str = "average"):
+        if reduction not in ("average", "adasum"):
+            raise ValueError(f"unknown reduction {reduction!r} (average | adasum)")
         self.model = model
+        self.reduction = reduction
         self.comm = comm
         self.optimizer = optimizer
         self.compress_dtype = _COMPRESS[compression]
@@ -109,7 +118,9 @@ class ElasticDDP:
         # extend to the padded end so the bucket slices tile the flat buffer exactly
         nxt = [g.slots[i].offset for i in range(len(g.params)) if g.slots[i].offset >= hi]
         hi = min(nxt) if nxt else g.numel
-        self.buckets.append(Bucket(gi, lo, hi, [g.params[i] for i in idxs]))
+        offs = sorted(g.slots[i].offset for i in idxs)
+        segs = [(o - lo, (offs[k + 1] if k + 1 < len(offs) else hi) - lo) for k, o in enumerate(offs)]
+        self.buckets.append(Bucket(gi, lo, hi, [g.params[i] for i in idxs], segments=segs))
 
     def bucket_sizes_mb(self) -> list[float]:
         return [b.numel * self.groups[b.group].grad.element_size() / 2 ** 20 for b in self.buckets]
@@ -147,7 +158,12 @@ class ElasticDDP:
         else:
             ctx = _nullctx()
         with ctx:
-            if self.compress_dtype is not None and flat.dtype != self.compress_dtype:
+            if self.reduction == "adasum":
+                if b.plan is None:
+                    b.plan = AdasumPlan(b.segments, flat.device)
+                gathered = self.comm.allgather(flat)          # [world, n]
+                flat.copy_(adasum_tree_(gathered, b.plan))
+            elif self.compress_dtype is not None and flat.dtype != self.compress_dtype:
                 if b.comm_buf is None:
                     b.comm_buf = torch.empty(b.numel, dtype=self.compress_dtype, device=flat.device)
                 cast_scale_(flat, b.comm_buf, 1.0 / self.world)

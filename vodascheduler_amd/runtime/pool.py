@@ -46,6 +46,9 @@ def job_train_config(job, defaults: dict | None = None) -> dict:
     if "lr" in wl:
         d["lr"] = float(wl["lr"])
     d.update(defaults or {})
+    for k in ("reduction", "compression"):  # the job's own choice beats the cluster default
+        if wl.get(k):
+            d[k] = wl[k]
     return d
 
 

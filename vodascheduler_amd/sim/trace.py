@@ -152,6 +152,11 @@ def workload_from_launcher(spec: dict) -> dict | None:
            "epoch_time_1gpu": spe * prof.step_time_1gpu}
     if "lr" in opts:
         out["lr"] = float(opts["lr"])
+    # boolean flags of the reference scripts (pytorch_mnist_elastic.py:32, cifar :145)
+    if "--use-adasum" in toks:
+        out["reduction"] = "adasum"
+    if "--fp16-allreduce" in toks:
+        out["compression"] = "fp16"
     return out
 
 

@@ -45,6 +45,7 @@ class TrainConfig:
     amp: bool = True                   # bf16 autocast
     compression: str | None = None     # gradient all-reduce compression: None | bf16 | fp16
     bucket_cap_mb: float = 64.0
+    reduction: str = "average"         # average | adasum (Horovod op=hvd.Adasum; LR not scaled by world)
     metrics_dir: str | None = None
     checkpoint_every_epoch: bool = False
     seed: int = 0
@@ -80,7 +81,7 @@ class _Warm:
                 b = tuple(t.to(memory_format=torch.channels_last) if t.dim() == 4 else t for t in b)
             self.pool.append(b)
         self.ddp = ElasticDDP(self.model, None, self.opt, bucket_cap_mb=cfg.bucket_cap_mb,
-                              compression=cfg.compression)
+                              compression=cfg.compression, reduction=cfg.reduction)
         self._init = [t.detach().clone() for t in self._tensors()]
 
     def _tensors(self):
@@ -101,7 +102,8 @@ WARM_CACHE_MAX = 4
 
 
 def _warm_key(cfg: TrainConfig, device: torch.device) -> tuple:
-    return (cfg.model, cfg.per_gpu_batch, cfg.lr, cfg.compression, cfg.bucket_cap_mb, cfg.seed, str(device))
+    return (cfg.model, cfg.per_gpu_batch, cfg.lr, cfg.compression, cfg.bucket_cap_mb, cfg.reduction, cfg.seed,
+            str(device))
 
 
 def get_warm(cfg: TrainConfig, device: torch.device, use_cache: bool = True) -> _Warm:
@@ -148,8 +150,9 @@ def train_elastic(ctx: ElasticContext, cfg: TrainConfig, use_cache: bool = True)
     def train(state):
         ddp.set_communicator(ctx.comm)
         world = ctx.size
+        lr_scaler = 1 if cfg.reduction == "adasum" else world  # Horovod examples: Adasum keeps the base LR
         for gr in opt.param_groups:
-            gr["lr"] = base_lr * world
+            gr["lr"] = base_lr * lr_scaler
         logger.set_params(world)
         # world 1: the whole step replays as one hipGraph (launch-bound models); collectives
         # of world > 1 stay eager.  Re-captured after every membership change.
@@ -204,6 +207,7 @@ def main(argv=None):
     ap.add_argument("--commit-every", type=int, default=1)
     ap.add_argument("--fp16-allreduce", action="store_true")
     ap.add_argument("--compression", default=None)
+    ap.add_argument("--use-adasum", action="store_true", help="Adasum gradient reduction instead of averaging")
     ap.add_argument("--metrics-dir", default=os.environ.get("VODA_METRICS_DIR"))
     ap.add_argument("--no-amp", action="store_true")
     a = ap.parse_args(argv)
@@ -219,7 +223,8 @@ def main(argv=None):
     ctx = ElasticContext(store, a.name, os.environ["VODA_WORKER_ID"], dev, watch_store=watch,
                          join_epoch=int(os.environ.get("VODA_JOIN_EPOCH", "0")))
     cfg = TrainConfig(a.model, a.epochs, a.steps_per_epoch, a.batch_size, a.lr, a.commit_every, not a.no_amp,
-                      "fp16" if a.fp16_allreduce else a.compression, metrics_dir=a.metrics_dir)
+                      "fp16" if a.fp16_allreduce else a.compression, metrics_dir=a.metrics_dir,
+                      reduction="adasum" if a.use_adasum else "average")
     out = train_elastic(ctx, cfg)
     log.info("worker %s finished job %s: %s", ctx.worker_id, a.name, out)
 
