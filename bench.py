@@ -114,6 +114,7 @@ def main():
     ap.add_argument("--compression", default=None, choices=[None, "bf16", "fp16"])
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--out", default=None, help="also write the JSON line (+details) to this file")
+    ap.add_argument("--trace", default=None, help="write the scheduler timeline (Chrome-trace JSON) here")
     ap.add_argument("--device", default="cuda", choices=["cuda", "cpu"],
                     help="cpu: rehearse the multi-rank orchestration on gloo with tiny models (tests only)")
     ap.add_argument("--comm-backend", default=None, choices=[None, "rccl", "gloo"],
@@ -179,7 +180,7 @@ def main():
             try:
                 result.update(run_trace(store, trace, locs, a.algorithm, rate_limit_sec=a.rate_limit,
                                         tick_sec=1.0, train_defaults=defaults, timeout=3000,
-                                        progress=lambda s: log(0, s)))
+                                        progress=lambda s: log(0, s), trace_path=a.trace))
             except BaseException as e:  # never leave the pool hanging
                 result["error"] = repr(e)
                 store.set("pool/shutdown", "1")

@@ -34,6 +34,11 @@ void multi_tensor_copy(const std::vector<uintptr_t>& srcs, const std::vector<uin
 void adasum_combine(uintptr_t a, uintptr_t b, uintptr_t out, int dt, uintptr_t meta, int64_t nblk, int64_t nseg,
                     uintptr_t partials, uintptr_t stream);
 
+// ---- Linear weight-gradient GEMM + fused bias gradient, split-K MFMA (wgrad.hip) ----
+int64_t wgrad_workspace_floats(int M, int N, int K, int splits);
+void wgrad_gemm(uintptr_t dy, int64_t ldy, uintptr_t x, int64_t ldx, uintptr_t dw, int64_t ldw, uintptr_t db, int M,
+                int N, int K, int splits, uintptr_t ws, bool accumulate, uintptr_t stream);
+
 // ---- LayerNorm (layernorm.hip) ----
 void layernorm_fwd(uintptr_t x, uintptr_t gamma, uintptr_t beta, uintptr_t y, uintptr_t mean, uintptr_t rstd,
                    int64_t M, int N, float eps, int dt, int wdt, uintptr_t stream);

@@ -1,0 +1,320 @@
+// Weight-gradient GEMM of Linear layers on CDNA4 MFMA (gfx950), bias gradient fused.
+//
+//   dW[N][K] (+)= dY[M][N]^T . X[M][K]        db[N] (+)= sum_m dY[m][N]
+//
+// hipBLASLt runs these "reduction = tokens" GEMMs at 190-490 TFLOP/s on BERT-base (M = 8192
+// tokens, N, K in {768, 2304, 3072}; profiles/): a 768 x 768 weight is only 36 output tiles
+// of 128 x 128 on 256 CUs.  Design:
+//  * split-K over the token dimension so the grid covers the chip; each split writes an fp32
+//    partial slab and a reduce kernel sums the slabs and accumulates into the optimizer's
+//    flat bf16 gradient (beta = 1).  With one split the GEMM epilogue accumulates directly.
+//  * both operands are row-major with the REDUCTION dimension as rows, so a 64-token x
+//    128-column tile is staged into LDS as-is (16-byte global loads, XOR-swizzled 256-byte
+//    rows) and the MFMA fragments -- 8 consecutive tokens of one column per lane -- come out
+//    of the gfx950 transposing LDS read ds_read_b64_tr_b16 (guide T10, layout (b)); no
+//    transpose pass anywhere.
+//  * v_mfma_f32_32x32x16_bf16; 4 waves as 2 x 2, each wave a 64 x 64 sub-tile (2 x 2 MFMA
+//    tiles, 64 fp32 accumulators per lane).  LDS double-buffered with register staging: the
+//    loads of stage s+1 are issued before the MFMAs of stage s and written after them.
+//  * XCD-aware block remap (guide T1): consecutive logical blocks -- the splits of one tile,
+//    then neighbouring tiles that share operand panels -- land on the same XCD / L2.
+//  * the bias gradient rides along: in workgroups of output-column block 0 the waves of
+//    column half 0 also multiply their dY fragments by a ones operand (one extra MFMA per
+//    dY fragment), which is sum_m dY[m][n] in fp32 with no second pass over dY.
+#include "common.h"
+#include "ops.h"
+
+namespace voda {
+
+namespace {
+
+typedef __bf16 wg_bf16x8 __attribute__((ext_vector_type(8)));
+typedef float wg_f32x16 __attribute__((ext_vector_type(16)));
+typedef __bf16 wg_bf16x4_v __attribute__((__vector_size__(4 * sizeof(__bf16))));
+typedef __attribute__((address_space(3))) wg_bf16x4_v wg_lds_bf16x4;
+
+constexpr int kWgBN = 128;                          // output rows (n) per workgroup
+constexpr int kWgBK = 128;                          // output cols (k) per workgroup
+constexpr int kWgBM = 64;                           // tokens per LDS stage
+constexpr int kWgThreads = 256;
+constexpr int kWgRowBytes = 256;                    // 128 bf16 per LDS row
+constexpr int kWgTileBytes = kWgBM * kWgRowBytes;   // 16 KB per operand tile
+
+struct WgradArgs {
+  const uint16_t* dy; int64_t ldy;   // [M][N]
+  const uint16_t* x; int64_t ldx;    // [M][K]
+  uint16_t* dw; int64_t ldw;         // [N][K]        (splits == 1)
+  uint16_t* db;                      // [N] or null   (splits == 1)
+  float* ws;                         // [S][N][K] + [S][N] partial slabs (splits > 1)
+  int M, N, K, S, m_split, tiles_k, remap, accumulate, bias;
+};
+
+// byte offset of 16-byte chunk ``ch`` (0..15) of LDS row ``r``: XOR swizzle that keeps both
+// the 16-B row writes and the 32x32x16 transposed reads conflict-free (guide T10 (b))
+__device__ __forceinline__ int wg_swz(int r, int ch) {
+  return r * kWgRowBytes + 16 * (ch ^ (((r & 3) << 2) | ((r >> 2) & 3)));
+}
+
+__device__ __forceinline__ uint2 wg_tr_read(const uint8_t* base, int off) {
+  wg_bf16x4_v v = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((wg_lds_bf16x4*)(base + off));
+  return __builtin_bit_cast(uint2, v);
+}
+
+// MFMA operand: 8 consecutive tokens (rows r .. r+3 and r+4 .. r+7 of the tile) of the column
+// this lane receives; ``ch``/``bo`` address the lane's 4-column piece (guide T10 mechanism).
+__device__ __forceinline__ wg_bf16x8 wg_frag(const uint8_t* tile, int r, int ch, int bo) {
+  const uint2 lo = wg_tr_read(tile, wg_swz(r, ch) + bo);
+  const uint2 hi = wg_tr_read(tile, wg_swz(r + 4, ch) + bo);
+  return __builtin_bit_cast(wg_bf16x8, make_uint4(lo.x, lo.y, hi.x, hi.y));
+}
+
+// v if keep else 0, as lane-wise ANDs (a struct select here becomes a scratch round trip)
+__device__ __forceinline__ uint4 wg_keep(uint4 v, bool keep) {
+  const uint32_t m = keep ? 0xffffffffu : 0u;
+  return make_uint4(v.x & m, v.y & m, v.z & m, v.w & m);
+}
+
+__device__ __forceinline__ wg_f32x16 wg_mfma(wg_bf16x8 a, wg_bf16x8 b, wg_f32x16 c) {
+  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+}
+
+__global__ __launch_bounds__(kWgThreads, 2) void wgrad_kernel(WgradArgs p) {
+  __shared__ __attribute__((aligned(16))) uint8_t smem[4 * kWgTileBytes];  // [buffer][dY | X]
+
+  int bid = blockIdx.x;
+  if (p.remap) bid = (bid & 7) * int(gridDim.x >> 3) + (bid >> 3);
+  const int split = bid % p.S;
+  const int tile = bid / p.S;
+  const int n0 = (tile / p.tiles_k) * kWgBN;
+  const int k0 = (tile % p.tiles_k) * kWgBK;
+  const int mb = split * p.m_split;
+  const int me = min(p.M, mb + p.m_split);
+  const int nst = me > mb ? (me - mb + kWgBM - 1) / kWgBM : 0;
+
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const int wn = wave >> 1, wk = wave & 1;
+  const bool do_bias = __builtin_amdgcn_readfirstlane(p.bias && k0 == 0 && wk == 0);  // wave-uniform
+
+  // ---- global -> register staging: thread t moves chunks idx = t + 256 i (row idx>>4, chunk idx&15).
+  // Out-of-range chunks load from a clamped address and are zeroed at the LDS write, after the
+  // MFMAs: masking right after the load would make hipcc wait for every load before the MFMAs.
+  uint4 ra[4], rb[4];
+  uint32_t keep = 0;  // bit i: chunk i of dY in range, bit 4+i: chunk i of X in range
+  auto gload = [&](int st) {
+    const int m_base = mb + st * kWgBM;
+    keep = 0;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int idx = t + kWgThreads * i;
+      const int r = idx >> 4, ch = idx & 15;
+      const int m = m_base + r;
+      const int mc = min(m, p.M - 1);
+      const int na = n0 + ch * 8, kb = k0 + ch * 8;
+      ra[i] = *reinterpret_cast<const uint4*>(p.dy + int64_t(mc) * p.ldy + min(na, p.N - 8));
+      rb[i] = *reinterpret_cast<const uint4*>(p.x + int64_t(mc) * p.ldx + min(kb, p.K - 8));
+      const bool okm = m < me;
+      keep |= (uint32_t(okm && na < p.N) << i) | (uint32_t(okm && kb < p.K) << (4 + i));
+    }
+  };
+  auto swrite = [&](int buf) {
+    uint8_t* A = smem + buf * 2 * kWgTileBytes;
+    uint8_t* B = A + kWgTileBytes;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int idx = t + kWgThreads * i;
+      const int off = wg_swz(idx >> 4, idx & 15);
+      *reinterpret_cast<uint4*>(A + off) = wg_keep(ra[i], (keep >> i) & 1);
+      *reinterpret_cast<uint4*>(B + off) = wg_keep(rb[i], (keep >> (4 + i)) & 1);
+    }
+  };
+
+  wg_f32x16 c00, c01, c10, c11, cb0, cb1;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    c00[i] = 0.f; c01[i] = 0.f; c10[i] = 0.f; c11[i] = 0.f; cb0[i] = 0.f; cb1[i] = 0.f;
+  }
+  wg_bf16x8 ones;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) ones[j] = static_cast<__bf16>(1.0f);
+
+  // lane-constant parts of the transposed-read addresses (guide T10: lane 4q+p of a 16-lane
+  // group reads row q of the block, columns 4p..4p+3; lane i of the group gets column i)
+  const int g = lane >> 4, i16 = lane & 15, q = i16 >> 2, pp = i16 & 3, h = lane >> 5;
+  const int bo = 8 * (pp & 1);
+  const int chA = ((wn * 64 + 16 * (g & 1)) >> 3) + (pp >> 1);  // sub-tile 1: +4 chunks (32 columns)
+  const int chB = ((wk * 64 + 16 * (g & 1)) >> 3) + (pp >> 1);
+
+  if (nst > 0) {
+    gload(0);
+    swrite(0);
+  }
+  __syncthreads();
+  for (int st = 0; st < nst; ++st) {
+    const uint8_t* A = smem + (st & 1) * 2 * kWgTileBytes;
+    const uint8_t* B = A + kWgTileBytes;
+    if (st + 1 < nst) gload(st + 1);
+    // fragments of k-step kk+1 are read while the MFMAs of k-step kk run
+    wg_bf16x8 a0, a1, b0, b1;
+    {
+      const int r = 8 * h + q;
+      a0 = wg_frag(A, r, chA, bo); a1 = wg_frag(A, r, chA + 4, bo);
+      b0 = wg_frag(B, r, chB, bo); b1 = wg_frag(B, r, chB + 4, bo);
+    }
+#pragma unroll
+    for (int kk = 0; kk < kWgBM / 16; ++kk) {
+      wg_bf16x8 na0 = a0, na1 = a1, nb0 = b0, nb1 = b1;
+      if (kk + 1 < kWgBM / 16) {
+        const int r = 16 * (kk + 1) + 8 * h + q;
+        na0 = wg_frag(A, r, chA, bo); na1 = wg_frag(A, r, chA + 4, bo);
+        nb0 = wg_frag(B, r, chB, bo); nb1 = wg_frag(B, r, chB + 4, bo);
+      }
+      c00 = wg_mfma(a0, b0, c00);
+      c01 = wg_mfma(a0, b1, c01);
+      c10 = wg_mfma(a1, b0, c10);
+      c11 = wg_mfma(a1, b1, c11);
+      if (do_bias) {
+        cb0 = wg_mfma(a0, ones, cb0);
+        cb1 = wg_mfma(a1, ones, cb1);
+      }
+      a0 = na0; a1 = na1; b0 = nb0; b1 = nb1;
+    }
+    if (st + 1 < nst) swrite((st + 1) & 1);
+    __syncthreads();
+  }
+
+  // ---- epilogue: C/D lane map col = lane & 31, row = (reg&3) + 8*(reg>>2) + 4*h
+  const int col_l = lane & 31;
+  auto store_tile = [&](const wg_f32x16& acc, int rbase, int cbase) {
+    const int col = cbase + col_l;
+    if (col >= p.K) return;
+#pragma unroll
+    for (int reg = 0; reg < 16; ++reg) {
+      const int row = rbase + (reg & 3) + 8 * (reg >> 2) + 4 * h;
+      if (row < p.N) {
+        if (p.S == 1) {
+          uint16_t* o = p.dw + int64_t(row) * p.ldw + col;
+          const float v = acc[reg] + (p.accumulate ? bf2f(*o) : 0.f);
+          *o = f2bf(v);
+        } else {
+          p.ws[(int64_t(split) * p.N + row) * p.K + col] = acc[reg];
+        }
+      }
+    }
+  };
+  const int rb0 = n0 + wn * 64, cb0i = k0 + wk * 64;
+  store_tile(c00, rb0, cb0i);
+  store_tile(c01, rb0, cb0i + 32);
+  store_tile(c10, rb0 + 32, cb0i);
+  store_tile(c11, rb0 + 32, cb0i + 32);
+  if (do_bias && col_l == 0) {  // every column of cb holds the row sums; lanes 0 and 32 write
+    float* wsb = p.ws + int64_t(p.S) * p.N * p.K + int64_t(split) * p.N;
+    auto store_bias = [&](const wg_f32x16& acc, int rbase) {
+#pragma unroll
+      for (int reg = 0; reg < 16; ++reg) {
+        const int row = rbase + (reg & 3) + 8 * (reg >> 2) + 4 * h;
+        if (row < p.N) {
+          if (p.S == 1) {
+            const float v = acc[reg] + (p.accumulate ? bf2f(p.db[row]) : 0.f);
+            p.db[row] = f2bf(v);
+          } else {
+            wsb[row] = acc[reg];
+          }
+        }
+      }
+    };
+    store_bias(cb0, rb0);
+    store_bias(cb1, rb0 + 32);
+  }
+}
+
+// dW[n][k] (+)= sum_s ws[s][n][k]; db[n] (+)= sum_s wsb[s][n].  4 columns per thread (K % 8 == 0).
+__global__ __launch_bounds__(256) void wgrad_reduce_kernel(const float* __restrict__ ws, int S, int N, int K,
+                                                           uint16_t* __restrict__ dw, int64_t ldw,
+                                                           uint16_t* __restrict__ db, int accumulate) {
+  const int64_t NK = int64_t(N) * K;
+  const int64_t n4 = NK >> 2;
+  const int64_t total = n4 + (db != nullptr ? N : 0);
+  const int64_t stride = int64_t(gridDim.x) * blockDim.x;
+  for (int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < total; i += stride) {
+    if (i < n4) {
+      float4 s = reinterpret_cast<const float4*>(ws)[i];
+      for (int sp = 1; sp < S; ++sp) {
+        const float4 v = reinterpret_cast<const float4*>(ws + int64_t(sp) * NK)[i];
+        s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
+      }
+      const int64_t e = i << 2;
+      const int64_t row = e / K, col = e - row * K;
+      uint2* o = reinterpret_cast<uint2*>(dw + row * ldw + col);
+      if (accumulate) {
+        const uint2 u = *o;
+        s.x += bf2f(u.x & 0xffff); s.y += bf2f(u.x >> 16); s.z += bf2f(u.y & 0xffff); s.w += bf2f(u.y >> 16);
+      }
+      uint2 r;
+      r.x = uint32_t(f2bf(s.x)) | (uint32_t(f2bf(s.y)) << 16);
+      r.y = uint32_t(f2bf(s.z)) | (uint32_t(f2bf(s.w)) << 16);
+      *o = r;
+    } else {
+      const int64_t n = i - n4;
+      const float* wsb = ws + int64_t(S) * NK;
+      float s = 0.f;
+      for (int sp = 0; sp < S; ++sp) s += wsb[int64_t(sp) * N + n];
+      if (accumulate) s += bf2f(db[n]);
+      db[n] = f2bf(s);
+    }
+  }
+}
+
+struct WgradPlan {
+  int S, m_split, tiles_k, grid;
+};
+
+WgradPlan wgrad_plan(int M, int N, int K, int splits) {
+  WgradPlan pl;
+  const int tiles_n = (N + kWgBN - 1) / kWgBN;
+  pl.tiles_k = (K + kWgBK - 1) / kWgBK;
+  int S = std::max(1, splits);
+  const int per = (M + S - 1) / S;
+  pl.m_split = std::max(kWgBM, (per + kWgBM - 1) / kWgBM * kWgBM);
+  pl.S = (M + pl.m_split - 1) / pl.m_split;  // no empty splits
+  pl.grid = tiles_n * pl.tiles_k * pl.S;
+  return pl;
+}
+
+}  // namespace
+
+int64_t wgrad_workspace_floats(int M, int N, int K, int splits) {
+  const WgradPlan pl = wgrad_plan(M, N, K, splits);
+  return pl.S > 1 ? int64_t(pl.S) * (int64_t(N) * K + N) : 0;
+}
+
+void wgrad_gemm(uintptr_t dy, int64_t ldy, uintptr_t x, int64_t ldx, uintptr_t dw, int64_t ldw, uintptr_t db, int M,
+                int N, int K, int splits, uintptr_t ws, bool accumulate, uintptr_t stream) {
+  VODA_CHECK(M > 0 && N >= 8 && K >= 8, "wgrad: empty problem");
+  VODA_CHECK(N % 8 == 0 && K % 8 == 0, "wgrad: N and K must be multiples of 8");
+  VODA_CHECK(ldy >= N && ldx >= K && ldw >= K, "wgrad: leading dimension too small");
+  VODA_CHECK(ldy % 8 == 0 && ldx % 8 == 0 && ldw % 8 == 0, "wgrad: rows must be 16-byte aligned");
+  VODA_CHECK(dy % 16 == 0 && x % 16 == 0 && dw % 16 == 0, "wgrad: operands must be 16-byte aligned");
+  const WgradPlan pl = wgrad_plan(M, N, K, splits);
+  VODA_CHECK(pl.S == 1 || ws != 0, "wgrad: split-K needs a workspace");
+  WgradArgs a;
+  a.dy = reinterpret_cast<const uint16_t*>(dy); a.ldy = ldy;
+  a.x = reinterpret_cast<const uint16_t*>(x); a.ldx = ldx;
+  a.dw = reinterpret_cast<uint16_t*>(dw); a.ldw = ldw;
+  a.db = reinterpret_cast<uint16_t*>(db);
+  a.ws = reinterpret_cast<float*>(ws);
+  a.M = M; a.N = N; a.K = K; a.S = pl.S; a.m_split = pl.m_split; a.tiles_k = pl.tiles_k;
+  a.remap = (pl.grid % 8 == 0) ? 1 : 0;
+  a.accumulate = accumulate ? 1 : 0;
+  a.bias = db != 0 ? 1 : 0;
+  hipStream_t s = as_stream(stream);
+  hipLaunchKernelGGL(wgrad_kernel, dim3(unsigned(pl.grid)), dim3(kWgThreads), 0, s, a);
+  check_launch();
+  if (pl.S > 1) {
+    const int64_t work = (int64_t(N) * K) / 4 + (db != 0 ? N : 0);
+    hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(stream_grid(work)), dim3(256), 0, s, a.ws, pl.S, N, K, a.dw, ldw,
+                       a.db, a.accumulate);
+    check_launch();
+  }
+}
+
+}  // namespace voda

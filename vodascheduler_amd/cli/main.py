@@ -3,6 +3,7 @@
     vodascheduler create -f job.yaml              POST  <service>/training   (raw YAML body)
     vodascheduler delete NAME [NAME ...]          DELETE <service>/training  (JSON string body, per name)
     vodascheduler get jobs                        GET   <scheduler>/training (status table)
+    vodascheduler get trace                       GET   <scheduler>/trace    (Chrome-trace JSON timeline)
     vodascheduler set algorithm ElasticTiresias   PUT   <scheduler>/algorithm
     vodascheduler set ratelimit 30                PUT   <scheduler>/ratelimit
     vodascheduler up [--gpus 0,1,...]             all-in-one: service + scheduler + allocator + node agent
@@ -54,8 +55,10 @@ def cmd_delete(a) -> int:
 
 
 def cmd_get(a) -> int:
+    if a.what == "trace":
+        return _out(*http_request("GET", _scheduler(a) + "/trace"))
     if a.what not in ("jobs", "job", "training"):
-        print(f"unknown resource {a.what!r}; try: get jobs", file=sys.stderr)
+        print(f"unknown resource {a.what!r}; try: get jobs | get trace", file=sys.stderr)
         return 2
     return _out(*http_request("GET", _scheduler(a) + ENTRY_POINT))
 
@@ -120,7 +123,8 @@ def cmd_simulate(a) -> int:
     trace = philly_trace(a.jobs, seed=a.seed, mean_interarrival_s=a.interarrival)
     algos = a.algorithm.split(",")
     for algo in algos:
-        r = simulate(trace, algorithm=algo, gpus=a.gpus, rate_limit_sec=a.rate_limit)
+        tp = a.trace.replace("{algorithm}", algo) if a.trace else None
+        r = simulate(trace, algorithm=algo, gpus=a.gpus, rate_limit_sec=a.rate_limit, trace_path=tp)
         print(r.to_json(), flush=True)
     return 0
 
@@ -171,6 +175,7 @@ def build_parser() -> argparse.ArgumentParser:
     p.add_argument("--rate-limit", type=float, default=30.0)
     p.add_argument("--interarrival", type=float, default=30.0)
     p.add_argument("--seed", type=int, default=0)
+    p.add_argument("--trace", default=None, help="Chrome-trace JSON of each run ({algorithm} is substituted)")
     p.set_defaults(fn=cmd_simulate)
 
     p = sub.add_parser("version", help="print the version")

@@ -9,13 +9,23 @@ buffer (marked ``_voda_flat_grad``), the backward accumulates in place -- ``grad
 (one GEMM with beta = 1) and the HIP column-sum kernel -- and then signals the
 data-parallel engine's readiness hook (``_voda_grad_ready``) itself, exactly as autograd's
 post-accumulate hook would.  Otherwise it returns ordinary gradients.
+
+On GPU the in-place weight gradient (and the bias gradient with it) is the split-K MFMA
+kernel of ``ops/wgrad.py`` (csrc/hip/wgrad.hip): the "reduction over tokens" GEMMs are
+too narrow for hipBLASLt to fill 256 CUs.  ``USE_WGRAD_KERNEL = False`` (or
+``VODA_WGRAD=0``) switches back to ``addmm_`` + the column-sum kernel.
 """
 from __future__ import annotations
+
+import os
 
 import torch
 import torch.nn.functional as F
 
 from . import _native as N
+from . import wgrad as W
+
+USE_WGRAD_KERNEL = os.environ.get("VODA_WGRAD", "1") != "0"
 
 
 def _direct(p: torch.Tensor | None) -> bool:
@@ -69,13 +79,22 @@ class _DenseFn(torch.autograd.Function):
         dx = dw = db = None
         if ctx.needs_input_grad[0]:
             dx = (dy2 @ weight).view(x.shape)
-        if ctx.needs_input_grad[1]:
+        need_w, need_b = ctx.needs_input_grad[1], bias is not None and ctx.needs_input_grad[2]
+        fused = (USE_WGRAD_KERNEL and need_w and _direct(weight) and (not need_b or _direct(bias))
+                 and W.supported(dy2, x2, weight.grad, bias.grad if need_b else None))
+        if fused:
+            W.wgrad_accumulate_(dy2, x2, weight.grad, bias.grad if need_b else None)
+            _ready(weight)
+            if need_b:
+                _ready(bias)
+            return dx, None, None
+        if need_w:
             if _direct(weight):
                 weight.grad.addmm_(dy2.t(), x2)
                 _ready(weight)
             else:
                 dw = dy2.t() @ x2
-        if bias is not None and ctx.needs_input_grad[2]:
+        if need_b:
             if _direct(bias):
                 colsum_accumulate_(dy2, bias.grad)
                 _ready(bias)

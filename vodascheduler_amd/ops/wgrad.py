@@ -1,0 +1,83 @@
+"""Linear-layer weight gradient (+ fused bias gradient) on the split-K MFMA kernel of
+csrc/hip/wgrad.hip, with the fp32 PyTorch reference of the same op.
+
+    dW (+)= dY^T X        db (+)= dY.sum(0)        dY [M, N], X [M, K], dW [N, K], db [N]
+
+These are the "reduction over tokens" GEMMs of every Linear backward (BERT-base: M = 8192
+tokens); ``ops/dense.py`` routes them here when the layer accumulates straight into the
+optimizer's flat bf16 gradient buffer.
+"""
+from __future__ import annotations
+
+import math
+
+import torch
+
+from . import _native as N
+
+TILE = 128
+
+
+def default_splits(M: int, N_: int, K: int, target_blocks: int = 256) -> int:
+    """Split the token dimension until the grid covers the 256 CUs once (>= 8 k-stages of 64
+    tokens per split, at most 16 splits)."""
+    tiles = math.ceil(N_ / TILE) * math.ceil(K / TILE)
+    s = math.ceil(target_blocks / tiles)
+    return max(1, min(s, 16, M // 512 if M >= 512 else 1))
+
+
+def supported(dy2: torch.Tensor, x2: torch.Tensor, gw: torch.Tensor, gb: torch.Tensor | None = None) -> bool:
+    """True when the HIP kernel can run these operands (bf16, 16-byte aligned rows)."""
+    if not (dy2.is_cuda and x2.is_cuda and gw.is_cuda):
+        return False
+    if dy2.dtype != torch.bfloat16 or x2.dtype != torch.bfloat16 or gw.dtype != torch.bfloat16:
+        return False
+    if dy2.dim() != 2 or x2.dim() != 2 or gw.dim() != 2:
+        return False
+    M, N_ = dy2.shape
+    K = x2.shape[1]
+    if x2.shape[0] != M or tuple(gw.shape) != (N_, K) or M == 0 or N_ % 8 or K % 8:
+        return False
+    if dy2.stride(1) != 1 or x2.stride(1) != 1 or gw.stride(1) != 1:
+        return False
+    if dy2.stride(0) % 8 or x2.stride(0) % 8 or gw.stride(0) % 8:
+        return False
+    if dy2.data_ptr() % 16 or x2.data_ptr() % 16 or gw.data_ptr() % 16:
+        return False
+    if gb is not None and (gb.dtype != torch.bfloat16 or not gb.is_contiguous() or gb.numel() != N_):
+        return False
+    return True
+
+
+def wgrad_ref(dy2: torch.Tensor, x2: torch.Tensor, gw: torch.Tensor, gb: torch.Tensor | None = None,
+              accumulate: bool = True) -> tuple[torch.Tensor, torch.Tensor | None]:
+    """fp32 reference: returns the new (dW, db) in fp32 without touching the inputs."""
+    w = dy2.float().t() @ x2.float()
+    b = dy2.float().sum(0) if gb is not None else None
+    if accumulate:
+        w = w + gw.float()
+        if b is not None:
+            b = b + gb.float()
+    return w, b
+
+
+def wgrad_accumulate_(dy2: torch.Tensor, x2: torch.Tensor, gw: torch.Tensor, gb: torch.Tensor | None = None,
+                      accumulate: bool = True, splits: int | None = None) -> None:
+    """``gw (+)= dy2^T x2`` and ``gb (+)= dy2.sum(0)`` in place (fp32 accumulation, one rounding)."""
+    if not dy2.is_cuda:
+        w, b = wgrad_ref(dy2, x2, gw, gb, accumulate)
+        gw.copy_(w.to(gw.dtype))
+        if gb is not None:
+            gb.copy_(b.to(gb.dtype))
+        return
+    if not supported(dy2, x2, gw, gb):
+        raise ValueError(f"wgrad: unsupported operands dy {tuple(dy2.shape)} {dy2.dtype} stride {dy2.stride()}, "
+                         f"x {tuple(x2.shape)} {x2.dtype} stride {x2.stride()}, dw {tuple(gw.shape)} {gw.dtype}")
+    M, N_ = dy2.shape
+    K = x2.shape[1]
+    s = splits if splits is not None else default_splits(M, N_, K)
+    h = N.hip()
+    nws = h.wgrad_workspace_floats(M, N_, K, s)
+    ws = torch.empty(nws, dtype=torch.float32, device=dy2.device) if nws else None
+    h.wgrad_gemm(dy2.data_ptr(), dy2.stride(0), x2.data_ptr(), x2.stride(0), gw.data_ptr(), gw.stride(0),
+                 N.ptr(gb), M, N_, K, s, N.ptr(ws), bool(accumulate), N.stream_of(dy2))

@@ -169,7 +169,13 @@ class RcclCommunicator(Communicator):
         self._c.abort()
 
     def destroy(self):
-        self._c.destroy()
+        # ncclCommFinalize completes only when the communicator is GLOBALLY quiescent
+        # (rccl.h), i.e. when every peer finalizes too.  Members tear communicators down at
+        # different times -- the per-process CommCache evicts by its own LRU, a member that
+        # left a job drops its copy later -- so a finalize here could block until the peers
+        # reach theirs, or until the timeout.  Abort is local and never waits for peers; an
+        # idle communicator has nothing in flight to lose.
+        self._c.abort()
 
     @property
     def alive(self):

@@ -37,7 +37,7 @@ def free_port() -> int:
 def run_trace(store, trace: list[TraceJob], worker_locs, algorithm: str = "ElasticFIFO",
               rate_limit_sec: float = 1.0, tick_sec: float = 1.0, train_defaults: dict | None = None,
               timeout: float = 3600.0, gpu_type: str = DEFAULT_GPU_TYPE, progress=None,
-              collect_every_s: float = 2.0) -> dict:
+              collect_every_s: float = 2.0, trace_path: str | None = None) -> dict:
     """Submit ``trace`` in real time (``submit_time`` seconds after start) and wait until every
     job completed.  Returns JCT / makespan / resize-latency statistics."""
     db = MemoryStore()
@@ -46,6 +46,11 @@ def run_trace(store, trace: list[TraceJob], worker_locs, algorithm: str = "Elast
     backend = PoolBackend(store, worker_locs, train_defaults)
     core = SchedulerCore(gpu_type, db, ResourceAllocator(db), backend, algorithm=algorithm,
                          rate_limit_sec=rate_limit_sec, tick_sec=tick_sec)
+    tracer = None
+    if trace_path:
+        from ..utils.tracing import SchedulerTracer
+
+        tracer = SchedulerTracer(core)
     runner = SchedulerRunner(core, mq).start()
     collector = None
     mdir = (train_defaults or {}).get("metrics_dir")
@@ -81,6 +86,8 @@ def run_trace(store, trace: list[TraceJob], worker_locs, algorithm: str = "Elast
     finally:
         runner.stop()
         backend.shutdown()
+        if tracer is not None:
+            tracer.save(trace_path)
     failed = [n for n, j in jobs.items() if j.status != JobStatus.COMPLETED.value]
     jct = {n: j.finish_timestamp - j.submit_timestamp for n, j in jobs.items()}
     lat = sorted(r["latency_s"] for r in backend.resize_latency)

@@ -32,6 +32,7 @@ from typing import Any, Callable
 import torch
 
 from ..parallel.comm import COMM_CACHE, CommError, Communicator, create_communicator
+from ..utils.tracing import trace_range
 from .rendezvous import JobRendezvous, connect_store
 
 log = logging.getLogger("vodascheduler_amd.elastic")
@@ -308,8 +309,9 @@ class State:
 
     def commit(self) -> None:
         """Snapshot + agree on membership; raises HostsUpdatedInterrupt when it changed."""
-        self.save()
-        self.check_host_updates()
+        with trace_range("commit", "elastic"):
+            self.save()
+            self.check_host_updates()
 
     def check_host_updates(self) -> None:
         e = self.ctx.agree_on_epoch()
@@ -455,8 +457,10 @@ def run(func: Callable) -> Callable:
                 _leave(state, e)
                 return None
             try:
-                ctx.join(e)
-                state.sync()
+                with trace_range("comm_bootstrap", "elastic", job=ctx.job, epoch=e):
+                    ctx.join(e)
+                with trace_range("state_sync", "elastic", job=ctx.job, epoch=e, world=ctx.size):
+                    state.sync()
             except CommError as err:  # superseded / peer lost during bootstrap or sync
                 log.warning("%s/%s: epoch %d not established (%s); waiting for a newer one", ctx.job,
                             ctx.worker_id, e, err)

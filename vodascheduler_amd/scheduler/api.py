@@ -1,7 +1,9 @@
 """Scheduler REST API on :55588 (reference scheduler.go:256-261,1127-1183; doc/apis.md).
 
 ``GET /training`` status table, ``PUT /algorithm`` (JSON string), ``PUT /ratelimit`` (JSON
-int seconds), ``GET /metrics``.  Every call is executed on the scheduler thread.
+int seconds), ``GET /metrics``; plus ``GET /trace``: the scheduler timeline as Chrome-trace
+JSON (utils/tracing.py; no reference counterpart).  Every call is executed on the scheduler
+thread.
 """
 from __future__ import annotations
 
@@ -13,7 +15,7 @@ from ..utils.http import Router, text
 from .runner import SchedulerRunner
 
 
-def scheduler_router(runner: SchedulerRunner) -> Router:
+def scheduler_router(runner: SchedulerRunner, tracer=None) -> Router:
     core = runner.core
     r = Router()
 
@@ -50,5 +52,11 @@ def scheduler_router(runner: SchedulerRunner) -> Router:
     r.add("GET", ENTRY_POINT, get_jobs)
     r.add("PUT", "/algorithm", put_algorithm)
     r.add("PUT", "/ratelimit", put_ratelimit)
+    def trace(_b, _q):
+        if tracer is None:
+            return text(404, "tracing is not enabled on this scheduler\n")
+        return 200, "application/json", runner.call(tracer.to_json).encode()
+
     r.add("GET", "/metrics", metrics)
+    r.add("GET", "/trace", trace)
     return r

@@ -11,7 +11,7 @@ runs in-process.  Backends: ``local`` (node agent + warm per-GPU workers, the MI
 path), ``k8s`` (MPIJob CRD + pod tolerations on a Kubernetes cluster, the reference's
 deployment model) and ``null`` (record actions only; the virtual-time cluster lives in
 ``vodascheduler simulate``).  REST on :55588:
-``GET /training``, ``PUT /algorithm``, ``PUT /ratelimit``, ``GET /metrics``.
+``GET /training``, ``PUT /algorithm``, ``PUT /ratelimit``, ``GET /metrics``, ``GET /trace``.
 """
 from __future__ import annotations
 
@@ -109,6 +109,9 @@ class SchedulerProcess:
         self.core = SchedulerCore(a.gpu_type, self.store, alloc, self.backend, algorithm=a.algorithm,
                                   rate_limit_sec=a.rate_limit, tick_sec=a.tick, resume=a.resume,
                                   use_placement=not a.no_placement, work_conserving=not a.strict_rate_limit)
+        from ..utils.tracing import SchedulerTracer
+
+        self.tracer = SchedulerTracer(self.core)
         self.runner = SchedulerRunner(self.core, self.mq, queue_name=a.gpu_type)
         self.http: HttpServer | None = None
         self._collector_stop = threading.Event()
@@ -121,7 +124,8 @@ class SchedulerProcess:
             # workers join the inventory as they heartbeat (LocalBackend emits EV_NODES)
             self.agent.start()
         if serve_http:
-            self.http = HttpServer(scheduler_router(self.runner), port=self.args.port, name="scheduler").start()
+            self.http = HttpServer(scheduler_router(self.runner, self.tracer), port=self.args.port,
+                                   name="scheduler").start()
             log.info("scheduler %s listening on :%d", self.args.gpu_type, self.http.port)
         if self.args.backend == "local" and self.args.metrics_dir:
             from ..collector.collector import MetricsCollector

@@ -52,8 +52,9 @@ def simulate(trace: list[TraceJob], algorithm: str = "ElasticFIFO", gpus: int = 
              nodes: dict[str, list[int]] | None = None, rate_limit_sec: float = 30.0, tick_sec: float = 5.0,
              resize_overhead_s: float = 5.0, restart_overhead_s: float = 15.0, use_placement: bool = True,
              drain: list[tuple[float, str, int]] | None = None, max_time: float = 1e9,
-             gpu_type: str = DEFAULT_GPU_TYPE) -> SimResult:
-    """Run a trace to completion.  ``drain`` = [(time, node, gpu)] GPU drain events."""
+             gpu_type: str = DEFAULT_GPU_TYPE, trace_path: str | None = None) -> SimResult:
+    """Run a trace to completion.  ``drain`` = [(time, node, gpu)] GPU drain events;
+    ``trace_path`` writes the scheduler timeline (Chrome-trace JSON, virtual time)."""
     clock = ManualClock(0.0)
     store = MemoryStore()
     mq = InProcQueue(maxsize=10 ** 6)
@@ -62,6 +63,11 @@ def simulate(trace: list[TraceJob], algorithm: str = "ElasticFIFO", gpus: int = 
     backend = SimBackend(clock, nodes, store, resize_overhead_s, restart_overhead_s)
     core = SchedulerCore(gpu_type, store, ResourceAllocator(store), backend, clock=clock, algorithm=algorithm,
                          rate_limit_sec=rate_limit_sec, tick_sec=tick_sec, use_placement=use_placement)
+    tracer = None
+    if trace_path:
+        from ..utils.tracing import SchedulerTracer
+
+        tracer = SchedulerTracer(core)
     pending = sorted(trace, key=lambda tj: tj.submit_time)
     drains = sorted(drain or [])
     names: list[str] = []
@@ -101,6 +107,8 @@ def simulate(trace: list[TraceJob], algorithm: str = "ElasticFIFO", gpus: int = 
         steps += 1
         if steps > 10_000_000:
             raise RuntimeError("simulation did not converge")
+    if tracer is not None:
+        tracer.save(trace_path)
     jct = {}
     waits = []
     for n in names:

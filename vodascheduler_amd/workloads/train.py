@@ -29,6 +29,7 @@ from ..ops.optim import make_optimizer
 from ..parallel.ddp import ElasticDDP
 from ..runtime.elastic import ElasticContext, TorchState, run
 from ..runtime.stepgraph import GraphedStepper
+from ..utils.tracing import trace_range
 from .metrics_logger import MetricsCSVLogger
 
 log = logging.getLogger("vodascheduler_amd.train")
@@ -164,7 +165,8 @@ def train_elastic(ctx: ElasticContext, cfg: TrainConfig, use_cache: bool = True)
             steps = 0
             while state.samples < samples_per_epoch:
                 batch = pool[state.step % len(pool)]
-                loss_t = stepper(batch).detach()
+                with trace_range("train_step", "train", world=world):
+                    loss_t = stepper(batch).detach()
                 state.samples += bs * world
                 state.step += 1
                 steps += 1
