@@ -1,0 +1,30 @@
+"""Host native core under AddressSanitizer + UndefinedBehaviorSanitizer.
+
+Builds csrc/host/tests/selftest.cpp together with the sources of the ``_vodacore``
+extension (Hungarian assignment, FfDL dynamic program) as a standalone executable with
+``-fsanitize=address,undefined`` and runs it: random problems checked against brute force,
+error paths checked to throw.  Any sanitizer report fails the test (non-recoverable UBSan,
+ASan aborts by default)."""
+import os
+import shutil
+import subprocess
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HOST = os.path.join(ROOT, "csrc", "host")
+
+
+@pytest.mark.skipif(shutil.which("g++") is None, reason="needs g++")
+def test_host_core_clean_under_asan_ubsan(tmp_path):
+    exe = str(tmp_path / "voda_selftest")
+    srcs = [os.path.join(HOST, "tests", "selftest.cpp"), os.path.join(HOST, "hungarian.cpp"),
+            os.path.join(HOST, "ffdl.cpp")]
+    cmd = ["g++", "-std=c++17", "-O1", "-g", "-fno-omit-frame-pointer", "-fsanitize=address,undefined",
+           "-fno-sanitize-recover=undefined", f"-I{HOST}", *srcs, "-o", exe]
+    b = subprocess.run(cmd, capture_output=True, text=True, timeout=300)
+    assert b.returncode == 0, b.stderr[-3000:]
+    env = dict(os.environ, ASAN_OPTIONS="detect_leaks=1:abort_on_error=0", UBSAN_OPTIONS="print_stacktrace=1")
+    r = subprocess.run([exe], capture_output=True, text=True, timeout=300, env=env)
+    assert r.returncode == 0 and "selftest OK" in r.stdout, (r.stdout[-2000:], r.stderr[-3000:])
+    assert "runtime error" not in r.stderr and "AddressSanitizer" not in r.stderr, r.stderr[-3000:]

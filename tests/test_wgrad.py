@@ -8,9 +8,10 @@ from vodascheduler_amd.ops import wgrad as W
 
 
 def test_default_splits_cover_the_chip():
-    assert W.default_splits(8192, 768, 768) == 8        # 36 tiles -> 288 workgroups
-    assert W.default_splits(8192, 3072, 768) == 2       # 144 tiles
-    assert W.default_splits(8192, 2304, 768) == 3
+    assert W.default_splits(8192, 768, 768) == 12       # 36 tiles -> 432 workgroups
+    assert W.default_splits(8192, 3072, 768) == 3       # 144 tiles
+    assert W.default_splits(8192, 2304, 768) == 4
+    assert W.default_splits(1280, 768, 768) == 5
     assert W.default_splits(300, 768, 768) == 1         # few tokens: no split
     assert W.default_splits(8192, 4096, 4096) == 1
 
