@@ -60,13 +60,14 @@ def main():
         w_ref, b_ref = W.wgrad_ref(dy, x, gw, gb)
         W.wgrad_accumulate_(dy, x, gw, gb)
         res["max_rel_err"] = float(((gw.float() - w_ref).norm() / w_ref.norm()).item())
-        for s in [int(v) for v in a.splits.split(",")]:
-            t = timeit(lambda: W.wgrad_accumulate_(dy, x, gw, gb, splits=s))
-            res[f"hip_s{s}_us"] = round(t, 2)
-        best = min((v, k) for k, v in res.items() if k.startswith("hip_s"))
+        for v in (0, 1):
+            for s in [int(x_) for x_ in a.splits.split(",")]:
+                t = timeit(lambda: W.wgrad_accumulate_(dy, x, gw, gb, splits=s, variant=v))
+                res[f"hip_v{v}_s{s}_us"] = round(t, 2)
+        best = min((v, k) for k, v in res.items() if k.startswith("hip_v"))
         res["hip_best"] = best[1]
         res["hip_best_tflops"] = round(tf / (best[0] * 1e-6), 1)
-        res["hip_default_us"] = res.get(f"hip_s{res['default_splits']}_us")
+        res["hip_default_us"] = res.get(f"hip_v{W.VARIANT}_s{res['default_splits']}_us")
         res["speedup_vs_hipblaslt+colsum"] = round(t_blas_b / best[0], 2)
         print(json.dumps(res), flush=True)
         out.append(res)

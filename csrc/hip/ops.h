@@ -37,7 +37,8 @@ void adasum_combine(uintptr_t a, uintptr_t b, uintptr_t out, int dt, uintptr_t m
 // ---- Linear weight-gradient GEMM + fused bias gradient, split-K MFMA (wgrad.hip) ----
 int64_t wgrad_workspace_floats(int M, int N, int K, int splits);
 void wgrad_gemm(uintptr_t dy, int64_t ldy, uintptr_t x, int64_t ldx, uintptr_t dw, int64_t ldw, uintptr_t db, int M,
-                int N, int K, int splits, uintptr_t ws, bool accumulate, uintptr_t stream);
+                int N, int K, int splits, uintptr_t ws, bool accumulate, uintptr_t zero, int variant,
+                uintptr_t stream);
 
 // ---- LayerNorm (layernorm.hip) ----
 void layernorm_fwd(uintptr_t x, uintptr_t gamma, uintptr_t beta, uintptr_t y, uintptr_t mean, uintptr_t rstd,

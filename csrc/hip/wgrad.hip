@@ -46,6 +46,7 @@ struct WgradArgs {
   uint16_t* dw; int64_t ldw;         // [N][K]        (splits == 1)
   uint16_t* db;                      // [N] or null   (splits == 1)
   float* ws;                         // [S][N][K] + [S][N] partial slabs (splits > 1)
+  const uint16_t* zero;              // >= 16 zero bytes: source of rows past the split (LDS-DMA path)
   int M, N, K, S, m_split, tiles_k, remap, accumulate, bias;
 };
 
@@ -76,6 +77,57 @@ __device__ __forceinline__ uint4 wg_keep(uint4 v, bool keep) {
 
 __device__ __forceinline__ wg_f32x16 wg_mfma(wg_bf16x8 a, wg_bf16x8 b, wg_f32x16 c) {
   return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+}
+
+// C/D lane map of v_mfma_f32_32x32x16_bf16: col = lane & 31, row = (reg&3) + 8*(reg>>2) + 4*h.
+// splits == 1: accumulate into dW / db directly; else write this split's fp32 slab.
+__device__ __forceinline__ void wgrad_epilogue(const WgradArgs& p, int split, int n0, int k0, int wn, int wk,
+                                               int lane, const wg_f32x16& c00, const wg_f32x16& c01,
+                                               const wg_f32x16& c10, const wg_f32x16& c11, const wg_f32x16& cb0,
+                                               const wg_f32x16& cb1, bool do_bias) {
+  const int h = lane >> 5;
+  const int col_l = lane & 31;
+  auto store_tile = [&](const wg_f32x16& acc, int rbase, int cbase) {
+    const int col = cbase + col_l;
+    if (col >= p.K) return;
+#pragma unroll
+    for (int reg = 0; reg < 16; ++reg) {
+      const int row = rbase + (reg & 3) + 8 * (reg >> 2) + 4 * h;
+      if (row < p.N) {
+        if (p.S == 1) {
+          uint16_t* o = p.dw + int64_t(row) * p.ldw + col;
+          const float v = acc[reg] + (p.accumulate ? bf2f(*o) : 0.f);
+          *o = f2bf(v);
+        } else {
+          p.ws[(int64_t(split) * p.N + row) * p.K + col] = acc[reg];
+        }
+      }
+    }
+  };
+  const int rb0 = n0 + wn * 64, cb0i = k0 + wk * 64;
+  store_tile(c00, rb0, cb0i);
+  store_tile(c01, rb0, cb0i + 32);
+  store_tile(c10, rb0 + 32, cb0i);
+  store_tile(c11, rb0 + 32, cb0i + 32);
+  if (do_bias && col_l == 0) {  // every column of cb holds the row sums; lanes 0 and 32 write
+    float* wsb = p.ws + int64_t(p.S) * p.N * p.K + int64_t(split) * p.N;
+    auto store_bias = [&](const wg_f32x16& acc, int rbase) {
+#pragma unroll
+      for (int reg = 0; reg < 16; ++reg) {
+        const int row = rbase + (reg & 3) + 8 * (reg >> 2) + 4 * h;
+        if (row < p.N) {
+          if (p.S == 1) {
+            const float v = acc[reg] + (p.accumulate ? bf2f(p.db[row]) : 0.f);
+            p.db[row] = f2bf(v);
+          } else {
+            wsb[row] = acc[reg];
+          }
+        }
+      }
+    };
+    store_bias(cb0, rb0);
+    store_bias(cb1, rb0 + 32);
+  }
 }
 
 __global__ __launch_bounds__(kWgThreads, 2) void wgrad_kernel(WgradArgs p) {
@@ -182,49 +234,135 @@ __global__ __launch_bounds__(kWgThreads, 2) void wgrad_kernel(WgradArgs p) {
     __syncthreads();
   }
 
-  // ---- epilogue: C/D lane map col = lane & 31, row = (reg&3) + 8*(reg>>2) + 4*h
-  const int col_l = lane & 31;
-  auto store_tile = [&](const wg_f32x16& acc, int rbase, int cbase) {
-    const int col = cbase + col_l;
-    if (col >= p.K) return;
+  wgrad_epilogue(p, split, n0, k0, wn, wk, lane, c00, c01, c10, c11, cb0, cb1, do_bias);
+}
+
+
+// ---------------------------------------------------------------------------------------
+// v2: the same tile, fed by an LDS ring of kWgStages stages filled with global_load_lds
+// (16-byte LDS-DMA, no staging registers).  At ~1 workgroup per CU (grid ~ 256-432) the
+// register-staged kernel above waits one full HBM latency per 64-token stage; here
+// kWgStages - 1 stages stay in flight while the MFMAs run (guide §5 'Async global->LDS
+// copy', 'Pipelining across barriers': one __shared__ array, counted vmcnt, raw
+// s_barrier).  The LDS image is the same XOR-swizzled one: LDS-DMA writes lane-linearly,
+// so the swizzle moves to the per-lane GLOBAL address (guide §5.4 rule 21): lane l of a
+// wave-instruction fills row r = 4j + l/16, slot s = l%16, and loads chunk s ^ f(r).
+// Rows past the split read a zero buffer; columns past N / K read clamped (finite) data
+// that only reaches output rows / columns that are never stored.
+// ---------------------------------------------------------------------------------------
+constexpr int kWgStages = 4;
+constexpr int kWgStageBytes = 2 * kWgTileBytes;   // dY tile + X tile
+
+// One 16-byte LDS-DMA per lane: LDS[m0 + 16 * lane] = global[gptr].  Issued as inline asm so
+// that hipcc does not see an LDS write in flight: it would otherwise guard the next
+// ds_read_b64_tr_b16 with s_waitcnt vmcnt(0) and drain the whole ring every stage.  The
+// ring's completion is tracked by hand (wg_wait_vm) and published by the barrier.
+__device__ __forceinline__ void wg_dma16(const void* gptr, uint32_t lds_addr) {
+  asm volatile("s_mov_b32 m0, %1\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(gptr), "s"(lds_addr) : "memory", "m0");
+}
+
+template <int N>
+__device__ __forceinline__ void wg_wait_vm() {
+  static_assert(N >= 0 && N < 64, "vmcnt range");
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+__global__ __launch_bounds__(kWgThreads, 1) void wgrad_glds_kernel(WgradArgs p) {
+  __shared__ __attribute__((aligned(16))) uint8_t smem[kWgStages * kWgStageBytes];
+  typedef __attribute__((address_space(3))) void lds_void;
+
+  int bid = blockIdx.x;
+  if (p.remap) bid = (bid & 7) * int(gridDim.x >> 3) + (bid >> 3);
+  const int split = bid % p.S;
+  const int tile = bid / p.S;
+  const int n0 = (tile / p.tiles_k) * kWgBN;
+  const int k0 = (tile % p.tiles_k) * kWgBK;
+  const int mb = split * p.m_split;
+  const int me = min(p.M, mb + p.m_split);
+  const int nst = me > mb ? (me - mb + kWgBM - 1) / kWgBM : 0;
+
+  const int t = threadIdx.x, lane = t & 63, wave = __builtin_amdgcn_readfirstlane(t >> 6);
+  const int wn = wave >> 1, wk = wave & 1;
+  const bool do_bias = __builtin_amdgcn_readfirstlane(p.bias && k0 == 0 && wk == 0);
+
+  // this lane's part of each of the wave's 4 wave-instructions per operand tile:
+  // instruction i covers tile rows 4j .. 4j+3 with j = 4*wave + i
+  const int lr = lane >> 4, slot = lane & 15;
+  auto issue = [&](int st) {
+    uint8_t* A = smem + (st % kWgStages) * kWgStageBytes;
+    uint8_t* B = A + kWgTileBytes;
+    const int m_base = mb + st * kWgBM;
 #pragma unroll
-    for (int reg = 0; reg < 16; ++reg) {
-      const int row = rbase + (reg & 3) + 8 * (reg >> 2) + 4 * h;
-      if (row < p.N) {
-        if (p.S == 1) {
-          uint16_t* o = p.dw + int64_t(row) * p.ldw + col;
-          const float v = acc[reg] + (p.accumulate ? bf2f(*o) : 0.f);
-          *o = f2bf(v);
-        } else {
-          p.ws[(int64_t(split) * p.N + row) * p.K + col] = acc[reg];
-        }
-      }
+    for (int i = 0; i < 4; ++i) {
+      const int j = 4 * wave + i;
+      const int r = 4 * j + lr;
+      const int ch = slot ^ (((r & 3) << 2) | ((r >> 2) & 3));
+      const int m = m_base + r;
+      const bool okm = m < me;
+      const uint16_t* ga = okm ? p.dy + int64_t(m) * p.ldy + min(n0 + ch * 8, p.N - 8) : p.zero;
+      const uint16_t* gb = okm ? p.x + int64_t(m) * p.ldx + min(k0 + ch * 8, p.K - 8) : p.zero;
+      wg_dma16(ga, __builtin_amdgcn_readfirstlane(uint32_t(size_t((lds_void*)(A + 1024 * j)))));
+      wg_dma16(gb, __builtin_amdgcn_readfirstlane(uint32_t(size_t((lds_void*)(B + 1024 * j)))));
     }
   };
-  const int rb0 = n0 + wn * 64, cb0i = k0 + wk * 64;
-  store_tile(c00, rb0, cb0i);
-  store_tile(c01, rb0, cb0i + 32);
-  store_tile(c10, rb0 + 32, cb0i);
-  store_tile(c11, rb0 + 32, cb0i + 32);
-  if (do_bias && col_l == 0) {  // every column of cb holds the row sums; lanes 0 and 32 write
-    float* wsb = p.ws + int64_t(p.S) * p.N * p.K + int64_t(split) * p.N;
-    auto store_bias = [&](const wg_f32x16& acc, int rbase) {
+
+  wg_f32x16 c00, c01, c10, c11, cb0, cb1;
 #pragma unroll
-      for (int reg = 0; reg < 16; ++reg) {
-        const int row = rbase + (reg & 3) + 8 * (reg >> 2) + 4 * h;
-        if (row < p.N) {
-          if (p.S == 1) {
-            const float v = acc[reg] + (p.accumulate ? bf2f(p.db[row]) : 0.f);
-            p.db[row] = f2bf(v);
-          } else {
-            wsb[row] = acc[reg];
-          }
-        }
-      }
-    };
-    store_bias(cb0, rb0);
-    store_bias(cb1, rb0 + 32);
+  for (int i = 0; i < 16; ++i) {
+    c00[i] = 0.f; c01[i] = 0.f; c10[i] = 0.f; c11[i] = 0.f; cb0[i] = 0.f; cb1[i] = 0.f;
   }
+  wg_bf16x8 ones;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) ones[j] = static_cast<__bf16>(1.0f);
+  const int g = lane >> 4, i16 = lane & 15, q = i16 >> 2, pp = i16 & 3, h = lane >> 5;
+  const int bo = 8 * (pp & 1);
+  const int chA = ((wn * 64 + 16 * (g & 1)) >> 3) + (pp >> 1);
+  const int chB = ((wk * 64 + 16 * (g & 1)) >> 3) + (pp >> 1);
+
+  constexpr int D = kWgStages - 1;  // stages in flight ahead of the one being computed
+#pragma unroll
+  for (int s0 = 0; s0 < D; ++s0)
+    if (s0 < nst) issue(s0);
+  for (int st = 0; st < nst; ++st) {
+    // stage st has landed once at most min(D - 1, nst - 1 - st) later stages are outstanding
+    // (8 LDS-DMA instructions per stage per lane)
+    const int ahead = min(D - 1, nst - 1 - st);
+    if (ahead >= 2) wg_wait_vm<16>();
+    else if (ahead == 1) wg_wait_vm<8>();
+    else wg_wait_vm<0>();
+    __builtin_amdgcn_s_barrier();  // every wave's DMA of stage st landed; stage st-1 fully read
+    if (st + D < nst) issue(st + D);  // refills the buffer of stage st-1
+    const uint8_t* A = smem + (st % kWgStages) * kWgStageBytes;
+    const uint8_t* B = A + kWgTileBytes;
+    wg_bf16x8 a0, a1, b0, b1;
+    {
+      const int r = 8 * h + q;
+      a0 = wg_frag(A, r, chA, bo); a1 = wg_frag(A, r, chA + 4, bo);
+      b0 = wg_frag(B, r, chB, bo); b1 = wg_frag(B, r, chB + 4, bo);
+    }
+#pragma unroll
+    for (int kk = 0; kk < kWgBM / 16; ++kk) {
+      wg_bf16x8 na0 = a0, na1 = a1, nb0 = b0, nb1 = b1;
+      if (kk + 1 < kWgBM / 16) {
+        const int r = 16 * (kk + 1) + 8 * h + q;
+        na0 = wg_frag(A, r, chA, bo); na1 = wg_frag(A, r, chA + 4, bo);
+        nb0 = wg_frag(B, r, chB, bo); nb1 = wg_frag(B, r, chB + 4, bo);
+      }
+      c00 = wg_mfma(a0, b0, c00);
+      c01 = wg_mfma(a0, b1, c01);
+      c10 = wg_mfma(a1, b0, c10);
+      c11 = wg_mfma(a1, b1, c11);
+      if (do_bias) {
+        cb0 = wg_mfma(a0, ones, cb0);
+        cb1 = wg_mfma(a1, ones, cb1);
+      }
+      a0 = na0; a1 = na1; b0 = nb0; b1 = nb1;
+    }
+    // all fragment reads of this stage are consumed by the MFMAs above before the next
+    // barrier, after which another wave may refill this buffer
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  }
+  wgrad_epilogue(p, split, n0, k0, wn, wk, lane, c00, c01, c10, c11, cb0, cb1, do_bias);
 }
 
 // dW[n][k] (+)= sum_s ws[s][n][k]; db[n] (+)= sum_s wsb[s][n].  4 columns per thread (K % 8 == 0).
@@ -288,7 +426,8 @@ int64_t wgrad_workspace_floats(int M, int N, int K, int splits) {
 }
 
 void wgrad_gemm(uintptr_t dy, int64_t ldy, uintptr_t x, int64_t ldx, uintptr_t dw, int64_t ldw, uintptr_t db, int M,
-                int N, int K, int splits, uintptr_t ws, bool accumulate, uintptr_t stream) {
+                int N, int K, int splits, uintptr_t ws, bool accumulate, uintptr_t zero, int variant,
+                uintptr_t stream) {
   VODA_CHECK(M > 0 && N >= 8 && K >= 8, "wgrad: empty problem");
   VODA_CHECK(N % 8 == 0 && K % 8 == 0, "wgrad: N and K must be multiples of 8");
   VODA_CHECK(ldy >= N && ldx >= K && ldw >= K, "wgrad: leading dimension too small");
@@ -296,18 +435,23 @@ void wgrad_gemm(uintptr_t dy, int64_t ldy, uintptr_t x, int64_t ldx, uintptr_t d
   VODA_CHECK(dy % 16 == 0 && x % 16 == 0 && dw % 16 == 0, "wgrad: operands must be 16-byte aligned");
   const WgradPlan pl = wgrad_plan(M, N, K, splits);
   VODA_CHECK(pl.S == 1 || ws != 0, "wgrad: split-K needs a workspace");
+  VODA_CHECK(variant == 0 || (zero != 0 && zero % 16 == 0), "wgrad: the LDS-DMA variant needs a zero buffer");
   WgradArgs a;
   a.dy = reinterpret_cast<const uint16_t*>(dy); a.ldy = ldy;
   a.x = reinterpret_cast<const uint16_t*>(x); a.ldx = ldx;
   a.dw = reinterpret_cast<uint16_t*>(dw); a.ldw = ldw;
   a.db = reinterpret_cast<uint16_t*>(db);
   a.ws = reinterpret_cast<float*>(ws);
+  a.zero = reinterpret_cast<const uint16_t*>(zero);
   a.M = M; a.N = N; a.K = K; a.S = pl.S; a.m_split = pl.m_split; a.tiles_k = pl.tiles_k;
   a.remap = (pl.grid % 8 == 0) ? 1 : 0;
   a.accumulate = accumulate ? 1 : 0;
   a.bias = db != 0 ? 1 : 0;
   hipStream_t s = as_stream(stream);
-  hipLaunchKernelGGL(wgrad_kernel, dim3(unsigned(pl.grid)), dim3(kWgThreads), 0, s, a);
+  if (variant == 0)
+    hipLaunchKernelGGL(wgrad_kernel, dim3(unsigned(pl.grid)), dim3(kWgThreads), 0, s, a);
+  else
+    hipLaunchKernelGGL(wgrad_glds_kernel, dim3(unsigned(pl.grid)), dim3(kWgThreads), 0, s, a);
   check_launch();
   if (pl.S > 1) {
     const int64_t work = (int64_t(N) * K) / 4 + (db != 0 ? N : 0);

@@ -35,10 +35,11 @@ def _case(M, N, K, seed=0, dev="cuda"):
     return dy, x, gw, gb
 
 
-def _check(dy, x, gw, gb, accumulate, splits, with_bias=True):
+def _check(dy, x, gw, gb, accumulate, splits, with_bias=True, variant=None):
     w_ref, b_ref = W.wgrad_ref(dy, x, gw, gb if with_bias else None, accumulate)
     gw2, gb2 = gw.clone(), gb.clone()
-    W.wgrad_accumulate_(dy, x, gw2, gb2 if with_bias else None, accumulate=accumulate, splits=splits)
+    W.wgrad_accumulate_(dy, x, gw2, gb2 if with_bias else None, accumulate=accumulate, splits=splits,
+                        variant=variant)
     torch.cuda.synchronize()
     M = dy.shape[0]
     tol = dict(rtol=2e-2, atol=2e-2 * max(1.0, (M / 64) ** 0.5))
@@ -53,17 +54,19 @@ def _check(dy, x, gw, gb, accumulate, splits, with_bias=True):
 @pytest.mark.parametrize("M,N,K", [(64, 128, 128), (200, 136, 72), (1280, 768, 768), (777, 256, 384),
                                    (8192, 768, 3072)])
 @pytest.mark.parametrize("splits", [1, 3, 8])
-def test_wgrad_kernel_matches_fp32(M, N, K, splits):
+@pytest.mark.parametrize("variant", [0, 1])
+def test_wgrad_kernel_matches_fp32(M, N, K, splits, variant):
     dy, x, gw, gb = _case(M, N, K)
-    _check(dy, x, gw, gb, True, splits)
+    _check(dy, x, gw, gb, True, splits, variant=variant)
 
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("splits", [1, 4])
-def test_wgrad_kernel_overwrite_and_no_bias(splits):
+@pytest.mark.parametrize("variant", [0, 1])
+def test_wgrad_kernel_overwrite_and_no_bias(splits, variant):
     dy, x, gw, gb = _case(512, 192, 320, seed=3)
-    _check(dy, x, gw, gb, False, splits)
-    _check(dy, x, gw, gb, True, splits, with_bias=False)
+    _check(dy, x, gw, gb, False, splits, variant=variant)
+    _check(dy, x, gw, gb, True, splits, with_bias=False, variant=variant)
 
 
 @pytest.mark.gpu
@@ -75,10 +78,10 @@ def test_wgrad_kernel_identity_operand():
     x = torch.randn(M, K, device="cuda").bfloat16()
     gw = torch.zeros(N, K, device="cuda", dtype=torch.bfloat16)
     gb = torch.zeros(N, device="cuda", dtype=torch.bfloat16)
-    for s in (1, 3):
+    for s, v in ((1, 0), (3, 0), (1, 1), (3, 1)):
         gw.zero_()
         gb.zero_()
-        W.wgrad_accumulate_(dy, x, gw, gb, splits=s)
+        W.wgrad_accumulate_(dy, x, gw, gb, splits=s, variant=v)
         torch.testing.assert_close(gw, x[:N], rtol=0, atol=0)
         torch.testing.assert_close(gb, torch.ones(N, device="cuda", dtype=torch.bfloat16), rtol=0, atol=0)
 

@@ -10,12 +10,25 @@ optimizer's flat bf16 gradient buffer.
 from __future__ import annotations
 
 import math
+import os
 
 import torch
 
 from . import _native as N
 
 TILE = 128
+# 0: register-staged LDS double buffer (default: faster inside the BERT step on MI355X,
+# profiles/r1_wgrad_v2.md); 1: LDS ring filled by global_load_lds
+VARIANT = int(os.environ.get("VODA_WGRAD_VARIANT", "0"))
+_ZERO: dict[torch.device, torch.Tensor] = {}
+
+
+def _zero_rows(device: torch.device) -> torch.Tensor:
+    """16-byte-aligned zeros the LDS-DMA variant reads for token rows past a split."""
+    z = _ZERO.get(device)
+    if z is None:
+        z = _ZERO[device] = torch.zeros(64, dtype=torch.bfloat16, device=device)
+    return z
 
 
 def default_splits(M: int, N_: int, K: int, target_blocks: int = 432) -> int:
@@ -64,7 +77,7 @@ def wgrad_ref(dy2: torch.Tensor, x2: torch.Tensor, gw: torch.Tensor, gb: torch.T
 
 
 def wgrad_accumulate_(dy2: torch.Tensor, x2: torch.Tensor, gw: torch.Tensor, gb: torch.Tensor | None = None,
-                      accumulate: bool = True, splits: int | None = None) -> None:
+                      accumulate: bool = True, splits: int | None = None, variant: int | None = None) -> None:
     """``gw (+)= dy2^T x2`` and ``gb (+)= dy2.sum(0)`` in place (fp32 accumulation, one rounding)."""
     if not dy2.is_cuda:
         w, b = wgrad_ref(dy2, x2, gw, gb, accumulate)
@@ -81,5 +94,7 @@ def wgrad_accumulate_(dy2: torch.Tensor, x2: torch.Tensor, gw: torch.Tensor, gb:
     h = N.hip()
     nws = h.wgrad_workspace_floats(M, N_, K, s)
     ws = torch.empty(nws, dtype=torch.float32, device=dy2.device) if nws else None
+    v = VARIANT if variant is None else int(variant)
     h.wgrad_gemm(dy2.data_ptr(), dy2.stride(0), x2.data_ptr(), x2.stride(0), gw.data_ptr(), gw.stride(0),
-                 N.ptr(gb), M, N_, K, s, N.ptr(ws), bool(accumulate), N.stream_of(dy2))
+                 N.ptr(gb), M, N_, K, s, N.ptr(ws), bool(accumulate), _zero_rows(dy2.device).data_ptr(), v,
+                 N.stream_of(dy2))

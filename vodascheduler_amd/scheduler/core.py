@@ -326,6 +326,12 @@ class SchedulerCore:
         self.nodes = nodes
         self.total_gpus = sum(len(v) for v in nodes.values())
         self._topology_dirty = True
+        # a GPU that vanished under a running worker (drain, failure) leaves that job broken:
+        # re-place it now instead of after the rate limit (work-conserving mode)
+        alive = {(n, g) for n, gs in nodes.items() for g in gs}
+        if self.work_conserving and any(tuple(loc) not in alive for locs in self.job_workers.values()
+                                        for loc in locs):
+            self._urgent = True
         if trigger:
             self.trigger_resched()
         self._emit("nodes", total_gpus=self.total_gpus)
