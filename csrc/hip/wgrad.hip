@@ -61,18 +61,19 @@ __device__ __forceinline__ uint2 wg_tr_read(const uint8_t* base, int off) {
   return __builtin_bit_cast(uint2, v);
 }
 
-// MFMA operand: 8 consecutive tokens (rows r .. r+3 and r+4 .. r+7 of the tile) of the column
-// this lane receives; ``ch``/``bo`` address the lane's 4-column piece (guide T10 mechanism).
-__device__ __forceinline__ wg_bf16x8 wg_frag(const uint8_t* tile, int r, int ch, int bo) {
-  const uint2 lo = wg_tr_read(tile, wg_swz(r, ch) + bo);
-  const uint2 hi = wg_tr_read(tile, wg_swz(r + 4, ch) + bo);
-  return __builtin_bit_cast(wg_bf16x8, make_uint4(lo.x, lo.y, hi.x, hi.y));
-}
-
 // v if keep else 0, as lane-wise ANDs (a struct select here becomes a scratch round trip)
 __device__ __forceinline__ uint4 wg_keep(uint4 v, bool keep) {
   const uint32_t m = keep ? 0xffffffffu : 0u;
   return make_uint4(v.x & m, v.y & m, v.z & m, v.w & m);
+}
+
+// MFMA operand -- 8 consecutive tokens (rows r..r+3 and r+4..r+7) of the column this lane
+// receives -- from precomputed lane offsets (the swizzle term of a row depends only on
+// row & 15 modulo the k-step, so a k-step's rows sit at a constant +4096 B: immediates).
+__device__ __forceinline__ wg_bf16x8 wg_frag_at(const uint8_t* tile, int off_lo, int off_hi) {
+  const uint2 lo = wg_tr_read(tile, off_lo);
+  const uint2 hi = wg_tr_read(tile, off_hi);
+  return __builtin_bit_cast(wg_bf16x8, make_uint4(lo.x, lo.y, hi.x, hi.y));
 }
 
 __device__ __forceinline__ wg_f32x16 wg_mfma(wg_bf16x8 a, wg_bf16x8 b, wg_f32x16 c) {
@@ -147,36 +148,47 @@ __global__ __launch_bounds__(kWgThreads, 2) void wgrad_kernel(WgradArgs p) {
   const int wn = wave >> 1, wk = wave & 1;
   const bool do_bias = __builtin_amdgcn_readfirstlane(p.bias && k0 == 0 && wk == 0);  // wave-uniform
 
-  // ---- global -> register staging: thread t moves chunks idx = t + 256 i (row idx>>4, chunk idx&15).
-  // Out-of-range chunks load from a clamped address and are zeroed at the LDS write, after the
-  // MFMAs: masking right after the load would make hipcc wait for every load before the MFMAs.
-  uint4 ra[4], rb[4];
-  uint32_t keep = 0;  // bit i: chunk i of dY in range, bit 4+i: chunk i of X in range
-  auto gload = [&](int st) {
-    const int m_base = mb + st * kWgBM;
-    keep = 0;
+  // ---- global -> register staging, two stages deep.  Thread t moves the 16-byte chunk
+  // (t & 15) of tile rows (t >> 4) + 16 i, i = 0..3.  Row pointers advance by 64 rows per
+  // stage (no per-load index arithmetic); rows past the split / matrix read a valid dummy
+  // address and are zeroed at the LDS write, after the MFMAs (masking right after the load
+  // would make hipcc wait for every load before the MFMAs).  Stage s+2 is loaded while stage s
+  // is computed and stage s+1 (loaded one stage earlier) is written to LDS.
+  struct Stg {
+    uint4 a[4], b[4];
+    uint32_t keep;  // bit i: chunk i of dY in range, bit 4+i: chunk i of X in range
+  };
+  Stg sx, sy;
+  const int ch_t = t & 15, r_t = t >> 4;
+  const bool col_a = n0 + ch_t * 8 < p.N, col_b = k0 + ch_t * 8 < p.K;
+  const int64_t sa16 = int64_t(16) * p.ldy, sb16 = int64_t(16) * p.ldx;
+  const uint16_t* cur_a = p.dy + int64_t(mb + r_t) * p.ldy + min(n0 + ch_t * 8, p.N - 8);
+  const uint16_t* cur_b = p.x + int64_t(mb + r_t) * p.ldx + min(k0 + ch_t * 8, p.K - 8);
+  int m_cur = mb + r_t;
+  auto gload = [&](Stg& d) {
+    d.keep = 0;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-      const int idx = t + kWgThreads * i;
-      const int r = idx >> 4, ch = idx & 15;
-      const int m = m_base + r;
-      const int mc = min(m, p.M - 1);
-      const int na = n0 + ch * 8, kb = k0 + ch * 8;
-      ra[i] = *reinterpret_cast<const uint4*>(p.dy + int64_t(mc) * p.ldy + min(na, p.N - 8));
-      rb[i] = *reinterpret_cast<const uint4*>(p.x + int64_t(mc) * p.ldx + min(kb, p.K - 8));
-      const bool okm = m < me;
-      keep |= (uint32_t(okm && na < p.N) << i) | (uint32_t(okm && kb < p.K) << (4 + i));
+      const bool okm = m_cur + 16 * i < me;
+      const uint16_t* ga = okm ? cur_a + i * sa16 : p.dy;
+      const uint16_t* gb = okm ? cur_b + i * sb16 : p.x;
+      d.a[i] = *reinterpret_cast<const uint4*>(ga);
+      d.b[i] = *reinterpret_cast<const uint4*>(gb);
+      d.keep |= (uint32_t(okm && col_a) << i) | (uint32_t(okm && col_b) << (4 + i));
     }
+    cur_a += 4 * sa16;
+    cur_b += 4 * sb16;
+    m_cur += kWgBM;
   };
-  auto swrite = [&](int buf) {
+  // LDS image offset of those chunks: the swizzle term of row r_t + 16 i does not depend on i
+  const int woff = wg_swz(r_t, ch_t);
+  auto swrite = [&](const Stg& d, int buf) {
     uint8_t* A = smem + buf * 2 * kWgTileBytes;
     uint8_t* B = A + kWgTileBytes;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-      const int idx = t + kWgThreads * i;
-      const int off = wg_swz(idx >> 4, idx & 15);
-      *reinterpret_cast<uint4*>(A + off) = wg_keep(ra[i], (keep >> i) & 1);
-      *reinterpret_cast<uint4*>(B + off) = wg_keep(rb[i], (keep >> (4 + i)) & 1);
+      *reinterpret_cast<uint4*>(A + woff + 4096 * i) = wg_keep(d.a[i], (d.keep >> i) & 1);
+      *reinterpret_cast<uint4*>(B + woff + 4096 * i) = wg_keep(d.b[i], (d.keep >> (4 + i)) & 1);
     }
   };
 
@@ -189,36 +201,32 @@ __global__ __launch_bounds__(kWgThreads, 2) void wgrad_kernel(WgradArgs p) {
 #pragma unroll
   for (int j = 0; j < 8; ++j) ones[j] = static_cast<__bf16>(1.0f);
 
-  // lane-constant parts of the transposed-read addresses (guide T10: lane 4q+p of a 16-lane
-  // group reads row q of the block, columns 4p..4p+3; lane i of the group gets column i)
+  // lane offsets of the transposed reads (guide T10: lane 4q+p of a 16-lane group reads row q
+  // of the block, columns 4p..4p+3; lane i of the group gets column i); k-step kk adds 4096*kk
   const int g = lane >> 4, i16 = lane & 15, q = i16 >> 2, pp = i16 & 3, h = lane >> 5;
   const int bo = 8 * (pp & 1);
   const int chA = ((wn * 64 + 16 * (g & 1)) >> 3) + (pp >> 1);  // sub-tile 1: +4 chunks (32 columns)
   const int chB = ((wk * 64 + 16 * (g & 1)) >> 3) + (pp >> 1);
+  const int r0 = 8 * h + q;
+  const int oa0l = wg_swz(r0, chA) + bo, oa0h = wg_swz(r0 + 4, chA) + bo;
+  const int oa1l = wg_swz(r0, chA + 4) + bo, oa1h = wg_swz(r0 + 4, chA + 4) + bo;
+  const int ob0l = wg_swz(r0, chB) + bo, ob0h = wg_swz(r0 + 4, chB) + bo;
+  const int ob1l = wg_swz(r0, chB + 4) + bo, ob1h = wg_swz(r0 + 4, chB + 4) + bo;
 
-  if (nst > 0) {
-    gload(0);
-    swrite(0);
-  }
-  __syncthreads();
-  for (int st = 0; st < nst; ++st) {
-    const uint8_t* A = smem + (st & 1) * 2 * kWgTileBytes;
+  auto compute = [&](int buf) {
+    const uint8_t* A = smem + buf * 2 * kWgTileBytes;
     const uint8_t* B = A + kWgTileBytes;
-    if (st + 1 < nst) gload(st + 1);
     // fragments of k-step kk+1 are read while the MFMAs of k-step kk run
-    wg_bf16x8 a0, a1, b0, b1;
-    {
-      const int r = 8 * h + q;
-      a0 = wg_frag(A, r, chA, bo); a1 = wg_frag(A, r, chA + 4, bo);
-      b0 = wg_frag(B, r, chB, bo); b1 = wg_frag(B, r, chB + 4, bo);
-    }
+    wg_bf16x8 a0 = wg_frag_at(A, oa0l, oa0h), a1 = wg_frag_at(A, oa1l, oa1h);
+    wg_bf16x8 b0 = wg_frag_at(B, ob0l, ob0h), b1 = wg_frag_at(B, ob1l, ob1h);
 #pragma unroll
     for (int kk = 0; kk < kWgBM / 16; ++kk) {
       wg_bf16x8 na0 = a0, na1 = a1, nb0 = b0, nb1 = b1;
       if (kk + 1 < kWgBM / 16) {
-        const int r = 16 * (kk + 1) + 8 * h + q;
-        na0 = wg_frag(A, r, chA, bo); na1 = wg_frag(A, r, chA + 4, bo);
-        nb0 = wg_frag(B, r, chB, bo); nb1 = wg_frag(B, r, chB + 4, bo);
+        const uint8_t* An = A + 4096 * (kk + 1);
+        const uint8_t* Bn = B + 4096 * (kk + 1);
+        na0 = wg_frag_at(An, oa0l, oa0h); na1 = wg_frag_at(An, oa1l, oa1h);
+        nb0 = wg_frag_at(Bn, ob0l, ob0h); nb1 = wg_frag_at(Bn, ob1l, ob1h);
       }
       c00 = wg_mfma(a0, b0, c00);
       c01 = wg_mfma(a0, b1, c01);
@@ -230,10 +238,25 @@ __global__ __launch_bounds__(kWgThreads, 2) void wgrad_kernel(WgradArgs p) {
       }
       a0 = na0; a1 = na1; b0 = nb0; b1 = nb1;
     }
-    if (st + 1 < nst) swrite((st + 1) & 1);
+  };
+  // one stage: load st+2 into ``ld``, compute st, write st+1 (held in ``wr``) to LDS
+  auto iter = [&](int st, const Stg& wr, Stg& ld) {
+    if (st + 2 < nst) gload(ld);
+    compute(st & 1);
+    if (st + 1 < nst) swrite(wr, (st + 1) & 1);
     __syncthreads();
-  }
+  };
 
+  if (nst > 0) {
+    gload(sx);
+    swrite(sx, 0);
+    if (nst > 1) gload(sy);
+  }
+  __syncthreads();
+  for (int st = 0; st < nst; st += 2) {  // unrolled by two: register sets stay compile-time
+    iter(st, sy, sx);
+    if (st + 1 < nst) iter(st + 1, sx, sy);
+  }
   wgrad_epilogue(p, split, n0, k0, wn, wk, lane, c00, c01, c10, c11, cb0, cb1, do_bias);
 }
 
@@ -250,7 +273,6 @@ __global__ __launch_bounds__(kWgThreads, 2) void wgrad_kernel(WgradArgs p) {
 // Rows past the split read a zero buffer; columns past N / K read clamped (finite) data
 // that only reaches output rows / columns that are never stored.
 // ---------------------------------------------------------------------------------------
-constexpr int kWgStages = 4;
 constexpr int kWgStageBytes = 2 * kWgTileBytes;   // dY tile + X tile
 
 // One 16-byte LDS-DMA per lane: LDS[m0 + 16 * lane] = global[gptr].  Issued as inline asm so
@@ -267,6 +289,8 @@ __device__ __forceinline__ void wg_wait_vm() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 }
 
+// kWgStages = 4: 128 KB ring, 1 workgroup/CU, 3 stages in flight; 2: 64 KB, 2 workgroups/CU
+template <int kWgStages>
 __global__ __launch_bounds__(kWgThreads, 1) void wgrad_glds_kernel(WgradArgs p) {
   __shared__ __attribute__((aligned(16))) uint8_t smem[kWgStages * kWgStageBytes];
   typedef __attribute__((address_space(3))) void lds_void;
@@ -318,6 +342,11 @@ __global__ __launch_bounds__(kWgThreads, 1) void wgrad_glds_kernel(WgradArgs p) 
   const int bo = 8 * (pp & 1);
   const int chA = ((wn * 64 + 16 * (g & 1)) >> 3) + (pp >> 1);
   const int chB = ((wk * 64 + 16 * (g & 1)) >> 3) + (pp >> 1);
+  const int r0 = 8 * h + q;
+  const int oa0l = wg_swz(r0, chA) + bo, oa0h = wg_swz(r0 + 4, chA) + bo;
+  const int oa1l = wg_swz(r0, chA + 4) + bo, oa1h = wg_swz(r0 + 4, chA + 4) + bo;
+  const int ob0l = wg_swz(r0, chB) + bo, ob0h = wg_swz(r0 + 4, chB) + bo;
+  const int ob1l = wg_swz(r0, chB + 4) + bo, ob1h = wg_swz(r0 + 4, chB + 4) + bo;
 
   constexpr int D = kWgStages - 1;  // stages in flight ahead of the one being computed
 #pragma unroll
@@ -327,26 +356,23 @@ __global__ __launch_bounds__(kWgThreads, 1) void wgrad_glds_kernel(WgradArgs p) 
     // stage st has landed once at most min(D - 1, nst - 1 - st) later stages are outstanding
     // (8 LDS-DMA instructions per stage per lane)
     const int ahead = min(D - 1, nst - 1 - st);
-    if (ahead >= 2) wg_wait_vm<16>();
-    else if (ahead == 1) wg_wait_vm<8>();
+    if (D >= 3 && ahead >= 2) wg_wait_vm<16>();
+    else if (D >= 2 && ahead == 1) wg_wait_vm<8>();
     else wg_wait_vm<0>();
     __builtin_amdgcn_s_barrier();  // every wave's DMA of stage st landed; stage st-1 fully read
     if (st + D < nst) issue(st + D);  // refills the buffer of stage st-1
     const uint8_t* A = smem + (st % kWgStages) * kWgStageBytes;
     const uint8_t* B = A + kWgTileBytes;
-    wg_bf16x8 a0, a1, b0, b1;
-    {
-      const int r = 8 * h + q;
-      a0 = wg_frag(A, r, chA, bo); a1 = wg_frag(A, r, chA + 4, bo);
-      b0 = wg_frag(B, r, chB, bo); b1 = wg_frag(B, r, chB + 4, bo);
-    }
+    wg_bf16x8 a0 = wg_frag_at(A, oa0l, oa0h), a1 = wg_frag_at(A, oa1l, oa1h);
+    wg_bf16x8 b0 = wg_frag_at(B, ob0l, ob0h), b1 = wg_frag_at(B, ob1l, ob1h);
 #pragma unroll
     for (int kk = 0; kk < kWgBM / 16; ++kk) {
       wg_bf16x8 na0 = a0, na1 = a1, nb0 = b0, nb1 = b1;
       if (kk + 1 < kWgBM / 16) {
-        const int r = 16 * (kk + 1) + 8 * h + q;
-        na0 = wg_frag(A, r, chA, bo); na1 = wg_frag(A, r, chA + 4, bo);
-        nb0 = wg_frag(B, r, chB, bo); nb1 = wg_frag(B, r, chB + 4, bo);
+        const uint8_t* An = A + 4096 * (kk + 1);
+        const uint8_t* Bn = B + 4096 * (kk + 1);
+        na0 = wg_frag_at(An, oa0l, oa0h); na1 = wg_frag_at(An, oa1l, oa1h);
+        nb0 = wg_frag_at(Bn, ob0l, ob0h); nb1 = wg_frag_at(Bn, ob1l, ob1h);
       }
       c00 = wg_mfma(a0, b0, c00);
       c01 = wg_mfma(a0, b1, c01);
@@ -448,10 +474,15 @@ void wgrad_gemm(uintptr_t dy, int64_t ldy, uintptr_t x, int64_t ldx, uintptr_t d
   a.accumulate = accumulate ? 1 : 0;
   a.bias = db != 0 ? 1 : 0;
   hipStream_t s = as_stream(stream);
+  VODA_CHECK(variant >= 0 && variant <= 3, "wgrad: variant must be 0..3");
   if (variant == 0)
     hipLaunchKernelGGL(wgrad_kernel, dim3(unsigned(pl.grid)), dim3(kWgThreads), 0, s, a);
+  else if (variant == 1)
+    hipLaunchKernelGGL(wgrad_glds_kernel<4>, dim3(unsigned(pl.grid)), dim3(kWgThreads), 0, s, a);
+  else if (variant == 2)
+    hipLaunchKernelGGL(wgrad_glds_kernel<2>, dim3(unsigned(pl.grid)), dim3(kWgThreads), 0, s, a);
   else
-    hipLaunchKernelGGL(wgrad_glds_kernel, dim3(unsigned(pl.grid)), dim3(kWgThreads), 0, s, a);
+    hipLaunchKernelGGL(wgrad_glds_kernel<3>, dim3(unsigned(pl.grid)), dim3(kWgThreads), 0, s, a);
   check_launch();
   if (pl.S > 1) {
     const int64_t work = (int64_t(N) * K) / 4 + (db != 0 ? N : 0);

@@ -17,9 +17,10 @@ import torch
 from . import _native as N
 
 TILE = 128
-# 0: register-staged LDS double buffer (default: faster inside the BERT step on MI355X,
-# profiles/r1_wgrad_v2.md); 1: LDS ring filled by global_load_lds
-VARIANT = int(os.environ.get("VODA_WGRAD_VARIANT", "0"))
+# 0: register-staged LDS double buffer; 1 / 2 / 3: LDS ring of 4 / 2 / 3 stages filled by
+# global_load_lds.  Default 2 (64 KB ring, 2 workgroups per CU): fastest in the BERT-base step
+# on MI355X (profiles/r1_wgrad_v3.md)
+VARIANT = int(os.environ.get("VODA_WGRAD_VARIANT", "2"))
 _ZERO: dict[torch.device, torch.Tensor] = {}
 
 
