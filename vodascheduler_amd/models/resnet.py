@@ -6,7 +6,9 @@ BASELINE config "8 ResNet-50 ImageNet-shape jobs".  Convolutions run on MIOpen
 through PyTorch-ROCm in channels_last bf16 (NHWC is MIOpen's fast layout on CDNA);
 random-init weights, synthetic data.  Every BatchNorm is the fused HIP
 BN(+residual)(+ReLU) of ops/batchnorm.py: the bottleneck's ``relu(bn3(conv3) + identity)``
-is ONE statistics pass + ONE apply pass forward, instead of MIOpen BN + add + ReLU.
+is ONE statistics pass + ONE apply pass forward, instead of MIOpen BN + add + ReLU.  The 1x1
+convolutions (with >= 128 input channels) run as GEMMs on the NHWC views with the split-K
+MFMA weight-gradient kernel (ops/conv1x1.py).
 """
 from __future__ import annotations
 
@@ -14,6 +16,7 @@ import torch
 from torch import nn
 
 from ..ops.batchnorm import FusedBatchNorm2d
+from ..ops.conv1x1 import Conv1x1
 from ..ops.pool import FusedMaxPool2d
 
 
@@ -23,11 +26,11 @@ class Bottleneck(nn.Module):
     def __init__(self, inplanes: int, planes: int, stride: int = 1, downsample: nn.Module | None = None):
         super().__init__()
         width = planes
-        self.conv1 = nn.Conv2d(inplanes, width, 1, bias=False)
+        self.conv1 = Conv1x1(inplanes, width)
         self.bn1 = FusedBatchNorm2d(width, relu=True)
         self.conv2 = nn.Conv2d(width, width, 3, stride=stride, padding=1, bias=False)  # v1.5: stride on 3x3
         self.bn2 = FusedBatchNorm2d(width, relu=True)
-        self.conv3 = nn.Conv2d(width, planes * self.expansion, 1, bias=False)
+        self.conv3 = Conv1x1(width, planes * self.expansion)
         self.bn3 = FusedBatchNorm2d(planes * self.expansion, relu=True)  # relu(bn3(.) + identity)
         self.downsample = downsample
 
@@ -84,7 +87,7 @@ class ResNet(nn.Module):
     def _make(self, block, planes, blocks, stride=1):
         down = None
         if stride != 1 or self.inplanes != planes * block.expansion:
-            down = nn.Sequential(nn.Conv2d(self.inplanes, planes * block.expansion, 1, stride=stride, bias=False),
+            down = nn.Sequential(Conv1x1(self.inplanes, planes * block.expansion, stride=stride),
                                  FusedBatchNorm2d(planes * block.expansion))
         layers = [block(self.inplanes, planes, stride, down)]
         self.inplanes = planes * block.expansion

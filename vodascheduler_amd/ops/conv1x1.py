@@ -1,0 +1,116 @@
+"""1x1 convolution of channels_last activations as GEMMs (ResNet bottlenecks).
+
+A 1x1 convolution over an NHWC tensor is a plain GEMM on its ``[N*H*W, C]`` view:
+
+    forward          Y[m, co] = X[m, :] . W[co, :]          hipBLASLt (view, no copy)
+    input gradient   dX[m, ci] = dY[m, :] . W[:, ci]        hipBLASLt
+    weight gradient  dW[co, ci] (+)= sum_m dY[m, co] X[m, ci]  split-K MFMA kernel
+                                                           (csrc/hip/wgrad.hip), accumulated
+                                                           straight into the optimizer's
+                                                           flat bf16 gradient
+
+MIOpen runs these as implicit-GEMM convolution kernels; the weight-gradient ones are the
+"reduction over 800k pixels" shape the split-K kernel is built for.  Stride-2 1x1
+convolutions (ResNet downsample) subsample the input first and scatter the input gradient
+back.  Convolutions with fewer than 128 input channels (ResNet stage 1: K = 64 is half an
+MFMA tile) stay on MIOpen, which is faster there (benchmarks/bench_conv1x1.py,
+profiles/raw/r1_bench_conv1x1.log: 11.7 -> 9.0 ms for all 1x1 convolutions of a ResNet-50
+bs256 step, 0.68-0.96x on the Cin = 64 shapes).  The layer is a drop-in ``nn.Conv2d`` (same parameters / state dict); anything it does
+not cover (CPU tensors, non-bf16, groups, padding, bias, a layout that is not
+channels_last) runs ``F.conv2d``.
+"""
+from __future__ import annotations
+
+import os
+
+import torch
+import torch.nn.functional as F
+
+from . import wgrad as W
+
+USE_CONV1X1_GEMM = os.environ.get("VODA_CONV1X1_GEMM", "1") != "0"
+
+
+def _direct(p: torch.Tensor) -> bool:
+    return (getattr(p, "_voda_flat_grad", False) and p.grad is not None and p.grad.dtype == p.dtype)
+
+
+def _ready(p: torch.Tensor) -> None:
+    fn = getattr(p, "_voda_grad_ready", None)
+    if fn is not None:
+        fn(p)
+
+
+def _as_2d(t: torch.Tensor) -> torch.Tensor:
+    """[N, C, H, W] channels_last -> [N*H*W, C] (a view when dense channels_last)."""
+    n, c, h, w = t.shape
+    return t.permute(0, 2, 3, 1).reshape(n * h * w, c)
+
+
+class _Conv1x1Fn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, weight, stride: int):
+        xs = x[:, :, ::stride, ::stride] if stride > 1 else x
+        n, cin, h, w = xs.shape
+        cout = weight.shape[0]
+        x2 = _as_2d(xs)
+        w2 = weight.reshape(cout, cin)
+        y2 = x2 @ w2.t()
+        ctx.save_for_backward(x2, weight)
+        ctx.meta = (x.shape, stride, n, h, w)
+        return y2.view(n, h, w, cout).permute(0, 3, 1, 2)  # channels_last NCHW
+
+    @staticmethod
+    def backward(ctx, dy):
+        x2, weight = ctx.saved_tensors
+        in_shape, stride, n, h, w = ctx.meta
+        cout, cin = weight.shape[0], weight.shape[1]
+        dy2 = _as_2d(dy)
+        if dy2.dtype != weight.dtype:
+            dy2 = dy2.to(weight.dtype)
+        if dy2.stride(1) != 1 or dy2.stride(0) != cout:
+            dy2 = dy2.contiguous()
+        w2 = weight.reshape(cout, cin)
+        dx = None
+        if ctx.needs_input_grad[0]:
+            dxs = (dy2 @ w2).view(n, h, w, cin).permute(0, 3, 1, 2)
+            if stride > 1:
+                N_, C_, H_, W_ = in_shape
+                dx = dxs.new_zeros((N_, H_, W_, C_)).permute(0, 3, 1, 2)  # channels_last
+                dx[:, :, ::stride, ::stride] = dxs
+            else:
+                dx = dxs
+        dw = None
+        if ctx.needs_input_grad[1]:
+            g2 = weight.grad.view(cout, cin) if _direct(weight) else None
+            if g2 is not None and W.supported(dy2, x2, g2):
+                W.wgrad_accumulate_(dy2, x2, g2)
+                _ready(weight)
+            elif g2 is not None:
+                g2.addmm_(dy2.t(), x2)
+                _ready(weight)
+            else:
+                dw = (dy2.t() @ x2).view(cout, cin, 1, 1)
+        return dx, dw, None
+
+
+class Conv1x1(torch.nn.Conv2d):
+    """``nn.Conv2d(cin, cout, 1, stride, bias=False)`` with the GEMM formulation on GPU."""
+
+    def __init__(self, in_channels: int, out_channels: int, stride: int = 1, **kw):
+        super().__init__(in_channels, out_channels, 1, stride=stride, bias=False, **kw)
+
+    def _gemm_ok(self, x: torch.Tensor) -> bool:
+        return (USE_CONV1X1_GEMM and x.is_cuda and x.dim() == 4 and x.dtype == torch.bfloat16
+                and self.weight.dtype == torch.bfloat16 and self.groups == 1 and self.padding == (0, 0)
+                and self.dilation == (1, 1) and self.stride[0] == self.stride[1]
+                and x.is_contiguous(memory_format=torch.channels_last)
+                and self.in_channels >= 128 and self.in_channels % 8 == 0 and self.out_channels % 8 == 0)
+
+    def forward(self, x):
+        if x.is_cuda and x.dtype != self.weight.dtype and torch.is_autocast_enabled("cuda"):
+            x = x.to(self.weight.dtype)
+        if self._gemm_ok(x):
+            with torch.autocast("cuda", enabled=False):
+                return _Conv1x1Fn.apply(x, self.weight, self.stride[0])
+        return super().forward(x)

@@ -36,10 +36,11 @@ def default_splits(M: int, N_: int, K: int, target_blocks: int = 432) -> int:
     """Split the token dimension until the grid is ~1.7 waves of workgroups on the 256 CUs
     (two fit per CU), keeping >= 4 k-stages of 64 tokens per split.  Measured optimum on
     MI355X for the BERT-base shapes (benchmarks/bench_wgrad.py, profiles/): 12 splits for
-    768x768 (36 tiles), 4 for 2304x768, 3 for 3072x768 / 768x3072."""
+    768x768 (36 tiles), 4 for 2304x768, 3 for 3072x768 / 768x3072.  Convolution-sized token
+    counts (ResNet 1x1 convs: 800k rows, 2-32 tiles) go up to 256 splits."""
     tiles = math.ceil(N_ / TILE) * math.ceil(K / TILE)
     s = math.ceil(target_blocks / tiles)
-    return max(1, min(s, 16, M // 256 if M >= 256 else 1))
+    return max(1, min(s, 256, M // 256 if M >= 256 else 1))
 
 
 def supported(dy2: torch.Tensor, x2: torch.Tensor, gw: torch.Tensor, gb: torch.Tensor | None = None) -> bool:
