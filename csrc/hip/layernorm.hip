@@ -15,6 +15,21 @@
 
 namespace voda {
 
+// 4 elements of T as raw bits (loaded now, converted later: lets several loads be in flight)
+template <typename T> struct Raw4 {
+  using type = uint2;
+  static __device__ __forceinline__ type load(const T* p, int64_t i4) { return reinterpret_cast<const uint2*>(p)[i4]; }
+  static __device__ __forceinline__ float4 cvt(type u) {
+    const T* q = reinterpret_cast<const T*>(&u);
+    return Vec4<T>::load(q, 0);
+  }
+};
+template <> struct Raw4<float> {
+  using type = float4;
+  static __device__ __forceinline__ type load(const float* p, int64_t i4) { return reinterpret_cast<const float4*>(p)[i4]; }
+  static __device__ __forceinline__ float4 cvt(type u) { return u; }
+};
+
 template <typename WT>
 __device__ __forceinline__ float4 load_w4(const void* w, int64_t c4) {
   return Vec4<WT>::load(reinterpret_cast<const WT*>(w), c4);
@@ -34,9 +49,11 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(const T* __restrict__ x, co
   float4 v[MAXITER];
   float s = 0.f;
 #pragma unroll
+  for (int it = 0; it < MAXITER; ++it)  // unconditional (clamped) loads, zeroed after
+    v[it] = Vec4<T>::load(xr, min(it * 64 + lane, N4 - 1));
+#pragma unroll
   for (int it = 0; it < MAXITER; ++it) {
-    const int c4 = it * 64 + lane;
-    v[it] = c4 < N4 ? Vec4<T>::load(xr, c4) : make_float4(0.f, 0.f, 0.f, 0.f);
+    if (it * 64 + lane >= N4) v[it] = make_float4(0.f, 0.f, 0.f, 0.f);
     s += (v[it].x + v[it].y) + (v[it].z + v[it].w);
   }
   const float inv_n = 1.f / float(N);
@@ -91,40 +108,76 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const T* __restrict__ dy, c
     ag[it] = make_float4(0.f, 0.f, 0.f, 0.f);
     ab[it] = make_float4(0.f, 0.f, 0.f, 0.f);
   }
-  for (int64_t row = int64_t(blockIdx.x) * 4 + wave; row < M; row += int64_t(gridDim.x) * 4) {
-    const float mu = mean[row], rs = rstd[row];
-    float4 xh[MAXITER], dg[MAXITER];
-    float s1 = 0.f, s2 = 0.f;
+  // A wave owns rows wave + 4*blockIdx.x + k * 4*gridDim.x.  The grid is capped (one fp32
+  // partial row per block for dgamma/dbeta), so a wave walks several rows; R of them are
+  // loaded together before any is reduced, which keeps R row-loads in flight per wave
+  // instead of one dependent HBM round trip per row (BERT-base 8192 x 768: 25 -> ~8 us).
+  constexpr int R = MAXITER <= 3 ? 4 : (MAXITER <= 4 ? 2 : 1);
+  const int64_t rstride = int64_t(gridDim.x) * 4;
+  for (int64_t row0 = int64_t(blockIdx.x) * 4 + wave; row0 < M; row0 += rstride * R) {
+    // every load is unconditional (clamped row / column) and kept as raw bits until all R
+    // rows are in flight; out-of-range lanes are zeroed after the conversion.  A branch or a
+    // conversion right behind each load makes hipcc wait for it before issuing the next one.
+    typename Raw4<T>::type xr[R][MAXITER], dr[R][MAXITER];
 #pragma unroll
-    for (int it = 0; it < MAXITER; ++it) {
-      const int c4 = it * 64 + lane;
-      if (c4 < N4) {
-        float4 xv = Vec4<T>::load(x + row * N, c4);
-        float4 dv = Vec4<T>::load(dy + row * N, c4);
-        xh[it] = make_float4((xv.x - mu) * rs, (xv.y - mu) * rs, (xv.z - mu) * rs, (xv.w - mu) * rs);
-        dg[it] = make_float4(dv.x * g[it].x, dv.y * g[it].y, dv.z * g[it].z, dv.w * g[it].w);
-        ag[it].x += dv.x * xh[it].x; ag[it].y += dv.y * xh[it].y;
-        ag[it].z += dv.z * xh[it].z; ag[it].w += dv.w * xh[it].w;
-        ab[it].x += dv.x; ab[it].y += dv.y; ab[it].z += dv.z; ab[it].w += dv.w;
-        s1 += (dg[it].x * xh[it].x + dg[it].y * xh[it].y) + (dg[it].z * xh[it].z + dg[it].w * xh[it].w);
-        s2 += (dg[it].x + dg[it].y) + (dg[it].z + dg[it].w);
-      } else {
-        xh[it] = make_float4(0.f, 0.f, 0.f, 0.f);
-        dg[it] = xh[it];
+    for (int j = 0; j < R; ++j) {
+      const int64_t row = min(row0 + j * rstride, M - 1);
+#pragma unroll
+      for (int it = 0; it < MAXITER; ++it) {
+        const int c4 = min(it * 64 + lane, N4 - 1);
+        xr[j][it] = Raw4<T>::load(x + row * N, c4);
+        dr[j][it] = Raw4<T>::load(dy + row * N, c4);
       }
     }
-    const float c1 = wave_sum(s1) * inv_n;
-    const float c2 = wave_sum(s2) * inv_n;
+    float4 xv[R][MAXITER], dv[R][MAXITER];
 #pragma unroll
-    for (int it = 0; it < MAXITER; ++it) {
-      const int c4 = it * 64 + lane;
-      if (c4 < N4) {
-        float4 o;
-        o.x = (dg[it].x - xh[it].x * c1 - c2) * rs;
-        o.y = (dg[it].y - xh[it].y * c1 - c2) * rs;
-        o.z = (dg[it].z - xh[it].z * c1 - c2) * rs;
-        o.w = (dg[it].w - xh[it].w * c1 - c2) * rs;
-        Vec4<T>::store(dx + row * N, c4, o);
+    for (int j = 0; j < R; ++j) {
+      const bool rok = row0 + j * rstride < M;
+#pragma unroll
+      for (int it = 0; it < MAXITER; ++it) {
+        const bool ok = rok && (it * 64 + lane < N4);
+        const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
+        xv[j][it] = ok ? Raw4<T>::cvt(xr[j][it]) : z;
+        dv[j][it] = ok ? Raw4<T>::cvt(dr[j][it]) : z;
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < R; ++j) {
+      const int64_t row = row0 + j * rstride;
+      if (row >= M) break;  // wave-uniform
+      const float mu = mean[row], rs = rstd[row];
+      float4 xh[MAXITER], dg[MAXITER];
+      float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+      for (int it = 0; it < MAXITER; ++it) {
+        const int c4 = it * 64 + lane;
+        if (c4 < N4) {
+          const float4 xw = xv[j][it], dw = dv[j][it];
+          xh[it] = make_float4((xw.x - mu) * rs, (xw.y - mu) * rs, (xw.z - mu) * rs, (xw.w - mu) * rs);
+          dg[it] = make_float4(dw.x * g[it].x, dw.y * g[it].y, dw.z * g[it].z, dw.w * g[it].w);
+          ag[it].x += dw.x * xh[it].x; ag[it].y += dw.y * xh[it].y;
+          ag[it].z += dw.z * xh[it].z; ag[it].w += dw.w * xh[it].w;
+          ab[it].x += dw.x; ab[it].y += dw.y; ab[it].z += dw.z; ab[it].w += dw.w;
+          s1 += (dg[it].x * xh[it].x + dg[it].y * xh[it].y) + (dg[it].z * xh[it].z + dg[it].w * xh[it].w);
+          s2 += (dg[it].x + dg[it].y) + (dg[it].z + dg[it].w);
+        } else {
+          xh[it] = make_float4(0.f, 0.f, 0.f, 0.f);
+          dg[it] = xh[it];
+        }
+      }
+      const float c1 = wave_sum(s1) * inv_n;
+      const float c2 = wave_sum(s2) * inv_n;
+#pragma unroll
+      for (int it = 0; it < MAXITER; ++it) {
+        const int c4 = it * 64 + lane;
+        if (c4 < N4) {
+          float4 o;
+          o.x = (dg[it].x - xh[it].x * c1 - c2) * rs;
+          o.y = (dg[it].y - xh[it].y * c1 - c2) * rs;
+          o.z = (dg[it].z - xh[it].z * c1 - c2) * rs;
+          o.w = (dg[it].w - xh[it].w * c1 - c2) * rs;
+          Vec4<T>::store(dx + row * N, c4, o);
+        }
       }
     }
   }
