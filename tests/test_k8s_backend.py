@@ -184,3 +184,19 @@ def test_pod_binding_tolerations_and_migration(env):
     core.poll()
     assert all(l[0] != node for l in backend.placement[a])
     assert f"{a}-worker-0" not in fake.pods
+
+
+def test_gen_manifests_one_scheduler_per_gpu_type(capsys):
+    """Reference helm/voda-scheduler/gen-scheduler-yaml.sh: one scheduler per GPU type."""
+    import yaml
+
+    from vodascheduler_amd.cli.main import main
+
+    assert main(["gen-manifests", "--gpu-type", "amd-instinct-mi355x", "--gpu-type", "amd-instinct-mi300x"]) == 0
+    docs = list(yaml.safe_load_all(capsys.readouterr().out))
+    kinds = [(d["kind"], d["metadata"]["name"]) for d in docs]
+    assert kinds == [("Deployment", "scheduler-amd-instinct-mi355x"), ("Service", "scheduler-amd-instinct-mi355x"),
+                     ("Deployment", "scheduler-amd-instinct-mi300x"), ("Service", "scheduler-amd-instinct-mi300x")]
+    cmd = docs[2]["spec"]["template"]["spec"]["containers"][0]["command"]
+    assert cmd[cmd.index("--gpu-type") + 1] == "amd-instinct-mi300x" and "--resume" in cmd
+    assert docs[1]["spec"]["ports"][0]["port"] == 55588

@@ -8,6 +8,7 @@
     vodascheduler set ratelimit 30                PUT   <scheduler>/ratelimit
     vodascheduler up [--gpus 0,1,...]             all-in-one: service + scheduler + allocator + node agent
     vodascheduler simulate --jobs 32 --gpus 8     discrete-event run of a Philly-style trace (no GPUs)
+    vodascheduler gen-manifests --gpu-type T ...  scheduler Deployment + Service per GPU type (k8s)
 
 Fixes of the reference CLI: ``delete`` deletes EVERY name given (the
 reference always sends ``Args().Get(0)``) and sends each as a JSON string (the service
@@ -129,6 +130,46 @@ def cmd_simulate(a) -> int:
     return 0
 
 
+SCHEDULER_MANIFEST = """apiVersion: apps/v1
+kind: Deployment
+metadata: {{name: scheduler-{gpu}, namespace: {ns}}}
+spec:
+  replicas: 1
+  selector: {{matchLabels: {{app: scheduler-{gpu}}}}}
+  template:
+    metadata: {{labels: {{app: scheduler-{gpu}}}}}
+    spec:
+      serviceAccountName: voda-scheduler
+      containers:
+        - name: scheduler
+          image: {image}
+          command: ["vodascheduler-scheduler", "--backend", "k8s", "--gpu-type", "{gpu}",
+                    "--algorithm", "{algorithm}", "--resume",
+                    "--store", "sqlite:///state/jobs.db", "--mq", "sqlite:///state/mq.db",
+                    "--allocator", "http://resource-allocator.{ns}.svc.cluster.local:55589"]
+          ports: [{{containerPort: 55588}}]
+          volumeMounts: [{{name: state, mountPath: /state}}]
+      volumes: [{{name: state, persistentVolumeClaim: {{claimName: voda-state}}}}]
+---
+apiVersion: v1
+kind: Service
+metadata: {{name: scheduler-{gpu}, namespace: {ns}}}
+spec:
+  selector: {{app: scheduler-{gpu}}}
+  ports: [{{name: port, port: 55588, targetPort: 55588}}]
+"""
+
+
+def cmd_gen_manifests(a) -> int:
+    """One scheduler Deployment + Service per GPU type (reference
+    helm/voda-scheduler/gen-scheduler-yaml.sh + scheduler.yaml.base): a heterogeneous cluster
+    runs one scheduler per ``vodascheduler/accelerator`` label value."""
+    docs = [SCHEDULER_MANIFEST.format(gpu=g, ns=a.namespace, image=a.image, algorithm=a.algorithm)
+            for g in a.gpu_type]
+    sys.stdout.write("---\n".join(docs))
+    return 0
+
+
 def build_parser() -> argparse.ArgumentParser:
     ap = argparse.ArgumentParser(NAME, description=f"{NAME} {VERSION}: elastic DL scheduler for AMD Instinct MI355X")
     ap.add_argument("--service", default=None, help=f"training service URL (default :{PORT_TRAINING_SERVICE})")
@@ -177,6 +218,13 @@ def build_parser() -> argparse.ArgumentParser:
     p.add_argument("--seed", type=int, default=0)
     p.add_argument("--trace", default=None, help="Chrome-trace JSON of each run ({algorithm} is substituted)")
     p.set_defaults(fn=cmd_simulate)
+
+    p = sub.add_parser("gen-manifests", help="scheduler Deployment + Service YAML per GPU type (k8s backend)")
+    p.add_argument("--gpu-type", action="append", required=True, help="repeat for every GPU type")
+    p.add_argument("--namespace", default="voda-scheduler")
+    p.add_argument("--image", default="vodascheduler-amd:latest")
+    p.add_argument("--algorithm", default="ElasticFIFO")
+    p.set_defaults(fn=cmd_gen_manifests)
 
     p = sub.add_parser("version", help="print the version")
     p.set_defaults(fn=lambda a: print(f"{NAME} {VERSION}") or 0)
