@@ -38,7 +38,8 @@ def timeit(fn, iters=50, warm=5) -> float:
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--splits", default="1,2,3,4,6,8,12")
+    ap.add_argument("--splits", default="1,2,3,4,6,8,12,16,28")
+    ap.add_argument("--variants", default="2,4,6,7,8")
     a = ap.parse_args()
     _native.hip()
     dev = torch.device("cuda", 0)
@@ -54,13 +55,14 @@ def main():
         res = {"shape": name, "M": M, "N": N, "K": K, "hipblaslt_us": round(t_blas, 2),
                "hipblaslt_tflops": round(tf / (t_blas * 1e-6), 1), "hipblaslt+colsum_us": round(t_blas_b, 2),
                "default_splits": W.default_splits(M, N, K)}
+        res["wide_default_splits"] = W.default_splits(M, N, K, variant=6)
         # correctness of the default configuration against fp32
         gw.normal_()
         gb.normal_()
         w_ref, b_ref = W.wgrad_ref(dy, x, gw, gb)
         W.wgrad_accumulate_(dy, x, gw, gb)
         res["max_rel_err"] = float(((gw.float() - w_ref).norm() / w_ref.norm()).item())
-        for v in (0, 1, 2, 3):
+        for v in [int(v_) for v_ in a.variants.split(",")]:
             for s in [int(x_) for x_ in a.splits.split(",")]:
                 t = timeit(lambda: W.wgrad_accumulate_(dy, x, gw, gb, splits=s, variant=v))
                 res[f"hip_v{v}_s{s}_us"] = round(t, 2)

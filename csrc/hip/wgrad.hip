@@ -273,7 +273,6 @@ __global__ __launch_bounds__(kWgThreads, 2) void wgrad_kernel(WgradArgs p) {
 // Rows past the split read a zero buffer; columns past N / K read clamped (finite) data
 // that only reaches output rows / columns that are never stored.
 // ---------------------------------------------------------------------------------------
-constexpr int kWgStageBytes = 2 * kWgTileBytes;   // dY tile + X tile
 
 // One 16-byte LDS-DMA per lane: LDS[m0 + 16 * lane] = global[gptr].  Issued as inline asm so
 // that hipcc does not see an LDS write in flight: it would otherwise guard the next
@@ -290,9 +289,27 @@ __device__ __forceinline__ void wg_wait_vm() {
 }
 
 // kWgStages = 4: 128 KB ring, 1 workgroup/CU, 3 stages in flight; 2: 64 KB, 2 workgroups/CU
-template <int kWgStages>
+template <int PER>
+__device__ __forceinline__ void wg_wait_ahead(int ahead) {  // vmcnt(ahead * PER), ahead <= 4
+  switch (ahead) {
+    case 4: wg_wait_vm<4 * PER>(); break;
+    case 3: wg_wait_vm<3 * PER>(); break;
+    case 2: wg_wait_vm<2 * PER>(); break;
+    case 1: wg_wait_vm<PER>(); break;
+    default: wg_wait_vm<0>(); break;
+  }
+}
+
+// kWgStages ring stages of BM tokens each: <4, 64> 128 KB, 1 workgroup/CU; <2, 64> 64 KB,
+// 2 workgroups/CU; <3, 64>; <4, 32> 64 KB with 3 stages in flight at 2 workgroups/CU.
+template <int kWgStages, int BM>
 __global__ __launch_bounds__(kWgThreads, 1) void wgrad_glds_kernel(WgradArgs p) {
-  __shared__ __attribute__((aligned(16))) uint8_t smem[kWgStages * kWgStageBytes];
+  constexpr int TB = BM * kWgRowBytes;   // bytes per operand tile
+  constexpr int SB = 2 * TB;             // bytes per stage (dY tile + X tile)
+  constexpr int IPW = BM / 16;           // 1 KB LDS-DMA wave-instructions per wave per operand tile
+  constexpr int PER = 2 * IPW;           // LDS-DMA instructions per lane per stage
+  static_assert(BM % 16 == 0 && BM <= 64, "stage depth");
+  __shared__ __attribute__((aligned(16))) uint8_t smem[kWgStages * SB];
   typedef __attribute__((address_space(3))) void lds_void;
 
   int bid = blockIdx.x;
@@ -303,22 +320,22 @@ __global__ __launch_bounds__(kWgThreads, 1) void wgrad_glds_kernel(WgradArgs p) 
   const int k0 = (tile % p.tiles_k) * kWgBK;
   const int mb = split * p.m_split;
   const int me = min(p.M, mb + p.m_split);
-  const int nst = me > mb ? (me - mb + kWgBM - 1) / kWgBM : 0;
+  const int nst = me > mb ? (me - mb + BM - 1) / BM : 0;
 
   const int t = threadIdx.x, lane = t & 63, wave = __builtin_amdgcn_readfirstlane(t >> 6);
   const int wn = wave >> 1, wk = wave & 1;
   const bool do_bias = __builtin_amdgcn_readfirstlane(p.bias && k0 == 0 && wk == 0);
 
-  // this lane's part of each of the wave's 4 wave-instructions per operand tile:
-  // instruction i covers tile rows 4j .. 4j+3 with j = 4*wave + i
+  // this lane's part of each of the wave's IPW wave-instructions per operand tile:
+  // instruction i covers tile rows 4j .. 4j+3 with j = IPW*wave + i
   const int lr = lane >> 4, slot = lane & 15;
   auto issue = [&](int st) {
-    uint8_t* A = smem + (st % kWgStages) * kWgStageBytes;
-    uint8_t* B = A + kWgTileBytes;
-    const int m_base = mb + st * kWgBM;
+    uint8_t* A = smem + (st % kWgStages) * SB;
+    uint8_t* B = A + TB;
+    const int m_base = mb + st * BM;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int j = 4 * wave + i;
+    for (int i = 0; i < IPW; ++i) {
+      const int j = IPW * wave + i;
       const int r = 4 * j + lr;
       const int ch = slot ^ (((r & 3) << 2) | ((r >> 2) & 3));
       const int m = m_base + r;
@@ -354,21 +371,18 @@ __global__ __launch_bounds__(kWgThreads, 1) void wgrad_glds_kernel(WgradArgs p) 
     if (s0 < nst) issue(s0);
   for (int st = 0; st < nst; ++st) {
     // stage st has landed once at most min(D - 1, nst - 1 - st) later stages are outstanding
-    // (8 LDS-DMA instructions per stage per lane)
-    const int ahead = min(D - 1, nst - 1 - st);
-    if (D >= 3 && ahead >= 2) wg_wait_vm<16>();
-    else if (D >= 2 && ahead == 1) wg_wait_vm<8>();
-    else wg_wait_vm<0>();
+    // (PER LDS-DMA instructions per stage per lane)
+    wg_wait_ahead<PER>(min(D - 1, nst - 1 - st));
     __builtin_amdgcn_s_barrier();  // every wave's DMA of stage st landed; stage st-1 fully read
     if (st + D < nst) issue(st + D);  // refills the buffer of stage st-1
-    const uint8_t* A = smem + (st % kWgStages) * kWgStageBytes;
-    const uint8_t* B = A + kWgTileBytes;
+    const uint8_t* A = smem + (st % kWgStages) * SB;
+    const uint8_t* B = A + TB;
     wg_bf16x8 a0 = wg_frag_at(A, oa0l, oa0h), a1 = wg_frag_at(A, oa1l, oa1h);
     wg_bf16x8 b0 = wg_frag_at(B, ob0l, ob0h), b1 = wg_frag_at(B, ob1l, ob1h);
 #pragma unroll
-    for (int kk = 0; kk < kWgBM / 16; ++kk) {
+    for (int kk = 0; kk < BM / 16; ++kk) {
       wg_bf16x8 na0 = a0, na1 = a1, nb0 = b0, nb1 = b1;
-      if (kk + 1 < kWgBM / 16) {
+      if (kk + 1 < BM / 16) {
         const uint8_t* An = A + 4096 * (kk + 1);
         const uint8_t* Bn = B + 4096 * (kk + 1);
         na0 = wg_frag_at(An, oa0l, oa0h); na1 = wg_frag_at(An, oa1l, oa1h);
@@ -389,6 +403,194 @@ __global__ __launch_bounds__(kWgThreads, 1) void wgrad_glds_kernel(WgradArgs p) 
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   }
   wgrad_epilogue(p, split, n0, k0, wn, wk, lane, c00, c01, c10, c11, cb0, cb1, do_bias);
+}
+
+// ---------------------------------------------------------------------------------------------
+// Wide tile: 256 x 256 outputs per workgroup, 8 waves as 2 (n) x 4 (k), each a 128 x 64 sub-tile
+// (4 x 2 MFMA tiles, 128 fp32 accumulators per lane).  Twice the MFMA work per operand byte of
+// the 128 x 128 tile (128 vs 64 FLOP per byte staged), which is what the LDS-DMA fill rate
+// per CU limits (MI355X_MICROARCH.md, ldsdma-fill): 6 fragment reads feed 8 MFMAs per k-step.
+// An operand stage is two 128-column halves, each the 256-byte-row swizzled image above, so
+// the fragment addressing is unchanged.  The bias gradient is a v_dot2c_f32_bf16 against ones
+// on the dY fragments the n-waves already hold (4 dot2 per fragment, no extra MFMA or
+// accumulator tile).
+constexpr int kWwTile = 256;
+constexpr int kWwThreads = 512;
+
+template <int kStages, int BM>
+__global__ __launch_bounds__(kWwThreads, 1) void wgrad_wide_kernel(WgradArgs p) {
+  constexpr int TH = BM * kWgRowBytes;   // bytes per operand half (BM rows x 128 columns)
+  constexpr int TB = 2 * TH;             // bytes per operand tile
+  constexpr int SB = 2 * TB;             // bytes per stage
+  constexpr int IPW = BM / 16;           // LDS-DMA wave-instructions per wave per operand tile
+  constexpr int PER = 2 * IPW;           // per lane per stage
+  constexpr int QR = BM / 4;             // wave-instructions per operand half
+  static_assert(BM % 16 == 0 && BM <= 64, "stage depth");
+  __shared__ __attribute__((aligned(16))) uint8_t smem[kStages * SB];
+  typedef __attribute__((address_space(3))) void lds_void;
+
+  int bid = blockIdx.x;
+  if (p.remap) bid = (bid & 7) * int(gridDim.x >> 3) + (bid >> 3);
+  const int split = bid % p.S;
+  const int tile = bid / p.S;
+  const int n0 = (tile / p.tiles_k) * kWwTile;
+  const int k0 = (tile % p.tiles_k) * kWwTile;
+  const int mb = split * p.m_split;
+  const int me = min(p.M, mb + p.m_split);
+  const int nst = me > mb ? (me - mb + BM - 1) / BM : 0;
+
+  const int t = threadIdx.x, lane = t & 63, wave = __builtin_amdgcn_readfirstlane(t >> 6);
+  const int wn = wave >> 2, wk = wave & 3;
+  const bool do_bias = __builtin_amdgcn_readfirstlane(p.bias && k0 == 0 && wk == 0);
+
+  const int lr = lane >> 4, slot = lane & 15;
+  auto issue = [&](int st) {
+    uint8_t* A = smem + (st % kStages) * SB;
+    uint8_t* B = A + TB;
+    const int m_base = mb + st * BM;
+#pragma unroll
+    for (int i = 0; i < IPW; ++i) {
+      const int j = IPW * wave + i;          // 0 .. 2*QR-1
+      const int half = j / QR, rq = j % QR;  // rows 4rq .. 4rq+3 of column half ``half``
+      const int r = 4 * rq + lr;
+      const int ch = slot ^ (((r & 3) << 2) | ((r >> 2) & 3));
+      const int m = m_base + r;
+      const bool okm = m < me;
+      const int cn = min(n0 + half * 128 + ch * 8, p.N - 8);
+      const int ck = min(k0 + half * 128 + ch * 8, p.K - 8);
+      const uint16_t* ga = okm ? p.dy + int64_t(m) * p.ldy + cn : p.zero;
+      const uint16_t* gb = okm ? p.x + int64_t(m) * p.ldx + ck : p.zero;
+      const int lo = half * TH + 1024 * rq;
+      wg_dma16(ga, __builtin_amdgcn_readfirstlane(uint32_t(size_t((lds_void*)(A + lo)))));
+      wg_dma16(gb, __builtin_amdgcn_readfirstlane(uint32_t(size_t((lds_void*)(B + lo)))));
+    }
+  };
+
+  wg_f32x16 c[4][2];
+#pragma unroll
+  for (int f = 0; f < 4; ++f)
+#pragma unroll
+    for (int e = 0; e < 2; ++e)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) c[f][e][i] = 0.f;
+  float bs[4] = {0.f, 0.f, 0.f, 0.f};
+
+  const int g = lane >> 4, i16 = lane & 15, q = i16 >> 2, pp = i16 & 3, h = lane >> 5;
+  const int bo = 8 * (pp & 1);
+  const int r0 = 8 * h + q;
+  const int cbase = 2 * (g & 1) + (pp >> 1);
+  int oa[4][2], ob[2][2];
+#pragma unroll
+  for (int f = 0; f < 4; ++f) {
+    oa[f][0] = wn * TH + wg_swz(r0, cbase + 4 * f) + bo;
+    oa[f][1] = wn * TH + wg_swz(r0 + 4, cbase + 4 * f) + bo;
+  }
+  const int kc = 8 * (wk & 1);  // 64-column quarter within the k half, in 8-column chunks
+#pragma unroll
+  for (int e = 0; e < 2; ++e) {
+    ob[e][0] = (wk >> 1) * TH + wg_swz(r0, kc + cbase + 4 * e) + bo;
+    ob[e][1] = (wk >> 1) * TH + wg_swz(r0 + 4, kc + cbase + 4 * e) + bo;
+  }
+  typedef __bf16 wg_bf16x2 __attribute__((ext_vector_type(2)));
+  const wg_bf16x2 one2 = {static_cast<__bf16>(1.0f), static_cast<__bf16>(1.0f)};
+
+  // Pipelined across stages: the wait + barrier for stage st+1 and its first fragment reads
+  // sit in front of the MFMAs of stage st's last k-step, so the reads' LDS latency hides
+  // behind those MFMAs instead of stalling every wave after every barrier.  The refill issued
+  // at that barrier overwrites stage st-1's buffer (consumed by MFMAs before the barrier), so
+  // D = kStages - 2 stages are in flight beyond the one being waited for.
+  static_assert(kStages >= 3, "cross-stage pipelining needs >= 3 ring stages");
+  constexpr int D = kStages - 2;
+  constexpr int KS = BM / 16;
+  auto load_frags = [&](int st, int kk, wg_bf16x8 (&fa)[4], wg_bf16x8 (&fb)[2]) {
+    const uint8_t* A = smem + (st % kStages) * SB + 4096 * kk;
+    const uint8_t* B = A + TB;
+#pragma unroll
+    for (int f = 0; f < 4; ++f) fa[f] = wg_frag_at(A, oa[f][0], oa[f][1]);
+#pragma unroll
+    for (int e = 0; e < 2; ++e) fb[e] = wg_frag_at(B, ob[e][0], ob[e][1]);
+  };
+#pragma unroll
+  for (int s0 = 0; s0 <= D; ++s0)
+    if (s0 < nst) issue(s0);
+  wg_bf16x8 a[4], b[2];
+  if (nst > 0) {
+    wg_wait_ahead<PER>(min(D, nst - 1));
+    __builtin_amdgcn_s_barrier();
+    load_frags(0, 0, a, b);
+  }
+  for (int st = 0; st < nst; ++st) {
+#pragma unroll
+    for (int kk = 0; kk < KS; ++kk) {
+      wg_bf16x8 na[4], nb[2];
+      if (kk + 1 < KS) {
+        load_frags(st, kk + 1, na, nb);
+      } else if (st + 1 < nst) {
+        wg_wait_ahead<PER>(min(D - 1, nst - 2 - st));
+        __builtin_amdgcn_s_barrier();  // stage st+1 landed everywhere; stage st-1 fully read
+        if (st + 1 + D < nst) issue(st + 1 + D);
+        load_frags(st + 1, 0, na, nb);
+      }
+#pragma unroll
+      for (int f = 0; f < 4; ++f)
+#pragma unroll
+        for (int e = 0; e < 2; ++e) c[f][e] = wg_mfma(a[f], b[e], c[f][e]);
+      if (do_bias) {
+#pragma unroll
+        for (int f = 0; f < 4; ++f) {
+          const uint4 u = __builtin_bit_cast(uint4, a[f]);
+          bs[f] = __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(wg_bf16x2, u.x), one2, bs[f], false);
+          bs[f] = __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(wg_bf16x2, u.y), one2, bs[f], false);
+          bs[f] = __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(wg_bf16x2, u.z), one2, bs[f], false);
+          bs[f] = __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(wg_bf16x2, u.w), one2, bs[f], false);
+        }
+      }
+#pragma unroll
+      for (int f = 0; f < 4; ++f) a[f] = na[f];
+#pragma unroll
+      for (int e = 0; e < 2; ++e) b[e] = nb[e];
+    }
+  }
+
+  // epilogue (C lane map as in wgrad_epilogue)
+  const int col_l = lane & 31;
+#pragma unroll
+  for (int f = 0; f < 4; ++f) {
+#pragma unroll
+    for (int e = 0; e < 2; ++e) {
+      const int col = k0 + (wk >> 1) * 128 + (wk & 1) * 64 + 32 * e + col_l;
+      if (col < p.K) {
+#pragma unroll
+        for (int reg = 0; reg < 16; ++reg) {
+          const int row = n0 + wn * 128 + 32 * f + (reg & 3) + 8 * (reg >> 2) + 4 * h;
+          if (row < p.N) {
+            if (p.S == 1) {
+              uint16_t* o = p.dw + int64_t(row) * p.ldw + col;
+              const float v = c[f][e][reg] + (p.accumulate ? bf2f(*o) : 0.f);
+              *o = f2bf(v);
+            } else {
+              p.ws[(int64_t(split) * p.N + row) * p.K + col] = c[f][e][reg];
+            }
+          }
+        }
+      }
+    }
+  }
+  if (do_bias) {
+    // lane l (< 32) and l + 32 hold tokens 8h..8h+7 of every k-step for row 32f + l
+#pragma unroll
+    for (int f = 0; f < 4; ++f) {
+      const float tot = bs[f] + __shfl_xor(bs[f], 32);
+      const int row = n0 + wn * 128 + 32 * f + col_l;
+      if (h == 0 && row < p.N) {
+        if (p.S == 1) {
+          p.db[row] = f2bf(tot + (p.accumulate ? bf2f(p.db[row]) : 0.f));
+        } else {
+          p.ws[int64_t(p.S) * p.N * p.K + int64_t(split) * p.N + row] = tot;
+        }
+      }
+    }
+  }
 }
 
 // dW[n][k] (+)= sum_s ws[s][n][k]; db[n] (+)= sum_s wsb[s][n].  4 columns per thread (K % 8 == 0).
@@ -432,10 +634,10 @@ struct WgradPlan {
   int S, m_split, tiles_k, grid;
 };
 
-WgradPlan wgrad_plan(int M, int N, int K, int splits) {
+WgradPlan wgrad_plan(int M, int N, int K, int splits, int tile = kWgBN) {
   WgradPlan pl;
-  const int tiles_n = (N + kWgBN - 1) / kWgBN;
-  pl.tiles_k = (K + kWgBK - 1) / kWgBK;
+  const int tiles_n = (N + tile - 1) / tile;
+  pl.tiles_k = (K + tile - 1) / tile;
   int S = std::max(1, splits);
   const int per = (M + S - 1) / S;
   pl.m_split = std::max(kWgBM, (per + kWgBM - 1) / kWgBM * kWgBM);
@@ -459,7 +661,8 @@ void wgrad_gemm(uintptr_t dy, int64_t ldy, uintptr_t x, int64_t ldx, uintptr_t d
   VODA_CHECK(ldy >= N && ldx >= K && ldw >= K, "wgrad: leading dimension too small");
   VODA_CHECK(ldy % 8 == 0 && ldx % 8 == 0 && ldw % 8 == 0, "wgrad: rows must be 16-byte aligned");
   VODA_CHECK(dy % 16 == 0 && x % 16 == 0 && dw % 16 == 0, "wgrad: operands must be 16-byte aligned");
-  const WgradPlan pl = wgrad_plan(M, N, K, splits);
+  const bool wide = variant >= 6;
+  const WgradPlan pl = wgrad_plan(M, N, K, splits, wide ? kWwTile : kWgBN);
   VODA_CHECK(pl.S == 1 || ws != 0, "wgrad: split-K needs a workspace");
   VODA_CHECK(variant == 0 || (zero != 0 && zero % 16 == 0), "wgrad: the LDS-DMA variant needs a zero buffer");
   WgradArgs a;
@@ -474,15 +677,25 @@ void wgrad_gemm(uintptr_t dy, int64_t ldy, uintptr_t x, int64_t ldx, uintptr_t d
   a.accumulate = accumulate ? 1 : 0;
   a.bias = db != 0 ? 1 : 0;
   hipStream_t s = as_stream(stream);
-  VODA_CHECK(variant >= 0 && variant <= 3, "wgrad: variant must be 0..3");
+  VODA_CHECK(variant >= 0 && variant <= 8, "wgrad: variant must be 0..8");
   if (variant == 0)
     hipLaunchKernelGGL(wgrad_kernel, dim3(unsigned(pl.grid)), dim3(kWgThreads), 0, s, a);
   else if (variant == 1)
-    hipLaunchKernelGGL(wgrad_glds_kernel<4>, dim3(unsigned(pl.grid)), dim3(kWgThreads), 0, s, a);
+    hipLaunchKernelGGL((wgrad_glds_kernel<4, 64>), dim3(unsigned(pl.grid)), dim3(kWgThreads), 0, s, a);
   else if (variant == 2)
-    hipLaunchKernelGGL(wgrad_glds_kernel<2>, dim3(unsigned(pl.grid)), dim3(kWgThreads), 0, s, a);
+    hipLaunchKernelGGL((wgrad_glds_kernel<2, 64>), dim3(unsigned(pl.grid)), dim3(kWgThreads), 0, s, a);
+  else if (variant == 3)
+    hipLaunchKernelGGL((wgrad_glds_kernel<3, 64>), dim3(unsigned(pl.grid)), dim3(kWgThreads), 0, s, a);
+  else if (variant == 4)
+    hipLaunchKernelGGL((wgrad_glds_kernel<4, 32>), dim3(unsigned(pl.grid)), dim3(kWgThreads), 0, s, a);
+  else if (variant == 5)
+    hipLaunchKernelGGL((wgrad_glds_kernel<5, 32>), dim3(unsigned(pl.grid)), dim3(kWgThreads), 0, s, a);
+  else if (variant == 6)
+    hipLaunchKernelGGL((wgrad_wide_kernel<4, 32>), dim3(unsigned(pl.grid)), dim3(kWwThreads), 0, s, a);
+  else if (variant == 7)
+    hipLaunchKernelGGL((wgrad_wide_kernel<5, 32>), dim3(unsigned(pl.grid)), dim3(kWwThreads), 0, s, a);
   else
-    hipLaunchKernelGGL(wgrad_glds_kernel<3>, dim3(unsigned(pl.grid)), dim3(kWgThreads), 0, s, a);
+    hipLaunchKernelGGL((wgrad_wide_kernel<3, 32>), dim3(unsigned(pl.grid)), dim3(kWwThreads), 0, s, a);
   check_launch();
   if (pl.S > 1) {
     const int64_t work = (int64_t(N) * K) / 4 + (db != 0 ? N : 0);

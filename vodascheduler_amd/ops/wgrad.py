@@ -17,8 +17,9 @@ import torch
 from . import _native as N
 
 TILE = 128
-# 0: register-staged LDS double buffer; 1 / 2 / 3: LDS ring of 4 / 2 / 3 stages filled by
-# global_load_lds.  Default 2 (64 KB ring, 2 workgroups per CU): fastest in the BERT-base step
+# 0: register-staged LDS double buffer; 1 / 2 / 3: LDS ring of 4 / 2 / 3 stages of 64 tokens
+# filled by global_load_lds; 4 / 5: ring of 4 / 5 stages of 32 tokens; 6 / 7 / 8: 256 x 256
+# tile, 8 waves, ring of 4 x 32 / 2 x 64 / 3 x 32 tokens.  Default 2 (64 KB ring, 2 workgroups per CU): fastest in the BERT-base step
 # on MI355X (profiles/r1_wgrad_v3.md)
 VARIANT = int(os.environ.get("VODA_WGRAD_VARIANT", "2"))
 _ZERO: dict[torch.device, torch.Tensor] = {}
@@ -32,13 +33,21 @@ def _zero_rows(device: torch.device) -> torch.Tensor:
     return z
 
 
-def default_splits(M: int, N_: int, K: int, target_blocks: int = 432) -> int:
+WIDE_TILE = 256  # variants 6-8: 256 x 256 outputs per workgroup, one workgroup per CU
+
+
+def default_splits(M: int, N_: int, K: int, target_blocks: int | None = None, variant: int | None = None) -> int:
     """Split the token dimension until the grid is ~1.7 waves of workgroups on the 256 CUs
     (two fit per CU), keeping >= 4 k-stages of 64 tokens per split.  Measured optimum on
     MI355X for the BERT-base shapes (benchmarks/bench_wgrad.py, profiles/): 12 splits for
     768x768 (36 tiles), 4 for 2304x768, 3 for 3072x768 / 768x3072.  Convolution-sized token
-    counts (ResNet 1x1 convs: 800k rows, 2-32 tiles) go up to 256 splits."""
-    tiles = math.ceil(N_ / TILE) * math.ceil(K / TILE)
+    counts (ResNet 1x1 convs: 800k rows, 2-32 tiles) go up to 256 splits.  The wide-tile
+    variants (one 512-thread workgroup per CU) aim at one wave of 256 workgroups."""
+    v = VARIANT if variant is None else int(variant)
+    tile = WIDE_TILE if v >= 6 else TILE
+    if target_blocks is None:
+        target_blocks = 256 if v >= 6 else 432
+    tiles = math.ceil(N_ / tile) * math.ceil(K / tile)
     s = math.ceil(target_blocks / tiles)
     return max(1, min(s, 256, M // 256 if M >= 256 else 1))
 
@@ -92,11 +101,11 @@ def wgrad_accumulate_(dy2: torch.Tensor, x2: torch.Tensor, gw: torch.Tensor, gb:
                          f"x {tuple(x2.shape)} {x2.dtype} stride {x2.stride()}, dw {tuple(gw.shape)} {gw.dtype}")
     M, N_ = dy2.shape
     K = x2.shape[1]
-    s = splits if splits is not None else default_splits(M, N_, K)
+    v = VARIANT if variant is None else int(variant)
+    s = splits if splits is not None else default_splits(M, N_, K, variant=v)
     h = N.hip()
     nws = h.wgrad_workspace_floats(M, N_, K, s)
     ws = torch.empty(nws, dtype=torch.float32, device=dy2.device) if nws else None
-    v = VARIANT if variant is None else int(variant)
     h.wgrad_gemm(dy2.data_ptr(), dy2.stride(0), x2.data_ptr(), x2.stride(0), gw.data_ptr(), gw.stride(0),
                  N.ptr(gb), M, N_, K, s, N.ptr(ws), bool(accumulate), _zero_rows(dy2.device).data_ptr(), v,
                  N.stream_of(dy2))
