@@ -5,12 +5,19 @@
 //   * linear_assignment: square and rectangular (both orientations), min and max, against
 //     enumeration of all injective row -> column maps;
 //   * ffdl_dp: against enumeration of all allocations within [min, max] (or 0 when allowed).
+//   * with the argument ``threads``: 8 threads call both entry points concurrently on their own
+//     random problems and compare with the single-threaded answers (the Python bindings release
+//     the GIL, so concurrent calls from scheduler/placement threads are real); built with
+//     ThreadSanitizer for this mode.
 // Exit status 0 and "selftest OK" on success.
 #include <algorithm>
 #include <cmath>
 #include <cstdio>
 #include <functional>
+#include <atomic>
+#include <cstring>
 #include <random>
+#include <thread>
 #include <vector>
 
 #include "../vodacore.h"
@@ -122,7 +129,57 @@ int check_ffdl(std::mt19937& rng) {
 
 }  // namespace
 
-int main() {
+// Each thread solves the same seeded problem sequence; the answers must match the serial run.
+int check_threads() {
+  constexpr int kThreads = 8, kIters = 40;
+  auto run = [](unsigned seed, std::vector<double>& out) {
+    std::mt19937 rng(seed);
+    std::uniform_real_distribution<double> u(0.0, 10.0);
+    for (int it = 0; it < kIters; ++it) {
+      const int rows = 2 + int(rng() % 9), cols = 2 + int(rng() % 9);
+      std::vector<double> c(size_t(rows) * cols);
+      for (auto& v : c) v = u(rng);
+      const std::vector<int> a = vodacore::linear_assignment(c, rows, cols, (it & 1) != 0);
+      out.push_back(assignment_cost(c, rows, cols, a));
+      const int jobs = 1 + int(rng() % 5), gpus = 1 + int(rng() % 8);
+      std::vector<std::vector<double>> sp(jobs);
+      std::vector<int> mn(jobs), mx(jobs);
+      for (int j = 0; j < jobs; ++j) {
+        mn[j] = 1;
+        mx[j] = 1 + int(rng() % gpus);
+        sp[j].assign(size_t(mx[j]) + 1, 0.0);
+        for (int g = 1; g <= mx[j]; ++g) sp[j][g] = sp[j][g - 1] + u(rng) / g;
+      }
+      out.push_back(vodacore::ffdl_dp(sp, mn, mx, gpus, true).first);
+    }
+  };
+  std::vector<std::vector<double>> serial(kThreads), par(kThreads);
+  for (int t = 0; t < kThreads; ++t) run(1000u + t, serial[t]);
+  std::atomic<int> go{0};
+  std::vector<std::thread> th;
+  for (int t = 0; t < kThreads; ++t)
+    th.emplace_back([&, t] {
+      while (!go.load()) std::this_thread::yield();
+      run(1000u + t, par[t]);
+    });
+  go.store(1);
+  for (auto& x : th) x.join();
+  int bad = 0;
+  for (int t = 0; t < kThreads; ++t)
+    if (serial[t] != par[t]) ++bad;
+  return bad;
+}
+
+int main(int argc, char** argv) {
+  if (argc > 1 && std::strcmp(argv[1], "threads") == 0) {
+    const int bad = check_threads();
+    if (bad) {
+      std::printf("selftest FAILED: %d thread(s) disagree with the serial run\n", bad);
+      return 1;
+    }
+    std::printf("selftest OK\n");
+    return 0;
+  }
   std::mt19937 rng(12345);
   int bad = check_assignment(rng) + check_ffdl(rng);
   // error paths must throw, not corrupt memory

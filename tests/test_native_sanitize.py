@@ -1,4 +1,5 @@
-"""Host native core under AddressSanitizer + UndefinedBehaviorSanitizer.
+"""Host native core under AddressSanitizer + UndefinedBehaviorSanitizer and ThreadSanitizer
+(SURVEY.md §5.2).
 
 Builds csrc/host/tests/selftest.cpp together with the sources of the ``_vodacore``
 extension (Hungarian assignment, FfDL dynamic program) as a standalone executable with
@@ -28,3 +29,23 @@ def test_host_core_clean_under_asan_ubsan(tmp_path):
     r = subprocess.run([exe], capture_output=True, text=True, timeout=300, env=env)
     assert r.returncode == 0 and "selftest OK" in r.stdout, (r.stdout[-2000:], r.stderr[-3000:])
     assert "runtime error" not in r.stderr and "AddressSanitizer" not in r.stderr, r.stderr[-3000:]
+
+
+@pytest.mark.skipif(shutil.which("g++") is None, reason="needs g++")
+def test_host_core_concurrent_calls_clean_under_tsan(tmp_path):
+    """The bindings release the GIL, so placement / allocator threads can run the Hungarian
+    solver and the FfDL DP at the same time: 8 threads under ThreadSanitizer must agree with
+    the serial answers and produce no race report."""
+    exe = str(tmp_path / "voda_selftest_tsan")
+    srcs = [os.path.join(HOST, "tests", "selftest.cpp"), os.path.join(HOST, "hungarian.cpp"),
+            os.path.join(HOST, "ffdl.cpp")]
+    cmd = ["g++", "-std=c++17", "-O1", "-g", "-fno-omit-frame-pointer", "-fsanitize=thread", "-pthread",
+           f"-I{HOST}", *srcs, "-o", exe]
+    b = subprocess.run(cmd, capture_output=True, text=True, timeout=300)
+    assert b.returncode == 0, b.stderr[-3000:]
+    env = dict(os.environ, TSAN_OPTIONS="halt_on_error=1:second_deadlock_stack=1")
+    r = subprocess.run([exe, "threads"], capture_output=True, text=True, timeout=300, env=env)
+    if r.returncode != 0 and "unexpected memory mapping" in r.stderr:
+        pytest.skip("ThreadSanitizer runtime cannot map its shadow memory on this kernel")
+    assert r.returncode == 0 and "selftest OK" in r.stdout, (r.stdout[-2000:], r.stderr[-3000:])
+    assert "ThreadSanitizer" not in r.stderr, r.stderr[-3000:]
