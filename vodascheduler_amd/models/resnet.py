@@ -16,7 +16,7 @@ import torch
 from torch import nn
 
 from ..ops.batchnorm import FusedBatchNorm2d
-from ..ops.conv1x1 import Conv1x1
+from ..ops.conv1x1 import USE_GRAD_SINK, Conv1x1, GradSink
 from ..ops.pool import FusedMaxPool2d
 
 
@@ -35,9 +35,21 @@ class Bottleneck(nn.Module):
         self.downsample = downsample
 
     def forward(self, x):
-        out = self.bn1(self.conv1(x))
+        # x feeds conv1 and the shortcut: the shortcut's input gradient is handed to conv1's
+        # input-gradient GEMM (beta = 1) instead of being added by autograd (ops/conv1x1.GradSink)
+        sink = None
+        if (USE_GRAD_SINK and self.training and torch.is_grad_enabled() and x.requires_grad
+                and self.conv1._gemm_ok(x)):
+            sink = GradSink()
+        out = self.bn1(self.conv1(x, sink_in=sink))
         out = self.bn2(self.conv2(out))
-        idt = x if self.downsample is None else self.downsample(x)
+        if self.downsample is None:
+            return self.bn3(self.conv3(out), x, sink=sink)
+        ds = self.downsample
+        if isinstance(ds, nn.Sequential) and len(ds) == 2 and isinstance(ds[0], Conv1x1):
+            idt = ds[1](ds[0](x, sink_out=sink))
+        else:
+            idt = ds(x)
         return self.bn3(self.conv3(out), idt)
 
 

@@ -47,7 +47,7 @@ def _direct_fp32(p) -> bool:
 
 class _BNActFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, residual, weight, bias, running_mean, running_var, momentum, eps, relu):
+    def forward(ctx, x, residual, weight, bias, running_mean, running_var, momentum, eps, relu, sink=None):
         C = x.shape[1]
         M = x.numel() // C
         h = N.hip()
@@ -63,6 +63,7 @@ class _BNActFn(torch.autograd.Function):
         ctx.relu = bool(relu)
         ctx.has_res = residual is not None
         ctx.bias = bias
+        ctx.sink = sink if residual is not None else None
         ctx.save_for_backward(x, mask, weight, save_mean, save_invstd)
         return y
 
@@ -91,13 +92,16 @@ class _BNActFn(torch.autograd.Function):
         h.bn_bwd(dy.data_ptr(), N.ptr(mask), x.data_ptr(), save_mean.data_ptr(), save_invstd.data_ptr(), N.ptr(weight),
                  dx.data_ptr(), N.ptr(dres), N.ptr(dw), N.ptr(db), ws.data_ptr(), M, C, ctx.relu, direct,
                  N.dtype_code(x.dtype), N.stream_of(x))
-        if dres is None and ctx.has_res and ctx.needs_input_grad[1]:
+        if dres is not None and ctx.sink is not None:
+            ctx.sink.put(dres)  # a fresh tensor: the consumer may accumulate into it in place
+            dres = None
+        if dres is None and ctx.has_res and ctx.needs_input_grad[1] and ctx.sink is None:
             dres = dy
         if direct:
             _ready(weight)
             _ready(bias)
-            return dx, dres, None, None, None, None, None, None, None
-        return dx, dres, dw, db, None, None, None, None, None
+            return dx, dres, None, None, None, None, None, None, None, None
+        return dx, dres, dw, db, None, None, None, None, None, None
 
 
 def _reference(x, weight, bias, running_mean, running_var, training, momentum, eps, residual, relu):
@@ -110,11 +114,16 @@ def _reference(x, weight, bias, running_mean, running_var, training, momentum, e
 def batch_norm_act(x: torch.Tensor, weight: torch.Tensor | None, bias: torch.Tensor | None,
                    running_mean: torch.Tensor | None, running_var: torch.Tensor | None, training: bool = True,
                    momentum: float = 0.1, eps: float = 1e-5, residual: torch.Tensor | None = None,
-                   relu: bool = True) -> torch.Tensor:
-    if not _supported(x, residual):
+                   relu: bool = True, sink=None) -> torch.Tensor:
+    """``sink``: hand the residual's gradient to a consumer (ops/conv1x1.GradSink) instead of
+    returning it; ignored (gradient returned normally) on the reference path."""
+    # the kernels read gamma / beta / running statistics as fp32 (normalisation parameters
+    # stay fp32 under cast_compute_weights_); anything else takes the reference path
+    params_fp32 = all(t is None or t.dtype == torch.float32 for t in (weight, bias, running_mean, running_var))
+    if not params_fp32 or not _supported(x, residual):
         return _reference(x, weight, bias, running_mean, running_var, training, momentum, eps, residual, relu)
     if training or running_mean is None:
-        return _BNActFn.apply(x, residual, weight, bias, running_mean, running_var, momentum, eps, relu)
+        return _BNActFn.apply(x, residual, weight, bias, running_mean, running_var, momentum, eps, relu, sink)
     # inference: per-channel affine from the running statistics, one apply pass
     C = x.shape[1]
     invstd = torch.rsqrt(running_var.float() + eps)
@@ -151,7 +160,7 @@ class FusedBatchNorm2d(torch.nn.BatchNorm2d):
             self.num_batches_tracked.add_(n)
             self._pending_batches = 0
 
-    def forward(self, x, residual=None):
+    def forward(self, x, residual=None, sink=None):
         if self.training and self.track_running_stats:
             if self.momentum is None:  # cumulative average needs the device count now
                 self.num_batches_tracked.add_(1)
@@ -163,11 +172,11 @@ class FusedBatchNorm2d(torch.nn.BatchNorm2d):
             with torch.autocast("cuda", enabled=False):  # keep the activation dtype, fp32 stats
                 return batch_norm_act(x, self.weight, self.bias, self.running_mean if self.track_running_stats
                                       else None, self.running_var if self.track_running_stats else None,
-                                      use_batch, momentum, self.eps, residual, self.relu)
+                                      use_batch, momentum, self.eps, residual, self.relu, sink)
         return batch_norm_act(x, self.weight, self.bias,
                               self.running_mean if self.track_running_stats else None,
                               self.running_var if self.track_running_stats else None,
-                              use_batch, momentum, self.eps, residual, self.relu)
+                              use_batch, momentum, self.eps, residual, self.relu, sink)
 
     def extra_repr(self):
         return super().extra_repr() + f", relu={self.relu}"
