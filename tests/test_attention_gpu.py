@@ -111,3 +111,32 @@ def test_bert_layer_uses_fused_attention_kernel():
     y.float().mean().backward()
     assert torch.isfinite(y.float()).all()
     assert all(torch.isfinite(p.grad.float()).all() for p in m.parameters() if p.grad is not None)
+
+
+@pytest.mark.gpu
+def test_bert_residual_grad_sink_gpu(monkeypatch):
+    """BERT-base layer stack on the GPU path (bf16 weights, fused attention / LayerNorm):
+    residual-stream gradient hand-off on vs off agree to bf16 accuracy."""
+    import vodascheduler_amd.models.layers as L
+    from vodascheduler_amd.models import cast_compute_weights_
+    from vodascheduler_amd.models.transformer import BertBase
+
+    torch.manual_seed(0)
+    m = cast_compute_weights_(BertBase(vocab=1000, seq_len=64, layers=2).cuda())
+    ids = torch.randint(1, 1000, (4, 64), device="cuda")
+
+    def run(on):
+        monkeypatch.setattr(L, "USE_GRAD_SINK", on)
+        m.zero_grad(set_to_none=True)
+        with torch.autocast("cuda", dtype=torch.bfloat16):
+            out = m(ids, torch.ones_like(ids, dtype=torch.bool)).float()
+        out.square().mean().backward()
+        return {n: p.grad.detach().float().clone() for n, p in m.named_parameters() if p.grad is not None}
+
+    run(False)
+    g0 = run(False)
+    g1 = run(True)
+    assert set(g0) == set(g1)
+    for n in g0:
+        rel = float((g1[n] - g0[n]).norm() / g0[n].norm().clamp_min(1e-12))
+        assert rel < 3e-2, (n, rel)

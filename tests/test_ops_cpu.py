@@ -158,3 +158,32 @@ def test_fused_bn_batches_tracked_and_state_dict():
     m2.load_state_dict(m.state_dict())
     m2(torch.randn(2, 8, 3, 3))
     assert int(m2.state_dict()["num_batches_tracked"]) == 4
+
+
+def test_encoder_residual_grad_sink_matches_autograd(monkeypatch):
+    """The residual-stream gradient handed to the sublayer's first GEMM (ops/dense.residual_add
+    + FusedLinear sink_in) equals autograd's sum, and the hand-off is actually taken."""
+    import vodascheduler_amd.models.layers as L
+    from vodascheduler_amd.ops import conv1x1 as C
+
+    torch.manual_seed(0)
+    m = L.EncoderLayer(64, 4, 128, act="gelu")
+    x = torch.randn(2, 10, 64)
+    taken = []
+    orig = C.GradSink.take
+    monkeypatch.setattr(C.GradSink, "take", lambda self: (lambda g: (taken.append(g is not None), g)[1])(orig(self)))
+
+    def run(on):
+        monkeypatch.setattr(L, "USE_GRAD_SINK", on)
+        xi = x.clone().requires_grad_(True)
+        m.zero_grad()
+        m(xi).square().sum().backward()
+        return xi.grad.clone(), [p.grad.clone() for p in m.parameters()]
+
+    dx0, g0 = run(False)
+    assert taken == []
+    dx1, g1 = run(True)
+    assert taken == [True, True]
+    torch.testing.assert_close(dx1, dx0)
+    for a, b in zip(g1, g0):
+        torch.testing.assert_close(a, b)

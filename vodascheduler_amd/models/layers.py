@@ -17,7 +17,8 @@ import torch.nn.functional as F
 from torch import nn
 
 from ..ops.attention import attention_q_kvpacked, attention_qkvpacked
-from ..ops.dense import FusedLinear
+from ..ops.conv1x1 import USE_GRAD_SINK, GradSink
+from ..ops.dense import FusedLinear, residual_add
 from ..ops.layernorm import FusedLayerNorm
 
 
@@ -40,14 +41,15 @@ class MultiHeadAttention(nn.Module):
         self.dropout = dropout
 
     def forward(self, x: torch.Tensor, kv: torch.Tensor | None = None, key_mask: torch.Tensor | None = None,
-                causal: bool = False) -> torch.Tensor:
-        """x: [B, Tq, D]; kv: [B, Tk, D] (default x); key_mask: [B, Tk] (nonzero = attend)."""
+                causal: bool = False, sink_in=None) -> torch.Tensor:
+        """x: [B, Tq, D]; kv: [B, Tk, D] (default x); key_mask: [B, Tk] (nonzero = attend);
+        sink_in: GradSink of the residual stream x (self-attention only)."""
         B, Tq, _ = x.shape
         E = self.inner
         drop = self.dropout if self.training else 0.0
         scale = 1.0 / math.sqrt(self.dk)
         if kv is None:
-            qkv = self.qkv(x).view(B, Tq, 3, self.h, self.dk)
+            qkv = self.qkv(x, sink_in).view(B, Tq, 3, self.h, self.dk)
             o = attention_qkvpacked(qkv, key_mask, causal, scale, drop)
         else:
             Tk = kv.shape[1]
@@ -65,8 +67,13 @@ class FeedForward(nn.Module):
         self.fc2 = FusedLinear(d_ff, d_model)
         self.act = nn.GELU(approximate="tanh") if act == "gelu" else nn.ReLU()
 
-    def forward(self, x):
-        return self.fc2(self.act(self.fc1(x)))
+    def forward(self, x, sink_in=None):
+        return self.fc2(self.act(self.fc1(x, sink_in)))
+
+
+def _sink(module: nn.Module, x: torch.Tensor) -> GradSink | None:
+    return GradSink() if (USE_GRAD_SINK and module.training and torch.is_grad_enabled()
+                          and x.requires_grad) else None
 
 
 class EncoderLayer(nn.Module):
@@ -81,8 +88,13 @@ class EncoderLayer(nn.Module):
         self.drop = nn.Dropout(dropout)
 
     def forward(self, x, key_mask=None):
-        x = self.ln1(x + self.drop(self.attn(x, key_mask=key_mask)))
-        return self.ln2(x + self.drop(self.ff(x)))
+        # the residual stream x feeds the sublayer's first GEMM and the residual add: its
+        # gradient from the add is accumulated by that GEMM's input-gradient GEMM (beta = 1)
+        # instead of by a separate autograd add (ops/dense.residual_add)
+        s1 = _sink(self, x)
+        x = self.ln1(residual_add(x, self.drop(self.attn(x, key_mask=key_mask, sink_in=s1)), s1))
+        s2 = _sink(self, x)
+        return self.ln2(residual_add(x, self.drop(self.ff(x, sink_in=s2)), s2))
 
 
 class DecoderLayer(nn.Module):

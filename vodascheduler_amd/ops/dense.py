@@ -56,13 +56,16 @@ def colsum_accumulate_(dy2: torch.Tensor, out: torch.Tensor) -> None:
 
 class _DenseFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, weight, bias):
+    def forward(ctx, x, weight, bias, sink_in=None):
+        """``sink_in`` (ops/conv1x1.GradSink): accumulate the input gradient into the
+        residual-stream gradient a producer left there (one GEMM with beta = 1)."""
         if x.dtype != weight.dtype and torch.is_autocast_enabled(x.device.type):
             x = x.to(weight.dtype)
         with torch.autocast(x.device.type, enabled=False):
             y = F.linear(x, weight, bias.to(weight.dtype) if bias is not None else None)
         ctx.save_for_backward(x, weight)
         ctx.bias = bias
+        ctx.sink_in = sink_in
         return y
 
     @staticmethod
@@ -77,7 +80,13 @@ class _DenseFn(torch.autograd.Function):
         if not dy2.is_contiguous():
             dy2 = dy2.contiguous()
         dx = dw = db = None
-        if ctx.needs_input_grad[0]:
+        acc = ctx.sink_in.take() if ctx.sink_in is not None and ctx.needs_input_grad[0] else None
+        if acc is not None:
+            if acc.shape != x.shape or acc.dtype != dy2.dtype or not acc.is_contiguous():
+                acc = acc.to(dy2.dtype).contiguous()
+            acc.view(-1, K).addmm_(dy2, weight)  # dX = residual gradient + dY . W
+            dx = acc
+        elif ctx.needs_input_grad[0]:
             dx = (dy2 @ weight).view(x.shape)
         need_w, need_b = ctx.needs_input_grad[1], bias is not None and ctx.needs_input_grad[2]
         fused = (USE_WGRAD_KERNEL and need_w and _direct(weight) and (not need_b or _direct(bias))
@@ -87,7 +96,7 @@ class _DenseFn(torch.autograd.Function):
             _ready(weight)
             if need_b:
                 _ready(bias)
-            return dx, None, None
+            return dx, None, None, None
         if need_w:
             if _direct(weight):
                 weight.grad.addmm_(dy2.t(), x2)
@@ -100,11 +109,37 @@ class _DenseFn(torch.autograd.Function):
                 _ready(bias)
             else:
                 db = dy2.float().sum(0).to(bias.dtype)
-        return dx, dw, db
+        return dx, dw, db, None
 
+
+class _ResidualAddFn(torch.autograd.Function):
+    """``x + y`` whose backward hands the gradient of ``x`` to ``sink`` (a later consumer
+    accumulates into it in place) and returns it for ``y`` only."""
+
+    @staticmethod
+    def forward(ctx, x, y, sink):
+        ctx.sink = sink
+        return x + y
+
+    @staticmethod
+    def backward(ctx, g):
+        if ctx.needs_input_grad[0]:
+            # a fresh copy only when the y branch could still read g after the consumer ran;
+            # here the consumer is the first GEMM applied to x, which autograd can reach only
+            # after the whole y branch has been back-propagated (same stream)
+            ctx.sink.put(g)
+        return None, (g if ctx.needs_input_grad[1] else None), None
+
+
+def residual_add(x: torch.Tensor, y: torch.Tensor, sink=None) -> torch.Tensor:
+    """``x + y``; with a GradSink, x's gradient is accumulated by the GEMM that consumes x
+    first (``FusedLinear(..., sink_in=sink)``) instead of by an autograd add."""
+    if sink is None or x.shape != y.shape or x.dtype != y.dtype:
+        return x + y
+    return _ResidualAddFn.apply(x, y, sink)
 
 class FusedLinear(torch.nn.Linear):
     """Drop-in ``nn.Linear`` using :class:`_DenseFn` (state-dict compatible)."""
 
-    def forward(self, x):
-        return _DenseFn.apply(x, self.weight, self.bias)
+    def forward(self, x, sink_in=None):
+        return _DenseFn.apply(x, self.weight, self.bias, sink_in)
