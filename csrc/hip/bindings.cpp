@@ -24,6 +24,8 @@ PYBIND11_MODULE(_vodahip, m) {
   m.def("adasum_combine", &adasum_combine);
   m.def("wgrad_workspace_floats", &wgrad_workspace_floats);
   m.def("wgrad_gemm", &wgrad_gemm);
+  m.def("wgrad_conv_workspace_floats", &wgrad_conv_workspace_floats);
+  m.def("wgrad_conv", &wgrad_conv);
   m.def("layernorm_fwd", &layernorm_fwd);
   m.def("layernorm_bwd", &layernorm_bwd);
   m.def("layernorm_bwd_partial_rows", &layernorm_bwd_partial_rows);

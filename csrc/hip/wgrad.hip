@@ -48,6 +48,13 @@ struct WgradArgs {
   float* ws;                         // [S][N][K] + [S][N] partial slabs (splits > 1)
   const uint16_t* zero;              // >= 16 zero bytes: source of rows past the split (LDS-DMA path)
   int M, N, K, S, m_split, tiles_k, remap, accumulate, bias;
+  // epilogue addressing: dW column (and workspace column) offset and workspace row stride
+  int col0, ws_ld;
+  // implicit-GEMM convolution weight gradient (CONV kernels only): X rows are the input
+  // pixels under kernel tap (kh, kw) of output pixel m = (img, ho, wo); taps = KH * KW
+  // launches' worth of tiles share one grid, tap-major
+  int taps, KW, H, W, Ho, Wo, cstride, pad, tiles_nk;
+  int adv_n, adv_ho, adv_wo;  // BM output pixels expressed as (images, rows, columns)
 };
 
 // byte offset of 16-byte chunk ``ch`` (0..15) of LDS row ``r``: XOR swizzle that keeps both
@@ -96,11 +103,11 @@ __device__ __forceinline__ void wgrad_epilogue(const WgradArgs& p, int split, in
       const int row = rbase + (reg & 3) + 8 * (reg >> 2) + 4 * h;
       if (row < p.N) {
         if (p.S == 1) {
-          uint16_t* o = p.dw + int64_t(row) * p.ldw + col;
+          uint16_t* o = p.dw + int64_t(row) * p.ldw + p.col0 + col;
           const float v = acc[reg] + (p.accumulate ? bf2f(*o) : 0.f);
           *o = f2bf(v);
         } else {
-          p.ws[(int64_t(split) * p.N + row) * p.K + col] = acc[reg];
+          p.ws[(int64_t(split) * p.N + row) * p.ws_ld + p.col0 + col] = acc[reg];
         }
       }
     }
@@ -111,7 +118,7 @@ __device__ __forceinline__ void wgrad_epilogue(const WgradArgs& p, int split, in
   store_tile(c10, rb0 + 32, cb0i);
   store_tile(c11, rb0 + 32, cb0i + 32);
   if (do_bias && col_l == 0) {  // every column of cb holds the row sums; lanes 0 and 32 write
-    float* wsb = p.ws + int64_t(p.S) * p.N * p.K + int64_t(split) * p.N;
+    float* wsb = p.ws + int64_t(p.S) * p.N * p.ws_ld + int64_t(split) * p.N;
     auto store_bias = [&](const wg_f32x16& acc, int rbase) {
 #pragma unroll
       for (int reg = 0; reg < 16; ++reg) {
@@ -302,7 +309,7 @@ __device__ __forceinline__ void wg_wait_ahead(int ahead) {  // vmcnt(ahead * PER
 
 // kWgStages ring stages of BM tokens each: <4, 64> 128 KB, 1 workgroup/CU; <2, 64> 64 KB,
 // 2 workgroups/CU; <3, 64>; <4, 32> 64 KB with 3 stages in flight at 2 workgroups/CU.
-template <int kWgStages, int BM>
+template <int kWgStages, int BM, bool CONV = false>
 __global__ __launch_bounds__(kWgThreads, 1) void wgrad_glds_kernel(WgradArgs p) {
   constexpr int TB = BM * kWgRowBytes;   // bytes per operand tile
   constexpr int SB = 2 * TB;             // bytes per stage (dY tile + X tile)
@@ -314,6 +321,13 @@ __global__ __launch_bounds__(kWgThreads, 1) void wgrad_glds_kernel(WgradArgs p) 
 
   int bid = blockIdx.x;
   if (p.remap) bid = (bid & 7) * int(gridDim.x >> 3) + (bid >> 3);
+  int tap = 0;
+  if constexpr (CONV) {
+    const int per_tap = p.S * p.tiles_nk;
+    tap = bid / per_tap;
+    bid -= tap * per_tap;
+    p.col0 = tap * p.K;
+  }
   const int split = bid % p.S;
   const int tile = bid / p.S;
   const int n0 = (tile / p.tiles_k) * kWgBN;
@@ -329,6 +343,23 @@ __global__ __launch_bounds__(kWgThreads, 1) void wgrad_glds_kernel(WgradArgs p) 
   // this lane's part of each of the wave's IPW wave-instructions per operand tile:
   // instruction i covers tile rows 4j .. 4j+3 with j = IPW*wave + i
   const int lr = lane >> 4, slot = lane & 15;
+  // CONV: output pixel (img, ho, wo) of each of this lane's IPW rows, advanced by BM pixels
+  // per issued stage (issue() is called for stages 0, 1, 2, ... in order)
+  int pn[IPW], pho[IPW], pwo[IPW];
+  int dh = 0, dw = 0;
+  if constexpr (CONV) {
+    dh = tap / p.KW - p.pad;
+    dw = tap % p.KW - p.pad;
+    const int hw = p.Ho * p.Wo;
+#pragma unroll
+    for (int i = 0; i < IPW; ++i) {
+      const int m = mb + 4 * (IPW * wave + i) + lr;
+      pn[i] = m / hw;
+      const int rem = m - pn[i] * hw;
+      pho[i] = rem / p.Wo;
+      pwo[i] = rem - pho[i] * p.Wo;
+    }
+  }
   auto issue = [&](int st) {
     uint8_t* A = smem + (st % kWgStages) * SB;
     uint8_t* B = A + TB;
@@ -341,7 +372,20 @@ __global__ __launch_bounds__(kWgThreads, 1) void wgrad_glds_kernel(WgradArgs p) 
       const int m = m_base + r;
       const bool okm = m < me;
       const uint16_t* ga = okm ? p.dy + int64_t(m) * p.ldy + min(n0 + ch * 8, p.N - 8) : p.zero;
-      const uint16_t* gb = okm ? p.x + int64_t(m) * p.ldx + min(k0 + ch * 8, p.K - 8) : p.zero;
+      const uint16_t* gb;
+      if constexpr (CONV) {
+        const int hi = pho[i] * p.cstride + dh, wi = pwo[i] * p.cstride + dw;
+        const bool ok = okm && hi >= 0 && hi < p.H && wi >= 0 && wi < p.W;
+        gb = ok ? p.x + (int64_t(pn[i] * p.H + hi) * p.W + wi) * p.ldx + min(k0 + ch * 8, p.K - 8) : p.zero;
+        // advance this row by BM output pixels (single carries: the steps are < Wo and < Ho)
+        pwo[i] += p.adv_wo;
+        pho[i] += p.adv_ho;
+        pn[i] += p.adv_n;
+        if (pwo[i] >= p.Wo) { pwo[i] -= p.Wo; pho[i] += 1; }
+        if (pho[i] >= p.Ho) { pho[i] -= p.Ho; pn[i] += 1; }
+      } else {
+        gb = okm ? p.x + int64_t(m) * p.ldx + min(k0 + ch * 8, p.K - 8) : p.zero;
+      }
       wg_dma16(ga, __builtin_amdgcn_readfirstlane(uint32_t(size_t((lds_void*)(A + 1024 * j)))));
       wg_dma16(gb, __builtin_amdgcn_readfirstlane(uint32_t(size_t((lds_void*)(B + 1024 * j)))));
     }
@@ -569,7 +613,7 @@ __global__ __launch_bounds__(kWwThreads, 1) void wgrad_wide_kernel(WgradArgs p) 
               const float v = c[f][e][reg] + (p.accumulate ? bf2f(*o) : 0.f);
               *o = f2bf(v);
             } else {
-              p.ws[(int64_t(split) * p.N + row) * p.K + col] = c[f][e][reg];
+              p.ws[(int64_t(split) * p.N + row) * p.ws_ld + col] = c[f][e][reg];
             }
           }
         }
@@ -586,7 +630,7 @@ __global__ __launch_bounds__(kWwThreads, 1) void wgrad_wide_kernel(WgradArgs p) 
         if (p.S == 1) {
           p.db[row] = f2bf(tot + (p.accumulate ? bf2f(p.db[row]) : 0.f));
         } else {
-          p.ws[int64_t(p.S) * p.N * p.K + int64_t(split) * p.N + row] = tot;
+          p.ws[int64_t(p.S) * p.N * p.ws_ld + int64_t(split) * p.N + row] = tot;
         }
       }
     }
@@ -673,6 +717,9 @@ void wgrad_gemm(uintptr_t dy, int64_t ldy, uintptr_t x, int64_t ldx, uintptr_t d
   a.ws = reinterpret_cast<float*>(ws);
   a.zero = reinterpret_cast<const uint16_t*>(zero);
   a.M = M; a.N = N; a.K = K; a.S = pl.S; a.m_split = pl.m_split; a.tiles_k = pl.tiles_k;
+  a.col0 = 0; a.ws_ld = K;
+  a.taps = 1; a.KW = 1; a.H = a.W = a.Ho = a.Wo = 1; a.cstride = 1; a.pad = 0; a.tiles_nk = 0;
+  a.adv_n = a.adv_ho = a.adv_wo = 0;
   a.remap = (pl.grid % 8 == 0) ? 1 : 0;
   a.accumulate = accumulate ? 1 : 0;
   a.bias = db != 0 ? 1 : 0;
@@ -701,6 +748,61 @@ void wgrad_gemm(uintptr_t dy, int64_t ldy, uintptr_t x, int64_t ldx, uintptr_t d
     const int64_t work = (int64_t(N) * K) / 4 + (db != 0 ? N : 0);
     hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(stream_grid(work)), dim3(256), 0, s, a.ws, pl.S, N, K, a.dw, ldw,
                        a.db, a.accumulate);
+    check_launch();
+  }
+}
+
+int64_t wgrad_conv_workspace_floats(int M, int Cout, int Cin, int taps, int splits) {
+  const WgradPlan pl = wgrad_plan(M, Cout, Cin, splits);
+  return pl.S > 1 ? int64_t(pl.S) * (int64_t(Cout) * Cin * taps + Cout) : 0;
+}
+
+// Convolution weight gradient dW[co][kh][kw][ci] (+)= sum_{img,ho,wo} dY[img,ho,wo][co] *
+// X[img, ho*s+kh-pad, wo*s+kw-pad][ci] on NHWC activations and a channels_last weight
+// ([Cout][KH][KW][Cin] in memory): one implicit GEMM per tap, all taps in one launch, X rows
+// gathered by the LDS-DMA loader (zero rows outside the image).
+void wgrad_conv(uintptr_t dy, uintptr_t x, uintptr_t dw, int Nimg, int H, int W, int Cin, int Ho, int Wo, int Cout,
+                int KH, int KW, int stride, int pad, int splits, uintptr_t ws, bool accumulate, uintptr_t zero,
+                uintptr_t stream) {
+  VODA_CHECK(Nimg > 0 && H > 0 && W > 0 && Ho > 0 && Wo > 0 && KH > 0 && KW > 0 && stride > 0 && pad >= 0,
+             "wgrad_conv: bad geometry");
+  VODA_CHECK(Cin % 8 == 0 && Cout % 8 == 0 && Cin >= 8 && Cout >= 8, "wgrad_conv: channels must be multiples of 8");
+  VODA_CHECK((Ho - 1) * stride - pad + KH - 1 < H + pad && (Wo - 1) * stride - pad + KW - 1 < W + pad,
+             "wgrad_conv: output size inconsistent with the input");
+  VODA_CHECK(dy % 16 == 0 && x % 16 == 0 && dw % 16 == 0 && zero != 0 && zero % 16 == 0,
+             "wgrad_conv: operands must be 16-byte aligned");
+  const int64_t M64 = int64_t(Nimg) * Ho * Wo;
+  VODA_CHECK(M64 < (int64_t(1) << 31) && int64_t(Nimg) * H * W < (int64_t(1) << 31), "wgrad_conv: too many pixels");
+  const int M = int(M64), taps = KH * KW;
+  const WgradPlan pl = wgrad_plan(M, Cout, Cin, splits);
+  VODA_CHECK(pl.S == 1 || ws != 0, "wgrad_conv: split-K needs a workspace");
+  WgradArgs a;
+  a.dy = reinterpret_cast<const uint16_t*>(dy); a.ldy = Cout;
+  a.x = reinterpret_cast<const uint16_t*>(x); a.ldx = Cin;
+  a.dw = reinterpret_cast<uint16_t*>(dw); a.ldw = int64_t(taps) * Cin;
+  a.db = nullptr;
+  a.ws = reinterpret_cast<float*>(ws);
+  a.zero = reinterpret_cast<const uint16_t*>(zero);
+  a.M = M; a.N = Cout; a.K = Cin; a.S = pl.S; a.m_split = pl.m_split; a.tiles_k = pl.tiles_k;
+  a.col0 = 0; a.ws_ld = taps * Cin;
+  a.taps = taps; a.KW = KW; a.H = H; a.W = W; a.Ho = Ho; a.Wo = Wo; a.cstride = stride; a.pad = pad;
+  a.tiles_nk = pl.grid / pl.S;
+  constexpr int BM = 64;  // tokens per stage of the kernel launched below
+  a.adv_n = BM / (Ho * Wo);
+  a.adv_ho = (BM % (Ho * Wo)) / Wo;
+  a.adv_wo = (BM % (Ho * Wo)) % Wo;
+  a.accumulate = accumulate ? 1 : 0;
+  a.bias = 0;
+  const int64_t grid = int64_t(pl.grid) * taps;
+  a.remap = (grid % 8 == 0) ? 1 : 0;
+  hipStream_t s = as_stream(stream);
+  hipLaunchKernelGGL((wgrad_glds_kernel<2, BM, true>), dim3(unsigned(grid)), dim3(kWgThreads), 0, s, a);
+  check_launch();
+  if (pl.S > 1) {
+    const int Kt = taps * Cin;
+    const int64_t work = (int64_t(Cout) * Kt) / 4;
+    hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(stream_grid(work)), dim3(256), 0, s, a.ws, pl.S, Cout, Kt, a.dw,
+                       a.ldw, static_cast<uint16_t*>(nullptr), a.accumulate);
     check_launch();
   }
 }

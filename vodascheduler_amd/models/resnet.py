@@ -8,7 +8,10 @@ random-init weights, synthetic data.  Every BatchNorm is the fused HIP
 BN(+residual)(+ReLU) of ops/batchnorm.py: the bottleneck's ``relu(bn3(conv3) + identity)``
 is ONE statistics pass + ONE apply pass forward, instead of MIOpen BN + add + ReLU.  The 1x1
 convolutions (with >= 128 input channels) run as GEMMs on the NHWC views with the split-K
-MFMA weight-gradient kernel (ops/conv1x1.py).
+MFMA weight-gradient kernel (ops/conv1x1.py); the 3x3 convolutions with >= 128 channels take
+their weight gradient from the implicit-GEMM form of the same kernel (ops/conv3x3.py), and
+the bottleneck's shortcut gradient is accumulated by conv1's input-gradient GEMM
+(ops/conv1x1.GradSink).
 """
 from __future__ import annotations
 
@@ -17,6 +20,7 @@ from torch import nn
 
 from ..ops.batchnorm import FusedBatchNorm2d
 from ..ops.conv1x1 import USE_GRAD_SINK, Conv1x1, GradSink
+from ..ops.conv3x3 import ConvKxK
 from ..ops.pool import FusedMaxPool2d
 
 
@@ -28,7 +32,7 @@ class Bottleneck(nn.Module):
         width = planes
         self.conv1 = Conv1x1(inplanes, width)
         self.bn1 = FusedBatchNorm2d(width, relu=True)
-        self.conv2 = nn.Conv2d(width, width, 3, stride=stride, padding=1, bias=False)  # v1.5: stride on 3x3
+        self.conv2 = ConvKxK(width, width, 3, stride=stride, padding=1)  # v1.5: stride on 3x3
         self.bn2 = FusedBatchNorm2d(width, relu=True)
         self.conv3 = Conv1x1(width, planes * self.expansion)
         self.bn3 = FusedBatchNorm2d(planes * self.expansion, relu=True)  # relu(bn3(.) + identity)
@@ -58,9 +62,9 @@ class BasicBlock(nn.Module):
 
     def __init__(self, inplanes: int, planes: int, stride: int = 1, downsample: nn.Module | None = None):
         super().__init__()
-        self.conv1 = nn.Conv2d(inplanes, planes, 3, stride=stride, padding=1, bias=False)
+        self.conv1 = ConvKxK(inplanes, planes, 3, stride=stride, padding=1)
         self.bn1 = FusedBatchNorm2d(planes, relu=True)
-        self.conv2 = nn.Conv2d(planes, planes, 3, padding=1, bias=False)
+        self.conv2 = ConvKxK(planes, planes, 3, padding=1)
         self.bn2 = FusedBatchNorm2d(planes, relu=True)  # relu(bn2(.) + identity)
         self.downsample = downsample
 

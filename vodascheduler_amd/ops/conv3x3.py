@@ -1,0 +1,145 @@
+"""KxK convolutions (ResNet 3x3) whose weight gradient is an implicit-GEMM split-K MFMA
+kernel (csrc/hip/wgrad.hip, ``wgrad_conv``) accumulated straight into the optimizer's flat
+bf16 gradient.
+
+    forward          MIOpen (F.conv2d, exhaustive find)
+    input gradient   MIOpen (aten.convolution_backward, input only)
+    weight gradient  dW[co][kh][kw][ci] (+)= sum_{img,ho,wo} dY[img,ho,wo][co] *
+                                              X[img, ho*s+kh-p, wo*s+kw-p][ci]
+
+MIOpen runs the weight gradient of these layers as atomic split-K ``igemm_wrw`` kernels plus
+a workspace clear and a cast pass; autograd then adds the result into ``.grad`` with another
+elementwise kernel.  Here the KH*KW taps are KH*KW "reduction over output pixels" GEMMs of
+the same kind as the Linear / 1x1 weight gradients (``ops/wgrad.py``), launched as one grid:
+the LDS-DMA loader gathers the input row of each output pixel under the tap (zero rows
+outside the image), and the epilogue (or the split-K reduce) writes the tap's Cin columns of
+the channels_last weight gradient with beta = 1.  The layer is a drop-in ``nn.Conv2d``;
+anything the kernel does not cover (CPU, non-bf16, groups, dilation, a layout that is not
+channels_last, channel counts not multiples of 8 or below 128, no flat gradient) runs stock
+autograd.
+"""
+from __future__ import annotations
+
+import math
+import os
+
+import torch
+import torch.nn.functional as F
+
+from . import _native as N
+from . import wgrad as W
+from .conv1x1 import _direct, _ready
+
+USE_CONV_WGRAD = os.environ.get("VODA_CONV_WGRAD", "1") != "0"
+
+
+def default_splits(M: int, Cout: int, Cin: int, taps: int, target_blocks: int = 432) -> int:
+    tiles = math.ceil(Cout / W.TILE) * math.ceil(Cin / W.TILE) * taps
+    s = math.ceil(target_blocks / tiles)
+    return max(1, min(s, 256, M // 256 if M >= 256 else 1))
+
+
+def conv_wgrad_ref(dy: torch.Tensor, x: torch.Tensor, weight_shape, stride: int, padding: int) -> torch.Tensor:
+    """fp32 reference of the weight gradient [Cout, Cin, KH, KW]."""
+    return torch.nn.grad.conv2d_weight(x.float(), weight_shape, dy.float(), stride=stride, padding=padding)
+
+
+def conv_wgrad_accumulate_(dy: torch.Tensor, x: torch.Tensor, gw: torch.Tensor, stride: int, padding: int,
+                           accumulate: bool = True, splits: int | None = None) -> None:
+    """``gw (+)= dW`` in place; dy [N, Cout, Ho, Wo], x [N, Cin, H, W] channels_last bf16, gw
+    [Cout, Cin, KH, KW] channels_last bf16 (memory [Cout][KH][KW][Cin])."""
+    if not dy.is_cuda:
+        w = conv_wgrad_ref(dy, x, gw.shape, stride, padding)
+        gw.copy_((w + gw.float() if accumulate else w).to(gw.dtype))
+        return
+    if not supported(dy, x, gw):
+        raise ValueError(f"conv_wgrad: unsupported operands dy {tuple(dy.shape)} {dy.dtype}, x {tuple(x.shape)} "
+                         f"{x.dtype}, dw {tuple(gw.shape)} {gw.dtype}")
+    n, cin, H, Wd = x.shape
+    cout, _, kh, kw = gw.shape
+    ho, wo = dy.shape[2], dy.shape[3]
+    M = n * ho * wo
+    s = splits if splits is not None else default_splits(M, cout, cin, kh * kw)
+    h = N.hip()
+    nws = h.wgrad_conv_workspace_floats(M, cout, cin, kh * kw, s)
+    ws = torch.empty(nws, dtype=torch.float32, device=dy.device) if nws else None
+    h.wgrad_conv(dy.data_ptr(), x.data_ptr(), gw.data_ptr(), n, H, Wd, cin, ho, wo, cout, kh, kw, int(stride),
+                 int(padding), s, N.ptr(ws), bool(accumulate), W._zero_rows(dy.device).data_ptr(), N.stream_of(dy))
+
+
+def supported(dy: torch.Tensor, x: torch.Tensor, gw: torch.Tensor) -> bool:
+    cl = torch.channels_last
+    if not (dy.is_cuda and x.is_cuda and gw.is_cuda):
+        return False
+    if dy.dtype != torch.bfloat16 or x.dtype != torch.bfloat16 or gw.dtype != torch.bfloat16:
+        return False
+    if dy.dim() != 4 or x.dim() != 4 or gw.dim() != 4:
+        return False
+    if not (dy.is_contiguous(memory_format=cl) and x.is_contiguous(memory_format=cl)
+            and gw.is_contiguous(memory_format=cl)):
+        return False
+    n, cin, _, _ = x.shape
+    cout = gw.shape[0]
+    if gw.shape[1] != cin or dy.shape[0] != n or dy.shape[1] != cout or cin % 8 or cout % 8:
+        return False
+    return dy.data_ptr() % 16 == 0 and x.data_ptr() % 16 == 0 and gw.data_ptr() % 16 == 0
+
+
+class _ConvKxKFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, weight, stride: int, padding: int):
+        y = F.conv2d(x, weight, None, stride, padding)
+        ctx.save_for_backward(x, weight)
+        ctx.conf = (stride, padding)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, weight = ctx.saved_tensors
+        stride, padding = ctx.conf
+        if not dy.is_contiguous(memory_format=torch.channels_last):
+            dy = dy.contiguous(memory_format=torch.channels_last)
+        dx = None
+        if ctx.needs_input_grad[0]:
+            dx = torch.ops.aten.convolution_backward(dy, x, weight, None, [stride, stride], [padding, padding],
+                                                     [1, 1], False, [0, 0], 1, [True, False, False])[0]
+        dw = None
+        if ctx.needs_input_grad[1]:
+            gw = weight.grad if _direct(weight) else None
+            if gw is not None and supported(dy, x, gw):
+                conv_wgrad_accumulate_(dy, x, gw, stride, padding)
+                _ready(weight)
+            else:
+                dw = torch.ops.aten.convolution_backward(dy, x, weight, None, [stride, stride], [padding, padding],
+                                                         [1, 1], False, [0, 0], 1, [False, True, False])[1]
+        return dx, dw, None, None
+
+
+class ConvKxK(torch.nn.Conv2d):
+    """``nn.Conv2d(cin, cout, k, stride, padding, bias=False)`` whose weight gradient runs on the
+    implicit-GEMM MFMA kernel when the optimizer owns a flat bf16 gradient for it."""
+
+    def __init__(self, in_channels: int, out_channels: int, kernel_size: int = 3, stride: int = 1,
+                 padding: int = 1, **kw):
+        super().__init__(in_channels, out_channels, kernel_size, stride=stride, padding=padding, bias=False, **kw)
+
+    def _fast_ok(self, x: torch.Tensor) -> bool:
+        return (USE_CONV_WGRAD and x.is_cuda and x.dim() == 4 and x.dtype == torch.bfloat16
+                and self.weight.dtype == torch.bfloat16 and self.groups == 1 and self.dilation == (1, 1)
+                and self.stride[0] == self.stride[1] and self.padding[0] == self.padding[1]
+                and isinstance(self.padding[0], int) and x.is_contiguous(memory_format=torch.channels_last)
+                and self.weight.is_contiguous(memory_format=torch.channels_last)
+                and self.in_channels % 8 == 0 and self.out_channels % 8 == 0
+                # 64-channel layers fill a quarter of the 128 x 128 MFMA tile: ResNet-50's
+                # layer1 3x3 weight gradient took 360 us here vs 150 us (+35 us of workspace
+                # passes) on MIOpen; from 128 channels on this kernel is the faster one
+                # (profiles/r1_conv3x3_wgrad.md)
+                and self.in_channels >= 128 and self.out_channels >= 128)
+
+    def forward(self, x):
+        if x.is_cuda and x.dtype != self.weight.dtype and torch.is_autocast_enabled("cuda"):
+            x = x.to(self.weight.dtype)
+        if self._fast_ok(x):
+            with torch.autocast("cuda", enabled=False):
+                return _ConvKxKFn.apply(x, self.weight, self.stride[0], self.padding[0])
+        return super().forward(x)
