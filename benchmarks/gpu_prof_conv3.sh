@@ -13,4 +13,4 @@ run() {  # name, env assignment
   python3 $R/benchmarks/trace_dispatches.py /tmp/prof_$name/${name}_kernel_trace.csv $R/gpurun_out/prof_$name/wgrad_dispatches.csv wgrad igemm_wrw SubTensorOp >> $R/gpurun_out/prof_$name.log 2>&1 || return 4
 }
 run c3on VODA_CONV_WGRAD=1 || exit $?
-run c3off VODA_CONV_WGRAD=0 || exit $?
+[ -n "$ONLY_ON" ] || run c3off VODA_CONV_WGRAD=0 || exit $?

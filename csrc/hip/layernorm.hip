@@ -200,10 +200,15 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const T* __restrict__ dy, c
 // 32 columns x 8 row-groups per block; every thread keeps 4 independent loads in flight
 // (rows <= 256, so <= 32 loads per thread) -- the first version (64 columns x 4 groups,
 // 1024 rows) was latency-bound at 64 us per call on BERT (rocprof, profiles/).
+// blockIdx.y selects (part, out) or (part_b, out_b): dgamma and dbeta in one launch;
+// accumulate: out += sum (the optimizer's flat gradient buffer, no autograd add afterwards).
 template <typename WT>
-__global__ __launch_bounds__(256) void col_sum_kernel(const float* __restrict__ part, WT* __restrict__ out,
-                                                      int rows, int N) {
+__global__ __launch_bounds__(256) void col_sum_kernel(const float* __restrict__ part_a, WT* __restrict__ out_a,
+                                                      const float* __restrict__ part_b, WT* __restrict__ out_b,
+                                                      int rows, int N, int accumulate) {
   __shared__ float red[8][33];
+  const float* __restrict__ part = blockIdx.y == 0 ? part_a : part_b;
+  WT* __restrict__ out = blockIdx.y == 0 ? out_a : out_b;
   const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;
   const int c = blockIdx.x * 32 + tx;
   float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
@@ -223,6 +228,7 @@ __global__ __launch_bounds__(256) void col_sum_kernel(const float* __restrict__ 
     float t = 0.f;
 #pragma unroll
     for (int k = 0; k < 8; ++k) t += red[k][tx];
+    if (accumulate) t += Vec4<WT>::load1(out, c);
     Vec4<WT>::store1(out, c, t);
   }
 }
@@ -274,7 +280,7 @@ int layernorm_bwd_partial_rows(int64_t M) {
 
 void layernorm_bwd(uintptr_t dy, uintptr_t x, uintptr_t mean, uintptr_t rstd, uintptr_t gamma, uintptr_t dx,
                    uintptr_t dgamma, uintptr_t dbeta, uintptr_t workspace, int64_t M, int N, int dt, int wdt,
-                   uintptr_t stream) {
+                   bool accumulate, uintptr_t stream) {
   VODA_CHECK(N > 0 && N % 4 == 0 && N <= kLayerNormMaxN, "layernorm: N must be a multiple of 4 and <= 4096");
   if (M == 0) return;
   const int grid = layernorm_bwd_partial_rows(M);
@@ -295,10 +301,9 @@ void layernorm_bwd(uintptr_t dy, uintptr_t x, uintptr_t mean, uintptr_t rstd, ui
     });
     if (pg) {
       const unsigned cg = unsigned((N + 31) / 32);
-      hipLaunchKernelGGL((col_sum_kernel<WT>), dim3(cg), dim3(256), 0, as_stream(stream), pg,
-                         reinterpret_cast<WT*>(dgamma), grid, N);
-      hipLaunchKernelGGL((col_sum_kernel<WT>), dim3(cg), dim3(256), 0, as_stream(stream), pb,
-                         reinterpret_cast<WT*>(dbeta), grid, N);
+      hipLaunchKernelGGL((col_sum_kernel<WT>), dim3(cg, 2), dim3(256), 0, as_stream(stream), pg,
+                         reinterpret_cast<WT*>(dgamma), pb, reinterpret_cast<WT*>(dbeta), grid, N,
+                         accumulate ? 1 : 0);
     }
   });
   check_launch();

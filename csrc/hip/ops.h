@@ -50,7 +50,7 @@ void layernorm_fwd(uintptr_t x, uintptr_t gamma, uintptr_t beta, uintptr_t y, ui
 int layernorm_bwd_partial_rows(int64_t M);
 void layernorm_bwd(uintptr_t dy, uintptr_t x, uintptr_t mean, uintptr_t rstd, uintptr_t gamma, uintptr_t dx,
                    uintptr_t dgamma, uintptr_t dbeta, uintptr_t workspace, int64_t M, int N, int dt, int wdt,
-                   uintptr_t stream);
+                   bool accumulate, uintptr_t stream);
 
 // ---- masked softmax (softmax.hip) ----
 void masked_softmax_fwd(uintptr_t x, uintptr_t mask, int mask_dt, uintptr_t y, int64_t B, int H, int Tq, int S,

@@ -136,6 +136,31 @@ def test_fused_layernorm_module_bf16_weights():
     assert ln.weight.grad is not None and ln.weight.grad.dtype == torch.bfloat16
 
 
+def test_fused_layernorm_flat_grads_accumulate_in_place():
+    """gamma / beta gradients summed straight into the optimizer's flat fp32 buffer (one
+    column-sum launch, beta = 1): equal to autograd's, and a second backward accumulates."""
+    from vodascheduler_amd.ops.optim import make_optimizer
+
+    torch.manual_seed(0)
+    ln = FusedLayerNorm(768).to(DEV)
+    torch.nn.init.normal_(ln.weight)
+    torch.nn.init.normal_(ln.bias)
+    opt = make_optimizer("adamw", ln.parameters(), lr=0.0)
+    assert getattr(ln.weight, "_voda_flat_grad", False)
+    x = torch.randn(4, 128, 768, device=DEV, dtype=torch.bfloat16)
+    dy = torch.randn(4, 128, 768, device=DEV, dtype=torch.bfloat16)
+    opt.zero_grad()
+    ln(x).backward(dy)
+    ref = torch.nn.LayerNorm(768).to(DEV)
+    ref.load_state_dict(ln.state_dict())
+    ref(x.float()).backward(dy.float())
+    for got, want in ((ln.weight.grad, ref.weight.grad), (ln.bias.grad, ref.bias.grad)):
+        torch.testing.assert_close(got, want, rtol=2e-2, atol=5e-2)
+    ln(x).backward(dy)
+    for got, want in ((ln.weight.grad, ref.weight.grad), (ln.bias.grad, ref.bias.grad)):
+        torch.testing.assert_close(got, 2 * want, rtol=2e-2, atol=1e-1)
+
+
 @pytest.mark.parametrize("B,H,Tq,S", [(512, 8, 20, 20), (4, 12, 128, 128), (2, 2, 7, 512), (1, 1, 3, 2048)])
 @pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
 @pytest.mark.parametrize("causal", [False, True])

@@ -6,11 +6,21 @@ PyTorch reference ``torch.nn.functional.layer_norm`` in fp32.
 """
 from __future__ import annotations
 
+import os
+
 import torch
 
 from . import _native as N
+from .dense import _ready
 
 MAX_N = 4096
+LN_DIRECT_GRADS = os.environ.get("VODA_LN_DIRECT", "1") != "0"
+
+
+def _direct(p) -> bool:
+    """The optimizer's flat gradient owns p.grad (ops/dense.py contract)."""
+    return (p is not None and getattr(p, "_voda_flat_grad", False) and p.grad is not None
+            and p.grad.dtype == p.dtype and p.grad.is_contiguous())
 
 
 def _supported(x: torch.Tensor, weight: torch.Tensor | None) -> bool:
@@ -40,6 +50,7 @@ class _LayerNormFn(torch.autograd.Function):
                               m, n, float(eps), N.dtype_code(x.dtype), N.dtype_code(wdt), N.stream_of(x))
         ctx.save_for_backward(xc, w, mean, rstd)
         ctx.has_bias = bias is not None
+        ctx.params = (weight, bias)
         ctx.wdt = wdt
         return y.view_as(x)
 
@@ -53,14 +64,26 @@ class _LayerNormFn(torch.autograd.Function):
         need_w = w is not None and ctx.needs_input_grad[1]
         need_b = ctx.has_bias and ctx.needs_input_grad[2]
         dgamma = dbeta = ws = None
+        weight, bias = ctx.params
+        # gamma / beta gradients summed straight into the optimizer's flat buffer (one column-sum
+        # launch for both, no autograd add afterwards) when it owns them
+        direct = (LN_DIRECT_GRADS and need_w and need_b and _direct(weight) and _direct(bias) and weight.grad.dtype == ctx.wdt
+                  and bias.grad.dtype == ctx.wdt)
         if need_w or need_b:
             rows = N.hip().layernorm_bwd_partial_rows(m)
             ws = torch.empty(2 * rows * n, dtype=torch.float32, device=xc.device)
-            dgamma = torch.empty(n, dtype=ctx.wdt, device=xc.device)
-            dbeta = torch.empty(n, dtype=ctx.wdt, device=xc.device)
+            if direct:
+                dgamma, dbeta = weight.grad, bias.grad
+            else:
+                dgamma = torch.empty(n, dtype=ctx.wdt, device=xc.device)
+                dbeta = torch.empty(n, dtype=ctx.wdt, device=xc.device)
         N.hip().layernorm_bwd(dyc.data_ptr(), xc.data_ptr(), mean.data_ptr(), rstd.data_ptr(), N.ptr(w),
                               dx.data_ptr(), N.ptr(dgamma), N.ptr(dbeta), N.ptr(ws), m, n,
-                              N.dtype_code(xc.dtype), N.dtype_code(ctx.wdt), N.stream_of(xc))
+                              N.dtype_code(xc.dtype), N.dtype_code(ctx.wdt), bool(direct), N.stream_of(xc))
+        if direct:
+            _ready(weight)
+            _ready(bias)
+            return dx.view_as(dy), None, None, None
         return (dx.view_as(dy), dgamma if need_w else None, dbeta if need_b else None, None)
 
 
