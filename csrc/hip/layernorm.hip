@@ -36,11 +36,15 @@ __device__ __forceinline__ float4 load_w4(const void* w, int64_t c4) {
 }
 
 // MAXITER: upper bound on 256-column chunks per row (row held as MAXITER float4 per lane)
-template <typename T, typename WT, int MAXITER>
+// RES: y = LN(x + res) with the rounded sum written to ``sum`` (the residual-stream value the
+// next sublayer reads and the backward normalises): the transformer block's residual add
+// fused into the normalisation pass (one read of each input, no separate add kernel).
+template <typename T, typename WT, int MAXITER, bool RES = false>
 __global__ __launch_bounds__(256) void ln_fwd_kernel(const T* __restrict__ x, const void* __restrict__ gamma,
                                                      const void* __restrict__ beta, T* __restrict__ y,
                                                      float* __restrict__ mean_out, float* __restrict__ rstd_out,
-                                                     int64_t M, int N, float eps) {
+                                                     int64_t M, int N, float eps, const T* __restrict__ res,
+                                                     T* __restrict__ sum) {
   const int lane = threadIdx.x & 63;
   const int64_t row = int64_t(blockIdx.x) * 4 + (threadIdx.x >> 6);
   if (row >= M) return;
@@ -51,6 +55,21 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(const T* __restrict__ x, co
 #pragma unroll
   for (int it = 0; it < MAXITER; ++it)  // unconditional (clamped) loads, zeroed after
     v[it] = Vec4<T>::load(xr, min(it * 64 + lane, N4 - 1));
+  if constexpr (RES) {
+    const T* rr = res + row * N;
+    T* sr = sum + row * N;
+    float4 r[MAXITER];
+#pragma unroll
+    for (int it = 0; it < MAXITER; ++it) r[it] = Vec4<T>::load(rr, min(it * 64 + lane, N4 - 1));
+#pragma unroll
+    for (int it = 0; it < MAXITER; ++it) {
+      float4 t = make_float4(v[it].x + r[it].x, v[it].y + r[it].y, v[it].z + r[it].z, v[it].w + r[it].w);
+      alignas(16) T q[4];
+      Vec4<T>::store(q, 0, t);  // round to T: statistics of exactly the stored sum
+      v[it] = Vec4<T>::load(q, 0);
+      if (it * 64 + lane < N4) Vec4<T>::store(sr, it * 64 + lane, v[it]);
+    }
+  }
 #pragma unroll
   for (int it = 0; it < MAXITER; ++it) {
     if (it * 64 + lane >= N4) v[it] = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -257,17 +276,26 @@ __global__ __launch_bounds__(256) void col_sum_kernel(const float* __restrict__ 
   }()
 
 void layernorm_fwd(uintptr_t x, uintptr_t gamma, uintptr_t beta, uintptr_t y, uintptr_t mean, uintptr_t rstd,
-                   int64_t M, int N, float eps, int dt, int wdt, uintptr_t stream) {
+                   int64_t M, int N, float eps, int dt, int wdt, uintptr_t residual, uintptr_t sum, uintptr_t stream) {
+  VODA_CHECK((residual == 0) == (sum == 0), "layernorm: residual and sum go together");
   VODA_CHECK(N > 0 && N % 4 == 0 && N <= kLayerNormMaxN, "layernorm: N must be a multiple of 4 and <= 4096");
   VODA_CHECK(dt != kF32 || wdt == kF32, "layernorm: fp32 input needs fp32 weights");
   if (M == 0) return;
   const unsigned grid = unsigned((M + 3) / 4);
   LN_DISPATCH_T(dt, wdt, [&] {
     LN_DISPATCH_ITER(N, [&] {
-      hipLaunchKernelGGL((ln_fwd_kernel<T, WT, MI>), dim3(grid), dim3(256), 0, as_stream(stream),
-                         reinterpret_cast<const T*>(x), reinterpret_cast<const void*>(gamma),
-                         reinterpret_cast<const void*>(beta), reinterpret_cast<T*>(y),
-                         reinterpret_cast<float*>(mean), reinterpret_cast<float*>(rstd), M, N, eps);
+      if (residual)
+        hipLaunchKernelGGL((ln_fwd_kernel<T, WT, MI, true>), dim3(grid), dim3(256), 0, as_stream(stream),
+                           reinterpret_cast<const T*>(x), reinterpret_cast<const void*>(gamma),
+                           reinterpret_cast<const void*>(beta), reinterpret_cast<T*>(y),
+                           reinterpret_cast<float*>(mean), reinterpret_cast<float*>(rstd), M, N, eps,
+                           reinterpret_cast<const T*>(residual), reinterpret_cast<T*>(sum));
+      else
+        hipLaunchKernelGGL((ln_fwd_kernel<T, WT, MI, false>), dim3(grid), dim3(256), 0, as_stream(stream),
+                           reinterpret_cast<const T*>(x), reinterpret_cast<const void*>(gamma),
+                           reinterpret_cast<const void*>(beta), reinterpret_cast<T*>(y),
+                           reinterpret_cast<float*>(mean), reinterpret_cast<float*>(rstd), M, N, eps,
+                           static_cast<const T*>(nullptr), static_cast<T*>(nullptr));
     });
   });
   check_launch();

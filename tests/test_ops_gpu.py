@@ -126,6 +126,34 @@ def test_layernorm_fwd_bwd(shape, dt):
     torch.testing.assert_close(b.grad, br.grad, **gt)
 
 
+@pytest.mark.parametrize("shape", [(512, 768), (3, 5, 1024), (7, 12)])
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+def test_layernorm_fused_residual(shape, dt):
+    """LN(x + residual) in one kernel (the sum rounded to dt, as the unfused add would store
+    it) vs an fp32 reference; both inputs receive the same gradient."""
+    torch.manual_seed(0)
+    n = shape[-1]
+    x = torch.randn(shape, device=DEV).to(dt).requires_grad_()
+    r = torch.randn(shape, device=DEV).mul(2).to(dt).requires_grad_()
+    w = torch.randn(n, device=DEV).requires_grad_()
+    b = torch.randn(n, device=DEV).requires_grad_()
+    y = layer_norm(x, w, b, 1e-5, residual=r)
+    dy = torch.randn_like(y)
+    y.backward(dy)
+    s = (x.detach() + r.detach()).float().requires_grad_()  # rounded sum, like the kernel's
+    wr = w.detach().clone().requires_grad_()
+    br = b.detach().clone().requires_grad_()
+    yr = torch.nn.functional.layer_norm(s, (n,), wr, br, 1e-5)
+    yr.backward(dy.float())
+    tol = dict(rtol=2e-2, atol=3e-2) if dt == torch.bfloat16 else dict(rtol=1e-4, atol=1e-4)
+    torch.testing.assert_close(y.float(), yr, **tol)
+    torch.testing.assert_close(x.grad.float(), s.grad, **tol)
+    torch.testing.assert_close(r.grad.float(), s.grad, **tol)
+    gt = dict(rtol=2e-2, atol=2e-1) if dt == torch.bfloat16 else dict(rtol=1e-3, atol=1e-3)
+    torch.testing.assert_close(w.grad, wr.grad, **gt)
+    torch.testing.assert_close(b.grad, br.grad, **gt)
+
+
 def test_fused_layernorm_module_bf16_weights():
     ln = FusedLayerNorm(768).to(DEV).to(torch.bfloat16)
     x = torch.randn(4, 128, 768, device=DEV, dtype=torch.bfloat16, requires_grad=True)

@@ -11,6 +11,7 @@ dimension is supported.  LayerNorm is the HIP FusedLayerNorm.
 from __future__ import annotations
 
 import math
+import os
 
 import torch
 import torch.nn.functional as F
@@ -20,6 +21,10 @@ from ..ops.attention import attention_q_kvpacked, attention_qkvpacked
 from ..ops.conv1x1 import USE_GRAD_SINK, GradSink
 from ..ops.dense import FusedLinear, residual_add
 from ..ops.layernorm import FusedLayerNorm
+
+# residual add of each post-LN sublayer fused into the LayerNorm kernel (VODA_LN_RESIDUAL=0:
+# a separate add, for A/B runs)
+FUSED_RESIDUAL_LN = os.environ.get("VODA_LN_RESIDUAL", "1") != "0"
 
 
 class MultiHeadAttention(nn.Module):
@@ -90,11 +95,14 @@ class EncoderLayer(nn.Module):
     def forward(self, x, key_mask=None):
         # the residual stream x feeds the sublayer's first GEMM and the residual add: its
         # gradient from the add is accumulated by that GEMM's input-gradient GEMM (beta = 1)
-        # instead of by a separate autograd add (ops/dense.residual_add)
+        # instead of by a separate autograd add (ops/conv1x1.GradSink)
+        # the add itself runs inside the LayerNorm kernel (FusedLayerNorm(x, residual=...))
         s1 = _sink(self, x)
-        x = self.ln1(residual_add(x, self.drop(self.attn(x, key_mask=key_mask, sink_in=s1)), s1))
+        a = self.drop(self.attn(x, key_mask=key_mask, sink_in=s1))
+        x = self.ln1(a, residual=x, sink=s1) if FUSED_RESIDUAL_LN else self.ln1(residual_add(x, a, s1))
         s2 = _sink(self, x)
-        return self.ln2(residual_add(x, self.drop(self.ff(x, sink_in=s2)), s2))
+        f = self.drop(self.ff(x, sink_in=s2))
+        return self.ln2(f, residual=x, sink=s2) if FUSED_RESIDUAL_LN else self.ln2(residual_add(x, f, s2))
 
 
 class DecoderLayer(nn.Module):
@@ -108,6 +116,10 @@ class DecoderLayer(nn.Module):
         self.ln3 = FusedLayerNorm(d_model, eps=eps)
 
     def forward(self, y, enc, tgt_mask=None, src_mask=None):
-        y = self.ln1(y + self.self_attn(y, key_mask=tgt_mask, causal=True))
-        y = self.ln2(y + self.cross(y, kv=enc, key_mask=src_mask))
-        return self.ln3(y + self.ff(y))
+        if not FUSED_RESIDUAL_LN:
+            y = self.ln1(y + self.self_attn(y, key_mask=tgt_mask, causal=True))
+            y = self.ln2(y + self.cross(y, kv=enc, key_mask=src_mask))
+            return self.ln3(y + self.ff(y))
+        y = self.ln1(self.self_attn(y, key_mask=tgt_mask, causal=True), residual=y)
+        y = self.ln2(self.cross(y, kv=enc, key_mask=src_mask), residual=y)
+        return self.ln3(self.ff(y), residual=y)

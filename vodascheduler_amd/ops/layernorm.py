@@ -34,7 +34,10 @@ def _supported(x: torch.Tensor, weight: torch.Tensor | None) -> bool:
 
 class _LayerNormFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, weight, bias, eps):
+    def forward(ctx, x, weight, bias, eps, residual=None, sink=None):
+        """``residual``: normalise ``x + residual`` (the kernel writes the sum, which the backward
+        normalises again); ``sink`` (ops/conv1x1.GradSink): hand the residual's gradient to the
+        GEMM that consumed the residual stream instead of returning it."""
         n = x.shape[-1]
         xc = x.contiguous()
         m = xc.numel() // n
@@ -44,14 +47,19 @@ class _LayerNormFn(torch.autograd.Function):
         wdt = weight.dtype if weight is not None else (torch.float32 if x.dtype == torch.float32 else x.dtype)
         w = weight.contiguous() if weight is not None else None
         b = bias.to(wdt).contiguous() if bias is not None else None
+        rc = residual.contiguous() if residual is not None else None
+        sm = torch.empty_like(xc) if residual is not None else None
         for t, nm in ((xc, "x"), (y, "y")):
             N.check_gpu_tensor(t, nm, align=8)
         N.hip().layernorm_fwd(xc.data_ptr(), N.ptr(w), N.ptr(b), y.data_ptr(), mean.data_ptr(), rstd.data_ptr(),
-                              m, n, float(eps), N.dtype_code(x.dtype), N.dtype_code(wdt), N.stream_of(x))
-        ctx.save_for_backward(xc, w, mean, rstd)
+                              m, n, float(eps), N.dtype_code(x.dtype), N.dtype_code(wdt), N.ptr(rc), N.ptr(sm),
+                              N.stream_of(x))
+        ctx.save_for_backward(sm if sm is not None else xc, w, mean, rstd)
         ctx.has_bias = bias is not None
         ctx.params = (weight, bias)
         ctx.wdt = wdt
+        ctx.has_res = residual is not None
+        ctx.sink = sink if residual is not None else None
         return y.view_as(x)
 
     @staticmethod
@@ -80,18 +88,34 @@ class _LayerNormFn(torch.autograd.Function):
         N.hip().layernorm_bwd(dyc.data_ptr(), xc.data_ptr(), mean.data_ptr(), rstd.data_ptr(), N.ptr(w),
                               dx.data_ptr(), N.ptr(dgamma), N.ptr(dbeta), N.ptr(ws), m, n,
                               N.dtype_code(xc.dtype), N.dtype_code(ctx.wdt), bool(direct), N.stream_of(xc))
+        dx = dx.view_as(dy)
+        dres = None
+        if ctx.has_res:
+            if ctx.sink is not None and ctx.needs_input_grad[4]:
+                ctx.sink.put(dx)  # the consumer accumulates into it after x's branch is done
+            elif ctx.needs_input_grad[4]:
+                dres = dx
+        gw = None if direct or not need_w else dgamma
+        gb = None if direct or not need_b else dbeta
         if direct:
             _ready(weight)
             _ready(bias)
-            return dx.view_as(dy), None, None, None
-        return (dx.view_as(dy), dgamma if need_w else None, dbeta if need_b else None, None)
+        return dx if ctx.needs_input_grad[0] else None, gw, gb, None, dres, None
 
 
 def layer_norm(x: torch.Tensor, weight: torch.Tensor | None = None, bias: torch.Tensor | None = None,
-               eps: float = 1e-5) -> torch.Tensor:
+               eps: float = 1e-5, residual: torch.Tensor | None = None, sink=None) -> torch.Tensor:
+    """LayerNorm over the last dimension; with ``residual``, of ``x + residual`` (one fused pass
+    on GPU).  ``sink``: see ops/conv1x1.GradSink (the residual's gradient is handed over)."""
+    if residual is not None and (not x.is_cuda or residual.shape != x.shape or residual.dtype != x.dtype):
+        from .dense import residual_add
+
+        x, residual = residual_add(residual, x, sink), None
     if x.is_cuda:
         if not _supported(x, weight):
             raise ValueError(f"fused layer_norm: unsupported shape/dtype {tuple(x.shape)} {x.dtype}")
+        if residual is not None:
+            return _LayerNormFn.apply(x, weight, bias, eps, residual, sink)
         return _LayerNormFn.apply(x, weight, bias, eps)
     n = x.shape[-1]
     y = torch.nn.functional.layer_norm(x.float(), (n,), None if weight is None else weight.float(),
@@ -118,12 +142,13 @@ class FusedLayerNorm(torch.nn.Module):
             self.register_parameter("weight", None)
             self.register_parameter("bias", None)
 
-    def forward(self, x):
+    def forward(self, x, residual=None, sink=None):
+        """``LN(x)``, or ``LN(x + residual)`` with the add fused into the normalisation pass."""
         if x.is_cuda and torch.is_autocast_enabled("cuda"):
             # keep the input dtype (bf16 out, fp32 statistics inside the kernel)
             with torch.autocast("cuda", enabled=False):
-                return layer_norm(x, self.weight, self.bias, self.eps)
-        return layer_norm(x, self.weight, self.bias, self.eps)
+                return layer_norm(x, self.weight, self.bias, self.eps, residual, sink)
+        return layer_norm(x, self.weight, self.bias, self.eps, residual, sink)
 
     def extra_repr(self):
         return f"{self.normalized_shape}, eps={self.eps}"
