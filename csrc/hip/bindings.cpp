@@ -26,6 +26,8 @@ PYBIND11_MODULE(_vodahip, m) {
   m.def("wgrad_gemm", &wgrad_gemm);
   m.def("wgrad_conv_workspace_floats", &wgrad_conv_workspace_floats);
   m.def("wgrad_conv", &wgrad_conv);
+  m.def("gelu_tanh_fwd", &gelu_tanh_fwd);
+  m.def("gelu_tanh_bwd", &gelu_tanh_bwd);
   m.def("layernorm_fwd", &layernorm_fwd);
   m.def("layernorm_bwd", &layernorm_bwd);
   m.def("layernorm_bwd_partial_rows", &layernorm_bwd_partial_rows);

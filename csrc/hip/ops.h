@@ -44,6 +44,10 @@ void wgrad_gemm(uintptr_t dy, int64_t ldy, uintptr_t x, int64_t ldx, uintptr_t d
                 int N, int K, int splits, uintptr_t ws, bool accumulate, uintptr_t zero, int variant,
                 uintptr_t stream);
 
+// ---- tanh GELU (activation.hip); bwd may run in place (dh == dy) ----
+void gelu_tanh_fwd(uintptr_t h, uintptr_t y, int64_t n, int dt, uintptr_t stream);
+void gelu_tanh_bwd(uintptr_t h, uintptr_t dy, uintptr_t dh, int64_t n, int dt, uintptr_t stream);
+
 // ---- LayerNorm (layernorm.hip) ----
 void layernorm_fwd(uintptr_t x, uintptr_t gamma, uintptr_t beta, uintptr_t y, uintptr_t mean, uintptr_t rstd,
                    int64_t M, int N, float eps, int dt, int wdt, uintptr_t residual, uintptr_t sum, uintptr_t stream);

@@ -78,6 +78,21 @@ def test_cpu_cast_and_multi_copy():
     torch.testing.assert_close(out[1], ts[1] * 2)
 
 
+def test_cpu_layernorm_residual_and_gelu_fallbacks():
+    """``layer_norm(x, residual=r)`` == LN(x + r) with both gradients; CPU tanh-GELU."""
+    from vodascheduler_amd.ops.activation import gelu_tanh
+
+    x = torch.randn(3, 16, requires_grad=True)
+    r = torch.randn(3, 16, requires_grad=True)
+    layer_norm(x, residual=r).square().sum().backward()
+    xs = (x.detach() + r.detach()).requires_grad_()
+    torch.nn.functional.layer_norm(xs, (16,)).square().sum().backward()
+    torch.testing.assert_close(x.grad, xs.grad)
+    torch.testing.assert_close(r.grad, xs.grad)
+    h = torch.randn(100)
+    torch.testing.assert_close(gelu_tanh(h), torch.nn.functional.gelu(h, approximate="tanh"))
+
+
 def test_cpu_layernorm_and_softmax_reference():
     x = torch.randn(3, 16)
     torch.testing.assert_close(layer_norm(x), torch.nn.functional.layer_norm(x, (16,)))

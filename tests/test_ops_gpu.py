@@ -154,6 +154,26 @@ def test_layernorm_fused_residual(shape, dt):
     torch.testing.assert_close(b.grad, br.grad, **gt)
 
 
+@pytest.mark.parametrize("n", [8192 * 3072, 1000, 7, 8 * 257 + 5])
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16, torch.float16])
+def test_gelu_tanh_fwd_bwd(n, dt):
+    """HIP tanh-GELU (csrc/hip/activation.hip) vs PyTorch's fp32 GELU, incl. the < 8 tail."""
+    from vodascheduler_amd.ops.activation import gelu_tanh
+
+    torch.manual_seed(0)
+    h = torch.randn(n, device=DEV).mul(3).to(dt).requires_grad_()
+    y = gelu_tanh(h)
+    dy = torch.randn_like(y)
+    y.backward(dy)
+    hr = h.detach().float().requires_grad_()
+    yr = torch.nn.functional.gelu(hr, approximate="tanh")
+    yr.backward(dy.float())
+    tol = dict(rtol=1e-5, atol=1e-5) if dt == torch.float32 else dict(rtol=1e-2, atol=1e-2)
+    torch.testing.assert_close(y.float(), yr, **tol)
+    torch.testing.assert_close(h.grad.float(), hr.grad, **tol)
+    assert torch.isfinite(gelu_tanh(torch.tensor([-1e4, 1e4, -90.0, 90.0], device=DEV))).all()
+
+
 def test_fused_layernorm_module_bf16_weights():
     ln = FusedLayerNorm(768).to(DEV).to(torch.bfloat16)
     x = torch.randn(4, 128, 768, device=DEV, dtype=torch.bfloat16, requires_grad=True)

@@ -17,6 +17,7 @@ import torch
 import torch.nn.functional as F
 from torch import nn
 
+from ..ops.activation import GeluTanh
 from ..ops.attention import attention_q_kvpacked, attention_qkvpacked
 from ..ops.conv1x1 import USE_GRAD_SINK, GradSink
 from ..ops.dense import FusedLinear, residual_add
@@ -25,6 +26,8 @@ from ..ops.layernorm import FusedLayerNorm
 # residual add of each post-LN sublayer fused into the LayerNorm kernel (VODA_LN_RESIDUAL=0:
 # a separate add, for A/B runs)
 FUSED_RESIDUAL_LN = os.environ.get("VODA_LN_RESIDUAL", "1") != "0"
+# FFN GELU on the HIP kernel (ops/activation.py; VODA_HIP_GELU=0: PyTorch's, for A/B runs)
+HIP_GELU = os.environ.get("VODA_HIP_GELU", "1") != "0"
 
 
 class MultiHeadAttention(nn.Module):
@@ -70,7 +73,10 @@ class FeedForward(nn.Module):
         super().__init__()
         self.fc1 = FusedLinear(d_model, d_ff)
         self.fc2 = FusedLinear(d_ff, d_model)
-        self.act = nn.GELU(approximate="tanh") if act == "gelu" else nn.ReLU()
+        if act == "gelu":
+            self.act = GeluTanh() if HIP_GELU else nn.GELU(approximate="tanh")
+        else:
+            self.act = nn.ReLU()
 
     def forward(self, x, sink_in=None):
         return self.fc2(self.act(self.fc1(x, sink_in)))

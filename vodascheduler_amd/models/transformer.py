@@ -14,7 +14,7 @@ from torch import nn
 
 from ..ops.dense import FusedLinear
 from ..ops.layernorm import FusedLayerNorm
-from .layers import DecoderLayer, EncoderLayer
+from .layers import HIP_GELU, DecoderLayer, EncoderLayer, GeluTanh
 
 
 class PositionalEmbedding(nn.Module):
@@ -62,7 +62,7 @@ class BertBase(nn.Module):
         self.mlm_ln = FusedLayerNorm(d_model, eps=1e-12)
         self.mlm_out = nn.Linear(d_model, vocab)
         self.mlm_out.weight = self.emb.tok.weight  # tied embeddings, as in BERT
-        self.act = nn.GELU(approximate="tanh")
+        self.act = GeluTanh() if HIP_GELU else nn.GELU(approximate="tanh")
         for m in self.modules():
             if isinstance(m, (nn.Linear, nn.Embedding)):
                 nn.init.normal_(m.weight, std=0.02)
