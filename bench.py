@@ -3,34 +3,73 @@
 with elastic-resize latency (BASELINE.json metric; config "FfDL Optimizer, 32-job
 Philly-style synthetic trace, autoscale 1->8 MI355X").
 
-One process per GPU (``python -m torch.distributed.run --nproc-per-node N bench.py --gpus N``
-or plain ``python bench.py`` for N=1).  Every rank is a warm pool worker; rank 0 also runs
-the real control plane (training service -> scheduler with the chosen policy + Munkres
-placement -> PoolBackend) and submits the trace in real time.  Jobs are ResNet-50
-(ImageNet 224x224, batch 256/GPU) and BERT-base (seq 128) elastic data-parallel jobs in bf16
-(autocast) on PyTorch-ROCm, gradient all-reduce on RCCL over xGMI with bucket overlap,
-fused HIP optimizers, resized live (communicator rebuild + state broadcast).
+One process per GPU.  ``python bench.py --gpus N`` launches the N ranks itself (a child
+``python -m torch.distributed.run --nproc-per-node N`` started BEFORE this process touches
+the GPU; it exits with the child's code); under an external torchrun (WORLD_SIZE set) it
+runs as one of the ranks.  Every rank is a warm pool worker; rank 0 also runs the real
+control plane (training service -> scheduler with the chosen policy + Munkres placement ->
+PoolBackend) and submits the trace in real time.  Jobs are ResNet-50 (ImageNet 224x224,
+batch 256/GPU) and BERT-base (seq 128, batch 64/GPU) elastic data-parallel jobs: bf16
+autocast compute on PyTorch-ROCm + the HIP kernels, fp32 gradients all-reduced in fp32 on
+RCCL over xGMI with bucket overlap, fused HIP optimizers, resized live (communicator
+rebuild + state broadcast).
 
 Semantics of the driver flags:
-  --steps K   mean job length in single-GPU training steps (trace scale); weak scaling:
-              every job's work is multiplied by N, so per-GPU work is fixed as N grows.
+  --steps K   trace scale: the mean job is K x STEP_SCALE (=10) single-GPU training steps at
+              the per-GPU batch; weak scaling: every job's work is multiplied by N, so the
+              per-GPU work is fixed as N grows (~4 s of GPU work per job at N=1 for K=20).
   --warmup W  untimed warm-up steps of every model on every GPU (MIOpen/hipBLASLt caches,
               RCCL init) before the timed trace.
 The timed region (barrier + synchronize on both sides) is the whole trace: first submission
-to last completion.  ``value`` = average JCT in seconds (lower is better); makespan, resize
-latency and aggregate throughput are reported alongside.
+to last completion.  ``value`` = average JCT in seconds (lower is better); makespan, job-start
+latency, resize latency (world >= 2 transitions only: RCCL communicator rebuild + state
+broadcast) and aggregate throughput are reported alongside.
 """
 from __future__ import annotations
 
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import threading
 import time
 
 os.environ.setdefault("GLOO_SOCKET_IFNAME", "lo")
 os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+
+STEP_SCALE = 10  # single-GPU steps per unit of --steps in the mean job
+
+
+def _self_launch() -> None:
+    """``--gpus N`` (N > 1) without a torchrun around us: start the N ranks as a child
+    ``torch.distributed.run`` and exit with its code.  Runs before ``import torch`` -- this
+    process never initialises the GPU, so starting a child is safe."""
+    if "WORLD_SIZE" in os.environ:
+        return
+    ap = argparse.ArgumentParser(add_help=False)
+    ap.add_argument("--gpus", type=int, default=1)
+    a, _ = ap.parse_known_args()
+    if a.gpus <= 1:
+        return
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={a.gpus}",
+           "--master-addr=127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ, OMP_NUM_THREADS=os.environ.get("OMP_NUM_THREADS", "1"))
+    p = subprocess.Popen(cmd, env=env)
+    try:
+        rc = p.wait()
+    except KeyboardInterrupt:
+        p.terminate()
+        rc = p.wait()
+    sys.exit(rc)
+
+
+if __name__ == "__main__":
+    _self_launch()
 
 import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
@@ -45,6 +84,14 @@ from vodascheduler_amd.runtime.rendezvous import connect_store  # noqa: E402
 from vodascheduler_amd.sim.trace import bench_trace  # noqa: E402
 
 BASELINE_METRIC = "avg JCT + makespan, 32-job trace on 1/2/4/8 MI355X; elastic-resize latency"
+# Reschedule rate limit.  The reference's 30 s (scheduler.go:212) amortises a resize that costs
+# a pod deletion/creation + ConfigMap propagation (tens of seconds); here a resize is a
+# membership epoch on warm per-GPU workers (RCCL rebuild + state broadcast, ~0.01-1 s), so the
+# limit is scaled with that cost -- and with this trace's seconds-long jobs -- to 2 s.
+RATE_LIMIT_S = 2.0
+RATE_LIMIT_NOTE = ("reference default 30 s amortises pod-based resizes (tens of s); warm-pool resizes cost "
+                   "~0.01-1 s and jobs here last seconds, so the limit is scaled to 2 s; completions and "
+                   "arrivals on idle GPUs reschedule at once (work-conserving, docs/deviations.md)")
 MODELS = ("resnet50", "bert-base")
 BATCH = {"resnet50": 256, "bert-base": 64}
 # --device cpu: rehearsal of the multi-rank orchestration on gloo with tiny models (tests);
@@ -63,7 +110,7 @@ def sync(device):
         torch.cuda.synchronize(device)
 
 
-def warmup(device, steps: int, models, batch, compression=None):
+def warmup(device, steps: int, models, batch, compression=None, grad_dtype="fp32"):
     """Untimed warm-up of every model in the mix on this device (single-GPU steps).
 
     The steps run on the pool worker's own warm workload cache (``workloads.train.get_warm``
@@ -76,7 +123,8 @@ def warmup(device, steps: int, models, batch, compression=None):
 
     out = {}
     for name in models:
-        wm = get_warm(TrainConfig(model=name, per_gpu_batch=batch[name], compression=compression), device)
+        wm = get_warm(TrainConfig(model=name, per_gpu_batch=batch[name], compression=compression,
+                                  grad_dtype=grad_dtype), device)
         m, opt, b = wm.model, wm.opt, wm.pool[0]
         t0 = None
         for i in range(max(2, steps)):
@@ -106,14 +154,18 @@ def main():
                             format=f"%(asctime)s [rank {os.environ.get('RANK', '0')}] %(name)s: %(message)s")
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=30)
+    ap.add_argument("--steps", type=int, default=20,
+                    help=f"trace scale: mean job = steps x {STEP_SCALE} single-GPU steps (x N GPUs, weak scaling)")
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--jobs", type=int, default=32)
     ap.add_argument("--algorithm", default="FfDLOptimizer")
-    ap.add_argument("--rate-limit", type=float, default=2.0)
-    ap.add_argument("--interarrival", type=float, default=0.5)
+    ap.add_argument("--rate-limit", type=float, default=RATE_LIMIT_S)
+    ap.add_argument("--interarrival", type=float, default=2.0, help="mean Poisson interarrival (s)")
     ap.add_argument("--commit-every", type=int, default=4)
-    ap.add_argument("--compression", default=None, choices=[None, "bf16", "fp16"])
+    ap.add_argument("--compression", default=None, choices=[None, "bf16", "fp16"],
+                    help="gradient all-reduce compression (Horovod --fp16-allreduce); default: fp32 all-reduce")
+    ap.add_argument("--grad-dtype", default="fp32", choices=["fp32", "bf16"],
+                    help="flat gradient buffer precision (bf16 = opt-in low-precision gradients)")
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--out", default=None, help="also write the JSON line (+details) to this file")
     ap.add_argument("--trace", default=None, help="write the scheduler timeline (Chrome-trace JSON) here")
@@ -153,7 +205,7 @@ def main():
 
     # ---------------- untimed warm-up ----------------
     log(rank, f"warm-up: {a.warmup} steps x {models} on {world} {a.device} device(s)")
-    step_ms = warmup(device, a.warmup, models, batch, a.compression)
+    step_ms = warmup(device, a.warmup, models, batch, a.compression, a.grad_dtype)
     if world > 1:
         if comm_backend == "rccl":
             comm = RcclCommunicator(store, "bench/warm", rank, world, device)
@@ -164,11 +216,12 @@ def main():
         dist.barrier()
     log(rank, f"warm-up single-GPU step ms: {step_ms}")
 
-    trace = bench_trace(a.jobs, a.steps, world, a.seed, a.interarrival, models, batch)
+    trace = bench_trace(a.jobs, a.steps * STEP_SCALE, world, a.seed, a.interarrival, models, batch)
     locs = [("node0", r) for r in range(world)]
     os.environ.setdefault("VODA_CKPT_DIR", f"/tmp/voda_ckpt_{os.getpid()}")
     metrics_dir = f"/tmp/voda_metrics_{port[0]}"
-    defaults = {"commit_every": a.commit_every, "compression": a.compression, "metrics_dir": metrics_dir}
+    defaults = {"commit_every": a.commit_every, "compression": a.compression, "metrics_dir": metrics_dir,
+                "grad_dtype": a.grad_dtype}
 
     # ---------------- timed region ----------------
     if world > 1:
@@ -202,7 +255,8 @@ def main():
     # ---------------- aggregate ----------------
     my = {"steps": sum((r["result"] or {}).get("steps", 0) for r in recs if isinstance(r["result"], dict)),
           "train_time": sum((r["result"] or {}).get("train_time", 0.0) for r in recs if isinstance(r["result"], dict)),
-          "comm_init": [x.get("comm_init_s") for r in recs for x in r["resize_log"]]}
+          "comm_init": [(x.get("world"), x.get("comm_init_s"), x.get("cached")) for r in recs
+                        for x in r["resize_log"]]}
     allrec = [my]
     if world > 1:
         allrec = [None] * world
@@ -217,6 +271,9 @@ def main():
             raise SystemExit(f"bench failed: {result['error']}")
         tot_steps = sum(r["steps"] for r in allrec)
         tot_train = sum(r["train_time"] for r in allrec)
+        inits = [(w, t, c) for r in allrec for (w, t, c) in r["comm_init"] if w and w > 1 and t is not None]
+        fresh = sorted(t for w, t, c in inits if not c)
+        q = lambda xs, p: round(xs[min(len(xs) - 1, int(p * len(xs)))], 4) if xs else None  # noqa: E731
         samples = 0
         for tj in trace:
             from vodascheduler_amd.sim.trace import workload_of
@@ -235,6 +292,8 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "bf16" if a.device == "cuda" else "fp32",
+            "grad_dtype": a.grad_dtype,
+            "allreduce_dtype": a.compression or a.grad_dtype,
             "data": "synthetic (random-init weights, synthetic batches of the real shapes)"
                     + ("" if a.device == "cuda" else "; CPU/gloo orchestration rehearsal, not a benchmark")
                     + ("; all ranks share cuda:0 over gloo: rehearsal, not a benchmark" if a.share_gpu else ""),
@@ -250,9 +309,21 @@ def main():
             "makespan_s": round(result["makespan_s"], 3),
             "p95_jct_s": round(result["p95_jct_s"], 3),
             "wall_s": round(wall_s, 3),
-            "resize_events": result["resize_events"],
+            "mean_job_steps_1gpu": a.steps * STEP_SCALE,
+            "rate_limit_s": a.rate_limit,
+            "rate_limit_note": RATE_LIMIT_NOTE,
+            "membership_changes": result["resize_events"],
+            "resize_events": result["n_resizes"],
+            "job_start_latency_p50_s": result["start_latency_p50_s"],
+            "job_start_latency_p95_s": result["start_latency_p95_s"],
             "resize_latency_p50_s": result["resize_latency_p50_s"],
             "resize_latency_p95_s": result["resize_latency_p95_s"],
+            "resize_latency_note": "world>=2 transitions only (membership published -> new epoch synced: "
+                                   "RCCL communicator rebuild or cache hit + state broadcast)",
+            "rccl_comm_builds": len(fresh),
+            "rccl_comm_cache_hits": sum(1 for w, t, c in inits if c),
+            "rccl_init_p50_s": q(fresh, 0.5),
+            "rccl_init_p95_s": q(fresh, 0.95),
             "throughput_samples_per_s": round(samples / wall_s, 1),
             "warmup_single_gpu_step_ms": {k: round(v, 2) for k, v in step_ms.items()},
         }

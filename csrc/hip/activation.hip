@@ -4,7 +4,7 @@
 // batch 64 x 128) is the largest activation of the transformer step; PyTorch's elementwise
 // GELU kernels ran at ~60 % of HBM bandwidth (0.62 ms per step, profiles/).  Here every lane
 // moves 16 B per access (8 bf16), the math is fp32 with one v_exp_f32 + one v_rcp_f32 per element, and the
-// backward writes dh over the incoming gradient's buffer (no allocation; the caller owns it).
+// backward writes dh into a separate buffer the caller allocates (dy may still be read by others).
 //
 //   g(h)  = 0.5 h (1 + tanh(u)),             u = k (h + c h^3), k = sqrt(2/pi), c = 0.044715
 //   g'(h) = 0.5 (1 + t) + 0.5 h (1 - t^2) k (1 + 3 c h^2)

@@ -38,11 +38,11 @@ void adasum_combine(uintptr_t a, uintptr_t b, uintptr_t out, int dt, uintptr_t m
 int64_t wgrad_conv_workspace_floats(int M, int Cout, int Cin, int taps, int splits);
 void wgrad_conv(uintptr_t dy, uintptr_t x, uintptr_t dw, int Nimg, int H, int W, int Cin, int Ho, int Wo, int Cout,
                 int KH, int KW, int stride, int pad, int splits, uintptr_t ws, bool accumulate, uintptr_t zero,
-                uintptr_t stream);
+                int out_dt, uintptr_t stream);
 int64_t wgrad_workspace_floats(int M, int N, int K, int splits);
 void wgrad_gemm(uintptr_t dy, int64_t ldy, uintptr_t x, int64_t ldx, uintptr_t dw, int64_t ldw, uintptr_t db, int M,
                 int N, int K, int splits, uintptr_t ws, bool accumulate, uintptr_t zero, int variant,
-                uintptr_t stream);
+                int out_dt, uintptr_t stream);
 
 // ---- tanh GELU (activation.hip); bwd may run in place (dh == dy) ----
 void gelu_tanh_fwd(uintptr_t h, uintptr_t y, int64_t n, int dt, uintptr_t stream);

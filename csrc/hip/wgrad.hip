@@ -45,6 +45,10 @@ struct WgradArgs {
   const uint16_t* x; int64_t ldx;    // [M][K]
   uint16_t* dw; int64_t ldw;         // [N][K]        (splits == 1)
   uint16_t* db;                      // [N] or null   (splits == 1)
+  // out_f32: dW / db are fp32 (the optimizer's fp32 flat gradient of a bf16 model: one
+  // rounding of the fp32 MFMA accumulators, none of the bf16 accumulate-and-round); the
+  // pointers above are then reinterpreted as float*
+  int out_f32;
   float* ws;                         // [S][N][K] + [S][N] partial slabs (splits > 1)
   const uint16_t* zero;              // >= 16 zero bytes: source of rows past the split (LDS-DMA path)
   int M, N, K, S, m_split, tiles_k, remap, accumulate, bias;
@@ -87,6 +91,17 @@ __device__ __forceinline__ wg_f32x16 wg_mfma(wg_bf16x8 a, wg_bf16x8 b, wg_f32x16
   return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
 }
 
+// dW / db element (+)= v in the output precision (bf16 or fp32)
+__device__ __forceinline__ void wg_store_out(uint16_t* base, int64_t idx, float v, int accumulate, int out_f32) {
+  if (out_f32) {
+    float* o = reinterpret_cast<float*>(base) + idx;
+    *o = v + (accumulate ? *o : 0.f);
+  } else {
+    uint16_t* o = base + idx;
+    *o = f2bf(v + (accumulate ? bf2f(*o) : 0.f));
+  }
+}
+
 // C/D lane map of v_mfma_f32_32x32x16_bf16: col = lane & 31, row = (reg&3) + 8*(reg>>2) + 4*h.
 // splits == 1: accumulate into dW / db directly; else write this split's fp32 slab.
 __device__ __forceinline__ void wgrad_epilogue(const WgradArgs& p, int split, int n0, int k0, int wn, int wk,
@@ -103,9 +118,7 @@ __device__ __forceinline__ void wgrad_epilogue(const WgradArgs& p, int split, in
       const int row = rbase + (reg & 3) + 8 * (reg >> 2) + 4 * h;
       if (row < p.N) {
         if (p.S == 1) {
-          uint16_t* o = p.dw + int64_t(row) * p.ldw + p.col0 + col;
-          const float v = acc[reg] + (p.accumulate ? bf2f(*o) : 0.f);
-          *o = f2bf(v);
+          wg_store_out(p.dw, int64_t(row) * p.ldw + p.col0 + col, acc[reg], p.accumulate, p.out_f32);
         } else {
           p.ws[(int64_t(split) * p.N + row) * p.ws_ld + p.col0 + col] = acc[reg];
         }
@@ -125,8 +138,7 @@ __device__ __forceinline__ void wgrad_epilogue(const WgradArgs& p, int split, in
         const int row = rbase + (reg & 3) + 8 * (reg >> 2) + 4 * h;
         if (row < p.N) {
           if (p.S == 1) {
-            const float v = acc[reg] + (p.accumulate ? bf2f(p.db[row]) : 0.f);
-            p.db[row] = f2bf(v);
+            wg_store_out(p.db, row, acc[reg], p.accumulate, p.out_f32);
           } else {
             wsb[row] = acc[reg];
           }
@@ -609,9 +621,7 @@ __global__ __launch_bounds__(kWwThreads, 1) void wgrad_wide_kernel(WgradArgs p) 
           const int row = n0 + wn * 128 + 32 * f + (reg & 3) + 8 * (reg >> 2) + 4 * h;
           if (row < p.N) {
             if (p.S == 1) {
-              uint16_t* o = p.dw + int64_t(row) * p.ldw + col;
-              const float v = c[f][e][reg] + (p.accumulate ? bf2f(*o) : 0.f);
-              *o = f2bf(v);
+              wg_store_out(p.dw, int64_t(row) * p.ldw + col, c[f][e][reg], p.accumulate, p.out_f32);
             } else {
               p.ws[(int64_t(split) * p.N + row) * p.ws_ld + col] = c[f][e][reg];
             }
@@ -628,7 +638,7 @@ __global__ __launch_bounds__(kWwThreads, 1) void wgrad_wide_kernel(WgradArgs p) 
       const int row = n0 + wn * 128 + 32 * f + col_l;
       if (h == 0 && row < p.N) {
         if (p.S == 1) {
-          p.db[row] = f2bf(tot + (p.accumulate ? bf2f(p.db[row]) : 0.f));
+          wg_store_out(p.db, row, tot, p.accumulate, p.out_f32);
         } else {
           p.ws[int64_t(p.S) * p.N * p.ws_ld + int64_t(split) * p.N + row] = tot;
         }
@@ -638,9 +648,35 @@ __global__ __launch_bounds__(kWwThreads, 1) void wgrad_wide_kernel(WgradArgs p) 
 }
 
 // dW[n][k] (+)= sum_s ws[s][n][k]; db[n] (+)= sum_s wsb[s][n].  4 columns per thread (K % 8 == 0).
+// OutT = uint16_t (bf16 gradient) or float (fp32 gradient).
+__device__ __forceinline__ void wg_acc4(uint16_t* o, float4 s, int accumulate) {
+  uint2* o2 = reinterpret_cast<uint2*>(o);
+  if (accumulate) {
+    const uint2 u = *o2;
+    s.x += bf2f(u.x & 0xffff); s.y += bf2f(u.x >> 16); s.z += bf2f(u.y & 0xffff); s.w += bf2f(u.y >> 16);
+  }
+  uint2 r;
+  r.x = uint32_t(f2bf(s.x)) | (uint32_t(f2bf(s.y)) << 16);
+  r.y = uint32_t(f2bf(s.z)) | (uint32_t(f2bf(s.w)) << 16);
+  *o2 = r;
+}
+__device__ __forceinline__ void wg_acc4(float* o, float4 s, int accumulate) {
+  float4* o4 = reinterpret_cast<float4*>(o);
+  if (accumulate) {
+    const float4 u = *o4;
+    s.x += u.x; s.y += u.y; s.z += u.z; s.w += u.w;
+  }
+  *o4 = s;
+}
+__device__ __forceinline__ float wg_ld(const uint16_t* o) { return bf2f(*o); }
+__device__ __forceinline__ float wg_ld(const float* o) { return *o; }
+__device__ __forceinline__ void wg_st(uint16_t* o, float v) { *o = f2bf(v); }
+__device__ __forceinline__ void wg_st(float* o, float v) { *o = v; }
+
+template <typename OutT>
 __global__ __launch_bounds__(256) void wgrad_reduce_kernel(const float* __restrict__ ws, int S, int N, int K,
-                                                           uint16_t* __restrict__ dw, int64_t ldw,
-                                                           uint16_t* __restrict__ db, int accumulate) {
+                                                           OutT* __restrict__ dw, int64_t ldw,
+                                                           OutT* __restrict__ db, int accumulate) {
   const int64_t NK = int64_t(N) * K;
   const int64_t n4 = NK >> 2;
   const int64_t total = n4 + (db != nullptr ? N : 0);
@@ -654,24 +690,24 @@ __global__ __launch_bounds__(256) void wgrad_reduce_kernel(const float* __restri
       }
       const int64_t e = i << 2;
       const int64_t row = e / K, col = e - row * K;
-      uint2* o = reinterpret_cast<uint2*>(dw + row * ldw + col);
-      if (accumulate) {
-        const uint2 u = *o;
-        s.x += bf2f(u.x & 0xffff); s.y += bf2f(u.x >> 16); s.z += bf2f(u.y & 0xffff); s.w += bf2f(u.y >> 16);
-      }
-      uint2 r;
-      r.x = uint32_t(f2bf(s.x)) | (uint32_t(f2bf(s.y)) << 16);
-      r.y = uint32_t(f2bf(s.z)) | (uint32_t(f2bf(s.w)) << 16);
-      *o = r;
+      wg_acc4(dw + row * ldw + col, s, accumulate);
     } else {
       const int64_t n = i - n4;
       const float* wsb = ws + int64_t(S) * NK;
       float s = 0.f;
       for (int sp = 0; sp < S; ++sp) s += wsb[int64_t(sp) * N + n];
-      if (accumulate) s += bf2f(db[n]);
-      db[n] = f2bf(s);
+      if (accumulate) s += wg_ld(db + n);
+      wg_st(db + n, s);
     }
   }
+}
+
+template <typename OutT>
+void wg_launch_reduce(const WgradArgs& a, int S, int N, int K, int64_t ldw, bool bias, hipStream_t s) {
+  const int64_t work = (int64_t(N) * K) / 4 + (bias ? N : 0);
+  hipLaunchKernelGGL((wgrad_reduce_kernel<OutT>), dim3(stream_grid(work)), dim3(256), 0, s, a.ws, S, N, K,
+                     reinterpret_cast<OutT*>(a.dw), ldw, bias ? reinterpret_cast<OutT*>(a.db) : nullptr,
+                     a.accumulate);
 }
 
 struct WgradPlan {
@@ -699,7 +735,8 @@ int64_t wgrad_workspace_floats(int M, int N, int K, int splits) {
 
 void wgrad_gemm(uintptr_t dy, int64_t ldy, uintptr_t x, int64_t ldx, uintptr_t dw, int64_t ldw, uintptr_t db, int M,
                 int N, int K, int splits, uintptr_t ws, bool accumulate, uintptr_t zero, int variant,
-                uintptr_t stream) {
+                int out_dt, uintptr_t stream) {
+  VODA_CHECK(out_dt == kBF16 || out_dt == kF32, "wgrad: dW must be bf16 or fp32");
   VODA_CHECK(M > 0 && N >= 8 && K >= 8, "wgrad: empty problem");
   VODA_CHECK(N % 8 == 0 && K % 8 == 0, "wgrad: N and K must be multiples of 8");
   VODA_CHECK(ldy >= N && ldx >= K && ldw >= K, "wgrad: leading dimension too small");
@@ -723,6 +760,8 @@ void wgrad_gemm(uintptr_t dy, int64_t ldy, uintptr_t x, int64_t ldx, uintptr_t d
   a.remap = (pl.grid % 8 == 0) ? 1 : 0;
   a.accumulate = accumulate ? 1 : 0;
   a.bias = db != 0 ? 1 : 0;
+  a.out_f32 = out_dt == kF32 ? 1 : 0;
+  VODA_CHECK(!a.out_f32 || (ldw % 4 == 0 && dw % 16 == 0), "wgrad: fp32 dW rows must be 16-byte aligned");
   hipStream_t s = as_stream(stream);
   VODA_CHECK(variant >= 0 && variant <= 8, "wgrad: variant must be 0..8");
   if (variant == 0)
@@ -745,9 +784,10 @@ void wgrad_gemm(uintptr_t dy, int64_t ldy, uintptr_t x, int64_t ldx, uintptr_t d
     hipLaunchKernelGGL((wgrad_wide_kernel<3, 32>), dim3(unsigned(pl.grid)), dim3(kWwThreads), 0, s, a);
   check_launch();
   if (pl.S > 1) {
-    const int64_t work = (int64_t(N) * K) / 4 + (db != 0 ? N : 0);
-    hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(stream_grid(work)), dim3(256), 0, s, a.ws, pl.S, N, K, a.dw, ldw,
-                       a.db, a.accumulate);
+    if (a.out_f32)
+      wg_launch_reduce<float>(a, pl.S, N, K, ldw, db != 0, s);
+    else
+      wg_launch_reduce<uint16_t>(a, pl.S, N, K, ldw, db != 0, s);
     check_launch();
   }
 }
@@ -763,7 +803,8 @@ int64_t wgrad_conv_workspace_floats(int M, int Cout, int Cin, int taps, int spli
 // gathered by the LDS-DMA loader (zero rows outside the image).
 void wgrad_conv(uintptr_t dy, uintptr_t x, uintptr_t dw, int Nimg, int H, int W, int Cin, int Ho, int Wo, int Cout,
                 int KH, int KW, int stride, int pad, int splits, uintptr_t ws, bool accumulate, uintptr_t zero,
-                uintptr_t stream) {
+                int out_dt, uintptr_t stream) {
+  VODA_CHECK(out_dt == kBF16 || out_dt == kF32, "wgrad_conv: dW must be bf16 or fp32");
   VODA_CHECK(Nimg > 0 && H > 0 && W > 0 && Ho > 0 && Wo > 0 && KH > 0 && KW > 0 && stride > 0 && pad >= 0,
              "wgrad_conv: bad geometry");
   VODA_CHECK(Cin % 8 == 0 && Cout % 8 == 0 && Cin >= 8 && Cout >= 8, "wgrad_conv: channels must be multiples of 8");
@@ -793,6 +834,7 @@ void wgrad_conv(uintptr_t dy, uintptr_t x, uintptr_t dw, int Nimg, int H, int W,
   a.adv_wo = (BM % (Ho * Wo)) % Wo;
   a.accumulate = accumulate ? 1 : 0;
   a.bias = 0;
+  a.out_f32 = out_dt == kF32 ? 1 : 0;
   const int64_t grid = int64_t(pl.grid) * taps;
   a.remap = (grid % 8 == 0) ? 1 : 0;
   hipStream_t s = as_stream(stream);
@@ -800,9 +842,10 @@ void wgrad_conv(uintptr_t dy, uintptr_t x, uintptr_t dw, int Nimg, int H, int W,
   check_launch();
   if (pl.S > 1) {
     const int Kt = taps * Cin;
-    const int64_t work = (int64_t(Cout) * Kt) / 4;
-    hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(stream_grid(work)), dim3(256), 0, s, a.ws, pl.S, Cout, Kt, a.dw,
-                       a.ldw, static_cast<uint16_t*>(nullptr), a.accumulate);
+    if (a.out_f32)
+      wg_launch_reduce<float>(a, pl.S, Cout, Kt, a.ldw, false, s);
+    else
+      wg_launch_reduce<uint16_t>(a, pl.S, Cout, Kt, a.ldw, false, s);
     check_launch();
   }
 }

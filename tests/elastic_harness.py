@@ -1,0 +1,132 @@
+"""Scripted elastic-job controller + pool-worker processes for the elastic-state equivalence
+tests (CPU/gloo here, RCCL on a multi-GPU box).  The controller speaks the PoolBackend
+protocol directly (membership epochs + worker mailboxes, runtime/pool.py) so a test can
+resize, halt, restart and kill at chosen steps."""
+from __future__ import annotations
+
+import json
+import multiprocessing as mp
+import os
+import time
+from dataclasses import asdict
+
+import torch
+
+from vodascheduler_amd.runtime.rendezvous import JobRendezvous, connect_store
+
+
+def worker_proc(port: int, wid: str, device: str, backend: str, q) -> None:
+    torch.set_num_threads(1)
+    from vodascheduler_amd.runtime.pool import PoolWorker
+
+    dev = torch.device(device)
+    if dev.type == "cuda":
+        torch.cuda.set_device(dev)
+    store = connect_store("127.0.0.1", port)
+    watch = connect_store("127.0.0.1", port)
+    recs = PoolWorker(store, watch, wid, dev, backend=backend, timeout=120.0).serve()
+    q.put((wid, [{k: r[k] for k in ("job", "result")} for r in recs]))
+
+
+class Controller:
+    def __init__(self, store, job: str, cfg):
+        self.store = store
+        self.job = job
+        self.cfg = asdict(cfg)
+        self.rdzv = JobRendezvous(store, job)
+        self.members: list[str] = []
+        self.mail_n: dict[str, int] = {}
+
+    def _mail(self, wid: str, msg: dict) -> None:
+        n = self.mail_n.get(wid, 0) + 1
+        self.mail_n[wid] = n
+        self.store.set(f"pool/{wid}/msg/{n}", json.dumps(msg))
+        self.store.add(f"pool/{wid}/n", 1)
+
+    def publish(self, members: list[str], abort: bool = False, wait_sync: bool = True, timeout: float = 60) -> int:
+        e = self.rdzv.publish(members, abort=abort)
+        for w in members:
+            if w not in self.members:
+                self._mail(w, {"job": self.job, "epoch": e, "cfg": self.cfg})
+        self.members = list(members)
+        if wait_sync and members:
+            self.wait(lambda: self.rdzv.get(f"e/{e}/synced") is not None or self.rdzv.outcome() is not None,
+                      timeout, f"epoch {e} synced")
+        return e
+
+    def progress(self) -> int:
+        v = self.rdzv.get("progress")
+        return int(v) if v is not None else -1
+
+    def wait_progress(self, step: int, timeout: float = 60) -> None:
+        self.wait(lambda: self.progress() >= step or self.rdzv.outcome() is not None, timeout, f"step {step}")
+
+    def wait_state_at_rest(self, timeout: float = 60) -> None:
+        self.wait(lambda: (self.rdzv.get_live_epoch() or 0) < 0, timeout, "state at rest")
+
+    def wait_done(self, timeout: float = 120) -> str:
+        self.wait(lambda: self.rdzv.outcome() is not None, timeout, "job outcome")
+        return self.rdzv.outcome()
+
+    @staticmethod
+    def wait(cond, timeout: float, what: str) -> None:
+        deadline = time.monotonic() + timeout
+        while not cond():
+            if time.monotonic() > deadline:
+                raise TimeoutError(f"timed out waiting for {what}")
+            time.sleep(0.005)
+
+
+def start_pool(wids: list[str], devices: list[str], backend: str):
+    """Store server (this process) + one spawned PoolWorker per wid."""
+    from vodascheduler_amd.runtime.cluster import free_port
+
+    port = free_port()
+    store = connect_store("127.0.0.1", port, is_master=True)
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = {w: ctx.Process(target=worker_proc, args=(port, w, d, backend, q), daemon=True)
+             for w, d in zip(wids, devices)}
+    for p in procs.values():
+        p.start()
+    return store, procs, q
+
+
+def stop_pool(store, procs, q, timeout: float = 30) -> dict:
+    store.set("pool/shutdown", "1")
+    out = {}
+    deadline = time.monotonic() + timeout
+    alive = [w for w, p in procs.items() if p.is_alive() or p.exitcode == 0]
+    while len(out) < len(alive) and time.monotonic() < deadline:
+        try:
+            w, recs = q.get(timeout=max(0.1, deadline - time.monotonic()))
+            out[w] = recs
+        except Exception:
+            break
+    for p in procs.values():
+        p.join(5)
+        if p.is_alive():
+            p.kill()
+    return out
+
+
+def assert_matches_replay(cfg, path: str, device: str, exact: bool = True) -> dict:
+    """The elastic run's final state (rank 0's checkpoint) equals the uninterrupted replay."""
+    from vodascheduler_amd.workloads.train import replay_reference
+
+    payload = torch.load(path, map_location="cpu", weights_only=True)
+    ex = payload["extras"]
+    nthreads = torch.get_num_threads()
+    torch.set_num_threads(1)
+    try:
+        ref, ref_ex = replay_reference(cfg, list(ex["world_log"]), int(ex["__step__"]), torch.device(device))
+    finally:
+        torch.set_num_threads(nthreads)
+    assert len(ref) == len(payload["tensors"])
+    for i, (a, b) in enumerate(zip(payload["tensors"], ref)):
+        if exact:
+            assert torch.equal(a, b), (i, float((a.float() - b.float()).abs().max()))
+        else:  # GPU: nondeterministic reductions (atomics) make trajectories differ in the last bits
+            torch.testing.assert_close(a.float(), b.float(), rtol=2e-3, atol=2e-4)
+    assert ex["epoch"] == ref_ex["epoch"] and ex["samples"] == ref_ex["samples"]
+    return ex

@@ -89,3 +89,17 @@ def test_convkxk_layer_flat_grads_match_autograd():
     for got, want in ((m.weight.grad, ref_w.grad), (xg.grad, xr.grad)):
         rel = float((got.float() - want).norm() / want.norm())
         assert rel < 1e-2, rel
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n,cin,cout,h,w,stride", [(2, 128, 128, 56, 56, 2), (4, 256, 256, 14, 14, 1)])
+@pytest.mark.parametrize("splits", [1, 16])
+def test_conv_wgrad_fp32_output(n, cin, cout, h, w, stride, splits):
+    """fp32 weight gradient (the default flat-gradient precision of a bf16 model)."""
+    dy, x, gw = _case(n, cin, cout, h, w, stride, seed=2)
+    g32 = gw.float().contiguous(memory_format=torch.channels_last)
+    want = C.conv_wgrad_ref(dy, x, gw.shape, stride, 1) + g32
+    C.conv_wgrad_accumulate_(dy, x, g32, stride, 1, splits=splits)
+    torch.cuda.synchronize()
+    rel = float((g32 - want).norm() / want.norm())
+    assert rel < 1e-4, rel

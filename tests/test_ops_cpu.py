@@ -130,9 +130,57 @@ def test_optimizer_splits_param_groups_by_dtype():
     dts = sorted(str(fg.param_dtype) for fg in opt.flat_groups)
     assert dts == ["torch.bfloat16", "torch.float32"]
     bf = next(fg for fg in opt.flat_groups if fg.param_dtype == torch.bfloat16)
-    assert bf.master.dtype == torch.float32 and bf.lowp.dtype == torch.bfloat16 and bf.grad.dtype == torch.bfloat16
+    # fp32 gradients by default, also for the bf16 compute weights
+    assert bf.master.dtype == torch.float32 and bf.lowp.dtype == torch.bfloat16 and bf.grad.dtype == torch.float32
+    assert bf.mixed and all(p.grad is None for p in bf.params)
     n = sum(p.numel() for p in {id(p): p for p in m.parameters()}.values())
     assert sum(sum(s.numel for s in fg.slots) for fg in opt.flat_groups) == n
+    # bf16 gradients are opt-in
+    m2 = cast_compute_weights_(BertBase(vocab=100, seq_len=8, d_model=32, heads=2, d_ff=64, layers=1))
+    opt2 = FusedAdamW(m2.parameters(), lr=1e-3, grad_dtype=torch.bfloat16)
+    bf2 = next(fg for fg in opt2.flat_groups if fg.param_dtype == torch.bfloat16)
+    assert bf2.grad.dtype == torch.bfloat16 and not bf2.mixed
+
+
+def test_mixed_precision_flat_grads_fold_autograd_grads():
+    """bf16 weights + fp32 flat gradient: autograd's bf16 .grad is folded into the fp32 slot
+    (post-accumulate hook) before the data-parallel readiness hook, and dropped."""
+    from vodascheduler_amd.models import cast_compute_weights_
+    from vodascheduler_amd.ops.optim import FusedSGD
+    from vodascheduler_amd.parallel.ddp import ElasticDDP
+    from vodascheduler_amd.utils.flat import grad_of
+
+    torch.manual_seed(0)
+    m = cast_compute_weights_(torch.nn.Sequential(torch.nn.Linear(16, 32), torch.nn.ReLU(), torch.nn.Linear(32, 4)))
+    ref = cast_compute_weights_(torch.nn.Sequential(torch.nn.Linear(16, 32), torch.nn.ReLU(), torch.nn.Linear(32, 4)))
+    ref.load_state_dict(m.state_dict())
+    opt = FusedSGD(m.parameters(), lr=0.1)
+    order = []
+    ddp = ElasticDDP(m, None, opt)
+    real = ddp._on_grad
+
+    def spy(p):
+        order.append((id(p), p.grad is None, float(grad_of(p).abs().sum())))
+        real(p)
+
+    for p in m.parameters():
+        h = p._post_accumulate_grad_hooks
+        # replace DDP's readiness hook (registered last) by the spy
+        k = list(h)[-1]
+        h[k] = spy
+    x = torch.randn(8, 16).bfloat16()
+    for _ in range(2):  # grads accumulate in fp32 across two backward passes
+        m(x).float().sum().backward()
+        ref(x).float().sum().backward()
+    for p, q in zip(m.parameters(), ref.parameters()):
+        assert p.grad is None
+        g = grad_of(p)
+        assert g.dtype == torch.float32
+        torch.testing.assert_close(g, q.grad.float(), atol=3e-2, rtol=2e-2)
+    # the readiness hook saw the folded gradient (fold runs first)
+    assert order and all(none and s > 0 for _, none, s in order)
+    ddp.finalize()
+    assert ddp.calibrated
 
 
 def test_fused_linear_direct_accumulation_matches_autograd():

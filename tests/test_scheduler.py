@@ -327,3 +327,29 @@ def test_simulated_drain_migrations():
     tr = philly_trace(16, seed=3)
     r = simulate(tr, "ElasticFIFO", gpus=8, drain=[(100.0, "node0", 3), (200.0, "node0", 5)])
     assert r.n_jobs == 16 and r.migrations >= 1
+
+
+def test_gpu_time_charged_at_allocation_held_during_interval():
+    """the interval closed at a halt / scale-out is charged at the OLD allocation."""
+    e = Env(gpus=4, algorithm="Tiresias", rate=0)
+    low = e.submit("low", 2, 2, 2, prio=1)
+    e.step()
+    assert e.core.job_num_gpu[low] == 2
+    e.clock.advance(10)
+    hi = e.submit("hi", 4, 4, 4, prio=0)
+    e.step()  # low is halted: its last 10 s ran on 2 GPUs
+    assert e.core.job_num_gpu[low] == 0
+    m = e.core.ready_jobs[low].time_metrics
+    assert m.gpu_time == pytest.approx(20.0)
+    assert m.last_gpu_time == pytest.approx(20.0)
+    # scale-out: a 1-GPU elastic job grows to 4 once the other finishes
+    e2 = Env(gpus=4, algorithm="ElasticFIFO", rate=0)
+    a = e2.submit("a", 2, 2, 2)
+    b = e2.submit("b", 1, 1, 4)
+    e2.step()
+    assert e2.core.job_num_gpu[b] == 2
+    e2.clock.advance(5)
+    e2.core.handle_job_finished(a, True)
+    e2.step()
+    assert e2.core.job_num_gpu[b] == 4
+    assert e2.core.ready_jobs[b].time_metrics.gpu_time == pytest.approx(10.0)

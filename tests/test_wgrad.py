@@ -122,6 +122,46 @@ def test_fused_linear_backward_uses_kernel_and_matches_autograd():
     opt.zero_grad()
     lin(x.bfloat16()).float().square().mean().backward()
     ref(x.bfloat16().float()).square().mean().backward()
-    for got, want in ((lin.weight.grad, ref.weight.grad), (lin.bias.grad, ref.bias.grad)):
+    from vodascheduler_amd.utils.flat import grad_of
+
+    for got, want in ((grad_of(lin.weight), ref.weight.grad), (grad_of(lin.bias), ref.bias.grad)):
         rel = (got.float() - want).norm() / want.norm()
         assert rel < 1e-2, rel
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("variant", [0, 2, 6])
+@pytest.mark.parametrize("splits", [1, 4])
+@pytest.mark.parametrize("accumulate", [True, False])
+def test_wgrad_kernel_fp32_output(variant, splits, accumulate):
+    """fp32 dW / db (the default flat-gradient precision): the fp32 MFMA accumulators are
+    rounded once, so the result matches the fp32 reference to summation-order error."""
+    M, N, K = 1000, 264, 392
+    dy, x, gw, gb = _case(M, N, K, seed=5)
+    gw32, gb32 = gw.float(), gb.float()
+    w_ref, b_ref = W.wgrad_ref(dy, x, gw32, gb32, accumulate)
+    assert W.supported(dy, x, gw32, gb32)
+    W.wgrad_accumulate_(dy, x, gw32, gb32, accumulate=accumulate, splits=splits, variant=variant)
+    torch.cuda.synchronize()
+    torch.testing.assert_close(gw32, w_ref, rtol=1e-4, atol=1e-3)
+    torch.testing.assert_close(gb32, b_ref, rtol=1e-4, atol=1e-3)
+
+
+@pytest.mark.gpu
+def test_fused_linear_fp32_flat_grad_default_and_bf16_opt_in():
+    from vodascheduler_amd.ops import dense
+    from vodascheduler_amd.ops.optim import make_optimizer
+    from vodascheduler_amd.utils.flat import grad_of
+
+    torch.manual_seed(1)
+    x = torch.randn(2048, 768, device="cuda").bfloat16()
+    for gdt in (None, torch.bfloat16):
+        lin = dense.FusedLinear(768, 768).cuda().bfloat16()
+        opt = make_optimizer("sgd", lin.parameters(), lr=0.0, grad_dtype=gdt)
+        opt.zero_grad()
+        lin(x).float().square().mean().backward()
+        g = grad_of(lin.weight)
+        assert g.dtype == (gdt or torch.float32)
+        want = (2.0 / lin(x).numel()) * (lin(x).float().t() @ x.float())
+        rel = float((g.float() - want).norm() / want.norm())
+        assert rel < (1e-3 if gdt is None else 1e-2), (gdt, rel)

@@ -26,6 +26,8 @@ class _GeluTanhFn(torch.autograd.Function):
     def backward(ctx, dy):
         (h,) = ctx.saved_tensors
         dyc = dy.contiguous()
+        if dyc.data_ptr() % 16 != 0:
+            dyc = dyc.clone()  # 16-B vector loads
         dh = torch.empty_like(h)
         N.check_gpu_tensor(dyc, "dy", align=16)
         N.hip().gelu_tanh_bwd(h.data_ptr(), dyc.data_ptr(), dh.data_ptr(), h.numel(), N.dtype_code(h.dtype),
@@ -36,6 +38,8 @@ class _GeluTanhFn(torch.autograd.Function):
 def gelu_tanh(h: torch.Tensor) -> torch.Tensor:
     """GELU with the tanh approximation (``F.gelu(h, approximate="tanh")``)."""
     if h.is_cuda and h.dtype in (torch.float32, torch.bfloat16, torch.float16):
+        if h.is_contiguous() and h.data_ptr() % 16 != 0:
+            h = h.clone()  # offset view: the kernel's 16-B vector loads need an aligned base
         return _GeluTanhFn.apply(h)
     return torch.nn.functional.gelu(h, approximate="tanh")
 

@@ -18,6 +18,7 @@ from __future__ import annotations
 import torch
 import torch.nn.functional as F
 
+from ..utils.flat import flat_grad
 from . import _native as N
 from .dense import _ready
 
@@ -41,8 +42,8 @@ def _supported(x, residual) -> bool:
 
 
 def _direct_fp32(p) -> bool:
-    return (p is not None and getattr(p, "_voda_flat_grad", False) and p.grad is not None
-            and p.grad.dtype == torch.float32 and p.grad.is_contiguous())
+    g = flat_grad(p)
+    return g is not None and g.dtype == torch.float32 and g.is_contiguous()
 
 
 class _BNActFn(torch.autograd.Function):
@@ -84,7 +85,7 @@ class _BNActFn(torch.autograd.Function):
         # owns them (same contract as ops/dense.py), else into fresh tensors
         direct = (need_w and need_b and _direct_fp32(weight) and _direct_fp32(bias))
         if direct:
-            dw, db = weight.grad, bias.grad
+            dw, db = flat_grad(weight), flat_grad(bias)
         else:
             dw = torch.empty(C, dtype=torch.float32, device=x.device) if need_w else None
             db = torch.empty(C, dtype=torch.float32, device=x.device) if need_b else None

@@ -7,7 +7,7 @@ A 1x1 convolution over an NHWC tensor is a plain GEMM on its ``[N*H*W, C]`` view
     weight gradient  dW[co, ci] (+)= sum_m dY[m, co] X[m, ci]  split-K MFMA kernel
                                                            (csrc/hip/wgrad.hip), accumulated
                                                            straight into the optimizer's
-                                                           flat bf16 gradient
+                                                           flat gradient (fp32)
 
 MIOpen runs these as implicit-GEMM convolution kernels; the weight-gradient ones are the
 "reduction over 800k pixels" shape the split-K kernel is built for.  Stride-2 1x1
@@ -26,6 +26,7 @@ import os
 import torch
 import torch.nn.functional as F
 
+from ..utils.flat import flat_grad
 from . import wgrad as W
 
 USE_CONV1X1_GEMM = os.environ.get("VODA_CONV1X1_GEMM", "1") != "0"
@@ -58,7 +59,7 @@ class GradSink:
 
 
 def _direct(p: torch.Tensor) -> bool:
-    return (getattr(p, "_voda_flat_grad", False) and p.grad is not None and p.grad.dtype == p.dtype)
+    return flat_grad(p) is not None
 
 
 def _ready(p: torch.Tensor) -> None:
@@ -120,12 +121,15 @@ class _Conv1x1Fn(torch.autograd.Function):
                 dx = dxs
         dw = None
         if ctx.needs_input_grad[1]:
-            g2 = weight.grad.view(cout, cin) if _direct(weight) else None
+            g2 = flat_grad(weight).view(cout, cin) if _direct(weight) else None
             if g2 is not None and W.supported(dy2, x2, g2):
                 W.wgrad_accumulate_(dy2, x2, g2)
                 _ready(weight)
             elif g2 is not None:
-                g2.addmm_(dy2.t(), x2)
+                if g2.dtype == dy2.dtype:
+                    g2.addmm_(dy2.t(), x2)
+                else:  # fp32 flat gradient of a bf16 weight
+                    g2.add_(dy2.t() @ x2)
                 _ready(weight)
             else:
                 dw = (dy2.t() @ x2).view(cout, cin, 1, 1)

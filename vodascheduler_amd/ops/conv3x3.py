@@ -28,6 +28,7 @@ import torch.nn.functional as F
 
 from . import _native as N
 from . import wgrad as W
+from ..utils.flat import flat_grad
 from .conv1x1 import _direct, _ready
 
 USE_CONV_WGRAD = os.environ.get("VODA_CONV_WGRAD", "1") != "0"
@@ -47,7 +48,7 @@ def conv_wgrad_ref(dy: torch.Tensor, x: torch.Tensor, weight_shape, stride: int,
 def conv_wgrad_accumulate_(dy: torch.Tensor, x: torch.Tensor, gw: torch.Tensor, stride: int, padding: int,
                            accumulate: bool = True, splits: int | None = None) -> None:
     """``gw (+)= dW`` in place; dy [N, Cout, Ho, Wo], x [N, Cin, H, W] channels_last bf16, gw
-    [Cout, Cin, KH, KW] channels_last bf16 (memory [Cout][KH][KW][Cin])."""
+    [Cout, Cin, KH, KW] channels_last bf16 or fp32 (memory [Cout][KH][KW][Cin])."""
     if not dy.is_cuda:
         w = conv_wgrad_ref(dy, x, gw.shape, stride, padding)
         gw.copy_((w + gw.float() if accumulate else w).to(gw.dtype))
@@ -64,14 +65,15 @@ def conv_wgrad_accumulate_(dy: torch.Tensor, x: torch.Tensor, gw: torch.Tensor, 
     nws = h.wgrad_conv_workspace_floats(M, cout, cin, kh * kw, s)
     ws = torch.empty(nws, dtype=torch.float32, device=dy.device) if nws else None
     h.wgrad_conv(dy.data_ptr(), x.data_ptr(), gw.data_ptr(), n, H, Wd, cin, ho, wo, cout, kh, kw, int(stride),
-                 int(padding), s, N.ptr(ws), bool(accumulate), W._zero_rows(dy.device).data_ptr(), N.stream_of(dy))
+                 int(padding), s, N.ptr(ws), bool(accumulate), W._zero_rows(dy.device).data_ptr(),
+                 N.dtype_code(gw.dtype), N.stream_of(dy))
 
 
 def supported(dy: torch.Tensor, x: torch.Tensor, gw: torch.Tensor) -> bool:
     cl = torch.channels_last
     if not (dy.is_cuda and x.is_cuda and gw.is_cuda):
         return False
-    if dy.dtype != torch.bfloat16 or x.dtype != torch.bfloat16 or gw.dtype != torch.bfloat16:
+    if dy.dtype != torch.bfloat16 or x.dtype != torch.bfloat16 or gw.dtype not in (torch.bfloat16, torch.float32):
         return False
     if dy.dim() != 4 or x.dim() != 4 or gw.dim() != 4:
         return False
@@ -105,13 +107,17 @@ class _ConvKxKFn(torch.autograd.Function):
                                                      [1, 1], False, [0, 0], 1, [True, False, False])[0]
         dw = None
         if ctx.needs_input_grad[1]:
-            gw = weight.grad if _direct(weight) else None
+            gw = flat_grad(weight) if _direct(weight) else None
             if gw is not None and supported(dy, x, gw):
                 conv_wgrad_accumulate_(dy, x, gw, stride, padding)
                 _ready(weight)
             else:
                 dw = torch.ops.aten.convolution_backward(dy, x, weight, None, [stride, stride], [padding, padding],
                                                          [1, 1], False, [0, 0], 1, [False, True, False])[1]
+                if gw is not None:  # flat gradient the kernel cannot take: fold it here
+                    gw.add_(dw)
+                    _ready(weight)
+                    dw = None
         return dx, dw, None, None
 
 

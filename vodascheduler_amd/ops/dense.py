@@ -22,6 +22,7 @@ import os
 import torch
 import torch.nn.functional as F
 
+from ..utils.flat import flat_grad
 from . import _native as N
 from . import wgrad as W
 
@@ -29,8 +30,8 @@ USE_WGRAD_KERNEL = os.environ.get("VODA_WGRAD", "1") != "0"
 
 
 def _direct(p: torch.Tensor | None) -> bool:
-    return (p is not None and getattr(p, "_voda_flat_grad", False) and p.grad is not None
-            and p.grad.dtype == p.dtype and p.grad.is_contiguous())
+    g = flat_grad(p)
+    return g is not None and g.is_contiguous()
 
 
 def _ready(p: torch.Tensor) -> None:
@@ -90,22 +91,26 @@ class _DenseFn(torch.autograd.Function):
             dx = (dy2 @ weight).view(x.shape)
         need_w, need_b = ctx.needs_input_grad[1], bias is not None and ctx.needs_input_grad[2]
         fused = (USE_WGRAD_KERNEL and need_w and _direct(weight) and (not need_b or _direct(bias))
-                 and W.supported(dy2, x2, weight.grad, bias.grad if need_b else None))
+                 and W.supported(dy2, x2, flat_grad(weight), flat_grad(bias) if need_b else None))
         if fused:
-            W.wgrad_accumulate_(dy2, x2, weight.grad, bias.grad if need_b else None)
+            W.wgrad_accumulate_(dy2, x2, flat_grad(weight), flat_grad(bias) if need_b else None)
             _ready(weight)
             if need_b:
                 _ready(bias)
             return dx, None, None, None
         if need_w:
             if _direct(weight):
-                weight.grad.addmm_(dy2.t(), x2)
+                gw = flat_grad(weight)
+                if gw.dtype == dy2.dtype:
+                    gw.addmm_(dy2.t(), x2)
+                else:  # fp32 flat gradient of a bf16 weight
+                    gw.add_(dy2.t() @ x2)
                 _ready(weight)
             else:
                 dw = dy2.t() @ x2
         if need_b:
             if _direct(bias):
-                colsum_accumulate_(dy2, bias.grad)
+                colsum_accumulate_(dy2, flat_grad(bias))
                 _ready(bias)
             else:
                 db = dy2.float().sum(0).to(bias.dtype)

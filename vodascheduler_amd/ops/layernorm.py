@@ -10,6 +10,7 @@ import os
 
 import torch
 
+from ..utils.flat import flat_grad
 from . import _native as N
 from .dense import _ready
 
@@ -18,9 +19,9 @@ LN_DIRECT_GRADS = os.environ.get("VODA_LN_DIRECT", "1") != "0"
 
 
 def _direct(p) -> bool:
-    """The optimizer's flat gradient owns p.grad (ops/dense.py contract)."""
-    return (p is not None and getattr(p, "_voda_flat_grad", False) and p.grad is not None
-            and p.grad.dtype == p.dtype and p.grad.is_contiguous())
+    """The optimizer's flat gradient owns p's gradient (ops/dense.py contract)."""
+    g = flat_grad(p)
+    return g is not None and g.is_contiguous()
 
 
 def _supported(x: torch.Tensor, weight: torch.Tensor | None) -> bool:
@@ -40,6 +41,8 @@ class _LayerNormFn(torch.autograd.Function):
         GEMM that consumed the residual stream instead of returning it."""
         n = x.shape[-1]
         xc = x.contiguous()
+        if xc.data_ptr() % 16 != 0:
+            xc = xc.clone()
         m = xc.numel() // n
         y = torch.empty_like(xc)
         mean = torch.empty(m, dtype=torch.float32, device=x.device)
@@ -48,8 +51,10 @@ class _LayerNormFn(torch.autograd.Function):
         w = weight.contiguous() if weight is not None else None
         b = bias.to(wdt).contiguous() if bias is not None else None
         rc = residual.contiguous() if residual is not None else None
+        if rc is not None and rc.data_ptr() % 16 != 0:
+            rc = rc.clone()  # the kernel reads the residual with 16-B vector loads
         sm = torch.empty_like(xc) if residual is not None else None
-        for t, nm in ((xc, "x"), (y, "y")):
+        for t, nm in ((xc, "x"), (y, "y")) + (((rc, "residual"),) if rc is not None else ()):
             N.check_gpu_tensor(t, nm, align=8)
         N.hip().layernorm_fwd(xc.data_ptr(), N.ptr(w), N.ptr(b), y.data_ptr(), mean.data_ptr(), rstd.data_ptr(),
                               m, n, float(eps), N.dtype_code(x.dtype), N.dtype_code(wdt), N.ptr(rc), N.ptr(sm),
@@ -68,6 +73,8 @@ class _LayerNormFn(torch.autograd.Function):
         n = xc.shape[-1]
         m = xc.numel() // n
         dyc = dy.contiguous()
+        if dyc.data_ptr() % 16 != 0:
+            dyc = dyc.clone()  # offset view: the kernel reads dy with vector loads
         dx = torch.empty_like(xc)
         need_w = w is not None and ctx.needs_input_grad[1]
         need_b = ctx.has_bias and ctx.needs_input_grad[2]
@@ -75,13 +82,13 @@ class _LayerNormFn(torch.autograd.Function):
         weight, bias = ctx.params
         # gamma / beta gradients summed straight into the optimizer's flat buffer (one column-sum
         # launch for both, no autograd add afterwards) when it owns them
-        direct = (LN_DIRECT_GRADS and need_w and need_b and _direct(weight) and _direct(bias) and weight.grad.dtype == ctx.wdt
-                  and bias.grad.dtype == ctx.wdt)
+        direct = (LN_DIRECT_GRADS and need_w and need_b and _direct(weight) and _direct(bias)
+                  and flat_grad(weight).dtype == ctx.wdt and flat_grad(bias).dtype == ctx.wdt)
         if need_w or need_b:
             rows = N.hip().layernorm_bwd_partial_rows(m)
             ws = torch.empty(2 * rows * n, dtype=torch.float32, device=xc.device)
             if direct:
-                dgamma, dbeta = weight.grad, bias.grad
+                dgamma, dbeta = flat_grad(weight), flat_grad(bias)
             else:
                 dgamma = torch.empty(n, dtype=ctx.wdt, device=xc.device)
                 dbeta = torch.empty(n, dtype=ctx.wdt, device=xc.device)

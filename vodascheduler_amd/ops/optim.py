@@ -280,7 +280,8 @@ class FusedRMSprop(_FusedFlatOptimizer):
 
 
 def make_optimizer(name: str, params, **kw) -> _FusedFlatOptimizer:
-    """Factory used by the workload specs (``--optimizer SGD|Adam|AdamW|RMSprop``)."""
+    """Factory used by the workload specs (``--optimizer SGD|Adam|AdamW|RMSprop``).
+    ``grad_dtype`` (default fp32) is the precision of the flat gradient buffers."""
     key = name.lower()
     table = {"sgd": FusedSGD, "adam": FusedAdam, "adamw": FusedAdamW, "rmsprop": FusedRMSprop}
     if key not in table:

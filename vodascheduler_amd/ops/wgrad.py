@@ -5,7 +5,8 @@ csrc/hip/wgrad.hip, with the fp32 PyTorch reference of the same op.
 
 These are the "reduction over tokens" GEMMs of every Linear backward (BERT-base: M = 8192
 tokens); ``ops/dense.py`` routes them here when the layer accumulates straight into the
-optimizer's flat bf16 gradient buffer.
+optimizer's flat gradient buffer -- fp32 by default (the kernel rounds its fp32 MFMA
+accumulators once into the fp32 gradient), bf16 when low-precision gradients were chosen.
 """
 from __future__ import annotations
 
@@ -53,10 +54,11 @@ def default_splits(M: int, N_: int, K: int, target_blocks: int | None = None, va
 
 
 def supported(dy2: torch.Tensor, x2: torch.Tensor, gw: torch.Tensor, gb: torch.Tensor | None = None) -> bool:
-    """True when the HIP kernel can run these operands (bf16, 16-byte aligned rows)."""
+    """True when the HIP kernel can run these operands (bf16 inputs, bf16 or fp32 dW/db,
+    16-byte aligned rows)."""
     if not (dy2.is_cuda and x2.is_cuda and gw.is_cuda):
         return False
-    if dy2.dtype != torch.bfloat16 or x2.dtype != torch.bfloat16 or gw.dtype != torch.bfloat16:
+    if dy2.dtype != torch.bfloat16 or x2.dtype != torch.bfloat16 or gw.dtype not in (torch.bfloat16, torch.float32):
         return False
     if dy2.dim() != 2 or x2.dim() != 2 or gw.dim() != 2:
         return False
@@ -70,7 +72,7 @@ def supported(dy2: torch.Tensor, x2: torch.Tensor, gw: torch.Tensor, gb: torch.T
         return False
     if dy2.data_ptr() % 16 or x2.data_ptr() % 16 or gw.data_ptr() % 16:
         return False
-    if gb is not None and (gb.dtype != torch.bfloat16 or not gb.is_contiguous() or gb.numel() != N_):
+    if gb is not None and (gb.dtype != gw.dtype or not gb.is_contiguous() or gb.numel() != N_):
         return False
     return True
 
@@ -108,4 +110,4 @@ def wgrad_accumulate_(dy2: torch.Tensor, x2: torch.Tensor, gw: torch.Tensor, gb:
     ws = torch.empty(nws, dtype=torch.float32, device=dy2.device) if nws else None
     h.wgrad_gemm(dy2.data_ptr(), dy2.stride(0), x2.data_ptr(), x2.stride(0), gw.data_ptr(), gw.stride(0),
                  N.ptr(gb), M, N_, K, s, N.ptr(ws), bool(accumulate), _zero_rows(dy2.device).data_ptr(), v,
-                 N.stream_of(dy2))
+                 N.dtype_code(gw.dtype), N.stream_of(dy2))

@@ -20,10 +20,18 @@ MI355X-first design:
   all-gathers the bucket and runs the deterministic per-parameter Adasum tree of
   ``ops/adasum.py`` on every rank (HIP segmented combine kernels);
 * ``finalize()`` flushes buckets whose parameters got no gradient this step (zeros) and makes
-  the compute stream wait for the comm stream before the optimizer step.
+  the compute stream wait for the comm stream before the optimizer step;
+* readiness is counted per parameter against the number of gradient contributions the
+  parameter received in a calibration step (the first synced step: no overlap, every bucket
+  launched by ``finalize``).  A parameter a fused layer signals itself AND autograd
+  accumulates (or one used by two fused layers) therefore never launches its bucket early --
+  a bucket launched before its last contribution would all-reduce a partial gradient and
+  let the ranks diverge silently.  (Static-graph assumption, as PyTorch DDP's
+  ``static_graph``; a step that deviates is detected at ``finalize`` and logged.)
 """
 from __future__ import annotations
 
+import logging
 from contextlib import contextmanager
 from dataclasses import dataclass
 
@@ -35,6 +43,7 @@ from ..utils.flat import FlatGroup
 from .comm import Communicator, LocalCommunicator
 
 _COMPRESS = {None: None, "none": None, "bf16": torch.bfloat16, "fp16": torch.float16}
+log = logging.getLogger("vodascheduler_amd.ddp")
 
 
 @dataclass
@@ -75,6 +84,8 @@ class ElasticDDP:
         self._build_buckets()
         self._hooks = []
         self._sync = True
+        self._expect: dict[int, int] | None = None   # contributions per parameter per step
+        self._count: dict[int, int] = {}
         self._param_bucket: dict[int, Bucket] = {}
         for b in self.buckets:
             for p in b.params:
@@ -131,13 +142,26 @@ class ElasticDDP:
 
     def _reset(self) -> None:
         self._next = 0
+        self._count = {}
         for b in self.buckets:
-            b.pending = sum(1 for p in b.params if p.requires_grad)
+            if self._expect is None:
+                b.pending = sum(1 for p in b.params if p.requires_grad)
+            else:
+                b.pending = sum(self._expect.get(id(p), 0) for p in b.params)
             b.launched = False
+
+    @property
+    def calibrated(self) -> bool:
+        return self._expect is not None
 
     # ------------------------------------------------------------------ hooks
     def _on_grad(self, p: torch.nn.Parameter) -> None:
-        if not self._sync or self.world == 1:
+        if not self._sync:
+            return
+        if self._expect is None:  # calibration step: count contributions, launch at finalize
+            self._count[id(p)] = self._count.get(id(p), 0) + 1
+            return
+        if self.world == 1:
             return
         b = self._param_bucket[id(p)]
         b.pending -= 1
@@ -191,7 +215,14 @@ class ElasticDDP:
 
     def finalize(self) -> None:
         """Flush remaining buckets in order and order the compute stream after them."""
-        if self.world > 1 and self._sync:
+        if self._sync and self._expect is None and self._count:
+            self._expect = dict(self._count)  # calibration step done: every bucket launches below
+        elif self._sync and self.world > 1:
+            bad = [i for i, b in enumerate(self.buckets) if b.pending < 0]
+            if bad:
+                log.error("buckets %s received more gradient contributions than in the calibration step "
+                          "(dynamic graph?): their all-reduce may have started early", bad)
+        if self._sync and self.world > 1:
             while self._next < len(self.buckets):
                 self._launch(self.buckets[self._next])
                 self._next += 1
@@ -203,10 +234,13 @@ class ElasticDDP:
         """Synchronous all-reduce of all gradients (no overlap); for debugging/tests."""
         if self.world == 1:
             return
-        for b in self.buckets:
-            b.pending = 0
-        self._launch_ready()
+        self._launch_ready_all()
         self.finalize()
+
+    def _launch_ready_all(self) -> None:
+        while self._next < len(self.buckets):
+            self._launch(self.buckets[self._next])
+            self._next += 1
 
     def step(self) -> None:
         self.finalize()

@@ -90,16 +90,42 @@ def run_trace(store, trace: list[TraceJob], worker_locs, algorithm: str = "Elast
             tracer.save(trace_path)
     failed = [n for n, j in jobs.items() if j.status != JobStatus.COMPLETED.value]
     jct = {n: j.finish_timestamp - j.submit_timestamp for n, j in jobs.items()}
-    lat = sorted(r["latency_s"] for r in backend.resize_latency)
+    lat = classify_latencies(backend.events, backend.resize_latency)
     vals = sorted(jct.values())
     q = lambda xs, p: xs[min(len(xs) - 1, int(p * len(xs)))] if xs else None  # noqa: E731
     return {
         "n_jobs": len(names), "failed": failed, "avg_jct_s": statistics.fmean(vals), "p50_jct_s": q(vals, 0.5),
         "p95_jct_s": q(vals, 0.95), "makespan_s": max(j.finish_timestamp for j in jobs.values()) - t0,
-        "wall_s": t1 - t0, "resize_events": len(backend.events), "resize_latency_p50_s": q(lat, 0.5),
-        "resize_latency_p95_s": q(lat, 0.95), "reschedules": core.resched_count, "jct": jct,
+        "wall_s": t1 - t0, "resize_events": len(backend.events),
+        "n_starts": len(lat["start"]), "n_resizes": len(lat["resize"]), "n_shrinks_to_1": len(lat["to_one"]),
+        "start_latency_p50_s": q(lat["start"], 0.5), "start_latency_p95_s": q(lat["start"], 0.95),
+        "resize_latency_p50_s": q(lat["resize"], 0.5), "resize_latency_p95_s": q(lat["resize"], 0.95),
+        "reschedules": core.resched_count, "jct": jct,
         "events": backend.events, "resize_latency": backend.resize_latency,
     }
+
+
+def classify_latencies(events: list[dict], synced: list[dict]) -> dict[str, list[float]]:
+    """Split membership-change latencies (request -> new epoch synced and training) into
+    * ``start``: the job had no workers (first start, or restart after a halt);
+    * ``resize``: a running job moves to a world of >= 2 (scale-in/out or migration): an RCCL
+      communicator rebuild (or cache hit) + state broadcast;
+    * ``to_one``: a running job shrinks to one worker (no communicator)."""
+    by_key = {(e["job"], e["epoch"]): e for e in events}
+    out: dict[str, list[float]] = {"start": [], "resize": [], "to_one": []}
+    for r in synced:
+        e = by_key.get((r["job"], r["epoch"]))
+        if e is None:
+            continue
+        if e["prev_world"] == 0:
+            out["start"].append(r["latency_s"])
+        elif e["world"] >= 2:
+            out["resize"].append(r["latency_s"])
+        elif e["world"] == 1:
+            out["to_one"].append(r["latency_s"])
+    for v in out.values():
+        v.sort()
+    return out
 
 
 def cpu_worker_main(host: str, port: int, wid: str, threads: int = 1) -> None:

@@ -156,12 +156,14 @@ class ElasticContext:
         # a newer epoch published before this one's bootstrap finished, or the job ending
         # (finished by the old members before they saw this epoch), means some member will
         # never arrive here: abandon instead of blocking until the timeout
+        hits0 = COMM_CACHE.hits
         self.comm = create_communicator(self.rdzv.store, self.rdzv.comm_prefix(epoch), self.rank, self.size,
                                         self.device, self.backend, self.timeout,
                                         cancel=lambda: (self.rdzv.latest_epoch() > epoch
                                                         or self.rdzv.outcome() is not None),
                                         members=self.members if self.cache_comms else None)
-        self.resize_log.append({"epoch": epoch, "world": self.size, "comm_init_s": time.perf_counter() - t0})
+        self.resize_log.append({"epoch": epoch, "world": self.size, "comm_init_s": time.perf_counter() - t0,
+                                "cached": COMM_CACHE.hits > hits0})
 
     def destroy_comm(self, abort: bool = False) -> None:
         """Release the epoch's communicator: back into the per-process cache when it is
@@ -201,10 +203,14 @@ class ElasticContext:
             self.comm.check()
             prev = int(self._agree_host[0])
         t = torch.tensor([seen], dtype=torch.int64, device=self.comm.device)
-        self.comm.allreduce_(t, "max")
         cs = getattr(self.comm, "stream", None)
+        cur = torch.cuda.current_stream(self.comm.device)
         if cs is not None:
-            torch.cuda.current_stream(self.comm.device).wait_stream(cs)
+            cs.wait_stream(cur)  # the H2D copy of ``t`` was enqueued on the current stream
+        self.comm.allreduce_(t, "max")
+        if cs is not None:
+            t.record_stream(cs)
+            cur.wait_stream(cs)
         if getattr(self, "_agree_host", None) is None:
             self._agree_host = torch.zeros(1, dtype=torch.int64, pin_memory=True)
         self._agree_host.copy_(t, non_blocking=True)

@@ -94,7 +94,11 @@ class PoolBackend(Backend):
         else:
             if a.workers is None:
                 raise ValueError("PoolBackend needs placement (worker locations) for every action")
-            new_members = [worker_id(l) for l in a.workers]
+            # members in GPU order: the ordered member list keys the per-process communicator
+            # cache (parallel/comm.py), so a job that returns to a GPU set it used before --
+            # whatever order placement listed it in -- reuses that RCCL communicator.  The
+            # state root is chosen by holder (State.sync), so rank order carries no state.
+            new_members = [worker_id(l) for l in sorted(a.workers, key=lambda l: (l[0], int(l[1])))]
         old = self.members.get(name, [])
         if new_members == old:
             return

@@ -215,7 +215,9 @@ class SchedulerCore:
         now = self.clock.now()
         for a in actions:
             job = a.job
-            self._accumulate(job, now)  # close the waiting/running interval at the switch
+            # close the waiting/running interval at the switch, charged at the allocation the
+            # job held DURING it (job_num_gpu already holds the new one)
+            self._accumulate(job, now, old.get(job.name, 0))
             if a.kind == HALT:
                 job.status = JobStatus.WAITING.value
                 job.time_metrics.last_waiting_time = 0.0
@@ -337,10 +339,12 @@ class SchedulerCore:
         self._emit("nodes", total_gpus=self.total_gpus)
 
     # ------------------------------------------------------------------ time metrics
-    def _accumulate(self, job: TrainingJob, now: float) -> None:
+    def _accumulate(self, job: TrainingJob, now: float, num_gpu: int | None = None) -> None:
+        """Close the interval since the last update; ``num_gpu`` = GPUs held during it
+        (default: the current allocation)."""
         m = job.time_metrics
         dt = max(0.0, now - m.last_update_timestamp)
-        n = self.job_num_gpu.get(job.name, 0)
+        n = self.job_num_gpu.get(job.name, 0) if num_gpu is None else num_gpu
         if job.status == JobStatus.RUNNING:
             m.running_time += dt
             m.gpu_time += dt * n

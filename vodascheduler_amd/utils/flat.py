@@ -7,6 +7,18 @@ the bucketed all-reduce engine (buckets are slices of the flat gradient buffer, 
 step) are built around.  Each tensor starts on a 64-element boundary so every slice is
 >= 128-byte aligned for the 8/16-B vector loads of the kernels.  On a 288 GB MI355X the
 padding and the resident snapshots (``snapshot()``) are free.
+
+Gradient precision: the flat gradient buffer is fp32 by default, also for a model whose
+GEMM/conv weights are stored in bf16 (Horovod reduces fp32 gradients unless
+``--fp16-allreduce`` is given; reference pytorch_mnist_elastic.py:116).  Such a parameter
+cannot carry an fp32 ``.grad`` (autograd requires grad dtype == param dtype), so its flat
+gradient view is published as ``p._voda_gview`` instead:
+* the fused layers (ops/dense.py, conv1x1.py, conv3x3.py, layernorm.py, batchnorm.py)
+  accumulate their weight gradients straight into it (the MFMA weight-gradient kernels
+  round their fp32 accumulators once, into fp32);
+* for every other op autograd produces the usual bf16 ``.grad``; a post-accumulate hook
+  adds it into the fp32 slot and drops it (one small cast-add per such parameter).
+``grad_of(p)`` returns the flat gradient view in either mode.
 """
 from __future__ import annotations
 
@@ -35,6 +47,19 @@ class Slot:
     numel: int
 
 
+def grad_of(p: torch.Tensor) -> torch.Tensor | None:
+    """The optimizer-owned flat gradient view of ``p`` (any dtype), else ``p.grad``."""
+    g = getattr(p, "_voda_gview", None)
+    return g if g is not None else p.grad
+
+
+def flat_grad(p: torch.Tensor | None) -> torch.Tensor | None:
+    """The flat gradient view a fused layer may accumulate into in place, or None."""
+    if p is None:
+        return None
+    return getattr(p, "_voda_gview", None)
+
+
 class FlatGroup:
     """Contiguous storage for a list of parameters.
 
@@ -43,7 +68,7 @@ class FlatGroup:
         flatten_params: re-point ``p.data`` into the flat buffers (needed by the fused
             optimizers); False keeps the parameters where they are and only flattens
             gradients (the all-reduce engine's grad-only mode).
-        grad_dtype: dtype of the flat gradient buffer (default: parameter dtype).
+        grad_dtype: dtype of the flat gradient buffer (default: fp32).
     """
 
     def __init__(self, params, flatten_params: bool = True, grad_dtype: torch.dtype | None = None):
@@ -58,7 +83,10 @@ class FlatGroup:
         if len(pdts) != 1:
             raise ValueError(f"mixed parameter dtypes in one group: {pdts}")
         self.param_dtype = pdts.pop()
-        self.grad_dtype = grad_dtype or self.param_dtype
+        self.grad_dtype = grad_dtype or torch.float32
+        # mixed: bf16/fp16 parameters with an fp32 flat gradient (see module docstring)
+        self.mixed = self.grad_dtype != self.param_dtype
+        self._hooks: list = []
         self.slots: list[Slot] = []
         off = 0
         for p in self.params:
@@ -90,19 +118,37 @@ class FlatGroup:
         return torch.as_strided(flat, p.shape, p.stride(), s.offset)
 
     def attach_grads(self) -> None:
-        """(Re-)point every ``p.grad`` into the flat gradient buffer.  ``_voda_flat_grad``
-        tells fused layers (ops/dense.py) they may accumulate into ``p.grad`` in place."""
+        """(Re-)point every parameter's gradient into the flat buffer.  ``_voda_gview`` tells
+        the fused layers (ops/dense.py) they may accumulate into it in place; when the dtypes
+        match it is also ``p.grad`` (autograd accumulates into it in place)."""
         for p, s in zip(self.params, self.slots):
-            p.grad = self.view(self.grad, p, s)
+            v = self.view(self.grad, p, s)
+            p._voda_gview = v
             p._voda_flat_grad = True
+            if self.mixed:
+                p.grad = None
+            else:
+                p.grad = v
+        if self.mixed and not self._hooks and any(p.requires_grad for p in self.params):
+            for p in self.params:
+                if p.requires_grad:
+                    self._hooks.append(p.register_post_accumulate_grad_hook(_fold_lowp_grad))
 
     def zero_grad(self) -> None:
         self.grad.zero_()
         # autograd may have replaced a grad (e.g. user set p.grad = None); re-attach
         for p, s in zip(self.params, self.slots):
             g = p.grad
-            if g is None or g.data_ptr() != self.grad.data_ptr() + s.offset * self.grad.element_size():
+            if self.mixed:
+                if g is not None:
+                    p.grad = None
+            elif g is None or g.data_ptr() != self.grad.data_ptr() + s.offset * self.grad.element_size():
                 p.grad = self.view(self.grad, p, s)
+
+    def remove_hooks(self) -> None:
+        for h in self._hooks:
+            h.remove()
+        self._hooks = []
 
     def param_storage(self) -> torch.Tensor:
         """The buffer holding the authoritative parameter values (fp32 master)."""
@@ -113,3 +159,14 @@ class FlatGroup:
     def sync_lowp_from_master(self) -> None:
         if self.lowp is not None and self.master is not None:
             self.lowp.copy_(self.master)
+
+
+def _fold_lowp_grad(p: torch.Tensor) -> None:
+    """Post-accumulate hook of a low-precision parameter with an fp32 flat gradient: add the
+    autograd-produced ``.grad`` into the fp32 slot and drop it.  Registered before the
+    data-parallel engine's readiness hook, so a bucket is launched only after the fold."""
+    g = p.grad
+    if g is None:
+        return
+    p._voda_gview.add_(g)
+    p.grad = None

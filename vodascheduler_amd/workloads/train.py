@@ -16,6 +16,7 @@ Standalone (one process per GPU, launched by the local node agent):
 from __future__ import annotations
 
 import argparse
+import hashlib
 import logging
 import math
 import os
@@ -45,6 +46,9 @@ class TrainConfig:
     commit_every: int = 1
     amp: bool = True                   # bf16 autocast
     compression: str | None = None     # gradient all-reduce compression: None | bf16 | fp16
+    # flat gradient buffer precision: fp32 (default; bf16 compute weights keep fp32 gradients,
+    # as Horovod reduces fp32 unless --fp16-allreduce) | bf16 (opt-in low-precision gradients)
+    grad_dtype: str = "fp32"
     bucket_cap_mb: float = 64.0
     reduction: str = "average"         # average | adasum (Horovod op=hvd.Adasum; LR not scaled by world)
     metrics_dir: str | None = None
@@ -52,6 +56,8 @@ class TrainConfig:
     seed: int = 0
     data_pool: int = 2                 # distinct synthetic batches cycled through
     graph: bool = True                 # capture the whole step in a hipGraph when world == 1 (graph-safe models)
+    final_state_path: str | None = None  # rank 0 saves the final state (checkpoint format) here
+    report_progress: bool = False      # rank 0 publishes the committed step under job/<name>/progress
 
 
 def build(cfg: TrainConfig, device: torch.device):
@@ -61,8 +67,11 @@ def build(cfg: TrainConfig, device: torch.device):
     kw = dict(w.opt_kwargs)
     if cfg.lr is not None:
         kw["lr"] = cfg.lr
-    opt = make_optimizer(w.optimizer, model.parameters(), **kw)
+    opt = make_optimizer(w.optimizer, model.parameters(), grad_dtype=GRAD_DTYPES[cfg.grad_dtype], **kw)
     return w, model, opt, kw["lr"]
+
+
+GRAD_DTYPES = {"fp32": torch.float32, "bf16": torch.bfloat16, "fp16": torch.float16}
 
 
 class _Warm:
@@ -104,7 +113,7 @@ WARM_CACHE_MAX = 4
 
 def _warm_key(cfg: TrainConfig, device: torch.device) -> tuple:
     return (cfg.model, cfg.per_gpu_batch, cfg.lr, cfg.compression, cfg.bucket_cap_mb, cfg.reduction, cfg.seed,
-            str(device))
+            cfg.grad_dtype, str(device))
 
 
 def get_warm(cfg: TrainConfig, device: torch.device, use_cache: bool = True) -> _Warm:
@@ -127,7 +136,10 @@ def train_elastic(ctx: ElasticContext, cfg: TrainConfig, use_cache: bool = True)
     device = ctx.device
     wm = get_warm(cfg, device, use_cache)
     w, model, opt, base_lr, bs, pool, ddp = wm.w, wm.model, wm.opt, wm.base_lr, wm.bs, wm.pool, wm.ddp
-    state = TorchState(ctx, model, opt, epoch=0, samples=0)
+    # world_log: flat [start_step, world, ...] segments -- the world size every step ran at.
+    # Part of the synced / committed state, so a restore rolls it back with the step counter
+    # and a joining member inherits it: ``replay_reference`` re-runs the same trajectory.
+    state = TorchState(ctx, model, opt, epoch=0, samples=0, world_log=[])
     logger = MetricsCSVLogger(cfg.metrics_dir, ctx.job, cfg.epochs, bs)
     samples_per_epoch = cfg.steps_per_epoch * bs
     stats = {"steps": 0, "samples": 0, "train_time": 0.0, "model": cfg.model, "resizes": 0}
@@ -154,6 +166,7 @@ def train_elastic(ctx: ElasticContext, cfg: TrainConfig, use_cache: bool = True)
         lr_scaler = 1 if cfg.reduction == "adasum" else world  # Horovod examples: Adasum keeps the base LR
         for gr in opt.param_groups:
             gr["lr"] = base_lr * lr_scaler
+        state.world_log = list(state.world_log) + [state.step, world]
         logger.set_params(world)
         # world 1: the whole step replays as one hipGraph (launch-bound models); collectives
         # of world > 1 stay eager.  Re-captured after every membership change.
@@ -174,6 +187,8 @@ def train_elastic(ctx: ElasticContext, cfg: TrainConfig, use_cache: bool = True)
                 stats["samples"] += bs * world
                 if state.step % cfg.commit_every == 0:
                     state.commit()
+                    if cfg.report_progress and ctx.rank == 0:
+                        ctx.rdzv.set("progress", str(state.step))
             if device.type == "cuda":
                 torch.cuda.synchronize(device)
             ep_time = time.time() - t_ep
@@ -188,7 +203,17 @@ def train_elastic(ctx: ElasticContext, cfg: TrainConfig, use_cache: bool = True)
                 state.save_checkpoint()
         if device.type == "cuda":
             torch.cuda.synchronize(device)
-        return dict(stats, final_loss=float(loss_t) if loss_t is not None else None, world=ctx.size)
+        digest = None
+        if cfg.final_state_path:
+            if ctx.rank == 0:
+                state.save_checkpoint(cfg.final_state_path)
+            # every member's final state, hashed: the members must hold bitwise-identical state
+            h = hashlib.sha1()
+            for t in state.tensors():
+                h.update(t.detach().contiguous().cpu().view(-1).view(torch.uint8).numpy().tobytes())
+            digest = h.hexdigest()
+        return dict(stats, final_loss=float(loss_t) if loss_t is not None else None, world=ctx.size,
+                    final_step=state.step, world_log=list(state.world_log), state_digest=digest)
 
     try:
         return train(state)
@@ -196,6 +221,56 @@ def train_elastic(ctx: ElasticContext, cfg: TrainConfig, use_cache: bool = True)
         ddp.comm = None  # never keep a dead epoch's communicator alive in the warm cache
         if not use_cache:
             ddp.remove_hooks()
+
+
+def replay_reference(cfg: TrainConfig, world_log: list[int], total_steps: int, device: torch.device):
+    """Uninterrupted single-process replay of an elastic run: step ``s`` runs at the world
+    size of the last ``world_log`` segment starting at or before ``s`` (LR = base x world,
+    the same synthetic batch every rank of the elastic run used).  The elastic run's final
+    state must equal this one -- exactly for worlds whose all-reduce average of identical
+    per-rank gradients is exact (1, 2) -- whatever resizes, halts and restores happened.
+    Returns (state tensors, extras)."""
+    w, model, opt, base_lr = build(cfg, device)
+    bs = cfg.per_gpu_batch or w.per_gpu_batch
+    g = torch.Generator(device=device).manual_seed(cfg.seed + 1)
+    pool = []
+    for _ in range(max(1, cfg.data_pool)):
+        b = w.make_batch(bs, device, g)
+        if w.channels_last and device.type == "cuda":
+            b = tuple(t.to(memory_format=torch.channels_last) if t.dim() == 4 else t for t in b)
+        pool.append(b)
+    ddp = ElasticDDP(model, None, opt, bucket_cap_mb=cfg.bucket_cap_mb, compression=cfg.compression,
+                     reduction=cfg.reduction)
+    segs = [(world_log[i], world_log[i + 1]) for i in range(0, len(world_log), 2)]
+
+    def world_at(step: int) -> int:
+        wd = segs[0][1]
+        for st, wv in segs:
+            if st <= step:
+                wd = wv
+        return wd
+
+    samples_per_epoch = cfg.steps_per_epoch * bs
+    epoch = samples = 0
+    for step in range(total_steps):
+        world = world_at(step)
+        lr_scaler = 1 if cfg.reduction == "adasum" else world
+        for gr in opt.param_groups:
+            gr["lr"] = base_lr * lr_scaler
+        ddp.zero_grad()
+        with torch.autocast(device.type, dtype=torch.bfloat16, enabled=cfg.amp and device.type == "cuda",
+                            cache_enabled=False):
+            loss = w.loss(model, pool[step % len(pool)])
+        loss.backward()
+        ddp.step()
+        samples += bs * world
+        if samples >= samples_per_epoch:
+            epoch, samples = epoch + 1, 0
+    for m in model.modules():  # host-side BN counters -> buffers (as TorchState.tensors)
+        if hasattr(m, "sync_batches_tracked"):
+            m.sync_batches_tracked()
+    ts = opt.flat_state_tensors() + [b for b in model.buffers() if b.dtype.is_floating_point or b.dtype == torch.int64]
+    return [t.detach().cpu() for t in ts], {"epoch": epoch, "samples": samples, "__step__": total_steps}
 
 
 def main(argv=None):
