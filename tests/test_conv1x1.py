@@ -45,10 +45,13 @@ def test_conv1x1_gemm_matches_conv2d(cin, cout, stride, hw):
     y.backward(g.bfloat16().to(memory_format=torch.channels_last))
     y_ref.backward(g)
     assert _rel(xg.grad, xr.grad) < 1e-2
-    assert _rel(m.weight.grad, ref_w.grad) < 1e-2
+    from vodascheduler_amd.utils.flat import grad_of
+
+    assert grad_of(m.weight).dtype == torch.float32  # fp32 flat gradient of the bf16 weight
+    assert _rel(grad_of(m.weight), ref_w.grad) < 1e-2
     # a second backward accumulates (beta = 1), as autograd does
     m(xg).backward(g.bfloat16().to(memory_format=torch.channels_last))
-    assert _rel(m.weight.grad, 2 * ref_w.grad) < 1e-2
+    assert _rel(grad_of(m.weight), 2 * ref_w.grad) < 1e-2
 
 
 @pytest.mark.gpu

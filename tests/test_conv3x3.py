@@ -75,7 +75,7 @@ def test_convkxk_layer_flat_grads_match_autograd():
     cl = torch.channels_last
     m = C.ConvKxK(128, 128, 3, stride=2, padding=1).cuda().to(memory_format=cl).bfloat16()
     ref_w = m.weight.detach().float().clone().requires_grad_(True)
-    opt = make_optimizer("sgd", m.parameters(), lr=0.0)  # flat bf16 grads: kernel path
+    opt = make_optimizer("sgd", m.parameters(), lr=0.0)  # flat fp32 grads: kernel path
     x = torch.randn(8, 128, 28, 28, device="cuda").bfloat16().to(memory_format=cl)
     xg = x.detach().requires_grad_(True)
     xr = x.float().detach().requires_grad_(True)
@@ -86,7 +86,9 @@ def test_convkxk_layer_flat_grads_match_autograd():
     g = torch.randn_like(yr)
     y.backward(g.bfloat16().to(memory_format=cl))
     yr.backward(g)
-    for got, want in ((m.weight.grad, ref_w.grad), (xg.grad, xr.grad)):
+    from vodascheduler_amd.utils.flat import grad_of
+
+    for got, want in ((grad_of(m.weight), ref_w.grad), (xg.grad, xr.grad)):
         rel = float((got.float() - want).norm() / want.norm())
         assert rel < 1e-2, rel
 

@@ -45,7 +45,8 @@ def test_two_mnist_jobs_elastic_fifo_two_slots(tmp_path):
     assert ("mnist-a", "start", 2) in kinds
     assert any(k[0] == "mnist-a" and k[1] == "scale_in" and k[2] == 1 for k in kinds), kinds
     assert any(k[0] == "mnist-b" and k[1] == "start" for k in kinds), kinds
-    assert r["resize_latency_p50_s"] is not None and r["resize_latency_p50_s"] < 30
+    assert r["start_latency_p50_s"] is not None and r["start_latency_p50_s"] < 30
+    assert r["n_starts"] >= 2 and r["n_shrinks_to_1"] >= 1  # a: 2 -> 1 (no communicator at world 1)
     csvs = sorted(os.listdir(tmp_path / "metrics"))
     assert len(csvs) == 2
     rows = open(tmp_path / "metrics" / csvs[0]).read().splitlines()

@@ -34,6 +34,18 @@ class Workload:
     # models whose MIOpen conv solvers or GEMM paths are not capture-safe: ResNet-50/224
     # replayed with wrong weight gradients and the NMT Transformer faulted (docs/kernels.md)
     graph_safe: bool = False
+    # (loss, #correct predictions, #predictions) of one batch, all device tensors: the
+    # training step logs accuracy from the same forward (Keras ``metrics=["accuracy"]``,
+    # reference tensorflow2_keras_cifar_elastic.py:168) and the eval pass (reference
+    # pytorch_mnist_elastic.py:155-176 ``test()``) sums them across ranks
+    metrics: Callable[[torch.nn.Module, tuple], tuple] | None = None
+
+    def loss_metrics(self, model: torch.nn.Module, batch: tuple) -> tuple:
+        if self.metrics is not None:
+            return self.metrics(model, batch)
+        loss = self.loss(model, batch)
+        z = torch.zeros((), device=loss.device)
+        return loss, z, z
 
 
 def _img_batch(c, h, w, classes):
@@ -52,6 +64,35 @@ def _ce(model, batch):
 def _nll(model, batch):
     x, y = batch
     return F.nll_loss(model(x).float(), y)
+
+
+def _cls_metrics(log_probs: bool = False):
+    def f(model, batch):
+        x, y = batch
+        out = model(x).float()
+        loss = F.nll_loss(out, y) if log_probs else F.cross_entropy(out, y)
+        correct = (out.argmax(1) == y).sum()
+        return loss, correct, torch.full((), y.numel(), device=y.device)
+    return f
+
+
+def _nmt_metrics(model, batch):
+    src, tin, tout = batch
+    logits = model(src, tin).float()
+    logits = logits.reshape(-1, logits.shape[-1])
+    t = tout.reshape(-1)
+    loss = F.cross_entropy(logits, t, ignore_index=0)
+    valid = t != 0  # masked accuracy over real tokens (the reference's masked_accuracy)
+    correct = ((logits.argmax(1) == t) & valid).sum()
+    return loss, correct, valid.sum()
+
+
+def _bert_metrics(model, batch):
+    ids, mask, pos, labels = batch
+    logits = model(ids, mask, pos).float()
+    y = labels.reshape(-1)
+    loss = F.cross_entropy(logits, y)
+    return loss, (logits.argmax(1) == y).sum(), torch.full((), y.numel(), device=y.device)
 
 
 def _nmt_batch(b, dev, g=None, vocab=15000, T=20):
@@ -85,25 +126,28 @@ def _bert_loss(model, batch):
     return F.cross_entropy(logits.float(), labels.reshape(-1))
 
 
+_CE, _NLL = _cls_metrics(), _cls_metrics(log_probs=True)
+
 WORKLOADS: dict[str, Workload] = {
     "resnet50": Workload("resnet50", lambda: resnet50(1000), _img_batch(3, 224, 224, 1000), _ce, 256, "sgd",
-                         dict(lr=0.1, momentum=0.9, weight_decay=5e-5), channels_last=True),
+                         dict(lr=0.1, momentum=0.9, weight_decay=5e-5), channels_last=True, metrics=_CE),
     "resnet50-cifar": Workload("resnet50-cifar", lambda: resnet50(10, small_input=True), _img_batch(3, 32, 32, 10),
-                               _ce, 128, "sgd", dict(lr=0.01, momentum=0.9), channels_last=True),
+                               _ce, 128, "sgd", dict(lr=0.01, momentum=0.9), channels_last=True, metrics=_CE),
     "resnet18": Workload("resnet18", lambda: resnet18(1000), _img_batch(3, 224, 224, 1000), _ce, 256, "sgd",
-                         dict(lr=0.1, momentum=0.9), channels_last=True),
+                         dict(lr=0.1, momentum=0.9), channels_last=True, metrics=_CE),
     "vgg16": Workload("vgg16", vgg16_cifar, _img_batch(3, 32, 32, 10), _ce, 128, "sgd",
-                      dict(lr=0.01, momentum=0.9), channels_last=True),
+                      dict(lr=0.01, momentum=0.9), channels_last=True, metrics=_CE),
     "inceptionv3": Workload("inceptionv3", InceptionV3, _img_batch(3, 75, 75, 10), _ce, 128, "rmsprop",
-                            dict(lr=1e-3), channels_last=True),
+                            dict(lr=1e-3), channels_last=True, metrics=_CE),
     "mnist": Workload("mnist", KerasMnistCNN, _img_batch(1, 28, 28, 10), _ce, 128, "adam", dict(lr=1e-3),
-                      graph_safe=True),
+                      graph_safe=True, metrics=_CE),
     "mnist-torch": Workload("mnist-torch", TorchMnistNet, _img_batch(1, 28, 28, 10), _nll, 64, "sgd",
-                            dict(lr=0.01, momentum=0.5), graph_safe=True),
+                            dict(lr=0.01, momentum=0.5), graph_safe=True, metrics=_NLL),
     "transformer": Workload("transformer", TransformerNMT, _nmt_batch, _nmt_loss, 512, "rmsprop", dict(lr=1e-3),
-                            samples_unit="tok", tokens_per_sample=20),
+                            samples_unit="tok", tokens_per_sample=20, metrics=_nmt_metrics),
     "bert-base": Workload("bert-base", BertBase, _bert_batch, _bert_loss, 64, "adamw",
-                          dict(lr=1e-4, weight_decay=0.01), samples_unit="tok", tokens_per_sample=128),
+                          dict(lr=1e-4, weight_decay=0.01), samples_unit="tok", tokens_per_sample=128,
+                          metrics=_bert_metrics),
 }
 
 

@@ -7,8 +7,12 @@
   tensorflow2_keras_mnist_elastic.py:101-110; 1,199,882 params).
 * ``TorchMnistNet``: the PyTorch elastic example's 2-conv Net (reference
   examples/py/pytorch/pytorch_mnist_elastic.py:80-96; 21,840 params).
-* ``inception_v3``: InceptionV3 at 75x75 for CIFAR (reference
-  tf2-keras-cifar10-inceptionv3-elastic.yaml).
+* ``InceptionV3``: ``applications.InceptionV3(weights=None, include_top=True, classes=10)`` at
+  75x75 for CIFAR (reference tensorflow2_keras_cifar_elastic.py:107-108,148,
+  tf2-keras-cifar10-inceptionv3-elastic.yaml): the full Keras topology -- stem, mixed0-2 (A),
+  mixed3 (B), mixed4-7 (C), mixed8 (D), mixed9-10 (E), global average pool, 2048 -> 10 head --
+  with Keras' conv2d_bn (bias-free conv + BatchNormalization(scale=False, eps=1e-3) + ReLU).
+  21,823,274 parameters counted the Keras way (weights + BN beta + moving mean/var).
 """
 from __future__ import annotations
 
@@ -74,18 +78,29 @@ class TorchMnistNet(nn.Module):
         return F.log_softmax(self.fc2(x), dim=1)
 
 
-# ----------------------------------------------------------------- InceptionV3 (compact)
+# ----------------------------------------------------------------- InceptionV3 (Keras)
 class BasicConv(nn.Module):
+    """Keras ``conv2d_bn``: Conv2D(use_bias=False) -> BatchNormalization(scale=False) -> ReLU,
+    the BN + ReLU as one fused HIP pass."""
+
     def __init__(self, cin, cout, **kw):
         super().__init__()
         self.conv = nn.Conv2d(cin, cout, bias=False, **kw)
-        self.bn = FusedBatchNorm2d(cout, eps=0.001, relu=True)
+        self.bn = FusedBatchNorm2d(cout, eps=0.001, momentum=0.01, relu=True, scale=False)
 
     def forward(self, x):
-        return self.bn(self.conv(x))  # fused BN + ReLU (HIP)
+        return self.bn(self.conv(x))
+
+
+def _avg3(x):
+    # Keras AveragePooling2D((3, 3), strides=1, padding="same") averages over the valid
+    # window only (count_include_pad=False)
+    return F.avg_pool2d(x, 3, 1, 1, count_include_pad=False)
 
 
 class InceptionA(nn.Module):
+    """mixed0-2: 1x1 | 1x1-5x5 | 1x1-3x3-3x3 | avgpool-1x1."""
+
     def __init__(self, cin, pool):
         super().__init__()
         self.b1 = BasicConv(cin, 64, kernel_size=1)
@@ -95,10 +110,12 @@ class InceptionA(nn.Module):
         self.bp = BasicConv(cin, pool, kernel_size=1)
 
     def forward(self, x):
-        return torch.cat([self.b1(x), self.b5(x), self.b3(x), self.bp(F.avg_pool2d(x, 3, 1, 1))], 1)
+        return torch.cat([self.b1(x), self.b5(x), self.b3(x), self.bp(_avg3(x))], 1)
 
 
 class InceptionB(nn.Module):
+    """mixed3 (grid reduction): 3x3/2 | 1x1-3x3-3x3/2 | maxpool/2."""
+
     def __init__(self, cin):
         super().__init__()
         self.b3 = BasicConv(cin, 384, kernel_size=3, stride=2)
@@ -110,6 +127,8 @@ class InceptionB(nn.Module):
 
 
 class InceptionC(nn.Module):
+    """mixed4-7: factorised 7x7 branches."""
+
     def __init__(self, cin, c7):
         super().__init__()
         self.b1 = BasicConv(cin, 192, kernel_size=1)
@@ -122,22 +141,70 @@ class InceptionC(nn.Module):
         self.bp = BasicConv(cin, 192, kernel_size=1)
 
     def forward(self, x):
-        return torch.cat([self.b1(x), self.b7(x), self.bd(x), self.bp(F.avg_pool2d(x, 3, 1, 1))], 1)
+        return torch.cat([self.b1(x), self.b7(x), self.bd(x), self.bp(_avg3(x))], 1)
+
+
+class InceptionD(nn.Module):
+    """mixed8 (grid reduction): 1x1-3x3/2 | 1x1-1x7-7x1-3x3/2 | maxpool/2."""
+
+    def __init__(self, cin):
+        super().__init__()
+        self.b3 = nn.Sequential(BasicConv(cin, 192, kernel_size=1), BasicConv(192, 320, kernel_size=3, stride=2))
+        self.b7 = nn.Sequential(BasicConv(cin, 192, kernel_size=1),
+                                BasicConv(192, 192, kernel_size=(1, 7), padding=(0, 3)),
+                                BasicConv(192, 192, kernel_size=(7, 1), padding=(3, 0)),
+                                BasicConv(192, 192, kernel_size=3, stride=2))
+
+    def forward(self, x):
+        return torch.cat([self.b3(x), self.b7(x), max_pool2d(x, 3, 2)], 1)
+
+
+class InceptionE(nn.Module):
+    """mixed9-10: 1x1 | 1x1-(1x3 | 3x1) | 1x1-3x3-(1x3 | 3x1) | avgpool-1x1."""
+
+    def __init__(self, cin):
+        super().__init__()
+        self.b1 = BasicConv(cin, 320, kernel_size=1)
+        self.b3 = BasicConv(cin, 384, kernel_size=1)
+        self.b3a = BasicConv(384, 384, kernel_size=(1, 3), padding=(0, 1))
+        self.b3b = BasicConv(384, 384, kernel_size=(3, 1), padding=(1, 0))
+        self.bd = nn.Sequential(BasicConv(cin, 448, kernel_size=1), BasicConv(448, 384, kernel_size=3, padding=1))
+        self.bda = BasicConv(384, 384, kernel_size=(1, 3), padding=(0, 1))
+        self.bdb = BasicConv(384, 384, kernel_size=(3, 1), padding=(1, 0))
+        self.bp = BasicConv(cin, 192, kernel_size=1)
+
+    def forward(self, x):
+        b3 = self.b3(x)
+        bd = self.bd(x)
+        return torch.cat([self.b1(x), self.b3a(b3), self.b3b(b3), self.bda(bd), self.bdb(bd), self.bp(_avg3(x))], 1)
 
 
 class InceptionV3(nn.Module):
-    """InceptionV3 trunk (A/B/C stages) + head; sized for 75x75 inputs."""
+    """Keras ``applications.InceptionV3(include_top=True)``; 75x75 inputs give 7x7 after the
+    stem, 3x3 after mixed3 and 1x1 after mixed8."""
 
     def __init__(self, num_classes=10):
         super().__init__()
         self.stem = nn.Sequential(BasicConv(3, 32, kernel_size=3, stride=2), BasicConv(32, 32, kernel_size=3),
                                   BasicConv(32, 64, kernel_size=3, padding=1), FusedMaxPool2d(3, 2),
-                                  BasicConv(64, 80, kernel_size=1), BasicConv(80, 192, kernel_size=3))
+                                  BasicConv(64, 80, kernel_size=1), BasicConv(80, 192, kernel_size=3),
+                                  FusedMaxPool2d(3, 2))
         self.a = nn.Sequential(InceptionA(192, 32), InceptionA(256, 64), InceptionA(288, 64))
         self.b = InceptionB(288)
         self.c = nn.Sequential(InceptionC(768, 128), InceptionC(768, 160), InceptionC(768, 160), InceptionC(768, 192))
-        self.fc = nn.Linear(768, num_classes)
+        self.d = InceptionD(768)
+        self.e = nn.Sequential(InceptionE(1280), InceptionE(2048))
+        self.fc = nn.Linear(2048, num_classes)
 
     def forward(self, x):
-        x = self.c(self.b(self.a(self.stem(x))))
+        x = self.e(self.d(self.c(self.b(self.a(self.stem(x))))))
         return self.fc(torch.flatten(F.adaptive_avg_pool2d(x, 1), 1))
+
+
+def keras_param_count(model: nn.Module) -> int:
+    """Parameters counted as Keras' ``model.count_params()``: weights + BN moving statistics."""
+    n = sum(p.numel() for p in model.parameters())
+    for m in model.modules():
+        if isinstance(m, nn.BatchNorm2d) and m.track_running_stats:
+            n += m.running_mean.numel() + m.running_var.numel()
+    return n

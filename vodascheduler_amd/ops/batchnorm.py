@@ -83,7 +83,7 @@ class _BNActFn(torch.autograd.Function):
         bias = ctx.bias
         # fp32 gamma/beta grads go straight into the optimizer's flat grad buffer when it
         # owns them (same contract as ops/dense.py), else into fresh tensors
-        direct = (need_w and need_b and _direct_fp32(weight) and _direct_fp32(bias))
+        direct = (need_b and _direct_fp32(bias) and ((need_w and _direct_fp32(weight)) or weight is None))
         if direct:
             dw, db = flat_grad(weight), flat_grad(bias)
         else:
@@ -99,7 +99,8 @@ class _BNActFn(torch.autograd.Function):
         if dres is None and ctx.has_res and ctx.needs_input_grad[1] and ctx.sink is None:
             dres = dy
         if direct:
-            _ready(weight)
+            if weight is not None:
+                _ready(weight)
             _ready(bias)
             return dx, dres, None, None, None, None, None, None, None, None
         return dx, dres, dw, db, None, None, None, None, None, None
@@ -142,9 +143,14 @@ class FusedBatchNorm2d(torch.nn.BatchNorm2d):
     ``forward(x, residual=None) = relu?(bn(x) + residual)``.  State dict compatible with
     ``torch.nn.BatchNorm2d``."""
 
-    def __init__(self, num_features: int, eps: float = 1e-5, momentum: float = 0.1, relu: bool = False, **kw):
+    def __init__(self, num_features: int, eps: float = 1e-5, momentum: float = 0.1, relu: bool = False,
+                 scale: bool = True, **kw):
+        """``scale=False``: no gamma (Keras ``BatchNormalization(scale=False)``, used by the
+        reference's InceptionV3 conv2d_bn blocks); beta and the running statistics remain."""
         super().__init__(num_features, eps=eps, momentum=momentum, **kw)
         self.relu = relu
+        if not scale and self.affine:
+            self.register_parameter("weight", None)
 
     def _load_from_state_dict(self, state_dict, prefix, *args, **kwargs):
         self._pending_batches = 0

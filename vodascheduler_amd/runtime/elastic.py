@@ -221,6 +221,30 @@ class ElasticContext:
     def reset_agreement(self) -> None:
         self._agree_evt = None
 
+    def allreduce_values(self, values, op: str = "avg") -> list[float]:
+        """All-reduce a few host/device scalars across the current members and return them on
+        the host (Horovod ``metric_average`` = ``hvd.allreduce(tensor)``, reference
+        pytorch_mnist_elastic.py:119-122).  Every member must call it at the same point."""
+        dev = self.comm.device if self.comm is not None else self.device
+        t = torch.as_tensor(values, dtype=torch.float64 if dev.type == "cpu" else torch.float32).to(dev).reshape(-1)
+        if self.comm is None or self.size <= 1:
+            return [float(v) for v in t.tolist()]
+        if dev.type == "cuda":
+            cs = getattr(self.comm, "stream", None)
+            cur = torch.cuda.current_stream(dev)
+            if cs is not None:
+                cs.wait_stream(cur)
+            self.comm.allreduce_(t, op)
+            if cs is not None:
+                t.record_stream(cs)
+                cur.wait_stream(cs)
+        else:
+            self.comm.allreduce_(t, op)
+        return [float(v) for v in t.tolist()]
+
+    def metric_average(self, value: float) -> float:
+        return self.allreduce_values([value], "avg")[0]
+
 
 # ------------------------------------------------------------------------------------
 # state

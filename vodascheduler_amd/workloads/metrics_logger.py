@@ -10,7 +10,7 @@ import os
 from datetime import datetime
 
 FIELDS = ["epoch", "start_time", "epoch_time_sec", "step_time_sec", "steps", "workers", "local_batch_size",
-          "global_batch_size", "total_epochs", "loss", "samples_per_sec"]
+          "global_batch_size", "total_epochs", "loss", "samples_per_sec", "acc", "val_loss", "val_acc"]
 TIME_FMT = "%Y-%m-%d %H:%M:%S.%f"
 
 
@@ -35,7 +35,10 @@ class MetricsCSVLogger:
         return int(rows[-1]["epoch"]) + 1 if rows else 0
 
     def log_epoch(self, epoch: int, start_time: float, epoch_time: float, steps: int, loss: float | None,
-                  workers: int | None = None) -> dict:
+                  workers: int | None = None, acc: float | None = None, val_loss: float | None = None,
+                  val_acc: float | None = None) -> dict:
+        """One row; ``loss`` / ``acc`` are the epoch's training metrics averaged over the
+        workers, ``val_loss`` / ``val_acc`` the eval pass (Keras ``val_*`` names)."""
         w = workers or self.workers
         row = {
             "epoch": epoch,
@@ -49,6 +52,9 @@ class MetricsCSVLogger:
             "total_epochs": self.total_epochs,
             "loss": "" if loss is None else round(float(loss), 6),
             "samples_per_sec": round(steps * self.local_batch_size * w / max(epoch_time, 1e-9), 3),
+            "acc": "" if acc is None else round(float(acc), 6),
+            "val_loss": "" if val_loss is None else round(float(val_loss), 6),
+            "val_acc": "" if val_acc is None else round(float(val_acc), 6),
         }
         if self.path:
             new = not os.path.exists(self.path)

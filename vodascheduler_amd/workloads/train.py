@@ -57,6 +57,7 @@ class TrainConfig:
     data_pool: int = 2                 # distinct synthetic batches cycled through
     graph: bool = True                 # capture the whole step in a hipGraph when world == 1 (graph-safe models)
     final_state_path: str | None = None  # rank 0 saves the final state (checkpoint format) here
+    eval_batches: int = 0              # held-out synthetic batches evaluated after every epoch (0: no eval)
     report_progress: bool = False      # rank 0 publishes the committed step under job/<name>/progress
 
 
@@ -154,10 +155,37 @@ def train_elastic(ctx: ElasticContext, cfg: TrainConfig, use_cache: bool = True)
         # autocast's weight-cast cache must be off inside a captured graph
         with torch.autocast(device.type, dtype=torch.bfloat16, enabled=cfg.amp and device.type == "cuda",
                             cache_enabled=False):
-            loss = w.loss(model, batch)
+            loss, correct, n = w.loss_metrics(model, batch)
         loss.backward()
         ddp.step()
-        return loss
+        # [loss, #correct, #predictions] on the device: no host sync per step
+        return torch.stack([loss.detach().float(), correct.float(), n.float()])
+
+    eval_pool = None
+    if cfg.eval_batches > 0:
+        g = torch.Generator(device=device).manual_seed(cfg.seed + 7919)  # held out from the training pool
+        eval_pool = [w.make_batch(bs, device, g) for _ in range(cfg.eval_batches)]
+        if w.channels_last and device.type == "cuda":
+            eval_pool = [tuple(t.to(memory_format=torch.channels_last) if t.dim() == 4 else t for t in b)
+                         for b in eval_pool]
+
+    @torch.no_grad()
+    def evaluate() -> tuple[float, float]:
+        """Validation pass (reference ``test()``, pytorch_mnist_elastic.py:155-176): the
+        held-out batches are sharded over the current members, per-rank sums are all-reduced,
+        so the result is the exact global mean whatever the world size."""
+        model.eval()
+        tot = torch.zeros(3, device=device, dtype=torch.float32)
+        try:
+            for i in range(ctx.rank if ctx.rank >= 0 else 0, len(eval_pool), max(1, ctx.size)):
+                with torch.autocast(device.type, dtype=torch.bfloat16, enabled=cfg.amp and device.type == "cuda",
+                                    cache_enabled=False):
+                    loss, correct, n = w.loss_metrics(model, eval_pool[i])
+                tot += torch.stack([loss.float() * n.float(), correct.float(), n.float()])
+        finally:
+            model.train()
+        s_loss, s_corr, s_n = ctx.allreduce_values(tot, "sum")
+        return s_loss / max(s_n, 1.0), s_corr / max(s_n, 1.0)
 
     @run
     def train(state):
@@ -176,10 +204,13 @@ def train_elastic(ctx: ElasticContext, cfg: TrainConfig, use_cache: bool = True)
         while state.epoch < cfg.epochs:
             t_ep = time.time()
             steps = 0
+            ep_acc = torch.zeros(3, device=device)  # sum over steps of [loss, #correct, #predictions]
             while state.samples < samples_per_epoch:
                 batch = pool[state.step % len(pool)]
                 with trace_range("train_step", "train", world=world):
-                    loss_t = stepper(batch).detach()
+                    m_t = stepper(batch)
+                ep_acc += m_t
+                loss_t = m_t[0]
                 state.samples += bs * world
                 state.step += 1
                 steps += 1
@@ -193,9 +224,18 @@ def train_elastic(ctx: ElasticContext, cfg: TrainConfig, use_cache: bool = True)
                 torch.cuda.synchronize(device)
             ep_time = time.time() - t_ep
             stats["train_time"] += ep_time
+            # epoch training loss / accuracy averaged over the members (metric_average); the
+            # steps since this membership began (a resize restarts the epoch's tally)
+            loc = ep_acc.tolist()
+            mean_loss = loc[0] / steps if steps else float("nan")
+            acc = loc[1] / loc[2] if loc[2] > 0 else float("nan")
+            mean_loss, acc = ctx.allreduce_values([mean_loss, acc], "avg")
+            val = evaluate() if eval_pool is not None else (None, None)
             if ctx.rank == 0:
-                logger.log_epoch(state.epoch, t_ep, ep_time, steps, float(loss_t) if loss_t is not None else None,
-                                 world)
+                logger.log_epoch(state.epoch, t_ep, ep_time, steps, None if steps == 0 else mean_loss, world,
+                                 acc=None if acc != acc else acc, val_loss=val[0], val_acc=val[1])
+            stats.setdefault("epoch_metrics", []).append({"loss": mean_loss, "acc": acc, "val_loss": val[0],
+                                                          "val_acc": val[1], "world": world})
             state.epoch += 1
             state.samples = 0
             state.commit()
@@ -260,7 +300,7 @@ def replay_reference(cfg: TrainConfig, world_log: list[int], total_steps: int, d
         ddp.zero_grad()
         with torch.autocast(device.type, dtype=torch.bfloat16, enabled=cfg.amp and device.type == "cuda",
                             cache_enabled=False):
-            loss = w.loss(model, pool[step % len(pool)])
+            loss = w.loss_metrics(model, pool[step % len(pool)])[0]
         loss.backward()
         ddp.step()
         samples += bs * world
