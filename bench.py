@@ -37,6 +37,9 @@ import threading
 import time
 
 os.environ.setdefault("GLOO_SOCKET_IFNAME", "lo")
+# single node: RCCL's bootstrap (unique-id exchange, proxy handshakes) over loopback; the data
+# path is P2P over xGMI regardless of the socket interface
+os.environ.setdefault("NCCL_SOCKET_IFNAME", "lo")
 os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
 
 STEP_SCALE = 10  # single-GPU steps per unit of --steps in the mean job
@@ -187,10 +190,17 @@ def main():
     comm_backend = a.comm_backend or ("rccl" if a.device == "cuda" else "gloo")
     if a.share_gpu and comm_backend != "gloo":
         raise SystemExit("--share-gpu needs --comm-backend gloo")
+    topo_info = {}
     if a.device == "cuda":
         device = torch.device("cuda", 0 if a.share_gpu else local)
         torch.cuda.set_device(device)
         _native.hip()  # the HIP extension must be present on a GPU box
+        from vodascheduler_amd.utils.topology import discover, pin_to_gpu_numa
+
+        cpus = pin_to_gpu_numa(device.index) if os.environ.get("VODA_NUMA_PIN", "1") != "0" else []
+        topo = discover()
+        topo_info = {"kfd_gpus": topo.n, "xgmi_links_per_gpu": topo.links_per_gpu(), "xgmi_full_mesh": topo.full_mesh(),
+                     "numa_domains": len(topo.numa_groups()) if topo.n else 0, "numa_pinned_cpus": len(cpus)}
     else:
         device = torch.device("cpu")
         torch.set_num_threads(1)
@@ -233,9 +243,12 @@ def main():
     if rank == 0:
         def drive():
             try:
+                gpu_numa = None
+                if a.device == "cuda" and topo.n >= world and not a.share_gpu:
+                    gpu_numa = {"node0": {r: topo.numa.get(r, 0) for r in range(world)}}
                 result.update(run_trace(store, trace, locs, a.algorithm, rate_limit_sec=a.rate_limit,
                                         tick_sec=1.0, train_defaults=defaults, timeout=3000,
-                                        progress=lambda s: log(0, s), trace_path=a.trace))
+                                        progress=lambda s: log(0, s), trace_path=a.trace, gpu_numa=gpu_numa))
             except BaseException as e:  # never leave the pool hanging
                 result["error"] = repr(e)
                 store.set("pool/shutdown", "1")
@@ -325,6 +338,7 @@ def main():
             "rccl_init_p50_s": q(fresh, 0.5),
             "rccl_init_p95_s": q(fresh, 0.95),
             "throughput_samples_per_s": round(samples / wall_s, 1),
+            "topology": topo_info,
             "warmup_single_gpu_step_ms": {k: round(v, 2) for k, v in step_ms.items()},
         }
         print(json.dumps(line), flush=True)

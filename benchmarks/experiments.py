@@ -20,7 +20,8 @@ import sys
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from vodascheduler_amd.algorithm import ALGORITHMS  # noqa: E402
 from vodascheduler_amd.sim.simulator import simulate  # noqa: E402
-from vodascheduler_amd.sim.trace import TraceJob, make_spec, philly_trace  # noqa: E402
+from vodascheduler_amd.sim.trace import (ASSUMED_BUSBW_GBS, ASSUMED_INTERNODE_BUSBW_GBS, TraceJob,  # noqa: E402
+                                         make_spec, philly_trace)
 
 ORDER = ["FIFO", "ElasticFIFO", "SRJF", "ElasticSRJF", "Tiresias", "ElasticTiresias", "FfDLOptimizer", "AFS-L"]
 
@@ -49,9 +50,9 @@ def exp4():
     nodes = {"node0": list(range(8)), "node1": list(range(8))}
     drains = [(300.0, "node0", 2), (600.0, "node1", 5), (900.0, "node0", 6)]
     out = []
-    for placement in (True, False):
-        r = simulate(tr, "ElasticFIFO", nodes=nodes, drain=drains, use_placement=placement)
-        out.append((placement, r))
+    for name, kw in (("Munkres + best-fit", {}), ("best-fit, migration-naive binding", {"naive_placement": True})):
+        r = simulate(tr, "ElasticFIFO", nodes=nodes, drain=drains, **kw)
+        out.append((name, r))
     return out
 
 
@@ -67,22 +68,29 @@ def exp5():
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--out", default="profiles/r1_sim_experiments.md")
+    ap.add_argument("--out", default="profiles/r2_sim_experiments.md")
     a = ap.parse_args()
     assert set(ORDER) == set(ALGORITHMS)
-    lines = ["# BASELINE.json configs in the discrete-event simulator (round 1)", "",
-             "Real scheduler / allocator / placement code driven in virtual time (`benchmarks/experiments.py`); "
-             "job speed curves from the MI355X-calibrated profiles in `vodascheduler_amd/sim/trace.py`. "
-             "Resize pause 5 s, restart-from-checkpoint pause 15 s, rate limit 30 s (reference default).", ""]
+    lines = ["# BASELINE.json configs in the discrete-event simulator (round 2)", "",
+             "Real scheduler / allocator / placement code driven in virtual time (`benchmarks/experiments.py`). "
+             "Job speed model (`vodascheduler_amd/sim/trace.py`): single-GPU step times MEASURED on MI355X for "
+             "ResNet-50 and BERT-base (`benchmarks/model_step.py`, fp32 gradients), estimated for the others; "
+             "fp32 gradient bytes exact; ring all-reduce bus bandwidth ASSUMED "
+             f"({ASSUMED_BUSBW_GBS:.0f} GB/s intra-node, {ASSUMED_INTERNODE_BUSBW_GBS:.0f} GB/s across nodes) until "
+             "the 8-GPU bench measures it; 30 % of a step hides the all-reduce.  Resize pause 5 s, "
+             "restart-from-checkpoint pause 15 s, rate limit 30 s (reference default).", ""]
     lines += ["## Config 2: Elastic-Tiresias vs Tiresias, 8 ResNet-50 jobs, 8 GPUs", "", HEADER]
     lines += [row(r) for r in exp2()]
     lines += ["", "## Config 3: AFS-L on a mixed ResNet-50 + BERT-base trace, 8 GPUs", "", HEADER]
     lines += [row(r) for r in exp3()]
-    lines += ["", "## Config 4: GPU drain on 2 x 8 GPUs, Elastic-FIFO, with vs without Munkres placement", "",
+    lines += ["", "## Config 4: GPU drain on 2 x 8 GPUs, Elastic-FIFO: Munkres vs migration-naive binding", "",
+              "Both use the same best-fit packing; the naive binding maps virtual nodes and GPU slots in index "
+              "order, ignoring where workers run (reference bindNodes, placement_manager.go:492-522, is what "
+              "the Munkres binding reproduces).  A job split across nodes all-reduces at inter-node bandwidth.",
+              "",
               "| placement | avg JCT (s) | makespan (s) | resizes | worker migrations |", "|---|---:|---:|---:|---:|"]
-    for placement, r in exp4():
-        lines.append(f"| {'Munkres + best-fit' if placement else 'none'} | {r.avg_jct:.0f} | {r.makespan:.0f} | "
-                     f"{r.resizes} | {r.migrations} |")
+    for name, r in exp4():
+        lines.append(f"| {name} | {r.avg_jct:.0f} | {r.makespan:.0f} | {r.resizes} | {r.migrations} |")
     lines += ["", "## Config 5: 32-job Philly-style trace, all 8 policies, 1/2/4/8 GPUs", "", HEADER]
     res5 = exp5()
     lines += [row(r) for r in res5]

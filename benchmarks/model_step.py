@@ -22,13 +22,15 @@ from vodascheduler_amd.ops.optim import make_optimizer  # noqa: E402
 from vodascheduler_amd.runtime.stepgraph import GraphedStepper  # noqa: E402
 
 
-def run(model: str, batch: int | None, steps: int, warmup: int, marker: bool = False, graph: bool = False) -> dict:
+def run(model: str, batch: int | None, steps: int, warmup: int, marker: bool = False, graph: bool = False,
+        grad_dtype: str = "fp32") -> dict:
     dev = torch.device("cuda", 0)
     w = get_workload(model)
     bs = batch or w.per_gpu_batch
     torch.manual_seed(0)
     m = prepare_model(w, dev)
-    opt = make_optimizer(w.optimizer, m.parameters(), **w.opt_kwargs)
+    opt = make_optimizer(w.optimizer, m.parameters(), grad_dtype={"fp32": torch.float32, "bf16": torch.bfloat16}[grad_dtype],
+                         **w.opt_kwargs)
     b = w.make_batch(bs, dev, None)
     if w.channels_last:
         b = tuple(t.to(memory_format=torch.channels_last) if t.dim() == 4 else t for t in b)
@@ -70,11 +72,14 @@ def main():
     ap.add_argument("--cudnn-benchmark", action="store_true", help="MIOpen exhaustive find (benchmark mode)")
     ap.add_argument("--profile-marker", action="store_true", help="launch a marker kernel before the timed steps")
     ap.add_argument("--graph", action="store_true", help="replay the whole step as one captured hipGraph")
+    ap.add_argument("--grad-dtype", default="fp32", choices=["fp32", "bf16"], help="flat gradient precision")
     a = ap.parse_args()
     if a.cudnn_benchmark:
         torch.backends.cudnn.benchmark = True
     _native.hip()
-    print(json.dumps(run(a.model, a.batch, a.steps, a.warmup, a.profile_marker, a.graph)), flush=True)
+    out = run(a.model, a.batch, a.steps, a.warmup, a.profile_marker, a.graph, a.grad_dtype)
+    out["grad_dtype"] = a.grad_dtype
+    print(json.dumps(out), flush=True)
 
 
 if __name__ == "__main__":

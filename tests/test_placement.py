@@ -165,3 +165,32 @@ def test_placement_metrics_exposed():
                  "voda_scheduler_amd_instinct_mi355x_scheduler_placement_launchers_deleted",
                  "voda_scheduler_amd_instinct_mi355x_scheduler_placement_jobs_cross_node"):
         assert name in text
+
+
+def test_topology_discovery_from_mi355x_fixture():
+    import os
+
+    from vodascheduler_amd.utils.topology import from_dump, parse_cpulist
+
+    here = os.path.dirname(os.path.abspath(__file__))
+    t = from_dump(open(os.path.join(here, "fixtures", "mi355x_kfd_topology_1gpu_box.txt")).read())
+    assert t.n == 8 and t.links_per_gpu() == 7 and t.full_mesh()
+    assert t.numa_groups() == {0: [0, 1, 2, 3], 1: [4, 5, 6, 7]}
+    assert set(t.xgmi_bw_mbs.values()) == {76000}
+    assert 32 <= t.bucket_mb(8) <= 256
+    assert parse_cpulist("0-3,8,10-11") == [0, 1, 2, 3, 8, 10, 11]
+
+
+def test_placement_keeps_new_jobs_inside_one_numa_domain():
+    from vodascheduler_amd.placement.manager import PlacementManager
+
+    numa = {g: (0 if g < 4 else 1) for g in range(8)}
+    pm = PlacementManager("t", {"node0": list(range(8))}, gpu_numa={"node0": numa})
+    p1 = pm.place({"a": 2})
+    p2 = pm.place({"a": 2, "b": 4})
+    gb = [g for _, g in p2.workers["b"]]
+    assert len({numa[g] for g in gb}) == 1, gb          # b gets a whole NUMA domain
+    assert p2.workers["a"] == p1.workers["a"]            # a never moves for it
+    p3 = pm.place({"a": 2, "b": 4, "c": 2})
+    assert len({numa[g] for _, g in p3.workers["c"]}) == 1
+    assert p3.num_migrated == 0

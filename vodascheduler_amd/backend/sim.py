@@ -13,8 +13,8 @@ from dataclasses import dataclass, field
 
 from ..common.store import JobStore, NotFound
 from ..common.types import MAX_NUM_GPU
-from ..sim.trace import PROFILES, ModelProfile, workload_of
-from .base import EV_FINISHED, HALT, MIGRATE, START, Backend, JobAction
+from ..sim.trace import ASSUMED_INTERNODE_BUSBW_GBS, PROFILES, ModelProfile, workload_of
+from .base import EV_FINISHED, HALT, START, Backend, JobAction
 
 Loc = tuple[str, int]
 
@@ -32,9 +32,15 @@ class SimJob:
     workers: list[Loc] = field(default_factory=list)
     resizes: int = 0
     migrations: int = 0
+    cross_node: bool = False     # workers span nodes: the all-reduce runs at inter-node bandwidth
+
+    def speed(self) -> float:
+        if self.n == 0:
+            return 0.0
+        return self.profile.speedup(self.n, ASSUMED_INTERNODE_BUSBW_GBS if self.cross_node else None)
 
     def rate(self, t: float) -> float:
-        return 0.0 if self.n == 0 or t < self.paused_until else self.profile.speedup(self.n)
+        return 0.0 if self.n == 0 or t < self.paused_until else self.speed()
 
 
 class SimBackend(Backend):
@@ -75,7 +81,7 @@ class SimBackend(Backend):
                 continue
             run_from = max(t0, j.paused_until)
             if t > run_from:
-                j.work -= j.profile.speedup(j.n) * (t - run_from)
+                j.work -= j.speed() * (t - run_from)
             self.gpu_busy_seconds += j.n * (t - t0)
         self.t_last = t
 
@@ -85,7 +91,7 @@ class SimBackend(Backend):
             if j.n == 0:
                 continue
             start = max(self.t_last, j.paused_until)
-            te = start + max(j.work, 0.0) / j.profile.speedup(j.n)
+            te = start + max(j.work, 0.0) / j.speed()
             best = te if best is None else min(best, te)
         return best
 
@@ -105,7 +111,7 @@ class SimBackend(Backend):
             if j is None:
                 wl = workload_of(a.job.spec)
                 prof = PROFILES.get(wl["model"], ModelProfile(wl["model"], wl.get("alpha", 0.05), 0.05))
-                if "alpha" in wl:
+                if "alpha" in wl and prof.grad_mb <= 0:
                     prof = ModelProfile(prof.name, float(wl["alpha"]), prof.step_time_1gpu)
                 total = float(wl["epoch_time_1gpu"]) * max(1, a.job.config.epochs)
                 j = SimJob(name, a.job.job_category, prof, total, total, a.job.config.epochs)
@@ -115,13 +121,17 @@ class SimBackend(Backend):
                 j.workers = []
                 continue
             overhead = self.restart_overhead_s if a.kind == START else self.resize_overhead_s
-            if a.kind == MIGRATE:
-                j.migrations += 1
-                self.total_migrations += 1
+            new_w = list(a.workers or [])
+            if j.workers and new_w:
+                # workers that had to move: the kept-worker count falls short of the overlap
+                moved = min(len(j.workers), len(new_w)) - len(set(j.workers) & set(new_w))
+                j.migrations += moved
+                self.total_migrations += moved
             j.resizes += 1
             self.total_resizes += 1
             j.n = a.num_workers
             j.workers = list(a.workers or [])
+            j.cross_node = len({w[0] for w in j.workers}) > 1
             j.paused_until = now + overhead
         if self.info_mode == "oracle":
             self.publish_info()

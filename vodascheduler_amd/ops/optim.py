@@ -46,7 +46,11 @@ class _FusedFlatOptimizer(torch.optim.Optimizer):
         self._flat_state: list[dict[str, torch.Tensor]] = []
         self._steps: list[int] = []
         for g in self.param_groups:
-            fg = FlatGroup(g["params"], flatten_params=True, grad_dtype=grad_dtype)
+            # a low-precision gradient request applies to low-precision (bf16/fp16) weights only;
+            # fp32 parameters (norm layers) always keep fp32 gradients
+            pdt = g["params"][0].dtype if g["params"] else torch.float32
+            gdt = grad_dtype if (grad_dtype is not None and pdt != torch.float32) else torch.float32
+            fg = FlatGroup(g["params"], flatten_params=True, grad_dtype=gdt)
             self.flat_groups.append(fg)
             self._flat_state.append({})
             self._steps.append(0)

@@ -274,9 +274,36 @@ def _nullctx():
     yield
 
 
-def broadcast_tensors(comm: Communicator, tensors: list[torch.Tensor], root: int = 0) -> None:
-    """Broadcast a list of tensors from ``root`` (state sync on elastic resize)."""
+def broadcast_tensors(comm: Communicator, tensors: list[torch.Tensor], root: int = 0,
+                      small_bytes: int = 1 << 20) -> None:
+    """Broadcast a list of tensors from ``root`` in place (state sync on elastic resize).
+
+    Tensors under ``small_bytes`` (BN statistics, biases, step counters: hundreds per model)
+    are packed per dtype into one flat buffer and sent as ONE collective instead of one
+    latency-bound collective each; large tensors (the flat parameter / optimizer-slot
+    buffers) are broadcast in place.  Non-contiguous tensors go through a contiguous copy that
+    is written back."""
     if comm is None or isinstance(comm, LocalCommunicator) or comm.size == 1:
         return
+    small: dict[torch.dtype, list[torch.Tensor]] = {}
     for t in tensors:
-        comm.broadcast_(t if t.is_contiguous() else t.contiguous(), root)
+        if t.numel() == 0:
+            continue
+        if t.numel() * t.element_size() < small_bytes:
+            small.setdefault(t.dtype, []).append(t)
+        elif t.is_contiguous():
+            comm.broadcast_(t, root)
+        else:
+            c = t.contiguous()
+            comm.broadcast_(c, root)
+            with torch.no_grad():
+                t.copy_(c)
+    for dt, ts in small.items():
+        flat = torch.cat([t.detach().reshape(-1) for t in ts])
+        comm.broadcast_(flat, root)
+        with torch.no_grad():
+            off = 0
+            for t in ts:
+                n = t.numel()
+                t.copy_(flat[off:off + n].view_as(t))
+                off += n

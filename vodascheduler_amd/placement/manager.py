@@ -64,9 +64,20 @@ class PlacementPlan:
 
 
 class PlacementManager:
+    """``naive=True``: the migration-naive baseline -- the same best-fit packing, but virtual
+    nodes are bound to real nodes in index order and each node's GPUs are handed out in index
+    order, ignoring where workers currently run (no Munkres at either level).  Used by the
+    GPU-drain experiment to measure what the Munkres binding saves."""
+
     def __init__(self, scheduler_id: str, nodes: dict[str, list[int]] | None = None,
-                 metrics: PlacementMetrics | None = None):
+                 metrics: PlacementMetrics | None = None, naive: bool = False,
+                 gpu_numa: dict[str, dict[int, int]] | None = None):
+        """``gpu_numa``: node -> {GPU index: NUMA domain} from runtime topology discovery
+        (utils/topology.py); a job's GPUs are then kept inside one NUMA domain when that costs
+        no migration (tie-breaker)."""
         self.scheduler_id = scheduler_id
+        self.naive = naive
+        self.gpu_numa = {k: dict(v) for k, v in (gpu_numa or {}).items()}
         self.lock = threading.Lock()
         self.nodes: dict[str, NodeState] = {}
         self.job_nodes: dict[str, list[list]] = {}      # job -> ordered [[node, n], ...]
@@ -207,6 +218,10 @@ class PlacementManager:
         if not real:
             return
         size = len(real)
+        if self.naive:
+            for vi, v in enumerate(virtual[:size]):
+                real[vi].job_num_workers = dict(v.job_num_workers)
+            return
         big = 10 ** 6
         scores = []
         for v in virtual:
@@ -251,13 +266,19 @@ class PlacementManager:
                 gpu_of[node.name] = {}
                 continue
             # keeping a worker on its GPU scores 2 (+ up to 0.5 for low old worker indices, so a
-            # shrinking job keeps its lowest ranks -- rank 0 holds the state); tie-break to
+            # shrinking job keeps its lowest ranks -- rank 0 holds the state); a GPU in the job's
+            # preferred NUMA domain scores 0.1 (never outweighs a kept worker); tie-break to
             # lower GPU ids
+            numa = self.gpu_numa.get(node.name, {})
+            pref = self._preferred_numa(node, numa, occupant) if numa and not self.naive else {}
+
             def score(job: str, k: int, g: int) -> float:
                 occ = occupant.get(g)
                 s = 0.0
-                if occ is not None and occ[0] == job:
+                if occ is not None and occ[0] == job and not self.naive:
                     s = 2.0 + 0.5 / (1 + occ[1])
+                if job in pref and numa.get(g) == pref[job]:
+                    s += 0.1
                 return s - 1e-6 * k
 
             scores = [[score(job, k, g) for k, g in enumerate(gpus)] for job in slots]
@@ -286,6 +307,28 @@ class PlacementManager:
         self.worker_loc = workers
         return PlacementPlan(workers=workers, migrated=migrated, restarted=restarted, cross_node_jobs=0,
                              duration_s=0.0)
+
+    @staticmethod
+    def _preferred_numa(node: NodeState, numa: dict[int, int], occupant: dict[int, tuple[str, int]]) -> dict[str, int]:
+        """Per job on this node: the NUMA domain holding most of its current workers, else
+        (new arrivals, largest demand first) the domain with the most GPUs left unclaimed."""
+        free: dict[int, int] = {}
+        for g in node.gpus:
+            if g not in occupant:
+                free[numa.get(g, 0)] = free.get(numa.get(g, 0), 0) + 1
+        pref: dict[str, int] = {}
+        for job in sorted(node.job_num_workers, key=lambda j: (-node.job_num_workers[j], j)):
+            have: dict[int, int] = {}
+            for g, (oj, _i) in occupant.items():
+                if oj == job and g in node.gpus:
+                    have[numa.get(g, 0)] = have.get(numa.get(g, 0), 0) + 1
+            if have:
+                pref[job] = max(have, key=lambda d: (have[d], -d))
+            elif free:
+                d = max(free, key=lambda x: (free[x], -x))
+                pref[job] = d
+                free[d] -= min(free[d], node.job_num_workers[job])
+        return pref
 
     # ------------------------------ restart ------------------------------
     def construct_status_on_restart(self, worker_loc: dict[str, list[Loc]]) -> None:

@@ -37,14 +37,19 @@ def free_port() -> int:
 def run_trace(store, trace: list[TraceJob], worker_locs, algorithm: str = "ElasticFIFO",
               rate_limit_sec: float = 1.0, tick_sec: float = 1.0, train_defaults: dict | None = None,
               timeout: float = 3600.0, gpu_type: str = DEFAULT_GPU_TYPE, progress=None,
-              collect_every_s: float = 2.0, trace_path: str | None = None) -> dict:
+              collect_every_s: float = 2.0, trace_path: str | None = None,
+              gpu_numa: dict[str, dict[int, int]] | None = None) -> dict:
     """Submit ``trace`` in real time (``submit_time`` seconds after start) and wait until every
-    job completed.  Returns JCT / makespan / resize-latency statistics."""
+    job completed.  Returns JCT / makespan / resize-latency statistics.  ``gpu_numa``: node ->
+    {GPU: NUMA domain} from topology discovery (placement tie-breaker)."""
     db = MemoryStore()
     mq = InProcQueue(maxsize=10 ** 6)
     svc = TrainingService(db, mq)
     backend = PoolBackend(store, worker_locs, train_defaults)
+    from ..placement.manager import PlacementManager
+
     core = SchedulerCore(gpu_type, db, ResourceAllocator(db), backend, algorithm=algorithm,
+                         placement=PlacementManager(gpu_type, gpu_numa=gpu_numa),
                          rate_limit_sec=rate_limit_sec, tick_sec=tick_sec)
     tracer = None
     if trace_path:

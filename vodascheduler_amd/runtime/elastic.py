@@ -368,9 +368,10 @@ class State:
             root = 0
             if ctx.rank == 0:
                 self._load_from_rest()
-        for t in self.tensors():
-            if comm is not None and comm.size > 1:
-                comm.broadcast_(t, root)
+        if comm is not None and comm.size > 1:
+            from ..parallel.ddp import broadcast_tensors
+
+            broadcast_tensors(comm, self.tensors(), root)  # small tensors coalesced per dtype
         extras = dict(self._extras, __step__=self.step)
         extras = broadcast_object(comm, extras, root)
         self.step = extras.pop("__step__")

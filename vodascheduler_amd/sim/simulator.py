@@ -52,17 +52,25 @@ def simulate(trace: list[TraceJob], algorithm: str = "ElasticFIFO", gpus: int = 
              nodes: dict[str, list[int]] | None = None, rate_limit_sec: float = 30.0, tick_sec: float = 5.0,
              resize_overhead_s: float = 5.0, restart_overhead_s: float = 15.0, use_placement: bool = True,
              drain: list[tuple[float, str, int]] | None = None, max_time: float = 1e9,
-             gpu_type: str = DEFAULT_GPU_TYPE, trace_path: str | None = None) -> SimResult:
+             gpu_type: str = DEFAULT_GPU_TYPE, trace_path: str | None = None,
+             naive_placement: bool = False) -> SimResult:
     """Run a trace to completion.  ``drain`` = [(time, node, gpu)] GPU drain events;
-    ``trace_path`` writes the scheduler timeline (Chrome-trace JSON, virtual time)."""
+    ``trace_path`` writes the scheduler timeline (Chrome-trace JSON, virtual time);
+    ``naive_placement``: best-fit without the Munkres bindings (placement/manager.py)."""
     clock = ManualClock(0.0)
     store = MemoryStore()
     mq = InProcQueue(maxsize=10 ** 6)
     svc = TrainingService(store, mq, clock)
     nodes = nodes or {"node0": list(range(gpus))}
     backend = SimBackend(clock, nodes, store, resize_overhead_s, restart_overhead_s)
-    core = SchedulerCore(gpu_type, store, ResourceAllocator(store), backend, clock=clock, algorithm=algorithm,
-                         rate_limit_sec=rate_limit_sec, tick_sec=tick_sec, use_placement=use_placement)
+    placement = None
+    if use_placement and naive_placement:
+        from ..placement.manager import PlacementManager
+
+        placement = PlacementManager(gpu_type, naive=True)
+    core = SchedulerCore(gpu_type, store, ResourceAllocator(store), backend, placement=placement, clock=clock,
+                         algorithm=algorithm, rate_limit_sec=rate_limit_sec, tick_sec=tick_sec,
+                         use_placement=use_placement)
     tracer = None
     if trace_path:
         from ..utils.tracing import SchedulerTracer

@@ -19,36 +19,67 @@ from ..common.types import DEFAULT_GPU_TYPE, GPU_NAME_LABEL, GPU_RESOURCE
 WORKLOAD_ANNOTATION = "vodascheduler/workload"
 
 
+# Ring all-reduce bus bandwidth assumed for the speed model until the multi-GPU bench measures
+# it (GB/s, fp32 gradients, one 8 x MI355X node over xGMI).  ASSUMED, not measured.
+ASSUMED_BUSBW_GBS = 300.0
+# Cross-node all-reduce bus bandwidth assumed for jobs whose workers span nodes (GB/s).
+ASSUMED_INTERNODE_BUSBW_GBS = 40.0
+
+
 @dataclass
 class ModelProfile:
-    """Scaling model of a workload: speedup(n) = n / (1 + alpha * (n - 1)) (Amdahl-like
-    communication share alpha).  Defaults are calibrated from MI355X measurements where
-    available (see docs/PERFORMANCE.md)."""
+    """Scaling model of a workload.
+
+    With ``grad_mb`` > 0 (the models measured on MI355X): one step on ``n`` GPUs takes
+    ``t1 + exposed(n)`` with ``t1 = step_time_1gpu`` (MEASURED, single MI355X, bf16 compute,
+    fp32 gradients) and the ring all-reduce ``c(n) = 2 (n-1)/n * grad_bytes / busbw`` of which
+    the part not hidden behind the backward pass (``overlap`` x t1) is exposed;
+    ``speedup(n) = n t1 / (t1 + exposed(n))``.  ``busbw`` is ASSUMED (``ASSUMED_BUSBW_GBS``)
+    until the 8-GPU bench measures it.  Otherwise the Amdahl-like fallback
+    ``n / (1 + alpha (n - 1))`` with a guessed ``alpha``."""
 
     name: str
     alpha: float
     step_time_1gpu: float  # seconds per step at the per-GPU batch on one GPU
+    grad_mb: float = 0.0   # fp32 gradient bytes per step (MB) -- exact, from the parameter count
+    overlap: float = 0.3   # fraction of t1 that hides the all-reduce (bucket overlap with backward)
+    measured: bool = False
 
-    def speedup(self, n: int) -> float:
+    def comm_time(self, n: int, busbw_gbs: float = ASSUMED_BUSBW_GBS) -> float:
+        if n <= 1:
+            return 0.0
+        return 2.0 * (n - 1) / n * self.grad_mb * 1e6 / (busbw_gbs * 1e9)
+
+    def speedup(self, n: int, busbw_gbs: float | None = None) -> float:
         if n <= 0:
             return 0.0
+        if self.grad_mb > 0:
+            t1 = self.step_time_1gpu
+            c = self.comm_time(n, busbw_gbs or ASSUMED_BUSBW_GBS)
+            exposed = max(0.0, c - self.overlap * t1)
+            return n * t1 / (t1 + exposed)
         return n / (1.0 + self.alpha * (n - 1))
 
 
+# step_time_1gpu: MI355X measurements (benchmarks/model_step.py, bf16 autocast, fp32 flat
+# gradients, profiles/r2_*): ResNet-50 bs256 and BERT-base bs64 seq128.  The others are the
+# round-1 estimates (marked measured=False).  grad_mb = 4 bytes x parameter count.
 PROFILES = {
-    "resnet50": ModelProfile("resnet50", alpha=0.03, step_time_1gpu=0.043),
-    "bert-base": ModelProfile("bert-base", alpha=0.05, step_time_1gpu=0.060),
-    "vgg16": ModelProfile("vgg16", alpha=0.08, step_time_1gpu=0.030),
-    "transformer": ModelProfile("transformer", alpha=0.10, step_time_1gpu=0.020),
-    "mnist": ModelProfile("mnist", alpha=0.30, step_time_1gpu=0.004),
-    "mnist-torch": ModelProfile("mnist-torch", alpha=0.40, step_time_1gpu=0.002),
-    "resnet50-cifar": ModelProfile("resnet50-cifar", alpha=0.05, step_time_1gpu=0.020),
-    "resnet18": ModelProfile("resnet18", alpha=0.04, step_time_1gpu=0.020),
-    "inceptionv3": ModelProfile("inceptionv3", alpha=0.05, step_time_1gpu=0.030),
+    "resnet50": ModelProfile("resnet50", alpha=0.01, step_time_1gpu=0.0277, grad_mb=102.2, measured=True),
+    "bert-base": ModelProfile("bert-base", alpha=0.05, step_time_1gpu=0.0119, grad_mb=438.0, measured=True),
+    "vgg16": ModelProfile("vgg16", alpha=0.08, step_time_1gpu=0.030, grad_mb=134.6),
+    "transformer": ModelProfile("transformer", alpha=0.10, step_time_1gpu=0.020, grad_mb=79.8),
+    "mnist": ModelProfile("mnist", alpha=0.30, step_time_1gpu=0.004, grad_mb=4.8),
+    "mnist-torch": ModelProfile("mnist-torch", alpha=0.40, step_time_1gpu=0.002, grad_mb=0.087),
+    "resnet50-cifar": ModelProfile("resnet50-cifar", alpha=0.05, step_time_1gpu=0.020, grad_mb=94.1),
+    "resnet18": ModelProfile("resnet18", alpha=0.04, step_time_1gpu=0.020, grad_mb=46.8),
+    "inceptionv3": ModelProfile("inceptionv3", alpha=0.05, step_time_1gpu=0.030, grad_mb=87.2),
 }
 
 
 def speedup_table(profile: ModelProfile, max_gpu: int = 32) -> dict[str, float]:
+    """Speedup keyed by the worker count as a decimal string, "0".."max_gpu+1"
+    (reference trainingjob.go:168-187)."""
     return {str(i): profile.speedup(i) for i in range(0, max_gpu + 2)}
 
 
