@@ -23,7 +23,7 @@ from vodascheduler_amd.runtime.stepgraph import GraphedStepper  # noqa: E402
 
 
 def run(model: str, batch: int | None, steps: int, warmup: int, marker: bool = False, graph: bool = False,
-        grad_dtype: str = "fp32") -> dict:
+        grad_dtype: str = "fp32", overlap_opt: bool = False) -> dict:
     dev = torch.device("cuda", 0)
     w = get_workload(model)
     bs = batch or w.per_gpu_batch
@@ -35,12 +35,18 @@ def run(model: str, batch: int | None, steps: int, warmup: int, marker: bool = F
     if w.channels_last:
         b = tuple(t.to(memory_format=torch.channels_last) if t.dim() == 4 else t for t in b)
 
+    ddp = None
+    if overlap_opt:  # the trainer's path: per-bucket optimizer updates overlapping backward
+        from vodascheduler_amd.parallel.ddp import ElasticDDP
+
+        ddp = ElasticDDP(m, None, opt, overlap_optimizer=True)
+
     def step_fn(bb):
-        opt.zero_grad()
+        (ddp or opt).zero_grad()
         with torch.autocast("cuda", dtype=torch.bfloat16, cache_enabled=not graph):
             loss = w.loss(m, bb)
         loss.backward()
-        opt.step()
+        (ddp or opt).step()
         return loss
 
     stepper = GraphedStepper(step_fn, m, opt, warmup=2, enabled=graph)
@@ -73,12 +79,14 @@ def main():
     ap.add_argument("--profile-marker", action="store_true", help="launch a marker kernel before the timed steps")
     ap.add_argument("--graph", action="store_true", help="replay the whole step as one captured hipGraph")
     ap.add_argument("--grad-dtype", default="fp32", choices=["fp32", "bf16"], help="flat gradient precision")
+    ap.add_argument("--overlap-opt", action="store_true", help="per-bucket optimizer overlapping backward (ElasticDDP)")
     a = ap.parse_args()
     if a.cudnn_benchmark:
         torch.backends.cudnn.benchmark = True
     _native.hip()
-    out = run(a.model, a.batch, a.steps, a.warmup, a.profile_marker, a.graph, a.grad_dtype)
+    out = run(a.model, a.batch, a.steps, a.warmup, a.profile_marker, a.graph, a.grad_dtype, a.overlap_opt)
     out["grad_dtype"] = a.grad_dtype
+    out["overlap_opt"] = a.overlap_opt
     print(json.dumps(out), flush=True)
 
 

@@ -250,3 +250,41 @@ def test_encoder_residual_grad_sink_matches_autograd(monkeypatch):
     torch.testing.assert_close(dx1, dx0)
     for a, b in zip(g1, g0):
         torch.testing.assert_close(a, b)
+
+
+@pytest.mark.parametrize("name,kw", [("sgd", dict(lr=0.1, momentum=0.9, weight_decay=1e-4)),
+                                     ("adamw", dict(lr=1e-3, weight_decay=0.01)),
+                                     ("rmsprop", dict(lr=1e-3, momentum=0.5, centered=True))])
+def test_step_range_pieces_equal_whole_step(name, kw):
+    """Per-bucket updates (begin_step + step_range over a partition) == one optimizer.step()."""
+    from vodascheduler_amd.ops.optim import make_optimizer
+
+    def build():
+        torch.manual_seed(0)
+        return torch.nn.Sequential(torch.nn.Linear(16, 64), torch.nn.Tanh(), torch.nn.Linear(64, 8))
+
+    a, b = build(), build()
+    oa, ob = make_optimizer(name, a.parameters(), **kw), make_optimizer(name, b.parameters(), **kw)
+    x = torch.randn(32, 16)
+    for _ in range(3):
+        for m, o in ((a, oa), (b, ob)):
+            o.zero_grad()
+            m(x).square().mean().backward()
+        oa.step()
+        ob.begin_step()
+        n = ob.flat_groups[0].numel
+        cuts = [0, 64, 1088, n]  # slot-aligned pieces, applied out of order
+        for lo, hi in sorted(zip(cuts[:-1], cuts[1:]), key=lambda r: -r[0]):
+            ob.step_range(0, lo, hi)
+    for pa, pb in zip(a.parameters(), b.parameters()):
+        assert torch.equal(pa, pb)
+
+
+def test_ddp_overlap_optimizer_is_opt_in_and_cpu_off():
+    from vodascheduler_amd.ops.optim import make_optimizer
+    from vodascheduler_amd.parallel.ddp import ElasticDDP
+
+    m = torch.nn.Linear(8, 8)
+    o = make_optimizer("sgd", m.parameters(), lr=0.1)
+    assert not ElasticDDP(m, None, o).overlap_optimizer
+    assert not ElasticDDP(m, None, o, overlap_optimizer=True).overlap_optimizer  # CPU: never

@@ -269,3 +269,40 @@ def test_fused_linear_bf16_flat_grads_gpu():
     assert m.weight.grad is None and grad_of(m.weight).dtype == torch.float32  # fp32 flat gradient
     torch.testing.assert_close(grad_of(m.weight), ref.weight.grad, atol=0.5, rtol=5e-2)
     torch.testing.assert_close(grad_of(m.bias), ref.bias.grad, atol=0.5, rtol=5e-2)
+
+
+@pytest.mark.parametrize("opt_name", ["adamw", "sgd"])
+def test_overlapped_per_bucket_optimizer_matches_plain_step(opt_name):
+    """ElasticDDP(overlap_optimizer=True): per-bucket updates on the comm stream during
+    backward give bitwise the same weights as one optimizer pass after backward."""
+    from vodascheduler_amd.models import cast_compute_weights_
+    from vodascheduler_amd.ops.dense import FusedLinear
+    from vodascheduler_amd.ops.layernorm import FusedLayerNorm
+    from vodascheduler_amd.ops.optim import make_optimizer
+    from vodascheduler_amd.parallel.ddp import ElasticDDP
+
+    def build():
+        torch.manual_seed(0)
+        layers = []
+        for _ in range(6):
+            layers += [FusedLinear(512, 512), FusedLayerNorm(512)]
+        return cast_compute_weights_(torch.nn.Sequential(*layers).cuda())
+
+    kw = dict(lr=1e-3, weight_decay=0.01) if opt_name == "adamw" else dict(lr=0.05, momentum=0.9)
+    runs = []
+    for overlap in (False, True):
+        m = build()
+        opt = make_optimizer(opt_name, m.parameters(), **kw)
+        ddp = ElasticDDP(m, None, opt, bucket_cap_mb=1.0, first_bucket_mb=0.5, overlap_optimizer=overlap)
+        assert len(ddp.buckets) >= 4
+        x = torch.randn(1024, 512, device="cuda").bfloat16()
+        for _ in range(3):
+            ddp.zero_grad()
+            with torch.autocast("cuda", dtype=torch.bfloat16, cache_enabled=False):
+                loss = m(x).float().square().mean()
+            loss.backward()
+            ddp.step()
+        torch.cuda.synchronize()
+        runs.append([t.clone() for t in opt.flat_state_tensors()])
+    for a, b in zip(*runs):
+        assert torch.equal(a, b)

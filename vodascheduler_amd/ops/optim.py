@@ -77,20 +77,41 @@ class _FusedFlatOptimizer(torch.optim.Optimizer):
         if closure is not None:
             with torch.enable_grad():
                 loss = closure()
-        self._step_t.add_(1)
-        for gi, group in enumerate(self.param_groups):
-            self._steps[gi] += 1
-            fg = self.flat_groups[gi]
-            if fg.master.is_cuda:
-                self._step_gpu(gi, group, fg)
-            else:
-                self._step_cpu(gi, group, fg)
+        self.begin_step()
+        for gi, fg in enumerate(self.flat_groups):
+            self.step_range(gi, 0, fg.numel)
         return loss
 
-    def _lowp_args(self, fg: FlatGroup) -> tuple[int, int]:
+    @torch.no_grad()
+    def begin_step(self) -> None:
+        """Advance the step counters (host + device) once per training step; the updates then
+        run as one ``step_range`` per group or per gradient bucket (parallel/ddp.py overlaps
+        them with backward)."""
+        self._step_t.add_(1)
+        for gi in range(len(self._steps)):
+            self._steps[gi] += 1
+
+    @torch.no_grad()
+    def step_range(self, gi: int, start: int, end: int) -> None:
+        """Update flat elements ``[start, end)`` of group ``gi`` (bucket boundaries are slot
+        offsets: 64-element aligned, so every sliced pointer stays 256-byte aligned)."""
+        if end <= start:
+            return
+        group, fg = self.param_groups[gi], self.flat_groups[gi]
+        if fg.master.is_cuda:
+            self._step_gpu(gi, group, fg, start, end)
+        else:
+            self._step_cpu(gi, group, fg, start, end)
+
+    def _lowp_args(self, fg: FlatGroup, start: int = 0) -> tuple[int, int]:
         if fg.lowp is None:
             return 0, -1
-        return fg.lowp.data_ptr(), N.dtype_code(fg.lowp.dtype)
+        return fg.lowp.data_ptr() + start * fg.lowp.element_size(), N.dtype_code(fg.lowp.dtype)
+
+    @staticmethod
+    def _at(t: torch.Tensor | None, start: int) -> int:
+        """Device pointer of element ``start`` of a flat buffer (0 for None)."""
+        return 0 if t is None else t.data_ptr() + start * t.element_size()
 
     def _check(self, fg: FlatGroup) -> None:
         N.check_gpu_tensor(fg.master, "master")
@@ -165,29 +186,32 @@ class FusedSGD(_FusedFlatOptimizer):
     def _state_names_for(self, gi):
         return ("momentum_buffer",) if self.param_groups[gi]["momentum"] != 0 else ()
 
-    def _step_gpu(self, gi, g, fg):
+    def _step_gpu(self, gi, g, fg, start=0, end=None):
+        end = fg.numel if end is None else end
         self._check(fg)
         mom = g["momentum"]
         buf = self._buf(gi, "momentum_buffer") if mom != 0 else None
-        lp, lpdt = self._lowp_args(fg)
-        N.hip().sgd_step(fg.master.data_ptr(), fg.grad.data_ptr(), N.dtype_code(fg.grad.dtype), N.ptr(buf), lp, lpdt,
-                         fg.numel, float(g["lr"]), float(mom), float(g["dampening"]), float(g["weight_decay"]),
-                         bool(g["nesterov"]), self._steps[gi] == 1, float(g["grad_scale"]), N.stream_of(fg.master))
+        lp, lpdt = self._lowp_args(fg, start)
+        N.hip().sgd_step(self._at(fg.master, start), self._at(fg.grad, start), N.dtype_code(fg.grad.dtype),
+                         self._at(buf, start), lp, lpdt, end - start, float(g["lr"]), float(mom),
+                         float(g["dampening"]), float(g["weight_decay"]), bool(g["nesterov"]), self._steps[gi] == 1,
+                         float(g["grad_scale"]), N.stream_of(fg.master))
 
-    def _step_cpu(self, gi, g, fg):
-        p = fg.master
-        d = fg.grad.float() * g["grad_scale"]
+    def _step_cpu(self, gi, g, fg, start=0, end=None):
+        sl = slice(start, fg.numel if end is None else end)
+        p = fg.master[sl]
+        d = fg.grad[sl].float() * g["grad_scale"]
         if g["weight_decay"] != 0:
             d = d + g["weight_decay"] * p
         if g["momentum"] != 0:
-            buf = self._buf(gi, "momentum_buffer")
+            buf = self._buf(gi, "momentum_buffer")[sl]
             if self._steps[gi] == 1:
                 buf.copy_(d)
             else:
                 buf.mul_(g["momentum"]).add_(d, alpha=1 - g["dampening"])
             d = d + g["momentum"] * buf if g["nesterov"] else buf
         p.add_(d, alpha=-g["lr"])
-        fg.sync_lowp_from_master()
+        _sync_lowp(fg, sl)
 
 
 class FusedAdam(_FusedFlatOptimizer):
@@ -199,22 +223,24 @@ class FusedAdam(_FusedFlatOptimizer):
         super().__init__(params, dict(lr=lr, betas=tuple(betas), eps=eps, weight_decay=weight_decay,
                                       adamw=adamw, grad_scale=grad_scale), grad_dtype)
 
-    def _step_gpu(self, gi, g, fg):
+    def _step_gpu(self, gi, g, fg, start=0, end=None):
+        end = fg.numel if end is None else end
         self._check(fg)
         m, v = self._buf(gi, "exp_avg"), self._buf(gi, "exp_avg_sq")
-        lp, lpdt = self._lowp_args(fg)
+        lp, lpdt = self._lowp_args(fg, start)
         b1, b2 = g["betas"]
-        N.hip().adam_step(fg.master.data_ptr(), fg.grad.data_ptr(), N.dtype_code(fg.grad.dtype), m.data_ptr(),
-                          v.data_ptr(), lp, lpdt, fg.numel, float(g["lr"]), float(b1), float(b2), float(g["eps"]),
-                          float(g["weight_decay"]), bool(g["adamw"]), self._steps[gi], float(g["grad_scale"]),
-                          self._step_t.data_ptr() + gi * 8, N.stream_of(fg.master))
+        N.hip().adam_step(self._at(fg.master, start), self._at(fg.grad, start), N.dtype_code(fg.grad.dtype),
+                          self._at(m, start), self._at(v, start), lp, lpdt, end - start, float(g["lr"]), float(b1),
+                          float(b2), float(g["eps"]), float(g["weight_decay"]), bool(g["adamw"]), self._steps[gi],
+                          float(g["grad_scale"]), self._step_t.data_ptr() + gi * 8, N.stream_of(fg.master))
 
-    def _step_cpu(self, gi, g, fg):
-        p = fg.master
-        m, v = self._buf(gi, "exp_avg"), self._buf(gi, "exp_avg_sq")
+    def _step_cpu(self, gi, g, fg, start=0, end=None):
+        sl = slice(start, fg.numel if end is None else end)
+        p = fg.master[sl]
+        m, v = self._buf(gi, "exp_avg")[sl], self._buf(gi, "exp_avg_sq")[sl]
         b1, b2 = g["betas"]
         t = self._steps[gi]
-        d = fg.grad.float() * g["grad_scale"]
+        d = fg.grad[sl].float() * g["grad_scale"]
         if g["adamw"]:
             p.mul_(1 - g["lr"] * g["weight_decay"])
         elif g["weight_decay"] != 0:
@@ -224,7 +250,7 @@ class FusedAdam(_FusedFlatOptimizer):
         bc1, bc2 = 1 - b1 ** t, 1 - b2 ** t
         denom = (v.sqrt() / math.sqrt(bc2)).add_(g["eps"])
         p.addcdiv_(m, denom, value=-g["lr"] / bc1)
-        fg.sync_lowp_from_master()
+        _sync_lowp(fg, sl)
 
 
 class FusedAdamW(FusedAdam):
@@ -250,37 +276,45 @@ class FusedRMSprop(_FusedFlatOptimizer):
             names.append("grad_avg")
         return tuple(names)
 
-    def _step_gpu(self, gi, g, fg):
+    def _step_gpu(self, gi, g, fg, start=0, end=None):
+        end = fg.numel if end is None else end
         self._check(fg)
         sq = self._buf(gi, "square_avg")
         buf = self._buf(gi, "momentum_buffer") if g["momentum"] > 0 else None
         ga = self._buf(gi, "grad_avg") if g["centered"] else None
-        lp, lpdt = self._lowp_args(fg)
-        N.hip().rmsprop_step(fg.master.data_ptr(), fg.grad.data_ptr(), N.dtype_code(fg.grad.dtype), sq.data_ptr(),
-                             N.ptr(buf), N.ptr(ga), lp, lpdt, fg.numel, float(g["lr"]), float(g["alpha"]),
-                             float(g["eps"]), float(g["weight_decay"]), float(g["momentum"]), bool(g["centered"]),
-                             float(g["grad_scale"]), N.stream_of(fg.master))
+        lp, lpdt = self._lowp_args(fg, start)
+        N.hip().rmsprop_step(self._at(fg.master, start), self._at(fg.grad, start), N.dtype_code(fg.grad.dtype),
+                             self._at(sq, start), self._at(buf, start), self._at(ga, start), lp, lpdt, end - start,
+                             float(g["lr"]), float(g["alpha"]), float(g["eps"]), float(g["weight_decay"]),
+                             float(g["momentum"]), bool(g["centered"]), float(g["grad_scale"]),
+                             N.stream_of(fg.master))
 
-    def _step_cpu(self, gi, g, fg):
-        p = fg.master
-        d = fg.grad.float() * g["grad_scale"]
+    def _step_cpu(self, gi, g, fg, start=0, end=None):
+        sl = slice(start, fg.numel if end is None else end)
+        p = fg.master[sl]
+        d = fg.grad[sl].float() * g["grad_scale"]
         if g["weight_decay"] != 0:
             d = d + g["weight_decay"] * p
-        sq = self._buf(gi, "square_avg")
+        sq = self._buf(gi, "square_avg")[sl]
         sq.mul_(g["alpha"]).addcmul_(d, d, value=1 - g["alpha"])
         if g["centered"]:
-            ga = self._buf(gi, "grad_avg")
+            ga = self._buf(gi, "grad_avg")[sl]
             ga.mul_(g["alpha"]).add_(d, alpha=1 - g["alpha"])
             avg = (sq - ga * ga).sqrt_().add_(g["eps"])
         else:
             avg = sq.sqrt().add_(g["eps"])
         if g["momentum"] > 0:
-            buf = self._buf(gi, "momentum_buffer")
+            buf = self._buf(gi, "momentum_buffer")[sl]
             buf.mul_(g["momentum"]).addcdiv_(d, avg)
             p.add_(buf, alpha=-g["lr"])
         else:
             p.addcdiv_(d, avg, value=-g["lr"])
-        fg.sync_lowp_from_master()
+        _sync_lowp(fg, sl)
+
+
+def _sync_lowp(fg: FlatGroup, sl: slice) -> None:
+    if fg.lowp is not None:
+        fg.lowp[sl].copy_(fg.master[sl])
 
 
 def make_optimizer(name: str, params, **kw) -> _FusedFlatOptimizer:

@@ -57,6 +57,7 @@ class Bucket:
     comm_buf: torch.Tensor | None = None
     segments: list[tuple[int, int]] | None = None   # per-parameter ranges, relative to start
     plan: AdasumPlan | None = None
+    opt_done: bool = False   # the optimizer update of this bucket ran this step
 
     @property
     def numel(self) -> int:
@@ -64,8 +65,20 @@ class Bucket:
 
 
 class ElasticDDP:
+    """Bucketed gradient all-reduce engine (see module docstring).
+
+    ``overlap_optimizer`` (opt-in; the trainer turns it on with a fused flat optimizer): the optimizer
+    update of a bucket's parameters runs on the comm stream right after the bucket's
+    all-reduce -- overlapping the remaining backward -- instead of one whole-model optimizer
+    pass after backward.  Safe because a bucket launches only after every gradient
+    contribution of its parameters, i.e. after every backward node that reads those weights
+    has been enqueued on the compute stream, which the comm stream waits for.  At world 1
+    the same per-bucket updates overlap backward with no collective.  With it on, finish a
+    step with ``step()`` (``finalize()`` alone also completes the updates already begun)."""
+
     def __init__(self, model: torch.nn.Module, comm: Communicator, optimizer=None, bucket_cap_mb: float = 64.0,
-                 first_bucket_mb: float = 8.0, compression: str | None = None, reduction: str = "average"):
+                 first_bucket_mb: float = 8.0, compression: str | None = None, reduction: str = "average",
+                 overlap_optimizer: bool = False):
         if reduction not in ("average", "adasum"):
             raise ValueError(f"unknown reduction {reduction!r} (average | adasum)")
         self.model = model
@@ -79,6 +92,8 @@ class ElasticDDP:
             params = [p for p in model.parameters() if p.requires_grad]
             self.groups = [FlatGroup(params, flatten_params=False)]
         self.device = self.groups[0].device
+        self.overlap_optimizer = bool(overlap_optimizer and optimizer is not None
+                                      and hasattr(optimizer, "step_range") and self.device.type == "cuda")
         self.bucket_cap_mb = bucket_cap_mb
         self.first_bucket_mb = first_bucket_mb
         self._build_buckets()
@@ -98,6 +113,7 @@ class ElasticDDP:
                     # signal readiness through this attribute instead of autograd's hook
                     p._voda_grad_ready = self._on_grad
         self._next = 0
+        self._opt_begun = False
         self.comm_stream = torch.cuda.Stream(self.device) if self.device.type == "cuda" else None
         if comm is not None and hasattr(comm, "stream") and self.comm_stream is not None:
             comm.stream = self.comm_stream
@@ -143,16 +159,26 @@ class ElasticDDP:
     def _reset(self) -> None:
         self._next = 0
         self._count = {}
+        self._opt_begun = False
         for b in self.buckets:
             if self._expect is None:
                 b.pending = sum(1 for p in b.params if p.requires_grad)
             else:
                 b.pending = sum(self._expect.get(id(p), 0) for p in b.params)
             b.launched = False
+            b.opt_done = False
 
     @property
     def calibrated(self) -> bool:
         return self._expect is not None
+
+    def _overlap_active(self) -> bool:
+        # never inside a hipGraph capture: the captured step runs the whole-model update
+        return self.overlap_optimizer and not torch.cuda.is_current_stream_capturing()
+
+    def _launching(self) -> bool:
+        """Do buckets launch during backward this step?"""
+        return self._sync and (self.world > 1 or self._overlap_active())
 
     # ------------------------------------------------------------------ hooks
     def _on_grad(self, p: torch.nn.Parameter) -> None:
@@ -161,7 +187,7 @@ class ElasticDDP:
         if self._expect is None:  # calibration step: count contributions, launch at finalize
             self._count[id(p)] = self._count.get(id(p), 0) + 1
             return
-        if self.world == 1:
+        if not self._launching():
             return
         b = self._param_bucket[id(p)]
         b.pending -= 1
@@ -173,28 +199,36 @@ class ElasticDDP:
             self._launch(self.buckets[self._next])
             self._next += 1
 
-    def _launch(self, b: Bucket) -> None:
+    def _launch(self, b: Bucket, apply_opt: bool = True) -> None:
         g = self.groups[b.group]
         flat = g.grad[b.start:b.end]
+        use_opt = apply_opt and self._overlap_active()
+        if use_opt and not self._opt_begun:
+            self.optimizer.begin_step()  # step counters, on the compute stream
+            self._opt_begun = True
         if self.comm_stream is not None:
             self.comm_stream.wait_stream(torch.cuda.current_stream(self.device))
             ctx = torch.cuda.stream(self.comm_stream)
         else:
             ctx = _nullctx()
         with ctx:
-            if self.reduction == "adasum":
-                if b.plan is None:
-                    b.plan = AdasumPlan(b.segments, flat.device)
-                gathered = self.comm.allgather(flat)          # [world, n]
-                flat.copy_(adasum_tree_(gathered, b.plan))
-            elif self.compress_dtype is not None and flat.dtype != self.compress_dtype:
-                if b.comm_buf is None:
-                    b.comm_buf = torch.empty(b.numel, dtype=self.compress_dtype, device=flat.device)
-                cast_scale_(flat, b.comm_buf, 1.0 / self.world)
-                self.comm.allreduce_(b.comm_buf, "sum")
-                cast_scale_(b.comm_buf, flat, 1.0)
-            else:
-                self.comm.allreduce_(flat, "avg")
+            if self.world > 1:
+                if self.reduction == "adasum":
+                    if b.plan is None:
+                        b.plan = AdasumPlan(b.segments, flat.device)
+                    gathered = self.comm.allgather(flat)          # [world, n]
+                    flat.copy_(adasum_tree_(gathered, b.plan))
+                elif self.compress_dtype is not None and flat.dtype != self.compress_dtype:
+                    if b.comm_buf is None:
+                        b.comm_buf = torch.empty(b.numel, dtype=self.compress_dtype, device=flat.device)
+                    cast_scale_(flat, b.comm_buf, 1.0 / self.world)
+                    self.comm.allreduce_(b.comm_buf, "sum")
+                    cast_scale_(b.comm_buf, flat, 1.0)
+                else:
+                    self.comm.allreduce_(flat, "avg")
+            if use_opt:
+                self.optimizer.step_range(b.group, b.start, b.end)
+                b.opt_done = True
         b.launched = True
 
     # ------------------------------------------------------------------ API
@@ -213,8 +247,9 @@ class ElasticDDP:
         finally:
             self._sync = old
 
-    def finalize(self) -> None:
-        """Flush remaining buckets in order and order the compute stream after them."""
+    def _flush(self, apply_opt: bool) -> None:
+        """Calibration bookkeeping + launch every bucket not yet launched, then order the
+        compute stream after the comm stream."""
         if self._sync and self._expect is None and self._count:
             self._expect = dict(self._count)  # calibration step done: every bucket launches below
         elif self._sync and self.world > 1:
@@ -222,13 +257,25 @@ class ElasticDDP:
             if bad:
                 log.error("buckets %s received more gradient contributions than in the calibration step "
                           "(dynamic graph?): their all-reduce may have started early", bad)
-        if self._sync and self.world > 1:
+        if self._sync and (self.world > 1 or (apply_opt and self._overlap_active())):
             while self._next < len(self.buckets):
-                self._launch(self.buckets[self._next])
+                self._launch(self.buckets[self._next], apply_opt)
                 self._next += 1
             if self.comm_stream is not None:
                 torch.cuda.current_stream(self.device).wait_stream(self.comm_stream)
+
+    def finalize(self) -> None:
+        """Flush remaining buckets (gradients only) and order the compute stream after them."""
+        self._flush(apply_opt=False)
+        if self._opt_begun:  # some buckets already applied their update: finish the rest
+            self._apply_remaining_updates()
         self._reset()
+
+    def _apply_remaining_updates(self) -> None:
+        for b in self.buckets:
+            if not b.opt_done:
+                self.optimizer.step_range(b.group, b.start, b.end)
+                b.opt_done = True
 
     def allreduce_gradients(self) -> None:
         """Synchronous all-reduce of all gradients (no overlap); for debugging/tests."""
@@ -239,13 +286,25 @@ class ElasticDDP:
 
     def _launch_ready_all(self) -> None:
         while self._next < len(self.buckets):
-            self._launch(self.buckets[self._next])
+            self._launch(self.buckets[self._next], apply_opt=False)
             self._next += 1
 
     def step(self) -> None:
+        """Finish the step: all-reduce what is left and apply the optimizer update (per
+        bucket on the comm stream when overlapping, else one whole-model pass)."""
+        if self.optimizer is None:
+            self.finalize()
+            return
+        if self._sync and self._overlap_active():
+            self._flush(apply_opt=True)
+            if not self._opt_begun:
+                self.optimizer.begin_step()
+                self._opt_begun = True
+            self._apply_remaining_updates()
+            self._reset()
+            return
         self.finalize()
-        if self.optimizer is not None:
-            self.optimizer.step()
+        self.optimizer.step()
 
     def zero_grad(self) -> None:
         for g in self.groups:

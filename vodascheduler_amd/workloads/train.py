@@ -50,6 +50,7 @@ class TrainConfig:
     # as Horovod reduces fp32 unless --fp16-allreduce) | bf16 (opt-in low-precision gradients)
     grad_dtype: str = "fp32"
     bucket_cap_mb: float = 64.0
+    overlap_optimizer: bool = True     # per-bucket optimizer updates on the comm stream, overlapping backward
     reduction: str = "average"         # average | adasum (Horovod op=hvd.Adasum; LR not scaled by world)
     metrics_dir: str | None = None
     checkpoint_every_epoch: bool = False
@@ -92,7 +93,8 @@ class _Warm:
                 b = tuple(t.to(memory_format=torch.channels_last) if t.dim() == 4 else t for t in b)
             self.pool.append(b)
         self.ddp = ElasticDDP(self.model, None, self.opt, bucket_cap_mb=cfg.bucket_cap_mb,
-                              compression=cfg.compression, reduction=cfg.reduction)
+                              compression=cfg.compression, reduction=cfg.reduction,
+                              overlap_optimizer=cfg.overlap_optimizer)
         self._init = [t.detach().clone() for t in self._tensors()]
 
     def _tensors(self):
@@ -114,7 +116,7 @@ WARM_CACHE_MAX = 4
 
 def _warm_key(cfg: TrainConfig, device: torch.device) -> tuple:
     return (cfg.model, cfg.per_gpu_batch, cfg.lr, cfg.compression, cfg.bucket_cap_mb, cfg.reduction, cfg.seed,
-            cfg.grad_dtype, str(device))
+            cfg.grad_dtype, cfg.overlap_optimizer, str(device))
 
 
 def get_warm(cfg: TrainConfig, device: torch.device, use_cache: bool = True) -> _Warm:
@@ -280,7 +282,7 @@ def replay_reference(cfg: TrainConfig, world_log: list[int], total_steps: int, d
             b = tuple(t.to(memory_format=torch.channels_last) if t.dim() == 4 else t for t in b)
         pool.append(b)
     ddp = ElasticDDP(model, None, opt, bucket_cap_mb=cfg.bucket_cap_mb, compression=cfg.compression,
-                     reduction=cfg.reduction)
+                     reduction=cfg.reduction, overlap_optimizer=cfg.overlap_optimizer)
     segs = [(world_log[i], world_log[i + 1]) for i in range(0, len(world_log), 2)]
 
     def world_at(step: int) -> int:
