@@ -5,10 +5,12 @@
 //   O = softmax(scale * Q K^T + mask) V      mask: key padding (-1e9, the reference's additive
 //                                            mask), causal (-1e9), keys >= Tk (-inf)
 //
-// One workgroup = 4 waves = 128 rows of one (batch, head); K/V (forward, dQ pass) or Q/dO
-// (dK/dV pass) of the whole (b, h) sequence are staged ONCE in LDS, so the kernels are
-// restricted to Tq, Tk <= 128 (longer sequences take the materialised path: hipBLASLt
-// GEMMs + the HIP masked-softmax kernel).  All products are v_mfma_f32_32x32x16_bf16 tiles
+// One workgroup = W waves (1, 2 or 4, from the row count: a T = 20 sequence of the reference
+// NMT Transformer gets ONE wave, not a 128-row block that is 84 % padding) = 32 W rows of
+// one (batch, head).  The other operand streams through LDS in tiles of 32 rows
+// (flash-attention style, online softmax in the forward), so the sequence length is bounded
+// only by ``kMaxT`` (BERT at seq 512) and the head dim by registers: D = 32 / 64 / 128 / 256
+// (the reference Transformer's key_dim = 256).  All products are v_mfma_f32_32x32x16_bf16 tiles
 // (lane l, r = l & 31, h = l >> 5: A[r][8h+j], B[8h+j][r]; C/D col = r,
 // row = (reg&3) + 8*(reg>>2) + 4h), arranged so that no accumulator has to cross lanes:
 //
@@ -25,7 +27,9 @@
 //
 // Nothing is materialised in HBM except O, the log-sum-exp per row and delta per row; the
 // q/k/v/o/dq/dk/dv tensors are addressed through (batch, head, row) strides, so packed
-// [B, T, 3, H, D] projections are read and their gradients written in place.
+// [B, T, 3, H, D] projections are read and their gradients written in place.  For D = 256
+// the dK/dV pass runs twice (dV, then dK) so each pass keeps only one 256-wide accumulator
+// set (8 x 16 fp32 registers per lane) next to the two operand fragment sets.
 #include "common.h"
 #include "ops.h"
 
@@ -37,9 +41,8 @@ typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 
-constexpr int kWaves = 4;
-constexpr int kRows = 32 * kWaves;     // rows per workgroup
-constexpr int kMaxT = 128;             // max staged sequence length
+constexpr int kTile = 32;              // rows of the streamed operand per LDS stage
+constexpr int kMaxT = 4096;            // max sequence length (host check)
 constexpr float kMaskNeg = -1e9f;      // reference additive mask value
 constexpr float kNegInf = -__builtin_huge_valf();
 
@@ -95,16 +98,16 @@ __device__ __forceinline__ bf16x8 perm_frag(const uint16_t* rowT, int s, int h) 
   return __builtin_bit_cast(bf16x8, make_uint4(lo.x, lo.y, hi.x, hi.y));
 }
 
-// Stage rows [0, T) of a (b, h) slice (row stride st, D contiguous) into LDS row-major
-// [Tpad][D + PAD] and optionally transposed [D][Tpad + PADT]; rows >= T are zero.
+// Stage rows [t0, t0 + kTile) of a (b, h) slice (row stride st, D contiguous) into LDS
+// row-major [kTile][D + PAD] and optionally transposed [D][kTile + PADT]; rows >= T are zero.
 template <int D, bool ROWS, bool TRANS>
-__device__ __forceinline__ void stage(const uint16_t* __restrict__ g, int64_t st, int T, int Tpad, uint16_t* rows,
-                                      int rstride, uint16_t* trans, int tstride) {
+__device__ __forceinline__ void stage_tile(const uint16_t* __restrict__ g, int64_t st, int t0, int T, uint16_t* rows,
+                                           int rstride, uint16_t* trans, int tstride) {
   constexpr int VPR = D / 8;  // 16-byte vectors per row
-  for (int i = threadIdx.x; i < Tpad * VPR; i += blockDim.x) {
+  for (int i = threadIdx.x; i < kTile * VPR; i += blockDim.x) {
     const int r = i / VPR, c = (i % VPR) * 8;
     uint4 u = make_uint4(0, 0, 0, 0);
-    if (r < T) u = *reinterpret_cast<const uint4*>(g + int64_t(r) * st + c);
+    if (t0 + r < T) u = *reinterpret_cast<const uint4*>(g + int64_t(t0 + r) * st + c);
     if constexpr (ROWS) *reinterpret_cast<uint4*>(rows + r * rstride + c) = u;
     if constexpr (TRANS) {
       const uint32_t w[4] = {u.x, u.y, u.z, u.w};
@@ -141,37 +144,39 @@ __device__ __forceinline__ void store_lane_rows(uint16_t* __restrict__ out, int6
 }
 
 // ======================================================================== forward
-template <int D>
-__global__ __launch_bounds__(256) void attn_fwd_kernel(AttnArgs a) {
+template <int D, int W>
+__global__ __launch_bounds__(64 * W) void attn_fwd_kernel(AttnArgs a) {
   constexpr int KS = D / 16;           // k-steps over the head dim
   constexpr int DT = D / 32;           // 32-wide output tiles over the head dim
   constexpr int RS = D + 8;            // LDS row stride (elements)
-  constexpr int TS = kMaxT + 8;        // transposed row stride
-  __shared__ __attribute__((aligned(16))) uint16_t Ks[kMaxT * RS];
+  constexpr int TS = kTile + 8;        // transposed row stride
+  __shared__ __attribute__((aligned(16))) uint16_t Ks[kTile * RS];
   __shared__ __attribute__((aligned(16))) uint16_t Vt[D * TS];
 
   const int bh = blockIdx.y, b = bh / a.H, hh = bh % a.H;
-  const int Tkp = (a.Tk + 31) & ~31;
-  stage<D, true, false>(a.k + b * a.k_sb + hh * a.k_sh, a.k_st, a.Tk, Tkp, Ks, RS, nullptr, 0);
-  stage<D, false, true>(a.v + b * a.v_sb + hh * a.v_sh, a.v_st, a.Tk, Tkp, nullptr, 0, Vt, TS);
+  const uint16_t* kb = a.k + b * a.k_sb + hh * a.k_sh;
+  const uint16_t* vb = a.v + b * a.v_sb + hh * a.v_sh;
 
   const int lane = threadIdx.x & 63, r = lane & 31, h = lane >> 5, w = threadIdx.x >> 6;
-  const int q = blockIdx.x * kRows + w * 32 + r;  // this lane's query
+  const int q = blockIdx.x * (32 * W) + w * 32 + r;  // this lane's query
   const uint16_t* qrow = a.q + b * a.q_sb + hh * a.q_sh + int64_t(q) * a.q_st;
   bf16x8 qf[KS];
 #pragma unroll
   for (int s = 0; s < KS; ++s) qf[s] = q < a.Tq ? ld16(qrow + 16 * s + 8 * h) : zero_bf8();
   const uint8_t* mrow = a.mask != nullptr ? a.mask + b * a.mask_sb : nullptr;
-  __syncthreads();
 
   f32x16 o[DT];
 #pragma unroll
   for (int t = 0; t < DT; ++t) o[t] = zero16();
   float m = -1e30f, l = 0.f;
-  for (int kt = 0; kt < Tkp; kt += 32) {
+  for (int kt = 0; kt < a.Tk; kt += kTile) {
+    __syncthreads();  // every wave is done with the previous tile
+    stage_tile<D, true, false>(kb, a.k_st, kt, a.Tk, Ks, RS, nullptr, 0);
+    stage_tile<D, false, true>(vb, a.v_st, kt, a.Tk, nullptr, 0, Vt, TS);
+    __syncthreads();
     f32x16 s_acc = zero16();
 #pragma unroll
-    for (int s = 0; s < KS; ++s) s_acc = mfma(ld16(Ks + (kt + r) * RS + 16 * s + 8 * h), qf[s], s_acc);
+    for (int s = 0; s < KS; ++s) s_acc = mfma(ld16(Ks + r * RS + 16 * s + 8 * h), qf[s], s_acc);
     float tmax = -1e30f;
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
@@ -199,7 +204,7 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(AttnArgs a) {
     const bf16x8 p0 = acc_frag(s_acc, 0), p1 = acc_frag(s_acc, 1);
 #pragma unroll
     for (int t = 0; t < DT; ++t) {
-      const uint16_t* vrow = Vt + (32 * t + r) * TS + kt;
+      const uint16_t* vrow = Vt + (32 * t + r) * TS;
       o[t] = mfma(perm_frag(vrow, 0, h), p0, o[t]);
       o[t] = mfma(perm_frag(vrow, 1, h), p1, o[t]);
     }
@@ -212,20 +217,19 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(AttnArgs a) {
 }
 
 // ======================================================================== backward: dQ (+ delta)
-template <int D>
-__global__ __launch_bounds__(256) void attn_bwd_dq_kernel(AttnArgs a) {
-  constexpr int KS = D / 16, DT = D / 32, RS = D + 8, TS = kMaxT + 8;
-  __shared__ __attribute__((aligned(16))) uint16_t Ks[kMaxT * RS];
-  __shared__ __attribute__((aligned(16))) uint16_t Vs[kMaxT * RS];
+template <int D, int W>
+__global__ __launch_bounds__(64 * W) void attn_bwd_dq_kernel(AttnArgs a) {
+  constexpr int KS = D / 16, DT = D / 32, RS = D + 8, TS = kTile + 8;
+  __shared__ __attribute__((aligned(16))) uint16_t Ks[kTile * RS];
+  __shared__ __attribute__((aligned(16))) uint16_t Vs[kTile * RS];
   __shared__ __attribute__((aligned(16))) uint16_t Kt[D * TS];
 
   const int bh = blockIdx.y, b = bh / a.H, hh = bh % a.H;
-  const int Tkp = (a.Tk + 31) & ~31;
-  stage<D, true, true>(a.k + b * a.k_sb + hh * a.k_sh, a.k_st, a.Tk, Tkp, Ks, RS, Kt, TS);
-  stage<D, true, false>(a.v + b * a.v_sb + hh * a.v_sh, a.v_st, a.Tk, Tkp, Vs, RS, nullptr, 0);
+  const uint16_t* kb = a.k + b * a.k_sb + hh * a.k_sh;
+  const uint16_t* vb = a.v + b * a.v_sb + hh * a.v_sh;
 
   const int lane = threadIdx.x & 63, r = lane & 31, h = lane >> 5, w = threadIdx.x >> 6;
-  const int q = blockIdx.x * kRows + w * 32 + r;
+  const int q = blockIdx.x * (32 * W) + w * 32 + r;
   const bool qv = q < a.Tq;
   const uint16_t* qrow = a.q + b * a.q_sb + hh * a.q_sh + int64_t(q) * a.q_st;
   const uint16_t* dorow = a.dout + b * a.do_sb + hh * a.do_sh + int64_t(q) * a.do_st;
@@ -244,17 +248,20 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(AttnArgs a) {
   const float lse = qv ? a.lse[int64_t(bh) * a.Tq + q] : 0.f;
   if (h == 0 && qv) a.delta[int64_t(bh) * a.Tq + q] = delta;
   const uint8_t* mrow = a.mask != nullptr ? a.mask + b * a.mask_sb : nullptr;
-  __syncthreads();
 
   f32x16 dq[DT];
 #pragma unroll
   for (int t = 0; t < DT; ++t) dq[t] = zero16();
-  for (int kt = 0; kt < Tkp; kt += 32) {
+  for (int kt = 0; kt < a.Tk; kt += kTile) {
+    __syncthreads();
+    stage_tile<D, true, true>(kb, a.k_st, kt, a.Tk, Ks, RS, Kt, TS);
+    stage_tile<D, true, false>(vb, a.v_st, kt, a.Tk, Vs, RS, nullptr, 0);
+    __syncthreads();
     f32x16 s_acc = zero16(), dp = zero16();
 #pragma unroll
     for (int s = 0; s < KS; ++s) {
-      s_acc = mfma(ld16(Ks + (kt + r) * RS + 16 * s + 8 * h), qf[s], s_acc);
-      dp = mfma(ld16(Vs + (kt + r) * RS + 16 * s + 8 * h), dof[s], dp);
+      s_acc = mfma(ld16(Ks + r * RS + 16 * s + 8 * h), qf[s], s_acc);
+      dp = mfma(ld16(Vs + r * RS + 16 * s + 8 * h), dof[s], dp);
     }
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
@@ -264,7 +271,7 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(AttnArgs a) {
     const bf16x8 d0 = acc_frag(s_acc, 0), d1 = acc_frag(s_acc, 1);
 #pragma unroll
     for (int t = 0; t < DT; ++t) {
-      const uint16_t* krow = Kt + (32 * t + r) * TS + kt;
+      const uint16_t* krow = Kt + (32 * t + r) * TS;
       dq[t] = mfma(perm_frag(krow, 0, h), d0, dq[t]);
       dq[t] = mfma(perm_frag(krow, 1, h), d1, dq[t]);
     }
@@ -275,74 +282,93 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(AttnArgs a) {
 }
 
 // ======================================================================== backward: dK, dV
-template <int D>
-__global__ __launch_bounds__(256) void attn_bwd_dkv_kernel(AttnArgs a) {
-  constexpr int KS = D / 16, DT = D / 32, RS = D + 8, TS = kMaxT + 8;
-  __shared__ __attribute__((aligned(16))) uint16_t Qs[kMaxT * RS];
-  __shared__ __attribute__((aligned(16))) uint16_t Qt[D * TS];
-  __shared__ __attribute__((aligned(16))) uint16_t Ds[kMaxT * RS];
-  __shared__ __attribute__((aligned(16))) uint16_t Dt[D * TS];
-  __shared__ float lse_s[kMaxT], del_s[kMaxT];
+// MODE 0: dK and dV; 1: dV only; 2: dK only (D = 256 runs 1 then 2: one accumulator set each)
+template <int D, int W, int MODE>
+__global__ __launch_bounds__(64 * W) void attn_bwd_dkv_kernel(AttnArgs a) {
+  constexpr int KS = D / 16, DT = D / 32, RS = D + 8, TS = kTile + 8;
+  constexpr bool DO_DV = MODE != 2, DO_DK = MODE != 1;
+  __shared__ __attribute__((aligned(16))) uint16_t Qs[kTile * RS];
+  __shared__ __attribute__((aligned(16))) uint16_t Qt[DO_DK ? D * TS : 8];
+  __shared__ __attribute__((aligned(16))) uint16_t Ds[DO_DK ? kTile * RS : 8];
+  __shared__ __attribute__((aligned(16))) uint16_t Dt[DO_DV ? D * TS : 8];
+  __shared__ float lse_s[kTile], del_s[kTile];
 
   const int bh = blockIdx.y, b = bh / a.H, hh = bh % a.H;
-  const int Tqp = (a.Tq + 31) & ~31;
-  stage<D, true, true>(a.q + b * a.q_sb + hh * a.q_sh, a.q_st, a.Tq, Tqp, Qs, RS, Qt, TS);
-  stage<D, true, true>(a.dout + b * a.do_sb + hh * a.do_sh, a.do_st, a.Tq, Tqp, Ds, RS, Dt, TS);
-  for (int i = threadIdx.x; i < Tqp; i += blockDim.x) {
-    const bool ok = i < a.Tq;
-    lse_s[i] = ok ? a.lse[int64_t(bh) * a.Tq + i] : __builtin_huge_valf();  // pad rows: P = 0
-    del_s[i] = ok ? a.delta[int64_t(bh) * a.Tq + i] : 0.f;
-  }
+  const uint16_t* qb = a.q + b * a.q_sb + hh * a.q_sh;
+  const uint16_t* db = a.dout + b * a.do_sb + hh * a.do_sh;
 
   const int lane = threadIdx.x & 63, r = lane & 31, h = lane >> 5, w = threadIdx.x >> 6;
-  const int key = blockIdx.x * kRows + w * 32 + r;
+  const int key = blockIdx.x * (32 * W) + w * 32 + r;
   const bool kv = key < a.Tk;
   const uint16_t* krow = a.k + b * a.k_sb + hh * a.k_sh + int64_t(key) * a.k_st;
   const uint16_t* vrow = a.v + b * a.v_sb + hh * a.v_sh + int64_t(key) * a.v_st;
-  bf16x8 kf[KS], vf[KS];
+  bf16x8 kf[KS], vf[DO_DK ? KS : 1];
 #pragma unroll
-  for (int s = 0; s < KS; ++s) {
-    kf[s] = kv ? ld16(krow + 16 * s + 8 * h) : zero_bf8();
-    vf[s] = kv ? ld16(vrow + 16 * s + 8 * h) : zero_bf8();
+  for (int s = 0; s < KS; ++s) kf[s] = kv ? ld16(krow + 16 * s + 8 * h) : zero_bf8();
+  if constexpr (DO_DK) {
+#pragma unroll
+    for (int s = 0; s < KS; ++s) vf[s] = kv ? ld16(vrow + 16 * s + 8 * h) : zero_bf8();
   }
   const uint8_t* mrow = a.mask != nullptr ? a.mask + b * a.mask_sb : nullptr;
   const bool kmasked = !kv ? true : (mrow != nullptr && mrow[key] == 0);
-  __syncthreads();
 
-  f32x16 dk[DT], dv[DT];
+  f32x16 dk[DO_DK ? DT : 1], dv[DO_DV ? DT : 1];
+  if constexpr (DO_DK) {
 #pragma unroll
-  for (int t = 0; t < DT; ++t) { dk[t] = zero16(); dv[t] = zero16(); }
-  for (int qt = 0; qt < Tqp; qt += 32) {
+    for (int t = 0; t < DT; ++t) dk[t] = zero16();
+  }
+  if constexpr (DO_DV) {
+#pragma unroll
+    for (int t = 0; t < DT; ++t) dv[t] = zero16();
+  }
+  for (int qt = 0; qt < a.Tq; qt += kTile) {
+    __syncthreads();
+    stage_tile<D, true, DO_DK>(qb, a.q_st, qt, a.Tq, Qs, RS, Qt, TS);
+    if constexpr (DO_DK) stage_tile<D, true, DO_DV>(db, a.do_st, qt, a.Tq, Ds, RS, Dt, TS);
+    else stage_tile<D, false, true>(db, a.do_st, qt, a.Tq, nullptr, 0, Dt, TS);
+    for (int i = threadIdx.x; i < kTile; i += blockDim.x) {
+      const bool ok = qt + i < a.Tq;
+      lse_s[i] = ok ? a.lse[int64_t(bh) * a.Tq + qt + i] : __builtin_huge_valf();  // pad rows: P = 0
+      del_s[i] = ok ? a.delta[int64_t(bh) * a.Tq + qt + i] : 0.f;
+    }
+    __syncthreads();
     f32x16 s_acc = zero16(), dp = zero16();
 #pragma unroll
     for (int s = 0; s < KS; ++s) {
-      s_acc = mfma(ld16(Qs + (qt + r) * RS + 16 * s + 8 * h), kf[s], s_acc);  // S[query][key]
-      dp = mfma(ld16(Ds + (qt + r) * RS + 16 * s + 8 * h), vf[s], dp);      // dP[query][key]
+      s_acc = mfma(ld16(Qs + r * RS + 16 * s + 8 * h), kf[s], s_acc);             // S[query][key]
+      if constexpr (DO_DK) dp = mfma(ld16(Ds + r * RS + 16 * s + 8 * h), vf[s], dp);  // dP[query][key]
     }
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
-      const int qq = qt + crow(i, h);
+      const int ql = crow(i, h);
       float add = 0.f;
       if (!kv) add = kNegInf;
-      else if (kmasked || (a.causal && key > qq)) add = kMaskNeg;
-      const float p = __expf(s_acc[i] * a.scale + add - lse_s[qq]);
-      s_acc[i] = p;                        // P
-      dp[i] = p * (dp[i] - del_s[qq]);      // dS
+      else if (kmasked || (a.causal && key > qt + ql)) add = kMaskNeg;
+      const float p = __expf(s_acc[i] * a.scale + add - lse_s[ql]);
+      s_acc[i] = p;                                      // P
+      if constexpr (DO_DK) dp[i] = p * (dp[i] - del_s[ql]);  // dS
     }
-    const bf16x8 p0 = acc_frag(s_acc, 0), p1 = acc_frag(s_acc, 1);
-    const bf16x8 g0 = acc_frag(dp, 0), g1 = acc_frag(dp, 1);
+    if constexpr (DO_DV) {
+      const bf16x8 p0 = acc_frag(s_acc, 0), p1 = acc_frag(s_acc, 1);
 #pragma unroll
-    for (int t = 0; t < DT; ++t) {
-      const uint16_t* drow = Dt + (32 * t + r) * TS + qt;  // dO^T row (d = 32t + r)
-      const uint16_t* qrow = Qt + (32 * t + r) * TS + qt;  // Q^T row
-      dv[t] = mfma(p0, perm_frag(drow, 0, h), dv[t]);
-      dv[t] = mfma(p1, perm_frag(drow, 1, h), dv[t]);
-      dk[t] = mfma(g0, perm_frag(qrow, 0, h), dk[t]);
-      dk[t] = mfma(g1, perm_frag(qrow, 1, h), dk[t]);
+      for (int t = 0; t < DT; ++t) {
+        const uint16_t* drow = Dt + (32 * t + r) * TS;  // dO^T row (d = 32t + r)
+        dv[t] = mfma(p0, perm_frag(drow, 0, h), dv[t]);
+        dv[t] = mfma(p1, perm_frag(drow, 1, h), dv[t]);
+      }
+    }
+    if constexpr (DO_DK) {
+      const bf16x8 g0 = acc_frag(dp, 0), g1 = acc_frag(dp, 1);
+#pragma unroll
+      for (int t = 0; t < DT; ++t) {
+        const uint16_t* qrow = Qt + (32 * t + r) * TS;  // Q^T row
+        dk[t] = mfma(g0, perm_frag(qrow, 0, h), dk[t]);
+        dk[t] = mfma(g1, perm_frag(qrow, 1, h), dk[t]);
+      }
     }
   }
   // dv[t] / dk[t]: lane = d (32t + r), regs = keys (block-local crow)
-  const int key0 = blockIdx.x * kRows + w * 32;
+  const int key0 = blockIdx.x * (32 * W) + w * 32;
   uint16_t* dkb = a.dk + b * a.dk_sb + hh * a.dk_sh;
   uint16_t* dvb = a.dv + b * a.dv_sb + hh * a.dv_sh;
 #pragma unroll
@@ -351,8 +377,8 @@ __global__ __launch_bounds__(256) void attn_bwd_dkv_kernel(AttnArgs a) {
     for (int i = 0; i < 16; ++i) {
       const int kk = key0 + crow(i, h);
       if (kk < a.Tk) {
-        dkb[int64_t(kk) * a.dk_st + 32 * t + r] = f2bf(dk[t][i] * a.scale);
-        dvb[int64_t(kk) * a.dv_st + 32 * t + r] = f2bf(dv[t][i]);
+        if constexpr (DO_DK) dkb[int64_t(kk) * a.dk_st + 32 * t + r] = f2bf(dk[t][i] * a.scale);
+        if constexpr (DO_DV) dvb[int64_t(kk) * a.dv_st + 32 * t + r] = f2bf(dv[t][i]);
       }
     }
 }
@@ -362,7 +388,16 @@ void dispatch_d(int D, F&& f) {
   if (D == 32) f(std::integral_constant<int, 32>{});
   else if (D == 64) f(std::integral_constant<int, 64>{});
   else if (D == 128) f(std::integral_constant<int, 128>{});
+  else if (D == 256) f(std::integral_constant<int, 256>{});
   else throw std::invalid_argument("attention: unsupported head dim");
+}
+
+// waves per workgroup from the number of rows the workgroup's lanes own
+template <typename F>
+void dispatch_w(int rows, F&& f) {
+  if (rows <= 32) f(std::integral_constant<int, 1>{});
+  else if (rows <= 64) f(std::integral_constant<int, 2>{});
+  else f(std::integral_constant<int, 4>{});
 }
 
 AttnArgs make_args(const std::vector<int64_t>& t, int B, int H, int Tq, int Tk, float scale, bool causal) {
@@ -388,17 +423,22 @@ AttnArgs make_args(const std::vector<int64_t>& t, int B, int H, int Tq, int Tk, 
 }  // namespace
 
 bool attention_supported(int D, int Tq, int Tk, int dt) {
-  return dt == kBF16 && (D == 32 || D == 64 || D == 128) && Tq >= 1 && Tk >= 1 && Tq <= kMaxT && Tk <= kMaxT;
+  return dt == kBF16 && (D == 32 || D == 64 || D == 128 || D == 256) && Tq >= 1 && Tk >= 1 && Tq <= kMaxT &&
+         Tk <= kMaxT;
 }
 
 void attention_fwd(const std::vector<int64_t>& t, int B, int H, int Tq, int Tk, int D, float scale, bool causal,
                    uintptr_t stream) {
   VODA_CHECK(t.size() == 36, "attention_fwd: bad argument vector");
   VODA_CHECK(attention_supported(D, Tq, Tk, kBF16), "attention_fwd: unsupported shape");
+  VODA_CHECK(int64_t(B) * H <= 65535, "attention_fwd: B*H exceeds the grid's y dimension");
   const AttnArgs a = make_args(t, B, H, Tq, Tk, scale, causal);
-  const dim3 grid((Tq + kRows - 1) / kRows, unsigned(B * H));
   dispatch_d(D, [&](auto dc) {
-    hipLaunchKernelGGL((attn_fwd_kernel<decltype(dc)::value>), grid, dim3(256), 0, as_stream(stream), a);
+    dispatch_w(Tq, [&](auto wc) {
+      constexpr int DD = decltype(dc)::value, WW = decltype(wc)::value;
+      const dim3 grid((Tq + 32 * WW - 1) / (32 * WW), unsigned(B * H));
+      hipLaunchKernelGGL((attn_fwd_kernel<DD, WW>), grid, dim3(64 * WW), 0, as_stream(stream), a);
+    });
   });
   check_launch();
 }
@@ -407,13 +447,26 @@ void attention_bwd(const std::vector<int64_t>& t, int B, int H, int Tq, int Tk, 
                    uintptr_t stream) {
   VODA_CHECK(t.size() == 36, "attention_bwd: bad argument vector");
   VODA_CHECK(attention_supported(D, Tq, Tk, kBF16), "attention_bwd: unsupported shape");
+  VODA_CHECK(int64_t(B) * H <= 65535, "attention_bwd: B*H exceeds the grid's y dimension");
   const AttnArgs a = make_args(t, B, H, Tq, Tk, scale, causal);
+  hipStream_t s = as_stream(stream);
   dispatch_d(D, [&](auto dc) {
     constexpr int DD = decltype(dc)::value;
-    hipLaunchKernelGGL((attn_bwd_dq_kernel<DD>), dim3((Tq + kRows - 1) / kRows, unsigned(B * H)), dim3(256), 0,
-                       as_stream(stream), a);
-    hipLaunchKernelGGL((attn_bwd_dkv_kernel<DD>), dim3((Tk + kRows - 1) / kRows, unsigned(B * H)), dim3(256), 0,
-                       as_stream(stream), a);
+    dispatch_w(Tq, [&](auto wc) {
+      constexpr int WW = decltype(wc)::value;
+      hipLaunchKernelGGL((attn_bwd_dq_kernel<DD, WW>), dim3((Tq + 32 * WW - 1) / (32 * WW), unsigned(B * H)),
+                         dim3(64 * WW), 0, s, a);
+    });
+    dispatch_w(Tk, [&](auto wc) {
+      constexpr int WW = decltype(wc)::value;
+      const dim3 grid((Tk + 32 * WW - 1) / (32 * WW), unsigned(B * H));
+      if constexpr (DD == 256) {
+        hipLaunchKernelGGL((attn_bwd_dkv_kernel<DD, WW, 1>), grid, dim3(64 * WW), 0, s, a);
+        hipLaunchKernelGGL((attn_bwd_dkv_kernel<DD, WW, 2>), grid, dim3(64 * WW), 0, s, a);
+      } else {
+        hipLaunchKernelGGL((attn_bwd_dkv_kernel<DD, WW, 0>), grid, dim3(64 * WW), 0, s, a);
+      }
+    });
   });
   check_launch();
 }

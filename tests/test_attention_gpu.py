@@ -30,7 +30,10 @@ def _mask(B, Tk, dev, full_masked_row=False):
     return m
 
 
-@pytest.mark.parametrize("B,H,T,D", [(4, 12, 128, 64), (3, 8, 20, 32), (2, 4, 77, 128), (2, 2, 33, 64)])
+@pytest.mark.parametrize("B,H,T,D", [(4, 12, 128, 64), (3, 8, 20, 32), (2, 4, 77, 128), (2, 2, 33, 64),
+                                     # reference NMT shape (T = 20, key_dim = 256), BERT at seq 512,
+                                     # a long odd length on 4-wave blocks, D = 256 over several tiles
+                                     (16, 8, 20, 256), (2, 12, 512, 64), (2, 2, 200, 128), (2, 2, 70, 256)])
 @pytest.mark.parametrize("causal", [False, True])
 @pytest.mark.parametrize("masked", [False, True])
 def test_qkvpacked_fwd_bwd(B, H, T, D, causal, masked):
@@ -52,7 +55,8 @@ def test_qkvpacked_fwd_bwd(B, H, T, D, causal, masked):
     torch.testing.assert_close(qkv.grad.float(), x.grad, atol=5e-2, rtol=5e-2)
 
 
-@pytest.mark.parametrize("Tq,Tk,D", [(20, 20, 64), (17, 45, 32), (128, 96, 64), (64, 128, 128)])
+@pytest.mark.parametrize("Tq,Tk,D", [(20, 20, 64), (17, 45, 32), (128, 96, 64), (64, 128, 128), (20, 20, 256),
+                                     (300, 129, 64), (40, 513, 128)])
 def test_cross_attention_q_kvpacked(Tq, Tk, D):
     torch.manual_seed(1)
     dev, B, H = "cuda", 3, 4
@@ -93,8 +97,9 @@ def test_generic_entry_and_fallback_agree():
 
     b = materialized_attention(q, k, v, km, True, 64 ** -0.5)
     torch.testing.assert_close(a.float(), b.float(), atol=2e-2, rtol=2e-2)
-    # unsupported (long) sequence takes the materialised path
-    assert not flash.supported(64, 256, 256, torch.bfloat16)
+    # long sequences and head dim 256 are on the fused path now; other head dims are not
+    assert flash.supported(64, 512, 512, torch.bfloat16) and flash.supported(256, 20, 20, torch.bfloat16)
+    assert not flash.supported(96, 64, 64, torch.bfloat16)
 
 
 def test_bert_layer_uses_fused_attention_kernel():
@@ -111,6 +116,35 @@ def test_bert_layer_uses_fused_attention_kernel():
     y.float().mean().backward()
     assert torch.isfinite(y.float()).all()
     assert all(torch.isfinite(p.grad.float()).all() for p in m.parameters() if p.grad is not None)
+
+
+def test_nmt_transformer_runs_fused_attention(monkeypatch):
+    """The reference Transformer's attention (8 heads x key_dim 256, T = 20) is on the fused
+    kernel: every attention call goes through flash, none through the materialised path."""
+    from vodascheduler_amd.models import cast_compute_weights_
+    from vodascheduler_amd.models.transformer import TransformerNMT
+    from vodascheduler_amd.ops import attention as A
+
+    calls = {"flash": 0, "materialized": 0}
+    real_fa, real_mat = A.flash.attention_qkvpacked, A.materialized_attention
+    real_fq = A.flash.attention_q_kvpacked
+    monkeypatch.setattr(A.flash, "attention_qkvpacked",
+                        lambda *a, **k: (calls.__setitem__("flash", calls["flash"] + 1), real_fa(*a, **k))[1])
+    monkeypatch.setattr(A.flash, "attention_q_kvpacked",
+                        lambda *a, **k: (calls.__setitem__("flash", calls["flash"] + 1), real_fq(*a, **k))[1])
+    monkeypatch.setattr(A, "materialized_attention",
+                        lambda *a, **k: (calls.__setitem__("materialized", calls["materialized"] + 1),
+                                         real_mat(*a, **k))[1])
+    torch.manual_seed(0)
+    m = cast_compute_weights_(TransformerNMT().cuda())
+    src = torch.randint(1, 15000, (32, 20), device="cuda")
+    tgt = torch.randint(1, 15000, (32, 20), device="cuda")
+    src[:, -3:] = 0
+    with torch.autocast("cuda", dtype=torch.bfloat16):
+        y = m(src, tgt)
+    y.float().mean().backward()
+    assert calls == {"flash": 3, "materialized": 0}, calls
+    assert torch.isfinite(y.float()).all()
 
 
 @pytest.mark.gpu

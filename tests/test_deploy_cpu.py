@@ -1,0 +1,67 @@
+"""Deployment bundle: Helm chart (values, templates for every control-plane component, the
+MPIJob CRD with the reference's replica validation) and example PVCs parse and cover what
+the reference chart deploys (helm/voda-scheduler/templates/*)."""
+import os
+import re
+
+import yaml
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+CHART = os.path.join(ROOT, "deploy", "helm", "vodascheduler-amd")
+
+
+def _render_lite(text: str, values: dict) -> str:
+    """Tiny stand-in for helm's renderer, enough for a structural check: drops control
+    lines and substitutes simple ``.Values`` paths."""
+    out = []
+    for line in text.splitlines():
+        if re.match(r"^\s*\{\{-?\s*(if|end|range|else|define)", line):
+            continue
+
+        def sub(m):
+            path = m.group(1).split(".")
+            v = values
+            for k in path:
+                v = v.get(k, "x") if isinstance(v, dict) else "x"
+            v = str(v) if not isinstance(v, (dict, list)) else "x"
+            return '"%s"' % v if "quote" in m.group(0) else v
+
+        line = re.sub(r"\{\{-?\s*\$?\.Values\.([\w.]+)[^}]*\}\}", sub, line)
+        line = re.sub(r"\{\{-?[^}]*\}\}", "x", line)
+        out.append(line)
+    return "\n".join(out)
+
+
+def test_chart_files_and_components():
+    chart = yaml.safe_load(open(os.path.join(CHART, "Chart.yaml")))
+    values = yaml.safe_load(open(os.path.join(CHART, "values.yaml")))
+    assert chart["name"] == "vodascheduler-amd" and values["gpuTypes"]
+    assert values["scheduler"]["rateLimitSec"] == 30 and values["metricsCollector"]["schedule"] == "*/1 * * * *"
+    kinds = {}
+    for fn in sorted(os.listdir(os.path.join(CHART, "templates"))):
+        if not fn.endswith(".yaml"):
+            continue
+        docs = [d for d in yaml.safe_load_all(_render_lite(open(os.path.join(CHART, "templates", fn)).read(),
+                                                           values)) if d]
+        for d in docs:
+            kinds.setdefault(d["kind"], []).append(d["metadata"]["name"])
+    assert {"training-service", "resource-allocator"} <= set(kinds["Deployment"])
+    assert any(n.startswith("scheduler-") for n in kinds["Deployment"])
+    assert "metrics-collector" in kinds["CronJob"] and "gpu-exporter" in kinds["DaemonSet"]
+    assert kinds["CustomResourceDefinition"] == ["mpijobs.kubeflow.org"]
+    assert {"training-service", "resource-allocator"} <= set(kinds["Service"])
+
+
+def test_mpijob_crd_validates_replicas_like_reference():
+    values = yaml.safe_load(open(os.path.join(CHART, "values.yaml")))
+    crd = yaml.safe_load(_render_lite(open(os.path.join(CHART, "templates", "mpi-operator-crd.yaml")).read(), values))
+    spec = crd["spec"]["versions"][0]["schema"]["openAPIV3Schema"]["properties"]["spec"]["properties"]
+    reps = spec["mpiReplicaSpecs"]["properties"]
+    assert reps["Launcher"]["properties"]["replicas"] == {"type": "integer", "minimum": 1, "maximum": 1}
+    assert reps["Worker"]["properties"]["replicas"]["minimum"] == 1
+
+
+def test_example_pvcs_parse():
+    docs = list(yaml.safe_load_all(open(os.path.join(ROOT, "examples", "pvc", "pvc-nfs.yaml"))))
+    claims = [d["metadata"]["name"] for d in docs if d["kind"] == "PersistentVolumeClaim"]
+    assert {"voda-pvc-data", "voda-pvc-repos", "voda-pvc-outputs-nfs", "voda-pvc-metrics-nfs"} == set(claims)

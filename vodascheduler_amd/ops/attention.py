@@ -1,7 +1,7 @@
 """Scaled dot-product attention with key-padding + causal masks.
 
 Dispatch (GPU): the fused MFMA attention HIP kernels (csrc/hip/attention.hip, ops/flash.py)
-when the shape is supported (bf16, head dim 32/64/128, Tq, Tk <= 128, no dropout);
+when the shape is supported (bf16, head dim 32/64/128/256, Tq, Tk <= 4096, no dropout);
 otherwise the materialised path -- scores by hipBLASLt GEMM, the hand-written
 masked-softmax HIP kernel, dropout, PV GEMM.  The reference's Transformer materialises
 the full [B, H, Tq, S] scores (layers_tf25.py:450-461).  CPU: the same materialised math

@@ -1,6 +1,7 @@
 """Fused MFMA attention (csrc/hip/attention.hip): forward, dQ pass and dK/dV pass.
 
-Entry points (all bf16, head dim 32/64/128, Tq, Tk <= 128):
+Entry points (all bf16, head dim 32/64/128/256, Tq, Tk <= 4096; the streamed operand goes
+through LDS in 32-row tiles, so long sequences -- BERT at 512 -- stay on the fused path):
 
 * ``attention_qkvpacked(qkv)`` -- self-attention straight from the packed projection
   ``qkv`` [B, T, 3, H, D] (one fused QKV GEMM); the gradient is written into ONE
@@ -18,8 +19,8 @@ import torch
 
 from . import _native as N
 
-MAX_T = 128
-HEAD_DIMS = (32, 64, 128)
+MAX_T = 4096
+HEAD_DIMS = (32, 64, 128, 256)
 
 
 def supported(D: int, Tq: int, Tk: int, dtype: torch.dtype, device_is_cuda: bool = True) -> bool:
