@@ -26,6 +26,7 @@ class FakeK8s:
         self.pods: dict[str, dict] = {}
         self.log: list[tuple[str, str]] = []
         self.rv = 0
+        self.watches = 0
         fake = self
 
         class H(BaseHTTPRequestHandler):
@@ -41,10 +42,41 @@ class FakeK8s:
                 n = int(self.headers.get("Content-Length") or 0)
                 return json.loads(self.rfile.read(n)) if n else None
 
+            def _watch(self, path, query):
+                """Stream ADDED/MODIFIED/DELETED lines by diffing the collection (2 s per stream;
+                the first poll re-announces every item, as after a re-LIST)."""
+                import time as _t
+
+                self.send_response(200)
+                self.send_header("Content-Type", "application/json")
+                self.end_headers()
+                prev: dict[str, str] = {}
+                t_end = _t.time() + 2.0
+                while _t.time() < t_end:
+                    code, lst = fake.handle("GET", path, None)
+                    cur = {o["metadata"]["name"]: json.dumps(o, sort_keys=True) for o in lst.get("items", [])}
+                    lines = []
+                    for n, js in cur.items():
+                        if prev.get(n) != js:
+                            lines.append({"type": "ADDED" if n not in prev else "MODIFIED", "object": json.loads(js)})
+                    for n in set(prev) - set(cur):
+                        lines.append({"type": "DELETED", "object": json.loads(prev[n])})
+                    prev = cur
+                    try:
+                        for ev in lines:
+                            self.wfile.write((json.dumps(ev) + "\n").encode())
+                        self.wfile.flush()
+                    except OSError:
+                        return
+                    _t.sleep(0.02)
+
             def _route(self, method):
                 u = urlparse(self.path)
                 path = unquote(u.path)
                 fake.log.append((method, path))
+                if method == "GET" and "watch=1" in u.query:
+                    fake.watches += 1
+                    return self._watch(path, u.query)
                 code, obj = fake.handle(method, path, self._body() if method in ("POST", "PUT", "PATCH") else None)
                 self._send(code, obj)
 
@@ -200,3 +232,43 @@ def test_gen_manifests_one_scheduler_per_gpu_type(capsys):
     cmd = docs[2]["spec"]["template"]["spec"]["containers"][0]["command"]
     assert cmd[cmd.index("--gpu-type") + 1] == "amd-instinct-mi300x" and "--resume" in cmd
     assert docs[1]["spec"]["ports"][0]["port"] == 55588
+
+
+def test_watch_informers_bind_pods_and_report_completion():
+    """Informer path: with the resync period effectively off, LIST + WATCH streams alone bind a
+    new worker pod to its placed node and report the MPIJob's Succeeded condition."""
+    import time
+
+    from vodascheduler_amd.backend.base import EV_FINISHED, START, JobAction
+    from vodascheduler_amd.common.trainingjob import TrainingJob
+
+    fake = FakeK8s({"nodeA": 4})
+    backend = K8sBackend(K8sClient(fake.url), DEFAULT_GPU_TYPE, poll_interval=3600.0)
+    events = []
+    backend.set_event_sink(lambda *ev: events.append(ev))
+    try:
+        store, mq = MemoryStore(), InProcQueue()
+        svc = TrainingService(store, mq, ManualClock(0.0))
+        name = svc.create_training_job(json.dumps(make_spec("w", "resnet50", 2, 1, 2, 1, 10)))
+        job = TrainingJob.from_dict(store.find_metadata(name))
+        backend.apply([JobAction(START, job, 2, [("nodeA", 0), ("nodeA", 1)], [])])
+        fake.pods[f"{name}-worker-1"] = {"metadata": {"name": f"{name}-worker-1", "labels": {}},
+                                         "status": {"phase": "Pending"}, "spec": {}}
+
+        def wait(cond, t=10.0):
+            end = time.time() + t
+            while time.time() < end:
+                if cond():
+                    return True
+                time.sleep(0.02)
+            return False
+
+        assert wait(lambda: fake.pods[f"{name}-worker-1"]["spec"].get("tolerations"))
+        tol = fake.pods[f"{name}-worker-1"]["spec"]["tolerations"][0]
+        assert tol["key"] == TAINT_KEY and tol["value"] == "nodeA"
+        fake.mpijobs[name]["status"] = {"conditions": [{"type": "Succeeded", "status": "True"}]}
+        assert wait(lambda: (EV_FINISHED, name, True) in events)
+        assert fake.watches >= 3  # mpijobs, pods, nodes
+    finally:
+        backend.shutdown()
+        fake.stop()

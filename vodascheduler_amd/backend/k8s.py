@@ -19,7 +19,11 @@ exactly the API operations of the reference scheduler and placement manager, aga
 
 The API client is a small stdlib HTTPS/JSON client (in-cluster service-account token or an
 explicit URL + bearer token); nothing is imported from the kubernetes Python package, which
-is not in this image.  A background thread polls job conditions, node inventory and pods.
+is not in this image.  Change notification follows the informer pattern of the reference
+(scheduler.go:170-185,230-242; placement_manager.go:84-134): per resource (MPIJobs, our pods,
+GPU nodes) a LIST, then a streaming WATCH from its resourceVersion (re-LIST on 410 Gone or a
+dropped stream); events drive completion reports, pod binding and node inventory at once.
+A slow periodic resync (default 30 s) re-reads everything, as informers do.
 """
 from __future__ import annotations
 
@@ -91,6 +95,39 @@ class K8sClient:
     def patch(self, path: str, body) -> dict:
         return self.request("PATCH", path, body, content_type="application/merge-patch+json")
 
+    def watch(self, path: str, resource_version: str | None, on_event, stop: threading.Event,
+              timeout_s: int = 300) -> str | None:
+        """Stream ``?watch=1`` events of a collection until the server closes the stream, the
+        timeout passes or ``stop`` is set; returns the last resourceVersion seen.  Raises
+        :class:`ApiError` (410 when the version expired: re-LIST and watch again)."""
+        sep = "&" if "?" in path else "?"
+        url = f"{path}{sep}watch=1&allowWatchBookmarks=true&timeoutSeconds={int(timeout_s)}"
+        if resource_version:
+            url += f"&resourceVersion={resource_version}"
+        req = urllib.request.Request(self.base + url, method="GET")
+        req.add_header("Accept", "application/json")
+        if self.token:
+            req.add_header("Authorization", f"Bearer {self.token}")
+        rv = resource_version
+        try:
+            with urllib.request.urlopen(req, timeout=timeout_s + 30, context=self.ctx) as r:
+                for line in r:
+                    if stop.is_set():
+                        break
+                    line = line.strip()
+                    if not line:
+                        continue
+                    ev = json.loads(line)
+                    typ, obj = ev.get("type"), ev.get("object") or {}
+                    if typ == "ERROR":
+                        raise ApiError(int(obj.get("code", 500)), json.dumps(obj))
+                    rv = (obj.get("metadata") or {}).get("resourceVersion", rv)
+                    if typ != "BOOKMARK":
+                        on_event(typ, obj)
+        except urllib.error.HTTPError as e:
+            raise ApiError(e.code, e.read().decode(errors="replace")) from None
+        return rv
+
 
 def _rand(n: int = 5) -> str:
     return "".join(random.choice(string.ascii_lowercase + string.digits) for _ in range(n))
@@ -98,13 +135,17 @@ def _rand(n: int = 5) -> str:
 
 class K8sBackend(Backend):
     def __init__(self, client: K8sClient, gpu_type: str, namespace: str = NAMESPACE, configmap_opt: bool = True,
-                 poll_interval: float = 2.0, start_thread: bool = True):
+                 poll_interval: float = 30.0, start_thread: bool = True, watch: bool = True):
+        """``poll_interval``: informer resync period; ``watch``: stream change events (off:
+        resync polling only)."""
         super().__init__()
         self.c = client
         self.gpu_type = gpu_type
         self.ns = namespace
         self.configmap_opt = configmap_opt
         self.poll_interval = poll_interval
+        self.watch_enabled = watch
+        self._watchers: list[threading.Thread] = []
         self._lock = threading.Lock()
         self.jobs: dict[str, dict] = {}                # job -> spec as submitted
         self.placement: dict[str, list[tuple[str, int]]] = {}   # job -> worker i -> (node, gpu)
@@ -116,6 +157,8 @@ class K8sBackend(Backend):
         if start_thread:
             self._thread = threading.Thread(target=self._loop, daemon=True, name="k8s-backend")
             self._thread.start()
+            if watch:
+                self.start_watches()
 
     # ------------------------------------------------------------------ paths
     def _mpijobs(self) -> str:
@@ -228,6 +271,8 @@ class K8sBackend(Backend):
         self._stop.set()
         if self._thread is not None:
             self._thread.join(5)
+        for t in self._watchers:
+            t.join(2)
 
     # ------------------------------------------------------------------ watchers
     def refresh_nodes(self, emit: bool = True) -> None:
@@ -253,33 +298,76 @@ class K8sBackend(Backend):
                 self._finished.add(name)
                 self.emit(EV_FINISHED, name, mpijob.is_succeeded(st))
 
+    def _job_event(self, typ: str, obj: dict) -> None:
+        name = obj.get("metadata", {}).get("name")
+        st = obj.get("status")
+        if typ in ("ADDED", "MODIFIED") and name in self.jobs and name not in self._finished \
+                and mpijob.is_finished(st):
+            self._finished.add(name)
+            self.emit(EV_FINISHED, name, mpijob.is_succeeded(st))
+
     def bind_pods(self) -> None:
         """Give pending pods of our jobs the toleration of their placed node."""
         sel = urllib.request.quote(GPU_NAME_LABEL)
         pods = self.c.get(f"{self._pods()}?labelSelector={sel}").get("items", [])
         for p in pods:
-            md = p["metadata"]
-            name = md["name"]
-            if p.get("status", {}).get("phase") not in (None, "Pending"):
-                continue
-            tols = p.get("spec", {}).get("tolerations") or []
-            if any(t.get("key") == TAINT_KEY for t in tols):
-                continue
-            job, _, rest = name.rpartition("-worker-")
-            if job and rest.isdigit():
-                locs = self.placement.get(job) or []
-                i = int(rest)
-                if i >= len(locs) or not locs[i][0]:
-                    continue
-                tol = {"key": TAINT_KEY, "operator": "Equal", "value": locs[i][0], "effect": "NoExecute"}
-            elif name.endswith("-launcher") and name[:-len("-launcher")] in self.jobs:
-                tol = {"key": TAINT_KEY, "operator": "Exists", "effect": "NoExecute"}
-            else:
-                continue
+            self._bind_pod(p)
+
+    def _bind_pod(self, p: dict) -> None:
+        md = p["metadata"]
+        name = md["name"]
+        if p.get("status", {}).get("phase") not in (None, "Pending"):
+            return
+        tols = p.get("spec", {}).get("tolerations") or []
+        if any(t.get("key") == TAINT_KEY for t in tols):
+            return
+        job, _, rest = name.rpartition("-worker-")
+        if job and rest.isdigit():
+            locs = self.placement.get(job) or []
+            i = int(rest)
+            if i >= len(locs) or not locs[i][0]:
+                return
+            tol = {"key": TAINT_KEY, "operator": "Equal", "value": locs[i][0], "effect": "NoExecute"}
+        elif name.endswith("-launcher") and name[:-len("-launcher")] in self.jobs:
+            tol = {"key": TAINT_KEY, "operator": "Exists", "effect": "NoExecute"}
+        else:
+            return
+        try:
+            self.c.patch(f"{self._pods()}/{name}", {"spec": {"tolerations": tols + [tol]}})
+        except ApiError as e:
+            log.warning("binding %s failed: %s", name, e)
+
+    # ------------------------------------------------------------------ informers
+    def start_watches(self) -> None:
+        gsel = urllib.request.quote(f"{GPU_NAME_LABEL}={self.gpu_type}")
+        psel = urllib.request.quote(GPU_NAME_LABEL)
+        specs = [
+            ("mpijobs", self._mpijobs(), self._job_event),
+            ("pods", f"{self._pods()}?labelSelector={psel}",
+             lambda typ, obj: self._bind_pod(obj) if typ in ("ADDED", "MODIFIED") else None),
+            ("nodes", f"/api/v1/nodes?labelSelector={gsel}", lambda typ, obj: self.refresh_nodes()),
+        ]
+        for name, path, handler in specs:
+            t = threading.Thread(target=self._informer, args=(path, handler), daemon=True, name=f"k8s-watch-{name}")
+            t.start()
+            self._watchers.append(t)
+
+    def _informer(self, path: str, handler) -> None:
+        """LIST + WATCH loop of one collection (re-LIST when the stream breaks or expires)."""
+        while not self._stop.is_set():
             try:
-                self.c.patch(f"{self._pods()}/{name}", {"spec": {"tolerations": tols + [tol]}})
+                lst = self.c.get(path)
+                for obj in lst.get("items", []):
+                    handler("ADDED", obj)
+                rv = (lst.get("metadata") or {}).get("resourceVersion")
+                while not self._stop.is_set():
+                    rv = self.c.watch(path, rv, handler, self._stop)
             except ApiError as e:
-                log.warning("binding %s failed: %s", name, e)
+                if e.status != 410:
+                    log.warning("watch %s failed: %s", path, e)
+            except Exception as e:  # dropped stream / transient API failure
+                log.debug("watch %s interrupted: %s", path, e)
+            self._stop.wait(1.0)
 
     def _loop(self) -> None:
         while not self._stop.wait(self.poll_interval):

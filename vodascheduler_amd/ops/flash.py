@@ -19,8 +19,11 @@ import torch
 
 from . import _native as N
 
+import os
+
 MAX_T = 4096
-HEAD_DIMS = (32, 64, 128, 256)
+# VODA_FLASH_MAX_D: A/B switch that sends larger head dims to the materialised path
+HEAD_DIMS = tuple(d for d in (32, 64, 128, 256) if d <= int(os.environ.get("VODA_FLASH_MAX_D", "256")))
 
 
 def supported(D: int, Tq: int, Tk: int, dtype: torch.dtype, device_is_cuda: bool = True) -> bool:

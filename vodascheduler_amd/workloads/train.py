@@ -50,7 +50,10 @@ class TrainConfig:
     # as Horovod reduces fp32 unless --fp16-allreduce) | bf16 (opt-in low-precision gradients)
     grad_dtype: str = "fp32"
     bucket_cap_mb: float = 64.0
-    overlap_optimizer: bool = True     # per-bucket optimizer updates on the comm stream, overlapping backward
+    # per-bucket optimizer updates on the comm stream, overlapping backward: measured 1-1.5 %
+    # SLOWER at world 1 on MI355X (BERT-base 11.84 vs 11.68 ms, ResNet-50 27.67 vs 27.35 ms;
+    # profiles/r2_ab_overlap_optimizer.jsonl: the memory-bound updates contend with backward), so off
+    overlap_optimizer: bool = False
     reduction: str = "average"         # average | adasum (Horovod op=hvd.Adasum; LR not scaled by world)
     metrics_dir: str | None = None
     checkpoint_every_epoch: bool = False
