@@ -15,3 +15,11 @@ cat gpurun_out/r2c3_nmt_fused.json gpurun_out/r2c3_nmt_materialized.json
 timeout -k 10 300 python3 benchmarks/graph_diag.py --model resnet50 --batch 32 > gpurun_out/r2c3_graph_diag_resnet50.json 2> gpurun_out/r2c3_graph_diag.err
 echo "graph diag rc=$?"
 head -60 gpurun_out/r2c3_graph_diag_resnet50.json
+# BN reduction-pass depth A/B (VODA_BN_UNROLL=0: round-1 depths)
+for u in 0 1 0 1; do
+  VODA_BN_UNROLL=$u timeout -k 10 300 python3 benchmarks/bench_bn_passes.py > gpurun_out/r2c3_bn_u$u.json || exit 3
+  VODA_BN_UNROLL=$u timeout -k 10 240 python3 benchmarks/model_step.py --model resnet50 --batch 256 --steps 20 --warmup 6 >> gpurun_out/r2c3_resnet_bn_ab.jsonl || exit 3
+  echo "{\"bn_unroll\": $u}" >> gpurun_out/r2c3_resnet_bn_ab.jsonl
+done
+cat gpurun_out/r2c3_resnet_bn_ab.jsonl
+python3 -c "import json;[print(u, json.load(open(f'gpurun_out/r2c3_bn_u{u}.json'))['per_step_fwd_ms'], json.load(open(f'gpurun_out/r2c3_bn_u{u}.json'))['per_step_bwd_ms']) for u in (0,1)]"

@@ -25,6 +25,8 @@
 // channel slices.  Partial sums are fp32 per block; the finalize kernels reduce them with
 // 32 row-groups per channel group and double accumulation.
 #include "common.h"
+
+#include <cstdlib>
 #include "ops.h"
 
 namespace voda {
@@ -133,7 +135,7 @@ __device__ __forceinline__ void reduce_and_store(const Map& m, float (&s1)[8], f
 }
 
 // ---------------------------------------------------------------- forward: statistics
-template <typename T>
+template <typename T, int U>
 __global__ __launch_bounds__(kBlock) void bn_stats_kernel(const T* __restrict__ x, float* __restrict__ part,
                                                           int64_t M, int C) {
   const Map m = make_map(C);
@@ -144,18 +146,15 @@ __global__ __launch_bounds__(kBlock) void bn_stats_kernel(const T* __restrict__ 
     const int64_t col = int64_t(m.cg) * kVec;
     int64_t r = r0 + m.rsub;
     const int64_t step = m.rpi;
-    // 4 rows in flight per thread
-    for (; r + 3 * step < r1; r += 4 * step) {
-      float v0[8], v1[8], v2[8], v3[8];
-      Vec8<T>::load(x, r * C + col, v0);
-      Vec8<T>::load(x, (r + step) * C + col, v1);
-      Vec8<T>::load(x, (r + 2 * step) * C + col, v2);
-      Vec8<T>::load(x, (r + 3 * step) * C + col, v3);
+    // U rows (U x 16 B per lane) in flight per thread
+    for (; r + (U - 1) * step < r1; r += U * step) {
+      float v[U][8];
 #pragma unroll
-      for (int k = 0; k < 8; ++k) {
-        s1[k] += (v0[k] + v1[k]) + (v2[k] + v3[k]);
-        s2[k] += (v0[k] * v0[k] + v1[k] * v1[k]) + (v2[k] * v2[k] + v3[k] * v3[k]);
-      }
+      for (int u = 0; u < U; ++u) Vec8<T>::load(x, (r + u * step) * C + col, v[u]);
+#pragma unroll
+      for (int u = 0; u < U; ++u)
+#pragma unroll
+        for (int k = 0; k < 8; ++k) { s1[k] += v[u][k]; s2[k] += v[u][k] * v[u][k]; }
     }
     for (; r < r1; r += step) {
       float v[8];
@@ -173,7 +172,7 @@ __device__ __forceinline__ void apply_mask(float (&g)[8], uint8_t mb) {
   for (int k = 0; k < 8; ++k) g[k] = ((mb >> k) & 1) ? g[k] : 0.f;
 }
 
-template <typename T, bool RELU>
+template <typename T, bool RELU, int U>
 __global__ __launch_bounds__(kBlock) void bn_bwd_reduce_kernel(const T* __restrict__ dy,
                                                                const uint8_t* __restrict__ mask,
                                                                const T* __restrict__ x, float* __restrict__ part,
@@ -185,29 +184,30 @@ __global__ __launch_bounds__(kBlock) void bn_bwd_reduce_kernel(const T* __restri
   if (m.active) {
     const int64_t col = int64_t(m.cg) * kVec;
     const int64_t step = m.rpi;
+    const int CB = C / kVec;
     int64_t r = r0 + m.rsub;
-    for (; r + step < r1; r += 2 * step) {
-      float g0[8], x0[8], g1[8], x1[8];
-      Vec8<T>::load(dy, r * C + col, g0);
-      Vec8<T>::load(x, r * C + col, x0);
-      Vec8<T>::load(dy, (r + step) * C + col, g1);
-      Vec8<T>::load(x, (r + step) * C + col, x1);
-      if constexpr (RELU) {
-        const int CB = C / kVec;
-        apply_mask(g0, mask[r * CB + m.cg]);
-        apply_mask(g1, mask[(r + step) * CB + m.cg]);
+    // U rows of dy and x (2U x 16 B per lane) + their mask bytes in flight per thread
+    for (; r + (U - 1) * step < r1; r += U * step) {
+      float g[U][8], xv[U][8];
+      uint8_t mb[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        Vec8<T>::load(dy, (r + u * step) * C + col, g[u]);
+        Vec8<T>::load(x, (r + u * step) * C + col, xv[u]);
+        if constexpr (RELU) mb[u] = mask[(r + u * step) * CB + m.cg];
       }
 #pragma unroll
-      for (int k = 0; k < 8; ++k) {
-        s1[k] += g0[k] + g1[k];
-        s2[k] += g0[k] * x0[k] + g1[k] * x1[k];
+      for (int u = 0; u < U; ++u) {
+        if constexpr (RELU) apply_mask(g[u], mb[u]);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) { s1[k] += g[u][k]; s2[k] += g[u][k] * xv[u][k]; }
       }
     }
     for (; r < r1; r += step) {
       float g[8], xv[8];
       Vec8<T>::load(dy, r * C + col, g);
       Vec8<T>::load(x, r * C + col, xv);
-      if constexpr (RELU) apply_mask(g, mask[r * (C / kVec) + m.cg]);
+      if constexpr (RELU) apply_mask(g, mask[r * CB + m.cg]);
 #pragma unroll
       for (int k = 0; k < 8; ++k) { s1[k] += g[k]; s2[k] += g[k] * xv[k]; }
     }
@@ -418,6 +418,16 @@ Grid reduce_grid(int64_t M, int C) {
   return bn_grid(M, C, cap, 8);
 }
 
+// rows in flight of the reduction passes: 8 (stats) / 4 (backward reduce); VODA_BN_UNROLL=0
+// selects the round-1 depths 4 / 2 (A/B runs)
+bool bn_deep_unroll() {
+  static const bool deep = [] {
+    const char* e = std::getenv("VODA_BN_UNROLL");
+    return e == nullptr || e[0] != '0';
+  }();
+  return deep;
+}
+
 template <typename F>
 void dispatch_dt(int dt, F&& f) {
   if (dt == kBF16) f(BF16{});
@@ -447,7 +457,10 @@ void bn_fwd_train(uintptr_t x, uintptr_t residual, uintptr_t gamma, uintptr_t be
   dispatch_dt(dt, [&](auto tag) {
     using T = decltype(tag);
     const T* xp = reinterpret_cast<const T*>(x);
-    hipLaunchKernelGGL((bn_stats_kernel<T>), rg.grid, dim3(kBlock), 0, s, xp, ws, M, C);
+    if (bn_deep_unroll())
+      hipLaunchKernelGGL((bn_stats_kernel<T, 8>), rg.grid, dim3(kBlock), 0, s, xp, ws, M, C);
+    else
+      hipLaunchKernelGGL((bn_stats_kernel<T, 4>), rg.grid, dim3(kBlock), 0, s, xp, ws, M, C);
     hipLaunchKernelGGL(bn_fwd_finalize_kernel, dim3((C + kFinCh - 1) / kFinCh), dim3(kFinCh * kFinRg), 0, s, ws,
                        rg.nb, M, C, reinterpret_cast<const float*>(gamma), reinterpret_cast<const float*>(beta),
                        reinterpret_cast<float*>(running_mean), reinterpret_cast<float*>(running_var),
@@ -504,8 +517,11 @@ void bn_bwd(uintptr_t dy, uintptr_t mask, uintptr_t x, uintptr_t save_mean, uint
     const T* dyp = reinterpret_cast<const T*>(dy);
     const uint8_t* yp = reinterpret_cast<const uint8_t*>(mask);
     const T* xp = reinterpret_cast<const T*>(x);
-    if (relu) hipLaunchKernelGGL((bn_bwd_reduce_kernel<T, true>), rg.grid, dim3(kBlock), 0, s, dyp, yp, xp, ws, M, C);
-    else hipLaunchKernelGGL((bn_bwd_reduce_kernel<T, false>), rg.grid, dim3(kBlock), 0, s, dyp, yp, xp, ws, M, C);
+    const bool deep = bn_deep_unroll();
+    if (relu && deep) hipLaunchKernelGGL((bn_bwd_reduce_kernel<T, true, 4>), rg.grid, dim3(kBlock), 0, s, dyp, yp, xp, ws, M, C);
+    else if (relu) hipLaunchKernelGGL((bn_bwd_reduce_kernel<T, true, 2>), rg.grid, dim3(kBlock), 0, s, dyp, yp, xp, ws, M, C);
+    else if (deep) hipLaunchKernelGGL((bn_bwd_reduce_kernel<T, false, 4>), rg.grid, dim3(kBlock), 0, s, dyp, yp, xp, ws, M, C);
+    else hipLaunchKernelGGL((bn_bwd_reduce_kernel<T, false, 2>), rg.grid, dim3(kBlock), 0, s, dyp, yp, xp, ws, M, C);
     hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + kFinCh - 1) / kFinCh), dim3(kFinCh * kFinRg), 0, s, ws,
                        rg.nb, M, C, reinterpret_cast<const float*>(gamma), reinterpret_cast<const float*>(save_mean),
                        reinterpret_cast<const float*>(save_invstd), reinterpret_cast<float*>(dgamma),
