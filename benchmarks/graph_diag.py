@@ -25,16 +25,58 @@ from vodascheduler_amd.runtime.stepgraph import StepGraph  # noqa: E402
 from vodascheduler_amd.utils.flat import grad_of  # noqa: E402
 
 
-def build(w, dev, seed=0):
+def build(w, dev, seed=0, frozen=True):
+    """frozen: lr = 0 (and no momentum / decay) so every step sees the same weights."""
     torch.manual_seed(seed)
     m = prepare_model(w, dev)
     kw = dict(w.opt_kwargs)
-    kw["lr"] = 0.0
-    for k in ("momentum", "weight_decay"):
-        if k in kw:
-            kw[k] = 0.0
+    if frozen:
+        kw["lr"] = 0.0
+        for k in ("momentum", "weight_decay"):
+            if k in kw:
+                kw[k] = 0.0
     opt = make_optimizer(w.optimizer, m.parameters(), **kw)
     return m, opt
+
+
+def update_check(w, dev, batch, warmup: int, steps: int) -> dict:
+    """Real optimizer updates: ``steps`` eager steps vs ``steps`` graph replays after the same
+    eager warm-up; parameter / optimizer-state relative differences and loss trajectories."""
+    def make_step(m, opt):
+        def step_fn(b):
+            opt.zero_grad()
+            with torch.autocast("cuda", dtype=torch.bfloat16, cache_enabled=False):
+                loss = w.loss(m, b)
+            loss.backward()
+            opt.step()
+            return loss
+        return step_fn
+
+    me, oe = build(w, dev, frozen=False)
+    mg, og = build(w, dev, frozen=False)
+    se, sg = make_step(me, oe), make_step(mg, og)
+    side = torch.cuda.Stream()
+    for _ in range(warmup):
+        se(batch)
+        side.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(side):
+            sg(batch)
+        torch.cuda.current_stream().wait_stream(side)
+    torch.cuda.synchronize()
+    graph = StepGraph(sg, batch, mg, og)
+    le, lg = [], []
+    for _ in range(steps):
+        le.append(float(se(batch)))
+        lg.append(float(graph.replay(batch)))
+    torch.cuda.synchronize()
+    worst = []
+    for i, (a, b) in enumerate(zip(oe.flat_state_tensors(), og.flat_state_tensors())):
+        if a.dtype.is_floating_point:
+            rel = float((b.float() - a.float()).norm() / a.float().norm().clamp_min(1e-20))
+            worst.append((rel, i))
+    worst.sort(reverse=True)
+    return {"losses_eager": le, "losses_graph": lg, "state_rel_err_max": worst[0][0] if worst else 0.0,
+            "steps_host": [oe._steps, og._steps], "step_t": [oe._step_t.tolist(), og._step_t.tolist()]}
 
 
 def main():
@@ -43,6 +85,7 @@ def main():
     ap.add_argument("--batch", type=int, default=32)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--tol", type=float, default=2e-2)
+    ap.add_argument("--update-steps", type=int, default=5, help="real-update check length (0: skip)")
     a = ap.parse_args()
     _native.hip()
     dev = torch.device("cuda", 0)
@@ -98,6 +141,8 @@ def main():
             if not rel < 0.05:
                 bn_bad.append({"buffer": n, "rel_err": rel})
     out["buffers_off"] = bn_bad[:20]
+    if a.update_steps > 0:
+        out["update_check"] = update_check(w, dev, batch, a.warmup, a.update_steps)
     print(json.dumps(out, indent=1), flush=True)
 
 
