@@ -54,9 +54,11 @@ def run(model: str, batch: int | None, steps: int, warmup: int, marker: bool = F
     def step():
         return stepper(b)
 
+    t_w = time.perf_counter()
     for _ in range(warmup):
         step()
     torch.cuda.synchronize(dev)
+    warm_s = time.perf_counter() - t_w
     if marker:  # trace_window_stats.py keeps only kernels after this one
         torch.cuda._sleep(1000)
         torch.cuda.synchronize(dev)
@@ -66,7 +68,8 @@ def run(model: str, batch: int | None, steps: int, warmup: int, marker: bool = F
     torch.cuda.synchronize(dev)
     dt = (time.perf_counter() - t0) / steps
     return {"model": model, "batch": bs, "ms_per_step": round(dt * 1e3, 3),
-            "samples_per_s": round(bs / dt, 1), "loss": float(loss.detach()), "graph": stepper.graph is not None}
+            "samples_per_s": round(bs / dt, 1), "loss": float(loss.detach()), "graph": stepper.graph is not None,
+            "warmup_s": round(warm_s, 3)}
 
 
 def main():

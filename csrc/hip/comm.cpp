@@ -77,7 +77,15 @@ RcclComm::RcclComm(const std::string& uid, int nranks, int rank, int device, dou
   if (wait) wait_ready("init");
 }
 
+template <typename F>
+int RcclComm::locked_call(F&& f) {
+  std::lock_guard<std::mutex> g(mu_);
+  check_live();
+  return static_cast<int>(f());
+}
+
 bool RcclComm::poll_ready() {
+  std::lock_guard<std::mutex> g(mu_);
   check_live();
   ncclResult_t st = ncclSuccess;
   ncclResult_t r = ncclCommGetAsyncError(comm_, &st);
@@ -90,6 +98,7 @@ bool RcclComm::poll_ready() {
 }
 
 RcclComm::~RcclComm() {
+  std::lock_guard<std::mutex> g(mu_);
   if (comm_ != nullptr) {
     // destructor must not throw; abort is the only call that never blocks on peers
     ncclCommAbort(comm_);
@@ -102,20 +111,25 @@ void RcclComm::wait_ready(const char* what) {
   const auto t0 = clock::now();
   int spins = 0;
   while (true) {
-    ncclResult_t st = ncclSuccess;
-    ncclResult_t r = ncclCommGetAsyncError(comm_, &st);
-    if (r != ncclSuccess) nccl_throw(r, "ncclCommGetAsyncError");
-    if (st == ncclSuccess) return;
-    if (st != ncclInProgress) {
-      aborted_ = true;
-      nccl_throw(st, what);
+    {
+      std::lock_guard<std::mutex> g(mu_);
+      if (comm_ == nullptr || aborted_) throw std::runtime_error(std::string("RCCL ") + what + ": communicator aborted");
+      ncclResult_t st = ncclSuccess;
+      ncclResult_t r = ncclCommGetAsyncError(comm_, &st);
+      if (r != ncclSuccess) nccl_throw(r, "ncclCommGetAsyncError");
+      if (st == ncclSuccess) return;
+      if (st != ncclInProgress) {
+        aborted_ = true;
+        nccl_throw(st, what);
+      }
+      if (timeout_s_ > 0 && std::chrono::duration<double>(clock::now() - t0).count() > timeout_s_) {
+        ncclCommAbort(comm_);
+        comm_ = nullptr;
+        aborted_ = true;
+        throw std::runtime_error(std::string("RCCL ") + what + " timed out");
+      }
     }
-    if (timeout_s_ > 0 && std::chrono::duration<double>(clock::now() - t0).count() > timeout_s_) {
-      ncclCommAbort(comm_);
-      comm_ = nullptr;
-      aborted_ = true;
-      throw std::runtime_error(std::string("RCCL ") + what + " timed out");
-    }
+    // lock released between polls: a watchdog abort() can get in
     if (++spins > 64) std::this_thread::sleep_for(std::chrono::microseconds(50));
   }
 }
@@ -135,37 +149,49 @@ void RcclComm::finish(int r_, const char* what) {
 }
 
 void RcclComm::allreduce(uintptr_t send, uintptr_t recv, int64_t count, int dtype, int op, uintptr_t stream) {
-  check_live();
-  finish(ncclAllReduce(reinterpret_cast<const void*>(send), reinterpret_cast<void*>(recv), size_t(count),
-                       to_nccl_dtype(dtype), to_nccl_op(op), comm_, as_stream(stream)),
+  const ncclDataType_t dt = to_nccl_dtype(dtype);
+  const ncclRedOp_t rop = to_nccl_op(op);
+  finish(locked_call([&] {
+           return ncclAllReduce(reinterpret_cast<const void*>(send), reinterpret_cast<void*>(recv), size_t(count), dt,
+                                rop, comm_, as_stream(stream));
+         }),
          "allreduce");
 }
 
 void RcclComm::broadcast(uintptr_t send, uintptr_t recv, int64_t count, int dtype, int root, uintptr_t stream) {
-  check_live();
-  finish(ncclBroadcast(reinterpret_cast<const void*>(send), reinterpret_cast<void*>(recv), size_t(count),
-                       to_nccl_dtype(dtype), root, comm_, as_stream(stream)),
+  const ncclDataType_t dt = to_nccl_dtype(dtype);
+  finish(locked_call([&] {
+           return ncclBroadcast(reinterpret_cast<const void*>(send), reinterpret_cast<void*>(recv), size_t(count), dt,
+                                root, comm_, as_stream(stream));
+         }),
          "broadcast");
 }
 
 void RcclComm::allgather(uintptr_t send, uintptr_t recv, int64_t count, int dtype, uintptr_t stream) {
-  check_live();
-  finish(ncclAllGather(reinterpret_cast<const void*>(send), reinterpret_cast<void*>(recv), size_t(count),
-                       to_nccl_dtype(dtype), comm_, as_stream(stream)),
+  const ncclDataType_t dt = to_nccl_dtype(dtype);
+  finish(locked_call([&] {
+           return ncclAllGather(reinterpret_cast<const void*>(send), reinterpret_cast<void*>(recv), size_t(count), dt,
+                                comm_, as_stream(stream));
+         }),
          "allgather");
 }
 
 void RcclComm::reduce_scatter(uintptr_t send, uintptr_t recv, int64_t count, int dtype, int op, uintptr_t stream) {
-  check_live();
-  finish(ncclReduceScatter(reinterpret_cast<const void*>(send), reinterpret_cast<void*>(recv), size_t(count),
-                           to_nccl_dtype(dtype), to_nccl_op(op), comm_, as_stream(stream)),
+  const ncclDataType_t dt = to_nccl_dtype(dtype);
+  const ncclRedOp_t rop = to_nccl_op(op);
+  finish(locked_call([&] {
+           return ncclReduceScatter(reinterpret_cast<const void*>(send), reinterpret_cast<void*>(recv), size_t(count),
+                                    dt, rop, comm_, as_stream(stream));
+         }),
          "reduce_scatter");
 }
 
 void RcclComm::alltoall(uintptr_t send, uintptr_t recv, int64_t count, int dtype, uintptr_t stream) {
-  check_live();
-  finish(ncclAllToAll(reinterpret_cast<const void*>(send), reinterpret_cast<void*>(recv), size_t(count),
-                      to_nccl_dtype(dtype), comm_, as_stream(stream)),
+  const ncclDataType_t dt = to_nccl_dtype(dtype);
+  finish(locked_call([&] {
+           return ncclAllToAll(reinterpret_cast<const void*>(send), reinterpret_cast<void*>(recv), size_t(count), dt,
+                               comm_, as_stream(stream));
+         }),
          "alltoall");
 }
 
@@ -180,6 +206,7 @@ void RcclComm::group_end() {
 }
 
 std::string RcclComm::async_error() const {
+  std::lock_guard<std::mutex> g(mu_);
   if (comm_ == nullptr) return aborted_ ? "aborted" : "destroyed";
   ncclResult_t st = ncclSuccess;
   ncclCommGetAsyncError(comm_, &st);
@@ -188,28 +215,36 @@ std::string RcclComm::async_error() const {
 }
 
 void RcclComm::abort() {
+  // Safe from a watchdog thread: waits for any in-progress NCCL call on this communicator
+  // (all of them return promptly in non-blocking mode), then aborts -- kernels of this
+  // communicator spinning on a dead peer observe the abort flag and exit.
+  aborted_ = true;
+  std::lock_guard<std::mutex> g(mu_);
   if (comm_ != nullptr) {
     ncclCommAbort(comm_);
     comm_ = nullptr;
   }
-  aborted_ = true;
 }
 
 void RcclComm::destroy() {
+  std::unique_lock<std::mutex> g(mu_);
   if (comm_ == nullptr) return;
   ncclResult_t r = ncclCommFinalize(comm_);
+  g.unlock();
   if (r == ncclInProgress) {
     try {
       wait_ready("finalize");
     } catch (...) {
-      // wait_ready aborted the communicator on timeout
+      // wait_ready aborted the communicator on timeout / abort
       return;
     }
   }
+  g.lock();
   if (comm_ != nullptr) {
     ncclCommDestroy(comm_);
     comm_ = nullptr;
   }
+  aborted_ = true;  // no longer usable
 }
 
 }  // namespace voda

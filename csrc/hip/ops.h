@@ -3,6 +3,8 @@
 
 #include <cstdint>
 #include <cstring>
+#include <atomic>
+#include <mutex>
 #include <string>
 #include <vector>
 
@@ -121,16 +123,22 @@ class RcclComm {
   void destroy();
   int rank() const { return rank_; }
   int size() const { return nranks_; }
-  bool alive() const { return comm_ != nullptr && !aborted_; }
+  bool alive() const { return !aborted_.load(); }
 
  private:
+  // Every NCCL call on comm_ runs under mu_, and waits poll with the lock released between
+  // polls, so abort() from a watchdog thread never frees the communicator under another
+  // thread's NCCL call (it takes effect at the waiter's next poll, which then throws).
+  template <typename F>
+  int locked_call(F&& f);
   void wait_ready(const char* what);
   void check_live() const;
   void finish(int r, const char* what);
+  mutable std::mutex mu_;
   ncclComm_t comm_ = nullptr;
   int nranks_, rank_;
   double timeout_s_;
-  bool aborted_ = false;
+  std::atomic<bool> aborted_{false};
 };
 
 }  // namespace voda

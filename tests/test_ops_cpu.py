@@ -288,3 +288,22 @@ def test_ddp_overlap_optimizer_is_opt_in_and_cpu_off():
     o = make_optimizer("sgd", m.parameters(), lr=0.1)
     assert not ElasticDDP(m, None, o).overlap_optimizer
     assert not ElasticDDP(m, None, o, overlap_optimizer=True).overlap_optimizer  # CPU: never
+
+
+def test_conv_sep_bias_matches_conv2d_and_flat_grad():
+    from vodascheduler_amd.ops.conv_bias import Conv2dSepBias
+    from vodascheduler_amd.ops.optim import make_optimizer
+    from vodascheduler_amd.utils.flat import grad_of
+
+    torch.manual_seed(0)
+    ref = torch.nn.Conv2d(4, 8, 3, padding=1)
+    m = Conv2dSepBias(4, 8, 3, padding=1)
+    m.load_state_dict(ref.state_dict())
+    x = torch.randn(2, 4, 9, 7)
+    torch.testing.assert_close(m(x), ref(x))
+    opt = make_optimizer("sgd", m.parameters(), lr=0.0)  # flat grads: the direct column-sum path
+    opt.zero_grad()
+    (m(x) ** 2).sum().backward()
+    (ref(x) ** 2).sum().backward()
+    torch.testing.assert_close(grad_of(m.bias), ref.bias.grad, rtol=1e-5, atol=1e-5)
+    torch.testing.assert_close(grad_of(m.weight), ref.weight.grad, rtol=1e-5, atol=1e-5)

@@ -21,13 +21,15 @@ import torch.nn.functional as F
 from torch import nn
 
 from ..ops.batchnorm import FusedBatchNorm2d
+from ..ops.conv_bias import Conv2dSepBias
 from ..ops.pool import FusedMaxPool2d, max_pool2d
 
 
 def _vgg_block(cin, cout, n):
     layers = []
     for i in range(n):
-        layers += [nn.Conv2d(cin if i == 0 else cout, cout, 3, padding=1), nn.ReLU(inplace=True)]
+        # bias add + bias gradient on our column-sum kernel (hipGraph-safe; ops/conv_bias.py)
+        layers += [Conv2dSepBias(cin if i == 0 else cout, cout, 3, padding=1), nn.ReLU(inplace=True)]
     layers.append(FusedMaxPool2d(2))
     return layers
 

@@ -326,9 +326,15 @@ class CommCache:
     Reuse is agreed collectively: every member announces the id of the communicator it
     holds for the member list; only if ALL hold the same id is it reused, otherwise a new
     one is built (a restarted or evicted member therefore forces a rebuild, never a hang).
-    Aborted communicators are never cached."""
+    Aborted communicators are never cached.
 
-    def __init__(self, max_entries: int = 16):
+    Capacity: each idle RCCL communicator keeps its channel buffers and proxy thread, so the
+    cache is bounded (``VODA_COMM_CACHE_MAX``, default 8 per process -- on an 8-GPU node the
+    distinct member lists a GPU takes part in at a time are few; evicted ones are aborted)."""
+
+    def __init__(self, max_entries: int | None = None):
+        if max_entries is None:
+            max_entries = int(os.environ.get("VODA_COMM_CACHE_MAX", "8"))
         self.max_entries = max_entries
         self._d: "OrderedDict[tuple, Communicator]" = OrderedDict()
         self._lock = threading.Lock()
