@@ -12,12 +12,13 @@
 //     instead of a wedged process; abort() can be called from a watchdog thread.
 //   * collectives are enqueued on the caller's HIP stream (the DDP engine passes its
 //     dedicated comm stream), so they overlap backward compute on the compute stream.
-#include "common.h"
+#include "host_common.h"
 #include "ops.h"
 
 #include <rccl/rccl.h>
 
 #include <chrono>
+#include <cstring>
 #include <thread>
 
 namespace voda {

@@ -11,26 +11,14 @@
 
 #include <hip/hip_runtime.h>
 #include <cmath>
+
+#include "host_common.h"
 #include <cstdint>
 #include <stdexcept>
 #include <string>
 
 namespace voda {
 
-#define VODA_HIP_CHECK(expr)                                                              \
-  do {                                                                                   \
-    hipError_t _e = (expr);                                                              \
-    if (_e != hipSuccess)                                                                \
-      throw std::runtime_error(std::string("HIP error ") + hipGetErrorString(_e) +       \
-                               " at " __FILE__ ":" + std::to_string(__LINE__));         \
-  } while (0)
-
-#define VODA_CHECK(cond, msg)                                                            \
-  do {                                                                                   \
-    if (!(cond)) throw std::invalid_argument(std::string("vodascheduler_amd: ") + (msg)); \
-  } while (0)
-
-enum DType : int { kF32 = 0, kBF16 = 1, kF16 = 2 };
 
 inline int dtype_size(int dt) { return dt == kF32 ? 4 : 2; }
 
@@ -108,7 +96,6 @@ inline unsigned stream_grid(int64_t work_items, int block = 256, int64_t cap = 2
   return static_cast<unsigned>(g);
 }
 
-inline hipStream_t as_stream(uintptr_t s) { return reinterpret_cast<hipStream_t>(s); }
 
 inline void check_launch() { VODA_HIP_CHECK(hipGetLastError()); }
 

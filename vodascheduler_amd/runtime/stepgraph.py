@@ -67,13 +67,16 @@ class GraphedStepper:
     """Runs training steps eagerly for ``warmup`` steps on a side stream, then captures and
     replays.  Falls back to eager for good if capture fails."""
 
-    def __init__(self, step_fn, model=None, optimizer=None, warmup: int = 2, enabled: bool = True):
+    def __init__(self, step_fn, model=None, optimizer=None, warmup: int = 2, enabled: bool = True,
+                 graph: "StepGraph | None" = None):
+        """``graph``: a step captured earlier for the same model / optimizer / batch shapes (a
+        warm worker's next job of the same kind replays it without warm-up or capture)."""
         self.step_fn = step_fn
         self.model = model
         self.optimizer = optimizer
         self.warmup = warmup
         self.enabled = enabled and torch.cuda.is_available()
-        self.graph: StepGraph | None = None
+        self.graph: StepGraph | None = graph if self.enabled else None
         self.eager_steps = 0
         self._side = None
 

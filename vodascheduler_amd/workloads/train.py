@@ -99,6 +99,7 @@ class _Warm:
                               compression=cfg.compression, reduction=cfg.reduction,
                               overlap_optimizer=cfg.overlap_optimizer)
         self._init = [t.detach().clone() for t in self._tensors()]
+        self.step_graph = None  # world-1 step captured by an earlier job (runtime/stepgraph.py)
 
     def _tensors(self):
         return self.opt.flat_state_tensors() + [b for b in self.model.buffers()]
@@ -204,7 +205,8 @@ def train_elastic(ctx: ElasticContext, cfg: TrainConfig, use_cache: bool = True)
         # world 1: the whole step replays as one hipGraph (launch-bound models); collectives
         # of world > 1 stay eager.  Re-captured after every membership change.
         stepper = GraphedStepper(step_fn, model, opt, warmup=2,
-                                 enabled=cfg.graph and w.graph_safe and world == 1 and device.type == "cuda")
+                                 enabled=cfg.graph and w.graph_safe and world == 1 and device.type == "cuda",
+                                 graph=wm.step_graph if use_cache else None)
         loss_t = None
         while state.epoch < cfg.epochs:
             t_ep = time.time()
@@ -248,6 +250,8 @@ def train_elastic(ctx: ElasticContext, cfg: TrainConfig, use_cache: bool = True)
                 state.save_checkpoint()
         if device.type == "cuda":
             torch.cuda.synchronize(device)
+        if use_cache and stepper.graph is not None:
+            wm.step_graph = stepper.graph  # the next job of this kind replays it directly
         digest = None
         if cfg.final_state_path:
             if ctx.rank == 0:
