@@ -35,7 +35,7 @@ def _train(name, graph, steps=8, bs=16):
     return losses, torch.cat([p.detach().float().flatten() for p in m.parameters()]), opt, m
 
 
-@pytest.mark.parametrize("name", ["mnist", "mnist-torch"])
+@pytest.mark.parametrize("name", ["mnist", "mnist-torch", "vgg16", "resnet50-cifar"])
 def test_graph_matches_eager(name):
     le, pe, oe, me = _train(name, False)
     lg, pg, og, mg = _train(name, True)
@@ -51,4 +51,4 @@ def test_graph_matches_eager(name):
 def test_only_validated_workloads_are_graph_safe():
     from vodascheduler_amd.models import WORKLOADS
 
-    assert {n for n, w in WORKLOADS.items() if w.graph_safe} == {"mnist", "mnist-torch"}
+    assert {n for n, w in WORKLOADS.items() if w.graph_safe} == {"mnist", "mnist-torch", "vgg16", "resnet50-cifar"}

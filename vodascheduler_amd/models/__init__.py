@@ -30,9 +30,10 @@ class Workload:
     channels_last: bool = False
     samples_unit: str = "img"   # throughput unit (img or tok)
     tokens_per_sample: int = 1
-    # whole-step hipGraph capture validated on MI355X (tests/test_stepgraph_gpu.py).  Not for
-    # models whose MIOpen conv solvers or GEMM paths are not capture-safe: ResNet-50/224
-    # replayed with wrong weight gradients and the NMT Transformer faulted (docs/kernels.md)
+    # whole-step hipGraph capture validated on MI355X (benchmarks/graph_diag.py: replayed
+    # gradients == eager, real-update trajectories match; tests/test_stepgraph_gpu.py).  Not
+    # for models with library paths that are not capture-safe (InceptionV3's MIOpen backward
+    # solvers; docs/kernels.md)
     graph_safe: bool = False
     # (loss, #correct predictions, #predictions) of one batch, all device tensors: the
     # training step logs accuracy from the same forward (Keras ``metrics=["accuracy"]``,
@@ -132,11 +133,13 @@ WORKLOADS: dict[str, Workload] = {
     "resnet50": Workload("resnet50", lambda: resnet50(1000), _img_batch(3, 224, 224, 1000), _ce, 256, "sgd",
                          dict(lr=0.1, momentum=0.9, weight_decay=5e-5), channels_last=True, metrics=_CE),
     "resnet50-cifar": Workload("resnet50-cifar", lambda: resnet50(10, small_input=True), _img_batch(3, 32, 32, 10),
-                               _ce, 128, "sgd", dict(lr=0.01, momentum=0.9), channels_last=True, metrics=_CE),
+                               _ce, 128, "sgd", dict(lr=0.01, momentum=0.9), channels_last=True, metrics=_CE,
+                               graph_safe=True),  # 14.33 -> 7.86 ms per step as a graph
     "resnet18": Workload("resnet18", lambda: resnet18(1000), _img_batch(3, 224, 224, 1000), _ce, 256, "sgd",
                          dict(lr=0.1, momentum=0.9), channels_last=True, metrics=_CE),
     "vgg16": Workload("vgg16", vgg16_cifar, _img_batch(3, 32, 32, 10), _ce, 128, "sgd",
-                      dict(lr=0.01, momentum=0.9), channels_last=True, metrics=_CE),
+                      dict(lr=0.01, momentum=0.9), channels_last=True, metrics=_CE,
+                      graph_safe=True),  # conv bias on ops/conv_bias.py: 2.63 -> 2.36 ms as a graph
     "inceptionv3": Workload("inceptionv3", InceptionV3, _img_batch(3, 75, 75, 10), _ce, 128, "rmsprop",
                             dict(lr=1e-3), channels_last=True, metrics=_CE),
     "mnist": Workload("mnist", KerasMnistCNN, _img_batch(1, 28, 28, 10), _ce, 128, "adam", dict(lr=1e-3),
