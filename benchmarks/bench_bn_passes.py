@@ -41,7 +41,12 @@ def timeit(fn, iters=20, warmup=3):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--batch", type=int, default=256)
+    ap.add_argument("--tuning", default="", help="deep,blocks,sweep for the reduction passes (A/B)")
     a = ap.parse_args()
+    if a.tuning:
+        from vodascheduler_amd.ops import _native
+
+        _native.hip().bn_set_tuning(*[int(v) for v in a.tuning.split(",")])
     dev = "cuda"
     cl = torch.channels_last
     rows, tot_f, tot_b = [], 0.0, 0.0
@@ -65,7 +70,7 @@ def main():
                      "bwd_TBs": round(bb / (bwd * 1e-6) / 1e12, 2)})
         tot_f += cnt * fwd
         tot_b += cnt * bwd
-    print(json.dumps({"batch": a.batch, "copy_TBs": round(copy_tbs, 2), "per_step_fwd_ms": round(tot_f / 1e3, 3),
+    print(json.dumps({"batch": a.batch, "tuning": a.tuning, "copy_TBs": round(copy_tbs, 2), "per_step_fwd_ms": round(tot_f / 1e3, 3),
                       "per_step_bwd_ms": round(tot_b / 1e3, 3), "shapes": rows}, indent=1))
 
 

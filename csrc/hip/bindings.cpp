@@ -35,6 +35,8 @@ PYBIND11_MODULE(_vodahip, m) {
   m.def("masked_softmax_bwd", &masked_softmax_bwd);
 
   m.def("bn_workspace_floats", &bn_workspace_floats);
+  m.def("bn_set_tuning", &bn_set_tuning, py::arg("deep") = -1, py::arg("blocks") = -1, py::arg("sweep") = -1);
+  m.def("bn_get_tuning", &bn_get_tuning);
   m.def("bn_fwd_train", &bn_fwd_train);
   m.def("bn_apply", &bn_apply);
   m.def("bn_bwd", &bn_bwd);

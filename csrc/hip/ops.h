@@ -67,6 +67,10 @@ void masked_softmax_bwd(uintptr_t y, uintptr_t dy, uintptr_t dx, int64_t rows, i
 
 // ---- fused BatchNorm(+add)(+ReLU), channels_last [M][C] (batchnorm.hip) ----
 int64_t bn_workspace_floats(int64_t M, int C);
+// reduction-pass tuning (deep unroll, grid cap, sweep order); negative = unchanged.  Not
+// thread-safe against concurrent BN launches: set it before a run (tests, A/B benchmarks).
+void bn_set_tuning(int deep, int blocks, int sweep);
+std::vector<int> bn_get_tuning();
 void bn_fwd_train(uintptr_t x, uintptr_t residual, uintptr_t gamma, uintptr_t beta, uintptr_t running_mean,
                   uintptr_t running_var, uintptr_t save_mean, uintptr_t save_invstd, uintptr_t y, uintptr_t mask,
                   uintptr_t workspace, int64_t M, int C, float eps, float momentum, bool relu, int dt,

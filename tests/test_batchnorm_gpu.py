@@ -51,6 +51,44 @@ def test_bn_act_fwd_bwd(shape, res, relu, dt):
         torch.testing.assert_close(r.grad.float(), rr.grad, atol=gtol, rtol=gtol)
 
 
+@pytest.mark.parametrize("tuning", [(1, 2048, 1), (0, 1024, 0), (1, 64, 1), (1, 1024, 1)])
+@pytest.mark.parametrize("shape", [(8, 64, 14, 14), (3, 2048, 3, 3), (16, 256, 28, 28)])
+def test_bn_reduction_orders_agree(shape, tuning):
+    """Every reduction walk (chunked / grid sweep, grid caps, unroll depths, buffer-descriptor
+    tail clamping) gives the same statistics and gradients as the default."""
+    from vodascheduler_amd.ops import _native
+
+    h = _native.hip()
+    saved = list(h.bn_get_tuning())
+    torch.manual_seed(0)
+    C = shape[1]
+    x = (torch.randn(shape, device="cuda") + 0.3).to(torch.bfloat16).to(memory_format=torch.channels_last)
+    r = torch.randn_like(x)
+    dy = torch.randn_like(x)
+    w = torch.rand(C, device="cuda") + 0.5
+    b = torch.randn(C, device="cuda")
+
+    def run():
+        xi, ri = x.clone().requires_grad_(), r.clone().requires_grad_()
+        wi, bi = w.clone().requires_grad_(), b.clone().requires_grad_()
+        rm, rv = torch.zeros(C, device="cuda"), torch.ones(C, device="cuda")
+        y = batch_norm_act(xi, wi, bi, rm, rv, True, 0.1, 1e-5, ri, True)
+        y.backward(dy)
+        return [y.float(), rm, rv, xi.grad.float(), ri.grad.float(), wi.grad, bi.grad]
+
+    try:
+        h.bn_set_tuning(1, 1024, 0)
+        base = run()
+        h.bn_set_tuning(*tuning)
+        other = run()
+    finally:
+        h.bn_set_tuning(*saved)
+    M = x.numel() // C
+    for i, (a, o) in enumerate(zip(base, other)):
+        tol = 2e-2 * (M ** 0.5 if i >= 5 else 1)
+        torch.testing.assert_close(o, a, atol=tol, rtol=2e-2, msg=f"output {i}")
+
+
 def test_fused_bn_module_eval_and_autocast():
     torch.manual_seed(0)
     m = FusedBatchNorm2d(64, relu=True).cuda()

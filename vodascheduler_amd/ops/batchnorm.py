@@ -15,12 +15,18 @@ composition (which the GPU tests compare against).
 """
 from __future__ import annotations
 
+import os
+
 import torch
 import torch.nn.functional as F
 
 from ..utils.flat import flat_grad
 from . import _native as N
 from .dense import _ready
+
+# VODA_FUSED_BN=0: every BatchNorm takes the PyTorch reference composition (A/B and bisection
+# runs, e.g. benchmarks/graph_diag.py)
+USE_FUSED_BN = os.environ.get("VODA_FUSED_BN", "1") != "0"
 
 
 def _rows_view_ok(x: torch.Tensor) -> bool:
@@ -122,7 +128,7 @@ def batch_norm_act(x: torch.Tensor, weight: torch.Tensor | None, bias: torch.Ten
     # the kernels read gamma / beta / running statistics as fp32 (normalisation parameters
     # stay fp32 under cast_compute_weights_); anything else takes the reference path
     params_fp32 = all(t is None or t.dtype == torch.float32 for t in (weight, bias, running_mean, running_var))
-    if not params_fp32 or not _supported(x, residual):
+    if not USE_FUSED_BN or not params_fp32 or not _supported(x, residual):
         return _reference(x, weight, bias, running_mean, running_var, training, momentum, eps, residual, relu)
     if training or running_mean is None:
         return _BNActFn.apply(x, residual, weight, bias, running_mean, running_var, momentum, eps, relu, sink)

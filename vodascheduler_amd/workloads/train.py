@@ -212,18 +212,38 @@ def train_elastic(ctx: ElasticContext, cfg: TrainConfig, use_cache: bool = True)
             t_ep = time.time()
             steps = 0
             ep_acc = torch.zeros(3, device=device)  # sum over steps of [loss, #correct, #predictions]
+            guard = torch.zeros((), device=device)  # graph replays: loss sum since the last commit
             while state.samples < samples_per_epoch:
                 batch = pool[state.step % len(pool)]
                 with trace_range("train_step", "train", world=world):
                     m_t = stepper(batch)
                 ep_acc += m_t
                 loss_t = m_t[0]
+                if stepper.graph is not None:
+                    guard += m_t[0]
                 state.samples += bs * world
                 state.step += 1
                 steps += 1
                 stats["steps"] += 1
                 stats["samples"] += bs * world
                 if state.step % cfg.commit_every == 0:
+                    if stepper.graph is not None:
+                        # replay guard (one host sync per commit): a captured step whose library
+                        # kernels misbehave on replay shows up as a non-finite loss; roll back to
+                        # the last commit and continue eagerly (docs/kernels.md, hipGraph section)
+                        if not bool(torch.isfinite(guard)):
+                            log.warning("%s: non-finite loss under graph replay; restoring step %d, eager from now on",
+                                        ctx.job, ctx.committed_step)
+                            stepper.release()
+                            stepper.enabled = False
+                            wm.step_graph = None
+                            state.restore()
+                            stats["graph_fallbacks"] = stats.get("graph_fallbacks", 0) + 1
+                            ep_acc.zero_()
+                            steps = 0
+                            guard.zero_()
+                            continue
+                        guard.zero_()
                     state.commit()
                     if cfg.report_progress and ctx.rank == 0:
                         ctx.rdzv.set("progress", str(state.step))
