@@ -66,17 +66,24 @@ class KerasMnistCNN(nn.Module):
 
 
 class TorchMnistNet(nn.Module):
+    """The reference's PyTorch MNIST net (pytorch_mnist_elastic.py:80-96), dropout included:
+    Dropout2d after conv2 and dropout(0.5) after fc1, active in training mode only.  The
+    random masks are reproducible across resizes and restores because the trainer's elastic
+    state carries the RNG state (runtime/elastic.py TorchState)."""
+
     def __init__(self):
         super().__init__()
         self.conv1 = nn.Conv2d(1, 10, kernel_size=5)
         self.conv2 = nn.Conv2d(10, 20, kernel_size=5)
+        self.conv2_drop = nn.Dropout2d()
         self.fc1 = nn.Linear(320, 50)
         self.fc2 = nn.Linear(50, 10)
 
     def forward(self, x):
         x = F.relu(F.max_pool2d(self.conv1(x), 2))
-        x = F.relu(F.max_pool2d(self.conv2(x), 2))
+        x = F.relu(F.max_pool2d(self.conv2_drop(self.conv2(x)), 2))
         x = F.relu(self.fc1(x.view(-1, 320)))
+        x = F.dropout(x, training=self.training)
         return F.log_softmax(self.fc2(x), dim=1)
 
 

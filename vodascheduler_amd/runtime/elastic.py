@@ -437,14 +437,41 @@ def _to_plain(d: dict) -> dict:
     return out
 
 
+def rng_state(device: torch.device) -> list[int]:
+    """The generator state that random layers (dropout) on ``device`` draw from, as plain ints
+    (picklable, broadcastable, storable in a weights-only checkpoint)."""
+    if device.type == "cuda":
+        return torch.cuda.get_rng_state(device).tolist()
+    return torch.get_rng_state().tolist()
+
+
+def set_rng_state(device: torch.device, state: list[int]) -> None:
+    t = torch.tensor(state, dtype=torch.uint8)
+    if device.type == "cuda":
+        torch.cuda.set_rng_state(t, device)
+    else:
+        torch.set_rng_state(t)
+
+
 class TorchState(State):
     """Model + (fused flat) optimizer + extras.  Syncs parameters (fp32 masters when the
-    optimizer is a fused flat one), every optimizer slot and the model buffers (BN stats)."""
+    optimizer is a fused flat one), every optimizer slot and the model buffers (BN stats).
+
+    The RNG state of the model's device is part of the committed state (extra ``rng``): a
+    commit records it, a restore rewinds it and a (re)joining member receives the root's, so
+    dropout masks follow one sequence whatever resizes, restores or restarts happen -- every
+    member draws the same masks and an elastic run equals an uninterrupted one.  (Horovod's
+    TorchState leaves the generators alone; this makes the equivalence testable with dropout.)"""
 
     def __init__(self, ctx: ElasticContext, model: torch.nn.Module, optimizer=None, **extras):
         self.model = model
         self.optimizer = optimizer
-        super().__init__(ctx, **extras)
+        self._rng_device = ctx.device if isinstance(ctx.device, torch.device) else torch.device(ctx.device)
+        super().__init__(ctx, rng=rng_state(self._rng_device), **extras)
+
+    def save(self) -> None:
+        self._extras["rng"] = rng_state(self._rng_device)
+        super().save()
 
     def tensors(self):
         ts: list[torch.Tensor] = []
@@ -465,6 +492,9 @@ class TorchState(State):
     def after_load(self):
         if self.optimizer is not None and hasattr(self.optimizer, "after_external_update"):
             self.optimizer.after_external_update()
+        rng = self._extras.get("rng")
+        if rng:
+            set_rng_state(self._rng_device, rng)
 
 
 # ------------------------------------------------------------------------------------

@@ -28,7 +28,7 @@ import torch
 from ..models import get_workload, prepare_model
 from ..ops.optim import make_optimizer
 from ..parallel.ddp import ElasticDDP
-from ..runtime.elastic import ElasticContext, TorchState, run
+from ..runtime.elastic import ElasticContext, TorchState, rng_state, run, set_rng_state
 from ..runtime.stepgraph import GraphedStepper
 from ..utils.tracing import trace_range
 from .metrics_logger import MetricsCSVLogger
@@ -99,6 +99,8 @@ class _Warm:
                               compression=cfg.compression, reduction=cfg.reduction,
                               overlap_optimizer=cfg.overlap_optimizer)
         self._init = [t.detach().clone() for t in self._tensors()]
+        self._rng0 = rng_state(device)  # generator state right after the seeded build
+        self.device = device
         self.step_graph = None  # world-1 step captured by an earlier job (runtime/stepgraph.py)
 
     def _tensors(self):
@@ -112,6 +114,7 @@ class _Warm:
         self.opt.reset_steps()
         for g in self.opt.param_groups:
             g["lr"] = self.base_lr
+        set_rng_state(self.device, self._rng0)  # a reused model draws the masks a fresh build would
 
 
 _WARM: dict[tuple, _Warm] = {}
