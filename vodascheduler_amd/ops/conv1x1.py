@@ -31,6 +31,13 @@ from . import wgrad as W
 
 USE_CONV1X1_GEMM = os.environ.get("VODA_CONV1X1_GEMM", "1") != "0"
 USE_GRAD_SINK = os.environ.get("VODA_GRAD_SINK", "1") != "0"
+# Opt-in (VODA_CONV1X1_HYBRID=1): for Cin < 128 (ResNet stage 1: 64 -> 256) keep forward and
+# input gradient on MIOpen and send the weight gradient to the split-K kernel, straight into
+# the fp32 flat gradient.  In isolation the kernel matches MIOpen's igemm_wrw (156 vs 155 us)
+# without its workspace clear / cast / fold passes (profiles/raw/r2_wgrad_fp32_vs_hipblaslt.jsonl),
+# but the ResNet-50 step got SLOWER: 27.55 vs 27.28 ms (two interleaved pairs,
+# profiles/raw/r2_ab_conv1x1_hybrid.jsonl) -- so off by default
+USE_CONV1X1_HYBRID = os.environ.get("VODA_CONV1X1_HYBRID", "0") == "1"
 
 
 class GradSink:
@@ -139,6 +146,40 @@ class _Conv1x1Fn(torch.autograd.Function):
         return dx, dw, None, None, None
 
 
+class _Conv1x1HybridFn(torch.autograd.Function):
+    """MIOpen forward / input gradient, split-K MFMA weight gradient (stride 1)."""
+
+    @staticmethod
+    def forward(ctx, x, weight):
+        ctx.save_for_backward(x, weight)
+        return F.conv2d(x, weight)
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, weight = ctx.saved_tensors
+        if not dy.is_contiguous(memory_format=torch.channels_last):
+            dy = dy.contiguous(memory_format=torch.channels_last)
+        dx = None
+        if ctx.needs_input_grad[0]:
+            dx = torch.ops.aten.convolution_backward(dy, x, weight, None, [1, 1], [0, 0], [1, 1], False, [0, 0], 1,
+                                                     [True, False, False])[0]
+        dw = None
+        if ctx.needs_input_grad[1]:
+            cout, cin = weight.shape[0], weight.shape[1]
+            dy2, x2 = _as_2d(dy), _as_2d(x)
+            g2 = flat_grad(weight).view(cout, cin) if _direct(weight) else None
+            if g2 is not None and W.supported(dy2, x2, g2):
+                W.wgrad_accumulate_(dy2, x2, g2)
+                _ready(weight)
+            else:
+                dw = (dy2.t() @ x2).view(cout, cin, 1, 1)
+                if g2 is not None:
+                    g2.add_(dw.view(cout, cin).to(g2.dtype))
+                    _ready(weight)
+                    dw = None
+        return dx, dw
+
+
 class Conv1x1(torch.nn.Conv2d):
     """``nn.Conv2d(cin, cout, 1, stride, bias=False)`` with the GEMM formulation on GPU."""
 
@@ -152,14 +193,25 @@ class Conv1x1(torch.nn.Conv2d):
                 and x.is_contiguous(memory_format=torch.channels_last)
                 and self.in_channels >= 128 and self.in_channels % 8 == 0 and self.out_channels % 8 == 0)
 
+    def _hybrid_ok(self, x: torch.Tensor) -> bool:
+        return (USE_CONV1X1_HYBRID and x.is_cuda and x.dim() == 4 and x.dtype == torch.bfloat16
+                and self.weight.dtype == torch.bfloat16 and self.groups == 1 and self.padding == (0, 0)
+                and self.dilation == (1, 1) and self.stride == (1, 1)
+                and x.is_contiguous(memory_format=torch.channels_last)
+                and self.in_channels % 8 == 0 and self.out_channels >= 128 and self.out_channels % 8 == 0
+                and flat_grad(self.weight) is not None)
+
     def forward(self, x, sink_in: GradSink | None = None, sink_out: GradSink | None = None):
         """``sink_in`` / ``sink_out``: see GradSink.  A caller passes ``sink_in`` only after
         checking ``_gemm_ok(x)`` (the consumer must run on this path); ``sink_out`` is
-        ignored on the fallback path (the gradient is then returned normally)."""
+        ignored on the fallback paths (the gradient is then returned normally)."""
         if x.is_cuda and x.dtype != self.weight.dtype and torch.is_autocast_enabled("cuda"):
             x = x.to(self.weight.dtype)
         if self._gemm_ok(x):
             with torch.autocast("cuda", enabled=False):
                 return _Conv1x1Fn.apply(x, self.weight, self.stride[0], sink_in, sink_out)
         assert sink_in is None, "a GradSink consumer must run on the GEMM path"
+        if self._hybrid_ok(x):
+            with torch.autocast("cuda", enabled=False):
+                return _Conv1x1HybridFn.apply(x, self.weight)
         return super().forward(x)
