@@ -18,6 +18,7 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from vodascheduler_amd.ops.batchnorm import FusedBatchNorm2d  # noqa: E402
 
 # (C, H, residual, relu, count per step) of the ResNet-50 v1.5 BN layers at 224x224
+ITERS = [20]
 SHAPES = [(64, 112, False, True, 1), (64, 56, False, True, 6), (256, 56, True, True, 3), (256, 56, False, False, 1),
           (128, 56, False, True, 1), (128, 28, False, True, 7), (512, 28, True, True, 4), (512, 28, False, False, 1),
           (256, 28, False, True, 1), (256, 14, False, True, 11), (1024, 14, True, True, 6),
@@ -26,6 +27,7 @@ SHAPES = [(64, 112, False, True, 1), (64, 56, False, True, 6), (256, 56, True, T
 
 
 def timeit(fn, iters=20, warmup=3):
+    iters = ITERS[0]
     for _ in range(warmup):
         fn()
     torch.cuda.synchronize()
@@ -42,7 +44,10 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--batch", type=int, default=256)
     ap.add_argument("--tuning", default="", help="deep,blocks,sweep for the reduction passes (A/B)")
+    ap.add_argument("--shapes", default="", help="comma-separated indices into SHAPES (PMC runs)")
+    ap.add_argument("--iters", type=int, default=20)
     a = ap.parse_args()
+    ITERS[0] = a.iters
     if a.tuning:
         from vodascheduler_amd.ops import _native
 
@@ -53,7 +58,8 @@ def main():
     big = torch.empty(1 << 28, dtype=torch.bfloat16, device=dev)
     copy_us = timeit(lambda: big.clone())
     copy_tbs = 2 * big.numel() * 2 / (copy_us * 1e-6) / 1e12
-    for C, H, res, relu, cnt in SHAPES:
+    shapes = [SHAPES[int(i)] for i in a.shapes.split(",")] if a.shapes else SHAPES
+    for C, H, res, relu, cnt in shapes:
         bn = FusedBatchNorm2d(C, relu=relu).to(dev)
         x = torch.randn(a.batch, C, H, H, device=dev).to(torch.bfloat16).to(memory_format=cl).requires_grad_()
         r = torch.randn_like(x).requires_grad_() if res else None

@@ -55,9 +55,17 @@ def blaslt_form(gw, a, b):
 
 
 def main():
+    import argparse
+
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--only", default="", help="substring filter on shape names")
+    ap.add_argument("--no-blaslt", action="store_true")
+    a = ap.parse_args()
     _native.hip()
     dev = torch.device("cuda", 0)
     for name, M, N, K in SHAPES:
+        if a.only and a.only not in name:
+            continue
         torch.manual_seed(0)
         dy = torch.randn(M, N, device=dev).bfloat16()
         x = torch.randn(M, K, device=dev).bfloat16()
@@ -71,6 +79,9 @@ def main():
             r["ours_rel_err"] = float((gw - ref).norm() / ref.norm())
         t = timeit(lambda: W.wgrad_accumulate_(dy, x, gw))
         r["ours_us"], r["ours_tflops"] = round(t, 2), round(tf / (t * 1e-6), 1)
+        if a.no_blaslt:
+            print(json.dumps(r), flush=True)
+            continue
         gw.zero_()
         form, fn = blaslt_form(gw, dy.t(), x)
         torch.cuda.synchronize()
