@@ -4,6 +4,7 @@ nvidia_smi_exporter, README.md:94).  The CSVs are written by the workloads' own
 MetricsCSVLogger, so the producer/consumer contract is tested end to end; the rocm-smi JSON
 is a synthetic document in the rocm-smi 3.x key format (no GPU needed)."""
 import json
+import os
 import time
 
 import pytest
@@ -114,9 +115,48 @@ def test_parse_rocm_smi_json():
 
 
 def test_gpu_exporter_exposition_names():
-    exp = GpuExporter(query=lambda: parse_rocm_smi_json(json.dumps(ROCM_SMI)))
+    exp = GpuExporter(query=lambda: parse_rocm_smi_json(json.dumps(ROCM_SMI)), query_xgmi=None)
     text = exp.exposition().decode()
     for f in GpuExporter.FIELDS:
         assert f"voda_scheduler_gpu_{f}" in text
     assert 'voda_scheduler_gpu_utilization_percent{gpu="0"} 87.0' in text
     assert 'voda_scheduler_gpu_memory_total_bytes{gpu="1"} 3.09220868096e+11' in text
+
+
+FIXTURES = os.path.join(os.path.dirname(__file__), "fixtures")
+
+
+def test_parse_rocm_smi_json_captured_on_mi355x():
+    with open(os.path.join(FIXTURES, "mi355x_rocm_smi_1gpu_box.json")) as f:
+        g = parse_rocm_smi_json(f.read())
+    assert g[0]["memory_total_bytes"] == 309220868096.0  # 288 GiB HBM3E
+    assert g[0]["power_watts"] == 268.0 and g[0]["temperature_celsius"] == 48.0
+
+
+def test_parse_amdsmi_xgmi_captured_on_mi355x():
+    from vodascheduler_amd.collector.gpu_exporter import parse_amdsmi_xgmi_json
+
+    with open(os.path.join(FIXTURES, "mi355x_amdsmi_xgmi_1gpu_box.json")) as f:
+        x = parse_amdsmi_xgmi_json(f.read())
+    assert x[0]["bit_rate_gbps"] == 38.0 and x[0]["max_bandwidth_gbps"] == 608.0
+    # 8 ports: the one facing the GPU itself ("X") is not a link, the other 7 are up
+    assert x[0]["ports"] == {p: 1 for p in range(1, 8)}
+    assert x[0]["read_bytes"] == {} and x[0]["write_bytes"] == {}  # "N/A" in a 1-GPU container
+
+
+def test_xgmi_numeric_link_counters_and_gauges():
+    from vodascheduler_amd.collector.gpu_exporter import parse_amdsmi_xgmi_json
+
+    doc = {"xgmi_metric": [[{"gpu": 1, "link_metrics": {
+        "bit_rate": {"value": 38, "unit": "Gb/s"}, "max_bandwidth": {"value": 608, "unit": "Gb/s"},
+        "links": [{"gpu": 0, "read": {"value": 12, "unit": "KB"}, "write": {"value": 3, "unit": "MB"}},
+                  {"gpu": 2, "read": 7, "write": "N/A"}]}}]],
+        "link_port_status": [{"gpu": 1, "link_status": ["U", "X", "D"]}]}
+    x = parse_amdsmi_xgmi_json(json.dumps(doc))
+    assert x[1]["read_bytes"] == {0: 12e3, 2: 7.0} and x[1]["write_bytes"] == {0: 3e6}
+    assert x[1]["ports"] == {0: 1, 2: 0}
+    exp = GpuExporter(query=lambda: {}, query_xgmi=lambda: x)
+    text = exp.exposition().decode()
+    assert 'voda_scheduler_gpu_xgmi_max_bandwidth_gbps{gpu="1"} 608.0' in text
+    assert 'voda_scheduler_gpu_xgmi_link_up{gpu="1",port="2"} 0.0' in text
+    assert 'voda_scheduler_gpu_xgmi_read_bytes{gpu="1",peer="0"} 12000.0' in text
