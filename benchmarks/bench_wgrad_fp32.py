@@ -60,6 +60,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--only", default="", help="substring filter on shape names")
     ap.add_argument("--no-blaslt", action="store_true")
+    ap.add_argument("--sweep", action="store_true", help="time every variant x split count (no hipBLASLt)")
     a = ap.parse_args()
     _native.hip()
     dev = torch.device("cuda", 0)
@@ -79,6 +80,23 @@ def main():
             r["ours_rel_err"] = float((gw - ref).norm() / ref.norm())
         t = timeit(lambda: W.wgrad_accumulate_(dy, x, gw))
         r["ours_us"], r["ours_tflops"] = round(t, 2), round(tf / (t * 1e-6), 1)
+        if a.sweep:
+            best = None
+            for v in range(0, 9):
+                base = W.default_splits(M, N, K, variant=v)
+                for sp in sorted({max(1, base // 4), max(1, base // 2), base, min(256, base * 2)}):
+                    try:
+                        t = timeit(lambda: W.wgrad_accumulate_(dy, x, gw, splits=sp, variant=v), iters=10, warm=2)
+                    except Exception as e:  # a variant may reject a shape
+                        r[f"v{v}_s{sp}"] = f"error: {e}"[:60]
+                        continue
+                    r[f"v{v}_s{sp}"] = round(t, 1)
+                    if best is None or t < best[0]:
+                        best = (t, v, sp)
+            r["best_us"], r["best_variant"], r["best_splits"] = round(best[0], 2), best[1], best[2]
+            r["best_TBs"] = round(2 * M * (N + K) / (best[0] * 1e-6) / 1e12, 2)
+            print(json.dumps(r), flush=True)
+            continue
         if a.no_blaslt:
             print(json.dumps(r), flush=True)
             continue

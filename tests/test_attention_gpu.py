@@ -174,3 +174,39 @@ def test_bert_residual_grad_sink_gpu(monkeypatch):
     for n in g0:
         rel = float((g1[n] - g0[n]).norm() / g0[n].norm().clamp_min(1e-12))
         assert rel < 3e-2, (n, rel)
+
+
+class _NanTorch:
+    """``torch`` stand-in for ops/flash.py whose empty / empty_like return NaN-filled tensors:
+    every output element a kernel fails to write stays NaN (fresh device memory is often zero,
+    which hides such gaps; a replayed hipGraph reuses memory that is not)."""
+
+    def __getattr__(self, k):
+        return getattr(torch, k)
+
+    @staticmethod
+    def empty(*a, **kw):
+        return torch.full_like(torch.empty(*a, **kw), float("nan"))
+
+    @staticmethod
+    def empty_like(t, **kw):
+        return torch.full_like(t, float("nan"), **kw)
+
+
+@pytest.mark.parametrize("B,Tq,Tk,H,D,causal", [(16, 20, 20, 8, 256, False), (16, 20, 20, 8, 256, True),
+                                                (4, 77, 45, 4, 64, False), (2, 130, 200, 2, 128, False)])
+def test_attention_writes_every_output_element(B, Tq, Tk, H, D, causal, monkeypatch):
+    monkeypatch.setattr(flash, "torch", _NanTorch())
+    torch.manual_seed(3)
+    q = torch.randn(B, Tq, H, D, device="cuda").to(torch.bfloat16).requires_grad_()
+    kv = torch.randn(B, Tk, 2, H, D, device="cuda").to(torch.bfloat16).requires_grad_()
+    km = _mask(B, Tk, "cuda")
+    km[:, -3:] = False  # the NMT batches' padded tail
+    o = attention_q_kvpacked(q, kv, km, causal, D ** -0.5)
+    assert torch.isfinite(o.float()).all()
+    o.backward(torch.randn_like(o))
+    assert torch.isfinite(q.grad.float()).all() and torch.isfinite(kv.grad.float()).all()
+    qf, kvf = q.detach().float().requires_grad_(), kv.detach().float().requires_grad_()
+    ref = ref_attn(qf.transpose(1, 2), kvf[:, :, 0].transpose(1, 2), kvf[:, :, 1].transpose(1, 2), km, causal,
+                   D ** -0.5).transpose(1, 2)
+    torch.testing.assert_close(o.float(), ref, atol=2e-2, rtol=2e-2)

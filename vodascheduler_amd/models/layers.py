@@ -14,7 +14,6 @@ import math
 import os
 
 import torch
-import torch.nn.functional as F
 from torch import nn
 
 from ..ops.activation import GeluTanh
@@ -32,18 +31,25 @@ HIP_GELU = os.environ.get("VODA_HIP_GELU", "1") != "0"
 
 class MultiHeadAttention(nn.Module):
     def __init__(self, d_model: int, num_heads: int, key_dim: int | None = None, dropout: float = 0.0,
-                 bias: bool = True):
+                 bias: bool = True, cross: bool = False):
         super().__init__()
         self.h = num_heads
         self.dk = key_dim or d_model // num_heads
         inner = self.h * self.dk
-        # Q, K and V projections as ONE [d_model -> 3*inner] GEMM (self-attention) and the
-        # K/V pair as one [d_model -> 2*inner] GEMM (cross-attention): the weight-gradient
-        # GEMMs (K = batch*tokens) of 768x768 outputs tile only 36 128x128 blocks on 256
-        # CUs and ran at ~190 TFLOP/s on MI355X (profiles/); the fused 2304-wide one is
-        # 3x the tiles.  The fused weights are the concatenation of Keras/PyTorch's
-        # separate q/k/v kernels.
-        self.qkv = FusedLinear(d_model, 3 * inner, bias=bias)
+        # Self-attention: Q, K and V projections as ONE [d_model -> 3*inner] GEMM; the
+        # weight-gradient GEMMs (K = batch*tokens) of 768x768 outputs tile only 36 128x128
+        # blocks on 256 CUs and ran at ~190 TFLOP/s on MI355X (profiles/), the fused 2304-wide
+        # one is 3x the tiles.  Cross-attention (``cross=True``): a Q projection of the query
+        # stream and ONE [d_model -> 2*inner] K/V projection of the memory, each its own
+        # FusedLinear, so both gradients go straight into the flat fp32 buffers (an earlier
+        # version sliced one packed weight and let autograd assemble the slice gradients).
+        # The fused weights are the concatenation of Keras/PyTorch's separate q/k/v kernels.
+        self.cross = cross
+        if cross:
+            self.q = FusedLinear(d_model, inner, bias=bias)
+            self.kv = FusedLinear(d_model, 2 * inner, bias=bias)
+        else:
+            self.qkv = FusedLinear(d_model, 3 * inner, bias=bias)
         self.o = FusedLinear(inner, d_model, bias=bias)
         self.inner = inner
         self.dropout = dropout
@@ -60,10 +66,11 @@ class MultiHeadAttention(nn.Module):
             qkv = self.qkv(x, sink_in).view(B, Tq, 3, self.h, self.dk)
             o = attention_qkvpacked(qkv, key_mask, causal, scale, drop)
         else:
+            if not self.cross:
+                raise ValueError("kv given to a self-attention module (build it with cross=True)")
             Tk = kv.shape[1]
-            w, b = self.qkv.weight, self.qkv.bias
-            q = F.linear(x, w[:E], None if b is None else b[:E]).view(B, Tq, self.h, self.dk)
-            kvp = F.linear(kv, w[E:], None if b is None else b[E:]).view(B, Tk, 2, self.h, self.dk)
+            q = self.q(x).view(B, Tq, self.h, self.dk)
+            kvp = self.kv(kv).view(B, Tk, 2, self.h, self.dk)
             o = attention_q_kvpacked(q, kvp, key_mask, causal, scale, drop)
         return self.o(o.reshape(B, Tq, E))
 
@@ -116,7 +123,7 @@ class DecoderLayer(nn.Module):
         super().__init__()
         self.self_attn = MultiHeadAttention(d_model, heads, key_dim, dropout)
         self.ln1 = FusedLayerNorm(d_model, eps=eps)
-        self.cross = MultiHeadAttention(d_model, heads, key_dim, dropout)
+        self.cross = MultiHeadAttention(d_model, heads, key_dim, dropout, cross=True)
         self.ln2 = FusedLayerNorm(d_model, eps=eps)
         self.ff = FeedForward(d_model, d_ff)
         self.ln3 = FusedLayerNorm(d_model, eps=eps)
