@@ -23,6 +23,20 @@ TILE = 128
 # tile, 8 waves, ring of 4 x 32 / 2 x 64 / 3 x 32 tokens.  Default 2 (64 KB ring, 2 workgroups per CU): fastest in the BERT-base step
 # on MI355X (profiles/r1_wgrad_v3.md)
 VARIANT = int(os.environ.get("VODA_WGRAD_VARIANT", "2"))
+# VODA_WGRAD_VARIANT set explicitly = that variant for every shape (A/B runs); otherwise
+# tall convolution-sized reductions use the deeper LDS rings at half the default split count
+# (per-shape sweep on MI355X, fp32 output, profiles/raw/r2_wgrad_variant_split_sweep.jsonl:
+# ResNet-50 stage 1 (M = 802816) 150-155 -> 131-137 us with variant 1, stage 2 (M = 200704)
+# 95-96 -> 79 us with variant 3; stages 3-4 and the BERT shapes gain nothing)
+_VARIANT_FIXED = "VODA_WGRAD_VARIANT" in os.environ
+
+
+def choose(M: int, N_: int, K: int) -> tuple[int, int]:
+    """(variant, splits) for a weight-gradient GEMM of M reduction rows."""
+    if _VARIANT_FIXED or M < 150_000:
+        return VARIANT, default_splits(M, N_, K, variant=VARIANT)
+    v = 1 if M >= 600_000 else 3
+    return v, max(1, default_splits(M, N_, K, variant=v) // 2)
 _ZERO: dict[torch.device, torch.Tensor] = {}
 
 
@@ -103,8 +117,11 @@ def wgrad_accumulate_(dy2: torch.Tensor, x2: torch.Tensor, gw: torch.Tensor, gb:
                          f"x {tuple(x2.shape)} {x2.dtype} stride {x2.stride()}, dw {tuple(gw.shape)} {gw.dtype}")
     M, N_ = dy2.shape
     K = x2.shape[1]
-    v = VARIANT if variant is None else int(variant)
-    s = splits if splits is not None else default_splits(M, N_, K, variant=v)
+    if variant is None and splits is None:
+        v, s = choose(M, N_, K)
+    else:
+        v = VARIANT if variant is None else int(variant)
+        s = splits if splits is not None else default_splits(M, N_, K, variant=v)
     h = N.hip()
     nws = h.wgrad_workspace_floats(M, N_, K, s)
     ws = torch.empty(nws, dtype=torch.float32, device=dy2.device) if nws else None
