@@ -90,11 +90,18 @@ __device__ __forceinline__ bf16x8 acc_frag(const f32x16& x, int s) {
   return f;
 }
 
+// Transposed LDS images store row d's 32 keys rotated by 8 * ((d >> 3) & 3) (mod 32): the
+// staging writes (8 lanes of a wave-instruction on rows 8 apart) then spread over 16 banks
+// instead of one -- 16-way -> 4-way write conflicts -- and the fragment reads of lanes r and
+// r + 16 (rows 16 apart) no longer share banks.  Groups of 4 keys stay contiguous.
+__device__ __forceinline__ int trans_rot(int d) { return 8 * ((d >> 3) & 3); }
+
 // Operand paired with an accumulator fragment: element j of lane half h must come from
-// k-row 16s + 8(j>>2) + 4h + (j&3).  ``rowT`` points at a transposed LDS row (k contiguous).
-__device__ __forceinline__ bf16x8 perm_frag(const uint16_t* rowT, int s, int h) {
-  const uint2 lo = *reinterpret_cast<const uint2*>(rowT + 16 * s + 4 * h);
-  const uint2 hi = *reinterpret_cast<const uint2*>(rowT + 16 * s + 8 + 4 * h);
+// k-row 16s + 8(j>>2) + 4h + (j&3).  ``rowT`` points at transposed LDS row d (k contiguous,
+// rotated by ``rot`` = trans_rot(d)).
+__device__ __forceinline__ bf16x8 perm_frag(const uint16_t* rowT, int s, int h, int rot) {
+  const uint2 lo = *reinterpret_cast<const uint2*>(rowT + ((16 * s + 4 * h + rot) & 31));
+  const uint2 hi = *reinterpret_cast<const uint2*>(rowT + ((16 * s + 8 + 4 * h + rot) & 31));
   return __builtin_bit_cast(bf16x8, make_uint4(lo.x, lo.y, hi.x, hi.y));
 }
 
@@ -113,8 +120,9 @@ __device__ __forceinline__ void stage_tile(const uint16_t* __restrict__ g, int64
       const uint32_t w[4] = {u.x, u.y, u.z, u.w};
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
-        trans[(c + 2 * k) * tstride + r] = uint16_t(w[k] & 0xffff);
-        trans[(c + 2 * k + 1) * tstride + r] = uint16_t(w[k] >> 16);
+        const int d0 = c + 2 * k, d1 = d0 + 1;
+        trans[d0 * tstride + ((r + trans_rot(d0)) & 31)] = uint16_t(w[k] & 0xffff);
+        trans[d1 * tstride + ((r + trans_rot(d1)) & 31)] = uint16_t(w[k] >> 16);
       }
     }
   }
@@ -205,8 +213,8 @@ __global__ __launch_bounds__(64 * W) void attn_fwd_kernel(AttnArgs a) {
 #pragma unroll
     for (int t = 0; t < DT; ++t) {
       const uint16_t* vrow = Vt + (32 * t + r) * TS;
-      o[t] = mfma(perm_frag(vrow, 0, h), p0, o[t]);
-      o[t] = mfma(perm_frag(vrow, 1, h), p1, o[t]);
+      o[t] = mfma(perm_frag(vrow, 0, h, trans_rot(r)), p0, o[t]);
+      o[t] = mfma(perm_frag(vrow, 1, h, trans_rot(r)), p1, o[t]);
     }
   }
   const float inv = 1.f / l;
@@ -272,8 +280,8 @@ __global__ __launch_bounds__(64 * W) void attn_bwd_dq_kernel(AttnArgs a) {
 #pragma unroll
     for (int t = 0; t < DT; ++t) {
       const uint16_t* krow = Kt + (32 * t + r) * TS;
-      dq[t] = mfma(perm_frag(krow, 0, h), d0, dq[t]);
-      dq[t] = mfma(perm_frag(krow, 1, h), d1, dq[t]);
+      dq[t] = mfma(perm_frag(krow, 0, h, trans_rot(r)), d0, dq[t]);
+      dq[t] = mfma(perm_frag(krow, 1, h, trans_rot(r)), d1, dq[t]);
     }
   }
   uint16_t* base = a.out + b * a.out_sb + hh * a.out_sh;
@@ -353,8 +361,8 @@ __global__ __launch_bounds__(64 * W) void attn_bwd_dkv_kernel(AttnArgs a) {
 #pragma unroll
       for (int t = 0; t < DT; ++t) {
         const uint16_t* drow = Dt + (32 * t + r) * TS;  // dO^T row (d = 32t + r)
-        dv[t] = mfma(p0, perm_frag(drow, 0, h), dv[t]);
-        dv[t] = mfma(p1, perm_frag(drow, 1, h), dv[t]);
+        dv[t] = mfma(p0, perm_frag(drow, 0, h, trans_rot(r)), dv[t]);
+        dv[t] = mfma(p1, perm_frag(drow, 1, h, trans_rot(r)), dv[t]);
       }
     }
     if constexpr (DO_DK) {
@@ -362,8 +370,8 @@ __global__ __launch_bounds__(64 * W) void attn_bwd_dkv_kernel(AttnArgs a) {
 #pragma unroll
       for (int t = 0; t < DT; ++t) {
         const uint16_t* qrow = Qt + (32 * t + r) * TS;  // Q^T row
-        dk[t] = mfma(g0, perm_frag(qrow, 0, h), dk[t]);
-        dk[t] = mfma(g1, perm_frag(qrow, 1, h), dk[t]);
+        dk[t] = mfma(g0, perm_frag(qrow, 0, h, trans_rot(r)), dk[t]);
+        dk[t] = mfma(g1, perm_frag(qrow, 1, h, trans_rot(r)), dk[t]);
       }
     }
   }
