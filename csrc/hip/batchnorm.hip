@@ -506,22 +506,25 @@ Grid bn_grid(int64_t M, int C, int64_t cap_blocks, int iters_per_block) {
   return {dim3(unsigned(nb), unsigned(slices)), int(nb)};
 }
 
-// Tuning knobs of the reduction passes, read once (A/B runs: benchmarks/bench_bn_passes.py):
-//   VODA_BN_UNROLL=0   rows in flight 4 (stats) / 2 (backward reduce) instead of 8 / 4
-//   VODA_BN_BLOCKS=n   reduction grid cap (default 1024 = 4 blocks of 4 waves per CU)
-//   VODA_BN_SWEEP=1    grid-sweep reduction + mirrored apply order (MALL reuse, see Walk)
-// Measured on the ResNet-50 bs-256 step (profiles/r2_bn_reduce_ab.md): buffer-descriptor loads
-// 27.27 ms vs 27.32 ms for the round-1 flat-address kernels (3 interleaved pairs); grid cap
-// 1024 vs 2048: 27.41 vs 27.73 ms; sweep order: no gain (27.75 ms).
+// Tuning knobs of the reduction passes, read once (A/B runs: benchmarks/bench_bn_passes.py,
+// benchmarks/gpu_r2_bn_trace.sh for per-shape dispatch times):
+//   VODA_BN_UNROLL=0|1|2  rows in flight 4 / 8 / 16 (stats) and 2 / 4 / 8 (backward reduce)
+//   VODA_BN_BLOCKS=n      reduction grid cap (default 256 = one 4-wave block per CU)
+//   VODA_BN_SWEEP=0|1     grid-sweep reduction + mirrored apply order (default 1, see Walk)
+// Measured on MI355X (profiles/raw/r2_bn_grid_trace.md, ResNet-50 bs-256 step A/B in
+// profiles/raw/r2_ab_bn_grid.jsonl): the reduction passes of the large tensors ran at 3.8-4.2
+// TB/s with 1024 long-lived blocks each walking its own chunk; one block per CU sweeping
+// the tensor together brings the per-step stats + reduce + finalize time 4.64 -> 4.02 ms,
+// and the step 26.95 -> 26.23 ms.  Unroll level 2 and grids of 384-2048 blocks are slower.
 struct BnTune {
-  bool deep;
+  int deep;  // rows in flight: 0 -> 4 (stats) / 2 (backward reduce), 1 -> 8 / 4, 2 -> 16 / 8
   int blocks;
   int sweep;
 };
 BnTune& bn_tune() {
   static BnTune t = [] {
-    BnTune v{true, 1024, 0};
-    if (const char* e = std::getenv("VODA_BN_UNROLL")) v.deep = e[0] != '0';
+    BnTune v{1, 256, 1};
+    if (const char* e = std::getenv("VODA_BN_UNROLL")) v.deep = std::max(0, std::min(2, std::atoi(e)));
     if (const char* e = std::getenv("VODA_BN_BLOCKS")) v.blocks = std::max(64, std::min(8192, std::atoi(e)));
     if (const char* e = std::getenv("VODA_BN_SWEEP")) v.sweep = e[0] == '1' ? 1 : 0;
     return v;
@@ -535,7 +538,7 @@ Grid reduce_grid(int64_t M, int C) {
   return bn_grid(M, C, cap, 8);
 }
 
-bool bn_deep_unroll() { return bn_tune().deep; }
+int bn_unroll_level() { return bn_tune().deep; }
 
 template <typename F>
 void dispatch_dt(int dt, F&& f) {
@@ -549,14 +552,14 @@ void dispatch_dt(int dt, F&& f) {
 
 void bn_set_tuning(int deep, int blocks, int sweep) {
   BnTune& t = bn_tune();
-  if (deep >= 0) t.deep = deep != 0;
+  if (deep >= 0) t.deep = std::min(2, deep);
   if (blocks > 0) t.blocks = std::max(64, std::min(8192, blocks));
   if (sweep >= 0) t.sweep = sweep != 0;
 }
 
 std::vector<int> bn_get_tuning() {
   const BnTune& t = bn_tune();
-  return {int(t.deep), t.blocks, t.sweep};
+  return {t.deep, t.blocks, t.sweep};
 }
 
 int64_t bn_workspace_floats(int64_t M, int C) {
@@ -579,7 +582,10 @@ void bn_fwd_train(uintptr_t x, uintptr_t residual, uintptr_t gamma, uintptr_t be
   dispatch_dt(dt, [&](auto tag) {
     using T = decltype(tag);
     const T* xp = reinterpret_cast<const T*>(x);
-    if (bn_deep_unroll())
+    const int lv = bn_unroll_level();
+    if (lv >= 2)
+      hipLaunchKernelGGL((bn_stats_kernel<T, 16>), rg.grid, dim3(kBlock), 0, s, xp, ws, M, C, sw);
+    else if (lv == 1)
       hipLaunchKernelGGL((bn_stats_kernel<T, 8>), rg.grid, dim3(kBlock), 0, s, xp, ws, M, C, sw);
     else
       hipLaunchKernelGGL((bn_stats_kernel<T, 4>), rg.grid, dim3(kBlock), 0, s, xp, ws, M, C, sw);
@@ -640,11 +646,23 @@ void bn_bwd(uintptr_t dy, uintptr_t mask, uintptr_t x, uintptr_t save_mean, uint
     const T* dyp = reinterpret_cast<const T*>(dy);
     const uint8_t* yp = reinterpret_cast<const uint8_t*>(mask);
     const T* xp = reinterpret_cast<const T*>(x);
-    const bool deep = bn_deep_unroll();
-    if (relu && deep) hipLaunchKernelGGL((bn_bwd_reduce_kernel<T, true, 4>), rg.grid, dim3(kBlock), 0, s, dyp, yp, xp, ws, M, C, sw);
-    else if (relu) hipLaunchKernelGGL((bn_bwd_reduce_kernel<T, true, 2>), rg.grid, dim3(kBlock), 0, s, dyp, yp, xp, ws, M, C, sw);
-    else if (deep) hipLaunchKernelGGL((bn_bwd_reduce_kernel<T, false, 4>), rg.grid, dim3(kBlock), 0, s, dyp, yp, xp, ws, M, C, sw);
-    else hipLaunchKernelGGL((bn_bwd_reduce_kernel<T, false, 2>), rg.grid, dim3(kBlock), 0, s, dyp, yp, xp, ws, M, C, sw);
+    const int lv = bn_unroll_level();
+    auto red = [&](auto relu_c, auto u_c) {
+      constexpr bool RL = decltype(relu_c)::value;
+      constexpr int UU = decltype(u_c)::value;
+      hipLaunchKernelGGL((bn_bwd_reduce_kernel<T, RL, UU>), rg.grid, dim3(kBlock), 0, s, dyp, yp, xp, ws, M, C, sw);
+    };
+    using RT = std::true_type;
+    using RF = std::false_type;
+    if (relu) {
+      if (lv >= 2) red(RT{}, std::integral_constant<int, 8>{});
+      else if (lv == 1) red(RT{}, std::integral_constant<int, 4>{});
+      else red(RT{}, std::integral_constant<int, 2>{});
+    } else {
+      if (lv >= 2) red(RF{}, std::integral_constant<int, 8>{});
+      else if (lv == 1) red(RF{}, std::integral_constant<int, 4>{});
+      else red(RF{}, std::integral_constant<int, 2>{});
+    }
     hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + kFinCh - 1) / kFinCh), dim3(kFinCh * kFinRg), 0, s, ws,
                        rg.nb, M, C, reinterpret_cast<const float*>(gamma), reinterpret_cast<const float*>(save_mean),
                        reinterpret_cast<const float*>(save_invstd), reinterpret_cast<float*>(dgamma),
