@@ -520,6 +520,8 @@ struct BnTune {
   int deep;  // rows in flight: 0 -> 4 (stats) / 2 (backward reduce), 1 -> 8 / 4, 2 -> 16 / 8
   int blocks;
   int sweep;
+  int apply_cap = 8192;   // apply-pass grid cap (VODA_BN_APPLY_CAP)
+  int apply_iters = 4;    // row iterations per apply block (VODA_BN_APPLY_ITERS)
 };
 BnTune& bn_tune() {
   static BnTune t = [] {
@@ -527,10 +529,14 @@ BnTune& bn_tune() {
     if (const char* e = std::getenv("VODA_BN_UNROLL")) v.deep = std::max(0, std::min(2, std::atoi(e)));
     if (const char* e = std::getenv("VODA_BN_BLOCKS")) v.blocks = std::max(64, std::min(8192, std::atoi(e)));
     if (const char* e = std::getenv("VODA_BN_SWEEP")) v.sweep = e[0] == '1' ? 1 : 0;
+    if (const char* e = std::getenv("VODA_BN_APPLY_CAP")) v.apply_cap = std::max(256, std::atoi(e));
+    if (const char* e = std::getenv("VODA_BN_APPLY_ITERS")) v.apply_iters = std::max(1, std::atoi(e));
     return v;
   }();
   return t;
 }
+
+Grid apply_grid(int64_t M, int C) { return bn_grid(M, C, bn_tune().apply_cap, bn_tune().apply_iters); }
 
 // partial-sum blocks: bounded so that the partial arrays stay <= 2M floats each
 Grid reduce_grid(int64_t M, int C) {
@@ -577,7 +583,7 @@ void bn_fwd_train(uintptr_t x, uintptr_t residual, uintptr_t gamma, uintptr_t be
   float* ws = reinterpret_cast<float*>(workspace);
   const Grid rg = reduce_grid(M, C);
   float* ab = ws + int64_t(2) * rg.nb * C;
-  const Grid ag = bn_grid(M, C, 8192, 4);
+  const Grid ag = apply_grid(M, C);
   const int sw = bn_tune().sweep;
   dispatch_dt(dt, [&](auto tag) {
     using T = decltype(tag);
@@ -611,7 +617,7 @@ void bn_apply(uintptr_t x, uintptr_t residual, uintptr_t ab, uintptr_t y, int64_
               uintptr_t stream) {
   VODA_CHECK(C % kVec == 0, "batchnorm: C must be a multiple of 8");
   hipStream_t s = as_stream(stream);
-  const Grid ag = bn_grid(M, C, 8192, 4);
+  const Grid ag = apply_grid(M, C);
   const float* abp = reinterpret_cast<const float*>(ab);
   dispatch_dt(dt, [&](auto tag) {
     using T = decltype(tag);
@@ -639,7 +645,7 @@ void bn_bwd(uintptr_t dy, uintptr_t mask, uintptr_t x, uintptr_t save_mean, uint
   float* ws = reinterpret_cast<float*>(workspace);
   const Grid rg = reduce_grid(M, C);
   float* k3 = ws + int64_t(2) * rg.nb * C;
-  const Grid ag = bn_grid(M, C, 8192, 4);
+  const Grid ag = apply_grid(M, C);
   const int sw = bn_tune().sweep;
   dispatch_dt(dt, [&](auto tag) {
     using T = decltype(tag);
