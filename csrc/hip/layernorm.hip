@@ -11,6 +11,8 @@
 //     then combines the 4 waves through LDS and writes ONE partial row per block;
 //     a second small kernel sums those partials per column.
 #include "common.h"
+
+#include <cstdlib>
 #include "ops.h"
 
 namespace voda {
@@ -301,9 +303,21 @@ void layernorm_fwd(uintptr_t x, uintptr_t gamma, uintptr_t beta, uintptr_t y, ui
   check_launch();
 }
 
+// Backward grid cap = rows of fp32 dgamma/dbeta partials (VODA_LN_BWD_BLOCKS, A/B switch):
+// 256 blocks of 4 waves is ONE wave per SIMD, each walking M / 1024 rows with R rows of loads
+// in flight; more blocks put more waves (and loads) per SIMD at the cost of more partial rows
+// for col_sum_kernel to add up.
+int ln_bwd_block_cap() {
+  static const int cap = [] {
+    const char* e = std::getenv("VODA_LN_BWD_BLOCKS");
+    return e ? std::max(64, std::min(4096, std::atoi(e))) : 256;
+  }();
+  return cap;
+}
+
 int layernorm_bwd_partial_rows(int64_t M) {
   int64_t g = (M + 3) / 4;
-  return int(std::max<int64_t>(1, std::min<int64_t>(g, 256)));
+  return int(std::max<int64_t>(1, std::min<int64_t>(g, ln_bwd_block_cap())));
 }
 
 void layernorm_bwd(uintptr_t dy, uintptr_t x, uintptr_t mean, uintptr_t rstd, uintptr_t gamma, uintptr_t dx,
