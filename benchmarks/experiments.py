@@ -74,7 +74,7 @@ def main():
     lines = ["# BASELINE.json configs in the discrete-event simulator (round 2)", "",
              "Real scheduler / allocator / placement code driven in virtual time (`benchmarks/experiments.py`). "
              "Job speed model (`vodascheduler_amd/sim/trace.py`): single-GPU step times MEASURED on MI355X for "
-             "ResNet-50 and BERT-base (`benchmarks/model_step.py`, fp32 gradients), estimated for the others; "
+             "every workload but the PyTorch MNIST net (`benchmarks/model_step.py`, fp32 gradients, eager step); "
              "fp32 gradient bytes exact; ring all-reduce bus bandwidth ASSUMED "
              f"({ASSUMED_BUSBW_GBS:.0f} GB/s intra-node, {ASSUMED_INTERNODE_BUSBW_GBS:.0f} GB/s across nodes) until "
              "the 8-GPU bench measures it; 30 % of a step hides the all-reduce.  Resize pause 5 s, "

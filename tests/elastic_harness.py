@@ -68,12 +68,14 @@ class Controller:
         self.wait(lambda: self.rdzv.outcome() is not None, timeout, "job outcome")
         return self.rdzv.outcome()
 
-    @staticmethod
-    def wait(cond, timeout: float, what: str) -> None:
+    def wait(self, cond, timeout: float, what: str) -> None:
         deadline = time.monotonic() + timeout
         while not cond():
             if time.monotonic() > deadline:
-                raise TimeoutError(f"timed out waiting for {what}")
+                r = self.rdzv
+                raise TimeoutError(f"timed out waiting for {what} (progress={self.progress()} "
+                                   f"latest_epoch={r.latest_epoch()} live_epoch={r.get_live_epoch()} "
+                                   f"outcome={r.outcome()} ckpt={r.get_ckpt()})")
             time.sleep(0.005)
 
 

@@ -87,6 +87,7 @@ class ElasticContext:
         # after a failed collective only a NEWER epoch can be joined: the failed one still
         # lists the dead peer, and rebuilding its communicator would block until timeout
         self.min_epoch = 0
+        self.agreed_epoch = 0   # the epoch a commit's agreement interrupted for (0 = none)
         self.cache_comms = os.environ.get("VODA_COMM_CACHE", "1") != "0"
 
     # ---------------------------------------------------------------- watcher
@@ -346,6 +347,10 @@ class State:
     def check_host_updates(self) -> None:
         e = self.ctx.agree_on_epoch()
         if e > self.ctx.epoch:
+            # every member hands off against the AGREED epoch: a member whose own watcher has
+            # not polled the store yet would otherwise see the old membership in _transition,
+            # skip the at-rest checkpoint of a halt and leave with nobody holding the state
+            self.ctx.agreed_epoch = e
             raise HostsUpdatedInterrupt()
 
     # -- sync on (re)join --
@@ -560,7 +565,8 @@ def run(func: Callable) -> Callable:
 def _transition(state: State) -> bool:
     """At an agreed interrupt: hand off the state if nobody survives; False = leave."""
     ctx = state.ctx
-    new_e = ctx.latest_seen()
+    new_e = ctx.agreed_epoch or ctx.latest_seen()
+    ctx.agreed_epoch = 0
     new_members = ctx.rdzv.members(new_e) if new_e > 0 else []
     survivors = [m for m in ctx.members if m in new_members]
     if not survivors and ctx.rank == 0:

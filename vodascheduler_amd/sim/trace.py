@@ -61,19 +61,23 @@ class ModelProfile:
         return n / (1.0 + self.alpha * (n - 1))
 
 
-# step_time_1gpu: MI355X measurements (benchmarks/model_step.py, bf16 autocast, fp32 flat
-# gradients, profiles/r2_*): ResNet-50 bs256 and BERT-base bs64 seq128.  The others are the
-# round-1 estimates (marked measured=False).  grad_mb = 4 bytes x parameter count.
+# step_time_1gpu: MI355X measurements of the eager step (benchmarks/model_step.py, bf16
+# autocast, fp32 flat gradients; profiles/r2_*, docs/PERFORMANCE.md), end of round 2:
+# ResNet-50 bs256 26.2 ms, BERT-base bs64 seq128 11.45 ms, VGG16 bs128 2.63 ms, NMT
+# Transformer bs512 5.24 ms, ResNet-50-CIFAR bs128 14.3 ms, ResNet-18 bs256 10.05 ms,
+# InceptionV3 bs128 13.5 ms, Keras MNIST 0.74 ms.  mnist-torch is an estimate
+# (measured=False).  grad_mb = 4 bytes x parameter count; alpha is only the fallback when
+# grad_mb is unknown (the speed model prices the all-reduce from grad_mb and an ASSUMED busbw).
 PROFILES = {
-    "resnet50": ModelProfile("resnet50", alpha=0.01, step_time_1gpu=0.0277, grad_mb=102.2, measured=True),
-    "bert-base": ModelProfile("bert-base", alpha=0.05, step_time_1gpu=0.0119, grad_mb=438.0, measured=True),
-    "vgg16": ModelProfile("vgg16", alpha=0.08, step_time_1gpu=0.030, grad_mb=134.6),
-    "transformer": ModelProfile("transformer", alpha=0.10, step_time_1gpu=0.020, grad_mb=79.8),
-    "mnist": ModelProfile("mnist", alpha=0.30, step_time_1gpu=0.004, grad_mb=4.8),
+    "resnet50": ModelProfile("resnet50", alpha=0.01, step_time_1gpu=0.0262, grad_mb=102.2, measured=True),
+    "bert-base": ModelProfile("bert-base", alpha=0.05, step_time_1gpu=0.01145, grad_mb=438.0, measured=True),
+    "vgg16": ModelProfile("vgg16", alpha=0.08, step_time_1gpu=0.00263, grad_mb=134.6, measured=True),
+    "transformer": ModelProfile("transformer", alpha=0.10, step_time_1gpu=0.00524, grad_mb=79.8, measured=True),
+    "mnist": ModelProfile("mnist", alpha=0.30, step_time_1gpu=0.00074, grad_mb=4.8, measured=True),
     "mnist-torch": ModelProfile("mnist-torch", alpha=0.40, step_time_1gpu=0.002, grad_mb=0.087),
-    "resnet50-cifar": ModelProfile("resnet50-cifar", alpha=0.05, step_time_1gpu=0.020, grad_mb=94.1),
-    "resnet18": ModelProfile("resnet18", alpha=0.04, step_time_1gpu=0.020, grad_mb=46.8),
-    "inceptionv3": ModelProfile("inceptionv3", alpha=0.05, step_time_1gpu=0.030, grad_mb=87.2),
+    "resnet50-cifar": ModelProfile("resnet50-cifar", alpha=0.05, step_time_1gpu=0.0143, grad_mb=94.1, measured=True),
+    "resnet18": ModelProfile("resnet18", alpha=0.04, step_time_1gpu=0.01005, grad_mb=46.8, measured=True),
+    "inceptionv3": ModelProfile("inceptionv3", alpha=0.05, step_time_1gpu=0.0135, grad_mb=87.3, measured=True),
 }
 
 
