@@ -23,7 +23,7 @@ from vodascheduler_amd.runtime.stepgraph import GraphedStepper  # noqa: E402
 
 
 def run(model: str, batch: int | None, steps: int, warmup: int, marker: bool = False, graph: bool = False,
-        grad_dtype: str = "fp32", overlap_opt: bool = False) -> dict:
+        grad_dtype: str = "fp32", overlap_opt: bool = False, torch_profile: str | None = None) -> dict:
     dev = torch.device("cuda", 0)
     w = get_workload(model)
     bs = batch or w.per_gpu_batch
@@ -67,6 +67,20 @@ def run(model: str, batch: int | None, steps: int, warmup: int, marker: bool = F
         loss = step()
     torch.cuda.synchronize(dev)
     dt = (time.perf_counter() - t0) / steps
+    if torch_profile:  # which aten op launched each library / PyTorch kernel, by input shape
+        from torch.profiler import ProfilerActivity, profile
+
+        with profile(activities=[ProfilerActivity.CPU, ProfilerActivity.CUDA], record_shapes=True) as prof:
+            for _ in range(3):
+                step()
+            torch.cuda.synchronize(dev)
+        with open(torch_profile, "w") as f:
+            f.write(prof.key_averages(group_by_input_shape=True).table(sort_by="self_device_time_total",
+                                                                      row_limit=80, max_name_column_width=60,
+                                                                      max_shapes_column_width=90))
+            f.write("\n\n")
+            f.write(prof.key_averages().table(sort_by="device_time_total", row_limit=80,
+                                              max_name_column_width=60))
     return {"model": model, "batch": bs, "ms_per_step": round(dt * 1e3, 3),
             "samples_per_s": round(bs / dt, 1), "loss": float(loss.detach()), "graph": stepper.graph is not None,
             "warmup_s": round(warm_s, 3)}
@@ -83,11 +97,13 @@ def main():
     ap.add_argument("--graph", action="store_true", help="replay the whole step as one captured hipGraph")
     ap.add_argument("--grad-dtype", default="fp32", choices=["fp32", "bf16"], help="flat gradient precision")
     ap.add_argument("--overlap-opt", action="store_true", help="per-bucket optimizer overlapping backward (ElasticDDP)")
+    ap.add_argument("--torch-profile", default=None, help="write a torch.profiler op table (3 steps) to this path")
     a = ap.parse_args()
     if a.cudnn_benchmark:
         torch.backends.cudnn.benchmark = True
     _native.hip()
-    out = run(a.model, a.batch, a.steps, a.warmup, a.profile_marker, a.graph, a.grad_dtype, a.overlap_opt)
+    out = run(a.model, a.batch, a.steps, a.warmup, a.profile_marker, a.graph, a.grad_dtype, a.overlap_opt,
+              a.torch_profile)
     out["grad_dtype"] = a.grad_dtype
     out["overlap_opt"] = a.overlap_opt
     print(json.dumps(out), flush=True)
