@@ -23,7 +23,8 @@ from vodascheduler_amd.runtime.stepgraph import GraphedStepper  # noqa: E402
 
 
 def run(model: str, batch: int | None, steps: int, warmup: int, marker: bool = False, graph: bool = False,
-        grad_dtype: str = "fp32", overlap_opt: bool = False, torch_profile: str | None = None) -> dict:
+        grad_dtype: str = "fp32", overlap_opt: bool = False, torch_profile: str | None = None,
+        record_losses: int = 0) -> dict:
     dev = torch.device("cuda", 0)
     w = get_workload(model)
     bs = batch or w.per_gpu_batch
@@ -54,6 +55,9 @@ def run(model: str, batch: int | None, steps: int, warmup: int, marker: bool = F
     def step():
         return stepper(b)
 
+    losses = []
+    for _ in range(record_losses):  # trajectory check (untimed): the first losses from init
+        losses.append(round(float(step().detach()), 5))
     t_w = time.perf_counter()
     for _ in range(warmup):
         step()
@@ -83,7 +87,7 @@ def run(model: str, batch: int | None, steps: int, warmup: int, marker: bool = F
                                               max_name_column_width=60))
     return {"model": model, "batch": bs, "ms_per_step": round(dt * 1e3, 3),
             "samples_per_s": round(bs / dt, 1), "loss": float(loss.detach()), "graph": stepper.graph is not None,
-            "warmup_s": round(warm_s, 3)}
+            "warmup_s": round(warm_s, 3), **({"losses": losses} if losses else {})}
 
 
 def main():
@@ -98,12 +102,13 @@ def main():
     ap.add_argument("--grad-dtype", default="fp32", choices=["fp32", "bf16"], help="flat gradient precision")
     ap.add_argument("--overlap-opt", action="store_true", help="per-bucket optimizer overlapping backward (ElasticDDP)")
     ap.add_argument("--torch-profile", default=None, help="write a torch.profiler op table (3 steps) to this path")
+    ap.add_argument("--losses", type=int, default=0, help="record the first N step losses (trajectory checks)")
     a = ap.parse_args()
     if a.cudnn_benchmark:
         torch.backends.cudnn.benchmark = True
     _native.hip()
     out = run(a.model, a.batch, a.steps, a.warmup, a.profile_marker, a.graph, a.grad_dtype, a.overlap_opt,
-              a.torch_profile)
+              a.torch_profile, a.losses)
     out["grad_dtype"] = a.grad_dtype
     out["overlap_opt"] = a.overlap_opt
     print(json.dumps(out), flush=True)

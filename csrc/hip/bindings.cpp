@@ -33,6 +33,8 @@ PYBIND11_MODULE(_vodahip, m) {
   m.def("layernorm_bwd_partial_rows", &layernorm_bwd_partial_rows);
   m.def("masked_softmax_fwd", &masked_softmax_fwd);
   m.def("masked_softmax_bwd", &masked_softmax_bwd);
+  m.def("xent_fwd", &xent_fwd);
+  m.def("xent_bwd", &xent_bwd);
 
   m.def("bn_workspace_floats", &bn_workspace_floats);
   m.def("bn_set_tuning", &bn_set_tuning, py::arg("deep") = -1, py::arg("blocks") = -1, py::arg("sweep") = -1);

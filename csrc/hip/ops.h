@@ -58,6 +58,15 @@ void layernorm_bwd(uintptr_t dy, uintptr_t x, uintptr_t mean, uintptr_t rstd, ui
                    uintptr_t dgamma, uintptr_t dbeta, uintptr_t workspace, int64_t M, int N, int dt, int wdt,
                    bool accumulate, uintptr_t stream);
 
+// ---- fused softmax cross-entropy (xent.hip) ----
+// logits [rows][ld] (bf16 / fp32, 16-byte rows), V <= ld valid classes; per-row lse / loss /
+// correct (fp32); labels int64, ``ignore`` rows contribute 0.  Backward: dx (same layout) =
+// (*scale) * (softmax - onehot) over the V classes, 0 in the padding columns.
+void xent_fwd(uintptr_t x, int64_t rows, int64_t ld, int V, int dt, uintptr_t labels, int64_t ignore, uintptr_t lse,
+              uintptr_t loss, uintptr_t correct, uintptr_t stream);
+void xent_bwd(uintptr_t x, uintptr_t dx, int64_t rows, int64_t ld, int V, int dt, uintptr_t labels, int64_t ignore,
+              uintptr_t lse, uintptr_t scale, uintptr_t stream);
+
 // ---- masked softmax (softmax.hip) ----
 void masked_softmax_fwd(uintptr_t x, uintptr_t mask, int mask_dt, uintptr_t y, int64_t B, int H, int Tq, int S,
                         int64_t mask_bstride, int64_t mask_qstride, bool causal, float scale, int dt,

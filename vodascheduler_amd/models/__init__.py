@@ -7,12 +7,14 @@ real shapes (no datasets are available offline).
 """
 from __future__ import annotations
 
+import os
 from dataclasses import dataclass, field
 from typing import Callable
 
 import torch
 import torch.nn.functional as F
 
+from ..ops.xent import softmax_cross_entropy
 from .convnets import InceptionV3, KerasMnistCNN, TorchMnistNet, vgg16_cifar
 from .resnet import resnet18, resnet50
 from .transformer import BertBase, TransformerNMT
@@ -78,22 +80,18 @@ def _cls_metrics(log_probs: bool = False):
 
 
 def _nmt_metrics(model, batch):
+    """Loss over real tokens (padding id 0 ignored) and the reference's masked accuracy, from
+    one fused cross-entropy pass over the vocab logits (ops/xent.py)."""
     src, tin, tout = batch
-    logits = model(src, tin).float()
-    logits = logits.reshape(-1, logits.shape[-1])
-    t = tout.reshape(-1)
-    loss = F.cross_entropy(logits, t, ignore_index=0)
-    valid = t != 0  # masked accuracy over real tokens (the reference's masked_accuracy)
-    correct = ((logits.argmax(1) == t) & valid).sum()
-    return loss, correct, valid.sum()
+    logits = model(src, tin)
+    return softmax_cross_entropy(logits.reshape(-1, logits.shape[-1]), tout.reshape(-1),
+                                 getattr(model, "num_classes", None), ignore_index=0)
 
 
 def _bert_metrics(model, batch):
     ids, mask, pos, labels = batch
-    logits = model(ids, mask, pos).float()
-    y = labels.reshape(-1)
-    loss = F.cross_entropy(logits, y)
-    return loss, (logits.argmax(1) == y).sum(), torch.full((), y.numel(), device=y.device)
+    logits = model(ids, mask, pos)
+    return softmax_cross_entropy(logits, labels.reshape(-1), getattr(model, "num_classes", None))
 
 
 def _nmt_batch(b, dev, g=None, vocab=15000, T=20):
@@ -104,9 +102,7 @@ def _nmt_batch(b, dev, g=None, vocab=15000, T=20):
 
 
 def _nmt_loss(model, batch):
-    src, tin, tout = batch
-    logits = model(src, tin)
-    return F.cross_entropy(logits.float().reshape(-1, logits.shape[-1]), tout.reshape(-1), ignore_index=0)
+    return _nmt_metrics(model, batch)[0]
 
 
 def _bert_batch(b, dev, g=None, vocab=30522, T=128, P=20):
@@ -122,9 +118,7 @@ def _bert_batch(b, dev, g=None, vocab=30522, T=128, P=20):
 
 
 def _bert_loss(model, batch):
-    ids, mask, pos, labels = batch
-    logits = model(ids, mask, pos)
-    return F.cross_entropy(logits.float(), labels.reshape(-1))
+    return _bert_metrics(model, batch)[0]
 
 
 _CE, _NLL = _cls_metrics(), _cls_metrics(log_probs=True)
@@ -177,6 +171,9 @@ def prepare_model(w: "Workload", device: torch.device, amp: bool = True) -> torc
     """Build a workload's model on ``device`` in the layout/precision the trainer uses:
     channels_last for convnets, bf16 compute weights on GPU with autocast."""
     m = w.build().to(device)
+    blas = os.environ.get("VODA_BLAS")  # A/B knob: library GEMMs on rocBLAS instead of hipBLASLt
+    if blas in ("rocblas", "hipblaslt") and device.type == "cuda":
+        torch.backends.cuda.preferred_blas_library("cublas" if blas == "rocblas" else "cublaslt")
     if w.channels_last and device.type == "cuda":
         m = m.to(memory_format=torch.channels_last)
         # MIOpen exhaustive find once per conv shape (cached in-process and in MIOpen's

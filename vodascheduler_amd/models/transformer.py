@@ -13,6 +13,7 @@ import torch
 from torch import nn
 
 from ..ops.dense import FusedLinear
+from ..ops.embedding import FusedEmbedding
 from ..ops.layernorm import FusedLayerNorm
 from .layers import HIP_GELU, DecoderLayer, EncoderLayer, GeluTanh
 
@@ -20,8 +21,8 @@ from .layers import HIP_GELU, DecoderLayer, EncoderLayer, GeluTanh
 class PositionalEmbedding(nn.Module):
     def __init__(self, seq_len: int, vocab: int, dim: int):
         super().__init__()
-        self.tok = nn.Embedding(vocab, dim)
-        self.pos = nn.Embedding(seq_len, dim)
+        self.tok = FusedEmbedding(vocab, dim)
+        self.pos = FusedEmbedding(seq_len, dim)
 
     def forward(self, ids):
         pos = torch.arange(ids.shape[1], device=ids.device)
@@ -36,7 +37,8 @@ class TransformerNMT(nn.Module):
         self.tgt_emb = PositionalEmbedding(seq_len, vocab, d_model)
         self.enc = nn.ModuleList([EncoderLayer(d_model, heads, d_ff, key_dim, dropout=dropout) for _ in range(layers)])
         self.dec = nn.ModuleList([DecoderLayer(d_model, heads, d_ff, key_dim, dropout=dropout) for _ in range(layers)])
-        self.head = nn.Linear(d_model, vocab)
+        self.head = FusedLinear(d_model, vocab)
+        self.num_classes = vocab
 
     def forward(self, src, tgt):
         src_mask = (src != 0)
@@ -49,18 +51,30 @@ class TransformerNMT(nn.Module):
         return self.head(y)
 
 
+def padded_vocab(vocab: int, multiple: int = 64) -> int:
+    return -(-vocab // multiple) * multiple
+
+
 class BertBase(nn.Module):
+    """The token table and the tied MLM decoder have ``padded_vocab(vocab)`` rows (30522 ->
+    30528, as NVIDIA's BERT does): 16-byte rows for the decoder's HIP weight-gradient kernel
+    and the fused cross-entropy, which takes only the first ``num_classes`` = ``vocab``
+    columns into the softmax (ops/xent.py), so the loss is the unpadded model's.  The padding
+    rows are never looked up and get zero gradient (weight decay only)."""
+
     def __init__(self, vocab: int = 30522, seq_len: int = 128, d_model: int = 768, heads: int = 12,
                  d_ff: int = 3072, layers: int = 12, dropout: float = 0.0):
         super().__init__()
-        self.emb = PositionalEmbedding(seq_len, vocab, d_model)
+        self.num_classes = vocab
+        vp = padded_vocab(vocab)
+        self.emb = PositionalEmbedding(seq_len, vp, d_model)
         self.type_emb = nn.Embedding(2, d_model)
         self.emb_ln = FusedLayerNorm(d_model, eps=1e-12)
         self.layers = nn.ModuleList([EncoderLayer(d_model, heads, d_ff, act="gelu", dropout=dropout, eps=1e-12)
                                      for _ in range(layers)])
         self.mlm_dense = FusedLinear(d_model, d_model)
         self.mlm_ln = FusedLayerNorm(d_model, eps=1e-12)
-        self.mlm_out = nn.Linear(d_model, vocab)
+        self.mlm_out = FusedLinear(d_model, vp)
         self.mlm_out.weight = self.emb.tok.weight  # tied embeddings, as in BERT
         self.act = GeluTanh() if HIP_GELU else nn.GELU(approximate="tanh")
         for m in self.modules():
@@ -73,7 +87,8 @@ class BertBase(nn.Module):
         """``masked_positions`` [B, P] (the standard BERT pretraining input
         ``masked_lm_positions``): the MLM head runs on those B*P rows only -- the loss is
         identical (unmasked tokens carry no label) and the vocab GEMMs + softmax shrink by
-        T/P (6.4x at T=128, P=20)."""
+        T/P (6.4x at T=128, P=20).  Returns [rows, padded vocab] logits; the classes are the
+        first ``num_classes`` columns."""
         x = self.emb_ln(self.emb(ids) + self.type_emb.weight[0])
         for l in self.layers:
             x = l(x, key_mask=attention_mask)

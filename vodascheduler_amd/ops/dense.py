@@ -27,6 +27,47 @@ from . import _native as N
 from . import wgrad as W
 
 USE_WGRAD_KERNEL = os.environ.get("VODA_WGRAD", "1") != "0"
+USE_SPLIT_DGRAD = os.environ.get("VODA_SPLIT_DGRAD", "1") != "0"
+_BMM_F32: bool | None = None  # torch.bmm(..., out_dtype=float32) available (probed once)
+
+
+def _split_count(M: int, n_out: int, K: int) -> int:
+    """Splits of the reduction (output-feature) dimension for dX = dY . W, or 1.
+
+    A vocab-sized head's input gradient (BERT MLM: [1280 x 30528] . [30528 x 768]) has a long
+    reduction and only ~60 output tiles of 128 x 128, so hipBLASLt runs it on a quarter of the
+    CUs (233 us, profiles/r2_rocprof_bert_final.md).  Splitting the reduction into S batched
+    GEMMs (fp32 partials, summed after) fills the chip; chunks stay multiples of 8 columns."""
+    tiles = -(-M // 128) * -(-K // 128)
+    if n_out < 8192 or tiles >= 128:
+        return 1
+    target = max(2, min(16, 256 // max(tiles, 1)))
+    for s in range(target, 1, -1):
+        if n_out % (8 * s) == 0:
+            return s
+    return 1
+
+
+def _dgrad(dy2: torch.Tensor, weight: torch.Tensor) -> torch.Tensor:
+    """dY [M, n_out] . W [n_out, K] -> [M, K] in dY's dtype (split-K for long reductions)."""
+    global _BMM_F32
+    M, n_out = dy2.shape
+    K = weight.shape[1]
+    S = _split_count(M, n_out, K) if (USE_SPLIT_DGRAD and dy2.is_cuda and weight.is_contiguous()) else 1
+    if S == 1:
+        return dy2 @ weight
+    c = n_out // S
+    a = dy2.view(M, S, c).transpose(0, 1)   # [S, M, c], row stride n_out
+    b = weight.view(S, c, K)
+    if _BMM_F32 is not False:
+        try:
+            part = torch.bmm(a, b, out_dtype=torch.float32)
+            _BMM_F32 = True
+        except (RuntimeError, TypeError):
+            _BMM_F32 = False
+    if _BMM_F32 is False:
+        part = torch.bmm(a, b).float()
+    return part.sum(0).to(dy2.dtype)
 
 
 def _direct(p: torch.Tensor | None) -> bool:
@@ -88,7 +129,7 @@ class _DenseFn(torch.autograd.Function):
             acc.view(-1, K).addmm_(dy2, weight)  # dX = residual gradient + dY . W
             dx = acc
         elif ctx.needs_input_grad[0]:
-            dx = (dy2 @ weight).view(x.shape)
+            dx = _dgrad(dy2, weight).view(x.shape)
         need_w, need_b = ctx.needs_input_grad[1], bias is not None and ctx.needs_input_grad[2]
         fused = (USE_WGRAD_KERNEL and need_w and _direct(weight) and (not need_b or _direct(bias))
                  and W.supported(dy2, x2, flat_grad(weight), flat_grad(bias) if need_b else None))
