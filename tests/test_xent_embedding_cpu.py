@@ -54,3 +54,42 @@ def test_fused_embedding_scatters_into_flat_gradient():
     (m(ids) * dy).sum().backward()
     (ref(ids) * dy).sum().backward()
     torch.testing.assert_close(grad_of(m.weight), ref.weight.grad)
+
+
+def test_add_rows_gradients_match_broadcast_add():
+    from vodascheduler_amd.ops.embedding import add_rows
+
+    torch.manual_seed(0)
+    w = torch.nn.Parameter(torch.randn(2, 16))
+    wr = torch.nn.Parameter(w.detach().clone())
+    x = torch.randn(3, 5, 16, requires_grad=True)
+    xr = x.detach().clone().requires_grad_(True)
+    dy = torch.randn(3, 5, 16)
+    (add_rows(x, w, 0) * dy).sum().backward()
+    ((xr + wr[0]) * dy).sum().backward()
+    torch.testing.assert_close(w.grad, wr.grad)
+    torch.testing.assert_close(x.grad, xr.grad)
+    # flat fp32 gradient path (the trainer's): accumulated into the row's slot
+    opt = FusedAdamW([w], lr=1e-3)
+    opt.zero_grad()
+    (add_rows(x, w, 1) * dy).sum().backward()
+    ref = torch.zeros(2, 16)
+    ref[1] = dy.reshape(-1, 16).sum(0)
+    torch.testing.assert_close(grad_of(w), ref)
+
+
+def test_add_rows_position_block():
+    from vodascheduler_amd.ops.embedding import add_rows
+
+    torch.manual_seed(0)
+    w = torch.nn.Parameter(torch.randn(8, 16))
+    wr = torch.nn.Parameter(w.detach().clone())
+    x = torch.randn(3, 5, 16)
+    dy = torch.randn(3, 5, 16)
+    (add_rows(x, w, 0, 5) * dy).sum().backward()
+    ((x + wr[:5][None]) * dy).sum().backward()
+    torch.testing.assert_close(w.grad, wr.grad)
+    opt = FusedAdamW([w], lr=1e-3)
+    opt.zero_grad()
+    (add_rows(x, w, 0, 5) * dy).sum().backward()
+    torch.testing.assert_close(grad_of(w), wr.grad)

@@ -13,7 +13,7 @@ import torch
 from torch import nn
 
 from ..ops.dense import FusedLinear
-from ..ops.embedding import FusedEmbedding
+from ..ops.embedding import FusedEmbedding, add_rows
 from ..ops.layernorm import FusedLayerNorm
 from .layers import HIP_GELU, DecoderLayer, EncoderLayer, GeluTanh
 
@@ -25,8 +25,7 @@ class PositionalEmbedding(nn.Module):
         self.pos = FusedEmbedding(seq_len, dim)
 
     def forward(self, ids):
-        pos = torch.arange(ids.shape[1], device=ids.device)
-        return self.tok(ids) + self.pos(pos)[None]
+        return add_rows(self.tok(ids), self.pos.weight, 0, ids.shape[1])
 
 
 class TransformerNMT(nn.Module):
@@ -89,7 +88,7 @@ class BertBase(nn.Module):
         identical (unmasked tokens carry no label) and the vocab GEMMs + softmax shrink by
         T/P (6.4x at T=128, P=20).  Returns [rows, padded vocab] logits; the classes are the
         first ``num_classes`` columns."""
-        x = self.emb_ln(self.emb(ids) + self.type_emb.weight[0])
+        x = self.emb_ln(add_rows(self.emb(ids), self.type_emb.weight, 0, 1))
         for l in self.layers:
             x = l(x, key_mask=attention_mask)
         if masked_positions is not None:
