@@ -145,9 +145,10 @@ __device__ __forceinline__ void block_rows(int64_t M, int rpi, int64_t bid, int6
 //              covers one contiguous span), so the data read LAST sits at the END of the
 //              tensor -- the apply pass that follows walks its blocks back to front and
 //              meets those rows first, while they can still be in the 256 MB MALL.
-// Apply passes: chunk of block blockIdx.x, or of the mirrored block in sweep mode.
+//   sweep = 2: the reduction sweeps back to front (Walk below), the apply pass front to back.
+// Apply passes: chunk of block blockIdx.x, or of the mirrored block in sweep mode 1.
 __device__ __forceinline__ void apply_rows(int64_t M, int rpi, int sweep, int64_t& r0, int64_t& r1) {
-  block_rows(M, rpi, sweep ? int64_t(gridDim.x) - 1 - blockIdx.x : int64_t(blockIdx.x), r0, r1);
+  block_rows(M, rpi, sweep == 1 ? int64_t(gridDim.x) - 1 - blockIdx.x : int64_t(blockIdx.x), r0, r1);
 }
 
 // Block-level reduction of two 8-channel accumulators over the row offsets that share a
@@ -212,17 +213,33 @@ template <> struct BufRow<float> {
   }
 };
 
-// Uniform walk of a reduction pass: iterations at base rows first, first + step, ... < end.
-__device__ __forceinline__ void reduce_walk(const Map& m, int64_t M, int sweep, int64_t& first, int64_t& step,
-                                            int64_t& end) {
-  if (sweep) {
-    first = int64_t(blockIdx.x) * m.rpi;
-    step = int64_t(gridDim.x) * m.rpi;
-    end = M;
-  } else {
-    block_rows(M, m.rpi, blockIdx.x, first, end);
-    step = m.rpi;
+// Uniform walk of a reduction pass: iterations at base rows first, first + step, ... < end,
+// taken U at a time.  ``groups`` = number of U-iteration groups; group i starts at row
+// first + order(i) * U * step, with order(i) = n - 1 - i when ``rev`` (sweep = 2: the grid
+// sweeps the tensor BACK to front, so it first meets the rows the producing GEMM / conv wrote
+// last -- still in the 256 MB MALL -- and the front-to-back apply pass that follows meets the
+// rows the reduction read last).
+struct Walk {
+  int64_t first, step, end, groups;
+  bool rev;
+  __device__ __forceinline__ int64_t base(int64_t i, int U) const {
+    return first + (rev ? groups - 1 - i : i) * U * step;
   }
+};
+__device__ __forceinline__ Walk reduce_walk(const Map& m, int64_t M, int sweep, int U) {
+  Walk w;
+  if (sweep) {
+    w.first = int64_t(blockIdx.x) * m.rpi;
+    w.step = int64_t(gridDim.x) * m.rpi;
+    w.end = M;
+  } else {
+    block_rows(M, m.rpi, blockIdx.x, w.first, w.end);
+    w.step = m.rpi;
+  }
+  const int64_t stride = int64_t(U) * w.step;
+  w.groups = w.end > w.first ? (w.end - w.first + stride - 1) / stride : 0;
+  w.rev = sweep == 2;
+  return w;
 }
 
 template <typename T, int U>
@@ -231,12 +248,13 @@ __global__ __launch_bounds__(kBlock) void bn_stats_kernel(const T* __restrict__ 
   const Map m = make_map(C);
   float s1[8] = {0, 0, 0, 0, 0, 0, 0, 0}, s2[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   if (m.active) {
-    int64_t b, step, end;
-    reduce_walk(m, M, sweep, b, step, end);
+    const Walk w = reduce_walk(m, M, sweep, U);
+    const int64_t end = w.end;
     const int64_t row_bytes = int64_t(C) * sizeof(T);
     const int voff = int(m.rsub * row_bytes + int64_t(m.cg) * kVec * sizeof(T));
-    const int sstep = int(step * row_bytes);  // <= 2048 blocks x 4 KB
-    for (; b < end; b += U * step) {
+    const int sstep = int(w.step * row_bytes);  // <= 2048 blocks x 4 KB
+    for (int64_t i = 0; i < w.groups; ++i) {
+      const int64_t b = w.base(i, U);
       const auto rs = rows_rsrc(x + b * C, (end - b) * row_bytes);
       typename BufRow<T>::Raw raw[U];
 #pragma unroll
@@ -267,15 +285,16 @@ __global__ __launch_bounds__(kBlock) void bn_bwd_reduce_kernel(const T* __restri
   const Map m = make_map(C);
   float s1[8] = {0, 0, 0, 0, 0, 0, 0, 0}, s2[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   if (m.active) {
-    int64_t b, step, end;
-    reduce_walk(m, M, sweep, b, step, end);
+    const Walk w = reduce_walk(m, M, sweep, U);
+    const int64_t end = w.end;
     const int CB = C / kVec;
     const int64_t row_bytes = int64_t(C) * sizeof(T);
     const int voff = int(m.rsub * row_bytes + int64_t(m.cg) * kVec * sizeof(T));
     const int moff = m.rsub * CB + m.cg;
-    const int sstep = int(step * row_bytes), mstep = int(step * CB);
+    const int sstep = int(w.step * row_bytes), mstep = int(w.step * CB);
     // U rows of dy and x (2U x 16 B per lane) + their mask bytes in flight per thread
-    for (; b < end; b += U * step) {
+    for (int64_t i = 0; i < w.groups; ++i) {
+      const int64_t b = w.base(i, U);
       const auto rg = rows_rsrc(dy + b * C, (end - b) * row_bytes);
       const auto rx = rows_rsrc(x + b * C, (end - b) * row_bytes);
       const auto rm = rows_rsrc(mask + (RELU ? b * CB : 0), RELU ? (end - b) * CB : 0);
@@ -510,7 +529,8 @@ Grid bn_grid(int64_t M, int C, int64_t cap_blocks, int iters_per_block) {
 // benchmarks/gpu_r2_bn_trace.sh for per-shape dispatch times):
 //   VODA_BN_UNROLL=0|1|2  rows in flight 4 / 8 / 16 (stats) and 2 / 4 / 8 (backward reduce)
 //   VODA_BN_BLOCKS=n      reduction grid cap (default 256 = one 4-wave block per CU)
-//   VODA_BN_SWEEP=0|1     grid-sweep reduction + mirrored apply order (default 1, see Walk)
+//   VODA_BN_SWEEP=0|1|2   grid-sweep reduction + mirrored apply order (default 1); 2 = sweep
+//                         back to front + apply front to back (see Walk)
 // Measured on MI355X (profiles/raw/r2_bn_grid_trace.md, ResNet-50 bs-256 step A/B in
 // profiles/raw/r2_ab_bn_grid.jsonl): the reduction passes of the large tensors ran at 3.8-4.2
 // TB/s with 1024 long-lived blocks each walking its own chunk; one block per CU sweeping
@@ -528,7 +548,7 @@ BnTune& bn_tune() {
     BnTune v{1, 256, 1};
     if (const char* e = std::getenv("VODA_BN_UNROLL")) v.deep = std::max(0, std::min(2, std::atoi(e)));
     if (const char* e = std::getenv("VODA_BN_BLOCKS")) v.blocks = std::max(64, std::min(8192, std::atoi(e)));
-    if (const char* e = std::getenv("VODA_BN_SWEEP")) v.sweep = e[0] == '1' ? 1 : 0;
+    if (const char* e = std::getenv("VODA_BN_SWEEP")) v.sweep = std::max(0, std::min(2, std::atoi(e)));
     if (const char* e = std::getenv("VODA_BN_APPLY_CAP")) v.apply_cap = std::max(256, std::atoi(e));
     if (const char* e = std::getenv("VODA_BN_APPLY_ITERS")) v.apply_iters = std::max(1, std::atoi(e));
     return v;
@@ -560,7 +580,7 @@ void bn_set_tuning(int deep, int blocks, int sweep) {
   BnTune& t = bn_tune();
   if (deep >= 0) t.deep = std::min(2, deep);
   if (blocks > 0) t.blocks = std::max(64, std::min(8192, blocks));
-  if (sweep >= 0) t.sweep = sweep != 0;
+  if (sweep >= 0) t.sweep = std::min(2, sweep);
 }
 
 std::vector<int> bn_get_tuning() {

@@ -45,80 +45,77 @@ template <> struct V8<float> {
   }
 };
 
+// One workgroup row per output (forward) / input (backward) pixel row: blockIdx.x = n * rows +
+// row (scalar decode), threads over (column, channel group) of that row in 32-bit math.  The
+// first version decoded a flat 64-bit index per element (three 64-bit div/mod sequences per
+// thread) and ran VALU-bound at 2.5-3.5 TB/s (profiles/r2_rocprof_resnet50_final.md).
 template <typename T>
 __global__ __launch_bounds__(256) void maxpool_fwd_kernel(const T* __restrict__ x, T* __restrict__ y,
                                                           uint8_t* __restrict__ idx, PoolGeom g) {
   const int CG = g.C / 8;
-  const int64_t total = int64_t(g.N) * g.Ho * g.Wo * CG;
-  for (int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < total; i += int64_t(gridDim.x) * blockDim.x) {
-    const int cg = int(i % CG);
-    int64_t pix = i / CG;
-    const int wo = int(pix % g.Wo);
-    pix /= g.Wo;
-    const int ho = int(pix % g.Ho);
-    const int n = int(pix / g.Ho);
-    float best[8];
-    uint32_t arg[8];
+  const int j = int(blockIdx.y) * 256 + int(threadIdx.x);
+  if (j >= g.Wo * CG) return;
+  const int n = int(blockIdx.x) / g.Ho, ho = int(blockIdx.x) % g.Ho;
+  const int wo = j / CG, cg = j - wo * CG;
+  float best[8];
+  uint32_t arg[8];
 #pragma unroll
-    for (int c = 0; c < 8; ++c) { best[c] = -__builtin_huge_valf(); arg[c] = 0; }
-    for (int kh = 0; kh < g.k; ++kh) {
-      const int h = ho * g.s - g.p + kh;
-      if (h < 0 || h >= g.H) continue;
-      for (int kw = 0; kw < g.k; ++kw) {
-        const int w = wo * g.s - g.p + kw;
-        if (w < 0 || w >= g.W) continue;
-        float v[8];
-        V8<T>::load(x + ((int64_t(n) * g.H + h) * g.W + w) * g.C + cg * 8, v);
-        const uint32_t o = uint32_t(kh * g.k + kw);
+  for (int c = 0; c < 8; ++c) { best[c] = -__builtin_huge_valf(); arg[c] = 0; }
+  const T* xn = x + int64_t(n) * g.H * g.W * g.C + cg * 8;
+  for (int kh = 0; kh < g.k; ++kh) {
+    const int h = ho * g.s - g.p + kh;
+    if (h < 0 || h >= g.H) continue;
+    for (int kw = 0; kw < g.k; ++kw) {
+      const int w = wo * g.s - g.p + kw;
+      if (w < 0 || w >= g.W) continue;
+      float v[8];
+      V8<T>::load(xn + (int64_t(h) * g.W + w) * g.C, v);
+      const uint32_t o = uint32_t(kh * g.k + kw);
 #pragma unroll
-        for (int c = 0; c < 8; ++c)
-          if (v[c] > best[c] || (v[c] != v[c] && best[c] == best[c])) { best[c] = v[c]; arg[c] = o; }
-      }
+      for (int c = 0; c < 8; ++c)
+        if (v[c] > best[c] || (v[c] != v[c] && best[c] == best[c])) { best[c] = v[c]; arg[c] = o; }
     }
-    V8<T>::store(y + i * 8, best);
-    uint2 a;
-    a.x = arg[0] | (arg[1] << 8) | (arg[2] << 16) | (arg[3] << 24);
-    a.y = arg[4] | (arg[5] << 8) | (arg[6] << 16) | (arg[7] << 24);
-    *reinterpret_cast<uint2*>(idx + i * 8) = a;
   }
+  const int64_t i = (int64_t(blockIdx.x) * g.Wo + wo) * CG + cg;
+  V8<T>::store(y + i * 8, best);
+  uint2 a;
+  a.x = arg[0] | (arg[1] << 8) | (arg[2] << 16) | (arg[3] << 24);
+  a.y = arg[4] | (arg[5] << 8) | (arg[6] << 16) | (arg[7] << 24);
+  *reinterpret_cast<uint2*>(idx + i * 8) = a;
 }
 
 template <typename T>
 __global__ __launch_bounds__(256) void maxpool_bwd_kernel(const T* __restrict__ dy, const uint8_t* __restrict__ idx,
                                                           T* __restrict__ dx, PoolGeom g) {
   const int CG = g.C / 8;
-  const int64_t total = int64_t(g.N) * g.H * g.W * CG;
-  for (int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < total; i += int64_t(gridDim.x) * blockDim.x) {
-    const int cg = int(i % CG);
-    int64_t pix = i / CG;
-    const int w = int(pix % g.W);
-    pix /= g.W;
-    const int h = int(pix % g.H);
-    const int n = int(pix / g.H);
-    float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    // windows (ho, wo) with ho*s - p <= h <= ho*s - p + k - 1
-    const int ho0 = max(0, (h + g.p - g.k + g.s) / g.s), ho1 = min(g.Ho - 1, (h + g.p) / g.s);
-    const int wo0 = max(0, (w + g.p - g.k + g.s) / g.s), wo1 = min(g.Wo - 1, (w + g.p) / g.s);
-    for (int ho = ho0; ho <= ho1; ++ho) {
-      const int kh = h - (ho * g.s - g.p);
-      if (kh < 0 || kh >= g.k) continue;
-      for (int wo = wo0; wo <= wo1; ++wo) {
-        const int kw = w - (wo * g.s - g.p);
-        if (kw < 0 || kw >= g.k) continue;
-        const int64_t o = ((int64_t(n) * g.Ho + ho) * g.Wo + wo) * g.C + cg * 8;
-        const uint2 a = *reinterpret_cast<const uint2*>(idx + o);
-        const uint32_t want = uint32_t(kh * g.k + kw);
-        float d[8];
-        V8<T>::load(dy + o, d);
+  const int j = int(blockIdx.y) * 256 + int(threadIdx.x);
+  if (j >= g.W * CG) return;
+  const int n = int(blockIdx.x) / g.H, h = int(blockIdx.x) % g.H;
+  const int w = j / CG, cg = j - w * CG;
+  float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  // windows (ho, wo) with ho*s - p <= h <= ho*s - p + k - 1
+  const int ho0 = max(0, (h + g.p - g.k + g.s) / g.s), ho1 = min(g.Ho - 1, (h + g.p) / g.s);
+  const int wo0 = max(0, (w + g.p - g.k + g.s) / g.s), wo1 = min(g.Wo - 1, (w + g.p) / g.s);
+  const int64_t nbase = int64_t(n) * g.Ho * g.Wo * g.C + cg * 8;
+  for (int ho = ho0; ho <= ho1; ++ho) {
+    const int kh = h - (ho * g.s - g.p);
+    if (kh < 0 || kh >= g.k) continue;
+    for (int wo = wo0; wo <= wo1; ++wo) {
+      const int kw = w - (wo * g.s - g.p);
+      if (kw < 0 || kw >= g.k) continue;
+      const int64_t o = nbase + (int64_t(ho) * g.Wo + wo) * g.C;
+      const uint2 a = *reinterpret_cast<const uint2*>(idx + o);
+      const uint32_t want = uint32_t(kh * g.k + kw);
+      float d[8];
+      V8<T>::load(dy + o, d);
 #pragma unroll
-        for (int c = 0; c < 8; ++c) {
-          const uint32_t ac = ((c < 4 ? a.x : a.y) >> (8 * (c & 3))) & 0xff;
-          if (ac == want) acc[c] += d[c];
-        }
+      for (int c = 0; c < 8; ++c) {
+        const uint32_t ac = ((c < 4 ? a.x : a.y) >> (8 * (c & 3))) & 0xff;
+        if (ac == want) acc[c] += d[c];
       }
     }
-    V8<T>::store(dx + i * 8, acc);
   }
+  V8<T>::store(dx + ((int64_t(blockIdx.x) * g.W + w) * CG + cg) * 8, acc);
 }
 
 }  // namespace
@@ -126,8 +123,9 @@ __global__ __launch_bounds__(256) void maxpool_bwd_kernel(const T* __restrict__ 
 void maxpool2d_fwd(uintptr_t x, uintptr_t y, uintptr_t idx, int N, int H, int W, int C, int Ho, int Wo, int k, int s,
                    int p, int dt, uintptr_t stream) {
   VODA_CHECK(C % 8 == 0 && k * k <= 255, "maxpool: C % 8 == 0 and k*k < 256 required");
+  VODA_CHECK(int64_t(Wo) * (C / 8) < (int64_t(1) << 24) && int64_t(N) * Ho < (int64_t(1) << 31), "maxpool: shape too large");
   const PoolGeom g{N, H, W, C, Ho, Wo, k, s, p};
-  const unsigned grid = stream_grid(int64_t(N) * Ho * Wo * (C / 8), 256, 8192);
+  const dim3 grid(unsigned(int64_t(N) * Ho), unsigned((Wo * (C / 8) + 255) / 256));
   if (dt == kBF16)
     hipLaunchKernelGGL((maxpool_fwd_kernel<BF16>), dim3(grid), dim3(256), 0, as_stream(stream),
                        reinterpret_cast<const BF16*>(x), reinterpret_cast<BF16*>(y), reinterpret_cast<uint8_t*>(idx), g);
@@ -142,8 +140,9 @@ void maxpool2d_fwd(uintptr_t x, uintptr_t y, uintptr_t idx, int N, int H, int W,
 void maxpool2d_bwd(uintptr_t dy, uintptr_t idx, uintptr_t dx, int N, int H, int W, int C, int Ho, int Wo, int k, int s,
                    int p, int dt, uintptr_t stream) {
   VODA_CHECK(C % 8 == 0, "maxpool: C % 8 == 0 required");
+  VODA_CHECK(int64_t(W) * (C / 8) < (int64_t(1) << 24) && int64_t(N) * H < (int64_t(1) << 31), "maxpool: shape too large");
   const PoolGeom g{N, H, W, C, Ho, Wo, k, s, p};
-  const unsigned grid = stream_grid(int64_t(N) * H * W * (C / 8), 256, 8192);
+  const dim3 grid(unsigned(int64_t(N) * H), unsigned((W * (C / 8) + 255) / 256));
   if (dt == kBF16)
     hipLaunchKernelGGL((maxpool_bwd_kernel<BF16>), dim3(grid), dim3(256), 0, as_stream(stream),
                        reinterpret_cast<const BF16*>(dy), reinterpret_cast<const uint8_t*>(idx), reinterpret_cast<BF16*>(dx), g);

@@ -51,7 +51,8 @@ def test_bn_act_fwd_bwd(shape, res, relu, dt):
         torch.testing.assert_close(r.grad.float(), rr.grad, atol=gtol, rtol=gtol)
 
 
-@pytest.mark.parametrize("tuning", [(1, 2048, 1), (0, 1024, 0), (1, 64, 1), (1, 1024, 1), (2, 256, 0), (1, 256, 0)])
+@pytest.mark.parametrize("tuning", [(1, 2048, 1), (0, 1024, 0), (1, 64, 1), (1, 1024, 1), (2, 256, 0), (1, 256, 0),
+                                    (1, 256, 2), (0, 64, 2), (2, 1024, 2)])
 @pytest.mark.parametrize("shape", [(8, 64, 14, 14), (3, 2048, 3, 3), (16, 256, 28, 28)])
 def test_bn_reduction_orders_agree(shape, tuning):
     """Every reduction walk (chunked / grid sweep, grid caps, unroll depths, buffer-descriptor
