@@ -76,5 +76,38 @@ def main():
                           "wgrad_rel_err_vs_cin3": err}), flush=True)
 
 
+def bn_pool():
+    """Stem BN + ReLU + 3x3/2 max pool, bs 256 x 64 x 112 x 112 bf16: fused kernels vs the
+    fused BN(+ReLU) followed by the HIP max pool (forward + backward, flat-free gradients)."""
+    import sys
+    import os
+
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    from vodascheduler_amd.ops.batchnorm import FusedBatchNorm2d, FusedBNReLUMaxPool2d
+    from vodascheduler_amd.ops.pool import max_pool2d
+
+    torch.manual_seed(0)
+    x = torch.randn(B, 64, 112, 112, device="cuda", dtype=torch.bfloat16).to(memory_format=torch.channels_last)
+    fused = FusedBNReLUMaxPool2d(64).cuda()
+    bn = FusedBatchNorm2d(64, relu=True).cuda()
+    dy = torch.randn(B, 64, 56, 56, device="cuda", dtype=torch.bfloat16).to(memory_format=torch.channels_last)
+    xi = x.clone().requires_grad_()
+
+    def run_fused():
+        xi.grad = None
+        fused(xi).backward(dy)
+
+    def run_split():
+        xi.grad = None
+        max_pool2d(bn(xi), 3, 2, 1).backward(dy)
+
+    for name, fn in (("split", run_split), ("fused", run_fused), ("split", run_split), ("fused", run_fused)):
+        print(json.dumps({"stem_bn_relu_pool": name, "fwd_bwd_us": round(t_us(fn), 1)}), flush=True)
+
+
 if __name__ == "__main__":
-    main()
+    import sys as _sys
+
+    if "--only-bn-pool" not in _sys.argv:
+        main()
+    bn_pool()

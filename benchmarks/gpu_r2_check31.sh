@@ -1,6 +1,6 @@
 #!/bin/bash
-# Round-2 check 31: BN back-to-front reduction sweep (VODA_BN_SWEEP=2) and row-per-block
-# maxpool kernels (numerics + ResNet-50 A/B), stem channel-padding micro-benchmark, then the
+# Round-2 check 31: BN back-to-front reduction sweep (VODA_BN_SWEEP=2), row-per-block
+# maxpool kernels and the fused stem BN+ReLU+maxpool (VODA_FUSED_BN_POOL) (numerics + ResNet-50 A/B), stem channel-padding micro-benchmark, then the
 # BERT-base / NMT whole-step hipGraph replay checks with the flat-gradient embeddings.
 set -o pipefail
 export TMPDIR=/tmp
@@ -12,8 +12,8 @@ tail -1 $O/bn_tests.log
 timeout -k 10 200 python3 -u benchmarks/bench_stem.py > $O/stem.jsonl 2> $O/stem.err || { tail -10 $O/stem.err; exit 3; }
 cat $O/stem.jsonl
 for rep in 1 2; do
-  for sw in 1 2; do
-    VODA_BN_SWEEP=$sw timeout -k 10 300 python3 -u benchmarks/model_step.py --model resnet50 --steps 20 --warmup 5 | sed "s/^{/{\"env\": \"VODA_BN_SWEEP=$sw\", /" >> $O/ab_sweep.jsonl || exit 4
+  for env in "VODA_BN_SWEEP=1 VODA_FUSED_BN_POOL=0" "VODA_BN_SWEEP=2 VODA_FUSED_BN_POOL=0" "VODA_BN_SWEEP=1 VODA_FUSED_BN_POOL=1" "VODA_BN_SWEEP=2 VODA_FUSED_BN_POOL=1"; do
+    env $env timeout -k 10 300 python3 -u benchmarks/model_step.py --model resnet50 --steps 20 --warmup 5 | sed "s/^{/{\"env\": \"$env\", /" >> $O/ab_sweep.jsonl || exit 4
   done
 done
 cat $O/ab_sweep.jsonl

@@ -508,6 +508,145 @@ __global__ __launch_bounds__(kBlock) void bn_bwd_apply_kernel(const T* __restric
   }
 }
 
+// ---------------------------------------------------------------- stem: BN + ReLU + max pool
+// ResNet stem: relu(bn(conv7x7(x))) -> maxpool 3x3/2.  Unfused, the 112x112 activation (411 MB
+// at bs 256) is written by the BN apply pass, read by the pool, and in backward the pool
+// writes its 411 MB gradient that both BN passes read again.  Fused:
+//   forward : stats pass over x (as above), then ONE pass that computes relu(a*x+b) in
+//             registers for each pooling window and writes only the pooled output and a
+//             1-byte argmax per element (0xFF when the window max is 0: relu clamped every
+//             element, so no gradient flows -- relu'(<=0) = 0, as in the unfused backward);
+//   backward: the BN reduce and apply passes gather g = (pool backward of dy) on the fly
+//             from dy_pool + argmax bytes (cached: 1/4 of the input's pixels) and never
+//             materialise it.
+struct PoolG {
+  int N, H, W, C, Ho, Wo, k, s, p;
+};
+
+template <typename T>
+__global__ __launch_bounds__(kBlock) void bn_pool_fwd_kernel(const T* __restrict__ x, const float* __restrict__ ab,
+                                                             T* __restrict__ y, uint8_t* __restrict__ idx, PoolG g) {
+  const int CG = g.C / kVec;
+  const int j = int(blockIdx.y) * kBlock + int(threadIdx.x);
+  if (j >= g.Wo * CG) return;
+  const int n = int(blockIdx.x) / g.Ho, ho = int(blockIdx.x) % g.Ho;
+  const int wo = j / CG, cg = j - wo * CG;
+  float a[8], b[8], best[8];
+  uint32_t arg[8];
+#pragma unroll
+  for (int c = 0; c < 8; ++c) {
+    a[c] = ab[cg * kVec + c];
+    b[c] = ab[g.C + cg * kVec + c];
+    best[c] = 0.f;  // relu output >= 0: a window whose max stays 0 passes no gradient
+    arg[c] = 0xFF;
+  }
+  const T* xn = x + int64_t(n) * g.H * g.W * g.C + cg * kVec;
+  for (int kh = 0; kh < g.k; ++kh) {
+    const int h = ho * g.s - g.p + kh;
+    if (h < 0 || h >= g.H) continue;
+    for (int kw = 0; kw < g.k; ++kw) {
+      const int w = wo * g.s - g.p + kw;
+      if (w < 0 || w >= g.W) continue;
+      float v[8];
+      Vec8<T>::load(xn, (int64_t(h) * g.W + w) * g.C, v);
+      const uint32_t o = uint32_t(kh * g.k + kw);
+#pragma unroll
+      for (int c = 0; c < 8; ++c) {
+        // bf16 rounding is monotonic, so max-then-round == round-then-max (the unfused values)
+        const float r = fmaf(v[c], a[c], b[c]);
+        if (r > best[c]) { best[c] = r; arg[c] = o; }
+      }
+    }
+  }
+  const int64_t i = (int64_t(blockIdx.x) * g.Wo + wo) * CG + cg;
+  Vec8<T>::store(y, i * kVec, best);
+  uint2 u;
+  u.x = arg[0] | (arg[1] << 8) | (arg[2] << 16) | (arg[3] << 24);
+  u.y = arg[4] | (arg[5] << 8) | (arg[6] << 16) | (arg[7] << 24);
+  *reinterpret_cast<uint2*>(idx + i * kVec) = u;
+}
+
+// g[8] at input pixel (n, h, w), channel group cg: the sum of dy_pool over the windows whose
+// argmax byte names this pixel (0xFF never does).
+template <typename T>
+__device__ __forceinline__ void pool_grad_gather(const T* __restrict__ dyp, const uint8_t* __restrict__ idx,
+                                                 const PoolG& g, int n, int h, int w, int cg, float (&acc)[8]) {
+#pragma unroll
+  for (int c = 0; c < 8; ++c) acc[c] = 0.f;
+  const int ho0 = max(0, (h + g.p - g.k + g.s) / g.s), ho1 = min(g.Ho - 1, (h + g.p) / g.s);
+  const int wo0 = max(0, (w + g.p - g.k + g.s) / g.s), wo1 = min(g.Wo - 1, (w + g.p) / g.s);
+  const int64_t nbase = int64_t(n) * g.Ho * g.Wo * g.C + cg * kVec;
+  for (int ho = ho0; ho <= ho1; ++ho) {
+    const int kh = h - (ho * g.s - g.p);
+    if (kh < 0 || kh >= g.k) continue;
+    for (int wo = wo0; wo <= wo1; ++wo) {
+      const int kw = w - (wo * g.s - g.p);
+      if (kw < 0 || kw >= g.k) continue;
+      const int64_t o = nbase + (int64_t(ho) * g.Wo + wo) * g.C;
+      const uint2 u = *reinterpret_cast<const uint2*>(idx + o);
+      const uint32_t want = uint32_t(kh * g.k + kw);
+      float d[8];
+      Vec8<T>::load(dyp, o, d);
+#pragma unroll
+      for (int c = 0; c < 8; ++c) {
+        const uint32_t ac = ((c < 4 ? u.x : u.y) >> (8 * (c & 3))) & 0xff;
+        if (ac == want) acc[c] += d[c];
+      }
+    }
+  }
+}
+
+// Reduce pass: block b owns image rows [b*per, (b+1)*per) of the N*H rows; thread (cg =
+// t % tpr, column offset t / tpr) walks the row's columns with step rpi.
+template <typename T>
+__global__ __launch_bounds__(kBlock) void bn_pool_bwd_reduce_kernel(const T* __restrict__ dyp,
+                                                                    const uint8_t* __restrict__ idx,
+                                                                    const T* __restrict__ x, float* __restrict__ part,
+                                                                    PoolG g) {
+  const Map m = make_map(g.C);
+  float s1[8] = {0, 0, 0, 0, 0, 0, 0, 0}, s2[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  if (m.active) {
+    const int rows = g.N * g.H;
+    const int per = (rows + int(gridDim.x) - 1) / int(gridDim.x);
+    const int r0 = int(blockIdx.x) * per, r1 = min(rows, r0 + per);
+    for (int r = r0; r < r1; ++r) {
+      const int n = r / g.H, h = r - n * g.H;
+      const T* xr = x + int64_t(r) * g.W * g.C + int64_t(m.cg) * kVec;
+      for (int w = m.rsub; w < g.W; w += m.rpi) {
+        float gr[8], xv[8];
+        pool_grad_gather(dyp, idx, g, n, h, w, m.cg, gr);
+        Vec8<T>::load(xr, int64_t(w) * g.C, xv);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) { s1[k] += gr[k]; s2[k] = fmaf(gr[k], xv[k], s2[k]); }
+      }
+    }
+  }
+  reduce_and_store(m, s1, s2, part, part + int64_t(gridDim.x) * g.C, g.C);
+}
+
+template <typename T>
+__global__ __launch_bounds__(kBlock) void bn_pool_bwd_apply_kernel(const T* __restrict__ dyp,
+                                                                   const uint8_t* __restrict__ idx,
+                                                                   const T* __restrict__ x,
+                                                                   const float* __restrict__ k3, T* __restrict__ dx,
+                                                                   PoolG g) {
+  const int CG = g.C / kVec;
+  const int j = int(blockIdx.y) * kBlock + int(threadIdx.x);
+  if (j >= g.W * CG) return;
+  const int n = int(blockIdx.x) / g.H, h = int(blockIdx.x) % g.H;
+  const int w = j / CG, cg = j - w * CG;
+  float gr[8], xv[8], o[8];
+  pool_grad_gather(dyp, idx, g, n, h, w, cg, gr);
+  const int64_t off = (int64_t(blockIdx.x) * g.W + w) * g.C + cg * kVec;
+  Vec8<T>::load(x, off, xv);
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    const int c = cg * kVec + k;
+    o[k] = fmaf(k3[c], gr[k], fmaf(k3[g.C + c], xv[k], k3[2 * g.C + c]));
+  }
+  Vec8<T>::store(dx, off, o);
+}
+
 // ---------------------------------------------------------------- launch helpers
 struct Grid {
   dim3 grid;
@@ -702,6 +841,77 @@ void bn_bwd(uintptr_t dy, uintptr_t mask, uintptr_t x, uintptr_t save_mean, uint
       if (dres) hipLaunchKernelGGL((bn_bwd_apply_kernel<T, false, true>), ag.grid, dim3(kBlock), 0, s, dyp, yp, xp, k3, dxp, drp, M, C, sw);
       else hipLaunchKernelGGL((bn_bwd_apply_kernel<T, false, false>), ag.grid, dim3(kBlock), 0, s, dyp, yp, xp, k3, dxp, drp, M, C, sw);
     }
+  });
+  check_launch();
+}
+
+// ---- stem BN + ReLU + max pool ----
+namespace {
+constexpr int kPoolRedBlocks = 2048;  // 8 four-wave blocks per CU: the gather loop is latency-bound
+int pool_red_blocks(int N, int H) { return std::max(1, std::min(kPoolRedBlocks, N * H)); }
+void check_pool(int N, int H, int W, int C, int Ho, int Wo, int k, int s, int p) {
+  VODA_CHECK(C % kVec == 0 && C <= kVec * kMaxTpr, "bn_pool: C must be a multiple of 8 and <= 2048");
+  VODA_CHECK(k >= 1 && k * k < 255 && s >= 1 && p >= 0 && 2 * p <= k, "bn_pool: unsupported window");
+  VODA_CHECK(Ho == (H + 2 * p - k) / s + 1 && Wo == (W + 2 * p - k) / s + 1, "bn_pool: output size mismatch");
+  VODA_CHECK(int64_t(N) * H < (int64_t(1) << 31) && int64_t(W) * (C / kVec) < (int64_t(1) << 24),
+             "bn_pool: shape too large");
+}
+}  // namespace
+
+int64_t bn_pool_workspace_floats(int N, int H, int C) {
+  return int64_t(2) * pool_red_blocks(N, H) * C + 3 * int64_t(C);
+}
+
+void bn_pool_fwd_train(uintptr_t x, uintptr_t gamma, uintptr_t beta, uintptr_t running_mean, uintptr_t running_var,
+                       uintptr_t save_mean, uintptr_t save_invstd, uintptr_t y, uintptr_t idx, uintptr_t workspace,
+                       int N, int H, int W, int C, int Ho, int Wo, int k, int s, int p, float eps, float momentum,
+                       int dt, uintptr_t stream) {
+  check_pool(N, H, W, C, Ho, Wo, k, s, p);
+  hipStream_t st = as_stream(stream);
+  const int64_t M = int64_t(N) * H * W;
+  float* ws = reinterpret_cast<float*>(workspace);
+  // the statistics pass on a grid of at most pool_red_blocks partial rows (fits the workspace)
+  const Grid rg = bn_grid(M, C, pool_red_blocks(N, H), 8);
+  float* ab = ws + int64_t(2) * rg.nb * C;
+  const PoolG g{N, H, W, C, Ho, Wo, k, s, p};
+  const dim3 pgrid(unsigned(int64_t(N) * Ho), unsigned((Wo * (C / kVec) + kBlock - 1) / kBlock));
+  dispatch_dt(dt, [&](auto tag) {
+    using T = decltype(tag);
+    const T* xp = reinterpret_cast<const T*>(x);
+    hipLaunchKernelGGL((bn_stats_kernel<T, 8>), rg.grid, dim3(kBlock), 0, st, xp, ws, M, C, 1);
+    hipLaunchKernelGGL(bn_fwd_finalize_kernel, dim3((C + kFinCh - 1) / kFinCh), dim3(kFinCh * kFinRg), 0, st, ws,
+                       rg.nb, M, C, reinterpret_cast<const float*>(gamma), reinterpret_cast<const float*>(beta),
+                       reinterpret_cast<float*>(running_mean), reinterpret_cast<float*>(running_var),
+                       reinterpret_cast<float*>(save_mean), reinterpret_cast<float*>(save_invstd), ab, eps, momentum);
+    hipLaunchKernelGGL((bn_pool_fwd_kernel<T>), pgrid, dim3(kBlock), 0, st, xp, ab, reinterpret_cast<T*>(y),
+                       reinterpret_cast<uint8_t*>(idx), g);
+  });
+  check_launch();
+}
+
+void bn_pool_bwd(uintptr_t dy, uintptr_t idx, uintptr_t x, uintptr_t save_mean, uintptr_t save_invstd,
+                 uintptr_t gamma, uintptr_t dx, uintptr_t dgamma, uintptr_t dbeta, uintptr_t workspace, int N, int H,
+                 int W, int C, int Ho, int Wo, int k, int s, int p, bool accumulate, int dt, uintptr_t stream) {
+  check_pool(N, H, W, C, Ho, Wo, k, s, p);
+  hipStream_t st = as_stream(stream);
+  const int64_t M = int64_t(N) * H * W;
+  float* ws = reinterpret_cast<float*>(workspace);
+  const int nb = pool_red_blocks(N, H);
+  float* k3 = ws + int64_t(2) * nb * C;
+  const PoolG g{N, H, W, C, Ho, Wo, k, s, p};
+  const dim3 agrid(unsigned(int64_t(N) * H), unsigned((W * (C / kVec) + kBlock - 1) / kBlock));
+  dispatch_dt(dt, [&](auto tag) {
+    using T = decltype(tag);
+    const T* dyp = reinterpret_cast<const T*>(dy);
+    const uint8_t* ip = reinterpret_cast<const uint8_t*>(idx);
+    const T* xp = reinterpret_cast<const T*>(x);
+    hipLaunchKernelGGL((bn_pool_bwd_reduce_kernel<T>), dim3(nb), dim3(kBlock), 0, st, dyp, ip, xp, ws, g);
+    hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + kFinCh - 1) / kFinCh), dim3(kFinCh * kFinRg), 0, st, ws,
+                       nb, M, C, reinterpret_cast<const float*>(gamma), reinterpret_cast<const float*>(save_mean),
+                       reinterpret_cast<const float*>(save_invstd), reinterpret_cast<float*>(dgamma),
+                       reinterpret_cast<float*>(dbeta), k3, int(accumulate));
+    hipLaunchKernelGGL((bn_pool_bwd_apply_kernel<T>), agrid, dim3(kBlock), 0, st, dyp, ip, xp, k3,
+                       reinterpret_cast<T*>(dx), g);
   });
   check_launch();
 }

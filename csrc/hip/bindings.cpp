@@ -43,6 +43,9 @@ PYBIND11_MODULE(_vodahip, m) {
   m.def("bn_apply", &bn_apply);
   m.def("bn_bwd", &bn_bwd);
 
+  m.def("bn_pool_workspace_floats", &bn_pool_workspace_floats);
+  m.def("bn_pool_fwd_train", &bn_pool_fwd_train);
+  m.def("bn_pool_bwd", &bn_pool_bwd);
   m.def("maxpool2d_fwd", &maxpool2d_fwd);
   m.def("maxpool2d_bwd", &maxpool2d_bwd);
   m.def("colsum_workspace_floats", &colsum_workspace_floats);

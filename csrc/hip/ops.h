@@ -90,6 +90,16 @@ void bn_bwd(uintptr_t dy, uintptr_t mask, uintptr_t x, uintptr_t save_mean, uint
             uintptr_t dx, uintptr_t dres, uintptr_t dgamma, uintptr_t dbeta, uintptr_t workspace, int64_t M, int C,
             bool relu, bool accumulate, int dt, uintptr_t stream);
 
+// ---- ResNet stem: BN(train) + ReLU + max pool fused (batchnorm.hip) ----
+int64_t bn_pool_workspace_floats(int N, int H, int C);
+void bn_pool_fwd_train(uintptr_t x, uintptr_t gamma, uintptr_t beta, uintptr_t running_mean, uintptr_t running_var,
+                       uintptr_t save_mean, uintptr_t save_invstd, uintptr_t y, uintptr_t idx, uintptr_t workspace,
+                       int N, int H, int W, int C, int Ho, int Wo, int k, int s, int p, float eps, float momentum,
+                       int dt, uintptr_t stream);
+void bn_pool_bwd(uintptr_t dy, uintptr_t idx, uintptr_t x, uintptr_t save_mean, uintptr_t save_invstd,
+                 uintptr_t gamma, uintptr_t dx, uintptr_t dgamma, uintptr_t dbeta, uintptr_t workspace, int N, int H,
+                 int W, int C, int Ho, int Wo, int k, int s, int p, bool accumulate, int dt, uintptr_t stream);
+
 // ---- NHWC max pooling with argmax bytes + gather backward (pool.hip) ----
 void maxpool2d_fwd(uintptr_t x, uintptr_t y, uintptr_t idx, int N, int H, int W, int C, int Ho, int Wo, int k, int s,
                    int p, int dt, uintptr_t stream);

@@ -162,3 +162,55 @@ def test_bn_param_grads_accumulate_into_flat_buffer():
     assert len(ready) == 4
     torch.testing.assert_close(b.weight.grad, a.weight.grad, atol=1e-3, rtol=1e-3)
     torch.testing.assert_close(b.bias.grad, a.bias.grad, atol=1e-3, rtol=1e-3)
+
+
+@pytest.mark.parametrize("shape,k,s,p", [((4, 64, 112, 112), 3, 2, 1), ((3, 16, 17, 13), 3, 2, 1), ((2, 24, 9, 9), 2, 2, 0),
+                                         ((2, 8, 7, 7), 3, 1, 1)])
+@pytest.mark.parametrize("dt", [torch.bfloat16, torch.float32])
+def test_bn_relu_maxpool_fused_matches_composition(shape, k, s, p, dt, monkeypatch):
+    """maxpool(relu(bn(x))) on the fused stem kernels == the fp32 PyTorch composition:
+    output, running statistics, input / gamma / beta gradients (the pooled gradient is
+    gathered inside both BN backward passes)."""
+    from vodascheduler_amd.ops import batchnorm
+    from vodascheduler_amd.ops.batchnorm import FusedBNReLUMaxPool2d
+
+    monkeypatch.setattr(batchnorm, "USE_FUSED_BN_POOL", True)
+
+    torch.manual_seed(0)
+    C = shape[1]
+    m = FusedBNReLUMaxPool2d(C, k, s, p).cuda()
+    with torch.no_grad():
+        m.weight.uniform_(0.5, 1.5)
+        m.bias.uniform_(-0.5, 0.5)
+    ref = torch.nn.BatchNorm2d(C).cuda()
+    ref.load_state_dict({kk: v for kk, v in m.state_dict().items()})
+    x = (torch.randn(shape, device="cuda") * 2 + 0.5).to(dt).to(memory_format=torch.channels_last)
+    xi = x.clone().requires_grad_()
+    y = m(xi)
+    assert m._fused_ok(xi)
+    xr = x.float().clone().requires_grad_()
+    yr = F.max_pool2d(F.relu(ref(xr)), k, s, p)
+    tol = 2e-2 if dt == torch.bfloat16 else 1e-4
+    torch.testing.assert_close(y.float(), yr, atol=tol, rtol=tol)
+    torch.testing.assert_close(m.running_mean, ref.running_mean, atol=1e-4, rtol=1e-4)
+    torch.testing.assert_close(m.running_var, ref.running_var, atol=1e-3, rtol=1e-3)
+    dy = torch.randn_like(yr)
+    y.backward(dy.to(dt))
+    yr.backward(dy)
+    M = x.numel() // C
+    torch.testing.assert_close(xi.grad.float(), xr.grad, atol=5 * tol, rtol=5 * tol)
+    torch.testing.assert_close(m.weight.grad, ref.weight.grad, atol=tol * M ** 0.5, rtol=tol)
+    torch.testing.assert_close(m.bias.grad, ref.bias.grad, atol=tol * M ** 0.5, rtol=tol)
+
+
+def test_bn_relu_maxpool_eval_path():
+    from vodascheduler_amd.ops.batchnorm import FusedBNReLUMaxPool2d
+
+    torch.manual_seed(0)
+    m = FusedBNReLUMaxPool2d(16).cuda()
+    x = torch.randn(2, 16, 12, 12, device="cuda").to(memory_format=torch.channels_last)
+    m(x)
+    m.eval()
+    ref = torch.nn.BatchNorm2d(16).cuda().eval()
+    ref.load_state_dict(m.state_dict())
+    torch.testing.assert_close(m(x), F.max_pool2d(F.relu(ref(x)), 3, 2, 1), atol=1e-5, rtol=1e-5)

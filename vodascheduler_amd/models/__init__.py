@@ -144,7 +144,11 @@ WORKLOADS: dict[str, Workload] = {
                             samples_unit="tok", tokens_per_sample=20, metrics=_nmt_metrics),
     "bert-base": Workload("bert-base", BertBase, _bert_batch, _bert_loss, 64, "adamw",
                           dict(lr=1e-4, weight_decay=0.01), samples_unit="tok", tokens_per_sample=128,
-                          metrics=_bert_metrics),
+                          metrics=_bert_metrics,
+                          # replays exact at bs 64 once the embeddings' backward is the flat-gradient
+                          # column-sum / index_add path (check 31: frozen grads bitwise, 5-step
+                          # trajectory equal); 11.0-11.28 -> 10.75 ms per step as a graph
+                          graph_safe=True),
 }
 
 

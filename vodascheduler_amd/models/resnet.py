@@ -18,10 +18,9 @@ from __future__ import annotations
 import torch
 from torch import nn
 
-from ..ops.batchnorm import FusedBatchNorm2d
+from ..ops.batchnorm import FusedBatchNorm2d, FusedBNReLUMaxPool2d
 from ..ops.conv1x1 import USE_GRAD_SINK, Conv1x1, GradSink
 from ..ops.conv3x3 import ConvKxK
-from ..ops.pool import FusedMaxPool2d
 
 
 class Bottleneck(nn.Module):
@@ -80,8 +79,10 @@ class ResNet(nn.Module):
         if small_input:  # CIFAR-style 32x32 stem
             self.stem = nn.Sequential(nn.Conv2d(3, 64, 3, padding=1, bias=False), FusedBatchNorm2d(64, relu=True))
         else:
+            # BN + ReLU + 3x3/2 max pool as one fused op (ops/batchnorm.FusedBNReLUMaxPool2d);
+            # state dict keys stem.0.* / stem.1.* as with a separate BN and pool
             self.stem = nn.Sequential(nn.Conv2d(3, 64, 7, stride=2, padding=3, bias=False),
-                                      FusedBatchNorm2d(64, relu=True), FusedMaxPool2d(3, stride=2, padding=1))
+                                      FusedBNReLUMaxPool2d(64, 3, stride=2, padding=1))
         self.layer1 = self._make(block, 64, layers[0])
         self.layer2 = self._make(block, 128, layers[1], stride=2)
         self.layer3 = self._make(block, 256, layers[2], stride=2)

@@ -27,6 +27,9 @@ from .dense import _ready
 # VODA_FUSED_BN=0: every BatchNorm takes the PyTorch reference composition (A/B and bisection
 # runs, e.g. benchmarks/graph_diag.py)
 USE_FUSED_BN = os.environ.get("VODA_FUSED_BN", "1") != "0"
+# VODA_FUSED_BN_POOL=1: the ResNet stem's BN+ReLU+maxpool on the fused kernels (opt-in until
+# the A/B favours it: profiles/raw/r2_ab_bn_sweep2_stem_pool.jsonl)
+USE_FUSED_BN_POOL = os.environ.get("VODA_FUSED_BN_POOL", "0") == "1"
 
 
 def _rows_view_ok(x: torch.Tensor) -> bool:
@@ -144,6 +147,61 @@ def batch_norm_act(x: torch.Tensor, weight: torch.Tensor | None, bias: torch.Ten
     return y
 
 
+def _pool_out(n: int, k: int, s: int, p: int) -> int:
+    return (n + 2 * p - k) // s + 1
+
+
+class _BNPoolFn(torch.autograd.Function):
+    """maxpool(relu(bn(x))) in training mode (csrc/hip/batchnorm.hip ``bn_pool_*``): the
+    full-resolution BN output and its gradient are never written to memory."""
+
+    @staticmethod
+    def forward(ctx, x, weight, bias, running_mean, running_var, momentum, eps, k, s, p):
+        Nb, C, H, W = x.shape
+        Ho, Wo = _pool_out(H, k, s, p), _pool_out(W, k, s, p)
+        h = N.hip()
+        y = torch.empty(Nb, C, Ho, Wo, dtype=x.dtype, device=x.device, memory_format=torch.channels_last)
+        idx = torch.empty(Nb * Ho * Wo * C, dtype=torch.uint8, device=x.device)
+        save_mean = torch.empty(C, dtype=torch.float32, device=x.device)
+        save_invstd = torch.empty(C, dtype=torch.float32, device=x.device)
+        ws = torch.empty(h.bn_pool_workspace_floats(Nb, H, C), dtype=torch.float32, device=x.device)
+        h.bn_pool_fwd_train(x.data_ptr(), N.ptr(weight), N.ptr(bias), N.ptr(running_mean), N.ptr(running_var),
+                            save_mean.data_ptr(), save_invstd.data_ptr(), y.data_ptr(), idx.data_ptr(), ws.data_ptr(),
+                            Nb, H, W, C, Ho, Wo, k, s, p, float(eps), float(momentum), N.dtype_code(x.dtype),
+                            N.stream_of(x))
+        ctx.geom = (Nb, H, W, C, Ho, Wo, k, s, p)
+        ctx.bias = bias
+        ctx.save_for_backward(x, idx, weight, save_mean, save_invstd)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, idx, weight, save_mean, save_invstd = ctx.saved_tensors
+        Nb, H, W, C, Ho, Wo, k, s, p = ctx.geom
+        h = N.hip()
+        dy = dy.to(x.dtype).contiguous(memory_format=torch.channels_last)
+        dx = torch.empty_like(x)
+        need_w = weight is not None and ctx.needs_input_grad[1]
+        need_b = ctx.needs_input_grad[2]
+        bias = ctx.bias
+        direct = (need_b and _direct_fp32(bias) and ((need_w and _direct_fp32(weight)) or weight is None))
+        if direct:
+            dw, db = flat_grad(weight), flat_grad(bias)
+        else:
+            dw = torch.empty(C, dtype=torch.float32, device=x.device) if need_w else None
+            db = torch.empty(C, dtype=torch.float32, device=x.device) if need_b else None
+        ws = torch.empty(h.bn_pool_workspace_floats(Nb, H, C), dtype=torch.float32, device=x.device)
+        h.bn_pool_bwd(dy.data_ptr(), idx.data_ptr(), x.data_ptr(), save_mean.data_ptr(), save_invstd.data_ptr(),
+                      N.ptr(weight), dx.data_ptr(), N.ptr(dw), N.ptr(db), ws.data_ptr(), Nb, H, W, C, Ho, Wo, k, s, p,
+                      direct, N.dtype_code(x.dtype), N.stream_of(x))
+        if direct:
+            if weight is not None:
+                _ready(weight)
+            _ready(bias)
+            return dx, None, None, None, None, None, None, None, None, None
+        return dx, dw, db, None, None, None, None, None, None, None
+
+
 class FusedBatchNorm2d(torch.nn.BatchNorm2d):
     """``BatchNorm2d`` whose forward optionally adds a residual and applies ReLU:
     ``forward(x, residual=None) = relu?(bn(x) + residual)``.  State dict compatible with
@@ -193,3 +251,38 @@ class FusedBatchNorm2d(torch.nn.BatchNorm2d):
 
     def extra_repr(self):
         return super().extra_repr() + f", relu={self.relu}"
+
+
+class FusedBNReLUMaxPool2d(FusedBatchNorm2d):
+    """``maxpool(relu(bn(x)))`` -- the ResNet stem's BN + ReLU + MaxPool2d(k, s, p) -- as one
+    module (state dict of the ``BatchNorm2d``).  Training on the GPU path runs the fused
+    kernels (``_BNPoolFn``); evaluation and unsupported inputs run the composition."""
+
+    def __init__(self, num_features: int, kernel_size: int = 3, stride: int = 2, padding: int = 1, **kw):
+        super().__init__(num_features, relu=True, **kw)
+        self.pool = (kernel_size, stride, padding)
+
+    def _fused_ok(self, x) -> bool:
+        k, s, p = self.pool
+        return (USE_FUSED_BN and USE_FUSED_BN_POOL and self.training and self.track_running_stats
+                and x.is_cuda and x.dim() == 4 and x.dtype in (torch.bfloat16, torch.float32)
+                and x.is_contiguous(memory_format=torch.channels_last) and x.shape[1] % 8 == 0
+                and x.shape[1] <= 2048 and 2 * p <= k and k * k < 255
+                and all(t is None or t.dtype == torch.float32 for t in (self.weight, self.bias)))
+
+    def forward(self, x, residual=None, sink=None):
+        from .pool import max_pool2d
+
+        if residual is None and self._fused_ok(x):
+            if self.momentum is None:
+                self.num_batches_tracked.add_(1)
+            else:
+                self._pending_batches = getattr(self, "_pending_batches", 0) + 1
+            k, s, p = self.pool
+            with torch.autocast("cuda", enabled=False):
+                return _BNPoolFn.apply(x, self.weight, self.bias, self.running_mean, self.running_var,
+                                       self.momentum if self.momentum is not None else 0.1, self.eps, k, s, p)
+        return max_pool2d(super().forward(x, residual, sink), *self.pool)
+
+    def extra_repr(self):
+        return super().extra_repr() + f", pool={self.pool}"
