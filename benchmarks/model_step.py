@@ -80,7 +80,7 @@ def run(model: str, batch: int | None, steps: int, warmup: int, marker: bool = F
             torch.cuda.synchronize(dev)
         with open(torch_profile, "w") as f:
             f.write(prof.key_averages(group_by_input_shape=True).table(sort_by="self_device_time_total",
-                                                                      row_limit=80, max_name_column_width=60,
+                                                                      row_limit=250, max_name_column_width=60,
                                                                       max_shapes_column_width=90))
             f.write("\n\n")
             f.write(prof.key_averages().table(sort_by="device_time_total", row_limit=80,

@@ -523,7 +523,9 @@ struct PoolG {
   int N, H, W, C, Ho, Wo, k, s, p;
 };
 
-template <typename T>
+// Window shape K x K, stride S at compile time (the stem's 3x3/2): all window loads of a
+// thread are issued before the first use (clamped addresses, out-of-image taps masked).
+template <typename T, int K, int S>
 __global__ __launch_bounds__(kBlock) void bn_pool_fwd_kernel(const T* __restrict__ x, const float* __restrict__ ab,
                                                              T* __restrict__ y, uint8_t* __restrict__ idx, PoolG g) {
   const int CG = g.C / kVec;
@@ -531,6 +533,16 @@ __global__ __launch_bounds__(kBlock) void bn_pool_fwd_kernel(const T* __restrict
   if (j >= g.Wo * CG) return;
   const int n = int(blockIdx.x) / g.Ho, ho = int(blockIdx.x) % g.Ho;
   const int wo = j / CG, cg = j - wo * CG;
+  const T* xn = x + int64_t(n) * g.H * g.W * g.C + cg * kVec;
+  const int h0 = ho * S - g.p, w0 = wo * S - g.p;
+  typename Vec8<T>::Raw raw[K * K];
+#pragma unroll
+  for (int kh = 0; kh < K; ++kh) {
+    const int hc = min(max(h0 + kh, 0), g.H - 1);
+#pragma unroll
+    for (int kw = 0; kw < K; ++kw)
+      raw[kh * K + kw] = Vec8<T>::load_raw(xn, (int64_t(hc) * g.W + min(max(w0 + kw, 0), g.W - 1)) * g.C);
+  }
   float a[8], b[8], best[8];
   uint32_t arg[8];
 #pragma unroll
@@ -540,21 +552,18 @@ __global__ __launch_bounds__(kBlock) void bn_pool_fwd_kernel(const T* __restrict
     best[c] = 0.f;  // relu output >= 0: a window whose max stays 0 passes no gradient
     arg[c] = 0xFF;
   }
-  const T* xn = x + int64_t(n) * g.H * g.W * g.C + cg * kVec;
-  for (int kh = 0; kh < g.k; ++kh) {
-    const int h = ho * g.s - g.p + kh;
-    if (h < 0 || h >= g.H) continue;
-    for (int kw = 0; kw < g.k; ++kw) {
-      const int w = wo * g.s - g.p + kw;
-      if (w < 0 || w >= g.W) continue;
+#pragma unroll
+  for (int kh = 0; kh < K; ++kh) {
+#pragma unroll
+    for (int kw = 0; kw < K; ++kw) {
+      const bool ok = unsigned(h0 + kh) < unsigned(g.H) && unsigned(w0 + kw) < unsigned(g.W);
       float v[8];
-      Vec8<T>::load(xn, (int64_t(h) * g.W + w) * g.C, v);
-      const uint32_t o = uint32_t(kh * g.k + kw);
+      Vec8<T>::cvt(raw[kh * K + kw], v);
 #pragma unroll
       for (int c = 0; c < 8; ++c) {
         // bf16 rounding is monotonic, so max-then-round == round-then-max (the unfused values)
         const float r = fmaf(v[c], a[c], b[c]);
-        if (r > best[c]) { best[c] = r; arg[c] = o; }
+        if (ok && r > best[c]) { best[c] = r; arg[c] = uint32_t(kh * K + kw); }
       }
     }
   }
@@ -567,26 +576,38 @@ __global__ __launch_bounds__(kBlock) void bn_pool_fwd_kernel(const T* __restrict
 }
 
 // g[8] at input pixel (n, h, w), channel group cg: the sum of dy_pool over the windows whose
-// argmax byte names this pixel (0xFF never does).
-template <typename T>
+// argmax byte names this pixel (0xFF never does); all (K+S-1)/S squared windows loaded first.
+template <typename T, int K, int S>
 __device__ __forceinline__ void pool_grad_gather(const T* __restrict__ dyp, const uint8_t* __restrict__ idx,
                                                  const PoolG& g, int n, int h, int w, int cg, float (&acc)[8]) {
+  constexpr int NW = (K + S - 1) / S;
+  const int ho0 = max(0, (h + g.p - K + S) / S), wo0 = max(0, (w + g.p - K + S) / S);
+  const int64_t nbase = int64_t(n) * g.Ho * g.Wo * g.C + cg * kVec;
+  uint2 a[NW * NW];
+  typename Vec8<T>::Raw raw[NW * NW];
+#pragma unroll
+  for (int dh = 0; dh < NW; ++dh) {
+    const int hoc = min(ho0 + dh, g.Ho - 1);
+#pragma unroll
+    for (int dw = 0; dw < NW; ++dw) {
+      const int64_t o = nbase + (int64_t(hoc) * g.Wo + min(wo0 + dw, g.Wo - 1)) * g.C;
+      a[dh * NW + dw] = *reinterpret_cast<const uint2*>(idx + o);
+      raw[dh * NW + dw] = Vec8<T>::load_raw(dyp, o);
+    }
+  }
 #pragma unroll
   for (int c = 0; c < 8; ++c) acc[c] = 0.f;
-  const int ho0 = max(0, (h + g.p - g.k + g.s) / g.s), ho1 = min(g.Ho - 1, (h + g.p) / g.s);
-  const int wo0 = max(0, (w + g.p - g.k + g.s) / g.s), wo1 = min(g.Wo - 1, (w + g.p) / g.s);
-  const int64_t nbase = int64_t(n) * g.Ho * g.Wo * g.C + cg * kVec;
-  for (int ho = ho0; ho <= ho1; ++ho) {
-    const int kh = h - (ho * g.s - g.p);
-    if (kh < 0 || kh >= g.k) continue;
-    for (int wo = wo0; wo <= wo1; ++wo) {
-      const int kw = w - (wo * g.s - g.p);
-      if (kw < 0 || kw >= g.k) continue;
-      const int64_t o = nbase + (int64_t(ho) * g.Wo + wo) * g.C;
-      const uint2 u = *reinterpret_cast<const uint2*>(idx + o);
-      const uint32_t want = uint32_t(kh * g.k + kw);
+#pragma unroll
+  for (int dh = 0; dh < NW; ++dh) {
+    const int ho = ho0 + dh, kh = h - (ho * S - g.p);
+#pragma unroll
+    for (int dw = 0; dw < NW; ++dw) {
+      const int wo = wo0 + dw, kw = w - (wo * S - g.p);
+      const bool ok = ho < g.Ho && wo < g.Wo && unsigned(kh) < unsigned(K) && unsigned(kw) < unsigned(K);
+      const uint32_t want = ok ? uint32_t(kh * K + kw) : 0x100u;  // 0x100 matches no byte
       float d[8];
-      Vec8<T>::load(dyp, o, d);
+      Vec8<T>::cvt(raw[dh * NW + dw], d);
+      const uint2 u = a[dh * NW + dw];
 #pragma unroll
       for (int c = 0; c < 8; ++c) {
         const uint32_t ac = ((c < 4 ? u.x : u.y) >> (8 * (c & 3))) & 0xff;
@@ -598,7 +619,7 @@ __device__ __forceinline__ void pool_grad_gather(const T* __restrict__ dyp, cons
 
 // Reduce pass: block b owns image rows [b*per, (b+1)*per) of the N*H rows; thread (cg =
 // t % tpr, column offset t / tpr) walks the row's columns with step rpi.
-template <typename T>
+template <typename T, int K, int S>
 __global__ __launch_bounds__(kBlock) void bn_pool_bwd_reduce_kernel(const T* __restrict__ dyp,
                                                                     const uint8_t* __restrict__ idx,
                                                                     const T* __restrict__ x, float* __restrict__ part,
@@ -613,9 +634,10 @@ __global__ __launch_bounds__(kBlock) void bn_pool_bwd_reduce_kernel(const T* __r
       const int n = r / g.H, h = r - n * g.H;
       const T* xr = x + int64_t(r) * g.W * g.C + int64_t(m.cg) * kVec;
       for (int w = m.rsub; w < g.W; w += m.rpi) {
+        const auto xraw = Vec8<T>::load_raw(xr, int64_t(w) * g.C);
         float gr[8], xv[8];
-        pool_grad_gather(dyp, idx, g, n, h, w, m.cg, gr);
-        Vec8<T>::load(xr, int64_t(w) * g.C, xv);
+        pool_grad_gather<T, K, S>(dyp, idx, g, n, h, w, m.cg, gr);
+        Vec8<T>::cvt(xraw, xv);
 #pragma unroll
         for (int k = 0; k < 8; ++k) { s1[k] += gr[k]; s2[k] = fmaf(gr[k], xv[k], s2[k]); }
       }
@@ -624,7 +646,7 @@ __global__ __launch_bounds__(kBlock) void bn_pool_bwd_reduce_kernel(const T* __r
   reduce_and_store(m, s1, s2, part, part + int64_t(gridDim.x) * g.C, g.C);
 }
 
-template <typename T>
+template <typename T, int K, int S>
 __global__ __launch_bounds__(kBlock) void bn_pool_bwd_apply_kernel(const T* __restrict__ dyp,
                                                                    const uint8_t* __restrict__ idx,
                                                                    const T* __restrict__ x,
@@ -635,10 +657,11 @@ __global__ __launch_bounds__(kBlock) void bn_pool_bwd_apply_kernel(const T* __re
   if (j >= g.W * CG) return;
   const int n = int(blockIdx.x) / g.H, h = int(blockIdx.x) % g.H;
   const int w = j / CG, cg = j - w * CG;
-  float gr[8], xv[8], o[8];
-  pool_grad_gather(dyp, idx, g, n, h, w, cg, gr);
   const int64_t off = (int64_t(blockIdx.x) * g.W + w) * g.C + cg * kVec;
-  Vec8<T>::load(x, off, xv);
+  const auto xraw = Vec8<T>::load_raw(x, off);
+  float gr[8], xv[8], o[8];
+  pool_grad_gather<T, K, S>(dyp, idx, g, n, h, w, cg, gr);
+  Vec8<T>::cvt(xraw, xv);
 #pragma unroll
   for (int k = 0; k < 8; ++k) {
     const int c = cg * kVec + k;
@@ -851,7 +874,7 @@ constexpr int kPoolRedBlocks = 2048;  // 8 four-wave blocks per CU: the gather l
 int pool_red_blocks(int N, int H) { return std::max(1, std::min(kPoolRedBlocks, N * H)); }
 void check_pool(int N, int H, int W, int C, int Ho, int Wo, int k, int s, int p) {
   VODA_CHECK(C % kVec == 0 && C <= kVec * kMaxTpr, "bn_pool: C must be a multiple of 8 and <= 2048");
-  VODA_CHECK(k >= 1 && k * k < 255 && s >= 1 && p >= 0 && 2 * p <= k, "bn_pool: unsupported window");
+  VODA_CHECK(k == 3 && s == 2 && p >= 0 && 2 * p <= k, "bn_pool: only the 3x3 / stride-2 window is compiled");
   VODA_CHECK(Ho == (H + 2 * p - k) / s + 1 && Wo == (W + 2 * p - k) / s + 1, "bn_pool: output size mismatch");
   VODA_CHECK(int64_t(N) * H < (int64_t(1) << 31) && int64_t(W) * (C / kVec) < (int64_t(1) << 24),
              "bn_pool: shape too large");
@@ -883,7 +906,7 @@ void bn_pool_fwd_train(uintptr_t x, uintptr_t gamma, uintptr_t beta, uintptr_t r
                        rg.nb, M, C, reinterpret_cast<const float*>(gamma), reinterpret_cast<const float*>(beta),
                        reinterpret_cast<float*>(running_mean), reinterpret_cast<float*>(running_var),
                        reinterpret_cast<float*>(save_mean), reinterpret_cast<float*>(save_invstd), ab, eps, momentum);
-    hipLaunchKernelGGL((bn_pool_fwd_kernel<T>), pgrid, dim3(kBlock), 0, st, xp, ab, reinterpret_cast<T*>(y),
+    hipLaunchKernelGGL((bn_pool_fwd_kernel<T, 3, 2>), pgrid, dim3(kBlock), 0, st, xp, ab, reinterpret_cast<T*>(y),
                        reinterpret_cast<uint8_t*>(idx), g);
   });
   check_launch();
@@ -905,12 +928,12 @@ void bn_pool_bwd(uintptr_t dy, uintptr_t idx, uintptr_t x, uintptr_t save_mean, 
     const T* dyp = reinterpret_cast<const T*>(dy);
     const uint8_t* ip = reinterpret_cast<const uint8_t*>(idx);
     const T* xp = reinterpret_cast<const T*>(x);
-    hipLaunchKernelGGL((bn_pool_bwd_reduce_kernel<T>), dim3(nb), dim3(kBlock), 0, st, dyp, ip, xp, ws, g);
+    hipLaunchKernelGGL((bn_pool_bwd_reduce_kernel<T, 3, 2>), dim3(nb), dim3(kBlock), 0, st, dyp, ip, xp, ws, g);
     hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + kFinCh - 1) / kFinCh), dim3(kFinCh * kFinRg), 0, st, ws,
                        nb, M, C, reinterpret_cast<const float*>(gamma), reinterpret_cast<const float*>(save_mean),
                        reinterpret_cast<const float*>(save_invstd), reinterpret_cast<float*>(dgamma),
                        reinterpret_cast<float*>(dbeta), k3, int(accumulate));
-    hipLaunchKernelGGL((bn_pool_bwd_apply_kernel<T>), agrid, dim3(kBlock), 0, st, dyp, ip, xp, k3,
+    hipLaunchKernelGGL((bn_pool_bwd_apply_kernel<T, 3, 2>), agrid, dim3(kBlock), 0, st, dyp, ip, xp, k3,
                        reinterpret_cast<T*>(dx), g);
   });
   check_launch();

@@ -19,6 +19,13 @@ struct PoolGeom {
 
 template <typename T> struct V8;
 template <> struct V8<BF16> {
+  using Raw = uint4;  // loaded now, converted later: many loads in flight per thread
+  static __device__ __forceinline__ Raw load_raw(const BF16* p) { return *reinterpret_cast<const uint4*>(p); }
+  static __device__ __forceinline__ void cvt(const Raw& u, float (&v)[8]) {
+    const uint32_t w[4] = {u.x, u.y, u.z, u.w};
+#pragma unroll
+    for (int k = 0; k < 4; ++k) { v[2 * k] = bf2f(w[k] & 0xffff); v[2 * k + 1] = bf2f(w[k] >> 16); }
+  }
   static __device__ __forceinline__ void load(const BF16* p, float (&v)[8]) {
     const uint4 u = *reinterpret_cast<const uint4*>(p);
     const uint32_t w[4] = {u.x, u.y, u.z, u.w};
@@ -35,6 +42,15 @@ template <> struct V8<BF16> {
   }
 };
 template <> struct V8<float> {
+  struct Raw {
+    float4 a, b;
+  };
+  static __device__ __forceinline__ Raw load_raw(const float* p) {
+    return {*reinterpret_cast<const float4*>(p), *reinterpret_cast<const float4*>(p + 4)};
+  }
+  static __device__ __forceinline__ void cvt(const Raw& r, float (&v)[8]) {
+    v[0] = r.a.x; v[1] = r.a.y; v[2] = r.a.z; v[3] = r.a.w; v[4] = r.b.x; v[5] = r.b.y; v[6] = r.b.z; v[7] = r.b.w;
+  }
   static __device__ __forceinline__ void load(const float* p, float (&v)[8]) {
     const float4 a = *reinterpret_cast<const float4*>(p), b = *reinterpret_cast<const float4*>(p + 4);
     v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
@@ -118,6 +134,101 @@ __global__ __launch_bounds__(256) void maxpool_bwd_kernel(const T* __restrict__ 
   V8<T>::store(dx + ((int64_t(blockIdx.x) * g.W + w) * CG + cg) * 8, acc);
 }
 
+// Compile-time windows (ResNet's 3x3 / stride 2): every window load of a thread is issued
+// before the first compare (clamped addresses, out-of-image taps masked afterwards).  The
+// runtime-window kernels above branch between loads, so each thread waits on one load at
+// a time: 3.3 TB/s forward, 2.4 TB/s backward on the 411 MB stem tensor (rocprofv3,
+// profiles/raw/r2_stem_split_kernel_stats.csv).
+template <typename T, int K, int S>
+__global__ __launch_bounds__(256) void maxpool_fwd_fixed_kernel(const T* __restrict__ x, T* __restrict__ y,
+                                                                uint8_t* __restrict__ idx, PoolGeom g) {
+  const int CG = g.C / 8;
+  const int j = int(blockIdx.y) * 256 + int(threadIdx.x);
+  if (j >= g.Wo * CG) return;
+  const int n = int(blockIdx.x) / g.Ho, ho = int(blockIdx.x) % g.Ho;
+  const int wo = j / CG, cg = j - wo * CG;
+  const T* xn = x + int64_t(n) * g.H * g.W * g.C + cg * 8;
+  const int h0 = ho * S - g.p, w0 = wo * S - g.p;
+  typename V8<T>::Raw raw[K * K];
+#pragma unroll
+  for (int kh = 0; kh < K; ++kh) {
+    const int hc = min(max(h0 + kh, 0), g.H - 1);
+#pragma unroll
+    for (int kw = 0; kw < K; ++kw) {
+      const int wc = min(max(w0 + kw, 0), g.W - 1);
+      raw[kh * K + kw] = V8<T>::load_raw(xn + (int64_t(hc) * g.W + wc) * g.C);
+    }
+  }
+  float best[8];
+  uint32_t arg[8];
+#pragma unroll
+  for (int c = 0; c < 8; ++c) { best[c] = -__builtin_huge_valf(); arg[c] = 0; }
+#pragma unroll
+  for (int kh = 0; kh < K; ++kh) {
+#pragma unroll
+    for (int kw = 0; kw < K; ++kw) {
+      const bool ok = unsigned(h0 + kh) < unsigned(g.H) && unsigned(w0 + kw) < unsigned(g.W);
+      float v[8];
+      V8<T>::cvt(raw[kh * K + kw], v);
+#pragma unroll
+      for (int c = 0; c < 8; ++c)
+        if (ok && (v[c] > best[c] || (v[c] != v[c] && best[c] == best[c]))) { best[c] = v[c]; arg[c] = kh * K + kw; }
+    }
+  }
+  const int64_t i = (int64_t(blockIdx.x) * g.Wo + wo) * CG + cg;
+  V8<T>::store(y + i * 8, best);
+  uint2 a;
+  a.x = arg[0] | (arg[1] << 8) | (arg[2] << 16) | (arg[3] << 24);
+  a.y = arg[4] | (arg[5] << 8) | (arg[6] << 16) | (arg[7] << 24);
+  *reinterpret_cast<uint2*>(idx + i * 8) = a;
+}
+
+template <typename T, int K, int S>
+__global__ __launch_bounds__(256) void maxpool_bwd_fixed_kernel(const T* __restrict__ dy,
+                                                                const uint8_t* __restrict__ idx,
+                                                                T* __restrict__ dx, PoolGeom g) {
+  constexpr int NW = (K + S - 1) / S;  // windows per dimension covering a pixel
+  const int CG = g.C / 8;
+  const int j = int(blockIdx.y) * 256 + int(threadIdx.x);
+  if (j >= g.W * CG) return;
+  const int n = int(blockIdx.x) / g.H, h = int(blockIdx.x) % g.H;
+  const int w = j / CG, cg = j - w * CG;
+  const int ho0 = max(0, (h + g.p - K + S) / S), wo0 = max(0, (w + g.p - K + S) / S);
+  const int64_t nbase = int64_t(n) * g.Ho * g.Wo * g.C + cg * 8;
+  uint2 a[NW * NW];
+  typename V8<T>::Raw raw[NW * NW];
+#pragma unroll
+  for (int dh = 0; dh < NW; ++dh) {
+    const int hoc = min(ho0 + dh, g.Ho - 1);
+#pragma unroll
+    for (int dw = 0; dw < NW; ++dw) {
+      const int64_t o = nbase + (int64_t(hoc) * g.Wo + min(wo0 + dw, g.Wo - 1)) * g.C;
+      a[dh * NW + dw] = *reinterpret_cast<const uint2*>(idx + o);
+      raw[dh * NW + dw] = V8<T>::load_raw(dy + o);
+    }
+  }
+  float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+#pragma unroll
+  for (int dh = 0; dh < NW; ++dh) {
+    const int ho = ho0 + dh, kh = h - (ho * S - g.p);
+#pragma unroll
+    for (int dw = 0; dw < NW; ++dw) {
+      const int wo = wo0 + dw, kw = w - (wo * S - g.p);
+      const bool ok = ho < g.Ho && wo < g.Wo && unsigned(kh) < unsigned(K) && unsigned(kw) < unsigned(K);
+      const uint32_t want = ok ? uint32_t(kh * K + kw) : 0x100u;  // 0x100 matches no byte
+      float d[8];
+      V8<T>::cvt(raw[dh * NW + dw], d);
+      const uint2 u = a[dh * NW + dw];
+#pragma unroll
+      for (int c = 0; c < 8; ++c) {
+        const uint32_t ac = ((c < 4 ? u.x : u.y) >> (8 * (c & 3))) & 0xff;
+        if (ac == want) acc[c] += d[c];
+      }
+    }
+  }
+  V8<T>::store(dx + ((int64_t(blockIdx.x) * g.W + w) * CG + cg) * 8, acc);
+}
+
 }  // namespace
 
 void maxpool2d_fwd(uintptr_t x, uintptr_t y, uintptr_t idx, int N, int H, int W, int C, int Ho, int Wo, int k, int s,
@@ -126,7 +237,14 @@ void maxpool2d_fwd(uintptr_t x, uintptr_t y, uintptr_t idx, int N, int H, int W,
   VODA_CHECK(int64_t(Wo) * (C / 8) < (int64_t(1) << 24) && int64_t(N) * Ho < (int64_t(1) << 31), "maxpool: shape too large");
   const PoolGeom g{N, H, W, C, Ho, Wo, k, s, p};
   const dim3 grid(unsigned(int64_t(N) * Ho), unsigned((Wo * (C / 8) + 255) / 256));
-  if (dt == kBF16)
+  const bool k3s2 = k == 3 && s == 2;
+  if (dt == kBF16 && k3s2)
+    hipLaunchKernelGGL((maxpool_fwd_fixed_kernel<BF16, 3, 2>), dim3(grid), dim3(256), 0, as_stream(stream),
+                       reinterpret_cast<const BF16*>(x), reinterpret_cast<BF16*>(y), reinterpret_cast<uint8_t*>(idx), g);
+  else if (dt == kF32 && k3s2)
+    hipLaunchKernelGGL((maxpool_fwd_fixed_kernel<float, 3, 2>), dim3(grid), dim3(256), 0, as_stream(stream),
+                       reinterpret_cast<const float*>(x), reinterpret_cast<float*>(y), reinterpret_cast<uint8_t*>(idx), g);
+  else if (dt == kBF16)
     hipLaunchKernelGGL((maxpool_fwd_kernel<BF16>), dim3(grid), dim3(256), 0, as_stream(stream),
                        reinterpret_cast<const BF16*>(x), reinterpret_cast<BF16*>(y), reinterpret_cast<uint8_t*>(idx), g);
   else if (dt == kF32)
@@ -143,7 +261,14 @@ void maxpool2d_bwd(uintptr_t dy, uintptr_t idx, uintptr_t dx, int N, int H, int 
   VODA_CHECK(int64_t(W) * (C / 8) < (int64_t(1) << 24) && int64_t(N) * H < (int64_t(1) << 31), "maxpool: shape too large");
   const PoolGeom g{N, H, W, C, Ho, Wo, k, s, p};
   const dim3 grid(unsigned(int64_t(N) * H), unsigned((W * (C / 8) + 255) / 256));
-  if (dt == kBF16)
+  const bool k3s2 = k == 3 && s == 2;
+  if (dt == kBF16 && k3s2)
+    hipLaunchKernelGGL((maxpool_bwd_fixed_kernel<BF16, 3, 2>), dim3(grid), dim3(256), 0, as_stream(stream),
+                       reinterpret_cast<const BF16*>(dy), reinterpret_cast<const uint8_t*>(idx), reinterpret_cast<BF16*>(dx), g);
+  else if (dt == kF32 && k3s2)
+    hipLaunchKernelGGL((maxpool_bwd_fixed_kernel<float, 3, 2>), dim3(grid), dim3(256), 0, as_stream(stream),
+                       reinterpret_cast<const float*>(dy), reinterpret_cast<const uint8_t*>(idx), reinterpret_cast<float*>(dx), g);
+  else if (dt == kBF16)
     hipLaunchKernelGGL((maxpool_bwd_kernel<BF16>), dim3(grid), dim3(256), 0, as_stream(stream),
                        reinterpret_cast<const BF16*>(dy), reinterpret_cast<const uint8_t*>(idx), reinterpret_cast<BF16*>(dx), g);
   else if (dt == kF32)

@@ -16,12 +16,18 @@
 //  * v_mfma_f32_32x32x16_bf16; 4 waves as 2 x 2, each wave a 64 x 64 sub-tile (2 x 2 MFMA
 //    tiles, 64 fp32 accumulators per lane).  LDS double-buffered with register staging: the
 //    loads of stage s+1 are issued before the MFMAs of stage s and written after them.
-//  * XCD-aware block remap (guide T1): consecutive logical blocks -- the splits of one tile,
-//    then neighbouring tiles that share operand panels -- land on the same XCD / L2.
+//  * XCD-aware block remap (guide T1): consecutive logical blocks land on the same XCD / L2.
+//    Logical order split-major (default, VODA_WGRAD_ORDER=1): an XCD's ~grid/8 blocks are
+//    neighbouring tiles of ONE split -- a (rows x cols) patch of the output whose workgroups
+//    stream the same token range, so each dY / X stage fetched into the XCD's L2 feeds a whole
+//    row / column of the patch.  The older order (0) put the splits of one tile on one XCD:
+//    they read disjoint token ranges and share nothing.
 //  * the bias gradient rides along: in workgroups of output-column block 0 the waves of
 //    column half 0 also multiply their dY fragments by a ones operand (one extra MFMA per
 //    dY fragment), which is sum_m dY[m][n] in fp32 with no second pass over dY.
 #include "common.h"
+
+#include <cstdlib>
 #include "ops.h"
 
 namespace voda {
@@ -52,6 +58,8 @@ struct WgradArgs {
   float* ws;                         // [S][N][K] + [S][N] partial slabs (splits > 1)
   const uint16_t* zero;              // >= 16 zero bytes: source of rows past the split (LDS-DMA path)
   int M, N, K, S, m_split, tiles_k, remap, accumulate, bias;
+  int split_major;  // logical block order: 0 = splits of one tile adjacent, 1 = tiles of one split adjacent
+  int tiles_total;  // output tiles per tap (split_major decode)
   // epilogue addressing: dW column (and workspace column) offset and workspace row stride
   int col0, ws_ld;
   // implicit-GEMM convolution weight gradient (CONV kernels only): X rows are the input
@@ -155,8 +163,8 @@ __global__ __launch_bounds__(kWgThreads, 2) void wgrad_kernel(WgradArgs p) {
 
   int bid = blockIdx.x;
   if (p.remap) bid = (bid & 7) * int(gridDim.x >> 3) + (bid >> 3);
-  const int split = bid % p.S;
-  const int tile = bid / p.S;
+  const int split = p.split_major ? bid / p.tiles_total : bid % p.S;
+  const int tile = p.split_major ? bid - split * p.tiles_total : bid / p.S;
   const int n0 = (tile / p.tiles_k) * kWgBN;
   const int k0 = (tile % p.tiles_k) * kWgBK;
   const int mb = split * p.m_split;
@@ -340,8 +348,8 @@ __global__ __launch_bounds__(kWgThreads, 1) void wgrad_glds_kernel(WgradArgs p) 
     bid -= tap * per_tap;
     p.col0 = tap * p.K;
   }
-  const int split = bid % p.S;
-  const int tile = bid / p.S;
+  const int split = p.split_major ? bid / p.tiles_total : bid % p.S;
+  const int tile = p.split_major ? bid - split * p.tiles_total : bid / p.S;
   const int n0 = (tile / p.tiles_k) * kWgBN;
   const int k0 = (tile % p.tiles_k) * kWgBK;
   const int mb = split * p.m_split;
@@ -487,8 +495,8 @@ __global__ __launch_bounds__(kWwThreads, 1) void wgrad_wide_kernel(WgradArgs p) 
 
   int bid = blockIdx.x;
   if (p.remap) bid = (bid & 7) * int(gridDim.x >> 3) + (bid >> 3);
-  const int split = bid % p.S;
-  const int tile = bid / p.S;
+  const int split = p.split_major ? bid / p.tiles_total : bid % p.S;
+  const int tile = p.split_major ? bid - split * p.tiles_total : bid / p.S;
   const int n0 = (tile / p.tiles_k) * kWwTile;
   const int k0 = (tile % p.tiles_k) * kWwTile;
   const int mb = split * p.m_split;
@@ -714,6 +722,15 @@ struct WgradPlan {
   int S, m_split, tiles_k, grid;
 };
 
+// VODA_WGRAD_ORDER=0|1 (A/B switch, read once): logical block order, see the header
+int wgrad_split_major() {
+  static const int v = [] {
+    const char* e = std::getenv("VODA_WGRAD_ORDER");
+    return e ? (std::atoi(e) != 0 ? 1 : 0) : 1;
+  }();
+  return v;
+}
+
 WgradPlan wgrad_plan(int M, int N, int K, int splits, int tile = kWgBN) {
   WgradPlan pl;
   const int tiles_n = (N + tile - 1) / tile;
@@ -758,6 +775,8 @@ void wgrad_gemm(uintptr_t dy, int64_t ldy, uintptr_t x, int64_t ldx, uintptr_t d
   a.taps = 1; a.KW = 1; a.H = a.W = a.Ho = a.Wo = 1; a.cstride = 1; a.pad = 0; a.tiles_nk = 0;
   a.adv_n = a.adv_ho = a.adv_wo = 0;
   a.remap = (pl.grid % 8 == 0) ? 1 : 0;
+  a.split_major = wgrad_split_major();
+  a.tiles_total = pl.grid / pl.S;
   a.accumulate = accumulate ? 1 : 0;
   a.bias = db != 0 ? 1 : 0;
   a.out_f32 = out_dt == kF32 ? 1 : 0;
@@ -837,6 +856,8 @@ void wgrad_conv(uintptr_t dy, uintptr_t x, uintptr_t dw, int Nimg, int H, int W,
   a.out_f32 = out_dt == kF32 ? 1 : 0;
   const int64_t grid = int64_t(pl.grid) * taps;
   a.remap = (grid % 8 == 0) ? 1 : 0;
+  a.split_major = wgrad_split_major();
+  a.tiles_total = pl.grid / pl.S;
   hipStream_t s = as_stream(stream);
   hipLaunchKernelGGL((wgrad_glds_kernel<2, BM, true>), dim3(unsigned(grid)), dim3(kWgThreads), 0, s, a);
   check_launch();

@@ -126,6 +126,7 @@ def test_resnet50_step_uses_fused_bn_kernels():
 
 
 @pytest.mark.parametrize("shape,k,s,p", [((8, 64, 112, 112), 3, 2, 1), ((4, 96, 17, 17), 3, 2, 0), ((2, 64, 32, 32), 2, 2, 0),
+                                         ((2, 8, 1, 5), 3, 2, 1), ((2, 16, 6, 6), 3, 2, 1),
                                          ((3, 8, 9, 7), 3, 1, 1)])
 @pytest.mark.parametrize("dt", [torch.bfloat16, torch.float32])
 def test_maxpool_nhwc_fwd_bwd(shape, k, s, p, dt):
@@ -164,8 +165,8 @@ def test_bn_param_grads_accumulate_into_flat_buffer():
     torch.testing.assert_close(b.bias.grad, a.bias.grad, atol=1e-3, rtol=1e-3)
 
 
-@pytest.mark.parametrize("shape,k,s,p", [((4, 64, 112, 112), 3, 2, 1), ((3, 16, 17, 13), 3, 2, 1), ((2, 24, 9, 9), 2, 2, 0),
-                                         ((2, 8, 7, 7), 3, 1, 1)])
+@pytest.mark.parametrize("shape,k,s,p", [((4, 64, 112, 112), 3, 2, 1), ((3, 16, 17, 13), 3, 2, 1), ((2, 24, 9, 9), 3, 2, 0),
+                                         ((2, 8, 7, 7), 3, 2, 1), ((2, 8, 1, 5), 3, 2, 1)])
 @pytest.mark.parametrize("dt", [torch.bfloat16, torch.float32])
 def test_bn_relu_maxpool_fused_matches_composition(shape, k, s, p, dt, monkeypatch):
     """maxpool(relu(bn(x))) on the fused stem kernels == the fp32 PyTorch composition:
@@ -201,6 +202,19 @@ def test_bn_relu_maxpool_fused_matches_composition(shape, k, s, p, dt, monkeypat
     torch.testing.assert_close(xi.grad.float(), xr.grad, atol=5 * tol, rtol=5 * tol)
     torch.testing.assert_close(m.weight.grad, ref.weight.grad, atol=tol * M ** 0.5, rtol=tol)
     torch.testing.assert_close(m.bias.grad, ref.bias.grad, atol=tol * M ** 0.5, rtol=tol)
+
+
+def test_bn_relu_maxpool_other_windows_compose(monkeypatch):
+    """Windows other than 3x3/2 (not compiled into the fused kernels) take the composition."""
+    from vodascheduler_amd.ops import batchnorm
+    from vodascheduler_amd.ops.batchnorm import FusedBNReLUMaxPool2d
+
+    monkeypatch.setattr(batchnorm, "USE_FUSED_BN_POOL", True)
+    m = FusedBNReLUMaxPool2d(8, 2, 2, 0).cuda()
+    x = torch.randn(2, 8, 8, 8, device="cuda").to(memory_format=torch.channels_last)
+    assert not m._fused_ok(x)
+    ref = torch.nn.BatchNorm2d(8).cuda()
+    torch.testing.assert_close(m(x), F.max_pool2d(F.relu(ref(x)), 2, 2, 0), atol=1e-5, rtol=1e-5)
 
 
 def test_bn_relu_maxpool_eval_path():

@@ -27,9 +27,10 @@ from .dense import _ready
 # VODA_FUSED_BN=0: every BatchNorm takes the PyTorch reference composition (A/B and bisection
 # runs, e.g. benchmarks/graph_diag.py)
 USE_FUSED_BN = os.environ.get("VODA_FUSED_BN", "1") != "0"
-# VODA_FUSED_BN_POOL=1: the ResNet stem's BN+ReLU+maxpool on the fused kernels (opt-in until
-# the A/B favours it: profiles/raw/r2_ab_bn_sweep2_stem_pool.jsonl)
-USE_FUSED_BN_POOL = os.environ.get("VODA_FUSED_BN_POOL", "0") == "1"
+# VODA_FUSED_BN_POOL=0: the ResNet stem runs BN+ReLU and the max pool as two ops (A/B switch;
+# fused: stem fwd+bwd 1014-1051 -> 744 us, ResNet-50 bs-256 step 26.43/26.47 -> 26.17/26.18 ms,
+# profiles/raw/r2_ab_fused_stem.jsonl)
+USE_FUSED_BN_POOL = os.environ.get("VODA_FUSED_BN_POOL", "1") != "0"
 
 
 def _rows_view_ok(x: torch.Tensor) -> bool:
@@ -267,7 +268,7 @@ class FusedBNReLUMaxPool2d(FusedBatchNorm2d):
         return (USE_FUSED_BN and USE_FUSED_BN_POOL and self.training and self.track_running_stats
                 and x.is_cuda and x.dim() == 4 and x.dtype in (torch.bfloat16, torch.float32)
                 and x.is_contiguous(memory_format=torch.channels_last) and x.shape[1] % 8 == 0
-                and x.shape[1] <= 2048 and 2 * p <= k and k * k < 255
+                and x.shape[1] <= 2048 and (k, s) == (3, 2) and 2 * p <= k
                 and all(t is None or t.dtype == torch.float32 for t in (self.weight, self.bias)))
 
     def forward(self, x, residual=None, sink=None):
