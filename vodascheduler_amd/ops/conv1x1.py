@@ -30,6 +30,9 @@ from ..utils.flat import flat_grad
 from . import wgrad as W
 
 USE_CONV1X1_GEMM = os.environ.get("VODA_CONV1X1_GEMM", "1") != "0"
+# VODA_STRIDED_SINK=0: a stride-2 convolution hands its input gradient through the GradSink as a
+# zero-filled full-resolution tensor (A/B switch for _StridedGrad)
+USE_STRIDED_SINK = os.environ.get("VODA_STRIDED_SINK", "1") != "0"
 USE_GRAD_SINK = os.environ.get("VODA_GRAD_SINK", "1") != "0"
 # Opt-in (VODA_CONV1X1_HYBRID=1): for Cin < 128 (ResNet stage 1: 64 -> 256) keep forward and
 # input gradient on MIOpen and send the weight gradient to the split-K kernel, straight into
@@ -63,6 +66,27 @@ class GradSink:
     def take(self) -> torch.Tensor | None:
         g, self.buf = self.buf, None
         return g
+
+
+class _StridedGrad:
+    """Input gradient of a stride-s 1x1 convolution, handed through a GradSink WITHOUT the
+    zero-filled full-resolution tensor: ``g`` holds the gradient of the subsampled pixels
+    (every s-th row / column).  The consumer's GEMM writes its own full gradient (beta = 0)
+    and adds ``g`` into the strided positions -- instead of a full-size zero fill + scatter
+    that the GEMM then re-reads as its C operand (ResNet-50 downsample blocks: ~1 GB of
+    traffic per step less)."""
+
+    __slots__ = ("g", "stride", "shape")
+
+    def __init__(self, g: torch.Tensor, stride: int, shape):
+        self.g, self.stride, self.shape = g, stride, shape
+
+    def dense(self) -> torch.Tensor:
+        N_, C_, H_, W_ = self.shape
+        s = self.stride
+        dx = self.g.new_zeros((N_, H_, W_, C_)).permute(0, 3, 1, 2)  # channels_last
+        dx[:, :, ::s, ::s] = self.g
+        return dx
 
 
 def _direct(p: torch.Tensor) -> bool:
@@ -112,15 +136,27 @@ class _Conv1x1Fn(torch.autograd.Function):
         w2 = weight.reshape(cout, cin)
         dx = None
         acc = ctx.sink_in.take() if ctx.sink_in is not None and ctx.needs_input_grad[0] else None
+        strided = None
+        if isinstance(acc, _StridedGrad):
+            if tuple(acc.shape) == tuple(in_shape) and acc.g.dtype == dy2.dtype:
+                strided, acc = acc, None
+            else:
+                acc = acc.dense()
         if acc is not None and (acc.shape != in_shape or acc.dtype != dy2.dtype
                                 or not acc.is_contiguous(memory_format=torch.channels_last)):
             acc = acc.to(dy2.dtype).contiguous(memory_format=torch.channels_last)  # still owned here
-        if acc is not None:
+        if strided is not None:
+            dx = (dy2 @ w2).view(n, h, w, cin).permute(0, 3, 1, 2)
+            s_ = strided.stride
+            dx[:, :, ::s_, ::s_].add_(strided.g)
+        elif acc is not None:
             _as_2d(acc).addmm_(dy2, w2)  # dX = shortcut gradient + dY . W (one GEMM, beta = 1)
             dx = acc
         elif ctx.needs_input_grad[0]:
             dxs = (dy2 @ w2).view(n, h, w, cin).permute(0, 3, 1, 2)
-            if stride > 1:
+            if stride > 1 and ctx.sink_out is not None and USE_STRIDED_SINK:
+                dx = _StridedGrad(dxs, stride, in_shape)  # the consumer adds it in place
+            elif stride > 1:
                 N_, C_, H_, W_ = in_shape
                 dx = dxs.new_zeros((N_, H_, W_, C_)).permute(0, 3, 1, 2)  # channels_last
                 dx[:, :, ::stride, ::stride] = dxs
