@@ -61,6 +61,8 @@ def main():
     ap.add_argument("--only", default="", help="substring filter on shape names")
     ap.add_argument("--no-blaslt", action="store_true")
     ap.add_argument("--sweep", action="store_true", help="time every variant x split count (no hipBLASLt)")
+    ap.add_argument("--variants", default="0,1,2,3,4,5,6,7,8", help="sweep: variants to time")
+    ap.add_argument("--split-mults", default="0.25,0.5,1,2", help="sweep: multiples of the default split count")
     a = ap.parse_args()
     _native.hip()
     dev = torch.device("cuda", 0)
@@ -82,9 +84,9 @@ def main():
         r["ours_us"], r["ours_tflops"] = round(t, 2), round(tf / (t * 1e-6), 1)
         if a.sweep:
             best = None
-            for v in range(0, 9):
+            for v in [int(t) for t in a.variants.split(",")]:
                 base = W.default_splits(M, N, K, variant=v)
-                for sp in sorted({max(1, base // 4), max(1, base // 2), base, min(256, base * 2)}):
+                for sp in sorted({max(1, min(256, round(base * float(f)))) for f in a.split_mults.split(",")}):
                     try:
                         t = timeit(lambda: W.wgrad_accumulate_(dy, x, gw, splits=sp, variant=v), iters=10, warm=2)
                     except Exception as e:  # a variant may reject a shape
