@@ -128,9 +128,28 @@ __device__ __forceinline__ void stage_tile(const uint16_t* __restrict__ g, int64
   }
 }
 
-__device__ __forceinline__ float mask_add(const AttnArgs& a, const uint8_t* mrow, int key, int query) {
-  if (key >= a.Tk) return kNegInf;
-  if (mrow != nullptr && mrow[key] == 0) return kMaskNeg;
+// Mask codes of one 32-key tile, staged into LDS next to the K/V tile: 0 attend, 1 key
+// padding (the reference's additive -1e9), 2 past Tk (-inf).  A lane needs 16 of the 32 keys
+// (crow(i, h): four runs of 4 consecutive keys), i.e. four 4-byte LDS reads per tile instead
+// of sixteen global byte loads on the softmax's critical path.
+__device__ __forceinline__ void stage_mask(const AttnArgs& a, const uint8_t* mrow, int kt, uint8_t* ms) {
+  const int t = threadIdx.x;
+  if (t < kTile) {
+    const int key = kt + t;
+    ms[t] = key >= a.Tk ? 2 : ((mrow != nullptr && mrow[key] == 0) ? 1 : 0);
+  }
+}
+__device__ __forceinline__ void load_mask_words(const uint8_t* ms, int h, uint32_t (&mw)[4]) {
+#pragma unroll
+  for (int g = 0; g < 4; ++g) mw[g] = *reinterpret_cast<const uint32_t*>(ms + 8 * g + 4 * h);
+}
+// additive mask of accumulator register i (key kt + crow(i, h)): -inf past Tk, -1e9 for key
+// padding and (causal) future keys, else 0
+__device__ __forceinline__ float mask_code_add(const AttnArgs& a, const uint32_t (&mw)[4], int i, int key,
+                                               int query) {
+  const uint32_t code = (mw[i >> 2] >> (8 * (i & 3))) & 0xffu;
+  if (code == 2) return kNegInf;
+  if (code == 1) return kMaskNeg;
   if (a.causal && key > query) return kMaskNeg;
   return 0.f;
 }
@@ -160,6 +179,7 @@ __global__ __launch_bounds__(64 * W) void attn_fwd_kernel(AttnArgs a) {
   constexpr int TS = kTile + 8;        // transposed row stride
   __shared__ __attribute__((aligned(16))) uint16_t Ks[kTile * RS];
   __shared__ __attribute__((aligned(16))) uint16_t Vt[D * TS];
+  __shared__ __attribute__((aligned(16))) uint8_t Ms[kTile];
 
   const int bh = blockIdx.y, b = bh / a.H, hh = bh % a.H;
   const uint16_t* kb = a.k + b * a.k_sb + hh * a.k_sh;
@@ -181,14 +201,17 @@ __global__ __launch_bounds__(64 * W) void attn_fwd_kernel(AttnArgs a) {
     __syncthreads();  // every wave is done with the previous tile
     stage_tile<D, true, false>(kb, a.k_st, kt, a.Tk, Ks, RS, nullptr, 0);
     stage_tile<D, false, true>(vb, a.v_st, kt, a.Tk, nullptr, 0, Vt, TS);
+    stage_mask(a, mrow, kt, Ms);
     __syncthreads();
+    uint32_t mw[4];
+    load_mask_words(Ms, h, mw);
     f32x16 s_acc = zero16();
 #pragma unroll
     for (int s = 0; s < KS; ++s) s_acc = mfma(ld16(Ks + r * RS + 16 * s + 8 * h), qf[s], s_acc);
     float tmax = -1e30f;
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
-      const float v = s_acc[i] * a.scale + mask_add(a, mrow, kt + crow(i, h), q);
+      const float v = s_acc[i] * a.scale + mask_code_add(a, mw, i, kt + crow(i, h), q);
       s_acc[i] = v;
       tmax = fmaxf(tmax, v);
     }
@@ -231,6 +254,7 @@ __global__ __launch_bounds__(64 * W) void attn_bwd_dq_kernel(AttnArgs a) {
   __shared__ __attribute__((aligned(16))) uint16_t Ks[kTile * RS];
   __shared__ __attribute__((aligned(16))) uint16_t Vs[kTile * RS];
   __shared__ __attribute__((aligned(16))) uint16_t Kt[D * TS];
+  __shared__ __attribute__((aligned(16))) uint8_t Ms[kTile];
 
   const int bh = blockIdx.y, b = bh / a.H, hh = bh % a.H;
   const uint16_t* kb = a.k + b * a.k_sb + hh * a.k_sh;
@@ -264,7 +288,10 @@ __global__ __launch_bounds__(64 * W) void attn_bwd_dq_kernel(AttnArgs a) {
     __syncthreads();
     stage_tile<D, true, true>(kb, a.k_st, kt, a.Tk, Ks, RS, Kt, TS);
     stage_tile<D, true, false>(vb, a.v_st, kt, a.Tk, Vs, RS, nullptr, 0);
+    stage_mask(a, mrow, kt, Ms);
     __syncthreads();
+    uint32_t mw[4];
+    load_mask_words(Ms, h, mw);
     f32x16 s_acc = zero16(), dp = zero16();
 #pragma unroll
     for (int s = 0; s < KS; ++s) {
@@ -273,7 +300,7 @@ __global__ __launch_bounds__(64 * W) void attn_bwd_dq_kernel(AttnArgs a) {
     }
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
-      const float p = qv ? __expf(s_acc[i] * a.scale + mask_add(a, mrow, kt + crow(i, h), q) - lse) : 0.f;
+      const float p = qv ? __expf(s_acc[i] * a.scale + mask_code_add(a, mw, i, kt + crow(i, h), q) - lse) : 0.f;
       s_acc[i] = p * (dp[i] - delta);  // dS^T
     }
     const bf16x8 d0 = acc_frag(s_acc, 0), d1 = acc_frag(s_acc, 1);

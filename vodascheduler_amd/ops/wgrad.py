@@ -27,7 +27,8 @@ VARIANT = int(os.environ.get("VODA_WGRAD_VARIANT", "2"))
 # tall convolution-sized reductions use the deeper LDS rings at half the default split count
 # (per-shape sweep on MI355X, fp32 output, profiles/raw/r2_wgrad_variant_split_sweep.jsonl:
 # ResNet-50 stage 1 (M = 802816) 150-155 -> 131-137 us with variant 1, stage 2 (M = 200704)
-# 95-96 -> 79 us with variant 3; stages 3-4 and the BERT shapes gain nothing)
+# 95-96 -> 79 us with variant 3, and variant 1 once the block order became split-major;
+# stages 3-4 and the BERT shapes gain nothing)
 _VARIANT_FIXED = "VODA_WGRAD_VARIANT" in os.environ
 
 
@@ -35,8 +36,9 @@ def choose(M: int, N_: int, K: int) -> tuple[int, int]:
     """(variant, splits) for a weight-gradient GEMM of M reduction rows."""
     if _VARIANT_FIXED or M < 150_000:
         return VARIANT, default_splits(M, N_, K, variant=VARIANT)
-    v = 1 if M >= 600_000 else 3
-    return v, max(1, default_splits(M, N_, K, variant=v) // 2)
+    # split-major block order re-sweep (profiles/raw/r2_wgrad_sweep_split_major.jsonl): the
+    # 4-stage ring at half the default split count is best for stage 2 too (75-76 -> 72 us)
+    return 1, max(1, default_splits(M, N_, K, variant=1) // 2)
 _ZERO: dict[torch.device, torch.Tensor] = {}
 
 
