@@ -57,6 +57,15 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(const T* __restrict__ x, co
 #pragma unroll
   for (int it = 0; it < MAXITER; ++it)  // unconditional (clamped) loads, zeroed after
     v[it] = Vec4<T>::load(xr, min(it * 64 + lane, N4 - 1));
+  // gamma / beta issued with the row, not after the two reductions (a dependent L2 round trip
+  // at the end of every row otherwise)
+  float4 gw[MAXITER], bw[MAXITER];
+#pragma unroll
+  for (int it = 0; it < MAXITER; ++it) {
+    const int c4 = min(it * 64 + lane, N4 - 1);
+    gw[it] = gamma ? load_w4<WT>(gamma, c4) : make_float4(1.f, 1.f, 1.f, 1.f);
+    bw[it] = beta ? load_w4<WT>(beta, c4) : make_float4(0.f, 0.f, 0.f, 0.f);
+  }
   if constexpr (RES) {
     const T* rr = res + row * N;
     T* sr = sum + row * N;
@@ -94,8 +103,7 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(const T* __restrict__ x, co
   for (int it = 0; it < MAXITER; ++it) {
     const int c4 = it * 64 + lane;
     if (c4 < N4) {
-      float4 g = gamma ? load_w4<WT>(gamma, c4) : make_float4(1.f, 1.f, 1.f, 1.f);
-      float4 b = beta ? load_w4<WT>(beta, c4) : make_float4(0.f, 0.f, 0.f, 0.f);
+      const float4 g = gw[it], b = bw[it];
       float4 o;
       o.x = (v[it].x - mu) * rs * g.x + b.x;
       o.y = (v[it].y - mu) * rs * g.y + b.y;
@@ -140,6 +148,8 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const T* __restrict__ dy, c
     // rows are in flight; out-of-range lanes are zeroed after the conversion.  A branch or a
     // conversion right behind each load makes hipcc wait for it before issuing the next one.
     typename Raw4<T>::type xr[R][MAXITER], dr[R][MAXITER];
+    float mur[R], rsr[R];  // the rows' statistics ride with the row loads (a load issued in the
+                           // compute loop below would put one more dependent round trip per row)
 #pragma unroll
     for (int j = 0; j < R; ++j) {
       const int64_t row = min(row0 + j * rstride, M - 1);
@@ -149,6 +159,8 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const T* __restrict__ dy, c
         xr[j][it] = Raw4<T>::load(x + row * N, c4);
         dr[j][it] = Raw4<T>::load(dy + row * N, c4);
       }
+      mur[j] = mean[row];
+      rsr[j] = rstd[row];
     }
     float4 xv[R][MAXITER], dv[R][MAXITER];
 #pragma unroll
@@ -166,7 +178,7 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const T* __restrict__ dy, c
     for (int j = 0; j < R; ++j) {
       const int64_t row = row0 + j * rstride;
       if (row >= M) break;  // wave-uniform
-      const float mu = mean[row], rs = rstd[row];
+      const float mu = mur[j], rs = rsr[j];
       float4 xh[MAXITER], dg[MAXITER];
       float s1 = 0.f, s2 = 0.f;
 #pragma unroll

@@ -122,6 +122,24 @@ def test_grad_sink_handoff_cpu_semantics():
     assert s.take() is g and s.take() is None
 
 
+def test_strided_grad_dense_is_the_zero_filled_scatter():
+    """_StridedGrad (stride-2 downsample input gradient handed over subsampled) densifies to
+    exactly the zero-filled channels_last scatter the consumer would otherwise receive."""
+    from vodascheduler_amd.ops.conv1x1 import _StridedGrad
+
+    g = torch.randn(2, 8, 3, 4).to(memory_format=torch.channels_last)
+    d = _StridedGrad(g, 2, (2, 8, 6, 7)).dense()
+    ref = torch.zeros(2, 8, 6, 7)
+    ref[:, :, ::2, ::2] = g
+    assert d.is_contiguous(memory_format=torch.channels_last)
+    torch.testing.assert_close(d, ref, atol=0, rtol=0)
+    # the consumer's in-place form: full GEMM gradient + strided add == dense sum
+    full = torch.randn(2, 8, 6, 7).to(memory_format=torch.channels_last)
+    alt = full.clone()
+    alt[:, :, ::2, ::2].add_(g)
+    torch.testing.assert_close(alt, full + d, atol=0, rtol=0)
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("downsample", [False, True])
 def test_bottleneck_grad_sink_matches_autograd_sum(downsample, monkeypatch):
