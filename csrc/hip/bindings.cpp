@@ -27,6 +27,9 @@ PYBIND11_MODULE(_vodahip, m) {
   m.def("wgrad_conv_workspace_floats", &wgrad_conv_workspace_floats);
   m.def("wgrad_conv", &wgrad_conv);
   m.def("gelu_tanh_fwd", &gelu_tanh_fwd);
+  m.def("gemm_gelu_aux", &gemm_gelu_aux);
+  m.def("gemm_dgelu", &gemm_dgelu);
+  m.def("gemm_epilogue_algos", &gemm_epilogue_algos);
   m.def("gelu_tanh_bwd", &gelu_tanh_bwd);
   m.def("layernorm_fwd", &layernorm_fwd);
   m.def("layernorm_bwd", &layernorm_bwd);

@@ -140,10 +140,11 @@ def build_hip(verbose: bool = False, force: bool = False) -> Path:
             sys.stderr.write(f"$ {' '.join(cmd)}\n{outp}\n")
     if failed:
         raise RuntimeError("HIP extension compile failed")
-    # Link against the HIP runtime + RCCL bundled with torch (SONAME libamdhip64.so.7 /
-    # librccl.so.1 — identical to /opt/rocm, so the already-loaded copies are reused).
+    # Link against the HIP runtime + RCCL + hipBLASLt bundled with torch (SONAME
+    # libamdhip64.so.7 / librccl.so.1 / libhipblaslt.so.1 — the copies torch already loaded
+    # are reused).
     link = [hipcc, f"--offload-arch={GPU_ARCH}", "-shared", "-fPIC", *map(str, objs),
-            f"-L{tlib}", "-lamdhip64", "-lrccl", f"-Wl,-rpath,{tlib}", "-o", str(out)]
+            f"-L{tlib}", "-lamdhip64", "-lrccl", "-lhipblaslt", f"-Wl,-rpath,{tlib}", "-o", str(out)]
     _run(link, verbose)
     _write_stamp(out, digest)
     return out

@@ -96,6 +96,40 @@ def colsum_accumulate_(dy2: torch.Tensor, out: torch.Tensor) -> None:
                         ws.data_ptr(), N.stream_of(dy2))
 
 
+def linear_weight_grads(dy2: torch.Tensor, x2: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor | None,
+                        need_w: bool, need_b: bool):
+    """Weight / bias gradients of ``y = x W^T + b`` from dY [M, n_out] and X [M, K].  When the
+    optimizer owns flat gradients for them they are accumulated in place (split-K MFMA kernel
+    with the fused bias gradient, ops/wgrad.py) and the DDP engine is signalled; returns the
+    (dw, db) autograd must still deliver (None for the in-place ones)."""
+    dw = db = None
+    fused = (USE_WGRAD_KERNEL and need_w and _direct(weight) and (not need_b or _direct(bias))
+             and W.supported(dy2, x2, flat_grad(weight), flat_grad(bias) if need_b else None))
+    if fused:
+        W.wgrad_accumulate_(dy2, x2, flat_grad(weight), flat_grad(bias) if need_b else None)
+        _ready(weight)
+        if need_b:
+            _ready(bias)
+        return None, None
+    if need_w:
+        if _direct(weight):
+            gw = flat_grad(weight)
+            if gw.dtype == dy2.dtype:
+                gw.addmm_(dy2.t(), x2)
+            else:  # fp32 flat gradient of a bf16 weight
+                gw.add_(dy2.t() @ x2)
+            _ready(weight)
+        else:
+            dw = dy2.t() @ x2
+    if need_b:
+        if _direct(bias):
+            colsum_accumulate_(dy2, flat_grad(bias))
+            _ready(bias)
+        else:
+            db = dy2.float().sum(0).to(bias.dtype)
+    return dw, db
+
+
 class _DenseFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, weight, bias, sink_in=None):
@@ -131,30 +165,7 @@ class _DenseFn(torch.autograd.Function):
         elif ctx.needs_input_grad[0]:
             dx = _dgrad(dy2, weight).view(x.shape)
         need_w, need_b = ctx.needs_input_grad[1], bias is not None and ctx.needs_input_grad[2]
-        fused = (USE_WGRAD_KERNEL and need_w and _direct(weight) and (not need_b or _direct(bias))
-                 and W.supported(dy2, x2, flat_grad(weight), flat_grad(bias) if need_b else None))
-        if fused:
-            W.wgrad_accumulate_(dy2, x2, flat_grad(weight), flat_grad(bias) if need_b else None)
-            _ready(weight)
-            if need_b:
-                _ready(bias)
-            return dx, None, None, None
-        if need_w:
-            if _direct(weight):
-                gw = flat_grad(weight)
-                if gw.dtype == dy2.dtype:
-                    gw.addmm_(dy2.t(), x2)
-                else:  # fp32 flat gradient of a bf16 weight
-                    gw.add_(dy2.t() @ x2)
-                _ready(weight)
-            else:
-                dw = dy2.t() @ x2
-        if need_b:
-            if _direct(bias):
-                colsum_accumulate_(dy2, flat_grad(bias))
-                _ready(bias)
-            else:
-                db = dy2.float().sum(0).to(bias.dtype)
+        dw, db = linear_weight_grads(dy2, x2, weight, bias, need_w, need_b)
         return dx, dw, db, None
 
 
