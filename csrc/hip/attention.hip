@@ -128,6 +128,53 @@ __device__ __forceinline__ void stage_tile(const uint16_t* __restrict__ g, int64
   }
 }
 
+// Register-staged prefetch of one kTile-row tile (threads NT): the global loads of tile t + 1
+// are issued right after tile t reached LDS, so they are in flight while tile t is computed,
+// and land in LDS behind the next barrier.  PER = 16-byte vectors per thread per tile; used
+// when PER <= 4 (head dim 64 at any workgroup size, 128 with >= 2 waves), else the kernels
+// stage synchronously (stage_tile).  Out-of-range rows are clamped for the load and zeroed
+// after it (no branch between the loads).
+template <int D, int NT>
+struct TileRegs {
+  static constexpr int VPR = D / 8;
+  static constexpr int NV = kTile * VPR;
+  static constexpr int PER = (NV + NT - 1) / NT;
+  uint4 v[PER];
+  __device__ __forceinline__ void load(const uint16_t* __restrict__ g, int64_t st, int t0, int T) {
+#pragma unroll
+    for (int j = 0; j < PER; ++j) {
+      const int i = min(int(threadIdx.x) + j * NT, NV - 1);
+      const int r = i / VPR, c = (i % VPR) * 8;
+      v[j] = *reinterpret_cast<const uint4*>(g + int64_t(min(t0 + r, T - 1)) * st + c);
+    }
+#pragma unroll
+    for (int j = 0; j < PER; ++j) {
+      const int i = int(threadIdx.x) + j * NT;
+      if (t0 + i / VPR >= T) v[j] = make_uint4(0, 0, 0, 0);
+    }
+  }
+  template <bool ROWS, bool TRANS>
+  __device__ __forceinline__ void store(uint16_t* rows, int rstride, uint16_t* trans, int tstride) const {
+#pragma unroll
+    for (int j = 0; j < PER; ++j) {
+      const int i = int(threadIdx.x) + j * NT;
+      if (NV % NT != 0 && i >= NV) break;
+      const int r = i / VPR, c = (i % VPR) * 8;
+      const uint4 u = v[j];
+      if constexpr (ROWS) *reinterpret_cast<uint4*>(rows + r * rstride + c) = u;
+      if constexpr (TRANS) {
+        const uint32_t w[4] = {u.x, u.y, u.z, u.w};
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const int d0 = c + 2 * k, d1 = d0 + 1;
+          trans[d0 * tstride + ((r + trans_rot(d0)) & 31)] = uint16_t(w[k] & 0xffff);
+          trans[d1 * tstride + ((r + trans_rot(d1)) & 31)] = uint16_t(w[k] >> 16);
+        }
+      }
+    }
+  }
+};
+
 // Mask codes of one 32-key tile, staged into LDS next to the K/V tile: 0 attend, 1 key
 // padding (the reference's additive -1e9), 2 past Tk (-inf).  A lane needs 16 of the 32 keys
 // (crow(i, h): four runs of 4 consecutive keys), i.e. four 4-byte LDS reads per tile instead
@@ -197,12 +244,30 @@ __global__ __launch_bounds__(64 * W) void attn_fwd_kernel(AttnArgs a) {
 #pragma unroll
   for (int t = 0; t < DT; ++t) o[t] = zero16();
   float m = -1e30f, l = 0.f;
+  using Regs = TileRegs<D, 64 * W>;
+  constexpr bool PF = Regs::PER <= 4;
+  Regs kr, vr;
+  if constexpr (PF) {
+    kr.load(kb, a.k_st, 0, a.Tk);
+    vr.load(vb, a.v_st, 0, a.Tk);
+  }
   for (int kt = 0; kt < a.Tk; kt += kTile) {
     __syncthreads();  // every wave is done with the previous tile
-    stage_tile<D, true, false>(kb, a.k_st, kt, a.Tk, Ks, RS, nullptr, 0);
-    stage_tile<D, false, true>(vb, a.v_st, kt, a.Tk, nullptr, 0, Vt, TS);
+    if constexpr (PF) {
+      kr.template store<true, false>(Ks, RS, nullptr, 0);
+      vr.template store<false, true>(nullptr, 0, Vt, TS);
+    } else {
+      stage_tile<D, true, false>(kb, a.k_st, kt, a.Tk, Ks, RS, nullptr, 0);
+      stage_tile<D, false, true>(vb, a.v_st, kt, a.Tk, nullptr, 0, Vt, TS);
+    }
     stage_mask(a, mrow, kt, Ms);
     __syncthreads();
+    if constexpr (PF) {
+      if (kt + kTile < a.Tk) {  // next tile's loads overlap this tile's compute
+        kr.load(kb, a.k_st, kt + kTile, a.Tk);
+        vr.load(vb, a.v_st, kt + kTile, a.Tk);
+      }
+    }
     uint32_t mw[4];
     load_mask_words(Ms, h, mw);
     f32x16 s_acc = zero16();
@@ -284,12 +349,30 @@ __global__ __launch_bounds__(64 * W) void attn_bwd_dq_kernel(AttnArgs a) {
   f32x16 dq[DT];
 #pragma unroll
   for (int t = 0; t < DT; ++t) dq[t] = zero16();
+  using Regs = TileRegs<D, 64 * W>;
+  constexpr bool PF = Regs::PER <= 4;
+  Regs kr, vr;
+  if constexpr (PF) {
+    kr.load(kb, a.k_st, 0, a.Tk);
+    vr.load(vb, a.v_st, 0, a.Tk);
+  }
   for (int kt = 0; kt < a.Tk; kt += kTile) {
     __syncthreads();
-    stage_tile<D, true, true>(kb, a.k_st, kt, a.Tk, Ks, RS, Kt, TS);
-    stage_tile<D, true, false>(vb, a.v_st, kt, a.Tk, Vs, RS, nullptr, 0);
+    if constexpr (PF) {
+      kr.template store<true, true>(Ks, RS, Kt, TS);
+      vr.template store<true, false>(Vs, RS, nullptr, 0);
+    } else {
+      stage_tile<D, true, true>(kb, a.k_st, kt, a.Tk, Ks, RS, Kt, TS);
+      stage_tile<D, true, false>(vb, a.v_st, kt, a.Tk, Vs, RS, nullptr, 0);
+    }
     stage_mask(a, mrow, kt, Ms);
     __syncthreads();
+    if constexpr (PF) {
+      if (kt + kTile < a.Tk) {
+        kr.load(kb, a.k_st, kt + kTile, a.Tk);
+        vr.load(vb, a.v_st, kt + kTile, a.Tk);
+      }
+    }
     uint32_t mw[4];
     load_mask_words(Ms, h, mw);
     f32x16 s_acc = zero16(), dp = zero16();
@@ -356,17 +439,45 @@ __global__ __launch_bounds__(64 * W) void attn_bwd_dkv_kernel(AttnArgs a) {
 #pragma unroll
     for (int t = 0; t < DT; ++t) dv[t] = zero16();
   }
+  using Regs = TileRegs<D, 64 * W>;
+  constexpr bool PF = Regs::PER <= 4;
+  Regs qr, dr;
+  float lse_r = 0.f, del_r = 0.f;  // row threadIdx.x of the prefetched tile (threads < kTile)
+  auto load_rows = [&](int qt) {
+    qr.load(qb, a.q_st, qt, a.Tq);
+    dr.load(db, a.do_st, qt, a.Tq);
+    const int i = min(int(threadIdx.x), kTile - 1);
+    const bool ok = qt + i < a.Tq;
+    const int64_t o = int64_t(bh) * a.Tq + min(qt + i, a.Tq - 1);
+    lse_r = a.lse[o];
+    del_r = a.delta[o];
+    if (!ok) { lse_r = __builtin_huge_valf(); del_r = 0.f; }  // pad rows: P = 0
+  };
+  if constexpr (PF) load_rows(0);
   for (int qt = 0; qt < a.Tq; qt += kTile) {
     __syncthreads();
-    stage_tile<D, true, DO_DK>(qb, a.q_st, qt, a.Tq, Qs, RS, Qt, TS);
-    if constexpr (DO_DK) stage_tile<D, true, DO_DV>(db, a.do_st, qt, a.Tq, Ds, RS, Dt, TS);
-    else stage_tile<D, false, true>(db, a.do_st, qt, a.Tq, nullptr, 0, Dt, TS);
-    for (int i = threadIdx.x; i < kTile; i += blockDim.x) {
-      const bool ok = qt + i < a.Tq;
-      lse_s[i] = ok ? a.lse[int64_t(bh) * a.Tq + qt + i] : __builtin_huge_valf();  // pad rows: P = 0
-      del_s[i] = ok ? a.delta[int64_t(bh) * a.Tq + qt + i] : 0.f;
+    if constexpr (PF) {
+      qr.template store<true, DO_DK>(Qs, RS, Qt, TS);
+      if constexpr (DO_DK) dr.template store<true, DO_DV>(Ds, RS, Dt, TS);
+      else dr.template store<false, true>(nullptr, 0, Dt, TS);
+      if (threadIdx.x < kTile) {
+        lse_s[threadIdx.x] = lse_r;
+        del_s[threadIdx.x] = del_r;
+      }
+    } else {
+      stage_tile<D, true, DO_DK>(qb, a.q_st, qt, a.Tq, Qs, RS, Qt, TS);
+      if constexpr (DO_DK) stage_tile<D, true, DO_DV>(db, a.do_st, qt, a.Tq, Ds, RS, Dt, TS);
+      else stage_tile<D, false, true>(db, a.do_st, qt, a.Tq, nullptr, 0, Dt, TS);
+      for (int i = threadIdx.x; i < kTile; i += blockDim.x) {
+        const bool ok = qt + i < a.Tq;
+        lse_s[i] = ok ? a.lse[int64_t(bh) * a.Tq + qt + i] : __builtin_huge_valf();  // pad rows: P = 0
+        del_s[i] = ok ? a.delta[int64_t(bh) * a.Tq + qt + i] : 0.f;
+      }
     }
     __syncthreads();
+    if constexpr (PF) {
+      if (qt + kTile < a.Tq) load_rows(qt + kTile);  // in flight during this tile's compute
+    }
     f32x16 s_acc = zero16(), dp = zero16();
 #pragma unroll
     for (int s = 0; s < KS; ++s) {
