@@ -31,6 +31,8 @@
 // the dK/dV pass runs twice (dV, then dK) so each pass keeps only one 256-wide accumulator
 // set (8 x 16 fp32 registers per lane) next to the two operand fragment sets.
 #include "common.h"
+
+#include <cstdlib>
 #include "ops.h"
 
 namespace voda {
@@ -541,8 +543,15 @@ void dispatch_d(int D, F&& f) {
 // waves per workgroup from the number of rows the workgroup's lanes own
 template <typename F>
 void dispatch_w(int rows, F&& f) {
-  if (rows <= 32) f(std::integral_constant<int, 1>{});
-  else if (rows <= 64) f(std::integral_constant<int, 2>{});
+  // VODA_ATTN_MAXW=1|2|4 (A/B switch, read once): cap on waves per workgroup -- smaller
+  // workgroups = more of them per (batch, head) to hide each one's per-tile latency
+  static const int maxw = [] {
+    const char* e = std::getenv("VODA_ATTN_MAXW");
+    const int v = e ? std::atoi(e) : 4;
+    return v >= 4 ? 4 : (v >= 2 ? 2 : 1);
+  }();
+  if (rows <= 32 || maxw == 1) f(std::integral_constant<int, 1>{});
+  else if (rows <= 64 || maxw == 2) f(std::integral_constant<int, 2>{});
   else f(std::integral_constant<int, 4>{});
 }
 
