@@ -156,8 +156,10 @@ class RcclCommunicator(Communicator):
 
     def barrier(self):
         x = torch.ones(1, device=self.device)
+        s = self.stream if self.stream is not None else torch.cuda.current_stream(self.device)
+        s.wait_stream(torch.cuda.current_stream(self.device))  # x is written on the current stream
         self.allreduce_(x)
-        torch.cuda.current_stream(self.device).synchronize()
+        s.synchronize()  # the stream the collective was enqueued on (the DDP side stream if set)
         self.check()
 
     def check(self) -> None:

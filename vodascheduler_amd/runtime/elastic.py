@@ -21,6 +21,8 @@ Protocol (see ``rendezvous.py`` for the store layout):
 """
 from __future__ import annotations
 
+import contextlib
+
 import io
 import logging
 import os
@@ -274,6 +276,25 @@ def broadcast_object(comm: Communicator, obj: Any, root: int) -> Any:
     return pickle.loads(data.cpu().numpy().tobytes())
 
 
+@contextlib.contextmanager
+def _collectives_on_current_stream(comm: Communicator | None):
+    """Run ``comm``'s collectives on the current stream for the duration (the state sync reads
+    their results on the host right away: ``.item()`` / ``.cpu()`` order against the current
+    stream only).  After ``ElasticDDP.set_communicator`` an RCCL communicator enqueues on the
+    DDP side stream; the current stream first waits for anything still queued there, so the
+    collective order every rank issues is kept."""
+    s = getattr(comm, "stream", None) if comm is not None else None
+    if s is None:
+        yield
+        return
+    torch.cuda.current_stream(comm.device).wait_stream(s)
+    comm.stream = None
+    try:
+        yield
+    finally:
+        comm.stream = s
+
+
 class State:
     """Elastic state: tensors (synced by broadcast) + picklable extras (epoch, batch, ...)."""
 
@@ -358,6 +379,11 @@ class State:
     def sync(self) -> None:
         ctx = self.ctx
         comm = ctx.comm
+        with _collectives_on_current_stream(comm):
+            self._sync_on(comm)
+
+    def _sync_on(self, comm) -> None:
+        ctx = self.ctx
         held = ctx.committed_step if ctx.holds_state else -1
         if comm is not None and comm.size > 1:
             t = torch.tensor([held], dtype=torch.int64, device=comm.device)
