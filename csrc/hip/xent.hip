@@ -103,9 +103,8 @@ __global__ __launch_bounds__(kXentThreads) void xent_fwd_kernel(const T* __restr
   XState st{-INFINITY, 0.f, -INFINITY, 0x7fffffff};
   bool nan_seen = false;
   const int vfull = V / VN * VN;
-  for (int c = threadIdx.x * VN; c < vfull; c += kXentThreads * VN) {
-    float v[VN];
-    XVec<T>::load(row + c, v);
+  // online (max, sum-exp, argmax) update with one loaded vector of columns c .. c+VN-1
+  auto absorb = [&](const float (&v)[VN], int c) {
     float vm = v[0];
     int vi = 0;
 #pragma unroll
@@ -121,6 +120,23 @@ __global__ __launch_bounds__(kXentThreads) void xent_fwd_kernel(const T* __restr
     st.s = s;
     st.m = m;
     if (vm > st.am) { st.am = vm; st.ai = c + vi; }  // columns grow within a lane: strict >
+  };
+  // XU vectors per lane loaded before the first is absorbed: XU loads in flight instead of
+  // one dependent HBM round trip per vector (the online update chains the iterations)
+  constexpr int XU = 4;
+  constexpr int kStride = kXentThreads * VN;
+  int c = threadIdx.x * VN;
+  for (; c + (XU - 1) * kStride < vfull; c += XU * kStride) {
+    float v[XU][VN];
+#pragma unroll
+    for (int u = 0; u < XU; ++u) XVec<T>::load(row + c + u * kStride, v[u]);
+#pragma unroll
+    for (int u = 0; u < XU; ++u) absorb(v[u], c + u * kStride);
+  }
+  for (; c < vfull; c += kStride) {
+    float v[VN];
+    XVec<T>::load(row + c, v);
+    absorb(v, c);
   }
   for (int c = vfull + threadIdx.x; c < V; c += kXentThreads) {  // tail (V not a multiple of VN)
     const float v = xload1(row + c);
@@ -164,9 +180,7 @@ __global__ __launch_bounds__(kXentThreads) void xent_bwd_kernel(const T* __restr
   const float l = lse[r];
   const int ldi = int(ld);
   const int vfull = ldi / VN * VN;  // ld is a multiple of VN (checked on the host)
-  for (int c = threadIdx.x * VN; c < vfull; c += kXentThreads * VN) {
-    float v[VN];
-    XVec<T>::load(row + c, v);
+  auto emit = [&](float (&v)[VN], int c) {
 #pragma unroll
     for (int j = 0; j < VN; ++j) {
       const int col = c + j;
@@ -174,6 +188,21 @@ __global__ __launch_bounds__(kXentThreads) void xent_bwd_kernel(const T* __restr
       v[j] = col < V ? scale * (p - (int64_t(col) == y ? 1.f : 0.f)) : 0.f;
     }
     XVec<T>::store(drow + c, v);
+  };
+  constexpr int XU = 4;  // loads in flight per lane, as in the forward
+  constexpr int kStride = kXentThreads * VN;
+  int c = threadIdx.x * VN;
+  for (; c + (XU - 1) * kStride < vfull; c += XU * kStride) {
+    float v[XU][VN];
+#pragma unroll
+    for (int u = 0; u < XU; ++u) XVec<T>::load(row + c + u * kStride, v[u]);
+#pragma unroll
+    for (int u = 0; u < XU; ++u) emit(v[u], c + u * kStride);
+  }
+  for (; c < vfull; c += kStride) {
+    float v[VN];
+    XVec<T>::load(row + c, v);
+    emit(v, c);
   }
 }
 
