@@ -123,7 +123,8 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const T* __restrict__ dy, c
                                                      const float* __restrict__ mean, const float* __restrict__ rstd,
                                                      const void* __restrict__ gamma, T* __restrict__ dx,
                                                      float* __restrict__ part_g, float* __restrict__ part_b,
-                                                     int64_t M, int N) {
+                                                     int64_t M, int N, float* __restrict__ acc_g,
+                                                     float* __restrict__ acc_b) {
   extern __shared__ __attribute__((aligned(16))) float lds[];  // [4][N]
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
@@ -214,8 +215,10 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const T* __restrict__ dy, c
       }
     }
   }
-  if (part_g == nullptr) return;  // gamma/beta gradients not requested
-  // combine the 4 waves' column partials through LDS, gamma then beta
+  if (part_g == nullptr && acc_g == nullptr) return;  // gamma/beta gradients not requested
+  // combine the 4 waves' column partials through LDS, gamma then beta; then either one
+  // partial row per block (col_sum_kernel adds them up) or -- acc_g/acc_b: the optimizer's
+  // fp32 flat gradient -- coalesced fp32 atomic adds straight into it (no second launch)
   for (int pass = 0; pass < 2; ++pass) {
 #pragma unroll
     for (int it = 0; it < MAXITER; ++it) {
@@ -223,8 +226,14 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const T* __restrict__ dy, c
       if (c4 < N4) reinterpret_cast<float4*>(lds + wave * N)[c4] = pass == 0 ? ag[it] : ab[it];
     }
     __syncthreads();
-    float* out = (pass == 0 ? part_g : part_b) + int64_t(blockIdx.x) * N;
-    for (int c = threadIdx.x; c < N; c += 256) out[c] = (lds[c] + lds[N + c]) + (lds[2 * N + c] + lds[3 * N + c]);
+    if (acc_g != nullptr) {
+      float* out = pass == 0 ? acc_g : acc_b;
+      for (int c = threadIdx.x; c < N; c += 256)
+        atomicAdd(out + c, (lds[c] + lds[N + c]) + (lds[2 * N + c] + lds[3 * N + c]));
+    } else {
+      float* out = (pass == 0 ? part_g : part_b) + int64_t(blockIdx.x) * N;
+      for (int c = threadIdx.x; c < N; c += 256) out[c] = (lds[c] + lds[N + c]) + (lds[2 * N + c] + lds[3 * N + c]);
+    }
     __syncthreads();
   }
 }
@@ -327,6 +336,17 @@ int ln_bwd_block_cap() {
   return cap;
 }
 
+// VODA_LN_ATOMIC=0 (A/B switch): fp32 flat-gradient dgamma/dbeta through the partial rows +
+// col_sum_kernel instead of atomic adds from the backward kernel.  The atomic form is not
+// bitwise reproducible run to run (fp32 addition order), like any atomic reduction.
+bool ln_bwd_atomic() {
+  static const bool on = [] {
+    const char* e = std::getenv("VODA_LN_ATOMIC");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+
 int layernorm_bwd_partial_rows(int64_t M) {
   int64_t g = (M + 3) / 4;
   return int(std::max<int64_t>(1, std::min<int64_t>(g, ln_bwd_block_cap())));
@@ -340,18 +360,26 @@ void layernorm_bwd(uintptr_t dy, uintptr_t x, uintptr_t mean, uintptr_t rstd, ui
   const int grid = layernorm_bwd_partial_rows(M);
   float* pg = nullptr;
   float* pb = nullptr;
+  float* ag = nullptr;
+  float* ab = nullptr;
   if (dgamma != 0) {
-    VODA_CHECK(workspace != 0 && dbeta != 0, "layernorm_bwd: workspace and dbeta required");
-    pg = reinterpret_cast<float*>(workspace);
-    pb = pg + int64_t(grid) * N;
+    VODA_CHECK(dbeta != 0, "layernorm_bwd: dbeta required");
+    if (accumulate && wdt == kF32 && ln_bwd_atomic()) {
+      ag = reinterpret_cast<float*>(dgamma);
+      ab = reinterpret_cast<float*>(dbeta);
+    } else {
+      VODA_CHECK(workspace != 0, "layernorm_bwd: workspace required");
+      pg = reinterpret_cast<float*>(workspace);
+      pb = pg + int64_t(grid) * N;
+    }
   }
   const size_t lds = size_t(4) * N * sizeof(float);
   LN_DISPATCH_T(dt, wdt, [&] {
     LN_DISPATCH_ITER(N, [&] {
-      hipLaunchKernelGGL((ln_bwd_kernel<T, WT, MI>), dim3(grid), dim3(256), pg ? lds : 0, as_stream(stream),
-                         reinterpret_cast<const T*>(dy), reinterpret_cast<const T*>(x),
+      hipLaunchKernelGGL((ln_bwd_kernel<T, WT, MI>), dim3(grid), dim3(256), (pg || ag) ? lds : 0,
+                         as_stream(stream), reinterpret_cast<const T*>(dy), reinterpret_cast<const T*>(x),
                          reinterpret_cast<const float*>(mean), reinterpret_cast<const float*>(rstd),
-                         reinterpret_cast<const void*>(gamma), reinterpret_cast<T*>(dx), pg, pb, M, N);
+                         reinterpret_cast<const void*>(gamma), reinterpret_cast<T*>(dx), pg, pb, M, N, ag, ab);
     });
     if (pg) {
       const unsigned cg = unsigned((N + 31) / 32);
