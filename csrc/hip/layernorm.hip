@@ -336,13 +336,14 @@ int ln_bwd_block_cap() {
   return cap;
 }
 
-// VODA_LN_ATOMIC=0 (A/B switch): fp32 flat-gradient dgamma/dbeta through the partial rows +
-// col_sum_kernel instead of atomic adds from the backward kernel.  The atomic form is not
-// bitwise reproducible run to run (fp32 addition order), like any atomic reduction.
+// VODA_LN_ATOMIC=1 (opt-in): fp32 flat-gradient dgamma/dbeta as atomic adds from the backward
+// kernel instead of partial rows + col_sum_kernel.  Off by default: the BERT-base A/B shows no
+// gain within run-to-run noise (10.88/10.55 vs 10.82/10.59 ms, profiles/raw/r2_ab_ln_atomic.jsonl)
+// and the atomic form is not bitwise reproducible run to run (fp32 addition order).
 bool ln_bwd_atomic() {
   static const bool on = [] {
     const char* e = std::getenv("VODA_LN_ATOMIC");
-    return !(e && e[0] == '0');
+    return e && e[0] == '1';
   }();
   return on;
 }
