@@ -226,7 +226,11 @@ __global__ __launch_bounds__(64 * W) void attn_fwd_kernel(AttnArgs a) {
   constexpr int DT = D / 32;           // 32-wide output tiles over the head dim
   constexpr int RS = D + 8;            // LDS row stride (elements)
   constexpr int TS = kTile + 8;        // transposed row stride
-  __shared__ __attribute__((aligned(16))) uint16_t Ks[kTile * RS];
+  // DIRECT (head dim >= 128 without the register prefetch, e.g. the NMT's D = 256 at T = 20):
+  // the row-operand fragments come straight from global / L2 instead of an LDS image, which
+  // cuts the workgroup's LDS from ~37 KB to ~20 KB (one-wave workgroups: LDS sets occupancy)
+  constexpr bool DIRECT = TileRegs<D, 64 * W>::PER > 4 && D >= 128;
+  __shared__ __attribute__((aligned(16))) uint16_t Ks[DIRECT ? 8 : kTile * RS];
   __shared__ __attribute__((aligned(16))) uint16_t Vt[D * TS];
   __shared__ __attribute__((aligned(16))) uint8_t Ms[kTile];
 
@@ -259,7 +263,7 @@ __global__ __launch_bounds__(64 * W) void attn_fwd_kernel(AttnArgs a) {
       kr.template store<true, false>(Ks, RS, nullptr, 0);
       vr.template store<false, true>(nullptr, 0, Vt, TS);
     } else {
-      stage_tile<D, true, false>(kb, a.k_st, kt, a.Tk, Ks, RS, nullptr, 0);
+      if constexpr (!DIRECT) stage_tile<D, true, false>(kb, a.k_st, kt, a.Tk, Ks, RS, nullptr, 0);
       stage_tile<D, false, true>(vb, a.v_st, kt, a.Tk, nullptr, 0, Vt, TS);
     }
     stage_mask(a, mrow, kt, Ms);
@@ -273,8 +277,15 @@ __global__ __launch_bounds__(64 * W) void attn_fwd_kernel(AttnArgs a) {
     uint32_t mw[4];
     load_mask_words(Ms, h, mw);
     f32x16 s_acc = zero16();
+    if constexpr (DIRECT) {
+      const bool kv = kt + r < a.Tk;
+      const uint16_t* krow = kb + int64_t(kt + r) * a.k_st + 8 * h;
 #pragma unroll
-    for (int s = 0; s < KS; ++s) s_acc = mfma(ld16(Ks + r * RS + 16 * s + 8 * h), qf[s], s_acc);
+      for (int s = 0; s < KS; ++s) s_acc = mfma(kv ? ld16(krow + 16 * s) : zero_bf8(), qf[s], s_acc);
+    } else {
+#pragma unroll
+      for (int s = 0; s < KS; ++s) s_acc = mfma(ld16(Ks + r * RS + 16 * s + 8 * h), qf[s], s_acc);
+    }
     float tmax = -1e30f;
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
@@ -318,8 +329,9 @@ __global__ __launch_bounds__(64 * W) void attn_fwd_kernel(AttnArgs a) {
 template <int D, int W>
 __global__ __launch_bounds__(64 * W) void attn_bwd_dq_kernel(AttnArgs a) {
   constexpr int KS = D / 16, DT = D / 32, RS = D + 8, TS = kTile + 8;
-  __shared__ __attribute__((aligned(16))) uint16_t Ks[kTile * RS];
-  __shared__ __attribute__((aligned(16))) uint16_t Vs[kTile * RS];
+  constexpr bool DIRECT = TileRegs<D, 64 * W>::PER > 4 && D >= 128;  // as in the forward
+  __shared__ __attribute__((aligned(16))) uint16_t Ks[DIRECT ? 8 : kTile * RS];
+  __shared__ __attribute__((aligned(16))) uint16_t Vs[DIRECT ? 8 : kTile * RS];
   __shared__ __attribute__((aligned(16))) uint16_t Kt[D * TS];
   __shared__ __attribute__((aligned(16))) uint8_t Ms[kTile];
 
@@ -363,6 +375,8 @@ __global__ __launch_bounds__(64 * W) void attn_bwd_dq_kernel(AttnArgs a) {
     if constexpr (PF) {
       kr.template store<true, true>(Ks, RS, Kt, TS);
       vr.template store<true, false>(Vs, RS, nullptr, 0);
+    } else if constexpr (DIRECT) {
+      stage_tile<D, false, true>(kb, a.k_st, kt, a.Tk, nullptr, 0, Kt, TS);  // K^T only
     } else {
       stage_tile<D, true, true>(kb, a.k_st, kt, a.Tk, Ks, RS, Kt, TS);
       stage_tile<D, true, false>(vb, a.v_st, kt, a.Tk, Vs, RS, nullptr, 0);
@@ -378,10 +392,21 @@ __global__ __launch_bounds__(64 * W) void attn_bwd_dq_kernel(AttnArgs a) {
     uint32_t mw[4];
     load_mask_words(Ms, h, mw);
     f32x16 s_acc = zero16(), dp = zero16();
+    if constexpr (DIRECT) {
+      const bool kv = kt + r < a.Tk;
+      const uint16_t* krow = kb + int64_t(kt + r) * a.k_st + 8 * h;
+      const uint16_t* vrow = vb + int64_t(kt + r) * a.v_st + 8 * h;
 #pragma unroll
-    for (int s = 0; s < KS; ++s) {
-      s_acc = mfma(ld16(Ks + r * RS + 16 * s + 8 * h), qf[s], s_acc);
-      dp = mfma(ld16(Vs + r * RS + 16 * s + 8 * h), dof[s], dp);
+      for (int s = 0; s < KS; ++s) {
+        s_acc = mfma(kv ? ld16(krow + 16 * s) : zero_bf8(), qf[s], s_acc);
+        dp = mfma(kv ? ld16(vrow + 16 * s) : zero_bf8(), dof[s], dp);
+      }
+    } else {
+#pragma unroll
+      for (int s = 0; s < KS; ++s) {
+        s_acc = mfma(ld16(Ks + r * RS + 16 * s + 8 * h), qf[s], s_acc);
+        dp = mfma(ld16(Vs + r * RS + 16 * s + 8 * h), dof[s], dp);
+      }
     }
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
@@ -407,9 +432,10 @@ template <int D, int W, int MODE>
 __global__ __launch_bounds__(64 * W) void attn_bwd_dkv_kernel(AttnArgs a) {
   constexpr int KS = D / 16, DT = D / 32, RS = D + 8, TS = kTile + 8;
   constexpr bool DO_DV = MODE != 2, DO_DK = MODE != 1;
-  __shared__ __attribute__((aligned(16))) uint16_t Qs[kTile * RS];
+  constexpr bool DIRECT = TileRegs<D, 64 * W>::PER > 4 && D >= 128;  // as in the forward
+  __shared__ __attribute__((aligned(16))) uint16_t Qs[DIRECT ? 8 : kTile * RS];
   __shared__ __attribute__((aligned(16))) uint16_t Qt[DO_DK ? D * TS : 8];
-  __shared__ __attribute__((aligned(16))) uint16_t Ds[DO_DK ? kTile * RS : 8];
+  __shared__ __attribute__((aligned(16))) uint16_t Ds[(DO_DK && !DIRECT) ? kTile * RS : 8];
   __shared__ __attribute__((aligned(16))) uint16_t Dt[DO_DV ? D * TS : 8];
   __shared__ float lse_s[kTile], del_s[kTile];
 
@@ -466,6 +492,14 @@ __global__ __launch_bounds__(64 * W) void attn_bwd_dkv_kernel(AttnArgs a) {
         lse_s[threadIdx.x] = lse_r;
         del_s[threadIdx.x] = del_r;
       }
+    } else if constexpr (DIRECT) {  // transposed images only: row fragments come from global
+      if constexpr (DO_DK) stage_tile<D, false, true>(qb, a.q_st, qt, a.Tq, nullptr, 0, Qt, TS);
+      if constexpr (DO_DV) stage_tile<D, false, true>(db, a.do_st, qt, a.Tq, nullptr, 0, Dt, TS);
+      for (int i = threadIdx.x; i < kTile; i += blockDim.x) {
+        const bool ok = qt + i < a.Tq;
+        lse_s[i] = ok ? a.lse[int64_t(bh) * a.Tq + qt + i] : __builtin_huge_valf();  // pad rows: P = 0
+        del_s[i] = ok ? a.delta[int64_t(bh) * a.Tq + qt + i] : 0.f;
+      }
     } else {
       stage_tile<D, true, DO_DK>(qb, a.q_st, qt, a.Tq, Qs, RS, Qt, TS);
       if constexpr (DO_DK) stage_tile<D, true, DO_DV>(db, a.do_st, qt, a.Tq, Ds, RS, Dt, TS);
@@ -481,10 +515,21 @@ __global__ __launch_bounds__(64 * W) void attn_bwd_dkv_kernel(AttnArgs a) {
       if (qt + kTile < a.Tq) load_rows(qt + kTile);  // in flight during this tile's compute
     }
     f32x16 s_acc = zero16(), dp = zero16();
+    if constexpr (DIRECT) {
+      const bool qv = qt + r < a.Tq;
+      const uint16_t* qrow = qb + int64_t(qt + r) * a.q_st + 8 * h;
+      const uint16_t* drow = db + int64_t(qt + r) * a.do_st + 8 * h;
 #pragma unroll
-    for (int s = 0; s < KS; ++s) {
-      s_acc = mfma(ld16(Qs + r * RS + 16 * s + 8 * h), kf[s], s_acc);             // S[query][key]
-      if constexpr (DO_DK) dp = mfma(ld16(Ds + r * RS + 16 * s + 8 * h), vf[s], dp);  // dP[query][key]
+      for (int s = 0; s < KS; ++s) {
+        s_acc = mfma(qv ? ld16(qrow + 16 * s) : zero_bf8(), kf[s], s_acc);
+        if constexpr (DO_DK) dp = mfma(qv ? ld16(drow + 16 * s) : zero_bf8(), vf[s], dp);
+      }
+    } else {
+#pragma unroll
+      for (int s = 0; s < KS; ++s) {
+        s_acc = mfma(ld16(Qs + r * RS + 16 * s + 8 * h), kf[s], s_acc);             // S[query][key]
+        if constexpr (DO_DK) dp = mfma(ld16(Ds + r * RS + 16 * s + 8 * h), vf[s], dp);  // dP[query][key]
+      }
     }
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
