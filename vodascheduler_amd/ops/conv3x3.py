@@ -28,7 +28,7 @@ import torch.nn.functional as F
 
 from . import _native as N
 from . import wgrad as W
-from ..utils.flat import flat_grad
+from ..utils.flat import FOLD_CAST, flat_grad
 from .conv1x1 import _direct, _ready
 
 USE_CONV_WGRAD = os.environ.get("VODA_CONV_WGRAD", "1") != "0"
@@ -115,7 +115,7 @@ class _ConvKxKFn(torch.autograd.Function):
                 dw = torch.ops.aten.convolution_backward(dy, x, weight, None, [stride, stride], [padding, padding],
                                                          [1, 1], False, [0, 0], 1, [False, True, False])[1]
                 if gw is not None:  # flat gradient the kernel cannot take: fold it here
-                    gw.add_(dw)
+                    gw.add_(dw.to(gw.dtype) if FOLD_CAST else dw)  # see utils/flat.FOLD_CAST
                     _ready(weight)
                     dw = None
         return dx, dw, None, None
