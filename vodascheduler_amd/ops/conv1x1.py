@@ -171,8 +171,8 @@ class _Conv1x1Fn(torch.autograd.Function):
             elif g2 is not None:
                 if g2.dtype == dy2.dtype:
                     g2.addmm_(dy2.t(), x2)
-                else:  # fp32 flat gradient of a bf16 weight
-                    g2.add_(dy2.t() @ x2)
+                else:  # fp32 flat gradient of a bf16 weight (cast first: see utils/flat.FOLD_CAST)
+                    g2.add_((dy2.t() @ x2).to(g2.dtype))
                 _ready(weight)
             else:
                 dw = (dy2.t() @ x2).view(cout, cin, 1, 1)

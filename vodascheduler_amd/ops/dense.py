@@ -116,8 +116,8 @@ def linear_weight_grads(dy2: torch.Tensor, x2: torch.Tensor, weight: torch.Tenso
             gw = flat_grad(weight)
             if gw.dtype == dy2.dtype:
                 gw.addmm_(dy2.t(), x2)
-            else:  # fp32 flat gradient of a bf16 weight
-                gw.add_(dy2.t() @ x2)
+            else:  # fp32 flat gradient of a bf16 weight (cast first: see utils/flat.FOLD_CAST)
+                gw.add_((dy2.t() @ x2).to(gw.dtype))
             _ready(weight)
         else:
             dw = dy2.t() @ x2
