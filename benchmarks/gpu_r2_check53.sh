@@ -1,5 +1,5 @@
 #!/bin/bash
-# Round-2 check 53 (final validation of the session tree: + large-head-dim attention direct loads): full GPU suite + smoke,
+# Round-2 check 53 (final validation of the session tree: + large-head-dim attention direct loads, fold cast): full GPU suite + smoke,
 # BERT-base eager vs graph, N=1 bench with detail, steady-state rocprofv3 kernel stats of
 # ResNet-50 / BERT-base.
 set -o pipefail
