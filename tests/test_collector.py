@@ -60,9 +60,10 @@ def test_collector_updates_job_and_category_history(tmp_path):
     cat = _job(store, job, epochs=10)
     lg = MetricsCSVLogger(str(tmp_path), job, total_epochs=10, local_batch_size=128)
     t0 = time.time()
-    # epochs 0-1 on 1 worker (20 s), 2-3 on 2 workers (11 s), 4 on 4 workers (6.5 s)
+    # epochs 0-1 on 1 worker (20 s), 2-3 on 2 workers (11 s), 4 on 4 workers (6.5 s); an epoch
+    # is split over the workers (steps_per_epoch // size, tensorflow2_keras_cifar_elastic.py:223)
     for e, (w, et) in enumerate([(1, 20.0), (1, 20.0), (2, 11.0), (2, 11.0), (4, 6.5)]):
-        lg.log_epoch(e, t0 + 30 * e, et, steps=100, loss=1.0 / (e + 1), workers=w)
+        lg.log_epoch(e, t0 + 30 * e, et, steps=100 // w, loss=1.0 / (e + 1), workers=w)
     assert lg.restored_epoch() == 5                       # a preempted job resumes at epoch 5
     c = MetricsCollector(store, str(tmp_path))
     assert c.jobs() == [job]

@@ -47,11 +47,17 @@ def test_two_mnist_jobs_elastic_fifo_two_slots(tmp_path):
     assert any(k[0] == "mnist-b" and k[1] == "start" for k in kinds), kinds
     assert r["start_latency_p50_s"] is not None and r["start_latency_p50_s"] < 30
     assert r["n_starts"] >= 2 and r["n_shrinks_to_1"] >= 1  # a: 2 -> 1 (no communicator at world 1)
-    csvs = sorted(os.listdir(tmp_path / "metrics"))
+    csvs = sorted(f for f in os.listdir(tmp_path / "metrics") if f.endswith(".csv"))
     assert len(csvs) == 2
     rows = open(tmp_path / "metrics" / csvs[0]).read().splitlines()
     assert rows[0].startswith("epoch,start_time,epoch_time_sec,step_time_sec,steps,workers")
     assert len(rows) == 3  # header + 2 epochs
+    # fast online profiling: rank 0's progress file holds GPU/CPU-timed steps per world size
+    import json
+
+    prog = json.load(open(tmp_path / "metrics" / csvs[0].replace(".csv", ".progress.json")))
+    assert prog["samples_done"] == prog["samples_total"] > 0
+    assert prog["perf"] and all(int(n) > 0 and s > 0 for n, s in prog["perf"].values())
 
 
 def _ddp_worker(port, rank, world, q):

@@ -4,8 +4,16 @@ A job's work is ``epochs * epoch_time_1gpu`` one-GPU-seconds; on ``n`` GPUs it a
 ``speedup(n)`` one-GPU-seconds per second.  Every start / resize / migration costs a pause
 (``resize_overhead_s`` for the elastic runtime's warm-worker path; a restart from a
 checkpoint after a halt costs ``restart_overhead_s``), so policies that churn pay for it.
-In ``oracle`` info mode the backend keeps each job's ``job_info`` record (remaining time,
-speedup table) current, which is what the metrics collector converges to on hardware.
+Info modes (what the info-driven policies see):
+
+* ``oracle`` -- every submitted job's ``job_info`` (remaining time, speedup table) is kept
+  exact, started or not;
+* ``online`` -- what the metrics collector delivers on hardware: a started job's record is
+  refreshed every ``collector_period_s`` (its exact progress + its speed curve); an
+  unstarted job keeps the estimate the training service seeded at submission;
+* ``prior`` -- only the submission-time estimates (no collector);
+* ``placeholder`` -- the reference as written: no collector, and the service seeds nothing
+  (1 s epochs, linear speedup; use with ``TrainingService(seed_from_workload=False)``).
 """
 from __future__ import annotations
 
@@ -13,7 +21,7 @@ from dataclasses import dataclass, field
 
 from ..common.store import JobStore, NotFound
 from ..common.types import MAX_NUM_GPU
-from ..sim.trace import ASSUMED_INTERNODE_BUSBW_GBS, PROFILES, ModelProfile, workload_of
+from ..common.workload import ASSUMED_INTERNODE_BUSBW_GBS, profile_of, workload_of
 from .base import EV_FINISHED, HALT, START, Backend, JobAction
 
 Loc = tuple[str, int]
@@ -33,6 +41,8 @@ class SimJob:
     resizes: int = 0
     migrations: int = 0
     cross_node: bool = False     # workers span nodes: the all-reduce runs at inter-node bandwidth
+    info_sent: bool = False      # speed curve published to job_info
+    info_sent_remaining: float = -1.0
 
     def speed(self) -> float:
         if self.n == 0:
@@ -45,8 +55,13 @@ class SimJob:
 
 class SimBackend(Backend):
     def __init__(self, clock, nodes: dict[str, list[int]] | None = None, store: JobStore | None = None,
-                 resize_overhead_s: float = 5.0, restart_overhead_s: float = 15.0, info_mode: str = "oracle"):
+                 resize_overhead_s: float = 5.0, restart_overhead_s: float = 15.0, info_mode: str = "oracle",
+                 collector_period_s: float = 60.0):
         super().__init__()
+        if info_mode not in ("oracle", "online", "prior", "placeholder"):
+            raise ValueError(f"unknown info mode {info_mode!r}")
+        self.collector_period_s = collector_period_s
+        self._last_collect = -1e18
         self.clock = clock
         self._nodes = nodes or {"node0": list(range(8))}
         self.store = store
@@ -71,6 +86,7 @@ class SimBackend(Backend):
             for j in list(self.jobs.values()):
                 if j.n > 0 and j.work <= 1e-9:
                     self._finish(j)
+        self._maybe_publish(t)
 
     def _progress(self, t: float) -> None:
         t0 = self.t_last
@@ -109,13 +125,7 @@ class SimBackend(Backend):
             name = a.job.name
             j = self.jobs.get(name)
             if j is None:
-                wl = workload_of(a.job.spec)
-                prof = PROFILES.get(wl["model"], ModelProfile(wl["model"], wl.get("alpha", 0.05), 0.05))
-                if "alpha" in wl and prof.grad_mb <= 0:
-                    prof = ModelProfile(prof.name, float(wl["alpha"]), prof.step_time_1gpu)
-                total = float(wl["epoch_time_1gpu"]) * max(1, a.job.config.epochs)
-                j = SimJob(name, a.job.job_category, prof, total, total, a.job.config.epochs)
-                self.jobs[name] = j
+                j = self._new_job(name, a.job.job_category, a.job.spec, a.job.config.epochs)
             if a.kind == HALT:
                 j.n = 0
                 j.workers = []
@@ -133,20 +143,46 @@ class SimBackend(Backend):
             j.workers = list(a.workers or [])
             j.cross_node = len({w[0] for w in j.workers}) > 1
             j.paused_until = now + overhead
+        self._maybe_publish(now)
+
+    def _new_job(self, name: str, category: str, spec: dict, epochs: int) -> SimJob:
+        wl = workload_of(spec)
+        total = float(wl["epoch_time_1gpu"]) * max(1, epochs)
+        j = SimJob(name, category, profile_of(wl), total, total, epochs)
+        self.jobs[name] = j
+        return j
+
+    def on_submit(self, name: str, category: str, spec: dict, epochs: int) -> None:
+        """The simulator calls this when the training service accepted a job, so ``oracle``
+        info covers jobs that have not started yet."""
+        if name not in self.jobs:
+            self._new_job(name, category, spec, epochs)
+        if self.info_mode == "oracle":
+            self.publish_info([name])
+
+    def _maybe_publish(self, now: float) -> None:
         if self.info_mode == "oracle":
             self.publish_info()
+        elif self.info_mode == "online" and now - self._last_collect >= self.collector_period_s:
+            self._last_collect = now
+            self.publish_info([n for n, j in self.jobs.items() if j.total_work - j.work > 0 or j.n > 0])
 
-    def publish_info(self) -> None:
+    def publish_info(self, names: list[str] | None = None) -> None:
         if self.store is None:
             return
-        for j in self.jobs.values():
-            sp = {str(i): j.profile.speedup(i) for i in range(0, MAX_NUM_GPU + 2)}
+        for j in (self.jobs.values() if names is None else [self.jobs[n] for n in names if n in self.jobs]):
+            rem = max(j.work, 0.0)
+            fields = {"estimated_remainning_time_sec": rem}
+            if not j.info_sent:  # the speed curve is static: send it once
+                sp = {str(i): j.profile.speedup(i) for i in range(0, MAX_NUM_GPU + 2)}
+                fields["speedup"] = sp
+                fields["efficiency"] = {k: (v / int(k) if int(k) else 0.0) for k, v in sp.items()}
+            elif j.info_sent_remaining == rem:
+                continue
             try:
-                self.store.update_job_info(j.category, j.name, {
-                    "estimated_remainning_time_sec": max(j.work, 0.0),
-                    "speedup": sp,
-                    "efficiency": {k: (v / int(k) if int(k) else 0.0) for k, v in sp.items()},
-                })
+                self.store.update_job_info(j.category, j.name, fields)
+                j.info_sent = True
+                j.info_sent_remaining = rem
             except NotFound:
                 pass
 

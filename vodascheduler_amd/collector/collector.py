@@ -18,6 +18,7 @@ Improvements over the reference (documented deviations):
 from __future__ import annotations
 
 import csv
+import json
 import logging
 import os
 import re
@@ -65,7 +66,57 @@ def speedup_table(epoch_time: dict[int, float], max_gpu: int = MAX_NUM_GPU) -> d
     return sp
 
 
+def estimate_tables(step_t: dict[int, float], prior: dict | None = None,
+                    max_gpu: int = MAX_NUM_GPU) -> tuple[dict[str, float], dict[str, float]]:
+    """Speedup and per-worker-count step-time tables from measured step times.
+
+    ``step_t[k]``: seconds per training step with ``k`` workers (each step processes ``k``
+    per-GPU batches), so ``speedup(k) = k t(1) / t(k)`` -- robust to epochs cut short by a
+    resize, unlike the epoch-time ratio.  ``t(1)``: measured, else the prior's (the
+    workload's MI355X profile or the category's history), else linear below the smallest
+    measured count.  Unmeasured counts: Amdahl fit through the measured points when one with
+    k > 1 exists, else the prior's curve, else linear."""
+    ks = sorted(k for k, v in step_t.items() if k > 0 and v > 0)
+    prior_sp = (prior or {}).get("speedup") or {}
+    prior_t1 = float(((prior or {}).get("step_time_sec") or {}).get("1", 0.0) or 0.0)
+    if (prior or {}).get("info_source", "placeholder") == "placeholder":
+        prior_sp, prior_t1 = {}, 0.0
+    if 1 in step_t and step_t[1] > 0:
+        t1 = step_t[1]
+    elif prior_t1 > 0:
+        t1 = prior_t1
+    elif ks:
+        t1 = step_t[ks[0]]  # linear below the smallest measured count
+    else:
+        return {}, {}
+    measured = {k: min(float(k), k * t1 / step_t[k]) for k in ks}
+    multi = [k for k in ks if k > 1]
+    a = fit_amdahl(measured) if multi else None
+    sp = {"0": 0.0}
+    st = {"0": 0.0}
+    for k in range(1, max_gpu + 2):
+        if k in measured:
+            v = measured[k]
+        elif a is not None:
+            v = k / (1.0 + a * (k - 1))
+        elif str(k) in prior_sp and float(prior_sp[str(k)]) > 0:
+            v = float(prior_sp[str(k)])
+        else:
+            v = float(k)
+        sp[str(k)] = v
+        st[str(k)] = step_t[k] if k in measured else k * t1 / v
+    return sp, st
+
+
 class MetricsCollector:
+    """``update_info_all`` is one collector pass (the reference's cron job).  Two inputs per
+    job, both written by the job's rank 0 into ``metrics_dir``:
+
+    * ``<job>.csv`` -- one row per epoch (the reference's ``MetricsCSVLogger``);
+    * ``<job>.progress.json`` -- fast online profiling (extension): rewritten at most every
+      second with the samples done / total and the GPU-timed step time per world size, so a
+      job's estimate tracks it from its first commits instead of its first epoch row."""
+
     def __init__(self, store: JobStore, metrics_dir: str, update_category_base: bool = True):
         self.store = store
         self.metrics_dir = metrics_dir
@@ -74,7 +125,13 @@ class MetricsCollector:
     def jobs(self) -> list[str]:
         if not os.path.isdir(self.metrics_dir):
             return []
-        return sorted(f[:-4] for f in os.listdir(self.metrics_dir) if f.endswith(".csv"))
+        out = set()
+        for f in os.listdir(self.metrics_dir):
+            if f.endswith(".progress.json"):
+                out.add(f[:-len(".progress.json")])
+            elif f.endswith(".csv"):
+                out.add(f[:-4])
+        return sorted(out)
 
     def update_info_all(self, jobs: list[str] | None = None) -> int:
         n = 0
@@ -85,49 +142,80 @@ class MetricsCollector:
                 log.exception("collector: job %s", j)
         return n
 
+    def _category(self, job: str) -> str:
+        try:
+            return self.store.find_metadata(job).get("job_category") or category_of(job)
+        except (NotFound, AttributeError):
+            return category_of(job)
+
+    def _read_progress(self, job: str) -> dict | None:
+        try:
+            with open(os.path.join(self.metrics_dir, job + ".progress.json")) as f:
+                return json.load(f)
+        except (OSError, ValueError):
+            return None
+
     def parse_csv_and_update_db(self, job: str) -> dict | None:
         path = os.path.join(self.metrics_dir, job + ".csv")
         try:
             with open(path) as f:
                 rows = list(csv.DictReader(f))
         except OSError:
+            rows = []
+        prog = self._read_progress(job)
+        if not rows and not prog:
             return None
-        if not rows:
-            return None
-        cat = category_of(job)
+        cat = self._category(job)
         try:
             post = self.store.find_job_info(cat, job)
         except NotFound:
             return None
-        last_epoch = int(rows[-1]["epoch"])
-        if int(post.get("current_epoch", -1)) == last_epoch and post.get("_rows") == len(rows):
+        if post.get("_rows") == len(rows) and post.get("_progress_t") == (prog or {}).get("t"):
             return None  # nothing new
+        # ---- step times per worker count: GPU-timed progress first, epoch rows second
+        step_t: dict[int, float] = {}
+        for k, (n, sec) in ((prog or {}).get("perf") or {}).items():
+            if int(n) > 0 and float(sec) > 0:
+                step_t[int(k)] = float(sec) / int(n)
         by_w: dict[int, list[dict]] = {}
         for r in rows:
             by_w.setdefault(int(r["workers"]), []).append(r)
-        step_t = {k: statistics.fmean(float(r["step_time_sec"]) for r in v) for k, v in by_w.items()}
+        for k, v in by_w.items():
+            if k not in step_t:
+                step_t[k] = statistics.fmean(float(r["step_time_sec"]) for r in v)
         epoch_t = {k: statistics.fmean(float(r["epoch_time_sec"]) for r in v) for k, v in by_w.items()}
-        sp = speedup_table(epoch_t)
+        sp, st = estimate_tables(step_t, post)
+        if not sp:
+            return None
         eff = {k: (v / int(k) if int(k) else 0.0) for k, v in sp.items()}
-        total = int(post.get("total_epochs", rows[-1].get("total_epochs", 1)))
-        remaining = max(0, total - last_epoch - 1)
-        t1 = epoch_t.get(1, epoch_t[min(epoch_t)] * min(epoch_t))
-        start = datetime.strptime(rows[0]["start_time"], TIME_FMT)
-        end = datetime.strptime(rows[-1]["start_time"], TIME_FMT)
-        elapsed = (end - start).total_seconds() + float(rows[-1]["epoch_time_sec"])
-        running = sum(float(r["epoch_time_sec"]) for r in rows)
-        gpu = sum(float(r["epoch_time_sec"]) * int(r["workers"]) for r in rows)
-        fields = {
-            "current_epoch": last_epoch,
-            "remainning_epochs": remaining,
-            "estimated_remainning_time_sec": float(t1 * remaining),
-            "running_time_sec": running,
-            "waiting_time_sec": max(0.0, elapsed - running),
-            "gpu_time_sec": gpu,
-            "elasped_time_sec": elapsed,
-            "_rows": len(rows),
-        }
-        for k, v in step_t.items():
+        t1 = st["1"]
+        total = int(post.get("total_epochs", rows[-1].get("total_epochs", 1) if rows else 1))
+        fields: dict = {"_rows": len(rows), "_progress_t": (prog or {}).get("t"), "info_source": "measured",
+                        "measured_workers": sorted(step_t)}
+        if prog and int(prog.get("per_gpu_batch", 0)) > 0:
+            # exact progress: remaining single-GPU steps x the single-GPU step time
+            bs = int(prog["per_gpu_batch"])
+            left = max(0.0, float(prog["samples_total"]) - float(prog["samples_done"]))
+            fields["estimated_remainning_time_sec"] = left / bs * t1
+            fields["current_epoch"] = int(prog.get("epoch", 0))
+            fields["remainning_epochs"] = max(0, int(prog.get("epochs", total)) - int(prog.get("epoch", 0)))
+        else:
+            last_epoch = int(rows[-1]["epoch"])
+            remaining = max(0, total - last_epoch - 1)
+            spe = int(post.get("steps_per_epoch", 0) or 0)
+            ep1 = spe * t1 if spe > 0 else epoch_t.get(1, epoch_t[min(epoch_t)] * min(epoch_t))
+            fields["estimated_remainning_time_sec"] = float(ep1 * remaining)
+            fields["current_epoch"] = last_epoch
+            fields["remainning_epochs"] = remaining
+        if rows:
+            start = datetime.strptime(rows[0]["start_time"], TIME_FMT)
+            end = datetime.strptime(rows[-1]["start_time"], TIME_FMT)
+            elapsed = (end - start).total_seconds() + float(rows[-1]["epoch_time_sec"])
+            running = sum(float(r["epoch_time_sec"]) for r in rows)
+            fields.update(running_time_sec=running, waiting_time_sec=max(0.0, elapsed - running),
+                          gpu_time_sec=sum(float(r["epoch_time_sec"]) * int(r["workers"]) for r in rows),
+                          elasped_time_sec=elapsed)
+        for k, v in st.items():
             fields[f"step_time_sec.{k}"] = v
         for k, v in epoch_t.items():
             fields[f"epoch_time_sec.{k}"] = v
@@ -137,13 +225,42 @@ class MetricsCollector:
             fields[f"efficiency.{k}"] = v
         self.store.update_job_info(cat, job, fields)
         if self.update_category_base:
-            base = {k: v for k, v in fields.items() if k.split(".")[0] in
-                    ("step_time_sec", "epoch_time_sec", "speedup", "efficiency")}
-            try:
-                self.store.update_job_info(cat, cat, base)
-            except NotFound:
-                pass
+            self._refresh_base(cat, step_t, post, epoch_t)
         return fields
+
+    def _refresh_base(self, cat: str, step_t: dict[int, float], prior: dict,
+                      epoch_t: dict[int, float] | None = None) -> None:
+        """Fold this job's measured step times into the category's base record, so the next
+        job of the category starts from measured history.  Worker
+        counts measured by earlier jobs of the category are kept."""
+        try:
+            base = self.store.find_job_info(cat, cat)
+        except NotFound:
+            return
+        merged = {int(k): float(v) for k, v in (base.get("measured_step_time") or {}).items()}
+        merged.update(step_t)
+        sp, st = estimate_tables(merged, prior)
+        if not sp:
+            return
+        fields: dict = {"info_source": "measured", "measured_step_time": {str(k): v for k, v in merged.items()}}
+        for k, v in st.items():
+            fields[f"step_time_sec.{k}"] = v
+        for k, v in sp.items():
+            fields[f"speedup.{k}"] = v
+            fields[f"efficiency.{k}"] = v / int(k) if int(k) else 0.0
+        spe = int(prior.get("steps_per_epoch", 0) or 0)
+        if spe > 0:
+            for k, v in st.items():
+                if int(k):
+                    fields[f"epoch_time_sec.{k}"] = spe / int(k) * v
+        else:  # no declared epoch length: the measured epoch rows (reference semantics)
+            ep = dict(epoch_t or {})
+            if ep and 1 not in ep:
+                k0 = min(ep)
+                ep[1] = ep[k0] * float(sp[str(k0)])
+            for k, v in ep.items():
+                fields[f"epoch_time_sec.{k}"] = v
+        self.store.update_job_info(cat, cat, fields)
 
 
 def main(argv=None) -> int:

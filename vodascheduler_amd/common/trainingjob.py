@@ -150,6 +150,8 @@ def create_base_job_info_record(job_name: str, max_gpu: int = MAX_NUM_GPU) -> di
         "speedup": linear_speedup(max_gpu),
         "step_time_sec": dict(t),
         "total_epochs": 1,
+        # extension: where the estimates come from (placeholder | profile | measured)
+        "info_source": "placeholder",
     }
 
 

@@ -16,6 +16,9 @@ class JobConfigEnv(str, Enum):
     EPOCHS = "EPOCHS"
     JOB_NAME = "JOB_NAME"
     JOB_PRIORITY = "JOB_PRIORITY"
+    # extension: jobs naming the same category share job-info history (the reference uses the
+    # un-timestamped job name as the category, handlers.go:180-206)
+    JOB_CATEGORY = "JOB_CATEGORY"
 
 
 class JobStatus(str, Enum):

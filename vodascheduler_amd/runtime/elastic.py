@@ -465,6 +465,9 @@ def _to_plain(d: dict) -> dict:
             out[k] = list(v)
         elif isinstance(v, dict) and all(isinstance(x, (int, float, str, bool)) for x in v.values()):
             out[k] = dict(v)
+        elif isinstance(v, dict) and all(isinstance(x, (list, tuple)) and all(isinstance(y, (int, float)) for y in x)
+                                         for x in v.values()):
+            out[k] = {kk: list(x) for kk, x in v.items()}  # e.g. perf: {world: [steps, seconds]}
     return out
 
 

@@ -16,7 +16,9 @@ from ..common.mq import VERB_CREATE, VERB_DELETE, MessageQueue, Msg
 from ..common.store import JobStore, NotFound
 from ..common.trainingjob import (TrainingJob, create_base_job_info_record, init_job_info_record,
                                   new_training_job)
-from ..common.types import ENTRY_POINT, NAME, VERSION
+from ..common.types import ENTRY_POINT, NAME, VERSION, JobConfigEnv
+from ..common.workload import (INFO_MEASURED, INFO_PLACEHOLDER, declared_workload, prior_fields,
+                               remaining_from_history)
 from ..utils.clock import Clock, RealClock
 from ..utils.http import Router, as_json, text
 from ..utils.metrics import ServiceMetrics
@@ -26,11 +28,14 @@ log = logging.getLogger("vodascheduler_amd.service")
 
 class TrainingService:
     def __init__(self, store: JobStore, mq: MessageQueue, clock: Clock | None = None,
-                 metrics: ServiceMetrics | None = None):
+                 metrics: ServiceMetrics | None = None, seed_from_workload: bool = True):
         self.store = store
         self.mq = mq
         self.clock = clock or RealClock()
         self.metrics = metrics or ServiceMetrics()
+        # False: the reference's behaviour -- a category without history starts from the
+        # CreateBaseJobInfo placeholder (1 s epochs, linear speedup); kept for A/B only
+        self.seed_from_workload = seed_from_workload
 
     # ------------------------------------------------------------ job info history
     def get_or_create_base_job_info(self, category: str) -> dict:
@@ -47,12 +52,41 @@ class TrainingService:
                 return self.store.find_job_info(category, category)
             return info
 
+    def initial_job_info(self, base: dict, name: str, epochs: int, spec: dict) -> dict:
+        """The new job's job_info record (``initJobInfo``, handlers.go:212-223), with an
+        estimate that means something before the job has run a step:
+
+        1. the category has measured history (the collector refreshed its base record):
+           measured speedup, remaining = measured 1-GPU step time x the job's own declared
+           step count (or the reference's ``epochs x epoch_time(1)``);
+        2. else the job declares a workload (annotation or reference launcher flags): the
+           MI355X speed model of that model (``common/workload.prior_fields``);
+        3. else the reference placeholder (1 s epochs, linear speedup)."""
+        info = init_job_info_record(base, name, epochs)
+        try:
+            wl = declared_workload(spec)
+        except Exception:  # an unparsable annotation must not fail the submission
+            log.warning("job %s: unreadable workload declaration", name, exc_info=True)
+            wl = None
+        if base.get("info_source") == INFO_MEASURED:
+            info["estimated_remainning_time_sec"] = remaining_from_history(base, wl, epochs)
+            info["info_source"] = INFO_MEASURED
+        elif wl is not None and self.seed_from_workload:
+            info.update(prior_fields(wl, epochs))
+        else:
+            info["info_source"] = INFO_PLACEHOLDER
+        if wl is not None:
+            info["per_gpu_batch"] = int(wl.get("per_gpu_batch", 0) or 0)
+            info["steps_per_epoch"] = int(wl.get("steps_per_epoch", 0) or 0)
+        return info
+
     # ------------------------------------------------------------ create / delete
     def create_training_job(self, data: bytes | str, submit_time: float | None = None) -> str:
         t0 = time.perf_counter()
         try:
             spec = mpijob.load_spec(data)
-            category = spec["metadata"]["name"]
+            # JOB_CATEGORY knob, else the reference's category = the submitted name
+            category = mpijob.get_env(spec, JobConfigEnv.JOB_CATEGORY.value) or spec["metadata"]["name"]
             base = self.get_or_create_base_job_info(category)
             now = self.clock.now() if submit_time is None else submit_time
             name = mpijob.timestamped_name(category, now)
@@ -63,7 +97,7 @@ class TrainingService:
                 k += 1
             mpijob.set_name(spec, name)
             job = new_training_job(spec, category, now)
-            info = init_job_info_record(base, name, job.config.epochs)
+            info = self.initial_job_info(base, name, job.config.epochs, spec)
             self.store.insert_job_info(category, info)
             try:
                 self.store.insert_metadata(job.to_dict())

@@ -53,16 +53,22 @@ def simulate(trace: list[TraceJob], algorithm: str = "ElasticFIFO", gpus: int = 
              resize_overhead_s: float = 5.0, restart_overhead_s: float = 15.0, use_placement: bool = True,
              drain: list[tuple[float, str, int]] | None = None, max_time: float = 1e9,
              gpu_type: str = DEFAULT_GPU_TYPE, trace_path: str | None = None,
-             naive_placement: bool = False) -> SimResult:
+             naive_placement: bool = False, info_mode: str = "online",
+             collector_period_s: float = 60.0) -> SimResult:
     """Run a trace to completion.  ``drain`` = [(time, node, gpu)] GPU drain events;
     ``trace_path`` writes the scheduler timeline (Chrome-trace JSON, virtual time);
-    ``naive_placement``: best-fit without the Munkres bindings (placement/manager.py)."""
+    ``naive_placement``: best-fit without the Munkres bindings (placement/manager.py);
+    ``info_mode``: what the info-driven policies see (backend/sim.py): ``online`` (default:
+    submission-time estimates from the declared workload, then the collector every
+    ``collector_period_s``, the reference cron's 1 min), ``oracle``, ``prior`` or
+    ``placeholder`` (the reference as written: 1 s epochs, linear speedup)."""
     clock = ManualClock(0.0)
     store = MemoryStore()
     mq = InProcQueue(maxsize=10 ** 6)
-    svc = TrainingService(store, mq, clock)
+    svc = TrainingService(store, mq, clock, seed_from_workload=info_mode != "placeholder")
     nodes = nodes or {"node0": list(range(gpus))}
-    backend = SimBackend(clock, nodes, store, resize_overhead_s, restart_overhead_s)
+    backend = SimBackend(clock, nodes, store, resize_overhead_s, restart_overhead_s, info_mode=info_mode,
+                         collector_period_s=collector_period_s)
     placement = None
     if use_placement and naive_placement:
         from ..placement.manager import PlacementManager
@@ -98,7 +104,10 @@ def simulate(trace: list[TraceJob], algorithm: str = "ElasticFIFO", gpus: int = 
         backend.advance(t)
         while pending and pending[0].submit_time <= t:
             tj = pending.pop(0)
-            names.append(svc.create_training_job(json.dumps(tj.spec), submit_time=tj.submit_time))
+            name = svc.create_training_job(json.dumps(tj.spec), submit_time=tj.submit_time)
+            names.append(name)
+            doc = store.find_metadata(name)
+            backend.on_submit(name, doc["job_category"], doc["spec"], int(doc["config"]["epochs"]))
         while drains and drains[0][0] <= t:
             _, node, gpu = drains.pop(0)
             cur = backend.nodes()

@@ -16,7 +16,9 @@ Standalone (one process per GPU, launched by the local node agent):
 from __future__ import annotations
 
 import argparse
+import collections
 import hashlib
+import json
 import logging
 import math
 import os
@@ -63,6 +65,7 @@ class TrainConfig:
     final_state_path: str | None = None  # rank 0 saves the final state (checkpoint format) here
     eval_batches: int = 0              # held-out synthetic batches evaluated after every epoch (0: no eval)
     report_progress: bool = False      # rank 0 publishes the committed step under job/<name>/progress
+    progress_every_s: float = 1.0      # rank 0 rewrites <metrics_dir>/<job>.progress.json at most this often
 
 
 def build(cfg: TrainConfig, device: torch.device):
@@ -142,6 +145,63 @@ def get_warm(cfg: TrainConfig, device: torch.device, use_cache: bool = True) -> 
     return wm
 
 
+class StepProfiler:
+    """Fast online profiling: GPU-timed seconds per step at each world size.
+
+    ``mark(step)`` at every commit records a timing event on the compute stream; events are
+    resolved lazily once the GPU has passed them (``Event.query``), so no host sync is added.
+    Consecutive resolved marks of one chain add ``(steps, seconds)`` to ``perf[world]``.  A
+    chain restarts at every membership change, epoch boundary (eval / metric all-reduce are
+    not training steps) and restore, and its first interval starts at the first commit (the
+    hipGraph warm-up / capture steps are not timed).  ``perf`` lives in the elastic state's
+    extras, so it is committed, restored and inherited by joining members like the step
+    counter."""
+
+    def __init__(self, device: torch.device):
+        self.cuda = device.type == "cuda"
+        self.marks: collections.deque = collections.deque()
+        self.anchor = None
+
+    def reset_chain(self) -> None:
+        self.marks.clear()
+        self.anchor = None
+
+    def mark(self, step: int, world: int, perf: dict) -> None:
+        if self.cuda:
+            ev = torch.cuda.Event(enable_timing=True)
+            ev.record()
+        else:
+            ev = time.perf_counter()
+        self.marks.append((ev, step))
+        self.resolve(world, perf)
+
+    def resolve(self, world: int, perf: dict) -> None:
+        while self.marks:
+            ev, step = self.marks[0]
+            if self.cuda and not ev.query():
+                break
+            self.marks.popleft()
+            if self.anchor is not None:
+                a_ev, a_step = self.anchor
+                dt = a_ev.elapsed_time(ev) / 1e3 if self.cuda else ev - a_ev
+                n = step - a_step
+                if n > 0 and dt > 0:
+                    rec = perf.setdefault(str(world), [0, 0.0])
+                    rec[0] += n
+                    rec[1] += dt
+            self.anchor = (ev, step)
+
+
+def write_progress(metrics_dir: str, job: str, doc: dict) -> None:
+    """Atomically replace ``<metrics_dir>/<job>.progress.json`` (read by the collector)."""
+    os.makedirs(metrics_dir, exist_ok=True)
+    path = os.path.join(metrics_dir, f"{job}.progress.json")
+    tmp = f"{path}.{os.getpid()}.tmp"
+    with open(tmp, "w") as f:
+        json.dump(doc, f)
+    os.replace(tmp, path)
+
+
 def train_elastic(ctx: ElasticContext, cfg: TrainConfig, use_cache: bool = True) -> dict | None:
     device = ctx.device
     wm = get_warm(cfg, device, use_cache)
@@ -149,10 +209,30 @@ def train_elastic(ctx: ElasticContext, cfg: TrainConfig, use_cache: bool = True)
     # world_log: flat [start_step, world, ...] segments -- the world size every step ran at.
     # Part of the synced / committed state, so a restore rolls it back with the step counter
     # and a joining member inherits it: ``replay_reference`` re-runs the same trajectory.
-    state = TorchState(ctx, model, opt, epoch=0, samples=0, world_log=[])
+    # perf: {world: [steps, seconds]} measured by StepProfiler (fast online profiling)
+    state = TorchState(ctx, model, opt, epoch=0, samples=0, world_log=[], perf={})
     logger = MetricsCSVLogger(cfg.metrics_dir, ctx.job, cfg.epochs, bs)
     samples_per_epoch = cfg.steps_per_epoch * bs
     stats = {"steps": 0, "samples": 0, "train_time": 0.0, "model": cfg.model, "resizes": 0}
+    prof = StepProfiler(device)
+    last_pub = [0.0]
+
+    def publish(world: int, force: bool = False) -> None:
+        """Rank 0: progress + per-world step times for the collector, at most once a second."""
+        if not cfg.metrics_dir or ctx.rank != 0:
+            return
+        now = time.time()
+        if not force and now - last_pub[0] < cfg.progress_every_s:
+            return
+        last_pub[0] = now
+        prof.resolve(world, state.perf)
+        try:
+            write_progress(cfg.metrics_dir, ctx.job, {
+                "job": ctx.job, "t": now, "world": world, "per_gpu_batch": bs, "epoch": state.epoch,
+                "epochs": cfg.epochs, "samples_done": state.epoch * samples_per_epoch + state.samples,
+                "samples_total": cfg.epochs * samples_per_epoch, "perf": state.perf})
+        except OSError:
+            log.warning("%s: cannot write the progress file", ctx.job, exc_info=True)
 
     def on_reset():
         stats["resizes"] += 1
@@ -213,6 +293,7 @@ def train_elastic(ctx: ElasticContext, cfg: TrainConfig, use_cache: bool = True)
         loss_t = None
         while state.epoch < cfg.epochs:
             t_ep = time.time()
+            prof.reset_chain()
             steps = 0
             ep_acc = torch.zeros(3, device=device)  # sum over steps of [loss, #correct, #predictions]
             guard = torch.zeros((), device=device)  # graph replays: loss sum since the last commit
@@ -242,12 +323,15 @@ def train_elastic(ctx: ElasticContext, cfg: TrainConfig, use_cache: bool = True)
                             wm.step_graph = None
                             state.restore()
                             stats["graph_fallbacks"] = stats.get("graph_fallbacks", 0) + 1
+                            prof.reset_chain()
                             ep_acc.zero_()
                             steps = 0
                             guard.zero_()
                             continue
                         guard.zero_()
+                    prof.mark(state.step, world, state.perf)
                     state.commit()
+                    publish(world)
                     if cfg.report_progress and ctx.rank == 0:
                         ctx.rdzv.set("progress", str(state.step))
             if device.type == "cuda":
@@ -266,9 +350,11 @@ def train_elastic(ctx: ElasticContext, cfg: TrainConfig, use_cache: bool = True)
                                  acc=None if acc != acc else acc, val_loss=val[0], val_acc=val[1])
             stats.setdefault("epoch_metrics", []).append({"loss": mean_loss, "acc": acc, "val_loss": val[0],
                                                           "val_acc": val[1], "world": world})
+            prof.resolve(world, state.perf)  # the epoch-end sync passed every mark
             state.epoch += 1
             state.samples = 0
             state.commit()
+            publish(world, force=True)
             if cfg.checkpoint_every_epoch and ctx.rank == 0:
                 state.save_checkpoint()
         if device.type == "cuda":
