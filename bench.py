@@ -24,10 +24,24 @@ The timed region (barrier + synchronize on both sides) is the whole trace: first
 to last completion.  ``value`` = average JCT in seconds (lower is better); makespan, job-start
 latency, resize latency (world >= 2 transitions only: RCCL communicator rebuild + state
 broadcast) and aggregate throughput are reported alongside.
+
+Also reported (none of it inside the timed region):
+  * at N >= 2, RCCL all-reduce bus bandwidth at 16 / 64 / 256 MB for every power-of-two
+    sub-world (the ring sizes jobs run at) and the communicator init time, measured during
+    warm-up -- the simulator's speed model loads these (``common/workload.load_busbw``);
+  * per-model, per-world GPU-timed seconds per step (the workers' online profiling);
+  * a like-for-like control: the same trace replayed on the same warm pool with the
+    non-elastic FIFO policy (reference pkg/algorithm/fifo.go:25-52); ``vs_baseline`` =
+    avg JCT(FIFO) / avg JCT(policy) (> 1: the policy beats the control).  Skipped, with the
+    reason logged, when the deadline leaves too little time.
+``--deadline`` (default 540 s, below the driver's 600 s): a watchdog on every rank dumps all
+thread stacks, rank 0 prints a ``"status": "timeout"`` JSON line without ``value``, and the
+process exits non-zero.  ``--precision fp32`` runs the reference's precision (no autocast).
 """
 from __future__ import annotations
 
 import argparse
+import copy
 import json
 import os
 import socket
@@ -113,7 +127,7 @@ def sync(device):
         torch.cuda.synchronize(device)
 
 
-def warmup(device, steps: int, models, batch, compression=None, grad_dtype="fp32"):
+def warmup(device, steps: int, models, batch, compression=None, grad_dtype="fp32", amp=True):
     """Untimed warm-up of every model in the mix on this device (single-GPU steps).
 
     The steps run on the pool worker's own warm workload cache (``workloads.train.get_warm``
@@ -127,7 +141,7 @@ def warmup(device, steps: int, models, batch, compression=None, grad_dtype="fp32
     out = {}
     for name in models:
         wm = get_warm(TrainConfig(model=name, per_gpu_batch=batch[name], compression=compression,
-                                  grad_dtype=grad_dtype), device)
+                                  grad_dtype=grad_dtype, amp=amp), device)
         m, opt, b = wm.model, wm.opt, wm.pool[0]
         t0 = None
         for i in range(max(2, steps)):
@@ -135,7 +149,7 @@ def warmup(device, steps: int, models, batch, compression=None, grad_dtype="fp32
                 sync(device)
                 t0 = time.perf_counter()
             wm.ddp.zero_grad()
-            with torch.autocast(device.type, dtype=torch.bfloat16, enabled=device.type == "cuda",
+            with torch.autocast(device.type, dtype=torch.bfloat16, enabled=amp and device.type == "cuda",
                                 cache_enabled=False):
                 loss = wm.w.loss(m, b)
             loss.backward()
@@ -143,6 +157,91 @@ def warmup(device, steps: int, models, batch, compression=None, grad_dtype="fp32
         sync(device)
         out[name] = (time.perf_counter() - t0) / (max(2, steps) - 1) * 1e3
     return out
+
+
+class Watchdog:
+    """Bench deadline below the driver's: on expiry every rank dumps all thread stacks, rank 0
+    prints a ``status: timeout`` JSON line (no ``value``) and the process exits non-zero."""
+
+    def __init__(self, deadline_s: float, rank: int, world: int, base: dict):
+        self.t0 = time.monotonic()
+        self.deadline_s = deadline_s
+        self.rank, self.world, self.base = rank, world, base
+        self.phase = "startup"
+        self._done = threading.Event()
+        if deadline_s > 0:
+            threading.Thread(target=self._run, daemon=True, name="bench-deadline").start()
+
+    def left(self) -> float:
+        return self.deadline_s - (time.monotonic() - self.t0) if self.deadline_s > 0 else float("inf")
+
+    def done(self) -> None:
+        self._done.set()
+
+    def _run(self) -> None:
+        if self._done.wait(self.deadline_s):
+            return
+        import faulthandler
+
+        print(f"[bench rank {self.rank}] deadline {self.deadline_s:.0f}s expired in phase {self.phase!r}; "
+              "thread stacks follow", file=sys.stderr, flush=True)
+        faulthandler.dump_traceback(file=sys.stderr, all_threads=True)
+        if self.rank == 0:
+            print(json.dumps(dict(self.base, status="timeout", value=None, phase=self.phase,
+                                  elapsed_s=round(time.monotonic() - self.t0, 1))), flush=True)
+        sys.stdout.flush()
+        sys.stderr.flush()
+        os._exit(3)
+
+
+def measure_busbw(store, rank: int, world: int, device, sizes_mb=(16, 64, 256), iters: int = 5) -> dict:
+    """RCCL all-reduce bus bandwidth over xGMI for every power-of-two sub-world <= N (and N):
+    ranks [0, k) build a fresh communicator (its init time is reported), run 2 warm + ``iters``
+    timed fp32 all-reduces per size; busbw = bytes / t x 2 (k-1) / k (ring all-reduce
+    traffic per link).  Outside the timed trace."""
+    ks = sorted({k for k in (2, 4, 8, 16, 32) if k <= world} | {world})
+    out: dict = {"by_world": {}, "init_s": {}}
+    for k in ks:
+        if rank < k:
+            t0 = time.perf_counter()
+            comm = RcclCommunicator(store, f"bench/bw/{k}", rank, k, device, timeout=120)
+            sync(device)
+            out["init_s"][str(k)] = round(time.perf_counter() - t0, 4)
+            res = {}
+            for mb in sizes_mb:
+                x = torch.ones(mb << 18, device=device)  # mb MiB of fp32
+                for _ in range(2):
+                    comm.allreduce_(x, "sum")
+                sync(device)
+                t0 = time.perf_counter()
+                for _ in range(iters):
+                    comm.allreduce_(x, "sum")
+                sync(device)
+                dt = (time.perf_counter() - t0) / iters
+                res[str(mb)] = round(x.numel() * 4 / dt / 1e9 * 2 * (k - 1) / k, 1)
+                del x
+            out["by_world"][str(k)] = res
+            comm.destroy()
+        dist.barrier()
+    return out
+
+
+def per_world_step_ms(allrec: list[dict]) -> dict:
+    """{model: {world: GPU-timed ms per training step}} from the workers' online profiling
+    (one record per job: every member returns the same synced ``perf``)."""
+    seen = set()
+    acc: dict = {}
+    for r in allrec:
+        for job, model, perf in r.get("perf", []):
+            if job in seen or not perf:
+                continue
+            seen.add(job)
+            for w, (n, sec) in perf.items():
+                a = acc.setdefault(model, {}).setdefault(w, [0, 0.0])
+                a[0] += n
+                a[1] += sec
+    return {m: {w: round(sec / n * 1e3, 3) for w, (n, sec) in sorted(d.items(), key=lambda x: int(x[0])) if n}
+            for m, d in acc.items()}
 
 
 def main():
@@ -176,6 +275,16 @@ def main():
                     help="cpu: rehearse the multi-rank orchestration on gloo with tiny models (tests only)")
     ap.add_argument("--comm-backend", default=None, choices=[None, "rccl", "gloo"],
                     help="data-plane collectives (default: rccl on cuda, gloo on cpu)")
+    ap.add_argument("--precision", default="bf16-amp", choices=["bf16-amp", "fp32"],
+                    help="compute precision: bf16 autocast (fp32 master weights / gradients) or fp32 "
+                         "(the reference's precision)")
+    ap.add_argument("--deadline", type=float, default=540.0,
+                    help="seconds: dump stacks + print a status=timeout line + exit non-zero (0 = none)")
+    ap.add_argument("--control", default="FIFO",
+                    help="non-elastic control policy replayed on the same trace after the timed run "
+                         "('none' to skip); vs_baseline = avg JCT(control) / avg JCT(policy)")
+    ap.add_argument("--resize-timeout", type=float, default=60.0,
+                    help="a resize whose previous epoch has not synced after this long becomes an abort epoch")
     ap.add_argument("--share-gpu", action="store_true",
                     help="rehearsal only: every rank uses cuda:0 (needs --comm-backend gloo; "
                          "RCCL refuses two ranks on one GPU). Never a benchmark number")
@@ -188,6 +297,12 @@ def main():
     if world != a.gpus:
         raise SystemExit(f"--gpus {a.gpus} but WORLD_SIZE={world}")
     comm_backend = a.comm_backend or ("rccl" if a.device == "cuda" else "gloo")
+    amp = a.precision != "fp32"
+    dtype = ("bf16" if amp else "fp32") if a.device == "cuda" else "fp32"
+    base_line = {"metric": BASELINE_METRIC, "unit": "s (avg JCT)", "n_gpus": world, "steps": a.steps,
+                 "warmup": a.warmup, "higher_is_better": False, "scaling": "weak", "dtype": dtype,
+                 "precision": a.precision, "data": "synthetic"}
+    dog = Watchdog(a.deadline, rank, world, base_line)
     if a.share_gpu and comm_backend != "gloo":
         raise SystemExit("--share-gpu needs --comm-backend gloo")
     topo_info = {}
@@ -214,15 +329,15 @@ def main():
     watch = connect_store("127.0.0.1", port[0])
 
     # ---------------- untimed warm-up ----------------
-    log(rank, f"warm-up: {a.warmup} steps x {models} on {world} {a.device} device(s)")
-    step_ms = warmup(device, a.warmup, models, batch, a.compression, a.grad_dtype)
+    dog.phase = "warmup"
+    log(rank, f"warm-up: {a.warmup} steps x {models} on {world} {a.device} device(s), {a.precision}")
+    step_ms = warmup(device, a.warmup, models, batch, a.compression, a.grad_dtype, amp)
+    bw = {"by_world": {}, "init_s": {}}
     if world > 1:
         if comm_backend == "rccl":
-            comm = RcclCommunicator(store, "bench/warm", rank, world, device)
-            x = torch.ones(16 << 20, device=device)
-            comm.allreduce_(x, "sum")
-            torch.cuda.synchronize(device)
-            comm.destroy()
+            dog.phase = "allreduce-busbw"
+            bw = measure_busbw(store, rank, world, device)
+            log(rank, f"RCCL all-reduce busbw (GB/s) by world: {bw['by_world']}; init s: {bw['init_s']}")
         dist.barrier()
     log(rank, f"warm-up single-GPU step ms: {step_ms}")
 
@@ -231,14 +346,25 @@ def main():
     os.environ.setdefault("VODA_CKPT_DIR", f"/tmp/voda_ckpt_{os.getpid()}")
     metrics_dir = f"/tmp/voda_metrics_{port[0]}"
     defaults = {"commit_every": a.commit_every, "compression": a.compression, "metrics_dir": metrics_dir,
-                "grad_dtype": a.grad_dtype}
+                "grad_dtype": a.grad_dtype, "amp": amp}
+    control = None if a.control.lower() == "none" else a.control
+    ctl_trace = []
+    for tj in trace:  # same jobs, own names (own rendezvous keys) for the control replay
+        spec = copy.deepcopy(tj.spec)
+        from vodascheduler_amd.common.mpijob import set_name
+
+        set_name(spec, "ctl-" + spec["metadata"]["name"])
+        ctl_trace.append(type(tj)(tj.submit_time, spec))
 
     # ---------------- timed region ----------------
     if world > 1:
         dist.barrier()
     sync(device)
+    dog.phase = "trace"
     t0 = time.perf_counter()
     result: dict = {}
+    ctl: dict = {}
+    t_main = [0.0]
     sched = None
     if rank == 0:
         def drive():
@@ -246,9 +372,25 @@ def main():
                 gpu_numa = None
                 if a.device == "cuda" and topo.n >= world and not a.share_gpu:
                     gpu_numa = {"node0": {r: topo.numa.get(r, 0) for r in range(world)}}
-                result.update(run_trace(store, trace, locs, a.algorithm, rate_limit_sec=a.rate_limit,
-                                        tick_sec=1.0, train_defaults=defaults, timeout=3000,
-                                        progress=lambda s: log(0, s), trace_path=a.trace, gpu_numa=gpu_numa))
+                kw = dict(rate_limit_sec=a.rate_limit, tick_sec=1.0, progress=lambda s: log(0, s),
+                          gpu_numa=gpu_numa, settle_timeout=a.resize_timeout)
+                result.update(run_trace(store, trace, locs, a.algorithm, train_defaults=defaults,
+                                        timeout=max(30.0, dog.left() - 15), trace_path=a.trace,
+                                        stop_pool=control is None, **kw))
+                t_main[0] = time.perf_counter()
+                if control is not None:
+                    need = 1.3 * result["wall_s"] + 20
+                    if dog.left() < need:
+                        ctl["skipped"] = (f"{dog.left():.0f} s left before the deadline, the control needs "
+                                          f"~{need:.0f} s (1.3 x the timed trace)")
+                        log(0, f"control run skipped: {ctl['skipped']}")
+                        store.set("pool/shutdown", "1")
+                        return
+                    dog.phase = "control"
+                    log(0, f"control: same trace with {control} on the same warm pool")
+                    ctl.update(run_trace(store, ctl_trace, locs, control,
+                                         train_defaults=dict(defaults, metrics_dir=metrics_dir + "_ctl"),
+                                         timeout=max(30.0, dog.left() - 10), stop_pool=True, **kw))
             except BaseException as e:  # never leave the pool hanging
                 result["error"] = repr(e)
                 store.set("pool/shutdown", "1")
@@ -256,7 +398,7 @@ def main():
         sched = threading.Thread(target=drive, name="control-plane", daemon=True)
         sched.start()
     worker = PoolWorker(store, watch, f"node0:{rank}", device, backend=comm_backend,
-                        timeout=900)
+                        timeout=120)
     recs = worker.serve()
     if sched is not None:
         sched.join()
@@ -264,21 +406,28 @@ def main():
     if world > 1:
         dist.barrier()
     t1 = time.perf_counter()
+    dog.phase = "report"
+    main_recs = [r for r in recs if not r["job"].startswith("ctl-")]
 
     # ---------------- aggregate ----------------
-    my = {"steps": sum((r["result"] or {}).get("steps", 0) for r in recs if isinstance(r["result"], dict)),
-          "train_time": sum((r["result"] or {}).get("train_time", 0.0) for r in recs if isinstance(r["result"], dict)),
-          "comm_init": [(x.get("world"), x.get("comm_init_s"), x.get("cached")) for r in recs
-                        for x in r["resize_log"]]}
+    ok = [r for r in main_recs if isinstance(r["result"], dict)]
+    my = {"steps": sum(r["result"].get("steps", 0) for r in ok),
+          "train_time": sum(r["result"].get("train_time", 0.0) for r in ok),
+          "comm_init": [(x.get("world"), x.get("comm_init_s"), x.get("cached")) for r in main_recs
+                        for x in r["resize_log"]],
+          "perf": [(r["job"], r["result"].get("model"), r["result"].get("perf")) for r in ok]}
     allrec = [my]
+    # the timed region ends when the main trace's last job completed (rank 0's control plane
+    # stamps it); with the control replay running after it, the ranks' own t1 is later
+    main_end = (t_main[0] - t0) if (rank == 0 and control is not None and t_main[0] > 0) else -1.0
     if world > 1:
         allrec = [None] * world
         dist.all_gather_object(allrec, my)
-        wall = torch.tensor([t1 - t0], dtype=torch.float64)
+        wall = torch.tensor([main_end, t1 - t0], dtype=torch.float64)
         dist.all_reduce(wall, op=dist.ReduceOp.MAX)
-        wall_s = float(wall.item())
+        wall_s = float(wall[0]) if float(wall[0]) > 0 else float(wall[1])
     else:
-        wall_s = t1 - t0
+        wall_s = main_end if main_end > 0 else t1 - t0
     if rank == 0:
         if "error" in result:
             raise SystemExit(f"bench failed: {result['error']}")
@@ -293,18 +442,33 @@ def main():
 
             wl = workload_of(tj.spec)
             samples += wl["steps_per_epoch"] * 2 * batch[wl["model"]]
+        if ctl.get("avg_jct_s"):
+            control_out = {"algorithm": control, "avg_jct_s": round(ctl["avg_jct_s"], 3),
+                           "makespan_s": round(ctl["makespan_s"], 3), "p95_jct_s": round(ctl["p95_jct_s"], 3),
+                           "wall_s": round(ctl["wall_s"], 3), "resize_events": ctl["n_resizes"],
+                           "failed": ctl["failed"]}
+            vs = round(ctl["avg_jct_s"] / result["avg_jct_s"], 4)
+        else:
+            control_out = {"algorithm": control, "skipped": ctl.get("skipped", "disabled (--control none)")}
+            vs = None
         line = {
             "metric": BASELINE_METRIC,
+            "status": "ok",
             "value": round(result["avg_jct_s"], 3),
             "unit": "s (avg JCT)",
             "n_gpus": world,
             "steps": a.steps,
             "warmup": a.warmup,
-            "ms_per_step": round(tot_train / max(tot_steps, 1) * 1e3, 3),
+            # timed wall / K: steps x ms_per_step = the timed region (the trace)
+            "ms_per_step": round(wall_s / max(a.steps, 1) * 1e3, 3),
             "higher_is_better": False,
             "scaling": "weak",
-            "vs_baseline": None,
-            "dtype": "bf16" if a.device == "cuda" else "fp32",
+            "vs_baseline": vs,
+            "vs_baseline_note": (f"avg JCT of the non-elastic {control} control on the same trace and warm pool / "
+                                 f"avg JCT of {a.algorithm} (> 1: the policy beats the control); no published "
+                                 "reference number exists (BASELINE.json published: {})"),
+            "dtype": dtype,
+            "precision": a.precision,
             "grad_dtype": a.grad_dtype,
             "allreduce_dtype": a.compression or a.grad_dtype,
             "data": "synthetic (random-init weights, synthetic batches of the real shapes)"
@@ -337,6 +501,14 @@ def main():
             "rccl_comm_cache_hits": sum(1 for w, t, c in inits if c),
             "rccl_init_p50_s": q(fresh, 0.5),
             "rccl_init_p95_s": q(fresh, 0.95),
+            "forced_abort_epochs": result.get("forced_abort_epochs", 0),
+            "allreduce_busbw_gbs": bw["by_world"].get(str(world)),
+            "allreduce_busbw_by_world": bw["by_world"],
+            "rccl_init_s": bw["init_s"],
+            "step_ms_by_world": per_world_step_ms(allrec),
+            "gpu_ms_per_train_step": round(tot_train / max(tot_steps, 1) * 1e3, 3),
+            "control": control_out,
+            "deadline_s": a.deadline,
             "throughput_samples_per_s": round(samples / wall_s, 1),
             "topology": topo_info,
             "warmup_single_gpu_step_ms": {k: round(v, 2) for k, v in step_ms.items()},
@@ -345,7 +517,9 @@ def main():
         if a.out:
             with open(a.out, "w") as f:
                 json.dump({"line": line, "jct": result["jct"], "events": result["events"],
-                           "resize_latency": result["resize_latency"], "workers": allrec}, f, indent=1)
+                           "resize_latency": result["resize_latency"], "workers": allrec,
+                           "control_jct": ctl.get("jct")}, f, indent=1)
+    dog.done()
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()

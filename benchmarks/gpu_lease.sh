@@ -1,0 +1,84 @@
+#!/usr/bin/env bash
+# One GPU lease, several named steps, each under its own time limit; the first failing step
+# ends the lease (no retries: a fault, abort or timeout means read the logs, then fix).
+#
+#   gpurun --timeout 1200 -- bash benchmarks/gpu_lease.sh TAG STEP [STEP ...]
+#
+# Steps (outputs under gpurun_out/TAG/):
+#   tests            pytest -m gpu (one process, per-test 120 s timeout)
+#   smoke            __graft_entry__.smoke()
+#   bench            bench.py N=1, driver flags (--steps 20 --warmup 5), with the FIFO control
+#   bench-fp32       bench.py N=1 at the reference's precision (fp32)
+#   step-MODEL[-fp32]        benchmarks/model_step.py timing of one model (resnet50, bert-base, ...)
+#   prof-MODEL[-fp32]        rocprofv3 --kernel-trace --stats of 10 steps of one model
+#   pmc-MODEL:COUNTERS       one rocprofv3 --pmc pass (comma-separated counters)
+#   py:SCRIPT[:ARGS]         python benchmarks/SCRIPT ARGS (comma-separated args)
+set -o pipefail
+TAG=${1:?tag}
+shift
+OUT=gpurun_out/$TAG
+mkdir -p "$OUT"
+export TMPDIR=/tmp
+export HSA_ENABLE_IPC_MODE_LEGACY=0
+export MIOPEN_USER_DB_PATH=${MIOPEN_USER_DB_PATH:-$PWD/var/miopen/db}
+export MIOPEN_CUSTOM_CACHE_DIR=${MIOPEN_CUSTOM_CACHE_DIR:-/tmp/miopen-cache}
+
+run() {  # run SECONDS NAME CMD...
+  local secs=$1 name=$2
+  shift 2
+  echo "[lease $(date +%T)] $name: $*"
+  timeout -k 10 "$secs" "$@" > "$OUT/$name.log" 2>&1
+  local rc=$?
+  echo "[lease $(date +%T)] $name rc=$rc"
+  tail -n 5 "$OUT/$name.log"
+  return $rc
+}
+
+for step in "$@"; do
+  case "$step" in
+    tests)
+      run 600 tests python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread || exit $? ;;
+    smoke)
+      run 300 smoke python -c "import __graft_entry__ as g; g.smoke()" || exit $? ;;
+    bench)
+      run 590 bench python -u bench.py --steps 20 --warmup 5 --out "$OUT/bench.json" || exit $? ;;
+    bench-fp32)
+      run 590 bench-fp32 python -u bench.py --steps 20 --warmup 5 --precision fp32 --out "$OUT/bench_fp32.json" \
+        || exit $? ;;
+    step-*)
+      m=${step#step-}
+      prec=bf16-amp
+      if [[ $m == *-fp32 ]]; then m=${m%-fp32}; prec=fp32; fi
+      run 300 "$step" python -u benchmarks/model_step.py --model "$m" --steps 20 --warmup 5 --precision "$prec" \
+        || exit $? ;;
+    prof-*)
+      m=${step#prof-}
+      prec=bf16-amp
+      if [[ $m == *-fp32 ]]; then m=${m%-fp32}; prec=fp32; fi
+      R=$PWD
+      ( cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "/tmp/$step" -o k -- \
+          python3 "$R/benchmarks/model_step.py" --model "$m" --steps 10 --warmup 6 --precision "$prec" \
+          --profile-marker ) > "$OUT/$step.log" 2>&1 || { tail -20 "$OUT/$step.log"; exit 6; }
+      mkdir -p "$OUT/$step"
+      python3 benchmarks/trace_window_stats.py "/tmp/$step/k_kernel_trace.csv" "$OUT/$step/steady_kernel_stats.csv" \
+        >> "$OUT/$step.log" 2>&1 || exit 7
+      python3 benchmarks/rocprof_summary.py "$OUT/$step/steady_kernel_stats.csv" "$m $prec steady state (10 steps)" 45 10 \
+        > "$OUT/$step.md" || exit 7
+      tail -n 3 "$OUT/$step.log" ;;
+    pmc-*)
+      spec=${step#pmc-}
+      m=${spec%%:*}
+      ctr=${spec#*:}
+      run 120 "pmc-$m" rocprofv3 --kernel-trace --pmc ${ctr//,/ } -d "$OUT/pmc-$m" -o run -- \
+        python -u benchmarks/model_step.py --model "$m" --steps 3 --warmup 3 || exit $? ;;
+    py:*)
+      spec=${step#py:}
+      script=${spec%%:*}
+      args=""
+      [[ $spec == *:* ]] && args=${spec#*:}
+      run 600 "py-${script%.py}" python -u "benchmarks/$script" ${args//,/ } || exit $? ;;
+    *)
+      echo "unknown step $step"; exit 2 ;;
+  esac
+done
+echo "[lease $(date +%T)] all steps ok"

@@ -24,12 +24,12 @@ from vodascheduler_amd.runtime.stepgraph import GraphedStepper  # noqa: E402
 
 def run(model: str, batch: int | None, steps: int, warmup: int, marker: bool = False, graph: bool = False,
         grad_dtype: str = "fp32", overlap_opt: bool = False, torch_profile: str | None = None,
-        record_losses: int = 0) -> dict:
+        record_losses: int = 0, amp: bool = True) -> dict:
     dev = torch.device("cuda", 0)
     w = get_workload(model)
     bs = batch or w.per_gpu_batch
     torch.manual_seed(0)
-    m = prepare_model(w, dev)
+    m = prepare_model(w, dev, amp)
     opt = make_optimizer(w.optimizer, m.parameters(), grad_dtype={"fp32": torch.float32, "bf16": torch.bfloat16}[grad_dtype],
                          **w.opt_kwargs)
     b = w.make_batch(bs, dev, None)
@@ -44,7 +44,7 @@ def run(model: str, batch: int | None, steps: int, warmup: int, marker: bool = F
 
     def step_fn(bb):
         (ddp or opt).zero_grad()
-        with torch.autocast("cuda", dtype=torch.bfloat16, cache_enabled=not graph):
+        with torch.autocast("cuda", dtype=torch.bfloat16, enabled=amp, cache_enabled=not graph):
             loss = w.loss(m, bb)
         loss.backward()
         (ddp or opt).step()
@@ -103,12 +103,14 @@ def main():
     ap.add_argument("--overlap-opt", action="store_true", help="per-bucket optimizer overlapping backward (ElasticDDP)")
     ap.add_argument("--torch-profile", default=None, help="write a torch.profiler op table (3 steps) to this path")
     ap.add_argument("--losses", type=int, default=0, help="record the first N step losses (trajectory checks)")
+    ap.add_argument("--precision", default="bf16-amp", choices=["bf16-amp", "fp32"])
     a = ap.parse_args()
     if a.cudnn_benchmark:
         torch.backends.cudnn.benchmark = True
     _native.hip()
     out = run(a.model, a.batch, a.steps, a.warmup, a.profile_marker, a.graph, a.grad_dtype, a.overlap_opt,
-              a.torch_profile, a.losses)
+              a.torch_profile, a.losses, a.precision != "fp32")
+    out["precision"] = a.precision
     out["grad_dtype"] = a.grad_dtype
     out["overlap_opt"] = a.overlap_opt
     print(json.dumps(out), flush=True)

@@ -132,3 +132,48 @@ def assert_matches_replay(cfg, path: str, device: str, exact: bool = True) -> di
             torch.testing.assert_close(a.float(), b.float(), rtol=2e-3, atol=2e-4)
     assert ex["epoch"] == ref_ex["epoch"] and ex["samples"] == ref_ex["samples"]
     return ex
+
+
+def spawn_ranks(target, world, *args, timeout: float = 180.0):
+    """Run ``target(port, rank, world, q, *args)`` in ``world`` daemon processes and collect
+    one result per rank.  Never wedges the test session: on a hang, a failure or a bad exit
+    code every surviving rank is killed, and the assertion names the ranks that hung."""
+    import queue
+
+    from vodascheduler_amd.runtime.cluster import free_port
+
+    port = free_port()
+    store = connect_store("127.0.0.1", port, is_master=True)
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    ps = [ctx.Process(target=target, args=(port, r, world, q) + args, daemon=True) for r in range(world)]
+    res: dict = {}
+    try:
+        for p in ps:
+            p.start()
+        deadline = time.monotonic() + timeout
+        while len(res) < world:
+            left = deadline - time.monotonic()
+            if left <= 0:
+                break
+            try:
+                r, v = q.get(timeout=min(left, 5.0))
+                res[r] = v
+            except queue.Empty:
+                dead = [i for i, p in enumerate(ps) if p.exitcode not in (None, 0) and i not in res]
+                if dead:
+                    break  # a rank crashed: the others would wait for it forever
+        hung = [r for r in range(world) if r not in res]
+        assert not hung, (f"ranks {hung} of {world} returned no result within {timeout:.0f}s "
+                          f"(exit codes {[p.exitcode for p in ps]})")
+        for i, p in enumerate(ps):
+            p.join(60)
+            assert p.exitcode == 0, f"rank {i} exit code {p.exitcode}"
+    finally:
+        for p in ps:
+            if p.is_alive():
+                p.kill()
+        for p in ps:
+            p.join(10)
+        del store
+    return res

@@ -6,6 +6,8 @@ import os
 import subprocess
 import sys
 
+import pytest
+
 from vodascheduler_amd.runtime.cluster import free_port
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -28,9 +30,47 @@ def test_bench_two_ranks_cpu_rehearsal():
     assert d["value"] > 0 and d["makespan_s"] >= d["value"]
     assert d["membership_changes"] >= 6  # every job started; some were resized across the two ranks
     assert d["grad_dtype"] == "fp32" and d["allreduce_dtype"] == "fp32"
+    assert d["status"] == "ok" and d["precision"] == "bf16-amp"
+    # the like-for-like control replayed on the same warm pool (VERDICT r2 Next #6)
+    assert d["control"]["algorithm"] == "FIFO" and d["control"]["avg_jct_s"] > 0 and not d["control"]["failed"]
+    assert d["vs_baseline"] == pytest.approx(d["control"]["avg_jct_s"] / d["value"], rel=1e-3)
+    # online profiling: GPU/CPU-timed ms per step for every model at every world it ran at
+    assert set(d["step_ms_by_world"]) <= {"mnist-torch", "mnist"} and d["step_ms_by_world"]
+    assert all(v > 0 for m in d["step_ms_by_world"].values() for v in m.values())
+    assert d["steps"] * d["ms_per_step"] / 1e3 == pytest.approx(d["wall_s"], rel=1e-2)
 
 
-import pytest  # noqa: E402
+def test_bench_eight_ranks_cpu_rehearsal():
+    """The driver's N=8 case rehearsed on gloo: 8 pool workers, jobs resized across up to 8
+    ranks, control replay, one JSON line (VERDICT r2 Next #2d)."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "8", "--master-addr",
+           "127.0.0.1", "--master-port", str(free_port()), os.path.join(ROOT, "bench.py"), "--gpus", "8", "--steps",
+           "2", "--warmup", "1", "--jobs", "8", "--device", "cpu", "--interarrival", "0.3"]
+    r = subprocess.run(cmd, cwd="/tmp", capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 8 and d["status"] == "ok" and d["value"] > 0
+    assert d["resize_events"] >= 1 and d["forced_abort_epochs"] == 0
+    assert max(int(w) for m in d["step_ms_by_world"].values() for w in m) >= 4
+    assert d["vs_baseline"] is not None
+
+
+def test_bench_deadline_prints_timeout_line_and_fails():
+    """``--deadline`` below the driver's limit: stacks dumped, a status=timeout line without a
+    value, non-zero exit -- never a silent hang (VERDICT r2 Weak #6)."""
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "50", "--warmup", "1",
+           "--jobs", "8", "--device", "cpu", "--deadline", "12"]
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    r = subprocess.run(cmd, cwd="/tmp", env=env, capture_output=True, text=True, timeout=120)
+    assert r.returncode != 0
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    d = json.loads(lines[0])
+    assert d["status"] == "timeout" and d["value"] is None and d["phase"] in ("warmup", "trace")
+    assert "deadline 12s expired" in r.stderr and "File " in r.stderr  # thread stacks
+
 
 
 @pytest.mark.parametrize("n", [2, 4])

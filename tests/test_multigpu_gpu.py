@@ -47,23 +47,7 @@ def _coll_worker(port, rank, world, q):
     q.put((rank, {k: v.numpy() for k, v in out.items()}))
 
 
-def _spawn(target, world, *args):
-    from vodascheduler_amd.runtime.cluster import free_port
-    from vodascheduler_amd.runtime.rendezvous import connect_store
-
-    port = free_port()
-    store = connect_store("127.0.0.1", port, is_master=True)
-    ctx = mp.get_context("spawn")
-    q = ctx.Queue()
-    ps = [ctx.Process(target=target, args=(port, r, world, q) + args) for r in range(world)]
-    for p in ps:
-        p.start()
-    res = dict(q.get(timeout=240) for _ in ps)
-    for p in ps:
-        p.join(60)
-        assert p.exitcode == 0
-    del store
-    return res
+from elastic_harness import spawn_ranks as _spawn  # noqa: E402
 
 
 @pytest.mark.parametrize("world", sorted({2, min(4, N_DEV), min(8, N_DEV)}))

@@ -38,14 +38,16 @@ def run_trace(store, trace: list[TraceJob], worker_locs, algorithm: str = "Elast
               rate_limit_sec: float = 1.0, tick_sec: float = 1.0, train_defaults: dict | None = None,
               timeout: float = 3600.0, gpu_type: str = DEFAULT_GPU_TYPE, progress=None,
               collect_every_s: float = 2.0, trace_path: str | None = None,
-              gpu_numa: dict[str, dict[int, int]] | None = None) -> dict:
+              gpu_numa: dict[str, dict[int, int]] | None = None, stop_pool: bool = True,
+              settle_timeout: float = 120.0) -> dict:
     """Submit ``trace`` in real time (``submit_time`` seconds after start) and wait until every
     job completed.  Returns JCT / makespan / resize-latency statistics.  ``gpu_numa``: node ->
-    {GPU: NUMA domain} from topology discovery (placement tie-breaker)."""
+    {GPU: NUMA domain} from topology discovery (placement tie-breaker).  ``stop_pool=False``
+    leaves the pool workers serving (another trace follows on the same warm pool)."""
     db = MemoryStore()
     mq = InProcQueue(maxsize=10 ** 6)
     svc = TrainingService(db, mq)
-    backend = PoolBackend(store, worker_locs, train_defaults)
+    backend = PoolBackend(store, worker_locs, train_defaults, settle_timeout=settle_timeout)
     from ..placement.manager import PlacementManager
 
     core = SchedulerCore(gpu_type, db, ResourceAllocator(db), backend, algorithm=algorithm,
@@ -90,7 +92,7 @@ def run_trace(store, trace: list[TraceJob], worker_locs, algorithm: str = "Elast
         jobs = runner.call(lambda: {n: core.done_jobs[n].clone() for n in names})
     finally:
         runner.stop()
-        backend.shutdown()
+        backend.shutdown(stop_pool)
         if tracer is not None:
             tracer.save(trace_path)
     failed = [n for n, j in jobs.items() if j.status != JobStatus.COMPLETED.value]
@@ -105,7 +107,7 @@ def run_trace(store, trace: list[TraceJob], worker_locs, algorithm: str = "Elast
         "n_starts": len(lat["start"]), "n_resizes": len(lat["resize"]), "n_shrinks_to_1": len(lat["to_one"]),
         "start_latency_p50_s": q(lat["start"], 0.5), "start_latency_p95_s": q(lat["start"], 0.95),
         "resize_latency_p50_s": q(lat["resize"], 0.5), "resize_latency_p95_s": q(lat["resize"], 0.95),
-        "reschedules": core.resched_count, "jct": jct,
+        "reschedules": core.resched_count, "jct": jct, "forced_abort_epochs": backend.forced_epochs,
         "events": backend.events, "resize_latency": backend.resize_latency,
     }
 

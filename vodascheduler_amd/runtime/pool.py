@@ -54,7 +54,7 @@ def job_train_config(job, defaults: dict | None = None) -> dict:
 
 class PoolBackend(Backend):
     def __init__(self, store, worker_locs: list[Loc], train_defaults: dict | None = None,
-                 poll_interval: float = 0.05):
+                 poll_interval: float = 0.05, settle_timeout: float = 120.0):
         super().__init__()
         self.store = store
         self._lock = threading.Lock()
@@ -67,12 +67,18 @@ class PoolBackend(Backend):
         self.members: dict[str, list[str]] = {}    # desired membership (scheduler view)
         self.live: dict[str, tuple[int, list[str]]] = {}  # last published (epoch, members)
         self.pending: dict[str, tuple] = {}           # membership waiting for the live epoch to sync
-        self.settle_timeout = 120.0
+        # a membership change whose previous epoch has not synced after this long is forced
+        # through as an ABORT epoch: members stuck in the stale epoch's collectives abort
+        # their communicator instead of blocking (bounds a single resize)
+        self.settle_timeout = settle_timeout
         self.active: set[str] = set()
         self.published: dict[tuple[str, int], float] = {}
         self.resize_latency: list[dict] = []
         self.events: list[dict] = []
-        self._mail_n: dict[str, int] = {}
+        self.forced_epochs = 0
+        # mailbox counters continue where an earlier backend on the same warm pool stopped
+        # (several traces in a row on one pool: bench.py's control run)
+        self._mail_n: dict[str, int] = {w: int(store.add(f"pool/{w}/n", 0)) for w in self.workers}
         self._stop = threading.Event()
         self._poll = poll_interval
         self._mon = threading.Thread(target=self._monitor, daemon=True, name="pool-monitor")
@@ -124,16 +130,19 @@ class PoolBackend(Backend):
             return
         rdzv = JobRendezvous(self.store, name)
         live_e, live_m = self.live.get(name, (0, []))
+        abort = False
         if live_m and not force and rdzv.get(f"e/{live_e}/synced") is None and rdzv.outcome() is None:
             t_req = self.pending[name][2]
             if time.time() - t_req < self.settle_timeout:
                 return  # the monitor retries
-            log.warning("job %s: epoch %d not synced after %.0fs; publishing anyway", name, live_e,
+            log.warning("job %s: epoch %d not synced after %.0fs; publishing an abort epoch", name, live_e,
                         self.settle_timeout)
+            abort = True
+            self.forced_epochs += 1
         new_members, kind, t, cfg = self.pending.pop(name)
         if new_members == live_m:
             return
-        e = rdzv.publish(new_members)
+        e = rdzv.publish(new_members, abort=abort)
         log.debug("publish %s epoch %d members %s (was %s)", name, e, new_members, live_m)
         with self._lock:
             self.live[name] = (e, list(new_members))
@@ -171,9 +180,12 @@ class PoolBackend(Backend):
         return {j: [(m.rsplit(":", 1)[0], int(m.rsplit(":", 1)[1])) for m in mem]
                 for j, mem in self.members.items() if mem}
 
-    def shutdown(self) -> None:
+    def shutdown(self, stop_pool: bool = True) -> None:
+        """Stop the monitor; ``stop_pool`` also ends every pool worker's ``serve`` loop (keep
+        the pool warm for another trace with ``stop_pool=False``)."""
         self._stop.set()
-        self.store.set("pool/shutdown", "1")
+        if stop_pool:
+            self.store.set("pool/shutdown", "1")
         self._mon.join(5)
 
     # ------------------------------------------------------------------ monitor

@@ -126,7 +126,7 @@ WARM_CACHE_MAX = 4
 
 def _warm_key(cfg: TrainConfig, device: torch.device) -> tuple:
     return (cfg.model, cfg.per_gpu_batch, cfg.lr, cfg.compression, cfg.bucket_cap_mb, cfg.reduction, cfg.seed,
-            cfg.grad_dtype, cfg.overlap_optimizer, str(device))
+            cfg.grad_dtype, cfg.overlap_optimizer, cfg.amp, str(device))
 
 
 def get_warm(cfg: TrainConfig, device: torch.device, use_cache: bool = True) -> _Warm:
@@ -371,7 +371,8 @@ def train_elastic(ctx: ElasticContext, cfg: TrainConfig, use_cache: bool = True)
                 h.update(t.detach().contiguous().cpu().view(-1).view(torch.uint8).numpy().tobytes())
             digest = h.hexdigest()
         return dict(stats, final_loss=float(loss_t) if loss_t is not None else None, world=ctx.size,
-                    final_step=state.step, world_log=list(state.world_log), state_digest=digest)
+                    final_step=state.step, world_log=list(state.world_log), state_digest=digest,
+                    perf={k: list(v) for k, v in state.perf.items()}, per_gpu_batch=bs)
 
     try:
         return train(state)
