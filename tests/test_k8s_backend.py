@@ -272,3 +272,33 @@ def test_watch_informers_bind_pods_and_report_completion():
     finally:
         backend.shutdown()
         fake.stop()
+
+
+def test_completion_emitted_once_when_watch_and_resync_race():
+    """ADVICE r2 (medium): the watch thread and the resync loop both see a finished MPIJob;
+    the scheduler must get exactly one EV_FINISHED."""
+
+    class NoClient:
+        def get(self, path):
+            return {"items": []}
+
+    b = K8sBackend(NoClient(), DEFAULT_GPU_TYPE, start_thread=False)
+    b.jobs["j"] = {}
+    got = []
+    b.set_event_sink(lambda ev, *a: got.append((ev, a)))
+    st = {"conditions": [{"type": "Succeeded", "status": "True"}]}
+    barrier = threading.Barrier(8)
+
+    def hit(i):
+        barrier.wait()
+        if i % 2:
+            b._job_event("MODIFIED", {"metadata": {"name": "j"}, "status": st})
+        else:
+            b._maybe_finished("j", st)
+
+    ts = [threading.Thread(target=hit, args=(i,)) for i in range(8)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join()
+    assert len([g for g in got if g[0] == "finished"]) == 1, got

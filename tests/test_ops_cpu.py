@@ -1,4 +1,5 @@
 """CPU reference paths of the fused ops (the same flat-buffer math the HIP kernels run)."""
+import copy
 import pytest
 import torch
 
@@ -307,3 +308,30 @@ def test_conv_sep_bias_matches_conv2d_and_flat_grad():
     (ref(x) ** 2).sum().backward()
     torch.testing.assert_close(grad_of(m.bias), ref.bias.grad, rtol=1e-5, atol=1e-5)
     torch.testing.assert_close(grad_of(m.weight), ref.weight.grad, rtol=1e-5, atol=1e-5)
+
+
+def test_grad_only_ddp_bf16_params_with_stock_optimizer():
+    """ElasticDDP in grad-only mode with bf16 parameters and a stock
+    torch.optim optimizer -- the gradients must land in p.grad (bf16 flat buffer), so SGD
+    actually updates, exactly as without the engine."""
+    from vodascheduler_amd.parallel.ddp import ElasticDDP
+
+    torch.manual_seed(0)
+    ref = torch.nn.Sequential(torch.nn.Linear(16, 32), torch.nn.ReLU(), torch.nn.Linear(32, 4)).to(torch.bfloat16)
+    m = copy.deepcopy(ref)
+    w0 = next(m.parameters()).detach().clone()
+    x = torch.randn(8, 16, dtype=torch.bfloat16)
+    o_ref = torch.optim.SGD(ref.parameters(), lr=0.1)
+    o = torch.optim.SGD(m.parameters(), lr=0.1)
+    ddp = ElasticDDP(m, None, o)
+    for _ in range(3):
+        o_ref.zero_grad()
+        ref(x).float().square().mean().backward()
+        o_ref.step()
+        ddp.zero_grad()
+        m(x).float().square().mean().backward()
+        ddp.step()
+    for a, b in zip(m.parameters(), ref.parameters()):
+        assert a.grad is not None and a.grad.dtype == torch.bfloat16
+        assert torch.equal(a, b)
+    assert not torch.equal(next(m.parameters()), w0)  # the optimizer did update

@@ -107,3 +107,20 @@ def test_bert_head_loss_matches_stock_path():
     ref = F.cross_entropy(logits[:, :30522].float(), b[3].reshape(-1))
     torch.testing.assert_close(loss, ref, rtol=1e-4, atol=1e-4)
     assert int(n) == b[3].numel()
+
+
+def test_xent_out_of_range_labels_excluded_from_mean():
+    """rows whose label lies outside [0, V) get zero loss and gradient in the
+    kernel, so they must not count toward the mean either (same predicate)."""
+    _native.hip()
+    torch.manual_seed(1)
+    R, V = 96, 200
+    x = torch.randn(R, V, device=DEV).requires_grad_(True)
+    y = torch.randint(0, V, (R,), device=DEV)
+    y[::5] = V + 3      # out of range
+    y[1::11] = -7       # negative, not ignore_index
+    loss, _, n = softmax_cross_entropy(x, y, V)
+    ok = (y >= 0) & (y < V)
+    assert int(n) == int(ok.sum())
+    lr = F.cross_entropy(x.detach()[ok], y[ok])
+    torch.testing.assert_close(loss, lr, rtol=1e-5, atol=1e-5)

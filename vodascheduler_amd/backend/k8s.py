@@ -151,6 +151,7 @@ class K8sBackend(Backend):
         self.placement: dict[str, list[tuple[str, int]]] = {}   # job -> worker i -> (node, gpu)
         self._nodes: dict[str, list[int]] = {}
         self._finished: set[str] = set()
+        self._watches_down: set[str] = set()   # informer streams currently failing
         self._stop = threading.Event()
         self.refresh_nodes(emit=False)
         self._thread = None
@@ -294,17 +295,23 @@ class K8sBackend(Backend):
         for obj in items:
             name = obj["metadata"]["name"]
             st = obj.get("status")
-            if name in self.jobs and name not in self._finished and mpijob.is_finished(st):
-                self._finished.add(name)
-                self.emit(EV_FINISHED, name, mpijob.is_succeeded(st))
+            self._maybe_finished(name, st)
 
     def _job_event(self, typ: str, obj: dict) -> None:
-        name = obj.get("metadata", {}).get("name")
-        st = obj.get("status")
-        if typ in ("ADDED", "MODIFIED") and name in self.jobs and name not in self._finished \
-                and mpijob.is_finished(st):
+        if typ in ("ADDED", "MODIFIED"):
+            self._maybe_finished(obj.get("metadata", {}).get("name"), obj.get("status"))
+
+    def _maybe_finished(self, name: str | None, st: dict | None) -> None:
+        """Emit a job's completion exactly once: the watch stream and the resync loop both
+        see it, and only the thread that records it under the lock emits (the reference's
+        informer delivers each completion once)."""
+        if not name or not mpijob.is_finished(st):
+            return
+        with self._lock:
+            if name not in self.jobs or name in self._finished:
+                return
             self._finished.add(name)
-            self.emit(EV_FINISHED, name, mpijob.is_succeeded(st))
+        self.emit(EV_FINISHED, name, mpijob.is_succeeded(st))
 
     def bind_pods(self) -> None:
         """Give pending pods of our jobs the toleration of their placed node."""
@@ -353,24 +360,52 @@ class K8sBackend(Backend):
             self._watchers.append(t)
 
     def _informer(self, path: str, handler) -> None:
-        """LIST + WATCH loop of one collection (re-LIST when the stream breaks or expires)."""
+        """LIST + WATCH loop of one collection (re-LIST when the stream breaks or expires).
+        A stream that keeps failing is logged at warning level and marks the watch down, so
+        the resync loop polls at ``DEGRADED_POLL_S`` until it is back."""
+        fails = 0
+
+        def safe(typ, obj):
+            try:
+                handler(typ, obj)
+            except Exception:  # a bad event must not kill the stream, but must be visible
+                log.warning("watch %s: handler failed on %s event", path, typ, exc_info=True)
+
         while not self._stop.is_set():
             try:
                 lst = self.c.get(path)
                 for obj in lst.get("items", []):
-                    handler("ADDED", obj)
+                    safe("ADDED", obj)
                 rv = (lst.get("metadata") or {}).get("resourceVersion")
+                if fails:
+                    log.info("watch %s re-established after %d failure(s)", path, fails)
+                    self._set_watch_down(path, False)
+                fails = 0
                 while not self._stop.is_set():
-                    rv = self.c.watch(path, rv, handler, self._stop)
+                    rv = self.c.watch(path, rv, safe, self._stop)
             except ApiError as e:
-                if e.status != 410:
-                    log.warning("watch %s failed: %s", path, e)
+                if e.status != 410:  # 410 Gone: resourceVersion expired, a normal re-LIST
+                    fails += 1
+                    log.warning("watch %s failed (%d in a row): %s", path, fails, e)
+                    self._set_watch_down(path, True)
             except Exception as e:  # dropped stream / transient API failure
-                log.debug("watch %s interrupted: %s", path, e)
-            self._stop.wait(1.0)
+                fails += 1
+                (log.warning if fails >= 2 else log.debug)("watch %s interrupted (%d in a row): %s", path, fails, e)
+                if fails >= 2:
+                    self._set_watch_down(path, True)
+            self._stop.wait(min(30.0, 1.0 * 2 ** min(fails, 5)) if fails else 1.0)
+
+    DEGRADED_POLL_S = 2.0
+
+    def _set_watch_down(self, path: str, down: bool) -> None:
+        with self._lock:
+            if down:
+                self._watches_down.add(path)
+            else:
+                self._watches_down.discard(path)
 
     def _loop(self) -> None:
-        while not self._stop.wait(self.poll_interval):
+        while not self._stop.wait(self.DEGRADED_POLL_S if self._watches_down else self.poll_interval):
             for fn in (self.refresh_nodes, self.poll_jobs, self.bind_pods):
                 try:
                     fn()

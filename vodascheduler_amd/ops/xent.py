@@ -25,6 +25,8 @@ import torch.nn.functional as F
 from . import _native as N
 
 USE_FUSED_XENT = os.environ.get("VODA_FUSED_XENT", "1") != "0"
+# host-synchronising check that every label lies in [0, V) or is ignore_index (debug only)
+DEBUG_LABELS = os.environ.get("VODA_DEBUG_LABELS", "0") == "1"
 
 
 def _supported(logits: torch.Tensor, labels: torch.Tensor, num_classes: int) -> bool:
@@ -58,7 +60,11 @@ class _XentFn(torch.autograd.Function):
         lse, rl, rc = torch.empty(R, **f32), torch.empty(R, **f32), torch.empty(R, **f32)
         h.xent_fwd(logits.data_ptr(), R, ld, V, N.dtype_code(logits.dtype), labels.data_ptr(), ignore_index,
                    lse.data_ptr(), rl.data_ptr(), rc.data_ptr(), N.stream_of(logits))
-        n = (labels != ignore_index).sum()
+        # the kernel's validity predicate (xent.hip): ignore_index rows AND labels outside
+        # [0, V) carry no loss / gradient, so neither counts toward the mean
+        n = ((labels != ignore_index) & (labels >= 0) & (labels < V)).sum()
+        if DEBUG_LABELS and bool((((labels < 0) | (labels >= V)) & (labels != ignore_index)).any()):
+            raise ValueError(f"softmax_cross_entropy: label outside [0, {V}) (F.cross_entropy would raise)")
         nf = n.clamp(min=1).float()
         loss = rl.sum() / nf
         correct = rc.sum()

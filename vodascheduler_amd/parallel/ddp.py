@@ -89,8 +89,14 @@ class ElasticDDP:
         if optimizer is not None and hasattr(optimizer, "flat_groups"):
             self.groups: list[FlatGroup] = list(optimizer.flat_groups)
         else:
-            params = [p for p in model.parameters() if p.requires_grad]
-            self.groups = [FlatGroup(params, flatten_params=False)]
+            # grad-only mode (no optimizer, or a stock torch.optim one that reads p.grad): the
+            # flat gradient keeps each parameter's own dtype, so gradients stay visible in
+            # p.grad -- an fp32 flat buffer for bf16 parameters would fold them away from it
+            by_dtype: dict[torch.dtype, list] = {}
+            for p in model.parameters():
+                if p.requires_grad:
+                    by_dtype.setdefault(p.dtype, []).append(p)
+            self.groups = [FlatGroup(ps, flatten_params=False, grad_dtype=dt) for dt, ps in by_dtype.items()]
         self.device = self.groups[0].device
         self.overlap_optimizer = bool(overlap_optimizer and optimizer is not None
                                       and hasattr(optimizer, "step_range") and self.device.type == "cuda")

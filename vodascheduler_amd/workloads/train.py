@@ -105,6 +105,28 @@ class _Warm:
         self._rng0 = rng_state(device)  # generator state right after the seeded build
         self.device = device
         self.step_graph = None  # world-1 step captured by an earlier job (runtime/stepgraph.py)
+        self._graph_hp = None   # optimizer hyperparameters baked into that capture
+
+    @staticmethod
+    def _hparams(opt) -> tuple:
+        return tuple(tuple(sorted((k, v) for k, v in g.items() if k != "params" and isinstance(v, (int, float, bool))))
+                     for g in opt.param_groups)
+
+    def keep_graph(self, graph, opt) -> None:
+        self.step_graph = graph
+        self._graph_hp = self._hparams(opt)
+
+    def reusable_graph(self, opt):
+        """The cached step graph, when replaying it from a fresh optimizer state is exact: a
+        capture bakes host scalars in (the LR, and the first-step flag of momentum buffers,
+        captured as "not first"), so the hyperparameters must match the capture's and no
+        group may use dampening (with dampening 0 the first step ``buf = d`` equals the
+        general ``buf = m * 0 + d``).  Otherwise the job captures its own graph."""
+        if self.step_graph is None or self._hparams(opt) != self._graph_hp:
+            return None
+        if any(float(g.get("dampening", 0.0) or 0.0) != 0.0 for g in opt.param_groups):
+            return None
+        return self.step_graph
 
     def _tensors(self):
         return self.opt.flat_state_tensors() + [b for b in self.model.buffers()]
@@ -289,7 +311,7 @@ def train_elastic(ctx: ElasticContext, cfg: TrainConfig, use_cache: bool = True)
         # of world > 1 stay eager.  Re-captured after every membership change.
         stepper = GraphedStepper(step_fn, model, opt, warmup=2,
                                  enabled=cfg.graph and w.graph_safe and world == 1 and device.type == "cuda",
-                                 graph=wm.step_graph if use_cache else None)
+                                 graph=wm.reusable_graph(opt) if use_cache else None)
         loss_t = None
         while state.epoch < cfg.epochs:
             t_ep = time.time()
@@ -360,7 +382,7 @@ def train_elastic(ctx: ElasticContext, cfg: TrainConfig, use_cache: bool = True)
         if device.type == "cuda":
             torch.cuda.synchronize(device)
         if use_cache and stepper.graph is not None:
-            wm.step_graph = stepper.graph  # the next job of this kind replays it directly
+            wm.keep_graph(stepper.graph, opt)  # the next job of this kind replays it directly
         digest = None
         if cfg.final_state_path:
             if ctx.rank == 0:
