@@ -454,6 +454,34 @@ def replay_reference(cfg: TrainConfig, world_log: list[int], total_steps: int, d
     return [t.detach().cpu() for t in ts], {"epoch": epoch, "samples": samples, "__step__": total_steps}
 
 
+@torch.no_grad()
+def evaluate_checkpoint(cfg: TrainConfig, path: str, device: torch.device) -> tuple[float, float]:
+    """Single-process evaluation of a saved elastic state on the trainer's held-out batches
+    (the reference's ``test()`` run once, pytorch_mnist_elastic.py:155-176): the exact global
+    mean loss / accuracy the distributed eval pass must reproduce."""
+    w, model, opt, _ = build(cfg, device)
+    payload = torch.load(path, map_location=device, weights_only=True)
+    ts = opt.flat_state_tensors() + [b for b in model.buffers() if b.dtype.is_floating_point or b.dtype == torch.int64]
+    if len(ts) != len(payload["tensors"]):
+        raise ValueError("checkpoint does not match the workload's state layout")
+    for t, v in zip(ts, payload["tensors"]):
+        t.copy_(v)
+    opt.after_external_update()
+    bs = cfg.per_gpu_batch or w.per_gpu_batch
+    g = torch.Generator(device=device).manual_seed(cfg.seed + 7919)
+    model.eval()
+    s_loss = s_corr = s_n = 0.0
+    for _ in range(cfg.eval_batches):
+        b = w.make_batch(bs, device, g)
+        with torch.autocast(device.type, dtype=torch.bfloat16, enabled=cfg.amp and device.type == "cuda",
+                            cache_enabled=False):
+            loss, correct, n = w.loss_metrics(model, b)
+        s_loss += float(loss) * float(n)
+        s_corr += float(correct)
+        s_n += float(n)
+    return s_loss / max(s_n, 1.0), s_corr / max(s_n, 1.0)
+
+
 def main(argv=None):
     ap = argparse.ArgumentParser("vodascheduler_amd.workloads.train")
     ap.add_argument("--model", required=True)
