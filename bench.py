@@ -154,6 +154,9 @@ def warmup(device, steps: int, models, batch, compression=None, grad_dtype="fp32
                 loss = wm.w.loss(m, b)
             loss.backward()
             wm.ddp.step()
+            if i == 0:
+                sync(device)
+                log(0, f"warm-up {name}: first step done (library autotuning included)")
         sync(device)
         out[name] = (time.perf_counter() - t0) / (max(2, steps) - 1) * 1e3
     return out

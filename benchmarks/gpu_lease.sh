@@ -49,8 +49,16 @@ for step in "$@"; do
       m=${step#step-}
       prec=bf16-amp
       if [[ $m == *-fp32 ]]; then m=${m%-fp32}; prec=fp32; fi
-      run 300 "$step" python -u benchmarks/model_step.py --model "$m" --steps 20 --warmup 5 --precision "$prec" \
-        || exit $? ;;
+      # fp32 convolutions meet MIOpen's exhaustive find for the first time (minutes, silent):
+      # MIOpen's own info log is the progress signal until the find-db holds the shapes
+      if [[ $prec == fp32 ]]; then export MIOPEN_ENABLE_LOGGING=1 MIOPEN_LOG_LEVEL=5; fi
+      run 900 "$step" python -u benchmarks/model_step.py --model "$m" --steps 20 --warmup 5 --precision "$prec"
+      rc=$?
+      unset MIOPEN_ENABLE_LOGGING MIOPEN_LOG_LEVEL
+      [[ $rc == 0 ]] || exit $rc
+      grep '^{' "$OUT/$step.log" || true ;;
+    miopen-save)  # the find-db / perf-db this lease added, to commit under var/miopen/db
+      mkdir -p "$OUT/miopen_db" && cp "$MIOPEN_USER_DB_PATH"/*.txt "$OUT/miopen_db/" && ls -la "$OUT/miopen_db" ;;
     prof-*)
       m=${step#prof-}
       prec=bf16-amp

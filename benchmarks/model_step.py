@@ -59,9 +59,13 @@ def run(model: str, batch: int | None, steps: int, warmup: int, marker: bool = F
     for _ in range(record_losses):  # trajectory check (untimed): the first losses from init
         losses.append(round(float(step().detach()), 5))
     t_w = time.perf_counter()
-    for _ in range(warmup):
+    for i in range(warmup):
+        t_i = time.perf_counter()
         step()
-    torch.cuda.synchronize(dev)
+        torch.cuda.synchronize(dev)
+        # one line per warm-up step: the first ones run MIOpen's find / library autotuning,
+        # which can take minutes (fp32), and a silent run looks hung
+        print(f"warm-up step {i}: {time.perf_counter() - t_i:.2f} s", file=sys.stderr, flush=True)
     warm_s = time.perf_counter() - t_w
     if marker:  # trace_window_stats.py keeps only kernels after this one
         torch.cuda._sleep(1000)

@@ -36,6 +36,7 @@ def test_unstarted_job_seeded_from_declared_workload():
     name = svc.create_training_job(json.dumps(spec))
     meta = store.find_metadata(name)
     assert meta["job_category"] == "bert-base"          # JOB_CATEGORY knob, not the job name
+    assert name.startswith("bert-j07-")                  # the name keeps the submitted name
     info = store.find_job_info("bert-base", name)
     prof = PROFILES["bert-base"]
     assert info["info_source"] == "profile"

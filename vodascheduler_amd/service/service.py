@@ -86,14 +86,15 @@ class TrainingService:
         try:
             spec = mpijob.load_spec(data)
             # JOB_CATEGORY knob, else the reference's category = the submitted name
-            category = mpijob.get_env(spec, JobConfigEnv.JOB_CATEGORY.value) or spec["metadata"]["name"]
+            submitted = spec["metadata"]["name"]
+            category = mpijob.get_env(spec, JobConfigEnv.JOB_CATEGORY.value) or submitted
             base = self.get_or_create_base_job_info(category)
             now = self.clock.now() if submit_time is None else submit_time
-            name = mpijob.timestamped_name(category, now)
-            # guarantee uniqueness when several jobs of a category arrive within a second
+            name = mpijob.timestamped_name(submitted, now)
+            # guarantee uniqueness when several jobs of a name arrive within a second
             k = 1
             while self._exists(name):
-                name = f"{mpijob.timestamped_name(category, now)}-{k}"
+                name = f"{mpijob.timestamped_name(submitted, now)}-{k}"
                 k += 1
             mpijob.set_name(spec, name)
             job = new_training_job(spec, category, now)
