@@ -623,7 +623,8 @@ AttnArgs make_args(const std::vector<int64_t>& t, int B, int H, int Tq, int Tk, 
 }  // namespace
 
 bool attention_supported(int D, int Tq, int Tk, int dt) {
-  return dt == kBF16 && (D == 32 || D == 64 || D == 128 || D == 256) && Tq >= 1 && Tk >= 1 && Tq <= kMaxT &&
+  // kF32: attention_f32.hip (same shapes, fp32 MFMA)
+  return (dt == kBF16 || dt == kF32) && (D == 32 || D == 64 || D == 128 || D == 256) && Tq >= 1 && Tk >= 1 && Tq <= kMaxT &&
          Tk <= kMaxT;
 }
 

@@ -27,9 +27,6 @@ PYBIND11_MODULE(_vodahip, m) {
   m.def("wgrad_conv_workspace_floats", &wgrad_conv_workspace_floats);
   m.def("wgrad_conv", &wgrad_conv);
   m.def("gelu_tanh_fwd", &gelu_tanh_fwd);
-  m.def("gemm_gelu_aux", &gemm_gelu_aux);
-  m.def("gemm_dgelu", &gemm_dgelu);
-  m.def("gemm_epilogue_algos", &gemm_epilogue_algos);
   m.def("gelu_tanh_bwd", &gelu_tanh_bwd);
   m.def("layernorm_fwd", &layernorm_fwd);
   m.def("layernorm_bwd", &layernorm_bwd);
@@ -56,6 +53,8 @@ PYBIND11_MODULE(_vodahip, m) {
   m.def("attention_supported", &attention_supported);
   m.def("attention_fwd", &attention_fwd);
   m.def("attention_bwd", &attention_bwd);
+  m.def("attention_fwd_f32", &attention_fwd_f32);
+  m.def("attention_bwd_f32", &attention_bwd_f32);
 
   m.def("rccl_unique_id", [] { return py::bytes(rccl_unique_id()); });
   m.def("rccl_version", &rccl_version);

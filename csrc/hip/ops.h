@@ -100,15 +100,6 @@ void bn_pool_bwd(uintptr_t dy, uintptr_t idx, uintptr_t x, uintptr_t save_mean, 
                  uintptr_t gamma, uintptr_t dx, uintptr_t dgamma, uintptr_t dbeta, uintptr_t workspace, int N, int H,
                  int W, int C, int Ho, int Wo, int k, int s, int p, bool accumulate, int dt, uintptr_t stream);
 
-// ---- hipBLASLt GEMMs with a fused GELU epilogue (blaslt_epi.cpp), row-major bf16 ----
-// y = gelu_tanh(x W^T + b), h = x W^T + b;  x [M][K], W [N][K], b [N], h / y [M][N]
-void gemm_gelu_aux(uintptr_t x, uintptr_t w, uintptr_t bias, uintptr_t h, uintptr_t y, int64_t M, int64_t N,
-                   int64_t K, uintptr_t ws, int64_t ws_bytes, uintptr_t stream);
-int gemm_epilogue_algos(int epi, bool trans_a, int64_t m, int64_t n, int64_t k);
-// dh = (dy W) * gelu_tanh'(h);  dy [M][N], W [N][K], h / dh [M][K]
-void gemm_dgelu(uintptr_t dy, uintptr_t w, uintptr_t h, uintptr_t dh, int64_t M, int64_t N, int64_t K, uintptr_t ws,
-                int64_t ws_bytes, uintptr_t stream);
-
 // ---- NHWC max pooling with argmax bytes + gather backward (pool.hip) ----
 void maxpool2d_fwd(uintptr_t x, uintptr_t y, uintptr_t idx, int N, int H, int W, int C, int Ho, int Wo, int k, int s,
                    int p, int dt, uintptr_t stream);
@@ -128,6 +119,11 @@ void attention_fwd(const std::vector<int64_t>& t, int B, int H, int Tq, int Tk, 
                    uintptr_t stream);
 void attention_bwd(const std::vector<int64_t>& t, int B, int H, int Tq, int Tk, int D, float scale, bool causal,
                    uintptr_t stream);
+// ---- fused attention at fp32 on v_mfma_f32_32x32x2_f32 (attention_f32.hip) ----
+void attention_fwd_f32(const std::vector<int64_t>& t, int B, int H, int Tq, int Tk, int D, float scale, bool causal,
+                       uintptr_t stream);
+void attention_bwd_f32(const std::vector<int64_t>& t, int B, int H, int Tq, int Tk, int D, float scale, bool causal,
+                       uintptr_t stream);
 
 // ---- RCCL engine (comm.cpp) ----
 std::string rccl_unique_id();

@@ -1,0 +1,136 @@
+"""fp32 fused attention on v_mfma_f32_32x32x2_f32 (csrc/hip/attention_f32.hip) vs an fp64
+PyTorch reference: the reference trains in fp32 (pytorch_mnist_elastic.py:80-122, Keras MHA
+layers_tf25.py:421-463 without a mixed-precision policy), so an fp32 job must stay on the
+fused HIP path (VERDICT r2 Next #3)."""
+import pytest
+import torch
+
+from vodascheduler_amd.ops import _native, flash
+from vodascheduler_amd.ops.attention import attention_q_kvpacked, attention_qkvpacked
+
+pytestmark = pytest.mark.gpu
+
+TOL = dict(atol=3e-5, rtol=3e-4)
+
+
+def ref_attn(q, k, v, key_mask, causal, scale):
+    """q/k/v [B, H, T, D] fp64, reference additive -1e9 masking."""
+    s = (q @ k.transpose(-1, -2)) * scale
+    Tq, Tk = s.shape[-2:]
+    add = torch.zeros_like(s)
+    if key_mask is not None:
+        add = add.masked_fill(~key_mask.bool()[:, None, None, :], -1e9)
+    if causal:
+        add = add.masked_fill(torch.ones(Tq, Tk, dtype=torch.bool, device=s.device).triu(1), -1e9)
+    return torch.softmax(s + add, -1) @ v
+
+
+def _mask(B, Tk, dev):
+    m = torch.ones(B, Tk, dtype=torch.bool, device=dev)
+    for b in range(B):
+        m[b, Tk - (b % 5):] = False
+    return m
+
+
+@pytest.mark.parametrize("B,H,T,D", [(4, 12, 128, 64), (3, 8, 20, 32), (2, 4, 77, 128), (16, 8, 20, 256),
+                                     (2, 2, 200, 64), (2, 2, 70, 256)])
+@pytest.mark.parametrize("causal", [False, True])
+@pytest.mark.parametrize("masked", [False, True])
+def test_f32_qkvpacked_fwd_bwd_vs_fp64(B, H, T, D, causal, masked):
+    _native.hip()
+    torch.manual_seed(0)
+    qkv = torch.randn(B, T, 3, H, D, device="cuda", requires_grad=True)
+    km = _mask(B, T, "cuda") if masked else None
+    scale = D ** -0.5
+    assert flash.supported(D, T, T, torch.float32)
+    o = attention_qkvpacked(qkv, km, causal, scale)
+    assert o.dtype == torch.float32 and type(o.grad_fn).__name__.startswith("_AttnFn")
+    x = qkv.detach().double().requires_grad_()
+    q, k, v = (x[:, :, i].transpose(1, 2) for i in range(3))
+    ref = ref_attn(q, k, v, km, causal, scale).transpose(1, 2)
+    torch.testing.assert_close(o.double(), ref, **TOL)
+    do = torch.randn_like(ref)
+    o.backward(do.float())
+    ref.backward(do)
+    torch.testing.assert_close(qkv.grad.double(), x.grad, **TOL)
+
+
+@pytest.mark.parametrize("Tq,Tk,D", [(20, 20, 64), (17, 45, 32), (64, 128, 128), (20, 20, 256), (300, 129, 64)])
+@pytest.mark.parametrize("causal", [False, True])
+def test_f32_cross_attention_vs_fp64(Tq, Tk, D, causal):
+    _native.hip()
+    torch.manual_seed(1)
+    B, H = 3, 4
+    q = torch.randn(B, Tq, H, D, device="cuda", requires_grad=True)
+    kv = torch.randn(B, Tk, 2, H, D, device="cuda", requires_grad=True)
+    km = _mask(B, Tk, "cuda")
+    o = attention_q_kvpacked(q, kv, km, causal, D ** -0.5)
+    qd, kvd = q.detach().double().requires_grad_(), kv.detach().double().requires_grad_()
+    ref = ref_attn(qd.transpose(1, 2), kvd[:, :, 0].transpose(1, 2), kvd[:, :, 1].transpose(1, 2), km, causal,
+                   D ** -0.5).transpose(1, 2)
+    torch.testing.assert_close(o.double(), ref, **TOL)
+    do = torch.randn_like(ref)
+    o.backward(do.float())
+    ref.backward(do)
+    torch.testing.assert_close(q.grad.double(), qd.grad, **TOL)
+    torch.testing.assert_close(kv.grad.double(), kvd.grad, **TOL)
+
+
+def test_f32_attention_writes_every_element(monkeypatch):
+    """NaN-filled outputs: every element the fp32 kernels own must be written (fresh memory
+    is often zero and would hide a gap)."""
+
+    class NanTorch:
+        def __getattr__(self, k):
+            return getattr(torch, k)
+
+        @staticmethod
+        def empty(*a, **kw):
+            return torch.full_like(torch.empty(*a, **kw), float("nan"))
+
+        @staticmethod
+        def empty_like(t, **kw):
+            return torch.full_like(t, float("nan"), **kw)
+
+    monkeypatch.setattr(flash, "torch", NanTorch())
+    torch.manual_seed(3)
+    for B, Tq, Tk, H, D in [(16, 20, 20, 8, 256), (4, 77, 45, 4, 64), (2, 130, 200, 2, 128)]:
+        q = torch.randn(B, Tq, H, D, device="cuda", requires_grad=True)
+        kv = torch.randn(B, Tk, 2, H, D, device="cuda", requires_grad=True)
+        o = attention_q_kvpacked(q, kv, _mask(B, Tk, "cuda"), False, D ** -0.5)
+        assert torch.isfinite(o).all()
+        o.backward(torch.randn_like(o))
+        assert torch.isfinite(q.grad).all() and torch.isfinite(kv.grad).all()
+
+
+def test_bert_fp32_layer_runs_fp32_kernel(monkeypatch):
+    """An fp32 BERT step (no autocast, as the reference trains) goes through the fp32 HIP
+    kernels, not the materialised PyTorch fallback."""
+    from vodascheduler_amd.models.transformer import BertBase
+
+    h = _native.hip()
+    calls = {"fwd": 0, "bwd": 0}
+
+    class Spy:
+        def __getattr__(self, k):
+            f = getattr(h, k)
+            if k == "attention_fwd_f32":
+                def g(*a):
+                    calls["fwd"] += 1
+                    return f(*a)
+                return g
+            if k == "attention_bwd_f32":
+                def g2(*a):
+                    calls["bwd"] += 1
+                    return f(*a)
+                return g2
+            return f
+
+    monkeypatch.setattr(flash.N, "hip", lambda: Spy())
+    torch.manual_seed(0)
+    m = BertBase(vocab=1000, seq_len=64, layers=2).cuda()
+    ids = torch.randint(1, 1000, (4, 64), device="cuda")
+    loss = m(ids, torch.ones_like(ids, dtype=torch.bool)).float().pow(2).mean()
+    loss.backward()
+    assert calls["fwd"] == 2 and calls["bwd"] == 2, calls
+    assert all(p.grad is None or torch.isfinite(p.grad).all() for p in m.parameters())

@@ -18,9 +18,6 @@ from torch import nn
 
 from ..ops.activation import GeluTanh
 from ..ops.attention import attention_q_kvpacked, attention_qkvpacked
-from ..ops import ffn as _ffn
-from ..ops.ffn import ffn_gelu
-from ..ops.ffn import supported as ffn_supported
 from ..ops.conv1x1 import USE_GRAD_SINK, GradSink
 from ..ops.dense import FusedLinear, residual_add
 from ..ops.layernorm import FusedLayerNorm
@@ -89,15 +86,8 @@ class FeedForward(nn.Module):
             self.act = nn.ReLU()
 
     def forward(self, x, sink_in=None):
-        if isinstance(self.act, GeluTanh) and x.is_cuda:
-            if x.dtype != self.fc1.weight.dtype and torch.is_autocast_enabled("cuda"):
-                x = x.to(self.fc1.weight.dtype)
-            if ffn_supported(x, self.fc1.weight, self.fc1.bias, self.fc2.weight, self.fc2.bias):
-                # GELU in the GEMM epilogues (ops/ffn.py): no separate GELU kernels
-                try:
-                    return ffn_gelu(x, self.fc1.weight, self.fc1.bias, self.fc2.weight, self.fc2.bias, sink_in)
-                except (RuntimeError, ValueError) as e:  # hipBLASLt has no epilogue kernel for it
-                    _ffn.disable_epilogue(repr(e))
+        # GELU runs as the HIP activation kernels between the two GEMMs: hipBLASLt on gfx950
+        # has no GELU_AUX / DGELU epilogue kernels (probe: profiles/raw/r2_blaslt_epilogue_probe.jsonl)
         return self.fc2(self.act(self.fc1(x, sink_in)))
 
 

@@ -1,7 +1,9 @@
 """Fused MFMA attention (csrc/hip/attention.hip): forward, dQ pass and dK/dV pass.
 
-Entry points (all bf16, head dim 32/64/128/256, Tq, Tk <= 4096; the streamed operand goes
-through LDS in 32-row tiles, so long sequences -- BERT at 512 -- stay on the fused path):
+Entry points (bf16 on v_mfma_f32_32x32x16_bf16, or fp32 -- the reference's precision -- on
+v_mfma_f32_32x32x2_f32, csrc/hip/attention_f32.hip; head dim 32/64/128/256, Tq, Tk <= 4096;
+the streamed operand goes through LDS in 32-row tiles, so long sequences -- BERT at 512 --
+stay on the fused path):
 
 * ``attention_qkvpacked(qkv)`` -- self-attention straight from the packed projection
   ``qkv`` [B, T, 3, H, D] (one fused QKV GEMM); the gradient is written into ONE
@@ -26,14 +28,17 @@ MAX_T = 4096
 HEAD_DIMS = tuple(d for d in (32, 64, 128, 256) if d <= int(os.environ.get("VODA_FLASH_MAX_D", "256")))
 
 
+DTYPES = {torch.bfloat16: "DT_BF16", torch.float32: "DT_F32"}
+
+
 def supported(D: int, Tq: int, Tk: int, dtype: torch.dtype, device_is_cuda: bool = True) -> bool:
-    if not device_is_cuda or dtype != torch.bfloat16 or D not in HEAD_DIMS or Tq > MAX_T or Tk > MAX_T:
+    if not device_is_cuda or dtype not in DTYPES or D not in HEAD_DIMS or Tq > MAX_T or Tk > MAX_T:
         return False
     try:
         h = N.hip()
     except RuntimeError:
         return False
-    return bool(h.attention_supported(D, Tq, Tk, N.DT_BF16))
+    return bool(h.attention_supported(D, Tq, Tk, getattr(N, DTYPES[dtype])))
 
 
 def _d(t: torch.Tensor | None, b: int, h: int, r: int) -> list[int]:
@@ -68,13 +73,21 @@ def _launch(fwd: bool, q, k, v, o, dout, out, dk, dv, lse, delta, mptr, msb, B, 
          + _d(out, 0, 2, 1) + _d(dk, 0, 2, 1) + _d(dv, 0, 2, 1)
          + [N.ptr(lse), N.ptr(delta), mptr, msb])
     h = N.hip()
-    (h.attention_fwd if fwd else h.attention_bwd)(t, B, H, Tq, Tk, D, float(scale), bool(causal), stream)
+    if q.dtype == torch.float32:
+        fn = h.attention_fwd_f32 if fwd else h.attention_bwd_f32
+    else:
+        fn = h.attention_fwd if fwd else h.attention_bwd
+    fn(t, B, H, Tq, Tk, D, float(scale), bool(causal), stream)
 
 
 def _check(*ts):
+    dt = ts[0].dtype
     for x in ts:
-        if x.stride(-1) != 1 or x.data_ptr() % 16 != 0 or not x.is_cuda:
-            raise ValueError("attention operands must be 16-byte aligned CUDA tensors with a contiguous last dim")
+        if x.stride(-1) != 1 or x.data_ptr() % 16 != 0 or not x.is_cuda or x.dtype != dt:
+            raise ValueError("attention operands must be 16-byte aligned CUDA tensors of one dtype with a "
+                             "contiguous last dim")
+        if dt == torch.float32 and any(st % 4 for st in x.stride()[:-1]):
+            raise ValueError("fp32 attention operands need row strides that are multiples of 4 elements")
 
 
 class _AttnFn(torch.autograd.Function):
@@ -115,7 +128,10 @@ class _AttnFn(torch.autograd.Function):
             dq = torch.empty_like(q_src)
             dkv = torch.empty_like(kv_src)
             dk, dv = _slices5(dkv, 2)
-        if dout.stride(-1) != 1 or dout.data_ptr() % 16 != 0:
+        if dout.dtype != q.dtype:
+            dout = dout.to(q.dtype)
+        if (dout.stride(-1) != 1 or dout.data_ptr() % 16 != 0
+                or (dout.dtype == torch.float32 and any(st % 4 for st in dout.stride()[:-1]))):
             dout = dout.contiguous()
         B, Tq, H, D = q.shape
         Tk = k.shape[1]
