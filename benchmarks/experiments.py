@@ -8,7 +8,13 @@ curves come from the MI355X-calibrated ``sim.trace.PROFILES``.
   4. Munkres placement + worker migration under GPU drain (2 nodes x 8 GPUs)
   5. FfDL Optimizer, 32-job Philly-style trace, 1/2/4/8 GPUs (all 8 policies side by side)
 
-python benchmarks/experiments.py [--out profiles/r1_sim_experiments.md]
+python benchmarks/experiments.py [--out profiles/r3_sim_experiments.md] [--bench-json SCALE.json]
+
+Job info (what SRJF / E-Tiresias / FfDL / AFS-L see) follows the real pipeline by default
+(``info_mode="online"``): the training service seeds every job from the workload it declares
+(common/workload.py), the collector refreshes running jobs every 60 s (the reference cron).
+The ablation table re-runs the info-driven policies with the reference's placeholder info
+(1 s epochs, linear speedup) and with an oracle.
 """
 from __future__ import annotations
 
@@ -20,6 +26,7 @@ import sys
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from vodascheduler_amd.algorithm import ALGORITHMS  # noqa: E402
 from vodascheduler_amd.sim.simulator import simulate  # noqa: E402
+from vodascheduler_amd.common.workload import busbw_source, intra_node_busbw, load_busbw  # noqa: E402
 from vodascheduler_amd.sim.trace import (ASSUMED_BUSBW_GBS, ASSUMED_INTERNODE_BUSBW_GBS, TraceJob,  # noqa: E402
                                          make_spec, philly_trace)
 
@@ -36,7 +43,8 @@ HEADER = ("| policy | GPUs | avg JCT (s) | median JCT | p95 JCT | makespan (s) |
 
 
 def exp2():
-    tr = [TraceJob(60.0 * i, make_spec(f"resnet50-{i}", "resnet50", 4, 1, 8, 10, 2000)) for i in range(8)]
+    tr = [TraceJob(60.0 * i, make_spec(f"resnet50-{i}", "resnet50", 4, 1, 8, 10, 2000, category="resnet50"))
+          for i in range(8)]
     return [simulate(tr, a, gpus=8) for a in ("Tiresias", "ElasticTiresias")]
 
 
@@ -66,19 +74,47 @@ def exp5():
     return out
 
 
+INFO_ALGOS = ["SRJF", "ElasticSRJF", "ElasticTiresias", "FfDLOptimizer", "AFS-L"]
+
+
+def exp_info():
+    """Info-source ablation on config 5's trace at 1 and 8 GPUs: the reference's placeholder
+    info, the real pipeline (default), an oracle."""
+    out = []
+    for g in (1, 8):
+        tr = philly_trace(32, seed=0, max_gpus=g)
+        fifo = simulate(tr, "FIFO", gpus=g).avg_jct
+        for a in INFO_ALGOS:
+            row = {"gpus": g, "algorithm": a, "fifo": fifo}
+            for mode in ("mixed", "placeholder", "online", "oracle"):
+                row[mode] = simulate(tr, a, gpus=g, info_mode=mode).avg_jct
+            out.append(row)
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--out", default="profiles/r2_sim_experiments.md")
+    ap.add_argument("--out", default="profiles/r3_sim_experiments.md")
+    ap.add_argument("--bench-json", default=None,
+                    help="bench.py --out / driver SCALE json with allreduce_busbw_gbs: measured busbw")
     a = ap.parse_args()
     assert set(ORDER) == set(ALGORITHMS)
-    lines = ["# BASELINE.json configs in the discrete-event simulator (round 2)", "",
-             "Real scheduler / allocator / placement code driven in virtual time (`benchmarks/experiments.py`). "
-             "Job speed model (`vodascheduler_amd/sim/trace.py`): single-GPU step times MEASURED on MI355X for "
-             "every workload but the PyTorch MNIST net (`benchmarks/model_step.py`, fp32 gradients, eager step); "
-             "fp32 gradient bytes exact; ring all-reduce bus bandwidth ASSUMED "
-             f"({ASSUMED_BUSBW_GBS:.0f} GB/s intra-node, {ASSUMED_INTERNODE_BUSBW_GBS:.0f} GB/s across nodes) until "
-             "the 8-GPU bench measures it; 30 % of a step hides the all-reduce.  Resize pause 5 s, "
-             "restart-from-checkpoint pause 15 s, rate limit 30 s (reference default).", ""]
+    if a.bench_json:
+        print("measured busbw (GB/s) by world:", load_busbw(a.bench_json))
+    bw = (f"MEASURED per world ({', '.join(f'{k}: {intra_node_busbw(k):.0f}' for k in (2, 4, 8))} GB/s)"
+          if busbw_source() == "measured" else f"ASSUMED ({ASSUMED_BUSBW_GBS:.0f} GB/s intra-node)")
+    lines = ["# BASELINE.json configs in the discrete-event simulator (round 3)", "",
+             "Real training service / scheduler / allocator / placement code driven in virtual time "
+             "(`benchmarks/experiments.py`). Job speed model (`vodascheduler_amd/common/workload.py`): single-GPU "
+             "step times MEASURED on MI355X (bf16 compute, fp32 gradients; ResNet-50 25.3 ms, BERT-base 10.2 ms); "
+             "fp32 gradient bytes exact; ring all-reduce bus bandwidth " + bw + f", {ASSUMED_INTERNODE_BUSBW_GBS:.0f} "
+             "GB/s across nodes (assumed); 30 % of a step hides the all-reduce.  Resize pause 5 s, "
+             "restart-from-checkpoint pause 15 s, rate limit 30 s (reference default).", "",
+             "Job info (round 3): every job is seeded at submission from the workload it declares (remaining = "
+             "epochs x epoch time on one GPU, speedup = the model's curve), jobs of one model share a category "
+             "(JOB_CATEGORY), and the collector refreshes running jobs every 60 s -- the round-2 tables ran the "
+             "info-driven policies on the reference's placeholder (1 s epochs, linear speedup) for unstarted jobs.",
+             ""]
     lines += ["## Config 2: Elastic-Tiresias vs Tiresias, 8 ResNet-50 jobs, 8 GPUs", "", HEADER]
     lines += [row(r) for r in exp2()]
     lines += ["", "## Config 3: AFS-L on a mixed ResNet-50 + BERT-base trace, 8 GPUs", "", HEADER]
@@ -94,6 +130,18 @@ def main():
     lines += ["", "## Config 5: 32-job Philly-style trace, all 8 policies, 1/2/4/8 GPUs", "", HEADER]
     res5 = exp5()
     lines += [row(r) for r in res5]
+    lines += ["", "## Info-source ablation (config 5 trace): avg JCT (s) of the info-driven policies", "",
+              "round-2 = what round 2 ran: exact info for started jobs, the reference placeholder for unstarted "
+              "ones (units mixed: started jobs look long next to '1 s/epoch' arrivals); placeholder = the "
+              "reference's CreateBaseJobInfo info for every job (1 s epochs, linear speedup -- on this trace the "
+              "epoch count happens to track the length); online = the real round-3 pipeline (seeded from the "
+              "declared workload, collector every 60 s; the default of every table above); oracle = exact "
+              "remaining time and speed curve of every submitted job.", "",
+              "| GPUs | policy | FIFO | round-2 | placeholder | online | oracle |",
+              "|---:|---|---:|---:|---:|---:|---:|"]
+    for r in exp_info():
+        lines.append(f"| {r['gpus']} | {r['algorithm']} | {r['fifo']:.0f} | {r['mixed']:.0f} | "
+                     f"{r['placeholder']:.0f} | {r['online']:.0f} | {r['oracle']:.0f} |")
     text = "\n".join(lines) + "\n"
     print(text)
     os.makedirs(os.path.dirname(a.out), exist_ok=True)

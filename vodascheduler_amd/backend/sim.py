@@ -13,7 +13,10 @@ Info modes (what the info-driven policies see):
   unstarted job keeps the estimate the training service seeded at submission;
 * ``prior`` -- only the submission-time estimates (no collector);
 * ``placeholder`` -- the reference as written: no collector, and the service seeds nothing
-  (1 s epochs, linear speedup; use with ``TrainingService(seed_from_workload=False)``).
+  (1 s epochs, linear speedup; use with ``TrainingService(seed_from_workload=False)``);
+* ``mixed`` -- round 2's simulator: exact info for jobs that have started, the placeholder
+  for the rest (the two are in different units, so shortest-first policies keep preempting
+  long running jobs for "1 s/epoch" arrivals -- VERDICT r2 Weak #1's reproduction).
 """
 from __future__ import annotations
 
@@ -58,7 +61,7 @@ class SimBackend(Backend):
                  resize_overhead_s: float = 5.0, restart_overhead_s: float = 15.0, info_mode: str = "oracle",
                  collector_period_s: float = 60.0):
         super().__init__()
-        if info_mode not in ("oracle", "online", "prior", "placeholder"):
+        if info_mode not in ("oracle", "online", "prior", "placeholder", "mixed"):
             raise ValueError(f"unknown info mode {info_mode!r}")
         self.collector_period_s = collector_period_s
         self._last_collect = -1e18
@@ -163,6 +166,8 @@ class SimBackend(Backend):
     def _maybe_publish(self, now: float) -> None:
         if self.info_mode == "oracle":
             self.publish_info()
+        elif self.info_mode == "mixed":
+            self.publish_info([n for n, j in self.jobs.items() if j.total_work - j.work > 0 or j.n > 0])
         elif self.info_mode == "online" and now - self._last_collect >= self.collector_period_s:
             self._last_collect = now
             self.publish_info([n for n, j in self.jobs.items() if j.total_work - j.work > 0 or j.n > 0])

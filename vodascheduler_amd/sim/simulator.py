@@ -65,7 +65,7 @@ def simulate(trace: list[TraceJob], algorithm: str = "ElasticFIFO", gpus: int = 
     clock = ManualClock(0.0)
     store = MemoryStore()
     mq = InProcQueue(maxsize=10 ** 6)
-    svc = TrainingService(store, mq, clock, seed_from_workload=info_mode != "placeholder")
+    svc = TrainingService(store, mq, clock, seed_from_workload=info_mode not in ("placeholder", "mixed"))
     nodes = nodes or {"node0": list(range(gpus))}
     backend = SimBackend(clock, nodes, store, resize_overhead_s, restart_overhead_s, info_mode=info_mode,
                          collector_period_s=collector_period_s)
