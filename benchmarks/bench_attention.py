@@ -24,14 +24,21 @@ def main():
     ap.add_argument("--T", type=int, default=128)
     ap.add_argument("--D", type=int, default=64)
     ap.add_argument("--iters", type=int, default=20)
+    ap.add_argument("--fwd-only", action="store_true")
+    ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
     a = ap.parse_args()
     _native.hip()
     dev = "cuda"
-    qkv = torch.randn(a.B, a.T, 3, a.H, a.D, device=dev).to(torch.bfloat16).requires_grad_()
+    dt = torch.bfloat16 if a.dtype == "bf16" else torch.float32
+    qkv = torch.randn(a.B, a.T, 3, a.H, a.D, device=dev).to(dt).requires_grad_()
     km = torch.ones(a.B, a.T, dtype=torch.bool, device=dev)
-    do = torch.randn(a.B, a.T, a.H, a.D, device=dev).to(torch.bfloat16)
+    do = torch.randn(a.B, a.T, a.H, a.D, device=dev).to(dt)
 
     def step():
+        if a.fwd_only:
+            with torch.no_grad():
+                attention_qkvpacked(qkv, km, False)
+            return
         o = attention_qkvpacked(qkv, km, False)
         o.backward(do)
 
@@ -45,9 +52,10 @@ def main():
     e1.record()
     torch.cuda.synchronize()
     us = e0.elapsed_time(e1) / a.iters * 1e3
-    flops = 4 * a.B * a.H * a.T * a.T * a.D * 3.5  # fwd 2 GEMMs + bwd 5 GEMMs
-    print(json.dumps({"B": a.B, "H": a.H, "T": a.T, "D": a.D, "fwd_bwd_us": round(us, 1),
-                      "tflops": round(flops / (us * 1e-6) / 1e12, 1)}))
+    flops = 4 * a.B * a.H * a.T * a.T * a.D * (1.0 if a.fwd_only else 3.5)  # fwd 2 GEMMs + bwd 5 GEMMs
+    print(json.dumps({"B": a.B, "H": a.H, "T": a.T, "D": a.D, "dtype": a.dtype, "fwd_only": a.fwd_only,
+                      "env_resident": os.environ.get("VODA_ATTN_RESIDENT", "1"),
+                      "us": round(us, 1), "tflops": round(flops / (us * 1e-6) / 1e12, 1)}))
 
 
 if __name__ == "__main__":
