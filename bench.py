@@ -93,6 +93,7 @@ import torch.distributed as dist  # noqa: E402
 
 sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 
+from vodascheduler_amd.common.workload import busbw_source, set_measured_busbw  # noqa: E402
 from vodascheduler_amd.ops import _native  # noqa: E402
 from vodascheduler_amd.parallel.comm import RcclCommunicator  # noqa: E402
 from vodascheduler_amd.runtime.cluster import free_port, run_trace  # noqa: E402
@@ -341,6 +342,9 @@ def main():
             dog.phase = "allreduce-busbw"
             bw = measure_busbw(store, rank, world, device)
             log(rank, f"RCCL all-reduce busbw (GB/s) by world: {bw['by_world']}; init s: {bw['init_s']}")
+            # the control plane (rank 0) prices all-reduces with what was just measured: job-info
+            # priors (common/workload.prior_fields) use the 64 MB (bucket-size) busbw per world
+            set_measured_busbw({int(k): v.get("64") for k, v in bw["by_world"].items()})
         dist.barrier()
     log(rank, f"warm-up single-GPU step ms: {step_ms}")
 
@@ -507,6 +511,7 @@ def main():
             "forced_abort_epochs": result.get("forced_abort_epochs", 0),
             "allreduce_busbw_gbs": bw["by_world"].get(str(world)),
             "allreduce_busbw_by_world": bw["by_world"],
+            "busbw_source_for_priors": busbw_source(),
             "rccl_init_s": bw["init_s"],
             "step_ms_by_world": per_world_step_ms(allrec),
             "gpu_ms_per_train_step": round(tot_train / max(tot_steps, 1) * 1e3, 3),
