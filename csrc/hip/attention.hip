@@ -325,101 +325,6 @@ __global__ __launch_bounds__(64 * W) void attn_fwd_kernel(AttnArgs a) {
   if (h == 0 && q < a.Tq) a.lse[int64_t(bh) * a.Tq + q] = m + __logf(l);
 }
 
-// ======================================================================== forward, K/V resident
-// Short key sequences (Tk <= kResT, e.g. BERT at 128): every K tile and V^T tile is loaded
-// up front -- all global loads in flight at once, ONE barrier -- and the tiles are then
-// consumed from LDS with no barrier between them.  The streaming kernel above pays a
-// load -> LDS -> barrier round trip (and a second barrier) per 32-key tile.  Same math,
-// same accumulation order as attn_fwd_kernel.
-constexpr int kResT = 128;
-
-template <int D, int W>
-__global__ __launch_bounds__(64 * W) void attn_fwd_res_kernel(AttnArgs a) {
-  constexpr int KS = D / 16, DT = D / 32, RS = D + 8, TS = kTile + 8, NT = kResT / kTile;
-  __shared__ __attribute__((aligned(16))) uint16_t Ks[NT * kTile * RS];
-  __shared__ __attribute__((aligned(16))) uint16_t Vt[NT * D * TS];
-  __shared__ __attribute__((aligned(16))) uint8_t Ms[kResT];
-
-  const int bh = blockIdx.y, b = bh / a.H, hh = bh % a.H;
-  const uint16_t* kb = a.k + b * a.k_sb + hh * a.k_sh;
-  const uint16_t* vb = a.v + b * a.v_sb + hh * a.v_sh;
-  const int lane = threadIdx.x & 63, r = lane & 31, h = lane >> 5, w = threadIdx.x >> 6;
-  const int q = blockIdx.x * (32 * W) + w * 32 + r;
-  const int nt = (a.Tk + kTile - 1) / kTile;
-  using Regs = TileRegs<D, 64 * W>;
-  Regs kr[NT], vr[NT];
-#pragma unroll
-  for (int ti = 0; ti < NT; ++ti)
-    if (ti < nt) {
-      kr[ti].load(kb, a.k_st, ti * kTile, a.Tk);
-      vr[ti].load(vb, a.v_st, ti * kTile, a.Tk);
-    }
-  const uint16_t* qrow = a.q + b * a.q_sb + hh * a.q_sh + int64_t(q) * a.q_st;
-  bf16x8 qf[KS];
-#pragma unroll
-  for (int s = 0; s < KS; ++s) qf[s] = q < a.Tq ? ld16(qrow + 16 * s + 8 * h) : zero_bf8();
-  const uint8_t* mrow = a.mask != nullptr ? a.mask + b * a.mask_sb : nullptr;
-#pragma unroll
-  for (int ti = 0; ti < NT; ++ti)
-    if (ti < nt) {
-      kr[ti].template store<true, false>(Ks + ti * kTile * RS, RS, nullptr, 0);
-      vr[ti].template store<false, true>(nullptr, 0, Vt + ti * D * TS, TS);
-      stage_mask(a, mrow, ti * kTile, Ms + ti * kTile);
-    }
-  __syncthreads();
-
-  f32x16 o[DT];
-#pragma unroll
-  for (int t = 0; t < DT; ++t) o[t] = zero16();
-  float m = -1e30f, l = 0.f;
-  for (int ti = 0; ti < nt; ++ti) {
-    const int kt = ti * kTile;
-    const uint16_t* K_ = Ks + ti * kTile * RS;
-    const uint16_t* V_ = Vt + ti * D * TS;
-    uint32_t mw[4];
-    load_mask_words(Ms + kt, h, mw);
-    f32x16 s_acc = zero16();
-#pragma unroll
-    for (int s = 0; s < KS; ++s) s_acc = mfma(ld16(K_ + r * RS + 16 * s + 8 * h), qf[s], s_acc);
-    float tmax = -1e30f;
-#pragma unroll
-    for (int i = 0; i < 16; ++i) {
-      const float v = s_acc[i] * a.scale + mask_code_add(a, mw, i, kt + crow(i, h), q);
-      s_acc[i] = v;
-      tmax = fmaxf(tmax, v);
-    }
-    tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64));
-    const float mn = fmaxf(m, tmax);
-    const float alpha = __expf(m - mn);
-    float psum = 0.f;
-#pragma unroll
-    for (int i = 0; i < 16; ++i) {
-      const float p = __expf(s_acc[i] - mn);
-      s_acc[i] = p;
-      psum += p;
-    }
-    psum += __shfl_xor(psum, 32, 64);
-    l = l * alpha + psum;
-    m = mn;
-#pragma unroll
-    for (int t = 0; t < DT; ++t)
-#pragma unroll
-      for (int i = 0; i < 16; ++i) o[t][i] *= alpha;
-    const bf16x8 p0 = acc_frag(s_acc, 0), p1 = acc_frag(s_acc, 1);
-#pragma unroll
-    for (int t = 0; t < DT; ++t) {
-      const uint16_t* vrow = V_ + (32 * t + r) * TS;
-      o[t] = mfma(perm_frag(vrow, 0, h, trans_rot(r)), p0, o[t]);
-      o[t] = mfma(perm_frag(vrow, 1, h, trans_rot(r)), p1, o[t]);
-    }
-  }
-  const float inv = 1.f / l;
-  uint16_t* obase = a.out + b * a.out_sb + hh * a.out_sh;
-#pragma unroll
-  for (int t = 0; t < DT; ++t) store_lane_rows(obase, a.out_st, q, a.Tq, 32 * t, o[t], inv, h);
-  if (h == 0 && q < a.Tq) a.lse[int64_t(bh) * a.Tq + q] = m + __logf(l);
-}
-
 // ======================================================================== backward: dQ (+ delta)
 template <int D, int W>
 __global__ __launch_bounds__(64 * W) void attn_bwd_dq_kernel(AttnArgs a) {
@@ -512,90 +417,6 @@ __global__ __launch_bounds__(64 * W) void attn_bwd_dq_kernel(AttnArgs a) {
 #pragma unroll
     for (int t = 0; t < DT; ++t) {
       const uint16_t* krow = Kt + (32 * t + r) * TS;
-      dq[t] = mfma(perm_frag(krow, 0, h, trans_rot(r)), d0, dq[t]);
-      dq[t] = mfma(perm_frag(krow, 1, h, trans_rot(r)), d1, dq[t]);
-    }
-  }
-  uint16_t* base = a.out + b * a.out_sb + hh * a.out_sh;
-#pragma unroll
-  for (int t = 0; t < DT; ++t) store_lane_rows(base, a.out_st, q, a.Tq, 32 * t, dq[t], a.scale, h);
-}
-
-// dQ pass with every K / V tile resident (Tk <= kResT; see attn_fwd_res_kernel)
-template <int D, int W>
-__global__ __launch_bounds__(64 * W) void attn_bwd_dq_res_kernel(AttnArgs a) {
-  constexpr int KS = D / 16, DT = D / 32, RS = D + 8, TS = kTile + 8, NT = kResT / kTile;
-  __shared__ __attribute__((aligned(16))) uint16_t Ks[NT * kTile * RS];
-  __shared__ __attribute__((aligned(16))) uint16_t Vs[NT * kTile * RS];
-  __shared__ __attribute__((aligned(16))) uint16_t Kt[NT * D * TS];
-  __shared__ __attribute__((aligned(16))) uint8_t Ms[kResT];
-
-  const int bh = blockIdx.y, b = bh / a.H, hh = bh % a.H;
-  const uint16_t* kb = a.k + b * a.k_sb + hh * a.k_sh;
-  const uint16_t* vb = a.v + b * a.v_sb + hh * a.v_sh;
-  const int lane = threadIdx.x & 63, r = lane & 31, h = lane >> 5, w = threadIdx.x >> 6;
-  const int q = blockIdx.x * (32 * W) + w * 32 + r;
-  const bool qv = q < a.Tq;
-  const int nt = (a.Tk + kTile - 1) / kTile;
-  using Regs = TileRegs<D, 64 * W>;
-  Regs kr[NT], vr[NT];
-#pragma unroll
-  for (int ti = 0; ti < NT; ++ti)
-    if (ti < nt) {
-      kr[ti].load(kb, a.k_st, ti * kTile, a.Tk);
-      vr[ti].load(vb, a.v_st, ti * kTile, a.Tk);
-    }
-  const uint16_t* qrow = a.q + b * a.q_sb + hh * a.q_sh + int64_t(q) * a.q_st;
-  const uint16_t* dorow = a.dout + b * a.do_sb + hh * a.do_sh + int64_t(q) * a.do_st;
-  const uint16_t* orow = a.o + b * a.o_sb + hh * a.o_sh + int64_t(q) * a.o_st;
-  bf16x8 qf[KS], dof[KS];
-  float dpart = 0.f;
-#pragma unroll
-  for (int s = 0; s < KS; ++s) {
-    qf[s] = qv ? ld16(qrow + 16 * s + 8 * h) : zero_bf8();
-    dof[s] = qv ? ld16(dorow + 16 * s + 8 * h) : zero_bf8();
-    const bf16x8 of = qv ? ld16(orow + 16 * s + 8 * h) : zero_bf8();
-#pragma unroll
-    for (int j = 0; j < 8; ++j) dpart += float(dof[s][j]) * float(of[j]);
-  }
-  const float delta = dpart + __shfl_xor(dpart, 32, 64);
-  const float lse = qv ? a.lse[int64_t(bh) * a.Tq + q] : 0.f;
-  if (h == 0 && qv) a.delta[int64_t(bh) * a.Tq + q] = delta;
-  const uint8_t* mrow = a.mask != nullptr ? a.mask + b * a.mask_sb : nullptr;
-#pragma unroll
-  for (int ti = 0; ti < NT; ++ti)
-    if (ti < nt) {
-      kr[ti].template store<true, true>(Ks + ti * kTile * RS, RS, Kt + ti * D * TS, TS);
-      vr[ti].template store<true, false>(Vs + ti * kTile * RS, RS, nullptr, 0);
-      stage_mask(a, mrow, ti * kTile, Ms + ti * kTile);
-    }
-  __syncthreads();
-
-  f32x16 dq[DT];
-#pragma unroll
-  for (int t = 0; t < DT; ++t) dq[t] = zero16();
-  for (int ti = 0; ti < nt; ++ti) {
-    const int kt = ti * kTile;
-    const uint16_t* K_ = Ks + ti * kTile * RS;
-    const uint16_t* V_ = Vs + ti * kTile * RS;
-    const uint16_t* KT_ = Kt + ti * D * TS;
-    uint32_t mw[4];
-    load_mask_words(Ms + kt, h, mw);
-    f32x16 s_acc = zero16(), dp = zero16();
-#pragma unroll
-    for (int s = 0; s < KS; ++s) {
-      s_acc = mfma(ld16(K_ + r * RS + 16 * s + 8 * h), qf[s], s_acc);
-      dp = mfma(ld16(V_ + r * RS + 16 * s + 8 * h), dof[s], dp);
-    }
-#pragma unroll
-    for (int i = 0; i < 16; ++i) {
-      const float p = qv ? __expf(s_acc[i] * a.scale + mask_code_add(a, mw, i, kt + crow(i, h), q) - lse) : 0.f;
-      s_acc[i] = p * (dp[i] - delta);  // dS^T
-    }
-    const bf16x8 d0 = acc_frag(s_acc, 0), d1 = acc_frag(s_acc, 1);
-#pragma unroll
-    for (int t = 0; t < DT; ++t) {
-      const uint16_t* krow = KT_ + (32 * t + r) * TS;
       dq[t] = mfma(perm_frag(krow, 0, h, trans_rot(r)), d0, dq[t]);
       dq[t] = mfma(perm_frag(krow, 1, h, trans_rot(r)), d1, dq[t]);
     }
@@ -755,106 +576,6 @@ __global__ __launch_bounds__(64 * W) void attn_bwd_dkv_kernel(AttnArgs a) {
     }
 }
 
-// dK/dV pass with every Q / dO tile resident (Tq <= kResT; see attn_fwd_res_kernel)
-template <int D, int W>
-__global__ __launch_bounds__(64 * W) void attn_bwd_dkv_res_kernel(AttnArgs a) {
-  constexpr int KS = D / 16, DT = D / 32, RS = D + 8, TS = kTile + 8, NT = kResT / kTile;
-  __shared__ __attribute__((aligned(16))) uint16_t Qs[NT * kTile * RS];
-  __shared__ __attribute__((aligned(16))) uint16_t Ds[NT * kTile * RS];
-  __shared__ __attribute__((aligned(16))) uint16_t Qt[NT * D * TS];
-  __shared__ __attribute__((aligned(16))) uint16_t Dt[NT * D * TS];
-  __shared__ float lse_s[kResT], del_s[kResT];
-
-  const int bh = blockIdx.y, b = bh / a.H, hh = bh % a.H;
-  const uint16_t* qb = a.q + b * a.q_sb + hh * a.q_sh;
-  const uint16_t* db = a.dout + b * a.do_sb + hh * a.do_sh;
-  const int lane = threadIdx.x & 63, r = lane & 31, h = lane >> 5, w = threadIdx.x >> 6;
-  const int key = blockIdx.x * (32 * W) + w * 32 + r;
-  const bool kv = key < a.Tk;
-  const int nt = (a.Tq + kTile - 1) / kTile;
-  using Regs = TileRegs<D, 64 * W>;
-  Regs qr[NT], dr[NT];
-#pragma unroll
-  for (int ti = 0; ti < NT; ++ti)
-    if (ti < nt) {
-      qr[ti].load(qb, a.q_st, ti * kTile, a.Tq);
-      dr[ti].load(db, a.do_st, ti * kTile, a.Tq);
-    }
-  for (int i = threadIdx.x; i < kResT; i += blockDim.x) {
-    const bool ok = i < a.Tq;
-    lse_s[i] = ok ? a.lse[int64_t(bh) * a.Tq + i] : __builtin_huge_valf();  // pad rows: P = 0
-    del_s[i] = ok ? a.delta[int64_t(bh) * a.Tq + i] : 0.f;
-  }
-  const uint16_t* krow = a.k + b * a.k_sb + hh * a.k_sh + int64_t(key) * a.k_st;
-  const uint16_t* vrow = a.v + b * a.v_sb + hh * a.v_sh + int64_t(key) * a.v_st;
-  bf16x8 kf[KS], vf[KS];
-#pragma unroll
-  for (int s = 0; s < KS; ++s) {
-    kf[s] = kv ? ld16(krow + 16 * s + 8 * h) : zero_bf8();
-    vf[s] = kv ? ld16(vrow + 16 * s + 8 * h) : zero_bf8();
-  }
-  const uint8_t* mrow = a.mask != nullptr ? a.mask + b * a.mask_sb : nullptr;
-  const bool kmasked = !kv ? true : (mrow != nullptr && mrow[key] == 0);
-#pragma unroll
-  for (int ti = 0; ti < NT; ++ti)
-    if (ti < nt) {
-      qr[ti].template store<true, true>(Qs + ti * kTile * RS, RS, Qt + ti * D * TS, TS);
-      dr[ti].template store<true, true>(Ds + ti * kTile * RS, RS, Dt + ti * D * TS, TS);
-    }
-  __syncthreads();
-
-  f32x16 dk[DT], dv[DT];
-#pragma unroll
-  for (int t = 0; t < DT; ++t) { dk[t] = zero16(); dv[t] = zero16(); }
-  for (int ti = 0; ti < nt; ++ti) {
-    const int qt = ti * kTile;
-    const uint16_t* Q_ = Qs + ti * kTile * RS;
-    const uint16_t* D_ = Ds + ti * kTile * RS;
-    const uint16_t* QT_ = Qt + ti * D * TS;
-    const uint16_t* DT_ = Dt + ti * D * TS;
-    f32x16 s_acc = zero16(), dp = zero16();
-#pragma unroll
-    for (int s = 0; s < KS; ++s) {
-      s_acc = mfma(ld16(Q_ + r * RS + 16 * s + 8 * h), kf[s], s_acc);   // S[query][key]
-      dp = mfma(ld16(D_ + r * RS + 16 * s + 8 * h), vf[s], dp);         // dP[query][key]
-    }
-#pragma unroll
-    for (int i = 0; i < 16; ++i) {
-      const int ql = crow(i, h);
-      float add = 0.f;
-      if (!kv) add = kNegInf;
-      else if (kmasked || (a.causal && key > qt + ql)) add = kMaskNeg;
-      const float p = __expf(s_acc[i] * a.scale + add - lse_s[qt + ql]);
-      s_acc[i] = p;
-      dp[i] = p * (dp[i] - del_s[qt + ql]);
-    }
-    const bf16x8 p0 = acc_frag(s_acc, 0), p1 = acc_frag(s_acc, 1);
-    const bf16x8 g0 = acc_frag(dp, 0), g1 = acc_frag(dp, 1);
-#pragma unroll
-    for (int t = 0; t < DT; ++t) {
-      const uint16_t* drow = DT_ + (32 * t + r) * TS;
-      dv[t] = mfma(p0, perm_frag(drow, 0, h, trans_rot(r)), dv[t]);
-      dv[t] = mfma(p1, perm_frag(drow, 1, h, trans_rot(r)), dv[t]);
-      const uint16_t* qrow = QT_ + (32 * t + r) * TS;
-      dk[t] = mfma(g0, perm_frag(qrow, 0, h, trans_rot(r)), dk[t]);
-      dk[t] = mfma(g1, perm_frag(qrow, 1, h, trans_rot(r)), dk[t]);
-    }
-  }
-  const int key0 = blockIdx.x * (32 * W) + w * 32;
-  uint16_t* dkb = a.dk + b * a.dk_sb + hh * a.dk_sh;
-  uint16_t* dvb = a.dv + b * a.dv_sb + hh * a.dv_sh;
-#pragma unroll
-  for (int t = 0; t < DT; ++t)
-#pragma unroll
-    for (int i = 0; i < 16; ++i) {
-      const int kk = key0 + crow(i, h);
-      if (kk < a.Tk) {
-        dkb[int64_t(kk) * a.dk_st + 32 * t + r] = f2bf(dk[t][i] * a.scale);
-        dvb[int64_t(kk) * a.dv_st + 32 * t + r] = f2bf(dv[t][i]);
-      }
-    }
-}
-
 template <typename F>
 void dispatch_d(int D, F&& f) {
   if (D == 32) f(std::integral_constant<int, 32>{});
@@ -877,15 +598,6 @@ void dispatch_w(int rows, F&& f) {
   if (rows <= 32 || maxw == 1) f(std::integral_constant<int, 1>{});
   else if (rows <= 64 || maxw == 2) f(std::integral_constant<int, 2>{});
   else f(std::integral_constant<int, 4>{});
-}
-
-// VODA_ATTN_RESIDENT=0 (A/B switch, read once): stream K/V tiles even when they all fit
-bool attn_resident() {
-  static const bool v = [] {
-    const char* e = std::getenv("VODA_ATTN_RESIDENT");
-    return e == nullptr || std::atoi(e) != 0;
-  }();
-  return v;
 }
 
 AttnArgs make_args(const std::vector<int64_t>& t, int B, int H, int Tq, int Tk, float scale, bool causal) {
@@ -926,12 +638,6 @@ void attention_fwd(const std::vector<int64_t>& t, int B, int H, int Tq, int Tk, 
     dispatch_w(Tq, [&](auto wc) {
       constexpr int DD = decltype(dc)::value, WW = decltype(wc)::value;
       const dim3 grid((Tq + 32 * WW - 1) / (32 * WW), unsigned(B * H));
-      if constexpr (DD <= 64 && WW == 4) {
-        if (Tk <= kResT && attn_resident()) {
-          hipLaunchKernelGGL((attn_fwd_res_kernel<DD, WW>), grid, dim3(64 * WW), 0, as_stream(stream), a);
-          return;
-        }
-      }
       hipLaunchKernelGGL((attn_fwd_kernel<DD, WW>), grid, dim3(64 * WW), 0, as_stream(stream), a);
     });
   });
@@ -949,24 +655,12 @@ void attention_bwd(const std::vector<int64_t>& t, int B, int H, int Tq, int Tk, 
     constexpr int DD = decltype(dc)::value;
     dispatch_w(Tq, [&](auto wc) {
       constexpr int WW = decltype(wc)::value;
-      const dim3 grid((Tq + 32 * WW - 1) / (32 * WW), unsigned(B * H));
-      if constexpr (DD <= 64 && WW == 4) {
-        if (Tk <= kResT && attn_resident()) {
-          hipLaunchKernelGGL((attn_bwd_dq_res_kernel<DD, WW>), grid, dim3(64 * WW), 0, s, a);
-          return;
-        }
-      }
-      hipLaunchKernelGGL((attn_bwd_dq_kernel<DD, WW>), grid, dim3(64 * WW), 0, s, a);
+      hipLaunchKernelGGL((attn_bwd_dq_kernel<DD, WW>), dim3((Tq + 32 * WW - 1) / (32 * WW), unsigned(B * H)),
+                         dim3(64 * WW), 0, s, a);
     });
     dispatch_w(Tk, [&](auto wc) {
       constexpr int WW = decltype(wc)::value;
       const dim3 grid((Tk + 32 * WW - 1) / (32 * WW), unsigned(B * H));
-      if constexpr (DD <= 64 && WW == 4) {
-        if (Tq <= kResT && attn_resident()) {
-          hipLaunchKernelGGL((attn_bwd_dkv_res_kernel<DD, WW>), grid, dim3(64 * WW), 0, s, a);
-          return;
-        }
-      }
       if constexpr (DD == 256) {
         hipLaunchKernelGGL((attn_bwd_dkv_kernel<DD, WW, 1>), grid, dim3(64 * WW), 0, s, a);
         hipLaunchKernelGGL((attn_bwd_dkv_kernel<DD, WW, 2>), grid, dim3(64 * WW), 0, s, a);
