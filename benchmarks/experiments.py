@@ -26,7 +26,7 @@ import sys
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from vodascheduler_amd.algorithm import ALGORITHMS  # noqa: E402
 from vodascheduler_amd.sim.simulator import simulate  # noqa: E402
-from vodascheduler_amd.common.workload import busbw_source, intra_node_busbw, load_busbw  # noqa: E402
+from vodascheduler_amd.common.workload import busbw_source, intra_node_busbw, load_bench_json  # noqa: E402
 from vodascheduler_amd.sim.trace import (ASSUMED_BUSBW_GBS, ASSUMED_INTERNODE_BUSBW_GBS, TraceJob,  # noqa: E402
                                          make_spec, philly_trace)
 
@@ -100,7 +100,7 @@ def main():
     a = ap.parse_args()
     assert set(ORDER) == set(ALGORITHMS)
     if a.bench_json:
-        print("measured busbw (GB/s) by world:", load_busbw(a.bench_json))
+        print("measured (busbw GB/s by world, step ms by model/world):", load_bench_json(a.bench_json))
     bw = (f"MEASURED per world ({', '.join(f'{k}: {intra_node_busbw(k):.0f}' for k in (2, 4, 8))} GB/s)"
           if busbw_source() == "measured" else f"ASSUMED ({ASSUMED_BUSBW_GBS:.0f} GB/s intra-node)")
     lines = ["# BASELINE.json configs in the discrete-event simulator (round 3)", "",

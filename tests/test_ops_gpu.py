@@ -267,8 +267,16 @@ def test_fused_linear_bf16_flat_grads_gpu():
     from vodascheduler_amd.utils.flat import grad_of
 
     assert m.weight.grad is None and grad_of(m.weight).dtype == torch.float32  # fp32 flat gradient
+    # loose: against the stock layer (its own autocast GEMM rounds dW to bf16)
     torch.testing.assert_close(grad_of(m.weight), ref.weight.grad, atol=0.5, rtol=5e-2)
     torch.testing.assert_close(grad_of(m.bias), ref.bias.grad, atol=0.5, rtol=5e-2)
+    # tight: against the exact (fp64) product of the bf16 operands the kernel consumes -- the
+    # MFMA kernel accumulates in fp32 and rounds once, so a wrong tile / k-step / lane map
+    # (errors of the gradient's own magnitude, ~30 here) cannot hide under the tolerance
+    gq = g.bfloat16().double().reshape(-1, 3072)
+    xq = x.bfloat16().double().reshape(-1, 768)
+    torch.testing.assert_close(grad_of(m.weight).double(), gq.t() @ xq, rtol=1e-4, atol=2e-3)
+    torch.testing.assert_close(grad_of(m.bias).double(), gq.sum(0), rtol=1e-4, atol=2e-3)
 
 
 @pytest.mark.parametrize("opt_name", ["adamw", "sgd"])

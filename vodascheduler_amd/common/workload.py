@@ -99,6 +99,52 @@ def load_busbw(path: str, bucket_mb: int = 64) -> dict[int, float]:
     return table
 
 
+# model -> {world size: measured seconds per training step} from a bench run's online
+# profiling (``step_ms_by_world``); overrides the speed model at the measured world sizes
+_MEASURED_STEP: dict[str, dict[int, float]] = {}
+
+
+def set_measured_step_times(table: dict[str, dict] | None) -> None:
+    """Install measured per-world step times ({model: {world: ms}}); None clears them."""
+    _MEASURED_STEP.clear()
+    for model, per in (table or {}).items():
+        d = {int(w): float(ms) / 1e3 for w, ms in (per or {}).items() if ms and float(ms) > 0}
+        if d:
+            _MEASURED_STEP[model] = d
+
+
+def load_bench_json(path: str, bucket_mb: int = 64) -> dict:
+    """Measured busbw (``load_busbw``) AND per-model per-world step times from bench JSON(s):
+    the simulator then prices jobs with the hardware's own numbers."""
+    bw = load_busbw(path, bucket_mb)
+    with open(path) as f:
+        doc = json.load(f)
+    steps: dict[str, dict[str, float]] = {}
+
+    def walk(x):
+        if isinstance(x, dict):
+            if isinstance(x.get("step_ms_by_world"), dict):
+                for m, per in x["step_ms_by_world"].items():
+                    steps.setdefault(m, {}).update(per)
+            for v in x.values():
+                walk(v)
+        elif isinstance(x, list):
+            for v in x:
+                walk(v)
+        elif isinstance(x, str) and "step_ms_by_world" in x:
+            for ln in x.splitlines():
+                ln = ln.strip()
+                if ln.startswith("{") and "step_ms_by_world" in ln:
+                    try:
+                        walk(json.loads(ln))
+                    except json.JSONDecodeError:
+                        pass
+
+    walk(doc)
+    set_measured_step_times(steps)
+    return {"busbw_gbs": bw, "step_ms_by_world": steps}
+
+
 @dataclass
 class ModelProfile:
     """Scaling model of a workload.
@@ -127,6 +173,11 @@ class ModelProfile:
     def speedup(self, n: int, busbw_gbs: float | None = None) -> float:
         if n <= 0:
             return 0.0
+        meas = _MEASURED_STEP.get(self.name)
+        if meas and n in meas and busbw_gbs is None:
+            # measured: n workers each process one per-GPU batch per step of meas[n] seconds
+            t1 = meas.get(1, self.step_time_1gpu)
+            return n * t1 / meas[n]
         if self.grad_mb > 0:
             t1 = self.step_time_1gpu
             c = self.comm_time(n, busbw_gbs)
