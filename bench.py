@@ -95,7 +95,6 @@ sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 
 from vodascheduler_amd.common.workload import busbw_source, set_measured_busbw  # noqa: E402
 from vodascheduler_amd.ops import _native  # noqa: E402
-from vodascheduler_amd.parallel.comm import RcclCommunicator  # noqa: E402
 from vodascheduler_amd.runtime.cluster import free_port, run_trace  # noqa: E402
 from vodascheduler_amd.runtime.pool import PoolWorker  # noqa: E402
 from vodascheduler_amd.runtime.rendezvous import connect_store  # noqa: E402
@@ -200,32 +199,45 @@ class Watchdog:
 
 def measure_busbw(store, rank: int, world: int, device, sizes_mb=(16, 64, 256), iters: int = 5) -> dict:
     """RCCL all-reduce bus bandwidth over xGMI for every power-of-two sub-world <= N (and N):
-    ranks [0, k) build a fresh communicator (its init time is reported), run 2 warm + ``iters``
-    timed fp32 all-reduces per size; busbw = bytes / t x 2 (k-1) / k (ring all-reduce
-    traffic per link).  Outside the timed trace."""
+    for each size k the ranks form aligned groups [g k, (g+1) k) that build their
+    communicators concurrently (the init time of group 0 is reported); group 0 runs 2 warm +
+    ``iters`` timed fp32 all-reduces per size, busbw = bytes / t x 2 (k-1) / k (ring
+    all-reduce traffic per link).  Outside the timed trace.
+
+    Every communicator built here is keyed by its ordered member list and handed to the
+    per-process communicator cache (parallel/comm.py CommCache) instead of being destroyed:
+    the first job that lands on an aligned GPU group -- which placement prefers (buddy
+    alignment, placement/manager.py) -- reuses it instead of paying an RCCL bootstrap."""
+    from vodascheduler_amd.parallel.comm import COMM_CACHE, create_communicator
+
     ks = sorted({k for k in (2, 4, 8, 16, 32) if k <= world} | {world})
-    out: dict = {"by_world": {}, "init_s": {}}
+    out: dict = {"by_world": {}, "init_s": {}, "prewarmed_groups": 0}
     for k in ks:
-        if rank < k:
+        g = rank // k
+        if (g + 1) * k <= world:
+            members = [f"node0:{r}" for r in range(g * k, (g + 1) * k)]
             t0 = time.perf_counter()
-            comm = RcclCommunicator(store, f"bench/bw/{k}", rank, k, device, timeout=120)
+            comm = create_communicator(store, f"bench/bw/{k}/{g}", rank - g * k, k, device, backend="rccl",
+                                       timeout=120, members=members)
             sync(device)
-            out["init_s"][str(k)] = round(time.perf_counter() - t0, 4)
-            res = {}
-            for mb in sizes_mb:
-                x = torch.ones(mb << 18, device=device)  # mb MiB of fp32
-                for _ in range(2):
-                    comm.allreduce_(x, "sum")
-                sync(device)
-                t0 = time.perf_counter()
-                for _ in range(iters):
-                    comm.allreduce_(x, "sum")
-                sync(device)
-                dt = (time.perf_counter() - t0) / iters
-                res[str(mb)] = round(x.numel() * 4 / dt / 1e9 * 2 * (k - 1) / k, 1)
-                del x
-            out["by_world"][str(k)] = res
-            comm.destroy()
+            if g == 0:
+                out["init_s"][str(k)] = round(time.perf_counter() - t0, 4)
+                res = {}
+                for mb in sizes_mb:
+                    x = torch.ones(mb << 18, device=device)  # mb MiB of fp32
+                    for _ in range(2):
+                        comm.allreduce_(x, "sum")
+                    sync(device)
+                    t0 = time.perf_counter()
+                    for _ in range(iters):
+                        comm.allreduce_(x, "sum")
+                    sync(device)
+                    dt = (time.perf_counter() - t0) / iters
+                    res[str(mb)] = round(x.numel() * 4 / dt / 1e9 * 2 * (k - 1) / k, 1)
+                    del x
+                out["by_world"][str(k)] = res
+            COMM_CACHE.put(comm)  # idle, keyed by its members: a later job on these GPUs reuses it
+            out["prewarmed_groups"] += 1
         dist.barrier()
     return out
 
@@ -513,6 +525,7 @@ def main():
             "allreduce_busbw_by_world": bw["by_world"],
             "busbw_source_for_priors": busbw_source(),
             "rccl_init_s": bw["init_s"],
+            "rccl_prewarmed_groups_rank0": bw.get("prewarmed_groups", 0),
             "step_ms_by_world": per_world_step_ms(allrec),
             "gpu_ms_per_train_step": round(tot_train / max(tot_steps, 1) * 1e3, 3),
             "control": control_out,

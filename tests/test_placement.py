@@ -194,3 +194,18 @@ def test_placement_keeps_new_jobs_inside_one_numa_domain():
     p3 = pm.place({"a": 2, "b": 4, "c": 2})
     assert len({numa[g] for _, g in p3.workers["c"]}) == 1
     assert p3.num_migrated == 0
+
+
+def test_buddy_aligned_gpu_sets():
+    """Jobs fill power-of-two aligned GPU blocks ([0,1], [2,3], [0..3], ...): aligned member
+    sets recur, so their RCCL communicators come from the workers' cache (bench.py pre-builds
+    one per aligned group); kept workers still never move."""
+    pm = _pm()
+    p1 = pm.place({"a": 1})
+    assert [g for _, g in p1.workers["a"]] == [0]
+    p2 = pm.place({"a": 1, "b": 2})
+    assert sorted(g for _, g in p2.workers["b"]) == [2, 3]      # not [1, 2]: block [0,1] is a's
+    p3 = pm.place({"a": 2, "b": 2, "c": 4})
+    assert sorted(g for _, g in p3.workers["a"]) == [0, 1]      # a grows into its buddy
+    assert sorted(g for _, g in p3.workers["c"]) == [4, 5, 6, 7]
+    assert [g for _, g in p3.workers["b"]] == [2, 3] and not p3.migrated
