@@ -13,10 +13,13 @@
 #   prof-MODEL[-fp32]        rocprofv3 --kernel-trace --stats of 10 steps of one model
 #   pmc-MODEL:COUNTERS       one rocprofv3 --pmc pass (comma-separated counters)
 #   py:SCRIPT[:ARGS]         python benchmarks/SCRIPT ARGS (comma-separated args)
+#   pytest:FILE[,ARGS]       pytest -m gpu of one test file (comma-separated extra args)
+#   env:NAME=VALUE           export for the following steps (their logs get a "+NAME=VALUE" suffix)
 set -o pipefail
 TAG=${1:?tag}
 shift
 OUT=gpurun_out/$TAG
+SUFFIX=""
 mkdir -p "$OUT"
 export TMPDIR=/tmp
 export HSA_ENABLE_IPC_MODE_LEGACY=0
@@ -26,6 +29,7 @@ export MIOPEN_CUSTOM_CACHE_DIR=${MIOPEN_CUSTOM_CACHE_DIR:-/tmp/miopen-cache}
 run() {  # run SECONDS NAME CMD...
   local secs=$1 name=$2
   shift 2
+  name=$name$SUFFIX
   echo "[lease $(date +%T)] $name: $*"
   timeout -k 10 "$secs" "$@" > "$OUT/$name.log" 2>&1
   local rc=$?
@@ -56,7 +60,7 @@ for step in "$@"; do
       rc=$?
       unset MIOPEN_ENABLE_LOGGING MIOPEN_LOG_LEVEL
       [[ $rc == 0 ]] || exit $rc
-      grep '^{' "$OUT/$step.log" || true ;;
+      grep '^{' "$OUT/$step$SUFFIX.log" || true ;;
     miopen-save)  # the find-db / perf-db this lease added, to commit under var/miopen/db
       mkdir -p "$OUT/miopen_db" && cp "$MIOPEN_USER_DB_PATH"/*.txt "$OUT/miopen_db/" && ls -la "$OUT/miopen_db" ;;
     prof-*)
@@ -70,6 +74,8 @@ for step in "$@"; do
       mkdir -p "$OUT/$step"
       python3 benchmarks/trace_window_stats.py "/tmp/$step/k_kernel_trace.csv" "$OUT/$step/steady_kernel_stats.csv" \
         >> "$OUT/$step.log" 2>&1 || exit 7
+      python3 benchmarks/trace_dispatches.py "/tmp/$step/k_kernel_trace.csv" "$OUT/$step/sequence.csv" "" \
+        >> "$OUT/$step.log" 2>&1 || exit 7
       python3 benchmarks/rocprof_summary.py "$OUT/$step/steady_kernel_stats.csv" "$m $prec steady state (10 steps)" 45 10 \
         > "$OUT/$step.md" || exit 7
       tail -n 3 "$OUT/$step.log" ;;
@@ -79,6 +85,15 @@ for step in "$@"; do
       ctr=${spec#*:}
       run 120 "pmc-$m" rocprofv3 --kernel-trace --pmc ${ctr//,/ } -d "$OUT/pmc-$m" -o run -- \
         python -u benchmarks/model_step.py --model "$m" --steps 3 --warmup 3 || exit $? ;;
+    pytest:*)  # pytest:tests/FILE.py[,-k,EXPR] -- one GPU test file
+      spec=${step#pytest:}
+      run 300 "pytest-$(basename "${spec%%,*}" .py)" python -u -m pytest ${spec//,/ } -m gpu -x -q --timeout 120 \
+        --timeout-method thread || exit $? ;;
+    env:*)  # env:NAME=VALUE -- exported for the steps that follow
+      kv=${step#env:}
+      export "${kv?}"
+      SUFFIX="$SUFFIX+$kv"
+      echo "[lease] export $kv" ;;
     py:*)
       spec=${step#py:}
       script=${spec%%:*}

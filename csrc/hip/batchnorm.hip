@@ -670,6 +670,127 @@ __global__ __launch_bounds__(kBlock) void bn_pool_bwd_apply_kernel(const T* __re
   Vec8<T>::store(dx, off, o);
 }
 
+// 3x3 / stride-2 / pad-1 windows (the ResNet stem) with one thread per 2 x 2 block of input
+// pixels (rows 2m, 2m+1, columns 2k, 2k+1) and channel group: the 4 windows (m + a, k + b),
+// a, b in {0, 1}, that can select any of the 4 pixels are loaded once and shared, instead of
+// every pixel loading its (up to) 4 windows on its own -- the dy / argmax gather was 8 of
+// the 9 loads per pixel of the generic passes above (stem backward reduce + apply: 190 + 293
+// us per ResNet-50 bs-256 step, ~1.8x their byte floor).  Pixel (dh, dw) is tap
+// (kh, kw) = (dh - 2a + 1, dw - 2b + 1) of window (a, b) when both are in [0, 3).
+template <typename T>
+__device__ __forceinline__ void pool22_grads(const T* __restrict__ dyp, const uint8_t* __restrict__ idx,
+                                             const PoolG& g, int n, int m, int k, int cg, float (&gr)[4][8]) {
+  uint2 a[4];
+  typename Vec8<T>::Raw raw[4];
+  const int64_t nbase = int64_t(n) * g.Ho * g.Wo * g.C + cg * kVec;
+#pragma unroll
+  for (int wi = 0; wi < 4; ++wi) {
+    const int ho = min(m + (wi >> 1), g.Ho - 1), wo = min(k + (wi & 1), g.Wo - 1);
+    const int64_t o = nbase + (int64_t(ho) * g.Wo + wo) * g.C;
+    a[wi] = *reinterpret_cast<const uint2*>(idx + o);
+    raw[wi] = Vec8<T>::load_raw(dyp, o);
+  }
+#pragma unroll
+  for (int px = 0; px < 4; ++px)
+#pragma unroll
+    for (int c = 0; c < 8; ++c) gr[px][c] = 0.f;
+#pragma unroll
+  for (int wi = 0; wi < 4; ++wi) {
+    const int wa = wi >> 1, wb = wi & 1;
+    const bool win_ok = m + wa < g.Ho && k + wb < g.Wo;
+    float d[8];
+    Vec8<T>::cvt(raw[wi], d);
+#pragma unroll
+    for (int px = 0; px < 4; ++px) {
+      const int kh = (px >> 1) - 2 * wa + 1, kw = (px & 1) - 2 * wb + 1;
+      if (kh < 0 || kh > 2 || kw < 0 || kw > 2) continue;  // compile-time after unrolling
+      const uint32_t want = win_ok ? uint32_t(kh * 3 + kw) : 0x100u;
+#pragma unroll
+      for (int c = 0; c < 8; ++c) {
+        const uint32_t ac = ((c < 4 ? a[wi].x : a[wi].y) >> (8 * (c & 3))) & 0xff;
+        if (ac == want) gr[px][c] += d[c];
+      }
+    }
+  }
+}
+
+template <typename T>
+__global__ __launch_bounds__(kBlock) void bn_pool_bwd_reduce22_kernel(const T* __restrict__ dyp,
+                                                                      const uint8_t* __restrict__ idx,
+                                                                      const T* __restrict__ x,
+                                                                      float* __restrict__ part, PoolG g) {
+  const Map mp = make_map(g.C);
+  float s1[8] = {0, 0, 0, 0, 0, 0, 0, 0}, s2[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  if (mp.active) {
+    const int Hm = (g.H + 1) / 2, Wk = (g.W + 1) / 2;
+    const int rows = g.N * Hm;
+    const int per = (rows + int(gridDim.x) - 1) / int(gridDim.x);
+    const int r0 = int(blockIdx.x) * per, r1 = min(rows, r0 + per);
+    for (int r = r0; r < r1; ++r) {
+      const int n = r / Hm, m = r - n * Hm;
+      for (int k = mp.rsub; k < Wk; k += mp.rpi) {
+        typename Vec8<T>::Raw xr[4];
+#pragma unroll
+        for (int px = 0; px < 4; ++px) {
+          const int h = min(2 * m + (px >> 1), g.H - 1), w = min(2 * k + (px & 1), g.W - 1);
+          xr[px] = Vec8<T>::load_raw(x, ((int64_t(n) * g.H + h) * g.W + w) * g.C + int64_t(mp.cg) * kVec);
+        }
+        float gr[4][8];
+        pool22_grads<T>(dyp, idx, g, n, m, k, mp.cg, gr);
+#pragma unroll
+        for (int px = 0; px < 4; ++px) {
+          // a clamped duplicate pixel past the image edge has no window selecting it: gr = 0
+          float xv[8];
+          Vec8<T>::cvt(xr[px], xv);
+#pragma unroll
+          for (int c = 0; c < 8; ++c) { s1[c] += gr[px][c]; s2[c] = fmaf(gr[px][c], xv[c], s2[c]); }
+        }
+      }
+    }
+  }
+  reduce_and_store(mp, s1, s2, part, part + int64_t(gridDim.x) * g.C, g.C);
+}
+
+template <typename T>
+__global__ __launch_bounds__(kBlock) void bn_pool_bwd_apply22_kernel(const T* __restrict__ dyp,
+                                                                     const uint8_t* __restrict__ idx,
+                                                                     const T* __restrict__ x,
+                                                                     const float* __restrict__ k3, T* __restrict__ dx,
+                                                                     PoolG g) {
+  const int CG = g.C / kVec;
+  const int Hm = (g.H + 1) / 2, Wk = (g.W + 1) / 2;
+  const int j = int(blockIdx.y) * kBlock + int(threadIdx.x);
+  if (j >= Wk * CG) return;
+  const int n = int(blockIdx.x) / Hm, m = int(blockIdx.x) - (int(blockIdx.x) / Hm) * Hm;
+  const int k = j / CG, cg = j - k * CG;
+  typename Vec8<T>::Raw xr[4];
+  int64_t off[4];
+#pragma unroll
+  for (int px = 0; px < 4; ++px) {
+    const int h = min(2 * m + (px >> 1), g.H - 1), w = min(2 * k + (px & 1), g.W - 1);
+    off[px] = ((int64_t(n) * g.H + h) * g.W + w) * g.C + cg * kVec;
+    xr[px] = Vec8<T>::load_raw(x, off[px]);
+  }
+  float gr[4][8];
+  pool22_grads<T>(dyp, idx, g, n, m, k, cg, gr);
+  float a[8], c2[8], c0[8];
+#pragma unroll
+  for (int c = 0; c < 8; ++c) {
+    a[c] = k3[cg * kVec + c];
+    c2[c] = k3[g.C + cg * kVec + c];
+    c0[c] = k3[2 * g.C + cg * kVec + c];
+  }
+#pragma unroll
+  for (int px = 0; px < 4; ++px) {
+    if (2 * m + (px >> 1) >= g.H || 2 * k + (px & 1) >= g.W) continue;
+    float xv[8], o[8];
+    Vec8<T>::cvt(xr[px], xv);
+#pragma unroll
+    for (int c = 0; c < 8; ++c) o[c] = fmaf(a[c], gr[px][c], fmaf(c2[c], xv[c], c0[c]));
+    Vec8<T>::store(dx, off[px], o);
+  }
+}
+
 // ---------------------------------------------------------------- launch helpers
 struct Grid {
   dim3 grid;
@@ -872,6 +993,14 @@ void bn_bwd(uintptr_t dy, uintptr_t mask, uintptr_t x, uintptr_t save_mean, uint
 namespace {
 constexpr int kPoolRedBlocks = 2048;  // 8 four-wave blocks per CU: the gather loop is latency-bound
 int pool_red_blocks(int N, int H) { return std::max(1, std::min(kPoolRedBlocks, N * H)); }
+// VODA_POOL22=0: the generic one-pixel-per-thread backward passes (A/B switch)
+bool pool22_enabled() {
+  static const bool on = [] {
+    const char* e = std::getenv("VODA_POOL22");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
 void check_pool(int N, int H, int W, int C, int Ho, int Wo, int k, int s, int p) {
   VODA_CHECK(C % kVec == 0 && C <= kVec * kMaxTpr, "bn_pool: C must be a multiple of 8 and <= 2048");
   VODA_CHECK(k == 3 && s == 2 && p >= 0 && 2 * p <= k, "bn_pool: only the 3x3 / stride-2 window is compiled");
@@ -888,22 +1017,24 @@ int64_t bn_pool_workspace_floats(int N, int H, int C) {
 void bn_pool_fwd_train(uintptr_t x, uintptr_t gamma, uintptr_t beta, uintptr_t running_mean, uintptr_t running_var,
                        uintptr_t save_mean, uintptr_t save_invstd, uintptr_t y, uintptr_t idx, uintptr_t workspace,
                        int N, int H, int W, int C, int Ho, int Wo, int k, int s, int p, float eps, float momentum,
-                       int dt, uintptr_t stream) {
+                       int dt, uintptr_t stream, int pre_nb) {
   check_pool(N, H, W, C, Ho, Wo, k, s, p);
   hipStream_t st = as_stream(stream);
   const int64_t M = int64_t(N) * H * W;
   float* ws = reinterpret_cast<float*>(workspace);
-  // the statistics pass on a grid of at most pool_red_blocks partial rows (fits the workspace)
+  // the statistics pass on a grid of at most pool_red_blocks partial rows (fits the workspace),
+  // or the pre_nb rows the producing convolution already wrote (stem.hip)
   const Grid rg = bn_grid(M, C, pool_red_blocks(N, H), 8);
-  float* ab = ws + int64_t(2) * rg.nb * C;
+  const int nb = pre_nb > 0 ? pre_nb : rg.nb;
+  float* ab = ws + int64_t(2) * nb * C;
   const PoolG g{N, H, W, C, Ho, Wo, k, s, p};
   const dim3 pgrid(unsigned(int64_t(N) * Ho), unsigned((Wo * (C / kVec) + kBlock - 1) / kBlock));
   dispatch_dt(dt, [&](auto tag) {
     using T = decltype(tag);
     const T* xp = reinterpret_cast<const T*>(x);
-    hipLaunchKernelGGL((bn_stats_kernel<T, 8>), rg.grid, dim3(kBlock), 0, st, xp, ws, M, C, 1);
+    if (pre_nb <= 0) hipLaunchKernelGGL((bn_stats_kernel<T, 8>), rg.grid, dim3(kBlock), 0, st, xp, ws, M, C, 1);
     hipLaunchKernelGGL(bn_fwd_finalize_kernel, dim3((C + kFinCh - 1) / kFinCh), dim3(kFinCh * kFinRg), 0, st, ws,
-                       rg.nb, M, C, reinterpret_cast<const float*>(gamma), reinterpret_cast<const float*>(beta),
+                       nb, M, C, reinterpret_cast<const float*>(gamma), reinterpret_cast<const float*>(beta),
                        reinterpret_cast<float*>(running_mean), reinterpret_cast<float*>(running_var),
                        reinterpret_cast<float*>(save_mean), reinterpret_cast<float*>(save_invstd), ab, eps, momentum);
     hipLaunchKernelGGL((bn_pool_fwd_kernel<T, 3, 2>), pgrid, dim3(kBlock), 0, st, xp, ab, reinterpret_cast<T*>(y),
@@ -923,18 +1054,28 @@ void bn_pool_bwd(uintptr_t dy, uintptr_t idx, uintptr_t x, uintptr_t save_mean, 
   float* k3 = ws + int64_t(2) * nb * C;
   const PoolG g{N, H, W, C, Ho, Wo, k, s, p};
   const dim3 agrid(unsigned(int64_t(N) * H), unsigned((W * (C / kVec) + kBlock - 1) / kBlock));
+  // pad 1 (the stem): 2 x 2 input pixels per thread share their 4 windows (see pool22_grads)
+  const bool p22 = p == 1 && pool22_enabled();
+  const dim3 agrid22(unsigned(int64_t(N) * ((H + 1) / 2)), unsigned(((W + 1) / 2 * (C / kVec) + kBlock - 1) / kBlock));
   dispatch_dt(dt, [&](auto tag) {
     using T = decltype(tag);
     const T* dyp = reinterpret_cast<const T*>(dy);
     const uint8_t* ip = reinterpret_cast<const uint8_t*>(idx);
     const T* xp = reinterpret_cast<const T*>(x);
-    hipLaunchKernelGGL((bn_pool_bwd_reduce_kernel<T, 3, 2>), dim3(nb), dim3(kBlock), 0, st, dyp, ip, xp, ws, g);
+    if (p22)
+      hipLaunchKernelGGL((bn_pool_bwd_reduce22_kernel<T>), dim3(nb), dim3(kBlock), 0, st, dyp, ip, xp, ws, g);
+    else
+      hipLaunchKernelGGL((bn_pool_bwd_reduce_kernel<T, 3, 2>), dim3(nb), dim3(kBlock), 0, st, dyp, ip, xp, ws, g);
     hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + kFinCh - 1) / kFinCh), dim3(kFinCh * kFinRg), 0, st, ws,
                        nb, M, C, reinterpret_cast<const float*>(gamma), reinterpret_cast<const float*>(save_mean),
                        reinterpret_cast<const float*>(save_invstd), reinterpret_cast<float*>(dgamma),
                        reinterpret_cast<float*>(dbeta), k3, int(accumulate));
-    hipLaunchKernelGGL((bn_pool_bwd_apply_kernel<T, 3, 2>), agrid, dim3(kBlock), 0, st, dyp, ip, xp, k3,
-                       reinterpret_cast<T*>(dx), g);
+    if (p22)
+      hipLaunchKernelGGL((bn_pool_bwd_apply22_kernel<T>), agrid22, dim3(kBlock), 0, st, dyp, ip, xp, k3,
+                         reinterpret_cast<T*>(dx), g);
+    else
+      hipLaunchKernelGGL((bn_pool_bwd_apply_kernel<T, 3, 2>), agrid, dim3(kBlock), 0, st, dyp, ip, xp, k3,
+                         reinterpret_cast<T*>(dx), g);
   });
   check_launch();
 }

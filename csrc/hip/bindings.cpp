@@ -46,6 +46,15 @@ PYBIND11_MODULE(_vodahip, m) {
   m.def("bn_pool_workspace_floats", &bn_pool_workspace_floats);
   m.def("bn_pool_fwd_train", &bn_pool_fwd_train);
   m.def("bn_pool_bwd", &bn_pool_bwd);
+  m.def("global_avgpool_bwd", &global_avgpool_bwd);
+  m.def("subsample2d", &subsample2d);
+  m.def("conv3x3_c64_wgrad_workspace_floats", &conv3x3_c64_wgrad_workspace_floats);
+  m.def("conv3x3_c64_wgrad", &conv3x3_c64_wgrad);
+  m.def("stem_partial_rows", &stem_partial_rows);
+  m.def("stem_pack", &stem_pack);
+  m.def("stem_conv_fwd", &stem_conv_fwd);
+  m.def("stem_wgrad_workspace_floats", &stem_wgrad_workspace_floats);
+  m.def("stem_conv_wgrad", &stem_conv_wgrad);
   m.def("maxpool2d_fwd", &maxpool2d_fwd);
   m.def("maxpool2d_bwd", &maxpool2d_bwd);
   m.def("colsum_workspace_floats", &colsum_workspace_floats);

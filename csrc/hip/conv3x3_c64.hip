@@ -1,0 +1,260 @@
+// Weight gradient of a 3x3 / stride-1 / pad-1 convolution with 64 input and 64 output
+// channels (ResNet-50 layer1, ResNet-18/34 layer1), channels_last bf16 activations:
+//
+//   dW[co][kh][kw][ci] (+)= sum over pixels (n, h, w) of dY[n][h][w][co] * X[n][h+kh-1][w+kw-1][ci]
+//
+// MIOpen runs it as an atomic split-K igemm_wrw (~150 us at bs 256, 56 x 56) plus a workspace
+// clear, a cast and the fold into the flat fp32 gradient (~15 us); the repo's 128 x 128-tile
+// implicit-GEMM kernel (wgrad.hip) fills a quarter of its tile at 64 channels (360 us).
+// Here the problem is what it is: a 64 x 576 result reduced over 0.8 M pixels.
+//  * persistent workgroups (1 per CU, one wave per SIMD: the 144 accumulators and the 2-deep
+//    prefetch need more than the 256 registers of two waves) walk contiguous chunks of rows; per row the dY
+//    row is staged as [64 px][192 B] and the input rows h-1, h, h+1 sit in a 4-slot LDS ring
+//    of [66 px][192 B] rows (zero outside the image); the 192-byte pixel pitch makes the
+//    transposed reads below conflict-free;
+//  * both MFMA operands need 8 consecutive PIXELS per lane: ds_read_b64_tr_b16 reads them as
+//    columns (per-lane addresses: the im2col rows of tap (kh, kw) are the ring pixels shifted
+//    by kw, no im2col buffer);
+//  * D = 2 channel tiles x 18 (tap, 32-channel block) tiles of 32 x 32; wave w owns channel
+//    tile w & 1 and 9 of the 18 column tiles (144 accumulator registers), accumulated over the
+//    whole row chunk;
+//  * the next rows' loads run two rows ahead in registers (a global load's ~1-2 us latency is
+//    longer than a row's MFMA work), written into the LDS after each row's MFMAs;
+//  * one fp32 partial [64][576] per workgroup; two small passes sum them and add the result
+//    into the optimizer's flat gradient with the weight's strides.
+#include "common.h"
+#include "ops.h"
+
+namespace voda {
+
+namespace {
+
+typedef __bf16 c64_bf16x8 __attribute__((ext_vector_type(8)));
+typedef float c64_f32x16 __attribute__((ext_vector_type(16)));
+typedef __bf16 c64_bf16x4_v __attribute__((__vector_size__(4 * sizeof(__bf16))));
+typedef __attribute__((address_space(3))) c64_bf16x4_v c64_lds_bf16x4;
+
+constexpr int kC = 64;                     // channels in and out
+constexpr int kThreads = 256;
+constexpr int kMaxW = 64;                  // output pixels per row (4 k-steps of 16)
+constexpr int kPxB = 192;                  // LDS bytes per pixel (128 + 64 pad)
+constexpr int kRingPx = kMaxW + 2;         // 66 pixels per input row (pad 1 each side)
+constexpr int kSlotB = kRingPx * kPxB;     // 12672 B
+constexpr int kSlots = 4;                  // rows h-1, h, h+1 + the next row
+constexpr int kDyB = kMaxW * kPxB;         // 12288 B
+constexpr int kK = 9 * kC;                 // 576 result columns (tap-major, channels_last)
+constexpr int kRowChunks = kRingPx * 8;    // 16-B chunks of one ring row (528)
+constexpr int kXPf = (kRowChunks + kThreads - 1) / kThreads;  // 3
+constexpr int kDyPf = (kMaxW * 8 + kThreads - 1) / kThreads;  // 2
+
+struct C64Args {
+  const uint16_t* x;   // [N][H][W][64]
+  const uint16_t* dy;  // [N][H][W][64]
+  float* part;         // [gridDim.x][64][576]
+  int N, H, W;
+};
+
+__device__ __forceinline__ uint2 c64_tr(const unsigned char* p) {
+  const c64_bf16x4_v v = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((c64_lds_bf16x4*)(p));
+  return __builtin_bit_cast(uint2, v);
+}
+
+__device__ __forceinline__ c64_bf16x8 c64_frag(const unsigned char* lo, const unsigned char* hi) {
+  const uint2 a = c64_tr(lo), b = c64_tr(hi);
+  return __builtin_bit_cast(c64_bf16x8, make_uint4(a.x, a.y, b.x, b.y));
+}
+
+// 16-byte chunk c (0..527) of ring row hi of image n: pixel j = c / 8 is input column j - 1
+__device__ __forceinline__ uint4 c64_xchunk(const C64Args& a, int64_t n, int hi, int c) {
+  const int j = c >> 3, part = c & 7;
+  const int wi = j - 1;
+  const bool ok = unsigned(hi) < unsigned(a.H) && unsigned(wi) < unsigned(a.W);
+  const int hc = min(max(hi, 0), a.H - 1), wc = min(max(wi, 0), a.W - 1);
+  const uint4 v = reinterpret_cast<const uint4*>(a.x + ((n * a.H + hc) * a.W + wc) * kC)[part];
+  const uint32_t m = ok ? 0xffffffffu : 0u;
+  return make_uint4(v.x & m, v.y & m, v.z & m, v.w & m);
+}
+
+__global__ __launch_bounds__(kThreads, 1) void conv3x3_c64_wgrad_kernel(C64Args a) {
+  __shared__ __attribute__((aligned(16))) unsigned char ring[kSlots * kSlotB];
+  __shared__ __attribute__((aligned(16))) unsigned char dyt[kDyB];
+
+  const int tid = threadIdx.x;
+  const int wave = tid >> 6, lane = tid & 63;
+  const int lh = lane >> 5, lg = (lane >> 4) & 1, lq = (lane & 15) >> 2, lp = lane & 3;
+  const int ct = wave & 1;            // output-channel tile
+  const int kt0 = (wave >> 1) * 9;    // first of this wave's 9 (tap, channel-block) tiles
+
+  for (int i = tid; i < (kMaxW - a.W) * (kPxB / 16); i += kThreads)
+    *reinterpret_cast<uint4*>(dyt + a.W * kPxB + i * 16) = make_uint4(0u, 0u, 0u, 0u);
+
+  c64_f32x16 acc[9];
+#pragma unroll
+  for (int t = 0; t < 9; ++t) acc[t] = c64_f32x16{};
+
+  const int64_t rows = int64_t(a.N) * a.H;
+  const int64_t per = (rows + gridDim.x - 1) / gridDim.x;
+  const int64_t r0 = int64_t(blockIdx.x) * per;
+  const int64_t r1 = r0 + per < rows ? r0 + per : rows;
+  const int dchunks = a.W * 8;
+
+  // per-lane byte offsets of the transposed reads at k-step 0
+  const int a_off = (8 * lh + lq) * kPxB + (32 * ct + 16 * lg + 4 * lp) * 2;
+  const int b_off = (8 * lh + lq) * kPxB + (16 * lg + 4 * lp) * 2;
+
+  int64_t n = r0 / a.H;
+  int h = int(r0 - n * a.H);
+  uint4 xa0, xa1, xa2, xb0, xb1, xb2, da0, da1, db0, db1;
+  static_assert(kXPf == 3 && kDyPf == 2, "prefetch slots");
+  auto load_x = [&](int hi, uint4& v0, uint4& v1, uint4& v2) {
+    v0 = c64_xchunk(a, n, hi, tid);
+    v1 = c64_xchunk(a, n, hi, tid + kThreads);
+    v2 = c64_xchunk(a, n, hi, min(tid + 2 * kThreads, kRowChunks - 1));
+  };
+  auto load_dy = [&](int64_t r, uint4& v0, uint4& v1) {
+    const uint4* d = reinterpret_cast<const uint4*>(a.dy + r * a.W * kC);
+    v0 = d[min(tid, dchunks - 1)];
+    v1 = d[min(tid + kThreads, dchunks - 1)];
+  };
+  auto put_x = [&](int hi, int c, const uint4& v) {
+    if (c < kRowChunks)
+      *reinterpret_cast<uint4*>(ring + (hi & (kSlots - 1)) * kSlotB + (c >> 3) * kPxB + (c & 7) * 16) = v;
+  };
+  auto put_dy = [&](int c, const uint4& v) {
+    if (c < dchunks) *reinterpret_cast<uint4*>(dyt + (c >> 3) * kPxB + (c & 7) * 16) = v;
+  };
+  bool pa = false, in_lds = false;
+  for (int64_t row = r0; row < r1; ++row) {
+    if (!in_lds) {  // first row of the chunk or of an image: input rows h-1 .. h+1, dY row
+      for (int r = 0; r < 3; ++r)
+        for (int c = tid; c < kRowChunks; c += kThreads) put_x(h - 1 + r, c, c64_xchunk(a, n, h - 1 + r, c));
+      for (int c = tid; c < dchunks; c += kThreads)
+        put_dy(c, reinterpret_cast<const uint4*>(a.dy + row * a.W * kC)[c]);
+    }
+    __syncthreads();
+    const bool nxt1 = row + 1 < r1 && h + 1 < a.H;
+    const bool nxt2 = nxt1 && row + 2 < r1 && h + 2 < a.H;
+    if (nxt1 && !pa) {
+      load_x(h + 2, xa0, xa1, xa2);
+      load_dy(row + 1, da0, da1);
+      pa = true;
+    }
+    if (nxt2) {
+      load_x(h + 3, xb0, xb1, xb2);
+      load_dy(row + 2, db0, db1);
+    }
+    int so[3];
+#pragma unroll
+    for (int kh = 0; kh < 3; ++kh) so[kh] = ((h - 1 + kh) & (kSlots - 1)) * kSlotB;
+#pragma unroll
+    for (int ks = 0; ks < kMaxW / 16; ++ks) {
+      const unsigned char* ap = dyt + a_off + ks * 16 * kPxB;
+      const c64_bf16x8 af = c64_frag(ap, ap + 4 * kPxB);
+#pragma unroll
+      for (int t = 0; t < 9; ++t) {
+        const int kt = kt0 + t;  // tap = kt / 2, channel block = kt & 1 (kt0 is 0 or 9)
+        const int tap = kt >> 1, cb = kt & 1;
+        const int kh = tap / 3, kw = tap - 3 * (tap / 3);
+        const unsigned char* bp = ring + so[kh] + b_off + (ks * 16 + kw) * kPxB + cb * 64;
+        acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af, c64_frag(bp, bp + 4 * kPxB), acc[t], 0, 0, 0);
+      }
+    }
+    __syncthreads();  // every wave is done with this row's dY tile and window
+    if (pa) {
+      put_x(h + 2, tid, xa0);
+      put_x(h + 2, tid + kThreads, xa1);
+      put_x(h + 2, tid + 2 * kThreads, xa2);
+      put_dy(tid, da0);
+      put_dy(tid + kThreads, da1);
+    }
+    in_lds = pa;
+    xa0 = xb0; xa1 = xb1; xa2 = xb2; da0 = db0; da1 = db1;
+    pa = nxt2;
+    if (++h == a.H) { h = 0; ++n; }
+  }
+
+  float* out = a.part + int64_t(blockIdx.x) * kC * kK + (lane & 31);
+#pragma unroll
+  for (int t = 0; t < 9; ++t) {
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int co = 32 * ct + (r & 3) + 8 * (r >> 2) + 4 * lh;
+      out[co * kK + (kt0 + t) * 32] = acc[t][r];
+    }
+  }
+}
+
+__global__ __launch_bounds__(256) void c64_slice_kernel(const float* __restrict__ part, int nb,
+                                                        float* __restrict__ tmp) {
+  const int e = blockIdx.x * 256 + threadIdx.x;
+  if (e >= kC * kK) return;
+  const int sl = blockIdx.y, nsl = gridDim.y;
+  const int per = (nb + nsl - 1) / nsl;
+  const int b0 = sl * per, b1 = min(nb, b0 + per);
+  float s = 0.f;
+  for (int b = b0; b < b1; ++b) s += part[int64_t(b) * kC * kK + e];
+  tmp[int64_t(sl) * kC * kK + e] = s;
+}
+
+// [nsl][64][576] -> dW[co][ci][kh][kw] with element strides, fp32 or bf16, (+)=
+template <typename OutT>
+__global__ __launch_bounds__(256) void c64_final_kernel(const float* __restrict__ tmp, int nsl, OutT* __restrict__ dw,
+                                                        int64_t s0, int64_t s1, int64_t s2, int64_t s3,
+                                                        int accumulate) {
+  const int e = blockIdx.x * 256 + threadIdx.x;  // co * 576 + (kh * 3 + kw) * 64 + ci
+  if (e >= kC * kK) return;
+  const int co = e / kK, k = e - co * kK;
+  const int tap = k >> 6, ci = k & 63;
+  const int kh = tap / 3, kw = tap - 3 * kh;
+  float s = 0.f;
+  for (int sl = 0; sl < nsl; ++sl) s += tmp[int64_t(sl) * kC * kK + e];
+  OutT* o = dw + co * s0 + ci * s1 + kh * s2 + kw * s3;
+  if constexpr (sizeof(OutT) == 4) {
+    *reinterpret_cast<float*>(o) = s + (accumulate ? *reinterpret_cast<float*>(o) : 0.f);
+  } else {
+    uint16_t* q = reinterpret_cast<uint16_t*>(o);
+    *q = f2bf(s + (accumulate ? bf2f(*q) : 0.f));
+  }
+}
+
+int c64_grid() {
+  static int g = [] {
+    int dev = 0, cus = 256;
+    if (hipGetDevice(&dev) == hipSuccess) {
+      hipDeviceProp_t p;
+      if (hipGetDeviceProperties(&p, dev) == hipSuccess && p.multiProcessorCount > 0) cus = p.multiProcessorCount;
+    }
+    return cus;  // one 4-wave workgroup per CU: 144 accumulators + 2-deep prefetch > 256 VGPRs
+  }();
+  return g;
+}
+
+int c64_blocks(int N, int H) { return int(std::max<int64_t>(1, std::min<int64_t>(c64_grid(), int64_t(N) * H))); }
+
+}  // namespace
+
+int64_t conv3x3_c64_wgrad_workspace_floats(int N, int H) { return int64_t(c64_blocks(N, H) + 32) * kC * kK; }
+
+void conv3x3_c64_wgrad(uintptr_t x, uintptr_t dy, uintptr_t dw, int64_t s0, int64_t s1, int64_t s2, int64_t s3,
+                       uintptr_t ws, int N, int H, int W, bool accumulate, int out_dt, uintptr_t stream) {
+  VODA_CHECK(W >= 1 && W <= kMaxW && H >= 1, "conv3x3_c64_wgrad: image width must be 1..64");
+  VODA_CHECK(out_dt == kF32 || out_dt == kBF16, "conv3x3_c64_wgrad: dW must be fp32 or bf16");
+  VODA_CHECK(x % 16 == 0 && dy % 16 == 0 && ws % 16 == 0, "conv3x3_c64_wgrad: misaligned operands");
+  hipStream_t s = as_stream(stream);
+  const int nb = c64_blocks(N, H);
+  float* part = reinterpret_cast<float*>(ws);
+  float* tmp = part + int64_t(nb) * kC * kK;
+  const int nsl = std::min(32, nb);
+  C64Args a{reinterpret_cast<const uint16_t*>(x), reinterpret_cast<const uint16_t*>(dy), part, N, H, W};
+  hipLaunchKernelGGL(conv3x3_c64_wgrad_kernel, dim3(nb), dim3(kThreads), 0, s, a);
+  hipLaunchKernelGGL(c64_slice_kernel, dim3((kC * kK + 255) / 256, nsl), dim3(256), 0, s, part, nb, tmp);
+  if (out_dt == kF32)
+    hipLaunchKernelGGL((c64_final_kernel<float>), dim3((kC * kK + 255) / 256), dim3(256), 0, s, tmp, nsl,
+                       reinterpret_cast<float*>(dw), s0, s1, s2, s3, int(accumulate));
+  else
+    hipLaunchKernelGGL((c64_final_kernel<uint16_t>), dim3((kC * kK + 255) / 256), dim3(256), 0, s, tmp, nsl,
+                       reinterpret_cast<uint16_t*>(dw), s0, s1, s2, s3, int(accumulate));
+  check_launch();
+}
+
+}  // namespace voda

@@ -90,12 +90,36 @@ void bn_bwd(uintptr_t dy, uintptr_t mask, uintptr_t x, uintptr_t save_mean, uint
             uintptr_t dx, uintptr_t dres, uintptr_t dgamma, uintptr_t dbeta, uintptr_t workspace, int64_t M, int C,
             bool relu, bool accumulate, int dt, uintptr_t stream);
 
-// ---- ResNet stem: BN(train) + ReLU + max pool fused (batchnorm.hip) ----
+// ---- 3x3 / stride-1 conv weight gradient at 64 -> 64 channels (conv3x3_c64.hip) ----
+int64_t conv3x3_c64_wgrad_workspace_floats(int N, int H);
+void conv3x3_c64_wgrad(uintptr_t x, uintptr_t dy, uintptr_t dw, int64_t s0, int64_t s1, int64_t s2, int64_t s3,
+                       uintptr_t ws, int N, int H, int W, bool accumulate, int out_dt, uintptr_t stream);
+
+// ---- stride-s pixel subsampling of channels_last bf16 (gather, or dx[::s, ::s] += g) (pool.hip) ----
+void subsample2d(uintptr_t src, uintptr_t dst, int N, int H, int W, int C, int s, bool add, int dt, uintptr_t stream);
+
+// ---- global average pool backward, channels_last (pool.hip) ----
+void global_avgpool_bwd(uintptr_t g, uintptr_t dx, int N, int HW, int C, float scale, int g_dt, int dt,
+                        uintptr_t stream);
+
+// ---- ResNet stem: 7x7/2 convolution + BN statistics (stem.hip) ----
+int stem_partial_rows(int N, int Ho);
+void stem_pack(uintptr_t x, uintptr_t x4, int N, int C, int H, int W, int64_t sN, int64_t sC, int64_t sH, int64_t sW,
+               int dt, uintptr_t stream);
+int64_t stem_wgrad_workspace_floats(int N, int Ho);
+void stem_conv_wgrad(uintptr_t x4, uintptr_t dy, uintptr_t dw, int64_t s0, int64_t s1, int64_t s2, int64_t s3,
+                     int Cin, uintptr_t ws, int N, int H, int W, int Ho, int Wo, bool accumulate, int out_dt,
+                     uintptr_t stream);
+void stem_conv_fwd(uintptr_t x4, uintptr_t w, int64_t sw0, int64_t sw1, int64_t sw2, int64_t sw3, int Cin, int Cout,
+                   uintptr_t y, uintptr_t part, int nb, int N, int H, int W, int Ho, int Wo, uintptr_t stream);
+
+// ---- ResNet stem: BN(train) + ReLU + max pool fused (batchnorm.hip); pre_nb > 0: the
+// workspace already holds pre_nb partial rows of sum / sum of squares (stem_conv_fwd) ----
 int64_t bn_pool_workspace_floats(int N, int H, int C);
 void bn_pool_fwd_train(uintptr_t x, uintptr_t gamma, uintptr_t beta, uintptr_t running_mean, uintptr_t running_var,
                        uintptr_t save_mean, uintptr_t save_invstd, uintptr_t y, uintptr_t idx, uintptr_t workspace,
                        int N, int H, int W, int C, int Ho, int Wo, int k, int s, int p, float eps, float momentum,
-                       int dt, uintptr_t stream);
+                       int dt, uintptr_t stream, int pre_nb = 0);
 void bn_pool_bwd(uintptr_t dy, uintptr_t idx, uintptr_t x, uintptr_t save_mean, uintptr_t save_invstd,
                  uintptr_t gamma, uintptr_t dx, uintptr_t dgamma, uintptr_t dbeta, uintptr_t workspace, int N, int H,
                  int W, int C, int Ho, int Wo, int k, int s, int p, bool accumulate, int dt, uintptr_t stream);

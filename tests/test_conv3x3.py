@@ -105,3 +105,89 @@ def test_conv_wgrad_fp32_output(n, cin, cout, h, w, stride, splits):
     torch.cuda.synchronize()
     rel = float((g32 - want).norm() / want.norm())
     assert rel < 1e-4, rel
+
+
+@pytest.mark.parametrize("k,pad", [(3, 1), (3, 0), (5, 2), (7, 3), (1, 0)])
+def test_dgrad_as_forward_matches_conv2d_input(k, pad):
+    """dX of a stride-1 convolution == forward convolution of dY with the flipped,
+    channel-transposed filter (the VODA_CONV_DGRAD_FWD path), fp64 on the CPU."""
+    torch.manual_seed(k)
+    x = torch.randn(2, 6, 9, 11, dtype=torch.float64)
+    w = torch.randn(10, 6, k, k, dtype=torch.float64)
+    dy = torch.randn_like(F.conv2d(x, w, padding=pad))
+    want = torch.nn.grad.conv2d_input(x.shape, w, dy, stride=1, padding=pad)
+    torch.testing.assert_close(C.dgrad_as_forward(dy, w, pad), want)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("cin,cout", [(64, 64), (128, 128)])
+def test_convkxk_dgrad_forward_path_matches_autograd(monkeypatch, cin, cout):
+    """The ConvKxK layer with VODA_CONV_DGRAD_FWD on: bf16 input gradient == stock autograd's
+    (both are MIOpen bf16 convolutions; tolerance of bf16 rounding of the result)."""
+    monkeypatch.setattr(C, "DGRAD_FWD", True)
+    torch.manual_seed(0)
+    cl = torch.channels_last
+    m = C.ConvKxK(cin, cout, 3, stride=1, padding=1).cuda().bfloat16().to(memory_format=cl)
+    x = torch.randn(4, cin, 28, 28, device="cuda").bfloat16().to(memory_format=cl).requires_grad_()
+    y = m(x)
+    assert type(y.grad_fn).__name__.startswith("_ConvKxKFn")
+    dy = torch.randn_like(y)
+    y.backward(dy)
+    xr = x.detach().float().requires_grad_()
+    F.conv2d(xr, m.weight.float(), padding=1).backward(dy.float())
+    torch.testing.assert_close(x.grad.float(), xr.grad, rtol=2e-2, atol=2e-2 * xr.grad.abs().max().item())
+    assert m.weight.grad is not None
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n,h,w", [(2, 56, 56), (3, 17, 9), (1, 5, 64), (4, 30, 64), (2, 1, 1)])
+@pytest.mark.parametrize("out", ["fp32_acc", "bf16"])
+def test_conv3x3_c64_wgrad_vs_fp64(n, h, w, out):
+    """64 -> 64 3x3 / stride-1 weight gradient (csrc/hip/conv3x3_c64.hip): transposed-LDS-read
+    MFMA GEMM over the pixels, fp32 partials, two-pass reduce, vs fp64 conv2d_weight."""
+    torch.manual_seed(7)
+    cl = torch.channels_last
+    x = torch.randn(n, 64, h, w, device="cuda").bfloat16().to(memory_format=cl)
+    dy = torch.randn(n, 64, h, w, device="cuda").bfloat16().to(memory_format=cl)
+    want = torch.nn.grad.conv2d_weight(x.double(), (64, 64, 3, 3), dy.double(), stride=1, padding=1)
+    hip = C.N.hip()
+    ws = torch.empty(hip.conv3x3_c64_wgrad_workspace_floats(n, h), dtype=torch.float32, device="cuda")
+    if out == "fp32_acc":
+        base = torch.randn(64, 64, 3, 3, device="cuda").contiguous(memory_format=cl)
+        dw = base.clone()
+        hip.conv3x3_c64_wgrad(x.data_ptr(), dy.data_ptr(), dw.data_ptr(), *dw.stride(), ws.data_ptr(), n, h, w,
+                              True, C.N.dtype_code(dw.dtype), C.N.stream_of(x))
+        got, tol = (dw - base).double(), 1e-4
+    else:
+        dw = torch.empty(64, 64, 3, 3, device="cuda", dtype=torch.bfloat16)
+        hip.conv3x3_c64_wgrad(x.data_ptr(), dy.data_ptr(), dw.data_ptr(), *dw.stride(), ws.data_ptr(), n, h, w,
+                              False, C.N.dtype_code(dw.dtype), C.N.stream_of(x))
+        got, tol = dw.double(), 1e-2
+    torch.testing.assert_close(got, want, rtol=1e-2, atol=tol * want.abs().max().item())
+
+
+@pytest.mark.gpu
+def test_convkxk_c64_layer_uses_kernel_and_matches():
+    """A 64-channel ConvKxK under a flat-gradient optimizer: weight gradient from the c64
+    kernel into the fp32 flat buffer, input gradient as a forward conv."""
+    from vodascheduler_amd.ops.optim import make_optimizer
+    from vodascheduler_amd.utils.flat import grad_of
+
+    torch.manual_seed(8)
+    cl = torch.channels_last
+    m = C.ConvKxK(64, 64, 3, stride=1, padding=1).cuda().to(memory_format=cl).bfloat16()
+    ref_w = m.weight.detach().float().clone().requires_grad_(True)
+    opt = make_optimizer("sgd", m.parameters(), lr=0.0)
+    x = torch.randn(4, 64, 28, 28, device="cuda").bfloat16().to(memory_format=cl)
+    xg = x.detach().requires_grad_(True)
+    xr = x.float().detach().requires_grad_(True)
+    opt.zero_grad()
+    y = m(xg)
+    assert type(y.grad_fn).__name__.startswith("_ConvKxKFn")
+    yr = F.conv2d(xr, ref_w, padding=1)
+    g = torch.randn_like(yr)
+    y.backward(g.bfloat16().to(memory_format=cl))
+    yr.backward(g)
+    for got, want in ((grad_of(m.weight), ref_w.grad), (xg.grad, xr.grad)):
+        rel = float((got.float() - want).norm() / want.norm())
+        assert rel < 1e-2, rel

@@ -18,9 +18,11 @@ from __future__ import annotations
 import torch
 from torch import nn
 
-from ..ops.batchnorm import FusedBatchNorm2d, FusedBNReLUMaxPool2d
+from ..ops.batchnorm import FusedBatchNorm2d
 from ..ops.conv1x1 import USE_GRAD_SINK, Conv1x1, GradSink
 from ..ops.conv3x3 import ConvKxK
+from ..ops.pool import GlobalAvgPool2d
+from ..ops.stem import FusedStem
 
 
 class Bottleneck(nn.Module):
@@ -79,15 +81,15 @@ class ResNet(nn.Module):
         if small_input:  # CIFAR-style 32x32 stem
             self.stem = nn.Sequential(nn.Conv2d(3, 64, 3, padding=1, bias=False), FusedBatchNorm2d(64, relu=True))
         else:
-            # BN + ReLU + 3x3/2 max pool as one fused op (ops/batchnorm.FusedBNReLUMaxPool2d);
-            # state dict keys stem.0.* / stem.1.* as with a separate BN and pool
-            self.stem = nn.Sequential(nn.Conv2d(3, 64, 7, stride=2, padding=3, bias=False),
-                                      FusedBNReLUMaxPool2d(64, 3, stride=2, padding=1))
+            # conv 7x7/2 with the BN statistics in its epilogue, then BN + ReLU + 3x3/2 max
+            # pool as one fused op (ops/stem.FusedStem); state dict keys stem.0.* / stem.1.*
+            # as with a separate conv, BN and pool
+            self.stem = FusedStem(3, 64)
         self.layer1 = self._make(block, 64, layers[0])
         self.layer2 = self._make(block, 128, layers[1], stride=2)
         self.layer3 = self._make(block, 256, layers[2], stride=2)
         self.layer4 = self._make(block, 512, layers[3], stride=2)
-        self.pool = nn.AdaptiveAvgPool2d(1)
+        self.pool = GlobalAvgPool2d()  # nn.AdaptiveAvgPool2d(1), channels_last HIP backward
         self.fc = nn.Linear(512 * block.expansion, num_classes)
         for m in self.modules():
             if isinstance(m, nn.Conv2d):

@@ -152,25 +152,62 @@ def _pool_out(n: int, k: int, s: int, p: int) -> int:
     return (n + 2 * p - k) // s + 1
 
 
+def bn_pool_forward(x, weight, bias, running_mean, running_var, momentum, eps, k, s, p, ws=None, pre_nb=0):
+    """maxpool(relu(bn(x))) training forward; ``ws`` / ``pre_nb``: a workspace whose first
+    2 x pre_nb x C floats already hold the per-block sums / sums of squares of ``x`` (the
+    producing convolution's epilogue, ops/stem.py) -- the statistics pass is skipped.
+    Returns (y, idx, save_mean, save_invstd)."""
+    Nb, C, H, W = x.shape
+    Ho, Wo = _pool_out(H, k, s, p), _pool_out(W, k, s, p)
+    h = N.hip()
+    y = torch.empty(Nb, C, Ho, Wo, dtype=x.dtype, device=x.device, memory_format=torch.channels_last)
+    idx = torch.empty(Nb * Ho * Wo * C, dtype=torch.uint8, device=x.device)
+    save_mean = torch.empty(C, dtype=torch.float32, device=x.device)
+    save_invstd = torch.empty(C, dtype=torch.float32, device=x.device)
+    if ws is None:
+        ws = torch.empty(h.bn_pool_workspace_floats(Nb, H, C), dtype=torch.float32, device=x.device)
+    h.bn_pool_fwd_train(x.data_ptr(), N.ptr(weight), N.ptr(bias), N.ptr(running_mean), N.ptr(running_var),
+                        save_mean.data_ptr(), save_invstd.data_ptr(), y.data_ptr(), idx.data_ptr(), ws.data_ptr(),
+                        Nb, H, W, C, Ho, Wo, k, s, p, float(eps), float(momentum), N.dtype_code(x.dtype),
+                        N.stream_of(x), int(pre_nb))
+    return y, idx, save_mean, save_invstd
+
+
+def bn_pool_backward(dy, x, idx, weight, bias, save_mean, save_invstd, k, s, p, need_w, need_b):
+    """Gradients of :func:`bn_pool_forward`: (dx, dgamma, dbeta, direct) -- ``direct``: the
+    affine gradients went straight into the optimizer's flat fp32 buffers."""
+    Nb, C, H, W = x.shape
+    Ho, Wo = _pool_out(H, k, s, p), _pool_out(W, k, s, p)
+    h = N.hip()
+    dy = dy.to(x.dtype).contiguous(memory_format=torch.channels_last)
+    dx = torch.empty_like(x)
+    direct = (need_b and _direct_fp32(bias) and ((need_w and _direct_fp32(weight)) or weight is None))
+    if direct:
+        dw, db = flat_grad(weight), flat_grad(bias)
+    else:
+        dw = torch.empty(C, dtype=torch.float32, device=x.device) if need_w else None
+        db = torch.empty(C, dtype=torch.float32, device=x.device) if need_b else None
+    ws = torch.empty(h.bn_pool_workspace_floats(Nb, H, C), dtype=torch.float32, device=x.device)
+    h.bn_pool_bwd(dy.data_ptr(), idx.data_ptr(), x.data_ptr(), save_mean.data_ptr(), save_invstd.data_ptr(),
+                  N.ptr(weight), dx.data_ptr(), N.ptr(dw), N.ptr(db), ws.data_ptr(), Nb, H, W, C, Ho, Wo, k, s, p,
+                  direct, N.dtype_code(x.dtype), N.stream_of(x))
+    if direct:
+        if weight is not None:
+            _ready(weight)
+        _ready(bias)
+        return dx, None, None, True
+    return dx, dw, db, False
+
+
 class _BNPoolFn(torch.autograd.Function):
     """maxpool(relu(bn(x))) in training mode (csrc/hip/batchnorm.hip ``bn_pool_*``): the
     full-resolution BN output and its gradient are never written to memory."""
 
     @staticmethod
     def forward(ctx, x, weight, bias, running_mean, running_var, momentum, eps, k, s, p):
-        Nb, C, H, W = x.shape
-        Ho, Wo = _pool_out(H, k, s, p), _pool_out(W, k, s, p)
-        h = N.hip()
-        y = torch.empty(Nb, C, Ho, Wo, dtype=x.dtype, device=x.device, memory_format=torch.channels_last)
-        idx = torch.empty(Nb * Ho * Wo * C, dtype=torch.uint8, device=x.device)
-        save_mean = torch.empty(C, dtype=torch.float32, device=x.device)
-        save_invstd = torch.empty(C, dtype=torch.float32, device=x.device)
-        ws = torch.empty(h.bn_pool_workspace_floats(Nb, H, C), dtype=torch.float32, device=x.device)
-        h.bn_pool_fwd_train(x.data_ptr(), N.ptr(weight), N.ptr(bias), N.ptr(running_mean), N.ptr(running_var),
-                            save_mean.data_ptr(), save_invstd.data_ptr(), y.data_ptr(), idx.data_ptr(), ws.data_ptr(),
-                            Nb, H, W, C, Ho, Wo, k, s, p, float(eps), float(momentum), N.dtype_code(x.dtype),
-                            N.stream_of(x))
-        ctx.geom = (Nb, H, W, C, Ho, Wo, k, s, p)
+        y, idx, save_mean, save_invstd = bn_pool_forward(x, weight, bias, running_mean, running_var, momentum, eps,
+                                                         k, s, p)
+        ctx.pool = (k, s, p)
         ctx.bias = bias
         ctx.save_for_backward(x, idx, weight, save_mean, save_invstd)
         return y
@@ -178,28 +215,9 @@ class _BNPoolFn(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dy):
         x, idx, weight, save_mean, save_invstd = ctx.saved_tensors
-        Nb, H, W, C, Ho, Wo, k, s, p = ctx.geom
-        h = N.hip()
-        dy = dy.to(x.dtype).contiguous(memory_format=torch.channels_last)
-        dx = torch.empty_like(x)
         need_w = weight is not None and ctx.needs_input_grad[1]
-        need_b = ctx.needs_input_grad[2]
-        bias = ctx.bias
-        direct = (need_b and _direct_fp32(bias) and ((need_w and _direct_fp32(weight)) or weight is None))
-        if direct:
-            dw, db = flat_grad(weight), flat_grad(bias)
-        else:
-            dw = torch.empty(C, dtype=torch.float32, device=x.device) if need_w else None
-            db = torch.empty(C, dtype=torch.float32, device=x.device) if need_b else None
-        ws = torch.empty(h.bn_pool_workspace_floats(Nb, H, C), dtype=torch.float32, device=x.device)
-        h.bn_pool_bwd(dy.data_ptr(), idx.data_ptr(), x.data_ptr(), save_mean.data_ptr(), save_invstd.data_ptr(),
-                      N.ptr(weight), dx.data_ptr(), N.ptr(dw), N.ptr(db), ws.data_ptr(), Nb, H, W, C, Ho, Wo, k, s, p,
-                      direct, N.dtype_code(x.dtype), N.stream_of(x))
-        if direct:
-            if weight is not None:
-                _ready(weight)
-            _ready(bias)
-            return dx, None, None, None, None, None, None, None, None, None
+        dx, dw, db, _ = bn_pool_backward(dy, x, idx, weight, ctx.bias, save_mean, save_invstd, *ctx.pool, need_w,
+                                         ctx.needs_input_grad[2])
         return dx, dw, db, None, None, None, None, None, None, None
 
 

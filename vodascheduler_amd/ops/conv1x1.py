@@ -27,6 +27,7 @@ import torch
 import torch.nn.functional as F
 
 from ..utils.flat import flat_grad
+from . import _native as N
 from . import wgrad as W
 
 USE_CONV1X1_GEMM = os.environ.get("VODA_CONV1X1_GEMM", "1") != "0"
@@ -89,6 +90,33 @@ class _StridedGrad:
         return dx
 
 
+def _sub_ok(t: torch.Tensor) -> bool:
+    return (t.is_cuda and t.dim() == 4 and t.dtype == torch.bfloat16 and t.shape[1] % 8 == 0
+            and t.is_contiguous(memory_format=torch.channels_last) and t.data_ptr() % 16 == 0)
+
+
+def subsample(x: torch.Tensor, s: int) -> torch.Tensor:
+    """``x[:, :, ::s, ::s]`` as a dense channels_last tensor (pool.hip ``subsample2d`` for
+    channels_last bf16; a strided copy otherwise)."""
+    if not _sub_ok(x):
+        return x[:, :, ::s, ::s].contiguous(memory_format=torch.channels_last)
+    n, c, h, w = x.shape
+    y = torch.empty(n, c, (h + s - 1) // s, (w + s - 1) // s, dtype=x.dtype, device=x.device,
+                    memory_format=torch.channels_last)
+    N.hip().subsample2d(x.data_ptr(), y.data_ptr(), n, h, w, c, s, False, N.dtype_code(x.dtype), N.stream_of(x))
+    return y
+
+
+def subsample_add_(dx: torch.Tensor, g: torch.Tensor, s: int) -> None:
+    """``dx[:, :, ::s, ::s] += g`` in place."""
+    n, c, h, w = dx.shape
+    if _sub_ok(dx) and _sub_ok(g) and tuple(g.shape) == (n, c, (h + s - 1) // s, (w + s - 1) // s):
+        N.hip().subsample2d(g.data_ptr(), dx.data_ptr(), n, h, w, c, s, True, N.dtype_code(dx.dtype),
+                            N.stream_of(dx))
+    else:
+        dx[:, :, ::s, ::s].add_(g)
+
+
 def _direct(p: torch.Tensor) -> bool:
     return flat_grad(p) is not None
 
@@ -111,7 +139,7 @@ class _Conv1x1Fn(torch.autograd.Function):
         """``sink_in``: accumulate the input gradient into the tensor a producer left there
         (stride 1 only); ``sink_out``: hand the input gradient to a consumer instead of
         returning it."""
-        xs = x[:, :, ::stride, ::stride] if stride > 1 else x
+        xs = subsample(x, stride) if stride > 1 else x
         n, cin, h, w = xs.shape
         cout = weight.shape[0]
         x2 = _as_2d(xs)
@@ -148,7 +176,7 @@ class _Conv1x1Fn(torch.autograd.Function):
         if strided is not None:
             dx = (dy2 @ w2).view(n, h, w, cin).permute(0, 3, 1, 2)
             s_ = strided.stride
-            dx[:, :, ::s_, ::s_].add_(strided.g)
+            subsample_add_(dx, strided.g, strided.stride)
         elif acc is not None:
             _as_2d(acc).addmm_(dy2, w2)  # dX = shortcut gradient + dY . W (one GEMM, beta = 1)
             dx = acc

@@ -32,6 +32,60 @@ from ..utils.flat import FOLD_CAST, flat_grad
 from .conv1x1 import _direct, _ready
 
 USE_CONV_WGRAD = os.environ.get("VODA_CONV_WGRAD", "1") != "0"
+# VODA_CONV_DGRAD_FWD (default 1): the input gradient of a stride-1 KxK convolution runs as a
+# FORWARD convolution of dy with the transposed, spatially flipped filter
+#     dX[n, ci, h, w] = sum_{co, kh, kw} dY[n, co, h - kh + p, w - kw + p] * W[co, ci, kh, kw]
+#                     = conv2d(dY, W^T flipped, padding = K - 1 - p)
+# so MIOpen runs its forward solvers on it (the bottleneck 3x3 layers have Cin == Cout: the
+# very shape the forward pass already found) instead of the backward-data igemm solvers and
+# their output zero-fill (VERDICT r2 Next #4).  ResNet-50 bs-256 step, same box back to back:
+# 25.87 -> 25.57 ms (profiles/r3/ab_dgrad_fwd.md).
+DGRAD_FWD = os.environ.get("VODA_CONV_DGRAD_FWD", "1") != "0"
+
+
+# VODA_CONV_C64_WGRAD=0: the 64 -> 64 channel 3x3 weight gradient runs MIOpen (A/B switch)
+USE_C64_WGRAD = os.environ.get("VODA_CONV_C64_WGRAD", "1") != "0"
+
+
+def c64_ok(dy: torch.Tensor, x: torch.Tensor, weight: torch.Tensor, stride: int, padding: int) -> bool:
+    """The 64-channel 3x3 / stride-1 weight-gradient kernel (csrc/hip/conv3x3_c64.hip) covers
+    these operands: channels_last bf16 activations, width <= 64."""
+    cl = torch.channels_last
+    return (USE_C64_WGRAD and dy.is_cuda and stride == 1 and padding == 1 and tuple(weight.shape) == (64, 64, 3, 3)
+            and x.dtype == torch.bfloat16 and dy.dtype == torch.bfloat16 and x.dim() == 4
+            and x.shape == dy.shape and x.shape[3] <= 64 and x.is_contiguous(memory_format=cl)
+            and dy.is_contiguous(memory_format=cl) and x.data_ptr() % 16 == 0 and dy.data_ptr() % 16 == 0)
+
+
+def conv_c64_wgrad(dy: torch.Tensor, x: torch.Tensor, weight: torch.Tensor) -> torch.Tensor | None:
+    """dW of a 64 -> 64 3x3 / stride-1 convolution: added in fp32 into the optimizer's flat
+    gradient when it owns one (returns None), else returned in the weight's dtype."""
+    n, _, hh, ww = x.shape
+    h = N.hip()
+    ws = torch.empty(h.conv3x3_c64_wgrad_workspace_floats(n, hh), dtype=torch.float32, device=x.device)
+    gw = flat_grad(weight) if _direct(weight) else None
+    if gw is not None and gw.dtype in (torch.float32, torch.bfloat16):
+        h.conv3x3_c64_wgrad(x.data_ptr(), dy.data_ptr(), gw.data_ptr(), *gw.stride(), ws.data_ptr(), n, hh, ww, True,
+                            N.dtype_code(gw.dtype), N.stream_of(x))
+        _ready(weight)
+        return None
+    dw = torch.empty(weight.shape, dtype=torch.float32, device=x.device)
+    h.conv3x3_c64_wgrad(x.data_ptr(), dy.data_ptr(), dw.data_ptr(), *dw.stride(), ws.data_ptr(), n, hh, ww, False,
+                        N.dtype_code(dw.dtype), N.stream_of(x))
+    return dw.to(weight.dtype)
+
+
+def dgrad_as_forward(dy: torch.Tensor, weight: torch.Tensor, padding: int) -> torch.Tensor:
+    """Input gradient of a stride-1 KxK convolution as the forward convolution of ``dy`` with
+    the flipped, channel-transposed filter (channels_last in, channels_last out)."""
+    k = weight.shape[-1]
+    wt = weight.transpose(0, 1).flip(2, 3).contiguous(memory_format=torch.channels_last)
+    return F.conv2d(dy, wt, None, 1, k - 1 - padding)
+
+
+def dgrad_fwd_ok(weight: torch.Tensor, stride: int, padding: int) -> bool:
+    kh, kw = weight.shape[-2:]
+    return DGRAD_FWD and stride == 1 and kh == kw and 0 <= padding <= kh - 1
 
 
 def default_splits(M: int, Cout: int, Cin: int, taps: int, target_blocks: int = 432) -> int:
@@ -89,26 +143,30 @@ def supported(dy: torch.Tensor, x: torch.Tensor, gw: torch.Tensor) -> bool:
 
 class _ConvKxKFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, weight, stride: int, padding: int):
+    def forward(ctx, x, weight, stride: int, padding: int, kernel_wgrad: bool = True):
         y = F.conv2d(x, weight, None, stride, padding)
         ctx.save_for_backward(x, weight)
-        ctx.conf = (stride, padding)
+        ctx.conf = (stride, padding, kernel_wgrad)
         return y
 
     @staticmethod
     def backward(ctx, dy):
         x, weight = ctx.saved_tensors
-        stride, padding = ctx.conf
+        stride, padding, kernel_wgrad = ctx.conf
         if not dy.is_contiguous(memory_format=torch.channels_last):
             dy = dy.contiguous(memory_format=torch.channels_last)
         dx = None
-        if ctx.needs_input_grad[0]:
+        if ctx.needs_input_grad[0] and dgrad_fwd_ok(weight, stride, padding):
+            dx = dgrad_as_forward(dy, weight, padding)
+        elif ctx.needs_input_grad[0]:
             dx = torch.ops.aten.convolution_backward(dy, x, weight, None, [stride, stride], [padding, padding],
                                                      [1, 1], False, [0, 0], 1, [True, False, False])[0]
         dw = None
-        if ctx.needs_input_grad[1]:
+        if ctx.needs_input_grad[1] and not kernel_wgrad and c64_ok(dy, x, weight, stride, padding):
+            dw = conv_c64_wgrad(dy, x, weight)
+        elif ctx.needs_input_grad[1]:
             gw = flat_grad(weight) if _direct(weight) else None
-            if gw is not None and supported(dy, x, gw):
+            if gw is not None and kernel_wgrad and supported(dy, x, gw):
                 conv_wgrad_accumulate_(dy, x, gw, stride, padding)
                 _ready(weight)
             else:
@@ -118,7 +176,7 @@ class _ConvKxKFn(torch.autograd.Function):
                     gw.add_(dw.to(gw.dtype) if FOLD_CAST else dw)  # see utils/flat.FOLD_CAST
                     _ready(weight)
                     dw = None
-        return dx, dw, None, None
+        return dx, dw, None, None, None
 
 
 class ConvKxK(torch.nn.Conv2d):
@@ -129,17 +187,19 @@ class ConvKxK(torch.nn.Conv2d):
                  padding: int = 1, **kw):
         super().__init__(in_channels, out_channels, kernel_size, stride=stride, padding=padding, bias=False, **kw)
 
-    def _fast_ok(self, x: torch.Tensor) -> bool:
-        return (USE_CONV_WGRAD and x.is_cuda and x.dim() == 4 and x.dtype == torch.bfloat16
+    def _layout_ok(self, x: torch.Tensor) -> bool:
+        return (x.is_cuda and x.dim() == 4 and x.dtype == torch.bfloat16
                 and self.weight.dtype == torch.bfloat16 and self.groups == 1 and self.dilation == (1, 1)
                 and self.stride[0] == self.stride[1] and self.padding[0] == self.padding[1]
                 and isinstance(self.padding[0], int) and x.is_contiguous(memory_format=torch.channels_last)
                 and self.weight.is_contiguous(memory_format=torch.channels_last)
-                and self.in_channels % 8 == 0 and self.out_channels % 8 == 0
-                # 64-channel layers fill a quarter of the 128 x 128 MFMA tile: ResNet-50's
-                # layer1 3x3 weight gradient took 360 us here vs 150 us (+35 us of workspace
-                # passes) on MIOpen; from 128 channels on this kernel is the faster one
-                # (profiles/r1_conv3x3_wgrad.md)
+                and self.in_channels % 8 == 0 and self.out_channels % 8 == 0)
+
+    def _fast_ok(self, x: torch.Tensor) -> bool:
+        # 64-channel layers fill a quarter of the 128 x 128 MFMA tile: ResNet-50's layer1 3x3
+        # weight gradient took 360 us here vs 150 us (+35 us of workspace passes) on MIOpen;
+        # from 128 channels on this kernel is the faster one (profiles/r1_conv3x3_wgrad.md)
+        return (USE_CONV_WGRAD and self._layout_ok(x)
                 and self.in_channels >= 128 and self.out_channels >= 128)
 
     def forward(self, x):
@@ -147,5 +207,12 @@ class ConvKxK(torch.nn.Conv2d):
             x = x.to(self.weight.dtype)
         if self._fast_ok(x):
             with torch.autocast("cuda", enabled=False):
-                return _ConvKxKFn.apply(x, self.weight, self.stride[0], self.padding[0])
+                return _ConvKxKFn.apply(x, self.weight, self.stride[0], self.padding[0], True)
+        c64 = (USE_C64_WGRAD and self.in_channels == 64 and self.out_channels == 64 and self.kernel_size == (3, 3)
+               and self.stride[0] == 1 and self.padding[0] == 1)
+        if self._layout_ok(x) and (c64 or dgrad_fwd_ok(self.weight, self.stride[0], self.padding[0])):
+            # input gradient as a forward convolution (DGRAD_FWD); weight gradient on the
+            # 64-channel kernel (conv3x3_c64.hip) or MIOpen
+            with torch.autocast("cuda", enabled=False):
+                return _ConvKxKFn.apply(x, self.weight, self.stride[0], self.padding[0], False)
         return super().forward(x)

@@ -59,3 +59,41 @@ class FusedMaxPool2d(torch.nn.MaxPool2d):
                 and not self.ceil_mode and not self.return_indices:
             return max_pool2d(x, k, s, p)
         return super().forward(x)
+
+
+class _GlobalAvgPoolFn(torch.autograd.Function):
+    """mean over H, W of a channels_last [N, C, H, W] tensor -> [N, C, 1, 1]; the backward
+    writes the broadcast gradient straight into channels_last (``global_avgpool_bwd``)."""
+
+    @staticmethod
+    def forward(ctx, x):
+        ctx.shape = x.shape
+        ctx.dt = x.dtype
+        return x.mean((2, 3), keepdim=True)
+
+    @staticmethod
+    def backward(ctx, g):
+        Nb, C, H, W = ctx.shape
+        g2 = g.reshape(Nb, C)
+        if g2.dtype not in (torch.float32, torch.bfloat16) or (g2.dtype == torch.bfloat16 and ctx.dt != g2.dtype):
+            g2 = g2.float()
+        g2 = g2.contiguous()
+        dx = torch.empty(Nb, C, H, W, dtype=ctx.dt, device=g.device, memory_format=torch.channels_last)
+        N.hip().global_avgpool_bwd(g2.data_ptr(), dx.data_ptr(), Nb, H * W, C, 1.0 / (H * W),
+                                   N.dtype_code(g2.dtype), N.dtype_code(ctx.dt), N.stream_of(g))
+        return dx
+
+
+class GlobalAvgPool2d(torch.nn.AdaptiveAvgPool2d):
+    """``nn.AdaptiveAvgPool2d(1)`` (no state) whose training backward on channels_last GPU
+    tensors is one HIP kernel."""
+
+    def __init__(self):
+        super().__init__(1)
+
+    def forward(self, x):
+        if (x.is_cuda and x.dim() == 4 and x.requires_grad and x.dtype in (torch.bfloat16, torch.float32)
+                and x.shape[1] % 8 == 0 and x.is_contiguous(memory_format=torch.channels_last)
+                and x.data_ptr() % 16 == 0):
+            return _GlobalAvgPoolFn.apply(x)
+        return super().forward(x)
