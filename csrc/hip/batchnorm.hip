@@ -879,27 +879,30 @@ int64_t bn_workspace_floats(int64_t M, int C) {
 void bn_fwd_train(uintptr_t x, uintptr_t residual, uintptr_t gamma, uintptr_t beta, uintptr_t running_mean,
                   uintptr_t running_var, uintptr_t save_mean, uintptr_t save_invstd, uintptr_t y, uintptr_t mask,
                   uintptr_t workspace, int64_t M, int C, float eps, float momentum, bool relu, int dt,
-                  uintptr_t stream) {
+                  uintptr_t stream, int pre_nb) {
   VODA_CHECK(C % kVec == 0, "batchnorm: C must be a multiple of 8");
   VODA_CHECK(M > 0, "batchnorm: empty input");
   hipStream_t s = as_stream(stream);
   float* ws = reinterpret_cast<float*>(workspace);
+  // pre_nb > 0: the producing GEMM already wrote pre_nb partial rows (gemm_bnstats.hip)
   const Grid rg = reduce_grid(M, C);
-  float* ab = ws + int64_t(2) * rg.nb * C;
+  const int nb = pre_nb > 0 ? pre_nb : rg.nb;
+  float* ab = ws + int64_t(2) * nb * C;
   const Grid ag = apply_grid(M, C);
   const int sw = bn_tune().sweep;
   dispatch_dt(dt, [&](auto tag) {
     using T = decltype(tag);
     const T* xp = reinterpret_cast<const T*>(x);
     const int lv = bn_unroll_level();
-    if (lv >= 2)
+    if (pre_nb > 0) {
+    } else if (lv >= 2)
       hipLaunchKernelGGL((bn_stats_kernel<T, 16>), rg.grid, dim3(kBlock), 0, s, xp, ws, M, C, sw);
     else if (lv == 1)
       hipLaunchKernelGGL((bn_stats_kernel<T, 8>), rg.grid, dim3(kBlock), 0, s, xp, ws, M, C, sw);
     else
       hipLaunchKernelGGL((bn_stats_kernel<T, 4>), rg.grid, dim3(kBlock), 0, s, xp, ws, M, C, sw);
     hipLaunchKernelGGL(bn_fwd_finalize_kernel, dim3((C + kFinCh - 1) / kFinCh), dim3(kFinCh * kFinRg), 0, s, ws,
-                       rg.nb, M, C, reinterpret_cast<const float*>(gamma), reinterpret_cast<const float*>(beta),
+                       nb, M, C, reinterpret_cast<const float*>(gamma), reinterpret_cast<const float*>(beta),
                        reinterpret_cast<float*>(running_mean), reinterpret_cast<float*>(running_var),
                        reinterpret_cast<float*>(save_mean), reinterpret_cast<float*>(save_invstd), ab, eps, momentum);
     const T* rp = reinterpret_cast<const T*>(residual);

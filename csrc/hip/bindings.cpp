@@ -47,6 +47,9 @@ PYBIND11_MODULE(_vodahip, m) {
   m.def("bn_pool_fwd_train", &bn_pool_fwd_train);
   m.def("bn_pool_bwd", &bn_pool_bwd);
   m.def("global_avgpool_bwd", &global_avgpool_bwd);
+  m.def("gemm_bnstats_supported", &gemm_bnstats_supported);
+  m.def("gemm_bnstats_groups", &gemm_bnstats_groups);
+  m.def("gemm_bnstats", &gemm_bnstats);
   m.def("subsample2d", &subsample2d);
   m.def("conv3x3_c64_wgrad_workspace_floats", &conv3x3_c64_wgrad_workspace_floats);
   m.def("conv3x3_c64_wgrad", &conv3x3_c64_wgrad);

@@ -23,6 +23,7 @@
 //  * one fp32 partial [64][576] per workgroup; two small passes sum them and add the result
 //    into the optimizer's flat gradient with the weight's strides.
 #include "common.h"
+
 #include "ops.h"
 
 namespace voda {
@@ -184,36 +185,57 @@ __global__ __launch_bounds__(kThreads, 1) void conv3x3_c64_wgrad_kernel(C64Args 
   }
 }
 
-__global__ __launch_bounds__(256) void c64_slice_kernel(const float* __restrict__ part, int nb,
-                                                        float* __restrict__ tmp) {
+// partial sums in two passes: [nb][E] -> [nsl][E] (float4, each slice sums <= 8 partial rows)
+// -> dW.  (The first version summed nb / 32 scalar rows per thread and then 32 more: two
+// latency-bound ~10 us passes per call.)
+__global__ __launch_bounds__(256) void c64_slice_kernel(const float4* __restrict__ part, int nb, int e4,
+                                                        float4* __restrict__ tmp) {
   const int e = blockIdx.x * 256 + threadIdx.x;
-  if (e >= kC * kK) return;
+  if (e >= e4) return;
   const int sl = blockIdx.y, nsl = gridDim.y;
   const int per = (nb + nsl - 1) / nsl;
   const int b0 = sl * per, b1 = min(nb, b0 + per);
-  float s = 0.f;
-  for (int b = b0; b < b1; ++b) s += part[int64_t(b) * kC * kK + e];
-  tmp[int64_t(sl) * kC * kK + e] = s;
+  float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
+  for (int b = b0; b < b1; ++b) {
+    const float4 v = part[int64_t(b) * e4 + e];
+    s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
+  }
+  tmp[int64_t(sl) * e4 + e] = s;
 }
 
-// [nsl][64][576] -> dW[co][ci][kh][kw] with element strides, fp32 or bf16, (+)=
+// [nsl][64][576] -> dW[co][ci][kh][kw] with element strides, fp32 or bf16, (+)=; 4 consecutive
+// ci per thread (one float4 of every slice)
 template <typename OutT>
-__global__ __launch_bounds__(256) void c64_final_kernel(const float* __restrict__ tmp, int nsl, OutT* __restrict__ dw,
+__global__ __launch_bounds__(256) void c64_final_kernel(const float4* __restrict__ tmp, int nsl, OutT* __restrict__ dw,
                                                         int64_t s0, int64_t s1, int64_t s2, int64_t s3,
                                                         int accumulate) {
-  const int e = blockIdx.x * 256 + threadIdx.x;  // co * 576 + (kh * 3 + kw) * 64 + ci
-  if (e >= kC * kK) return;
+  const int e4 = blockIdx.x * 256 + threadIdx.x;  // (co * 576 + (kh * 3 + kw) * 64 + ci) / 4
+  if (e4 >= kC * kK / 4) return;
+  const int e = 4 * e4;
   const int co = e / kK, k = e - co * kK;
   const int tap = k >> 6, ci = k & 63;
   const int kh = tap / 3, kw = tap - 3 * kh;
-  float s = 0.f;
-  for (int sl = 0; sl < nsl; ++sl) s += tmp[int64_t(sl) * kC * kK + e];
-  OutT* o = dw + co * s0 + ci * s1 + kh * s2 + kw * s3;
-  if constexpr (sizeof(OutT) == 4) {
-    *reinterpret_cast<float*>(o) = s + (accumulate ? *reinterpret_cast<float*>(o) : 0.f);
-  } else {
-    uint16_t* q = reinterpret_cast<uint16_t*>(o);
-    *q = f2bf(s + (accumulate ? bf2f(*q) : 0.f));
+  float4 s0v = make_float4(0.f, 0.f, 0.f, 0.f), s1v = s0v;
+  int sl = 0;
+  for (; sl + 1 < nsl; sl += 2) {
+    const float4 a = tmp[int64_t(sl) * (kC * kK / 4) + e4], b = tmp[int64_t(sl + 1) * (kC * kK / 4) + e4];
+    s0v.x += a.x; s0v.y += a.y; s0v.z += a.z; s0v.w += a.w;
+    s1v.x += b.x; s1v.y += b.y; s1v.z += b.z; s1v.w += b.w;
+  }
+  if (sl < nsl) {
+    const float4 a = tmp[int64_t(sl) * (kC * kK / 4) + e4];
+    s0v.x += a.x; s0v.y += a.y; s0v.z += a.z; s0v.w += a.w;
+  }
+  const float v[4] = {s0v.x + s1v.x, s0v.y + s1v.y, s0v.z + s1v.z, s0v.w + s1v.w};
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    OutT* o = dw + co * s0 + (ci + q) * s1 + kh * s2 + kw * s3;
+    if constexpr (sizeof(OutT) == 4) {
+      *reinterpret_cast<float*>(o) = v[q] + (accumulate ? *reinterpret_cast<float*>(o) : 0.f);
+    } else {
+      uint16_t* p = reinterpret_cast<uint16_t*>(o);
+      *p = f2bf(v[q] + (accumulate ? bf2f(*p) : 0.f));
+    }
   }
 }
 
@@ -233,7 +255,11 @@ int c64_blocks(int N, int H) { return int(std::max<int64_t>(1, std::min<int64_t>
 
 }  // namespace
 
-int64_t conv3x3_c64_wgrad_workspace_floats(int N, int H) { return int64_t(c64_blocks(N, H) + 32) * kC * kK; }
+constexpr int kMaxSlices = 64;
+
+int64_t conv3x3_c64_wgrad_workspace_floats(int N, int H) {
+  return int64_t(c64_blocks(N, H) + kMaxSlices) * kC * kK;
+}
 
 void conv3x3_c64_wgrad(uintptr_t x, uintptr_t dy, uintptr_t dw, int64_t s0, int64_t s1, int64_t s2, int64_t s3,
                        uintptr_t ws, int N, int H, int W, bool accumulate, int out_dt, uintptr_t stream) {
@@ -244,16 +270,20 @@ void conv3x3_c64_wgrad(uintptr_t x, uintptr_t dy, uintptr_t dw, int64_t s0, int6
   const int nb = c64_blocks(N, H);
   float* part = reinterpret_cast<float*>(ws);
   float* tmp = part + int64_t(nb) * kC * kK;
-  const int nsl = std::min(32, nb);
+  const int nsl = std::min(kMaxSlices, nb);
   C64Args a{reinterpret_cast<const uint16_t*>(x), reinterpret_cast<const uint16_t*>(dy), part, N, H, W};
   hipLaunchKernelGGL(conv3x3_c64_wgrad_kernel, dim3(nb), dim3(kThreads), 0, s, a);
-  hipLaunchKernelGGL(c64_slice_kernel, dim3((kC * kK + 255) / 256, nsl), dim3(256), 0, s, part, nb, tmp);
+  const int e4 = kC * kK / 4;
+  hipLaunchKernelGGL(c64_slice_kernel, dim3((e4 + 255) / 256, nsl), dim3(256), 0, s,
+                     reinterpret_cast<const float4*>(part), nb, e4, reinterpret_cast<float4*>(tmp));
   if (out_dt == kF32)
-    hipLaunchKernelGGL((c64_final_kernel<float>), dim3((kC * kK + 255) / 256), dim3(256), 0, s, tmp, nsl,
-                       reinterpret_cast<float*>(dw), s0, s1, s2, s3, int(accumulate));
+    hipLaunchKernelGGL((c64_final_kernel<float>), dim3((e4 + 255) / 256), dim3(256), 0, s,
+                       reinterpret_cast<const float4*>(tmp), nsl, reinterpret_cast<float*>(dw), s0, s1, s2, s3,
+                       int(accumulate));
   else
-    hipLaunchKernelGGL((c64_final_kernel<uint16_t>), dim3((kC * kK + 255) / 256), dim3(256), 0, s, tmp, nsl,
-                       reinterpret_cast<uint16_t*>(dw), s0, s1, s2, s3, int(accumulate));
+    hipLaunchKernelGGL((c64_final_kernel<uint16_t>), dim3((e4 + 255) / 256), dim3(256), 0, s,
+                       reinterpret_cast<const float4*>(tmp), nsl, reinterpret_cast<uint16_t*>(dw), s0, s1, s2, s3,
+                       int(accumulate));
   check_launch();
 }
 

@@ -83,12 +83,18 @@ std::vector<int> bn_get_tuning();
 void bn_fwd_train(uintptr_t x, uintptr_t residual, uintptr_t gamma, uintptr_t beta, uintptr_t running_mean,
                   uintptr_t running_var, uintptr_t save_mean, uintptr_t save_invstd, uintptr_t y, uintptr_t mask,
                   uintptr_t workspace, int64_t M, int C, float eps, float momentum, bool relu, int dt,
-                  uintptr_t stream);
+                  uintptr_t stream, int pre_nb = 0);
 void bn_apply(uintptr_t x, uintptr_t residual, uintptr_t ab, uintptr_t y, int64_t M, int C, bool relu, int dt,
               uintptr_t stream);
 void bn_bwd(uintptr_t dy, uintptr_t mask, uintptr_t x, uintptr_t save_mean, uintptr_t save_invstd, uintptr_t gamma,
             uintptr_t dx, uintptr_t dres, uintptr_t dgamma, uintptr_t dbeta, uintptr_t workspace, int64_t M, int C,
             bool relu, bool accumulate, int dt, uintptr_t stream);
+
+// ---- 1x1 conv forward GEMM with BN statistics in the epilogue (gemm_bnstats.hip) ----
+bool gemm_bnstats_supported(int64_t M, int N, int K);
+int gemm_bnstats_groups(int64_t M, int N, int K);
+void gemm_bnstats(uintptr_t x, uintptr_t w, uintptr_t y, uintptr_t part, int64_t M, int N, int K, int G,
+                  uintptr_t stream);
 
 // ---- 3x3 / stride-1 conv weight gradient at 64 -> 64 channels (conv3x3_c64.hip) ----
 int64_t conv3x3_c64_wgrad_workspace_floats(int N, int H);

@@ -26,6 +26,9 @@
 //  * the output tile is transposed through LDS (row stride 144 B) and written as 16-byte
 //    stores of whole 128-byte pixel rows (channels_last).
 #include "common.h"
+
+#include <cstdlib>
+#include <type_traits>
 #include "ops.h"
 
 namespace voda {
@@ -44,7 +47,6 @@ constexpr int kSMaxWo = kSWaves * kSTile;       // 128
 constexpr int kSRowPx = 2 * kSMaxWo + 8;        // 264 LDS pixels per input row
 constexpr int kSRowB = kSRowPx * 8;             // 2112 B
 constexpr int kSOutStride = 144;                // B per staged output pixel (128 + 16 pad)
-constexpr int kSOutB = kSTile * kSOutStride;    // 4608 B per wave
 constexpr int kSKSteps = kSK * 2;               // 14
 constexpr int kSSlots = 16;                     // LDS ring of input rows (>= 7 in use + 2 refilled)
 constexpr int kSPf = (2 * kSRowPx + kSThreads - 1) / kSThreads;  // prefetch slots per thread (3)
@@ -57,6 +59,8 @@ struct StemArgs {
   uint16_t* y;           // [N][Ho][Wo][64] bf16
   float* part;           // [2][gridDim.x][64]
   int N, H, W, Ho, Wo;
+  int dbg;               // VODA_STEM_DEBUG bit mask (benchmarks/bench_stem.py ablations; 0 in use):
+                         // 1 no output stores, 2 no prefetch loads, 4 no MFMAs, 8 no epilogue
 };
 
 __device__ __forceinline__ st_f32x16 st_mfma(st_bf16x8 a, st_bf16x8 b, st_f32x16 c) {
@@ -73,48 +77,83 @@ __device__ __forceinline__ uint2 st_pixel(const uint2* x4, int H, int W, int64_t
   return make_uint2(v.x & m, v.y & m);
 }
 
+// the 7 input rows of output row ho into the ring, loads issued in batches of B before their
+// LDS writes (a load-then-write loop waited out one global latency per element: 8 per thread)
+template <int B>
+__device__ __forceinline__ void st_fill_window(unsigned char* ring, const uint2* x4, int H, int W, int64_t n, int ho,
+                                               int tid) {
+  constexpr int kTotal = kSK * kSRowPx;                    // 1848
+  constexpr int kIters = (kTotal + kSThreads - 1) / kSThreads;  // 8
+#pragma unroll
+  for (int b = 0; b < kIters; b += B) {
+    uint2 v[B];
+#pragma unroll
+    for (int u = 0; u < B; ++u) {
+      const int i = min(tid + (b + u) * kSThreads, kTotal - 1);
+      const int r = i / kSRowPx, j = i - r * kSRowPx;
+      v[u] = st_pixel(x4, H, W, n, kSS * ho - kSP + r, j - kSP);
+    }
+#pragma unroll
+    for (int u = 0; u < B; ++u) {
+      const int i = tid + (b + u) * kSThreads;
+      if (i < kTotal) {
+        const int r = i / kSRowPx, j = i - r * kSRowPx;
+        *reinterpret_cast<uint2*>(ring + ((kSS * ho - kSP + r) & (kSSlots - 1)) * kSRowB + j * 8) = v[u];
+      }
+    }
+  }
+}
+
 __global__ __launch_bounds__(kSThreads, 2) void stem_conv7x7_fwd_kernel(StemArgs a) {
   // input rows live in a ring of kSSlots LDS rows, slot = hi & (kSSlots - 1): consecutive
   // output rows share 5 of their 7 input rows, so the steady state loads 2 new rows per
-  // output row -- prefetched into registers while the MFMAs of the current row run
+  // output row -- prefetched into registers while the MFMAs of earlier rows run
   __shared__ __attribute__((aligned(16))) unsigned char lds_in[kSSlots * kSRowB];
-  __shared__ __attribute__((aligned(16))) unsigned char lds_out[kSWaves * kSOutB];
-  __shared__ float red[kSWaves][2][kSCo];
+  __shared__ __attribute__((aligned(16))) unsigned char lds_out[kSMaxWo * kSOutStride];
+  __shared__ float red[kSWaves][2][32];
 
   const int tid = threadIdx.x;
   const int wave = tid >> 6, lane = tid & 63;
   const int lc = lane & 31, lh = lane >> 5;
+  // wave = (channel tile ct) x (64-pixel half ph): 14 filter fragments per lane (56 VGPRs)
+  // instead of 28 -- the 2-tile variant sat at the 256-register limit with spills
+  const int ct = wave & 1, ph = wave >> 1;
 
-  // filter fragments: B[k][co] for co = 32 t + lc, k-chunk = 8 lh .. 8 lh + 7 of k-step ks
-  // (kh = ks / 2, pixels kw = 4 (ks & 1) + 2 lh + q, q = 0, 1, channels 0..3), packed into
-  // 32-bit pairs once (built element-wise, the compiler re-packed them with v_perm_b32 inside
-  // the row loop: 112 extra VALU per row, ~4x the MFMA issue time of the row)
-  st_bf16x8 wf[2][kSKSteps];
+  // filter fragments: B[k][co] for co = 32 ct + lc, k-chunk = 8 lh .. 8 lh + 7 of k-step ks
+  // (kh = ks / 2, pixels kw = 4 (ks & 1) + 2 lh + q, q = 0, 1, channels 0..3).  The workgroup
+  // first packs the filter as [64][224] bf16 (zeros at kw = 7 and past Cin) into the ring's
+  // LDS (coalesced 2-byte loads, 14 in flight per thread), then every lane reads its
+  // fragments as 16-byte LDS reads.  (Per-lane gathers -- 224 dependent 2-byte global loads per
+  // lane -- were a large part of a ~50 us fixed cost per launch.)
+  {
+    uint16_t* wp = reinterpret_cast<uint16_t*>(lds_in);
+    constexpr int kWElems = kSCo * kSKSteps * 16;  // 14336
+    constexpr int kPer = kWElems / kSThreads;       // 56
 #pragma unroll
-  for (int t = 0; t < 2; ++t) {
+    for (int b = 0; b < kPer; b += 14) {
+      uint16_t v[14];
 #pragma unroll
-    for (int ks = 0; ks < kSKSteps; ++ks) {
-      const int kh = ks >> 1;
-      uint32_t u[4];
-#pragma unroll
-      for (int q = 0; q < 2; ++q) {
-        const int kw = 4 * (ks & 1) + 2 * lh + q;
-#pragma unroll
-        for (int c2 = 0; c2 < 2; ++c2) {
-          uint32_t lo = 0, hi = 0;
-          const int64_t base = (32 * t + lc) * a.sw0 + kh * a.sw2 + kw * a.sw3;
-          if (kw < kSK && 2 * c2 < a.cin) lo = a.w[base + 2 * c2 * a.sw1];
-          if (kw < kSK && 2 * c2 + 1 < a.cin) hi = a.w[base + (2 * c2 + 1) * a.sw1];
-          u[q * 2 + c2] = lo | (hi << 16);
-        }
+      for (int i = 0; i < 14; ++i) {
+        const int e = tid + (b + i) * kSThreads;
+        const int co = e / (kSKSteps * 16), k = e - co * (kSKSteps * 16);
+        const int kh = k >> 5, kw = (k >> 2) & 7, c = k & 3;
+        v[i] = (kw < kSK && c < a.cin) ? a.w[co * a.sw0 + c * a.sw1 + kh * a.sw2 + kw * a.sw3] : uint16_t(0);
       }
-      uint4 pk = make_uint4(u[0], u[1], u[2], u[3]);
-      // opaque to the optimizer: keeps the packed fragment resident instead of re-packing
-      // it from 16-bit pieces inside the row loop (register-pressure rematerialisation)
-      asm volatile("" : "+v"(pk.x), "+v"(pk.y), "+v"(pk.z), "+v"(pk.w));
-      wf[t][ks] = __builtin_bit_cast(st_bf16x8, pk);
+#pragma unroll
+      for (int i = 0; i < 14; ++i) wp[tid + (b + i) * kSThreads] = v[i];
     }
   }
+  __syncthreads();
+  st_bf16x8 wf[kSKSteps];
+#pragma unroll
+  for (int ks = 0; ks < kSKSteps; ++ks) {
+    uint4 pk = *reinterpret_cast<const uint4*>(lds_in + ((32 * ct + lc) * kSKSteps * 16 + ks * 16 + 8 * lh) * 2);
+    // opaque to the optimizer: keeps the fragment resident instead of re-deriving it inside
+    // the row loop (register-pressure rematerialisation)
+    asm volatile("" : "+v"(pk.x), "+v"(pk.y), "+v"(pk.z), "+v"(pk.w));
+    wf[ks] = __builtin_bit_cast(st_bf16x8, pk);
+  }
+  __syncthreads();  // the ring's LDS is reused below
 
   // this thread's share of a 2-row refill: slots tid, tid + 256, tid + 512 of 2 x kSRowPx
   int pr[kSPf], pj[kSPf];
@@ -125,130 +164,130 @@ __global__ __launch_bounds__(kSThreads, 2) void stem_conv7x7_fwd_kernel(StemArgs
     pj[k] = i < 2 * kSRowPx ? i - (i / kSRowPx) * kSRowPx : 0;
   }
 
-  float s1[2] = {0.f, 0.f}, s2[2] = {0.f, 0.f};
+  float s1 = 0.f, s2 = 0.f;  // channel 32 ct + lc, pixel rows of half lh
   const int64_t rows = int64_t(a.N) * a.Ho;
   const int64_t per = (rows + gridDim.x - 1) / gridDim.x;
   const int64_t r0 = int64_t(blockIdx.x) * per;
   const int64_t r1 = r0 + per < rows ? r0 + per : rows;
-  const int wo = wave * kSTile + lc;  // this lane's output pixel as an MFMA A row
-  unsigned char* my_out = lds_out + wave * kSOutB;
+  const int px0 = 64 * ph;             // this wave's first output pixel
+  const int wo0 = px0 + lc;            // MFMA A rows of pixel tile 0 (tile 1: + 32)
 
   int64_t n = r0 / a.Ho;
   int ho = int(r0 - n * a.Ho);
-  // two rows of prefetch in flight: the 2 new input rows of row + 1 (pfa, written into the
-  // ring after this row's MFMAs) and of row + 2 (pfb, issued now) -- a global load's latency
-  // (~1-2 us) is longer than one row's MFMA work (~0.4 us), so a one-row-ahead prefetch left
-  // every row waiting on its own loads
-  uint2 pfa[kSPf], pfb[kSPf];
-  bool pa = false;      // pfa holds row + 1's new input rows
-  bool in_lds = false;  // this row's window is complete in the ring
-  auto load_rows = [&](uint2 (&dst)[kSPf], int hbase) {
+  // two rows of prefetch in flight: the 2 new input rows of row + 1 (written into the ring
+  // after this row's MFMAs) and of row + 2 (issued now) -- a global load's latency
+  // (~1-2 us) is longer than one row's MFMA work (~0.4 us)
+  // Two register buffers alternate roles row by row (the loop body is instantiated twice);
+  // a buffer copy-rotation at the end of each row made every row wait for the loads it had just
+  // issued (vmcnt is in order), i.e. a one-row prefetch distance again.
+  uint2 pf[2][kSPf];
+  bool vv[2] = {false, false};  // buffer b holds the next row's 2 new input rows
+  bool in_lds = false;          // this row's window is complete in the ring
+  auto load_rows = [&](uint2 (&dst)[kSPf], int hbase) __attribute__((always_inline)) {
 #pragma unroll
     for (int k = 0; k < kSPf; ++k) dst[k] = st_pixel(a.x4, a.H, a.W, n, hbase + max(pr[k], 0), pj[k] - kSP);
   };
-  for (int64_t row = r0; row < r1; ++row) {
+  // buffer [B]: row + 1's new rows (valid if vv[B]); [1 - B]: receives row + 2's new rows
+  auto step = [&](int64_t row, auto bc) __attribute__((always_inline)) {
+    constexpr int B = decltype(bc)::value, O = 1 - B;
     // ---- this row's input window: hi = 2 ho - 3 .. 2 ho + 3
-    if (!in_lds) {  // first row of the chunk or of an image: all 7 rows
-      for (int i = tid; i < kSK * kSRowPx; i += kSThreads) {
-        const int r = i / kSRowPx, j = i - r * kSRowPx;
-        const int hi = kSS * ho - kSP + r;
-        *reinterpret_cast<uint2*>(lds_in + (hi & (kSSlots - 1)) * kSRowB + j * 8) = st_pixel(a.x4, a.H, a.W, n, hi, j - kSP);
-      }
-    }
+    if (!in_lds) st_fill_window<4>(lds_in, a.x4, a.H, a.W, n, ho, tid);  // first row of a chunk / image
     __syncthreads();
     // ---- prefetch (same image only): rows 2 ho + 4, 2 ho + 5 for row + 1 unless already in
     // flight, rows 2 ho + 6, 2 ho + 7 for row + 2
     const bool nxt1 = row + 1 < r1 && ho + 1 < a.Ho;
     const bool nxt2 = nxt1 && row + 2 < r1 && ho + 2 < a.Ho;
-    if (nxt1 && !pa) {
-      load_rows(pfa, kSS * ho + 4);
-      pa = true;
+    if (nxt1 && !vv[B]) {
+      if (!(a.dbg & 2)) load_rows(pf[B], kSS * ho + 4);
+      vv[B] = true;
     }
-    if (nxt2) load_rows(pfb, kSS * ho + 6);
-    // ---- 14 k-steps, 2 channel tiles
+    vv[O] = nxt2;
+    if (nxt2 && !(a.dbg & 2)) load_rows(pf[O], kSS * ho + 6);
+    // ---- 14 k-steps (kh-outer, 2 per kh), 2 pixel tiles of 32
     st_f32x16 acc0 = {}, acc1 = {};
 #pragma unroll
-    for (int ks = 0; ks < kSKSteps; ++ks) {
-      const int kh = ks >> 1;
+    for (int kh = 0; kh < kSK; ++kh) {
+      if (a.dbg & 4) break;
       const int slot = (kSS * ho - kSP + kh) & (kSSlots - 1);
-      const int off = slot * kSRowB + (2 * wo + 4 * (ks & 1) + 2 * lh) * 8;
-      const st_bf16x8 pfr = *reinterpret_cast<const st_bf16x8*>(lds_in + off);
-      acc0 = st_mfma(pfr, wf[0][ks], acc0);
-      acc1 = st_mfma(pfr, wf[1][ks], acc1);
+      const int off = slot * kSRowB + (2 * wo0 + 2 * lh) * 8;
+      const st_bf16x8 p00 = *reinterpret_cast<const st_bf16x8*>(lds_in + off);
+      const st_bf16x8 p10 = *reinterpret_cast<const st_bf16x8*>(lds_in + off + 2 * 32 * 8);
+      const st_bf16x8 p01 = *reinterpret_cast<const st_bf16x8*>(lds_in + off + 4 * 8);
+      const st_bf16x8 p11 = *reinterpret_cast<const st_bf16x8*>(lds_in + off + 2 * 32 * 8 + 4 * 8);
+      acc0 = st_mfma(p00, wf[2 * kh], acc0);
+      acc1 = st_mfma(p10, wf[2 * kh], acc1);
+      acc0 = st_mfma(p01, wf[2 * kh + 1], acc0);
+      acc1 = st_mfma(p11, wf[2 * kh + 1], acc1);
     }
-    // ---- row + 1's 2 new input rows into their ring slots (outside this row's window).
-    // Written here, before this row's output stores are issued: the wait for those loads
-    // then never covers stores of the same row (vmcnt counts loads and stores in issue
-    // order)
-    if (pa) {
+    // ---- row + 1's 2 new input rows into their ring slots (outside this row's window),
+    // before this row's output stores are issued
+    if (vv[B]) {
 #pragma unroll
       for (int k = 0; k < kSPf; ++k)
         if (pr[k] >= 0) {
           const int hi = kSS * ho + 4 + pr[k];
-          *reinterpret_cast<uint2*>(lds_in + (hi & (kSSlots - 1)) * kSRowB + pj[k] * 8) = pfa[k];
+          *reinterpret_cast<uint2*>(lds_in + (hi & (kSSlots - 1)) * kSRowB + pj[k] * 8) = pf[B][k];
         }
     }
-    in_lds = pa;
+    in_lds = vv[B];
+    vv[B] = false;
+    // ---- epilogue: statistics of the valid pixels, bf16 tile into the staging rows
+    if (!(a.dbg & 8)) {
+      auto stats = [&](const st_f32x16& acc, int tbase) {
+        if (tbase + 32 <= a.Wo) {  // full tile (wave-uniform): no masking
 #pragma unroll
-    for (int k = 0; k < kSPf; ++k) pfa[k] = pfb[k];
-    pa = nxt2;
-    // ---- epilogue: statistics (valid pixels only), bf16 tile into the staging buffer
-    if (wave * kSTile + kSTile <= a.Wo) {  // full tile (wave-uniform): no masking
+          for (int r = 0; r < 16; ++r) { s1 += acc[r]; s2 = fmaf(acc[r], acc[r], s2); }
+        } else if (tbase < a.Wo) {
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const float keep = tbase + (r & 3) + 8 * (r >> 2) + 4 * lh < a.Wo ? 1.f : 0.f;
+            const float v = acc[r] * keep;
+            s1 += v; s2 = fmaf(v, v, s2);
+          }
+        }
+      };
+      stats(acc0, px0);
+      stats(acc1, px0 + 32);
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
-        s1[0] += acc0[r]; s2[0] = fmaf(acc0[r], acc0[r], s2[0]);
-        s1[1] += acc1[r]; s2[1] = fmaf(acc1[r], acc1[r], s2[1]);
+        const int px = px0 + (r & 3) + 8 * (r >> 2) + 4 * lh;
+        *reinterpret_cast<uint16_t*>(lds_out + px * kSOutStride + (32 * ct + lc) * 2) = f2bf(acc0[r]);
+        *reinterpret_cast<uint16_t*>(lds_out + (px + 32) * kSOutStride + (32 * ct + lc) * 2) = f2bf(acc1[r]);
       }
-    } else {
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int px = (r & 3) + 8 * (r >> 2) + 4 * lh;
-        const float keep = wave * kSTile + px < a.Wo ? 1.f : 0.f;
-        const float v0 = acc0[r] * keep, v1 = acc1[r] * keep;
-        s1[0] += v0; s2[0] = fmaf(v0, v0, s2[0]);
-        s1[1] += v1; s2[1] = fmaf(v1, v1, s2[1]);
-      }
-    }
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const int px = (r & 3) + 8 * (r >> 2) + 4 * lh;
-      *reinterpret_cast<uint16_t*>(my_out + px * kSOutStride + lc * 2) = f2bf(acc0[r]);
-      *reinterpret_cast<uint16_t*>(my_out + px * kSOutStride + (32 + lc) * 2) = f2bf(acc1[r]);
     }
     __syncthreads();  // staging complete; every wave is done reading this row's window
-    // ---- whole 128-byte pixel rows out: 32 px x 8 chunks of 16 B per wave
+    // ---- whole 128-byte pixel rows out: wave w stores pixels 32 w .. 32 w + 31
     uint16_t* ybase = a.y + (row * a.Wo + wave * kSTile) * kSCo;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int q = i * 64 + lane;
       const int px = q >> 3, part = q & 7;
-      if (wave * kSTile + px < a.Wo) {
-        const uint4 v = *reinterpret_cast<const uint4*>(my_out + px * kSOutStride + part * 16);
+      if (wave * kSTile + px < a.Wo && !(a.dbg & 1)) {
+        const uint4 v = *reinterpret_cast<const uint4*>(lds_out + (wave * kSTile + px) * kSOutStride + part * 16);
         *reinterpret_cast<uint4*>(ybase + px * kSCo + part * 8) = v;
       }
     }
     if (++ho == a.Ho) { ho = 0; ++n; }
+  };
+  for (int64_t row = r0; row < r1; row += 2) {
+    step(row, std::integral_constant<int, 0>{});
+    if (row + 1 < r1) step(row + 1, std::integral_constant<int, 1>{});
   }
 
-  // ---- one partial row per workgroup: lanes lc (+ half lh) hold channel 32 t + lc
-#pragma unroll
-  for (int t = 0; t < 2; ++t) {
-    s1[t] += __shfl_xor(s1[t], 32);
-    s2[t] += __shfl_xor(s2[t], 32);
-  }
+  // ---- one partial row per workgroup: lane lc (+ half lh) of wave (ct, ph) holds channel
+  // 32 ct + lc
+  s1 += __shfl_xor(s1, 32);
+  s2 += __shfl_xor(s2, 32);
   if (lh == 0) {
-    red[wave][0][lc] = s1[0];
-    red[wave][0][32 + lc] = s1[1];
-    red[wave][1][lc] = s2[0];
-    red[wave][1][32 + lc] = s2[1];
+    red[wave][0][lc] = s1;
+    red[wave][1][lc] = s2;
   }
   __syncthreads();
   if (tid < kSCo) {
-    float a1 = 0.f, a2 = 0.f;
-#pragma unroll
-    for (int w = 0; w < kSWaves; ++w) { a1 += red[w][0][tid]; a2 += red[w][1][tid]; }
-    a.part[int64_t(blockIdx.x) * kSCo + tid] = a1;
-    a.part[int64_t(gridDim.x) * kSCo + int64_t(blockIdx.x) * kSCo + tid] = a2;
+    const int c = tid, t = c >> 5, l = c & 31;  // waves t and t + 2 hold channel tile t
+    const float a1 = red[t][0][l] + red[t + 2][0][l], a2 = red[t][1][l] + red[t + 2][1][l];
+    a.part[int64_t(blockIdx.x) * kSCo + c] = a1;
+    a.part[int64_t(gridDim.x) * kSCo + int64_t(blockIdx.x) * kSCo + c] = a2;
   }
 }
 
@@ -282,6 +321,13 @@ struct StemWArgs {
 
 typedef __bf16 st_bf16x4_v __attribute__((__vector_size__(4 * sizeof(__bf16))));
 typedef __attribute__((address_space(3))) st_bf16x4_v st_lds_bf16x4;
+
+typedef uint32_t st_u32x4 __attribute__((ext_vector_type(4)));
+// named native vectors: HIP's uint4 struct is copied with memcpy, which kept an array of them
+// in scratch
+struct St4 {
+  st_u32x4 v0, v1, v2, v3;
+};
 
 __device__ __forceinline__ uint2 st_tr_read(const unsigned char* p) {
   const st_bf16x4_v v = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((st_lds_bf16x4*)(p));
@@ -428,36 +474,56 @@ __global__ __launch_bounds__(kSThreads, 2) void stem_conv7x7_wgrad_kernel(StemWA
   if (nkh == 4) put(acc3, kh0 + 3);
 }
 
-// partials [nb][64][224] -> [sl][64][224] sums over block slices (first pass)
-__global__ __launch_bounds__(256) void stem_wgrad_slice_kernel(const float* __restrict__ part, int nb,
-                                                               float* __restrict__ tmp) {
-  const int e = blockIdx.x * 256 + threadIdx.x;  // element of 64 x 224
-  if (e >= kSCo * kWK) return;
+// partials [nb][64][224] -> [nsl][64][224] (float4, each slice sums <= 8 partial rows)
+__global__ __launch_bounds__(256) void stem_wgrad_slice_kernel(const float4* __restrict__ part, int nb,
+                                                               float4* __restrict__ tmp) {
+  constexpr int e4n = kSCo * kWK / 4;
+  const int e = blockIdx.x * 256 + threadIdx.x;
+  if (e >= e4n) return;
   const int sl = blockIdx.y, nsl = gridDim.y;
   const int per = (nb + nsl - 1) / nsl;
   const int b0 = sl * per, b1 = min(nb, b0 + per);
-  float s = 0.f;
-  for (int b = b0; b < b1; ++b) s += part[int64_t(b) * kSCo * kWK + e];
-  tmp[int64_t(sl) * kSCo * kWK + e] = s;
+  float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
+  for (int b = b0; b < b1; ++b) {
+    const float4 v = part[int64_t(b) * e4n + e];
+    s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
+  }
+  tmp[int64_t(sl) * e4n + e] = s;
 }
 
-// [nsl][64][224] -> dW[co][c][kh][kw] (element strides), fp32 or bf16, (+)=
+// [nsl][64][224] -> dW[co][c][kh][kw] (element strides), fp32 or bf16, (+)=; one thread per
+// (co, kh, kw): its 4 packed channels are one float4 of every slice
 template <typename OutT>
-__global__ __launch_bounds__(256) void stem_wgrad_final_kernel(const float* __restrict__ tmp, int nsl, int cin,
+__global__ __launch_bounds__(256) void stem_wgrad_final_kernel(const float4* __restrict__ tmp, int nsl, int cin,
                                                                OutT* __restrict__ dw, int64_t s0, int64_t s1,
                                                                int64_t s2, int64_t s3, int accumulate) {
-  const int i = blockIdx.x * 256 + threadIdx.x;  // (co, c, kh, kw) flat
-  if (i >= kSCo * cin * kSK * kSK) return;
-  const int kw = i % kSK, kh = (i / kSK) % kSK, c = (i / (kSK * kSK)) % cin, co = i / (kSK * kSK * cin);
-  const int e = co * kWK + kh * 32 + kw * 4 + c;
-  float s = 0.f;
-  for (int sl = 0; sl < nsl; ++sl) s += tmp[int64_t(sl) * kSCo * kWK + e];
-  OutT* o = dw + co * s0 + c * s1 + kh * s2 + kw * s3;
-  if constexpr (sizeof(OutT) == 4) {
-    *reinterpret_cast<float*>(o) = s + (accumulate ? *reinterpret_cast<float*>(o) : 0.f);
-  } else {
-    uint16_t* q = reinterpret_cast<uint16_t*>(o);
-    *q = f2bf(s + (accumulate ? bf2f(*q) : 0.f));
+  constexpr int e4n = kSCo * kWK / 4;
+  const int i = blockIdx.x * 256 + threadIdx.x;  // (co, kh, kw)
+  if (i >= kSCo * kSK * kSK) return;
+  const int kw = i % kSK, kh = (i / kSK) % kSK, co = i / (kSK * kSK);
+  const int e4 = (co * kWK + kh * 32 + kw * 4) / 4;
+  float4 a = make_float4(0.f, 0.f, 0.f, 0.f), b = a;
+  int sl = 0;
+  for (; sl + 1 < nsl; sl += 2) {
+    const float4 u = tmp[int64_t(sl) * e4n + e4], v = tmp[int64_t(sl + 1) * e4n + e4];
+    a.x += u.x; a.y += u.y; a.z += u.z; a.w += u.w;
+    b.x += v.x; b.y += v.y; b.z += v.z; b.w += v.w;
+  }
+  if (sl < nsl) {
+    const float4 u = tmp[int64_t(sl) * e4n + e4];
+    a.x += u.x; a.y += u.y; a.z += u.z; a.w += u.w;
+  }
+  const float val[4] = {a.x + b.x, a.y + b.y, a.z + b.z, a.w + b.w};
+#pragma unroll
+  for (int c = 0; c < 4; ++c) {
+    if (c >= cin) break;
+    OutT* o = dw + co * s0 + c * s1 + kh * s2 + kw * s3;
+    if constexpr (sizeof(OutT) == 4) {
+      *reinterpret_cast<float*>(o) = val[c] + (accumulate ? *reinterpret_cast<float*>(o) : 0.f);
+    } else {
+      uint16_t* q = reinterpret_cast<uint16_t*>(o);
+      *q = f2bf(val[c] + (accumulate ? bf2f(*q) : 0.f));
+    }
   }
 }
 
@@ -536,8 +602,10 @@ int stem_grid_blocks() {
 
 }  // namespace
 
+constexpr int kWMaxSlices = 64;
+
 int64_t stem_wgrad_workspace_floats(int N, int Ho) {
-  return int64_t(stem_partial_rows(N, Ho) + 32) * kSCo * kWK;
+  return int64_t(stem_partial_rows(N, Ho) + kWMaxSlices) * kSCo * kWK;
 }
 
 void stem_conv_wgrad(uintptr_t x4, uintptr_t dy, uintptr_t dw, int64_t s0, int64_t s1, int64_t s2, int64_t s3,
@@ -553,16 +621,18 @@ void stem_conv_wgrad(uintptr_t x4, uintptr_t dy, uintptr_t dw, int64_t s0, int64
   const int nb = stem_partial_rows(N, Ho);
   float* part = reinterpret_cast<float*>(ws);
   float* tmp = part + int64_t(nb) * kSCo * kWK;
-  const int nsl = std::min(32, nb);
+  const int nsl = std::min(kWMaxSlices, nb);
   StemWArgs a{reinterpret_cast<const uint2*>(x4), reinterpret_cast<const uint16_t*>(dy), part, N, H, W, Ho, Wo};
   hipLaunchKernelGGL(stem_conv7x7_wgrad_kernel, dim3(nb), dim3(kSThreads), 0, s, a);
-  hipLaunchKernelGGL(stem_wgrad_slice_kernel, dim3((kSCo * kWK + 255) / 256, nsl), dim3(256), 0, s, part, nb, tmp);
-  const int total = kSCo * Cin * kSK * kSK;
+  hipLaunchKernelGGL(stem_wgrad_slice_kernel, dim3((kSCo * kWK / 4 + 255) / 256, nsl), dim3(256), 0, s,
+                     reinterpret_cast<const float4*>(part), nb, reinterpret_cast<float4*>(tmp));
+  const int total = kSCo * kSK * kSK;
+  const float4* t4 = reinterpret_cast<const float4*>(tmp);
   if (out_dt == kF32)
-    hipLaunchKernelGGL((stem_wgrad_final_kernel<float>), dim3((total + 255) / 256), dim3(256), 0, s, tmp, nsl, Cin,
+    hipLaunchKernelGGL((stem_wgrad_final_kernel<float>), dim3((total + 255) / 256), dim3(256), 0, s, t4, nsl, Cin,
                        reinterpret_cast<float*>(dw), s0, s1, s2, s3, int(accumulate));
   else
-    hipLaunchKernelGGL((stem_wgrad_final_kernel<uint16_t>), dim3((total + 255) / 256), dim3(256), 0, s, tmp, nsl, Cin,
+    hipLaunchKernelGGL((stem_wgrad_final_kernel<uint16_t>), dim3((total + 255) / 256), dim3(256), 0, s, t4, nsl, Cin,
                        reinterpret_cast<uint16_t*>(dw), s0, s1, s2, s3, int(accumulate));
   check_launch();
 }
@@ -612,8 +682,12 @@ void stem_conv_fwd(uintptr_t x4, uintptr_t w, int64_t sw0, int64_t sw1, int64_t 
   VODA_CHECK(Wo >= 1 && Wo <= kSMaxWo, "stem_conv: output width must be <= 128");
   VODA_CHECK(nb == stem_partial_rows(N, Ho), "stem_conv: partial-row count mismatch");
   VODA_CHECK(x4 % 8 == 0 && y % 16 == 0 && part % 4 == 0, "stem_conv: misaligned operands");
+  static const int dbg = [] {
+    const char* e = std::getenv("VODA_STEM_DEBUG");
+    return e ? std::atoi(e) : 0;
+  }();
   StemArgs a{reinterpret_cast<const uint2*>(x4), reinterpret_cast<const uint16_t*>(w), sw0, sw1, sw2, sw3, Cin,
-             reinterpret_cast<uint16_t*>(y), reinterpret_cast<float*>(part), N, H, W, Ho, Wo};
+             reinterpret_cast<uint16_t*>(y), reinterpret_cast<float*>(part), N, H, W, Ho, Wo, dbg};
   hipLaunchKernelGGL(stem_conv7x7_fwd_kernel, dim3(nb), dim3(kSThreads), 0, as_stream(stream), a);
   check_launch();
 }

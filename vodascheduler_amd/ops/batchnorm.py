@@ -58,19 +58,26 @@ def _direct_fp32(p) -> bool:
 
 class _BNActFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, residual, weight, bias, running_mean, running_var, momentum, eps, relu, sink=None):
+    def forward(ctx, x, residual, weight, bias, running_mean, running_var, momentum, eps, relu, sink=None,
+                stats=None):
+        """``stats``: (workspace, nb) whose first 2 x nb x C floats are the producing GEMM's
+        per-block sums / sums of squares of ``x`` (ops/conv1x1.py, gemm_bnstats.hip): the
+        statistics pass is skipped."""
         C = x.shape[1]
         M = x.numel() // C
         h = N.hip()
         y = torch.empty_like(x)
         save_mean = torch.empty(C, dtype=torch.float32, device=x.device)
         save_invstd = torch.empty(C, dtype=torch.float32, device=x.device)
-        ws = torch.empty(h.bn_workspace_floats(M, C), dtype=torch.float32, device=x.device)
+        if stats is not None:
+            ws, pre_nb = stats
+        else:
+            ws, pre_nb = torch.empty(h.bn_workspace_floats(M, C), dtype=torch.float32, device=x.device), 0
         mask = torch.empty(M * (C // 8), dtype=torch.uint8, device=x.device) if relu else None
         h.bn_fwd_train(x.data_ptr(), N.ptr(residual), N.ptr(weight), N.ptr(bias), N.ptr(running_mean),
                        N.ptr(running_var), save_mean.data_ptr(), save_invstd.data_ptr(), y.data_ptr(), N.ptr(mask),
                        ws.data_ptr(), M, C, float(eps), float(momentum), bool(relu), N.dtype_code(x.dtype),
-                       N.stream_of(x))
+                       N.stream_of(x), int(pre_nb))
         ctx.relu = bool(relu)
         ctx.has_res = residual is not None
         ctx.bias = bias
@@ -112,8 +119,26 @@ class _BNActFn(torch.autograd.Function):
             if weight is not None:
                 _ready(weight)
             _ready(bias)
-            return dx, dres, None, None, None, None, None, None, None, None
-        return dx, dres, dw, db, None, None, None, None, None, None
+            return dx, dres, None, None, None, None, None, None, None, None, None
+        return dx, dres, dw, db, None, None, None, None, None, None, None
+
+
+STATS_ATTR = "_voda_bn_stats"
+
+
+def attach_stats(y: torch.Tensor, ws: torch.Tensor, nb: int) -> torch.Tensor:
+    """Mark ``y`` as carrying its BN partial statistics (first 2 x nb x C floats of ``ws``,
+    which must also hold the finalize's 3 x C tail)."""
+    setattr(y, STATS_ATTR, (ws, int(nb)))
+    return y
+
+
+def take_stats(x: torch.Tensor):
+    """The partial statistics a producing GEMM attached to ``x`` (consumed once), or None."""
+    st = getattr(x, STATS_ATTR, None)
+    if st is not None:
+        delattr(x, STATS_ATTR)
+    return st
 
 
 def _reference(x, weight, bias, running_mean, running_var, training, momentum, eps, residual, relu):
@@ -135,7 +160,8 @@ def batch_norm_act(x: torch.Tensor, weight: torch.Tensor | None, bias: torch.Ten
     if not USE_FUSED_BN or not params_fp32 or not _supported(x, residual):
         return _reference(x, weight, bias, running_mean, running_var, training, momentum, eps, residual, relu)
     if training or running_mean is None:
-        return _BNActFn.apply(x, residual, weight, bias, running_mean, running_var, momentum, eps, relu, sink)
+        stats = take_stats(x)
+        return _BNActFn.apply(x, residual, weight, bias, running_mean, running_var, momentum, eps, relu, sink, stats)
     # inference: per-channel affine from the running statistics, one apply pass
     C = x.shape[1]
     invstd = torch.rsqrt(running_var.float() + eps)

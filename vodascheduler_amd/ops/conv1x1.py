@@ -26,7 +26,7 @@ import os
 import torch
 import torch.nn.functional as F
 
-from ..utils.flat import flat_grad
+from ..utils.flat import FOLD_CAST, flat_grad
 from . import _native as N
 from . import wgrad as W
 
@@ -35,6 +35,12 @@ USE_CONV1X1_GEMM = os.environ.get("VODA_CONV1X1_GEMM", "1") != "0"
 # zero-filled full-resolution tensor (A/B switch for _StridedGrad)
 USE_STRIDED_SINK = os.environ.get("VODA_STRIDED_SINK", "1") != "0"
 USE_GRAD_SINK = os.environ.get("VODA_GRAD_SINK", "1") != "0"
+# VODA_GEMM_BNSTATS=0: the expansion 1x1 convolutions (K = 64 / 128 in) stay on hipBLASLt /
+# MIOpen and their BN runs its own statistics pass (A/B switch for gemm_bnstats.hip)
+USE_GEMM_BNSTATS = os.environ.get("VODA_GEMM_BNSTATS", "1") != "0"
+# VODA_STATS_BWD_SPLIT=1: the Cin = 64 statistics layers run their MIOpen input and weight
+# gradients as two calls (A/B switch)
+STATS_BWD_SPLIT = os.environ.get("VODA_STATS_BWD_SPLIT", "0") == "1"
 # Opt-in (VODA_CONV1X1_HYBRID=1): for Cin < 128 (ResNet stage 1: 64 -> 256) keep forward and
 # input gradient on MIOpen and send the weight gradient to the split-K kernel, straight into
 # the fp32 flat gradient.  In isolation the kernel matches MIOpen's igemm_wrw (156 vs 155 us)
@@ -117,6 +123,37 @@ def subsample_add_(dx: torch.Tensor, g: torch.Tensor, s: int) -> None:
         dx[:, :, ::s, ::s].add_(g)
 
 
+class StatsHolder:
+    """Side channel from a forward GEMM that computed its output's BN partial statistics to
+    the module, which attaches them to the returned tensor (ops/batchnorm.attach_stats)."""
+
+    __slots__ = ("stats",)
+
+    def __init__(self):
+        self.stats = None
+
+
+def gemm_bnstats_2d(x2: torch.Tensor, w2: torch.Tensor, holder: StatsHolder | None) -> torch.Tensor | None:
+    """Y = X W^T on the MFMA kernel with the BN statistics of Y's columns (gemm_bnstats.hip)
+    when the shapes are covered and a holder wants them; else None."""
+    if holder is None or not USE_GEMM_BNSTATS or not x2.is_cuda:
+        return None
+    M, K = x2.shape
+    Nc = w2.shape[0]
+    if (x2.dtype != torch.bfloat16 or w2.dtype != torch.bfloat16 or not x2.is_contiguous() or not w2.is_contiguous()
+            or x2.data_ptr() % 16 or w2.data_ptr() % 16):
+        return None
+    h = N.hip()
+    if not h.gemm_bnstats_supported(M, Nc, K):
+        return None
+    G = h.gemm_bnstats_groups(M, Nc, K)
+    y2 = torch.empty(M, Nc, dtype=torch.bfloat16, device=x2.device)
+    ws = torch.empty(max(2 * G * Nc + 3 * Nc, h.bn_workspace_floats(M, Nc)), dtype=torch.float32, device=x2.device)
+    h.gemm_bnstats(x2.data_ptr(), w2.data_ptr(), y2.data_ptr(), ws.data_ptr(), M, Nc, K, G, N.stream_of(x2))
+    holder.stats = (ws, G)
+    return y2
+
+
 def _direct(p: torch.Tensor) -> bool:
     return flat_grad(p) is not None
 
@@ -135,16 +172,20 @@ def _as_2d(t: torch.Tensor) -> torch.Tensor:
 
 class _Conv1x1Fn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, weight, stride: int, sink_in: GradSink | None = None, sink_out: GradSink | None = None):
+    def forward(ctx, x, weight, stride: int, sink_in: GradSink | None = None, sink_out: GradSink | None = None,
+                holder: StatsHolder | None = None):
         """``sink_in``: accumulate the input gradient into the tensor a producer left there
         (stride 1 only); ``sink_out``: hand the input gradient to a consumer instead of
-        returning it."""
+        returning it; ``holder``: receives the output's BN partial statistics when the
+        statistics GEMM covers the shape."""
         xs = subsample(x, stride) if stride > 1 else x
         n, cin, h, w = xs.shape
         cout = weight.shape[0]
         x2 = _as_2d(xs)
         w2 = weight.reshape(cout, cin)
-        y2 = x2 @ w2.t()
+        y2 = gemm_bnstats_2d(x2, w2, holder)
+        if y2 is None:
+            y2 = x2 @ w2.t()
         ctx.save_for_backward(x2, weight)
         ctx.meta = (x.shape, stride, n, h, w)
         ctx.sink_in = sink_in if stride == 1 else None
@@ -207,7 +248,45 @@ class _Conv1x1Fn(torch.autograd.Function):
         if ctx.sink_out is not None and dx is not None:
             ctx.sink_out.put(dx)
             dx = None
-        return dx, dw, None, None, None
+        return dx, dw, None, None, None, None
+
+
+class _Conv1x1StatsFn(torch.autograd.Function):
+    """Stride-1 1x1 convolution whose forward is the statistics GEMM (gemm_bnstats.hip) and
+    whose backward is MIOpen's (the Cin = 64 layers, which stay off the hipBLASLt path)."""
+
+    @staticmethod
+    def forward(ctx, x, weight, holder):
+        n, cin, h, w = x.shape
+        cout = weight.shape[0]
+        y2 = gemm_bnstats_2d(_as_2d(x), weight.reshape(cout, cin), holder)
+        ctx.save_for_backward(x, weight)
+        return y2.view(n, h, w, cout).permute(0, 3, 1, 2)
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, weight = ctx.saved_tensors
+        if not dy.is_contiguous(memory_format=torch.channels_last):
+            dy = dy.contiguous(memory_format=torch.channels_last)
+        mask = [bool(ctx.needs_input_grad[0]), bool(ctx.needs_input_grad[1]), False]
+        dx = dw = None
+        if STATS_BWD_SPLIT:  # one MIOpen call per gradient (solver choice differs from the joint call)
+            if mask[0]:
+                dx = torch.ops.aten.convolution_backward(dy, x, weight, None, [1, 1], [0, 0], [1, 1], False, [0, 0], 1,
+                                                         [True, False, False])[0]
+            if mask[1]:
+                dw = torch.ops.aten.convolution_backward(dy, x, weight, None, [1, 1], [0, 0], [1, 1], False, [0, 0], 1,
+                                                         [False, True, False])[1]
+        elif mask[0] or mask[1]:
+            dx, dw, _ = torch.ops.aten.convolution_backward(dy, x, weight, None, [1, 1], [0, 0], [1, 1], False, [0, 0],
+                                                            1, mask)
+        if mask[1]:
+            g2 = flat_grad(weight) if _direct(weight) else None
+            if g2 is not None:  # fold into the optimizer's flat gradient (see utils/flat.FOLD_CAST)
+                g2.add_(dw.to(g2.dtype) if FOLD_CAST else dw)
+                _ready(weight)
+                dw = None
+        return dx, dw, None
 
 
 class _Conv1x1HybridFn(torch.autograd.Function):
@@ -244,6 +323,14 @@ class _Conv1x1HybridFn(torch.autograd.Function):
         return dx, dw
 
 
+def _attach(y: torch.Tensor, holder: StatsHolder | None) -> torch.Tensor:
+    if holder is not None and holder.stats is not None:
+        from .batchnorm import attach_stats
+
+        attach_stats(y, *holder.stats)
+    return y
+
+
 class Conv1x1(torch.nn.Conv2d):
     """``nn.Conv2d(cin, cout, 1, stride, bias=False)`` with the GEMM formulation on GPU."""
 
@@ -256,6 +343,19 @@ class Conv1x1(torch.nn.Conv2d):
                 and self.dilation == (1, 1) and self.stride[0] == self.stride[1]
                 and x.is_contiguous(memory_format=torch.channels_last)
                 and self.in_channels >= 128 and self.in_channels % 8 == 0 and self.out_channels % 8 == 0)
+
+    def _stats_ok(self, x: torch.Tensor) -> bool:
+        """The output feeds a training-mode BN and the statistics GEMM covers the layer
+        (K = 64 / 128 input channels, channels_last bf16)."""
+        if not (USE_GEMM_BNSTATS and self.training and torch.is_grad_enabled() and x.is_cuda and x.dim() == 4
+                and x.dtype == torch.bfloat16 and self.weight.dtype == torch.bfloat16
+                and self.in_channels in (64, 128) and self.groups == 1 and self.padding == (0, 0)
+                and self.dilation == (1, 1) and x.is_contiguous(memory_format=torch.channels_last)
+                and self.weight.is_contiguous()):
+            return False
+        s = self.stride[0]
+        m = x.shape[0] * ((x.shape[2] + s - 1) // s) * ((x.shape[3] + s - 1) // s)
+        return bool(N.hip().gemm_bnstats_supported(m, self.out_channels, self.in_channels))
 
     def _hybrid_ok(self, x: torch.Tensor) -> bool:
         return (USE_CONV1X1_HYBRID and x.is_cuda and x.dim() == 4 and x.dtype == torch.bfloat16
@@ -271,10 +371,16 @@ class Conv1x1(torch.nn.Conv2d):
         ignored on the fallback paths (the gradient is then returned normally)."""
         if x.is_cuda and x.dtype != self.weight.dtype and torch.is_autocast_enabled("cuda"):
             x = x.to(self.weight.dtype)
+        holder = StatsHolder() if self._stats_ok(x) else None
         if self._gemm_ok(x):
             with torch.autocast("cuda", enabled=False):
-                return _Conv1x1Fn.apply(x, self.weight, self.stride[0], sink_in, sink_out)
+                y = _Conv1x1Fn.apply(x, self.weight, self.stride[0], sink_in, sink_out, holder)
+            return _attach(y, holder)
         assert sink_in is None, "a GradSink consumer must run on the GEMM path"
+        if holder is not None and self.stride == (1, 1) and self.in_channels == 64:
+            with torch.autocast("cuda", enabled=False):
+                y = _Conv1x1StatsFn.apply(x, self.weight, holder)
+            return _attach(y, holder)
         if self._hybrid_ok(x):
             with torch.autocast("cuda", enabled=False):
                 return _Conv1x1HybridFn.apply(x, self.weight)
