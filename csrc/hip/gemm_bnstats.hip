@@ -3,10 +3,11 @@
 // workgroup partial sums of Y and Y^2 per output channel for the BN finalize kernel
 // (batchnorm.hip, unchanged).
 //
-// Target: ResNet-50's expansion convolutions (conv3 / downsample: K = 64 or 128 channels in,
-// N = 4K out, M = 0.8 M / 0.2 M pixels at bs 256).  They are memory-bound (K is short), and the
-// BN statistics pass that follows re-reads their 411 / 205 MB outputs at ~4.5 TB/s (~90 / ~45 us
-// per layer, profiles/r3/).  Here the statistics come from the accumulators.
+// Target: ResNet-50's stage-1/2 1x1 convolutions that are memory-bound -- the expansions
+// (conv3 / downsample: K = 64 or 128 channels in, N = 4K out) and the stage-1 reductions
+// (conv1: K = 256 in, N = 64 out) -- at M = 0.8 M / 0.2 M pixels (bs 256).  The BN statistics
+// pass that follows re-reads their outputs (411 / 205 MB for the expansions) at ~4.5 TB/s
+// (~90 / ~45 us per layer, profiles/r3/).  Here the statistics come from the accumulators.
 //
 // Design (v_mfma_f32_32x32x16_bf16, 4 waves, persistent, two workgroups per CU):
 //  * a workgroup owns one column tile (NT x 32 output channels) and walks every G-th 128-row
@@ -177,13 +178,15 @@ int gb_cus() {
   return g;
 }
 
-// columns per workgroup for a (K, N): NT x 32, NT = 8 at K = 64, 4 at K = 128
-int gb_nt(int K) { return K == 64 ? 8 : 4; }
+// columns per workgroup for a (K, N): NT x 32, NT = 8 at K = 64, 4 at K = 128, 2 at K = 256
+// (the W tile stays <= 64 KB of LDS and the double-buffered X fragments <= 128 VGPRs)
+int gb_nt(int K) { return K == 64 ? 8 : (K == 128 ? 4 : 2); }
 
 }  // namespace
 
 bool gemm_bnstats_supported(int64_t M, int N, int K) {
-  return M > 0 && (K == 64 || K == 128) && N % (32 * gb_nt(K)) == 0;
+  // K = 256: at most two column tiles (every column tile re-reads the whole X operand)
+  return M > 0 && (K == 64 || K == 128 || (K == 256 && N <= 128)) && N % (32 * gb_nt(K)) == 0;
 }
 
 int gemm_bnstats_groups(int64_t M, int N, int K) {
@@ -195,7 +198,7 @@ int gemm_bnstats_groups(int64_t M, int N, int K) {
 
 void gemm_bnstats(uintptr_t x, uintptr_t w, uintptr_t y, uintptr_t part, int64_t M, int N, int K, int G,
                   uintptr_t stream) {
-  VODA_CHECK(gemm_bnstats_supported(M, N, K), "gemm_bnstats: K must be 64 or 128 and N a multiple of the tile");
+  VODA_CHECK(gemm_bnstats_supported(M, N, K), "gemm_bnstats: K must be 64, 128 or 256 and N a multiple of the tile");
   VODA_CHECK(G == gemm_bnstats_groups(M, N, K), "gemm_bnstats: group count mismatch");
   VODA_CHECK(x % 16 == 0 && w % 16 == 0 && y % 16 == 0 && part % 4 == 0, "gemm_bnstats: misaligned operands");
   const int ncol = N / (32 * gb_nt(K));
@@ -204,8 +207,10 @@ void gemm_bnstats(uintptr_t x, uintptr_t w, uintptr_t y, uintptr_t part, int64_t
   hipStream_t s = as_stream(stream);
   if (K == 64)
     hipLaunchKernelGGL((gemm_bnstats_kernel<8, 4>), dim3(ncol * G), dim3(kGThreads), 0, s, a);
-  else
+  else if (K == 128)
     hipLaunchKernelGGL((gemm_bnstats_kernel<4, 8>), dim3(ncol * G), dim3(kGThreads), 0, s, a);
+  else
+    hipLaunchKernelGGL((gemm_bnstats_kernel<2, 16>), dim3(ncol * G), dim3(kGThreads), 0, s, a);
   check_launch();
 }
 

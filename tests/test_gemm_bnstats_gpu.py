@@ -13,7 +13,7 @@ pytestmark = pytest.mark.gpu
 
 
 @pytest.mark.parametrize("M,K,Nc", [(802816 // 64, 64, 256), (4096, 64, 512), (1000, 64, 256), (3136, 128, 512),
-                                    (200, 128, 128), (77, 64, 256)])
+                                    (200, 128, 128), (77, 64, 256), (5000, 256, 64), (333, 256, 128)])
 def test_gemm_bnstats_vs_fp32(M, K, Nc):
     torch.manual_seed(0)
     x = torch.randn(M, K, device="cuda").bfloat16()
@@ -34,10 +34,13 @@ def test_gemm_bnstats_shape_gate():
     h = N.hip()
     assert h.gemm_bnstats_supported(1000, 256, 64) and h.gemm_bnstats_supported(1000, 128, 128)
     assert not h.gemm_bnstats_supported(1000, 64, 64)  # column tile is 256 at K = 64
-    assert not h.gemm_bnstats_supported(1000, 256, 256)
+    assert h.gemm_bnstats_supported(1000, 64, 256)
+    assert not h.gemm_bnstats_supported(1000, 256, 256)  # K = 256: at most 2 column tiles
+    assert not h.gemm_bnstats_supported(1000, 256, 512)
 
 
-@pytest.mark.parametrize("cin,cout,stride,hw", [(64, 256, 1, 28), (128, 512, 1, 14), (128, 512, 2, 14)])
+@pytest.mark.parametrize("cin,cout,stride,hw", [(64, 256, 1, 28), (128, 512, 1, 14), (128, 512, 2, 14),
+                                                (256, 64, 1, 28)])
 def test_conv_then_bn_uses_gemm_stats_and_matches(cin, cout, stride, hw, monkeypatch):
     """Conv1x1 -> FusedBatchNorm2d(+ReLU) in training: the BN takes the GEMM's statistics
     (no stats pass) and matches the fp32 composition, forward, running stats and grads."""

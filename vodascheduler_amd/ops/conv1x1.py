@@ -346,10 +346,10 @@ class Conv1x1(torch.nn.Conv2d):
 
     def _stats_ok(self, x: torch.Tensor) -> bool:
         """The output feeds a training-mode BN and the statistics GEMM covers the layer
-        (K = 64 / 128 input channels, channels_last bf16)."""
+        (K = 64 / 128 / 256 input channels, channels_last bf16)."""
         if not (USE_GEMM_BNSTATS and self.training and torch.is_grad_enabled() and x.is_cuda and x.dim() == 4
                 and x.dtype == torch.bfloat16 and self.weight.dtype == torch.bfloat16
-                and self.in_channels in (64, 128) and self.groups == 1 and self.padding == (0, 0)
+                and self.in_channels in (64, 128, 256) and self.groups == 1 and self.padding == (0, 0)
                 and self.dilation == (1, 1) and x.is_contiguous(memory_format=torch.channels_last)
                 and self.weight.is_contiguous()):
             return False
