@@ -377,7 +377,7 @@ class Conv1x1(torch.nn.Conv2d):
                 y = _Conv1x1Fn.apply(x, self.weight, self.stride[0], sink_in, sink_out, holder)
             return _attach(y, holder)
         assert sink_in is None, "a GradSink consumer must run on the GEMM path"
-        if holder is not None and self.stride == (1, 1) and self.in_channels == 64:
+        if holder is not None and self.stride == (1, 1) and self.in_channels == 64 and not self._hybrid_ok(x):
             with torch.autocast("cuda", enabled=False):
                 y = _Conv1x1StatsFn.apply(x, self.weight, holder)
             return _attach(y, holder)
