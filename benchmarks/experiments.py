@@ -26,7 +26,8 @@ import sys
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from vodascheduler_amd.algorithm import ALGORITHMS  # noqa: E402
 from vodascheduler_amd.sim.simulator import simulate  # noqa: E402
-from vodascheduler_amd.common.workload import busbw_source, intra_node_busbw, load_bench_json  # noqa: E402
+from vodascheduler_amd.common.workload import (PROFILES, busbw_source, intra_node_busbw,  # noqa: E402
+                                               load_bench_json)
 from vodascheduler_amd.sim.trace import (ASSUMED_BUSBW_GBS, ASSUMED_INTERNODE_BUSBW_GBS, TraceJob,  # noqa: E402
                                          make_spec, philly_trace)
 
@@ -106,7 +107,9 @@ def main():
     lines = ["# BASELINE.json configs in the discrete-event simulator (round 3)", "",
              "Real training service / scheduler / allocator / placement code driven in virtual time "
              "(`benchmarks/experiments.py`). Job speed model (`vodascheduler_amd/common/workload.py`): single-GPU "
-             "step times MEASURED on MI355X (bf16 compute, fp32 gradients; ResNet-50 25.3 ms, BERT-base 10.2 ms); "
+             "step times MEASURED on MI355X (bf16 compute, fp32 gradients; "
+             f"ResNet-50 {PROFILES['resnet50'].step_time_1gpu * 1e3:.2f} ms, "
+             f"BERT-base {PROFILES['bert-base'].step_time_1gpu * 1e3:.2f} ms); "
              "fp32 gradient bytes exact; ring all-reduce bus bandwidth " + bw + f", {ASSUMED_INTERNODE_BUSBW_GBS:.0f} "
              "GB/s across nodes (assumed); 30 % of a step hides the all-reduce.  Resize pause 5 s, "
              "restart-from-checkpoint pause 15 s, rate limit 30 s (reference default).", "",
