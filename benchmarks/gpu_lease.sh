@@ -83,8 +83,8 @@ for step in "$@"; do
       spec=${step#pmc-}
       m=${spec%%:*}
       ctr=${spec#*:}
-      run 120 "pmc-$m" rocprofv3 --kernel-trace --pmc ${ctr//,/ } -d "$OUT/pmc-$m" -o run -- \
-        python -u benchmarks/model_step.py --model "$m" --steps 3 --warmup 3 || exit $? ;;
+      run 180 "pmc-$m" rocprofv3 --kernel-trace --pmc ${ctr//,/ } -d "$OUT/pmc-$m$SUFFIX" -o run \
+        --output-format csv -- python -u benchmarks/model_step.py --model "$m" --steps 3 --warmup 3 || exit $? ;;
     pytest:*)  # pytest:tests/FILE.py[,-k,EXPR] -- one GPU test file
       spec=${step#pytest:}
       run 300 "pytest-$(basename "${spec%%,*}" .py)" python -u -m pytest ${spec//,/ } -m gpu -x -q --timeout 120 \
