@@ -181,26 +181,49 @@ struct TileRegs {
 // padding (the reference's additive -1e9), 2 past Tk (-inf).  A lane needs 16 of the 32 keys
 // (crow(i, h): four runs of 4 consecutive keys), i.e. four 4-byte LDS reads per tile instead
 // of sixteen global byte loads on the softmax's critical path.
-__device__ __forceinline__ void stage_mask(const AttnArgs& a, const uint8_t* mrow, int kt, uint8_t* ms) {
-  const int t = threadIdx.x;
-  if (t < kTile) {
-    const int key = kt + t;
-    ms[t] = key >= a.Tk ? 2 : ((mrow != nullptr && mrow[key] == 0) ? 1 : 0);
+// ms[kTile] (a flag byte after the codes) = 1 when any key of the tile is masked, so an
+// unmasked tile -- every tile of an unpadded batch -- skips the per-element mask work with one
+// wave-uniform branch.  Wave 0 stages the codes (kTile <= 64 threads).
+// The mask bytes are loaded one tile ahead, with the K/V tile (a load issued after the
+// barrier and consumed before the next one put a full memory latency on every tile).
+constexpr int kMaskBytes = kTile + 4;
+struct MaskPF {
+  uint32_t raw;  // mask byte of key kt + threadIdx.x (threads < kTile)
+  __device__ __forceinline__ void load(const AttnArgs& a, const uint8_t* mrow, int kt) {
+    raw = 1;
+    if (mrow != nullptr && threadIdx.x < kTile) raw = mrow[min(kt + int(threadIdx.x), a.Tk - 1)];
   }
+  __device__ __forceinline__ void store(const AttnArgs& a, int kt, uint8_t* ms) const {
+    const int t = threadIdx.x;
+    if (t < 64) {
+      uint32_t code = 0;
+      if (t < kTile) {
+        code = kt + t >= a.Tk ? 2u : (raw == 0 ? 1u : 0u);
+        ms[t] = uint8_t(code);
+      }
+      const uint64_t any = __ballot(code != 0);
+      if (t == 0) ms[kTile] = any != 0 ? 1 : 0;
+    }
+  }
+};
+__device__ __forceinline__ bool tile_masked(const uint8_t* ms) {
+  return __builtin_amdgcn_readfirstlane(uint32_t(ms[kTile])) != 0;
 }
 __device__ __forceinline__ void load_mask_words(const uint8_t* ms, int h, uint32_t (&mw)[4]) {
 #pragma unroll
   for (int g = 0; g < 4; ++g) mw[g] = *reinterpret_cast<const uint32_t*>(ms + 8 * g + 4 * h);
 }
 // additive mask of accumulator register i (key kt + crow(i, h)): -inf past Tk, -1e9 for key
-// padding and (causal) future keys, else 0
-__device__ __forceinline__ float mask_code_add(const AttnArgs& a, const uint32_t (&mw)[4], int i, int key,
-                                               int query) {
+// padding, else 0 -- two selects, no branch (a branchy form here compiled to ~50 exec-mask
+// sequences per tile and made the softmax instruction-bound)
+__device__ __forceinline__ float mask_code_add(const uint32_t (&mw)[4], int i) {
   const uint32_t code = (mw[i >> 2] >> (8 * (i & 3))) & 0xffu;
-  if (code == 2) return kNegInf;
-  if (code == 1) return kMaskNeg;
-  if (a.causal && key > query) return kMaskNeg;
-  return 0.f;
+  const float pad = code != 0 ? kMaskNeg : 0.f;
+  return code > 1 ? kNegInf : pad;
+}
+// (causal) a future key gets the reference's -1e9 unless it is already past Tk
+__device__ __forceinline__ float causal_add(float add, int key, int query) {
+  return (key > query && add == 0.f) ? kMaskNeg : add;
 }
 
 // Write a [32 x 32] tile held as (lane = row-of-output r, regs = 16 columns) -- i.e. an
@@ -232,7 +255,7 @@ __global__ __launch_bounds__(64 * W) void attn_fwd_kernel(AttnArgs a) {
   constexpr bool DIRECT = TileRegs<D, 64 * W>::PER > 4 && D >= 128;
   __shared__ __attribute__((aligned(16))) uint16_t Ks[DIRECT ? 8 : kTile * RS];
   __shared__ __attribute__((aligned(16))) uint16_t Vt[D * TS];
-  __shared__ __attribute__((aligned(16))) uint8_t Ms[kTile];
+  __shared__ __attribute__((aligned(16))) uint8_t Ms[kMaskBytes];
 
   const int bh = blockIdx.y, b = bh / a.H, hh = bh % a.H;
   const uint16_t* kb = a.k + b * a.k_sb + hh * a.k_sh;
@@ -240,6 +263,7 @@ __global__ __launch_bounds__(64 * W) void attn_fwd_kernel(AttnArgs a) {
 
   const int lane = threadIdx.x & 63, r = lane & 31, h = lane >> 5, w = threadIdx.x >> 6;
   const int q = blockIdx.x * (32 * W) + w * 32 + r;  // this lane's query
+  const int q_lo = __builtin_amdgcn_readfirstlane(blockIdx.x * (32 * W) + w * 32);  // the wave's first query
   const uint16_t* qrow = a.q + b * a.q_sb + hh * a.q_sh + int64_t(q) * a.q_st;
   bf16x8 qf[KS];
 #pragma unroll
@@ -253,6 +277,8 @@ __global__ __launch_bounds__(64 * W) void attn_fwd_kernel(AttnArgs a) {
   using Regs = TileRegs<D, 64 * W>;
   constexpr bool PF = Regs::PER <= 4;
   Regs kr, vr;
+  MaskPF mp;
+  mp.load(a, mrow, 0);
   if constexpr (PF) {
     kr.load(kb, a.k_st, 0, a.Tk);
     vr.load(vb, a.v_st, 0, a.Tk);
@@ -266,16 +292,15 @@ __global__ __launch_bounds__(64 * W) void attn_fwd_kernel(AttnArgs a) {
       if constexpr (!DIRECT) stage_tile<D, true, false>(kb, a.k_st, kt, a.Tk, Ks, RS, nullptr, 0);
       stage_tile<D, false, true>(vb, a.v_st, kt, a.Tk, nullptr, 0, Vt, TS);
     }
-    stage_mask(a, mrow, kt, Ms);
+    mp.store(a, kt, Ms);
     __syncthreads();
-    if constexpr (PF) {
-      if (kt + kTile < a.Tk) {  // next tile's loads overlap this tile's compute
+    if (kt + kTile < a.Tk) {  // next tile's loads overlap this tile's compute
+      mp.load(a, mrow, kt + kTile);
+      if constexpr (PF) {
         kr.load(kb, a.k_st, kt + kTile, a.Tk);
         vr.load(vb, a.v_st, kt + kTile, a.Tk);
       }
     }
-    uint32_t mw[4];
-    load_mask_words(Ms, h, mw);
     f32x16 s_acc = zero16();
     if constexpr (DIRECT) {
       const bool kv = kt + r < a.Tk;
@@ -286,13 +311,23 @@ __global__ __launch_bounds__(64 * W) void attn_fwd_kernel(AttnArgs a) {
 #pragma unroll
       for (int s = 0; s < KS; ++s) s_acc = mfma(ld16(Ks + r * RS + 16 * s + 8 * h), qf[s], s_acc);
     }
+    // wave-uniform: per-element mask work only on tiles with a masked key or a future key
+    if (tile_masked(Ms) || (a.causal && kt + kTile - 1 > q_lo)) {
+      uint32_t mw[4];
+      load_mask_words(Ms, h, mw);
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        float add = mask_code_add(mw, i);
+        if (a.causal) add = causal_add(add, kt + crow(i, h), q);
+        s_acc[i] = s_acc[i] * a.scale + add;
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < 16; ++i) s_acc[i] *= a.scale;
+    }
     float tmax = -1e30f;
 #pragma unroll
-    for (int i = 0; i < 16; ++i) {
-      const float v = s_acc[i] * a.scale + mask_code_add(a, mw, i, kt + crow(i, h), q);
-      s_acc[i] = v;
-      tmax = fmaxf(tmax, v);
-    }
+    for (int i = 0; i < 16; ++i) tmax = fmaxf(tmax, s_acc[i]);
     tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64));
     const float mn = fmaxf(m, tmax);
     const float alpha = __expf(m - mn);
@@ -326,14 +361,17 @@ __global__ __launch_bounds__(64 * W) void attn_fwd_kernel(AttnArgs a) {
 }
 
 // ======================================================================== backward: dQ (+ delta)
+// D <= 64 with 4 waves (BERT-base): registers capped for 3 waves per SIMD (147 VGPRs, no
+// spill), so all 768 workgroups of a layer are resident at once (25.3 -> 23.9 us per layer).
 template <int D, int W>
-__global__ __launch_bounds__(64 * W) void attn_bwd_dq_kernel(AttnArgs a) {
+__global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu((D <= 64 && W == 4) ? 3 : 1)))
+void attn_bwd_dq_kernel(AttnArgs a) {
   constexpr int KS = D / 16, DT = D / 32, RS = D + 8, TS = kTile + 8;
   constexpr bool DIRECT = TileRegs<D, 64 * W>::PER > 4 && D >= 128;  // as in the forward
   __shared__ __attribute__((aligned(16))) uint16_t Ks[DIRECT ? 8 : kTile * RS];
   __shared__ __attribute__((aligned(16))) uint16_t Vs[DIRECT ? 8 : kTile * RS];
   __shared__ __attribute__((aligned(16))) uint16_t Kt[D * TS];
-  __shared__ __attribute__((aligned(16))) uint8_t Ms[kTile];
+  __shared__ __attribute__((aligned(16))) uint8_t Ms[kMaskBytes];
 
   const int bh = blockIdx.y, b = bh / a.H, hh = bh % a.H;
   const uint16_t* kb = a.k + b * a.k_sb + hh * a.k_sh;
@@ -341,6 +379,7 @@ __global__ __launch_bounds__(64 * W) void attn_bwd_dq_kernel(AttnArgs a) {
 
   const int lane = threadIdx.x & 63, r = lane & 31, h = lane >> 5, w = threadIdx.x >> 6;
   const int q = blockIdx.x * (32 * W) + w * 32 + r;
+  const int q_lo = __builtin_amdgcn_readfirstlane(blockIdx.x * (32 * W) + w * 32);
   const bool qv = q < a.Tq;
   const uint16_t* qrow = a.q + b * a.q_sb + hh * a.q_sh + int64_t(q) * a.q_st;
   const uint16_t* dorow = a.dout + b * a.do_sb + hh * a.do_sh + int64_t(q) * a.do_st;
@@ -356,7 +395,8 @@ __global__ __launch_bounds__(64 * W) void attn_bwd_dq_kernel(AttnArgs a) {
     for (int j = 0; j < 8; ++j) dpart += float(dof[s][j]) * float(of[j]);
   }
   const float delta = dpart + __shfl_xor(dpart, 32, 64);
-  const float lse = qv ? a.lse[int64_t(bh) * a.Tq + q] : 0.f;
+  // rows past Tq: lse = +inf makes every P of the row 0 without a per-element select
+  const float lse = qv ? a.lse[int64_t(bh) * a.Tq + q] : __builtin_huge_valf();
   if (h == 0 && qv) a.delta[int64_t(bh) * a.Tq + q] = delta;
   const uint8_t* mrow = a.mask != nullptr ? a.mask + b * a.mask_sb : nullptr;
 
@@ -366,6 +406,8 @@ __global__ __launch_bounds__(64 * W) void attn_bwd_dq_kernel(AttnArgs a) {
   using Regs = TileRegs<D, 64 * W>;
   constexpr bool PF = Regs::PER <= 4;
   Regs kr, vr;
+  MaskPF mp;
+  mp.load(a, mrow, 0);
   if constexpr (PF) {
     kr.load(kb, a.k_st, 0, a.Tk);
     vr.load(vb, a.v_st, 0, a.Tk);
@@ -381,16 +423,15 @@ __global__ __launch_bounds__(64 * W) void attn_bwd_dq_kernel(AttnArgs a) {
       stage_tile<D, true, true>(kb, a.k_st, kt, a.Tk, Ks, RS, Kt, TS);
       stage_tile<D, true, false>(vb, a.v_st, kt, a.Tk, Vs, RS, nullptr, 0);
     }
-    stage_mask(a, mrow, kt, Ms);
+    mp.store(a, kt, Ms);
     __syncthreads();
-    if constexpr (PF) {
-      if (kt + kTile < a.Tk) {
+    if (kt + kTile < a.Tk) {
+      mp.load(a, mrow, kt + kTile);
+      if constexpr (PF) {
         kr.load(kb, a.k_st, kt + kTile, a.Tk);
         vr.load(vb, a.v_st, kt + kTile, a.Tk);
       }
     }
-    uint32_t mw[4];
-    load_mask_words(Ms, h, mw);
     f32x16 s_acc = zero16(), dp = zero16();
     if constexpr (DIRECT) {
       const bool kv = kt + r < a.Tk;
@@ -408,11 +449,21 @@ __global__ __launch_bounds__(64 * W) void attn_bwd_dq_kernel(AttnArgs a) {
         dp = mfma(ld16(Vs + r * RS + 16 * s + 8 * h), dof[s], dp);
       }
     }
+    if (tile_masked(Ms) || (a.causal && kt + kTile - 1 > q_lo)) {  // wave-uniform, as in the forward
+      uint32_t mw[4];
+      load_mask_words(Ms, h, mw);
 #pragma unroll
-    for (int i = 0; i < 16; ++i) {
-      const float p = qv ? __expf(s_acc[i] * a.scale + mask_code_add(a, mw, i, kt + crow(i, h), q) - lse) : 0.f;
-      s_acc[i] = p * (dp[i] - delta);  // dS^T
+      for (int i = 0; i < 16; ++i) {
+        float add = mask_code_add(mw, i);
+        if (a.causal) add = causal_add(add, kt + crow(i, h), q);
+        s_acc[i] = s_acc[i] * a.scale + add;
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < 16; ++i) s_acc[i] *= a.scale;
     }
+#pragma unroll
+    for (int i = 0; i < 16; ++i) s_acc[i] = __expf(s_acc[i] - lse) * (dp[i] - delta);  // dS^T
     const bf16x8 d0 = acc_frag(s_acc, 0), d1 = acc_frag(s_acc, 1);
 #pragma unroll
     for (int t = 0; t < DT; ++t) {
@@ -428,6 +479,8 @@ __global__ __launch_bounds__(64 * W) void attn_bwd_dq_kernel(AttnArgs a) {
 
 // ======================================================================== backward: dK, dV
 // MODE 0: dK and dV; 1: dV only; 2: dK only (D = 256 runs 1 then 2: one accumulator set each)
+// (Capping this kernel at 3 waves per SIMD like the dQ pass spills the K / V fragments into
+// the loop: 29.1 -> 33.4 us per BERT-base layer, so it keeps 2.)
 template <int D, int W, int MODE>
 __global__ __launch_bounds__(64 * W) void attn_bwd_dkv_kernel(AttnArgs a) {
   constexpr int KS = D / 16, DT = D / 32, RS = D + 8, TS = kTile + 8;
@@ -456,7 +509,9 @@ __global__ __launch_bounds__(64 * W) void attn_bwd_dkv_kernel(AttnArgs a) {
     for (int s = 0; s < KS; ++s) vf[s] = kv ? ld16(vrow + 16 * s + 8 * h) : zero_bf8();
   }
   const uint8_t* mrow = a.mask != nullptr ? a.mask + b * a.mask_sb : nullptr;
-  const bool kmasked = !kv ? true : (mrow != nullptr && mrow[key] == 0);
+  // the key is the lane's: its additive mask is one constant (-inf past Tk, -1e9 padding)
+  const float kadd = !kv ? kNegInf : ((mrow != nullptr && mrow[key] == 0) ? kMaskNeg : 0.f);
+  const int key_hi = __builtin_amdgcn_readfirstlane(blockIdx.x * (32 * W) + w * 32 + 31);  // wave's last key
 
   f32x16 dk[DO_DK ? DT : 1], dv[DO_DV ? DT : 1];
   if constexpr (DO_DK) {
@@ -531,23 +586,31 @@ __global__ __launch_bounds__(64 * W) void attn_bwd_dkv_kernel(AttnArgs a) {
         if constexpr (DO_DK) dp = mfma(ld16(Ds + r * RS + 16 * s + 8 * h), vf[s], dp);  // dP[query][key]
       }
     }
+    // causal: only tiles with a query before the wave's last key need the per-element test
+    if (a.causal && qt < key_hi) {
 #pragma unroll
-    for (int i = 0; i < 16; ++i) {
-      const int ql = crow(i, h);
-      float add = 0.f;
-      if (!kv) add = kNegInf;
-      else if (kmasked || (a.causal && key > qt + ql)) add = kMaskNeg;
-      const float p = __expf(s_acc[i] * a.scale + add - lse_s[ql]);
-      s_acc[i] = p;                                      // P
-      if constexpr (DO_DK) dp[i] = p * (dp[i] - del_s[ql]);  // dS
+      for (int i = 0; i < 16; ++i) {
+        const int ql = crow(i, h);
+        const float add = causal_add(kadd, key, qt + ql);
+        s_acc[i] = __expf(s_acc[i] * a.scale + add - lse_s[ql]);
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < 16; ++i) s_acc[i] = __expf(s_acc[i] * a.scale + kadd - lse_s[crow(i, h)]);
     }
+    if constexpr (DO_DK) {
+#pragma unroll
+      for (int i = 0; i < 16; ++i) dp[i] = s_acc[i] * (dp[i] - del_s[crow(i, h)]);  // dS
+    }
+    // dV^T += dO^T P and dK^T += Q^T dS: the transposed products put the key on the lane
+    // (P / dS registers as the B operand, as P^T in the forward), so the epilogue stores rows
     if constexpr (DO_DV) {
       const bf16x8 p0 = acc_frag(s_acc, 0), p1 = acc_frag(s_acc, 1);
 #pragma unroll
       for (int t = 0; t < DT; ++t) {
         const uint16_t* drow = Dt + (32 * t + r) * TS;  // dO^T row (d = 32t + r)
-        dv[t] = mfma(p0, perm_frag(drow, 0, h, trans_rot(r)), dv[t]);
-        dv[t] = mfma(p1, perm_frag(drow, 1, h, trans_rot(r)), dv[t]);
+        dv[t] = mfma(perm_frag(drow, 0, h, trans_rot(r)), p0, dv[t]);
+        dv[t] = mfma(perm_frag(drow, 1, h, trans_rot(r)), p1, dv[t]);
       }
     }
     if constexpr (DO_DK) {
@@ -555,25 +618,19 @@ __global__ __launch_bounds__(64 * W) void attn_bwd_dkv_kernel(AttnArgs a) {
 #pragma unroll
       for (int t = 0; t < DT; ++t) {
         const uint16_t* qrow = Qt + (32 * t + r) * TS;  // Q^T row
-        dk[t] = mfma(g0, perm_frag(qrow, 0, h, trans_rot(r)), dk[t]);
-        dk[t] = mfma(g1, perm_frag(qrow, 1, h, trans_rot(r)), dk[t]);
+        dk[t] = mfma(perm_frag(qrow, 0, h, trans_rot(r)), g0, dk[t]);
+        dk[t] = mfma(perm_frag(qrow, 1, h, trans_rot(r)), g1, dk[t]);
       }
     }
   }
-  // dv[t] / dk[t]: lane = d (32t + r), regs = keys (block-local crow)
-  const int key0 = blockIdx.x * (32 * W) + w * 32;
+  // dv[t] / dk[t]: lane = key, regs = d (32t + crow): 8-byte row stores
   uint16_t* dkb = a.dk + b * a.dk_sb + hh * a.dk_sh;
   uint16_t* dvb = a.dv + b * a.dv_sb + hh * a.dv_sh;
 #pragma unroll
-  for (int t = 0; t < DT; ++t)
-#pragma unroll
-    for (int i = 0; i < 16; ++i) {
-      const int kk = key0 + crow(i, h);
-      if (kk < a.Tk) {
-        if constexpr (DO_DK) dkb[int64_t(kk) * a.dk_st + 32 * t + r] = f2bf(dk[t][i] * a.scale);
-        if constexpr (DO_DV) dvb[int64_t(kk) * a.dv_st + 32 * t + r] = f2bf(dv[t][i]);
-      }
-    }
+  for (int t = 0; t < DT; ++t) {
+    if constexpr (DO_DK) store_lane_rows(dkb, a.dk_st, key, a.Tk, 32 * t, dk[t], a.scale, h);
+    if constexpr (DO_DV) store_lane_rows(dvb, a.dv_st, key, a.Tk, 32 * t, dv[t], 1.f, h);
+  }
 }
 
 template <typename F>

@@ -380,18 +380,31 @@ __global__ __launch_bounds__(kWgThreads, 1) void wgrad_glds_kernel(WgradArgs p) 
       pwo[i] = rem - pho[i] * p.Wo;
     }
   }
+  // this lane's source rows of stage 0 (row 4j + lr of the tile, swizzled chunk), advanced by
+  // BM rows per stage with one scalar multiply: no per-load 64-bit index arithmetic
+  const uint16_t* row_a[IPW];
+  const uint16_t* row_b[IPW];
+#pragma unroll
+  for (int i = 0; i < IPW; ++i) {
+    const int r = 4 * (IPW * wave + i) + lr;
+    const int ch = slot ^ (((r & 3) << 2) | ((r >> 2) & 3));
+    row_a[i] = p.dy + int64_t(mb + r) * p.ldy + min(n0 + ch * 8, p.N - 8);
+    row_b[i] = CONV ? p.x : p.x + int64_t(mb + r) * p.ldx + min(k0 + ch * 8, p.K - 8);
+  }
   auto issue = [&](int st) {
     uint8_t* A = smem + (st % kWgStages) * SB;
     uint8_t* B = A + TB;
     const int m_base = mb + st * BM;
+    const int64_t adv_a = int64_t(st * BM) * p.ldy, adv_b = int64_t(st * BM) * p.ldx;
+    const bool full = m_base + BM <= me;  // wave-uniform: no row of this stage is past the split
 #pragma unroll
     for (int i = 0; i < IPW; ++i) {
       const int j = IPW * wave + i;
       const int r = 4 * j + lr;
       const int ch = slot ^ (((r & 3) << 2) | ((r >> 2) & 3));
       const int m = m_base + r;
-      const bool okm = m < me;
-      const uint16_t* ga = okm ? p.dy + int64_t(m) * p.ldy + min(n0 + ch * 8, p.N - 8) : p.zero;
+      const bool okm = full || m < me;
+      const uint16_t* ga = okm ? row_a[i] + adv_a : p.zero;
       const uint16_t* gb;
       if constexpr (CONV) {
         const int hi = pho[i] * p.cstride + dh, wi = pwo[i] * p.cstride + dw;
@@ -404,7 +417,7 @@ __global__ __launch_bounds__(kWgThreads, 1) void wgrad_glds_kernel(WgradArgs p) 
         if (pwo[i] >= p.Wo) { pwo[i] -= p.Wo; pho[i] += 1; }
         if (pho[i] >= p.Ho) { pho[i] -= p.Ho; pn[i] += 1; }
       } else {
-        gb = okm ? p.x + int64_t(m) * p.ldx + min(k0 + ch * 8, p.K - 8) : p.zero;
+        gb = okm ? row_b[i] + adv_b : p.zero;
       }
       wg_dma16(ga, __builtin_amdgcn_readfirstlane(uint32_t(size_t((lds_void*)(A + 1024 * j)))));
       wg_dma16(gb, __builtin_amdgcn_readfirstlane(uint32_t(size_t((lds_void*)(B + 1024 * j)))));
@@ -480,6 +493,108 @@ __global__ __launch_bounds__(kWgThreads, 1) void wgrad_glds_kernel(WgradArgs p) 
 // accumulator tile).
 constexpr int kWwTile = 256;
 constexpr int kWwThreads = 512;
+
+// Epilogue of the 256 x 256 kernels (C lane map as in wgrad_epilogue): wave (wn, wk) holds
+// rows n0 + 128 wn + 32 f, columns k0 + 128 (wk >> 1) + 64 (wk & 1) + 32 e; bs[f] = the bias
+// partial sums of its dY fragments (waves with wk == 0 of output-column block 0).
+__device__ __forceinline__ void wide_epilogue(const WgradArgs& p, int split, int n0, int k0, int wn, int wk, int lane,
+                                              const wg_f32x16 (&c)[4][2], const float (&bs)[4], bool do_bias) {
+  const int h = lane >> 5;
+  const int col_l = lane & 31;
+#pragma unroll
+  for (int f = 0; f < 4; ++f) {
+#pragma unroll
+    for (int e = 0; e < 2; ++e) {
+      const int col = k0 + (wk >> 1) * 128 + (wk & 1) * 64 + 32 * e + col_l;
+      if (col < p.K) {
+#pragma unroll
+        for (int reg = 0; reg < 16; ++reg) {
+          const int row = n0 + wn * 128 + 32 * f + (reg & 3) + 8 * (reg >> 2) + 4 * h;
+          if (row < p.N) {
+            if (p.S == 1) {
+              wg_store_out(p.dw, int64_t(row) * p.ldw + col, c[f][e][reg], p.accumulate, p.out_f32);
+            } else {
+              p.ws[(int64_t(split) * p.N + row) * p.ws_ld + col] = c[f][e][reg];
+            }
+          }
+        }
+      }
+    }
+  }
+  if (do_bias) {
+    // lane l (< 32) and l + 32 hold tokens 8h..8h+7 of every k-step for row 32f + l
+#pragma unroll
+    for (int f = 0; f < 4; ++f) {
+      const float tot = bs[f] + __shfl_xor(bs[f], 32);
+      const int row = n0 + wn * 128 + 32 * f + col_l;
+      if (h == 0 && row < p.N) {
+        if (p.S == 1) {
+          wg_store_out(p.db, row, tot, p.accumulate, p.out_f32);
+        } else {
+          p.ws[int64_t(p.S) * p.N * p.ws_ld + int64_t(split) * p.N + row] = tot;
+        }
+      }
+    }
+  }
+}
+
+// Epilogue of the transposed 256 x 256 accumulators (wgrad_wide2_kernel computes C^T = X^T dY:
+// lane = output row n = n0 + 128 wn + 32 f + (lane & 31), registers 4g..4g+3 = four
+// consecutive columns k = k0 + 128 (wk >> 1) + 64 (wk & 1) + 32 e + 8 g + 4 h + 0..3), so each
+// store moves 16 bytes (fp32) or 8 bytes (bf16): a quarter of the store instructions of the
+// one-dword-per-register layout, whose issue rate bounded the epilogue.
+__device__ __forceinline__ void wide_epilogue_t(const WgradArgs& p, int split, int n0, int k0, int wn, int wk,
+                                                int lane, const wg_f32x16 (&c)[4][2], const float (&bs)[4],
+                                                bool do_bias) {
+  const int h = lane >> 5;
+  const int col_l = lane & 31;
+#pragma unroll
+  for (int f = 0; f < 4; ++f) {
+    const int row = n0 + wn * 128 + 32 * f + col_l;
+    if (row >= p.N) continue;
+#pragma unroll
+    for (int e = 0; e < 2; ++e) {
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int col = k0 + (wk >> 1) * 128 + (wk & 1) * 64 + 32 * e + 8 * g + 4 * h;
+        if (col >= p.K) continue;
+        float4 v = make_float4(c[f][e][4 * g], c[f][e][4 * g + 1], c[f][e][4 * g + 2], c[f][e][4 * g + 3]);
+        if (p.S > 1) {
+          *reinterpret_cast<float4*>(p.ws + (int64_t(split) * p.N + row) * p.ws_ld + col) = v;
+        } else if (p.out_f32) {
+          float4* o = reinterpret_cast<float4*>(reinterpret_cast<float*>(p.dw) + int64_t(row) * p.ldw + col);
+          if (p.accumulate) {
+            const float4 u = *o;
+            v.x += u.x; v.y += u.y; v.z += u.z; v.w += u.w;
+          }
+          *o = v;
+        } else {
+          uint2* o = reinterpret_cast<uint2*>(p.dw + int64_t(row) * p.ldw + col);
+          if (p.accumulate) {
+            const uint2 u = *o;
+            v.x += bf2f(u.x & 0xffff); v.y += bf2f(u.x >> 16); v.z += bf2f(u.y & 0xffff); v.w += bf2f(u.y >> 16);
+          }
+          *o = make_uint2(uint32_t(f2bf(v.x)) | (uint32_t(f2bf(v.y)) << 16),
+                          uint32_t(f2bf(v.z)) | (uint32_t(f2bf(v.w)) << 16));
+        }
+      }
+    }
+  }
+  if (do_bias) {
+#pragma unroll
+    for (int f = 0; f < 4; ++f) {
+      const float tot = bs[f] + __shfl_xor(bs[f], 32);
+      const int row = n0 + wn * 128 + 32 * f + col_l;
+      if (h == 0 && row < p.N) {
+        if (p.S == 1) {
+          wg_store_out(p.db, row, tot, p.accumulate, p.out_f32);
+        } else {
+          p.ws[int64_t(p.S) * p.N * p.ws_ld + int64_t(split) * p.N + row] = tot;
+        }
+      }
+    }
+  }
+}
 
 template <int kStages, int BM>
 __global__ __launch_bounds__(kWwThreads, 1) void wgrad_wide_kernel(WgradArgs p) {
@@ -616,43 +731,149 @@ __global__ __launch_bounds__(kWwThreads, 1) void wgrad_wide_kernel(WgradArgs p) 
     }
   }
 
-  // epilogue (C lane map as in wgrad_epilogue)
-  const int col_l = lane & 31;
+  wide_epilogue(p, split, n0, k0, wn, wk, lane, c, bs, do_bias);
+}
+
+// 256 x 256 tile (8 waves as above) on 64-token stages: two LDS stages of 64 KB (128 KB),
+// one in flight while the other is computed, one barrier per stage.  At 64 tokens a stage is
+// 32 MFMAs per wave (2048 matrix cycles per SIMD at two waves per SIMD) behind each barrier
+// -- twice the 32-token ring's -- and the loads are addressed from per-lane row pointers
+// advanced by one scalar product per stage.  Waves 4-7 (the second-dispatched half, the
+// loser of every issue arbitration) run at priority 1 (MI355X_MICROARCH.md, two waves per
+// SIMD, item 4).
+__global__ __launch_bounds__(kWwThreads, 1) void wgrad_wide2_kernel(WgradArgs p) {
+  constexpr int BM = 64;
+  constexpr int TH = BM * kWgRowBytes;   // 16 KB: BM rows x 128 columns
+  constexpr int TB = 2 * TH;             // 32 KB per operand tile
+  constexpr int SB = 2 * TB;             // 64 KB per stage
+  constexpr int IPW = BM / 16;           // 1 KB LDS-DMA wave-instructions per wave per operand tile
+  constexpr int QR = BM / 4;             // wave-instructions per operand half
+  constexpr int KS = BM / 16;            // k-steps per stage
+  __shared__ __attribute__((aligned(16))) uint8_t smem[2 * SB];
+  typedef __attribute__((address_space(3))) void lds_void;
+
+  int bid = blockIdx.x;
+  if (p.remap) bid = (bid & 7) * int(gridDim.x >> 3) + (bid >> 3);
+  const int split = p.split_major ? bid / p.tiles_total : bid % p.S;
+  const int tile = p.split_major ? bid - split * p.tiles_total : bid / p.S;
+  const int n0 = (tile / p.tiles_k) * kWwTile;
+  const int k0 = (tile % p.tiles_k) * kWwTile;
+  const int mb = split * p.m_split;
+  const int me = min(p.M, mb + p.m_split);
+  const int nst = me > mb ? (me - mb + BM - 1) / BM : 0;
+
+  const int t = threadIdx.x, lane = t & 63, wave = __builtin_amdgcn_readfirstlane(t >> 6);
+  const int wn = wave >> 2, wk = wave & 3;
+  const bool do_bias = __builtin_amdgcn_readfirstlane(p.bias && k0 == 0 && wk == 0);
+  if (wave >= 4) __builtin_amdgcn_s_setprio(1);
+
+  // LDS-DMA source rows of stage 0: instruction i of this wave fills rows 4 rq .. 4 rq + 3 of
+  // column half ``half``; lane (lr, slot) row 4 rq + lr, swizzled 16-byte chunk
+  const int lr = lane >> 4, slot = lane & 15;
+  const uint16_t* row_a[IPW];
+  const uint16_t* row_b[IPW];
+  int row_r[IPW], lds_off[IPW];
+#pragma unroll
+  for (int i = 0; i < IPW; ++i) {
+    const int j = IPW * wave + i;          // 0 .. 2*QR-1
+    const int half = j / QR, rq = j % QR;
+    const int r = 4 * rq + lr;
+    const int ch = slot ^ (((r & 3) << 2) | ((r >> 2) & 3));
+    row_r[i] = r;
+    lds_off[i] = half * TH + 1024 * rq;
+    row_a[i] = p.dy + int64_t(mb + r) * p.ldy + min(n0 + half * 128 + ch * 8, p.N - 8);
+    row_b[i] = p.x + int64_t(mb + r) * p.ldx + min(k0 + half * 128 + ch * 8, p.K - 8);
+  }
+  auto issue = [&](int st) {
+    uint8_t* A = smem + (st & 1) * SB;
+    uint8_t* B = A + TB;
+    const int m_base = mb + st * BM;
+    const int64_t adv_a = int64_t(st * BM) * p.ldy, adv_b = int64_t(st * BM) * p.ldx;
+    const bool full = m_base + BM <= me;  // wave-uniform
+#pragma unroll
+    for (int i = 0; i < IPW; ++i) {
+      const bool okm = full || m_base + row_r[i] < me;
+      const uint16_t* ga = okm ? row_a[i] + adv_a : p.zero;
+      const uint16_t* gb = okm ? row_b[i] + adv_b : p.zero;
+      wg_dma16(ga, __builtin_amdgcn_readfirstlane(uint32_t(size_t((lds_void*)(A + lds_off[i])))));
+      wg_dma16(gb, __builtin_amdgcn_readfirstlane(uint32_t(size_t((lds_void*)(B + lds_off[i])))));
+    }
+  };
+
+  wg_f32x16 c[4][2];
+#pragma unroll
+  for (int f = 0; f < 4; ++f)
+#pragma unroll
+    for (int e = 0; e < 2; ++e)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) c[f][e][i] = 0.f;
+  float bs[4] = {0.f, 0.f, 0.f, 0.f};
+
+  const int g = lane >> 4, i16 = lane & 15, q = i16 >> 2, pp = i16 & 3, h = lane >> 5;
+  const int bo = 8 * (pp & 1);
+  const int r0 = 8 * h + q;
+  const int cbase = 2 * (g & 1) + (pp >> 1);
+  int oa[4][2], ob[2][2];
 #pragma unroll
   for (int f = 0; f < 4; ++f) {
+    oa[f][0] = wn * TH + wg_swz(r0, cbase + 4 * f) + bo;
+    oa[f][1] = wn * TH + wg_swz(r0 + 4, cbase + 4 * f) + bo;
+  }
+  const int kc = 8 * (wk & 1);
 #pragma unroll
-    for (int e = 0; e < 2; ++e) {
-      const int col = k0 + (wk >> 1) * 128 + (wk & 1) * 64 + 32 * e + col_l;
-      if (col < p.K) {
+  for (int e = 0; e < 2; ++e) {
+    ob[e][0] = (wk >> 1) * TH + wg_swz(r0, kc + cbase + 4 * e) + bo;
+    ob[e][1] = (wk >> 1) * TH + wg_swz(r0 + 4, kc + cbase + 4 * e) + bo;
+  }
+  typedef __bf16 wg_bf16x2 __attribute__((ext_vector_type(2)));
+  const wg_bf16x2 one2 = {static_cast<__bf16>(1.0f), static_cast<__bf16>(1.0f)};
+  auto load_frags = [&](const uint8_t* A, int kk, wg_bf16x8 (&fa)[4], wg_bf16x8 (&fb)[2]) {
+    const uint8_t* Ak = A + 4096 * kk;
+    const uint8_t* Bk = A + TB + 4096 * kk;
 #pragma unroll
-        for (int reg = 0; reg < 16; ++reg) {
-          const int row = n0 + wn * 128 + 32 * f + (reg & 3) + 8 * (reg >> 2) + 4 * h;
-          if (row < p.N) {
-            if (p.S == 1) {
-              wg_store_out(p.dw, int64_t(row) * p.ldw + col, c[f][e][reg], p.accumulate, p.out_f32);
-            } else {
-              p.ws[(int64_t(split) * p.N + row) * p.ws_ld + col] = c[f][e][reg];
-            }
-          }
+    for (int f = 0; f < 4; ++f) fa[f] = wg_frag_at(Ak, oa[f][0], oa[f][1]);
+#pragma unroll
+    for (int e = 0; e < 2; ++e) fb[e] = wg_frag_at(Bk, ob[e][0], ob[e][1]);
+  };
+
+  if (nst > 0) issue(0);
+  for (int st = 0; st < nst; ++st) {
+    wg_wait_vm<0>();                // this wave's DMAs of stage st landed
+    __builtin_amdgcn_s_barrier();   // everyone's landed; everyone finished reading stage st-1
+    if (st + 1 < nst) issue(st + 1);  // refills stage st-1's buffer while stage st is computed
+    const uint8_t* A = smem + (st & 1) * SB;
+    wg_bf16x8 a[4], b[2];
+    load_frags(A, 0, a, b);
+#pragma unroll
+    for (int kk = 0; kk < KS; ++kk) {
+      wg_bf16x8 na[4], nb[2];
+      if (kk + 1 < KS) load_frags(A, kk + 1, na, nb);
+#pragma unroll
+      for (int f = 0; f < 4; ++f)
+#pragma unroll
+        for (int e = 0; e < 2; ++e) c[f][e] = wg_mfma(b[e], a[f], c[f][e]);  // C^T tile: lane = n
+      if (do_bias) {
+#pragma unroll
+        for (int f = 0; f < 4; ++f) {
+          const uint4 u = __builtin_bit_cast(uint4, a[f]);
+          bs[f] = __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(wg_bf16x2, u.x), one2, bs[f], false);
+          bs[f] = __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(wg_bf16x2, u.y), one2, bs[f], false);
+          bs[f] = __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(wg_bf16x2, u.z), one2, bs[f], false);
+          bs[f] = __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(wg_bf16x2, u.w), one2, bs[f], false);
         }
       }
-    }
-  }
-  if (do_bias) {
-    // lane l (< 32) and l + 32 hold tokens 8h..8h+7 of every k-step for row 32f + l
+      if (kk + 1 < KS) {
 #pragma unroll
-    for (int f = 0; f < 4; ++f) {
-      const float tot = bs[f] + __shfl_xor(bs[f], 32);
-      const int row = n0 + wn * 128 + 32 * f + col_l;
-      if (h == 0 && row < p.N) {
-        if (p.S == 1) {
-          wg_store_out(p.db, row, tot, p.accumulate, p.out_f32);
-        } else {
-          p.ws[int64_t(p.S) * p.N * p.ws_ld + int64_t(split) * p.N + row] = tot;
-        }
+        for (int f = 0; f < 4; ++f) a[f] = na[f];
+#pragma unroll
+        for (int e = 0; e < 2; ++e) b[e] = nb[e];
       }
     }
+    // this stage's fragment reads are consumed before the next barrier releases its buffer
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   }
+  if (wave >= 4) __builtin_amdgcn_s_setprio(0);
+  wide_epilogue_t(p, split, n0, k0, wn, wk, lane, c, bs, do_bias);
 }
 
 // dW[n][k] (+)= sum_s ws[s][n][k]; db[n] (+)= sum_s wsb[s][n].  4 columns per thread (K % 8 == 0).
@@ -782,7 +1003,7 @@ void wgrad_gemm(uintptr_t dy, int64_t ldy, uintptr_t x, int64_t ldx, uintptr_t d
   a.out_f32 = out_dt == kF32 ? 1 : 0;
   VODA_CHECK(!a.out_f32 || (ldw % 4 == 0 && dw % 16 == 0), "wgrad: fp32 dW rows must be 16-byte aligned");
   hipStream_t s = as_stream(stream);
-  VODA_CHECK(variant >= 0 && variant <= 8, "wgrad: variant must be 0..8");
+  VODA_CHECK(variant >= 0 && variant <= 9, "wgrad: variant must be 0..9");
   if (variant == 0)
     hipLaunchKernelGGL(wgrad_kernel, dim3(unsigned(pl.grid)), dim3(kWgThreads), 0, s, a);
   else if (variant == 1)
@@ -799,8 +1020,10 @@ void wgrad_gemm(uintptr_t dy, int64_t ldy, uintptr_t x, int64_t ldx, uintptr_t d
     hipLaunchKernelGGL((wgrad_wide_kernel<4, 32>), dim3(unsigned(pl.grid)), dim3(kWwThreads), 0, s, a);
   else if (variant == 7)
     hipLaunchKernelGGL((wgrad_wide_kernel<5, 32>), dim3(unsigned(pl.grid)), dim3(kWwThreads), 0, s, a);
-  else
+  else if (variant == 8)
     hipLaunchKernelGGL((wgrad_wide_kernel<3, 32>), dim3(unsigned(pl.grid)), dim3(kWwThreads), 0, s, a);
+  else
+    hipLaunchKernelGGL(wgrad_wide2_kernel, dim3(unsigned(pl.grid)), dim3(kWwThreads), 0, s, a);
   check_launch();
   if (pl.S > 1) {
     if (a.out_f32)

@@ -16,8 +16,10 @@ def test_default_splits_cover_the_chip():
     assert ds(300, 768, 768) == 1         # few tokens: no split
     assert ds(8192, 4096, 4096) == 1
     # 256 x 256 tiles, one workgroup per CU
-    assert W.default_splits(8192, 3072, 768, variant=6) == 8     # 36 tiles
-    assert W.default_splits(8192, 768, 768, variant=6) == 29     # 9 tiles
+    # 256 x 256 tiles, one workgroup per CU: at most one round of 256 workgroups
+    assert W.default_splits(8192, 3072, 768, variant=6) == 7     # 36 tiles -> 252
+    assert W.default_splits(8192, 768, 768, variant=9) == 28     # 9 tiles -> 252
+    assert W.default_splits(8192, 2304, 768, variant=9) == 9     # 27 tiles -> 243
 
 
 def test_cpu_path_matches_reference():
@@ -58,7 +60,7 @@ def _check(dy, x, gw, gb, accumulate, splits, with_bias=True, variant=None):
 @pytest.mark.parametrize("M,N,K", [(64, 128, 128), (200, 136, 72), (1280, 768, 768), (777, 256, 384),
                                    (8192, 768, 3072)])
 @pytest.mark.parametrize("splits", [1, 3, 8])
-@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5, 6, 7, 8])
+@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5, 6, 7, 8, 9])
 def test_wgrad_kernel_matches_fp32(M, N, K, splits, variant):
     dy, x, gw, gb = _case(M, N, K)
     _check(dy, x, gw, gb, True, splits, variant=variant)
@@ -66,7 +68,7 @@ def test_wgrad_kernel_matches_fp32(M, N, K, splits, variant):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("splits", [1, 4])
-@pytest.mark.parametrize("variant", [0, 1, 4, 6, 7])
+@pytest.mark.parametrize("variant", [0, 1, 4, 6, 7, 9])
 def test_wgrad_kernel_overwrite_and_no_bias(splits, variant):
     dy, x, gw, gb = _case(512, 192, 320, seed=3)
     _check(dy, x, gw, gb, False, splits, variant=variant)
@@ -82,7 +84,7 @@ def test_wgrad_kernel_identity_operand():
     x = torch.randn(M, K, device="cuda").bfloat16()
     gw = torch.zeros(N, K, device="cuda", dtype=torch.bfloat16)
     gb = torch.zeros(N, device="cuda", dtype=torch.bfloat16)
-    for s, v in ((1, 0), (3, 0), (1, 1), (3, 1), (2, 2), (3, 3), (1, 4), (3, 4), (2, 5), (1, 6), (3, 6), (2, 7), (3, 8)):
+    for s, v in ((1, 0), (3, 0), (1, 1), (3, 1), (2, 2), (3, 3), (1, 4), (3, 4), (2, 5), (1, 6), (3, 6), (2, 7), (3, 8), (1, 9), (3, 9)):
         gw.zero_()
         gb.zero_()
         W.wgrad_accumulate_(dy, x, gw, gb, splits=s, variant=v)
@@ -97,7 +99,7 @@ def test_wgrad_strided_rows_and_deterministic():
     dy, x = base_dy[:, 128:128 + 768], base_x[:, :256]      # row strides 1024 / 512
     gw = torch.zeros(768, 256, device="cuda", dtype=torch.bfloat16)
     assert W.supported(dy, x, gw)
-    for v in (2, 6):
+    for v in (2, 6, 9):
         gw.zero_()
         W.wgrad_accumulate_(dy, x, gw, None, splits=4, variant=v)
         first = gw.clone()
@@ -130,7 +132,7 @@ def test_fused_linear_backward_uses_kernel_and_matches_autograd():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("variant", [0, 2, 6])
+@pytest.mark.parametrize("variant", [0, 2, 6, 9])
 @pytest.mark.parametrize("splits", [1, 4])
 @pytest.mark.parametrize("accumulate", [True, False])
 def test_wgrad_kernel_fp32_output(variant, splits, accumulate):

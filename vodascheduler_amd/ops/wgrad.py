@@ -20,7 +20,8 @@ from . import _native as N
 TILE = 128
 # 0: register-staged LDS double buffer; 1 / 2 / 3: LDS ring of 4 / 2 / 3 stages of 64 tokens
 # filled by global_load_lds; 4 / 5: ring of 4 / 5 stages of 32 tokens; 6 / 7 / 8: 256 x 256
-# tile, 8 waves, ring of 4 x 32 / 2 x 64 / 3 x 32 tokens.  Default 2 (64 KB ring, 2 workgroups per CU): fastest in the BERT-base step
+# tile, 8 waves, ring of 4 x 32 / 5 x 32 / 3 x 32 tokens; 9: 256 x 256 tile on two 64-token
+# stages (128 KB).  Default 2 (64 KB ring, 2 workgroups per CU): fastest in the BERT-base step
 # on MI355X (profiles/r1_wgrad_v3.md)
 VARIANT = int(os.environ.get("VODA_WGRAD_VARIANT", "2"))
 # VODA_WGRAD_VARIANT set explicitly = that variant for every shape (A/B runs); otherwise
@@ -30,11 +31,21 @@ VARIANT = int(os.environ.get("VODA_WGRAD_VARIANT", "2"))
 # 95-96 -> 79 us with variant 3, and variant 1 once the block order became split-major;
 # stages 3-4 and the BERT shapes gain nothing)
 _VARIANT_FIXED = "VODA_WGRAD_VARIANT" in os.environ
+# VODA_WGRAD_WIDE=0 (A/B switch): keep every shape on the 128 x 128 tile
+_WIDE = os.environ.get("VODA_WGRAD_WIDE", "1") != "0"
 
 
 def choose(M: int, N_: int, K: int) -> tuple[int, int]:
     """(variant, splits) for a weight-gradient GEMM of M reduction rows."""
-    if _VARIANT_FIXED or M < 150_000:
+    if _VARIANT_FIXED:
+        return VARIANT, default_splits(M, N_, K, variant=VARIANT)
+    if M < 150_000:
+        # >= 16 tiles of 256 x 256 and >= 4096 tokens: the wide two-stage kernel (variant 9)
+        # at one round of <= 256 workgroups; per-shape sweep on MI355X (BERT-base, fp32 dW,
+        # profiles/r3/wgrad_v9_sweep.jsonl): qkv 60.7 -> 55.2 us, fc1 67.8 -> 62.8, fc2
+        # 68.1 -> 62.4; the 768 x 768 projection (9 wide tiles) stays on the 128 x 128 tile
+        if _WIDE and M >= 4096 and math.ceil(N_ / WIDE_TILE) * math.ceil(K / WIDE_TILE) >= 16:
+            return 9, default_splits(M, N_, K, variant=9)
         return VARIANT, default_splits(M, N_, K, variant=VARIANT)
     # split-major block order re-sweep (profiles/raw/r2_wgrad_sweep_split_major.jsonl): the
     # 4-stage ring at half the default split count is best for stage 2 too (75-76 -> 72 us)
@@ -50,7 +61,7 @@ def _zero_rows(device: torch.device) -> torch.Tensor:
     return z
 
 
-WIDE_TILE = 256  # variants 6-8: 256 x 256 outputs per workgroup, one workgroup per CU
+WIDE_TILE = 256  # variants 6-9: 256 x 256 outputs per workgroup, one workgroup per CU
 
 
 def default_splits(M: int, N_: int, K: int, target_blocks: int | None = None, variant: int | None = None) -> int:
@@ -65,7 +76,8 @@ def default_splits(M: int, N_: int, K: int, target_blocks: int | None = None, va
     if target_blocks is None:
         target_blocks = 256 if v >= 6 else 432
     tiles = math.ceil(N_ / tile) * math.ceil(K / tile)
-    s = math.ceil(target_blocks / tiles)
+    # wide tiles: one workgroup per CU, so the grid must not spill into a second round
+    s = target_blocks // tiles if v >= 6 else math.ceil(target_blocks / tiles)
     return max(1, min(s, 256, M // 256 if M >= 256 else 1))
 
 
