@@ -633,6 +633,341 @@ __global__ __launch_bounds__(64 * W) void attn_bwd_dkv_kernel(AttnArgs a) {
   }
 }
 
+// ======================================================================== fused backward, T <= 128
+// One workgroup per (batch, head) computes dQ, dK and dV from a single read of Q, K, V, O and
+// dO (the two-pass form reads K / V in the dQ pass and Q / dO in the dK/dV pass, each tile
+// staged behind its own barrier pair): 4 waves, wave w owns keys 32w..32w+31 in the dK/dV
+// phase and queries 32w..32w+31 in the dQ phase.  Every operand lives in LDS as a plain row
+// image [128 rows][64] (128-byte rows); the transposed operands of the dV / dK / dQ products
+// come out of the same images through ds_read_b64_tr_b16, so nothing is staged transposed.
+//   prologue : Q, dO rows -> images A, B; delta = rowsum(dO o O); lse; mask codes
+//   dK / dV  : per 32-query tile  S = Q K^T, dP = dO V^T (key on the lane), P, dS,
+//              dV^T += dO^T P, dK^T += Q^T dS
+//   dQ       : K, V rows (held in registers since the prologue) -> images A, B, then per
+//              32-key tile S^T = K Q^T, dP^T = V dO^T (query on the lane), dQ^T += K^T dS^T
+// LDS 33 KB: up to 4 workgroups per CU by LDS, registers permitting.
+constexpr int kFusedT = 128;                       // max Tq, Tk
+constexpr int kFusedImg = kFusedT * 64 * 2;        // one row image, bytes
+
+// byte offset of element (row, col) of a row image: 16-byte chunk col / 8 XOR-swizzled by the
+// row so that the row-fragment reads (lane r: row r, one chunk), the transposed reads (4 rows
+// x 4 chunks per 32 lanes) and the 16-byte staging writes are all conflict-free
+__device__ __forceinline__ int fimg_off(int row, int col) {
+  const int x = (row >> 1) & 7;
+  const int sw = ((x & 1) << 2) | (x & 2) | ((x >> 2) & 1);
+  return row * 128 + 16 * ((col >> 3) ^ sw) + 2 * (col & 7);
+}
+// 8 consecutive elements (row, 8c .. 8c + 7)
+__device__ __forceinline__ bf16x8 fimg_row(const uint8_t* img, int row, int c8) {
+  return __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(img + fimg_off(row, 8 * c8)));
+}
+typedef __bf16 fimg_bf16x4 __attribute__((__vector_size__(4 * sizeof(__bf16))));
+typedef __attribute__((address_space(3))) fimg_bf16x4 fimg_lds_bf16x4;
+__device__ __forceinline__ uint2 fimg_tr(const uint8_t* img, int off) {
+  const fimg_bf16x4 v = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((fimg_lds_bf16x4*)(img + off));
+  return __builtin_bit_cast(uint2, v);
+}
+// Operand whose k index runs over the ROWS of an image, in acc_frag's permuted order (k-step
+// s): lane (r, h) gets column c0 + r, rows R0 + 16s + 4h + 0..3 and R0 + 16s + 8 + 4h + 0..3.
+// ds_read_b64_tr_b16: lane 4qq + p of a 16-lane group names row qq of a 4-row block, columns
+// 4p..4p+3 of the group's 16; lane i of the group receives column i.
+__device__ __forceinline__ bf16x8 fimg_trfrag(const uint8_t* img, int R0, int c0, int s, int lane) {
+  const int g = lane >> 4, i = lane & 15, qq = i >> 2, p = i & 3;
+  const int col = c0 + 16 * (g & 1) + 4 * p;
+  const int row = R0 + 16 * s + 4 * (g >> 1) + qq;
+  const uint2 lo = fimg_tr(img, fimg_off(row, col));
+  const uint2 hi = fimg_tr(img, fimg_off(row + 8, col));
+  return __builtin_bit_cast(bf16x8, make_uint4(lo.x, lo.y, hi.x, hi.y));
+}
+
+// Registers capped for 3 waves per SIMD (168; the K / V fragments spill 72 B): all 768
+// BERT-base workgroups resident at once, 39.2 -> 37.0 us per layer.
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void attn_bwd_fused_kernel(AttnArgs a) {
+  constexpr int D = 64, KS = 4, DT = 2;
+  __shared__ __attribute__((aligned(16))) uint8_t smem[2 * kFusedImg + 2 * kFusedT * 4 + kFusedT + 16];
+  uint8_t* imgA = smem;                 // Q rows, then K rows
+  uint8_t* imgB = smem + kFusedImg;     // dO rows, then V rows
+  float* lse_s = reinterpret_cast<float*>(smem + 2 * kFusedImg);
+  float* del_s = lse_s + kFusedT;
+  uint8_t* Ms = reinterpret_cast<uint8_t*>(del_s + kFusedT);  // codes of keys 0..127 + 4 tile flags
+
+  const int bh = blockIdx.x, b = bh / a.H, hh = bh % a.H;
+  const int t = threadIdx.x, lane = t & 63, r = lane & 31, h = lane >> 5, w = t >> 6;
+  const int own = 32 * w + r;  // this lane's key (dK/dV phase) and query (dQ phase)
+  const int Tq = a.Tq, Tk = a.Tk;
+
+  // ---- prologue: every global load issued before any is used
+  const bool kvv = own < Tk, qv = own < Tq;
+  const uint16_t* krow = a.k + b * a.k_sb + hh * a.k_sh + int64_t(min(own, Tk - 1)) * a.k_st;
+  const uint16_t* vrow = a.v + b * a.v_sb + hh * a.v_sh + int64_t(min(own, Tk - 1)) * a.v_st;
+  const uint16_t* qrow = a.q + b * a.q_sb + hh * a.q_sh + int64_t(min(own, Tq - 1)) * a.q_st;
+  const uint16_t* dorow = a.dout + b * a.do_sb + hh * a.do_sh + int64_t(min(own, Tq - 1)) * a.do_st;
+  const uint16_t* orow = a.o + b * a.o_sb + hh * a.o_sh + int64_t(min(own, Tq - 1)) * a.o_st;
+  bf16x8 kf[KS], vf[KS], qf[KS], dof[KS], of[KS];
+#pragma unroll
+  for (int s = 0; s < KS; ++s) {
+    kf[s] = ld16(krow + 16 * s + 8 * h);
+    vf[s] = ld16(vrow + 16 * s + 8 * h);
+    qf[s] = ld16(qrow + 16 * s + 8 * h);
+    dof[s] = ld16(dorow + 16 * s + 8 * h);
+    of[s] = ld16(orow + 16 * s + 8 * h);
+  }
+  const float lse_own = a.lse[int64_t(bh) * Tq + min(own, Tq - 1)];
+  const uint8_t* mrow = a.mask != nullptr ? a.mask + b * a.mask_sb : nullptr;
+  const uint32_t mraw = (mrow != nullptr && t < kFusedT) ? mrow[min(t, Tk - 1)] : 1u;
+#pragma unroll
+  for (int s = 0; s < KS; ++s) {  // rows past T are zero
+    if (!kvv) { kf[s] = zero_bf8(); vf[s] = zero_bf8(); }
+    if (!qv) { qf[s] = zero_bf8(); dof[s] = zero_bf8(); of[s] = zero_bf8(); }
+  }
+  float dpart = 0.f;
+#pragma unroll
+  for (int s = 0; s < KS; ++s) {
+    *reinterpret_cast<uint4*>(imgA + fimg_off(own, 16 * s + 8 * h)) = __builtin_bit_cast(uint4, qf[s]);
+    *reinterpret_cast<uint4*>(imgB + fimg_off(own, 16 * s + 8 * h)) = __builtin_bit_cast(uint4, dof[s]);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) dpart += float(dof[s][j]) * float(of[s][j]);
+  }
+  const float delta_own = dpart + __shfl_xor(dpart, 32, 64);
+  if (h == 0) {
+    lse_s[own] = qv ? lse_own : __builtin_huge_valf();  // rows past Tq: P = 0
+    del_s[own] = qv ? delta_own : 0.f;
+  }
+  // mask code of key t (threads 0..127 = waves 0, 1) and one flag per 32-key tile
+  const uint32_t code = t < kFusedT ? (t >= Tk ? 2u : (mraw == 0 ? 1u : 0u)) : 0u;
+  if (t < kFusedT) Ms[t] = uint8_t(code);
+  const uint64_t any = __ballot(code != 0);
+  if (w < 2 && lane == 0) {
+    Ms[kFusedT + 2 * w] = uint32_t(any) != 0 ? 1 : 0;
+    Ms[kFusedT + 2 * w + 1] = uint32_t(any >> 32) != 0 ? 1 : 0;
+  }
+  __syncthreads();
+
+  // ---- dK / dV: key = own on the lane
+  const uint32_t kcode = Ms[own];
+  const float kadd = kcode == 2 ? kNegInf : (kcode == 1 ? kMaskNeg : 0.f);
+  const int key_hi = __builtin_amdgcn_readfirstlane(32 * w + 31);
+  f32x16 dk[DT], dv[DT];
+#pragma unroll
+  for (int tt = 0; tt < DT; ++tt) { dk[tt] = zero16(); dv[tt] = zero16(); }
+  const int nqt = (Tq + 31) / 32;
+  for (int qt = 0; qt < nqt; ++qt) {
+    const int R0 = 32 * qt;
+    f32x16 sacc = zero16(), dp = zero16();
+#pragma unroll
+    for (int s = 0; s < KS; ++s) {
+      sacc = mfma(fimg_row(imgA, R0 + r, 2 * s + h), kf[s], sacc);   // S[query][key]
+      dp = mfma(fimg_row(imgB, R0 + r, 2 * s + h), vf[s], dp);       // dP[query][key]
+    }
+    if (a.causal && R0 < key_hi) {
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const int ql = R0 + crow(i, h);
+        sacc[i] = __expf(sacc[i] * a.scale + causal_add(kadd, own, ql) - lse_s[ql]);
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < 16; ++i) sacc[i] = __expf(sacc[i] * a.scale + kadd - lse_s[R0 + crow(i, h)]);
+    }
+#pragma unroll
+    for (int i = 0; i < 16; ++i) dp[i] = sacc[i] * (dp[i] - del_s[R0 + crow(i, h)]);  // dS
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      const bf16x8 pf = acc_frag(sacc, s), gf = acc_frag(dp, s);
+#pragma unroll
+      for (int tt = 0; tt < DT; ++tt) {
+        dv[tt] = mfma(fimg_trfrag(imgB, R0, 32 * tt, s, lane), pf, dv[tt]);  // dV^T[d][key] += dO^T P
+        dk[tt] = mfma(fimg_trfrag(imgA, R0, 32 * tt, s, lane), gf, dk[tt]);  // dK^T[d][key] += Q^T dS
+      }
+    }
+  }
+  uint16_t* dkb = a.dk + b * a.dk_sb + hh * a.dk_sh;
+  uint16_t* dvb = a.dv + b * a.dv_sb + hh * a.dv_sh;
+#pragma unroll
+  for (int tt = 0; tt < DT; ++tt) {
+    store_lane_rows(dkb, a.dk_st, own, Tk, 32 * tt, dk[tt], a.scale, h);
+    store_lane_rows(dvb, a.dv_st, own, Tk, 32 * tt, dv[tt], 1.f, h);
+  }
+
+  // ---- K, V rows replace Q, dO in the images; this lane's query fragments are read back
+  // first (re-read rather than held through the dK/dV phase: 32 fewer live registers there)
+  bf16x8 qf2[KS], dof2[KS];
+#pragma unroll
+  for (int s = 0; s < KS; ++s) {
+    qf2[s] = fimg_row(imgA, own, 2 * s + h);
+    dof2[s] = fimg_row(imgB, own, 2 * s + h);
+  }
+  __syncthreads();  // every wave is done reading images A / B
+#pragma unroll
+  for (int s = 0; s < KS; ++s) {
+    *reinterpret_cast<uint4*>(imgA + fimg_off(own, 16 * s + 8 * h)) = __builtin_bit_cast(uint4, kf[s]);
+    *reinterpret_cast<uint4*>(imgB + fimg_off(own, 16 * s + 8 * h)) = __builtin_bit_cast(uint4, vf[s]);
+  }
+  __syncthreads();
+
+  // ---- dQ: query = own on the lane
+  const float lse_q = qv ? lse_own : __builtin_huge_valf();
+  const float del_q = qv ? delta_own : 0.f;
+  const int q_lo = __builtin_amdgcn_readfirstlane(32 * w);
+  f32x16 dq[DT];
+#pragma unroll
+  for (int tt = 0; tt < DT; ++tt) dq[tt] = zero16();
+  const int nkt = (Tk + 31) / 32;
+  for (int kt = 0; kt < nkt; ++kt) {
+    const int R0 = 32 * kt;
+    f32x16 st = zero16(), dpt = zero16();
+#pragma unroll
+    for (int s = 0; s < KS; ++s) {
+      st = mfma(fimg_row(imgA, R0 + r, 2 * s + h), qf2[s], st);     // S^T[key][query]
+      dpt = mfma(fimg_row(imgB, R0 + r, 2 * s + h), dof2[s], dpt);  // dP^T[key][query]
+    }
+    const bool tile_mask = __builtin_amdgcn_readfirstlane(uint32_t(Ms[kFusedT + kt])) != 0;
+    if (tile_mask || (a.causal && R0 + 31 > q_lo)) {
+      uint32_t mw[4];
+      load_mask_words(Ms + R0, h, mw);
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        float add = mask_code_add(mw, i);
+        if (a.causal) add = causal_add(add, R0 + crow(i, h), own);
+        st[i] = st[i] * a.scale + add;
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < 16; ++i) st[i] *= a.scale;
+    }
+#pragma unroll
+    for (int i = 0; i < 16; ++i) st[i] = __expf(st[i] - lse_q) * (dpt[i] - del_q);  // dS^T
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      const bf16x8 gf = acc_frag(st, s);
+#pragma unroll
+      for (int tt = 0; tt < DT; ++tt) dq[tt] = mfma(fimg_trfrag(imgA, R0, 32 * tt, s, lane), gf, dq[tt]);  // K^T dS^T
+    }
+  }
+  uint16_t* dqb = a.out + b * a.out_sb + hh * a.out_sh;
+#pragma unroll
+  for (int tt = 0; tt < DT; ++tt) store_lane_rows(dqb, a.out_st, own, Tq, 32 * tt, dq[tt], a.scale, h);
+  if (h == 0 && qv) a.delta[int64_t(bh) * Tq + own] = delta_own;
+}
+
+// ======================================================================== resident forward, T <= 128
+// Same geometry as the fused backward: one workgroup per (batch, head), wave w owns queries
+// 32w..32w+31, K and V rows staged ONCE into two row images (each lane writes the row it
+// loaded), one barrier, then all key tiles from LDS.  Every score of a query row is in the
+// lane's registers (4 tiles x 16), so the softmax is exact in two passes -- no running max,
+// no rescaling of the output accumulators -- and V^T comes out of the V row image through
+// ds_read_b64_tr_b16 (no transposed staging writes).
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void attn_fwd_res_kernel(AttnArgs a) {
+  constexpr int KS = 4, DT = 2, NKT = kFusedT / 32;
+  __shared__ __attribute__((aligned(16))) uint8_t smem[2 * kFusedImg + kFusedT + 16];
+  uint8_t* imgK = smem;
+  uint8_t* imgV = smem + kFusedImg;
+  uint8_t* Ms = smem + 2 * kFusedImg;  // codes of keys 0..127 + 4 tile flags
+
+  const int bh = blockIdx.x, b = bh / a.H, hh = bh % a.H;
+  const int t = threadIdx.x, lane = t & 63, r = lane & 31, h = lane >> 5, w = t >> 6;
+  const int own = 32 * w + r;  // this lane's query; also the K / V row it stages
+  const int Tq = a.Tq, Tk = a.Tk;
+  const bool kvv = own < Tk, qv = own < Tq;
+  const uint16_t* krow = a.k + b * a.k_sb + hh * a.k_sh + int64_t(min(own, Tk - 1)) * a.k_st;
+  const uint16_t* vrow = a.v + b * a.v_sb + hh * a.v_sh + int64_t(min(own, Tk - 1)) * a.v_st;
+  const uint16_t* qrow = a.q + b * a.q_sb + hh * a.q_sh + int64_t(min(own, Tq - 1)) * a.q_st;
+  bf16x8 kf[KS], vf[KS], qf[KS];
+#pragma unroll
+  for (int s = 0; s < KS; ++s) {
+    kf[s] = ld16(krow + 16 * s + 8 * h);
+    vf[s] = ld16(vrow + 16 * s + 8 * h);
+    qf[s] = ld16(qrow + 16 * s + 8 * h);
+  }
+  const uint8_t* mrow = a.mask != nullptr ? a.mask + b * a.mask_sb : nullptr;
+  const uint32_t mraw = (mrow != nullptr && t < kFusedT) ? mrow[min(t, Tk - 1)] : 1u;
+#pragma unroll
+  for (int s = 0; s < KS; ++s) {
+    const uint4 kz = kvv ? __builtin_bit_cast(uint4, kf[s]) : make_uint4(0, 0, 0, 0);
+    const uint4 vz = kvv ? __builtin_bit_cast(uint4, vf[s]) : make_uint4(0, 0, 0, 0);
+    *reinterpret_cast<uint4*>(imgK + fimg_off(own, 16 * s + 8 * h)) = kz;
+    *reinterpret_cast<uint4*>(imgV + fimg_off(own, 16 * s + 8 * h)) = vz;
+    if (!qv) qf[s] = zero_bf8();
+  }
+  const uint32_t code = t < kFusedT ? (t >= Tk ? 2u : (mraw == 0 ? 1u : 0u)) : 0u;
+  if (t < kFusedT) Ms[t] = uint8_t(code);
+  const uint64_t any = __ballot(code != 0);
+  if (w < 2 && lane == 0) {
+    Ms[kFusedT + 2 * w] = uint32_t(any) != 0 ? 1 : 0;
+    Ms[kFusedT + 2 * w + 1] = uint32_t(any >> 32) != 0 ? 1 : 0;
+  }
+  __syncthreads();
+
+  // ---- scores S^T[key][query] of every key tile (lane = query), masked and scaled
+  const int nkt = (Tk + 31) / 32;
+  const int q_lo = __builtin_amdgcn_readfirstlane(32 * w);
+  f32x16 sc[NKT];
+  float m = -1e30f;
+#pragma unroll
+  for (int kt = 0; kt < NKT; ++kt) {
+    sc[kt] = zero16();
+    if (kt < nkt) {
+      const int R0 = 32 * kt;
+#pragma unroll
+      for (int s = 0; s < KS; ++s) sc[kt] = mfma(fimg_row(imgK, R0 + r, 2 * s + h), qf[s], sc[kt]);
+      const bool tile_mask = __builtin_amdgcn_readfirstlane(uint32_t(Ms[kFusedT + kt])) != 0;
+      if (tile_mask || (a.causal && R0 + 31 > q_lo)) {
+        uint32_t mw[4];
+        load_mask_words(Ms + R0, h, mw);
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          float add = mask_code_add(mw, i);
+          if (a.causal) add = causal_add(add, R0 + crow(i, h), own);
+          sc[kt][i] = sc[kt][i] * a.scale + add;
+        }
+      } else {
+#pragma unroll
+        for (int i = 0; i < 16; ++i) sc[kt][i] *= a.scale;
+      }
+#pragma unroll
+      for (int i = 0; i < 16; ++i) m = fmaxf(m, sc[kt][i]);
+    }
+  }
+  m = fmaxf(m, __shfl_xor(m, 32, 64));
+  // ---- P = exp(S - max), row sums, O^T[d][query] += V^T P^T
+  float l = 0.f;
+  f32x16 o[DT];
+#pragma unroll
+  for (int tt = 0; tt < DT; ++tt) o[tt] = zero16();
+#pragma unroll
+  for (int kt = 0; kt < NKT; ++kt) {
+    if (kt < nkt) {
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const float p = __expf(sc[kt][i] - m);
+        sc[kt][i] = p;
+        l += p;
+      }
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        const bf16x8 pf = acc_frag(sc[kt], s);
+#pragma unroll
+        for (int tt = 0; tt < DT; ++tt) o[tt] = mfma(fimg_trfrag(imgV, 32 * kt, 32 * tt, s, lane), pf, o[tt]);
+      }
+    }
+  }
+  l += __shfl_xor(l, 32, 64);
+  const float inv = 1.f / l;
+  uint16_t* obase = a.out + b * a.out_sb + hh * a.out_sh;
+#pragma unroll
+  for (int tt = 0; tt < DT; ++tt) store_lane_rows(obase, a.out_st, own, Tq, 32 * tt, o[tt], inv, h);
+  if (h == 0 && qv) a.lse[int64_t(bh) * Tq + own] = m + __logf(l);
+}
+
+// VODA_ATTN_FUSED_BWD=0 (A/B switch, read once): keep the two-pass backward for T <= 128
+bool attn_fused_bwd_enabled() {
+  static const bool on = [] {
+    const char* e = std::getenv("VODA_ATTN_FUSED_BWD");
+    return e == nullptr || std::atoi(e) != 0;
+  }();
+  return on;
+}
+
 template <typename F>
 void dispatch_d(int D, F&& f) {
   if (D == 32) f(std::integral_constant<int, 32>{});
@@ -691,6 +1026,15 @@ void attention_fwd(const std::vector<int64_t>& t, int B, int H, int Tq, int Tk, 
   VODA_CHECK(attention_supported(D, Tq, Tk, kBF16), "attention_fwd: unsupported shape");
   VODA_CHECK(int64_t(B) * H <= 65535, "attention_fwd: B*H exceeds the grid's y dimension");
   const AttnArgs a = make_args(t, B, H, Tq, Tk, scale, causal);
+  static const bool res_fwd = [] {  // VODA_ATTN_RES_FWD=0 (A/B switch): streamed forward for T <= 128
+    const char* e = std::getenv("VODA_ATTN_RES_FWD");
+    return e == nullptr || std::atoi(e) != 0;
+  }();
+  if (D == 64 && Tq <= kFusedT && Tk <= kFusedT && res_fwd) {
+    hipLaunchKernelGGL(attn_fwd_res_kernel, dim3(unsigned(B * H)), dim3(256), 0, as_stream(stream), a);
+    check_launch();
+    return;
+  }
   dispatch_d(D, [&](auto dc) {
     dispatch_w(Tq, [&](auto wc) {
       constexpr int DD = decltype(dc)::value, WW = decltype(wc)::value;
@@ -708,6 +1052,11 @@ void attention_bwd(const std::vector<int64_t>& t, int B, int H, int Tq, int Tk, 
   VODA_CHECK(int64_t(B) * H <= 65535, "attention_bwd: B*H exceeds the grid's y dimension");
   const AttnArgs a = make_args(t, B, H, Tq, Tk, scale, causal);
   hipStream_t s = as_stream(stream);
+  if (D == 64 && Tq <= kFusedT && Tk <= kFusedT && attn_fused_bwd_enabled()) {
+    hipLaunchKernelGGL(attn_bwd_fused_kernel, dim3(unsigned(B * H)), dim3(256), 0, s, a);
+    check_launch();
+    return;
+  }
   dispatch_d(D, [&](auto dc) {
     constexpr int DD = decltype(dc)::value;
     dispatch_w(Tq, [&](auto wc) {
