@@ -741,15 +741,22 @@ __global__ __launch_bounds__(kWwThreads, 1) void wgrad_wide_kernel(WgradArgs p) 
 // advanced by one scalar product per stage.  Waves 4-7 (the second-dispatched half, the
 // loser of every issue arbitration) run at priority 1 (MI355X_MICROARCH.md, two waves per
 // SIMD, item 4).
+//
+// Template: STAGES LDS stages of BM tokens (<2, 64>: 128 KB, one stage in flight; <3, 48>:
+// 144 KB, two in flight); FILL_ONLY = a probe with the MFMAs and the epilogue removed (output
+// undefined; benchmarks/bench_wgrad.py --variants 10,11 times the operand fill alone).
+template <int STAGES, int BM, bool FILL_ONLY>
 __global__ __launch_bounds__(kWwThreads, 1) void wgrad_wide2_kernel(WgradArgs p) {
-  constexpr int BM = 64;
-  constexpr int TH = BM * kWgRowBytes;   // 16 KB: BM rows x 128 columns
-  constexpr int TB = 2 * TH;             // 32 KB per operand tile
-  constexpr int SB = 2 * TB;             // 64 KB per stage
+  constexpr int TH = BM * kWgRowBytes;   // BM rows x 128 columns
+  constexpr int TB = 2 * TH;             // per operand tile
+  constexpr int SB = 2 * TB;             // per stage
   constexpr int IPW = BM / 16;           // 1 KB LDS-DMA wave-instructions per wave per operand tile
+  constexpr int PER = 2 * IPW;           // LDS-DMA instructions per lane per stage
   constexpr int QR = BM / 4;             // wave-instructions per operand half
   constexpr int KS = BM / 16;            // k-steps per stage
-  __shared__ __attribute__((aligned(16))) uint8_t smem[2 * SB];
+  constexpr int D = STAGES - 1;          // stages in flight beyond the one being computed
+  static_assert(BM % 16 == 0 && STAGES * SB <= 160 * 1024, "LDS ring");
+  __shared__ __attribute__((aligned(16))) uint8_t smem[STAGES * SB];
   typedef __attribute__((address_space(3))) void lds_void;
 
   int bid = blockIdx.x;
@@ -761,7 +768,6 @@ __global__ __launch_bounds__(kWwThreads, 1) void wgrad_wide2_kernel(WgradArgs p)
   const int mb = split * p.m_split;
   const int me = min(p.M, mb + p.m_split);
   const int nst = me > mb ? (me - mb + BM - 1) / BM : 0;
-
   const int t = threadIdx.x, lane = t & 63, wave = __builtin_amdgcn_readfirstlane(t >> 6);
   const int wn = wave >> 2, wk = wave & 3;
   const bool do_bias = __builtin_amdgcn_readfirstlane(p.bias && k0 == 0 && wk == 0);
@@ -785,7 +791,7 @@ __global__ __launch_bounds__(kWwThreads, 1) void wgrad_wide2_kernel(WgradArgs p)
     row_b[i] = p.x + int64_t(mb + r) * p.ldx + min(k0 + half * 128 + ch * 8, p.K - 8);
   }
   auto issue = [&](int st) {
-    uint8_t* A = smem + (st & 1) * SB;
+    uint8_t* A = smem + (st % STAGES) * SB;
     uint8_t* B = A + TB;
     const int m_base = mb + st * BM;
     const int64_t adv_a = int64_t(st * BM) * p.ldy, adv_b = int64_t(st * BM) * p.ldx;
@@ -836,12 +842,17 @@ __global__ __launch_bounds__(kWwThreads, 1) void wgrad_wide2_kernel(WgradArgs p)
     for (int e = 0; e < 2; ++e) fb[e] = wg_frag_at(Bk, ob[e][0], ob[e][1]);
   };
 
-  if (nst > 0) issue(0);
+#pragma unroll
+  for (int s0 = 0; s0 < D; ++s0)
+    if (s0 < nst) issue(s0);
   for (int st = 0; st < nst; ++st) {
-    wg_wait_vm<0>();                // this wave's DMAs of stage st landed
+    // this wave's DMAs of stage st landed (at most min(D - 1, nst - 1 - st) later stages
+    // outstanding, PER instructions each)
+    wg_wait_ahead<PER>(min(D - 1, nst - 1 - st));
     __builtin_amdgcn_s_barrier();   // everyone's landed; everyone finished reading stage st-1
-    if (st + 1 < nst) issue(st + 1);  // refills stage st-1's buffer while stage st is computed
-    const uint8_t* A = smem + (st & 1) * SB;
+    if (st + D < nst) issue(st + D);  // refills stage st-1's buffer while stage st is computed
+    if constexpr (FILL_ONLY) continue;
+    const uint8_t* A = smem + (st % STAGES) * SB;
     wg_bf16x8 a[4], b[2];
     load_frags(A, 0, a, b);
 #pragma unroll
@@ -873,6 +884,7 @@ __global__ __launch_bounds__(kWwThreads, 1) void wgrad_wide2_kernel(WgradArgs p)
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   }
   if (wave >= 4) __builtin_amdgcn_s_setprio(0);
+  if constexpr (FILL_ONLY) return;
   wide_epilogue_t(p, split, n0, k0, wn, wk, lane, c, bs, do_bias);
 }
 
@@ -1003,7 +1015,7 @@ void wgrad_gemm(uintptr_t dy, int64_t ldy, uintptr_t x, int64_t ldx, uintptr_t d
   a.out_f32 = out_dt == kF32 ? 1 : 0;
   VODA_CHECK(!a.out_f32 || (ldw % 4 == 0 && dw % 16 == 0), "wgrad: fp32 dW rows must be 16-byte aligned");
   hipStream_t s = as_stream(stream);
-  VODA_CHECK(variant >= 0 && variant <= 9, "wgrad: variant must be 0..9");
+  VODA_CHECK(variant >= 0 && variant <= 12, "wgrad: variant must be 0..12");
   if (variant == 0)
     hipLaunchKernelGGL(wgrad_kernel, dim3(unsigned(pl.grid)), dim3(kWgThreads), 0, s, a);
   else if (variant == 1)
@@ -1022,8 +1034,14 @@ void wgrad_gemm(uintptr_t dy, int64_t ldy, uintptr_t x, int64_t ldx, uintptr_t d
     hipLaunchKernelGGL((wgrad_wide_kernel<5, 32>), dim3(unsigned(pl.grid)), dim3(kWwThreads), 0, s, a);
   else if (variant == 8)
     hipLaunchKernelGGL((wgrad_wide_kernel<3, 32>), dim3(unsigned(pl.grid)), dim3(kWwThreads), 0, s, a);
-  else
-    hipLaunchKernelGGL(wgrad_wide2_kernel, dim3(unsigned(pl.grid)), dim3(kWwThreads), 0, s, a);
+  else if (variant == 9)
+    hipLaunchKernelGGL((wgrad_wide2_kernel<2, 64, false>), dim3(unsigned(pl.grid)), dim3(kWwThreads), 0, s, a);
+  else if (variant == 10)
+    hipLaunchKernelGGL((wgrad_wide2_kernel<3, 48, false>), dim3(unsigned(pl.grid)), dim3(kWwThreads), 0, s, a);
+  else if (variant == 11)  // probe: operand fill of variant 9 alone (dW undefined)
+    hipLaunchKernelGGL((wgrad_wide2_kernel<2, 64, true>), dim3(unsigned(pl.grid)), dim3(kWwThreads), 0, s, a);
+  else  // 12, probe: operand fill of variant 10 alone
+    hipLaunchKernelGGL((wgrad_wide2_kernel<3, 48, true>), dim3(unsigned(pl.grid)), dim3(kWwThreads), 0, s, a);
   check_launch();
   if (pl.S > 1) {
     if (a.out_f32)

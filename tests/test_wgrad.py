@@ -60,7 +60,7 @@ def _check(dy, x, gw, gb, accumulate, splits, with_bias=True, variant=None):
 @pytest.mark.parametrize("M,N,K", [(64, 128, 128), (200, 136, 72), (1280, 768, 768), (777, 256, 384),
                                    (8192, 768, 3072)])
 @pytest.mark.parametrize("splits", [1, 3, 8])
-@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5, 6, 7, 8, 9])
+@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10])
 def test_wgrad_kernel_matches_fp32(M, N, K, splits, variant):
     dy, x, gw, gb = _case(M, N, K)
     _check(dy, x, gw, gb, True, splits, variant=variant)
@@ -68,7 +68,7 @@ def test_wgrad_kernel_matches_fp32(M, N, K, splits, variant):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("splits", [1, 4])
-@pytest.mark.parametrize("variant", [0, 1, 4, 6, 7, 9])
+@pytest.mark.parametrize("variant", [0, 1, 4, 6, 7, 9, 10])
 def test_wgrad_kernel_overwrite_and_no_bias(splits, variant):
     dy, x, gw, gb = _case(512, 192, 320, seed=3)
     _check(dy, x, gw, gb, False, splits, variant=variant)
@@ -84,7 +84,7 @@ def test_wgrad_kernel_identity_operand():
     x = torch.randn(M, K, device="cuda").bfloat16()
     gw = torch.zeros(N, K, device="cuda", dtype=torch.bfloat16)
     gb = torch.zeros(N, device="cuda", dtype=torch.bfloat16)
-    for s, v in ((1, 0), (3, 0), (1, 1), (3, 1), (2, 2), (3, 3), (1, 4), (3, 4), (2, 5), (1, 6), (3, 6), (2, 7), (3, 8), (1, 9), (3, 9)):
+    for s, v in ((1, 0), (3, 0), (1, 1), (3, 1), (2, 2), (3, 3), (1, 4), (3, 4), (2, 5), (1, 6), (3, 6), (2, 7), (3, 8), (1, 9), (3, 9), (1, 10), (3, 10)):
         gw.zero_()
         gb.zero_()
         W.wgrad_accumulate_(dy, x, gw, gb, splits=s, variant=v)

@@ -20,8 +20,9 @@ from . import _native as N
 TILE = 128
 # 0: register-staged LDS double buffer; 1 / 2 / 3: LDS ring of 4 / 2 / 3 stages of 64 tokens
 # filled by global_load_lds; 4 / 5: ring of 4 / 5 stages of 32 tokens; 6 / 7 / 8: 256 x 256
-# tile, 8 waves, ring of 4 x 32 / 5 x 32 / 3 x 32 tokens; 9: 256 x 256 tile on two 64-token
-# stages (128 KB).  Default 2 (64 KB ring, 2 workgroups per CU): fastest in the BERT-base step
+# tile, 8 waves, ring of 4 x 32 / 5 x 32 / 3 x 32 tokens; 9 / 10: 256 x 256 tile on two
+# 64-token stages (128 KB) / three 48-token stages (144 KB); 11 / 12: fill-only probes of 9 / 10
+# (no MFMA, dW undefined: benchmarks only).  Default 2 (64 KB ring, 2 workgroups per CU): fastest in the BERT-base step
 # on MI355X (profiles/r1_wgrad_v3.md)
 VARIANT = int(os.environ.get("VODA_WGRAD_VARIANT", "2"))
 # VODA_WGRAD_VARIANT set explicitly = that variant for every shape (A/B runs); otherwise
