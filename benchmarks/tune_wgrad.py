@@ -124,6 +124,7 @@ def main():
                           "heuristic": [hv, hs], "heuristic_us": round(ht, 2)}), flush=True)
         del dy, x, gw, gb
         torch.cuda.empty_cache()
+    os.makedirs(os.path.dirname(os.path.abspath(a.out)), exist_ok=True)
     with open(a.out, "w") as f:
         json.dump(table, f, indent=1, sort_keys=True)
     print(json.dumps({"written": a.out, "entries": len(table),
