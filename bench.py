@@ -192,9 +192,16 @@ class Watchdog:
         if self.rank == 0:
             print(json.dumps(dict(self.base, status="timeout", value=None, phase=self.phase,
                                   elapsed_s=round(time.monotonic() - self.t0, 1))), flush=True)
+        else:
+            # the launcher tears every rank down when the first one exits: the other ranks
+            # hold on so that rank 0 (started a moment later, its deadline a moment later)
+            # prints the status line before anyone's exit can SIGTERM it
+            time.sleep(self.GRACE_S)
         sys.stdout.flush()
         sys.stderr.flush()
         os._exit(3)
+
+    GRACE_S = 15.0
 
 
 def measure_busbw(store, rank: int, world: int, device, sizes_mb=(16, 64, 256), iters: int = 5) -> dict:
