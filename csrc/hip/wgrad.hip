@@ -59,6 +59,7 @@ struct WgradArgs {
   const uint16_t* zero;              // >= 16 zero bytes: source of rows past the split (LDS-DMA path)
   int M, N, K, S, m_split, tiles_k, remap, accumulate, bias;
   int split_major;  // logical block order: 0 = splits of one tile adjacent, 1 = tiles of one split adjacent
+  int zcol;         // LDS-DMA kernels: chunks past N / K read the zero buffer (1) or a clamped duplicate (0)
   int tiles_total;  // output tiles per tap (split_major decode)
   // epilogue addressing: dW column (and workspace column) offset and workspace row stride
   int col0, ws_ld;
@@ -382,14 +383,21 @@ __global__ __launch_bounds__(kWgThreads, 1) void wgrad_glds_kernel(WgradArgs p) 
   }
   // this lane's source rows of stage 0 (row 4j + lr of the tile, swizzled chunk), advanced by
   // BM rows per stage with one scalar multiply: no per-load 64-bit index arithmetic
+  // Chunks past N / K (a 64-channel operand in a 128-column tile) read the zero buffer rather
+  // than a clamped duplicate of the last chunk: their outputs are never stored, and one
+  // shared 16-byte line costs the fill path nothing where 8 distinct duplicate reads per row
+  // did (p.zcol = 0 restores the clamped reads for A/B runs).
   const uint16_t* row_a[IPW];
   const uint16_t* row_b[IPW];
+  uint32_t colok_a = 0, colok_b = 0;
 #pragma unroll
   for (int i = 0; i < IPW; ++i) {
     const int r = 4 * (IPW * wave + i) + lr;
     const int ch = slot ^ (((r & 3) << 2) | ((r >> 2) & 3));
     row_a[i] = p.dy + int64_t(mb + r) * p.ldy + min(n0 + ch * 8, p.N - 8);
     row_b[i] = CONV ? p.x : p.x + int64_t(mb + r) * p.ldx + min(k0 + ch * 8, p.K - 8);
+    colok_a |= uint32_t(!p.zcol || n0 + ch * 8 < p.N) << i;
+    colok_b |= uint32_t(!p.zcol || k0 + ch * 8 < p.K) << i;
   }
   auto issue = [&](int st) {
     uint8_t* A = smem + (st % kWgStages) * SB;
@@ -404,11 +412,11 @@ __global__ __launch_bounds__(kWgThreads, 1) void wgrad_glds_kernel(WgradArgs p) 
       const int ch = slot ^ (((r & 3) << 2) | ((r >> 2) & 3));
       const int m = m_base + r;
       const bool okm = full || m < me;
-      const uint16_t* ga = okm ? row_a[i] + adv_a : p.zero;
+      const uint16_t* ga = (okm && ((colok_a >> i) & 1)) ? row_a[i] + adv_a : p.zero;
       const uint16_t* gb;
       if constexpr (CONV) {
         const int hi = pho[i] * p.cstride + dh, wi = pwo[i] * p.cstride + dw;
-        const bool ok = okm && hi >= 0 && hi < p.H && wi >= 0 && wi < p.W;
+        const bool ok = okm && ((colok_b >> i) & 1) && hi >= 0 && hi < p.H && wi >= 0 && wi < p.W;
         gb = ok ? p.x + (int64_t(pn[i] * p.H + hi) * p.W + wi) * p.ldx + min(k0 + ch * 8, p.K - 8) : p.zero;
         // advance this row by BM output pixels (single carries: the steps are < Wo and < Ho)
         pwo[i] += p.adv_wo;
@@ -417,7 +425,7 @@ __global__ __launch_bounds__(kWgThreads, 1) void wgrad_glds_kernel(WgradArgs p) 
         if (pwo[i] >= p.Wo) { pwo[i] -= p.Wo; pho[i] += 1; }
         if (pho[i] >= p.Ho) { pho[i] -= p.Ho; pn[i] += 1; }
       } else {
-        gb = okm ? row_b[i] + adv_b : p.zero;
+        gb = (okm && ((colok_b >> i) & 1)) ? row_b[i] + adv_b : p.zero;
       }
       wg_dma16(ga, __builtin_amdgcn_readfirstlane(uint32_t(size_t((lds_void*)(A + 1024 * j)))));
       wg_dma16(gb, __builtin_amdgcn_readfirstlane(uint32_t(size_t((lds_void*)(B + 1024 * j)))));
@@ -964,6 +972,15 @@ int wgrad_split_major() {
   return v;
 }
 
+// VODA_WGRAD_ZCOL=0|1 (A/B switch, read once): see WgradArgs::zcol
+int wgrad_zero_columns() {
+  static const int v = [] {
+    const char* e = std::getenv("VODA_WGRAD_ZCOL");
+    return e ? (std::atoi(e) != 0 ? 1 : 0) : 1;
+  }();
+  return v;
+}
+
 WgradPlan wgrad_plan(int M, int N, int K, int splits, int tile = kWgBN) {
   WgradPlan pl;
   const int tiles_n = (N + tile - 1) / tile;
@@ -1009,6 +1026,7 @@ void wgrad_gemm(uintptr_t dy, int64_t ldy, uintptr_t x, int64_t ldx, uintptr_t d
   a.adv_n = a.adv_ho = a.adv_wo = 0;
   a.remap = (pl.grid % 8 == 0) ? 1 : 0;
   a.split_major = wgrad_split_major();
+  a.zcol = wgrad_zero_columns();
   a.tiles_total = pl.grid / pl.S;
   a.accumulate = accumulate ? 1 : 0;
   a.bias = db != 0 ? 1 : 0;
@@ -1098,6 +1116,7 @@ void wgrad_conv(uintptr_t dy, uintptr_t x, uintptr_t dw, int Nimg, int H, int W,
   const int64_t grid = int64_t(pl.grid) * taps;
   a.remap = (grid % 8 == 0) ? 1 : 0;
   a.split_major = wgrad_split_major();
+  a.zcol = wgrad_zero_columns();
   a.tiles_total = pl.grid / pl.S;
   hipStream_t s = as_stream(stream);
   hipLaunchKernelGGL((wgrad_glds_kernel<2, BM, true>), dim3(unsigned(grid)), dim3(kWgThreads), 0, s, a);

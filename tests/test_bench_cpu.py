@@ -33,7 +33,9 @@ def test_bench_two_ranks_cpu_rehearsal():
     assert d["status"] == "ok" and d["precision"] == "bf16-amp"
     # the like-for-like control replayed on the same warm pool (VERDICT r2 Next #6)
     assert d["control"]["algorithm"] == "FIFO" and d["control"]["avg_jct_s"] > 0 and not d["control"]["failed"]
-    assert d["vs_baseline"] == pytest.approx(d["control"]["avg_jct_s"] / d["value"], rel=1e-3)
+    # both JCTs are printed rounded to 1 ms: on this sub-second CPU trace that alone moves the
+    # ratio by up to ~1e-3 / value
+    assert d["vs_baseline"] == pytest.approx(d["control"]["avg_jct_s"] / d["value"], rel=1e-3 + 1e-3 / d["value"])
     # online profiling: GPU/CPU-timed ms per step for every model at every world it ran at
     assert set(d["step_ms_by_world"]) <= {"mnist-torch", "mnist"} and d["step_ms_by_world"]
     assert all(v > 0 for m in d["step_ms_by_world"].values() for v in m.values())
