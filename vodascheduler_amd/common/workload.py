@@ -188,14 +188,15 @@ class ModelProfile:
 
 # step_time_1gpu: MI355X measurements (bf16 autocast compute, fp32 flat gradients): ResNet-50
 # bs256 23.15 ms (end of round 3, profiles/r3/resnet50_steps.md) and BERT-base bs64 seq128
-# 9.93 ms (bench workers' GPU-timed whole-step graph replays with the round-3 fused attention,
-# profiles/r3/bench_n1_bf16_attn_fused.json); VGG16 bs128 2.63 ms, NMT
+# 10.2 ms (kernel time per step: 10.21 ms in profiles/r3/rocprof_bert_bf16_final.md, 10.18 ms
+# with the fused attention in profiles/r3/rocprof_bert_bf16_session2_final.md; the bench
+# workers' graph replays run 9.9-10.5 ms by box); VGG16 bs128 2.63 ms, NMT
 # Transformer bs512 5.24 ms, ResNet-50-CIFAR bs128 14.3 ms, ResNet-18 bs256 10.05 ms,
 # InceptionV3 bs128 13.5 ms, Keras MNIST 0.74 ms (benchmarks/model_step.py).  mnist-torch is
 # an estimate (measured=False).  grad_mb = 4 bytes x parameter count.
 PROFILES = {
     "resnet50": ModelProfile("resnet50", alpha=0.01, step_time_1gpu=0.02315, grad_mb=102.2, measured=True),
-    "bert-base": ModelProfile("bert-base", alpha=0.05, step_time_1gpu=0.00993, grad_mb=438.0, measured=True),
+    "bert-base": ModelProfile("bert-base", alpha=0.05, step_time_1gpu=0.0102, grad_mb=438.0, measured=True),
     "vgg16": ModelProfile("vgg16", alpha=0.08, step_time_1gpu=0.00263, grad_mb=134.6, measured=True),
     "transformer": ModelProfile("transformer", alpha=0.10, step_time_1gpu=0.00524, grad_mb=79.8, measured=True),
     "mnist": ModelProfile("mnist", alpha=0.30, step_time_1gpu=0.00074, grad_mb=4.8, measured=True),
