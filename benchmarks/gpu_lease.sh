@@ -68,17 +68,18 @@ for step in "$@"; do
       prec=bf16-amp
       if [[ $m == *-fp32 ]]; then m=${m%-fp32}; prec=fp32; fi
       R=$PWD
-      ( cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "/tmp/$step" -o k -- \
+      st="$step$SUFFIX"  # env-suffixed outputs stay apart (A/B profiles in one lease)
+      ( cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "/tmp/$st" -o k -- \
           python3 "$R/benchmarks/model_step.py" --model "$m" --steps 10 --warmup 6 --precision "$prec" \
-          --profile-marker ) > "$OUT/$step.log" 2>&1 || { tail -20 "$OUT/$step.log"; exit 6; }
-      mkdir -p "$OUT/$step"
-      python3 benchmarks/trace_window_stats.py "/tmp/$step/k_kernel_trace.csv" "$OUT/$step/steady_kernel_stats.csv" \
-        >> "$OUT/$step.log" 2>&1 || exit 7
-      python3 benchmarks/trace_dispatches.py "/tmp/$step/k_kernel_trace.csv" "$OUT/$step/sequence.csv" "" \
-        >> "$OUT/$step.log" 2>&1 || exit 7
-      python3 benchmarks/rocprof_summary.py "$OUT/$step/steady_kernel_stats.csv" "$m $prec steady state (10 steps)" 45 10 \
-        > "$OUT/$step.md" || exit 7
-      tail -n 3 "$OUT/$step.log" ;;
+          --profile-marker ) > "$OUT/$st.log" 2>&1 || { tail -20 "$OUT/$st.log"; exit 6; }
+      mkdir -p "$OUT/$st"
+      python3 benchmarks/trace_window_stats.py "/tmp/$st/k_kernel_trace.csv" "$OUT/$st/steady_kernel_stats.csv" \
+        >> "$OUT/$st.log" 2>&1 || exit 7
+      python3 benchmarks/trace_dispatches.py "/tmp/$st/k_kernel_trace.csv" "$OUT/$st/sequence.csv" "" \
+        >> "$OUT/$st.log" 2>&1 || exit 7
+      python3 benchmarks/rocprof_summary.py "$OUT/$st/steady_kernel_stats.csv" "$m $prec steady state (10 steps)" 45 10 \
+        > "$OUT/$st.md" || exit 7
+      tail -n 3 "$OUT/$st.log" ;;
     pmc-*)
       spec=${step#pmc-}
       m=${spec%%:*}

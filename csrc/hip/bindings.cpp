@@ -49,7 +49,8 @@ PYBIND11_MODULE(_vodahip, m) {
   m.def("global_avgpool_bwd", &global_avgpool_bwd);
   m.def("gemm_bnstats_supported", &gemm_bnstats_supported);
   m.def("gemm_bnstats_groups", &gemm_bnstats_groups);
-  m.def("gemm_bnstats", &gemm_bnstats);
+  m.def("gemm_bnstats", &gemm_bnstats, py::arg("x"), py::arg("w"), py::arg("y"), py::arg("part"), py::arg("M"),
+        py::arg("N"), py::arg("K"), py::arg("G"), py::arg("stream"), py::arg("accumulate") = false);
   m.def("subsample2d", &subsample2d);
   m.def("conv3x3_c64_wgrad_workspace_floats", &conv3x3_c64_wgrad_workspace_floats);
   m.def("conv3x3_c64_wgrad", &conv3x3_c64_wgrad);

@@ -42,6 +42,7 @@ struct GArgs {
   float* part;        // [2][G][N]
   int64_t M;
   int N, G;
+  int accumulate;     // Y += X W^T (the statistics then describe X W^T alone)
 };
 
 __device__ __forceinline__ gb_bf16x8 gb_ld16(const uint16_t* p) {
@@ -133,9 +134,23 @@ __global__ __launch_bounds__(kGThreads, 2) void gemm_bnstats_kernel(GArgs p) {
       for (int i = 0; i < 4; ++i) {
         const int q = i * 64 + lane;
         const int px = q >> 3, part = q & 7;
-        const uint4 v = *reinterpret_cast<const uint4*>(my_stg + px * kGStgStride + part * 16);
-        if (rbase + px < p.M)
-          *reinterpret_cast<uint4*>(p.y + (rbase + px) * p.N + n0 + 64 * pp + part * 8) = v;
+        uint4 v = *reinterpret_cast<const uint4*>(my_stg + px * kGStgStride + part * 16);
+        if (rbase + px < p.M) {
+          uint4* dst = reinterpret_cast<uint4*>(p.y + (rbase + px) * p.N + n0 + 64 * pp + part * 8);
+          if (p.accumulate) {  // 8 bf16 sums in fp32, one rounding of each
+            const uint4 o = *dst;
+            const uint32_t a[4] = {v.x, v.y, v.z, v.w}, b[4] = {o.x, o.y, o.z, o.w};
+            uint32_t r[4];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+              const float lo = bf2f(uint16_t(a[q] & 0xffff)) + bf2f(uint16_t(b[q] & 0xffff));
+              const float hi = bf2f(uint16_t(a[q] >> 16)) + bf2f(uint16_t(b[q] >> 16));
+              r[q] = uint32_t(f2bf(lo)) | (uint32_t(f2bf(hi)) << 16);
+            }
+            v = make_uint4(r[0], r[1], r[2], r[3]);
+          }
+          *dst = v;
+        }
       }
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
       __builtin_amdgcn_wave_barrier();
@@ -197,13 +212,13 @@ int gemm_bnstats_groups(int64_t M, int N, int K) {
 }
 
 void gemm_bnstats(uintptr_t x, uintptr_t w, uintptr_t y, uintptr_t part, int64_t M, int N, int K, int G,
-                  uintptr_t stream) {
+                  uintptr_t stream, bool accumulate) {
   VODA_CHECK(gemm_bnstats_supported(M, N, K), "gemm_bnstats: K must be 64, 128 or 256 and N a multiple of the tile");
   VODA_CHECK(G == gemm_bnstats_groups(M, N, K), "gemm_bnstats: group count mismatch");
   VODA_CHECK(x % 16 == 0 && w % 16 == 0 && y % 16 == 0 && part % 4 == 0, "gemm_bnstats: misaligned operands");
   const int ncol = N / (32 * gb_nt(K));
   GArgs a{reinterpret_cast<const uint16_t*>(x), reinterpret_cast<const uint16_t*>(w), reinterpret_cast<uint16_t*>(y),
-          reinterpret_cast<float*>(part), M, N, G};
+          reinterpret_cast<float*>(part), M, N, G, accumulate ? 1 : 0};
   hipStream_t s = as_stream(stream);
   if (K == 64)
     hipLaunchKernelGGL((gemm_bnstats_kernel<8, 4>), dim3(ncol * G), dim3(kGThreads), 0, s, a);

@@ -94,7 +94,7 @@ void bn_bwd(uintptr_t dy, uintptr_t mask, uintptr_t x, uintptr_t save_mean, uint
 bool gemm_bnstats_supported(int64_t M, int N, int K);
 int gemm_bnstats_groups(int64_t M, int N, int K);
 void gemm_bnstats(uintptr_t x, uintptr_t w, uintptr_t y, uintptr_t part, int64_t M, int N, int K, int G,
-                  uintptr_t stream);
+                  uintptr_t stream, bool accumulate = false);
 
 // ---- 3x3 / stride-1 conv weight gradient at 64 -> 64 channels (conv3x3_c64.hip) ----
 int64_t conv3x3_c64_wgrad_workspace_floats(int N, int H);

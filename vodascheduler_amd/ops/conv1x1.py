@@ -41,6 +41,12 @@ USE_GEMM_BNSTATS = os.environ.get("VODA_GEMM_BNSTATS", "1") != "0"
 # VODA_STATS_BWD_SPLIT=1: the Cin = 64 statistics layers run their MIOpen input and weight
 # gradients as two calls (A/B switch)
 STATS_BWD_SPLIT = os.environ.get("VODA_STATS_BWD_SPLIT", "0") == "1"
+# Input gradients dX = dY . W of the memory-bound 1x1 shapes (K = Cout in {64, 128, 256}) that
+# overwrite their output, on the MFMA GEMM of gemm_bnstats.hip instead of hipBLASLt / MIOpen
+# (benchmarks/bench_dgrad_gemm.py: 802816 x 256 -> 64 167 -> 102 us, 64 -> 256 142 -> 108,
+# 128 -> 256 168 -> 130, 200704 x 128 -> 512 77 -> 59; ResNet-50 step kernel time 23.55 ->
+# 23.47 ms, profiles/r3/raw/mfma_dgrad/).  VODA_MFMA_DGRAD=0: A/B off.
+USE_MFMA_DGRAD = os.environ.get("VODA_MFMA_DGRAD", "1") != "0"
 # Opt-in (VODA_CONV1X1_HYBRID=1): for Cin < 128 (ResNet stage 1: 64 -> 256) keep forward and
 # input gradient on MIOpen and send the weight gradient to the split-K kernel, straight into
 # the fp32 flat gradient.  In isolation the kernel matches MIOpen's igemm_wrw (156 vs 155 us)
@@ -154,6 +160,31 @@ def gemm_bnstats_2d(x2: torch.Tensor, w2: torch.Tensor, holder: StatsHolder | No
     return y2
 
 
+def mfma_dgrad(dy2: torch.Tensor, w2: torch.Tensor, acc2: torch.Tensor | None = None) -> torch.Tensor | None:
+    """dX [M, Cin] = dY [M, Cout] . W [Cout, Cin] (+ acc2 in place) on the MFMA GEMM when the
+    shape is covered; None otherwise (the caller keeps its library path)."""
+    if not USE_MFMA_DGRAD or not dy2.is_cuda:
+        return None
+    M, K = dy2.shape
+    Nc = w2.shape[1]
+    if (dy2.dtype != torch.bfloat16 or w2.dtype != torch.bfloat16 or not dy2.is_contiguous()
+            or dy2.data_ptr() % 16):
+        return None
+    if acc2 is not None and (acc2.dtype != torch.bfloat16 or not acc2.is_contiguous() or acc2.data_ptr() % 16
+                             or tuple(acc2.shape) != (M, Nc)):
+        return None
+    h = N.hip()
+    if not h.gemm_bnstats_supported(M, Nc, K):
+        return None
+    G = h.gemm_bnstats_groups(M, Nc, K)
+    wt = w2.t().contiguous()  # [Cin][Cout]: the kernel's [N][K] operand
+    out = acc2 if acc2 is not None else torch.empty(M, Nc, dtype=torch.bfloat16, device=dy2.device)
+    ws = torch.empty(2 * G * Nc, dtype=torch.float32, device=dy2.device)  # statistics of dY . W: unused
+    h.gemm_bnstats(dy2.data_ptr(), wt.data_ptr(), out.data_ptr(), ws.data_ptr(), M, Nc, K, G, N.stream_of(dy2),
+                   acc2 is not None)
+    return out
+
+
 def _direct(p: torch.Tensor) -> bool:
     return flat_grad(p) is not None
 
@@ -215,14 +246,18 @@ class _Conv1x1Fn(torch.autograd.Function):
                                 or not acc.is_contiguous(memory_format=torch.channels_last)):
             acc = acc.to(dy2.dtype).contiguous(memory_format=torch.channels_last)  # still owned here
         if strided is not None:
-            dx = (dy2 @ w2).view(n, h, w, cin).permute(0, 3, 1, 2)
+            dx2 = mfma_dgrad(dy2, w2)
+            dx = (dx2 if dx2 is not None else dy2 @ w2).view(n, h, w, cin).permute(0, 3, 1, 2)
             s_ = strided.stride
             subsample_add_(dx, strided.g, strided.stride)
         elif acc is not None:
+            # beta = 1 stays on hipBLASLt: the MFMA GEMM's read-add-write epilogue made these
+            # calls 2x slower in the step (802816 x 64 -> 256: 203 us vs ~98 us)
             _as_2d(acc).addmm_(dy2, w2)  # dX = shortcut gradient + dY . W (one GEMM, beta = 1)
             dx = acc
         elif ctx.needs_input_grad[0]:
-            dxs = (dy2 @ w2).view(n, h, w, cin).permute(0, 3, 1, 2)
+            dx2 = mfma_dgrad(dy2, w2)
+            dxs = (dx2 if dx2 is not None else dy2 @ w2).view(n, h, w, cin).permute(0, 3, 1, 2)
             if stride > 1 and ctx.sink_out is not None and USE_STRIDED_SINK:
                 dx = _StridedGrad(dxs, stride, in_shape)  # the consumer adds it in place
             elif stride > 1:
@@ -270,6 +305,13 @@ class _Conv1x1StatsFn(torch.autograd.Function):
             dy = dy.contiguous(memory_format=torch.channels_last)
         mask = [bool(ctx.needs_input_grad[0]), bool(ctx.needs_input_grad[1]), False]
         dx = dw = None
+        if mask[0]:  # the input gradient on the MFMA GEMM where it covers the shape
+            n, cin, h, w = x.shape
+            cout = weight.shape[0]
+            dx2 = mfma_dgrad(_as_2d(dy), weight.reshape(cout, cin))
+            if dx2 is not None:
+                dx = dx2.view(n, h, w, cin).permute(0, 3, 1, 2)
+                mask[0] = False
         if STATS_BWD_SPLIT:  # one MIOpen call per gradient (solver choice differs from the joint call)
             if mask[0]:
                 dx = torch.ops.aten.convolution_backward(dy, x, weight, None, [1, 1], [0, 0], [1, 1], False, [0, 0], 1,
@@ -278,8 +320,10 @@ class _Conv1x1StatsFn(torch.autograd.Function):
                 dw = torch.ops.aten.convolution_backward(dy, x, weight, None, [1, 1], [0, 0], [1, 1], False, [0, 0], 1,
                                                          [False, True, False])[1]
         elif mask[0] or mask[1]:
-            dx, dw, _ = torch.ops.aten.convolution_backward(dy, x, weight, None, [1, 1], [0, 0], [1, 1], False, [0, 0],
-                                                            1, mask)
+            dx_m, dw, _ = torch.ops.aten.convolution_backward(dy, x, weight, None, [1, 1], [0, 0], [1, 1], False,
+                                                              [0, 0], 1, mask)
+            if mask[0]:
+                dx = dx_m
         if mask[1]:
             g2 = flat_grad(weight) if _direct(weight) else None
             if g2 is not None:  # fold into the optimizer's flat gradient (see utils/flat.FOLD_CAST)
