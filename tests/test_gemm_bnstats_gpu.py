@@ -83,3 +83,20 @@ def test_conv_then_bn_uses_gemm_stats_and_matches(cin, cout, stride, hw, monkeyp
     for got, want in ((x.grad, xr.grad), (conv.weight.grad, wr.grad)):
         rel = float((got.float() - want).norm() / want.norm())
         assert rel < 3e-2, rel
+
+
+@pytest.mark.parametrize("M,K,Nc", [(5000, 256, 64), (777, 64, 256), (3136, 128, 512)])
+@pytest.mark.parametrize("accumulate", [False, True])
+def test_mfma_dgrad_matches_fp32(M, K, Nc, accumulate):
+    """dX = dY . W on the MFMA GEMM (ops/conv1x1.mfma_dgrad): the [Cout][Cin] weight is
+    transposed for the kernel; with ``acc2`` the result is added in place (beta = 1)."""
+    torch.manual_seed(1)
+    dy = torch.randn(M, K, device="cuda").bfloat16()
+    w = (torch.randn(K, Nc, device="cuda") * 0.1).bfloat16()   # [Cout = K][Cin = Nc]
+    acc = torch.randn(M, Nc, device="cuda").bfloat16() if accumulate else None
+    ref = dy.float() @ w.float() + (acc.float() if accumulate else 0.0)
+    out = C.mfma_dgrad(dy, w, acc)
+    assert out is not None
+    if accumulate:
+        assert out.data_ptr() == acc.data_ptr()
+    torch.testing.assert_close(out.float(), ref, rtol=1e-2, atol=1e-2 * ref.abs().max().item())
