@@ -424,7 +424,11 @@ __device__ __forceinline__ uint8_t pos_bits(const float (&v)[8]) {
   return uint8_t(b);
 }
 
-template <typename T, bool RES, bool RELU>
+// Apply passes: U rows of every input in flight per thread (all loads issued before the
+// first store; VODA_BN_APPLY_U selects U, see bn_tune).  U = 4 vs the former fwd 2 / bwd 1:
+// ResNet-50 step kernel time 23.32 -> 23.21 ms, the residual passes ~2 % faster each
+// (profiles/r3/raw/bn_apply_u/); the passes stay near 4.5 TB/s, bandwidth- not latency-bound.
+template <typename T, bool RES, bool RELU, int U = 2>
 __global__ __launch_bounds__(kBlock) void bn_apply_kernel(const T* __restrict__ x, const T* __restrict__ res,
                                                           const float* __restrict__ ab, T* __restrict__ y,
                                                           uint8_t* __restrict__ mask, int64_t M, int C,
@@ -438,28 +442,29 @@ __global__ __launch_bounds__(kBlock) void bn_apply_kernel(const T* __restrict__ 
 #pragma unroll
   for (int k = 0; k < 8; ++k) { a[k] = ab[col + k]; b[k] = ab[C + col + k]; }
   const int64_t step = m.rpi;
+  const int CB = C / kVec;
   int64_t r = r0 + m.rsub;
-  for (; r + step < r1; r += 2 * step) {
-    float v0[8], v1[8], q0[8], q1[8];
-    Vec8<T>::load(x, r * C + col, v0);
-    Vec8<T>::load(x, (r + step) * C + col, v1);
-    if constexpr (RES) {
-      Vec8<T>::load(res, r * C + col, q0);
-      Vec8<T>::load(res, (r + step) * C + col, q1);
+  for (; r + (U - 1) * step < r1; r += U * step) {
+    typename Vec8<T>::Raw xr[U], qr[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      xr[u] = Vec8<T>::load_raw(x, (r + u * step) * C + col);
+      if constexpr (RES) qr[u] = Vec8<T>::load_raw(res, (r + u * step) * C + col);
     }
 #pragma unroll
-    for (int k = 0; k < 8; ++k) {
-      v0[k] = fmaf(v0[k], a[k], b[k]);
-      v1[k] = fmaf(v1[k], a[k], b[k]);
-      if constexpr (RES) { v0[k] += q0[k]; v1[k] += q1[k]; }
-      if constexpr (RELU) { v0[k] = fmaxf(v0[k], 0.f); v1[k] = fmaxf(v1[k], 0.f); }
-    }
-    Vec8<T>::store(y, r * C + col, v0);
-    Vec8<T>::store(y, (r + step) * C + col, v1);
-    if constexpr (RELU) {
-      if (mask != nullptr) {
-        mask[r * (C / kVec) + m.cg] = pos_bits(v0);
-        mask[(r + step) * (C / kVec) + m.cg] = pos_bits(v1);
+    for (int u = 0; u < U; ++u) {
+      float v[8], q[8];
+      Vec8<T>::cvt(xr[u], v);
+      if constexpr (RES) Vec8<T>::cvt(qr[u], q);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        v[k] = fmaf(v[k], a[k], b[k]);
+        if constexpr (RES) v[k] += q[k];
+        if constexpr (RELU) v[k] = fmaxf(v[k], 0.f);
+      }
+      Vec8<T>::store(y, (r + u * step) * C + col, v);
+      if constexpr (RELU) {
+        if (mask != nullptr) mask[(r + u * step) * CB + m.cg] = pos_bits(v);
       }
     }
   }
@@ -475,12 +480,12 @@ __global__ __launch_bounds__(kBlock) void bn_apply_kernel(const T* __restrict__ 
     }
     Vec8<T>::store(y, r * C + col, v);
     if constexpr (RELU) {
-      if (mask != nullptr) mask[r * (C / kVec) + m.cg] = pos_bits(v);
+      if (mask != nullptr) mask[r * CB + m.cg] = pos_bits(v);
     }
   }
 }
 
-template <typename T, bool RELU, bool DRES>
+template <typename T, bool RELU, bool DRES, int U = 1>
 __global__ __launch_bounds__(kBlock) void bn_bwd_apply_kernel(const T* __restrict__ dy,
                                                               const uint8_t* __restrict__ mask,
                                                               const T* __restrict__ x, const float* __restrict__ k3,
@@ -495,11 +500,36 @@ __global__ __launch_bounds__(kBlock) void bn_bwd_apply_kernel(const T* __restric
 #pragma unroll
   for (int k = 0; k < 8; ++k) { a[k] = k3[col + k]; c2[k] = k3[C + col + k]; c0[k] = k3[2 * C + col + k]; }
   const int64_t step = m.rpi;
-  for (int64_t r = r0 + m.rsub; r < r1; r += step) {
+  const int CB = C / kVec;
+  int64_t r = r0 + m.rsub;
+  if constexpr (U > 1) {
+    for (; r + (U - 1) * step < r1; r += U * step) {
+      typename Vec8<T>::Raw gr[U], xr[U];
+      uint8_t mb[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        gr[u] = Vec8<T>::load_raw(dy, (r + u * step) * C + col);
+        xr[u] = Vec8<T>::load_raw(x, (r + u * step) * C + col);
+        if constexpr (RELU) mb[u] = mask[(r + u * step) * CB + m.cg];
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        float g[8], xv[8], o[8];
+        Vec8<T>::cvt(gr[u], g);
+        Vec8<T>::cvt(xr[u], xv);
+        if constexpr (RELU) apply_mask(g, mb[u]);
+        if constexpr (DRES) Vec8<T>::store(dres, (r + u * step) * C + col, g);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) o[k] = fmaf(a[k], g[k], fmaf(c2[k], xv[k], c0[k]));
+        Vec8<T>::store(dx, (r + u * step) * C + col, o);
+      }
+    }
+  }
+  for (; r < r1; r += step) {
     float g[8], xv[8];
     Vec8<T>::load(dy, r * C + col, g);
     Vec8<T>::load(x, r * C + col, xv);
-    if constexpr (RELU) apply_mask(g, mask[r * (C / kVec) + m.cg]);
+    if constexpr (RELU) apply_mask(g, mask[r * CB + m.cg]);
     if constexpr (DRES) Vec8<T>::store(dres, r * C + col, g);
     float o[8];
 #pragma unroll
@@ -825,6 +855,7 @@ struct BnTune {
   int sweep;
   int apply_cap = 8192;   // apply-pass grid cap (VODA_BN_APPLY_CAP)
   int apply_iters = 4;    // row iterations per apply block (VODA_BN_APPLY_ITERS)
+  int apply_u = 4;        // rows in flight in the apply passes: 4, 2, or 0 -> fwd 2 / bwd 1 (VODA_BN_APPLY_U)
 };
 BnTune& bn_tune() {
   static BnTune t = [] {
@@ -834,6 +865,7 @@ BnTune& bn_tune() {
     if (const char* e = std::getenv("VODA_BN_SWEEP")) v.sweep = std::max(0, std::min(2, std::atoi(e)));
     if (const char* e = std::getenv("VODA_BN_APPLY_CAP")) v.apply_cap = std::max(256, std::atoi(e));
     if (const char* e = std::getenv("VODA_BN_APPLY_ITERS")) v.apply_iters = std::max(1, std::atoi(e));
+    if (const char* e = std::getenv("VODA_BN_APPLY_U")) v.apply_u = std::atoi(e) >= 4 ? 4 : (std::atoi(e) >= 2 ? 2 : 0);  // see bn_apply_kernel
     return v;
   }();
   return t;
@@ -908,12 +940,19 @@ void bn_fwd_train(uintptr_t x, uintptr_t residual, uintptr_t gamma, uintptr_t be
     const T* rp = reinterpret_cast<const T*>(residual);
     T* yp = reinterpret_cast<T*>(y);
     uint8_t* mp = reinterpret_cast<uint8_t*>(mask);
+    auto app = [&](auto res_c, auto relu_c) {
+      constexpr bool RS = decltype(res_c)::value, RL = decltype(relu_c)::value;
+      if (bn_tune().apply_u == 4)
+        hipLaunchKernelGGL((bn_apply_kernel<T, RS, RL, 4>), ag.grid, dim3(kBlock), 0, s, xp, rp, ab, yp, mp, M, C, sw);
+      else
+        hipLaunchKernelGGL((bn_apply_kernel<T, RS, RL, 2>), ag.grid, dim3(kBlock), 0, s, xp, rp, ab, yp, mp, M, C, sw);
+    };
     if (residual) {
-      if (relu) hipLaunchKernelGGL((bn_apply_kernel<T, true, true>), ag.grid, dim3(kBlock), 0, s, xp, rp, ab, yp, mp, M, C, sw);
-      else hipLaunchKernelGGL((bn_apply_kernel<T, true, false>), ag.grid, dim3(kBlock), 0, s, xp, rp, ab, yp, mp, M, C, sw);
+      if (relu) app(std::true_type{}, std::true_type{});
+      else app(std::true_type{}, std::false_type{});
     } else {
-      if (relu) hipLaunchKernelGGL((bn_apply_kernel<T, false, true>), ag.grid, dim3(kBlock), 0, s, xp, rp, ab, yp, mp, M, C, sw);
-      else hipLaunchKernelGGL((bn_apply_kernel<T, false, false>), ag.grid, dim3(kBlock), 0, s, xp, rp, ab, yp, mp, M, C, sw);
+      if (relu) app(std::false_type{}, std::true_type{});
+      else app(std::false_type{}, std::false_type{});
     }
   });
   check_launch();
@@ -981,12 +1020,22 @@ void bn_bwd(uintptr_t dy, uintptr_t mask, uintptr_t x, uintptr_t save_mean, uint
                        reinterpret_cast<float*>(dbeta), k3, int(accumulate));
     T* dxp = reinterpret_cast<T*>(dx);
     T* drp = reinterpret_cast<T*>(dres);
+    auto app = [&](auto relu_c, auto dres_c) {
+      constexpr bool RL = decltype(relu_c)::value, DR = decltype(dres_c)::value;
+      const int u = bn_tune().apply_u;
+      if (u == 4)
+        hipLaunchKernelGGL((bn_bwd_apply_kernel<T, RL, DR, 4>), ag.grid, dim3(kBlock), 0, s, dyp, yp, xp, k3, dxp, drp, M, C, sw);
+      else if (u == 2)
+        hipLaunchKernelGGL((bn_bwd_apply_kernel<T, RL, DR, 2>), ag.grid, dim3(kBlock), 0, s, dyp, yp, xp, k3, dxp, drp, M, C, sw);
+      else
+        hipLaunchKernelGGL((bn_bwd_apply_kernel<T, RL, DR, 1>), ag.grid, dim3(kBlock), 0, s, dyp, yp, xp, k3, dxp, drp, M, C, sw);
+    };
     if (relu) {
-      if (dres) hipLaunchKernelGGL((bn_bwd_apply_kernel<T, true, true>), ag.grid, dim3(kBlock), 0, s, dyp, yp, xp, k3, dxp, drp, M, C, sw);
-      else hipLaunchKernelGGL((bn_bwd_apply_kernel<T, true, false>), ag.grid, dim3(kBlock), 0, s, dyp, yp, xp, k3, dxp, drp, M, C, sw);
+      if (dres) app(std::true_type{}, std::true_type{});
+      else app(std::true_type{}, std::false_type{});
     } else {
-      if (dres) hipLaunchKernelGGL((bn_bwd_apply_kernel<T, false, true>), ag.grid, dim3(kBlock), 0, s, dyp, yp, xp, k3, dxp, drp, M, C, sw);
-      else hipLaunchKernelGGL((bn_bwd_apply_kernel<T, false, false>), ag.grid, dim3(kBlock), 0, s, dyp, yp, xp, k3, dxp, drp, M, C, sw);
+      if (dres) app(std::false_type{}, std::true_type{});
+      else app(std::false_type{}, std::false_type{});
     }
   });
   check_launch();
