@@ -112,8 +112,10 @@ def stop_pool(store, procs, q, timeout: float = 30) -> dict:
     return out
 
 
-def assert_matches_replay(cfg, path: str, device: str, exact: bool = True) -> dict:
-    """The elastic run's final state (rank 0's checkpoint) equals the uninterrupted replay."""
+def assert_matches_replay(cfg, path: str, device: str, exact: bool = True,
+                          tol: tuple[float, float] = (2e-3, 2e-4)) -> dict:
+    """The elastic run's final state (rank 0's checkpoint) equals the uninterrupted replay
+    (bitwise, or to ``tol`` = (rtol, atol) when ``exact`` is False)."""
     from vodascheduler_amd.workloads.train import replay_reference
 
     payload = torch.load(path, map_location="cpu", weights_only=True)
@@ -129,7 +131,7 @@ def assert_matches_replay(cfg, path: str, device: str, exact: bool = True) -> di
         if exact:
             assert torch.equal(a, b), (i, float((a.float() - b.float()).abs().max()))
         else:  # GPU: nondeterministic reductions (atomics) make trajectories differ in the last bits
-            torch.testing.assert_close(a.float(), b.float(), rtol=2e-3, atol=2e-4)
+            torch.testing.assert_close(a.float(), b.float(), rtol=tol[0], atol=tol[1])
     assert ex["epoch"] == ref_ex["epoch"] and ex["samples"] == ref_ex["samples"]
     return ex
 

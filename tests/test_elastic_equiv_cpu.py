@@ -115,7 +115,10 @@ def test_eight_worker_live_resize_8_4_8(tmp_path, monkeypatch):
         assert c.wait_done() == "done"
     finally:
         out = stop_pool(store, procs, q)
-    ex = assert_matches_replay(cfg, cfg.final_state_path, "cpu", exact=False)
+    # 8- and 4-rank gloo all-reduces sum in a different order than the replay, and the
+    # difference compounds over the run: 0.8 % of elements landed 5.5e-4 apart in one run
+    # (atol 2e-4 failed), so the 8-rank check allows 2e-3 absolute
+    ex = assert_matches_replay(cfg, cfg.final_state_path, "cpu", exact=False, tol=(1e-2, 2e-3))
     w = _worlds(ex)
     assert w[0] == 8 and 4 in w and w[-1] == 8, ex["world_log"]
     dig = {wid: r["result"]["state_digest"] for wid, recs in out.items() for r in recs if r["job"] == "r8"
