@@ -11,6 +11,8 @@
 // (bf16/f16 model weights + fp32 master), fusing the cast that would otherwise be a
 // second pass.  Semantics match torch.optim.{SGD,Adam,AdamW,RMSprop}.
 #include "common.h"
+
+#include <cstdlib>
 #include "ops.h"
 
 namespace voda {
@@ -97,7 +99,9 @@ __device__ __forceinline__ void adam1(float& p, float g, float& m, float& v, con
   p -= a.step_size * (m / denom);
 }
 
-template <typename GT, typename LP>
+// U float4 groups of every array in flight per thread (loads issued before the first store):
+// VODA_ADAM_U = 1 / 2 (adam_unroll below).
+template <typename GT, typename LP, int U>
 __global__ __launch_bounds__(256) void adam_kernel(float* __restrict__ p, const GT* __restrict__ g,
                                                    float* __restrict__ m, float* __restrict__ v,
                                                    LP* __restrict__ q, int64_t n, AdamArgs a,
@@ -111,7 +115,31 @@ __global__ __launch_bounds__(256) void adam_kernel(float* __restrict__ p, const 
   }
   const int64_t n4 = n >> 2;
   const int64_t stride = int64_t(gridDim.x) * blockDim.x;
-  for (int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < n4; i += stride) {
+  int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+  if constexpr (U > 1) {
+    for (; i + (U - 1) * stride < n4; i += U * stride) {
+      float4 pv[U], gv[U], mv[U], vv[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        pv[u] = Vec4<float>::load(p, i + u * stride);
+        gv[u] = Vec4<GT>::load(g, i + u * stride);
+        mv[u] = Vec4<float>::load(m, i + u * stride);
+        vv[u] = Vec4<float>::load(v, i + u * stride);
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        adam1(pv[u].x, gv[u].x, mv[u].x, vv[u].x, a);
+        adam1(pv[u].y, gv[u].y, mv[u].y, vv[u].y, a);
+        adam1(pv[u].z, gv[u].z, mv[u].z, vv[u].z, a);
+        adam1(pv[u].w, gv[u].w, mv[u].w, vv[u].w, a);
+        Vec4<float>::store(p, i + u * stride, pv[u]);
+        Vec4<float>::store(m, i + u * stride, mv[u]);
+        Vec4<float>::store(v, i + u * stride, vv[u]);
+        store_lp<LP>(q, i + u * stride, pv[u]);
+      }
+    }
+  }
+  for (; i < n4; i += stride) {
     float4 pv = Vec4<float>::load(p, i);
     float4 gv = Vec4<GT>::load(g, i);
     float4 mv = Vec4<float>::load(m, i);
@@ -126,13 +154,21 @@ __global__ __launch_bounds__(256) void adam_kernel(float* __restrict__ p, const 
     store_lp<LP>(q, i, pv);
   }
   if (blockIdx.x == 0) {
-    for (int64_t i = (n4 << 2) + threadIdx.x; i < n; i += blockDim.x) {
-      float pv = p[i], mv = m[i], vv = v[i];
-      adam1(pv, Vec4<GT>::load1(g, i), mv, vv, a);
-      p[i] = pv; m[i] = mv; v[i] = vv;
-      store_lp1<LP>(q, i, pv);
+    for (int64_t j = (n4 << 2) + threadIdx.x; j < n; j += blockDim.x) {
+      float pv = p[j], mv = m[j], vv = v[j];
+      adam1(pv, Vec4<GT>::load1(g, j), mv, vv, a);
+      p[j] = pv; m[j] = mv; v[j] = vv;
+      store_lp1<LP>(q, j, pv);
     }
   }
+}
+
+static int adam_unroll() {
+  static const int u = [] {
+    const char* e = std::getenv("VODA_ADAM_U");
+    return e != nullptr && std::atoi(e) >= 2 ? 2 : 1;
+  }();
+  return u;
 }
 
 // ---------------------------------------------------------------------------------
@@ -250,7 +286,8 @@ void adam_step(uintptr_t p, uintptr_t g, int g_dtype, uintptr_t m, uintptr_t v, 
              adamw ? 1 : 0};
   unsigned grid = stream_grid((n + 3) / 4);
   DISPATCH_GT_LP(g_dtype, lp_dtype, [&] {
-    hipLaunchKernelGGL((adam_kernel<GT, LP>), dim3(grid), dim3(256), 0, as_stream(stream),
+    auto* kern = adam_unroll() == 2 ? adam_kernel<GT, LP, 2> : adam_kernel<GT, LP, 1>;
+    hipLaunchKernelGGL(kern, dim3(grid), dim3(256), 0, as_stream(stream),
                        reinterpret_cast<float*>(p), reinterpret_cast<const GT*>(g),
                        reinterpret_cast<float*>(m), reinterpret_cast<float*>(v),
                        reinterpret_cast<LP*>(p_lp), n, a, reinterpret_cast<const int64_t*>(step_ptr));
