@@ -15,9 +15,10 @@ RCCL over xGMI with bucket overlap, fused HIP optimizers, resized live (communic
 rebuild + state broadcast).
 
 Semantics of the driver flags:
-  --steps K   trace scale: the mean job is K x STEP_SCALE (=10) single-GPU training steps at
-              the per-GPU batch; weak scaling: every job's work is multiplied by N, so the
-              per-GPU work is fixed as N grows (~4 s of GPU work per job at N=1 for K=20).
+  --steps K   trace scale: the mean job is K x STEP_SCALE[precision] (fp32: 3, bf16: 10)
+              single-GPU training steps at the per-GPU batch; weak scaling: every job's work
+              is multiplied by N, so the per-GPU work is fixed as N grows (~3.5 s of GPU work
+              per job at N=1 for K=20).
   --warmup W  untimed warm-up steps of every model on every GPU (MIOpen/hipBLASLt caches,
               RCCL init) before the timed trace.
 The timed region (barrier + synchronize on both sides) is the whole trace: first submission
@@ -36,7 +37,22 @@ Also reported (none of it inside the timed region):
     reason logged, when the deadline leaves too little time.
 ``--deadline`` (default 540 s, below the driver's 600 s): a watchdog on every rank dumps all
 thread stacks, rank 0 prints a ``"status": "timeout"`` JSON line without ``value``, and the
-process exits non-zero.  ``--precision fp32`` runs the reference's precision (no autocast).
+process exits non-zero.  A control replay that overruns or fails never costs the measured
+headline: it is cut off (its jobs deleted), reported as ``control.status`` and the line still
+carries ``value``; it is not even started when the simulator -- fed this run's measured step
+times and bus bandwidth, and calibrated on the main trace's predicted-vs-actual wall --
+predicts it cannot finish before the deadline.
+
+``--precision`` defaults to fp32, the reference's precision (tensorflow2_keras_cifar_elastic.py:
+147-166 and pytorch_mnist_elastic.py train without mixed precision); ``bf16-amp`` runs bf16
+autocast with fp32 master weights / gradients.  The warm-up's measured single-GPU step times
+at that precision price every job's declared work (the job-info priors of SRJF / AFS-L /
+FfDL) and the simulator's predictions.
+
+``--autoscale`` (BASELINE config 5, "autoscale 1->8"): the scheduler starts with one GPU of
+the pool in its inventory; the others are announced one node event at a time (capacity
+doubles every ``--autoscale-every`` seconds: 1 -> 2 -> 4 -> 8), as a cluster autoscaler adding
+nodes would (reference scheduler.go:689-747, placement_manager.go:239-304).
 """
 from __future__ import annotations
 
@@ -56,7 +72,11 @@ os.environ.setdefault("GLOO_SOCKET_IFNAME", "lo")
 os.environ.setdefault("NCCL_SOCKET_IFNAME", "lo")
 os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
 
-STEP_SCALE = 10  # single-GPU steps per unit of --steps in the mean job
+# single-GPU steps per unit of --steps in the mean job, per compute precision: the fp32 steps
+# of the mix are ~3.5x the bf16 ones (ResNet-50 76.9 vs 23.2 ms, BERT-base 39.7 vs 10.0 ms at
+# the end of round 3), so the fp32 trace carries ~the same GPU-seconds as the bf16 one and the
+# timed trace + its FIFO control fit the driver's lease
+STEP_SCALE = {"fp32": 3, "bf16-amp": 10}
 
 
 def _self_launch() -> None:
@@ -93,7 +113,8 @@ import torch.distributed as dist  # noqa: E402
 
 sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 
-from vodascheduler_amd.common.workload import busbw_source, set_measured_busbw  # noqa: E402
+from vodascheduler_amd.common.workload import (busbw_source, set_measured_busbw,  # noqa: E402
+                                               set_measured_step_times)
 from vodascheduler_amd.ops import _native  # noqa: E402
 from vodascheduler_amd.runtime.cluster import free_port, run_trace  # noqa: E402
 from vodascheduler_amd.runtime.pool import PoolWorker  # noqa: E402
@@ -249,6 +270,31 @@ def measure_busbw(store, rank: int, world: int, device, sizes_mb=(16, 64, 256), 
     return out
 
 
+def autoscale_schedule(world: int, every_s: float) -> list[tuple[float, int]]:
+    """[(t, gpus)]: the scheduler's inventory starts at 1 GPU and doubles every ``every_s``
+    seconds up to ``world`` (a cluster autoscaler adding nodes)."""
+    out, k, t = [(0.0, 1)], 1, 0.0
+    while k < world:
+        k, t = min(world, 2 * k), t + every_s
+        out.append((t, k))
+    return out
+
+
+def predict_wall(trace, algorithm: str, world: int, rate_limit: float, ramp=None) -> float:
+    """Simulated wall time (first submission -> last completion) of ``trace`` on ``world``
+    GPUs under ``algorithm`` (sim/simulator.py: the same service / scheduler / allocator /
+    placement code in virtual time), priced with the measured step times and busbw installed
+    in common.workload.  Warm-pool starts / resizes cost ~0.01-1 s (bench JSON)."""
+    from vodascheduler_amd.sim.simulator import simulate
+
+    nodes_events = None
+    if ramp:
+        nodes_events = [(t, {"node0": list(range(k))}) for t, k in ramp]
+    r = simulate(trace, algorithm=algorithm, gpus=world, rate_limit_sec=rate_limit, tick_sec=1.0,
+                 resize_overhead_s=0.3, restart_overhead_s=0.1, capacity=nodes_events)
+    return r.makespan + min(tj.submit_time for tj in trace)
+
+
 def per_world_step_ms(allrec: list[dict]) -> dict:
     """{model: {world: GPU-timed ms per training step}} from the workers' online profiling
     (one record per job: every member returns the same synced ``perf``)."""
@@ -298,14 +344,20 @@ def main():
                     help="cpu: rehearse the multi-rank orchestration on gloo with tiny models (tests only)")
     ap.add_argument("--comm-backend", default=None, choices=[None, "rccl", "gloo"],
                     help="data-plane collectives (default: rccl on cuda, gloo on cpu)")
-    ap.add_argument("--precision", default="bf16-amp", choices=["bf16-amp", "fp32"],
-                    help="compute precision: bf16 autocast (fp32 master weights / gradients) or fp32 "
-                         "(the reference's precision)")
+    ap.add_argument("--precision", default="fp32", choices=["bf16-amp", "fp32"],
+                    help="compute precision: fp32 (default: the reference's precision) or bf16 autocast "
+                         "(fp32 master weights / gradients)")
+    ap.add_argument("--autoscale", action="store_true",
+                    help="capacity ramp: the scheduler sees 1 GPU at the start, doubling every "
+                         "--autoscale-every seconds up to N (cluster-autoscaler node additions)")
+    ap.add_argument("--autoscale-every", type=float, default=15.0)
     ap.add_argument("--deadline", type=float, default=540.0,
                     help="seconds: dump stacks + print a status=timeout line + exit non-zero (0 = none)")
     ap.add_argument("--control", default="FIFO",
                     help="non-elastic control policy replayed on the same trace after the timed run "
                          "('none' to skip); vs_baseline = avg JCT(control) / avg JCT(policy)")
+    ap.add_argument("--control-timeout", type=float, default=None,
+                    help="cap on the control replay's seconds (default: until shortly before the deadline)")
     ap.add_argument("--resize-timeout", type=float, default=60.0,
                     help="a resize whose previous epoch has not synced after this long becomes an abort epoch")
     ap.add_argument("--share-gpu", action="store_true",
@@ -366,8 +418,13 @@ def main():
             set_measured_busbw({int(k): v.get("64") for k, v in bw["by_world"].items()})
         dist.barrier()
     log(rank, f"warm-up single-GPU step ms: {step_ms}")
-
-    trace = bench_trace(a.jobs, a.steps * STEP_SCALE, world, a.seed, a.interarrival, models, batch)
+    # this box's single-GPU step times at the run's precision price the priors and predictions
+    set_measured_step_times({m: {1: v} for m, v in step_ms.items()})
+    trace_prec = "fp32" if not amp else "bf16"
+    step_scale = STEP_SCALE[a.precision]
+    trace = bench_trace(a.jobs, a.steps * step_scale, world, a.seed, a.interarrival, models, batch,
+                        precision=trace_prec, step_time_s={m: v / 1e3 for m, v in step_ms.items()})
+    ramp = autoscale_schedule(world, a.autoscale_every) if a.autoscale else None
     locs = [("node0", r) for r in range(world)]
     os.environ.setdefault("VODA_CKPT_DIR", f"/tmp/voda_ckpt_{os.getpid()}")
     metrics_dir = f"/tmp/voda_metrics_{port[0]}"
@@ -392,33 +449,57 @@ def main():
     ctl: dict = {}
     t_main = [0.0]
     sched = None
+    pred: dict = {}
     if rank == 0:
+        pred["main_s"] = predict_wall(trace, a.algorithm, world, a.rate_limit, ramp)
+        log(0, f"simulator prediction for the timed trace ({a.algorithm}): {pred['main_s']:.1f} s")
+
         def drive():
             try:
                 gpu_numa = None
                 if a.device == "cuda" and topo.n >= world and not a.share_gpu:
                     gpu_numa = {"node0": {r: topo.numa.get(r, 0) for r in range(world)}}
                 kw = dict(rate_limit_sec=a.rate_limit, tick_sec=1.0, progress=lambda s: log(0, s),
-                          gpu_numa=gpu_numa, settle_timeout=a.resize_timeout)
+                          gpu_numa=gpu_numa, settle_timeout=a.resize_timeout, capacity_ramp=ramp)
                 result.update(run_trace(store, trace, locs, a.algorithm, train_defaults=defaults,
                                         timeout=max(30.0, dog.left() - 15), trace_path=a.trace,
                                         stop_pool=control is None, **kw))
                 t_main[0] = time.perf_counter()
-                if control is not None:
-                    need = 1.3 * result["wall_s"] + 20
-                    if dog.left() < need:
-                        ctl["skipped"] = (f"{dog.left():.0f} s left before the deadline, the control needs "
-                                          f"~{need:.0f} s (1.3 x the timed trace)")
-                        log(0, f"control run skipped: {ctl['skipped']}")
-                        store.set("pool/shutdown", "1")
-                        return
-                    dog.phase = "control"
-                    log(0, f"control: same trace with {control} on the same warm pool")
-                    ctl.update(run_trace(store, ctl_trace, locs, control,
-                                         train_defaults=dict(defaults, metrics_dir=metrics_dir + "_ctl"),
-                                         timeout=max(30.0, dog.left() - 10), stop_pool=True, **kw))
             except BaseException as e:  # never leave the pool hanging
                 result["error"] = repr(e)
+                store.set("pool/shutdown", "1")
+                return
+            if control is None:
+                return
+            # the control never costs the measured headline: predicted first, cut off at the
+            # deadline, and any failure is reported in ``control`` only
+            try:
+                p_ctl = predict_wall(ctl_trace, control, world, a.rate_limit, ramp)
+                calib = result["wall_s"] / pred["main_s"] if pred["main_s"] > 0 else 1.0
+                need = p_ctl * max(1.0, calib) * 1.15 + 20
+                ctl.update(predicted_wall_s=round(p_ctl * calib, 1), predicted_raw_s=round(p_ctl, 1),
+                           calibration=round(calib, 3))
+                if dog.left() < need:
+                    ctl.update(status="skipped", reason=(
+                        f"{dog.left():.0f} s left before the deadline; the simulator predicts the control "
+                        f"needs ~{need:.0f} s ({p_ctl:.0f} s simulated x {calib:.2f} main-trace calibration)"))
+                    log(0, f"control run skipped: {ctl['reason']}")
+                    return
+                dog.phase = "control"
+                log(0, f"control: same trace with {control} on the same warm pool "
+                       f"(predicted {p_ctl * calib:.0f} s)")
+                ctl.update(run_trace(store, ctl_trace, locs, control,
+                                     train_defaults=dict(defaults, metrics_dir=metrics_dir + "_ctl"),
+                                     timeout=min(a.control_timeout or float("inf"), max(10.0, dog.left() - 30)),
+                                     stop_pool=True, **kw))
+                ctl["status"] = "ok"
+            except TimeoutError as e:
+                ctl.update(status="timeout", reason=str(e))
+                log(0, f"control cut off: {e}")
+            except BaseException as e:
+                ctl.update(status="error", reason=repr(e))
+                log(0, f"control failed: {e!r}")
+            finally:
                 store.set("pool/shutdown", "1")
 
         sched = threading.Thread(target=drive, name="control-plane", daemon=True)
@@ -468,14 +549,16 @@ def main():
 
             wl = workload_of(tj.spec)
             samples += wl["steps_per_epoch"] * 2 * batch[wl["model"]]
-        if ctl.get("avg_jct_s"):
-            control_out = {"algorithm": control, "avg_jct_s": round(ctl["avg_jct_s"], 3),
+        pk = ("predicted_wall_s", "predicted_raw_s", "calibration")
+        if ctl.get("status") == "ok" and ctl.get("avg_jct_s"):
+            control_out = {"algorithm": control, "status": "ok", "avg_jct_s": round(ctl["avg_jct_s"], 3),
                            "makespan_s": round(ctl["makespan_s"], 3), "p95_jct_s": round(ctl["p95_jct_s"], 3),
                            "wall_s": round(ctl["wall_s"], 3), "resize_events": ctl["n_resizes"],
-                           "failed": ctl["failed"]}
+                           "failed": ctl["failed"], **{k: ctl[k] for k in pk if k in ctl}}
             vs = round(ctl["avg_jct_s"] / result["avg_jct_s"], 4)
         else:
-            control_out = {"algorithm": control, "skipped": ctl.get("skipped", "disabled (--control none)")}
+            control_out = {"algorithm": control, "status": ctl.get("status", "disabled"),
+                           "reason": ctl.get("reason", "--control none"), **{k: ctl[k] for k in pk if k in ctl}}
             vs = None
         line = {
             "metric": BASELINE_METRIC,
@@ -502,6 +585,8 @@ def main():
                     + ("; all ranks share cuda:0 over gloo: rehearsal, not a benchmark" if a.share_gpu else ""),
             "config": {
                 "model": "32-job Philly-style trace: ResNet-50 (ImageNet 224, bs256/GPU) + BERT-base (seq128, bs64/GPU)",
+                "trace_scale": f"mean job {a.steps * step_scale} single-GPU steps x N GPUs ({a.precision})",
+                "autoscale": (f"1 -> {world} GPUs, doubling every {a.autoscale_every:g} s" if a.autoscale else None),
                 "global_batch": "per job: per-GPU batch x elastic workers",
                 "seq_len": 128,
                 "parallelism": f"elastic-dp, {a.algorithm}, <= {world} GPU(s)/job, "
@@ -512,7 +597,10 @@ def main():
             "makespan_s": round(result["makespan_s"], 3),
             "p95_jct_s": round(result["p95_jct_s"], 3),
             "wall_s": round(wall_s, 3),
-            "mean_job_steps_1gpu": a.steps * STEP_SCALE,
+            "mean_job_steps_1gpu": a.steps * step_scale,
+            "step_scale": step_scale,
+            "predicted_wall_s": round(pred["main_s"], 1),
+            "capacity_timeline": result.get("capacity_timeline"),
             "rate_limit_s": a.rate_limit,
             "rate_limit_note": RATE_LIMIT_NOTE,
             "membership_changes": result["resize_events"],

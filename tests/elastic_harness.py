@@ -38,7 +38,9 @@ class Controller:
         self.mail_n: dict[str, int] = {}
 
     def _mail(self, wid: str, msg: dict) -> None:
-        n = self.mail_n.get(wid, 0) + 1
+        # the pool's mailbox counter, not a per-controller one: several controllers (jobs) may
+        # drive one pool one after another
+        n = int(self.store.add(f"pool/{wid}/n", 0)) + 1
         self.mail_n[wid] = n
         self.store.set(f"pool/{wid}/msg/{n}", json.dumps(msg))
         self.store.add(f"pool/{wid}/n", 1)
@@ -113,25 +115,42 @@ def stop_pool(store, procs, q, timeout: float = 30) -> dict:
 
 
 def assert_matches_replay(cfg, path: str, device: str, exact: bool = True,
-                          tol: tuple[float, float] = (2e-3, 2e-4)) -> dict:
-    """The elastic run's final state (rank 0's checkpoint) equals the uninterrupted replay
-    (bitwise, or to ``tol`` = (rtol, atol) when ``exact`` is False)."""
+                          tol: tuple[float, float] = (2e-3, 2e-4), backend: str | None = None,
+                          devices: list[str] | None = None, inject: dict | None = None) -> dict:
+    """The elastic run's final state (rank 0's checkpoint) equals the uninterrupted replay of
+    its ``world_log`` (bitwise, or to ``tol`` = (rtol, atol) when ``exact`` is False).
+
+    Runs that trained at a world size >= 3 -- or any run when ``backend`` is given -- are
+    replayed through real collectives of that backend (workloads/replay.py): a w-rank ring
+    average of identical gradients is not exact, so only a replay that performs the same
+    reduction is an oracle.  When the run logged lock-step digests (``step_digests``), a
+    mismatch names the first divergent step."""
+    from vodascheduler_amd.workloads.replay import first_divergence, replay_collective
     from vodascheduler_amd.workloads.train import replay_reference
 
     payload = torch.load(path, map_location="cpu", weights_only=True)
     ex = payload["extras"]
-    nthreads = torch.get_num_threads()
-    torch.set_num_threads(1)
-    try:
-        ref, ref_ex = replay_reference(cfg, list(ex["world_log"]), int(ex["__step__"]), torch.device(device))
-    finally:
-        torch.set_num_threads(nthreads)
+    wl = list(ex["world_log"])
+    if backend is None and max(wl[1::2]) > 2:
+        backend = "gloo" if device == "cpu" else "rccl"
+    if backend is not None:
+        ref, ref_ex = replay_collective(cfg, wl, int(ex["__step__"]), backend, devices, inject=inject)
+    else:
+        nthreads = torch.get_num_threads()
+        torch.set_num_threads(1)
+        try:
+            ref, ref_ex = replay_reference(cfg, wl, int(ex["__step__"]), torch.device(device))
+        finally:
+            torch.set_num_threads(nthreads)
+    div = first_divergence(list(ex.get("steplog") or []), list(ref_ex.get("steplog") or []))
     assert len(ref) == len(payload["tensors"])
     for i, (a, b) in enumerate(zip(payload["tensors"], ref)):
         if exact:
-            assert torch.equal(a, b), (i, float((a.float() - b.float()).abs().max()))
+            assert torch.equal(a, b), (i, float((a.float() - b.float()).abs().max()), div, wl)
         else:  # GPU: nondeterministic reductions (atomics) make trajectories differ in the last bits
-            torch.testing.assert_close(a.float(), b.float(), rtol=tol[0], atol=tol[1])
+            torch.testing.assert_close(a.float(), b.float(), rtol=tol[0], atol=tol[1], msg=lambda m: f"{m}\n{div}")
+    if exact:
+        assert div is None, div
     assert ex["epoch"] == ref_ex["epoch"] and ex["samples"] == ref_ex["samples"]
     return ex
 

@@ -16,7 +16,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 def test_bench_two_ranks_cpu_rehearsal():
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2", "--master-addr",
            "127.0.0.1", "--master-port", str(free_port()), os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps",
-           "1", "--warmup", "2", "--jobs", "6", "--device", "cpu", "--rate-limit", "0.5", "--interarrival", "0.3"]
+           "3", "--warmup", "2", "--jobs", "6", "--device", "cpu", "--rate-limit", "0.5", "--interarrival", "0.3"]
     env = dict(os.environ, VODA_STACKDUMP_S="100")
     r = subprocess.run(cmd, cwd="/tmp", env=env, capture_output=True, text=True, timeout=150)
     assert r.returncode == 0, r.stderr[-3000:]
@@ -30,9 +30,10 @@ def test_bench_two_ranks_cpu_rehearsal():
     assert d["value"] > 0 and d["makespan_s"] >= d["value"]
     assert d["membership_changes"] >= 6  # every job started; some were resized across the two ranks
     assert d["grad_dtype"] == "fp32" and d["allreduce_dtype"] == "fp32"
-    assert d["status"] == "ok" and d["precision"] == "bf16-amp"
+    assert d["status"] == "ok" and d["precision"] == "fp32" and d["dtype"] == "fp32"  # the reference's precision
     # the like-for-like control replayed on the same warm pool (VERDICT r2 Next #6)
     assert d["control"]["algorithm"] == "FIFO" and d["control"]["avg_jct_s"] > 0 and not d["control"]["failed"]
+    assert d["control"]["status"] == "ok" and d["control"]["predicted_wall_s"] > 0
     # both JCTs are printed rounded to 1 ms: on this sub-second CPU trace that alone moves the
     # ratio by up to ~1e-3 / value
     assert d["vs_baseline"] == pytest.approx(d["control"]["avg_jct_s"] / d["value"], rel=1e-3 + 1e-3 / d["value"])
@@ -47,7 +48,7 @@ def test_bench_eight_ranks_cpu_rehearsal():
     ranks, control replay, one JSON line (VERDICT r2 Next #2d)."""
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "8", "--master-addr",
            "127.0.0.1", "--master-port", str(free_port()), os.path.join(ROOT, "bench.py"), "--gpus", "8", "--steps",
-           "2", "--warmup", "1", "--jobs", "8", "--device", "cpu", "--interarrival", "0.3"]
+           "6", "--warmup", "1", "--jobs", "8", "--device", "cpu", "--interarrival", "0.3"]
     r = subprocess.run(cmd, cwd="/tmp", capture_output=True, text=True, timeout=240)
     assert r.returncode == 0, r.stderr[-3000:]
     lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
@@ -57,6 +58,47 @@ def test_bench_eight_ranks_cpu_rehearsal():
     assert d["resize_events"] >= 1 and d["forced_abort_epochs"] == 0
     assert max(int(w) for m in d["step_ms_by_world"].values() for w in m) >= 4
     assert d["vs_baseline"] is not None
+    # the simulator's predictions (used to decide whether the control fits) next to the actuals
+    assert d["predicted_wall_s"] > 0 and d["control"]["predicted_wall_s"] > 0 and d["control"]["wall_s"] > 0
+    print("predicted vs actual wall (s): main", d["predicted_wall_s"], d["wall_s"],
+          "control", d["control"]["predicted_wall_s"], d["control"]["wall_s"])
+
+
+def test_bench_control_overrun_keeps_headline():
+    """A control replay that cannot finish is cut off (its jobs deleted, the pool released)
+    and reported as control.status -- the measured headline still prints with its value
+    (VERDICT r3 Weak #2)."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2", "--master-addr",
+           "127.0.0.1", "--master-port", str(free_port()), os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps",
+           "4", "--warmup", "1", "--jobs", "6", "--device", "cpu", "--rate-limit", "0.5", "--interarrival", "0.3",
+           "--control-timeout", "1.5"]
+    r = subprocess.run(cmd, cwd="/tmp", capture_output=True, text=True, timeout=180)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    d = json.loads(lines[0])
+    assert d["status"] == "ok" and d["value"] > 0
+    assert d["control"]["status"] == "timeout" and d["vs_baseline"] is None, d["control"]
+
+
+def test_bench_autoscale_eight_ranks_cpu_rehearsal():
+    """BASELINE config 5's autoscale 1 -> 8 rehearsed on gloo: the scheduler starts with one
+    GPU of the 8-worker pool and capacity doubles on a schedule; jobs grow onto the new
+    GPUs, and the JSON line carries the capacity timeline."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "8", "--master-addr",
+           "127.0.0.1", "--master-port", str(free_port()), os.path.join(ROOT, "bench.py"), "--gpus", "8", "--steps",
+           "6", "--warmup", "1", "--jobs", "8", "--device", "cpu", "--interarrival", "0.3", "--autoscale",
+           "--autoscale-every", "2", "--control", "none"]
+    r = subprocess.run(cmd, cwd="/tmp", capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    d = json.loads(lines[0])
+    assert d["status"] == "ok" and d["value"] > 0 and d["config"]["autoscale"]
+    tl = d["capacity_timeline"]
+    assert tl[0][1] == 1 and [k for _, k in tl] == sorted(k for _, k in tl) and tl[-1][1] >= 4, tl
+    assert max(int(w) for m in d["step_ms_by_world"].values() for w in m) >= 2
+    print("capacity timeline:", tl)
 
 
 def test_bench_deadline_prints_timeout_line_and_fails():

@@ -161,3 +161,22 @@ def test_xgmi_numeric_link_counters_and_gauges():
     assert 'voda_scheduler_gpu_xgmi_max_bandwidth_gbps{gpu="1"} 608.0' in text
     assert 'voda_scheduler_gpu_xgmi_link_up{gpu="1",port="2"} 0.0' in text
     assert 'voda_scheduler_gpu_xgmi_read_bytes{gpu="1",peer="0"} 12000.0' in text
+
+
+def test_prior_gives_curve_shape_not_absolute_time():
+    """a job measured only at world 2 whose prior is for another precision
+    (bf16 t1 23 ms vs an fp32 step of ~77 ms) must not get speedup(2) = 2 x 23 / 80 < 1 --
+    the prior's curve supplies s(2), the measurement the absolute time."""
+    from vodascheduler_amd.collector.collector import estimate_tables
+    from vodascheduler_amd.common.workload import PROFILES, prior_fields
+
+    prior = prior_fields({"model": "resnet50", "steps_per_epoch": 100}, 1)   # bf16 prior: t1 = 23 ms
+    t2 = 0.080                                                                 # fp32, measured at world 2
+    sp, st = estimate_tables({2: t2}, prior)
+    s2_prior = PROFILES["resnet50"].speedup(2)
+    assert sp["2"] == pytest.approx(2 * (t2 * s2_prior / 2) / t2)            # = the prior's s(2)
+    assert st["1"] == pytest.approx(t2 * s2_prior / 2)                         # fp32-scale t1, ~77-80 ms
+    assert 0.07 < st["1"] < 0.09 and all(sp[str(k)] >= 1.0 for k in range(1, 9))
+    # without any prior: linear below the smallest measured count (unchanged)
+    sp0, st0 = estimate_tables({2: t2}, None)
+    assert sp0["2"] == pytest.approx(2.0) and st0["1"] == pytest.approx(t2)

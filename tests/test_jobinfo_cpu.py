@@ -107,12 +107,15 @@ def test_collector_online_progress_and_category_history(tmp_path):
 
 def test_estimate_tables_prior_and_fill():
     prior = prior_fields({"model": "resnet50", "steps_per_epoch": 10, "epoch_time_1gpu": 0.25}, 1)
-    # only world 4 measured: t(1) from the prior, s(4) from the measurement, Amdahl fill elsewhere
+    # only world 4 measured: the prior supplies the curve's shape (s(4)), the measurement the
+    # absolute time: t(1) = t(4) s_prior(4) / 4 -- never the prior's absolute t(1), which may
+    # be for another precision or batch
     sp, st = estimate_tables({4: 0.03}, prior, max_gpu=8)
-    assert sp["4"] == pytest.approx(4 * 0.025 / 0.03)
+    assert sp["4"] == pytest.approx(prior["speedup"]["4"])
     assert st["4"] == pytest.approx(0.03)
+    assert st["1"] == pytest.approx(0.03 * prior["speedup"]["4"] / 4)
     vals = [sp[str(k)] for k in range(1, 9)]
-    assert vals == sorted(vals) and sp["8"] < 8
+    assert vals == sorted(vals) and sp["8"] <= 8
     # only world 1 measured: unmeasured counts follow the prior's curve, not linear
     sp1, _ = estimate_tables({1: 0.02}, prior, max_gpu=8)
     assert sp1["8"] == pytest.approx(prior["speedup"]["8"])
@@ -178,3 +181,33 @@ def test_measured_step_times_override_speed_model(tmp_path):
         set_measured_step_times(None)
         set_measured_busbw(None)
     assert PROFILES["bert-base"].speedup(8) == pytest.approx(8.0)  # assumed 300 GB/s hides it
+
+
+def test_fp32_trace_priced_at_measured_fp32_step_times():
+    """VERDICT r3 Next #6: under ``--precision fp32`` the bench prices every job with the
+    warm-up's measured fp32 single-GPU step times, so the seeded job info is
+    ``steps x measured fp32 step time`` for both models (not the bf16 profile's)."""
+    from vodascheduler_amd.common.workload import model_profile, set_measured_step_times
+    from vodascheduler_amd.sim.trace import bench_trace
+
+    meas = {"resnet50": 0.0712, "bert-base": 0.0381}
+    tr = bench_trace(8, 60, 1, seed=3, precision="fp32", step_time_s=meas,
+                     batches={"resnet50": 256, "bert-base": 64})
+    set_measured_step_times({m: {1: v * 1e3} for m, v in meas.items()})
+    try:
+        store, svc = _svc()
+        for tj in tr:
+            wl = workload_of(tj.spec)
+            assert wl["precision"] == "fp32"
+            name = svc.create_training_job(json.dumps(tj.spec))
+            info = store.find_job_info(wl["model"], name)
+            epochs = int(store.find_metadata(name)["config"]["epochs"])
+            assert info["estimated_remainning_time_sec"] == pytest.approx(
+                epochs * wl["steps_per_epoch"] * meas[wl["model"]])
+            assert info["step_time_sec"]["1"] == pytest.approx(meas[wl["model"]])
+        # the fp32 profiles themselves are fp32-scale (3-4x the bf16 ones)
+        for m in meas:
+            assert model_profile(m, "fp32").step_time_1gpu > 3 * PROFILES[m].step_time_1gpu
+            assert model_profile(m, "fp32").t1() == pytest.approx(meas[m])   # measured beats profile
+    finally:
+        set_measured_step_times(None)

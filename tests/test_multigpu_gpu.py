@@ -5,7 +5,10 @@ than two GPUs; on an 8 x MI355X node it spawns 2 / 4 / 8 rank processes, one per
   fp32 and bf16;
 * ElasticDDP bucketed fp32 gradients == single-process full-batch gradients;
 * a live resize 2 -> 4 -> 2 of one job on RCCL: every member ends with bitwise-identical
-  parameters and optimizer slots, equal to an uninterrupted replay of the same trajectory;
+  parameters and optimizer slots, equal to a replay of the same trajectory through real
+  RCCL communicators of the same world sizes (workloads/replay.py: the replay performs the
+  same ring reduction, so only per-rank kernel nondeterminism is left to the tolerance; the
+  lock-step digests name the first divergent step on a failure);
 * the abort-epoch path: one rank is killed, the survivors restore the last commit and finish.
 """
 import multiprocessing as mp
@@ -144,7 +147,7 @@ def test_live_resize_2_4_2_on_rccl(gpu_pool, tmp_path):
     from elastic_harness import Controller, assert_matches_replay
 
     store, procs, wids, finish = gpu_pool
-    cfg = _cfg(tmp_path, "resize")
+    cfg = _cfg(tmp_path, "resize", step_digests=True)
     c = Controller(store, "resize", cfg)
     c.publish(wids[:2])
     c.wait_progress(20)
@@ -153,7 +156,7 @@ def test_live_resize_2_4_2_on_rccl(gpu_pool, tmp_path):
         c.wait_progress(c.progress() + 20)
     c.publish([wids[0], wids[-1]])   # shrink onto a different pair: one member migrates
     assert c.wait_done(timeout=240) == "done"
-    ex = assert_matches_replay(cfg, cfg.final_state_path, "cuda:0", exact=False)
+    ex = assert_matches_replay(cfg, cfg.final_state_path, "cuda:0", exact=False, backend="rccl")
     ws = [ex["world_log"][i + 1] for i in range(0, len(ex["world_log"]), 2)]
     assert ws[0] == 2 and ws[-1] == 2 and (len(wids) < 4 or 4 in ws), ex["world_log"]
     dig = _digests(finish(), "resize")
@@ -165,7 +168,7 @@ def test_abort_epoch_survivors_restore_and_finish(gpu_pool, tmp_path):
     from elastic_harness import Controller, assert_matches_replay
 
     store, procs, wids, finish = gpu_pool
-    cfg = _cfg(tmp_path, "kill", commit_every=4)
+    cfg = _cfg(tmp_path, "kill", commit_every=4, step_digests=True)
     c = Controller(store, "kill", cfg)
     c.publish(wids[:2])
     c.wait_progress(30)
@@ -173,5 +176,5 @@ def test_abort_epoch_survivors_restore_and_finish(gpu_pool, tmp_path):
     procs[wids[1]].join(10)
     c.publish(wids[:1], abort=True)
     assert c.wait_done(timeout=240) == "done"
-    ex = assert_matches_replay(cfg, cfg.final_state_path, "cuda:0", exact=False)
+    ex = assert_matches_replay(cfg, cfg.final_state_path, "cuda:0", exact=False, backend="rccl")
     assert ex["world_log"][-1] == 1 and ex["world_log"][-2] % 4 == 0

@@ -353,3 +353,52 @@ def test_gpu_time_charged_at_allocation_held_during_interval():
     e2.step()
     assert e2.core.job_num_gpu[b] == 4
     assert e2.core.ready_jobs[b].time_metrics.gpu_time == pytest.approx(10.0)
+
+
+def test_autoscale_node_addition_grows_jobs_in_place():
+    """Node addition (reference addNode / updateNode, scheduler.go:689-747;
+    placement_manager.go:239-304; README "node addition awareness"): a cluster that starts
+    with one GPU and gains GPUs, then a second node.  Elastic jobs grow onto the new
+    capacity at once (work-conserving, no rate-limit wait) and placement keeps every
+    running worker where it is."""
+    e = Env(rate=30.0, backend=NullBackend({"node0": [0]}))
+    a = e.submit("a", 1, 1, 4)
+    b = e.submit("b", 1, 1, 4)
+    e.step()
+    assert e.core.total_gpus == 1 and e.core.job_num_gpu == {a: 1, b: 0}
+    a_loc = list(e.core.job_workers[a])
+    e.backend._nodes = {"node0": [0, 1, 2]}
+    e.core.set_nodes(e.backend.nodes())
+    e.step()                                  # same instant: the added GPUs are used at once
+    assert e.core.total_gpus == 3
+    assert e.core.job_num_gpu[a] >= 1 and e.core.job_num_gpu[b] >= 1
+    assert sum(e.core.job_num_gpu.values()) == 3
+    assert set(a_loc) <= set(e.core.job_workers[a])           # a's worker did not move
+    held = {j: list(v) for j, v in e.core.job_workers.items()}
+    e.backend._nodes = {"node0": [0, 1, 2, 3], "node1": [0, 1, 2, 3]}
+    e.core.set_nodes(e.backend.nodes())
+    e.step()
+    assert e.core.total_gpus == 8
+    assert e.core.job_num_gpu == {a: 4, b: 4}                 # both at MAX_NP
+    # node-level best fit consolidates each 4-worker job on one node (the reference's
+    # objective); Munkres keeps the job holding most of node0 there, so only the smaller
+    # job's workers move to the new node
+    for j, locs in e.core.job_workers.items():
+        assert len({n for n, _ in locs}) == 1, (j, locs)        # no cross-node job
+    big = max(held, key=lambda j: len(held[j]))
+    assert set(held[big]) <= set(e.core.job_workers[big])
+    moved = sum(len(set(held[j]) - set(e.core.job_workers[j])) for j in held)
+    assert moved <= min(len(v) for v in held.values()), (held, e.core.job_workers)
+
+
+def test_simulated_capacity_ramp_1_to_8():
+    """BASELINE config 5 ("autoscale 1->8"): the 32-job trace while capacity ramps 1 -> 2 ->
+    4 -> 8 completes; JCT lands between the fixed-8 and fixed-1 clusters."""
+    tr = philly_trace(32, seed=5, mean_interarrival_s=30, mean_duration_1gpu_s=300, max_gpus=8)
+    ramp = [(0.0, {"node0": [0]}), (600.0, {"node0": [0, 1]}), (1200.0, {"node0": list(range(4))}),
+            (1800.0, {"node0": list(range(8))})]
+    r = simulate(tr, "FfDLOptimizer", gpus=8, capacity=ramp)
+    full = simulate(tr, "FfDLOptimizer", gpus=8)
+    one = simulate(tr, "FfDLOptimizer", gpus=1)
+    assert r.n_jobs == 32 and full.avg_jct <= r.avg_jct <= one.avg_jct
+    assert 0 < r.utilization <= 1.0

@@ -76,6 +76,8 @@ class SimBackend(Backend):
         self.gpu_busy_seconds = 0.0
         self.total_resizes = 0
         self.total_migrations = 0
+        self._inventory = [(clock.now(), sum(len(v) for v in self._nodes.values()))]  # (t, #GPUs)
+        self.max_gpus = self._inventory[0][1]
 
     # ------------------------------------------------------------ time
     def advance(self, t: float) -> None:
@@ -200,8 +202,22 @@ class SimBackend(Backend):
     def set_nodes(self, nodes: dict[str, list[int]]) -> None:
         from .base import EV_NODES
 
+        self.advance(self.clock.now())
         self._nodes = {k: list(v) for k, v in nodes.items()}
+        n = sum(len(v) for v in self._nodes.values())
+        self._inventory.append((self.clock.now(), n))
+        self.max_gpus = max(self.max_gpus, n)
         self.emit(EV_NODES, self.nodes())
+
+    def gpu_present_seconds(self, t0: float, t1: float) -> float:
+        """GPU-seconds of schedulable capacity between ``t0`` and ``t1``."""
+        tot = 0.0
+        inv = self._inventory + [(float("inf"), 0)]
+        for (ta, n), (tb, _) in zip(inv, inv[1:]):
+            lo, hi = max(ta, t0), min(tb, t1)
+            if hi > lo:
+                tot += n * (hi - lo)
+        return tot
 
     def list_running(self):
         return {n: list(j.workers) for n, j in self.jobs.items() if j.n > 0}

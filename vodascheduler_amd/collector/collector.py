@@ -72,10 +72,13 @@ def estimate_tables(step_t: dict[int, float], prior: dict | None = None,
 
     ``step_t[k]``: seconds per training step with ``k`` workers (each step processes ``k``
     per-GPU batches), so ``speedup(k) = k t(1) / t(k)`` -- robust to epochs cut short by a
-    resize, unlike the epoch-time ratio.  ``t(1)``: measured, else the prior's (the
-    workload's MI355X profile or the category's history), else linear below the smallest
-    measured count.  Unmeasured counts: Amdahl fit through the measured points when one with
-    k > 1 exists, else the prior's curve, else linear."""
+    resize, unlike the epoch-time ratio.  ``t(1)``: measured; else, when only larger counts
+    were measured, the smallest measured count's time scaled by the PRIOR CURVE's speedup
+    there (``t(1) = t(k) s_prior(k) / k``: the prior -- the workload's MI355X profile or the
+    category's history -- supplies the shape of the curve, never an absolute time that may
+    be for another precision or batch); else linear below the smallest measured count; with
+    nothing measured, the prior's own t(1).  Unmeasured counts: Amdahl fit through the
+    measured points when one with k > 1 exists, else the prior's curve, else linear."""
     ks = sorted(k for k, v in step_t.items() if k > 0 and v > 0)
     prior_sp = (prior or {}).get("speedup") or {}
     prior_t1 = float(((prior or {}).get("step_time_sec") or {}).get("1", 0.0) or 0.0)
@@ -83,10 +86,13 @@ def estimate_tables(step_t: dict[int, float], prior: dict | None = None,
         prior_sp, prior_t1 = {}, 0.0
     if 1 in step_t and step_t[1] > 0:
         t1 = step_t[1]
+    elif ks:
+        kmin = ks[0]
+        s_prior = float(prior_sp.get(str(kmin), 0.0) or 0.0)
+        # linear below the smallest measured count unless the prior curve says otherwise
+        t1 = step_t[kmin] * min(float(kmin), s_prior) / kmin if s_prior > 0 else step_t[kmin]
     elif prior_t1 > 0:
         t1 = prior_t1
-    elif ks:
-        t1 = step_t[ks[0]]  # linear below the smallest measured count
     else:
         return {}, {}
     measured = {k: min(float(k), k * t1 / step_t[k]) for k in ks}

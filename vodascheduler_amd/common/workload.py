@@ -170,16 +170,22 @@ class ModelProfile:
         bw = busbw_gbs if busbw_gbs is not None else intra_node_busbw(n)
         return 2.0 * (n - 1) / n * self.grad_mb * 1e6 / (bw * 1e9)
 
+    def t1(self) -> float:
+        """Seconds per single-GPU step: this box's measurement when one is installed
+        (``set_measured_step_times``: the bench warm-up at the run's precision), else the
+        profile's."""
+        meas = _MEASURED_STEP.get(self.name)
+        return meas.get(1, self.step_time_1gpu) if meas else self.step_time_1gpu
+
     def speedup(self, n: int, busbw_gbs: float | None = None) -> float:
         if n <= 0:
             return 0.0
         meas = _MEASURED_STEP.get(self.name)
         if meas and n in meas and busbw_gbs is None:
             # measured: n workers each process one per-GPU batch per step of meas[n] seconds
-            t1 = meas.get(1, self.step_time_1gpu)
-            return n * t1 / meas[n]
+            return n * self.t1() / meas[n]
         if self.grad_mb > 0:
-            t1 = self.step_time_1gpu
+            t1 = self.t1()
             c = self.comm_time(n, busbw_gbs)
             exposed = max(0.0, c - self.overlap * t1)
             return n * t1 / (t1 + exposed)
@@ -207,11 +213,32 @@ PROFILES = {
 }
 
 
+# fp32 compute (the reference's precision: tensorflow2_keras_cifar_elastic.py:147-166 builds
+# the Keras model with no mixed-precision policy; pytorch_mnist_elastic.py is plain fp32):
+# MI355X single-GPU step times, same batches.  ResNet-50 76.9 ms / BERT-base 39.7 ms at the
+# end of round 3 (profiles/r3/model_step_fp32.jsonl, rocprof_resnet50_fp32.md,
+# rocprof_bert_fp32.md); the other models keep their bf16 ratio to fp32 unmeasured, so they
+# fall back to the bf16 profile.
+PROFILES_FP32 = {
+    "resnet50": ModelProfile("resnet50", alpha=0.01, step_time_1gpu=0.0769, grad_mb=102.2, measured=True),
+    "bert-base": ModelProfile("bert-base", alpha=0.05, step_time_1gpu=0.0397, grad_mb=438.0, measured=True),
+}
+PRECISIONS = ("bf16", "fp32")
+
+
+def model_profile(model: str, precision: str = "bf16") -> ModelProfile | None:
+    """The MI355X profile of ``model`` at a compute precision (``bf16`` = bf16 autocast with
+    fp32 master weights / gradients, ``fp32`` = the reference's precision)."""
+    if precision == "fp32" and model in PROFILES_FP32:
+        return PROFILES_FP32[model]
+    return PROFILES.get(model)
+
+
 def profile_of(wl: dict) -> ModelProfile:
-    """The speed model of a declared workload: the model's MI355X profile; a model without
-    one gets the Amdahl fallback with the workload's own ``alpha`` and a step time derived
-    from its declared epoch time."""
-    prof = PROFILES.get(wl.get("model", ""))
+    """The speed model of a declared workload: the model's MI355X profile at the workload's
+    declared ``precision`` (default bf16); a model without one gets the Amdahl fallback with
+    the workload's own ``alpha`` and a step time derived from its declared epoch time."""
+    prof = model_profile(wl.get("model", ""), wl.get("precision", "bf16"))
     if prof is not None:
         return prof
     spe = max(1, int(wl.get("steps_per_epoch", 1)))

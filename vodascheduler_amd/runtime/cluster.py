@@ -39,15 +39,30 @@ def run_trace(store, trace: list[TraceJob], worker_locs, algorithm: str = "Elast
               timeout: float = 3600.0, gpu_type: str = DEFAULT_GPU_TYPE, progress=None,
               collect_every_s: float = 2.0, trace_path: str | None = None,
               gpu_numa: dict[str, dict[int, int]] | None = None, stop_pool: bool = True,
-              settle_timeout: float = 120.0) -> dict:
+              settle_timeout: float = 120.0, capacity_ramp: list[tuple[float, int]] | None = None) -> dict:
     """Submit ``trace`` in real time (``submit_time`` seconds after start) and wait until every
     job completed.  Returns JCT / makespan / resize-latency statistics.  ``gpu_numa``: node ->
     {GPU: NUMA domain} from topology discovery (placement tie-breaker).  ``stop_pool=False``
-    leaves the pool workers serving (another trace follows on the same warm pool)."""
+    leaves the pool workers serving (another trace follows on the same warm pool).
+    ``capacity_ramp`` = [(t, k)]: the scheduler's inventory is the first ``k`` pool GPUs from
+    ``t`` seconds on (node additions by an autoscaler; the first entry applies at start).
+    On a timeout or error every job still running is deleted (its workers leave at their
+    next commit), so the pool is free for whatever follows."""
     db = MemoryStore()
     mq = InProcQueue(maxsize=10 ** 6)
     svc = TrainingService(db, mq)
-    backend = PoolBackend(store, worker_locs, train_defaults, settle_timeout=settle_timeout)
+    ramp = sorted(capacity_ramp or [])
+
+    def inventory(k: int) -> dict[str, list[int]]:
+        inv: dict[str, list[int]] = {}
+        for n, g in list(worker_locs)[:k]:
+            inv.setdefault(n, []).append(g)
+        return inv
+
+    initial = inventory(ramp.pop(0)[1]) if ramp and ramp[0][0] <= 0 else None
+    backend = PoolBackend(store, worker_locs, train_defaults, settle_timeout=settle_timeout,
+                          initial_nodes=initial)
+    timeline = [(0.0, sum(len(v) for v in backend.nodes().values()))]
     from ..placement.manager import PlacementManager
 
     core = SchedulerCore(gpu_type, db, ResourceAllocator(db), backend, algorithm=algorithm,
@@ -69,9 +84,17 @@ def run_trace(store, trace: list[TraceJob], worker_locs, algorithm: str = "Elast
     names: list[str] = []
     pending = sorted(trace, key=lambda tj: tj.submit_time)
     last_report = last_collect = t0
+    ok = False
     try:
         while True:
             now = time.time()
+            while ramp and now - t0 >= ramp[0][0]:
+                _, k = ramp.pop(0)
+                backend.set_nodes(inventory(k))
+                timeline.append((round(now - t0, 2), k))
+                log.info("capacity: %d GPUs at t=%.1fs", k, now - t0)
+                if progress is not None:
+                    progress(f"t={now - t0:.0f}s capacity -> {k} GPUs")
             if collector is not None and now - last_collect > collect_every_s:
                 last_collect = now
                 collector.update_info_all(list(names))
@@ -90,8 +113,15 @@ def run_trace(store, trace: list[TraceJob], worker_locs, algorithm: str = "Elast
             time.sleep(0.05)
         t1 = time.time()
         jobs = runner.call(lambda: {n: core.done_jobs[n].clone() for n in names})
+        ok = True
     finally:
         runner.stop()
+        if not ok:  # cut the trace off: running jobs' workers leave at their next commit
+            for n in list(backend.active):
+                try:
+                    backend.delete_job(n)
+                except Exception:
+                    log.exception("deleting %s after the aborted trace failed", n)
         backend.shutdown(stop_pool)
         if tracer is not None:
             tracer.save(trace_path)
@@ -109,6 +139,7 @@ def run_trace(store, trace: list[TraceJob], worker_locs, algorithm: str = "Elast
         "resize_latency_p50_s": q(lat["resize"], 0.5), "resize_latency_p95_s": q(lat["resize"], 0.95),
         "reschedules": core.resched_count, "jct": jct, "forced_abort_epochs": backend.forced_epochs,
         "events": backend.events, "resize_latency": backend.resize_latency,
+        "capacity_timeline": timeline if len(timeline) > 1 else None,
     }
 
 

@@ -49,20 +49,27 @@ def job_train_config(job, defaults: dict | None = None) -> dict:
     for k in ("reduction", "compression"):  # the job's own choice beats the cluster default
         if wl.get(k):
             d[k] = wl[k]
+    if wl.get("precision"):  # declared compute precision: fp32 = no autocast (the reference's)
+        d["amp"] = wl["precision"] != "fp32"
     return d
 
 
 class PoolBackend(Backend):
     def __init__(self, store, worker_locs: list[Loc], train_defaults: dict | None = None,
-                 poll_interval: float = 0.05, settle_timeout: float = 120.0):
+                 poll_interval: float = 0.05, settle_timeout: float = 120.0,
+                 initial_nodes: dict[str, list[int]] | None = None):
         super().__init__()
         self.store = store
         self._lock = threading.Lock()
         self._pub_lock = threading.RLock()  # one publisher per job at a time (scheduler vs failure path)
         self.workers = [worker_id(l) for l in worker_locs]
-        self.node_gpus: dict[str, list[int]] = {}
+        self.node_gpus_all: dict[str, list[int]] = {}
         for n, g in worker_locs:
-            self.node_gpus.setdefault(n, []).append(g)
+            self.node_gpus_all.setdefault(n, []).append(g)
+        # the schedulable inventory: every pool GPU, or ``initial_nodes`` (an autoscaled
+        # cluster starts small; set_nodes announces the rest)
+        self.node_gpus: dict[str, list[int]] = {k: list(v) for k, v in
+                                                (initial_nodes or self.node_gpus_all).items()}
         self.train_defaults = dict(train_defaults or {})
         self.members: dict[str, list[str]] = {}    # desired membership (scheduler view)
         self.live: dict[str, tuple[int, list[str]]] = {}  # last published (epoch, members)
@@ -175,6 +182,22 @@ class PoolBackend(Backend):
 
     def nodes(self):
         return {k: list(v) for k, v in self.node_gpus.items()}
+
+    def set_nodes(self, nodes: dict[str, list[int]]) -> None:
+        """Announce a new schedulable inventory (a node / GPUs added by an autoscaler, or
+        drained): the scheduler re-plans on the EV_NODES event (reference addNode /
+        updateNode / deleteNode, scheduler.go:689-747).  Every announced GPU must have a
+        pool worker."""
+        known = {worker_id((n, g)) for n, gs in self.node_gpus_all.items() for g in gs}
+        for n, gs in nodes.items():
+            for g in gs:
+                if worker_id((n, g)) not in known:
+                    raise ValueError(f"no pool worker for GPU {n}:{g}")
+        with self._lock:
+            self.node_gpus = {k: sorted(v) for k, v in nodes.items() if v}
+        from ..backend.base import EV_NODES
+
+        self.emit(EV_NODES, self.nodes())
 
     def list_running(self):
         return {j: [(m.rsplit(":", 1)[0], int(m.rsplit(":", 1)[1])) for m in mem]

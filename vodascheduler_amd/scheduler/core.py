@@ -325,9 +325,14 @@ class SchedulerCore:
                     self.placement.delete_node(n)
             for n, g in nodes.items():
                 self.placement.update_node(n, g)
+        grew = sum(len(v) for v in nodes.values()) > self.total_gpus and bool(self.nodes)
         self.nodes = nodes
         self.total_gpus = sum(len(v) for v in nodes.values())
         self._topology_dirty = True
+        # capacity ARRIVED (autoscaler node addition, a drained GPU back): like freed GPUs,
+        # idle capacity is used at once instead of after the rate limit (work-conserving)
+        if self.work_conserving and grew:
+            self._urgent = True
         # a GPU that vanished under a running worker (drain, failure) leaves that job broken:
         # re-place it now instead of after the rate limit (work-conserving mode)
         alive = {(n, g) for n, gs in nodes.items() for g in gs}

@@ -54,20 +54,29 @@ def simulate(trace: list[TraceJob], algorithm: str = "ElasticFIFO", gpus: int = 
              drain: list[tuple[float, str, int]] | None = None, max_time: float = 1e9,
              gpu_type: str = DEFAULT_GPU_TYPE, trace_path: str | None = None,
              naive_placement: bool = False, info_mode: str = "online",
-             collector_period_s: float = 60.0) -> SimResult:
+             collector_period_s: float = 60.0,
+             capacity: list[tuple[float, dict[str, list[int]]]] | None = None) -> SimResult:
     """Run a trace to completion.  ``drain`` = [(time, node, gpu)] GPU drain events;
     ``trace_path`` writes the scheduler timeline (Chrome-trace JSON, virtual time);
     ``naive_placement``: best-fit without the Munkres bindings (placement/manager.py);
     ``info_mode``: what the info-driven policies see (backend/sim.py): ``online`` (default:
     submission-time estimates from the declared workload, then the collector every
     ``collector_period_s``, the reference cron's 1 min), ``oracle``, ``prior`` or
-    ``placeholder`` (the reference as written: 1 s epochs, linear speedup)."""
+    ``placeholder`` (the reference as written: 1 s epochs, linear speedup).
+    ``capacity`` = [(time, {node: [gpu, ...]})]: the schedulable inventory from ``time`` on
+    -- nodes / GPUs added (a cluster autoscaler, spot capacity returning) or removed; an
+    entry at time 0 is the starting inventory.  Utilisation is measured against the GPUs
+    present over time."""
     clock = ManualClock(0.0)
     store = MemoryStore()
     mq = InProcQueue(maxsize=10 ** 6)
     svc = TrainingService(store, mq, clock, seed_from_workload=info_mode not in ("placeholder", "mixed"))
     nodes = nodes or {"node0": list(range(gpus))}
-    backend = SimBackend(clock, nodes, store, resize_overhead_s, restart_overhead_s, info_mode=info_mode,
+    caps = sorted(capacity or [], key=lambda c: c[0])
+    start_nodes = nodes
+    if caps and caps[0][0] <= 0:
+        start_nodes = caps.pop(0)[1]
+    backend = SimBackend(clock, start_nodes, store, resize_overhead_s, restart_overhead_s, info_mode=info_mode,
                          collector_period_s=collector_period_s)
     placement = None
     if use_placement and naive_placement:
@@ -89,6 +98,8 @@ def simulate(trace: list[TraceJob], algorithm: str = "ElasticFIFO", gpus: int = 
     while True:
         t_arr = pending[0].submit_time if pending else None
         t_drain = drains[0][0] if drains else None
+        if caps and (t_drain is None or caps[0][0] < t_drain):
+            t_drain = caps[0][0]
         t_done = backend.next_event()
         t_sched = core.next_wakeup()
         active = bool(core.ready_jobs) or bool(pending)
@@ -108,6 +119,8 @@ def simulate(trace: list[TraceJob], algorithm: str = "ElasticFIFO", gpus: int = 
             names.append(name)
             doc = store.find_metadata(name)
             backend.on_submit(name, doc["job_category"], doc["spec"], int(doc["config"]["epochs"]))
+        while caps and caps[0][0] <= t:
+            backend.set_nodes(caps.pop(0)[1])
         while drains and drains[0][0] <= t:
             _, node, gpu = drains.pop(0)
             cur = backend.nodes()
@@ -136,10 +149,10 @@ def simulate(trace: list[TraceJob], algorithm: str = "ElasticFIFO", gpus: int = 
     first = min(tj.submit_time for tj in trace)
     last = max(core.done_jobs[n].finish_timestamp for n in names)
     vals = sorted(jct.values())
-    total_gpus = sum(len(v) for v in nodes.values())
+    total_gpus = max(sum(len(v) for v in nodes.values()), backend.max_gpus)
     return SimResult(algorithm=algorithm, gpus=total_gpus, n_jobs=len(names), avg_jct=statistics.fmean(vals),
                      median_jct=statistics.median(vals), p95_jct=vals[min(len(vals) - 1, int(0.95 * len(vals)))],
                      makespan=last - first, avg_wait=statistics.fmean(waits),
-                     utilization=backend.gpu_busy_seconds / max(1e-9, (last - first) * total_gpus),
+                     utilization=backend.gpu_busy_seconds / max(1e-9, backend.gpu_present_seconds(first, last)),
                      reschedules=core.resched_count,
                      resizes=backend.total_resizes, migrations=backend.total_migrations, jct=jct)

@@ -16,17 +16,20 @@ from dataclasses import dataclass
 
 from ..common.types import DEFAULT_GPU_TYPE, GPU_NAME_LABEL, GPU_RESOURCE, JobConfigEnv
 from ..common.workload import (ASSUMED_BUSBW_GBS, ASSUMED_INTERNODE_BUSBW_GBS, PROFILES,  # noqa: F401
-                               WORKLOAD_ANNOTATION, ModelProfile, speedup_table, workload_from_launcher,
-                               workload_of)
+                               WORKLOAD_ANNOTATION, ModelProfile, model_profile, speedup_table,
+                               workload_from_launcher, workload_of)
 
 
 def make_spec(name: str, model: str, np_: int, min_np: int, max_np: int, epochs: int, steps_per_epoch: int,
               gpu_type: str = DEFAULT_GPU_TYPE, priority: int | None = None, per_gpu_batch: int | None = None,
-              epoch_time_1gpu: float | None = None, category: str | None = None) -> dict:
+              epoch_time_1gpu: float | None = None, category: str | None = None,
+              precision: str | None = None) -> dict:
     """An MPIJob spec with the reference's launcher env knobs.  ``category``: the
     ``JOB_CATEGORY`` knob -- jobs of one category share measured job-info history (the
-    reference keys history by the un-timestamped job name, handlers.go:180-206)."""
-    prof = PROFILES[model]
+    reference keys history by the un-timestamped job name, handlers.go:180-206).
+    ``precision`` (bf16 | fp32) is declared in the workload annotation: it prices the job
+    (``common.workload.model_profile``) and selects the workers' compute precision."""
+    prof = model_profile(model, precision or "bf16")
     env = [{"name": "JOB_NAME", "value": name}, {"name": "NP", "value": str(np_)},
            {"name": "MIN_NP", "value": str(min_np)}, {"name": "MAX_NP", "value": str(max_np)},
            {"name": "EPOCHS", "value": str(epochs)}]
@@ -39,6 +42,8 @@ def make_spec(name: str, model: str, np_: int, min_np: int, max_np: int, epochs:
           "alpha": prof.alpha}
     if per_gpu_batch is not None:
         wl["per_gpu_batch"] = per_gpu_batch
+    if precision is not None:
+        wl["precision"] = precision
     cmd = (f"vodarun --min-np $(MIN_NP) --max-np $(MAX_NP) python -m vodascheduler_amd.workloads.train "
            f"--model {model} --epochs $(EPOCHS) --steps-per-epoch {steps_per_epoch} --name $(JOB_NAME)")
     return {
@@ -101,13 +106,17 @@ def philly_trace(n_jobs: int = 32, seed: int = 0, mean_interarrival_s: float = 3
 
 def bench_trace(n_jobs: int = 32, mean_steps: int = 30, n_gpus: int = 1, seed: int = 0,
                 mean_interarrival_s: float = 0.5, models: tuple[str, ...] = ("resnet50", "bert-base"),
-                batches: dict[str, int] | None = None, epochs: int = 2) -> list[TraceJob]:
+                batches: dict[str, int] | None = None, epochs: int = 2, precision: str | None = None,
+                step_time_s: dict[str, float] | None = None) -> list[TraceJob]:
     """The 32-job Philly-style trace run by ``bench.py`` on real MI355X GPUs.
 
     Weak scaling: every job's work (single-GPU steps at the per-GPU batch) is multiplied by
     ``n_gpus``, so the per-GPU work is fixed as the pool grows.  Requests follow the Philly
     size mix capped at ``n_gpus``; every job is elastic in ``[1, min(n_gpus, 2 x request)]``.
     Durations are log-normal (sigma 0.8) around ``mean_steps``; arrivals are Poisson.
+    ``precision`` is declared in every job's workload; ``step_time_s`` (model -> measured
+    seconds per single-GPU step on this box at that precision) prices the declared epoch
+    times -- the job-info priors of the info-driven policies -- instead of the profiles.
     """
     rng = random.Random(seed)
     sizes, weights = [1, 2, 4, 8], [0.50, 0.25, 0.15, 0.10]
@@ -122,8 +131,10 @@ def bench_trace(n_jobs: int = 32, mean_steps: int = 30, n_gpus: int = 1, seed: i
         steps = max(2 * epochs, int(round(rng.lognormvariate(math.log(mean_steps) - 0.32, 0.8) * n_gpus)))
         spe = max(1, steps // epochs)
         max_np = max(np_, min(n_gpus, 2 * np_))
+        ep1 = spe * step_time_s[model] if step_time_s and step_time_s.get(model) else None
         out.append(TraceJob(t, make_spec(f"{model}-j{i:02d}", model, np_, 1, max_np, epochs, spe,
-                                         per_gpu_batch=batches.get(model), category=model)))
+                                         per_gpu_batch=batches.get(model), category=model,
+                                         epoch_time_1gpu=ep1, precision=precision)))
     return out
 
 

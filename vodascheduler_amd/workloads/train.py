@@ -66,6 +66,9 @@ class TrainConfig:
     eval_batches: int = 0              # held-out synthetic batches evaluated after every epoch (0: no eval)
     report_progress: bool = False      # rank 0 publishes the committed step under job/<name>/progress
     progress_every_s: float = 1.0      # rank 0 rewrites <metrics_dir>/<job>.progress.json at most this often
+    # lock-step oracle (tests): every step appends "step:world:lr:sha1(optimizer state)" to the
+    # committed extras (workloads/replay.py); one host sync per step, never in production
+    step_digests: bool = False
 
 
 def build(cfg: TrainConfig, device: torch.device):
@@ -82,6 +85,19 @@ def build(cfg: TrainConfig, device: torch.device):
 GRAD_DTYPES = {"fp32": torch.float32, "bf16": torch.bfloat16, "fp16": torch.float16}
 
 
+def synthetic_pool(w, cfg: TrainConfig, bs: int, device: torch.device) -> list:
+    """The ``cfg.data_pool`` synthetic batches a job cycles through (seeded: every rank of
+    every run of the job draws the same ones)."""
+    g = torch.Generator(device=device).manual_seed(cfg.seed + 1)
+    pool = []
+    for _ in range(max(1, cfg.data_pool)):
+        b = w.make_batch(bs, device, g)
+        if w.channels_last and device.type == "cuda":
+            b = tuple(t.to(memory_format=torch.channels_last) if t.dim() == 4 else t for t in b)
+        pool.append(b)
+    return pool
+
+
 class _Warm:
     """A built workload kept resident on the worker's GPU between jobs (288 GB HBM): model,
     flat optimizer buffers, DDP hooks, synthetic batches and a device snapshot of the initial
@@ -91,13 +107,7 @@ class _Warm:
     def __init__(self, cfg: TrainConfig, device: torch.device):
         self.w, self.model, self.opt, self.base_lr = build(cfg, device)
         self.bs = cfg.per_gpu_batch or self.w.per_gpu_batch
-        g = torch.Generator(device=device).manual_seed(cfg.seed + 1)
-        self.pool = []
-        for _ in range(max(1, cfg.data_pool)):
-            b = self.w.make_batch(self.bs, device, g)
-            if self.w.channels_last and device.type == "cuda":
-                b = tuple(t.to(memory_format=torch.channels_last) if t.dim() == 4 else t for t in b)
-            self.pool.append(b)
+        self.pool = synthetic_pool(self.w, cfg, self.bs, device)
         self.ddp = ElasticDDP(self.model, None, self.opt, bucket_cap_mb=cfg.bucket_cap_mb,
                               compression=cfg.compression, reduction=cfg.reduction,
                               overlap_optimizer=cfg.overlap_optimizer)
@@ -232,7 +242,8 @@ def train_elastic(ctx: ElasticContext, cfg: TrainConfig, use_cache: bool = True)
     # Part of the synced / committed state, so a restore rolls it back with the step counter
     # and a joining member inherits it: ``replay_reference`` re-runs the same trajectory.
     # perf: {world: [steps, seconds]} measured by StepProfiler (fast online profiling)
-    state = TorchState(ctx, model, opt, epoch=0, samples=0, world_log=[], perf={})
+    # steplog: lock-step digests (cfg.step_digests), committed / restored with the step counter
+    state = TorchState(ctx, model, opt, epoch=0, samples=0, world_log=[], perf={}, steplog=[])
     logger = MetricsCSVLogger(cfg.metrics_dir, ctx.job, cfg.epochs, bs)
     samples_per_epoch = cfg.steps_per_epoch * bs
     stats = {"steps": 0, "samples": 0, "train_time": 0.0, "model": cfg.model, "resizes": 0}
@@ -330,6 +341,11 @@ def train_elastic(ctx: ElasticContext, cfg: TrainConfig, use_cache: bool = True)
                 state.samples += bs * world
                 state.step += 1
                 steps += 1
+                if cfg.step_digests:  # every member: the log is state, synced from any holder
+                    from .replay import step_record
+
+                    state.steplog = list(state.steplog) + [
+                        step_record(state.step, world, float(opt.param_groups[0]["lr"]), opt.flat_state_tensors())]
                 stats["steps"] += 1
                 stats["samples"] += bs * world
                 if state.step % cfg.commit_every == 0:
@@ -413,13 +429,7 @@ def replay_reference(cfg: TrainConfig, world_log: list[int], total_steps: int, d
     Returns (state tensors, extras)."""
     w, model, opt, base_lr = build(cfg, device)
     bs = cfg.per_gpu_batch or w.per_gpu_batch
-    g = torch.Generator(device=device).manual_seed(cfg.seed + 1)
-    pool = []
-    for _ in range(max(1, cfg.data_pool)):
-        b = w.make_batch(bs, device, g)
-        if w.channels_last and device.type == "cuda":
-            b = tuple(t.to(memory_format=torch.channels_last) if t.dim() == 4 else t for t in b)
-        pool.append(b)
+    pool = synthetic_pool(w, cfg, bs, device)
     ddp = ElasticDDP(model, None, opt, bucket_cap_mb=cfg.bucket_cap_mb, compression=cfg.compression,
                      reduction=cfg.reduction, overlap_optimizer=cfg.overlap_optimizer)
     segs = [(world_log[i], world_log[i + 1]) for i in range(0, len(world_log), 2)]
@@ -433,6 +443,7 @@ def replay_reference(cfg: TrainConfig, world_log: list[int], total_steps: int, d
 
     samples_per_epoch = cfg.steps_per_epoch * bs
     epoch = samples = 0
+    steplog: list[str] = []
     for step in range(total_steps):
         world = world_at(step)
         lr_scaler = 1 if cfg.reduction == "adasum" else world
@@ -447,11 +458,16 @@ def replay_reference(cfg: TrainConfig, world_log: list[int], total_steps: int, d
         samples += bs * world
         if samples >= samples_per_epoch:
             epoch, samples = epoch + 1, 0
+        if cfg.step_digests:
+            from .replay import step_record
+
+            steplog.append(step_record(step + 1, world, float(opt.param_groups[0]["lr"]), opt.flat_state_tensors()))
     for m in model.modules():  # host-side BN counters -> buffers (as TorchState.tensors)
         if hasattr(m, "sync_batches_tracked"):
             m.sync_batches_tracked()
     ts = opt.flat_state_tensors() + [b for b in model.buffers() if b.dtype.is_floating_point or b.dtype == torch.int64]
-    return [t.detach().cpu() for t in ts], {"epoch": epoch, "samples": samples, "__step__": total_steps}
+    return [t.detach().cpu() for t in ts], {"epoch": epoch, "samples": samples, "__step__": total_steps,
+                                            "steplog": steplog}
 
 
 @torch.no_grad()
