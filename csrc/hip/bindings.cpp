@@ -51,6 +51,13 @@ PYBIND11_MODULE(_vodahip, m) {
   m.def("gemm_bnstats_groups", &gemm_bnstats_groups);
   m.def("gemm_bnstats", &gemm_bnstats, py::arg("x"), py::arg("w"), py::arg("y"), py::arg("part"), py::arg("M"),
         py::arg("N"), py::arg("K"), py::arg("G"), py::arg("stream"), py::arg("accumulate") = false);
+  m.def("gemm_f32_stats_supported", &gemm_f32_stats_supported);
+  m.def("gemm_f32_stats_groups", &gemm_f32_stats_groups);
+  m.def("gemm_f32_stats", &gemm_f32_stats, py::arg("x"), py::arg("w"), py::arg("y"), py::arg("part"), py::arg("M"),
+        py::arg("N"), py::arg("K"), py::arg("G"), py::arg("stream"), py::arg("accumulate") = false);
+  m.def("wgrad_f32_workspace_floats", &wgrad_f32_workspace_floats);
+  m.def("wgrad_f32_config", &wgrad_f32_config);
+  m.def("wgrad_f32", &wgrad_f32);
   m.def("subsample2d", &subsample2d);
   m.def("conv3x3_c64_wgrad_workspace_floats", &conv3x3_c64_wgrad_workspace_floats);
   m.def("conv3x3_c64_wgrad", &conv3x3_c64_wgrad);

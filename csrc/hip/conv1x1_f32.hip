@@ -1,0 +1,474 @@
+// fp32 1x1-convolution GEMMs on the f32-input MFMA of gfx950 (v_mfma_f32_32x32x2_f32: exact
+// fp32, one rounding per product, 157 TF = the fp32 VALU rate; no xf32 on CDNA4).  The
+// reference trains in fp32 (tensorflow2_keras_cifar_elastic.py:147-166), so ResNet-50's
+// fp32 step is the headline's; these kernels own the 1x1 convolutions of its bottlenecks:
+//
+//   forward       Y[M][N] (+)= X[M][K] . W[N][K]^T  with the BN statistics of Y's columns in
+//                 the epilogue (per-workgroup partial sums for batchnorm.hip's finalize) --
+//                 the statistics pass over Y disappears;
+//   weight grad   dW[N][K] (+)= dY[M][N]^T . X[M][K]  (reduction over the M = N*H*W pixels),
+//                 split-K, accumulated straight into the optimizer's fp32 flat gradient.
+//
+// Operand layout of v_mfma_f32_32x32x2_f32: lane l holds A[i = l&31][k = l>>5] and
+// B[k = l>>5][j = l&31] (one f32 each); C/D: col = l&31, row = (reg&3) + 8(reg>>2) + 4(l>>5).
+//
+// Forward (gemm_f32_stats_kernel), the fp32 twin of gemm_bnstats.hip: a workgroup keeps the
+// W column tile [NC][K] in LDS (row pitch K + 4 floats: the 16-lane groups of ds_read_b128
+// cover all 64 banks once) and walks every G-th 128-row tile; each wave owns 32 rows.  The
+// reduction index is PERMUTED inside every 8-wide k chunk: lane half h takes k = 8q + 4h + s
+// for MFMA s = 0..3, so each lane feeds four MFMAs from ONE 16-byte load of X (straight from
+// global memory, double-buffered across row tiles) and one 16-byte LDS read of W -- the sum is
+// over the same k set, in a different (equally exact-per-product) order.
+//
+// Weight gradient (wgrad_f32_kernel): both operands are pixel-major ([M][N], [M][K]), which is
+// exactly the k-major operand layout of the f32 MFMA -- a 32-pixel stage of dY / X is staged
+// into LDS as-is ([pixel][column], conflict-free 128-byte half-wave reads), no transposes.
+// Waves tile the output (WN x WK waves of 64 x 64 = 2 x 2 MFMA tiles) and, for narrow
+// outputs, also split the stage's 16 k-steps (SW waves on one tile, summed through LDS).
+// Split-K over pixels fills the chip; each split writes an fp32 slab, a reduce kernel adds
+// the slabs into dW.  Blocks are remapped XCD-aware (consecutive logical blocks -- tiles of
+// one split, which stream the same pixels -- share an XCD's L2).
+#include "common.h"
+#include "ops.h"
+
+#include <algorithm>
+
+namespace voda {
+
+namespace {
+
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+__device__ __forceinline__ f32x16 mfma32(float a, float b, f32x16 c) {
+  return __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, c, 0, 0, 0);
+}
+
+// ------------------------------------------------------------------------------------------
+// forward GEMM + BN statistics
+// ------------------------------------------------------------------------------------------
+constexpr int kFThreads = 256;
+constexpr int kFRows = 128;  // rows per row tile (32 per wave)
+
+struct FArgs {
+  const float* x;  // [M][K]
+  const float* w;  // [N][K]
+  float* y;        // [M][N]
+  float* part;     // [2][G][N] (null: no statistics)
+  int64_t M;
+  int N, G;
+  int accumulate;  // Y += X W^T (statistics then describe X W^T alone)
+};
+
+template <int NT, int K, bool DBUF>
+__global__ __launch_bounds__(kFThreads, 2) void gemm_f32_stats_kernel(FArgs p) {
+  constexpr int PK = K + 4;     // LDS floats per W row
+  constexpr int NC = 32 * NT;   // columns per workgroup
+  constexpr int KQ = K / 8;     // 8-wide k chunks
+  __shared__ __attribute__((aligned(16))) float wl[NC * PK];
+  __shared__ float red[4][2][NC];
+
+  const int tid = threadIdx.x;
+  const int wave = tid >> 6, lane = tid & 63;
+  const int lc = lane & 31, lh = lane >> 5;
+  const int nt = blockIdx.x / p.G, g = blockIdx.x - nt * p.G;
+  const int n0 = nt * NC;
+
+  for (int i = tid; i < NC * (K / 4); i += kFThreads) {
+    const int r = i / (K / 4), c = i - r * (K / 4);
+    *reinterpret_cast<float4*>(wl + r * PK + 4 * c) = *reinterpret_cast<const float4*>(p.w + int64_t(n0 + r) * K + 4 * c);
+  }
+  __syncthreads();
+
+  f32x16 acc[NT];
+  float s1[NT], s2[NT];
+#pragma unroll
+  for (int t = 0; t < NT; ++t) { s1[t] = 0.f; s2[t] = 0.f; }
+
+  const int64_t ntiles = (p.M + kFRows - 1) / kFRows;
+  float4 cur[KQ], nxt[DBUF ? KQ : 1];
+  auto src_of = [&](int64_t mt) {
+    int64_t row = mt * kFRows + 32 * wave + lc;
+    row = row < p.M ? row : p.M - 1;  // rows past M: any valid row, masked in the epilogue
+    return p.x + row * K + 4 * lh;
+  };
+  auto load_a = [&](int64_t mt, float4 (&dst)[KQ]) {
+    const float* src = src_of(mt);
+#pragma unroll
+    for (int q = 0; q < KQ; ++q) dst[q] = *reinterpret_cast<const float4*>(src + 8 * q);
+  };
+  int64_t mt = g;
+  if (mt < ntiles) load_a(mt, cur);
+  for (; mt < ntiles; mt += p.G) {
+    const bool more = mt + p.G < ntiles;
+    if constexpr (DBUF) {
+      if (more) {
+        const float* src = src_of(mt + p.G);
+#pragma unroll
+        for (int q = 0; q < KQ; ++q) nxt[q] = *reinterpret_cast<const float4*>(src + 8 * q);
+      }
+    }
+#pragma unroll
+    for (int t = 0; t < NT; ++t) acc[t] = f32x16{};
+#pragma unroll
+    for (int q = 0; q < KQ; ++q) {
+      const float4 a = cur[q];
+#pragma unroll
+      for (int t = 0; t < NT; ++t) {
+        const float4 b = *reinterpret_cast<const float4*>(wl + (32 * t + lc) * PK + 8 * q + 4 * lh);
+        acc[t] = mfma32(a.x, b.x, acc[t]);
+        acc[t] = mfma32(a.y, b.y, acc[t]);
+        acc[t] = mfma32(a.z, b.z, acc[t]);
+        acc[t] = mfma32(a.w, b.w, acc[t]);
+      }
+      // keep the scheduler from hoisting every chunk's W reads ahead of the MFMAs (register
+      // pressure -> scratch spills at K >= 128)
+      if ((q & 1) == 1) __builtin_amdgcn_sched_barrier(0);
+    }
+    if constexpr (!DBUF) {
+      if (more) load_a(mt + p.G, cur);  // in flight during the epilogue
+    }
+    // ---- epilogue: statistics (rows < M) and the fp32 output (128-byte half-wave rows)
+    const int64_t rbase = mt * kFRows + 32 * wave;
+    const bool full = rbase + 32 <= p.M;
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+      float* ycol = p.y + n0 + 32 * t + lc;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int64_t row = rbase + (r & 3) + 8 * (r >> 2) + 4 * lh;
+        const bool keep = full || row < p.M;
+        const float v = acc[t][r];
+        if (keep) {
+          float* dst = ycol + row * p.N;
+          *dst = p.accumulate ? *dst + v : v;
+          s1[t] += v;
+          s2[t] = fmaf(v, v, s2[t]);
+        }
+      }
+    }
+    if constexpr (DBUF) {
+      if (more) {
+#pragma unroll
+        for (int q = 0; q < KQ; ++q) cur[q] = nxt[q];
+      }
+    }
+  }
+
+  if (p.part == nullptr) return;
+#pragma unroll
+  for (int t = 0; t < NT; ++t) {
+    s1[t] += __shfl_xor(s1[t], 32);
+    s2[t] += __shfl_xor(s2[t], 32);
+    if (lh == 0) {
+      red[wave][0][32 * t + lc] = s1[t];
+      red[wave][1][32 * t + lc] = s2[t];
+    }
+  }
+  __syncthreads();
+  for (int c = tid; c < NC; c += kFThreads) {
+    const float a1 = (red[0][0][c] + red[1][0][c]) + (red[2][0][c] + red[3][0][c]);
+    const float a2 = (red[0][1][c] + red[1][1][c]) + (red[2][1][c] + red[3][1][c]);
+    p.part[int64_t(g) * p.N + n0 + c] = a1;
+    p.part[int64_t(p.G) * p.N + int64_t(g) * p.N + n0 + c] = a2;
+  }
+}
+
+int f32_cus() {
+  static int g = [] {
+    int dev = 0, cus = 256;
+    if (hipGetDevice(&dev) == hipSuccess) {
+      hipDeviceProp_t pr;
+      if (hipGetDeviceProperties(&pr, dev) == hipSuccess && pr.multiProcessorCount > 0) cus = pr.multiProcessorCount;
+    }
+    return cus;
+  }();
+  return g;
+}
+
+// columns per workgroup: the W tile stays <= ~68 KB of LDS (two workgroups per CU)
+int gf_nt(int K) { return K == 64 ? 8 : (K == 128 ? 4 : 2); }
+
+// ------------------------------------------------------------------------------------------
+// weight gradient, split-K
+// ------------------------------------------------------------------------------------------
+constexpr int kWThreads = 256;
+constexpr int kWStage = 32;  // pixels per LDS stage (16 MFMA k-steps)
+
+struct WArgs {
+  const float* dy;  // [M][N]
+  const float* x;   // [M][K]
+  float* dw;        // [N][K] (S == 1)
+  float* ws;        // [S][N][K] slabs (S > 1)
+  int M, N, K, S, m_split, tiles_n, tiles_k, accumulate, remap;
+};
+
+template <int WN, int WK, int SW>
+__global__ __launch_bounds__(kWThreads, 2) void wgrad_f32_kernel(WArgs p) {
+  static_assert(WN * WK * SW == 4, "four waves");
+  constexpr int TN = 64 * WN, TK = 64 * WK;
+  constexpr int LD = TN + TK;                      // floats per staged pixel row: [dY cols | X cols]
+  constexpr int STAGE = kWStage * LD;               // floats per stage
+  __shared__ __attribute__((aligned(16))) float lds[2 * STAGE];
+
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int lc = lane & 31, lh = lane >> 5;
+  const int sw = wave % SW, wnk = wave / SW;
+  const int wn = wnk / WK, wk = wnk - (wnk / WK) * WK;
+
+  // logical block: split-major (the tiles of one split -- same pixels -- are neighbours);
+  // XCD-aware: hardware dispatches block b to XCD b % 8, so give XCD x a contiguous range
+  int bid = blockIdx.x;
+  if (p.remap) {
+    const int per = gridDim.x / 8;
+    bid = (bid % 8) * per + bid / 8;
+  }
+  const int tiles = p.tiles_n * p.tiles_k;
+  const int split = bid / tiles, tile = bid - split * tiles;
+  const int n0 = (tile / p.tiles_k) * TN, k0 = (tile % p.tiles_k) * TK;
+  const int m_beg = split * p.m_split;
+  const int m_end = min(p.M, m_beg + p.m_split);
+
+  // staging: a stage is the [pixel][dY cols | X cols] image; thread t loads float4s of the dY
+  // part (TN / 4 per pixel row) and of the X part (TK / 4 per row).  Branch-free: rows past
+  // the split / columns past N, K read a clamped valid address and are zeroed by a mask, so
+  // the loads of a stage are all in flight together (no per-load waits).
+  constexpr int NA = kWStage * TN / 4 / kWThreads, NB = kWStage * TK / 4 / kWThreads;
+  static_assert(NA * kWThreads * 4 == kWStage * TN && NB * kWThreads * 4 == kWStage * TK, "even split");
+  float4 ga[NA], gb[NB];
+  bool oka[NA], okb[NB];  // masks applied at the LDS store: no wait on the loads before the MFMAs
+  auto keep4 = [](float4 v, bool k) {
+    const uint32_t m = k ? 0xffffffffu : 0u;
+    return make_float4(__uint_as_float(__float_as_uint(v.x) & m), __uint_as_float(__float_as_uint(v.y) & m),
+                       __uint_as_float(__float_as_uint(v.z) & m), __uint_as_float(__float_as_uint(v.w) & m));
+  };
+  auto gload = [&](int m0) {
+#pragma unroll
+    for (int i = 0; i < NA; ++i) {
+      const int u = tid + i * kWThreads;
+      const int r = u / (TN / 4), col = n0 + 4 * (u - r * (TN / 4));
+      const int m = m0 + r;
+      oka[i] = m < m_end && col < p.N;
+      ga[i] = *reinterpret_cast<const float4*>(p.dy + int64_t(oka[i] ? m : m_beg) * p.N + (oka[i] ? col : 0));
+    }
+#pragma unroll
+    for (int i = 0; i < NB; ++i) {
+      const int u = tid + i * kWThreads;
+      const int r = u / (TK / 4), col = k0 + 4 * (u - r * (TK / 4));
+      const int m = m0 + r;
+      okb[i] = m < m_end && col < p.K;
+      gb[i] = *reinterpret_cast<const float4*>(p.x + int64_t(okb[i] ? m : m_beg) * p.K + (okb[i] ? col : 0));
+    }
+  };
+  auto sstore = [&](float* buf) {
+#pragma unroll
+    for (int i = 0; i < NA; ++i) {
+      const int u = tid + i * kWThreads;
+      const int r = u / (TN / 4), c4 = u - r * (TN / 4);
+      *reinterpret_cast<float4*>(buf + r * LD + 4 * c4) = keep4(ga[i], oka[i]);
+    }
+#pragma unroll
+    for (int i = 0; i < NB; ++i) {
+      const int u = tid + i * kWThreads;
+      const int r = u / (TK / 4), c4 = u - r * (TK / 4);
+      *reinterpret_cast<float4*>(buf + r * LD + TN + 4 * c4) = keep4(gb[i], okb[i]);
+    }
+  };
+
+  f32x16 c00{}, c01{}, c10{}, c11{};
+  const int an = wn * 64 + lc, bk = TN + wk * 64 + lc;
+  constexpr int KS = 16 / SW;  // k-steps of a stage per wave
+  int m0 = m_beg;
+  int buf = 0;
+  if (m0 < m_end) {
+    gload(m0);
+    sstore(lds);
+  }
+  __syncthreads();
+  for (; m0 < m_end; m0 += kWStage) {
+    const bool more = m0 + kWStage < m_end;
+    if (more) gload(m0 + kWStage);
+    __builtin_amdgcn_sched_barrier(0);
+    const float* st = lds + buf * STAGE + (2 * sw * KS + lh) * LD;
+    // LDS operands one k-step ahead of the MFMAs (register double buffer): the reads of step
+    // j + 1 are in flight while the four MFMAs of step j issue
+    float a0 = st[an], a1 = st[an + 32], b0 = st[bk], b1 = st[bk + 32];
+#pragma unroll
+    for (int j = 0; j < KS; ++j) {
+      float na0 = 0.f, na1 = 0.f, nb0 = 0.f, nb1 = 0.f;
+      if (j + 1 < KS) {
+        const float* row = st + 2 * (j + 1) * LD;
+        na0 = row[an]; na1 = row[an + 32]; nb0 = row[bk]; nb1 = row[bk + 32];
+      }
+      __builtin_amdgcn_sched_barrier(0);  // keep the next step's reads ahead of these MFMAs
+      c00 = mfma32(a0, b0, c00);
+      c01 = mfma32(a0, b1, c01);
+      c10 = mfma32(a1, b0, c10);
+      c11 = mfma32(a1, b1, c11);
+      __builtin_amdgcn_sched_barrier(0);
+      a0 = na0; a1 = na1; b0 = nb0; b1 = nb1;
+    }
+    // the next stage's global loads stay in flight during the MFMAs: their LDS stores (and
+    // the vmcnt waits they need) must not be hoisted above them
+    __builtin_amdgcn_sched_barrier(0);
+    if (more) sstore(lds + (buf ^ 1) * STAGE);
+    __syncthreads();
+    buf ^= 1;
+  }
+
+  // ---- waves sharing a tile (SW > 1): sum through LDS (the stage buffers are free now)
+  if constexpr (SW > 1) {
+    // tree: in each round the upper half of the remaining waves store their accumulators
+    // ([half][WN*WK][64 acc][64 lanes], lane-contiguous: conflict-free) and the lower half add
+    static_assert((SW / 2) * WN * WK * 64 * 64 <= 2 * STAGE, "reduction image must fit the stage buffers");
+    float* sum = lds;
+#pragma unroll
+    for (int half = SW / 2; half >= 1; half /= 2) {
+      if (sw >= half && sw < 2 * half) {
+        float* d = sum + ((sw - half) * (WN * WK) + wnk) * 64 * 64 + lane;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          d[64 * r] = c00[r]; d[64 * (16 + r)] = c01[r]; d[64 * (32 + r)] = c10[r]; d[64 * (48 + r)] = c11[r];
+        }
+      }
+      __syncthreads();
+      if (sw < half) {
+        const float* d = sum + (sw * (WN * WK) + wnk) * 64 * 64 + lane;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          c00[r] += d[64 * r]; c01[r] += d[64 * (16 + r)]; c10[r] += d[64 * (32 + r)]; c11[r] += d[64 * (48 + r)];
+        }
+      }
+      __syncthreads();
+    }
+    if (sw > 0) return;
+  }
+
+  // ---- epilogue: rows = output channels n (MFMA rows), cols = input channels k (lanes)
+  auto store = [&](const f32x16& acc, int rbase, int cbase) {
+    const int col = cbase + lc;
+    if (col >= p.K) return;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int row = rbase + (r & 3) + 8 * (r >> 2) + 4 * lh;
+      if (row < p.N) {
+        if (p.S == 1) {
+          float* o = p.dw + int64_t(row) * p.K + col;
+          *o = p.accumulate ? *o + acc[r] : acc[r];
+        } else {
+          p.ws[(int64_t(split) * p.N + row) * p.K + col] = acc[r];
+        }
+      }
+    }
+  };
+  const int rb = n0 + wn * 64, cb = k0 + wk * 64;
+  store(c00, rb, cb);
+  store(c01, rb, cb + 32);
+  store(c10, rb + 32, cb);
+  store(c11, rb + 32, cb + 32);
+}
+
+__global__ __launch_bounds__(256) void wgrad_f32_reduce_kernel(const float* __restrict__ ws, int S, int64_t NK4,
+                                                               float* __restrict__ dw, int accumulate) {
+  for (int64_t i = blockIdx.x * int64_t(256) + threadIdx.x; i < NK4; i += int64_t(gridDim.x) * 256) {
+    float4 a = accumulate ? reinterpret_cast<const float4*>(dw)[i] : make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int s = 0; s < S; ++s) {
+      const float4 v = reinterpret_cast<const float4*>(ws)[int64_t(s) * NK4 + i];
+      a.x += v.x; a.y += v.y; a.z += v.z; a.w += v.w;
+    }
+    reinterpret_cast<float4*>(dw)[i] = a;
+  }
+}
+
+struct WPlan {
+  int wn, wk, sw, tiles_n, tiles_k, S, m_split, grid;
+};
+
+WPlan wgrad_f32_plan(int M, int N, int K, int splits) {
+  WPlan pl;
+  // wave layout: the widest output tile that the channel counts fill
+  if (N >= 128 && K >= 128) { pl.wn = 2; pl.wk = 2; pl.sw = 1; }
+  else if (N < 128 && K >= 256) { pl.wn = 1; pl.wk = 4; pl.sw = 1; }
+  else if (K < 128 && N >= 256) { pl.wn = 4; pl.wk = 1; pl.sw = 1; }
+  else if (N < 128 && K >= 128) { pl.wn = 1; pl.wk = 2; pl.sw = 2; }
+  else if (K < 128 && N >= 128) { pl.wn = 2; pl.wk = 1; pl.sw = 2; }
+  else { pl.wn = 1; pl.wk = 1; pl.sw = 4; }
+  pl.tiles_n = (N + 64 * pl.wn - 1) / (64 * pl.wn);
+  pl.tiles_k = (K + 64 * pl.wk - 1) / (64 * pl.wk);
+  const int tiles = pl.tiles_n * pl.tiles_k;
+  int S = splits > 0 ? splits : std::max(1, (4 * f32_cus() + tiles - 1) / tiles);  // ~4 blocks per CU
+  const int per = (M + S - 1) / S;
+  pl.m_split = std::max(kWStage, (per + kWStage - 1) / kWStage * kWStage);
+  pl.S = (M + pl.m_split - 1) / pl.m_split;  // no empty splits
+  pl.grid = tiles * pl.S;
+  return pl;
+}
+
+}  // namespace
+
+bool gemm_f32_stats_supported(int64_t M, int N, int K) {
+  return M > 0 && (K == 64 || K == 128 || K == 256) && N % (32 * gf_nt(K)) == 0;
+}
+
+int gemm_f32_stats_groups(int64_t M, int N, int K) {
+  if (!gemm_f32_stats_supported(M, N, K)) return 0;
+  const int ncol = N / (32 * gf_nt(K));
+  const int64_t ntiles = (M + kFRows - 1) / kFRows;
+  return int(std::max<int64_t>(1, std::min<int64_t>(ntiles, (2 * f32_cus() + ncol - 1) / ncol)));
+}
+
+void gemm_f32_stats(uintptr_t x, uintptr_t w, uintptr_t y, uintptr_t part, int64_t M, int N, int K, int G,
+                    uintptr_t stream, bool accumulate) {
+  VODA_CHECK(gemm_f32_stats_supported(M, N, K), "gemm_f32_stats: K must be 64, 128 or 256 and N a multiple of the tile");
+  VODA_CHECK(G == gemm_f32_stats_groups(M, N, K), "gemm_f32_stats: group count mismatch");
+  VODA_CHECK(x % 16 == 0 && w % 16 == 0 && y % 4 == 0 && part % 4 == 0, "gemm_f32_stats: misaligned operands");
+  const int nt = gf_nt(K);
+  const int ncol = N / (32 * nt);
+  FArgs a{reinterpret_cast<const float*>(x), reinterpret_cast<const float*>(w), reinterpret_cast<float*>(y),
+          reinterpret_cast<float*>(part), M, N, G, accumulate ? 1 : 0};
+  hipStream_t s = as_stream(stream);
+  if (K == 64)
+    hipLaunchKernelGGL((gemm_f32_stats_kernel<8, 64, true>), dim3(ncol * G), dim3(kFThreads), 0, s, a);
+  else if (K == 128)
+    hipLaunchKernelGGL((gemm_f32_stats_kernel<4, 128, false>), dim3(ncol * G), dim3(kFThreads), 0, s, a);
+  else
+    hipLaunchKernelGGL((gemm_f32_stats_kernel<2, 256, false>), dim3(ncol * G), dim3(kFThreads), 0, s, a);
+  check_launch();
+}
+
+int64_t wgrad_f32_workspace_floats(int M, int N, int K, int splits) {
+  const WPlan pl = wgrad_f32_plan(M, N, K, splits);
+  return pl.S > 1 ? int64_t(pl.S) * N * K : 0;
+}
+
+std::vector<int> wgrad_f32_config(int M, int N, int K, int splits) {
+  const WPlan pl = wgrad_f32_plan(M, N, K, splits);
+  return {pl.wn, pl.wk, pl.sw, pl.S, pl.m_split, pl.grid};
+}
+
+void wgrad_f32(uintptr_t dy, uintptr_t x, uintptr_t dw, int M, int N, int K, int splits, uintptr_t ws,
+               bool accumulate, uintptr_t stream) {
+  VODA_CHECK(M > 0 && N >= 32 && K >= 32 && N % 32 == 0 && K % 32 == 0, "wgrad_f32: N and K must be multiples of 32");
+  VODA_CHECK(dy % 16 == 0 && x % 16 == 0 && dw % 16 == 0, "wgrad_f32: operands must be 16-byte aligned");
+  const WPlan pl = wgrad_f32_plan(M, N, K, splits);
+  VODA_CHECK(pl.S == 1 || (ws != 0 && ws % 16 == 0), "wgrad_f32: split-K needs a 16-byte aligned workspace");
+  WArgs a{reinterpret_cast<const float*>(dy), reinterpret_cast<const float*>(x), reinterpret_cast<float*>(dw),
+          reinterpret_cast<float*>(ws), M, N, K, pl.S, pl.m_split, pl.tiles_n, pl.tiles_k, accumulate ? 1 : 0,
+          pl.grid % 8 == 0 ? 1 : 0};
+  hipStream_t s = as_stream(stream);
+  const dim3 g(unsigned(pl.grid)), b(kWThreads);
+  if (pl.wn == 2 && pl.wk == 2) hipLaunchKernelGGL((wgrad_f32_kernel<2, 2, 1>), g, b, 0, s, a);
+  else if (pl.wn == 1 && pl.wk == 4) hipLaunchKernelGGL((wgrad_f32_kernel<1, 4, 1>), g, b, 0, s, a);
+  else if (pl.wn == 4 && pl.wk == 1) hipLaunchKernelGGL((wgrad_f32_kernel<4, 1, 1>), g, b, 0, s, a);
+  else if (pl.wn == 1 && pl.wk == 2) hipLaunchKernelGGL((wgrad_f32_kernel<1, 2, 2>), g, b, 0, s, a);
+  else if (pl.wn == 2 && pl.wk == 1) hipLaunchKernelGGL((wgrad_f32_kernel<2, 1, 2>), g, b, 0, s, a);
+  else hipLaunchKernelGGL((wgrad_f32_kernel<1, 1, 4>), g, b, 0, s, a);
+  check_launch();
+  if (pl.S > 1) {
+    const int64_t nk4 = int64_t(N) * K / 4;
+    hipLaunchKernelGGL(wgrad_f32_reduce_kernel, dim3(stream_grid(nk4)), dim3(256), 0, s, a.ws, pl.S, nk4, a.dw,
+                       a.accumulate);
+    check_launch();
+  }
+}
+
+}  // namespace voda

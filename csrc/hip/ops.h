@@ -90,6 +90,17 @@ void bn_bwd(uintptr_t dy, uintptr_t mask, uintptr_t x, uintptr_t save_mean, uint
             uintptr_t dx, uintptr_t dres, uintptr_t dgamma, uintptr_t dbeta, uintptr_t workspace, int64_t M, int C,
             bool relu, bool accumulate, int dt, uintptr_t stream);
 
+// ---- fp32 1x1 conv GEMMs on the f32 MFMA: forward + BN statistics, split-K weight gradient
+// (conv1x1_f32.hip) ----
+bool gemm_f32_stats_supported(int64_t M, int N, int K);
+int gemm_f32_stats_groups(int64_t M, int N, int K);
+void gemm_f32_stats(uintptr_t x, uintptr_t w, uintptr_t y, uintptr_t part, int64_t M, int N, int K, int G,
+                    uintptr_t stream, bool accumulate);
+int64_t wgrad_f32_workspace_floats(int M, int N, int K, int splits);
+std::vector<int> wgrad_f32_config(int M, int N, int K, int splits);
+void wgrad_f32(uintptr_t dy, uintptr_t x, uintptr_t dw, int M, int N, int K, int splits, uintptr_t ws,
+               bool accumulate, uintptr_t stream);
+
 // ---- 1x1 conv forward GEMM with BN statistics in the epilogue (gemm_bnstats.hip) ----
 bool gemm_bnstats_supported(int64_t M, int N, int K);
 int gemm_bnstats_groups(int64_t M, int N, int K);

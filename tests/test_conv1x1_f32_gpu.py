@@ -1,0 +1,120 @@
+"""fp32 1x1-convolution GEMMs on the f32 MFMA (csrc/hip/conv1x1_f32.hip) against fp64 PyTorch
+references of the same ops: the forward GEMM with its BN statistics epilogue (and the
+accumulating form used for input gradients), the split-K weight gradient in every wave
+layout, and the Conv1x1 module's fp32 GEMM path end to end (VERDICT r3 Next #4)."""
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+
+def _h():
+    from vodascheduler_amd.ops import _native as N
+
+    return N.hip(), N
+
+
+def _rel(a, b):
+    a, b = a.detach().double(), b.detach().double()
+    return float((a - b).norm() / b.norm().clamp_min(1e-30))
+
+
+@pytest.mark.parametrize("M,N,K", [(1000, 256, 64), (4096, 512, 64), (777, 128, 128), (2048, 256, 128),
+                                   (300, 64, 256), (5000, 128, 256)])
+def test_gemm_f32_stats_matches_fp64(M, N, K):
+    h, Nn = _h()
+    torch.manual_seed(M + N + K)
+    x = torch.randn(M, K, device="cuda")
+    w = torch.randn(N, K, device="cuda") * 0.1
+    assert h.gemm_f32_stats_supported(M, N, K)
+    G = h.gemm_f32_stats_groups(M, N, K)
+    y = torch.full((M, N), float("nan"), device="cuda")
+    part = torch.empty(2 * G * N, device="cuda")
+    h.gemm_f32_stats(x.data_ptr(), w.data_ptr(), y.data_ptr(), part.data_ptr(), M, N, K, G, Nn.stream_of(x), False)
+    ref = x.double() @ w.double().t()
+    assert _rel(y, ref) < 2e-6
+    s1 = part[:G * N].view(G, N).double().sum(0)
+    s2 = part[G * N:].view(G, N).double().sum(0)
+    assert _rel(s1, ref.sum(0)) < 1e-5 and _rel(s2, (ref * ref).sum(0)) < 1e-5
+    # accumulate form (input gradient into a tensor that already holds the shortcut's)
+    y0 = torch.randn(M, N, device="cuda")
+    y2 = y0.clone()
+    h.gemm_f32_stats(x.data_ptr(), w.data_ptr(), y2.data_ptr(), 0, M, N, K, G, Nn.stream_of(x), True)
+    assert _rel(y2, y0.double() + ref) < 2e-6
+
+
+@pytest.mark.parametrize("M,N,K,splits", [(4096, 256, 256, 0), (1000, 64, 512, 0), (3000, 512, 64, 3),
+                                          (2500, 64, 128, 0), (2048, 128, 64, 0), (6000, 64, 64, 0),
+                                          (800, 256, 128, 1)])
+def test_wgrad_f32_matches_fp64(M, N, K, splits):
+    from vodascheduler_amd.ops import wgrad as W
+
+    h, _ = _h()
+    torch.manual_seed(M + N + K)
+    dy = torch.randn(M, N, device="cuda")
+    x = torch.randn(M, K, device="cuda")
+    gw = torch.randn(N, K, device="cuda")
+    g0 = gw.clone()
+    wn, wk, sw, S, m_split, grid = h.wgrad_f32_config(M, N, K, splits)
+    assert wn * wk * sw == 4 and S >= 1 and grid >= 1
+    W.wgrad_f32_accumulate_(dy, x, gw, accumulate=True, splits=splits)
+    ref = dy.double().t() @ x.double()
+    assert _rel(gw.double() - g0.double(), ref) < 5e-6
+    out = torch.full((N, K), float("nan"), device="cuda")
+    W.wgrad_f32_accumulate_(dy, x, out, accumulate=False, splits=splits)
+    assert _rel(out, ref) < 5e-6
+
+
+@pytest.mark.parametrize("cin,cout,stride,hw", [(64, 256, 1, 14), (256, 64, 1, 9), (128, 512, 1, 7),
+                                               (512, 1024, 2, 14), (1024, 256, 1, 7), (256, 512, 2, 8)])
+def test_conv1x1_fp32_gemm_path_matches_fp64(cin, cout, stride, hw):
+    """fp32 channels_last Conv1x1 on the GEMM path (own forward / input gradient where K is 64 /
+    128 / 256, hipBLASLt elsewhere, split-K weight gradient into the fp32 flat gradient)."""
+    from vodascheduler_amd.ops.conv1x1 import Conv1x1
+    from vodascheduler_amd.ops.optim import make_optimizer
+    from vodascheduler_amd.utils.flat import grad_of
+
+    torch.manual_seed(0)
+    m = Conv1x1(cin, cout, stride=stride).cuda().to(memory_format=torch.channels_last)
+    ref_w = m.weight.detach().double().clone().requires_grad_(True)
+    opt = make_optimizer("sgd", m.parameters(), lr=0.0)
+    x = torch.randn(4, cin, hw, hw, device="cuda").to(memory_format=torch.channels_last)
+    xg = x.detach().requires_grad_(True)
+    xr = x.double().detach().requires_grad_(True)
+    assert m._gemm_ok(xg)
+    opt.zero_grad()
+    y = m(xg)
+    assert "Conv1x1Fn" in type(y.grad_fn).__name__
+    y_ref = F.conv2d(xr, ref_w, stride=stride)
+    assert _rel(y, y_ref) < 1e-5
+    g = torch.randn_like(y_ref)
+    y.backward(g.float().to(memory_format=torch.channels_last))
+    y_ref.backward(g)
+    assert _rel(xg.grad, xr.grad) < 1e-5
+    assert grad_of(m.weight).dtype == torch.float32
+    assert _rel(grad_of(m.weight), ref_w.grad) < 1e-5
+    m(xg).backward(g.float().to(memory_format=torch.channels_last))   # accumulates (beta = 1)
+    assert _rel(grad_of(m.weight), 2 * ref_w.grad) < 1e-5
+
+
+def test_conv1x1_fp32_bn_statistics_attached():
+    """Training-mode fp32 Conv1x1 -> FusedBatchNorm2d: the statistics come from the GEMM
+    epilogue and the BN output equals conv2d + batch_norm in fp64."""
+    from vodascheduler_amd.ops.batchnorm import FusedBatchNorm2d
+    from vodascheduler_amd.ops.conv1x1 import Conv1x1
+
+    torch.manual_seed(1)
+    conv = Conv1x1(128, 512).cuda().to(memory_format=torch.channels_last)
+    bn = FusedBatchNorm2d(512, relu=True).cuda()
+    conv.train(), bn.train()
+    x = torch.randn(8, 128, 14, 14, device="cuda").to(memory_format=torch.channels_last).requires_grad_(True)
+    assert conv._stats_ok(x)
+    y = conv(x)
+    from vodascheduler_amd.ops.batchnorm import STATS_ATTR
+
+    assert getattr(y, STATS_ATTR, None) is not None   # statistics from the GEMM epilogue
+    z = bn(y)
+    yr = F.conv2d(x.double(), conv.weight.double())
+    zr = F.relu(F.batch_norm(yr, None, None, bn.weight.double(), bn.bias.double(), training=True, eps=bn.eps))
+    assert _rel(z, zr) < 1e-5

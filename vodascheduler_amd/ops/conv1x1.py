@@ -54,6 +54,16 @@ USE_MFMA_DGRAD = os.environ.get("VODA_MFMA_DGRAD", "1") != "0"
 # but the ResNet-50 step got SLOWER: 27.55 vs 27.28 ms (two interleaved pairs,
 # profiles/raw/r2_ab_conv1x1_hybrid.jsonl) -- so off by default
 USE_CONV1X1_HYBRID = os.environ.get("VODA_CONV1X1_HYBRID", "0") == "1"
+# fp32 (the reference's precision): 1x1 convolutions as GEMMs with the f32-MFMA kernels of
+# conv1x1_f32.hip -- forward with the BN statistics in the epilogue and input gradient for
+# K = 64 / 128 / 256, split-K weight gradient into the fp32 flat gradient, hipBLASLt for the
+# rest -- and the GradSink hand-offs of the bf16 path (no residual-gradient adds).
+# VODA_CONV1X1_F32=0: fp32 1x1 convolutions stay on MIOpen (A/B switch)
+USE_CONV1X1_F32 = os.environ.get("VODA_CONV1X1_F32", "1") != "0"
+USE_GEMM_F32 = os.environ.get("VODA_GEMM_F32", "1") != "0"
+# fp32 weight gradients: the split-K f32-MFMA kernel (1) or MIOpen's weight-only convolution
+# backward (0), folded into the flat gradient
+USE_WGRAD_F32 = os.environ.get("VODA_WGRAD_F32", "1") != "0"
 
 
 class GradSink:
@@ -139,11 +149,45 @@ class StatsHolder:
         self.stats = None
 
 
+def _f32_ok(*ts: torch.Tensor) -> bool:
+    return all(t.dtype == torch.float32 and t.is_contiguous() and t.data_ptr() % 16 == 0 for t in ts)
+
+
+def gemm_f32_2d(x2: torch.Tensor, w2: torch.Tensor, holder: StatsHolder | None = None,
+                out: torch.Tensor | None = None) -> torch.Tensor | None:
+    """fp32 Y = X W^T (+ ``out`` in place) on the f32-MFMA kernel (conv1x1_f32.hip), with the
+    BN statistics of Y's columns when a holder wants them; None when K is not 64 / 128 / 256
+    or the operands are not dense fp32 (the caller keeps its library path)."""
+    if not USE_GEMM_F32 or not x2.is_cuda or not _f32_ok(x2, w2):
+        return None
+    M, K = x2.shape
+    Nc = w2.shape[0]
+    h = N.hip()
+    if not h.gemm_f32_stats_supported(M, Nc, K):
+        return None
+    if out is not None and (out.dtype != torch.float32 or not out.is_contiguous() or tuple(out.shape) != (M, Nc)):
+        return None
+    G = h.gemm_f32_stats_groups(M, Nc, K)
+    y2 = out if out is not None else torch.empty(M, Nc, dtype=torch.float32, device=x2.device)
+    ws = None
+    if holder is not None:
+        ws = torch.empty(max(2 * G * Nc + 3 * Nc, h.bn_workspace_floats(M, Nc)), dtype=torch.float32,
+                         device=x2.device)
+    h.gemm_f32_stats(x2.data_ptr(), w2.data_ptr(), y2.data_ptr(), N.ptr(ws), M, Nc, K, G, N.stream_of(x2),
+                     out is not None)
+    if holder is not None:
+        holder.stats = (ws, G)
+    return y2
+
+
 def gemm_bnstats_2d(x2: torch.Tensor, w2: torch.Tensor, holder: StatsHolder | None) -> torch.Tensor | None:
-    """Y = X W^T on the MFMA kernel with the BN statistics of Y's columns (gemm_bnstats.hip)
-    when the shapes are covered and a holder wants them; else None."""
+    """Y = X W^T on the MFMA kernel with the BN statistics of Y's columns (gemm_bnstats.hip,
+    or conv1x1_f32.hip for fp32) when the shapes are covered and a holder wants them; else
+    None."""
     if holder is None or not USE_GEMM_BNSTATS or not x2.is_cuda:
         return None
+    if x2.dtype == torch.float32:
+        return gemm_f32_2d(x2, w2, holder)
     M, K = x2.shape
     Nc = w2.shape[0]
     if (x2.dtype != torch.bfloat16 or w2.dtype != torch.bfloat16 or not x2.is_contiguous() or not w2.is_contiguous()
@@ -165,6 +209,8 @@ def mfma_dgrad(dy2: torch.Tensor, w2: torch.Tensor, acc2: torch.Tensor | None = 
     shape is covered; None otherwise (the caller keeps its library path)."""
     if not USE_MFMA_DGRAD or not dy2.is_cuda:
         return None
+    if dy2.dtype == torch.float32:
+        return gemm_f32_2d(dy2, w2.t().contiguous(), None, acc2)
     M, K = dy2.shape
     Nc = w2.shape[1]
     if (dy2.dtype != torch.bfloat16 or w2.dtype != torch.bfloat16 or not dy2.is_contiguous()
@@ -215,6 +261,8 @@ class _Conv1x1Fn(torch.autograd.Function):
         x2 = _as_2d(xs)
         w2 = weight.reshape(cout, cin)
         y2 = gemm_bnstats_2d(x2, w2, holder)
+        if y2 is None and x2.dtype == torch.float32:
+            y2 = gemm_f32_2d(x2, w2)
         if y2 is None:
             y2 = x2 @ w2.t()
         ctx.save_for_backward(x2, weight)
@@ -269,7 +317,24 @@ class _Conv1x1Fn(torch.autograd.Function):
         dw = None
         if ctx.needs_input_grad[1]:
             g2 = flat_grad(weight).view(cout, cin) if _direct(weight) else None
-            if g2 is not None and W.supported(dy2, x2, g2):
+            if dy2.dtype == torch.float32 and not USE_WGRAD_F32:
+                xs4 = x2.view(n, h, w, cin).permute(0, 3, 1, 2)
+                dy4 = dy2.view(n, h, w, cout).permute(0, 3, 1, 2)
+                dw4 = torch.ops.aten.convolution_backward(dy4, xs4, weight, None, [1, 1], [0, 0], [1, 1], False,
+                                                          [0, 0], 1, [False, True, False])[1]
+                if g2 is not None:
+                    g2.add_(dw4.view(cout, cin))
+                    _ready(weight)
+                else:
+                    dw = dw4
+            elif g2 is not None and W.supported_f32(dy2, x2, g2):
+                W.wgrad_f32_accumulate_(dy2, x2, g2)
+                _ready(weight)
+            elif g2 is None and W.supported_f32(dy2, x2, weight.view(cout, cin)):
+                dw2 = torch.empty(cout, cin, dtype=torch.float32, device=dy2.device)
+                W.wgrad_f32_accumulate_(dy2, x2, dw2, accumulate=False)
+                dw = dw2.view(cout, cin, 1, 1)
+            elif g2 is not None and W.supported(dy2, x2, g2):
                 W.wgrad_accumulate_(dy2, x2, g2)
                 _ready(weight)
             elif g2 is not None:
@@ -382,6 +447,11 @@ class Conv1x1(torch.nn.Conv2d):
         super().__init__(in_channels, out_channels, 1, stride=stride, bias=False, **kw)
 
     def _gemm_ok(self, x: torch.Tensor) -> bool:
+        if x.is_cuda and x.dtype == torch.float32:
+            return (USE_CONV1X1_F32 and x.dim() == 4 and self.weight.dtype == torch.float32 and self.groups == 1
+                    and self.padding == (0, 0) and self.dilation == (1, 1) and self.stride[0] == self.stride[1]
+                    and x.is_contiguous(memory_format=torch.channels_last)
+                    and self.in_channels % 32 == 0 and self.out_channels % 32 == 0)
         return (USE_CONV1X1_GEMM and x.is_cuda and x.dim() == 4 and x.dtype == torch.bfloat16
                 and self.weight.dtype == torch.bfloat16 and self.groups == 1 and self.padding == (0, 0)
                 and self.dilation == (1, 1) and self.stride[0] == self.stride[1]
@@ -391,6 +461,13 @@ class Conv1x1(torch.nn.Conv2d):
     def _stats_ok(self, x: torch.Tensor) -> bool:
         """The output feeds a training-mode BN and the statistics GEMM covers the layer
         (K = 64 / 128 / 256 input channels, channels_last bf16)."""
+        if (USE_GEMM_F32 and USE_GEMM_BNSTATS and self.training and torch.is_grad_enabled() and x.is_cuda
+                and x.dim() == 4 and x.dtype == torch.float32 and self.weight.dtype == torch.float32
+                and self.in_channels in (64, 128, 256) and self.groups == 1 and self.padding == (0, 0)
+                and self.dilation == (1, 1) and x.is_contiguous(memory_format=torch.channels_last)):
+            s = self.stride[0]
+            m = x.shape[0] * ((x.shape[2] + s - 1) // s) * ((x.shape[3] + s - 1) // s)
+            return bool(N.hip().gemm_f32_stats_supported(m, self.out_channels, self.in_channels))
         if not (USE_GEMM_BNSTATS and self.training and torch.is_grad_enabled() and x.is_cuda and x.dim() == 4
                 and x.dtype == torch.bfloat16 and self.weight.dtype == torch.bfloat16
                 and self.in_channels in (64, 128, 256) and self.groups == 1 and self.padding == (0, 0)

@@ -143,3 +143,38 @@ def wgrad_accumulate_(dy2: torch.Tensor, x2: torch.Tensor, gw: torch.Tensor, gb:
     h.wgrad_gemm(dy2.data_ptr(), dy2.stride(0), x2.data_ptr(), x2.stride(0), gw.data_ptr(), gw.stride(0),
                  N.ptr(gb), M, N_, K, s, N.ptr(ws), bool(accumulate), _zero_rows(dy2.device).data_ptr(), v,
                  N.dtype_code(gw.dtype), N.stream_of(dy2))
+
+
+# ---------------------------------------------------------------------------------------
+# fp32 (the reference's precision): the split-K f32-MFMA kernel of csrc/hip/conv1x1_f32.hip
+# ---------------------------------------------------------------------------------------
+def supported_f32(dy2: torch.Tensor, x2: torch.Tensor, gw: torch.Tensor) -> bool:
+    """fp32 dY [M, N], X [M, K] and dW [N, K], all dense row-major, 16-byte aligned, N and K
+    multiples of 32 (every ResNet 1x1 convolution)."""
+    if not (dy2.is_cuda and x2.is_cuda and gw.is_cuda):
+        return False
+    if not (dy2.dtype == x2.dtype == gw.dtype == torch.float32) or dy2.dim() != 2 or x2.dim() != 2:
+        return False
+    M, N_ = dy2.shape
+    K = x2.shape[1]
+    if x2.shape[0] != M or tuple(gw.shape) != (N_, K) or M == 0 or N_ % 32 or K % 32:
+        return False
+    if not (dy2.is_contiguous() and x2.is_contiguous() and gw.is_contiguous()):
+        return False
+    return not (dy2.data_ptr() % 16 or x2.data_ptr() % 16 or gw.data_ptr() % 16)
+
+
+def wgrad_f32_accumulate_(dy2: torch.Tensor, x2: torch.Tensor, gw: torch.Tensor, accumulate: bool = True,
+                          splits: int = 0) -> None:
+    """``gw (+)= dy2^T x2`` in fp32 on the f32 MFMA (split-K over the M rows; ``splits`` 0 =
+    the kernel's choice: ~4 workgroups per CU)."""
+    if not supported_f32(dy2, x2, gw):
+        raise ValueError(f"wgrad_f32: unsupported operands dy {tuple(dy2.shape)} {dy2.dtype}, "
+                         f"x {tuple(x2.shape)} {x2.dtype}, dw {tuple(gw.shape)} {gw.dtype}")
+    M, N_ = dy2.shape
+    K = x2.shape[1]
+    h = N.hip()
+    nws = h.wgrad_f32_workspace_floats(M, N_, K, splits)
+    ws = torch.empty(nws, dtype=torch.float32, device=dy2.device) if nws else None
+    h.wgrad_f32(dy2.data_ptr(), x2.data_ptr(), gw.data_ptr(), M, N_, K, splits, N.ptr(ws), bool(accumulate),
+                N.stream_of(dy2))
