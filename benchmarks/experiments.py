@@ -6,7 +6,8 @@ curves come from the MI355X-calibrated ``sim.trace.PROFILES``.
   2. Elastic-Tiresias, 8 ResNet-50 ImageNet-shape jobs on 8 GPUs (vs Tiresias)
   3. AFS-L, mixed ResNet-50 + BERT-base trace on 8 GPUs (vs FIFO / ElasticFIFO)
   4. Munkres placement + worker migration under GPU drain (2 nodes x 8 GPUs)
-  5. FfDL Optimizer, 32-job Philly-style trace, 1/2/4/8 GPUs (all 8 policies side by side)
+  5. FfDL Optimizer, 32-job Philly-style trace, 1/2/4/8 GPUs (all 8 policies side by side),
+     and with autoscale: capacity ramping 1 -> 2 -> 4 -> 8 GPUs during the trace
 
 python benchmarks/experiments.py [--out profiles/r3_sim_experiments.md] [--bench-json SCALE.json]
 
@@ -75,6 +76,22 @@ def exp5():
     return out
 
 
+RAMP_T = 600.0  # seconds between capacity doublings of the autoscale ramp
+
+
+def exp_autoscale():
+    """BASELINE config 5's "autoscale 1->8": the config-5 trace while the cluster grows 1 -> 2 ->
+    4 -> 8 GPUs (one doubling every RAMP_T s -- an autoscaler adding nodes), next to a fixed
+    8-GPU cluster.  Node addition: reference scheduler.go:689-747, placement_manager.go:239-304."""
+    tr = philly_trace(32, seed=0, max_gpus=8)
+    ramp = [(0.0, {"node0": [0]}), (RAMP_T, {"node0": [0, 1]}), (2 * RAMP_T, {"node0": list(range(4))}),
+            (3 * RAMP_T, {"node0": list(range(8))})]
+    out = []
+    for a in ORDER:
+        out.append((a, simulate(tr, a, gpus=8, capacity=ramp), simulate(tr, a, gpus=8)))
+    return out
+
+
 INFO_ALGOS = ["SRJF", "ElasticSRJF", "ElasticTiresias", "FfDLOptimizer", "AFS-L"]
 
 
@@ -95,7 +112,7 @@ def exp_info():
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--out", default="profiles/r3_sim_experiments.md")
+    ap.add_argument("--out", default="profiles/r4_sim_experiments.md")
     ap.add_argument("--bench-json", default=None,
                     help="bench.py --out / driver SCALE json with allreduce_busbw_gbs: measured busbw")
     a = ap.parse_args()
@@ -104,7 +121,7 @@ def main():
         print("measured (busbw GB/s by world, step ms by model/world):", load_bench_json(a.bench_json))
     bw = (f"MEASURED per world ({', '.join(f'{k}: {intra_node_busbw(k):.0f}' for k in (2, 4, 8))} GB/s)"
           if busbw_source() == "measured" else f"ASSUMED ({ASSUMED_BUSBW_GBS:.0f} GB/s intra-node)")
-    lines = ["# BASELINE.json configs in the discrete-event simulator (round 3)", "",
+    lines = ["# BASELINE.json configs in the discrete-event simulator (round 4)", "",
              "Real training service / scheduler / allocator / placement code driven in virtual time "
              "(`benchmarks/experiments.py`). Job speed model (`vodascheduler_amd/common/workload.py`): single-GPU "
              "step times MEASURED on MI355X (bf16 compute, fp32 gradients; "
@@ -133,6 +150,17 @@ def main():
     lines += ["", "## Config 5: 32-job Philly-style trace, all 8 policies, 1/2/4/8 GPUs", "", HEADER]
     res5 = exp5()
     lines += [row(r) for r in res5]
+    lines += ["", f"## Config 5 with autoscale: capacity 1 -> 2 -> 4 -> 8 GPUs (doubling every {RAMP_T:.0f} s)", "",
+              "The same 32-job trace (requests capped at 8) while GPUs ARRIVE: the scheduler learns of each "
+              "addition through a node event and re-plans at once (work-conserving); elastic jobs grow onto "
+              "the new GPUs, Munkres keeps running workers in place; a fixed 8-GPU cluster is the bound. "
+              "Utilization is measured against the GPUs present at each moment (a fixed 1-GPU cluster cannot "
+              "run this trace's non-elastic 8-GPU requests at all).", "",
+              "| policy | avg JCT ramp 1->8 (s) | avg JCT fixed 8 (s) | makespan ramp / fixed 8 (s) "
+              "| ramp utilization | ramp resizes | ramp migrations |", "|---|---:|---:|---|---:|---:|---:|"]
+    for pol, rr, r8 in exp_autoscale():
+        lines.append(f"| {pol} | {rr.avg_jct:.0f} | {r8.avg_jct:.0f} | {rr.makespan:.0f} / {r8.makespan:.0f} "
+                     f"| {100 * rr.utilization:.0f} % | {rr.resizes} | {rr.migrations} |")
     lines += ["", "## Info-source ablation (config 5 trace): avg JCT (s) of the info-driven policies", "",
               "round-2 = what round 2 ran: exact info for started jobs, the reference placeholder for unstarted "
               "ones (units mixed: started jobs look long next to '1 s/epoch' arrivals); placeholder = the "

@@ -18,6 +18,8 @@ PYBIND11_MODULE(_vodahip, m) {
 
   m.def("sgd_step", &sgd_step);
   m.def("adam_step", &adam_step);
+  m.def("adam_set_unroll", &adam_set_unroll);
+  m.def("adam_get_unroll", &adam_get_unroll);
   m.def("rmsprop_step", &rmsprop_step);
   m.def("cast_scale", &cast_scale);
   m.def("multi_tensor_copy", &multi_tensor_copy);

@@ -102,19 +102,25 @@ __global__ __launch_bounds__(kGThreads, 2) void gemm_bnstats_kernel(GArgs p) {
         acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(cur[ks], b, acc[t], 0, 0, 0);
       }
     }
-    // ---- epilogue: statistics (rows < M), bf16 through the staging tile, 16-byte stores
+    // ---- epilogue: statistics (rows < M), bf16 through the staging tile, 16-byte stores.
+    // The statistics are of the bf16-ROUNDED outputs -- the tensor BN then normalises (a BN
+    // statistics pass over the stored Y would see exactly these values), not of the fp32
+    // accumulators.  (Accumulating form: they describe the rounded X W^T alone.)
     const int64_t rbase = mt * kGRows + 32 * wave;
     const bool full = rbase + 32 <= p.M;
 #pragma unroll
     for (int t = 0; t < NT; ++t) {
       if (full) {
 #pragma unroll
-        for (int r = 0; r < 16; ++r) { s1[t] += acc[t][r]; s2[t] = fmaf(acc[t][r], acc[t][r], s2[t]); }
+        for (int r = 0; r < 16; ++r) {
+          const float v = bf2f(f2bf(acc[t][r]));
+          s1[t] += v; s2[t] = fmaf(v, v, s2[t]);
+        }
       } else {
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
           const float keep = rbase + (r & 3) + 8 * (r >> 2) + 4 * lh < p.M ? 1.f : 0.f;
-          const float v = acc[t][r] * keep;
+          const float v = bf2f(f2bf(acc[t][r])) * keep;
           s1[t] += v; s2[t] = fmaf(v, v, s2[t]);
         }
       }

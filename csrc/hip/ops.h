@@ -23,6 +23,10 @@ void sgd_step(uintptr_t p, uintptr_t g, int g_dtype, uintptr_t mom_buf, uintptr_
 void adam_step(uintptr_t p, uintptr_t g, int g_dtype, uintptr_t m, uintptr_t v, uintptr_t p_lp, int lp_dtype,
                int64_t n, float lr, float beta1, float beta2, float eps, float wd, bool adamw, int64_t step,
                float grad_scale, uintptr_t step_ptr, uintptr_t stream);
+// A/B of the Adam kernel's loads in flight (VODA_ADAM_U): 1 or 2 float4 groups per thread,
+// -1 = back to the environment's choice
+void adam_set_unroll(int u);
+int adam_get_unroll();
 void rmsprop_step(uintptr_t p, uintptr_t g, int g_dtype, uintptr_t sq, uintptr_t mom_buf, uintptr_t gavg,
                   uintptr_t p_lp, int lp_dtype, int64_t n, float lr, float alpha, float eps, float wd, float momentum,
                   bool centered, float grad_scale, uintptr_t stream);

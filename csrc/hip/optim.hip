@@ -163,12 +163,14 @@ __global__ __launch_bounds__(256) void adam_kernel(float* __restrict__ p, const 
   }
 }
 
+static int g_adam_unroll = -1;  // -1: VODA_ADAM_U (read once); 1 / 2 set by adam_set_unroll
+
 static int adam_unroll() {
-  static const int u = [] {
+  static const int env = [] {
     const char* e = std::getenv("VODA_ADAM_U");
     return e != nullptr && std::atoi(e) >= 2 ? 2 : 1;
   }();
-  return u;
+  return g_adam_unroll > 0 ? g_adam_unroll : env;
 }
 
 // ---------------------------------------------------------------------------------
@@ -294,6 +296,10 @@ void adam_step(uintptr_t p, uintptr_t g, int g_dtype, uintptr_t m, uintptr_t v, 
   });
   check_launch();
 }
+
+void adam_set_unroll(int u) { g_adam_unroll = u >= 2 ? 2 : (u == 1 ? 1 : -1); }
+
+int adam_get_unroll() { return adam_unroll(); }
 
 void rmsprop_step(uintptr_t p, uintptr_t g, int g_dtype, uintptr_t sq, uintptr_t mom_buf, uintptr_t gavg,
                   uintptr_t p_lp, int lp_dtype, int64_t n, float lr, float alpha, float eps, float wd,

@@ -28,6 +28,11 @@ def test_gemm_bnstats_vs_fp32(M, K, Nc):
     rd = ref.double()
     torch.testing.assert_close(part[0], rd.sum(0), rtol=1e-4, atol=1e-3 * M ** 0.5)
     torch.testing.assert_close(part[1], (rd * rd).sum(0), rtol=1e-4, atol=1e-3)
+    # the statistics are those of the STORED bf16 output (what BN normalises), up to fp32
+    # summation order -- not of the unrounded accumulators
+    yd = y.double()
+    torch.testing.assert_close(part[0], yd.sum(0), rtol=1e-5, atol=1e-5 * M ** 0.5)
+    torch.testing.assert_close(part[1], (yd * yd).sum(0), rtol=1e-5, atol=1e-5)
 
 
 def test_gemm_bnstats_shape_gate():

@@ -62,8 +62,11 @@ USE_CONV1X1_HYBRID = os.environ.get("VODA_CONV1X1_HYBRID", "0") == "1"
 USE_CONV1X1_F32 = os.environ.get("VODA_CONV1X1_F32", "1") != "0"
 USE_GEMM_F32 = os.environ.get("VODA_GEMM_F32", "1") != "0"
 # fp32 weight gradients: the split-K f32-MFMA kernel (1) or MIOpen's weight-only convolution
-# backward (0), folded into the flat gradient
-USE_WGRAD_F32 = os.environ.get("VODA_WGRAD_F32", "1") != "0"
+# backward (0, default), folded into the flat gradient.  MIOpen's igemm_wrw runs these at
+# 76-126 TF, the split-K kernel at 20-115 TF (benchmarks/bench_resnet_fp32_convs.py,
+# profiles/r4/resnet50_fp32_1x1_own_vs_miopen.jsonl); in the ResNet-50 fp32 step: 80.0 ms with
+# the kernel vs 75.4 ms with MIOpen's (profiles/r4/rocprof_resnet50_fp32_*.md)
+USE_WGRAD_F32 = os.environ.get("VODA_WGRAD_F32", "0") != "0"
 
 
 class GradSink:

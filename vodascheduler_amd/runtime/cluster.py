@@ -138,6 +138,7 @@ def run_trace(store, trace: list[TraceJob], worker_locs, algorithm: str = "Elast
         "start_latency_p50_s": q(lat["start"], 0.5), "start_latency_p95_s": q(lat["start"], 0.95),
         "resize_latency_p50_s": q(lat["resize"], 0.5), "resize_latency_p95_s": q(lat["resize"], 0.95),
         "reschedules": core.resched_count, "jct": jct, "forced_abort_epochs": backend.forced_epochs,
+        "forced_abort_log": backend.forced_log,
         "events": backend.events, "resize_latency": backend.resize_latency,
         "capacity_timeline": timeline if len(timeline) > 1 else None,
     }

@@ -40,6 +40,9 @@ from .rendezvous import JobRendezvous, connect_store
 log = logging.getLogger("vodascheduler_amd.elastic")
 
 
+HEARTBEAT_S = 1.0  # seconds between a member's liveness beats (hb/<worker> in the job's store space)
+
+
 class HostsUpdatedInterrupt(Exception):
     """Membership changed; raised on every member at the same commit."""
 
@@ -98,8 +101,15 @@ class ElasticContext:
             return
 
         def loop():
+            last_hb = 0.0
             while not self._stop.is_set():
                 try:
+                    now = time.time()
+                    if now - last_hb >= HEARTBEAT_S:
+                        # liveness for the backend: a member stuck in a collective keeps beating
+                        # (the GIL is released there), a dead process stops
+                        self._watch_rdzv.set(f"hb/{self.worker_id}", repr(now))
+                        last_hb = now
                     e = self._watch_rdzv.latest_epoch()
                     if e > self._latest_seen:
                         self._latest_seen = e

@@ -83,6 +83,7 @@ class PoolBackend(Backend):
         self.resize_latency: list[dict] = []
         self.events: list[dict] = []
         self.forced_epochs = 0
+        self.forced_log: list[dict] = []  # every forced abort epoch: job, epoch, wait, members without heartbeat
         # mailbox counters continue where an earlier backend on the same warm pool stopped
         # (several traces in a row on one pool: bench.py's control run)
         self._mail_n: dict[str, int] = {w: int(store.add(f"pool/{w}/n", 0)) for w in self.workers}
@@ -140,12 +141,20 @@ class PoolBackend(Backend):
         abort = False
         if live_m and not force and rdzv.get(f"e/{live_e}/synced") is None and rdzv.outcome() is None:
             t_req = self.pending[name][2]
-            if time.time() - t_req < self.settle_timeout:
+            waited = time.time() - t_req
+            if waited < self.settle_timeout:
                 return  # the monitor retries
-            log.warning("job %s: epoch %d not synced after %.0fs; publishing an abort epoch", name, live_e,
-                        self.settle_timeout)
+            # a slow but healthy epoch (a first MIOpen find, an fp32 find-db build, a graph
+            # capture) is left alone: abort only when a member is known to be gone -- its
+            # heartbeat stopped -- or after STUCK_FACTOR x settle_timeout in any case
+            stale = self._stale_members(rdzv, live_m)
+            if not stale and waited < self.STUCK_FACTOR * self.settle_timeout:
+                return
+            log.warning("job %s: epoch %d not synced after %.0fs (members without heartbeat: %s); "
+                        "publishing an abort epoch", name, live_e, waited, stale or "none, hard limit")
             abort = True
             self.forced_epochs += 1
+            self.forced_log.append({"job": name, "epoch": live_e, "waited_s": round(waited, 1), "stale": stale})
         new_members, kind, t, cfg = self.pending.pop(name)
         if new_members == live_m:
             return
@@ -159,6 +168,23 @@ class PoolBackend(Backend):
         for wid in new_members:
             if wid not in live_m:
                 self._mail(wid, {"job": name, "epoch": e, "cfg": cfg})
+
+    STUCK_FACTOR = 5.0    # abort a never-syncing epoch of live members after this x settle_timeout
+    HEARTBEAT_STALE_S = 10.0
+
+    def _stale_members(self, rdzv, members: list[str]) -> list[str]:
+        """Members whose liveness beat (runtime/elastic.py watcher) is missing or older than
+        HEARTBEAT_STALE_S."""
+        now = time.time()
+        out = []
+        for m in members:
+            v = rdzv.get(f"hb/{m}")
+            try:
+                if v is None or now - float(v) > self.HEARTBEAT_STALE_S:
+                    out.append(m)
+            except ValueError:
+                out.append(m)
+        return out
 
     def _mail(self, wid: str, msg: dict) -> None:
         n = self._mail_n.get(wid, 0) + 1
