@@ -439,6 +439,13 @@ def main():
         set_name(spec, "ctl-" + spec["metadata"]["name"])
         ctl_trace.append(type(tj)(tj.submit_time, spec))
 
+    # simulator prediction of the timed trace (outside the timed region): printed next to the
+    # actual wall, and the calibration of the control replay's prediction
+    pred: dict = {}
+    if rank == 0:
+        pred["main_s"] = predict_wall(trace, a.algorithm, world, a.rate_limit, ramp)
+        log(0, f"simulator prediction for the timed trace ({a.algorithm}): {pred['main_s']:.1f} s")
+
     # ---------------- timed region ----------------
     if world > 1:
         dist.barrier()
@@ -449,10 +456,7 @@ def main():
     ctl: dict = {}
     t_main = [0.0]
     sched = None
-    pred: dict = {}
     if rank == 0:
-        pred["main_s"] = predict_wall(trace, a.algorithm, world, a.rate_limit, ramp)
-        log(0, f"simulator prediction for the timed trace ({a.algorithm}): {pred['main_s']:.1f} s")
 
         def drive():
             try:

@@ -80,6 +80,44 @@ __device__ __forceinline__ void stage(const float* __restrict__ g, int64_t st, i
   }
 }
 
+// Register prefetch of one [kT][D] tile: the next tile's global loads are issued before the
+// current tile's MFMAs and written to LDS after them (the synchronous stage() above exposes
+// the global-load latency once per tile: 4 times per workgroup at T = 128).  Used when the
+// tile is at most 4 float4 per thread (D <= 64 with 4 waves).
+template <int D, int NT>
+struct TileRegs {
+  static constexpr int VPR = D / 4;
+  static constexpr int N = (kT * VPR + NT - 1) / NT;
+  static constexpr bool kOn = N <= 4;
+  float4 v[kOn ? N : 1];
+  __device__ __forceinline__ void load(const float* __restrict__ g, int64_t st, int t0, int T) {
+    if constexpr (kOn) {
+#pragma unroll
+      for (int j = 0; j < N; ++j) {
+        const int i = threadIdx.x + j * NT;
+        const int r = i / VPR, c = (i % VPR) * 4;
+        v[j] = (i < kT * VPR && t0 + r < T) ? *reinterpret_cast<const float4*>(g + int64_t(t0 + r) * st + c)
+                                            : make_float4(0.f, 0.f, 0.f, 0.f);
+      }
+    }
+  }
+  template <int RS>
+  __device__ __forceinline__ void store(float* lds) const {
+    if constexpr (kOn) {
+#pragma unroll
+      for (int j = 0; j < N; ++j) {
+        const int i = threadIdx.x + j * NT;
+        if (i < kT * VPR) {
+          const int r = i / VPR, c = (i % VPR) * 4;
+          float2* p = reinterpret_cast<float2*>(lds + r * RS + c);
+          p[0] = make_float2(v[j].x, v[j].y);
+          p[1] = make_float2(v[j].z, v[j].w);
+        }
+      }
+    }
+  }
+};
+
 // mask codes of one tile: 0 attend, 1 key padding (-1e9), 2 past Tk (-inf)
 __device__ __forceinline__ void stage_mask(const AttnArgsF& a, const uint8_t* mrow, int kt, uint8_t* ms) {
   const int t = threadIdx.x;
@@ -87,6 +125,13 @@ __device__ __forceinline__ void stage_mask(const AttnArgsF& a, const uint8_t* mr
     const int key = kt + t;
     ms[t] = key >= a.Tk ? 2 : ((mrow != nullptr && mrow[key] == 0) ? 1 : 0);
   }
+}
+
+__device__ __forceinline__ float mask_add_code(const AttnArgsF& a, uint32_t code, int key, int query) {
+  if (code == 2) return kNegInf;
+  if (code == 1) return kMaskNeg;
+  if (a.causal && key > query) return kMaskNeg;
+  return 0.f;
 }
 
 __device__ __forceinline__ float mask_add(const AttnArgsF& a, const uint8_t* ms, int kl, int key, int query) {
@@ -121,14 +166,51 @@ struct RowFrag {
 // [kT][RS], already offset by the lane half's 2h (k-step s reads d = 4 (s>>1) + 2h + (s&1))
 template <int D, int RS, bool REG>
 __device__ __forceinline__ void dot_hd(f32x16& acc, const float* lds_row, const RowFrag<D, REG>& fr) {
+  // LDS operand of step t + 1 read while the two MFMAs of step t issue (the scheduler would
+  // otherwise put a wait on each read right before its MFMAs)
+  float2 x = *reinterpret_cast<const float2*>(lds_row);
 #pragma unroll
   for (int t = 0; t < D / 4; ++t) {
-    const float2 x = *reinterpret_cast<const float2*>(lds_row + 4 * t);
+    float2 xn = x;
+    if (t + 1 < D / 4) xn = *reinterpret_cast<const float2*>(lds_row + 4 * (t + 1));
     const float2 y = fr.get(t);
+    __builtin_amdgcn_sched_barrier(0);
     acc = mfma(x.x, y.x, acc);
     acc = mfma(x.y, y.y, acc);
+    __builtin_amdgcn_sched_barrier(0);
+    x = xn;
   }
 }
+
+// A-operand column of a key / query reduction: the 16 LDS elements [crow(i, h)][col] this lane
+// feeds to MFMA step i, all read before the first of the 16 MFMAs
+__device__ __forceinline__ void col16(const float* lds, int RS, int col, int h, float (&v)[16]) {
+#pragma unroll
+  for (int i = 0; i < 16; ++i) v[i] = lds[crow(i, h) * RS + col];
+}
+
+// 32 per-row values of a tile (lse, delta) at rows crow(i, h): four float4 LDS reads
+__device__ __forceinline__ void rows16(const float* arr, int h, float (&v)[16]) {
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const float4 q = *reinterpret_cast<const float4*>(arr + 8 * j + 4 * h);
+    v[4 * j] = q.x; v[4 * j + 1] = q.y; v[4 * j + 2] = q.z; v[4 * j + 3] = q.w;
+  }
+}
+
+// mask codes of the tile's keys crow(i, h) (i = 0..15): the 32 code bytes are read once as
+// two broadcast 16-byte LDS loads instead of 16 dependent byte loads
+struct TileCodes {
+  uint32_t w[4];  // word j: codes of keys 8j + 4h .. 8j + 4h + 3
+  __device__ __forceinline__ void load(const uint8_t* ms, int h) {
+    const uint4 a = *reinterpret_cast<const uint4*>(ms), b = *reinterpret_cast<const uint4*>(ms + 16);
+    w[0] = h ? a.y : a.x;
+    w[1] = h ? a.w : a.z;
+    w[2] = h ? b.y : b.x;
+    w[3] = h ? b.w : b.z;
+  }
+  __device__ __forceinline__ uint32_t code(int i) const { return (w[i >> 2] >> (8 * (i & 3))) & 0xff; }
+};
 
 // store a transposed accumulator (lane = output row, regs = 16 columns) as float4s
 __device__ __forceinline__ void store_row(float* __restrict__ out, int64_t st, int row, int nrows, int col0,
@@ -148,7 +230,7 @@ __global__ __launch_bounds__(64 * W) void attn_f32_fwd(AttnArgsF a) {
   constexpr bool REG = D <= 128;
   __shared__ __attribute__((aligned(16))) float Ks[kT * RS];
   __shared__ __attribute__((aligned(16))) float Vs[kT * RS];
-  __shared__ uint8_t Ms[kT];
+  __shared__ __attribute__((aligned(16))) uint8_t Ms[kT];
   const int bh = blockIdx.y, b = bh / a.H, hh = bh % a.H;
   const float* kb = a.k + b * a.k_sb + hh * a.k_sh;
   const float* vb = a.v + b * a.v_sb + hh * a.v_sh;
@@ -161,19 +243,37 @@ __global__ __launch_bounds__(64 * W) void attn_f32_fwd(AttnArgsF a) {
 #pragma unroll
   for (int t = 0; t < DT; ++t) o[t] = zero16();
   float m = -1e30f, l = 0.f;
+  // no register prefetch of the next K / V tile here: measured slower on BERT-base (fwd 48.0 ->
+  // 51.2 us, dQ 75.9 -> 81.6 us per layer: the extra VGPRs cost a wave per SIMD); the dK/dV
+  // pass keeps it (109.3 -> 94.5 us)
+  TileRegs<D, 64 * W> kr, vr;
+  constexpr bool PF = false;
   for (int kt = 0; kt < a.Tk; kt += kT) {
     __syncthreads();
-    stage<D, RS>(kb, a.k_st, kt, a.Tk, Ks);
-    stage<D, RS>(vb, a.v_st, kt, a.Tk, Vs);
+    if constexpr (PF) {
+      kr.template store<RS>(Ks);
+      vr.template store<RS>(Vs);
+    } else {
+      stage<D, RS>(kb, a.k_st, kt, a.Tk, Ks);
+      stage<D, RS>(vb, a.v_st, kt, a.Tk, Vs);
+    }
     stage_mask(a, mrow, kt, Ms);
     __syncthreads();
+    if constexpr (PF) {
+      if (kt + kT < a.Tk) {  // the next tile's loads stay in flight during this tile's MFMAs
+        kr.load(kb, a.k_st, kt + kT, a.Tk);
+        vr.load(vb, a.v_st, kt + kT, a.Tk);
+      }
+    }
     f32x16 s = zero16();
     dot_hd<D, RS, REG>(s, Ks + r * RS + 2 * h, qf);  // S^T[key r][query]: lane = query
+    TileCodes tc;
+    tc.load(Ms, h);
     float tmax = -1e30f;
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
       const int kl = crow(i, h);
-      const float v = s[i] * a.scale + mask_add(a, Ms, kl, kt + kl, q);
+      const float v = s[i] * a.scale + mask_add_code(a, tc.code(i), kt + kl, q);
       s[i] = v;
       tmax = fmaxf(tmax, v);
     }
@@ -195,8 +295,11 @@ __global__ __launch_bounds__(64 * W) void attn_f32_fwd(AttnArgsF a) {
 #pragma unroll
       for (int i = 0; i < 16; ++i) o[t][i] *= alpha;
       // O^T[d][query] += V^T[d][key] P^T[key][query]: step i pairs key crow(i, h) (register i)
+      float vc[16];
+      col16(Vs, RS, 32 * t + r, h, vc);
+      __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-      for (int i = 0; i < 16; ++i) o[t] = mfma(Vs[crow(i, h) * RS + 32 * t + r], s[i], o[t]);
+      for (int i = 0; i < 16; ++i) o[t] = mfma(vc[i], s[i], o[t]);
     }
   }
   const float inv = 1.f / l;
@@ -213,7 +316,7 @@ __global__ __launch_bounds__(64 * W) void attn_f32_bwd_dq(AttnArgsF a) {
   constexpr bool REG = D <= 64;
   __shared__ __attribute__((aligned(16))) float Ks[kT * RS];
   __shared__ __attribute__((aligned(16))) float Vs[kT * RS];
-  __shared__ uint8_t Ms[kT];
+  __shared__ __attribute__((aligned(16))) uint8_t Ms[kT];
   const int bh = blockIdx.y, b = bh / a.H, hh = bh % a.H;
   const float* kb = a.k + b * a.k_sb + hh * a.k_sh;
   const float* vb = a.v + b * a.v_sb + hh * a.v_sh;
@@ -228,7 +331,9 @@ __global__ __launch_bounds__(64 * W) void attn_f32_bwd_dq(AttnArgsF a) {
   const float* orow = a.o + b * a.o_sb + hh * a.o_sh + int64_t(qc) * a.o_st + 2 * h;
   float dpart = 0.f;
   if (qv) {
-#pragma unroll 4
+    // fully unrolled: a runtime index into the register-resident dO fragment would move it
+    // to scratch memory (it did: 88-152 bytes per lane of spills in every dQ pass)
+#pragma unroll
     for (int t = 0; t < D / 4; ++t) {
       const float2 ov = *reinterpret_cast<const float2*>(orow + 4 * t);
       const float2 dv = df.get(t);
@@ -242,26 +347,48 @@ __global__ __launch_bounds__(64 * W) void attn_f32_bwd_dq(AttnArgsF a) {
   f32x16 dq[DT];
 #pragma unroll
   for (int t = 0; t < DT; ++t) dq[t] = zero16();
+  // no register prefetch of the next K / V tile here: measured slower on BERT-base (fwd 48.0 ->
+  // 51.2 us, dQ 75.9 -> 81.6 us per layer: the extra VGPRs cost a wave per SIMD); the dK/dV
+  // pass keeps it (109.3 -> 94.5 us)
+  TileRegs<D, 64 * W> kr, vr;
+  constexpr bool PF = false;
   for (int kt = 0; kt < a.Tk; kt += kT) {
     __syncthreads();
-    stage<D, RS>(kb, a.k_st, kt, a.Tk, Ks);
-    stage<D, RS>(vb, a.v_st, kt, a.Tk, Vs);
+    if constexpr (PF) {
+      kr.template store<RS>(Ks);
+      vr.template store<RS>(Vs);
+    } else {
+      stage<D, RS>(kb, a.k_st, kt, a.Tk, Ks);
+      stage<D, RS>(vb, a.v_st, kt, a.Tk, Vs);
+    }
     stage_mask(a, mrow, kt, Ms);
     __syncthreads();
+    if constexpr (PF) {
+      if (kt + kT < a.Tk) {
+        kr.load(kb, a.k_st, kt + kT, a.Tk);
+        vr.load(vb, a.v_st, kt + kT, a.Tk);
+      }
+    }
     f32x16 s = zero16(), dp = zero16();
     dot_hd<D, RS, REG>(s, Ks + r * RS + 2 * h, qf);   // S^T
     dot_hd<D, RS, REG>(dp, Vs + r * RS + 2 * h, df);  // dP^T = V dO^T
+    TileCodes tc;
+    tc.load(Ms, h);
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
       const int kl = crow(i, h);
-      const float p = qv ? __expf(s[i] * a.scale + mask_add(a, Ms, kl, kt + kl, q) - lse) : 0.f;
+      const float p = qv ? __expf(s[i] * a.scale + mask_add_code(a, tc.code(i), kt + kl, q) - lse) : 0.f;
       s[i] = p * (dp[i] - delta);  // dS^T
     }
     // dQ^T[d][query] += K^T[d][key] dS^T[key][query]
 #pragma unroll
-    for (int t = 0; t < DT; ++t)
+    for (int t = 0; t < DT; ++t) {
+      float kc[16];
+      col16(Ks, RS, 32 * t + r, h, kc);
+      __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-      for (int i = 0; i < 16; ++i) dq[t] = mfma(Ks[crow(i, h) * RS + 32 * t + r], s[i], dq[t]);
+      for (int i = 0; i < 16; ++i) dq[t] = mfma(kc[i], s[i], dq[t]);
+    }
   }
   float* base = a.out + b * a.out_sb + hh * a.out_sh;
 #pragma unroll
@@ -277,7 +404,8 @@ __global__ __launch_bounds__(64 * W) void attn_f32_bwd_dkv(AttnArgsF a) {
   constexpr bool DO_DV = MODE != 2, DO_DK = MODE != 1;
   __shared__ __attribute__((aligned(16))) float Qs[kT * RS];
   __shared__ __attribute__((aligned(16))) float Ds[kT * RS];
-  __shared__ float lse_s[kT], del_s[kT];
+  __shared__ __attribute__((aligned(16))) float lse_s[kT];
+  __shared__ __attribute__((aligned(16))) float del_s[kT];
   const int bh = blockIdx.y, b = bh / a.H, hh = bh % a.H;
   const float* qb = a.q + b * a.q_sb + hh * a.q_sh;
   const float* db = a.dout + b * a.do_sb + hh * a.do_sh;
@@ -295,37 +423,60 @@ __global__ __launch_bounds__(64 * W) void attn_f32_bwd_dkv(AttnArgsF a) {
   for (int t = 0; t < (DO_DK ? DT : 1); ++t) dk[t] = zero16();
 #pragma unroll
   for (int t = 0; t < (DO_DV ? DT : 1); ++t) dv[t] = zero16();
+  TileRegs<D, 64 * W> qr, dr;
+  constexpr bool PF = TileRegs<D, 64 * W>::kOn;
+  if constexpr (PF) {
+    qr.load(qb, a.q_st, 0, a.Tq);
+    dr.load(db, a.do_st, 0, a.Tq);
+  }
   for (int qt = 0; qt < a.Tq; qt += kT) {
     __syncthreads();
-    stage<D, RS>(qb, a.q_st, qt, a.Tq, Qs);
-    stage<D, RS>(db, a.do_st, qt, a.Tq, Ds);
+    if constexpr (PF) {
+      qr.template store<RS>(Qs);
+      dr.template store<RS>(Ds);
+    } else {
+      stage<D, RS>(qb, a.q_st, qt, a.Tq, Qs);
+      stage<D, RS>(db, a.do_st, qt, a.Tq, Ds);
+    }
     for (int i = threadIdx.x; i < kT; i += blockDim.x) {
       const bool ok = qt + i < a.Tq;
       lse_s[i] = ok ? a.lse[int64_t(bh) * a.Tq + qt + i] : __builtin_huge_valf();  // pad rows: P = 0
       del_s[i] = ok ? a.delta[int64_t(bh) * a.Tq + qt + i] : 0.f;
     }
     __syncthreads();
+    if constexpr (PF) {
+      if (qt + kT < a.Tq) {
+        qr.load(qb, a.q_st, qt + kT, a.Tq);
+        dr.load(db, a.do_st, qt + kT, a.Tq);
+      }
+    }
     f32x16 s = zero16(), dp = zero16();
     dot_hd<D, RS, REG>(s, Qs + r * RS + 2 * h, kf);               // S[query r][key]: lane = key
     if constexpr (DO_DK) dot_hd<D, RS, REG>(dp, Ds + r * RS + 2 * h, vf);  // dP = dO V^T
+    float ls[16], ds[16];
+    rows16(lse_s, h, ls);
+    if constexpr (DO_DK) rows16(del_s, h, ds);
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
       const int ql = crow(i, h);
       float add = 0.f;
       if (!kv) add = kNegInf;
       else if (kmasked || (a.causal && key > qt + ql)) add = kMaskNeg;
-      const float p = __expf(s[i] * a.scale + add - lse_s[ql]);
+      const float p = __expf(s[i] * a.scale + add - ls[i]);
       s[i] = p;
-      if constexpr (DO_DK) dp[i] = p * (dp[i] - del_s[ql]);  // dS
+      if constexpr (DO_DK) dp[i] = p * (dp[i] - ds[i]);  // dS
     }
     // dV^T[d][key] += dO^T[d][q] P[q][key];  dK^T[d][key] += Q^T[d][q] dS[q][key]
 #pragma unroll
     for (int t = 0; t < DT; ++t) {
+      float dc[16], qc[16];
+      if constexpr (DO_DV) col16(Ds, RS, 32 * t + r, h, dc);
+      if constexpr (DO_DK) col16(Qs, RS, 32 * t + r, h, qc);
+      __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
       for (int i = 0; i < 16; ++i) {
-        const int ql = crow(i, h);
-        if constexpr (DO_DV) dv[t] = mfma(Ds[ql * RS + 32 * t + r], s[i], dv[t]);
-        if constexpr (DO_DK) dk[t] = mfma(Qs[ql * RS + 32 * t + r], dp[i], dk[t]);
+        if constexpr (DO_DV) dv[t] = mfma(dc[i], s[i], dv[t]);
+        if constexpr (DO_DK) dk[t] = mfma(qc[i], dp[i], dk[t]);
       }
     }
   }

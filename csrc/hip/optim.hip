@@ -100,7 +100,10 @@ __device__ __forceinline__ void adam1(float& p, float g, float& m, float& v, con
 }
 
 // U float4 groups of every array in flight per thread (loads issued before the first store):
-// VODA_ADAM_U = 1 / 2 (adam_unroll below).
+// VODA_ADAM_U = 1 / 2 (adam_unroll below).  Measured on a 110 M-parameter AdamW step
+// (benchmarks/bench_adam.py): 708 / 690 us with a bf16 copy, 669 / 686 us without, i.e. equal
+// within noise at ~4.5-4.8 TB/s; non-temporal state stores did not help either (and changed
+// the compiler's FMA contraction, so they were not bitwise equal) and were dropped.
 template <typename GT, typename LP, int U>
 __global__ __launch_bounds__(256) void adam_kernel(float* __restrict__ p, const GT* __restrict__ g,
                                                    float* __restrict__ m, float* __restrict__ v,
@@ -172,6 +175,7 @@ static int adam_unroll() {
   }();
   return g_adam_unroll > 0 ? g_adam_unroll : env;
 }
+
 
 // ---------------------------------------------------------------------------------
 // RMSprop (+momentum, centered), torch.optim.RMSprop semantics.
