@@ -189,6 +189,10 @@ def prepare_model(w: "Workload", device: torch.device, amp: bool = True) -> torc
         # reference precision: true fp32 math in the library GEMMs / convolutions too
         torch.backends.cuda.matmul.allow_tf32 = False
         torch.backends.cudnn.allow_tf32 = False
+        # pre-tuned hipBLASLt solutions of the fp32 GEMMs (utils/tunable.py)
+        from ..utils.tunable import configure as _tunable
+
+        _tunable("fp32")
     return m
 
 
