@@ -499,10 +499,22 @@ void dispatch_d32(int D, F&& f) {
   else throw std::invalid_argument("attention (fp32): unsupported head dim");
 }
 
+// waves per workgroup (32 rows each): enough for the rows, at most VODA_ATTN_F32_MAXW (A/B
+// knob, read once; default 4)
+int f32_maxw() {
+  static const int v = [] {
+    const char* e = std::getenv("VODA_ATTN_F32_MAXW");
+    const int x = e ? std::atoi(e) : 4;
+    return x >= 4 ? 4 : (x >= 2 ? 2 : 1);
+  }();
+  return v;
+}
+
 template <typename F>
 void dispatch_w32(int rows, F&& f) {
-  if (rows <= 32) f(std::integral_constant<int, 1>{});
-  else if (rows <= 64) f(std::integral_constant<int, 2>{});
+  const int mw = f32_maxw();
+  if (rows <= 32 || mw == 1) f(std::integral_constant<int, 1>{});
+  else if (rows <= 64 || mw == 2) f(std::integral_constant<int, 2>{});
   else f(std::integral_constant<int, 4>{});
 }
 

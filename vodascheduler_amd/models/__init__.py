@@ -185,6 +185,9 @@ def prepare_model(w: "Workload", device: torch.device, amp: bool = True) -> torc
         torch.backends.cudnn.benchmark = True
     if amp and device.type == "cuda":
         cast_compute_weights_(m, torch.bfloat16)
+        from ..utils.tunable import configure as _tunable
+
+        _tunable("bf16")  # pre-tuned hipBLASLt solutions of the bf16 GEMMs, when shipped
     elif device.type == "cuda":
         # reference precision: true fp32 math in the library GEMMs / convolutions too
         torch.backends.cuda.matmul.allow_tf32 = False

@@ -25,8 +25,9 @@ def results_path(precision: str) -> str:
 
 
 def configure(precision: str = "fp32") -> bool:
-    """Enable TunableOp with the shipped results of ``precision`` (once per process).
-    Returns True when tuned solutions are in use."""
+    """Enable TunableOp with the shipped results of ``precision`` (once per process; the
+    results of several precisions can be loaded side by side -- entries are keyed by the
+    GEMM's dtype and shape).  Returns True when tuned solutions are in use."""
     if precision in _DONE:
         return _DONE[precision]
     ok = False
