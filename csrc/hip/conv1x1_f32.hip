@@ -123,9 +123,24 @@ __global__ __launch_bounds__(kFThreads, 2) void gemm_f32_stats_kernel(FArgs p) {
       // keep the scheduler from hoisting every chunk's W reads ahead of the MFMAs (register
       // pressure -> scratch spills at K >= 128)
       if ((q & 1) == 1) __builtin_amdgcn_sched_barrier(0);
+      if constexpr (!DBUF) {
+        // single buffer, pipelined by halves: once the first half of the k chunks has fed its
+        // MFMAs, those registers take the NEXT row tile's first half, so the loads are in
+        // flight during the second half's MFMAs (and the epilogue)
+        if (q == KQ / 2 - 1 && more) {
+          const float* src = src_of(mt + p.G);
+#pragma unroll
+          for (int qq = 0; qq < KQ / 2; ++qq) cur[qq] = *reinterpret_cast<const float4*>(src + 8 * qq);
+          __builtin_amdgcn_sched_barrier(0);
+        }
+      }
     }
     if constexpr (!DBUF) {
-      if (more) load_a(mt + p.G, cur);  // in flight during the epilogue
+      if (more) {  // the second half: in flight during the epilogue
+        const float* src = src_of(mt + p.G);
+#pragma unroll
+        for (int qq = KQ / 2; qq < KQ; ++qq) cur[qq] = *reinterpret_cast<const float4*>(src + 8 * qq);
+      }
     }
     // ---- epilogue: statistics (rows < M) and the fp32 output (128-byte half-wave rows)
     const int64_t rbase = mt * kFRows + 32 * wave;
