@@ -56,4 +56,4 @@ def status() -> dict:
 
     t = torch.cuda.tunable
     return {"enabled": bool(t.is_enabled()), "tuning": bool(t.tuning_is_enabled()),
-            "entries": sum(len(v) for v in t.get_results().values()) if t.is_enabled() else 0}
+            "entries": len(t.get_results()) if t.is_enabled() else 0}  # ((op, shape, solution, ms), ...)
