@@ -849,10 +849,16 @@ Grid bn_grid(int64_t M, int C, int64_t cap_blocks, int iters_per_block) {
 // TB/s with 1024 long-lived blocks each walking its own chunk; one block per CU sweeping
 // the tensor together brings the per-step stats + reduce + finalize time 4.64 -> 4.02 ms,
 // and the step 26.95 -> 26.23 ms.  Unroll level 2 and grids of 384-2048 blocks are slower.
+//   VODA_BN_BLOCKS_F32=n  the cap for fp32 tensors (default 512): with 32-byte rows per
+//                         thread one block per CU leaves the fp32 backward reduce at ~3.8
+//                         TB/s; two blocks per CU take the fp32 ResNet-50 step's reduce
+//                         passes 4.86 -> 3.52 ms (~5.2 TB/s), 1024 blocks 3.57 ms
+//                         (profiles/r4/bn_reduce_grid_fp32.md)
 struct BnTune {
   int deep;  // rows in flight: 0 -> 4 (stats) / 2 (backward reduce), 1 -> 8 / 4, 2 -> 16 / 8
   int blocks;
   int sweep;
+  int blocks_f32 = 512;   // reduction grid cap for fp32 tensors (VODA_BN_BLOCKS_F32)
   int apply_cap = 8192;   // apply-pass grid cap (VODA_BN_APPLY_CAP)
   int apply_iters = 4;    // row iterations per apply block (VODA_BN_APPLY_ITERS)
   int apply_u = 4;        // rows in flight in the apply passes: 4, 2, or 0 -> fwd 2 / bwd 1 (VODA_BN_APPLY_U)
@@ -862,6 +868,7 @@ BnTune& bn_tune() {
     BnTune v{1, 256, 1};
     if (const char* e = std::getenv("VODA_BN_UNROLL")) v.deep = std::max(0, std::min(2, std::atoi(e)));
     if (const char* e = std::getenv("VODA_BN_BLOCKS")) v.blocks = std::max(64, std::min(8192, std::atoi(e)));
+    if (const char* e = std::getenv("VODA_BN_BLOCKS_F32")) v.blocks_f32 = std::max(64, std::min(8192, std::atoi(e)));
     if (const char* e = std::getenv("VODA_BN_SWEEP")) v.sweep = std::max(0, std::min(2, std::atoi(e)));
     if (const char* e = std::getenv("VODA_BN_APPLY_CAP")) v.apply_cap = std::max(256, std::atoi(e));
     if (const char* e = std::getenv("VODA_BN_APPLY_ITERS")) v.apply_iters = std::max(1, std::atoi(e));
@@ -873,9 +880,12 @@ BnTune& bn_tune() {
 
 Grid apply_grid(int64_t M, int C) { return bn_grid(M, C, bn_tune().apply_cap, bn_tune().apply_iters); }
 
-// partial-sum blocks: bounded so that the partial arrays stay <= 2M floats each
-Grid reduce_grid(int64_t M, int C) {
-  const int64_t cap = std::max<int64_t>(1, std::min<int64_t>(bn_tune().blocks, (int64_t(1) << 21) / C));
+// partial-sum blocks: bounded so that the partial arrays stay <= 2M floats each.  dt < 0: the
+// largest grid of any dtype (workspace sizing)
+Grid reduce_grid(int64_t M, int C, int dt) {
+  const BnTune& t = bn_tune();
+  const int blocks = dt == kF32 ? t.blocks_f32 : (dt < 0 ? std::max(t.blocks, t.blocks_f32) : t.blocks);
+  const int64_t cap = std::max<int64_t>(1, std::min<int64_t>(blocks, (int64_t(1) << 21) / C));
   return bn_grid(M, C, cap, 8);
 }
 
@@ -904,7 +914,7 @@ std::vector<int> bn_get_tuning() {
 }
 
 int64_t bn_workspace_floats(int64_t M, int C) {
-  const Grid g = reduce_grid(M, C);
+  const Grid g = reduce_grid(M, C, -1);
   return int64_t(2) * g.nb * C + 3 * int64_t(C);
 }
 
@@ -917,7 +927,7 @@ void bn_fwd_train(uintptr_t x, uintptr_t residual, uintptr_t gamma, uintptr_t be
   hipStream_t s = as_stream(stream);
   float* ws = reinterpret_cast<float*>(workspace);
   // pre_nb > 0: the producing GEMM already wrote pre_nb partial rows (gemm_bnstats.hip)
-  const Grid rg = reduce_grid(M, C);
+  const Grid rg = reduce_grid(M, C, dt);
   const int nb = pre_nb > 0 ? pre_nb : rg.nb;
   float* ab = ws + int64_t(2) * nb * C;
   const Grid ag = apply_grid(M, C);
@@ -988,7 +998,7 @@ void bn_bwd(uintptr_t dy, uintptr_t mask, uintptr_t x, uintptr_t save_mean, uint
   VODA_CHECK(!relu || mask != 0, "batchnorm backward: ReLU needs the forward's bit-mask");
   hipStream_t s = as_stream(stream);
   float* ws = reinterpret_cast<float*>(workspace);
-  const Grid rg = reduce_grid(M, C);
+  const Grid rg = reduce_grid(M, C, dt);
   float* k3 = ws + int64_t(2) * rg.nb * C;
   const Grid ag = apply_grid(M, C);
   const int sw = bn_tune().sweep;
