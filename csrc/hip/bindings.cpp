@@ -56,7 +56,8 @@ PYBIND11_MODULE(_vodahip, m) {
   m.def("gemm_f32_stats_supported", &gemm_f32_stats_supported);
   m.def("gemm_f32_stats_groups", &gemm_f32_stats_groups);
   m.def("gemm_f32_stats", &gemm_f32_stats, py::arg("x"), py::arg("w"), py::arg("y"), py::arg("part"), py::arg("M"),
-        py::arg("N"), py::arg("K"), py::arg("G"), py::arg("stream"), py::arg("accumulate") = false);
+        py::arg("N"), py::arg("K"), py::arg("G"), py::arg("stream"), py::arg("accumulate") = false,
+        py::arg("w_kn") = false);
   m.def("wgrad_f32_workspace_floats", &wgrad_f32_workspace_floats);
   m.def("wgrad_f32_config", &wgrad_f32_config);
   m.def("wgrad_f32", &wgrad_f32);

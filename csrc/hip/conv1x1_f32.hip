@@ -51,12 +51,13 @@ constexpr int kFRows = 128;  // rows per row tile (32 per wave)
 
 struct FArgs {
   const float* x;  // [M][K]
-  const float* w;  // [N][K]
+  const float* w;  // [N][K], or [K][N] when w_kn (an input gradient's dY . W[Cout][Cin])
   float* y;        // [M][N]
   float* part;     // [2][G][N] (null: no statistics)
   int64_t M;
   int N, G;
   int accumulate;  // Y += X W^T (statistics then describe X W^T alone)
+  int w_kn;
 };
 
 template <int NT, int K, bool DBUF>
@@ -73,9 +74,22 @@ __global__ __launch_bounds__(kFThreads, 2) void gemm_f32_stats_kernel(FArgs p) {
   const int nt = blockIdx.x / p.G, g = blockIdx.x - nt * p.G;
   const int n0 = nt * NC;
 
-  for (int i = tid; i < NC * (K / 4); i += kFThreads) {
-    const int r = i / (K / 4), c = i - r * (K / 4);
-    *reinterpret_cast<float4*>(wl + r * PK + 4 * c) = *reinterpret_cast<const float4*>(p.w + int64_t(n0 + r) * K + 4 * c);
+  if (p.w_kn) {
+    // W^T stored [K][N]: 16-byte loads along n, transposed into the [n][k] LDS rows (the
+    // input gradient runs without a transposed copy of the weight per call)
+    for (int i = tid; i < K * (NC / 4); i += kFThreads) {
+      const int k = i / (NC / 4), c = i - k * (NC / 4);
+      const float4 v = *reinterpret_cast<const float4*>(p.w + int64_t(k) * p.N + n0 + 4 * c);
+      wl[(4 * c + 0) * PK + k] = v.x;
+      wl[(4 * c + 1) * PK + k] = v.y;
+      wl[(4 * c + 2) * PK + k] = v.z;
+      wl[(4 * c + 3) * PK + k] = v.w;
+    }
+  } else {
+    for (int i = tid; i < NC * (K / 4); i += kFThreads) {
+      const int r = i / (K / 4), c = i - r * (K / 4);
+      *reinterpret_cast<float4*>(wl + r * PK + 4 * c) = *reinterpret_cast<const float4*>(p.w + int64_t(n0 + r) * K + 4 * c);
+    }
   }
   __syncthreads();
 
@@ -432,14 +446,14 @@ int gemm_f32_stats_groups(int64_t M, int N, int K) {
 }
 
 void gemm_f32_stats(uintptr_t x, uintptr_t w, uintptr_t y, uintptr_t part, int64_t M, int N, int K, int G,
-                    uintptr_t stream, bool accumulate) {
+                    uintptr_t stream, bool accumulate, bool w_kn) {
   VODA_CHECK(gemm_f32_stats_supported(M, N, K), "gemm_f32_stats: K must be 64, 128 or 256 and N a multiple of the tile");
   VODA_CHECK(G == gemm_f32_stats_groups(M, N, K), "gemm_f32_stats: group count mismatch");
   VODA_CHECK(x % 16 == 0 && w % 16 == 0 && y % 4 == 0 && part % 4 == 0, "gemm_f32_stats: misaligned operands");
   const int nt = gf_nt(K);
   const int ncol = N / (32 * nt);
   FArgs a{reinterpret_cast<const float*>(x), reinterpret_cast<const float*>(w), reinterpret_cast<float*>(y),
-          reinterpret_cast<float*>(part), M, N, G, accumulate ? 1 : 0};
+          reinterpret_cast<float*>(part), M, N, G, accumulate ? 1 : 0, w_kn ? 1 : 0};
   hipStream_t s = as_stream(stream);
   if (K == 64)
     hipLaunchKernelGGL((gemm_f32_stats_kernel<8, 64, true>), dim3(ncol * G), dim3(kFThreads), 0, s, a);

@@ -98,8 +98,9 @@ void bn_bwd(uintptr_t dy, uintptr_t mask, uintptr_t x, uintptr_t save_mean, uint
 // (conv1x1_f32.hip) ----
 bool gemm_f32_stats_supported(int64_t M, int N, int K);
 int gemm_f32_stats_groups(int64_t M, int N, int K);
+// w: [N][K], or [K][N] with w_kn (the input gradient dX = dY . W with W [Cout][Cin] as stored)
 void gemm_f32_stats(uintptr_t x, uintptr_t w, uintptr_t y, uintptr_t part, int64_t M, int N, int K, int G,
-                    uintptr_t stream, bool accumulate);
+                    uintptr_t stream, bool accumulate, bool w_kn);
 int64_t wgrad_f32_workspace_floats(int M, int N, int K, int splits);
 std::vector<int> wgrad_f32_config(int M, int N, int K, int splits);
 void wgrad_f32(uintptr_t dy, uintptr_t x, uintptr_t dw, int M, int N, int K, int splits, uintptr_t ws,

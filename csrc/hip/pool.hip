@@ -323,7 +323,8 @@ void global_avgpool_bwd(uintptr_t g, uintptr_t dx, int N, int HW, int C, float s
 // ---- stride-s pixel subsampling of a channels_last tensor (the input of ResNet's stride-2
 // 1x1 downsample convolutions) and its adjoint, dx[:, :, ::s, ::s] += g.  PyTorch runs both
 // as generic strided elementwise kernels (69 + 38 + 21 us forward, 61 + 33 + 19 us backward
-// per ResNet-50 bs-256 step, 2.7-3.4 TB/s); a thread here moves 16 B (8 channels) of one pixel.
+// per ResNet-50 bs-256 step, 2.7-3.4 TB/s); a thread here moves 8 channels of one pixel (16 B
+// bf16, 32 B fp32: the fp32 strided add took 65 us per call as a PyTorch kernel).
 namespace {
 template <typename T, bool ADD>
 __global__ __launch_bounds__(256) void subsample_kernel(const T* __restrict__ src, T* __restrict__ dst, int H, int W,
@@ -337,7 +338,9 @@ __global__ __launch_bounds__(256) void subsample_kernel(const T* __restrict__ sr
   const int64_t full = ((int64_t(n) * H + int64_t(ho) * s) * W + int64_t(wo) * s) * C + cg * 8;
   const int64_t sub = (int64_t(nho) * Wo + wo) * C + cg * 8;
   if constexpr (!ADD) {
-    *reinterpret_cast<uint4*>(dst + sub) = *reinterpret_cast<const uint4*>(src + full);  // gather
+    float a[8];  // gather
+    V8<T>::load(src + full, a);
+    V8<T>::store(dst + sub, a);
   } else {
     float a[8], b[8];
     V8<T>::load(src + sub, a);   // g (subsampled)
@@ -357,11 +360,16 @@ void subsample2d(uintptr_t src, uintptr_t dst, int N, int H, int W, int C, int s
   if (int64_t(N) * Ho * Wo == 0) return;
   const dim3 grid(unsigned(N * Ho), unsigned((int64_t(Wo) * (C / 8) + 255) / 256));
   hipStream_t st = as_stream(stream);
-  VODA_CHECK(dt == kBF16, "subsample2d: bf16 activations only");
-  const BF16* a = reinterpret_cast<const BF16*>(src);
-  BF16* b = reinterpret_cast<BF16*>(dst);
-  if (add) hipLaunchKernelGGL((subsample_kernel<BF16, true>), grid, dim3(256), 0, st, a, b, H, W, C, Ho, Wo, s);
-  else hipLaunchKernelGGL((subsample_kernel<BF16, false>), grid, dim3(256), 0, st, a, b, H, W, C, Ho, Wo, s);
+  VODA_CHECK(dt == kBF16 || dt == kF32, "subsample2d: bf16 / fp32 activations only");
+  auto go = [&](auto tag) {
+    using T = decltype(tag);
+    const T* a = reinterpret_cast<const T*>(src);
+    T* b = reinterpret_cast<T*>(dst);
+    if (add) hipLaunchKernelGGL((subsample_kernel<T, true>), grid, dim3(256), 0, st, a, b, H, W, C, Ho, Wo, s);
+    else hipLaunchKernelGGL((subsample_kernel<T, false>), grid, dim3(256), 0, st, a, b, H, W, C, Ho, Wo, s);
+  };
+  if (dt == kF32) go(float{});
+  else go(BF16{});
   check_launch();
 }
 

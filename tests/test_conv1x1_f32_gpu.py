@@ -31,7 +31,7 @@ def test_gemm_f32_stats_matches_fp64(M, N, K):
     G = h.gemm_f32_stats_groups(M, N, K)
     y = torch.full((M, N), float("nan"), device="cuda")
     part = torch.empty(2 * G * N, device="cuda")
-    h.gemm_f32_stats(x.data_ptr(), w.data_ptr(), y.data_ptr(), part.data_ptr(), M, N, K, G, Nn.stream_of(x), False)
+    h.gemm_f32_stats(x.data_ptr(), w.data_ptr(), y.data_ptr(), part.data_ptr(), M, N, K, G, Nn.stream_of(x), False, False)
     ref = x.double() @ w.double().t()
     assert _rel(y, ref) < 2e-6
     s1 = part[:G * N].view(G, N).double().sum(0)
@@ -40,8 +40,13 @@ def test_gemm_f32_stats_matches_fp64(M, N, K):
     # accumulate form (input gradient into a tensor that already holds the shortcut's)
     y0 = torch.randn(M, N, device="cuda")
     y2 = y0.clone()
-    h.gemm_f32_stats(x.data_ptr(), w.data_ptr(), y2.data_ptr(), 0, M, N, K, G, Nn.stream_of(x), True)
+    h.gemm_f32_stats(x.data_ptr(), w.data_ptr(), y2.data_ptr(), 0, M, N, K, G, Nn.stream_of(x), True, False)
     assert _rel(y2, y0.double() + ref) < 2e-6
+    # W handed over as [K][N] (the input-gradient form: no transposed copy)
+    wkn = w.t().contiguous()
+    y3 = torch.full((M, N), float("nan"), device="cuda")
+    h.gemm_f32_stats(x.data_ptr(), wkn.data_ptr(), y3.data_ptr(), 0, M, N, K, G, Nn.stream_of(x), False, True)
+    assert torch.equal(y3, y)
 
 
 @pytest.mark.parametrize("M,N,K,splits", [(4096, 256, 256, 0), (1000, 64, 512, 0), (3000, 512, 64, 3),

@@ -1,5 +1,5 @@
-"""ResNet glue kernels (csrc/hip/pool.hip): stride-s pixel subsampling of channels_last bf16
-tensors (the stride-2 1x1 downsample input) and its adjoint, against PyTorch slicing."""
+"""ResNet glue kernels (csrc/hip/pool.hip): stride-s pixel subsampling of channels_last bf16 /
+fp32 tensors (the stride-2 1x1 downsample input) and its adjoint, against PyTorch slicing."""
 import pytest
 import torch
 
@@ -8,11 +8,12 @@ from vodascheduler_amd.ops.conv1x1 import subsample, subsample_add_
 pytestmark = pytest.mark.gpu
 
 
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
 @pytest.mark.parametrize("shape,s", [((4, 256, 56, 56), 2), ((3, 64, 17, 13), 2), ((2, 8, 9, 10), 3), ((1, 16, 1, 1), 2)])
-def test_subsample_gather_and_add_exact(shape, s):
+def test_subsample_gather_and_add_exact(shape, s, dtype):
     torch.manual_seed(0)
     cl = torch.channels_last
-    x = torch.randn(shape, device="cuda").bfloat16().to(memory_format=cl)
+    x = torch.randn(shape, device="cuda").to(dtype).to(memory_format=cl)
     y = subsample(x, s)
     assert y.is_contiguous(memory_format=cl)
     assert torch.equal(y, x[:, :, ::s, ::s])

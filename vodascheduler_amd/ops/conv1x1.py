@@ -67,6 +67,12 @@ USE_GEMM_F32 = os.environ.get("VODA_GEMM_F32", "1") != "0"
 # profiles/r4/resnet50_fp32_1x1_own_vs_miopen.jsonl); in the ResNet-50 fp32 step: 80.0 ms with
 # the kernel vs 75.4 ms with MIOpen's (profiles/r4/rocprof_resnet50_fp32_*.md)
 USE_WGRAD_F32 = os.environ.get("VODA_WGRAD_F32", "0") != "0"
+# input gradient accumulated onto a GradSink's shortcut gradient (beta = 1): the MFMA GEMM's
+# read-add epilogue (1) or hipBLASLt's addmm (0, default), per precision.  Measured in the
+# ResNet-50 step (profiles/r4/sink_gemm_ab.md): fp32 69.3 -> 73.0 ms, bf16 23.03 -> 23.10 ms
+# with the own GEMM -- hipBLASLt's beta = 1 kernels stay
+USE_SINK_GEMM_F32 = os.environ.get("VODA_SINK_GEMM_F32", "0") != "0"
+USE_SINK_GEMM_BF16 = os.environ.get("VODA_SINK_GEMM_BF16", "0") != "0"
 
 
 class GradSink:
@@ -116,7 +122,7 @@ class _StridedGrad:
 
 
 def _sub_ok(t: torch.Tensor) -> bool:
-    return (t.is_cuda and t.dim() == 4 and t.dtype == torch.bfloat16 and t.shape[1] % 8 == 0
+    return (t.is_cuda and t.dim() == 4 and t.dtype in (torch.bfloat16, torch.float32) and t.shape[1] % 8 == 0
             and t.is_contiguous(memory_format=torch.channels_last) and t.data_ptr() % 16 == 0)
 
 
@@ -157,14 +163,15 @@ def _f32_ok(*ts: torch.Tensor) -> bool:
 
 
 def gemm_f32_2d(x2: torch.Tensor, w2: torch.Tensor, holder: StatsHolder | None = None,
-                out: torch.Tensor | None = None) -> torch.Tensor | None:
+                out: torch.Tensor | None = None, w_kn: bool = False) -> torch.Tensor | None:
     """fp32 Y = X W^T (+ ``out`` in place) on the f32-MFMA kernel (conv1x1_f32.hip), with the
     BN statistics of Y's columns when a holder wants them; None when K is not 64 / 128 / 256
-    or the operands are not dense fp32 (the caller keeps its library path)."""
+    or the operands are not dense fp32 (the caller keeps its library path).  ``w_kn``: ``w2``
+    is W^T, stored [K][N] (Y = X . w2)."""
     if not USE_GEMM_F32 or not x2.is_cuda or not _f32_ok(x2, w2):
         return None
     M, K = x2.shape
-    Nc = w2.shape[0]
+    Nc = w2.shape[1] if w_kn else w2.shape[0]
     h = N.hip()
     if not h.gemm_f32_stats_supported(M, Nc, K):
         return None
@@ -177,7 +184,7 @@ def gemm_f32_2d(x2: torch.Tensor, w2: torch.Tensor, holder: StatsHolder | None =
         ws = torch.empty(max(2 * G * Nc + 3 * Nc, h.bn_workspace_floats(M, Nc)), dtype=torch.float32,
                          device=x2.device)
     h.gemm_f32_stats(x2.data_ptr(), w2.data_ptr(), y2.data_ptr(), N.ptr(ws), M, Nc, K, G, N.stream_of(x2),
-                     out is not None)
+                     out is not None, w_kn)
     if holder is not None:
         holder.stats = (ws, G)
     return y2
@@ -213,7 +220,7 @@ def mfma_dgrad(dy2: torch.Tensor, w2: torch.Tensor, acc2: torch.Tensor | None = 
     if not USE_MFMA_DGRAD or not dy2.is_cuda:
         return None
     if dy2.dtype == torch.float32:
-        return gemm_f32_2d(dy2, w2.t().contiguous(), None, acc2)
+        return gemm_f32_2d(dy2, w2, None, acc2, w_kn=True)  # W [Cout][Cin] = the kernel's [K][N]
     M, K = dy2.shape
     Nc = w2.shape[1]
     if (dy2.dtype != torch.bfloat16 or w2.dtype != torch.bfloat16 or not dy2.is_contiguous()
@@ -302,9 +309,12 @@ class _Conv1x1Fn(torch.autograd.Function):
             s_ = strided.stride
             subsample_add_(dx, strided.g, strided.stride)
         elif acc is not None:
-            # beta = 1 stays on hipBLASLt: the MFMA GEMM's read-add-write epilogue made these
-            # calls 2x slower in the step (802816 x 64 -> 256: 203 us vs ~98 us)
-            _as_2d(acc).addmm_(dy2, w2)  # dX = shortcut gradient + dY . W (one GEMM, beta = 1)
+            # bf16 beta = 1 stays on hipBLASLt: the MFMA GEMM's read-add-write epilogue made
+            # these calls 2x slower in the step (802816 x 64 -> 256: 203 us vs ~98 us)
+            use = USE_SINK_GEMM_F32 if dy2.dtype == torch.float32 else USE_SINK_GEMM_BF16
+            own = use and mfma_dgrad(dy2, w2, _as_2d(acc)) is not None
+            if not own:
+                _as_2d(acc).addmm_(dy2, w2)  # dX = shortcut gradient + dY . W (one GEMM, beta = 1)
             dx = acc
         elif ctx.needs_input_grad[0]:
             dx2 = mfma_dgrad(dy2, w2)
