@@ -313,6 +313,17 @@ def per_world_step_ms(allrec: list[dict]) -> dict:
             for m, d in acc.items()}
 
 
+def tunable_status(device: str) -> dict | None:
+    if device != "cuda":
+        return None
+    from vodascheduler_amd.utils import tunable
+
+    st = tunable.status()
+    st["files"] = [os.path.relpath(tunable.results_path(p)) for p in ("fp32", "bf16")
+                   if os.path.exists(tunable.results_path(p))]
+    return st
+
+
 def main():
     if os.environ.get("VODA_STACKDUMP_S"):  # debugging aid: dump every thread's stack once
         import faulthandler
@@ -632,6 +643,8 @@ def main():
             "throughput_samples_per_s": round(samples / wall_s, 1),
             "topology": topo_info,
             "warmup_single_gpu_step_ms": {k: round(v, 2) for k, v in step_ms.items()},
+            # pre-tuned hipBLASLt solutions (utils/tunable.py, var/tunableop/): loaded, never tuned here
+            "gemm_solutions": tunable_status(a.device),
         }
         print(json.dumps(line), flush=True)
         if a.out:

@@ -7,7 +7,9 @@ the results ship in ``var/tunableop/fp32.csv`` (a plain CSV: "op, shape, solutio
 behind validator rows for the PyTorch / HIP / hipBLASLt versions and the GPU arch -- a file
 from another software stack is ignored by PyTorch).  Workers load it with tuning OFF: a
 listed shape runs its tuned solution, any other shape the library default; nothing is timed
-at run time.  Measured: BERT-base fp32 step 39.22 -> 36.68 ms (``profiles/r4/tunableop_*``).
+at run time.  Measured (same box, ``profiles/r4/tunableop_ab.jsonl``): BERT-base fp32 step
+39.42 -> 36.88 ms, ResNet-50 fp32 73.89 -> 70.46 ms; the bf16 results (``bf16.csv``) are worth
+~1 % on the bf16-amp path.
 
 ``VODA_TUNABLEOP=0`` disables it (A/B); ``VODA_TUNABLEOP_TUNE=1`` tunes new shapes and
 writes them back (how the file is produced: ``benchmarks/gpu_tunableop.sh``).
