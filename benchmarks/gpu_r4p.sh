@@ -1,7 +1,7 @@
 # Round-end style checks: the driver's exact bench command (fp32 default, shipped TunableOp
 # results), then the GPU test suite and smoke.
 set -o pipefail
-OUT=gpurun_out/r4p
+OUT=gpurun_out/${R4P_OUT:-r4p}
 mkdir -p $OUT
 start=$(date +%s)
 timeout -k 10 600 python bench.py --gpus 1 --steps 20 --warmup 5 > $OUT/bench.json 2> $OUT/bench.err || { tail -30 $OUT/bench.err; exit 1; }
