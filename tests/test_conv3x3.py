@@ -191,3 +191,28 @@ def test_convkxk_c64_layer_uses_kernel_and_matches():
     for got, want in ((grad_of(m.weight), ref_w.grad), (xg.grad, xr.grad)):
         rel = float((got.float() - want).norm() / want.norm())
         assert rel < 1e-2, rel
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("cin,cout,stride", [(64, 64, 1), (128, 128, 1), (128, 128, 2), (256, 256, 2)])
+def test_convkxk_fp32_layer_matches_fp64(cin, cout, stride):
+    """fp32 (reference precision) ConvKxK: stride-1 input gradients run as forward
+    convolutions (VODA_CONV_F32_FN), weight gradients on MIOpen -- against fp64 autograd."""
+    torch.manual_seed(0)
+    cl = torch.channels_last
+    m = C.ConvKxK(cin, cout, 3, stride=stride, padding=1).cuda().to(memory_format=cl)
+    x = torch.randn(2, cin, 14, 14, device="cuda").to(memory_format=cl).requires_grad_()
+    y = m(x)
+    if C.CONV_F32_FN and stride == 1:
+        assert type(y.grad_fn).__name__.startswith("_ConvKxKFn")
+    dy = torch.randn_like(y)
+    y.backward(dy)
+    xr = x.detach().double().requires_grad_()
+    wr = m.weight.detach().double().requires_grad_()
+    yr = F.conv2d(xr, wr, stride=stride, padding=1)
+    yr.backward(dy.double())
+
+    def rel(a, b):
+        return float((a.double() - b).norm() / b.norm())
+
+    assert rel(y, yr) < 1e-5 and rel(x.grad, xr.grad) < 1e-5 and rel(m.weight.grad, wr.grad) < 1e-5

@@ -43,6 +43,13 @@ USE_CONV_WGRAD = os.environ.get("VODA_CONV_WGRAD", "1") != "0"
 DGRAD_FWD = os.environ.get("VODA_CONV_DGRAD_FWD", "1") != "0"
 
 
+# VODA_CONV_F32_FN (default 1): fp32 (reference-precision) stride-1 KxK convolutions take the
+# same autograd function, i.e. their input gradient also runs as a forward convolution (their
+# weight gradient stays on MIOpen, folded into the flat gradient).  fp32 ResNet-50 step, same
+# lease: 70.21 -> 70.08 ms kernel time (igemm_bwd 7.79 -> 1.63 ms, igemm_fwd 8.0 -> 14.0 ms;
+# gpurun_out/r4v, profiles/r4/README.md)
+CONV_F32_FN = os.environ.get("VODA_CONV_F32_FN", "1") != "0"
+
 # VODA_CONV_C64_WGRAD=0: the 64 -> 64 channel 3x3 weight gradient runs MIOpen (A/B switch)
 USE_C64_WGRAD = os.environ.get("VODA_CONV_C64_WGRAD", "1") != "0"
 
@@ -188,8 +195,9 @@ class ConvKxK(torch.nn.Conv2d):
         super().__init__(in_channels, out_channels, kernel_size, stride=stride, padding=padding, bias=False, **kw)
 
     def _layout_ok(self, x: torch.Tensor) -> bool:
-        return (x.is_cuda and x.dim() == 4 and x.dtype == torch.bfloat16
-                and self.weight.dtype == torch.bfloat16 and self.groups == 1 and self.dilation == (1, 1)
+        dt = (torch.bfloat16, torch.float32) if CONV_F32_FN else (torch.bfloat16,)
+        return (x.is_cuda and x.dim() == 4 and x.dtype in dt
+                and self.weight.dtype == x.dtype and self.groups == 1 and self.dilation == (1, 1)
                 and self.stride[0] == self.stride[1] and self.padding[0] == self.padding[1]
                 and isinstance(self.padding[0], int) and x.is_contiguous(memory_format=torch.channels_last)
                 and self.weight.is_contiguous(memory_format=torch.channels_last)
