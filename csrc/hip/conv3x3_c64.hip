@@ -185,6 +185,139 @@ __global__ __launch_bounds__(kThreads, 1) void conv3x3_c64_wgrad_kernel(C64Args 
   }
 }
 
+// ------------------------------------------------------------------------------------------
+// fp32 twin (the reference-precision run) on v_mfma_f32_32x32x2_f32: a k-step is TWO pixels,
+// and the f32 MFMA's operand layout (lane l: A[i = l&31][k = l>>5], B[k = l>>5][j = l&31]) is
+// the pixel-major [px][channel] LDS image read straight -- 32 consecutive channels of one
+// pixel per lane half, no transposed reads.  Same work split (wave w: output-channel tile
+// w & 1, 9 of the 18 (tap, 32-channel block) tiles, 144 accumulators), same 4-slot ring of
+// input rows (zero rows / pad pixels outside the image), one row of prefetch in registers
+// (a row is ~6.7 us of MFMA work per wave at 56 pixels, far longer than a load's latency),
+// LDS operands of the next pixel pair read while the current pair's 9 MFMAs issue.
+constexpr int kFPitch = 68;                     // floats per LDS pixel (64 + 4: 16-byte rows)
+constexpr int kFSlot = kRingPx * kFPitch;       // floats per ring row
+constexpr int kFChunks = kMaxW * 16;            // float4 chunks of a 64-pixel row
+constexpr int kFPf = kFChunks / kThreads;       // 4 per thread
+
+struct C64ArgsF {
+  const float* x;   // [N][H][W][64]
+  const float* dy;  // [N][H][W][64]
+  float* part;      // [gridDim.x][64][576]
+  int N, H, W;
+};
+
+typedef float c64_f32x16f __attribute__((ext_vector_type(16)));
+
+__device__ __forceinline__ float4 c64f_xchunk(const C64ArgsF& a, int64_t n, int hi, int c) {
+  const int px = c >> 4, part = c & 15;
+  const bool ok = unsigned(hi) < unsigned(a.H) && px < a.W;
+  const int hc = min(max(hi, 0), a.H - 1), pc = min(px, a.W - 1);
+  const float4 v = reinterpret_cast<const float4*>(a.x + ((n * a.H + hc) * a.W + pc) * kC)[part];
+  return ok ? v : make_float4(0.f, 0.f, 0.f, 0.f);
+}
+
+__global__ __launch_bounds__(kThreads, 1) void conv3x3_c64_wgrad_f32_kernel(C64ArgsF a) {
+  __shared__ __attribute__((aligned(16))) float ring[kSlots * kFSlot];
+  __shared__ __attribute__((aligned(16))) float dyt[kMaxW * kFPitch];
+
+  const int tid = threadIdx.x;
+  const int wave = tid >> 6, lane = tid & 63;
+  const int lh = lane >> 5, lr = lane & 31;
+  const int ct = wave & 1;
+  const int kt0 = (wave >> 1) * 9;
+
+  // everything zero once: pad pixels, pixels >= W and the dY pixels >= W stay zero (the
+  // staging below writes input pixels 1..W of a ring row and dY pixels 0..W-1 only)
+  for (int i = tid; i < kSlots * kFSlot / 4; i += kThreads) reinterpret_cast<float4*>(ring)[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+  for (int i = tid; i < kMaxW * kFPitch / 4; i += kThreads) reinterpret_cast<float4*>(dyt)[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+
+  c64_f32x16f acc[9];
+#pragma unroll
+  for (int t = 0; t < 9; ++t) acc[t] = c64_f32x16f{};
+
+  const int64_t rows = int64_t(a.N) * a.H;
+  const int64_t per = (rows + gridDim.x - 1) / gridDim.x;
+  const int64_t r0 = int64_t(blockIdx.x) * per;
+  const int64_t r1 = r0 + per < rows ? r0 + per : rows;
+  const int chunks = a.W * 16;
+  const int steps = (a.W + 1) / 2;
+
+  int64_t n = r0 / a.H;
+  int h = int(r0 - n * a.H);
+  float4 xr[kFPf], dr[kFPf];
+  auto put_x = [&](int hi, int c, const float4& v) {
+    if (c < chunks) *reinterpret_cast<float4*>(ring + (hi & (kSlots - 1)) * kFSlot + ((c >> 4) + 1) * kFPitch + (c & 15) * 4) = v;
+  };
+  auto put_dy = [&](int c, const float4& v) {
+    if (c < chunks) *reinterpret_cast<float4*>(dyt + (c >> 4) * kFPitch + (c & 15) * 4) = v;
+  };
+  bool in_lds = false;
+  __syncthreads();
+  for (int64_t row = r0; row < r1; ++row) {
+    if (!in_lds) {  // first row of the chunk or of an image: input rows h-1 .. h+1 and the dY row
+      for (int r = 0; r < 3; ++r)
+        for (int c = tid; c < chunks; c += kThreads) put_x(h - 1 + r, c, c64f_xchunk(a, n, h - 1 + r, c));
+      for (int c = tid; c < chunks; c += kThreads) put_dy(c, reinterpret_cast<const float4*>(a.dy + row * a.W * kC)[c]);
+    }
+    __syncthreads();
+    const bool nxt = row + 1 < r1 && h + 1 < a.H;
+    if (nxt) {  // the next row's new input row (h + 2) and dY row, in flight during this row
+#pragma unroll
+      for (int j = 0; j < kFPf; ++j) {
+        const int c = tid + j * kThreads;
+        xr[j] = c64f_xchunk(a, n, h + 2, min(c, kFChunks - 1));
+        dr[j] = reinterpret_cast<const float4*>(a.dy + (row + 1) * a.W * kC)[min(c, chunks - 1)];
+      }
+    }
+    const float* ap = dyt + lh * kFPitch + 32 * ct + lr;
+    const float* bp[9];
+#pragma unroll
+    for (int t = 0; t < 9; ++t) {
+      const int kt = kt0 + t;
+      const int tap = kt >> 1, cb = kt & 1;
+      const int kh = tap / 3, kw = tap - 3 * (tap / 3);
+      bp[t] = ring + ((h - 1 + kh) & (kSlots - 1)) * kFSlot + (lh + kw) * kFPitch + 32 * cb + lr;
+    }
+    float av = ap[0], bv[9];
+#pragma unroll
+    for (int t = 0; t < 9; ++t) bv[t] = bp[t][0];
+    for (int s = 0; s < steps; ++s) {
+      const int off = 2 * (s + 1 < steps ? s + 1 : s) * kFPitch;  // next pixel pair (clamped)
+      const float an = ap[off];
+      float bn[9];
+#pragma unroll
+      for (int t = 0; t < 9; ++t) bn[t] = bp[t][off];
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int t = 0; t < 9; ++t) acc[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(av, bv[t], acc[t], 0, 0, 0);
+      __builtin_amdgcn_sched_barrier(0);
+      av = an;
+#pragma unroll
+      for (int t = 0; t < 9; ++t) bv[t] = bn[t];
+    }
+    __syncthreads();  // every wave is done with this row's dY tile and window
+    if (nxt) {
+#pragma unroll
+      for (int j = 0; j < kFPf; ++j) {
+        put_x(h + 2, tid + j * kThreads, xr[j]);
+        put_dy(tid + j * kThreads, dr[j]);
+      }
+    }
+    in_lds = nxt;
+    if (++h == a.H) { h = 0; ++n; }
+  }
+
+  float* out = a.part + int64_t(blockIdx.x) * kC * kK + lr;
+#pragma unroll
+  for (int t = 0; t < 9; ++t) {
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int co = 32 * ct + (r & 3) + 8 * (r >> 2) + 4 * lh;
+      out[co * kK + (kt0 + t) * 32] = acc[t][r];
+    }
+  }
+}
+
 // partial sums in two passes: [nb][E] -> [nsl][E] (float4, each slice sums <= 8 partial rows)
 // -> dW.  (The first version summed nb / 32 scalar rows per thread and then 32 more: two
 // latency-bound ~10 us passes per call.)
@@ -262,7 +395,7 @@ int64_t conv3x3_c64_wgrad_workspace_floats(int N, int H) {
 }
 
 void conv3x3_c64_wgrad(uintptr_t x, uintptr_t dy, uintptr_t dw, int64_t s0, int64_t s1, int64_t s2, int64_t s3,
-                       uintptr_t ws, int N, int H, int W, bool accumulate, int out_dt, uintptr_t stream) {
+                       uintptr_t ws, int N, int H, int W, bool accumulate, int out_dt, uintptr_t stream, int in_dt) {
   VODA_CHECK(W >= 1 && W <= kMaxW && H >= 1, "conv3x3_c64_wgrad: image width must be 1..64");
   VODA_CHECK(out_dt == kF32 || out_dt == kBF16, "conv3x3_c64_wgrad: dW must be fp32 or bf16");
   VODA_CHECK(x % 16 == 0 && dy % 16 == 0 && ws % 16 == 0, "conv3x3_c64_wgrad: misaligned operands");
@@ -271,8 +404,14 @@ void conv3x3_c64_wgrad(uintptr_t x, uintptr_t dy, uintptr_t dw, int64_t s0, int6
   float* part = reinterpret_cast<float*>(ws);
   float* tmp = part + int64_t(nb) * kC * kK;
   const int nsl = std::min(kMaxSlices, nb);
-  C64Args a{reinterpret_cast<const uint16_t*>(x), reinterpret_cast<const uint16_t*>(dy), part, N, H, W};
-  hipLaunchKernelGGL(conv3x3_c64_wgrad_kernel, dim3(nb), dim3(kThreads), 0, s, a);
+  VODA_CHECK(in_dt == kBF16 || in_dt == kF32, "conv3x3_c64_wgrad: activations must be bf16 or fp32");
+  if (in_dt == kF32) {
+    C64ArgsF a{reinterpret_cast<const float*>(x), reinterpret_cast<const float*>(dy), part, N, H, W};
+    hipLaunchKernelGGL(conv3x3_c64_wgrad_f32_kernel, dim3(nb), dim3(kThreads), 0, s, a);
+  } else {
+    C64Args a{reinterpret_cast<const uint16_t*>(x), reinterpret_cast<const uint16_t*>(dy), part, N, H, W};
+    hipLaunchKernelGGL(conv3x3_c64_wgrad_kernel, dim3(nb), dim3(kThreads), 0, s, a);
+  }
   const int e4 = kC * kK / 4;
   hipLaunchKernelGGL(c64_slice_kernel, dim3((e4 + 255) / 256, nsl), dim3(256), 0, s,
                      reinterpret_cast<const float4*>(part), nb, e4, reinterpret_cast<float4*>(tmp));

@@ -156,14 +156,66 @@ def test_conv3x3_c64_wgrad_vs_fp64(n, h, w, out):
         base = torch.randn(64, 64, 3, 3, device="cuda").contiguous(memory_format=cl)
         dw = base.clone()
         hip.conv3x3_c64_wgrad(x.data_ptr(), dy.data_ptr(), dw.data_ptr(), *dw.stride(), ws.data_ptr(), n, h, w,
-                              True, C.N.dtype_code(dw.dtype), C.N.stream_of(x))
+                              True, C.N.dtype_code(dw.dtype), C.N.stream_of(x), C.N.dtype_code(x.dtype))
         got, tol = (dw - base).double(), 1e-4
     else:
         dw = torch.empty(64, 64, 3, 3, device="cuda", dtype=torch.bfloat16)
         hip.conv3x3_c64_wgrad(x.data_ptr(), dy.data_ptr(), dw.data_ptr(), *dw.stride(), ws.data_ptr(), n, h, w,
-                              False, C.N.dtype_code(dw.dtype), C.N.stream_of(x))
+                              False, C.N.dtype_code(dw.dtype), C.N.stream_of(x), C.N.dtype_code(x.dtype))
         got, tol = dw.double(), 1e-2
     torch.testing.assert_close(got, want, rtol=1e-2, atol=tol * want.abs().max().item())
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n,h,w", [(2, 56, 56), (3, 17, 9), (1, 5, 64), (4, 30, 63), (2, 1, 1), (16, 56, 56)])
+def test_conv3x3_c64_wgrad_f32_vs_fp64(n, h, w):
+    """fp32 twin of the 64-channel 3x3 weight gradient (f32 MFMA: exact products, fp32 sums):
+    fp32 accumulation into a base and plain output vs fp64 conv2d_weight."""
+    torch.manual_seed(9)
+    cl = torch.channels_last
+    x = torch.randn(n, 64, h, w, device="cuda").to(memory_format=cl)
+    dy = torch.randn(n, 64, h, w, device="cuda").to(memory_format=cl)
+    want = torch.nn.grad.conv2d_weight(x.double(), (64, 64, 3, 3), dy.double(), stride=1, padding=1)
+    hip = C.N.hip()
+    ws = torch.empty(hip.conv3x3_c64_wgrad_workspace_floats(n, h), dtype=torch.float32, device="cuda")
+    base = torch.randn(64, 64, 3, 3, device="cuda").contiguous(memory_format=cl)
+    dw = base.clone()
+    hip.conv3x3_c64_wgrad(x.data_ptr(), dy.data_ptr(), dw.data_ptr(), *dw.stride(), ws.data_ptr(), n, h, w, True,
+                          C.N.dtype_code(dw.dtype), C.N.stream_of(x), C.N.dtype_code(x.dtype))
+    rel = float(((dw - base).double() - want).norm() / want.norm())
+    assert rel < 1e-5, rel
+    out = torch.full((64, 64, 3, 3), float("nan"), device="cuda")
+    hip.conv3x3_c64_wgrad(x.data_ptr(), dy.data_ptr(), out.data_ptr(), *out.stride(), ws.data_ptr(), n, h, w, False,
+                          C.N.dtype_code(out.dtype), C.N.stream_of(x), C.N.dtype_code(x.dtype))
+    assert float((out.double() - want).norm() / want.norm()) < 1e-5
+
+
+@pytest.mark.gpu
+def test_convkxk_c64_fp32_layer_uses_kernel(monkeypatch):
+    """fp32 64-channel ConvKxK under a flat-gradient optimizer: weight gradient from the fp32
+    c64 kernel into the flat buffer (tight vs fp64), input gradient as a forward conv."""
+    from vodascheduler_amd.ops.optim import make_optimizer
+    from vodascheduler_amd.utils.flat import grad_of
+
+    monkeypatch.setattr(C, "USE_C64_WGRAD_F32", True)
+    torch.manual_seed(10)
+    cl = torch.channels_last
+    m = C.ConvKxK(64, 64, 3, stride=1, padding=1).cuda().to(memory_format=cl)
+    ref_w = m.weight.detach().double().clone().requires_grad_(True)
+    opt = make_optimizer("sgd", m.parameters(), lr=0.0)
+    x = torch.randn(4, 64, 28, 28, device="cuda").to(memory_format=cl)
+    xg = x.detach().requires_grad_(True)
+    xr = x.double().detach().requires_grad_(True)
+    opt.zero_grad()
+    y = m(xg)
+    assert type(y.grad_fn).__name__.startswith("_ConvKxKFn")
+    yr = F.conv2d(xr, ref_w, padding=1)
+    g = torch.randn_like(yr)
+    y.backward(g.float().to(memory_format=cl))
+    yr.backward(g)
+    for got, want in ((grad_of(m.weight), ref_w.grad), (xg.grad, xr.grad)):
+        rel = float((got.double() - want).norm() / want.norm())
+        assert rel < 1e-5, rel
 
 
 @pytest.mark.gpu

@@ -50,16 +50,20 @@ DGRAD_FWD = os.environ.get("VODA_CONV_DGRAD_FWD", "1") != "0"
 # gpurun_out/r4v, profiles/r4/README.md)
 CONV_F32_FN = os.environ.get("VODA_CONV_F32_FN", "1") != "0"
 
-# VODA_CONV_C64_WGRAD=0: the 64 -> 64 channel 3x3 weight gradient runs MIOpen (A/B switch)
+# VODA_CONV_C64_WGRAD=0: the 64 -> 64 channel 3x3 weight gradient runs MIOpen (A/B switch);
+# VODA_CONV_C64_WGRAD_F32=1: the f32-MFMA twin for fp32 activations (opt-in: 752 us vs MIOpen's
+# 594 us at bs 256, 56 x 56 -- benchmarks/bench_c64_wgrad.py; the bf16 kernel 141 vs 176 us)
 USE_C64_WGRAD = os.environ.get("VODA_CONV_C64_WGRAD", "1") != "0"
+USE_C64_WGRAD_F32 = os.environ.get("VODA_CONV_C64_WGRAD_F32", "0") != "0"
 
 
 def c64_ok(dy: torch.Tensor, x: torch.Tensor, weight: torch.Tensor, stride: int, padding: int) -> bool:
     """The 64-channel 3x3 / stride-1 weight-gradient kernel (csrc/hip/conv3x3_c64.hip) covers
-    these operands: channels_last bf16 activations, width <= 64."""
+    these operands: channels_last bf16 (or fp32: the f32-MFMA twin) activations, width <= 64."""
     cl = torch.channels_last
+    dts = (torch.bfloat16, torch.float32) if USE_C64_WGRAD_F32 else (torch.bfloat16,)
     return (USE_C64_WGRAD and dy.is_cuda and stride == 1 and padding == 1 and tuple(weight.shape) == (64, 64, 3, 3)
-            and x.dtype == torch.bfloat16 and dy.dtype == torch.bfloat16 and x.dim() == 4
+            and x.dtype in dts and dy.dtype == x.dtype and x.dim() == 4
             and x.shape == dy.shape and x.shape[3] <= 64 and x.is_contiguous(memory_format=cl)
             and dy.is_contiguous(memory_format=cl) and x.data_ptr() % 16 == 0 and dy.data_ptr() % 16 == 0)
 
@@ -73,12 +77,12 @@ def conv_c64_wgrad(dy: torch.Tensor, x: torch.Tensor, weight: torch.Tensor) -> t
     gw = flat_grad(weight) if _direct(weight) else None
     if gw is not None and gw.dtype in (torch.float32, torch.bfloat16):
         h.conv3x3_c64_wgrad(x.data_ptr(), dy.data_ptr(), gw.data_ptr(), *gw.stride(), ws.data_ptr(), n, hh, ww, True,
-                            N.dtype_code(gw.dtype), N.stream_of(x))
+                            N.dtype_code(gw.dtype), N.stream_of(x), N.dtype_code(x.dtype))
         _ready(weight)
         return None
     dw = torch.empty(weight.shape, dtype=torch.float32, device=x.device)
     h.conv3x3_c64_wgrad(x.data_ptr(), dy.data_ptr(), dw.data_ptr(), *dw.stride(), ws.data_ptr(), n, hh, ww, False,
-                        N.dtype_code(dw.dtype), N.stream_of(x))
+                        N.dtype_code(dw.dtype), N.stream_of(x), N.dtype_code(x.dtype))
     return dw.to(weight.dtype)
 
 
