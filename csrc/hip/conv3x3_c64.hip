@@ -190,14 +190,15 @@ __global__ __launch_bounds__(kThreads, 1) void conv3x3_c64_wgrad_kernel(C64Args 
 // and the f32 MFMA's operand layout (lane l: A[i = l&31][k = l>>5], B[k = l>>5][j = l&31]) is
 // the pixel-major [px][channel] LDS image read straight -- 32 consecutive channels of one
 // pixel per lane half, no transposed reads.  Same work split (wave w: output-channel tile
-// w & 1, 9 of the 18 (tap, 32-channel block) tiles, 144 accumulators), same 4-slot ring of
-// input rows (zero rows / pad pixels outside the image), one row of prefetch in registers
-// (a row is ~6.7 us of MFMA work per wave at 56 pixels, far longer than a load's latency),
-// LDS operands of the next pixel pair read while the current pair's 9 MFMAs issue.
-constexpr int kFPitch = 68;                     // floats per LDS pixel (64 + 4: 16-byte rows)
-constexpr int kFSlot = kRingPx * kFPitch;       // floats per ring row
-constexpr int kFChunks = kMaxW * 16;            // float4 chunks of a 64-pixel row
-constexpr int kFPf = kFChunks / kThreads;       // 4 per thread
+// w & 1, 9 of the 18 (tap, 32-channel block) tiles, 144 accumulators) and 4-slot ring of input
+// rows.  The rows arrive by LDS-DMA (global_load_lds_dwordx4: an NHWC row is W x 256 contiguous
+// bytes, the LDS image is unpadded [px][64 floats]): the next row's new input row and dY row
+// are issued at the start of a row into buffers nobody reads during it (ring slot h + 2 and
+// the other dY buffer) and waited for only before the row's closing barrier -- register
+// prefetch did not survive compilation (the loads were sunk to their use after the MFMA loop,
+// or the pad select hoisted above it: one exposed memory latency per chunk, half the time).
+constexpr int kFPitch = 64;                     // floats per LDS pixel (DMA writes linearly)
+constexpr int kFSlot = kRingPx * kFPitch;       // floats per ring row (pad pixel each side)
 
 struct C64ArgsF {
   const float* x;   // [N][H][W][64]
@@ -207,29 +208,40 @@ struct C64ArgsF {
 };
 
 typedef float c64_f32x16f __attribute__((ext_vector_type(16)));
+typedef __attribute__((address_space(3))) void c64_lds_void;
 
-__device__ __forceinline__ float4 c64f_xchunk(const C64ArgsF& a, int64_t n, int hi, int c) {
-  const int px = c >> 4, part = c & 15;
-  const bool ok = unsigned(hi) < unsigned(a.H) && px < a.W;
-  const int hc = min(max(hi, 0), a.H - 1), pc = min(px, a.W - 1);
-  const float4 v = reinterpret_cast<const float4*>(a.x + ((n * a.H + hc) * a.W + pc) * kC)[part];
-  return ok ? v : make_float4(0.f, 0.f, 0.f, 0.f);
+// LDS[m0 + 16 * lane] = global[gptr] (inline asm: hipcc must not see an LDS write in flight,
+// or it would guard every LDS read of the row with a wait on it)
+__device__ __forceinline__ void c64_dma16(const void* gptr, uint32_t lds_addr) {
+  asm volatile("s_mov_b32 m0, %1\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(gptr), "s"(lds_addr) : "memory", "m0");
 }
 
+// one row of `pieces` 16-byte pieces from global `src` to LDS `dst`, 1 KB per wave-instruction,
+// instructions dealt round-robin to the 4 waves; lanes past the row stay idle (exec-masked)
+__device__ __forceinline__ void c64_dma_row(const float* src, float* dst, int pieces, int wave, int lane) {
+  for (int i = wave; i * 64 < pieces; i += 4) {
+    const uint32_t m0 = __builtin_amdgcn_readfirstlane(uint32_t(size_t((c64_lds_void*)(dst + 256 * i))));
+    const int piece = i * 64 + lane;
+    if (piece < pieces) c64_dma16(src + 4 * piece, m0);
+  }
+}
+
+__device__ __forceinline__ void c64_wait_dma() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+
 __global__ __launch_bounds__(kThreads, 1) void conv3x3_c64_wgrad_f32_kernel(C64ArgsF a) {
-  __shared__ __attribute__((aligned(16))) float ring[kSlots * kFSlot];
-  __shared__ __attribute__((aligned(16))) float dyt[kMaxW * kFPitch];
+  __shared__ __attribute__((aligned(1024))) float ring[kSlots * kFSlot];
+  __shared__ __attribute__((aligned(1024))) float dyt[2][kMaxW * kFPitch];  // this row's / the next row's dY
 
   const int tid = threadIdx.x;
-  const int wave = tid >> 6, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
   const int lh = lane >> 5, lr = lane & 31;
   const int ct = wave & 1;
   const int kt0 = (wave >> 1) * 9;
 
-  // everything zero once: pad pixels, pixels >= W and the dY pixels >= W stay zero (the
-  // staging below writes input pixels 1..W of a ring row and dY pixels 0..W-1 only)
+  // everything zero once: pad pixels, pixels >= W and the dY pixels >= W stay zero (the DMA
+  // writes input pixels 1..W of a ring row and dY pixels 0..W-1 only)
   for (int i = tid; i < kSlots * kFSlot / 4; i += kThreads) reinterpret_cast<float4*>(ring)[i] = make_float4(0.f, 0.f, 0.f, 0.f);
-  for (int i = tid; i < kMaxW * kFPitch / 4; i += kThreads) reinterpret_cast<float4*>(dyt)[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+  for (int i = tid; i < 2 * kMaxW * kFPitch / 4; i += kThreads) reinterpret_cast<float4*>(&dyt[0][0])[i] = make_float4(0.f, 0.f, 0.f, 0.f);
 
   c64_f32x16f acc[9];
 #pragma unroll
@@ -239,37 +251,39 @@ __global__ __launch_bounds__(kThreads, 1) void conv3x3_c64_wgrad_f32_kernel(C64A
   const int64_t per = (rows + gridDim.x - 1) / gridDim.x;
   const int64_t r0 = int64_t(blockIdx.x) * per;
   const int64_t r1 = r0 + per < rows ? r0 + per : rows;
-  const int chunks = a.W * 16;
+  const int pieces = a.W * 16;
   const int steps = (a.W + 1) / 2;
 
   int64_t n = r0 / a.H;
   int h = int(r0 - n * a.H);
-  float4 xr[kFPf], dr[kFPf];
-  auto put_x = [&](int hi, int c, const float4& v) {
-    if (c < chunks) *reinterpret_cast<float4*>(ring + (hi & (kSlots - 1)) * kFSlot + ((c >> 4) + 1) * kFPitch + (c & 15) * 4) = v;
+  // input row hi of image n into its ring slot (pixels 1..W); rows outside the image: zeros
+  auto stage_x = [&](int hi) {
+    float* slot = ring + (hi & (kSlots - 1)) * kFSlot;
+    if (unsigned(hi) < unsigned(a.H)) {
+      c64_dma_row(a.x + (n * a.H + hi) * int64_t(a.W) * kC, slot + kFPitch, pieces, wave, lane);
+    } else {
+      for (int i = tid; i < pieces; i += kThreads)
+        reinterpret_cast<float4*>(slot + kFPitch)[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+    }
   };
-  auto put_dy = [&](int c, const float4& v) {
-    if (c < chunks) *reinterpret_cast<float4*>(dyt + (c >> 4) * kFPitch + (c & 15) * 4) = v;
-  };
+  int buf = 0;
   bool in_lds = false;
   __syncthreads();
   for (int64_t row = r0; row < r1; ++row) {
     if (!in_lds) {  // first row of the chunk or of an image: input rows h-1 .. h+1 and the dY row
-      for (int r = 0; r < 3; ++r)
-        for (int c = tid; c < chunks; c += kThreads) put_x(h - 1 + r, c, c64f_xchunk(a, n, h - 1 + r, c));
-      for (int c = tid; c < chunks; c += kThreads) put_dy(c, reinterpret_cast<const float4*>(a.dy + row * a.W * kC)[c]);
+      stage_x(h - 1);
+      stage_x(h);
+      stage_x(h + 1);
+      c64_dma_row(a.dy + row * a.W * kC, dyt[buf], pieces, wave, lane);
+      c64_wait_dma();
+      __syncthreads();
     }
-    __syncthreads();
     const bool nxt = row + 1 < r1 && h + 1 < a.H;
-    if (nxt) {  // the next row's new input row (h + 2) and dY row, in flight during this row
-#pragma unroll
-      for (int j = 0; j < kFPf; ++j) {
-        const int c = tid + j * kThreads;
-        xr[j] = c64f_xchunk(a, n, h + 2, min(c, kFChunks - 1));
-        dr[j] = reinterpret_cast<const float4*>(a.dy + (row + 1) * a.W * kC)[min(c, chunks - 1)];
-      }
+    if (nxt) {  // the next row's new input row (h + 2) and dY row, landing during this row
+      stage_x(h + 2);
+      c64_dma_row(a.dy + (row + 1) * a.W * kC, dyt[buf ^ 1], pieces, wave, lane);
     }
-    const float* ap = dyt + lh * kFPitch + 32 * ct + lr;
+    const float* ap = dyt[buf] + lh * kFPitch + 32 * ct + lr;
     const float* bp[9];
 #pragma unroll
     for (int t = 0; t < 9; ++t) {
@@ -278,32 +292,54 @@ __global__ __launch_bounds__(kThreads, 1) void conv3x3_c64_wgrad_f32_kernel(C64A
       const int kh = tap / 3, kw = tap - 3 * (tap / 3);
       bp[t] = ring + ((h - 1 + kh) & (kSlots - 1)) * kFSlot + (lh + kw) * kFPitch + 32 * cb + lr;
     }
-    float av = ap[0], bv[9];
+    // two register sets, ping-pong over pixel pairs: the operands of the next pair are read
+    // from LDS one per MFMA of the current pair (ds_read / MFMA interleaved by
+    // sched_group_barrier), no copies between the sets
+    float a0 = ap[0], a1, b0[9], b1[9];
 #pragma unroll
-    for (int t = 0; t < 9; ++t) bv[t] = bp[t][0];
-    for (int s = 0; s < steps; ++s) {
-      const int off = 2 * (s + 1 < steps ? s + 1 : s) * kFPitch;  // next pixel pair (clamped)
-      const float an = ap[off];
-      float bn[9];
-#pragma unroll
-      for (int t = 0; t < 9; ++t) bn[t] = bp[t][off];
+    for (int t = 0; t < 9; ++t) b0[t] = bp[t][0];
+    int s = 0;
+    for (; s + 1 < steps; s += 2) {
+      const int o1 = 2 * (s + 1) * kFPitch;
+      const int o2 = 2 * (s + 2 < steps ? s + 2 : steps - 1) * kFPitch;
       __builtin_amdgcn_sched_barrier(0);
+      a1 = ap[o1];
 #pragma unroll
-      for (int t = 0; t < 9; ++t) acc[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(av, bv[t], acc[t], 0, 0, 0);
-      __builtin_amdgcn_sched_barrier(0);
-      av = an;
-#pragma unroll
-      for (int t = 0; t < 9; ++t) bv[t] = bn[t];
-    }
-    __syncthreads();  // every wave is done with this row's dY tile and window
-    if (nxt) {
-#pragma unroll
-      for (int j = 0; j < kFPf; ++j) {
-        put_x(h + 2, tid + j * kThreads, xr[j]);
-        put_dy(tid + j * kThreads, dr[j]);
+      for (int t = 0; t < 9; ++t) {
+        b1[t] = bp[t][o1];
+        acc[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, b0[t], acc[t], 0, 0, 0);
       }
+      __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
+#pragma unroll
+      for (int t = 0; t < 8; ++t) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+        __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+      }
+      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+      __builtin_amdgcn_sched_barrier(0);
+      a0 = ap[o2];
+#pragma unroll
+      for (int t = 0; t < 9; ++t) {
+        b0[t] = bp[t][o2];
+        acc[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b1[t], acc[t], 0, 0, 0);
+      }
+      __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
+#pragma unroll
+      for (int t = 0; t < 8; ++t) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+        __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+      }
+      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+      __builtin_amdgcn_sched_barrier(0);
     }
+    if (s < steps) {
+#pragma unroll
+      for (int t = 0; t < 9; ++t) acc[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, b0[t], acc[t], 0, 0, 0);
+    }
+    c64_wait_dma();   // this wave's pieces of the next row have landed
+    __syncthreads();  // ... and everyone's; this row's reads are done
     in_lds = nxt;
+    if (nxt) buf ^= 1;
     if (++h == a.H) { h = 0; ++n; }
   }
 

@@ -51,8 +51,9 @@ DGRAD_FWD = os.environ.get("VODA_CONV_DGRAD_FWD", "1") != "0"
 CONV_F32_FN = os.environ.get("VODA_CONV_F32_FN", "1") != "0"
 
 # VODA_CONV_C64_WGRAD=0: the 64 -> 64 channel 3x3 weight gradient runs MIOpen (A/B switch);
-# VODA_CONV_C64_WGRAD_F32=1: the f32-MFMA twin for fp32 activations (opt-in: 752 us vs MIOpen's
-# 594 us at bs 256, 56 x 56 -- benchmarks/bench_c64_wgrad.py; the bf16 kernel 141 vs 176 us)
+# VODA_CONV_C64_WGRAD_F32=1: the f32-MFMA twin for fp32 activations (opt-in: 634-652 us vs
+# MIOpen's 557-575 us at bs 256, 56 x 56 -- benchmarks/bench_c64_wgrad.py, profiles/r4/README.md;
+# the bf16 kernel 126 vs 171 us)
 USE_C64_WGRAD = os.environ.get("VODA_CONV_C64_WGRAD", "1") != "0"
 USE_C64_WGRAD_F32 = os.environ.get("VODA_CONV_C64_WGRAD_F32", "0") != "0"
 
