@@ -26,6 +26,8 @@
 
 #include "ops.h"
 
+#include <cstdlib>
+
 namespace voda {
 
 namespace {
@@ -228,6 +230,9 @@ __device__ __forceinline__ void c64_dma_row(const float* src, float* dst, int pi
 
 __device__ __forceinline__ void c64_wait_dma() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
 
+// PROBE (timing experiments only, never a result): 1 = after the first row, skip every row's
+// staging and barrier and recompute on the same LDS rows (isolates the MFMA loop's rate)
+template <int PROBE>
 __global__ __launch_bounds__(kThreads, 1) void conv3x3_c64_wgrad_f32_kernel(C64ArgsF a) {
   __shared__ __attribute__((aligned(1024))) float ring[kSlots * kFSlot];
   __shared__ __attribute__((aligned(1024))) float dyt[2][kMaxW * kFPitch];  // this row's / the next row's dY
@@ -278,7 +283,7 @@ __global__ __launch_bounds__(kThreads, 1) void conv3x3_c64_wgrad_f32_kernel(C64A
       c64_wait_dma();
       __syncthreads();
     }
-    const bool nxt = row + 1 < r1 && h + 1 < a.H;
+    const bool nxt = PROBE ? false : (row + 1 < r1 && h + 1 < a.H);
     if (nxt) {  // the next row's new input row (h + 2) and dY row, landing during this row
       stage_x(h + 2);
       c64_dma_row(a.dy + (row + 1) * a.W * kC, dyt[buf ^ 1], pieces, wave, lane);
@@ -336,9 +341,11 @@ __global__ __launch_bounds__(kThreads, 1) void conv3x3_c64_wgrad_f32_kernel(C64A
 #pragma unroll
       for (int t = 0; t < 9; ++t) acc[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, b0[t], acc[t], 0, 0, 0);
     }
-    c64_wait_dma();   // this wave's pieces of the next row have landed
-    __syncthreads();  // ... and everyone's; this row's reads are done
-    in_lds = nxt;
+    if constexpr (PROBE == 0) {
+      c64_wait_dma();   // this wave's pieces of the next row have landed
+      __syncthreads();  // ... and everyone's; this row's reads are done
+    }
+    in_lds = PROBE ? true : nxt;
     if (nxt) buf ^= 1;
     if (++h == a.H) { h = 0; ++n; }
   }
@@ -443,7 +450,14 @@ void conv3x3_c64_wgrad(uintptr_t x, uintptr_t dy, uintptr_t dw, int64_t s0, int6
   VODA_CHECK(in_dt == kBF16 || in_dt == kF32, "conv3x3_c64_wgrad: activations must be bf16 or fp32");
   if (in_dt == kF32) {
     C64ArgsF a{reinterpret_cast<const float*>(x), reinterpret_cast<const float*>(dy), part, N, H, W};
-    hipLaunchKernelGGL(conv3x3_c64_wgrad_f32_kernel, dim3(nb), dim3(kThreads), 0, s, a);
+    static const int probe = [] {
+      const char* e = std::getenv("VODA_C64_F32_PROBE");
+      return e ? std::atoi(e) : 0;
+    }();
+    if (probe == 1)
+      hipLaunchKernelGGL(conv3x3_c64_wgrad_f32_kernel<1>, dim3(nb), dim3(kThreads), 0, s, a);
+    else
+      hipLaunchKernelGGL(conv3x3_c64_wgrad_f32_kernel<0>, dim3(nb), dim3(kThreads), 0, s, a);
   } else {
     C64Args a{reinterpret_cast<const uint16_t*>(x), reinterpret_cast<const uint16_t*>(dy), part, N, H, W};
     hipLaunchKernelGGL(conv3x3_c64_wgrad_kernel, dim3(nb), dim3(kThreads), 0, s, a);
