@@ -200,7 +200,6 @@ __global__ __launch_bounds__(kThreads, 1) void conv3x3_c64_wgrad_kernel(C64Args 
 // prefetch did not survive compilation (the loads were sunk to their use after the MFMA loop,
 // or the pad select hoisted above it: one exposed memory latency per chunk, half the time).
 constexpr int kFPitch = 64;                     // floats per LDS pixel (DMA writes linearly)
-constexpr int kFSlot = kRingPx * kFPitch;       // floats per ring row (pad pixel each side)
 
 struct C64ArgsF {
   const float* x;   // [N][H][W][64]
@@ -230,23 +229,73 @@ __device__ __forceinline__ void c64_dma_row(const float* src, float* dst, int pi
 
 __device__ __forceinline__ void c64_wait_dma() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
 
+// One row's MFMAs of a wave.  Tiles are (tap, cb) with the 32-channel blocks of a tap
+// INTERLEAVED: block cb holds input channels 2j + cb (j = lane & 31), so ONE ds_read_b64 of
+// channels (2j, 2j + 1) feeds both blocks' MFMAs -- 5 B reads + 1 A read per pixel pair
+// instead of 9 + 1.  Wave group g (= wave >> 1) owns tiles 0..7 = both blocks of taps
+// 5g .. 5g + 3 (pointer pairs q = 0..3) and tile 8 = (tap 4, cb g) (pair q = 4, component g):
+// the same code for both groups, so no per-group copies of the 144 accumulators.  Two register
+// sets ping-pong over pixel pairs: the next pair's operands are read while the current pair's
+// 9 MFMAs issue.
+__device__ __forceinline__ float c64f_b(const float2 (&b)[5], int t, bool g) {
+  return t < 8 ? ((t & 1) ? b[t >> 1].y : b[t >> 1].x) : (g ? b[4].y : b[4].x);
+}
+
+__device__ __forceinline__ void c64f_row_mfma(c64_f32x16f (&acc)[9], const float* ap, const float* const (&bq)[5],
+                                              int steps, bool g) {
+  float a0 = ap[0], a1;
+  float2 b0[5], b1[5];
+#pragma unroll
+  for (int q = 0; q < 5; ++q) b0[q] = *reinterpret_cast<const float2*>(bq[q]);
+  int s = 0;
+  for (; s + 1 < steps; s += 2) {
+    const int o1 = 2 * (s + 1) * kFPitch;
+    const int o2 = 2 * (s + 2 < steps ? s + 2 : steps - 1) * kFPitch;
+    __builtin_amdgcn_sched_barrier(0);
+    a1 = ap[o1];
+#pragma unroll
+    for (int q = 0; q < 5; ++q) b1[q] = *reinterpret_cast<const float2*>(bq[q] + o1);
+#pragma unroll
+    for (int t = 0; t < 9; ++t) acc[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, c64f_b(b0, t, g), acc[t], 0, 0, 0);
+    __builtin_amdgcn_sched_barrier(0);
+    a0 = ap[o2];
+#pragma unroll
+    for (int q = 0; q < 5; ++q) b0[q] = *reinterpret_cast<const float2*>(bq[q] + o2);
+#pragma unroll
+    for (int t = 0; t < 9; ++t) acc[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, c64f_b(b1, t, g), acc[t], 0, 0, 0);
+  }
+  __builtin_amdgcn_sched_barrier(0);
+  if (s < steps) {
+#pragma unroll
+    for (int t = 0; t < 9; ++t) acc[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, c64f_b(b0, t, g), acc[t], 0, 0, 0);
+  }
+}
+
+// WMAX: widest image row the LDS image holds.  WMAX = 56 (ResNet layer1) fits two workgroups
+// per CU (73.7 KB: a 4-slot ring of 58-pixel rows + ONE dY row buffer; 69 VGPRs + 144 AGPRs
+// leave room for two waves per SIMD), so one workgroup's row boundary -- closing barrier, dY
+// DMA, wait -- overlaps the other's MFMAs.  WMAX = 64: one workgroup per CU, dY double-
+// buffered and fetched during the previous row.
 // PROBE (timing experiments only, never a result): 1 = after the first row, skip every row's
 // staging and barrier and recompute on the same LDS rows (isolates the MFMA loop's rate)
-template <int PROBE>
-__global__ __launch_bounds__(kThreads, 1) void conv3x3_c64_wgrad_f32_kernel(C64ArgsF a) {
-  __shared__ __attribute__((aligned(1024))) float ring[kSlots * kFSlot];
-  __shared__ __attribute__((aligned(1024))) float dyt[2][kMaxW * kFPitch];  // this row's / the next row's dY
+template <int WMAX, int PROBE>
+__global__ __launch_bounds__(kThreads, WMAX <= 56 ? 2 : 1) void conv3x3_c64_wgrad_f32_kernel(C64ArgsF a) {
+  constexpr bool DBUF = WMAX > 56;
+  constexpr int SLOT = (WMAX + 2) * kFPitch;  // floats per ring row (pad pixel each side)
+  __shared__ __attribute__((aligned(1024))) float ring[kSlots * SLOT];
+  __shared__ __attribute__((aligned(1024))) float dyt[DBUF ? 2 : 1][WMAX * kFPitch];
 
   const int tid = threadIdx.x;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
   const int lh = lane >> 5, lr = lane & 31;
   const int ct = wave & 1;
-  const int kt0 = (wave >> 1) * 9;
+  const int grp = wave >> 1;  // tile group (see c64f_row_mfma)
 
   // everything zero once: pad pixels, pixels >= W and the dY pixels >= W stay zero (the DMA
   // writes input pixels 1..W of a ring row and dY pixels 0..W-1 only)
-  for (int i = tid; i < kSlots * kFSlot / 4; i += kThreads) reinterpret_cast<float4*>(ring)[i] = make_float4(0.f, 0.f, 0.f, 0.f);
-  for (int i = tid; i < 2 * kMaxW * kFPitch / 4; i += kThreads) reinterpret_cast<float4*>(&dyt[0][0])[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+  for (int i = tid; i < kSlots * SLOT / 4; i += kThreads) reinterpret_cast<float4*>(ring)[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+  for (int i = tid; i < (DBUF ? 2 : 1) * WMAX * kFPitch / 4; i += kThreads)
+    reinterpret_cast<float4*>(&dyt[0][0])[i] = make_float4(0.f, 0.f, 0.f, 0.f);
 
   c64_f32x16f acc[9];
 #pragma unroll
@@ -263,7 +312,7 @@ __global__ __launch_bounds__(kThreads, 1) void conv3x3_c64_wgrad_f32_kernel(C64A
   int h = int(r0 - n * a.H);
   // input row hi of image n into its ring slot (pixels 1..W); rows outside the image: zeros
   auto stage_x = [&](int hi) {
-    float* slot = ring + (hi & (kSlots - 1)) * kFSlot;
+    float* slot = ring + (hi & (kSlots - 1)) * SLOT;
     if (unsigned(hi) < unsigned(a.H)) {
       c64_dma_row(a.x + (n * a.H + hi) * int64_t(a.W) * kC, slot + kFPitch, pieces, wave, lane);
     } else {
@@ -284,79 +333,44 @@ __global__ __launch_bounds__(kThreads, 1) void conv3x3_c64_wgrad_f32_kernel(C64A
       __syncthreads();
     }
     const bool nxt = PROBE ? false : (row + 1 < r1 && h + 1 < a.H);
-    if (nxt) {  // the next row's new input row (h + 2) and dY row, landing during this row
+    if (nxt) {  // the next row's new input row (h + 2) [and dY row], landing during this row
       stage_x(h + 2);
-      c64_dma_row(a.dy + (row + 1) * a.W * kC, dyt[buf ^ 1], pieces, wave, lane);
+      if constexpr (DBUF) c64_dma_row(a.dy + (row + 1) * a.W * kC, dyt[buf ^ 1], pieces, wave, lane);
     }
     const float* ap = dyt[buf] + lh * kFPitch + 32 * ct + lr;
-    const float* bp[9];
+    const float* bq[5];  // taps 5g .. 5g + 3 and tap 4, channels (2j, 2j + 1)
 #pragma unroll
-    for (int t = 0; t < 9; ++t) {
-      const int kt = kt0 + t;
-      const int tap = kt >> 1, cb = kt & 1;
+    for (int q = 0; q < 5; ++q) {
+      const int tap = q < 4 ? 5 * grp + q : 4;
       const int kh = tap / 3, kw = tap - 3 * (tap / 3);
-      bp[t] = ring + ((h - 1 + kh) & (kSlots - 1)) * kFSlot + (lh + kw) * kFPitch + 32 * cb + lr;
+      bq[q] = ring + ((h - 1 + kh) & (kSlots - 1)) * SLOT + (lh + kw) * kFPitch + 2 * lr;
     }
-    // two register sets, ping-pong over pixel pairs: the operands of the next pair are read
-    // from LDS one per MFMA of the current pair (ds_read / MFMA interleaved by
-    // sched_group_barrier), no copies between the sets
-    float a0 = ap[0], a1, b0[9], b1[9];
-#pragma unroll
-    for (int t = 0; t < 9; ++t) b0[t] = bp[t][0];
-    int s = 0;
-    for (; s + 1 < steps; s += 2) {
-      const int o1 = 2 * (s + 1) * kFPitch;
-      const int o2 = 2 * (s + 2 < steps ? s + 2 : steps - 1) * kFPitch;
-      __builtin_amdgcn_sched_barrier(0);
-      a1 = ap[o1];
-#pragma unroll
-      for (int t = 0; t < 9; ++t) {
-        b1[t] = bp[t][o1];
-        acc[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, b0[t], acc[t], 0, 0, 0);
-      }
-      __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
-#pragma unroll
-      for (int t = 0; t < 8; ++t) {
-        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-        __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
-      }
-      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-      __builtin_amdgcn_sched_barrier(0);
-      a0 = ap[o2];
-#pragma unroll
-      for (int t = 0; t < 9; ++t) {
-        b0[t] = bp[t][o2];
-        acc[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b1[t], acc[t], 0, 0, 0);
-      }
-      __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
-#pragma unroll
-      for (int t = 0; t < 8; ++t) {
-        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-        __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
-      }
-      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-      __builtin_amdgcn_sched_barrier(0);
-    }
-    if (s < steps) {
-#pragma unroll
-      for (int t = 0; t < 9; ++t) acc[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, b0[t], acc[t], 0, 0, 0);
-    }
+    c64f_row_mfma(acc, ap, bq, steps, grp != 0);
     if constexpr (PROBE == 0) {
-      c64_wait_dma();   // this wave's pieces of the next row have landed
-      __syncthreads();  // ... and everyone's; this row's reads are done
+      if constexpr (DBUF) {
+        c64_wait_dma();   // this wave's pieces of the next row have landed
+        __syncthreads();  // ... and everyone's; this row's reads are done
+      } else {
+        __syncthreads();  // this row's dY reads done: the single buffer takes the next row
+        if (nxt) c64_dma_row(a.dy + (row + 1) * a.W * kC, dyt[0], pieces, wave, lane);
+        c64_wait_dma();
+        __syncthreads();
+      }
     }
     in_lds = PROBE ? true : nxt;
-    if (nxt) buf ^= 1;
+    if (DBUF && nxt) buf ^= 1;
     if (++h == a.H) { h = 0; ++n; }
   }
 
-  float* out = a.part + int64_t(blockIdx.x) * kC * kK + lr;
+  float* out = a.part + int64_t(blockIdx.x) * kC * kK + 2 * lr;
 #pragma unroll
   for (int t = 0; t < 9; ++t) {
+    const int tap = t < 8 ? 5 * grp + (t >> 1) : 4, cb = t < 8 ? (t & 1) : grp;
+    const int col = tap * kC + cb;  // tap * 64 + cb (+ 2j): interleaved channel blocks
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
       const int co = 32 * ct + (r & 3) + 8 * (r >> 2) + 4 * lh;
-      out[co * kK + (kt0 + t) * 32] = acc[t][r];
+      out[co * kK + col] = acc[t][r];
     }
   }
 }
@@ -427,14 +441,16 @@ int c64_grid() {
   return g;
 }
 
-int c64_blocks(int N, int H) { return int(std::max<int64_t>(1, std::min<int64_t>(c64_grid(), int64_t(N) * H))); }
+int c64_blocks(int N, int H, int per_cu = 1) {
+  return int(std::max<int64_t>(1, std::min<int64_t>(int64_t(per_cu) * c64_grid(), int64_t(N) * H)));
+}
 
 }  // namespace
 
 constexpr int kMaxSlices = 64;
 
 int64_t conv3x3_c64_wgrad_workspace_floats(int N, int H) {
-  return int64_t(c64_blocks(N, H) + kMaxSlices) * kC * kK;
+  return int64_t(c64_blocks(N, H, 2) + kMaxSlices) * kC * kK;  // the fp32 W <= 56 kernel: 2 per CU
 }
 
 void conv3x3_c64_wgrad(uintptr_t x, uintptr_t dy, uintptr_t dw, int64_t s0, int64_t s1, int64_t s2, int64_t s3,
@@ -443,7 +459,8 @@ void conv3x3_c64_wgrad(uintptr_t x, uintptr_t dy, uintptr_t dw, int64_t s0, int6
   VODA_CHECK(out_dt == kF32 || out_dt == kBF16, "conv3x3_c64_wgrad: dW must be fp32 or bf16");
   VODA_CHECK(x % 16 == 0 && dy % 16 == 0 && ws % 16 == 0, "conv3x3_c64_wgrad: misaligned operands");
   hipStream_t s = as_stream(stream);
-  const int nb = c64_blocks(N, H);
+  const bool f32_two = in_dt == kF32 && W <= 56;
+  const int nb = c64_blocks(N, H, f32_two ? 2 : 1);
   float* part = reinterpret_cast<float*>(ws);
   float* tmp = part + int64_t(nb) * kC * kK;
   const int nsl = std::min(kMaxSlices, nb);
@@ -454,10 +471,12 @@ void conv3x3_c64_wgrad(uintptr_t x, uintptr_t dy, uintptr_t dw, int64_t s0, int6
       const char* e = std::getenv("VODA_C64_F32_PROBE");
       return e ? std::atoi(e) : 0;
     }();
-    if (probe == 1)
-      hipLaunchKernelGGL(conv3x3_c64_wgrad_f32_kernel<1>, dim3(nb), dim3(kThreads), 0, s, a);
-    else
-      hipLaunchKernelGGL(conv3x3_c64_wgrad_f32_kernel<0>, dim3(nb), dim3(kThreads), 0, s, a);
+    if (f32_two) {
+      if (probe == 1) hipLaunchKernelGGL((conv3x3_c64_wgrad_f32_kernel<56, 1>), dim3(nb), dim3(kThreads), 0, s, a);
+      else hipLaunchKernelGGL((conv3x3_c64_wgrad_f32_kernel<56, 0>), dim3(nb), dim3(kThreads), 0, s, a);
+    } else {
+      hipLaunchKernelGGL((conv3x3_c64_wgrad_f32_kernel<kMaxW, 0>), dim3(nb), dim3(kThreads), 0, s, a);
+    }
   } else {
     C64Args a{reinterpret_cast<const uint16_t*>(x), reinterpret_cast<const uint16_t*>(dy), part, N, H, W};
     hipLaunchKernelGGL(conv3x3_c64_wgrad_kernel, dim3(nb), dim3(kThreads), 0, s, a);
