@@ -51,11 +51,12 @@ DGRAD_FWD = os.environ.get("VODA_CONV_DGRAD_FWD", "1") != "0"
 CONV_F32_FN = os.environ.get("VODA_CONV_F32_FN", "1") != "0"
 
 # VODA_CONV_C64_WGRAD=0: the 64 -> 64 channel 3x3 weight gradient runs MIOpen (A/B switch);
-# VODA_CONV_C64_WGRAD_F32=1: the f32-MFMA twin for fp32 activations (opt-in: 634-652 us vs
-# MIOpen's 557-575 us at bs 256, 56 x 56 -- benchmarks/bench_c64_wgrad.py, profiles/r4/README.md;
-# the bf16 kernel 126 vs 171 us)
+# VODA_CONV_C64_WGRAD_F32=0: fp32 activations keep MIOpen's.  The f32-MFMA twin runs 564 us vs
+# MIOpen's 579 us at bs 256, 56 x 56 (benchmarks/bench_c64_wgrad.py); in the fp32 ResNet-50 step
+# it is even with MIOpen's kernel + zero fill (69.39 vs 69.40 ms, profiles/r4/README.md) and
+# writes the flat gradient directly (the bf16 kernel: 126 vs 171 us)
 USE_C64_WGRAD = os.environ.get("VODA_CONV_C64_WGRAD", "1") != "0"
-USE_C64_WGRAD_F32 = os.environ.get("VODA_CONV_C64_WGRAD_F32", "0") != "0"
+USE_C64_WGRAD_F32 = os.environ.get("VODA_CONV_C64_WGRAD_F32", "1") != "0"
 
 
 def c64_ok(dy: torch.Tensor, x: torch.Tensor, weight: torch.Tensor, stride: int, padding: int) -> bool:
