@@ -303,8 +303,11 @@ __global__ __launch_bounds__(kWThreads, 2) void wgrad_f32_kernel(WArgs p) {
     }
   };
 
+  // the wave's 64 rows / 64 columns are two 32-wide MFMA tiles each, INTERLEAVED (tile 0 =
+  // even, tile 1 = odd channels): one ds_read_b64 of channels (2j, 2j + 1) feeds both tiles,
+  // 2 LDS reads per 4 MFMAs instead of 4
   f32x16 c00{}, c01{}, c10{}, c11{};
-  const int an = wn * 64 + lc, bk = TN + wk * 64 + lc;
+  const int an = wn * 64 + 2 * lc, bk = TN + wk * 64 + 2 * lc;
   constexpr int KS = 16 / SW;  // k-steps of a stage per wave
   int m0 = m_beg;
   int buf = 0;
@@ -320,21 +323,22 @@ __global__ __launch_bounds__(kWThreads, 2) void wgrad_f32_kernel(WArgs p) {
     const float* st = lds + buf * STAGE + (2 * sw * KS + lh) * LD;
     // LDS operands one k-step ahead of the MFMAs (register double buffer): the reads of step
     // j + 1 are in flight while the four MFMAs of step j issue
-    float a0 = st[an], a1 = st[an + 32], b0 = st[bk], b1 = st[bk + 32];
+    float2 av = *reinterpret_cast<const float2*>(st + an), bv = *reinterpret_cast<const float2*>(st + bk);
 #pragma unroll
     for (int j = 0; j < KS; ++j) {
-      float na0 = 0.f, na1 = 0.f, nb0 = 0.f, nb1 = 0.f;
+      float2 na = make_float2(0.f, 0.f), nb = make_float2(0.f, 0.f);
       if (j + 1 < KS) {
         const float* row = st + 2 * (j + 1) * LD;
-        na0 = row[an]; na1 = row[an + 32]; nb0 = row[bk]; nb1 = row[bk + 32];
+        na = *reinterpret_cast<const float2*>(row + an);
+        nb = *reinterpret_cast<const float2*>(row + bk);
       }
       __builtin_amdgcn_sched_barrier(0);  // keep the next step's reads ahead of these MFMAs
-      c00 = mfma32(a0, b0, c00);
-      c01 = mfma32(a0, b1, c01);
-      c10 = mfma32(a1, b0, c10);
-      c11 = mfma32(a1, b1, c11);
+      c00 = mfma32(av.x, bv.x, c00);
+      c01 = mfma32(av.x, bv.y, c01);
+      c10 = mfma32(av.y, bv.x, c10);
+      c11 = mfma32(av.y, bv.y, c11);
       __builtin_amdgcn_sched_barrier(0);
-      a0 = na0; a1 = na1; b0 = nb0; b1 = nb1;
+      av = na; bv = nb;
     }
     // the next stage's global loads stay in flight during the MFMAs: their LDS stores (and
     // the vmcnt waits they need) must not be hoisted above them
@@ -372,13 +376,14 @@ __global__ __launch_bounds__(kWThreads, 2) void wgrad_f32_kernel(WArgs p) {
     if (sw > 0) return;
   }
 
-  // ---- epilogue: rows = output channels n (MFMA rows), cols = input channels k (lanes)
+  // ---- epilogue: rows = output channels n (MFMA rows), cols = input channels k (lanes); tile
+  // (ra, ca) holds rows rbase + 2 i + ra and columns cbase + 2 j + ca (interleaved, see above)
   auto store = [&](const f32x16& acc, int rbase, int cbase) {
-    const int col = cbase + lc;
+    const int col = cbase + 2 * lc;
     if (col >= p.K) return;
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
-      const int row = rbase + (r & 3) + 8 * (r >> 2) + 4 * lh;
+      const int row = rbase + 2 * ((r & 3) + 8 * (r >> 2) + 4 * lh);
       if (row < p.N) {
         if (p.S == 1) {
           float* o = p.dw + int64_t(row) * p.K + col;
@@ -391,9 +396,9 @@ __global__ __launch_bounds__(kWThreads, 2) void wgrad_f32_kernel(WArgs p) {
   };
   const int rb = n0 + wn * 64, cb = k0 + wk * 64;
   store(c00, rb, cb);
-  store(c01, rb, cb + 32);
-  store(c10, rb + 32, cb);
-  store(c11, rb + 32, cb + 32);
+  store(c01, rb, cb + 1);
+  store(c10, rb + 1, cb);
+  store(c11, rb + 1, cb + 1);
 }
 
 __global__ __launch_bounds__(256) void wgrad_f32_reduce_kernel(const float* __restrict__ ws, int S, int64_t NK4,

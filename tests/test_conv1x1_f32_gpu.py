@@ -51,7 +51,8 @@ def test_gemm_f32_stats_matches_fp64(M, N, K):
 
 @pytest.mark.parametrize("M,N,K,splits", [(4096, 256, 256, 0), (1000, 64, 512, 0), (3000, 512, 64, 3),
                                           (2500, 64, 128, 0), (2048, 128, 64, 0), (6000, 64, 64, 0),
-                                          (800, 256, 128, 1)])
+                                          (800, 256, 128, 1), (1000, 96, 160, 0), (500, 32, 32, 0),
+                                          (777, 160, 96, 2)])
 def test_wgrad_f32_matches_fp64(M, N, K, splits):
     from vodascheduler_amd.ops import wgrad as W
 
