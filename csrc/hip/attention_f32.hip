@@ -224,7 +224,7 @@ __device__ __forceinline__ void store_row(float* __restrict__ out, int64_t st, i
 }
 
 // ======================================================================== forward
-template <int D, int W>
+template <int D, int W, bool PFT = false>
 __global__ __launch_bounds__(64 * W) void attn_f32_fwd(AttnArgsF a) {
   constexpr int RS = D + 2, DT = D / 32;
   constexpr bool REG = D <= 128;
@@ -247,7 +247,7 @@ __global__ __launch_bounds__(64 * W) void attn_f32_fwd(AttnArgsF a) {
   // 51.2 us, dQ 75.9 -> 81.6 us per layer: the extra VGPRs cost a wave per SIMD); the dK/dV
   // pass keeps it (109.3 -> 94.5 us)
   TileRegs<D, 64 * W> kr, vr;
-  constexpr bool PF = false;
+  constexpr bool PF = PFT && TileRegs<D, 64 * W>::kOn;
   for (int kt = 0; kt < a.Tk; kt += kT) {
     __syncthreads();
     if constexpr (PF) {
@@ -310,7 +310,7 @@ __global__ __launch_bounds__(64 * W) void attn_f32_fwd(AttnArgsF a) {
 }
 
 // ======================================================================== backward: dQ (+ delta)
-template <int D, int W>
+template <int D, int W, bool PFT = false>
 __global__ __launch_bounds__(64 * W) void attn_f32_bwd_dq(AttnArgsF a) {
   constexpr int RS = D + 2, DT = D / 32;
   constexpr bool REG = D <= 64;
@@ -351,7 +351,7 @@ __global__ __launch_bounds__(64 * W) void attn_f32_bwd_dq(AttnArgsF a) {
   // 51.2 us, dQ 75.9 -> 81.6 us per layer: the extra VGPRs cost a wave per SIMD); the dK/dV
   // pass keeps it (109.3 -> 94.5 us)
   TileRegs<D, 64 * W> kr, vr;
-  constexpr bool PF = false;
+  constexpr bool PF = PFT && TileRegs<D, 64 * W>::kOn;
   for (int kt = 0; kt < a.Tk; kt += kT) {
     __syncthreads();
     if constexpr (PF) {
@@ -397,8 +397,11 @@ __global__ __launch_bounds__(64 * W) void attn_f32_bwd_dq(AttnArgsF a) {
 
 // ======================================================================== backward: dK, dV
 // MODE 0: both; 1: dV only; 2: dK only (large head dims: one accumulator set per pass)
+// two waves per SIMD at D <= 64: unbounded, the pass took 226 VGPRs + 64 AGPRs (one wave per
+// SIMD, three rounds of the 768 BERT workgroups); bounded, 256 registers and no spills -- except
+// <64, 2> (68 bytes of scratch), which keeps one wave per SIMD
 template <int D, int W, int MODE>
-__global__ __launch_bounds__(64 * W) void attn_f32_bwd_dkv(AttnArgsF a) {
+__global__ __launch_bounds__(64 * W, (D < 64 || (D == 64 && W != 2)) ? 2 : 1) void attn_f32_bwd_dkv(AttnArgsF a) {
   constexpr int RS = D + 2, DT = D / 32;
   constexpr bool REG = D <= 64;
   constexpr bool DO_DV = MODE != 2, DO_DK = MODE != 1;
@@ -501,6 +504,16 @@ void dispatch_d32(int D, F&& f) {
 
 // waves per workgroup (32 rows each): enough for the rows, at most VODA_ATTN_F32_MAXW (A/B
 // knob, read once; default 4)
+// VODA_ATTN_F32_PF=1: register prefetch of the next K / V tile in the forward and dQ passes too
+// (A/B knob, read once)
+bool f32_pf() {
+  static const bool v = [] {
+    const char* e = std::getenv("VODA_ATTN_F32_PF");
+    return e != nullptr && std::atoi(e) != 0;
+  }();
+  return v;
+}
+
 int f32_maxw() {
   static const int v = [] {
     const char* e = std::getenv("VODA_ATTN_F32_MAXW");
@@ -552,8 +565,12 @@ void attention_fwd_f32(const std::vector<int64_t>& t, int B, int H, int Tq, int 
   dispatch_d32(D, [&](auto dc) {
     dispatch_w32(Tq, [&](auto wc) {
       constexpr int DD = decltype(dc)::value, WW = decltype(wc)::value;
-      hipLaunchKernelGGL((attn_f32_fwd<DD, WW>), dim3((Tq + 32 * WW - 1) / (32 * WW), unsigned(B * H)),
-                         dim3(64 * WW), 0, as_stream(stream), a);
+      if (f32_pf())
+        hipLaunchKernelGGL((attn_f32_fwd<DD, WW, true>), dim3((Tq + 32 * WW - 1) / (32 * WW), unsigned(B * H)),
+                           dim3(64 * WW), 0, as_stream(stream), a);
+      else
+        hipLaunchKernelGGL((attn_f32_fwd<DD, WW>), dim3((Tq + 32 * WW - 1) / (32 * WW), unsigned(B * H)),
+                           dim3(64 * WW), 0, as_stream(stream), a);
     });
   });
   check_launch();
@@ -570,8 +587,12 @@ void attention_bwd_f32(const std::vector<int64_t>& t, int B, int H, int Tq, int 
     constexpr int DD = decltype(dc)::value;
     dispatch_w32(Tq, [&](auto wc) {
       constexpr int WW = decltype(wc)::value;
-      hipLaunchKernelGGL((attn_f32_bwd_dq<DD, WW>), dim3((Tq + 32 * WW - 1) / (32 * WW), unsigned(B * H)),
-                         dim3(64 * WW), 0, s, a);
+      if (f32_pf())
+        hipLaunchKernelGGL((attn_f32_bwd_dq<DD, WW, true>), dim3((Tq + 32 * WW - 1) / (32 * WW), unsigned(B * H)),
+                           dim3(64 * WW), 0, s, a);
+      else
+        hipLaunchKernelGGL((attn_f32_bwd_dq<DD, WW>), dim3((Tq + 32 * WW - 1) / (32 * WW), unsigned(B * H)),
+                           dim3(64 * WW), 0, s, a);
     });
     dispatch_w32(Tk, [&](auto wc) {
       constexpr int WW = decltype(wc)::value;
