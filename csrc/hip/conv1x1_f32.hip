@@ -32,6 +32,7 @@
 #include "ops.h"
 
 #include <algorithm>
+#include <cstdlib>
 
 namespace voda {
 
@@ -401,6 +402,119 @@ __global__ __launch_bounds__(kWThreads, 2) void wgrad_f32_kernel(WArgs p) {
   store(c11, rb + 1, cb + 1);
 }
 
+// ------------------------------------------------------------------------------------------
+// weight gradient, streaming form for narrow outputs (N x K <= 256 x 256 in 64 x 64 blocks):
+// the split-K kernel above stages 32-pixel stages for a handful of MFMAs per block when the
+// whole output is one or two tiles wide (56x56 64 -> 256: 609 us vs MIOpen's 258).  Here a
+// workgroup owns a contiguous pixel range and ALL output blocks (BPW 64 x 64 blocks per wave),
+// 32-pixel chunks of dY and X arrive by LDS-DMA (the [M][N] / [M][K] rows of a chunk are one
+// contiguous span each) into a two-stage ring, and each wave's 64 x 64 block is four 32 x 32
+// tiles with INTERLEAVED channels (tile (a, b) = rows 2i + a, columns 2j + b) so one ds_read_b64
+// of each operand feeds all four MFMAs of a pixel pair.  One fp32 partial per workgroup,
+// summed by wgrad_f32_reduce_kernel.
+typedef __attribute__((address_space(3))) void wf_lds_void;
+
+__device__ __forceinline__ void wf_dma16(const void* gptr, uint32_t lds_addr) {
+  asm volatile("s_mov_b32 m0, %1\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(gptr), "s"(lds_addr) : "memory", "m0");
+}
+__device__ __forceinline__ void wf_wait_dma() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+
+constexpr int kSP = 32;  // pixels per chunk
+
+struct WSArgs {
+  const float* dy;  // [M][N]
+  const float* x;   // [M][K]
+  float* ws;        // [gridDim.x][N][K]
+  int64_t M;
+  int per;          // pixels per workgroup (multiple of kSP)
+};
+
+// `bytes` contiguous bytes from global `src` to LDS `dst`, 1 KB per wave-instruction dealt over
+// the 4 waves (every span here is a multiple of 1 KB)
+__device__ __forceinline__ void wf_dma_span(const float* src, float* dst, int bytes, int wave, int lane) {
+  for (int i = wave; i * 1024 < bytes; i += 4) {
+    const uint32_t m0 = __builtin_amdgcn_readfirstlane(uint32_t(size_t((wf_lds_void*)(dst + 256 * i))));
+    wf_dma16(src + 256 * i + 4 * lane, m0);
+  }
+}
+
+template <int N, int K, int BPW>
+__global__ __launch_bounds__(kWThreads, 1) void wgrad_f32_stream_kernel(WSArgs p) {
+  static_assert((N / 64) * (K / 64) == 4 * BPW, "BPW 64 x 64 blocks per wave");
+  constexpr int STG = kSP * (N + K);  // floats per stage: [32 px][N] dY then [32 px][K] X
+  __shared__ __attribute__((aligned(1024))) float lds[2 * STG];
+  const int tid = threadIdx.x, lane = tid & 63, lc = lane & 31, lh = lane >> 5;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int64_t m0 = int64_t(blockIdx.x) * p.per;
+  const int64_t m1 = min<int64_t>(p.M, m0 + p.per);
+  const int nchunks = int((m1 - m0 + kSP - 1) / kSP);
+
+  f32x16 acc[BPW][4];
+#pragma unroll
+  for (int b = 0; b < BPW; ++b)
+#pragma unroll
+    for (int t = 0; t < 4; ++t) acc[b][t] = f32x16{};
+  int an[BPW], bk[BPW];
+#pragma unroll
+  for (int b = 0; b < BPW; ++b) {
+    const int blk = wave * BPW + b;
+    an[b] = (blk / (K / 64)) * 64 + 2 * lc;       // dY column pair (output rows 2i + a)
+    bk[b] = kSP * N + (blk % (K / 64)) * 64 + 2 * lc;  // X column pair (output columns 2j + b)
+  }
+  // chunk c's full-size spans (the last partial chunk clamps its start so the DMA stays inside
+  // the tensors; its extra leading rows are skipped by the pixel loop)
+  auto issue = [&](int c, float* stg) {
+    int64_t r0 = m0 + int64_t(c) * kSP;
+    if (r0 + kSP > p.M) r0 = p.M - kSP;
+    wf_dma_span(p.dy + r0 * N, stg, kSP * N * 4, wave, lane);
+    wf_dma_span(p.x + r0 * K, stg + kSP * N, kSP * K * 4, wave, lane);
+  };
+  if (nchunks > 0) issue(0, lds);
+  wf_wait_dma();
+  __syncthreads();
+  for (int c = 0; c < nchunks; ++c) {
+    float* cur = lds + (c & 1) * STG;
+    if (c + 1 < nchunks) issue(c + 1, lds + ((c + 1) & 1) * STG);
+    const int64_t r0 = m0 + int64_t(c) * kSP;
+    const int64_t start = r0 + kSP > p.M ? p.M - kSP : r0;  // the rows the DMA fetched
+    const int first = int(r0 - start);                       // rows of an earlier chunk: skip
+    const int valid = int(min<int64_t>(kSP, m1 - r0));
+    // pixel pairs [first, first + valid): an odd tail pairs its last pixel with a zero weight
+    const int npairs = (valid + 1) / 2;
+    for (int s = 0; s < npairs; ++s) {
+      const int px = first + 2 * s + lh;
+      const bool live = 2 * s + lh < valid;
+#pragma unroll
+      for (int b = 0; b < BPW; ++b) {
+        float2 av = *reinterpret_cast<const float2*>(cur + px * N + an[b]);
+        const float2 bv = *reinterpret_cast<const float2*>(cur + px * K + bk[b]);
+        if (!live) av = make_float2(0.f, 0.f);
+        acc[b][0] = mfma32(av.x, bv.x, acc[b][0]);
+        acc[b][1] = mfma32(av.x, bv.y, acc[b][1]);
+        acc[b][2] = mfma32(av.y, bv.x, acc[b][2]);
+        acc[b][3] = mfma32(av.y, bv.y, acc[b][3]);
+      }
+    }
+    wf_wait_dma();
+    __syncthreads();
+  }
+  float* out = p.ws + int64_t(blockIdx.x) * N * K;
+#pragma unroll
+  for (int b = 0; b < BPW; ++b) {
+    const int blk = wave * BPW + b;
+    const int nb = (blk / (K / 64)) * 64, kb = (blk % (K / 64)) * 64;
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      const int ra = t >> 1, cb = t & 1;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int row = nb + 2 * ((r & 3) + 8 * (r >> 2) + 4 * lh) + ra;
+        out[int64_t(row) * K + kb + 2 * lc + cb] = acc[b][t][r];
+      }
+    }
+  }
+}
+
 __global__ __launch_bounds__(256) void wgrad_f32_reduce_kernel(const float* __restrict__ ws, int S, int64_t NK4,
                                                                float* __restrict__ dw, int accumulate) {
   for (int64_t i = blockIdx.x * int64_t(256) + threadIdx.x; i < NK4; i += int64_t(gridDim.x) * 256) {
@@ -415,10 +529,36 @@ __global__ __launch_bounds__(256) void wgrad_f32_reduce_kernel(const float* __re
 
 struct WPlan {
   int wn, wk, sw, tiles_n, tiles_k, S, m_split, grid;
+  int stream = 0;  // 1: wgrad_f32_stream_kernel (grid = S workgroups of m_split pixels)
 };
+
+bool wgrad_f32_stream_env() {
+  static const bool v = [] {
+    const char* e = std::getenv("VODA_WGRAD_F32_STREAM");
+    return e == nullptr || std::atoi(e) != 0;
+  }();
+  return v;
+}
+
+// the narrow-output shapes the streaming kernel covers
+bool wgrad_f32_stream_shape(int64_t M, int N, int K) {
+  return wgrad_f32_stream_env() && M >= 64 * kSP &&
+         ((N == 256 && K == 64) || (N == 64 && K == 256) || (N == 128 && K == 256) || (N == 256 && K == 128));
+}
 
 WPlan wgrad_f32_plan(int M, int N, int K, int splits) {
   WPlan pl;
+  if (splits <= 0 && wgrad_f32_stream_shape(M, N, K)) {
+    pl.stream = 1;
+    pl.wn = pl.wk = pl.sw = 0;
+    pl.tiles_n = pl.tiles_k = 1;
+    const int nb = std::max(1, std::min(2 * f32_cus(), M / (4 * kSP)));
+    const int per_chunks = ((M + kSP - 1) / kSP + nb - 1) / nb;
+    pl.m_split = per_chunks * kSP;
+    pl.S = (M + pl.m_split - 1) / pl.m_split;
+    pl.grid = pl.S;
+    return pl;
+  }
   // wave layout: the widest output tile that the channel counts fill
   if (N >= 128 && K >= 128) { pl.wn = 2; pl.wk = 2; pl.sw = 1; }
   else if (N < 128 && K >= 256) { pl.wn = 1; pl.wk = 4; pl.sw = 1; }
@@ -471,7 +611,7 @@ void gemm_f32_stats(uintptr_t x, uintptr_t w, uintptr_t y, uintptr_t part, int64
 
 int64_t wgrad_f32_workspace_floats(int M, int N, int K, int splits) {
   const WPlan pl = wgrad_f32_plan(M, N, K, splits);
-  return pl.S > 1 ? int64_t(pl.S) * N * K : 0;
+  return (pl.S > 1 || pl.stream) ? int64_t(pl.S) * N * K : 0;
 }
 
 std::vector<int> wgrad_f32_config(int M, int N, int K, int splits) {
@@ -490,6 +630,21 @@ void wgrad_f32(uintptr_t dy, uintptr_t x, uintptr_t dw, int M, int N, int K, int
           pl.grid % 8 == 0 ? 1 : 0};
   hipStream_t s = as_stream(stream);
   const dim3 g(unsigned(pl.grid)), b(kWThreads);
+  if (pl.stream) {
+    VODA_CHECK(ws != 0, "wgrad_f32: the streaming form needs its workspace");
+    WSArgs sa{reinterpret_cast<const float*>(dy), reinterpret_cast<const float*>(x), reinterpret_cast<float*>(ws),
+              int64_t(M), pl.m_split};
+    if (N == 256 && K == 64) hipLaunchKernelGGL((wgrad_f32_stream_kernel<256, 64, 1>), g, b, 0, s, sa);
+    else if (N == 64 && K == 256) hipLaunchKernelGGL((wgrad_f32_stream_kernel<64, 256, 1>), g, b, 0, s, sa);
+    else if (N == 128 && K == 256) hipLaunchKernelGGL((wgrad_f32_stream_kernel<128, 256, 2>), g, b, 0, s, sa);
+    else hipLaunchKernelGGL((wgrad_f32_stream_kernel<256, 128, 2>), g, b, 0, s, sa);
+    check_launch();
+    const int64_t nk4 = int64_t(N) * K / 4;
+    hipLaunchKernelGGL(wgrad_f32_reduce_kernel, dim3(stream_grid(nk4)), dim3(256), 0, s, a.ws, pl.S, nk4, a.dw,
+                       a.accumulate);
+    check_launch();
+    return;
+  }
   if (pl.wn == 2 && pl.wk == 2) hipLaunchKernelGGL((wgrad_f32_kernel<2, 2, 1>), g, b, 0, s, a);
   else if (pl.wn == 1 && pl.wk == 4) hipLaunchKernelGGL((wgrad_f32_kernel<1, 4, 1>), g, b, 0, s, a);
   else if (pl.wn == 4 && pl.wk == 1) hipLaunchKernelGGL((wgrad_f32_kernel<4, 1, 1>), g, b, 0, s, a);
