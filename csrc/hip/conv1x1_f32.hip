@@ -419,7 +419,8 @@ __device__ __forceinline__ void wf_dma16(const void* gptr, uint32_t lds_addr) {
 }
 __device__ __forceinline__ void wf_wait_dma() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
 
-constexpr int kSP = 32;  // pixels per chunk
+constexpr int kSP = 16;      // pixels per chunk
+constexpr int kSStages = 4;  // LDS ring: three chunks in flight while one is computed
 
 struct WSArgs {
   const float* dy;  // [M][N]
@@ -438,11 +439,19 @@ __device__ __forceinline__ void wf_dma_span(const float* src, float* dst, int by
   }
 }
 
+template <int N>
+__device__ __forceinline__ void wf_wait_vm() {
+  static_assert(N >= 0 && N < 64, "vmcnt range");
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
 template <int N, int K, int BPW>
 __global__ __launch_bounds__(kWThreads, 1) void wgrad_f32_stream_kernel(WSArgs p) {
   static_assert((N / 64) * (K / 64) == 4 * BPW, "BPW 64 x 64 blocks per wave");
-  constexpr int STG = kSP * (N + K);  // floats per stage: [32 px][N] dY then [32 px][K] X
-  __shared__ __attribute__((aligned(1024))) float lds[2 * STG];
+  constexpr int STG = kSP * (N + K);  // floats per stage: [kSP px][N] dY then [kSP px][K] X
+  constexpr int PW = (N + K) * kSP / 1024;  // DMA instructions per wave per chunk (4 waves, 1 KB each)
+  static_assert(PW * 4 * 256 == STG, "chunk spans must split evenly over the waves");
+  __shared__ __attribute__((aligned(1024))) float lds[kSStages * STG];
   const int tid = threadIdx.x, lane = tid & 63, lc = lane & 31, lh = lane >> 5;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int64_t m0 = int64_t(blockIdx.x) * p.per;
@@ -458,23 +467,28 @@ __global__ __launch_bounds__(kWThreads, 1) void wgrad_f32_stream_kernel(WSArgs p
 #pragma unroll
   for (int b = 0; b < BPW; ++b) {
     const int blk = wave * BPW + b;
-    an[b] = (blk / (K / 64)) * 64 + 2 * lc;       // dY column pair (output rows 2i + a)
+    an[b] = (blk / (K / 64)) * 64 + 2 * lc;            // dY column pair (output rows 2i + a)
     bk[b] = kSP * N + (blk % (K / 64)) * 64 + 2 * lc;  // X column pair (output columns 2j + b)
   }
   // chunk c's full-size spans (the last partial chunk clamps its start so the DMA stays inside
   // the tensors; its extra leading rows are skipped by the pixel loop)
-  auto issue = [&](int c, float* stg) {
+  auto issue = [&](int c) {
+    float* stg = lds + (c % kSStages) * STG;
     int64_t r0 = m0 + int64_t(c) * kSP;
     if (r0 + kSP > p.M) r0 = p.M - kSP;
     wf_dma_span(p.dy + r0 * N, stg, kSP * N * 4, wave, lane);
     wf_dma_span(p.x + r0 * K, stg + kSP * N, kSP * K * 4, wave, lane);
   };
-  if (nchunks > 0) issue(0, lds);
-  wf_wait_dma();
-  __syncthreads();
+  // kSStages - 1 chunks in flight ahead of the one being computed
+  for (int c = 0; c < kSStages - 1 && c < nchunks; ++c) issue(c);
   for (int c = 0; c < nchunks; ++c) {
-    float* cur = lds + (c & 1) * STG;
-    if (c + 1 < nchunks) issue(c + 1, lds + ((c + 1) & 1) * STG);
+    const int ahead = min(kSStages - 2, nchunks - 1 - c);  // chunks after c already issued
+    if (ahead >= 2) wf_wait_vm<2 * PW>();
+    else if (ahead == 1) wf_wait_vm<PW>();
+    else wf_wait_vm<0>();
+    __syncthreads();  // chunk c landed for every wave; chunk c - 1's stage is free again
+    if (c + kSStages - 1 < nchunks) issue(c + kSStages - 1);
+    const float* cur = lds + (c % kSStages) * STG;
     const int64_t r0 = m0 + int64_t(c) * kSP;
     const int64_t start = r0 + kSP > p.M ? p.M - kSP : r0;  // the rows the DMA fetched
     const int first = int(r0 - start);                       // rows of an earlier chunk: skip
@@ -495,8 +509,6 @@ __global__ __launch_bounds__(kWThreads, 1) void wgrad_f32_stream_kernel(WSArgs p
         acc[b][3] = mfma32(av.y, bv.y, acc[b][3]);
       }
     }
-    wf_wait_dma();
-    __syncthreads();
   }
   float* out = p.ws + int64_t(blockIdx.x) * N * K;
 #pragma unroll
@@ -542,7 +554,7 @@ bool wgrad_f32_stream_env() {
 
 // the narrow-output shapes the streaming kernel covers
 bool wgrad_f32_stream_shape(int64_t M, int N, int K) {
-  return wgrad_f32_stream_env() && M >= 64 * kSP &&
+  return wgrad_f32_stream_env() && M >= 128 * kSP &&
          ((N == 256 && K == 64) || (N == 64 && K == 256) || (N == 128 && K == 256) || (N == 256 && K == 128));
 }
 
