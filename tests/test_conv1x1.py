@@ -183,3 +183,14 @@ def test_bottleneck_grad_sink_matches_autograd_sum(downsample, monkeypatch):
     for n in pg_r:
         e0, e1 = _rel(pg0[n], pg_r[n]), _rel(pg1[n], pg_r[n])
         assert e1 < 0.2 and e1 < 1.1 * e0 + 5e-3, (n, e0, e1)
+
+
+def test_blas_wgrad_f32_rule():
+    """fp32 1x1 weight gradients go to hipBLASLt only for short reductions into wide outputs
+    (ResNet-50 stage 4 at bs 256), MIOpen keeps the rest (profiles/r4/blas_wgrad_f32_ab.jsonl)."""
+    from vodascheduler_amd.ops.conv1x1 import blas_wgrad_f32_ok
+
+    assert blas_wgrad_f32_ok(256 * 49, 2048, 512) and blas_wgrad_f32_ok(256 * 49, 512, 2048)
+    assert blas_wgrad_f32_ok(256 * 49, 2048, 1024)          # stride-2 shortcut into stage 4
+    assert not blas_wgrad_f32_ok(256 * 196, 1024, 256)      # stage 3: MIOpen 220 vs 558 us
+    assert not blas_wgrad_f32_ok(256 * 49, 512, 512)        # narrow output

@@ -75,10 +75,12 @@ def test_wgrad_f32_matches_fp64(M, N, K, splits):
 
 
 @pytest.mark.parametrize("cin,cout,stride,hw", [(64, 256, 1, 14), (256, 64, 1, 9), (128, 512, 1, 7),
-                                               (512, 1024, 2, 14), (1024, 256, 1, 7), (256, 512, 2, 8)])
+                                               (512, 1024, 2, 14), (1024, 256, 1, 7), (256, 512, 2, 8),
+                                               (512, 2048, 1, 7), (1024, 2048, 2, 14)])
 def test_conv1x1_fp32_gemm_path_matches_fp64(cin, cout, stride, hw):
     """fp32 channels_last Conv1x1 on the GEMM path (own forward / input gradient where K is 64 /
-    128 / 256, hipBLASLt elsewhere, split-K weight gradient into the fp32 flat gradient)."""
+    128 / 256, hipBLASLt elsewhere, weight gradient folded into the fp32 flat gradient -- from
+    MIOpen, or from one beta = 1 hipBLASLt GEMM for the wide stage-4 outputs)."""
     from vodascheduler_amd.ops.conv1x1 import Conv1x1
     from vodascheduler_amd.ops.optim import make_optimizer
     from vodascheduler_amd.utils.flat import grad_of

@@ -67,6 +67,19 @@ USE_GEMM_F32 = os.environ.get("VODA_GEMM_F32", "1") != "0"
 # profiles/r4/resnet50_fp32_1x1_own_vs_miopen.jsonl); in the ResNet-50 fp32 step: 80.0 ms with
 # the kernel vs 75.4 ms with MIOpen's (profiles/r4/rocprof_resnet50_fp32_*.md)
 USE_WGRAD_F32 = os.environ.get("VODA_WGRAD_F32", "0") != "0"
+# ... except the short-reduction, wide-output ones (stage 4 of ResNet-50: 7x7 maps, M = 12544
+# pixels into 1M-2M weights), where one hipBLASLt GEMM with beta = 1 into the flat gradient
+# runs 189-199 us vs MIOpen's 214-226 us plus the fold-in add, and 353 vs 417-434 us on the
+# stride-2 1024 -> 2048 shortcut (profiles/r4/resnet50_fp32_1x1_wgrad_*.jsonl).  MIOpen wins
+# everywhere M >= 50176.  VODA_BLAS_WGRAD_F32=0 keeps them on MIOpen (A/B switch)
+USE_BLAS_WGRAD_F32 = os.environ.get("VODA_BLAS_WGRAD_F32", "1") != "0"
+BLAS_WGRAD_F32_MAX_M = 16384
+BLAS_WGRAD_F32_MIN_OUT = 1 << 20
+
+
+def blas_wgrad_f32_ok(m: int, cout: int, cin: int) -> bool:
+    """fp32 1x1 weight gradient [cout, cin] = dY[m, cout]^T . X[m, cin] on hipBLASLt?"""
+    return USE_BLAS_WGRAD_F32 and m <= BLAS_WGRAD_F32_MAX_M and cout * cin >= BLAS_WGRAD_F32_MIN_OUT
 # input gradient accumulated onto a GradSink's shortcut gradient (beta = 1): the MFMA GEMM's
 # read-add epilogue (1) or hipBLASLt's addmm (0, default), per precision.  Measured in the
 # ResNet-50 step (profiles/r4/sink_gemm_ab.md): fp32 69.3 -> 73.0 ms, bf16 23.03 -> 23.10 ms
@@ -330,7 +343,11 @@ class _Conv1x1Fn(torch.autograd.Function):
         dw = None
         if ctx.needs_input_grad[1]:
             g2 = flat_grad(weight).view(cout, cin) if _direct(weight) else None
-            if dy2.dtype == torch.float32 and not USE_WGRAD_F32:
+            if (dy2.dtype == torch.float32 and g2 is not None and g2.dtype == torch.float32
+                    and blas_wgrad_f32_ok(dy2.shape[0], cout, cin)):
+                g2.addmm_(dy2.t(), x2)
+                _ready(weight)
+            elif dy2.dtype == torch.float32 and not USE_WGRAD_F32:
                 xs4 = x2.view(n, h, w, cin).permute(0, 3, 1, 2)
                 dy4 = dy2.view(n, h, w, cout).permute(0, 3, 1, 2)
                 dw4 = torch.ops.aten.convolution_backward(dy4, xs4, weight, None, [1, 1], [0, 0], [1, 1], False,
