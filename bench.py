@@ -280,11 +280,12 @@ def autoscale_schedule(world: int, every_s: float) -> list[tuple[float, int]]:
     return out
 
 
-def predict_wall(trace, algorithm: str, world: int, rate_limit: float, ramp=None) -> float:
-    """Simulated wall time (first submission -> last completion) of ``trace`` on ``world``
-    GPUs under ``algorithm`` (sim/simulator.py: the same service / scheduler / allocator /
-    placement code in virtual time), priced with the measured step times and busbw installed
-    in common.workload.  Warm-pool starts / resizes cost ~0.01-1 s (bench JSON)."""
+def predict(trace, algorithm: str, world: int, rate_limit: float, ramp=None) -> tuple[float, float]:
+    """Simulated (wall time, avg JCT) of ``trace`` on ``world`` GPUs under ``algorithm``
+    (sim/simulator.py: the same service / scheduler / allocator / placement code in virtual
+    time), priced with the measured step times and busbw installed in common.workload; wall
+    = first submission -> last completion.  Warm-pool starts / resizes cost ~0.01-1 s (bench
+    JSON)."""
     from vodascheduler_amd.sim.simulator import simulate
 
     nodes_events = None
@@ -292,7 +293,7 @@ def predict_wall(trace, algorithm: str, world: int, rate_limit: float, ramp=None
         nodes_events = [(t, {"node0": list(range(k))}) for t, k in ramp]
     r = simulate(trace, algorithm=algorithm, gpus=world, rate_limit_sec=rate_limit, tick_sec=1.0,
                  resize_overhead_s=0.3, restart_overhead_s=0.1, capacity=nodes_events)
-    return r.makespan + min(tj.submit_time for tj in trace)
+    return r.makespan + min(tj.submit_time for tj in trace), r.avg_jct
 
 
 def per_world_step_ms(allrec: list[dict]) -> dict:
@@ -430,8 +431,8 @@ def main():
         dist.barrier()
     log(rank, f"warm-up single-GPU step ms: {step_ms}")
     # this box's single-GPU step times at the run's precision price the priors and predictions
-    set_measured_step_times({m: {1: v} for m, v in step_ms.items()})
     trace_prec = "fp32" if not amp else "bf16"
+    set_measured_step_times({m: {1: v} for m, v in step_ms.items()}, trace_prec)
     step_scale = STEP_SCALE[a.precision]
     trace = bench_trace(a.jobs, a.steps * step_scale, world, a.seed, a.interarrival, models, batch,
                         precision=trace_prec, step_time_s={m: v / 1e3 for m, v in step_ms.items()})
@@ -454,7 +455,7 @@ def main():
     # actual wall, and the calibration of the control replay's prediction
     pred: dict = {}
     if rank == 0:
-        pred["main_s"] = predict_wall(trace, a.algorithm, world, a.rate_limit, ramp)
+        pred["main_s"], pred["main_jct_s"] = predict(trace, a.algorithm, world, a.rate_limit, ramp)
         log(0, f"simulator prediction for the timed trace ({a.algorithm}): {pred['main_s']:.1f} s")
 
     # ---------------- timed region ----------------
@@ -489,11 +490,18 @@ def main():
             # the control never costs the measured headline: predicted first, cut off at the
             # deadline, and any failure is reported in ``control`` only
             try:
-                p_ctl = predict_wall(ctl_trace, control, world, a.rate_limit, ramp)
+                p_ctl, p_ctl_jct = predict(ctl_trace, control, world, a.rate_limit, ramp)
                 calib = result["wall_s"] / pred["main_s"] if pred["main_s"] > 0 else 1.0
                 need = p_ctl * max(1.0, calib) * 1.15 + 20
+                # SIMULATED control avg JCT, calibrated by the main trace's measured / predicted
+                # avg JCT: what ``control`` reports when the replay is skipped or cut off, so the
+                # N where vs_baseline matters never ends up with nothing (never the headline)
+                jcal = result["avg_jct_s"] / pred["main_jct_s"] if pred["main_jct_s"] > 0 else 1.0
                 ctl.update(predicted_wall_s=round(p_ctl * calib, 1), predicted_raw_s=round(p_ctl, 1),
-                           calibration=round(calib, 3))
+                           calibration=round(calib, 3), predicted_avg_jct_s=round(p_ctl_jct * jcal, 3),
+                           predicted_avg_jct_raw_s=round(p_ctl_jct, 3), jct_calibration=round(jcal, 3),
+                           predicted_vs_baseline=round(p_ctl_jct * jcal / result["avg_jct_s"], 4)
+                           if result["avg_jct_s"] > 0 else None)
                 if dog.left() < need:
                     ctl.update(status="skipped", reason=(
                         f"{dog.left():.0f} s left before the deadline; the simulator predicts the control "
@@ -564,7 +572,8 @@ def main():
 
             wl = workload_of(tj.spec)
             samples += wl["steps_per_epoch"] * 2 * batch[wl["model"]]
-        pk = ("predicted_wall_s", "predicted_raw_s", "calibration")
+        pk = ("predicted_wall_s", "predicted_raw_s", "calibration", "predicted_avg_jct_s", "predicted_avg_jct_raw_s",
+              "jct_calibration", "predicted_vs_baseline")
         if ctl.get("status") == "ok" and ctl.get("avg_jct_s"):
             control_out = {"algorithm": control, "status": "ok", "avg_jct_s": round(ctl["avg_jct_s"], 3),
                            "makespan_s": round(ctl["makespan_s"], 3), "p95_jct_s": round(ctl["p95_jct_s"], 3),
@@ -574,6 +583,11 @@ def main():
         else:
             control_out = {"algorithm": control, "status": ctl.get("status", "disabled"),
                            "reason": ctl.get("reason", "--control none"), **{k: ctl[k] for k in pk if k in ctl}}
+            if "predicted_avg_jct_s" in control_out:
+                control_out["predicted_note"] = (
+                    "SIMULATED (sim/simulator.py priced with this run's measured step times and busbw, "
+                    "calibrated by the main trace's measured/predicted avg JCT); the control replay did not "
+                    "finish, so vs_baseline is null and predicted_vs_baseline is a prediction, not a measurement")
             vs = None
         line = {
             "metric": BASELINE_METRIC,
@@ -615,6 +629,7 @@ def main():
             "mean_job_steps_1gpu": a.steps * step_scale,
             "step_scale": step_scale,
             "predicted_wall_s": round(pred["main_s"], 1),
+            "predicted_avg_jct_s": round(pred["main_jct_s"], 3),
             "capacity_timeline": result.get("capacity_timeline"),
             "rate_limit_s": a.rate_limit,
             "rate_limit_note": RATE_LIMIT_NOTE,

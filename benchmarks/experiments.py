@@ -9,7 +9,11 @@ curves come from the MI355X-calibrated ``sim.trace.PROFILES``.
   5. FfDL Optimizer, 32-job Philly-style trace, 1/2/4/8 GPUs (all 8 policies side by side),
      and with autoscale: capacity ramping 1 -> 2 -> 4 -> 8 GPUs during the trace
 
-python benchmarks/experiments.py [--out profiles/r3_sim_experiments.md] [--bench-json SCALE.json]
+python benchmarks/experiments.py [--precision fp32] [--out profiles/r5_sim_experiments.md] [--bench-json SCALE.json]
+
+``--precision`` (default fp32, the reference's and the driver bench's precision) is declared by
+every job of every trace: the same steps are priced at that precision's measured step time
+(``common.workload.PROFILES_FP32``; models without an fp32 measurement keep the bf16 one).
 
 Job info (what SRJF / E-Tiresias / FfDL / AFS-L see) follows the real pipeline by default
 (``info_mode="online"``): the training service seeds every job from the workload it declares
@@ -27,8 +31,8 @@ import sys
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from vodascheduler_amd.algorithm import ALGORITHMS  # noqa: E402
 from vodascheduler_amd.sim.simulator import simulate  # noqa: E402
-from vodascheduler_amd.common.workload import (PROFILES, busbw_source, intra_node_busbw,  # noqa: E402
-                                               load_bench_json)
+from vodascheduler_amd.common.workload import (busbw_source, intra_node_busbw, load_bench_json,  # noqa: E402
+                                               model_profile)
 from vodascheduler_amd.sim.trace import (ASSUMED_BUSBW_GBS, ASSUMED_INTERNODE_BUSBW_GBS, TraceJob,  # noqa: E402
                                          make_spec, philly_trace)
 
@@ -44,19 +48,23 @@ HEADER = ("| policy | GPUs | avg JCT (s) | median JCT | p95 JCT | makespan (s) |
           "| migrations |\n|---|---:|---:|---:|---:|---:|---:|---:|---:|---:|")
 
 
+PREC = "fp32"  # compute precision every job declares (main: --precision)
+
+
 def exp2():
-    tr = [TraceJob(60.0 * i, make_spec(f"resnet50-{i}", "resnet50", 4, 1, 8, 10, 2000, category="resnet50"))
+    tr = [TraceJob(60.0 * i, make_spec(f"resnet50-{i}", "resnet50", 4, 1, 8, 10, 2000, category="resnet50",
+                                       precision=PREC))
           for i in range(8)]
     return [simulate(tr, a, gpus=8) for a in ("Tiresias", "ElasticTiresias")]
 
 
 def exp3():
-    tr = philly_trace(32, seed=3, models=("resnet50", "bert-base"))
+    tr = philly_trace(32, seed=3, models=("resnet50", "bert-base"), precision=PREC)
     return [simulate(tr, a, gpus=8) for a in ("FIFO", "ElasticFIFO", "AFS-L")]
 
 
 def exp4():
-    tr = philly_trace(24, seed=4, mean_interarrival_s=20.0)
+    tr = philly_trace(24, seed=4, mean_interarrival_s=20.0, precision=PREC)
     nodes = {"node0": list(range(8)), "node1": list(range(8))}
     drains = [(300.0, "node0", 2), (600.0, "node1", 5), (900.0, "node0", 6)]
     out = []
@@ -70,7 +78,7 @@ def exp5():
     out = []
     for g in (1, 2, 4, 8):
         # requests capped at the cluster size (a non-elastic 8-GPU job can never start on 4 GPUs)
-        tr32 = philly_trace(32, seed=0, max_gpus=g)
+        tr32 = philly_trace(32, seed=0, max_gpus=g, precision=PREC)
         for a in ORDER:
             out.append(simulate(tr32, a, gpus=g))
     return out
@@ -83,7 +91,7 @@ def exp_autoscale():
     """BASELINE config 5's "autoscale 1->8": the config-5 trace while the cluster grows 1 -> 2 ->
     4 -> 8 GPUs (one doubling every RAMP_T s -- an autoscaler adding nodes), next to a fixed
     8-GPU cluster.  Node addition: reference scheduler.go:689-747, placement_manager.go:239-304."""
-    tr = philly_trace(32, seed=0, max_gpus=8)
+    tr = philly_trace(32, seed=0, max_gpus=8, precision=PREC)
     ramp = [(0.0, {"node0": [0]}), (RAMP_T, {"node0": [0, 1]}), (2 * RAMP_T, {"node0": list(range(4))}),
             (3 * RAMP_T, {"node0": list(range(8))})]
     out = []
@@ -100,7 +108,7 @@ def exp_info():
     info, the real pipeline (default), an oracle."""
     out = []
     for g in (1, 8):
-        tr = philly_trace(32, seed=0, max_gpus=g)
+        tr = philly_trace(32, seed=0, max_gpus=g, precision=PREC)
         fifo = simulate(tr, "FIFO", gpus=g).avg_jct
         for a in INFO_ALGOS:
             row = {"gpus": g, "algorithm": a, "fifo": fifo}
@@ -112,23 +120,34 @@ def exp_info():
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--out", default="profiles/r4_sim_experiments.md")
+    ap.add_argument("--out", default="profiles/r5_sim_experiments.md")
+    ap.add_argument("--precision", default="fp32", choices=["fp32", "bf16"],
+                    help="compute precision every job declares (prices its steps)")
     ap.add_argument("--bench-json", default=None,
                     help="bench.py --out / driver SCALE json with allreduce_busbw_gbs: measured busbw")
     a = ap.parse_args()
+    global PREC
+    PREC = a.precision
     assert set(ORDER) == set(ALGORITHMS)
     if a.bench_json:
         print("measured (busbw GB/s by world, step ms by model/world):", load_bench_json(a.bench_json))
     bw = (f"MEASURED per world ({', '.join(f'{k}: {intra_node_busbw(k):.0f}' for k in (2, 4, 8))} GB/s)"
           if busbw_source() == "measured" else f"ASSUMED ({ASSUMED_BUSBW_GBS:.0f} GB/s intra-node)")
-    lines = ["# BASELINE.json configs in the discrete-event simulator (round 4)", "",
+    rn, bb = model_profile("resnet50", PREC), model_profile("bert-base", PREC)
+    what = ("fp32 compute, the reference's precision and the driver bench's" if PREC == "fp32"
+            else "bf16 autocast compute, fp32 gradients")
+    lines = [f"# BASELINE.json configs in the discrete-event simulator (round 5, {PREC})", "",
              "Real training service / scheduler / allocator / placement code driven in virtual time "
-             "(`benchmarks/experiments.py`). Job speed model (`vodascheduler_amd/common/workload.py`): single-GPU "
-             "step times MEASURED on MI355X (bf16 compute, fp32 gradients; "
-             f"ResNet-50 {PROFILES['resnet50'].step_time_1gpu * 1e3:.2f} ms, "
-             f"BERT-base {PROFILES['bert-base'].step_time_1gpu * 1e3:.2f} ms); "
-             "fp32 gradient bytes exact; ring all-reduce bus bandwidth " + bw + f", {ASSUMED_INTERNODE_BUSBW_GBS:.0f} "
-             "GB/s across nodes (assumed); 30 % of a step hides the all-reduce.  Resize pause 5 s, "
+             f"(`benchmarks/experiments.py --precision {PREC}`). Job speed model (`vodascheduler_amd/common/"
+             f"workload.py`): single-GPU step times MEASURED on MI355X ({what}; "
+             f"ResNet-50 {rn.step_time_1gpu * 1e3:.2f} ms, "
+             f"BERT-base {bb.step_time_1gpu * 1e3:.2f} ms"
+             + ("; VGG16 / Transformer have no fp32 measurement and keep their bf16 step times" if PREC == "fp32"
+                else "") + "); "
+             "fp32 gradient bytes exact; ring all-reduce bus bandwidth **" + bw + "** on every row, "
+             f"{ASSUMED_INTERNODE_BUSBW_GBS:.0f} GB/s across nodes (ASSUMED); 30 % of a step hides the all-reduce.  "
+             "Every job declares its precision and keeps the step count of the bf16 trace, so the fp32 "
+             "tables carry ~3x the GPU-seconds of round 4's bf16 tables.  Resize pause 5 s, "
              "restart-from-checkpoint pause 15 s, rate limit 30 s (reference default).", "",
              "Job info (round 3): every job is seeded at submission from the workload it declares (remaining = "
              "epochs x epoch time on one GPU, speedup = the model's curve), jobs of one model share a category "

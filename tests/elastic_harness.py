@@ -124,7 +124,10 @@ def assert_matches_replay(cfg, path: str, device: str, exact: bool = True,
     replayed through real collectives of that backend (workloads/replay.py): a w-rank ring
     average of identical gradients is not exact, so only a replay that performs the same
     reduction is an oracle.  When the run logged lock-step digests (``step_digests``), a
-    mismatch names the first divergent step."""
+    mismatch names the first divergent step, and the digests are ASSERTED: every field of
+    every common step when ``exact``, the world size and LR of every common step otherwise
+    (only the state digest may differ on GPU), so a one-step LR or world error at a resize
+    cannot hide inside ``tol``."""
     from vodascheduler_amd.workloads.replay import first_divergence, replay_collective
     from vodascheduler_amd.workloads.train import replay_reference
 
@@ -142,7 +145,14 @@ def assert_matches_replay(cfg, path: str, device: str, exact: bool = True,
             ref, ref_ex = replay_reference(cfg, wl, int(ex["__step__"]), torch.device(device))
         finally:
             torch.set_num_threads(nthreads)
-    div = first_divergence(list(ex.get("steplog") or []), list(ref_ex.get("steplog") or []))
+    run_log, ref_log = list(ex.get("steplog") or []), list(ref_ex.get("steplog") or [])
+    div = first_divergence(run_log, ref_log)
+    if run_log or ref_log:  # the run asked for lock-step digests: both logs must hold them
+        assert run_log and ref_log, (len(run_log), len(ref_log))
+        common = {e.split(":", 1)[0] for e in run_log} & {e.split(":", 1)[0] for e in ref_log}
+        assert common, "no common step between the run's and the replay's lock-step logs"
+        sched = first_divergence(run_log, ref_log, fields=("world", "lr"))
+        assert sched is None, sched
     assert len(ref) == len(payload["tensors"])
     for i, (a, b) in enumerate(zip(payload["tensors"], ref)):
         if exact:

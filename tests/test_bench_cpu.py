@@ -60,6 +60,7 @@ def test_bench_eight_ranks_cpu_rehearsal():
     assert d["vs_baseline"] is not None
     # the simulator's predictions (used to decide whether the control fits) next to the actuals
     assert d["predicted_wall_s"] > 0 and d["control"]["predicted_wall_s"] > 0 and d["control"]["wall_s"] > 0
+    assert d["control"]["predicted_avg_jct_s"] > 0 and d["predicted_avg_jct_s"] > 0
     print("predicted vs actual wall (s): main", d["predicted_wall_s"], d["wall_s"],
           "control", d["control"]["predicted_wall_s"], d["control"]["wall_s"])
 
@@ -79,6 +80,11 @@ def test_bench_control_overrun_keeps_headline():
     d = json.loads(lines[0])
     assert d["status"] == "ok" and d["value"] > 0
     assert d["control"]["status"] == "timeout" and d["vs_baseline"] is None, d["control"]
+    # ... and a labelled SIMULATED control avg JCT stands in for it (VERDICT r4 Next #2)
+    c = d["control"]
+    assert c["predicted_avg_jct_s"] > 0 and c["predicted_vs_baseline"] > 0 and "SIMULATED" in c["predicted_note"]
+    assert c["predicted_vs_baseline"] == pytest.approx(c["predicted_avg_jct_s"] / d["value"], rel=1e-2)
+    assert d["predicted_avg_jct_s"] > 0
 
 
 def test_bench_autoscale_eight_ranks_cpu_rehearsal():

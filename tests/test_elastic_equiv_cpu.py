@@ -165,10 +165,20 @@ def test_oracle_catches_one_step_error_at_a_resize(pool8, tmp_path):
     _, bad = replay_collective(cfg, wl, ex["__step__"], "gloo", inject={"lr_step": b, "lr_factor": 2.0})
     msg = first_divergence(ex["steplog"], bad["steplog"])
     assert msg is not None and msg.startswith(f"step {b + 1}:") and "lr" in msg, msg
+    # the relaxed (GPU, exact=False) check ignores the state digest but still names the LR
+    msg = first_divergence(ex["steplog"], bad["steplog"], fields=("world", "lr"))
+    assert msg is not None and msg.startswith(f"step {b + 1}:") and "lr" in msg and "state" not in msg, msg
     shifted = wl[:2] + [b + 1] + wl[3:]                              # the resize one step late
     _, bad = replay_collective(cfg, shifted, ex["__step__"], "gloo")
     msg = first_divergence(ex["steplog"], bad["steplog"])
     assert msg is not None and msg.startswith(f"step {b + 1}:") and "world" in msg, msg
+    msg = first_divergence(ex["steplog"], bad["steplog"], fields=("world", "lr"))
+    assert msg is not None and "world" in msg, msg
+    # end to end: the tolerance-only mode of assert_matches_replay fails on the injected LR
+    # even though the final tensors would pass a loose tolerance
+    with pytest.raises(AssertionError, match="lr"):
+        assert_matches_replay(cfg, cfg.final_state_path, "cpu", exact=False, tol=(1e9, 1e9), backend="gloo",
+                              inject={"lr_step": b, "lr_factor": 2.0})
 
 
 def test_eval_metric_average_across_resizes(pool, tmp_path):

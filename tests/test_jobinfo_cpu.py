@@ -193,7 +193,7 @@ def test_fp32_trace_priced_at_measured_fp32_step_times():
     meas = {"resnet50": 0.0712, "bert-base": 0.0381}
     tr = bench_trace(8, 60, 1, seed=3, precision="fp32", step_time_s=meas,
                      batches={"resnet50": 256, "bert-base": 64})
-    set_measured_step_times({m: {1: v * 1e3} for m, v in meas.items()})
+    set_measured_step_times({m: {1: v * 1e3} for m, v in meas.items()}, "fp32")
     try:
         store, svc = _svc()
         for tj in tr:
@@ -209,5 +209,26 @@ def test_fp32_trace_priced_at_measured_fp32_step_times():
         for m in meas:
             assert model_profile(m, "fp32").step_time_1gpu > 3 * PROFILES[m].step_time_1gpu
             assert model_profile(m, "fp32").t1() == pytest.approx(meas[m])   # measured beats profile
+            # ... and only the fp32 profile: the bf16 one keeps its own step time
+            assert model_profile(m, "bf16").t1() == pytest.approx(PROFILES[m].step_time_1gpu)
+    finally:
+        set_measured_step_times(None)
+
+
+def test_measured_step_times_keyed_by_precision(tmp_path):
+    """A mixed bf16 / fp32 trace: each precision's measurements price only that precision's
+    profile, from bench lines that carry their ``precision``."""
+    from vodascheduler_amd.common.workload import load_bench_json, model_profile, set_measured_step_times
+
+    lines = [{"line": {"metric": "m", "n_gpus": 1, "precision": "fp32", "step_ms_by_world": {"resnet50": {"1": 70.0}}}},
+             {"line": {"metric": "m", "n_gpus": 1, "precision": "bf16-amp",
+                       "step_ms_by_world": {"resnet50": {"1": 23.0}}}}]
+    p = tmp_path / "mixed.json"
+    p.write_text(json.dumps(lines))
+    try:
+        out = load_bench_json(str(p))
+        assert set(out["step_ms_by_precision"]) == {"fp32", "bf16"}
+        assert model_profile("resnet50", "fp32").t1() == pytest.approx(0.070)
+        assert model_profile("resnet50", "bf16").t1() == pytest.approx(0.023)
     finally:
         set_measured_step_times(None)

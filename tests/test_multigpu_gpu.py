@@ -114,7 +114,8 @@ def _cfg(tmp_path, name, **kw):
     from vodascheduler_amd.workloads.train import TrainConfig
 
     d = dict(model="mnist-torch", epochs=2, steps_per_epoch=600, per_gpu_batch=64, lr=0.01, commit_every=1,
-             amp=False, report_progress=True, final_state_path=str(tmp_path / f"{name}.pt"), graph=False)
+             amp=False, report_progress=True, final_state_path=str(tmp_path / f"{name}.pt"), graph=False,
+             step_digests=True)  # every RCCL run is checked step by step (world + LR exact)
     d.update(kw)
     return TrainConfig(**d)
 
@@ -147,7 +148,7 @@ def test_live_resize_2_4_2_on_rccl(gpu_pool, tmp_path):
     from elastic_harness import Controller, assert_matches_replay
 
     store, procs, wids, finish = gpu_pool
-    cfg = _cfg(tmp_path, "resize", step_digests=True)
+    cfg = _cfg(tmp_path, "resize")
     c = Controller(store, "resize", cfg)
     c.publish(wids[:2])
     c.wait_progress(20)
@@ -168,7 +169,7 @@ def test_abort_epoch_survivors_restore_and_finish(gpu_pool, tmp_path):
     from elastic_harness import Controller, assert_matches_replay
 
     store, procs, wids, finish = gpu_pool
-    cfg = _cfg(tmp_path, "kill", commit_every=4, step_digests=True)
+    cfg = _cfg(tmp_path, "kill", commit_every=4)
     c = Controller(store, "kill", cfg)
     c.publish(wids[:2])
     c.wait_progress(30)

@@ -28,6 +28,24 @@ def test_first_divergence_names_the_step_and_what_differs():
     assert first_divergence([], a) is None
 
 
+def test_relaxed_lockstep_check_ignores_state_only():
+    """The GPU (exact=False) check compares world and LR of every common step, never the
+    state digest: atomics may change the last bits of the state, never the schedule."""
+    t, u = [torch.zeros(4)], [torch.ones(4)]
+    a = [step_record(1, 8, 0.08, t), step_record(2, 8, 0.08, t)]
+    only_state = [step_record(1, 8, 0.08, u), step_record(2, 8, 0.08, u)]
+    assert first_divergence(a, only_state) is not None
+    assert first_divergence(a, only_state, fields=("world", "lr")) is None
+    lr_off = [step_record(1, 8, 0.08, u), step_record(2, 8, 0.16, u)]
+    msg = first_divergence(a, lr_off, fields=("world", "lr"))
+    assert msg.startswith("step 2:") and "lr" in msg and "state" not in msg
+    world_off = [step_record(1, 4, 0.08, t)]
+    assert "world" in first_divergence(a, world_off, fields=("world", "lr"))
+    import pytest
+    with pytest.raises(ValueError):
+        first_divergence(a, a, fields=("loss",))
+
+
 def test_collective_replay_equals_single_process_replay_at_worlds_1_and_2():
     cfg = TrainConfig(model="mnist-torch", epochs=1, steps_per_epoch=40, per_gpu_batch=16, lr=0.01, amp=False,
                       graph=False, step_digests=True)

@@ -402,3 +402,14 @@ def test_simulated_capacity_ramp_1_to_8():
     one = simulate(tr, "FfDLOptimizer", gpus=1)
     assert r.n_jobs == 32 and full.avg_jct <= r.avg_jct <= one.avg_jct
     assert 0 < r.utilization <= 1.0
+    assert r.peak_gpus == 8 and 1 < r.avg_gpus < 8
+
+
+def test_simulated_drain_survives_later_capacity_snapshot():
+    """A GPU drained before a capacity step stays drained: the snapshot is applied
+    minus the drained GPUs, so the peak is 7 of the snapshot's 8."""
+    tr = philly_trace(8, seed=2, mean_interarrival_s=20, mean_duration_1gpu_s=200, max_gpus=8)
+    ramp = [(0.0, {"node0": list(range(4))}), (300.0, {"node0": list(range(8))})]
+    r = simulate(tr, "ElasticFIFO", gpus=8, capacity=ramp, drain=[(100.0, "node0", 2)])
+    assert r.n_jobs == 8 and r.peak_gpus == 7 and r.gpus == 7
+    assert r.avg_gpus <= 7

@@ -99,18 +99,27 @@ def load_busbw(path: str, bucket_mb: int = 64) -> dict[int, float]:
     return table
 
 
-# model -> {world size: measured seconds per training step} from a bench run's online
-# profiling (``step_ms_by_world``); overrides the speed model at the measured world sizes
-_MEASURED_STEP: dict[str, dict[int, float]] = {}
+# (model, precision) -> {world size: measured seconds per training step} from a bench run's
+# online profiling (``step_ms_by_world``); overrides the speed model of the profile of THAT
+# precision at the measured world sizes (a mixed bf16 / fp32 trace prices each job with its
+# own precision's measurements)
+_MEASURED_STEP: dict[tuple[str, str], dict[int, float]] = {}
 
 
-def set_measured_step_times(table: dict[str, dict] | None) -> None:
-    """Install measured per-world step times ({model: {world: ms}}); None clears them."""
-    _MEASURED_STEP.clear()
+def _prec(precision: str | None) -> str:
+    """bench / workload precision names -> profile precision (``bf16-amp`` is bf16)."""
+    return "fp32" if precision == "fp32" else "bf16"
+
+
+def set_measured_step_times(table: dict[str, dict] | None, precision: str = "bf16", clear: bool = True) -> None:
+    """Install measured per-world step times ({model: {world: ms}}) of one compute
+    ``precision``; None clears them (all precisions)."""
+    if clear or table is None:
+        _MEASURED_STEP.clear()
     for model, per in (table or {}).items():
         d = {int(w): float(ms) / 1e3 for w, ms in (per or {}).items() if ms and float(ms) > 0}
         if d:
-            _MEASURED_STEP[model] = d
+            _MEASURED_STEP[(model, _prec(precision))] = d
 
 
 def load_bench_json(path: str, bucket_mb: int = 64) -> dict:
@@ -119,13 +128,14 @@ def load_bench_json(path: str, bucket_mb: int = 64) -> dict:
     bw = load_busbw(path, bucket_mb)
     with open(path) as f:
         doc = json.load(f)
-    steps: dict[str, dict[str, float]] = {}
+    steps: dict[str, dict[str, dict[str, float]]] = {}  # precision -> model -> {world: ms}
 
     def walk(x):
         if isinstance(x, dict):
             if isinstance(x.get("step_ms_by_world"), dict):
+                by = steps.setdefault(_prec(x.get("precision")), {})
                 for m, per in x["step_ms_by_world"].items():
-                    steps.setdefault(m, {}).update(per)
+                    by.setdefault(m, {}).update(per)
             for v in x.values():
                 walk(v)
         elif isinstance(x, list):
@@ -141,8 +151,11 @@ def load_bench_json(path: str, bucket_mb: int = 64) -> dict:
                         pass
 
     walk(doc)
-    set_measured_step_times(steps)
-    return {"busbw_gbs": bw, "step_ms_by_world": steps}
+    set_measured_step_times(None)
+    for prec, table in steps.items():
+        set_measured_step_times(table, prec, clear=False)
+    flat = {m: per for table in steps.values() for m, per in table.items()}
+    return {"busbw_gbs": bw, "step_ms_by_world": flat, "step_ms_by_precision": steps}
 
 
 @dataclass
@@ -163,6 +176,7 @@ class ModelProfile:
     grad_mb: float = 0.0   # fp32 gradient bytes per step (MB) -- exact, from the parameter count
     overlap: float = 0.3   # fraction of t1 that hides the all-reduce (bucket overlap with backward)
     measured: bool = False
+    precision: str = "bf16"  # compute precision the step time is for ("bf16" autocast or "fp32")
 
     def comm_time(self, n: int, busbw_gbs: float | None = None) -> float:
         if n <= 1:
@@ -174,13 +188,13 @@ class ModelProfile:
         """Seconds per single-GPU step: this box's measurement when one is installed
         (``set_measured_step_times``: the bench warm-up at the run's precision), else the
         profile's."""
-        meas = _MEASURED_STEP.get(self.name)
+        meas = _MEASURED_STEP.get((self.name, self.precision))
         return meas.get(1, self.step_time_1gpu) if meas else self.step_time_1gpu
 
     def speedup(self, n: int, busbw_gbs: float | None = None) -> float:
         if n <= 0:
             return 0.0
-        meas = _MEASURED_STEP.get(self.name)
+        meas = _MEASURED_STEP.get((self.name, self.precision))
         if meas and n in meas and busbw_gbs is None:
             # measured: n workers each process one per-GPU batch per step of meas[n] seconds
             return n * self.t1() / meas[n]
@@ -215,13 +229,15 @@ PROFILES = {
 
 # fp32 compute (the reference's precision: tensorflow2_keras_cifar_elastic.py:147-166 builds
 # the Keras model with no mixed-precision policy; pytorch_mnist_elastic.py is plain fp32):
-# MI355X single-GPU step times, same batches.  ResNet-50 76.9 ms / BERT-base 39.7 ms at the
-# end of round 3 (profiles/r3/model_step_fp32.jsonl, rocprof_resnet50_fp32.md,
-# rocprof_bert_fp32.md); the other models keep their bf16 ratio to fp32 unmeasured, so they
-# fall back to the bf16 profile.
+# MI355X single-GPU step times, same batches.  ResNet-50 69.96 ms / BERT-base 37.1 ms at the
+# end of round 4 (the driver's BENCH_r04 warm-up, ``warmup_single_gpu_step_ms``; kernel time
+# profiles/r4/rocprof_resnet50_fp32_r4end.md); the other models' fp32 step times are
+# unmeasured, so they fall back to the bf16 profile.
 PROFILES_FP32 = {
-    "resnet50": ModelProfile("resnet50", alpha=0.01, step_time_1gpu=0.0769, grad_mb=102.2, measured=True),
-    "bert-base": ModelProfile("bert-base", alpha=0.05, step_time_1gpu=0.0397, grad_mb=438.0, measured=True),
+    "resnet50": ModelProfile("resnet50", alpha=0.01, step_time_1gpu=0.06996, grad_mb=102.2, measured=True,
+                             precision="fp32"),
+    "bert-base": ModelProfile("bert-base", alpha=0.05, step_time_1gpu=0.0371, grad_mb=438.0, measured=True,
+                              precision="fp32"),
 }
 PRECISIONS = ("bf16", "fp32")
 

@@ -106,9 +106,10 @@ class ElasticContext:
                 try:
                     now = time.time()
                     if now - last_hb >= HEARTBEAT_S:
-                        # liveness for the backend: a member stuck in a collective keeps beating
-                        # (the GIL is released there), a dead process stops
-                        self._watch_rdzv.set(f"hb/{self.worker_id}", repr(now))
+                        # liveness + progress for the backend: a dead process stops beating; a
+                        # member stuck in a collective keeps beating (the GIL is released there)
+                        # but its progress -- joined epoch, committed step -- stops advancing
+                        self._watch_rdzv.heartbeat(self.worker_id, self.epoch, self.committed_step)
                         last_hb = now
                     e = self._watch_rdzv.latest_epoch()
                     if e > self._latest_seen:
@@ -128,6 +129,10 @@ class ElasticContext:
         if self._watcher is not None:
             self._watcher.join(2)
             self._watcher = None
+            try:  # leaving the job: tombstone the beat (a re-listed worker is not "alive" here)
+                self._watch_rdzv.clear_heartbeat(self.worker_id)
+            except Exception:
+                pass
 
     def latest_seen(self) -> int:
         if self._watcher is None:

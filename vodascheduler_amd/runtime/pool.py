@@ -84,6 +84,7 @@ class PoolBackend(Backend):
         self.events: list[dict] = []
         self.forced_epochs = 0
         self.forced_log: list[dict] = []  # every forced abort epoch: job, epoch, wait, members without heartbeat
+        self._hb_seen: dict[tuple[str, str], list] = {}  # (job, member) -> beat / progress change times
         # mailbox counters continue where an earlier backend on the same warm pool stopped
         # (several traces in a row on one pool: bench.py's control run)
         self._mail_n: dict[str, int] = {w: int(store.add(f"pool/{w}/n", 0)) for w in self.workers}
@@ -142,19 +143,25 @@ class PoolBackend(Backend):
         if live_m and not force and rdzv.get(f"e/{live_e}/synced") is None and rdzv.outcome() is None:
             t_req = self.pending[name][2]
             waited = time.time() - t_req
+            stale = self._stale_members(rdzv, name, live_m)  # refreshes the beat records every poll
             if waited < self.settle_timeout:
                 return  # the monitor retries
-            # a slow but healthy epoch (a first MIOpen find, an fp32 find-db build, a graph
-            # capture) is left alone: abort only when a member is known to be gone -- its
-            # heartbeat stopped -- or after STUCK_FACTOR x settle_timeout in any case
-            stale = self._stale_members(rdzv, live_m)
-            if not stale and waited < self.STUCK_FACTOR * self.settle_timeout:
+            # a slow but healthy epoch (members still training towards the commit that joins
+            # it, a state sync in flight) is left alone.  Abort when a member is known to be
+            # gone (its beat counter stopped advancing), when NO member made progress (joined
+            # epoch / committed step) for settle_timeout -- live processes deadlocked in a
+            # collective keep beating but stop progressing -- or at the hard limit
+            stuck = not stale and self._no_progress(name, live_m)
+            hard = min(self.STUCK_FACTOR * self.settle_timeout, self.HARD_SETTLE_S)
+            if not stale and not stuck and waited < hard:
                 return
-            log.warning("job %s: epoch %d not synced after %.0fs (members without heartbeat: %s); "
-                        "publishing an abort epoch", name, live_e, waited, stale or "none, hard limit")
+            why = "stale" if stale else ("no progress" if stuck else "hard limit")
+            log.warning("job %s: epoch %d not synced after %.0fs (%s; members without heartbeat: %s); "
+                        "publishing an abort epoch", name, live_e, waited, why, stale or "none")
             abort = True
             self.forced_epochs += 1
-            self.forced_log.append({"job": name, "epoch": live_e, "waited_s": round(waited, 1), "stale": stale})
+            self.forced_log.append({"job": name, "epoch": live_e, "waited_s": round(waited, 1), "stale": stale,
+                                    "why": why})
         new_members, kind, t, cfg = self.pending.pop(name)
         if new_members == live_m:
             return
@@ -169,22 +176,46 @@ class PoolBackend(Backend):
             if wid not in live_m:
                 self._mail(wid, {"job": name, "epoch": e, "cfg": cfg})
 
-    STUCK_FACTOR = 5.0    # abort a never-syncing epoch of live members after this x settle_timeout
+    STUCK_FACTOR = 5.0      # hard limit: abort a never-syncing epoch after this x settle_timeout ...
+    HARD_SETTLE_S = 150.0   # ... or this many seconds, whichever is first (bench deadline 540 s)
     HEARTBEAT_STALE_S = 10.0
 
-    def _stale_members(self, rdzv, members: list[str]) -> list[str]:
-        """Members whose liveness beat (runtime/elastic.py watcher) is missing or older than
-        HEARTBEAT_STALE_S."""
-        now = time.time()
+    def _observe(self, rdzv, job: str, m: str):
+        """Track member ``m``'s beat on the backend's own monotonic clock: returns its record
+        [count, t_count_changed, progress, t_progress_changed], or None (never beat / left)."""
+        hb = rdzv.read_heartbeat(m)
+        key = (job, m)
+        if hb is None:
+            self._hb_seen.pop(key, None)
+            return None
+        now = time.monotonic()
+        n, prog = hb[0], hb[1:]
+        rec = self._hb_seen.get(key)
+        if rec is None:
+            rec = self._hb_seen[key] = [n, now, prog, now]
+        if n != rec[0]:
+            rec[0], rec[1] = n, now
+        if prog != rec[2]:
+            rec[2], rec[3] = prog, now
+        return rec
+
+    def _stale_members(self, rdzv, job: str, members: list[str]) -> list[str]:
+        """Members whose liveness beat (runtime/elastic.py watcher) is missing, tombstoned, or
+        has not advanced for HEARTBEAT_STALE_S of this backend's clock."""
+        now = time.monotonic()
         out = []
         for m in members:
-            v = rdzv.get(f"hb/{m}")
-            try:
-                if v is None or now - float(v) > self.HEARTBEAT_STALE_S:
-                    out.append(m)
-            except ValueError:
+            rec = self._observe(rdzv, job, m)
+            if rec is None or now - rec[1] > self.HEARTBEAT_STALE_S:
                 out.append(m)
         return out
+
+    def _no_progress(self, job: str, members: list[str]) -> bool:
+        """True when no member's progress (joined epoch, committed step) changed during the
+        last settle_timeout (records refreshed by the _stale_members call just before)."""
+        now = time.monotonic()
+        recs = [self._hb_seen.get((job, m)) for m in members]
+        return all(r is not None and now - r[3] > self.settle_timeout for r in recs)
 
     def _mail(self, wid: str, msg: dict) -> None:
         n = self._mail_n.get(wid, 0) + 1
@@ -205,6 +236,8 @@ class PoolBackend(Backend):
             with self._lock:
                 self.members.pop(job_name, None)
                 self.active.discard(job_name)
+            for k in [k for k in self._hb_seen if k[0] == job_name]:
+                del self._hb_seen[k]
 
     def nodes(self):
         return {k: list(v) for k, v in self.node_gpus.items()}

@@ -98,6 +98,32 @@ class JobRendezvous:
                 raise TimeoutError(f"{self.job}: previous members never handed the state off (live_epoch={le})")
             time.sleep(0.02)
 
+    # ----------------------------------------------------------- liveness / progress beats
+    def heartbeat(self, worker: str, epoch: int, step: int) -> None:
+        """One beat of ``worker``: a store-side counter (liveness: the backend checks that it
+        ADVANCES, on its own clock -- no wall-clock comparison across hosts) and the member's
+        progress, the epoch it joined and its last committed step."""
+        self.store.set(self.p + f"hb/{worker}/p", f"{int(epoch)}:{int(step)}")
+        self.store.add(self.p + f"hb/{worker}/n", 1)
+
+    def read_heartbeat(self, worker: str) -> tuple[int, int, int] | None:
+        """(beat count, joined epoch, committed step), or None when the worker never beat or
+        left the job (its beat tombstoned by ElasticContext.stop)."""
+        kp = self.p + f"hb/{worker}/p"
+        if not self.store.check([kp]):
+            return None
+        v = self.store.get(kp).decode()
+        if v == "left":
+            return None
+        n = int(self.store.add(self.p + f"hb/{worker}/n", 0))
+        e, st = v.split(":")
+        return n, int(e), int(st)
+
+    def clear_heartbeat(self, worker: str) -> None:
+        """Tombstone: a worker that left the job no longer counts as a live member, even if
+        it is re-listed before its beats would have gone stale."""
+        self.store.set(self.p + f"hb/{worker}/p", "left")
+
     def set(self, key: str, value: str) -> None:
         self.store.set(self.p + key, value)
 

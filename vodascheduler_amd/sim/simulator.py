@@ -38,6 +38,8 @@ class SimResult:
     resizes: int
     migrations: int
     jct: dict[str, float] = field(default_factory=dict)
+    peak_gpus: int = 0          # most GPUs schedulable at any time
+    avg_gpus: float = 0.0       # time-averaged schedulable GPUs over [first submission, last completion]
 
     def summary(self) -> dict:
         d = asdict(self)
@@ -65,8 +67,11 @@ def simulate(trace: list[TraceJob], algorithm: str = "ElasticFIFO", gpus: int = 
     ``placeholder`` (the reference as written: 1 s epochs, linear speedup).
     ``capacity`` = [(time, {node: [gpu, ...]})]: the schedulable inventory from ``time`` on
     -- nodes / GPUs added (a cluster autoscaler, spot capacity returning) or removed; an
-    entry at time 0 is the starting inventory.  Utilisation is measured against the GPUs
-    present over time."""
+    entry at time 0 is the starting inventory.  A drained GPU STAYS drained: every later
+    capacity snapshot is applied minus the GPUs drained so far, and at equal times the
+    capacity entry is applied first, then the drain.  Utilisation is measured against the
+    GPUs present over time; ``gpus`` / ``peak_gpus`` report the most GPUs schedulable at
+    once and ``avg_gpus`` the time average."""
     clock = ManualClock(0.0)
     store = MemoryStore()
     mq = InProcQueue(maxsize=10 ** 6)
@@ -93,6 +98,7 @@ def simulate(trace: list[TraceJob], algorithm: str = "ElasticFIFO", gpus: int = 
         tracer = SchedulerTracer(core)
     pending = sorted(trace, key=lambda tj: tj.submit_time)
     drains = sorted(drain or [])
+    drained: set[tuple[str, int]] = set()
     names: list[str] = []
     steps = 0
     while True:
@@ -120,11 +126,13 @@ def simulate(trace: list[TraceJob], algorithm: str = "ElasticFIFO", gpus: int = 
             doc = store.find_metadata(name)
             backend.on_submit(name, doc["job_category"], doc["spec"], int(doc["config"]["epochs"]))
         while caps and caps[0][0] <= t:
-            backend.set_nodes(caps.pop(0)[1])
+            snap = caps.pop(0)[1]
+            backend.set_nodes({n: [g for g in gs if (n, g) not in drained] for n, gs in snap.items()})
         while drains and drains[0][0] <= t:
             _, node, gpu = drains.pop(0)
+            drained.add((node, gpu))
             cur = backend.nodes()
-            cur[node] = [g for g in cur[node] if g != gpu]
+            cur[node] = [g for g in cur.get(node, []) if g != gpu]
             backend.set_nodes(cur)
         m = mq.get(gpu_type)
         while m is not None:
@@ -149,10 +157,12 @@ def simulate(trace: list[TraceJob], algorithm: str = "ElasticFIFO", gpus: int = 
     first = min(tj.submit_time for tj in trace)
     last = max(core.done_jobs[n].finish_timestamp for n in names)
     vals = sorted(jct.values())
-    total_gpus = max(sum(len(v) for v in nodes.values()), backend.max_gpus)
-    return SimResult(algorithm=algorithm, gpus=total_gpus, n_jobs=len(names), avg_jct=statistics.fmean(vals),
+    peak = backend.max_gpus  # the starting inventory and every later set_nodes
+    present = backend.gpu_present_seconds(first, last)
+    return SimResult(algorithm=algorithm, gpus=peak, n_jobs=len(names), avg_jct=statistics.fmean(vals),
                      median_jct=statistics.median(vals), p95_jct=vals[min(len(vals) - 1, int(0.95 * len(vals)))],
                      makespan=last - first, avg_wait=statistics.fmean(waits),
-                     utilization=backend.gpu_busy_seconds / max(1e-9, backend.gpu_present_seconds(first, last)),
+                     utilization=backend.gpu_busy_seconds / max(1e-9, present),
                      reschedules=core.resched_count,
-                     resizes=backend.total_resizes, migrations=backend.total_migrations, jct=jct)
+                     resizes=backend.total_resizes, migrations=backend.total_migrations, jct=jct,
+                     peak_gpus=peak, avg_gpus=present / max(1e-9, last - first))

@@ -79,9 +79,12 @@ class TraceJob:
 def philly_trace(n_jobs: int = 32, seed: int = 0, mean_interarrival_s: float = 30.0,
                  mean_duration_1gpu_s: float = 600.0, max_gpus: int = 8,
                  models: tuple[str, ...] = ("resnet50", "bert-base", "vgg16", "transformer"),
-                 elastic: bool = True, duration_scale: float = 1.0) -> list[TraceJob]:
+                 elastic: bool = True, duration_scale: float = 1.0, precision: str | None = None) -> list[TraceJob]:
     """Generate ``n_jobs`` jobs.  Sizes: 1 GPU 50 %, 2 GPUs 25 %, 4 GPUs 15 %, 8 GPUs 10 %
-    (capped at ``max_gpus``); durations log-normal (sigma 1.0) around the mean GPU-time."""
+    (capped at ``max_gpus``); durations log-normal (sigma 1.0) around the mean GPU-time of the
+    bf16 profile.  ``precision`` (bf16 | fp32) is declared by every job: the same steps
+    (the same work) are then priced at that precision's step time, so an fp32 trace runs
+    ~3x longer than the bf16 one (``common.workload.PROFILES_FP32``)."""
     rng = random.Random(seed)
     sizes, weights = [1, 2, 4, 8], [0.50, 0.25, 0.15, 0.10]
     t = 0.0
@@ -100,7 +103,7 @@ def philly_trace(n_jobs: int = 32, seed: int = 0, mean_interarrival_s: float = 3
         max_np = min(max_gpus, max(np_ * 2, 2)) if elastic else np_
         name = f"{model}-j{i:02d}"
         out.append(TraceJob(t, make_spec(name, model, np_, min_np, max_np, epochs, steps_per_epoch,
-                                         category=model)))
+                                         category=model, precision=precision)))
     return out
 
 

@@ -47,19 +47,27 @@ def step_record(step: int, world: int, lr: float, tensors: list[torch.Tensor]) -
     return f"{step}:{world}:{lr!r}:{state_digest(tensors)[:STEP_DIGEST_CHARS]}"
 
 
-def first_divergence(run: list[str], ref: list[str]) -> str | None:
-    """``None`` when the two lock-step logs agree, else a description of the first step at
-    which they differ (world, LR or state)."""
+DIGEST_FIELDS = ("world", "lr", "state")
+
+
+def first_divergence(run: list[str], ref: list[str], fields: tuple[str, ...] = DIGEST_FIELDS) -> str | None:
+    """``None`` when the two lock-step logs agree on ``fields`` at every common step, else a
+    description of the first step at which they differ.  ``fields=("world", "lr")`` is the
+    relaxed check of a GPU run, whose state digest legitimately differs (atomics make the
+    reductions nondeterministic) while its world size and LR schedule must still be exact."""
+    bad = set(fields) - set(DIGEST_FIELDS)
+    if bad:
+        raise ValueError(f"unknown digest fields {sorted(bad)}")
     rs = {r.split(":", 1)[0]: r for r in run}
     for e in ref:
         s = e.split(":", 1)[0]
         r = rs.get(s)
         if r is None:
             continue  # the elastic log only holds committed history (restores roll it back)
-        if r != e:
-            rw, rl, rd = r.split(":")[1:]
-            ew, el, ed = e.split(":")[1:]
-            what = [n for n, a, b in (("world", rw, ew), ("lr", rl, el), ("state", rd, ed)) if a != b]
+        got = dict(zip(DIGEST_FIELDS, r.split(":")[1:]))
+        want = dict(zip(DIGEST_FIELDS, e.split(":")[1:]))
+        what = [n for n in DIGEST_FIELDS if n in fields and got[n] != want[n]]
+        if what:
             return f"step {s}: {', '.join(what)} differ (run {r!r} vs replay {e!r})"
     if len(rs) and not any(e.split(":", 1)[0] in rs for e in ref):
         return "no common step between the logs"
