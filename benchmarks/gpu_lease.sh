@@ -15,6 +15,9 @@
 #   py:SCRIPT[:ARGS]         python benchmarks/SCRIPT ARGS (comma-separated args)
 #   pytest:FILE[,ARGS]       pytest -m gpu of one test file (comma-separated extra args)
 #   env:NAME=VALUE           export for the following steps (their logs get a "+NAME=VALUE" suffix)
+#   ab:NAME:MODEL[-fp32]:REPS  interleaved same-box A/B of one env switch: model_step.py with
+#                            NAME=1 then NAME=0, REPS times (30 timed steps each); one JSON line
+#                            per run in ab-NAME-MODEL.jsonl
 set -o pipefail
 TAG=${1:?tag}
 shift
@@ -101,6 +104,20 @@ for step in "$@"; do
       args=""
       [[ $spec == *:* ]] && args=${spec#*:}
       run 600 "py-${script%.py}" python -u "benchmarks/$script" ${args//,/ } || exit $? ;;
+    ab:*)
+      spec=${step#ab:}
+      IFS=: read -r name m reps <<< "$spec"
+      prec=bf16-amp
+      if [[ $m == *-fp32 ]]; then m=${m%-fp32}; prec=fp32; fi
+      jl="$OUT/ab-$name-$m.jsonl"
+      for ((i = 1; i <= ${reps:-2}; i++)); do
+        for v in 1 0; do
+          env "$name=$v" timeout -k 10 300 python -u benchmarks/model_step.py --model "$m" --steps 30 --warmup 10 \
+            --precision "$prec" > "$OUT/ab-$name-$v-$i.log" 2>&1 || { tail -20 "$OUT/ab-$name-$v-$i.log"; exit 1; }
+          echo "{\"$name\": $v, \"rep\": $i, \"run\": $(grep '^{' "$OUT/ab-$name-$v-$i.log" | tail -1)}" >> "$jl"
+          tail -n 1 "$jl" | cut -c1-200
+        done
+      done ;;
     *)
       echo "unknown step $step"; exit 2 ;;
   esac

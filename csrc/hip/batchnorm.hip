@@ -173,6 +173,26 @@ __device__ __forceinline__ void reduce_and_store(const Map& m, float (&s1)[8], f
   }
 }
 
+// Three-accumulator form (dual-BN backward reduce): part1/2/3 get sum g, sum g*x, sum g*x2.
+__device__ __forceinline__ void reduce_and_store3(const Map& m, float (&s1)[8], float (&s2)[8], float (&s3)[8],
+                                                  float* part1, float* part2, float* part3, int C) {
+  __shared__ float red3[3][kBlock][kVec + 1];
+  const int t = threadIdx.x;
+#pragma unroll
+  for (int k = 0; k < kVec; ++k) { red3[0][t][k] = s1[k]; red3[1][t][k] = s2[k]; red3[2][t][k] = s3[k]; }
+  __syncthreads();
+  if (m.active && m.rsub == 0) {
+    for (int r = 1; r < m.rpi; ++r) {
+      const int o = t + r * m.tpr;
+#pragma unroll
+      for (int k = 0; k < kVec; ++k) { s1[k] += red3[0][o][k]; s2[k] += red3[1][o][k]; s3[k] += red3[2][o][k]; }
+    }
+    const int64_t base = int64_t(blockIdx.x) * C + int64_t(m.cg) * kVec;
+#pragma unroll
+    for (int k = 0; k < kVec; ++k) { part1[base + k] = s1[k]; part2[base + k] = s2[k]; part3[base + k] = s3[k]; }
+  }
+}
+
 // ---------------------------------------------------------------- forward: statistics
 // Buffer-descriptor loads of the reduction passes.  The row walk is split into a
 // block-uniform part (the base row of an iteration -> descriptor base, and the row step ->
@@ -392,13 +412,15 @@ __global__ __launch_bounds__(kFinCh* kFinRg) void bn_fwd_finalize_kernel(
   }
 }
 
+// ``p1`` / ``p2``: the [nb][C] partials of sum g and sum g*x (a dual-BN backward shares p1
+// between its two BatchNorms, see bn_bwd_reduce2_kernel)
 __global__ __launch_bounds__(kFinCh* kFinRg) void bn_bwd_finalize_kernel(
-    const float* __restrict__ part, int nb, int64_t M, int C, const float* __restrict__ gamma,
-    const float* __restrict__ save_mean, const float* __restrict__ save_invstd, float* __restrict__ dgamma,
-    float* __restrict__ dbeta, float* __restrict__ k3, int accumulate) {
+    const float* __restrict__ p1, const float* __restrict__ p2, int nb, int64_t M, int C,
+    const float* __restrict__ gamma, const float* __restrict__ save_mean, const float* __restrict__ save_invstd,
+    float* __restrict__ dgamma, float* __restrict__ dbeta, float* __restrict__ k3, int accumulate) {
   const int c = blockIdx.x * kFinCh + threadIdx.x % kFinCh;
   double S1, S2;  // sum g, sum g*x
-  fin_reduce(part, part + int64_t(nb) * C, nb, C, c, S1, S2);
+  fin_reduce(p1, p2, nb, C, c, S1, S2);
   if (threadIdx.x / kFinCh == 0 && c < C) {
     const double mean = save_mean[c], invstd = save_invstd[c];
     const double db = S1;
@@ -536,6 +558,163 @@ __global__ __launch_bounds__(kBlock) void bn_bwd_apply_kernel(const T* __restric
     for (int k = 0; k < 8; ++k) o[k] = fmaf(a[k], g[k], fmaf(c2[k], xv[k], c0[k]));
     Vec8<T>::store(dx, r * C + col, o);
   }
+}
+
+// ---------------------------------------------------------------- dual BN (downsample blocks)
+// A ResNet downsample block ends in relu(bn3(y3) + bn_ds(y_ds)).  As two fused BNs that is
+// an apply pass writing bn_ds(y_ds) (read 1, write 1) that the bn3 pass reads back as its
+// residual, and backward a bn3 pass writing the residual gradient g that bn_ds reduces and
+// applies again: 11 tensor passes.  Both BNs see the same g = dy * (out > 0), so one reduce
+// pass (dy, mask, y3, y_ds -> sum g, sum g*y3, sum g*y_ds) and one apply pass
+// (-> dy3, dy_ds) cover both, and the forward reads y_ds directly: 3 + 3 + 5 = 11 -> 8 passes
+// of the block's largest tensor (stats of y3 / y_ds come from their GEMM epilogues).
+template <typename T, bool RELU, int U = 4>
+__global__ __launch_bounds__(kBlock) void bn_apply2_kernel(const T* __restrict__ x, const T* __restrict__ x2,
+                                                           const float* __restrict__ ab, const float* __restrict__ ab2,
+                                                           T* __restrict__ y, uint8_t* __restrict__ mask, int64_t M,
+                                                           int C, int sweep) {
+  const Map m = make_map(C);
+  if (!m.active) return;
+  int64_t r0, r1;
+  apply_rows(M, m.rpi, sweep, r0, r1);
+  const int64_t col = int64_t(m.cg) * kVec;
+  float a[8], b[8], a2[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    a[k] = ab[col + k];
+    a2[k] = ab2[col + k];
+    b[k] = ab[C + col + k] + ab2[C + col + k];  // both shifts folded into one
+  }
+  const int64_t step = m.rpi;
+  const int CB = C / kVec;
+  int64_t r = r0 + m.rsub;
+  auto body = [&](const typename Vec8<T>::Raw& xr, const typename Vec8<T>::Raw& qr, int64_t row) {
+    float v[8], q[8];
+    Vec8<T>::cvt(xr, v);
+    Vec8<T>::cvt(qr, q);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      v[k] = fmaf(v[k], a[k], fmaf(q[k], a2[k], b[k]));
+      if constexpr (RELU) v[k] = fmaxf(v[k], 0.f);
+    }
+    Vec8<T>::store(y, row * C + col, v);
+    if constexpr (RELU) mask[row * CB + m.cg] = pos_bits(v);
+  };
+  for (; r + (U - 1) * step < r1; r += U * step) {
+    typename Vec8<T>::Raw xr[U], qr[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      xr[u] = Vec8<T>::load_raw(x, (r + u * step) * C + col);
+      qr[u] = Vec8<T>::load_raw(x2, (r + u * step) * C + col);
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) body(xr[u], qr[u], r + u * step);
+  }
+  for (; r < r1; r += step) body(Vec8<T>::load_raw(x, r * C + col), Vec8<T>::load_raw(x2, r * C + col), r);
+}
+
+template <typename T, bool RELU, int U>
+__global__ __launch_bounds__(kBlock) void bn_bwd_reduce2_kernel(const T* __restrict__ dy,
+                                                                const uint8_t* __restrict__ mask,
+                                                                const T* __restrict__ x, const T* __restrict__ x2,
+                                                                float* __restrict__ part, int64_t M, int C, int sweep) {
+  const Map m = make_map(C);
+  float s1[8] = {0, 0, 0, 0, 0, 0, 0, 0}, s2[8] = {0, 0, 0, 0, 0, 0, 0, 0}, s3[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  if (m.active) {
+    const Walk w = reduce_walk(m, M, sweep, U);
+    const int64_t end = w.end;
+    const int CB = C / kVec;
+    const int64_t row_bytes = int64_t(C) * sizeof(T);
+    const int voff = int(m.rsub * row_bytes + int64_t(m.cg) * kVec * sizeof(T));
+    const int moff = m.rsub * CB + m.cg;
+    const int sstep = int(w.step * row_bytes), mstep = int(w.step * CB);
+    for (int64_t i = 0; i < w.groups; ++i) {
+      const int64_t b = w.base(i, U);
+      const auto rg = rows_rsrc(dy + b * C, (end - b) * row_bytes);
+      const auto rx = rows_rsrc(x + b * C, (end - b) * row_bytes);
+      const auto rq = rows_rsrc(x2 + b * C, (end - b) * row_bytes);
+      const auto rm = rows_rsrc(mask + (RELU ? b * CB : 0), RELU ? (end - b) * CB : 0);
+      typename BufRow<T>::Raw gr[U], xr[U], qr[U];
+      uint32_t mb[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        gr[u] = BufRow<T>::load(rg, voff, u * sstep);
+        xr[u] = BufRow<T>::load(rx, voff, u * sstep);
+        qr[u] = BufRow<T>::load(rq, voff, u * sstep);
+        if constexpr (RELU) mb[u] = __builtin_amdgcn_raw_buffer_load_b8(rm, moff, u * mstep, 0);
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        float g[8], xv[8], qv[8];
+        Vec8<T>::cvt(gr[u], g);
+        Vec8<T>::cvt(xr[u], xv);
+        Vec8<T>::cvt(qr[u], qv);
+        if constexpr (RELU) apply_mask(g, uint8_t(mb[u]));
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          s1[k] += g[k];
+          s2[k] = fmaf(g[k], xv[k], s2[k]);
+          s3[k] = fmaf(g[k], qv[k], s3[k]);
+        }
+      }
+    }
+  }
+  const int64_t nbC = int64_t(gridDim.x) * C;
+  reduce_and_store3(m, s1, s2, s3, part, part + nbC, part + 2 * nbC, C);
+}
+
+template <typename T, bool RELU, int U = 4>
+__global__ __launch_bounds__(kBlock) void bn_bwd_apply2_kernel(const T* __restrict__ dy,
+                                                               const uint8_t* __restrict__ mask,
+                                                               const T* __restrict__ x, const T* __restrict__ x2,
+                                                               const float* __restrict__ k3,
+                                                               const float* __restrict__ k3b, T* __restrict__ dx,
+                                                               T* __restrict__ dx2, int64_t M, int C, int sweep) {
+  const Map m = make_map(C);
+  if (!m.active) return;
+  int64_t r0, r1;
+  apply_rows(M, m.rpi, sweep, r0, r1);
+  const int64_t col = int64_t(m.cg) * kVec;
+  float a[8], c2[8], c0[8], e[8], e2[8], e0[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    a[k] = k3[col + k]; c2[k] = k3[C + col + k]; c0[k] = k3[2 * C + col + k];
+    e[k] = k3b[col + k]; e2[k] = k3b[C + col + k]; e0[k] = k3b[2 * C + col + k];
+  }
+  const int64_t step = m.rpi;
+  const int CB = C / kVec;
+  int64_t r = r0 + m.rsub;
+  auto body = [&](const typename Vec8<T>::Raw& gr, const typename Vec8<T>::Raw& xr, const typename Vec8<T>::Raw& qr,
+                  uint8_t mb, int64_t row) {
+    float g[8], xv[8], qv[8], o[8], o2[8];
+    Vec8<T>::cvt(gr, g);
+    Vec8<T>::cvt(xr, xv);
+    Vec8<T>::cvt(qr, qv);
+    if constexpr (RELU) apply_mask(g, mb);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      o[k] = fmaf(a[k], g[k], fmaf(c2[k], xv[k], c0[k]));
+      o2[k] = fmaf(e[k], g[k], fmaf(e2[k], qv[k], e0[k]));
+    }
+    Vec8<T>::store(dx, row * C + col, o);
+    Vec8<T>::store(dx2, row * C + col, o2);
+  };
+  for (; r + (U - 1) * step < r1; r += U * step) {
+    typename Vec8<T>::Raw gr[U], xr[U], qr[U];
+    uint8_t mb[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      gr[u] = Vec8<T>::load_raw(dy, (r + u * step) * C + col);
+      xr[u] = Vec8<T>::load_raw(x, (r + u * step) * C + col);
+      qr[u] = Vec8<T>::load_raw(x2, (r + u * step) * C + col);
+      mb[u] = RELU ? mask[(r + u * step) * CB + m.cg] : uint8_t(0);
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) body(gr[u], xr[u], qr[u], mb[u], r + u * step);
+  }
+  for (; r < r1; r += step)
+    body(Vec8<T>::load_raw(dy, r * C + col), Vec8<T>::load_raw(x, r * C + col), Vec8<T>::load_raw(x2, r * C + col),
+         RELU ? mask[r * CB + m.cg] : uint8_t(0), r);
 }
 
 // ---------------------------------------------------------------- stem: BN + ReLU + max pool
@@ -993,13 +1172,19 @@ void bn_apply(uintptr_t x, uintptr_t residual, uintptr_t ab, uintptr_t y, int64_
 
 void bn_bwd(uintptr_t dy, uintptr_t mask, uintptr_t x, uintptr_t save_mean, uintptr_t save_invstd, uintptr_t gamma,
             uintptr_t dx, uintptr_t dres, uintptr_t dgamma, uintptr_t dbeta, uintptr_t workspace, int64_t M, int C,
-            bool relu, bool accumulate, int dt, uintptr_t stream) {
+            bool relu, bool accumulate, int dt, uintptr_t stream, uintptr_t pre_part, int pre_nb) {
   VODA_CHECK(C % kVec == 0, "batchnorm: C must be a multiple of 8");
   VODA_CHECK(!relu || mask != 0, "batchnorm backward: ReLU needs the forward's bit-mask");
+  VODA_CHECK(pre_nb <= 0 || pre_part != 0, "batchnorm backward: precomputed sums need their partials");
   hipStream_t s = as_stream(stream);
   float* ws = reinterpret_cast<float*>(workspace);
   const Grid rg = reduce_grid(M, C, dt);
-  float* k3 = ws + int64_t(2) * rg.nb * C;
+  // pre_nb > 0: the producer of dy already reduced sum g / sum g*x (conv1x1_f32.hip
+  // gemm_f32_dgrad_bn): [2][pre_nb][C] partials at pre_part, no reduce pass
+  const bool pre = pre_nb > 0;
+  const int nb = pre ? pre_nb : rg.nb;
+  const float* p1 = pre ? reinterpret_cast<const float*>(pre_part) : ws;
+  float* k3 = pre ? ws : ws + int64_t(2) * rg.nb * C;
   const Grid ag = apply_grid(M, C);
   const int sw = bn_tune().sweep;
   dispatch_dt(dt, [&](auto tag) {
@@ -1015,7 +1200,8 @@ void bn_bwd(uintptr_t dy, uintptr_t mask, uintptr_t x, uintptr_t save_mean, uint
     };
     using RT = std::true_type;
     using RF = std::false_type;
-    if (relu) {
+    if (pre) {
+    } else if (relu) {
       if (lv >= 2) red(RT{}, std::integral_constant<int, 8>{});
       else if (lv == 1) red(RT{}, std::integral_constant<int, 4>{});
       else red(RT{}, std::integral_constant<int, 2>{});
@@ -1024,8 +1210,8 @@ void bn_bwd(uintptr_t dy, uintptr_t mask, uintptr_t x, uintptr_t save_mean, uint
       else if (lv == 1) red(RF{}, std::integral_constant<int, 4>{});
       else red(RF{}, std::integral_constant<int, 2>{});
     }
-    hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + kFinCh - 1) / kFinCh), dim3(kFinCh * kFinRg), 0, s, ws,
-                       rg.nb, M, C, reinterpret_cast<const float*>(gamma), reinterpret_cast<const float*>(save_mean),
+    hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + kFinCh - 1) / kFinCh), dim3(kFinCh * kFinRg), 0, s, p1,
+                       p1 + int64_t(nb) * C, nb, M, C, reinterpret_cast<const float*>(gamma), reinterpret_cast<const float*>(save_mean),
                        reinterpret_cast<const float*>(save_invstd), reinterpret_cast<float*>(dgamma),
                        reinterpret_cast<float*>(dbeta), k3, int(accumulate));
     T* dxp = reinterpret_cast<T*>(dx);
@@ -1047,6 +1233,110 @@ void bn_bwd(uintptr_t dy, uintptr_t mask, uintptr_t x, uintptr_t save_mean, uint
       if (dres) app(std::false_type{}, std::true_type{});
       else app(std::false_type{}, std::false_type{});
     }
+  });
+  check_launch();
+}
+
+// ---- dual BN: relu(bn(x) + bn2(x2)) (ResNet downsample blocks) ----
+int64_t bn2_workspace_floats(int64_t M, int C) {
+  const Grid g = reduce_grid(M, C, -1);
+  return int64_t(3) * g.nb * C + 6 * int64_t(C);
+}
+
+void bn2_fwd_train(uintptr_t x, uintptr_t x2, uintptr_t gamma, uintptr_t beta, uintptr_t running_mean,
+                   uintptr_t running_var, uintptr_t save_mean, uintptr_t save_invstd, uintptr_t gamma2, uintptr_t beta2,
+                   uintptr_t running_mean2, uintptr_t running_var2, uintptr_t save_mean2, uintptr_t save_invstd2,
+                   uintptr_t y, uintptr_t mask, uintptr_t workspace, uintptr_t workspace2, int64_t M, int C, float eps,
+                   float momentum, bool relu, int dt, uintptr_t stream, int pre_nb, int pre_nb2) {
+  VODA_CHECK(C % kVec == 0, "batchnorm: C must be a multiple of 8");
+  VODA_CHECK(M > 0, "batchnorm: empty input");
+  VODA_CHECK(!relu || mask != 0, "batchnorm: ReLU needs a mask buffer");
+  hipStream_t s = as_stream(stream);
+  const Grid rg = reduce_grid(M, C, dt);
+  const Grid ag = apply_grid(M, C);
+  const int sw = bn_tune().sweep;
+  float* abs_[2];
+  dispatch_dt(dt, [&](auto tag) {
+    using T = decltype(tag);
+    const uintptr_t xs[2] = {x, x2}, ws_[2] = {workspace, workspace2}, g_[2] = {gamma, gamma2}, b_[2] = {beta, beta2};
+    const uintptr_t rm_[2] = {running_mean, running_mean2}, rv_[2] = {running_var, running_var2};
+    const uintptr_t sm_[2] = {save_mean, save_mean2}, si_[2] = {save_invstd, save_invstd2};
+    const int pre[2] = {pre_nb, pre_nb2};
+    for (int i = 0; i < 2; ++i) {
+      float* ws = reinterpret_cast<float*>(ws_[i]);
+      const int nb = pre[i] > 0 ? pre[i] : rg.nb;
+      abs_[i] = ws + int64_t(2) * nb * C;
+      if (pre[i] <= 0)
+        hipLaunchKernelGGL((bn_stats_kernel<T, 8>), rg.grid, dim3(kBlock), 0, s, reinterpret_cast<const T*>(xs[i]),
+                           ws, M, C, sw);
+      hipLaunchKernelGGL(bn_fwd_finalize_kernel, dim3((C + kFinCh - 1) / kFinCh), dim3(kFinCh * kFinRg), 0, s, ws,
+                         nb, M, C, reinterpret_cast<const float*>(g_[i]), reinterpret_cast<const float*>(b_[i]),
+                         reinterpret_cast<float*>(rm_[i]), reinterpret_cast<float*>(rv_[i]),
+                         reinterpret_cast<float*>(sm_[i]), reinterpret_cast<float*>(si_[i]), abs_[i], eps, momentum);
+    }
+    const T* xp = reinterpret_cast<const T*>(x);
+    const T* qp = reinterpret_cast<const T*>(x2);
+    T* yp = reinterpret_cast<T*>(y);
+    uint8_t* mp = reinterpret_cast<uint8_t*>(mask);
+    if (relu)
+      hipLaunchKernelGGL((bn_apply2_kernel<T, true>), ag.grid, dim3(kBlock), 0, s, xp, qp, abs_[0], abs_[1], yp, mp, M, C,
+                         sw);
+    else
+      hipLaunchKernelGGL((bn_apply2_kernel<T, false>), ag.grid, dim3(kBlock), 0, s, xp, qp, abs_[0], abs_[1], yp, mp, M,
+                         C, sw);
+  });
+  check_launch();
+}
+
+void bn2_bwd(uintptr_t dy, uintptr_t mask, uintptr_t x, uintptr_t x2, uintptr_t save_mean, uintptr_t save_invstd,
+             uintptr_t gamma, uintptr_t save_mean2, uintptr_t save_invstd2, uintptr_t gamma2, uintptr_t dx,
+             uintptr_t dx2, uintptr_t dgamma, uintptr_t dbeta, uintptr_t dgamma2, uintptr_t dbeta2,
+             uintptr_t workspace, int64_t M, int C, bool relu, bool accumulate, int dt, uintptr_t stream,
+             uintptr_t pre_part, int pre_nb) {
+  VODA_CHECK(C % kVec == 0, "batchnorm: C must be a multiple of 8");
+  VODA_CHECK(!relu || mask != 0, "batchnorm backward: ReLU needs the forward's bit-mask");
+  VODA_CHECK(pre_nb <= 0 || pre_part != 0, "batchnorm backward: precomputed sums need their partials");
+  hipStream_t s = as_stream(stream);
+  float* ws = reinterpret_cast<float*>(workspace);
+  const Grid rg = reduce_grid(M, C, dt);
+  // pre_nb > 0: [3][pre_nb][C] partials (sum g, sum g*x, sum g*x2) from the producer of dy
+  const bool pre = pre_nb > 0;
+  const int nb = pre ? pre_nb : rg.nb;
+  const int64_t nbC = int64_t(nb) * C;
+  const float* part = pre ? reinterpret_cast<const float*>(pre_part) : ws;
+  float* k3 = pre ? ws : ws + 3 * nbC;
+  float* k3b = k3 + 3 * int64_t(C);
+  const Grid ag = apply_grid(M, C);
+  const int sw = bn_tune().sweep;
+  dispatch_dt(dt, [&](auto tag) {
+    using T = decltype(tag);
+    const T* dyp = reinterpret_cast<const T*>(dy);
+    const uint8_t* mp = reinterpret_cast<const uint8_t*>(mask);
+    const T* xp = reinterpret_cast<const T*>(x);
+    const T* qp = reinterpret_cast<const T*>(x2);
+    if (pre) {
+    } else if (relu)
+      hipLaunchKernelGGL((bn_bwd_reduce2_kernel<T, true, 4>), rg.grid, dim3(kBlock), 0, s, dyp, mp, xp, qp, ws, M, C, sw);
+    else
+      hipLaunchKernelGGL((bn_bwd_reduce2_kernel<T, false, 4>), rg.grid, dim3(kBlock), 0, s, dyp, mp, xp, qp, ws, M, C,
+                         sw);
+    const dim3 fg((C + kFinCh - 1) / kFinCh), fb(kFinCh * kFinRg);
+    hipLaunchKernelGGL(bn_bwd_finalize_kernel, fg, fb, 0, s, part, part + nbC, nb, M, C,
+                       reinterpret_cast<const float*>(gamma), reinterpret_cast<const float*>(save_mean),
+                       reinterpret_cast<const float*>(save_invstd), reinterpret_cast<float*>(dgamma),
+                       reinterpret_cast<float*>(dbeta), k3, int(accumulate));
+    hipLaunchKernelGGL(bn_bwd_finalize_kernel, fg, fb, 0, s, part, part + 2 * nbC, nb, M, C,
+                       reinterpret_cast<const float*>(gamma2), reinterpret_cast<const float*>(save_mean2),
+                       reinterpret_cast<const float*>(save_invstd2), reinterpret_cast<float*>(dgamma2),
+                       reinterpret_cast<float*>(dbeta2), k3b, int(accumulate));
+    T* dxp = reinterpret_cast<T*>(dx);
+    T* dqp = reinterpret_cast<T*>(dx2);
+    if (relu)
+      hipLaunchKernelGGL((bn_bwd_apply2_kernel<T, true>), ag.grid, dim3(kBlock), 0, s, dyp, mp, xp, qp, k3, k3b, dxp, dqp,
+                         M, C, sw);
+    else
+      hipLaunchKernelGGL((bn_bwd_apply2_kernel<T, false>), ag.grid, dim3(kBlock), 0, s, dyp, mp, xp, qp, k3, k3b, dxp,
+                         dqp, M, C, sw);
   });
   check_launch();
 }
@@ -1129,7 +1419,7 @@ void bn_pool_bwd(uintptr_t dy, uintptr_t idx, uintptr_t x, uintptr_t save_mean, 
     else
       hipLaunchKernelGGL((bn_pool_bwd_reduce_kernel<T, 3, 2>), dim3(nb), dim3(kBlock), 0, st, dyp, ip, xp, ws, g);
     hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + kFinCh - 1) / kFinCh), dim3(kFinCh * kFinRg), 0, st, ws,
-                       nb, M, C, reinterpret_cast<const float*>(gamma), reinterpret_cast<const float*>(save_mean),
+                       ws + int64_t(nb) * C, nb, M, C, reinterpret_cast<const float*>(gamma), reinterpret_cast<const float*>(save_mean),
                        reinterpret_cast<const float*>(save_invstd), reinterpret_cast<float*>(dgamma),
                        reinterpret_cast<float*>(dbeta), k3, int(accumulate));
     if (p22)

@@ -44,6 +44,9 @@ PYBIND11_MODULE(_vodahip, m) {
   m.def("bn_fwd_train", &bn_fwd_train);
   m.def("bn_apply", &bn_apply);
   m.def("bn_bwd", &bn_bwd);
+  m.def("bn2_workspace_floats", &bn2_workspace_floats);
+  m.def("bn2_fwd_train", &bn2_fwd_train);
+  m.def("bn2_bwd", &bn2_bwd);
 
   m.def("bn_pool_workspace_floats", &bn_pool_workspace_floats);
   m.def("bn_pool_fwd_train", &bn_pool_fwd_train);
@@ -54,6 +57,9 @@ PYBIND11_MODULE(_vodahip, m) {
   m.def("gemm_bnstats", &gemm_bnstats, py::arg("x"), py::arg("w"), py::arg("y"), py::arg("part"), py::arg("M"),
         py::arg("N"), py::arg("K"), py::arg("G"), py::arg("stream"), py::arg("accumulate") = false);
   m.def("gemm_f32_stats_supported", &gemm_f32_stats_supported);
+  m.def("gemm_f32_dgrad_bn", &gemm_f32_dgrad_bn);
+  m.def("gemm_f32_dgrad_bn_supported", &gemm_f32_dgrad_bn_supported);
+  m.def("gemm_f32_dgrad_bn_groups", &gemm_f32_dgrad_bn_groups);
   m.def("gemm_f32_stats_groups", &gemm_f32_stats_groups);
   m.def("gemm_f32_stats", &gemm_f32_stats, py::arg("x"), py::arg("w"), py::arg("y"), py::arg("part"), py::arg("M"),
         py::arg("N"), py::arg("K"), py::arg("G"), py::arg("stream"), py::arg("accumulate") = false,

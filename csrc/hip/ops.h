@@ -92,7 +92,21 @@ void bn_apply(uintptr_t x, uintptr_t residual, uintptr_t ab, uintptr_t y, int64_
               uintptr_t stream);
 void bn_bwd(uintptr_t dy, uintptr_t mask, uintptr_t x, uintptr_t save_mean, uintptr_t save_invstd, uintptr_t gamma,
             uintptr_t dx, uintptr_t dres, uintptr_t dgamma, uintptr_t dbeta, uintptr_t workspace, int64_t M, int C,
-            bool relu, bool accumulate, int dt, uintptr_t stream);
+            bool relu, bool accumulate, int dt, uintptr_t stream, uintptr_t pre_part = 0, int pre_nb = 0);
+// dual BN relu?(bn(x) + bn2(x2)) (ResNet downsample blocks): one apply pass forward, one reduce +
+// one apply pass backward for both BatchNorms (workspace = bn2_workspace_floats; the forward's
+// two workspaces are bn_workspace_floats each, or a producing GEMM's statistics, pre_nb > 0)
+int64_t bn2_workspace_floats(int64_t M, int C);
+void bn2_fwd_train(uintptr_t x, uintptr_t x2, uintptr_t gamma, uintptr_t beta, uintptr_t running_mean,
+                   uintptr_t running_var, uintptr_t save_mean, uintptr_t save_invstd, uintptr_t gamma2, uintptr_t beta2,
+                   uintptr_t running_mean2, uintptr_t running_var2, uintptr_t save_mean2, uintptr_t save_invstd2,
+                   uintptr_t y, uintptr_t mask, uintptr_t workspace, uintptr_t workspace2, int64_t M, int C, float eps,
+                   float momentum, bool relu, int dt, uintptr_t stream, int pre_nb, int pre_nb2);
+void bn2_bwd(uintptr_t dy, uintptr_t mask, uintptr_t x, uintptr_t x2, uintptr_t save_mean, uintptr_t save_invstd,
+             uintptr_t gamma, uintptr_t save_mean2, uintptr_t save_invstd2, uintptr_t gamma2, uintptr_t dx,
+             uintptr_t dx2, uintptr_t dgamma, uintptr_t dbeta, uintptr_t dgamma2, uintptr_t dbeta2,
+             uintptr_t workspace, int64_t M, int C, bool relu, bool accumulate, int dt, uintptr_t stream, uintptr_t pre_part = 0,
+             int pre_nb = 0);
 
 // ---- fp32 1x1 conv GEMMs on the f32 MFMA: forward + BN statistics, split-K weight gradient
 // (conv1x1_f32.hip) ----
@@ -101,6 +115,14 @@ int gemm_f32_stats_groups(int64_t M, int N, int K);
 // w: [N][K], or [K][N] with w_kn (the input gradient dX = dY . W with W [Cout][Cin] as stored)
 void gemm_f32_stats(uintptr_t x, uintptr_t w, uintptr_t y, uintptr_t part, int64_t M, int N, int K, int G,
                     uintptr_t stream, bool accumulate, bool w_kn);
+// dX = dY . W (W stored [K = Cout][N = Cin]) + dout * relu-bits(cmask); with nsums = 2 / 3 also the
+// downstream BN's backward partial sums (sum g, sum g*s1 [, sum g*s2], g = dX * bits(smask)) into
+// part[nsums][G][N] (conv1x1_f32.hip gemm_f32_dgrad_bn_kernel)
+bool gemm_f32_dgrad_bn_supported(int64_t M, int N, int K);
+int gemm_f32_dgrad_bn_groups(int64_t M, int N, int K, int nsums);
+void gemm_f32_dgrad_bn(uintptr_t dy, uintptr_t w, uintptr_t y, uintptr_t cg, uintptr_t cmask, uintptr_t smask,
+                       uintptr_t s1, uintptr_t s2, uintptr_t part, int64_t M, int N, int K, int G, int nsums,
+                       uintptr_t stream);
 int64_t wgrad_f32_workspace_floats(int M, int N, int K, int splits);
 std::vector<int> wgrad_f32_config(int M, int N, int K, int splits);
 void wgrad_f32(uintptr_t dy, uintptr_t x, uintptr_t dw, int M, int N, int K, int splits, uintptr_t ws,

@@ -228,3 +228,70 @@ def test_bn_relu_maxpool_eval_path():
     ref = torch.nn.BatchNorm2d(16).cuda().eval()
     ref.load_state_dict(m.state_dict())
     torch.testing.assert_close(m(x), F.max_pool2d(F.relu(ref(x)), 3, 2, 1), atol=1e-5, rtol=1e-5)
+
+
+@pytest.mark.parametrize("shape", [(8, 64, 14, 14), (4, 256, 7, 5), (2, 2048, 3, 3), (32, 256, 28, 28)])
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+def test_bn_pair_matches_fp64_composition(shape, dt):
+    """relu(bn(x) + bn2(x2)) as ONE dual-BN op (FusedBatchNorm2d.forward_pair, the ResNet
+    downsample block's output) vs the fp64 composition of two BatchNorms: output, running
+    statistics, and every gradient (x, x2, both gammas and betas)."""
+    torch.manual_seed(1)
+    dev = "cuda"
+    C = shape[1]
+    a = FusedBatchNorm2d(C, relu=True).to(dev)
+    b = FusedBatchNorm2d(C).to(dev)
+    with torch.no_grad():
+        for m in (a, b):
+            m.weight.uniform_(0.5, 1.5)
+            m.bias.normal_()
+    x = (torch.randn(shape, device=dev) * 2 + 0.5).to(dt).to(memory_format=torch.channels_last).requires_grad_()
+    x2 = (torch.randn(shape, device=dev) - 0.3).to(dt).to(memory_format=torch.channels_last).requires_grad_()
+    y = a.forward_pair(x, b, x2)
+    assert y.is_contiguous(memory_format=torch.channels_last) and y.grad_fn.__class__.__name__ == "_BNAct2FnBackward"
+    xr = x.detach().double().requires_grad_()
+    x2r = x2.detach().double().requires_grad_()
+    p = [t.detach().double().clone().requires_grad_() for t in (a.weight, a.bias, b.weight, b.bias)]
+    rms = [torch.zeros(C, device=dev, dtype=torch.float64) for _ in range(2)]
+    rvs = [torch.ones(C, device=dev, dtype=torch.float64) for _ in range(2)]
+    yr = F.relu(F.batch_norm(xr, rms[0], rvs[0], p[0], p[1], True, 0.1, 1e-5)
+                + F.batch_norm(x2r, rms[1], rvs[1], p[2], p[3], True, 0.1, 1e-5))
+    tol = 3e-2 if dt == torch.bfloat16 else 1e-4
+    torch.testing.assert_close(y.double(), yr, atol=tol, rtol=tol)
+    for m, rm, rv in ((a, rms[0], rvs[0]), (b, rms[1], rvs[1])):
+        torch.testing.assert_close(m.running_mean.double(), rm, atol=1e-4, rtol=1e-4)
+        torch.testing.assert_close(m.running_var.double(), rv, atol=1e-3, rtol=1e-3)
+    dy = torch.randn(shape, device=dev).to(dt).to(memory_format=torch.channels_last)
+    y.backward(dy)
+    yr.backward(dy.double())
+    gtol = 5e-2 if dt == torch.bfloat16 else 1e-3
+    torch.testing.assert_close(x.grad.double(), xr.grad, atol=gtol, rtol=gtol)
+    torch.testing.assert_close(x2.grad.double(), x2r.grad, atol=gtol, rtol=gtol)
+    M = x.numel() // C
+    for got, ref in zip((a.weight.grad, a.bias.grad, b.weight.grad, b.bias.grad), p):
+        torch.testing.assert_close(got.double(), ref.grad, atol=gtol * M ** 0.5, rtol=gtol)
+
+
+def test_resnet_downsample_block_pair_matches_two_bns(monkeypatch):
+    """A ResNet-50 downsample bottleneck (fp32, channels_last, the GEMM / GradSink path) gives
+    the same output and gradients with the dual-BN op as with bn3 + the shortcut BN apart."""
+    from vodascheduler_amd.models import resnet as R
+
+    torch.manual_seed(0)
+    blk = R.Bottleneck(256, 128, stride=2, downsample=torch.nn.Sequential(
+        R.Conv1x1(256, 512, stride=2), FusedBatchNorm2d(512))).cuda()
+    with torch.no_grad():
+        blk.bn3.weight.uniform_(0.5, 1.5)
+    x = torch.randn(16, 256, 28, 28, device="cuda").to(memory_format=torch.channels_last)
+    dy = torch.randn(16, 512, 14, 14, device="cuda").to(memory_format=torch.channels_last)
+    outs = []
+    for fuse in (True, False):
+        monkeypatch.setattr(R, "FUSE_DOWNSAMPLE_BN", fuse)
+        xi = x.clone().requires_grad_()
+        for p_ in blk.parameters():
+            p_.grad = None
+        y = blk(xi)
+        y.backward(dy)
+        outs.append([y.detach(), xi.grad] + [p_.grad.clone() for p_ in blk.parameters()])
+    for u, v in zip(*outs):
+        torch.testing.assert_close(u, v, atol=1e-3, rtol=1e-3)  # fp32 summation order only

@@ -128,3 +128,105 @@ def test_conv1x1_fp32_bn_statistics_attached():
     yr = F.conv2d(x.double(), conv.weight.double())
     zr = F.relu(F.batch_norm(yr, None, None, bn.weight.double(), bn.bias.double(), training=True, eps=bn.eps))
     assert _rel(z, zr) < 1e-5
+
+
+def _bits(m: torch.Tensor) -> torch.Tensor:
+    """[M, C] bool -> the BN forward's 1-bit ReLU mask ([M * C / 8] bytes, bit k of byte (r, g) =
+    channel 8 g + k)."""
+    M, C = m.shape
+    w = (m.view(M, C // 8, 8).to(torch.int32) << torch.arange(8, device=m.device, dtype=torch.int32)).sum(-1)
+    return w.to(torch.uint8).reshape(-1).contiguous()
+
+
+@pytest.mark.parametrize("M,K,N", [(4096, 64, 256), (3000, 128, 512), (1111, 256, 1024), (50176, 64, 256)])
+@pytest.mark.parametrize("nsums", [0, 2, 3])
+def test_fused_dgrad_bn_matches_fp64(M, K, N, nsums):
+    """gemm_f32_dgrad_bn: dX = dY . W + g * bits(cmask) and the downstream BN's backward sums
+    (sum h, sum h*y3 [, sum h*y_ds], h = dX * bits(smask)) vs fp64; ragged M exercises the
+    buffer-clamped tail rows."""
+    from vodascheduler_amd.ops import _native
+
+    h = _native.hip()
+    torch.manual_seed(M + K + nsums)
+    dev = "cuda"
+    dy = torch.randn(M, K, device=dev)
+    w = torch.randn(K, N, device=dev) / K ** 0.5
+    g = torch.randn(M, N, device=dev)
+    cm = torch.rand(M, N, device=dev) > 0.4
+    sm = torch.rand(M, N, device=dev) > 0.5
+    y3 = torch.randn(M, N, device=dev)
+    yd = torch.randn(M, N, device=dev)
+    G = h.gemm_f32_dgrad_bn_groups(M, N, K, nsums)
+    out = torch.empty(M, N, device=dev)
+    part = torch.empty(max(1, nsums * G * N), device=dev)
+    cmb, smb = _bits(cm), _bits(sm)
+    h.gemm_f32_dgrad_bn(dy.data_ptr(), w.data_ptr(), out.data_ptr(), g.data_ptr(), cmb.data_ptr(),
+                        smb.data_ptr() if nsums else 0, y3.data_ptr() if nsums else 0,
+                        yd.data_ptr() if nsums == 3 else 0, part.data_ptr() if nsums else 0, M, N, K, G, nsums,
+                        torch.cuda.current_stream().cuda_stream)
+    ref = dy.double() @ w.double() + g.double() * cm
+    torch.testing.assert_close(out.double(), ref, atol=1e-4, rtol=1e-5)
+    if nsums:
+        hh = ref * sm
+        want = [hh.sum(0), (hh * y3.double()).sum(0), (hh * yd.double()).sum(0)][:nsums]
+        got = part[:nsums * G * N].view(nsums, G, N).double().sum(1)
+        for j in range(nsums):
+            torch.testing.assert_close(got[j], want[j], atol=2e-3 * M ** 0.5, rtol=1e-4)
+
+
+@pytest.mark.parametrize("fuse_pair", [True, False])
+def test_resnet_stage_fused_dgrad_bn_matches_unfused(monkeypatch, fuse_pair):
+    """A ResNet-50 stage (downsample block + two identity blocks, fp32 channels_last): with the
+    fused input gradient + BN handoff the output, the input gradient and every parameter
+    gradient equal the unfused path's (hipBLASLt beta = 1 + BN reduce passes) to fp32 order."""
+    from vodascheduler_amd.models import resnet as R
+    from vodascheduler_amd.ops import conv1x1 as C
+    from vodascheduler_amd.ops.batchnorm import FusedBatchNorm2d
+
+    monkeypatch.setattr(R, "FUSE_DOWNSAMPLE_BN", fuse_pair)
+    torch.manual_seed(0)
+    blocks = torch.nn.Sequential(
+        R.Bottleneck(256, 128, stride=2, downsample=torch.nn.Sequential(R.Conv1x1(256, 512, stride=2),
+                                                                        FusedBatchNorm2d(512))),
+        R.Bottleneck(512, 128), R.Bottleneck(512, 128)).cuda()
+    with torch.no_grad():
+        for b in blocks:
+            b.bn3.weight.uniform_(0.5, 1.5)
+    x = torch.randn(8, 256, 28, 28, device="cuda").to(memory_format=torch.channels_last)
+    dy = torch.randn(8, 512, 14, 14, device="cuda").to(memory_format=torch.channels_last)
+    from vodascheduler_amd.ops import batchnorm as B
+
+    calls = {"kernel": 0, "sums": 0}
+    real_fused, real_take = C.fused_dgrad_bn, B.BwdHandoff.take
+
+    def fused(*a):
+        r = real_fused(*a)
+        calls["kernel"] += r is not None
+        return r
+
+    def take(self, dy):
+        r = real_take(self, dy)
+        calls["sums"] += r is not None
+        return r
+
+    monkeypatch.setattr(C, "fused_dgrad_bn", fused)
+    monkeypatch.setattr(B.BwdHandoff, "take", take)
+    outs = []
+    for fused_on in (True, False):
+        monkeypatch.setattr(C, "USE_FUSED_DGRAD_BN", fused_on)
+        xi = x.clone().requires_grad_()
+        for p_ in blocks.parameters():
+            p_.grad = None
+        y = blocks(xi)
+        y.backward(dy)
+        outs.append([y.detach(), xi.grad] + [p_.grad.clone() for p_ in blocks.parameters()])
+        if fused_on:  # both identity blocks ran the fused kernel; blocks 1 and 2's bn3 took its sums
+            assert calls == {"kernel": 2, "sums": 2}, calls
+    # relative Frobenius error per tensor: MIOpen's split-K convolutions accumulate with atomics,
+    # so two runs of the SAME path already differ in the last bits, and the BN backward's
+    # cancellations (sum g*x - mean * sum g) amplify any summation-order change elementwise;
+    # the exact semantics are pinned by test_fused_dgrad_bn_matches_fp64
+    names = ["y", "x.grad"] + [n for n, _ in blocks.named_parameters()]
+    rel = [(nm, float((u - v).norm() / v.norm().clamp_min(1e-12))) for nm, u, v in zip(names, *outs)]
+    bad = [(nm, e) for nm, e in rel if e > 1e-4]
+    assert not bad, bad

@@ -15,14 +15,20 @@ the bottleneck's shortcut gradient is accumulated by conv1's input-gradient GEMM
 """
 from __future__ import annotations
 
+import os
+
 import torch
 from torch import nn
 
 from ..ops.batchnorm import FusedBatchNorm2d
-from ..ops.conv1x1 import USE_GRAD_SINK, Conv1x1, GradSink
+from ..ops.conv1x1 import USE_GRAD_SINK, Conv1x1, GradSink, fused_dgrad_bn_ok
 from ..ops.conv3x3 import ConvKxK
 from ..ops.pool import GlobalAvgPool2d
 from ..ops.stem import FusedStem
+
+# VODA_BN_PAIR=0: downsample blocks run bn3 and the shortcut BN as two fused BNs (A/B switch for
+# ops/batchnorm._BNAct2Fn)
+FUSE_DOWNSAMPLE_BN = os.environ.get("VODA_BN_PAIR", "1") != "0"
 
 
 class Bottleneck(nn.Module):
@@ -45,14 +51,24 @@ class Bottleneck(nn.Module):
         sink = None
         if (USE_GRAD_SINK and self.training and torch.is_grad_enabled() and x.requires_grad
                 and self.conv1._gemm_ok(x)):
-            sink = GradSink()
+            # identity blocks at fp32: conv1's input gradient reads bn3's masked shortcut
+            # gradient in its epilogue (ops/conv1x1.fused_dgrad_bn), so bn3 hands it over unwritten
+            lazy = (self.downsample is None and x.dtype == torch.float32 and self.conv1.stride == (1, 1)
+                    and fused_dgrad_bn_ok(x.shape[0] * x.shape[2] * x.shape[3], self.conv1.in_channels,
+                                          self.conv1.out_channels))
+            sink = GradSink(lazy)
         out = self.bn1(self.conv1(x, sink_in=sink))
         out = self.bn2(self.conv2(out))
         if self.downsample is None:
             return self.bn3(self.conv3(out), x, sink=sink)
         ds = self.downsample
         if isinstance(ds, nn.Sequential) and len(ds) == 2 and isinstance(ds[0], Conv1x1):
-            idt = ds[1](ds[0](x, sink_out=sink))
+            y_ds = ds[0](x, sink_out=sink)
+            if FUSE_DOWNSAMPLE_BN and isinstance(ds[1], FusedBatchNorm2d):
+                # relu(bn3(y3) + bn_ds(y_ds)) as one dual-BN op: the shortcut tensor is never
+                # written, and one reduce + one apply pass give both BNs' gradients
+                return self.bn3.forward_pair(self.conv3(out), ds[1], y_ds)
+            idt = ds[1](y_ds)
         else:
             idt = ds(x)
         return self.bn3(self.conv3(out), idt)

@@ -56,10 +56,67 @@ def _direct_fp32(p) -> bool:
     return g is not None and g.dtype == torch.float32 and g.is_contiguous()
 
 
+class BwdHandoff:
+    """Side channel from the GEMM that produces a BN's output gradient to that BN's backward.
+
+    A ResNet block output ``x_b = relu(bn3(y3) + shortcut)`` feeds the next block's conv1,
+    whose input-gradient GEMM (conv1x1_f32.hip ``gemm_f32_dgrad_bn``) writes x_b's gradient.
+    The forward attaches this object to x_b (``HANDOFF_ATTR``) with what bn3's backward reduce
+    pass would read -- its ReLU bits and input(s) -- so the GEMM's epilogue accumulates the
+    reduce pass's sums (sum g, sum g*y3 [, sum g*y_ds]) and ``put``s them here; bn3's backward
+    ``take``s them and runs only its finalize and apply passes.  The sums are used only when
+    the gradient bn3 receives IS the tensor they were computed over."""
+
+    __slots__ = ("mask", "x", "x2", "part", "nb", "grad")
+
+    def __init__(self, mask, x, x2=None):
+        self.mask, self.x, self.x2 = mask, x, x2
+        self.part, self.nb, self.grad = None, 0, None
+
+    def put(self, part: torch.Tensor, nb: int, grad: torch.Tensor) -> None:
+        self.part, self.nb, self.grad = part, int(nb), grad
+
+    def take(self, dy: torch.Tensor):
+        """(partials, nb) when ``dy`` is the tensor the sums were computed over, else None."""
+        got, g = (self.part, self.nb), self.grad
+        self.part, self.nb, self.grad = None, 0, None
+        # the same storage, and dy a dense row-major [M][C] view of it (channels_last or 2-D)
+        if got[0] is None or g is None or dy.data_ptr() != g.data_ptr() or dy.numel() != g.numel() \
+                or not _rows_view_ok(dy):
+            return None
+        return got
+
+
+HANDOFF_ATTR = "_voda_bn_bwd_handoff"
+
+
+class MaskedGrad:
+    """A shortcut gradient ``g * relu_bits`` handed through a GradSink WITHOUT being
+    materialised: the consuming input-gradient GEMM reads ``g`` and the 1-bit ReLU mask of
+    the BN forward in its epilogue (ops/conv1x1.py fused path)."""
+
+    __slots__ = ("g", "mask")
+
+    def __init__(self, g: torch.Tensor, mask: torch.Tensor):
+        self.g, self.mask = g, mask
+
+    def dense(self) -> torch.Tensor:
+        """The masked gradient as a tensor (fallback consumers)."""
+        C = self.g.shape[1]
+        bits = (self.mask.view(-1, 1) >> torch.arange(8, device=self.mask.device, dtype=torch.uint8)) & 1
+        m = bits.view(-1, C).to(self.g.dtype)  # [M][C] in channels_last row order
+        g2 = self.g.permute(0, 2, 3, 1).reshape(-1, C) if self.g.dim() == 4 else self.g
+        out = (g2 * m)
+        if self.g.dim() == 4:
+            n, _, h, w = self.g.shape
+            return out.view(n, h, w, C).permute(0, 3, 1, 2)
+        return out
+
+
 class _BNActFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, residual, weight, bias, running_mean, running_var, momentum, eps, relu, sink=None,
-                stats=None):
+                stats=None, handoff=None):
         """``stats``: (workspace, nb) whose first 2 x nb x C floats are the producing GEMM's
         per-block sums / sums of squares of ``x`` (ops/conv1x1.py, gemm_bnstats.hip): the
         statistics pass is skipped."""
@@ -82,6 +139,9 @@ class _BNActFn(torch.autograd.Function):
         ctx.has_res = residual is not None
         ctx.bias = bias
         ctx.sink = sink if residual is not None else None
+        ctx.handoff = handoff
+        if handoff is not None:
+            handoff.mask, handoff.x = mask, x
         ctx.save_for_backward(x, mask, weight, save_mean, save_invstd)
         return y
 
@@ -94,7 +154,12 @@ class _BNActFn(torch.autograd.Function):
         if not _rows_view_ok(dy) or dy.stride() != x.stride():
             dy = dy.contiguous(memory_format=torch.channels_last) if dy.dim() == 4 else dy.contiguous()
         dx = torch.empty_like(x)
-        dres = torch.empty_like(x) if ctx.has_res and ctx.needs_input_grad[1] else None
+        pre = ctx.handoff.take(dy) if ctx.handoff is not None else None
+        # a sink whose consumer reads the masked shortcut gradient in its GEMM epilogue: hand
+        # over (dy, ReLU bits) instead of writing dres = dy * bits
+        lazy = (ctx.sink is not None and getattr(ctx.sink, "lazy", False) and ctx.relu and ctx.has_res
+                and ctx.needs_input_grad[1])
+        dres = torch.empty_like(x) if ctx.has_res and ctx.needs_input_grad[1] and not lazy else None
         need_w = weight is not None and ctx.needs_input_grad[2]
         need_b = ctx.needs_input_grad[3]
         bias = ctx.bias
@@ -109,8 +174,10 @@ class _BNActFn(torch.autograd.Function):
         ws = torch.empty(h.bn_workspace_floats(M, C), dtype=torch.float32, device=x.device)
         h.bn_bwd(dy.data_ptr(), N.ptr(mask), x.data_ptr(), save_mean.data_ptr(), save_invstd.data_ptr(), N.ptr(weight),
                  dx.data_ptr(), N.ptr(dres), N.ptr(dw), N.ptr(db), ws.data_ptr(), M, C, ctx.relu, direct,
-                 N.dtype_code(x.dtype), N.stream_of(x))
-        if dres is not None and ctx.sink is not None:
+                 N.dtype_code(x.dtype), N.stream_of(x), N.ptr(pre[0]) if pre else 0, pre[1] if pre else 0)
+        if lazy:
+            ctx.sink.put(MaskedGrad(dy, mask))
+        elif dres is not None and ctx.sink is not None:
             ctx.sink.put(dres)  # a fresh tensor: the consumer may accumulate into it in place
             dres = None
         if dres is None and ctx.has_res and ctx.needs_input_grad[1] and ctx.sink is None:
@@ -119,8 +186,76 @@ class _BNActFn(torch.autograd.Function):
             if weight is not None:
                 _ready(weight)
             _ready(bias)
-            return dx, dres, None, None, None, None, None, None, None, None, None
-        return dx, dres, dw, db, None, None, None, None, None, None, None
+            return dx, dres, None, None, None, None, None, None, None, None, None, None
+        return dx, dres, dw, db, None, None, None, None, None, None, None, None
+
+
+class _BNAct2Fn(torch.autograd.Function):
+    """``relu?(bn(x) + bn2(x2))`` in training mode (csrc/hip/batchnorm.hip ``bn2_*``): the
+    second BN's output -- a ResNet downsample block's shortcut -- is never materialised, and
+    both BNs share one reduce pass and one apply pass backward."""
+
+    @staticmethod
+    def forward(ctx, x, x2, weight, bias, running_mean, running_var, weight2, bias2, running_mean2, running_var2,
+                momentum, eps, relu, stats, stats2, handoff=None):
+        C = x.shape[1]
+        M = x.numel() // C
+        h = N.hip()
+        y = torch.empty_like(x)
+        f32 = dict(dtype=torch.float32, device=x.device)
+        sm, si, sm2, si2 = (torch.empty(C, **f32) for _ in range(4))
+        ws, nb = stats if stats is not None else (torch.empty(h.bn_workspace_floats(M, C), **f32), 0)
+        ws2, nb2 = stats2 if stats2 is not None else (torch.empty(h.bn_workspace_floats(M, C), **f32), 0)
+        mask = torch.empty(M * (C // 8), dtype=torch.uint8, device=x.device) if relu else None
+        h.bn2_fwd_train(x.data_ptr(), x2.data_ptr(), N.ptr(weight), N.ptr(bias), N.ptr(running_mean),
+                        N.ptr(running_var), sm.data_ptr(), si.data_ptr(), N.ptr(weight2), N.ptr(bias2),
+                        N.ptr(running_mean2), N.ptr(running_var2), sm2.data_ptr(), si2.data_ptr(), y.data_ptr(),
+                        N.ptr(mask), ws.data_ptr(), ws2.data_ptr(), M, C, float(eps), float(momentum), bool(relu),
+                        N.dtype_code(x.dtype), N.stream_of(x), int(nb), int(nb2))
+        ctx.relu = bool(relu)
+        ctx.biases = (bias, bias2)
+        ctx.handoff = handoff
+        if handoff is not None:
+            handoff.mask, handoff.x, handoff.x2 = mask, x, x2
+        ctx.save_for_backward(x, x2, mask, weight, weight2, sm, si, sm2, si2)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, x2, mask, weight, weight2, sm, si, sm2, si2 = ctx.saved_tensors
+        bias, bias2 = ctx.biases
+        C = x.shape[1]
+        M = x.numel() // C
+        h = N.hip()
+        if not _rows_view_ok(dy) or dy.stride() != x.stride():
+            dy = dy.contiguous(memory_format=torch.channels_last) if dy.dim() == 4 else dy.contiguous()
+        dx, dx2 = torch.empty_like(x), torch.empty_like(x2)
+        nw = (weight is not None and ctx.needs_input_grad[2], weight2 is not None and ctx.needs_input_grad[6])
+        nbias = (ctx.needs_input_grad[3], ctx.needs_input_grad[7])
+        # fp32 gamma / beta gradients straight into the optimizer's flat buffers when it owns
+        # all four, else into fresh tensors (same contract as _BNActFn)
+        direct = all(nbias) and all(_direct_fp32(b) for b in (bias, bias2)) and all(
+            (n and _direct_fp32(w_)) or w_ is None for n, w_ in zip(nw, (weight, weight2)))
+        f32 = dict(dtype=torch.float32, device=x.device)
+        if direct:
+            dw, db, dw2, db2 = flat_grad(weight), flat_grad(bias), flat_grad(weight2), flat_grad(bias2)
+        else:
+            dw = torch.empty(C, **f32) if nw[0] else None
+            db = torch.empty(C, **f32) if nbias[0] else None
+            dw2 = torch.empty(C, **f32) if nw[1] else None
+            db2 = torch.empty(C, **f32) if nbias[1] else None
+        pre = ctx.handoff.take(dy) if ctx.handoff is not None else None
+        ws = torch.empty(h.bn2_workspace_floats(M, C), **f32)
+        h.bn2_bwd(dy.data_ptr(), N.ptr(mask), x.data_ptr(), x2.data_ptr(), sm.data_ptr(), si.data_ptr(), N.ptr(weight),
+                  sm2.data_ptr(), si2.data_ptr(), N.ptr(weight2), dx.data_ptr(), dx2.data_ptr(), N.ptr(dw), N.ptr(db),
+                  N.ptr(dw2), N.ptr(db2), ws.data_ptr(), M, C, ctx.relu, direct, N.dtype_code(x.dtype),
+                  N.stream_of(x), N.ptr(pre[0]) if pre else 0, pre[1] if pre else 0)
+        if direct:
+            for t in (weight, bias, weight2, bias2):
+                if t is not None:
+                    _ready(t)
+            return dx, dx2, None, None, None, None, None, None, None, None, None, None, None, None, None, None
+        return dx, dx2, dw, db, None, None, dw2, db2, None, None, None, None, None, None, None, None
 
 
 STATS_ATTR = "_voda_bn_stats"
@@ -161,7 +296,12 @@ def batch_norm_act(x: torch.Tensor, weight: torch.Tensor | None, bias: torch.Ten
         return _reference(x, weight, bias, running_mean, running_var, training, momentum, eps, residual, relu)
     if training or running_mean is None:
         stats = take_stats(x)
-        return _BNActFn.apply(x, residual, weight, bias, running_mean, running_var, momentum, eps, relu, sink, stats)
+        hand = BwdHandoff(None, None) if (relu and residual is not None and x.dtype == torch.float32) else None
+        y = _BNActFn.apply(x, residual, weight, bias, running_mean, running_var, momentum, eps, relu, sink, stats,
+                           hand)
+        if hand is not None:
+            setattr(y, HANDOFF_ATTR, hand)
+        return y
     # inference: per-channel affine from the running statistics, one apply pass
     C = x.shape[1]
     invstd = torch.rsqrt(running_var.float() + eps)
@@ -293,6 +433,36 @@ class FusedBatchNorm2d(torch.nn.BatchNorm2d):
                               self.running_mean if self.track_running_stats else None,
                               self.running_var if self.track_running_stats else None,
                               use_batch, momentum, self.eps, residual, self.relu, sink)
+
+    def _count_batch(self) -> None:
+        if self.training and self.track_running_stats:
+            if self.momentum is None:
+                self.num_batches_tracked.add_(1)
+            else:
+                self._pending_batches = getattr(self, "_pending_batches", 0) + 1
+
+    def forward_pair(self, x, other: "FusedBatchNorm2d", x2):
+        """``relu?(self(x) + other(x2))`` -- a ResNet downsample block's output with its
+        shortcut BN folded in (``_BNAct2Fn``: no materialised shortcut, one shared backward
+        reduce / apply).  Falls back to the two-module composition off the fused path."""
+        ok = (USE_FUSED_BN and self.training and other.training and self.track_running_stats
+              and other.track_running_stats and not other.relu and self.momentum is not None
+              and other.momentum is not None and self.momentum == other.momentum and self.eps == other.eps
+              and _supported(x, x2) and x.shape == x2.shape
+              and all(t is None or t.dtype == torch.float32 for m_ in (self, other)
+                      for t in (m_.weight, m_.bias, m_.running_mean, m_.running_var)))
+        if not ok:
+            return self(x, other(x2))
+        self._count_batch()
+        other._count_batch()
+        hand = BwdHandoff(None, None) if (self.relu and x.dtype == torch.float32) else None
+        with torch.autocast("cuda", enabled=False):
+            y = _BNAct2Fn.apply(x, x2, self.weight, self.bias, self.running_mean, self.running_var, other.weight,
+                                other.bias, other.running_mean, other.running_var, self.momentum, self.eps,
+                                self.relu, take_stats(x), take_stats(x2), hand)
+        if hand is not None:
+            setattr(y, HANDOFF_ATTR, hand)
+        return y
 
     def extra_repr(self):
         return super().extra_repr() + f", relu={self.relu}"

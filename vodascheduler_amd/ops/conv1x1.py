@@ -88,6 +88,51 @@ USE_SINK_GEMM_F32 = os.environ.get("VODA_SINK_GEMM_F32", "0") != "0"
 USE_SINK_GEMM_BF16 = os.environ.get("VODA_SINK_GEMM_BF16", "0") != "0"
 
 
+# fp32 identity bottlenecks: conv1's input gradient reads the masked shortcut gradient and
+# accumulates the previous block's bn3 backward sums in its epilogue (gemm_f32_dgrad_bn,
+# ops/batchnorm.BwdHandoff / MaskedGrad).  VODA_FUSED_DGRAD_BN=0: hipBLASLt beta = 1 + separate
+# BN reduce pass (A/B switch)
+USE_FUSED_DGRAD_BN = os.environ.get("VODA_FUSED_DGRAD_BN", "1") != "0"
+
+
+def fused_dgrad_bn_ok(m: int, cin: int, cout: int) -> bool:
+    """Does gemm_f32_dgrad_bn cover dX [m, cin] = dY [m, cout] . W [cout, cin]?"""
+    return USE_FUSED_DGRAD_BN and bool(N.hip().gemm_f32_dgrad_bn_supported(m, cin, cout))
+
+
+def fused_dgrad_bn(dy2: torch.Tensor, w2: torch.Tensor, acc, handoff) -> torch.Tensor | None:
+    """dX [M, N] = dY [M, K] . W [K, N] + acc.g * relu_bits(acc.mask) on the fused kernel, with
+    the previous block's bn3 backward sums put into ``handoff`` when it describes dX; None when
+    the kernel does not cover the operands (the caller materialises the masked gradient)."""
+    from .batchnorm import BwdHandoff
+
+    M, K = dy2.shape
+    Nn = w2.shape[1]
+    g = acc.g
+    if (not USE_FUSED_DGRAD_BN or dy2.dtype != torch.float32 or g.dtype != torch.float32 or not dy2.is_contiguous()
+            or dy2.data_ptr() % 16 or not w2.is_contiguous() or g.numel() != M * Nn
+            or not g.is_contiguous(memory_format=torch.channels_last) or acc.mask.numel() * 8 != M * Nn):
+        return None
+    h = N.hip()
+    if not h.gemm_f32_dgrad_bn_supported(M, Nn, K):
+        return None
+    hand = handoff if isinstance(handoff, BwdHandoff) and handoff.mask is not None else None
+    if hand is not None and (hand.x.numel() != M * Nn or hand.x.dtype != torch.float32
+                             or (hand.x2 is not None and hand.x2.numel() != M * Nn)):
+        hand = None
+    ns = 0 if hand is None else (3 if hand.x2 is not None else 2)
+    G = h.gemm_f32_dgrad_bn_groups(M, Nn, K, ns)
+    out = torch.empty(M, Nn, dtype=torch.float32, device=dy2.device)
+    part = torch.empty(max(1, ns * G * Nn), dtype=torch.float32, device=dy2.device) if ns else None
+    h.gemm_f32_dgrad_bn(dy2.data_ptr(), w2.data_ptr(), out.data_ptr(), g.data_ptr(), acc.mask.data_ptr(),
+                        N.ptr(hand.mask) if hand else 0, N.ptr(hand.x) if hand else 0,
+                        N.ptr(hand.x2) if hand and hand.x2 is not None else 0, N.ptr(part), M, Nn, K, G, ns,
+                        N.stream_of(dy2))
+    if hand is not None:
+        hand.put(part, G, out)
+    return out
+
+
 class GradSink:
     """One-shot hand-off of an activation gradient between the two backward nodes of a
     tensor with two consumers (a residual block input feeds the block's first 1x1
@@ -100,10 +145,12 @@ class GradSink:
     output gradient only exists once the whole residual branch (which ends at the
     producer) has been back-propagated."""
 
-    __slots__ = ("buf",)
+    __slots__ = ("buf", "lazy")
 
-    def __init__(self):
+    def __init__(self, lazy: bool = False):
         self.buf = None
+        # the consumer runs the fused input gradient: the producer may hand over a MaskedGrad
+        self.lazy = lazy
 
     def put(self, g: torch.Tensor) -> None:
         self.buf = g
@@ -292,6 +339,11 @@ class _Conv1x1Fn(torch.autograd.Function):
         ctx.meta = (x.shape, stride, n, h, w)
         ctx.sink_in = sink_in if stride == 1 else None
         ctx.sink_out = sink_out
+        # the previous block's bn3 backward handoff (ops/batchnorm.BwdHandoff): filled by the
+        # fused input gradient below
+        from .batchnorm import HANDOFF_ATTR
+
+        ctx.handoff = getattr(x, HANDOFF_ATTR, None) if sink_in is not None else None
         return y2.view(n, h, w, cout).permute(0, 3, 1, 2)  # channels_last NCHW
 
     @staticmethod
@@ -307,6 +359,15 @@ class _Conv1x1Fn(torch.autograd.Function):
         w2 = weight.reshape(cout, cin)
         dx = None
         acc = ctx.sink_in.take() if ctx.sink_in is not None and ctx.needs_input_grad[0] else None
+        from .batchnorm import MaskedGrad
+
+        if isinstance(acc, MaskedGrad):
+            dx2 = fused_dgrad_bn(dy2, w2, acc, ctx.handoff)
+            if dx2 is not None:
+                acc = None
+                dx = dx2.view(n, h, w, cin).permute(0, 3, 1, 2)
+            else:
+                acc = acc.dense()
         strided = None
         if isinstance(acc, _StridedGrad):
             if tuple(acc.shape) == tuple(in_shape) and acc.g.dtype == dy2.dtype:
@@ -329,6 +390,8 @@ class _Conv1x1Fn(torch.autograd.Function):
             if not own:
                 _as_2d(acc).addmm_(dy2, w2)  # dX = shortcut gradient + dY . W (one GEMM, beta = 1)
             dx = acc
+        elif dx is not None:
+            pass  # the fused input gradient above
         elif ctx.needs_input_grad[0]:
             dx2 = mfma_dgrad(dy2, w2)
             dxs = (dx2 if dx2 is not None else dy2 @ w2).view(n, h, w, cin).permute(0, 3, 1, 2)
