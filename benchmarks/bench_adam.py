@@ -1,6 +1,6 @@
 """Fused Adam / AdamW step (csrc/hip/optim.hip) on a BERT-base-sized flat buffer (110 M fp32
-params, fp32 gradients, bf16 model copy): HBM throughput of the kernel variants -- one or two
-float4 groups in flight per thread (VODA_ADAM_U).  Bytes per element: p g m v read (16) + p m v written (12) + bf16 copy (2).
+params, fp32 gradients, bf16 model copy): HBM throughput, with and without the bf16 copy.  Bytes
+per element: p g m v read (16) + p m v written (12) + bf16 copy (2).
 
 python benchmarks/bench_adam.py [--n 110000000]
 """
@@ -31,27 +31,23 @@ def main():
     lp = torch.empty(n, device="cuda", dtype=torch.bfloat16)
     s = torch.cuda.current_stream().cuda_stream
     for lowp in (True, False):
-        for u in (1, 2):
-            h.adam_set_unroll(u)
-
-            def step(k):
-                h.adam_step(p.data_ptr(), g.data_ptr(), N.dtype_code(g.dtype), m.data_ptr(), v.data_ptr(),
-                            lp.data_ptr() if lowp else 0, N.dtype_code(lp.dtype) if lowp else -1, n, 1e-4, 0.9,
-                            0.999, 1e-8, 1e-2, True, k, 1.0, 0, s)
-            for k in range(3):
-                step(k + 1)
-            torch.cuda.synchronize()
-            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            e0.record()
-            for k in range(a.iters):
-                step(k + 4)
-            e1.record()
-            torch.cuda.synchronize()
-            us = e0.elapsed_time(e1) / a.iters * 1e3
-            nbytes = n * (28 + (2 if lowp else 0))
-            print(json.dumps({"n": n, "bf16_copy": lowp, "unroll": u, "us": round(us, 1),
-                              "TBps": round(nbytes / us / 1e6, 2)}), flush=True)
-    h.adam_set_unroll(-1)
+        def step(k):
+            h.adam_step(p.data_ptr(), g.data_ptr(), N.dtype_code(g.dtype), m.data_ptr(), v.data_ptr(),
+                        lp.data_ptr() if lowp else 0, N.dtype_code(lp.dtype) if lowp else -1, n, 1e-4, 0.9,
+                        0.999, 1e-8, 1e-2, True, k, 1.0, 0, s)
+        for k in range(3):
+            step(k + 1)
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for k in range(a.iters):
+            step(k + 4)
+        e1.record()
+        torch.cuda.synchronize()
+        us = e0.elapsed_time(e1) / a.iters * 1e3
+        nbytes = n * (28 + (2 if lowp else 0))
+        print(json.dumps({"n": n, "bf16_copy": lowp, "us": round(us, 1),
+                          "TBps": round(nbytes / us / 1e6, 2)}), flush=True)
 
 
 if __name__ == "__main__":

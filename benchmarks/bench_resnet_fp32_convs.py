@@ -79,7 +79,6 @@ def main():
             rec["blas_dgrad_us"] = timeit(lambda: dy2 @ w2)
             rec["blas_wgrad_us"] = timeit(lambda: dy2.t() @ x2)
             # own f32-MFMA kernels (csrc/hip/conv1x1_f32.hip)
-            from vodascheduler_amd.ops import wgrad as W
             from vodascheduler_amd.ops.conv1x1 import StatsHolder, gemm_f32_2d
 
             x2c = x2.contiguous()
@@ -88,12 +87,6 @@ def main():
             wt = w2.t().contiguous()
             if gemm_f32_2d(dy2, wt) is not None:
                 rec["own_dgrad_us"] = timeit(lambda: gemm_f32_2d(dy2, wt))
-            gw = torch.zeros(cout, cin, device=dev)
-            rec["own_wgrad_us"] = timeit(lambda: W.wgrad_f32_accumulate_(dy2, x2c, gw))
-            ref = (dy2.double().t() @ x2c.double()).float()
-            gw.zero_()
-            W.wgrad_f32_accumulate_(dy2, x2c, gw)
-            rec["own_wgrad_relerr"] = float((gw - ref).norm() / ref.norm())
         if a.only_1x1 and k != 1:
             continue
         for key in [k_ for k_ in rec if k_.endswith("_us")]:

@@ -1,17 +1,15 @@
 """ResNet-50 stem kernels (csrc/hip/stem.hip) at bs 256, 224 x 224: pack, conv forward with
 BN statistics, weight gradient -- and MIOpen's forward / weight gradient of the same conv for
-reference.  ``--debug MASK`` sets VODA_STEM_DEBUG for the forward-kernel ablations (1 no
-output stores, 2 no prefetch loads, 4 no MFMAs, 8 no epilogue); ``--sweep`` runs the
-ablations, each in its own process (the mask is read once).
+reference.  (The round-2 forward-kernel ablation masks were removed in round 5; their results
+are in profiles/raw/r2_stem_micro.jsonl.)
 
-python benchmarks/bench_stem.py [--sweep]
+python benchmarks/bench_stem.py
 """
 from __future__ import annotations
 
 import argparse
 import json
 import os
-import subprocess
 import sys
 
 B = 256
@@ -32,7 +30,7 @@ def t_us(fn, it=20):
     return e0.elapsed_time(e1) / it * 1e3
 
 
-def run(debug: int) -> dict:
+def run() -> dict:
     import torch
     import torch.nn.functional as F
 
@@ -48,33 +46,21 @@ def run(debug: int) -> dict:
     gw = torch.zeros(64, 3, 7, 7, device="cuda").to(memory_format=torch.channels_last)
     h = S.N.hip()
     ws = torch.empty(h.stem_wgrad_workspace_floats(B, 112), dtype=torch.float32, device="cuda")
-    out = {"debug": debug,
-           "pack_us": t_us(lambda: S.pack_nhwc4(x)),
+    out = {"pack_us": t_us(lambda: S.pack_nhwc4(x)),
            "conv_fwd_stats_us": t_us(lambda: S.stem_conv_stats(x4, w, 3))}
-    if debug == 0:
-        out["wgrad_us"] = t_us(lambda: h.stem_conv_wgrad(x4.data_ptr(), dyc.data_ptr(), gw.data_ptr(), *gw.stride(), 3,
-                                                         ws.data_ptr(), B, 224, 224, 112, 112, True, 0,
-                                                         S.N.stream_of(x4)))
-        xb = x.bfloat16()
-        out["miopen_fwd_us"] = t_us(lambda: F.conv2d(xb, w, stride=2, padding=3))
-        out["miopen_wgrad_us"] = t_us(lambda: torch.ops.aten.convolution_backward(
-            dyc, xb, w, None, [2, 2], [3, 3], [1, 1], False, [0, 0], 1, [False, True, False]))
+    out["wgrad_us"] = t_us(lambda: h.stem_conv_wgrad(x4.data_ptr(), dyc.data_ptr(), gw.data_ptr(), *gw.stride(), 3,
+                                                     ws.data_ptr(), B, 224, 224, 112, 112, True, 0,
+                                                     S.N.stream_of(x4)))
+    xb = x.bfloat16()
+    out["miopen_fwd_us"] = t_us(lambda: F.conv2d(xb, w, stride=2, padding=3))
+    out["miopen_wgrad_us"] = t_us(lambda: torch.ops.aten.convolution_backward(
+        dyc, xb, w, None, [2, 2], [3, 3], [1, 1], False, [0, 0], 1, [False, True, False]))
     return out
 
 
 def main():
-    ap = argparse.ArgumentParser()
-    ap.add_argument("--debug", type=int, default=None)
-    ap.add_argument("--sweep", action="store_true")
-    a = ap.parse_args()
-    if a.sweep:
-        for m in (0, 1, 2, 4, 8, 1 | 8, 4 | 8, 1 | 4 | 8, 2 | 4 | 8 | 1):
-            env = dict(os.environ, VODA_STEM_DEBUG=str(m))
-            r = subprocess.run([sys.executable, __file__, "--debug", str(m)], env=env, capture_output=True, text=True,
-                               timeout=300)
-            print(r.stdout.strip() or r.stderr[-2000:], flush=True)
-        return
-    print(json.dumps(run(a.debug or 0)), flush=True)
+    argparse.ArgumentParser().parse_args()
+    print(json.dumps(run()), flush=True)
 
 
 if __name__ == "__main__":

@@ -959,14 +959,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void a
   if (h == 0 && qv) a.lse[int64_t(bh) * Tq + own] = m + __logf(l);
 }
 
-// VODA_ATTN_FUSED_BWD=0 (A/B switch, read once): keep the two-pass backward for T <= 128
-bool attn_fused_bwd_enabled() {
-  static const bool on = [] {
-    const char* e = std::getenv("VODA_ATTN_FUSED_BWD");
-    return e == nullptr || std::atoi(e) != 0;
-  }();
-  return on;
-}
+// T <= 128: the fused single-pass backward (round 3: 53.0 -> 37.0 us per BERT-base layer); the
+// two-pass backward stays for longer sequences
+bool attn_fused_bwd_enabled() { return true; }
 
 template <typename F>
 void dispatch_d(int D, F&& f) {
@@ -980,15 +975,10 @@ void dispatch_d(int D, F&& f) {
 // waves per workgroup from the number of rows the workgroup's lanes own
 template <typename F>
 void dispatch_w(int rows, F&& f) {
-  // VODA_ATTN_MAXW=1|2|4 (A/B switch, read once): cap on waves per workgroup -- smaller
-  // workgroups = more of them per (batch, head) to hide each one's per-tile latency
-  static const int maxw = [] {
-    const char* e = std::getenv("VODA_ATTN_MAXW");
-    const int v = e ? std::atoi(e) : 4;
-    return v >= 4 ? 4 : (v >= 2 ? 2 : 1);
-  }();
-  if (rows <= 32 || maxw == 1) f(std::integral_constant<int, 1>{});
-  else if (rows <= 64 || maxw == 2) f(std::integral_constant<int, 2>{});
+  // at most 4 waves: smaller workgroups (more per (batch, head)) measured slower
+  // (profiles/raw/r2_ab_attn_maxw.jsonl)
+  if (rows <= 32) f(std::integral_constant<int, 1>{});
+  else if (rows <= 64) f(std::integral_constant<int, 2>{});
   else f(std::integral_constant<int, 4>{});
 }
 
@@ -1026,11 +1016,7 @@ void attention_fwd(const std::vector<int64_t>& t, int B, int H, int Tq, int Tk, 
   VODA_CHECK(attention_supported(D, Tq, Tk, kBF16), "attention_fwd: unsupported shape");
   VODA_CHECK(int64_t(B) * H <= 65535, "attention_fwd: B*H exceeds the grid's y dimension");
   const AttnArgs a = make_args(t, B, H, Tq, Tk, scale, causal);
-  static const bool res_fwd = [] {  // VODA_ATTN_RES_FWD=0 (A/B switch): streamed forward for T <= 128
-    const char* e = std::getenv("VODA_ATTN_RES_FWD");
-    return e == nullptr || std::atoi(e) != 0;
-  }();
-  if (D == 64 && Tq <= kFusedT && Tk <= kFusedT && res_fwd) {
+  if (D == 64 && Tq <= kFusedT && Tk <= kFusedT) {  // K / V-resident forward (round 3: 17.0 -> 14.9 us)
     hipLaunchKernelGGL(attn_fwd_res_kernel, dim3(unsigned(B * H)), dim3(256), 0, as_stream(stream), a);
     check_launch();
     return;

@@ -224,7 +224,7 @@ __device__ __forceinline__ void store_row(float* __restrict__ out, int64_t st, i
 }
 
 // ======================================================================== forward
-template <int D, int W, bool PFT = false>
+template <int D, int W>
 __global__ __launch_bounds__(64 * W) void attn_f32_fwd(AttnArgsF a) {
   constexpr int RS = D + 2, DT = D / 32;
   constexpr bool REG = D <= 128;
@@ -244,27 +244,14 @@ __global__ __launch_bounds__(64 * W) void attn_f32_fwd(AttnArgsF a) {
   for (int t = 0; t < DT; ++t) o[t] = zero16();
   float m = -1e30f, l = 0.f;
   // no register prefetch of the next K / V tile here: measured slower on BERT-base (fwd 48.0 ->
-  // 51.2 us, dQ 75.9 -> 81.6 us per layer: the extra VGPRs cost a wave per SIMD); the dK/dV
-  // pass keeps it (109.3 -> 94.5 us)
-  TileRegs<D, 64 * W> kr, vr;
-  constexpr bool PF = PFT && TileRegs<D, 64 * W>::kOn;
+  // 51.2 us, dQ 75.9 -> 81.6 us per layer: the extra VGPRs cost a wave per SIMD; the variant was
+  // removed in round 5); the dK/dV pass keeps it (109.3 -> 94.5 us)
   for (int kt = 0; kt < a.Tk; kt += kT) {
     __syncthreads();
-    if constexpr (PF) {
-      kr.template store<RS>(Ks);
-      vr.template store<RS>(Vs);
-    } else {
-      stage<D, RS>(kb, a.k_st, kt, a.Tk, Ks);
-      stage<D, RS>(vb, a.v_st, kt, a.Tk, Vs);
-    }
+    stage<D, RS>(kb, a.k_st, kt, a.Tk, Ks);
+    stage<D, RS>(vb, a.v_st, kt, a.Tk, Vs);
     stage_mask(a, mrow, kt, Ms);
     __syncthreads();
-    if constexpr (PF) {
-      if (kt + kT < a.Tk) {  // the next tile's loads stay in flight during this tile's MFMAs
-        kr.load(kb, a.k_st, kt + kT, a.Tk);
-        vr.load(vb, a.v_st, kt + kT, a.Tk);
-      }
-    }
     f32x16 s = zero16();
     dot_hd<D, RS, REG>(s, Ks + r * RS + 2 * h, qf);  // S^T[key r][query]: lane = query
     TileCodes tc;
@@ -309,136 +296,8 @@ __global__ __launch_bounds__(64 * W) void attn_f32_fwd(AttnArgsF a) {
   if (h == 0 && q < a.Tq) a.lse[int64_t(bh) * a.Tq + q] = m + __logf(l);
 }
 
-// ------------------------------------------------------------------------ forward, D = 64, LDS-DMA
-// The same forward with its K / V tiles arriving by LDS-DMA (global_load_lds_dwordx4) into a
-// two-stage ring: tile kt + 1 lands while tile kt's MFMAs run, with no staging registers (the
-// register-prefetch variant cost a wave per SIMD).  DMA writes LDS lane-linearly, so the tile
-// is unpadded ([32 rows][64 floats]) and XOR-swizzled at 16-byte chunks instead: row r's logical
-// chunk c sits at physical chunk c ^ (r & 15) -- the per-lane GLOBAL address does the swizzle.
-// The head-dim reads (one float2 of each of 32 rows per lane half) then spread over the banks,
-// and the V column reads (32 consecutive floats of one row) stay conflict-free.
-typedef __attribute__((address_space(3))) void attn_lds_void;
-
-__device__ __forceinline__ void attn_dma16(const void* gptr, uint32_t lds_addr) {
-  asm volatile("s_mov_b32 m0, %1\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(gptr), "s"(lds_addr) : "memory", "m0");
-}
-__device__ __forceinline__ void attn_wait_dma() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
-
-// one 32 x 64 fp32 tile (8 KB = 8 wave-instructions of 1 KB, dealt over the W waves): lane l of
-// instruction i fills tile row 4 i + l / 16, physical chunk l % 16 = logical chunk ^ (row & 15)
-template <int W>
-__device__ __forceinline__ void dma_tile64(const float* __restrict__ g, int64_t st, int t0, int T, float* lds,
-                                           int wave, int lane) {
-  for (int i = wave; i < 8; i += W) {
-    const int row = 4 * i + (lane >> 4);
-    const int c = (lane & 15) ^ (row & 15);
-    const int gr = min(t0 + row, T - 1);  // rows past T: finite data, masked (keys) / never stored
-    const uint32_t m0 = __builtin_amdgcn_readfirstlane(uint32_t(size_t((attn_lds_void*)(lds + 256 * i))));
-    attn_dma16(g + int64_t(gr) * st + 4 * c, m0);
-  }
-}
-
-__device__ __forceinline__ int sw64(int row, int col) {  // swizzled float index in a [32][64] tile
-  return row * 64 + ((((col >> 2) ^ (row & 15))) << 2) + (col & 3);
-}
-
-template <int W, int MINW = 1>
-__global__ __launch_bounds__(64 * W, MINW) void attn_f32_fwd_dma64(AttnArgsF a) {
-  constexpr int D = 64, DT = 2;
-  __shared__ __attribute__((aligned(1024))) float Ks[2][kT * D];
-  __shared__ __attribute__((aligned(1024))) float Vs[2][kT * D];
-  __shared__ __attribute__((aligned(16))) uint8_t Ms[2][kT];
-  const int bh = blockIdx.y, b = bh / a.H, hh = bh % a.H;
-  const float* kb = a.k + b * a.k_sb + hh * a.k_sh;
-  const float* vb = a.v + b * a.v_sb + hh * a.v_sh;
-  const int lane = threadIdx.x & 63, r = lane & 31, h = lane >> 5;
-  const int w = __builtin_amdgcn_readfirstlane(int(threadIdx.x >> 6));
-  const int q = blockIdx.x * (32 * W) + w * 32 + r;
-  RowFrag<D, true> qf;
-  qf.init(a.q + b * a.q_sb + hh * a.q_sh + int64_t(min(q, a.Tq - 1)) * a.q_st, q < a.Tq, h);
-  const uint8_t* mrow = a.mask != nullptr ? a.mask + b * a.mask_sb : nullptr;
-  f32x16 o[DT];
-#pragma unroll
-  for (int t = 0; t < DT; ++t) o[t] = zero16();
-  float m = -1e30f, l = 0.f;
-  int st = 0;
-  dma_tile64<W>(kb, a.k_st, 0, a.Tk, Ks[0], w, lane);
-  dma_tile64<W>(vb, a.v_st, 0, a.Tk, Vs[0], w, lane);
-  stage_mask(a, mrow, 0, Ms[0]);
-  attn_wait_dma();
-  __syncthreads();
-  for (int kt = 0; kt < a.Tk; kt += kT) {
-    if (kt + kT < a.Tk) {  // the next tile lands in the other stage during this tile's MFMAs
-      dma_tile64<W>(kb, a.k_st, kt + kT, a.Tk, Ks[st ^ 1], w, lane);
-      dma_tile64<W>(vb, a.v_st, kt + kT, a.Tk, Vs[st ^ 1], w, lane);
-      stage_mask(a, mrow, kt + kT, Ms[st ^ 1]);
-    }
-    const float* K = Ks[st];
-    const float* V = Vs[st];
-    // S^T[key r][query]: head-dim k-step t covers d = 4 (t >> 1) + 2h + (t & 1); the float2 of
-    // chunk t' = 2 t_pair .. read from the swizzled row r, one step ahead of its MFMAs
-    f32x16 s = zero16();
-    {
-      float2 x = *reinterpret_cast<const float2*>(K + sw64(r, 2 * h));
-#pragma unroll
-      for (int t = 0; t < D / 4; ++t) {
-        float2 xn = x;
-        if (t + 1 < D / 4) xn = *reinterpret_cast<const float2*>(K + sw64(r, 4 * (t + 1) + 2 * h));
-        const float2 y = qf.get(t);
-        __builtin_amdgcn_sched_barrier(0);
-        s = mfma(x.x, y.x, s);
-        s = mfma(x.y, y.y, s);
-        __builtin_amdgcn_sched_barrier(0);
-        x = xn;
-      }
-    }
-    TileCodes tc;
-    tc.load(Ms[st], h);
-    float tmax = -1e30f;
-#pragma unroll
-    for (int i = 0; i < 16; ++i) {
-      const int kl = crow(i, h);
-      const float v = s[i] * a.scale + mask_add_code(a, tc.code(i), kt + kl, q);
-      s[i] = v;
-      tmax = fmaxf(tmax, v);
-    }
-    tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64));
-    const float mn = fmaxf(m, tmax);
-    const float alpha = __expf(m - mn);
-    float psum = 0.f;
-#pragma unroll
-    for (int i = 0; i < 16; ++i) {
-      const float p = __expf(s[i] - mn);
-      s[i] = p;
-      psum += p;
-    }
-    psum += __shfl_xor(psum, 32, 64);
-    l = l * alpha + psum;
-    m = mn;
-#pragma unroll
-    for (int t = 0; t < DT; ++t) {
-#pragma unroll
-      for (int i = 0; i < 16; ++i) o[t][i] *= alpha;
-      float vc[16];
-#pragma unroll
-      for (int i = 0; i < 16; ++i) vc[i] = V[sw64(crow(i, h), 32 * t + r)];
-      __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-      for (int i = 0; i < 16; ++i) o[t] = mfma(vc[i], s[i], o[t]);
-    }
-    attn_wait_dma();  // this wave's pieces of the next tile
-    __syncthreads();  // everyone's; this tile's reads done
-    st ^= 1;
-  }
-  const float inv = 1.f / l;
-  float* ob = a.out + b * a.out_sb + hh * a.out_sh;
-#pragma unroll
-  for (int t = 0; t < DT; ++t) store_row(ob, a.out_st, q, a.Tq, 32 * t, o[t], inv, h);
-  if (h == 0 && q < a.Tq) a.lse[int64_t(bh) * a.Tq + q] = m + __logf(l);
-}
-
 // ======================================================================== backward: dQ (+ delta)
-template <int D, int W, bool PFT = false>
+template <int D, int W>
 __global__ __launch_bounds__(64 * W) void attn_f32_bwd_dq(AttnArgsF a) {
   constexpr int RS = D + 2, DT = D / 32;
   constexpr bool REG = D <= 64;
@@ -475,28 +334,13 @@ __global__ __launch_bounds__(64 * W) void attn_f32_bwd_dq(AttnArgsF a) {
   f32x16 dq[DT];
 #pragma unroll
   for (int t = 0; t < DT; ++t) dq[t] = zero16();
-  // no register prefetch of the next K / V tile here: measured slower on BERT-base (fwd 48.0 ->
-  // 51.2 us, dQ 75.9 -> 81.6 us per layer: the extra VGPRs cost a wave per SIMD); the dK/dV
-  // pass keeps it (109.3 -> 94.5 us)
-  TileRegs<D, 64 * W> kr, vr;
-  constexpr bool PF = PFT && TileRegs<D, 64 * W>::kOn;
+  // no register prefetch of the next K / V tile here (see attn_f32_fwd)
   for (int kt = 0; kt < a.Tk; kt += kT) {
     __syncthreads();
-    if constexpr (PF) {
-      kr.template store<RS>(Ks);
-      vr.template store<RS>(Vs);
-    } else {
-      stage<D, RS>(kb, a.k_st, kt, a.Tk, Ks);
-      stage<D, RS>(vb, a.v_st, kt, a.Tk, Vs);
-    }
+    stage<D, RS>(kb, a.k_st, kt, a.Tk, Ks);
+    stage<D, RS>(vb, a.v_st, kt, a.Tk, Vs);
     stage_mask(a, mrow, kt, Ms);
     __syncthreads();
-    if constexpr (PF) {
-      if (kt + kT < a.Tk) {
-        kr.load(kb, a.k_st, kt + kT, a.Tk);
-        vr.load(vb, a.v_st, kt + kT, a.Tk);
-      }
-    }
     f32x16 s = zero16(), dp = zero16();
     dot_hd<D, RS, REG>(s, Ks + r * RS + 2 * h, qf);   // S^T
     dot_hd<D, RS, REG>(dp, Vs + r * RS + 2 * h, df);  // dP^T = V dO^T
@@ -630,44 +474,15 @@ void dispatch_d32(int D, F&& f) {
   else throw std::invalid_argument("attention (fp32): unsupported head dim");
 }
 
-// waves per workgroup (32 rows each): enough for the rows, at most VODA_ATTN_F32_MAXW (A/B
-// knob, read once; default 4)
-// VODA_ATTN_F32_PF=1: register prefetch of the next K / V tile in the forward and dQ passes too
-// (A/B knob, read once)
-// VODA_ATTN_F32_DMA=1 (or 3: bounded to three waves per SIMD, 48 B of scratch): the D = 64
-// forward takes its K / V tiles through the LDS-DMA ring.  Off by default: BERT-base forward
-// 53.5 us (3: 52.9 us) vs 48.3 us register-staged -- the ring's swizzled addressing costs 65 VGPRs,
-// i.e. a wave per SIMD, more than the overlapped loads gain (profiles/r4/README.md, r4ad)
-int f32_dma() {
-  static const int v = [] {
-    const char* e = std::getenv("VODA_ATTN_F32_DMA");
-    return e == nullptr ? 0 : std::atoi(e);
-  }();
-  return v;
-}
-
-bool f32_pf() {
-  static const bool v = [] {
-    const char* e = std::getenv("VODA_ATTN_F32_PF");
-    return e != nullptr && std::atoi(e) != 0;
-  }();
-  return v;
-}
-
-int f32_maxw() {
-  static const int v = [] {
-    const char* e = std::getenv("VODA_ATTN_F32_MAXW");
-    const int x = e ? std::atoi(e) : 4;
-    return x >= 4 ? 4 : (x >= 2 ? 2 : 1);
-  }();
-  return v;
-}
-
+// waves per workgroup (32 rows each): enough for the rows, at most 4.  Removed in round 5 after
+// their recorded losses: a register prefetch of the next K / V tile in the forward and dQ passes
+// (fwd 48.0 -> 51.2 us, dQ 75.9 -> 81.6 us per BERT-base layer) and an LDS-DMA ring for the D = 64
+// forward (53.5 vs 48.3 us: its swizzled addressing cost a wave per SIMD; profiles/r4/README.md,
+// r4ad)
 template <typename F>
 void dispatch_w32(int rows, F&& f) {
-  const int mw = f32_maxw();
-  if (rows <= 32 || mw == 1) f(std::integral_constant<int, 1>{});
-  else if (rows <= 64 || mw == 2) f(std::integral_constant<int, 2>{});
+  if (rows <= 32) f(std::integral_constant<int, 1>{});
+  else if (rows <= 64) f(std::integral_constant<int, 2>{});
   else f(std::integral_constant<int, 4>{});
 }
 
@@ -705,17 +520,7 @@ void attention_fwd_f32(const std::vector<int64_t>& t, int B, int H, int Tq, int 
   dispatch_d32(D, [&](auto dc) {
     dispatch_w32(Tq, [&](auto wc) {
       constexpr int DD = decltype(dc)::value, WW = decltype(wc)::value;
-      if (DD == 64 && f32_dma() == 3)
-        hipLaunchKernelGGL((attn_f32_fwd_dma64<WW, 3>), dim3((Tq + 32 * WW - 1) / (32 * WW), unsigned(B * H)),
-                           dim3(64 * WW), 0, as_stream(stream), a);
-      else if (DD == 64 && f32_dma())
-        hipLaunchKernelGGL((attn_f32_fwd_dma64<WW>), dim3((Tq + 32 * WW - 1) / (32 * WW), unsigned(B * H)),
-                           dim3(64 * WW), 0, as_stream(stream), a);
-      else if (f32_pf())
-        hipLaunchKernelGGL((attn_f32_fwd<DD, WW, true>), dim3((Tq + 32 * WW - 1) / (32 * WW), unsigned(B * H)),
-                           dim3(64 * WW), 0, as_stream(stream), a);
-      else
-        hipLaunchKernelGGL((attn_f32_fwd<DD, WW>), dim3((Tq + 32 * WW - 1) / (32 * WW), unsigned(B * H)),
+      hipLaunchKernelGGL((attn_f32_fwd<DD, WW>), dim3((Tq + 32 * WW - 1) / (32 * WW), unsigned(B * H)),
                            dim3(64 * WW), 0, as_stream(stream), a);
     });
   });
@@ -733,11 +538,7 @@ void attention_bwd_f32(const std::vector<int64_t>& t, int B, int H, int Tq, int 
     constexpr int DD = decltype(dc)::value;
     dispatch_w32(Tq, [&](auto wc) {
       constexpr int WW = decltype(wc)::value;
-      if (f32_pf())
-        hipLaunchKernelGGL((attn_f32_bwd_dq<DD, WW, true>), dim3((Tq + 32 * WW - 1) / (32 * WW), unsigned(B * H)),
-                           dim3(64 * WW), 0, s, a);
-      else
-        hipLaunchKernelGGL((attn_f32_bwd_dq<DD, WW>), dim3((Tq + 32 * WW - 1) / (32 * WW), unsigned(B * H)),
+      hipLaunchKernelGGL((attn_f32_bwd_dq<DD, WW>), dim3((Tq + 32 * WW - 1) / (32 * WW), unsigned(B * H)),
                            dim3(64 * WW), 0, s, a);
     });
     dispatch_w32(Tk, [&](auto wc) {

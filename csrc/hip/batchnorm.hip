@@ -447,7 +447,7 @@ __device__ __forceinline__ uint8_t pos_bits(const float (&v)[8]) {
 }
 
 // Apply passes: U rows of every input in flight per thread (all loads issued before the
-// first store; VODA_BN_APPLY_U selects U, see bn_tune).  U = 4 vs the former fwd 2 / bwd 1:
+// first store; BnTune::apply_u selects U).  U = 4 vs the former fwd 2 / bwd 1:
 // ResNet-50 step kernel time 23.32 -> 23.21 ms, the residual passes ~2 % faster each
 // (profiles/r3/raw/bn_apply_u/); the passes stay near 4.5 TB/s, bandwidth- not latency-bound.
 template <typename T, bool RES, bool RELU, int U = 2>
@@ -1017,43 +1017,32 @@ Grid bn_grid(int64_t M, int C, int64_t cap_blocks, int iters_per_block) {
   return {dim3(unsigned(nb), unsigned(slices)), int(nb)};
 }
 
-// Tuning knobs of the reduction passes, read once (A/B runs: benchmarks/bench_bn_passes.py,
-// benchmarks/gpu_r2_bn_trace.sh for per-shape dispatch times):
-//   VODA_BN_UNROLL=0|1|2  rows in flight 4 / 8 / 16 (stats) and 2 / 4 / 8 (backward reduce)
-//   VODA_BN_BLOCKS=n      reduction grid cap (default 256 = one 4-wave block per CU)
-//   VODA_BN_SWEEP=0|1|2   grid-sweep reduction + mirrored apply order (default 1); 2 = sweep
-//                         back to front + apply front to back (see Walk)
+// Tuning of the reduction / apply passes (fixed at the measured defaults since round 5;
+// bn_set_tuning reaches the other settings, and tests/test_batchnorm_gpu.py checks that every
+// reduction walk gives the default's results):
+//   deep    rows in flight 4 / 8 / 16 (stats) and 2 / 4 / 8 (backward reduce): level 1
+//   blocks  reduction grid cap: 256 = one 4-wave block per CU (512 for fp32 tensors)
+//   sweep   grid-sweep reduction + mirrored apply order: 1 (2 = sweep back to front + apply
+//           front to back, see Walk)
 // Measured on MI355X (profiles/raw/r2_bn_grid_trace.md, ResNet-50 bs-256 step A/B in
 // profiles/raw/r2_ab_bn_grid.jsonl): the reduction passes of the large tensors ran at 3.8-4.2
 // TB/s with 1024 long-lived blocks each walking its own chunk; one block per CU sweeping
 // the tensor together brings the per-step stats + reduce + finalize time 4.64 -> 4.02 ms,
 // and the step 26.95 -> 26.23 ms.  Unroll level 2 and grids of 384-2048 blocks are slower.
-//   VODA_BN_BLOCKS_F32=n  the cap for fp32 tensors (default 512): with 32-byte rows per
-//                         thread one block per CU leaves the fp32 backward reduce at ~3.8
-//                         TB/s; two blocks per CU take the fp32 ResNet-50 step's reduce
-//                         passes 4.86 -> 3.52 ms (~5.2 TB/s), 1024 blocks 3.57 ms
-//                         (profiles/r4/bn_reduce_grid_fp32.md)
+// fp32 tensors: with 32-byte rows per thread one block per CU leaves the fp32 backward reduce at
+// ~3.8 TB/s; two blocks per CU take the fp32 ResNet-50 step's reduce passes 4.86 -> 3.52 ms
+// (~5.2 TB/s), 1024 blocks 3.57 ms (profiles/r4/bn_reduce_grid_fp32.md)
 struct BnTune {
   int deep;  // rows in flight: 0 -> 4 (stats) / 2 (backward reduce), 1 -> 8 / 4, 2 -> 16 / 8
   int blocks;
   int sweep;
-  int blocks_f32 = 512;   // reduction grid cap for fp32 tensors (VODA_BN_BLOCKS_F32)
-  int apply_cap = 8192;   // apply-pass grid cap (VODA_BN_APPLY_CAP)
-  int apply_iters = 4;    // row iterations per apply block (VODA_BN_APPLY_ITERS)
-  int apply_u = 4;        // rows in flight in the apply passes: 4, 2, or 0 -> fwd 2 / bwd 1 (VODA_BN_APPLY_U)
+  int blocks_f32 = 512;   // reduction grid cap for fp32 tensors
+  int apply_cap = 8192;   // apply-pass grid cap
+  int apply_iters = 4;    // row iterations per apply block
+  int apply_u = 4;        // rows in flight in the apply passes: 4, 2, or 0 -> fwd 2 / bwd 1
 };
 BnTune& bn_tune() {
-  static BnTune t = [] {
-    BnTune v{1, 256, 1};
-    if (const char* e = std::getenv("VODA_BN_UNROLL")) v.deep = std::max(0, std::min(2, std::atoi(e)));
-    if (const char* e = std::getenv("VODA_BN_BLOCKS")) v.blocks = std::max(64, std::min(8192, std::atoi(e)));
-    if (const char* e = std::getenv("VODA_BN_BLOCKS_F32")) v.blocks_f32 = std::max(64, std::min(8192, std::atoi(e)));
-    if (const char* e = std::getenv("VODA_BN_SWEEP")) v.sweep = std::max(0, std::min(2, std::atoi(e)));
-    if (const char* e = std::getenv("VODA_BN_APPLY_CAP")) v.apply_cap = std::max(256, std::atoi(e));
-    if (const char* e = std::getenv("VODA_BN_APPLY_ITERS")) v.apply_iters = std::max(1, std::atoi(e));
-    if (const char* e = std::getenv("VODA_BN_APPLY_U")) v.apply_u = std::atoi(e) >= 4 ? 4 : (std::atoi(e) >= 2 ? 2 : 0);  // see bn_apply_kernel
-    return v;
-  }();
+  static BnTune t{1, 256, 1};  // the measured defaults; bn_set_tuning changes them (tests)
   return t;
 }
 
@@ -1345,14 +1334,9 @@ void bn2_bwd(uintptr_t dy, uintptr_t mask, uintptr_t x, uintptr_t x2, uintptr_t 
 namespace {
 constexpr int kPoolRedBlocks = 2048;  // 8 four-wave blocks per CU: the gather loop is latency-bound
 int pool_red_blocks(int N, int H) { return std::max(1, std::min(kPoolRedBlocks, N * H)); }
-// VODA_POOL22=0: the generic one-pixel-per-thread backward passes (A/B switch)
-bool pool22_enabled() {
-  static const bool on = [] {
-    const char* e = std::getenv("VODA_POOL22");
-    return !(e && e[0] == '0');
-  }();
-  return on;
-}
+// 2x2-pixel-block backward passes (round 3: reduce 190 -> 130 us, apply 293 -> 177 us); the
+// generic one-pixel-per-thread passes stay for geometries they do not cover
+bool pool22_enabled() { return true; }
 void check_pool(int N, int H, int W, int C, int Ho, int Wo, int k, int s, int p) {
   VODA_CHECK(C % kVec == 0 && C <= kVec * kMaxTpr, "bn_pool: C must be a multiple of 8 and <= 2048");
   VODA_CHECK(k == 3 && s == 2 && p >= 0 && 2 * p <= k, "bn_pool: only the 3x3 / stride-2 window is compiled");

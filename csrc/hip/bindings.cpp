@@ -18,8 +18,6 @@ PYBIND11_MODULE(_vodahip, m) {
 
   m.def("sgd_step", &sgd_step);
   m.def("adam_step", &adam_step);
-  m.def("adam_set_unroll", &adam_set_unroll);
-  m.def("adam_get_unroll", &adam_get_unroll);
   m.def("rmsprop_step", &rmsprop_step);
   m.def("cast_scale", &cast_scale);
   m.def("multi_tensor_copy", &multi_tensor_copy);
@@ -64,9 +62,6 @@ PYBIND11_MODULE(_vodahip, m) {
   m.def("gemm_f32_stats", &gemm_f32_stats, py::arg("x"), py::arg("w"), py::arg("y"), py::arg("part"), py::arg("M"),
         py::arg("N"), py::arg("K"), py::arg("G"), py::arg("stream"), py::arg("accumulate") = false,
         py::arg("w_kn") = false);
-  m.def("wgrad_f32_workspace_floats", &wgrad_f32_workspace_floats);
-  m.def("wgrad_f32_config", &wgrad_f32_config);
-  m.def("wgrad_f32", &wgrad_f32);
   m.def("subsample2d", &subsample2d);
   m.def("conv3x3_c64_wgrad_workspace_floats", &conv3x3_c64_wgrad_workspace_floats);
   m.def("conv3x3_c64_wgrad", &conv3x3_c64_wgrad);

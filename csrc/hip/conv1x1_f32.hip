@@ -6,8 +6,6 @@
 //   forward       Y[M][N] (+)= X[M][K] . W[N][K]^T  with the BN statistics of Y's columns in
 //                 the epilogue (per-workgroup partial sums for batchnorm.hip's finalize) --
 //                 the statistics pass over Y disappears;
-//   weight grad   dW[N][K] (+)= dY[M][N]^T . X[M][K]  (reduction over the M = N*H*W pixels),
-//                 split-K, accumulated straight into the optimizer's fp32 flat gradient.
 //
 // Operand layout of v_mfma_f32_32x32x2_f32: lane l holds A[i = l&31][k = l>>5] and
 // B[k = l>>5][j = l&31] (one f32 each); C/D: col = l&31, row = (reg&3) + 8(reg>>2) + 4(l>>5).
@@ -20,14 +18,10 @@
 // global memory, double-buffered across row tiles) and one 16-byte LDS read of W -- the sum is
 // over the same k set, in a different (equally exact-per-product) order.
 //
-// Weight gradient (wgrad_f32_kernel): both operands are pixel-major ([M][N], [M][K]), which is
-// exactly the k-major operand layout of the f32 MFMA -- a 32-pixel stage of dY / X is staged
-// into LDS as-is ([pixel][column], conflict-free 128-byte half-wave reads), no transposes.
-// Waves tile the output (WN x WK waves of 64 x 64 = 2 x 2 MFMA tiles) and, for narrow
-// outputs, also split the stage's 16 k-steps (SW waves on one tile, summed through LDS).
-// Split-K over pixels fills the chip; each split writes an fp32 slab, a reduce kernel adds
-// the slabs into dW.  Blocks are remapped XCD-aware (consecutive logical blocks -- tiles of
-// one split, which stream the same pixels -- share an XCD's L2).
+// The split-K fp32 weight-gradient kernel and its streaming form for narrow outputs were removed
+// in round 5: MIOpen's igemm_wrw ran every ResNet-50 1x1 weight gradient faster (split-K 13.6 vs
+// 9.7 ms summed over the layers, streaming 400 vs 252 us on 56x56 64 -> 256;
+// profiles/r4/resnet50_fp32_1x1_own_vs_miopen.jsonl, resnet50_fp32_1x1_wgrad_stream.jsonl).
 #include "common.h"
 #include "ops.h"
 
@@ -432,377 +426,6 @@ int f32_cus() {
 // columns per workgroup: the W tile stays <= ~68 KB of LDS (two workgroups per CU)
 int gf_nt(int K) { return K == 64 ? 8 : (K == 128 ? 4 : 2); }
 
-// ------------------------------------------------------------------------------------------
-// weight gradient, split-K
-// ------------------------------------------------------------------------------------------
-constexpr int kWThreads = 256;
-constexpr int kWStage = 32;  // pixels per LDS stage (16 MFMA k-steps)
-
-struct WArgs {
-  const float* dy;  // [M][N]
-  const float* x;   // [M][K]
-  float* dw;        // [N][K] (S == 1)
-  float* ws;        // [S][N][K] slabs (S > 1)
-  int M, N, K, S, m_split, tiles_n, tiles_k, accumulate, remap;
-};
-
-template <int WN, int WK, int SW>
-__global__ __launch_bounds__(kWThreads, 2) void wgrad_f32_kernel(WArgs p) {
-  static_assert(WN * WK * SW == 4, "four waves");
-  constexpr int TN = 64 * WN, TK = 64 * WK;
-  constexpr int LD = TN + TK;                      // floats per staged pixel row: [dY cols | X cols]
-  constexpr int STAGE = kWStage * LD;               // floats per stage
-  __shared__ __attribute__((aligned(16))) float lds[2 * STAGE];
-
-  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
-  const int lc = lane & 31, lh = lane >> 5;
-  const int sw = wave % SW, wnk = wave / SW;
-  const int wn = wnk / WK, wk = wnk - (wnk / WK) * WK;
-
-  // logical block: split-major (the tiles of one split -- same pixels -- are neighbours);
-  // XCD-aware: hardware dispatches block b to XCD b % 8, so give XCD x a contiguous range
-  int bid = blockIdx.x;
-  if (p.remap) {
-    const int per = gridDim.x / 8;
-    bid = (bid % 8) * per + bid / 8;
-  }
-  const int tiles = p.tiles_n * p.tiles_k;
-  const int split = bid / tiles, tile = bid - split * tiles;
-  const int n0 = (tile / p.tiles_k) * TN, k0 = (tile % p.tiles_k) * TK;
-  const int m_beg = split * p.m_split;
-  const int m_end = min(p.M, m_beg + p.m_split);
-
-  // staging: a stage is the [pixel][dY cols | X cols] image; thread t loads float4s of the dY
-  // part (TN / 4 per pixel row) and of the X part (TK / 4 per row).  Branch-free: rows past
-  // the split / columns past N, K read a clamped valid address and are zeroed by a mask, so
-  // the loads of a stage are all in flight together (no per-load waits).
-  constexpr int NA = kWStage * TN / 4 / kWThreads, NB = kWStage * TK / 4 / kWThreads;
-  static_assert(NA * kWThreads * 4 == kWStage * TN && NB * kWThreads * 4 == kWStage * TK, "even split");
-  float4 ga[NA], gb[NB];
-  bool oka[NA], okb[NB];  // masks applied at the LDS store: no wait on the loads before the MFMAs
-  auto keep4 = [](float4 v, bool k) {
-    const uint32_t m = k ? 0xffffffffu : 0u;
-    return make_float4(__uint_as_float(__float_as_uint(v.x) & m), __uint_as_float(__float_as_uint(v.y) & m),
-                       __uint_as_float(__float_as_uint(v.z) & m), __uint_as_float(__float_as_uint(v.w) & m));
-  };
-  auto gload = [&](int m0) {
-#pragma unroll
-    for (int i = 0; i < NA; ++i) {
-      const int u = tid + i * kWThreads;
-      const int r = u / (TN / 4), col = n0 + 4 * (u - r * (TN / 4));
-      const int m = m0 + r;
-      oka[i] = m < m_end && col < p.N;
-      ga[i] = *reinterpret_cast<const float4*>(p.dy + int64_t(oka[i] ? m : m_beg) * p.N + (oka[i] ? col : 0));
-    }
-#pragma unroll
-    for (int i = 0; i < NB; ++i) {
-      const int u = tid + i * kWThreads;
-      const int r = u / (TK / 4), col = k0 + 4 * (u - r * (TK / 4));
-      const int m = m0 + r;
-      okb[i] = m < m_end && col < p.K;
-      gb[i] = *reinterpret_cast<const float4*>(p.x + int64_t(okb[i] ? m : m_beg) * p.K + (okb[i] ? col : 0));
-    }
-  };
-  auto sstore = [&](float* buf) {
-#pragma unroll
-    for (int i = 0; i < NA; ++i) {
-      const int u = tid + i * kWThreads;
-      const int r = u / (TN / 4), c4 = u - r * (TN / 4);
-      *reinterpret_cast<float4*>(buf + r * LD + 4 * c4) = keep4(ga[i], oka[i]);
-    }
-#pragma unroll
-    for (int i = 0; i < NB; ++i) {
-      const int u = tid + i * kWThreads;
-      const int r = u / (TK / 4), c4 = u - r * (TK / 4);
-      *reinterpret_cast<float4*>(buf + r * LD + TN + 4 * c4) = keep4(gb[i], okb[i]);
-    }
-  };
-
-  // the wave's 64 rows / 64 columns are two 32-wide MFMA tiles each, INTERLEAVED (tile 0 =
-  // even, tile 1 = odd channels): one ds_read_b64 of channels (2j, 2j + 1) feeds both tiles,
-  // 2 LDS reads per 4 MFMAs instead of 4
-  f32x16 c00{}, c01{}, c10{}, c11{};
-  const int an = wn * 64 + 2 * lc, bk = TN + wk * 64 + 2 * lc;
-  constexpr int KS = 16 / SW;  // k-steps of a stage per wave
-  int m0 = m_beg;
-  int buf = 0;
-  if (m0 < m_end) {
-    gload(m0);
-    sstore(lds);
-  }
-  __syncthreads();
-  for (; m0 < m_end; m0 += kWStage) {
-    const bool more = m0 + kWStage < m_end;
-    if (more) gload(m0 + kWStage);
-    __builtin_amdgcn_sched_barrier(0);
-    const float* st = lds + buf * STAGE + (2 * sw * KS + lh) * LD;
-    // LDS operands one k-step ahead of the MFMAs (register double buffer): the reads of step
-    // j + 1 are in flight while the four MFMAs of step j issue
-    float2 av = *reinterpret_cast<const float2*>(st + an), bv = *reinterpret_cast<const float2*>(st + bk);
-#pragma unroll
-    for (int j = 0; j < KS; ++j) {
-      float2 na = make_float2(0.f, 0.f), nb = make_float2(0.f, 0.f);
-      if (j + 1 < KS) {
-        const float* row = st + 2 * (j + 1) * LD;
-        na = *reinterpret_cast<const float2*>(row + an);
-        nb = *reinterpret_cast<const float2*>(row + bk);
-      }
-      __builtin_amdgcn_sched_barrier(0);  // keep the next step's reads ahead of these MFMAs
-      c00 = mfma32(av.x, bv.x, c00);
-      c01 = mfma32(av.x, bv.y, c01);
-      c10 = mfma32(av.y, bv.x, c10);
-      c11 = mfma32(av.y, bv.y, c11);
-      __builtin_amdgcn_sched_barrier(0);
-      av = na; bv = nb;
-    }
-    // the next stage's global loads stay in flight during the MFMAs: their LDS stores (and
-    // the vmcnt waits they need) must not be hoisted above them
-    __builtin_amdgcn_sched_barrier(0);
-    if (more) sstore(lds + (buf ^ 1) * STAGE);
-    __syncthreads();
-    buf ^= 1;
-  }
-
-  // ---- waves sharing a tile (SW > 1): sum through LDS (the stage buffers are free now)
-  if constexpr (SW > 1) {
-    // tree: in each round the upper half of the remaining waves store their accumulators
-    // ([half][WN*WK][64 acc][64 lanes], lane-contiguous: conflict-free) and the lower half add
-    static_assert((SW / 2) * WN * WK * 64 * 64 <= 2 * STAGE, "reduction image must fit the stage buffers");
-    float* sum = lds;
-#pragma unroll
-    for (int half = SW / 2; half >= 1; half /= 2) {
-      if (sw >= half && sw < 2 * half) {
-        float* d = sum + ((sw - half) * (WN * WK) + wnk) * 64 * 64 + lane;
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          d[64 * r] = c00[r]; d[64 * (16 + r)] = c01[r]; d[64 * (32 + r)] = c10[r]; d[64 * (48 + r)] = c11[r];
-        }
-      }
-      __syncthreads();
-      if (sw < half) {
-        const float* d = sum + (sw * (WN * WK) + wnk) * 64 * 64 + lane;
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          c00[r] += d[64 * r]; c01[r] += d[64 * (16 + r)]; c10[r] += d[64 * (32 + r)]; c11[r] += d[64 * (48 + r)];
-        }
-      }
-      __syncthreads();
-    }
-    if (sw > 0) return;
-  }
-
-  // ---- epilogue: rows = output channels n (MFMA rows), cols = input channels k (lanes); tile
-  // (ra, ca) holds rows rbase + 2 i + ra and columns cbase + 2 j + ca (interleaved, see above)
-  auto store = [&](const f32x16& acc, int rbase, int cbase) {
-    const int col = cbase + 2 * lc;
-    if (col >= p.K) return;
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const int row = rbase + 2 * ((r & 3) + 8 * (r >> 2) + 4 * lh);
-      if (row < p.N) {
-        if (p.S == 1) {
-          float* o = p.dw + int64_t(row) * p.K + col;
-          *o = p.accumulate ? *o + acc[r] : acc[r];
-        } else {
-          p.ws[(int64_t(split) * p.N + row) * p.K + col] = acc[r];
-        }
-      }
-    }
-  };
-  const int rb = n0 + wn * 64, cb = k0 + wk * 64;
-  store(c00, rb, cb);
-  store(c01, rb, cb + 1);
-  store(c10, rb + 1, cb);
-  store(c11, rb + 1, cb + 1);
-}
-
-// ------------------------------------------------------------------------------------------
-// weight gradient, streaming form for narrow outputs (N x K <= 256 x 256 in 64 x 64 blocks):
-// the split-K kernel above stages 32-pixel stages for a handful of MFMAs per block when the
-// whole output is one or two tiles wide (56x56 64 -> 256: 609 us vs MIOpen's 258).  Here a
-// workgroup owns a contiguous pixel range and ALL output blocks (BPW 64 x 64 blocks per wave),
-// 32-pixel chunks of dY and X arrive by LDS-DMA (the [M][N] / [M][K] rows of a chunk are one
-// contiguous span each) into a two-stage ring, and each wave's 64 x 64 block is four 32 x 32
-// tiles with INTERLEAVED channels (tile (a, b) = rows 2i + a, columns 2j + b) so one ds_read_b64
-// of each operand feeds all four MFMAs of a pixel pair.  One fp32 partial per workgroup,
-// summed by wgrad_f32_reduce_kernel.
-typedef __attribute__((address_space(3))) void wf_lds_void;
-
-__device__ __forceinline__ void wf_dma16(const void* gptr, uint32_t lds_addr) {
-  asm volatile("s_mov_b32 m0, %1\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(gptr), "s"(lds_addr) : "memory", "m0");
-}
-__device__ __forceinline__ void wf_wait_dma() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
-
-constexpr int kSP = 16;      // pixels per chunk
-constexpr int kSStages = 4;  // LDS ring: three chunks in flight while one is computed
-
-struct WSArgs {
-  const float* dy;  // [M][N]
-  const float* x;   // [M][K]
-  float* ws;        // [gridDim.x][N][K]
-  int64_t M;
-  int per;          // pixels per workgroup (multiple of kSP)
-};
-
-// `bytes` contiguous bytes from global `src` to LDS `dst`, 1 KB per wave-instruction dealt over
-// the 4 waves (every span here is a multiple of 1 KB)
-__device__ __forceinline__ void wf_dma_span(const float* src, float* dst, int bytes, int wave, int lane) {
-  for (int i = wave; i * 1024 < bytes; i += 4) {
-    const uint32_t m0 = __builtin_amdgcn_readfirstlane(uint32_t(size_t((wf_lds_void*)(dst + 256 * i))));
-    wf_dma16(src + 256 * i + 4 * lane, m0);
-  }
-}
-
-template <int N>
-__device__ __forceinline__ void wf_wait_vm() {
-  static_assert(N >= 0 && N < 64, "vmcnt range");
-  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
-}
-
-template <int N, int K, int BPW>
-__global__ __launch_bounds__(kWThreads, 1) void wgrad_f32_stream_kernel(WSArgs p) {
-  static_assert((N / 64) * (K / 64) == 4 * BPW, "BPW 64 x 64 blocks per wave");
-  constexpr int STG = kSP * (N + K);  // floats per stage: [kSP px][N] dY then [kSP px][K] X
-  constexpr int PW = (N + K) * kSP / 1024;  // DMA instructions per wave per chunk (4 waves, 1 KB each)
-  static_assert(PW * 4 * 256 == STG, "chunk spans must split evenly over the waves");
-  __shared__ __attribute__((aligned(1024))) float lds[kSStages * STG];
-  const int tid = threadIdx.x, lane = tid & 63, lc = lane & 31, lh = lane >> 5;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int64_t m0 = int64_t(blockIdx.x) * p.per;
-  const int64_t m1 = min<int64_t>(p.M, m0 + p.per);
-  const int nchunks = int((m1 - m0 + kSP - 1) / kSP);
-
-  f32x16 acc[BPW][4];
-#pragma unroll
-  for (int b = 0; b < BPW; ++b)
-#pragma unroll
-    for (int t = 0; t < 4; ++t) acc[b][t] = f32x16{};
-  int an[BPW], bk[BPW];
-#pragma unroll
-  for (int b = 0; b < BPW; ++b) {
-    const int blk = wave * BPW + b;
-    an[b] = (blk / (K / 64)) * 64 + 2 * lc;            // dY column pair (output rows 2i + a)
-    bk[b] = kSP * N + (blk % (K / 64)) * 64 + 2 * lc;  // X column pair (output columns 2j + b)
-  }
-  // chunk c's full-size spans (the last partial chunk clamps its start so the DMA stays inside
-  // the tensors; its extra leading rows are skipped by the pixel loop)
-  auto issue = [&](int c) {
-    float* stg = lds + (c % kSStages) * STG;
-    int64_t r0 = m0 + int64_t(c) * kSP;
-    if (r0 + kSP > p.M) r0 = p.M - kSP;
-    wf_dma_span(p.dy + r0 * N, stg, kSP * N * 4, wave, lane);
-    wf_dma_span(p.x + r0 * K, stg + kSP * N, kSP * K * 4, wave, lane);
-  };
-  // kSStages - 1 chunks in flight ahead of the one being computed
-  for (int c = 0; c < kSStages - 1 && c < nchunks; ++c) issue(c);
-  for (int c = 0; c < nchunks; ++c) {
-    const int ahead = min(kSStages - 2, nchunks - 1 - c);  // chunks after c already issued
-    if (ahead >= 2) wf_wait_vm<2 * PW>();
-    else if (ahead == 1) wf_wait_vm<PW>();
-    else wf_wait_vm<0>();
-    __syncthreads();  // chunk c landed for every wave; chunk c - 1's stage is free again
-    if (c + kSStages - 1 < nchunks) issue(c + kSStages - 1);
-    const float* cur = lds + (c % kSStages) * STG;
-    const int64_t r0 = m0 + int64_t(c) * kSP;
-    const int64_t start = r0 + kSP > p.M ? p.M - kSP : r0;  // the rows the DMA fetched
-    const int first = int(r0 - start);                       // rows of an earlier chunk: skip
-    const int valid = int(min<int64_t>(kSP, m1 - r0));
-    // pixel pairs [first, first + valid): an odd tail pairs its last pixel with a zero weight
-    const int npairs = (valid + 1) / 2;
-    for (int s = 0; s < npairs; ++s) {
-      const int px = first + 2 * s + lh;
-      const bool live = 2 * s + lh < valid;
-#pragma unroll
-      for (int b = 0; b < BPW; ++b) {
-        float2 av = *reinterpret_cast<const float2*>(cur + px * N + an[b]);
-        const float2 bv = *reinterpret_cast<const float2*>(cur + px * K + bk[b]);
-        if (!live) av = make_float2(0.f, 0.f);
-        acc[b][0] = mfma32(av.x, bv.x, acc[b][0]);
-        acc[b][1] = mfma32(av.x, bv.y, acc[b][1]);
-        acc[b][2] = mfma32(av.y, bv.x, acc[b][2]);
-        acc[b][3] = mfma32(av.y, bv.y, acc[b][3]);
-      }
-    }
-  }
-  float* out = p.ws + int64_t(blockIdx.x) * N * K;
-#pragma unroll
-  for (int b = 0; b < BPW; ++b) {
-    const int blk = wave * BPW + b;
-    const int nb = (blk / (K / 64)) * 64, kb = (blk % (K / 64)) * 64;
-#pragma unroll
-    for (int t = 0; t < 4; ++t) {
-      const int ra = t >> 1, cb = t & 1;
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int row = nb + 2 * ((r & 3) + 8 * (r >> 2) + 4 * lh) + ra;
-        out[int64_t(row) * K + kb + 2 * lc + cb] = acc[b][t][r];
-      }
-    }
-  }
-}
-
-__global__ __launch_bounds__(256) void wgrad_f32_reduce_kernel(const float* __restrict__ ws, int S, int64_t NK4,
-                                                               float* __restrict__ dw, int accumulate) {
-  for (int64_t i = blockIdx.x * int64_t(256) + threadIdx.x; i < NK4; i += int64_t(gridDim.x) * 256) {
-    float4 a = accumulate ? reinterpret_cast<const float4*>(dw)[i] : make_float4(0.f, 0.f, 0.f, 0.f);
-    for (int s = 0; s < S; ++s) {
-      const float4 v = reinterpret_cast<const float4*>(ws)[int64_t(s) * NK4 + i];
-      a.x += v.x; a.y += v.y; a.z += v.z; a.w += v.w;
-    }
-    reinterpret_cast<float4*>(dw)[i] = a;
-  }
-}
-
-struct WPlan {
-  int wn, wk, sw, tiles_n, tiles_k, S, m_split, grid;
-  int stream = 0;  // 1: wgrad_f32_stream_kernel (grid = S workgroups of m_split pixels)
-};
-
-bool wgrad_f32_stream_env() {
-  static const bool v = [] {
-    const char* e = std::getenv("VODA_WGRAD_F32_STREAM");
-    return e == nullptr || std::atoi(e) != 0;
-  }();
-  return v;
-}
-
-// the narrow-output shapes the streaming kernel covers
-bool wgrad_f32_stream_shape(int64_t M, int N, int K) {
-  return wgrad_f32_stream_env() && M >= 128 * kSP &&
-         ((N == 256 && K == 64) || (N == 64 && K == 256) || (N == 128 && K == 256) || (N == 256 && K == 128));
-}
-
-WPlan wgrad_f32_plan(int M, int N, int K, int splits) {
-  WPlan pl;
-  if (splits <= 0 && wgrad_f32_stream_shape(M, N, K)) {
-    pl.stream = 1;
-    pl.wn = pl.wk = pl.sw = 0;
-    pl.tiles_n = pl.tiles_k = 1;
-    const int nb = std::max(1, std::min(2 * f32_cus(), M / (4 * kSP)));
-    const int per_chunks = ((M + kSP - 1) / kSP + nb - 1) / nb;
-    pl.m_split = per_chunks * kSP;
-    pl.S = (M + pl.m_split - 1) / pl.m_split;
-    pl.grid = pl.S;
-    return pl;
-  }
-  // wave layout: the widest output tile that the channel counts fill
-  if (N >= 128 && K >= 128) { pl.wn = 2; pl.wk = 2; pl.sw = 1; }
-  else if (N < 128 && K >= 256) { pl.wn = 1; pl.wk = 4; pl.sw = 1; }
-  else if (K < 128 && N >= 256) { pl.wn = 4; pl.wk = 1; pl.sw = 1; }
-  else if (N < 128 && K >= 128) { pl.wn = 1; pl.wk = 2; pl.sw = 2; }
-  else if (K < 128 && N >= 128) { pl.wn = 2; pl.wk = 1; pl.sw = 2; }
-  else { pl.wn = 1; pl.wk = 1; pl.sw = 4; }
-  pl.tiles_n = (N + 64 * pl.wn - 1) / (64 * pl.wn);
-  pl.tiles_k = (K + 64 * pl.wk - 1) / (64 * pl.wk);
-  const int tiles = pl.tiles_n * pl.tiles_k;
-  int S = splits > 0 ? splits : std::max(1, (4 * f32_cus() + tiles - 1) / tiles);  // ~4 blocks per CU
-  const int per = (M + S - 1) / S;
-  pl.m_split = std::max(kWStage, (per + kWStage - 1) / kWStage * kWStage);
-  pl.S = (M + pl.m_split - 1) / pl.m_split;  // no empty splits
-  pl.grid = tiles * pl.S;
-  return pl;
-}
-
 }  // namespace
 
 // columns per wave of the fused input gradient (gemm_f32_dgrad_bn_kernel): what fits 256 VGPRs
@@ -883,57 +506,6 @@ void gemm_f32_dgrad_bn(uintptr_t dy, uintptr_t w, uintptr_t y, uintptr_t cg, uin
   else if (nsums == 2) go(std::integral_constant<int, 2>{});
   else go(std::integral_constant<int, 3>{});
   check_launch();
-}
-
-int64_t wgrad_f32_workspace_floats(int M, int N, int K, int splits) {
-  const WPlan pl = wgrad_f32_plan(M, N, K, splits);
-  return (pl.S > 1 || pl.stream) ? int64_t(pl.S) * N * K : 0;
-}
-
-std::vector<int> wgrad_f32_config(int M, int N, int K, int splits) {
-  const WPlan pl = wgrad_f32_plan(M, N, K, splits);
-  return {pl.wn, pl.wk, pl.sw, pl.S, pl.m_split, pl.grid};
-}
-
-void wgrad_f32(uintptr_t dy, uintptr_t x, uintptr_t dw, int M, int N, int K, int splits, uintptr_t ws,
-               bool accumulate, uintptr_t stream) {
-  VODA_CHECK(M > 0 && N >= 32 && K >= 32 && N % 32 == 0 && K % 32 == 0, "wgrad_f32: N and K must be multiples of 32");
-  VODA_CHECK(dy % 16 == 0 && x % 16 == 0 && dw % 16 == 0, "wgrad_f32: operands must be 16-byte aligned");
-  const WPlan pl = wgrad_f32_plan(M, N, K, splits);
-  VODA_CHECK(pl.S == 1 || (ws != 0 && ws % 16 == 0), "wgrad_f32: split-K needs a 16-byte aligned workspace");
-  WArgs a{reinterpret_cast<const float*>(dy), reinterpret_cast<const float*>(x), reinterpret_cast<float*>(dw),
-          reinterpret_cast<float*>(ws), M, N, K, pl.S, pl.m_split, pl.tiles_n, pl.tiles_k, accumulate ? 1 : 0,
-          pl.grid % 8 == 0 ? 1 : 0};
-  hipStream_t s = as_stream(stream);
-  const dim3 g(unsigned(pl.grid)), b(kWThreads);
-  if (pl.stream) {
-    VODA_CHECK(ws != 0, "wgrad_f32: the streaming form needs its workspace");
-    WSArgs sa{reinterpret_cast<const float*>(dy), reinterpret_cast<const float*>(x), reinterpret_cast<float*>(ws),
-              int64_t(M), pl.m_split};
-    if (N == 256 && K == 64) hipLaunchKernelGGL((wgrad_f32_stream_kernel<256, 64, 1>), g, b, 0, s, sa);
-    else if (N == 64 && K == 256) hipLaunchKernelGGL((wgrad_f32_stream_kernel<64, 256, 1>), g, b, 0, s, sa);
-    else if (N == 128 && K == 256) hipLaunchKernelGGL((wgrad_f32_stream_kernel<128, 256, 2>), g, b, 0, s, sa);
-    else hipLaunchKernelGGL((wgrad_f32_stream_kernel<256, 128, 2>), g, b, 0, s, sa);
-    check_launch();
-    const int64_t nk4 = int64_t(N) * K / 4;
-    hipLaunchKernelGGL(wgrad_f32_reduce_kernel, dim3(stream_grid(nk4)), dim3(256), 0, s, a.ws, pl.S, nk4, a.dw,
-                       a.accumulate);
-    check_launch();
-    return;
-  }
-  if (pl.wn == 2 && pl.wk == 2) hipLaunchKernelGGL((wgrad_f32_kernel<2, 2, 1>), g, b, 0, s, a);
-  else if (pl.wn == 1 && pl.wk == 4) hipLaunchKernelGGL((wgrad_f32_kernel<1, 4, 1>), g, b, 0, s, a);
-  else if (pl.wn == 4 && pl.wk == 1) hipLaunchKernelGGL((wgrad_f32_kernel<4, 1, 1>), g, b, 0, s, a);
-  else if (pl.wn == 1 && pl.wk == 2) hipLaunchKernelGGL((wgrad_f32_kernel<1, 2, 2>), g, b, 0, s, a);
-  else if (pl.wn == 2 && pl.wk == 1) hipLaunchKernelGGL((wgrad_f32_kernel<2, 1, 2>), g, b, 0, s, a);
-  else hipLaunchKernelGGL((wgrad_f32_kernel<1, 1, 4>), g, b, 0, s, a);
-  check_launch();
-  if (pl.S > 1) {
-    const int64_t nk4 = int64_t(N) * K / 4;
-    hipLaunchKernelGGL(wgrad_f32_reduce_kernel, dim3(stream_grid(nk4)), dim3(256), 0, s, a.ws, pl.S, nk4, a.dw,
-                       a.accumulate);
-    check_launch();
-  }
 }
 
 }  // namespace voda

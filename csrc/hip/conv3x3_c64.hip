@@ -276,9 +276,7 @@ __device__ __forceinline__ void c64f_row_mfma(c64_f32x16f (&acc)[9], const float
 // leave room for two waves per SIMD), so one workgroup's row boundary -- closing barrier, dY
 // DMA, wait -- overlaps the other's MFMAs.  WMAX = 64: one workgroup per CU, dY double-
 // buffered and fetched during the previous row.
-// PROBE (timing experiments only, never a result): 1 = after the first row, skip every row's
-// staging and barrier and recompute on the same LDS rows (isolates the MFMA loop's rate)
-template <int WMAX, int PROBE>
+template <int WMAX>
 __global__ __launch_bounds__(kThreads, WMAX <= 56 ? 2 : 1) void conv3x3_c64_wgrad_f32_kernel(C64ArgsF a) {
   constexpr bool DBUF = WMAX > 56;
   constexpr int SLOT = (WMAX + 2) * kFPitch;  // floats per ring row (pad pixel each side)
@@ -332,7 +330,7 @@ __global__ __launch_bounds__(kThreads, WMAX <= 56 ? 2 : 1) void conv3x3_c64_wgra
       c64_wait_dma();
       __syncthreads();
     }
-    const bool nxt = PROBE ? false : (row + 1 < r1 && h + 1 < a.H);
+    const bool nxt = row + 1 < r1 && h + 1 < a.H;
     if (nxt) {  // the next row's new input row (h + 2) [and dY row], landing during this row
       stage_x(h + 2);
       if constexpr (DBUF) c64_dma_row(a.dy + (row + 1) * a.W * kC, dyt[buf ^ 1], pieces, wave, lane);
@@ -346,18 +344,16 @@ __global__ __launch_bounds__(kThreads, WMAX <= 56 ? 2 : 1) void conv3x3_c64_wgra
       bq[q] = ring + ((h - 1 + kh) & (kSlots - 1)) * SLOT + (lh + kw) * kFPitch + 2 * lr;
     }
     c64f_row_mfma(acc, ap, bq, steps, grp != 0);
-    if constexpr (PROBE == 0) {
-      if constexpr (DBUF) {
-        c64_wait_dma();   // this wave's pieces of the next row have landed
-        __syncthreads();  // ... and everyone's; this row's reads are done
-      } else {
-        __syncthreads();  // this row's dY reads done: the single buffer takes the next row
-        if (nxt) c64_dma_row(a.dy + (row + 1) * a.W * kC, dyt[0], pieces, wave, lane);
-        c64_wait_dma();
-        __syncthreads();
-      }
+    if constexpr (DBUF) {
+      c64_wait_dma();   // this wave's pieces of the next row have landed
+      __syncthreads();  // ... and everyone's; this row's reads are done
+    } else {
+      __syncthreads();  // this row's dY reads done: the single buffer takes the next row
+      if (nxt) c64_dma_row(a.dy + (row + 1) * a.W * kC, dyt[0], pieces, wave, lane);
+      c64_wait_dma();
+      __syncthreads();
     }
-    in_lds = PROBE ? true : nxt;
+    in_lds = nxt;
     if (DBUF && nxt) buf ^= 1;
     if (++h == a.H) { h = 0; ++n; }
   }
@@ -467,16 +463,8 @@ void conv3x3_c64_wgrad(uintptr_t x, uintptr_t dy, uintptr_t dw, int64_t s0, int6
   VODA_CHECK(in_dt == kBF16 || in_dt == kF32, "conv3x3_c64_wgrad: activations must be bf16 or fp32");
   if (in_dt == kF32) {
     C64ArgsF a{reinterpret_cast<const float*>(x), reinterpret_cast<const float*>(dy), part, N, H, W};
-    static const int probe = [] {
-      const char* e = std::getenv("VODA_C64_F32_PROBE");
-      return e ? std::atoi(e) : 0;
-    }();
-    if (f32_two) {
-      if (probe == 1) hipLaunchKernelGGL((conv3x3_c64_wgrad_f32_kernel<56, 1>), dim3(nb), dim3(kThreads), 0, s, a);
-      else hipLaunchKernelGGL((conv3x3_c64_wgrad_f32_kernel<56, 0>), dim3(nb), dim3(kThreads), 0, s, a);
-    } else {
-      hipLaunchKernelGGL((conv3x3_c64_wgrad_f32_kernel<kMaxW, 0>), dim3(nb), dim3(kThreads), 0, s, a);
-    }
+    if (f32_two) hipLaunchKernelGGL((conv3x3_c64_wgrad_f32_kernel<56>), dim3(nb), dim3(kThreads), 0, s, a);
+    else hipLaunchKernelGGL((conv3x3_c64_wgrad_f32_kernel<kMaxW>), dim3(nb), dim3(kThreads), 0, s, a);
   } else {
     C64Args a{reinterpret_cast<const uint16_t*>(x), reinterpret_cast<const uint16_t*>(dy), part, N, H, W};
     hipLaunchKernelGGL(conv3x3_c64_wgrad_kernel, dim3(nb), dim3(kThreads), 0, s, a);

@@ -123,8 +123,7 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const T* __restrict__ dy, c
                                                      const float* __restrict__ mean, const float* __restrict__ rstd,
                                                      const void* __restrict__ gamma, T* __restrict__ dx,
                                                      float* __restrict__ part_g, float* __restrict__ part_b,
-                                                     int64_t M, int N, float* __restrict__ acc_g,
-                                                     float* __restrict__ acc_b) {
+                                                     int64_t M, int N) {
   extern __shared__ __attribute__((aligned(16))) float lds[];  // [4][N]
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
@@ -216,10 +215,9 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const T* __restrict__ dy, c
       }
     }
   }
-  if (part_g == nullptr && acc_g == nullptr) return;  // gamma/beta gradients not requested
-  // combine the 4 waves' column partials through LDS, gamma then beta; then either one
-  // partial row per block (col_sum_kernel adds them up) or -- acc_g/acc_b: the optimizer's
-  // fp32 flat gradient -- coalesced fp32 atomic adds straight into it (no second launch)
+  if (part_g == nullptr) return;  // gamma/beta gradients not requested
+  // combine the 4 waves' column partials through LDS, gamma then beta: one partial row per
+  // block (col_sum_kernel adds them up)
   for (int pass = 0; pass < 2; ++pass) {
 #pragma unroll
     for (int it = 0; it < MAXITER; ++it) {
@@ -227,14 +225,8 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const T* __restrict__ dy, c
       if (c4 < N4) reinterpret_cast<float4*>(lds + wave * N)[c4] = pass == 0 ? ag[it] : ab[it];
     }
     __syncthreads();
-    if (acc_g != nullptr) {
-      float* out = pass == 0 ? acc_g : acc_b;
-      for (int c = threadIdx.x; c < N; c += 256)
-        atomicAdd(out + c, (lds[c] + lds[N + c]) + (lds[2 * N + c] + lds[3 * N + c]));
-    } else {
-      float* out = (pass == 0 ? part_g : part_b) + int64_t(blockIdx.x) * N;
-      for (int c = threadIdx.x; c < N; c += 256) out[c] = (lds[c] + lds[N + c]) + (lds[2 * N + c] + lds[3 * N + c]);
-    }
+    float* out = (pass == 0 ? part_g : part_b) + int64_t(blockIdx.x) * N;
+    for (int c = threadIdx.x; c < N; c += 256) out[c] = (lds[c] + lds[N + c]) + (lds[2 * N + c] + lds[3 * N + c]);
     __syncthreads();
   }
 }
@@ -325,29 +317,14 @@ void layernorm_fwd(uintptr_t x, uintptr_t gamma, uintptr_t beta, uintptr_t y, ui
   check_launch();
 }
 
-// Backward grid cap = rows of fp32 dgamma/dbeta partials (VODA_LN_BWD_BLOCKS, A/B switch):
-// 256 blocks of 4 waves is ONE wave per SIMD, each walking M / 1024 rows with R rows of loads
-// in flight; more blocks put more waves (and loads) per SIMD at the cost of more partial rows
-// for col_sum_kernel to add up.
-int ln_bwd_block_cap() {
-  static const int cap = [] {
-    const char* e = std::getenv("VODA_LN_BWD_BLOCKS");
-    return e ? std::max(64, std::min(4096, std::atoi(e))) : 256;
-  }();
-  return cap;
-}
-
-// VODA_LN_ATOMIC=1 (opt-in): fp32 flat-gradient dgamma/dbeta as atomic adds from the backward
-// kernel instead of partial rows + col_sum_kernel.  Off by default: the BERT-base A/B shows no
-// gain within run-to-run noise (10.88/10.55 vs 10.82/10.59 ms, profiles/raw/r2_ab_ln_atomic.jsonl)
-// and the atomic form is not bitwise reproducible run to run (fp32 addition order).
-bool ln_bwd_atomic() {
-  static const bool on = [] {
-    const char* e = std::getenv("VODA_LN_ATOMIC");
-    return e && e[0] == '1';
-  }();
-  return on;
-}
+// Backward grid cap = rows of fp32 dgamma/dbeta partials: 256 blocks of 4 waves is ONE wave per
+// SIMD, each walking M / 1024 rows with R rows of loads in flight.  768 / 1024 blocks took the row
+// pass 17.0 -> 15.0 us but the dgamma/dbeta column sum over 3x / 4x the partial rows 5.1 -> 9.9 /
+// 12.4 us (profiles/r3/raw/ab_ln_bwd_grid_kernels.txt), so 256 it is.  (An atomic-add dgamma/dbeta
+// variant showed no gain within noise, profiles/raw/r2_ab_ln_atomic.jsonl, and was not bitwise
+// reproducible; removed in round 5.)
+constexpr int kLnBwdBlockCap = 256;
+int ln_bwd_block_cap() { return kLnBwdBlockCap; }
 
 int layernorm_bwd_partial_rows(int64_t M) {
   int64_t g = (M + 3) / 4;
@@ -362,26 +339,19 @@ void layernorm_bwd(uintptr_t dy, uintptr_t x, uintptr_t mean, uintptr_t rstd, ui
   const int grid = layernorm_bwd_partial_rows(M);
   float* pg = nullptr;
   float* pb = nullptr;
-  float* ag = nullptr;
-  float* ab = nullptr;
   if (dgamma != 0) {
     VODA_CHECK(dbeta != 0, "layernorm_bwd: dbeta required");
-    if (accumulate && wdt == kF32 && ln_bwd_atomic()) {
-      ag = reinterpret_cast<float*>(dgamma);
-      ab = reinterpret_cast<float*>(dbeta);
-    } else {
-      VODA_CHECK(workspace != 0, "layernorm_bwd: workspace required");
-      pg = reinterpret_cast<float*>(workspace);
-      pb = pg + int64_t(grid) * N;
-    }
+    VODA_CHECK(workspace != 0, "layernorm_bwd: workspace required");
+    pg = reinterpret_cast<float*>(workspace);
+    pb = pg + int64_t(grid) * N;
   }
   const size_t lds = size_t(4) * N * sizeof(float);
   LN_DISPATCH_T(dt, wdt, [&] {
     LN_DISPATCH_ITER(N, [&] {
-      hipLaunchKernelGGL((ln_bwd_kernel<T, WT, MI>), dim3(grid), dim3(256), (pg || ag) ? lds : 0,
+      hipLaunchKernelGGL((ln_bwd_kernel<T, WT, MI>), dim3(grid), dim3(256), pg ? lds : 0,
                          as_stream(stream), reinterpret_cast<const T*>(dy), reinterpret_cast<const T*>(x),
                          reinterpret_cast<const float*>(mean), reinterpret_cast<const float*>(rstd),
-                         reinterpret_cast<const void*>(gamma), reinterpret_cast<T*>(dx), pg, pb, M, N, ag, ab);
+                         reinterpret_cast<const void*>(gamma), reinterpret_cast<T*>(dx), pg, pb, M, N);
     });
     if (pg) {
       const unsigned cg = unsigned((N + 31) / 32);

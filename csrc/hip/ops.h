@@ -23,10 +23,6 @@ void sgd_step(uintptr_t p, uintptr_t g, int g_dtype, uintptr_t mom_buf, uintptr_
 void adam_step(uintptr_t p, uintptr_t g, int g_dtype, uintptr_t m, uintptr_t v, uintptr_t p_lp, int lp_dtype,
                int64_t n, float lr, float beta1, float beta2, float eps, float wd, bool adamw, int64_t step,
                float grad_scale, uintptr_t step_ptr, uintptr_t stream);
-// A/B of the Adam kernel's loads in flight (VODA_ADAM_U): 1 or 2 float4 groups per thread,
-// -1 = back to the environment's choice
-void adam_set_unroll(int u);
-int adam_get_unroll();
 void rmsprop_step(uintptr_t p, uintptr_t g, int g_dtype, uintptr_t sq, uintptr_t mom_buf, uintptr_t gavg,
                   uintptr_t p_lp, int lp_dtype, int64_t n, float lr, float alpha, float eps, float wd, float momentum,
                   bool centered, float grad_scale, uintptr_t stream);
@@ -123,10 +119,6 @@ int gemm_f32_dgrad_bn_groups(int64_t M, int N, int K, int nsums);
 void gemm_f32_dgrad_bn(uintptr_t dy, uintptr_t w, uintptr_t y, uintptr_t cg, uintptr_t cmask, uintptr_t smask,
                        uintptr_t s1, uintptr_t s2, uintptr_t part, int64_t M, int N, int K, int G, int nsums,
                        uintptr_t stream);
-int64_t wgrad_f32_workspace_floats(int M, int N, int K, int splits);
-std::vector<int> wgrad_f32_config(int M, int N, int K, int splits);
-void wgrad_f32(uintptr_t dy, uintptr_t x, uintptr_t dw, int M, int N, int K, int splits, uintptr_t ws,
-               bool accumulate, uintptr_t stream);
 
 // ---- 1x1 conv forward GEMM with BN statistics in the epilogue (gemm_bnstats.hip) ----
 bool gemm_bnstats_supported(int64_t M, int N, int K);

@@ -99,12 +99,11 @@ __device__ __forceinline__ void adam1(float& p, float g, float& m, float& v, con
   p -= a.step_size * (m / denom);
 }
 
-// U float4 groups of every array in flight per thread (loads issued before the first store):
-// VODA_ADAM_U = 1 / 2 (adam_unroll below).  Measured on a 110 M-parameter AdamW step
-// (benchmarks/bench_adam.py): 708 / 690 us with a bf16 copy, 669 / 686 us without, i.e. equal
-// within noise at ~4.5-4.8 TB/s; non-temporal state stores did not help either (and changed
-// the compiler's FMA contraction, so they were not bitwise equal) and were dropped.
-template <typename GT, typename LP, int U>
+// One float4 group of every array per thread and grid-stride iteration.  Two groups in flight
+// were measured equal within noise (110 M-parameter AdamW step, benchmarks/bench_adam.py:
+// 708 / 690 us with a bf16 copy, 669 / 686 us without; profiles/r4/bench_adam_variants.log) and
+// were removed in round 5; non-temporal state stores did not help either.
+template <typename GT, typename LP>
 __global__ __launch_bounds__(256) void adam_kernel(float* __restrict__ p, const GT* __restrict__ g,
                                                    float* __restrict__ m, float* __restrict__ v,
                                                    LP* __restrict__ q, int64_t n, AdamArgs a,
@@ -119,29 +118,6 @@ __global__ __launch_bounds__(256) void adam_kernel(float* __restrict__ p, const 
   const int64_t n4 = n >> 2;
   const int64_t stride = int64_t(gridDim.x) * blockDim.x;
   int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x;
-  if constexpr (U > 1) {
-    for (; i + (U - 1) * stride < n4; i += U * stride) {
-      float4 pv[U], gv[U], mv[U], vv[U];
-#pragma unroll
-      for (int u = 0; u < U; ++u) {
-        pv[u] = Vec4<float>::load(p, i + u * stride);
-        gv[u] = Vec4<GT>::load(g, i + u * stride);
-        mv[u] = Vec4<float>::load(m, i + u * stride);
-        vv[u] = Vec4<float>::load(v, i + u * stride);
-      }
-#pragma unroll
-      for (int u = 0; u < U; ++u) {
-        adam1(pv[u].x, gv[u].x, mv[u].x, vv[u].x, a);
-        adam1(pv[u].y, gv[u].y, mv[u].y, vv[u].y, a);
-        adam1(pv[u].z, gv[u].z, mv[u].z, vv[u].z, a);
-        adam1(pv[u].w, gv[u].w, mv[u].w, vv[u].w, a);
-        Vec4<float>::store(p, i + u * stride, pv[u]);
-        Vec4<float>::store(m, i + u * stride, mv[u]);
-        Vec4<float>::store(v, i + u * stride, vv[u]);
-        store_lp<LP>(q, i + u * stride, pv[u]);
-      }
-    }
-  }
   for (; i < n4; i += stride) {
     float4 pv = Vec4<float>::load(p, i);
     float4 gv = Vec4<GT>::load(g, i);
@@ -165,17 +141,6 @@ __global__ __launch_bounds__(256) void adam_kernel(float* __restrict__ p, const 
     }
   }
 }
-
-static int g_adam_unroll = -1;  // -1: VODA_ADAM_U (read once); 1 / 2 set by adam_set_unroll
-
-static int adam_unroll() {
-  static const int env = [] {
-    const char* e = std::getenv("VODA_ADAM_U");
-    return e != nullptr && std::atoi(e) >= 2 ? 2 : 1;
-  }();
-  return g_adam_unroll > 0 ? g_adam_unroll : env;
-}
-
 
 // ---------------------------------------------------------------------------------
 // RMSprop (+momentum, centered), torch.optim.RMSprop semantics.
@@ -292,18 +257,13 @@ void adam_step(uintptr_t p, uintptr_t g, int g_dtype, uintptr_t m, uintptr_t v, 
              adamw ? 1 : 0};
   unsigned grid = stream_grid((n + 3) / 4);
   DISPATCH_GT_LP(g_dtype, lp_dtype, [&] {
-    auto* kern = adam_unroll() == 2 ? adam_kernel<GT, LP, 2> : adam_kernel<GT, LP, 1>;
-    hipLaunchKernelGGL(kern, dim3(grid), dim3(256), 0, as_stream(stream),
+    hipLaunchKernelGGL((adam_kernel<GT, LP>), dim3(grid), dim3(256), 0, as_stream(stream),
                        reinterpret_cast<float*>(p), reinterpret_cast<const GT*>(g),
                        reinterpret_cast<float*>(m), reinterpret_cast<float*>(v),
                        reinterpret_cast<LP*>(p_lp), n, a, reinterpret_cast<const int64_t*>(step_ptr));
   });
   check_launch();
 }
-
-void adam_set_unroll(int u) { g_adam_unroll = u >= 2 ? 2 : (u == 1 ? 1 : -1); }
-
-int adam_get_unroll() { return adam_unroll(); }
 
 void rmsprop_step(uintptr_t p, uintptr_t g, int g_dtype, uintptr_t sq, uintptr_t mom_buf, uintptr_t gavg,
                   uintptr_t p_lp, int lp_dtype, int64_t n, float lr, float alpha, float eps, float wd,

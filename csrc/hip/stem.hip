@@ -59,8 +59,6 @@ struct StemArgs {
   uint16_t* y;           // [N][Ho][Wo][64] bf16
   float* part;           // [2][gridDim.x][64]
   int N, H, W, Ho, Wo;
-  int dbg;               // VODA_STEM_DEBUG bit mask (benchmarks/bench_stem.py ablations; 0 in use):
-                         // 1 no output stores, 2 no prefetch loads, 4 no MFMAs, 8 no epilogue
 };
 
 __device__ __forceinline__ st_f32x16 st_mfma(st_bf16x8 a, st_bf16x8 b, st_f32x16 c) {
@@ -198,16 +196,15 @@ __global__ __launch_bounds__(kSThreads, 2) void stem_conv7x7_fwd_kernel(StemArgs
     const bool nxt1 = row + 1 < r1 && ho + 1 < a.Ho;
     const bool nxt2 = nxt1 && row + 2 < r1 && ho + 2 < a.Ho;
     if (nxt1 && !vv[B]) {
-      if (!(a.dbg & 2)) load_rows(pf[B], kSS * ho + 4);
+      load_rows(pf[B], kSS * ho + 4);
       vv[B] = true;
     }
     vv[O] = nxt2;
-    if (nxt2 && !(a.dbg & 2)) load_rows(pf[O], kSS * ho + 6);
+    if (nxt2) load_rows(pf[O], kSS * ho + 6);
     // ---- 14 k-steps (kh-outer, 2 per kh), 2 pixel tiles of 32
     st_f32x16 acc0 = {}, acc1 = {};
 #pragma unroll
     for (int kh = 0; kh < kSK; ++kh) {
-      if (a.dbg & 4) break;
       const int slot = (kSS * ho - kSP + kh) & (kSSlots - 1);
       const int off = slot * kSRowB + (2 * wo0 + 2 * lh) * 8;
       const st_bf16x8 p00 = *reinterpret_cast<const st_bf16x8*>(lds_in + off);
@@ -232,7 +229,7 @@ __global__ __launch_bounds__(kSThreads, 2) void stem_conv7x7_fwd_kernel(StemArgs
     in_lds = vv[B];
     vv[B] = false;
     // ---- epilogue: statistics of the valid pixels, bf16 tile into the staging rows
-    if (!(a.dbg & 8)) {
+    {
       auto stats = [&](const st_f32x16& acc, int tbase) {
         if (tbase + 32 <= a.Wo) {  // full tile (wave-uniform): no masking
 #pragma unroll
@@ -262,7 +259,7 @@ __global__ __launch_bounds__(kSThreads, 2) void stem_conv7x7_fwd_kernel(StemArgs
     for (int i = 0; i < 4; ++i) {
       const int q = i * 64 + lane;
       const int px = q >> 3, part = q & 7;
-      if (wave * kSTile + px < a.Wo && !(a.dbg & 1)) {
+      if (wave * kSTile + px < a.Wo) {
         const uint4 v = *reinterpret_cast<const uint4*>(lds_out + (wave * kSTile + px) * kSOutStride + part * 16);
         *reinterpret_cast<uint4*>(ybase + px * kSCo + part * 8) = v;
       }
@@ -682,12 +679,8 @@ void stem_conv_fwd(uintptr_t x4, uintptr_t w, int64_t sw0, int64_t sw1, int64_t 
   VODA_CHECK(Wo >= 1 && Wo <= kSMaxWo, "stem_conv: output width must be <= 128");
   VODA_CHECK(nb == stem_partial_rows(N, Ho), "stem_conv: partial-row count mismatch");
   VODA_CHECK(x4 % 8 == 0 && y % 16 == 0 && part % 4 == 0, "stem_conv: misaligned operands");
-  static const int dbg = [] {
-    const char* e = std::getenv("VODA_STEM_DEBUG");
-    return e ? std::atoi(e) : 0;
-  }();
   StemArgs a{reinterpret_cast<const uint2*>(x4), reinterpret_cast<const uint16_t*>(w), sw0, sw1, sw2, sw3, Cin,
-             reinterpret_cast<uint16_t*>(y), reinterpret_cast<float*>(part), N, H, W, Ho, Wo, dbg};
+             reinterpret_cast<uint16_t*>(y), reinterpret_cast<float*>(part), N, H, W, Ho, Wo};
   hipLaunchKernelGGL(stem_conv7x7_fwd_kernel, dim3(nb), dim3(kSThreads), 0, as_stream(stream), a);
   check_launch();
 }

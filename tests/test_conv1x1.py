@@ -55,40 +55,6 @@ def test_conv1x1_gemm_matches_conv2d(cin, cout, stride, hw):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("cin,cout,hw", [(64, 256, 14), (64, 128, 9), (32, 256, 7)])
-def test_conv1x1_hybrid_matches_conv2d(cin, cout, hw, monkeypatch):
-    """Cin < 128 (opt-in path): MIOpen forward / input gradient, the split-K kernel's fp32
-    weight gradient."""
-    from vodascheduler_amd.ops import conv1x1 as C
-    from vodascheduler_amd.ops.optim import make_optimizer
-
-    monkeypatch.setattr(C, "USE_CONV1X1_HYBRID", True)
-    from vodascheduler_amd.utils.flat import grad_of
-
-    torch.manual_seed(0)
-    m = Conv1x1(cin, cout).cuda().to(memory_format=torch.channels_last).bfloat16()
-    ref_w = m.weight.detach().float().clone().requires_grad_(True)
-    opt = make_optimizer("sgd", m.parameters(), lr=0.0)
-    x = torch.randn(4, cin, hw, hw, device="cuda").bfloat16().to(memory_format=torch.channels_last)
-    xr = x.float().detach().requires_grad_(True)
-    xg = x.detach().requires_grad_(True)
-    assert not m._gemm_ok(xg) and m._hybrid_ok(xg)
-    opt.zero_grad()
-    y = m(xg)
-    assert y.grad_fn is not None and "Hybrid" in type(y.grad_fn).__name__
-    y_ref = F.conv2d(xr, ref_w)
-    assert _rel(y, y_ref) < 1e-2
-    g = torch.randn_like(y_ref)
-    y.backward(g.bfloat16().to(memory_format=torch.channels_last))
-    y_ref.backward(g)
-    assert _rel(xg.grad, xr.grad) < 1e-2
-    assert m.weight.grad is None  # went straight into the flat fp32 buffer (no autograd fold)
-    assert _rel(grad_of(m.weight), ref_w.grad) < 1e-2
-    m(xg).backward(g.bfloat16().to(memory_format=torch.channels_last))
-    assert _rel(grad_of(m.weight), 2 * ref_w.grad) < 1e-2
-
-
-@pytest.mark.gpu
 def test_resnet50_uses_gemm_path_and_trains():
     from vodascheduler_amd.models import get_workload, prepare_model
     from vodascheduler_amd.ops.optim import make_optimizer

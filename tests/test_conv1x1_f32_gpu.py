@@ -49,31 +49,6 @@ def test_gemm_f32_stats_matches_fp64(M, N, K):
     assert torch.equal(y3, y)
 
 
-@pytest.mark.parametrize("M,N,K,splits", [(4096, 256, 256, 0), (1000, 64, 512, 0), (3000, 512, 64, 3),
-                                          (2500, 64, 128, 0), (2048, 128, 64, 0), (6000, 64, 64, 0),
-                                          (800, 256, 128, 1), (1000, 96, 160, 0), (500, 32, 32, 0),
-                                          (777, 160, 96, 2), (5000, 256, 64, 0), (4100, 64, 256, 0),
-                                          (3333, 128, 256, 0), (2079, 256, 128, 0), (65536, 256, 64, 0)])
-def test_wgrad_f32_matches_fp64(M, N, K, splits):
-    from vodascheduler_amd.ops import wgrad as W
-
-    h, _ = _h()
-    torch.manual_seed(M + N + K)
-    dy = torch.randn(M, N, device="cuda")
-    x = torch.randn(M, K, device="cuda")
-    gw = torch.randn(N, K, device="cuda")
-    g0 = gw.clone()
-    wn, wk, sw, S, m_split, grid = h.wgrad_f32_config(M, N, K, splits)
-    # wave layouts of the split-K kernel, or (0, 0, 0): the streaming form for narrow outputs
-    assert wn * wk * sw in (0, 4) and S >= 1 and grid >= 1
-    W.wgrad_f32_accumulate_(dy, x, gw, accumulate=True, splits=splits)
-    ref = dy.double().t() @ x.double()
-    assert _rel(gw.double() - g0.double(), ref) < 5e-6
-    out = torch.full((N, K), float("nan"), device="cuda")
-    W.wgrad_f32_accumulate_(dy, x, out, accumulate=False, splits=splits)
-    assert _rel(out, ref) < 5e-6
-
-
 @pytest.mark.parametrize("cin,cout,stride,hw", [(64, 256, 1, 14), (256, 64, 1, 9), (128, 512, 1, 7),
                                                (512, 1024, 2, 14), (1024, 256, 1, 7), (256, 512, 2, 8),
                                                (512, 2048, 1, 7), (1024, 2048, 2, 14)])

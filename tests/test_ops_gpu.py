@@ -55,34 +55,6 @@ def test_fused_adam_matches_torch(adamw):
         torch.testing.assert_close(a, b, rtol=1e-5, atol=1e-6)
 
 
-@pytest.mark.parametrize("n", [1000, 4 * 524288 * 2 + 7, 5_000_003, 4_194_304 * 2 + 4 * 3])
-def test_adam_two_groups_in_flight_bitwise_equal(n):
-    """The unrolled Adam variant (two float4 groups per thread in flight, VODA_ADAM_U=2) equals
-    the plain one bitwise -- including sizes whose float4 count is not a multiple of the
-    2 x grid stride (remainder loop) and the scalar tail."""
-    h = _native.hip()
-    g0 = torch.Generator(device=DEV).manual_seed(n)
-    p0 = torch.randn(n, device=DEV, generator=g0)
-    gr = torch.randn(n, device=DEV, generator=g0)
-    m0 = torch.randn(n, device=DEV, generator=g0) * 0.1
-    v0 = torch.rand(n, device=DEV, generator=g0) * 0.01
-    out = {}
-    try:
-        for u in (1, 2):
-            h.adam_set_unroll(u)
-            assert h.adam_get_unroll() == u
-            p, m, v = p0.clone(), m0.clone(), v0.clone()
-            for step in (1, 2, 3):
-                h.adam_step(p.data_ptr(), gr.data_ptr(), _native.dtype_code(gr.dtype), m.data_ptr(), v.data_ptr(),
-                            0, -1, n, 1e-3, 0.9, 0.999, 1e-8, 1e-2, True, step, 1.0, 0,
-                            torch.cuda.current_stream().cuda_stream)
-            out[u] = (p, m, v)
-    finally:
-        h.adam_set_unroll(-1)
-    for a, b in zip(out[1], out[2]):
-        assert torch.equal(a, b)
-
-
 @pytest.mark.parametrize("kw", [dict(), dict(momentum=0.9), dict(centered=True, momentum=0.5)])
 def test_fused_rmsprop_matches_torch(kw):
     m1, m2 = _model_pair()

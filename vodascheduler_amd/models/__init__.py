@@ -175,9 +175,6 @@ def prepare_model(w: "Workload", device: torch.device, amp: bool = True) -> torc
     """Build a workload's model on ``device`` in the layout/precision the trainer uses:
     channels_last for convnets, bf16 compute weights on GPU with autocast."""
     m = w.build().to(device)
-    blas = os.environ.get("VODA_BLAS")  # A/B knob: library GEMMs on rocBLAS instead of hipBLASLt
-    if blas in ("rocblas", "hipblaslt") and device.type == "cuda":
-        torch.backends.cuda.preferred_blas_library("cublas" if blas == "rocblas" else "cublaslt")
     if w.channels_last and device.type == "cuda":
         m = m.to(memory_format=torch.channels_last)
         # MIOpen exhaustive find once per conv shape (cached in-process and in MIOpen's

@@ -22,11 +22,11 @@ from ..ops.conv1x1 import USE_GRAD_SINK, GradSink
 from ..ops.dense import FusedLinear, residual_add
 from ..ops.layernorm import FusedLayerNorm
 
-# residual add of each post-LN sublayer fused into the LayerNorm kernel (VODA_LN_RESIDUAL=0:
+# residual add of each post-LN sublayer fused into the LayerNorm kernel (FUSED_RESIDUAL_LN = False:
 # a separate add, for A/B runs)
-FUSED_RESIDUAL_LN = os.environ.get("VODA_LN_RESIDUAL", "1") != "0"
-# FFN GELU on the HIP kernel (ops/activation.py; VODA_HIP_GELU=0: PyTorch's, for A/B runs)
-HIP_GELU = os.environ.get("VODA_HIP_GELU", "1") != "0"
+FUSED_RESIDUAL_LN = True
+# FFN GELU on the HIP kernel (ops/activation.py; HIP_GELU = False: PyTorch's)
+HIP_GELU = True
 
 
 class MultiHeadAttention(nn.Module):

@@ -27,10 +27,10 @@ from .dense import _ready
 # VODA_FUSED_BN=0: every BatchNorm takes the PyTorch reference composition (A/B and bisection
 # runs, e.g. benchmarks/graph_diag.py)
 USE_FUSED_BN = os.environ.get("VODA_FUSED_BN", "1") != "0"
-# VODA_FUSED_BN_POOL=0: the ResNet stem runs BN+ReLU and the max pool as two ops (A/B switch;
+# USE_FUSED_BN_POOL = False: the ResNet stem runs BN+ReLU and the max pool as two ops (module switch;
 # fused: stem fwd+bwd 1014-1051 -> 744 us, ResNet-50 bs-256 step 26.43/26.47 -> 26.17/26.18 ms,
 # profiles/raw/r2_ab_fused_stem.jsonl)
-USE_FUSED_BN_POOL = os.environ.get("VODA_FUSED_BN_POOL", "1") != "0"
+USE_FUSED_BN_POOL = True
 
 
 def _rows_view_ok(x: torch.Tensor) -> bool:

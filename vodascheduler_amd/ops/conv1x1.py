@@ -30,49 +30,39 @@ from ..utils.flat import FOLD_CAST, flat_grad
 from . import _native as N
 from . import wgrad as W
 
-USE_CONV1X1_GEMM = os.environ.get("VODA_CONV1X1_GEMM", "1") != "0"
-# VODA_STRIDED_SINK=0: a stride-2 convolution hands its input gradient through the GradSink as a
-# zero-filled full-resolution tensor (A/B switch for _StridedGrad)
-USE_STRIDED_SINK = os.environ.get("VODA_STRIDED_SINK", "1") != "0"
-USE_GRAD_SINK = os.environ.get("VODA_GRAD_SINK", "1") != "0"
-# VODA_GEMM_BNSTATS=0: the expansion 1x1 convolutions (K = 64 / 128 in) stay on hipBLASLt /
-# MIOpen and their BN runs its own statistics pass (A/B switch for gemm_bnstats.hip)
+# Kernel-path switches (module constants; tests monkeypatch them to reach the other branch):
+USE_CONV1X1_GEMM = True   # bf16 1x1 convolutions with >= 128 input channels as GEMMs (else MIOpen)
+# stride-2 input gradients handed through a GradSink subsampled (_StridedGrad) instead of as a
+# zero-filled full-resolution tensor
+USE_STRIDED_SINK = True
+USE_GRAD_SINK = True      # GradSink shortcut-gradient hand-offs (else autograd adds them)
+# expansion 1x1 convolutions (K = 64 / 128 / 256 in) with the BN statistics in the GEMM epilogue
+# (gemm_bnstats.hip, conv1x1_f32.hip; ResNet-50 bf16 23.78 -> 23.15 ms); VODA_GEMM_BNSTATS=0 is the
+# A/B switch
 USE_GEMM_BNSTATS = os.environ.get("VODA_GEMM_BNSTATS", "1") != "0"
-# VODA_STATS_BWD_SPLIT=1: the Cin = 64 statistics layers run their MIOpen input and weight
-# gradients as two calls (A/B switch)
-STATS_BWD_SPLIT = os.environ.get("VODA_STATS_BWD_SPLIT", "0") == "1"
 # Input gradients dX = dY . W of the memory-bound 1x1 shapes (K = Cout in {64, 128, 256}) that
-# overwrite their output, on the MFMA GEMM of gemm_bnstats.hip instead of hipBLASLt / MIOpen
-# (benchmarks/bench_dgrad_gemm.py: 802816 x 256 -> 64 167 -> 102 us, 64 -> 256 142 -> 108,
-# 128 -> 256 168 -> 130, 200704 x 128 -> 512 77 -> 59; ResNet-50 step kernel time 23.55 ->
-# 23.47 ms, profiles/r3/raw/mfma_dgrad/).  VODA_MFMA_DGRAD=0: A/B off.
-USE_MFMA_DGRAD = os.environ.get("VODA_MFMA_DGRAD", "1") != "0"
-# Opt-in (VODA_CONV1X1_HYBRID=1): for Cin < 128 (ResNet stage 1: 64 -> 256) keep forward and
-# input gradient on MIOpen and send the weight gradient to the split-K kernel, straight into
-# the fp32 flat gradient.  In isolation the kernel matches MIOpen's igemm_wrw (156 vs 155 us)
-# without its workspace clear / cast / fold passes (profiles/raw/r2_wgrad_fp32_vs_hipblaslt.jsonl),
-# but the ResNet-50 step got SLOWER: 27.55 vs 27.28 ms (two interleaved pairs,
-# profiles/raw/r2_ab_conv1x1_hybrid.jsonl) -- so off by default
-USE_CONV1X1_HYBRID = os.environ.get("VODA_CONV1X1_HYBRID", "0") == "1"
+# overwrite their output, on the MFMA GEMM of gemm_bnstats.hip / conv1x1_f32.hip instead of
+# hipBLASLt / MIOpen (benchmarks/bench_dgrad_gemm.py: 802816 x 256 -> 64 167 -> 102 us, 64 -> 256
+# 142 -> 108, 128 -> 256 168 -> 130, 200704 x 128 -> 512 77 -> 59; profiles/r3/raw/mfma_dgrad/).
+# The accumulate (beta = 1) form of the same GEMMs is kept as a tested kernel feature, but the
+# models use hipBLASLt's beta = 1 (or, fp32 identity blocks, the fused input gradient below):
+# the own read-add-write epilogue measured 2x slower in the step (profiles/r4/sink_gemm_ab.md)
+USE_MFMA_DGRAD = True
 # fp32 (the reference's precision): 1x1 convolutions as GEMMs with the f32-MFMA kernels of
 # conv1x1_f32.hip -- forward with the BN statistics in the epilogue and input gradient for
-# K = 64 / 128 / 256, split-K weight gradient into the fp32 flat gradient, hipBLASLt for the
-# rest -- and the GradSink hand-offs of the bf16 path (no residual-gradient adds).
-# VODA_CONV1X1_F32=0: fp32 1x1 convolutions stay on MIOpen (A/B switch)
+# K = 64 / 128 / 256, hipBLASLt for the rest -- and the GradSink hand-offs of the bf16 path (no
+# residual-gradient adds).  Weight gradients stay on MIOpen (the own split-K / streaming fp32
+# weight-gradient kernels measured slower and were removed in round 5), except the
+# short-reduction, wide-output ones below.  VODA_CONV1X1_F32=0: fp32 1x1 convolutions stay on
+# MIOpen (A/B switch)
 USE_CONV1X1_F32 = os.environ.get("VODA_CONV1X1_F32", "1") != "0"
-USE_GEMM_F32 = os.environ.get("VODA_GEMM_F32", "1") != "0"
-# fp32 weight gradients: the split-K f32-MFMA kernel (1) or MIOpen's weight-only convolution
-# backward (0, default), folded into the flat gradient.  MIOpen's igemm_wrw runs these at
-# 76-126 TF, the split-K kernel at 20-115 TF (benchmarks/bench_resnet_fp32_convs.py,
-# profiles/r4/resnet50_fp32_1x1_own_vs_miopen.jsonl); in the ResNet-50 fp32 step: 80.0 ms with
-# the kernel vs 75.4 ms with MIOpen's (profiles/r4/rocprof_resnet50_fp32_*.md)
-USE_WGRAD_F32 = os.environ.get("VODA_WGRAD_F32", "0") != "0"
-# ... except the short-reduction, wide-output ones (stage 4 of ResNet-50: 7x7 maps, M = 12544
-# pixels into 1M-2M weights), where one hipBLASLt GEMM with beta = 1 into the flat gradient
-# runs 189-199 us vs MIOpen's 214-226 us plus the fold-in add, and 353 vs 417-434 us on the
-# stride-2 1024 -> 2048 shortcut (profiles/r4/resnet50_fp32_1x1_wgrad_*.jsonl).  MIOpen wins
-# everywhere M >= 50176.  VODA_BLAS_WGRAD_F32=0 keeps them on MIOpen (A/B switch)
-USE_BLAS_WGRAD_F32 = os.environ.get("VODA_BLAS_WGRAD_F32", "1") != "0"
+USE_GEMM_F32 = True
+# ... the short-reduction, wide-output fp32 weight gradients (stage 4 of ResNet-50: 7x7 maps,
+# M = 12544 pixels into 1M-2M weights), where one hipBLASLt GEMM with beta = 1 into the flat
+# gradient runs 189-199 us vs MIOpen's 214-226 us plus the fold-in add, and 353 vs 417-434 us on
+# the stride-2 1024 -> 2048 shortcut (profiles/r4/resnet50_fp32_1x1_wgrad_*.jsonl).  MIOpen wins
+# everywhere M >= 50176.
+USE_BLAS_WGRAD_F32 = True
 BLAS_WGRAD_F32_MAX_M = 16384
 BLAS_WGRAD_F32_MIN_OUT = 1 << 20
 
@@ -80,18 +70,13 @@ BLAS_WGRAD_F32_MIN_OUT = 1 << 20
 def blas_wgrad_f32_ok(m: int, cout: int, cin: int) -> bool:
     """fp32 1x1 weight gradient [cout, cin] = dY[m, cout]^T . X[m, cin] on hipBLASLt?"""
     return USE_BLAS_WGRAD_F32 and m <= BLAS_WGRAD_F32_MAX_M and cout * cin >= BLAS_WGRAD_F32_MIN_OUT
-# input gradient accumulated onto a GradSink's shortcut gradient (beta = 1): the MFMA GEMM's
-# read-add epilogue (1) or hipBLASLt's addmm (0, default), per precision.  Measured in the
-# ResNet-50 step (profiles/r4/sink_gemm_ab.md): fp32 69.3 -> 73.0 ms, bf16 23.03 -> 23.10 ms
-# with the own GEMM -- hipBLASLt's beta = 1 kernels stay
-USE_SINK_GEMM_F32 = os.environ.get("VODA_SINK_GEMM_F32", "0") != "0"
-USE_SINK_GEMM_BF16 = os.environ.get("VODA_SINK_GEMM_BF16", "0") != "0"
 
 
 # fp32 identity bottlenecks: conv1's input gradient reads the masked shortcut gradient and
 # accumulates the previous block's bn3 backward sums in its epilogue (gemm_f32_dgrad_bn,
-# ops/batchnorm.BwdHandoff / MaskedGrad).  VODA_FUSED_DGRAD_BN=0: hipBLASLt beta = 1 + separate
-# BN reduce pass (A/B switch)
+# ops/batchnorm.BwdHandoff / MaskedGrad; ResNet-50 fp32 68.0 -> 67.1 ms,
+# profiles/r5/ab_fused_dgrad_bn_resnet50_fp32.jsonl).  VODA_FUSED_DGRAD_BN=0: hipBLASLt beta = 1 +
+# separate BN reduce pass (A/B switch)
 USE_FUSED_DGRAD_BN = os.environ.get("VODA_FUSED_DGRAD_BN", "1") != "0"
 
 
@@ -383,12 +368,7 @@ class _Conv1x1Fn(torch.autograd.Function):
             s_ = strided.stride
             subsample_add_(dx, strided.g, strided.stride)
         elif acc is not None:
-            # bf16 beta = 1 stays on hipBLASLt: the MFMA GEMM's read-add-write epilogue made
-            # these calls 2x slower in the step (802816 x 64 -> 256: 203 us vs ~98 us)
-            use = USE_SINK_GEMM_F32 if dy2.dtype == torch.float32 else USE_SINK_GEMM_BF16
-            own = use and mfma_dgrad(dy2, w2, _as_2d(acc)) is not None
-            if not own:
-                _as_2d(acc).addmm_(dy2, w2)  # dX = shortcut gradient + dY . W (one GEMM, beta = 1)
+            _as_2d(acc).addmm_(dy2, w2)  # dX = shortcut gradient + dY . W (one hipBLASLt GEMM, beta = 1)
             dx = acc
         elif dx is not None:
             pass  # the fused input gradient above
@@ -410,7 +390,7 @@ class _Conv1x1Fn(torch.autograd.Function):
                     and blas_wgrad_f32_ok(dy2.shape[0], cout, cin)):
                 g2.addmm_(dy2.t(), x2)
                 _ready(weight)
-            elif dy2.dtype == torch.float32 and not USE_WGRAD_F32:
+            elif dy2.dtype == torch.float32:  # MIOpen's weight-only convolution backward
                 xs4 = x2.view(n, h, w, cin).permute(0, 3, 1, 2)
                 dy4 = dy2.view(n, h, w, cout).permute(0, 3, 1, 2)
                 dw4 = torch.ops.aten.convolution_backward(dy4, xs4, weight, None, [1, 1], [0, 0], [1, 1], False,
@@ -420,13 +400,6 @@ class _Conv1x1Fn(torch.autograd.Function):
                     _ready(weight)
                 else:
                     dw = dw4
-            elif g2 is not None and W.supported_f32(dy2, x2, g2):
-                W.wgrad_f32_accumulate_(dy2, x2, g2)
-                _ready(weight)
-            elif g2 is None and W.supported_f32(dy2, x2, weight.view(cout, cin)):
-                dw2 = torch.empty(cout, cin, dtype=torch.float32, device=dy2.device)
-                W.wgrad_f32_accumulate_(dy2, x2, dw2, accumulate=False)
-                dw = dw2.view(cout, cin, 1, 1)
             elif g2 is not None and W.supported(dy2, x2, g2):
                 W.wgrad_accumulate_(dy2, x2, g2)
                 _ready(weight)
@@ -470,14 +443,7 @@ class _Conv1x1StatsFn(torch.autograd.Function):
             if dx2 is not None:
                 dx = dx2.view(n, h, w, cin).permute(0, 3, 1, 2)
                 mask[0] = False
-        if STATS_BWD_SPLIT:  # one MIOpen call per gradient (solver choice differs from the joint call)
-            if mask[0]:
-                dx = torch.ops.aten.convolution_backward(dy, x, weight, None, [1, 1], [0, 0], [1, 1], False, [0, 0], 1,
-                                                         [True, False, False])[0]
-            if mask[1]:
-                dw = torch.ops.aten.convolution_backward(dy, x, weight, None, [1, 1], [0, 0], [1, 1], False, [0, 0], 1,
-                                                         [False, True, False])[1]
-        elif mask[0] or mask[1]:
+        if mask[0] or mask[1]:
             dx_m, dw, _ = torch.ops.aten.convolution_backward(dy, x, weight, None, [1, 1], [0, 0], [1, 1], False,
                                                               [0, 0], 1, mask)
             if mask[0]:
@@ -489,40 +455,6 @@ class _Conv1x1StatsFn(torch.autograd.Function):
                 _ready(weight)
                 dw = None
         return dx, dw, None
-
-
-class _Conv1x1HybridFn(torch.autograd.Function):
-    """MIOpen forward / input gradient, split-K MFMA weight gradient (stride 1)."""
-
-    @staticmethod
-    def forward(ctx, x, weight):
-        ctx.save_for_backward(x, weight)
-        return F.conv2d(x, weight)
-
-    @staticmethod
-    def backward(ctx, dy):
-        x, weight = ctx.saved_tensors
-        if not dy.is_contiguous(memory_format=torch.channels_last):
-            dy = dy.contiguous(memory_format=torch.channels_last)
-        dx = None
-        if ctx.needs_input_grad[0]:
-            dx = torch.ops.aten.convolution_backward(dy, x, weight, None, [1, 1], [0, 0], [1, 1], False, [0, 0], 1,
-                                                     [True, False, False])[0]
-        dw = None
-        if ctx.needs_input_grad[1]:
-            cout, cin = weight.shape[0], weight.shape[1]
-            dy2, x2 = _as_2d(dy), _as_2d(x)
-            g2 = flat_grad(weight).view(cout, cin) if _direct(weight) else None
-            if g2 is not None and W.supported(dy2, x2, g2):
-                W.wgrad_accumulate_(dy2, x2, g2)
-                _ready(weight)
-            else:
-                dw = (dy2.t() @ x2).view(cout, cin, 1, 1)
-                if g2 is not None:
-                    g2.add_(dw.view(cout, cin).to(g2.dtype))
-                    _ready(weight)
-                    dw = None
-        return dx, dw
 
 
 def _attach(y: torch.Tensor, holder: StatsHolder | None) -> torch.Tensor:
@@ -571,14 +503,6 @@ class Conv1x1(torch.nn.Conv2d):
         m = x.shape[0] * ((x.shape[2] + s - 1) // s) * ((x.shape[3] + s - 1) // s)
         return bool(N.hip().gemm_bnstats_supported(m, self.out_channels, self.in_channels))
 
-    def _hybrid_ok(self, x: torch.Tensor) -> bool:
-        return (USE_CONV1X1_HYBRID and x.is_cuda and x.dim() == 4 and x.dtype == torch.bfloat16
-                and self.weight.dtype == torch.bfloat16 and self.groups == 1 and self.padding == (0, 0)
-                and self.dilation == (1, 1) and self.stride == (1, 1)
-                and x.is_contiguous(memory_format=torch.channels_last)
-                and self.in_channels % 8 == 0 and self.out_channels >= 128 and self.out_channels % 8 == 0
-                and flat_grad(self.weight) is not None)
-
     def forward(self, x, sink_in: GradSink | None = None, sink_out: GradSink | None = None):
         """``sink_in`` / ``sink_out``: see GradSink.  A caller passes ``sink_in`` only after
         checking ``_gemm_ok(x)`` (the consumer must run on this path); ``sink_out`` is
@@ -591,11 +515,8 @@ class Conv1x1(torch.nn.Conv2d):
                 y = _Conv1x1Fn.apply(x, self.weight, self.stride[0], sink_in, sink_out, holder)
             return _attach(y, holder)
         assert sink_in is None, "a GradSink consumer must run on the GEMM path"
-        if holder is not None and self.stride == (1, 1) and self.in_channels == 64 and not self._hybrid_ok(x):
+        if holder is not None and self.stride == (1, 1) and self.in_channels == 64:
             with torch.autocast("cuda", enabled=False):
                 y = _Conv1x1StatsFn.apply(x, self.weight, holder)
             return _attach(y, holder)
-        if self._hybrid_ok(x):
-            with torch.autocast("cuda", enabled=False):
-                return _Conv1x1HybridFn.apply(x, self.weight)
         return super().forward(x)

@@ -31,8 +31,8 @@ from . import wgrad as W
 from ..utils.flat import FOLD_CAST, flat_grad
 from .conv1x1 import _direct, _ready
 
-USE_CONV_WGRAD = os.environ.get("VODA_CONV_WGRAD", "1") != "0"
-# VODA_CONV_DGRAD_FWD (default 1): the input gradient of a stride-1 KxK convolution runs as a
+USE_CONV_WGRAD = True
+# DGRAD_FWD (module switch, default on): the input gradient of a stride-1 KxK convolution runs as a
 # FORWARD convolution of dy with the transposed, spatially flipped filter
 #     dX[n, ci, h, w] = sum_{co, kh, kw} dY[n, co, h - kh + p, w - kw + p] * W[co, ci, kh, kw]
 #                     = conv2d(dY, W^T flipped, padding = K - 1 - p)
@@ -40,23 +40,23 @@ USE_CONV_WGRAD = os.environ.get("VODA_CONV_WGRAD", "1") != "0"
 # very shape the forward pass already found) instead of the backward-data igemm solvers and
 # their output zero-fill (VERDICT r2 Next #4).  ResNet-50 bs-256 step, same box back to back:
 # 25.87 -> 25.57 ms (profiles/r3/ab_dgrad_fwd.md).
-DGRAD_FWD = os.environ.get("VODA_CONV_DGRAD_FWD", "1") != "0"
+DGRAD_FWD = True
 
 
-# VODA_CONV_F32_FN (default 1): fp32 (reference-precision) stride-1 KxK convolutions take the
+# CONV_F32_FN (module switch, default on): fp32 (reference-precision) stride-1 KxK convolutions take the
 # same autograd function, i.e. their input gradient also runs as a forward convolution (their
 # weight gradient stays on MIOpen, folded into the flat gradient).  fp32 ResNet-50 step, same
 # lease: 70.21 -> 70.08 ms kernel time (igemm_bwd 7.79 -> 1.63 ms, igemm_fwd 8.0 -> 14.0 ms;
 # gpurun_out/r4v, profiles/r4/README.md)
-CONV_F32_FN = os.environ.get("VODA_CONV_F32_FN", "1") != "0"
+CONV_F32_FN = True
 
-# VODA_CONV_C64_WGRAD=0: the 64 -> 64 channel 3x3 weight gradient runs MIOpen (A/B switch);
-# VODA_CONV_C64_WGRAD_F32=0: fp32 activations keep MIOpen's.  The f32-MFMA twin runs 564 us vs
+# USE_C64_WGRAD = False: the 64 -> 64 channel 3x3 weight gradient runs MIOpen (module switch);
+# USE_C64_WGRAD_F32 = False: fp32 activations keep MIOpen's.  The f32-MFMA twin runs 564 us vs
 # MIOpen's 579 us at bs 256, 56 x 56 (benchmarks/bench_c64_wgrad.py); in the fp32 ResNet-50 step
 # it is even with MIOpen's kernel + zero fill (69.39 vs 69.40 ms, profiles/r4/README.md) and
 # writes the flat gradient directly (the bf16 kernel: 126 vs 171 us)
-USE_C64_WGRAD = os.environ.get("VODA_CONV_C64_WGRAD", "1") != "0"
-USE_C64_WGRAD_F32 = os.environ.get("VODA_CONV_C64_WGRAD_F32", "1") != "0"
+USE_C64_WGRAD = True
+USE_C64_WGRAD_F32 = True
 
 
 def c64_ok(dy: torch.Tensor, x: torch.Tensor, weight: torch.Tensor, stride: int, padding: int) -> bool:

@@ -13,7 +13,7 @@ post-accumulate hook would.  Otherwise it returns ordinary gradients.
 On GPU the in-place weight gradient (and the bias gradient with it) is the split-K MFMA
 kernel of ``ops/wgrad.py`` (csrc/hip/wgrad.hip): the "reduction over tokens" GEMMs are
 too narrow for hipBLASLt to fill 256 CUs.  ``USE_WGRAD_KERNEL = False`` (or
-``VODA_WGRAD=0``) switches back to ``addmm_`` + the column-sum kernel.
+``USE_WGRAD_KERNEL = False``) switches back to ``addmm_`` + the column-sum kernel.
 """
 from __future__ import annotations
 
@@ -26,8 +26,8 @@ from ..utils.flat import flat_grad
 from . import _native as N
 from . import wgrad as W
 
-USE_WGRAD_KERNEL = os.environ.get("VODA_WGRAD", "1") != "0"
-USE_SPLIT_DGRAD = os.environ.get("VODA_SPLIT_DGRAD", "1") != "0"
+USE_WGRAD_KERNEL = True
+USE_SPLIT_DGRAD = True
 _BMM_F32: bool | None = None  # torch.bmm(..., out_dtype=float32) available (probed once)
 
 

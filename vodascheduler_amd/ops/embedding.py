@@ -20,7 +20,7 @@ import torch.nn.functional as F
 from ..utils.flat import flat_grad
 from .dense import _direct, _ready, colsum_accumulate_
 
-USE_FUSED_EMBEDDING = os.environ.get("VODA_FUSED_EMBEDDING", "1") != "0"
+USE_FUSED_EMBEDDING = True
 
 
 class _EmbeddingFn(torch.autograd.Function):

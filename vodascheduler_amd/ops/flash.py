@@ -24,8 +24,8 @@ from . import _native as N
 import os
 
 MAX_T = 4096
-# VODA_FLASH_MAX_D: A/B switch that sends larger head dims to the materialised path
-HEAD_DIMS = tuple(d for d in (32, 64, 128, 256) if d <= int(os.environ.get("VODA_FLASH_MAX_D", "256")))
+# head dims the flash kernels cover (larger ones take the materialised path)
+HEAD_DIMS = tuple(d for d in (32, 64, 128, 256) if d <= 256)
 
 
 DTYPES = {torch.bfloat16: "DT_BF16", torch.float32: "DT_F32"}

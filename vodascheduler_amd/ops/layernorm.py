@@ -15,7 +15,7 @@ from . import _native as N
 from .dense import _ready
 
 MAX_N = 4096
-LN_DIRECT_GRADS = os.environ.get("VODA_LN_DIRECT", "1") != "0"
+LN_DIRECT_GRADS = True
 
 
 def _direct(p) -> bool:

@@ -28,8 +28,8 @@ from .batchnorm import FusedBNReLUMaxPool2d, bn_pool_backward, bn_pool_forward
 from .conv1x1 import _direct, _ready
 
 USE_STEM = os.environ.get("VODA_STEM", "1") != "0"
-# VODA_STEM_WGRAD=0: the weight gradient runs MIOpen's igemm_wrw on the packed image (A/B)
-USE_STEM_WGRAD = os.environ.get("VODA_STEM_WGRAD", "1") != "0"
+# USE_STEM_WGRAD = False: the weight gradient runs MIOpen's igemm_wrw on the packed image (module switch)
+USE_STEM_WGRAD = True
 COUT = 64
 
 

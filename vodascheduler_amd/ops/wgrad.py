@@ -24,16 +24,16 @@ TILE = 128
 # 64-token stages (128 KB) / three 48-token stages (144 KB); 11 / 12: fill-only probes of 9 / 10
 # (no MFMA, dW undefined: benchmarks only).  Default 2 (64 KB ring, 2 workgroups per CU): fastest in the BERT-base step
 # on MI355X (profiles/r1_wgrad_v3.md)
-VARIANT = int(os.environ.get("VODA_WGRAD_VARIANT", "2"))
-# VODA_WGRAD_VARIANT set explicitly = that variant for every shape (A/B runs); otherwise
-# tall convolution-sized reductions use the deeper LDS rings at half the default split count
+VARIANT = 2
+# _VARIANT_FIXED = True: VARIANT for every shape (benchmarks); otherwise tall
+# convolution-sized reductions use the deeper LDS rings at half the default split count
 # (per-shape sweep on MI355X, fp32 output, profiles/raw/r2_wgrad_variant_split_sweep.jsonl:
 # ResNet-50 stage 1 (M = 802816) 150-155 -> 131-137 us with variant 1, stage 2 (M = 200704)
 # 95-96 -> 79 us with variant 3, and variant 1 once the block order became split-major;
 # stages 3-4 and the BERT shapes gain nothing)
-_VARIANT_FIXED = "VODA_WGRAD_VARIANT" in os.environ
-# VODA_WGRAD_WIDE=0 (A/B switch): keep every shape on the 128 x 128 tile
-_WIDE = os.environ.get("VODA_WGRAD_WIDE", "1") != "0"
+_VARIANT_FIXED = False
+# _WIDE = False: keep every shape on the 128 x 128 tile
+_WIDE = True
 
 
 def choose(M: int, N_: int, K: int) -> tuple[int, int]:
@@ -143,38 +143,3 @@ def wgrad_accumulate_(dy2: torch.Tensor, x2: torch.Tensor, gw: torch.Tensor, gb:
     h.wgrad_gemm(dy2.data_ptr(), dy2.stride(0), x2.data_ptr(), x2.stride(0), gw.data_ptr(), gw.stride(0),
                  N.ptr(gb), M, N_, K, s, N.ptr(ws), bool(accumulate), _zero_rows(dy2.device).data_ptr(), v,
                  N.dtype_code(gw.dtype), N.stream_of(dy2))
-
-
-# ---------------------------------------------------------------------------------------
-# fp32 (the reference's precision): the split-K f32-MFMA kernel of csrc/hip/conv1x1_f32.hip
-# ---------------------------------------------------------------------------------------
-def supported_f32(dy2: torch.Tensor, x2: torch.Tensor, gw: torch.Tensor) -> bool:
-    """fp32 dY [M, N], X [M, K] and dW [N, K], all dense row-major, 16-byte aligned, N and K
-    multiples of 32 (every ResNet 1x1 convolution)."""
-    if not (dy2.is_cuda and x2.is_cuda and gw.is_cuda):
-        return False
-    if not (dy2.dtype == x2.dtype == gw.dtype == torch.float32) or dy2.dim() != 2 or x2.dim() != 2:
-        return False
-    M, N_ = dy2.shape
-    K = x2.shape[1]
-    if x2.shape[0] != M or tuple(gw.shape) != (N_, K) or M == 0 or N_ % 32 or K % 32:
-        return False
-    if not (dy2.is_contiguous() and x2.is_contiguous() and gw.is_contiguous()):
-        return False
-    return not (dy2.data_ptr() % 16 or x2.data_ptr() % 16 or gw.data_ptr() % 16)
-
-
-def wgrad_f32_accumulate_(dy2: torch.Tensor, x2: torch.Tensor, gw: torch.Tensor, accumulate: bool = True,
-                          splits: int = 0) -> None:
-    """``gw (+)= dy2^T x2`` in fp32 on the f32 MFMA (split-K over the M rows; ``splits`` 0 =
-    the kernel's choice: ~4 workgroups per CU)."""
-    if not supported_f32(dy2, x2, gw):
-        raise ValueError(f"wgrad_f32: unsupported operands dy {tuple(dy2.shape)} {dy2.dtype}, "
-                         f"x {tuple(x2.shape)} {x2.dtype}, dw {tuple(gw.shape)} {gw.dtype}")
-    M, N_ = dy2.shape
-    K = x2.shape[1]
-    h = N.hip()
-    nws = h.wgrad_f32_workspace_floats(M, N_, K, splits)
-    ws = torch.empty(nws, dtype=torch.float32, device=dy2.device) if nws else None
-    h.wgrad_f32(dy2.data_ptr(), x2.data_ptr(), gw.data_ptr(), M, N_, K, splits, N.ptr(ws), bool(accumulate),
-                N.stream_of(dy2))

@@ -24,7 +24,7 @@ import torch.nn.functional as F
 
 from . import _native as N
 
-USE_FUSED_XENT = os.environ.get("VODA_FUSED_XENT", "1") != "0"
+USE_FUSED_XENT = True
 # host-synchronising check that every label lies in [0, V) or is ignore_index (debug only)
 DEBUG_LABELS = os.environ.get("VODA_DEBUG_LABELS", "0") == "1"
 

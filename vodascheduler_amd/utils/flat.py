@@ -163,8 +163,8 @@ class FlatGroup:
             self.lowp.copy_(self.master)
 
 
-# VODA_FOLD_CAST=0: fold with a mixed-dtype add (A/B switch)
-FOLD_CAST = os.environ.get("VODA_FOLD_CAST", "1") != "0"
+# FOLD_CAST = False: fold with a mixed-dtype add (module switch)
+FOLD_CAST = True
 
 
 def _fold_lowp_grad(p: torch.Tensor) -> None:
