@@ -18,6 +18,8 @@
 #   ab:NAME:MODEL[-fp32]:REPS  interleaved same-box A/B of one env switch: model_step.py with
 #                            NAME=1 then NAME=0, REPS times (30 timed steps each); one JSON line
 #                            per run in ab-NAME-MODEL.jsonl
+#   abset:MODULE:ATTR:MODEL[-fp32]:REPS  the same for a module-level switch (docs/kernels.md):
+#                            model_step.py --set MODULE:ATTR=True, then =False
 set -o pipefail
 TAG=${1:?tag}
 shift
@@ -115,6 +117,21 @@ for step in "$@"; do
           env "$name=$v" timeout -k 10 300 python -u benchmarks/model_step.py --model "$m" --steps 30 --warmup 10 \
             --precision "$prec" > "$OUT/ab-$name-$v-$i.log" 2>&1 || { tail -20 "$OUT/ab-$name-$v-$i.log"; exit 1; }
           echo "{\"$name\": $v, \"rep\": $i, \"run\": $(grep '^{' "$OUT/ab-$name-$v-$i.log" | tail -1)}" >> "$jl"
+          tail -n 1 "$jl" | cut -c1-200
+        done
+      done ;;
+    abset:*)
+      spec=${step#abset:}
+      IFS=: read -r mod attr m reps <<< "$spec"
+      prec=bf16-amp
+      if [[ $m == *-fp32 ]]; then m=${m%-fp32}; prec=fp32; fi
+      jl="$OUT/ab-$attr-$m.jsonl"
+      for ((i = 1; i <= ${reps:-2}; i++)); do
+        for v in True False; do
+          timeout -k 10 300 python -u benchmarks/model_step.py --model "$m" --steps 30 --warmup 10 \
+            --precision "$prec" --set "$mod:$attr=$v" > "$OUT/ab-$attr-$v-$i.log" 2>&1 \
+            || { tail -20 "$OUT/ab-$attr-$v-$i.log"; exit 1; }
+          echo "{\"$attr\": \"$v\", \"rep\": $i, \"run\": $(grep '^{' "$OUT/ab-$attr-$v-$i.log" | tail -1)}" >> "$jl"
           tail -n 1 "$jl" | cut -c1-200
         done
       done ;;

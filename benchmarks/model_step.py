@@ -108,7 +108,18 @@ def main():
     ap.add_argument("--torch-profile", default=None, help="write a torch.profiler op table (3 steps) to this path")
     ap.add_argument("--losses", type=int, default=0, help="record the first N step losses (trajectory checks)")
     ap.add_argument("--precision", default="bf16-amp", choices=["bf16-amp", "fp32"])
+    ap.add_argument("--set", action="append", default=[], metavar="MODULE:ATTR=VALUE",
+                    help="set a module-level kernel-path switch before building the model (same-process A/B "
+                         "of the module constants listed in docs/kernels.md), e.g. "
+                         "vodascheduler_amd.models.layers:BIAS_HANDOFF=False")
     a = ap.parse_args()
+    for spec in a.set:
+        import ast
+        import importlib
+
+        mod, rest = spec.split(":", 1)
+        attr, val = rest.split("=", 1)
+        setattr(importlib.import_module(mod), attr, ast.literal_eval(val))
     if a.cudnn_benchmark:
         torch.backends.cudnn.benchmark = True
     _native.hip()
@@ -117,6 +128,8 @@ def main():
     out["precision"] = a.precision
     out["grad_dtype"] = a.grad_dtype
     out["overlap_opt"] = a.overlap_opt
+    if a.set:
+        out["set"] = a.set
     print(json.dumps(out), flush=True)
 
 

@@ -123,19 +123,23 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const T* __restrict__ dy, c
                                                      const float* __restrict__ mean, const float* __restrict__ rstd,
                                                      const void* __restrict__ gamma, T* __restrict__ dx,
                                                      float* __restrict__ part_g, float* __restrict__ part_b,
-                                                     int64_t M, int N) {
+                                                     int64_t M, int N, float* __restrict__ part_x) {
+  // part_x (optional): per-block column sums of dx -- the bias gradient of the Linear whose
+  // output is this LayerNorm's input (a post-LN sublayer's last projection), folded in here
+  // instead of a separate column-sum pass over dx (ops/dense.BiasHandoff)
   extern __shared__ __attribute__((aligned(16))) float lds[];  // [4][N]
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
   const int N4 = N >> 2;
   const float inv_n = 1.f / float(N);
-  float4 g[MAXITER], ag[MAXITER], ab[MAXITER];
+  float4 g[MAXITER], ag[MAXITER], ab[MAXITER], ax[MAXITER];
 #pragma unroll
   for (int it = 0; it < MAXITER; ++it) {
     const int c4 = it * 64 + lane;
     g[it] = (gamma && c4 < N4) ? load_w4<WT>(gamma, c4) : make_float4(1.f, 1.f, 1.f, 1.f);
     ag[it] = make_float4(0.f, 0.f, 0.f, 0.f);
     ab[it] = make_float4(0.f, 0.f, 0.f, 0.f);
+    ax[it] = make_float4(0.f, 0.f, 0.f, 0.f);
   }
   // A wave owns rows wave + 4*blockIdx.x + k * 4*gridDim.x.  The grid is capped (one fp32
   // partial row per block for dgamma/dbeta), so a wave walks several rows; R of them are
@@ -211,21 +215,23 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const T* __restrict__ dy, c
           o.z = (dg[it].z - xh[it].z * c1 - c2) * rs;
           o.w = (dg[it].w - xh[it].w * c1 - c2) * rs;
           Vec4<T>::store(dx + row * N, c4, o);
+          ax[it].x += o.x; ax[it].y += o.y; ax[it].z += o.z; ax[it].w += o.w;
         }
       }
     }
   }
   if (part_g == nullptr) return;  // gamma/beta gradients not requested
-  // combine the 4 waves' column partials through LDS, gamma then beta: one partial row per
+  // combine the 4 waves' column partials through LDS, gamma, beta [, dx]: one partial row per
   // block (col_sum_kernel adds them up)
-  for (int pass = 0; pass < 2; ++pass) {
+  const int passes = part_x != nullptr ? 3 : 2;
+  for (int pass = 0; pass < passes; ++pass) {
 #pragma unroll
     for (int it = 0; it < MAXITER; ++it) {
       const int c4 = it * 64 + lane;
-      if (c4 < N4) reinterpret_cast<float4*>(lds + wave * N)[c4] = pass == 0 ? ag[it] : ab[it];
+      if (c4 < N4) reinterpret_cast<float4*>(lds + wave * N)[c4] = pass == 0 ? ag[it] : (pass == 1 ? ab[it] : ax[it]);
     }
     __syncthreads();
-    float* out = (pass == 0 ? part_g : part_b) + int64_t(blockIdx.x) * N;
+    float* out = (pass == 0 ? part_g : (pass == 1 ? part_b : part_x)) + int64_t(blockIdx.x) * N;
     for (int c = threadIdx.x; c < N; c += 256) out[c] = (lds[c] + lds[N + c]) + (lds[2 * N + c] + lds[3 * N + c]);
     __syncthreads();
   }
@@ -235,15 +241,18 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const T* __restrict__ dy, c
 // 32 columns x 8 row-groups per block; every thread keeps 4 independent loads in flight
 // (rows <= 256, so <= 32 loads per thread) -- the first version (64 columns x 4 groups,
 // 1024 rows) was latency-bound at 64 us per call on BERT (rocprof, profiles/).
-// blockIdx.y selects (part, out) or (part_b, out_b): dgamma and dbeta in one launch;
-// accumulate: out += sum (the optimizer's flat gradient buffer, no autograd add afterwards).
+// blockIdx.y selects (part, out), (part_b, out_b) or (part_c, out_c): dgamma, dbeta [and the
+// input Linear's dbias] in one launch; accumulate: out += sum (the optimizer's flat gradient
+// buffer, no autograd add afterwards).
 template <typename WT>
 __global__ __launch_bounds__(256) void col_sum_kernel(const float* __restrict__ part_a, WT* __restrict__ out_a,
                                                       const float* __restrict__ part_b, WT* __restrict__ out_b,
-                                                      int rows, int N, int accumulate) {
+                                                      int rows, int N, int accumulate,
+                                                      const float* __restrict__ part_c = nullptr,
+                                                      WT* __restrict__ out_c = nullptr) {
   __shared__ float red[8][33];
-  const float* __restrict__ part = blockIdx.y == 0 ? part_a : part_b;
-  WT* __restrict__ out = blockIdx.y == 0 ? out_a : out_b;
+  const float* __restrict__ part = blockIdx.y == 0 ? part_a : (blockIdx.y == 1 ? part_b : part_c);
+  WT* __restrict__ out = blockIdx.y == 0 ? out_a : (blockIdx.y == 1 ? out_b : out_c);
   const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;
   const int c = blockIdx.x * 32 + tx;
   float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
@@ -333,17 +342,21 @@ int layernorm_bwd_partial_rows(int64_t M) {
 
 void layernorm_bwd(uintptr_t dy, uintptr_t x, uintptr_t mean, uintptr_t rstd, uintptr_t gamma, uintptr_t dx,
                    uintptr_t dgamma, uintptr_t dbeta, uintptr_t workspace, int64_t M, int N, int dt, int wdt,
-                   bool accumulate, uintptr_t stream) {
+                   bool accumulate, uintptr_t stream, uintptr_t dbias_in) {
   VODA_CHECK(N > 0 && N % 4 == 0 && N <= kLayerNormMaxN, "layernorm: N must be a multiple of 4 and <= 4096");
   if (M == 0) return;
   const int grid = layernorm_bwd_partial_rows(M);
   float* pg = nullptr;
   float* pb = nullptr;
+  float* px = nullptr;  // dbias_in: the input Linear's bias gradient, workspace holds 3 partial sets
   if (dgamma != 0) {
     VODA_CHECK(dbeta != 0, "layernorm_bwd: dbeta required");
     VODA_CHECK(workspace != 0, "layernorm_bwd: workspace required");
     pg = reinterpret_cast<float*>(workspace);
     pb = pg + int64_t(grid) * N;
+    if (dbias_in != 0) px = pb + int64_t(grid) * N;
+  } else {
+    VODA_CHECK(dbias_in == 0, "layernorm_bwd: the input bias sum rides with dgamma / dbeta");
   }
   const size_t lds = size_t(4) * N * sizeof(float);
   LN_DISPATCH_T(dt, wdt, [&] {
@@ -351,13 +364,13 @@ void layernorm_bwd(uintptr_t dy, uintptr_t x, uintptr_t mean, uintptr_t rstd, ui
       hipLaunchKernelGGL((ln_bwd_kernel<T, WT, MI>), dim3(grid), dim3(256), pg ? lds : 0,
                          as_stream(stream), reinterpret_cast<const T*>(dy), reinterpret_cast<const T*>(x),
                          reinterpret_cast<const float*>(mean), reinterpret_cast<const float*>(rstd),
-                         reinterpret_cast<const void*>(gamma), reinterpret_cast<T*>(dx), pg, pb, M, N);
+                         reinterpret_cast<const void*>(gamma), reinterpret_cast<T*>(dx), pg, pb, M, N, px);
     });
     if (pg) {
       const unsigned cg = unsigned((N + 31) / 32);
-      hipLaunchKernelGGL((col_sum_kernel<WT>), dim3(cg, 2), dim3(256), 0, as_stream(stream), pg,
+      hipLaunchKernelGGL((col_sum_kernel<WT>), dim3(cg, px ? 3 : 2), dim3(256), 0, as_stream(stream), pg,
                          reinterpret_cast<WT*>(dgamma), pb, reinterpret_cast<WT*>(dbeta), grid, N,
-                         accumulate ? 1 : 0);
+                         accumulate ? 1 : 0, px, reinterpret_cast<WT*>(dbias_in));
     }
   });
   check_launch();

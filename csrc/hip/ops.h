@@ -56,7 +56,8 @@ void layernorm_fwd(uintptr_t x, uintptr_t gamma, uintptr_t beta, uintptr_t y, ui
 int layernorm_bwd_partial_rows(int64_t M);
 void layernorm_bwd(uintptr_t dy, uintptr_t x, uintptr_t mean, uintptr_t rstd, uintptr_t gamma, uintptr_t dx,
                    uintptr_t dgamma, uintptr_t dbeta, uintptr_t workspace, int64_t M, int N, int dt, int wdt,
-                   bool accumulate, uintptr_t stream);
+                   bool accumulate, uintptr_t stream,
+                   uintptr_t dbias_in = 0);
 
 // ---- fused softmax cross-entropy (xent.hip) ----
 // logits [rows][ld] (bf16 / fp32, 16-byte rows), V <= ld valid classes; per-row lse / loss /

@@ -203,5 +203,7 @@ def test_resnet_stage_fused_dgrad_bn_matches_unfused(monkeypatch, fuse_pair):
     # the exact semantics are pinned by test_fused_dgrad_bn_matches_fp64
     names = ["y", "x.grad"] + [n for n, _ in blocks.named_parameters()]
     rel = [(nm, float((u - v).norm() / v.norm().clamp_min(1e-12))) for nm, u, v in zip(names, *outs)]
-    bad = [(nm, e) for nm, e in rel if e > 1e-4]
+    # observed 0.3-2.6e-4 between the paths over repeated runs; a wrong mask, a missing
+    # shortcut term or stale sums give O(1) errors
+    bad = [(nm, e) for nm, e in rel if e > 1e-3]
     assert not bad, bad

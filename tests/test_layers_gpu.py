@@ -59,3 +59,48 @@ def test_encoder_layer_fused_residual_and_sink_match_unfused(dropout, monkeypatc
         assert _rel(dx, dx_ref) < 2e-2, (fused, sink, _rel(dx, dx_ref))
         for n in pg_ref:
             assert _rel(pg[n], pg_ref[n]) < 3e-2, (fused, sink, n, _rel(pg[n], pg_ref[n]))
+
+
+@pytest.mark.gpu
+def test_fp32_encoder_bias_handoffs_match_unfused(monkeypatch):
+    """fp32 BERT-style encoder layer with flat gradients: the two sublayers' output-projection
+    bias gradients from the LayerNorm backwards (ops/dense.BiasHandoff) equal the Linear column
+    sums of the unfused path; those two Linears skip their own column-sum pass."""
+    import vodascheduler_amd.models.layers as L
+    from vodascheduler_amd.ops import dense
+    from vodascheduler_amd.ops.optim import make_optimizer
+    from vodascheduler_amd.utils.flat import grad_of
+
+    torch.manual_seed(0)
+    base = L.EncoderLayer(256, 4, 1024, act="gelu", dropout=0.0).cuda()
+    x0 = torch.randn(8, 64, 256, device="cuda")
+    seen = []
+    real = dense.linear_weight_grads
+
+    def spy(dy2, x2, weight, bias, need_w, need_b):
+        seen.append(need_b)
+        return real(dy2, x2, weight, bias, need_w, need_b)
+
+    monkeypatch.setattr(dense, "linear_weight_grads", spy)
+
+    real_target = dense.BiasHandoff.target
+
+    def run(fused):
+        # reference: every handoff declines (the Linears sum their own bias gradients)
+        monkeypatch.setattr(dense.BiasHandoff, "target", real_target if fused else (lambda self, dtype: None))
+        m = copy.deepcopy(base).train()
+        opt = make_optimizer("sgd", m.parameters(), lr=0.0)
+        opt.zero_grad()
+        x = x0.clone().requires_grad_(True)
+        m(x).square().mean().backward()
+        torch.cuda.synchronize()
+        return x.grad, {n: grad_of(p).clone() for n, p in m.named_parameters()}
+
+    dx_ref, pg_ref = run(False)
+    assert all(seen) and len(seen) == 4
+    seen.clear()
+    dx, pg = run(True)
+    assert sorted(seen) == [False, False, True, True], seen  # qkv and fc1 sum their own biases
+    assert _rel(dx, dx_ref) < 1e-5
+    for n in pg_ref:
+        assert _rel(pg[n], pg_ref[n]) < 1e-5, (n, _rel(pg[n], pg_ref[n]))

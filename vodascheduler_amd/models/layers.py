@@ -19,7 +19,7 @@ from torch import nn
 from ..ops.activation import GeluTanh
 from ..ops.attention import attention_q_kvpacked, attention_qkvpacked
 from ..ops.conv1x1 import USE_GRAD_SINK, GradSink
-from ..ops.dense import FusedLinear, residual_add
+from ..ops.dense import BiasHandoff, FusedLinear, residual_add
 from ..ops.layernorm import FusedLayerNorm
 
 # residual add of each post-LN sublayer fused into the LayerNorm kernel (FUSED_RESIDUAL_LN = False:
@@ -27,6 +27,9 @@ from ..ops.layernorm import FusedLayerNorm
 FUSED_RESIDUAL_LN = True
 # FFN GELU on the HIP kernel (ops/activation.py; HIP_GELU = False: PyTorch's)
 HIP_GELU = True
+# a post-LN sublayer's output-projection bias gradient summed by the LayerNorm backward
+# (ops/dense.BiasHandoff; BIAS_HANDOFF = False: the projection's own column-sum pass)
+BIAS_HANDOFF = True
 
 
 class MultiHeadAttention(nn.Module):
@@ -55,9 +58,10 @@ class MultiHeadAttention(nn.Module):
         self.dropout = dropout
 
     def forward(self, x: torch.Tensor, kv: torch.Tensor | None = None, key_mask: torch.Tensor | None = None,
-                causal: bool = False, sink_in=None) -> torch.Tensor:
+                causal: bool = False, sink_in=None, bias_handoff=None) -> torch.Tensor:
         """x: [B, Tq, D]; kv: [B, Tk, D] (default x); key_mask: [B, Tk] (nonzero = attend);
-        sink_in: GradSink of the residual stream x (self-attention only)."""
+        sink_in: GradSink of the residual stream x (self-attention only); bias_handoff: the
+        output projection's bias gradient comes from the next op (ops/dense.BiasHandoff)."""
         B, Tq, _ = x.shape
         E = self.inner
         drop = self.dropout if self.training else 0.0
@@ -72,7 +76,7 @@ class MultiHeadAttention(nn.Module):
             q = self.q(x).view(B, Tq, self.h, self.dk)
             kvp = self.kv(kv).view(B, Tk, 2, self.h, self.dk)
             o = attention_q_kvpacked(q, kvp, key_mask, causal, scale, drop)
-        return self.o(o.reshape(B, Tq, E))
+        return self.o(o.reshape(B, Tq, E), bias_handoff=bias_handoff)
 
 
 class FeedForward(nn.Module):
@@ -85,10 +89,14 @@ class FeedForward(nn.Module):
         else:
             self.act = nn.ReLU()
 
-    def forward(self, x, sink_in=None):
+    def forward(self, x, sink_in=None, bias_handoff=None):
         # GELU runs as the HIP activation kernels between the two GEMMs: hipBLASLt on gfx950
-        # has no GELU_AUX / DGELU epilogue kernels (probe: profiles/raw/r2_blaslt_epilogue_probe.jsonl)
-        return self.fc2(self.act(self.fc1(x, sink_in)))
+        # has no GELU_AUX / DGELU epilogue kernels (probe: profiles/raw/r2_blaslt_epilogue_probe.jsonl).
+        # fc1's bias gradient stays a column-sum pass: folding it into a row-mapped GELU
+        # backward (gelu_tanh_bwd_colsum) measured 72-94 us vs 69 us for the flat GELU kernel +
+        # column sum (BERT-base fp32, profiles/r5/gelu_colsum.jsonl; the fused kernel was removed).
+        # fc2's comes from the next LayerNorm's backward when the caller hands over ``bias_handoff``
+        return self.fc2(self.act(self.fc1(x, sink_in)), bias_handoff=bias_handoff)
 
 
 def _sink(module: nn.Module, x: torch.Tensor) -> GradSink | None:
@@ -113,6 +121,15 @@ class EncoderLayer(nn.Module):
         # instead of by a separate autograd add (ops/conv1x1.GradSink)
         # the add itself runs inside the LayerNorm kernel (FusedLayerNorm(x, residual=...))
         s1 = _sink(self, x)
+        if FUSED_RESIDUAL_LN and BIAS_HANDOFF and (self.drop.p == 0 or not self.training):
+            # no dropout between the sublayer's last projection and the LayerNorm: the
+            # LayerNorm backward sums that projection's bias gradient (ops/dense.BiasHandoff)
+            h1 = BiasHandoff(self.attn.o.bias)
+            x = self.ln1(self.attn(x, key_mask=key_mask, sink_in=s1, bias_handoff=h1), residual=x, sink=s1,
+                         bias_handoff=h1)
+            s2 = _sink(self, x)
+            h2 = BiasHandoff(self.ff.fc2.bias)
+            return self.ln2(self.ff(x, sink_in=s2, bias_handoff=h2), residual=x, sink=s2, bias_handoff=h2)
         a = self.drop(self.attn(x, key_mask=key_mask, sink_in=s1))
         x = self.ln1(a, residual=x, sink=s1) if FUSED_RESIDUAL_LN else self.ln1(residual_add(x, a, s1))
         s2 = _sink(self, x)

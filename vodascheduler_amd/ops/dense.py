@@ -130,11 +130,34 @@ def linear_weight_grads(dy2: torch.Tensor, x2: torch.Tensor, weight: torch.Tenso
     return dw, db
 
 
+class BiasHandoff:
+    """The bias gradient of a Linear computed by the NEXT op's backward, which reads the
+    Linear's output gradient anyway: the FFN's GELU backward for fc1 (``gelu_tanh_bwd_colsum``)
+    and a post-LN sublayer's LayerNorm backward for its last projection (``layernorm_bwd`` with
+    ``dbias_in``).  That op sums the gradient's columns into the bias's flat fp32 gradient,
+    signals it ready and sets ``done``; the Linear's backward then skips its column-sum pass.
+    Only valid when nothing between the two ops changes the gradient (no dropout), which the
+    model wiring guarantees (models/layers.py)."""
+
+    __slots__ = ("bias", "done")
+
+    def __init__(self, bias):
+        self.bias, self.done = bias, False
+
+    def target(self, dtype: torch.dtype):
+        """The flat gradient to accumulate into, or None (no flat gradient of that dtype)."""
+        if self.bias is None or not _direct(self.bias):
+            return None
+        g = flat_grad(self.bias)
+        return g if g.dtype == dtype else None
+
+
 class _DenseFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, weight, bias, sink_in=None):
+    def forward(ctx, x, weight, bias, sink_in=None, bias_handoff=None):
         """``sink_in`` (ops/conv1x1.GradSink): accumulate the input gradient into the
-        residual-stream gradient a producer left there (one GEMM with beta = 1)."""
+        residual-stream gradient a producer left there (one GEMM with beta = 1);
+        ``bias_handoff`` (BiasHandoff): the bias gradient may arrive from the next op."""
         if x.dtype != weight.dtype and torch.is_autocast_enabled(x.device.type):
             x = x.to(weight.dtype)
         with torch.autocast(x.device.type, enabled=False):
@@ -142,6 +165,7 @@ class _DenseFn(torch.autograd.Function):
         ctx.save_for_backward(x, weight)
         ctx.bias = bias
         ctx.sink_in = sink_in
+        ctx.bias_handoff = bias_handoff
         return y
 
     @staticmethod
@@ -165,8 +189,12 @@ class _DenseFn(torch.autograd.Function):
         elif ctx.needs_input_grad[0]:
             dx = _dgrad(dy2, weight).view(x.shape)
         need_w, need_b = ctx.needs_input_grad[1], bias is not None and ctx.needs_input_grad[2]
+        hb = ctx.bias_handoff
+        if need_b and hb is not None and hb.done:
+            need_b = False  # summed into the flat gradient by the next op's backward
+            hb.done = False
         dw, db = linear_weight_grads(dy2, x2, weight, bias, need_w, need_b)
-        return dx, dw, db, None
+        return dx, dw, db, None, None
 
 
 class _ResidualAddFn(torch.autograd.Function):
@@ -198,5 +226,5 @@ def residual_add(x: torch.Tensor, y: torch.Tensor, sink=None) -> torch.Tensor:
 class FusedLinear(torch.nn.Linear):
     """Drop-in ``nn.Linear`` using :class:`_DenseFn` (state-dict compatible)."""
 
-    def forward(self, x, sink_in=None):
-        return _DenseFn.apply(x, self.weight, self.bias, sink_in)
+    def forward(self, x, sink_in=None, bias_handoff=None):
+        return _DenseFn.apply(x, self.weight, self.bias, sink_in, bias_handoff)

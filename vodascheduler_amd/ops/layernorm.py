@@ -35,7 +35,7 @@ def _supported(x: torch.Tensor, weight: torch.Tensor | None) -> bool:
 
 class _LayerNormFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, weight, bias, eps, residual=None, sink=None):
+    def forward(ctx, x, weight, bias, eps, residual=None, sink=None, bias_handoff=None):
         """``residual``: normalise ``x + residual`` (the kernel writes the sum, which the backward
         normalises again); ``sink`` (ops/conv1x1.GradSink): hand the residual's gradient to the
         GEMM that consumed the residual stream instead of returning it."""
@@ -65,6 +65,7 @@ class _LayerNormFn(torch.autograd.Function):
         ctx.wdt = wdt
         ctx.has_res = residual is not None
         ctx.sink = sink if residual is not None else None
+        ctx.bias_handoff = bias_handoff
         return y.view_as(x)
 
     @staticmethod
@@ -84,9 +85,15 @@ class _LayerNormFn(torch.autograd.Function):
         # launch for both, no autograd add afterwards) when it owns them
         direct = (LN_DIRECT_GRADS and need_w and need_b and _direct(weight) and _direct(bias)
                   and flat_grad(weight).dtype == ctx.wdt and flat_grad(bias).dtype == ctx.wdt)
+        # the bias gradient of the Linear that produced x (BiasHandoff): column sums of dx,
+        # folded into this pass (needs the direct gamma / beta path and the same dtype)
+        hb = ctx.bias_handoff
+        tgt = hb.target(ctx.wdt) if (hb is not None and direct and ctx.needs_input_grad[0]) else None
+        if tgt is not None and tgt.numel() != n:
+            tgt = None
         if need_w or need_b:
             rows = N.hip().layernorm_bwd_partial_rows(m)
-            ws = torch.empty(2 * rows * n, dtype=torch.float32, device=xc.device)
+            ws = torch.empty((3 if tgt is not None else 2) * rows * n, dtype=torch.float32, device=xc.device)
             if direct:
                 dgamma, dbeta = flat_grad(weight), flat_grad(bias)
             else:
@@ -94,7 +101,11 @@ class _LayerNormFn(torch.autograd.Function):
                 dbeta = torch.empty(n, dtype=ctx.wdt, device=xc.device)
         N.hip().layernorm_bwd(dyc.data_ptr(), xc.data_ptr(), mean.data_ptr(), rstd.data_ptr(), N.ptr(w),
                               dx.data_ptr(), N.ptr(dgamma), N.ptr(dbeta), N.ptr(ws), m, n,
-                              N.dtype_code(xc.dtype), N.dtype_code(ctx.wdt), bool(direct), N.stream_of(xc))
+                              N.dtype_code(xc.dtype), N.dtype_code(ctx.wdt), bool(direct), N.stream_of(xc),
+                              N.ptr(tgt))
+        if tgt is not None:
+            hb.done = True
+            _ready(hb.bias)
         dx = dx.view_as(dy)
         dres = None
         if ctx.has_res:
@@ -107,13 +118,15 @@ class _LayerNormFn(torch.autograd.Function):
         if direct:
             _ready(weight)
             _ready(bias)
-        return dx if ctx.needs_input_grad[0] else None, gw, gb, None, dres, None
+        return dx if ctx.needs_input_grad[0] else None, gw, gb, None, dres, None, None
 
 
 def layer_norm(x: torch.Tensor, weight: torch.Tensor | None = None, bias: torch.Tensor | None = None,
-               eps: float = 1e-5, residual: torch.Tensor | None = None, sink=None) -> torch.Tensor:
+               eps: float = 1e-5, residual: torch.Tensor | None = None, sink=None,
+               bias_handoff=None) -> torch.Tensor:
     """LayerNorm over the last dimension; with ``residual``, of ``x + residual`` (one fused pass
-    on GPU).  ``sink``: see ops/conv1x1.GradSink (the residual's gradient is handed over)."""
+    on GPU).  ``sink``: see ops/conv1x1.GradSink (the residual's gradient is handed over);
+    ``bias_handoff``: ops/dense.BiasHandoff of the Linear that produced ``x``."""
     if residual is not None and (not x.is_cuda or residual.shape != x.shape or residual.dtype != x.dtype):
         from .dense import residual_add
 
@@ -122,8 +135,8 @@ def layer_norm(x: torch.Tensor, weight: torch.Tensor | None = None, bias: torch.
         if not _supported(x, weight):
             raise ValueError(f"fused layer_norm: unsupported shape/dtype {tuple(x.shape)} {x.dtype}")
         if residual is not None:
-            return _LayerNormFn.apply(x, weight, bias, eps, residual, sink)
-        return _LayerNormFn.apply(x, weight, bias, eps)
+            return _LayerNormFn.apply(x, weight, bias, eps, residual, sink, bias_handoff)
+        return _LayerNormFn.apply(x, weight, bias, eps, None, None, bias_handoff)
     n = x.shape[-1]
     y = torch.nn.functional.layer_norm(x.float(), (n,), None if weight is None else weight.float(),
                                        None if bias is None else bias.float(), eps)
@@ -149,13 +162,13 @@ class FusedLayerNorm(torch.nn.Module):
             self.register_parameter("weight", None)
             self.register_parameter("bias", None)
 
-    def forward(self, x, residual=None, sink=None):
+    def forward(self, x, residual=None, sink=None, bias_handoff=None):
         """``LN(x)``, or ``LN(x + residual)`` with the add fused into the normalisation pass."""
         if x.is_cuda and torch.is_autocast_enabled("cuda"):
             # keep the input dtype (bf16 out, fp32 statistics inside the kernel)
             with torch.autocast("cuda", enabled=False):
-                return layer_norm(x, self.weight, self.bias, self.eps, residual, sink)
-        return layer_norm(x, self.weight, self.bias, self.eps, residual, sink)
+                return layer_norm(x, self.weight, self.bias, self.eps, residual, sink, bias_handoff)
+        return layer_norm(x, self.weight, self.bias, self.eps, residual, sink, bias_handoff)
 
     def extra_repr(self):
         return f"{self.normalized_shape}, eps={self.eps}"
