@@ -16,6 +16,7 @@ import os
 import torch
 from torch import nn
 
+from ..ops import ffn as _ffn
 from ..ops.activation import GeluTanh
 from ..ops.attention import attention_q_kvpacked, attention_qkvpacked
 from ..ops.conv1x1 import USE_GRAD_SINK, GradSink
@@ -90,8 +91,18 @@ class FeedForward(nn.Module):
             self.act = nn.ReLU()
 
     def forward(self, x, sink_in=None, bias_handoff=None):
-        # GELU runs as the HIP activation kernels between the two GEMMs: hipBLASLt on gfx950
-        # has no GELU_AUX / DGELU epilogue kernels (probe: profiles/raw/r2_blaslt_epilogue_probe.jsonl).
+        if isinstance(self.act, GeluTanh) and x.is_cuda:
+            if x.dtype != self.fc1.weight.dtype and torch.is_autocast_enabled("cuda"):
+                x = x.to(self.fc1.weight.dtype)
+            if _ffn.supported(x, self.fc1.weight, self.fc1.bias, self.fc2.weight, self.fc2.bias):
+                # fp32: GELU in the hipBLASLt GEMM epilogues (ops/ffn.py), no GELU kernels
+                try:
+                    return _ffn.ffn_gelu(x, self.fc1.weight, self.fc1.bias, self.fc2.weight, self.fc2.bias,
+                                         sink_in, bias_handoff)
+                except (RuntimeError, ValueError) as e:  # no epilogue kernel for this shape
+                    _ffn.disable_epilogue(repr(e))
+        # Otherwise (bf16: hipBLASLt on gfx950 has no GELU_AUX / DGELU bf16 kernels, probe:
+        # profiles/raw/r2_blaslt_epilogue_probe.jsonl) GELU runs as the HIP activation kernels.
         # fc1's bias gradient stays a column-sum pass: folding it into a row-mapped GELU
         # backward (gelu_tanh_bwd_colsum) measured 72-94 us vs 69 us for the flat GELU kernel +
         # column sum (BERT-base fp32, profiles/r5/gelu_colsum.jsonl; the fused kernel was removed).
