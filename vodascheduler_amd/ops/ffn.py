@@ -27,7 +27,7 @@ import torch
 import torch.nn.functional as F
 
 from . import _native as N
-from .dense import _dgrad, linear_weight_grads
+from . import dense as D
 
 # VODA_GELU_EPILOGUE=0: the FFN runs FusedLinear -> GELU kernel -> FusedLinear (A/B switch)
 USE_GELU_EPILOGUE = os.environ.get("VODA_GELU_EPILOGUE", "1") != "0"
@@ -127,9 +127,9 @@ class _FFNGeluFn(torch.autograd.Function):
         if need_b2 and hb is not None and hb.done:
             need_b2 = False  # summed into the flat gradient by the LayerNorm backward
             hb.done = False
-        dw2, db2 = linear_weight_grads(do2, y, w2, b2, need[3], need_b2)
+        dw2, db2 = D.linear_weight_grads(do2, y, w2, b2, need[3], need_b2)
         dh = gemm_dgelu(do2, w2, h)
-        dw1, db1 = linear_weight_grads(dh, x2, w1, b1, need[1], need[2])
+        dw1, db1 = D.linear_weight_grads(dh, x2, w1, b1, need[1], need[2])
         dx = None
         acc = ctx.sink_in.take() if ctx.sink_in is not None and need[0] else None
         if acc is not None:
@@ -138,7 +138,7 @@ class _FFNGeluFn(torch.autograd.Function):
             acc.view(-1, w1.shape[1]).addmm_(dh, w1)  # residual-stream gradient + dh . W1
             dx = acc
         elif need[0]:
-            dx = _dgrad(dh, w1).view(ctx.x_shape)
+            dx = D._dgrad(dh, w1).view(ctx.x_shape)
         return dx, dw1, db1, dw2, db2, None, None
 
 
