@@ -56,6 +56,7 @@ PYBIND11_MODULE(_vodahip, m) {
         py::arg("N"), py::arg("K"), py::arg("G"), py::arg("stream"), py::arg("accumulate") = false);
   m.def("gemm_f32_stats_supported", &gemm_f32_stats_supported);
   m.def("gemm_f32_dgrad_bn", &gemm_f32_dgrad_bn);
+  m.def("stem_conv_fwd_f32", &stem_conv_fwd_f32);
   m.def("gemm_epilogue_algos", &gemm_epilogue_algos);
   m.def("gemm_gelu_aux", &gemm_gelu_aux);
   m.def("gemm_dgelu", &gemm_dgelu);

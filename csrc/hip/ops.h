@@ -156,6 +156,10 @@ int64_t stem_wgrad_workspace_floats(int N, int Ho);
 void stem_conv_wgrad(uintptr_t x4, uintptr_t dy, uintptr_t dw, int64_t s0, int64_t s1, int64_t s2, int64_t s3,
                      int Cin, uintptr_t ws, int N, int H, int W, int Ho, int Wo, bool accumulate, int out_dt,
                      uintptr_t stream);
+// fp32 stem (stem_f32.hip): the image read through its strides (1..3 channels), [N][Ho][Wo][64] fp32
+void stem_conv_fwd_f32(uintptr_t x, int64_t sN, int64_t sC, int64_t sH, int64_t sW, int Cin, uintptr_t w,
+                       int64_t sw0, int64_t sw1, int64_t sw2, int64_t sw3, uintptr_t y, uintptr_t part, int nb, int N,
+                       int H, int W, int Ho, int Wo, uintptr_t stream);
 void stem_conv_fwd(uintptr_t x4, uintptr_t w, int64_t sw0, int64_t sw1, int64_t sw2, int64_t sw3, int Cin, int Cout,
                    uintptr_t y, uintptr_t part, int nb, int N, int H, int W, int Ho, int Wo, uintptr_t stream);
 

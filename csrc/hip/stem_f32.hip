@@ -1,0 +1,312 @@
+// ResNet stem at the reference's precision (fp32): 7x7 / stride-2 / pad-3 convolution of a
+// 1..3-channel fp32 image into 64 channels on the f32-input MFMA (v_mfma_f32_32x32x2_f32,
+// exact fp32), with the batch-norm statistics of its output computed in the epilogue.
+//
+// What it replaces (profiles/r5/rocprof_resnet50_fp32_tile_gemm_off.md, one fp32 ResNet-50
+// bs256 step): MIOpen's output zero-fill (127 us), igemm_fwd (749 us, ~81 TF on the 60 GFLOP of
+// the layer) and the BN statistics pass that re-reads the 822 MB output (197 us).
+//
+// Design (same skeleton as the bf16 stem of stem.hip; the fp32 operands change the data layout):
+//  * the reduction of one filter row kh is k = kw * 3 + c (21 real terms, padded to 24 = three
+//    8-wide chunks with zero filter weights), not the bf16 kernel's 8 pixels x 4 channels = 32:
+//    168 instead of 224 MFMAs per output row and wave;
+//  * input rows live in a 16-slot LDS ring as flat fp32 [264 px][3 ch] (zero outside the image);
+//    output pixel wo's window of filter row kh starts at flat index 6 wo, so the permuted-k
+//    fragment of lane half h (k = 8 q + 4 h + s for MFMA s) is the float4 at 6 wo + 8 q + 4 h:
+//    two ds_read_b64 (24-byte pixel pitch: 8-byte aligned) feed four MFMAs;
+//  * a workgroup (4 waves = 2 channel tiles x 2 pixel halves) produces one output row
+//    (Wo <= 128) at a time; the filter fragments of the wave's channel tile (7 kh x 3 chunks
+//    x float4 = 84 VGPRs) stay in registers for the whole persistent row chunk;
+//  * consecutive output rows share 5 of their 7 input rows: the steady state loads the 2 new
+//    rows into registers two output rows ahead, while the current row's MFMAs run;
+//  * D rows = pixels, columns = channels: a lane holds one channel of 16 pixels, so the
+//    per-channel sums / sums of squares are in-lane adds carried across the chunk, and each
+//    output store is 32 lanes x 4 B = one 128-byte channels_last segment; stores go through a
+//    per-row buffer resource whose bound drops the pixels past Wo.
+#include "common.h"
+
+#include <algorithm>
+#include <type_traits>
+#include "ops.h"
+
+namespace voda {
+
+namespace {
+
+typedef float sf_f32x16 __attribute__((ext_vector_type(16)));
+
+constexpr int kFK = 7, kFS = 2, kFP = 3;           // filter, stride, padding
+constexpr int kFCo = 64;                           // output channels (two 32-wide MFMA tiles)
+constexpr int kFC = 3;                             // input channels held per pixel in LDS
+constexpr int kFWaves = 4;
+constexpr int kFThreads = 64 * kFWaves;
+constexpr int kFMaxWo = 128;                       // 2 pixel halves x 2 tiles x 32
+constexpr int kFRowPx = 2 * kFMaxWo + 8;           // 264 LDS pixels per input row (wi = -3 ..)
+constexpr int kFRowF = kFRowPx * kFC;              // 792 floats
+constexpr int kFRowB = kFRowF * 4;                 // 3168 B
+constexpr int kFSlots = 16;                        // LDS ring of input rows
+constexpr int kFKq = 3;                            // 8-wide k chunks per filter row (24 >= 21)
+constexpr int kFPf = (2 * kFRowF + kFThreads - 1) / kFThreads;  // prefetch floats per thread (7)
+
+struct StemF32Args {
+  const float* x;                     // image, element strides below
+  int64_t sN, sC, sH, sW;
+  int cin;
+  const float* w;                     // [64][cin][7][7], element strides below
+  int64_t sw0, sw1, sw2, sw3;
+  float* y;                           // [N][Ho][Wo][64] (channels_last)
+  float* part;                        // [2][gridDim.x][64]
+  int N, H, W, Ho, Wo;
+};
+
+__device__ __forceinline__ sf_f32x16 sf_mfma(float a, float b, sf_f32x16 c) {
+  return __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, c, 0, 0, 0);
+}
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t sf_rsrc(const void* base, int64_t bytes) {
+  const int64_t b = bytes < 0 ? 0 : (bytes > 0x7fffffff ? 0x7fffffff : bytes);
+  const uint64_t a = reinterpret_cast<uint64_t>(base);
+  const uint32_t lo = __builtin_amdgcn_readfirstlane(uint32_t(a));
+  const uint32_t hi = __builtin_amdgcn_readfirstlane(uint32_t(a >> 32));
+  return __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void*>((uint64_t(hi) << 32) | lo), 0,
+                                           __builtin_amdgcn_readfirstlane(int(b)), 0x00020000);
+}
+
+// byte offset of element j of the flat LDS row of input row hi (pixel wi = j / 3 - 3, channel
+// j % 3) in the image, or an offset past the buffer's bound (the load returns 0) outside the
+// image and for channels >= cin: branch-free, 32-bit
+__device__ __forceinline__ uint32_t sf_off(const StemF32Args& a, int64_t n, int hi, int j) {
+  const int px = j / kFC, c = j - px * kFC;
+  const int wi = px - kFP;
+  const bool ok = unsigned(hi) < unsigned(a.H) && unsigned(wi) < unsigned(a.W) && c < a.cin;
+  const uint32_t o = uint32_t((n * a.sN + c * a.sC + int64_t(hi) * a.sH + int64_t(wi) * a.sW) * 4);
+  return ok ? o : 0xfffffff0u;
+}
+
+__device__ __forceinline__ float sf_load(__amdgpu_buffer_rsrc_t rx, uint32_t off) {
+  return __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rx, int(off), 0, 0));
+}
+
+// the 7 input rows of output row ho into the ring, loads issued in batches of B before their
+// LDS writes
+template <int B>
+__device__ __forceinline__ void sf_fill_window(float* ring, const StemF32Args& a, __amdgpu_buffer_rsrc_t rx, int64_t n,
+                                               int ho, int tid) {
+  constexpr int kTotal = kFK * kFRowF;                          // 5544
+  constexpr int kIters = (kTotal + kFThreads - 1) / kFThreads;  // 22
+#pragma unroll
+  for (int b = 0; b < kIters; b += B) {
+    float v[B];
+#pragma unroll
+    for (int u = 0; u < B; ++u) {
+      const int i = min(tid + (b + u) * kFThreads, kTotal - 1);
+      const int r = i / kFRowF, j = i - r * kFRowF;
+      v[u] = sf_load(rx, sf_off(a, n, kFS * ho - kFP + r, j));
+    }
+#pragma unroll
+    for (int u = 0; u < B; ++u) {
+      const int i = tid + (b + u) * kFThreads;
+      if (b + u < kIters && i < kTotal) {
+        const int r = i / kFRowF, j = i - r * kFRowF;
+        ring[((kFS * ho - kFP + r) & (kFSlots - 1)) * kFRowF + j] = v[u];
+      }
+    }
+  }
+}
+
+__global__ __launch_bounds__(kFThreads, 2) void stem_f32_fwd_kernel(StemF32Args a) {
+  __shared__ __attribute__((aligned(16))) float ring[kFSlots * kFRowF];  // 50.7 KB
+  __shared__ float red[kFWaves][2][32];
+
+  const int tid = threadIdx.x;
+  const int wave = tid >> 6, lane = tid & 63;
+  const int lc = lane & 31, lh = lane >> 5;
+  const int ct = wave & 1, ph = wave >> 1;  // channel tile, pixel half
+
+  // ---- filter fragments: the workgroup packs W as [64 co][7 kh][24 k] (k = kw * 3 + c, zero
+  // for k >= 21 or c >= cin) into the ring's LDS, then lane (co = 32 ct + lc, half lh) reads
+  // float4 [co][kh][8 q + 4 lh] for q = 0..2
+  {
+    constexpr int kWElems = kFCo * kFK * kFKq * 8;  // 10752
+    constexpr int kPer = kWElems / kFThreads;       // 42
+#pragma unroll
+    for (int b = 0; b < kPer; b += 14) {
+      float v[14];
+#pragma unroll
+      for (int i = 0; i < 14; ++i) {
+        const int e = tid + (b + i) * kFThreads;
+        const int co = e / (kFK * 24), r = e - co * (kFK * 24);
+        const int kh = r / 24, k = r - kh * 24;
+        const int kw = k / kFC, c = k - kw * kFC;
+        v[i] = (k < kFK * kFC && c < a.cin) ? a.w[co * a.sw0 + c * a.sw1 + kh * a.sw2 + kw * a.sw3] : 0.f;
+      }
+#pragma unroll
+      for (int i = 0; i < 14; ++i) ring[tid + (b + i) * kFThreads] = v[i];
+    }
+  }
+  __syncthreads();
+  float4 wf[kFK][kFKq];
+#pragma unroll
+  for (int kh = 0; kh < kFK; ++kh)
+#pragma unroll
+    for (int q = 0; q < kFKq; ++q) {
+      float4 f = *reinterpret_cast<const float4*>(&ring[((32 * ct + lc) * kFK + kh) * 24 + 8 * q + 4 * lh]);
+      // opaque to the optimizer: keeps the fragment resident instead of re-deriving it
+      asm volatile("" : "+v"(f.x), "+v"(f.y), "+v"(f.z), "+v"(f.w));
+      wf[kh][q] = f;
+    }
+  __syncthreads();  // the ring's LDS is reused below
+
+  // the image through one buffer resource (32-bit offsets; out-of-image elements read 0)
+  const auto rx = sf_rsrc(a.x, (int64_t(a.N - 1) * a.sN + int64_t(a.cin - 1) * a.sC + int64_t(a.H - 1) * a.sH +
+                                int64_t(a.W - 1) * a.sW + 1) * 4);
+  // this thread's share of a 2-row refill: flat slot i = tid + 256 k of 2 x 792 is input row
+  // i / 792 (of the two), element i % 792
+
+  float s1 = 0.f, s2 = 0.f;  // channel 32 ct + lc
+  const int64_t rows = int64_t(a.N) * a.Ho;
+  const int64_t per = (rows + gridDim.x - 1) / gridDim.x;
+  const int64_t r0 = int64_t(blockIdx.x) * per;
+  const int64_t r1 = r0 + per < rows ? r0 + per : rows;
+  const int px0 = 64 * ph;  // this wave's first output pixel (tiles px0, px0 + 32)
+  // A operand of pixel tile t: flat index 6 (px0 + 32 t + lc) + 8 q + 4 lh of the row's slot
+  const int abase = 6 * (px0 + lc) + 4 * lh;
+  // output stores: lane (channel 32 ct + lc) of pixel px0 + 4 lh + row (r & 3) + 8 (r >> 2)
+  const int vy = ((px0 + 4 * lh) * kFCo + 32 * ct + lc) * 4;
+
+  int64_t n = r0 / a.Ho;
+  int ho = int(r0 - n * a.Ho);
+  float pf[2][kFPf];
+  bool vv[2] = {false, false};
+  bool in_lds = false;
+  auto load_rows = [&](float (&dst)[kFPf], int hbase) __attribute__((always_inline)) {
+#pragma unroll
+    for (int k = 0; k < kFPf; ++k) {
+      const int i = min(tid + k * kFThreads, 2 * kFRowF - 1);
+      const int r = i / kFRowF;
+      dst[k] = sf_load(rx, sf_off(a, n, hbase + r, i - r * kFRowF));
+    }
+  };
+  auto step = [&](int64_t row, auto bc) __attribute__((always_inline)) {
+    constexpr int B = decltype(bc)::value, O = 1 - B;
+    if (!in_lds) sf_fill_window<4>(ring, a, rx, n, ho, tid);  // first row of a chunk / image
+    __syncthreads();
+    const bool nxt1 = row + 1 < r1 && ho + 1 < a.Ho;
+    const bool nxt2 = nxt1 && row + 2 < r1 && ho + 2 < a.Ho;
+    if (nxt1 && !vv[B]) {
+      load_rows(pf[B], kFS * ho + 4);
+      vv[B] = true;
+    }
+    vv[O] = nxt2;
+    if (nxt2) load_rows(pf[O], kFS * ho + 6);
+    // ---- 7 filter rows x 3 chunks x 4 k-steps, 2 pixel tiles of 32
+    sf_f32x16 acc0 = {}, acc1 = {};
+#pragma unroll
+    for (int kh = 0; kh < kFK; ++kh) {
+      const float* src = &ring[((kFS * ho - kFP + kh) & (kFSlots - 1)) * kFRowF + abase];
+#pragma unroll
+      for (int q = 0; q < kFKq; ++q) {
+        const float2 a0l = *reinterpret_cast<const float2*>(src + 8 * q);
+        const float2 a0h = *reinterpret_cast<const float2*>(src + 8 * q + 2);
+        const float2 a1l = *reinterpret_cast<const float2*>(src + 6 * 32 + 8 * q);
+        const float2 a1h = *reinterpret_cast<const float2*>(src + 6 * 32 + 8 * q + 2);
+        const float4 f = wf[kh][q];
+        acc0 = sf_mfma(a0l.x, f.x, acc0);
+        acc1 = sf_mfma(a1l.x, f.x, acc1);
+        acc0 = sf_mfma(a0l.y, f.y, acc0);
+        acc1 = sf_mfma(a1l.y, f.y, acc1);
+        acc0 = sf_mfma(a0h.x, f.z, acc0);
+        acc1 = sf_mfma(a1h.x, f.z, acc1);
+        acc0 = sf_mfma(a0h.y, f.w, acc0);
+        acc1 = sf_mfma(a1h.y, f.w, acc1);
+      }
+    }
+    // ---- row + 1's 2 new input rows into their ring slots (outside this row's window)
+    if (vv[B]) {
+#pragma unroll
+      for (int k = 0; k < kFPf; ++k) {
+        const int i = tid + k * kFThreads;
+        if (i < 2 * kFRowF) {
+          const int r = i / kFRowF;
+          ring[((kFS * ho + 4 + r) & (kFSlots - 1)) * kFRowF + i - r * kFRowF] = pf[B][k];
+        }
+      }
+    }
+    in_lds = vv[B];
+    vv[B] = false;
+    // ---- epilogue: statistics of the valid pixels, stores (pixels >= Wo dropped by the bound)
+    auto stats = [&](const sf_f32x16& acc, int tbase) {
+      if (tbase + 32 <= a.Wo) {  // full tile (wave-uniform): no masking
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          s1 += acc[r];
+          s2 = fmaf(acc[r], acc[r], s2);
+        }
+      } else if (tbase < a.Wo) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const float keep = tbase + (r & 3) + 8 * (r >> 2) + 4 * lh < a.Wo ? 1.f : 0.f;
+          const float v = acc[r] * keep;
+          s1 += v;
+          s2 = fmaf(v, v, s2);
+        }
+      }
+    };
+    stats(acc0, px0);
+    stats(acc1, px0 + 32);
+    const auto ry = sf_rsrc(a.y + row * a.Wo * kFCo, int64_t(a.Wo) * kFCo * 4);
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int so = ((r & 3) + 8 * (r >> 2)) * kFCo * 4;
+      __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(acc0[r]), ry, vy, so, 0);
+      __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(acc1[r]), ry, vy, so + 32 * kFCo * 4, 0);
+    }
+    __syncthreads();  // every wave is done reading this row's window
+    if (++ho == a.Ho) {
+      ho = 0;
+      ++n;
+    }
+  };
+  for (int64_t row = r0; row < r1; row += 2) {
+    step(row, std::integral_constant<int, 0>{});
+    if (row + 1 < r1) step(row + 1, std::integral_constant<int, 1>{});
+  }
+
+  // ---- one partial row per workgroup: waves t and t + 2 hold channel tile t
+  s1 += __shfl_xor(s1, 32);
+  s2 += __shfl_xor(s2, 32);
+  if (lh == 0) {
+    red[wave][0][lc] = s1;
+    red[wave][1][lc] = s2;
+  }
+  __syncthreads();
+  if (tid < kFCo) {
+    const int c = tid, t = c >> 5, l = c & 31;
+    a.part[int64_t(blockIdx.x) * kFCo + c] = red[t][0][l] + red[t + 2][0][l];
+    a.part[int64_t(gridDim.x) * kFCo + int64_t(blockIdx.x) * kFCo + c] = red[t][1][l] + red[t + 2][1][l];
+  }
+}
+
+}  // namespace
+
+void stem_conv_fwd_f32(uintptr_t x, int64_t sN, int64_t sC, int64_t sH, int64_t sW, int Cin, uintptr_t w,
+                       int64_t sw0, int64_t sw1, int64_t sw2, int64_t sw3, uintptr_t y, uintptr_t part, int nb, int N,
+                       int H, int W, int Ho, int Wo, uintptr_t stream) {
+  VODA_CHECK(Cin >= 1 && Cin <= kFC, "stem_conv_f32: 1..3 input channels");
+  VODA_CHECK(Ho == (H + 2 * kFP - kFK) / kFS + 1 && Wo == (W + 2 * kFP - kFK) / kFS + 1,
+             "stem_conv_f32: output size mismatch (7x7, stride 2, pad 3)");
+  VODA_CHECK(Wo >= 1 && Wo <= kFMaxWo, "stem_conv_f32: output width must be <= 128");
+  VODA_CHECK(nb == stem_partial_rows(N, Ho), "stem_conv_f32: partial-row count mismatch");
+  VODA_CHECK(x % 4 == 0 && w % 4 == 0 && y % 16 == 0 && part % 4 == 0, "stem_conv_f32: misaligned operands");
+  VODA_CHECK(sN >= 0 && sC >= 0 && sH >= 0 && sW >= 0 &&
+                 (int64_t(N - 1) * sN + int64_t(Cin - 1) * sC + int64_t(H - 1) * sH + int64_t(W - 1) * sW + 1) * 4 <
+                     (int64_t(1) << 31),
+             "stem_conv_f32: image must span < 2 GB (32-bit buffer offsets)");
+  VODA_CHECK(int64_t(Wo) * kFCo * 4 < (int64_t(1) << 31), "stem_conv_f32: output row too large");
+  StemF32Args a{reinterpret_cast<const float*>(x), sN, sC, sH, sW, Cin, reinterpret_cast<const float*>(w), sw0, sw1,
+                sw2, sw3, reinterpret_cast<float*>(y), reinterpret_cast<float*>(part), N, H, W, Ho, Wo};
+  hipLaunchKernelGGL(stem_f32_fwd_kernel, dim3(nb), dim3(kFThreads), 0, as_stream(stream), a);
+  check_launch();
+}
+
+}  // namespace voda

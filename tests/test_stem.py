@@ -173,3 +173,76 @@ def test_stem_wgrad_vs_fp64(n, h, w, out):
         got = dw.double()
         tol = 1e-2 * want.abs().max().item()
     torch.testing.assert_close(got, want, rtol=1e-2, atol=tol)
+
+
+# ---------------------------------------------------------------- fp32 stem (stem_f32.hip)
+@pytest.mark.gpu
+@pytest.mark.parametrize("n,h,w,cl", [(2, 224, 224, False), (2, 224, 224, True), (3, 97, 61, False),
+                                      (1, 256, 255, True), (2, 9, 1, False), (5, 40, 36, False)])
+def test_stem_conv_f32_and_partial_stats_vs_fp64(n, h, w, cl):
+    """fp32 MFMA 7x7/2 convolution read straight from the image's strides (NCHW or
+    channels_last), ragged output widths, with the BN partial sums of its epilogue."""
+    torch.manual_seed(1)
+    x = _img(n, h, w, cl=cl)
+    wt = torch.randn(64, 3, 7, 7, device="cuda") * 0.1
+    y, ws, nb = S.stem_conv_stats_f32(x, wt)
+    ref = F.conv2d(x.double(), wt.double(), stride=2, padding=3)
+    assert y.shape == ref.shape and y.is_contiguous(memory_format=torch.channels_last)
+    torch.testing.assert_close(y.double(), ref, rtol=1e-5, atol=1e-5 * ref.abs().max().item())
+    part = ws[: 2 * nb * 64].view(2, nb, 64).double().sum(1)
+    torch.testing.assert_close(part[0], ref.sum((0, 2, 3)), rtol=1e-5, atol=1e-4 * ref.numel() ** 0.5)
+    torch.testing.assert_close(part[1], (ref * ref).sum((0, 2, 3)), rtol=1e-5, atol=1e-3)
+
+
+@pytest.mark.gpu
+def test_stem_conv_f32_weight_layouts_and_channels():
+    """Any filter strides; fewer than 3 input channels (the missing ones read as zero)."""
+    torch.manual_seed(2)
+    x = _img(2, 64, 64)
+    w = torch.randn(64, 3, 7, 7, device="cuda") * 0.1
+    y0, _, _ = S.stem_conv_stats_f32(x, w)
+    y1, _, _ = S.stem_conv_stats_f32(x, w.contiguous(memory_format=torch.channels_last))
+    assert torch.equal(y0, y1)
+    x1 = x[:, :1].contiguous()
+    y2, _, _ = S.stem_conv_stats_f32(x1, w[:, :1].contiguous())
+    ref = F.conv2d(x1.double(), w[:, :1].double(), stride=2, padding=3)
+    torch.testing.assert_close(y2.double(), ref, rtol=1e-5, atol=1e-5 * ref.abs().max().item())
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("cl", [False, True])
+def test_fused_stem_fp32_training_step_vs_composition(cl):
+    """fp32 FusedStem (own conv + statistics epilogue, fused BN/pool, MIOpen weight gradient)
+    vs the plain fp32 composition: output, running statistics, filter and BN gradients."""
+    torch.manual_seed(3)
+    m = S.FusedStem(3, 64).cuda()
+    ref = S.FusedStem(3, 64).cuda()
+    m[1].weight.data.uniform_(0.5, 1.5)
+    ref.load_state_dict(m.state_dict())
+    x = _img(4, 224, 224, cl=cl, seed=4)
+    assert m._fast_f32_ok(x)
+    y = m(x)
+    assert type(y.grad_fn).__name__ == "_StemF32FnBackward"
+    yc = F.conv2d(x, ref[0].weight, stride=2, padding=3).contiguous(memory_format=torch.channels_last)
+    yr = ref[1](yc)
+    torch.testing.assert_close(y, yr, rtol=1e-4, atol=1e-4)
+    m[1].sync_batches_tracked()
+    ref[1].sync_batches_tracked()
+    torch.testing.assert_close(m[1].running_mean, ref[1].running_mean, rtol=1e-5, atol=1e-6)
+    torch.testing.assert_close(m[1].running_var, ref[1].running_var, rtol=1e-5, atol=1e-6)
+    dy = torch.randn_like(y)
+    y.backward(dy)
+    yr.backward(dy)
+    for a, b in ((m[0].weight.grad, ref[0].weight.grad), (m[1].weight.grad, ref[1].weight.grad),
+                 (m[1].bias.grad, ref[1].bias.grad)):
+        rel = ((a - b).norm() / b.norm()).item()
+        assert rel < 1e-4, rel
+
+
+@pytest.mark.gpu
+def test_resnet50_fp32_uses_fused_stem_f32():
+    from vodascheduler_amd.models.resnet import resnet50
+
+    m = resnet50().cuda().to(memory_format=torch.channels_last)
+    x = _img(2, 224, 224, cl=True)
+    assert m.stem._fast_f32_ok(x) and not m.stem._fast_ok(x)

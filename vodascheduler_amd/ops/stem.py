@@ -12,8 +12,10 @@ im2col rows of the packed image, fp32 straight into the optimizer's flat gradien
 The module keeps the ``nn.Sequential(conv, bn_pool)`` state dict (``stem.0.weight``,
 ``stem.1.*``) of the reference ResNet-50 (examples/py/tensorflow2/
 tensorflow2_keras_cifar_elastic.py builds Keras ResNet50; torchvision layout here).  Anything
-the kernel does not cover -- evaluation, CPU, other geometry, fp32 weights (the reference-
-precision run), output width > 128 -- runs the composition.
+the kernels do not cover -- evaluation, CPU, other geometry, output width > 128 -- runs the
+composition.  The reference-precision (fp32) run takes ``_StemF32Fn``: the fp32 MFMA
+convolution of csrc/hip/stem_f32.hip with the statistics epilogue, the same fused BN/pool
+kernels, and MIOpen's weight gradient.
 """
 from __future__ import annotations
 
@@ -123,6 +125,56 @@ class _StemFn(torch.autograd.Function):
         return dx, dw, dgamma, dbeta, None, None, None, None
 
 
+def stem_conv_stats_f32(x: torch.Tensor, weight: torch.Tensor, ws: torch.Tensor | None = None):
+    """fp32 conv7x7/2 of the image (read through its strides) with the BN partial sums
+    (csrc/hip/stem_f32.hip): returns (y [N,64,Ho,Wo] channels_last fp32, workspace, partial-row
+    count)."""
+    n, cin, hh, ww = x.shape
+    ho, wo = _out(hh), _out(ww)
+    h = N.hip()
+    nb = h.stem_partial_rows(n, ho)
+    y = torch.empty(n, COUT, ho, wo, dtype=torch.float32, device=x.device, memory_format=torch.channels_last)
+    need = max(2 * nb * COUT + 3 * COUT, h.bn_pool_workspace_floats(n, ho, COUT))
+    if ws is None or ws.numel() < need:
+        ws = torch.empty(need, dtype=torch.float32, device=x.device)
+    h.stem_conv_fwd_f32(x.data_ptr(), *x.stride(), cin, weight.data_ptr(), *weight.stride(), y.data_ptr(),
+                        ws.data_ptr(), nb, n, hh, ww, ho, wo, N.stream_of(x))
+    return y, ws, nb
+
+
+class _StemF32Fn(torch.autograd.Function):
+    """The reference-precision stem: own fp32 MFMA convolution with the BN statistics in its
+    epilogue (no zero-fill, no statistics pass), the fused BN + ReLU + max pool, and MIOpen's
+    weight gradient on the original image."""
+
+    @staticmethod
+    def forward(ctx, x, weight, gamma, beta, running_mean, running_var, momentum, eps):
+        yc, ws, nb = stem_conv_stats_f32(x, weight)
+        y, idx, save_mean, save_invstd = bn_pool_forward(yc, gamma, beta, running_mean, running_var, momentum, eps,
+                                                         3, 2, 1, ws=ws, pre_nb=nb)
+        ctx.bias = beta
+        ctx.save_for_backward(x, weight, yc, idx, gamma, save_mean, save_invstd)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, weight, yc, idx, gamma, save_mean, save_invstd = ctx.saved_tensors
+        need_g = gamma is not None and ctx.needs_input_grad[2]
+        dyc, dgamma, dbeta, _ = bn_pool_backward(dy, yc, idx, gamma, ctx.bias, save_mean, save_invstd, 3, 2, 1,
+                                                 need_g, ctx.needs_input_grad[3])
+        mask = [bool(ctx.needs_input_grad[0]), bool(ctx.needs_input_grad[1]), False]
+        dx = dw = None
+        if mask[0] or mask[1]:
+            dx, dw, _ = torch.ops.aten.convolution_backward(dyc, x, weight, None, [2, 2], [3, 3], [1, 1], False,
+                                                            [0, 0], 1, mask)
+            gw = flat_grad(weight) if (mask[1] and _direct(weight)) else None
+            if gw is not None:  # fold into the optimizer's flat gradient
+                gw.add_(dw.to(gw.dtype))
+                _ready(weight)
+                dw = None
+        return dx, dw, dgamma, dbeta, None, None, None, None
+
+
 class FusedStem(nn.Sequential):
     """``nn.Sequential(Conv2d(cin, 64, 7, 2, 3, bias=False), FusedBNReLUMaxPool2d(64))``
     whose training forward runs :class:`_StemFn`."""
@@ -143,7 +195,25 @@ class FusedStem(nn.Sequential):
                         for t in (bn.weight, bn.bias, bn.running_mean, bn.running_var))
                 and (x.dtype == torch.bfloat16 or torch.is_autocast_enabled("cuda")))
 
+    def _fast_f32_ok(self, x: torch.Tensor) -> bool:
+        """The reference-precision path (fp32 image and weights, no autocast)."""
+        conv, bn = self[0], self[1]
+        return (USE_STEM and self.training and x.is_cuda and x.dim() == 4 and 1 <= x.shape[1] <= 3
+                and x.dtype == torch.float32 and conv.weight.dtype == torch.float32
+                and not torch.is_autocast_enabled("cuda") and x.data_ptr() % 4 == 0
+                and conv.out_channels == COUT and conv.groups == 1 and conv.kernel_size == (7, 7)
+                and conv.stride == (2, 2) and conv.padding == (3, 3) and conv.dilation == (1, 1)
+                and conv.bias is None and 1 <= _out(x.shape[3]) <= 128 and min(x.stride()) >= 0
+                and bn.pool == (3, 2, 1) and bn.track_running_stats and bn.momentum is not None
+                and all(t is None or t.dtype == torch.float32
+                        for t in (bn.weight, bn.bias, bn.running_mean, bn.running_var)))
+
     def forward(self, x):
+        if self._fast_f32_ok(x):
+            bn = self[1]
+            bn._pending_batches = getattr(bn, "_pending_batches", 0) + 1
+            return _StemF32Fn.apply(x, self[0].weight, bn.weight, bn.bias, bn.running_mean, bn.running_var,
+                                    bn.momentum, bn.eps)
         if not self._fast_ok(x):
             return super().forward(x)
         bn = self[1]
