@@ -160,6 +160,11 @@ void stem_conv_wgrad(uintptr_t x4, uintptr_t dy, uintptr_t dw, int64_t s0, int64
 void stem_conv_fwd_f32(uintptr_t x, int64_t sN, int64_t sC, int64_t sH, int64_t sW, int Cin, uintptr_t w,
                        int64_t sw0, int64_t sw1, int64_t sw2, int64_t sw3, uintptr_t y, uintptr_t part, int nb, int N,
                        int H, int W, int Ho, int Wo, uintptr_t stream);
+int64_t stem_wgrad_f32_workspace_floats(int N, int Ho);
+bool stem_wgrad_f32_supported(int Wo);
+void stem_conv_wgrad_f32(uintptr_t x, int64_t sN, int64_t sC, int64_t sH, int64_t sW, int Cin, uintptr_t dy,
+                         uintptr_t dw, int64_t s0, int64_t s1, int64_t s2, int64_t s3, uintptr_t ws, int N, int H,
+                         int W, int Ho, int Wo, bool accumulate, uintptr_t stream);
 void stem_conv_fwd(uintptr_t x4, uintptr_t w, int64_t sw0, int64_t sw1, int64_t sw2, int64_t sw3, int Cin, int Cout,
                    uintptr_t y, uintptr_t part, int nb, int N, int H, int W, int Ho, int Wo, uintptr_t stream);
 

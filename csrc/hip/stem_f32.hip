@@ -34,6 +34,8 @@ namespace voda {
 namespace {
 
 typedef float sf_f32x16 __attribute__((ext_vector_type(16)));
+typedef float sf_f32x4 __attribute__((ext_vector_type(4)));  // native vector: HIP's float4 struct
+                                                             // arrays are copied through scratch
 
 constexpr int kFK = 7, kFS = 2, kFP = 3;           // filter, stride, padding
 constexpr int kFCo = 64;                           // output channels (two 32-wide MFMA tiles)
@@ -75,7 +77,8 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t sf_rsrc(const void* base, int6
 // byte offset of element j of the flat LDS row of input row hi (pixel wi = j / 3 - 3, channel
 // j % 3) in the image, or an offset past the buffer's bound (the load returns 0) outside the
 // image and for channels >= cin: branch-free, 32-bit
-__device__ __forceinline__ uint32_t sf_off(const StemF32Args& a, int64_t n, int hi, int j) {
+template <typename Args>
+__device__ __forceinline__ uint32_t sf_off(const Args& a, int64_t n, int hi, int j) {
   const int px = j / kFC, c = j - px * kFC;
   const int wi = px - kFP;
   const bool ok = unsigned(hi) < unsigned(a.H) && unsigned(wi) < unsigned(a.W) && c < a.cin;
@@ -89,10 +92,10 @@ __device__ __forceinline__ float sf_load(__amdgpu_buffer_rsrc_t rx, uint32_t off
 
 // the 7 input rows of output row ho into the ring, loads issued in batches of B before their
 // LDS writes
-template <int B>
-__device__ __forceinline__ void sf_fill_window(float* ring, const StemF32Args& a, __amdgpu_buffer_rsrc_t rx, int64_t n,
-                                               int ho, int tid) {
-  constexpr int kTotal = kFK * kFRowF;                          // 5544
+template <int B, int RF = kFRowF, typename Args>
+__device__ __forceinline__ void sf_fill_window(float* ring, const Args& a, __amdgpu_buffer_rsrc_t rx, int64_t n, int ho,
+                                               int tid) {
+  constexpr int kTotal = kFK * RF;                              // 5544 (forward rows)
   constexpr int kIters = (kTotal + kFThreads - 1) / kFThreads;  // 22
 #pragma unroll
   for (int b = 0; b < kIters; b += B) {
@@ -100,15 +103,15 @@ __device__ __forceinline__ void sf_fill_window(float* ring, const StemF32Args& a
 #pragma unroll
     for (int u = 0; u < B; ++u) {
       const int i = min(tid + (b + u) * kFThreads, kTotal - 1);
-      const int r = i / kFRowF, j = i - r * kFRowF;
+      const int r = i / RF, j = i - r * RF;
       v[u] = sf_load(rx, sf_off(a, n, kFS * ho - kFP + r, j));
     }
 #pragma unroll
     for (int u = 0; u < B; ++u) {
       const int i = tid + (b + u) * kFThreads;
       if (b + u < kIters && i < kTotal) {
-        const int r = i / kFRowF, j = i - r * kFRowF;
-        ring[((kFS * ho - kFP + r) & (kFSlots - 1)) * kFRowF + j] = v[u];
+        const int r = i / RF, j = i - r * RF;
+        ring[((kFS * ho - kFP + r) & (kFSlots - 1)) * RF + j] = v[u];
       }
     }
   }
@@ -287,7 +290,232 @@ __global__ __launch_bounds__(kFThreads, 2) void stem_f32_fwd_kernel(StemF32Args 
   }
 }
 
+// ---------------------------------------------------------------- weight gradient
+// dW[co][c][kh][kw] = sum over output pixels p of dY[p][co] * X[2 ho - 3 + kh][2 wo - 3 + kw][c]:
+// a GEMM whose reduction runs over the 3.2 M output pixels (bs 256) into a 64 x 147 result.
+// MIOpen's igemm_wrw for it: 948 us per fp32 ResNet-50 bs256 step (~64 TF) plus a zero-fill
+// (profiles/r5/rocprof_resnet50_fp32_tile_gemm_off.md).  Here D^T[k][co] with k = kh * 21 +
+// kw * 3 + c on the MFMA rows (147 -> 5 tiles of 32) and the 64 channels on the columns
+// (2 tiles), so the padding is 9 % (the pixel-major formulation would pad 147 -> 7 x 32):
+//  * per output row (same persistent row chunks and 16-slot input ring as the forward, rows of
+//    232 pixels: Wo <= 112), the dY row is staged as-is ([px][64] fp32) and the 7 input rows
+//    as flat [px][3] rows; a k-step reduces 2 pixels (the lane halves);
+//  * the A operand of lane (k, half h) at pixel pair p is ring[slot(kh)][k % 21 + 6 (p + h)]: one
+//    ds_read_b32 at a per-lane base plus a compile-time offset; B is dY[p + h][co], one
+//    ds_read_b32 (lanes read 32 consecutive channels);
+//  * waves = 2 channel tiles x 2 groups of k tiles (3 + 2 tiles; the groups swap in the second
+//    half of the grid, so co-resident workgroups tend to balance the SIMDs); one fp32 partial [147][64]
+//    per workgroup, summed by the slice / final kernels below.
+constexpr int kWMaxWo = 112;
+constexpr int kWRowPx = 2 * kWMaxWo + 8;                        // 232
+constexpr int kWRowF = kWRowPx * kFC;                           // 696 floats
+constexpr int kWK = kFK * kFK * kFC;                            // 147
+constexpr int kWPf = (2 * kWRowF + kFThreads - 1) / kFThreads;  // 6 ring floats per thread
+constexpr int kWDy4 = kWMaxWo * kFCo / 4 / kFThreads;           // 7 dY float4 per thread
+
+struct StemF32WArgs {
+  const float* x;
+  int64_t sN, sC, sH, sW;
+  int cin;
+  const float* dy;  // [N][Ho][Wo][64] fp32 (channels_last)
+  float* part;      // [gridDim.x][147][64]
+  int N, H, W, Ho, Wo;
+};
+
+// every wave runs the same code (barriers included); a wave of the 2-tile group skips its
+// third MFMA per k-step on a wave-uniform branch
+constexpr int NT = 3;
+__device__ __forceinline__ void sf_wgrad_rows(const StemF32WArgs& a, float* ring, float* dyl, int t0, int nt) {
+  const int tid = threadIdx.x;
+  const int lane = tid & 63, lc = lane & 31, lh = lane >> 5;
+  const int ct = (tid >> 6) & 1;
+  const auto rx = sf_rsrc(a.x, (int64_t(a.N - 1) * a.sN + int64_t(a.cin - 1) * a.sC + int64_t(a.H - 1) * a.sH +
+                                int64_t(a.W - 1) * a.sW + 1) * 4);
+  const int64_t rows = int64_t(a.N) * a.Ho;
+  const int64_t per = (rows + gridDim.x - 1) / gridDim.x;
+  const int64_t r0 = int64_t(blockIdx.x) * per;
+  const int64_t r1 = r0 + per < rows ? r0 + per : rows;
+  const int ndy4 = a.Wo * kFCo / 4;  // float4 of one dY row
+  // k rows of this lane in tile t0 + i (clamped: rows past 146 are computed, never stored)
+  int kh_[NT], kr_[NT];
+#pragma unroll
+  for (int i = 0; i < NT; ++i) {
+    const int kk = min(32 * (t0 + i) + lc, kWK - 1);
+    kh_[i] = kk / (kFK * kFC);
+    kr_[i] = kk - kh_[i] * (kFK * kFC) + 6 * lh;
+  }
+  const int boff = lh * kFCo + 32 * ct + lc;
+
+  sf_f32x16 acc[NT];
+#pragma unroll
+  for (int i = 0; i < NT; ++i) acc[i] = sf_f32x16{};
+
+  int64_t n = r0 / a.Ho;
+  int ho = int(r0 - n * a.Ho);
+  float pf[2][kWPf];
+  sf_f32x4 pd[2][kWDy4];
+  bool vv[2] = {false, false};
+  bool in_lds = false;
+  auto load_rows = [&](float (&dst)[kWPf], sf_f32x4 (&dd)[kWDy4], int hbase, int64_t drow)
+      __attribute__((always_inline)) {
+#pragma unroll
+    for (int k = 0; k < kWPf; ++k) {
+      const int i = min(tid + k * kFThreads, 2 * kWRowF - 1);
+      const int r = i / kWRowF;
+      dst[k] = sf_load(rx, sf_off(a, n, hbase + r, i - r * kWRowF));
+    }
+    const sf_f32x4* src = reinterpret_cast<const sf_f32x4*>(a.dy + drow * a.Wo * kFCo);
+#pragma unroll
+    for (int k = 0; k < kWDy4; ++k) dd[k] = src[min(tid + k * kFThreads, ndy4 - 1)];
+  };
+  auto step = [&](int64_t row, auto bc) __attribute__((always_inline)) {
+    constexpr int B = decltype(bc)::value, O = 1 - B;
+    if (!in_lds) {  // first row of a chunk / image: the 7 ring rows and the dY row
+      sf_fill_window<4, kWRowF>(ring, a, rx, n, ho, tid);
+      const float4* src = reinterpret_cast<const float4*>(a.dy + row * a.Wo * kFCo);
+      for (int i = tid; i < ndy4; i += kFThreads) reinterpret_cast<float4*>(dyl)[i] = src[i];
+    }
+    __syncthreads();
+    const bool nxt1 = row + 1 < r1 && ho + 1 < a.Ho;
+    const bool nxt2 = nxt1 && row + 2 < r1 && ho + 2 < a.Ho;
+    if (nxt1 && !vv[B]) {
+      load_rows(pf[B], pd[B], kFS * ho + 4, row + 1);
+      vv[B] = true;
+    }
+    vv[O] = nxt2;
+    if (nxt2) load_rows(pf[O], pd[O], kFS * ho + 6, row + 2);
+    int ao[NT];
+#pragma unroll
+    for (int i = 0; i < NT; ++i) ao[i] = ((kFS * ho - kFP + kh_[i]) & (kFSlots - 1)) * kWRowF + kr_[i];
+    // ---- k-steps over pixel pairs (p, p + 1); dY rows past Wo are zero
+    for (int p = 0; p < a.Wo; p += 8) {
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int pp = p + 2 * u;
+        const float b = dyl[boff + pp * kFCo];
+#pragma unroll
+        for (int i = 0; i < NT; ++i)
+          if (i < 2 || nt == 3) acc[i] = sf_mfma(ring[ao[i] + 6 * pp], b, acc[i]);
+      }
+    }
+    __syncthreads();  // every wave is done with this row's window and dY row
+    if (vv[B]) {
+#pragma unroll
+      for (int k = 0; k < kWPf; ++k) {
+        const int i = tid + k * kFThreads;
+        if (i < 2 * kWRowF) {
+          const int r = i / kWRowF;
+          ring[((kFS * ho + 4 + r) & (kFSlots - 1)) * kWRowF + i - r * kWRowF] = pf[B][k];
+        }
+      }
+#pragma unroll
+      for (int k = 0; k < kWDy4; ++k) {
+        const int i = tid + k * kFThreads;
+        if (i < ndy4) reinterpret_cast<sf_f32x4*>(dyl)[i] = pd[B][k];
+      }
+    }
+    in_lds = vv[B];
+    vv[B] = false;
+    if (++ho == a.Ho) {
+      ho = 0;
+      ++n;
+    }
+  };
+  for (int64_t row = r0; row < r1; row += 2) {
+    step(row, std::integral_constant<int, 0>{});
+    if (row + 1 < r1) step(row + 1, std::integral_constant<int, 1>{});
+  }
+  // ---- partial [147][64]: lane holds column co = 32 ct + lc of rows k = 32 (t0 + i) + crow
+  float* out = a.part + int64_t(blockIdx.x) * kWK * kFCo + 32 * ct + lc;
+#pragma unroll
+  for (int i = 0; i < NT; ++i)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int k = 32 * (t0 + i) + (r & 3) + 8 * (r >> 2) + 4 * lh;
+      if (i < nt && k < kWK) out[k * kFCo] = acc[i][r];
+    }
+}
+
+__global__ __launch_bounds__(kFThreads, 2) void stem_f32_wgrad_kernel(StemF32WArgs a) {
+  __shared__ __attribute__((aligned(16))) float ring[kFSlots * kWRowF];  // 44.5 KB
+  __shared__ __attribute__((aligned(16))) float dyl[(kWMaxWo + 1) * kFCo];  // 29 KB (+ a zero row)
+  // pixel rows Wo .. 112 of the dY tile stay zero (an odd Wo pairs its last pixel with row Wo)
+  for (int i = threadIdx.x; i < (kWMaxWo + 1 - a.Wo) * kFCo; i += kFThreads) dyl[a.Wo * kFCo + i] = 0.f;
+  // wave-uniform: waves 0, 1 take k tiles 0-2 and waves 2, 3 tiles 3-4, swapped in the second
+  // half of the grid
+  const int grp = __builtin_amdgcn_readfirstlane(((threadIdx.x >> 7) & 1) ^ (blockIdx.x >= gridDim.x / 2 ? 1 : 0));
+  sf_wgrad_rows(a, ring, dyl, grp == 0 ? 0 : 3, grp == 0 ? 3 : 2);
+}
+
+// partials [nb][147][64] -> [nsl][147][64] (each slice sums <= ceil(nb / nsl) rows)
+__global__ __launch_bounds__(256) void stem_f32_wgrad_slice_kernel(const float4* __restrict__ part, int nb,
+                                                                   float4* __restrict__ tmp) {
+  constexpr int e4n = kWK * kFCo / 4;
+  const int e = blockIdx.x * 256 + threadIdx.x;
+  if (e >= e4n) return;
+  const int sl = blockIdx.y, nsl = gridDim.y;
+  const int per = (nb + nsl - 1) / nsl;
+  const int b0 = sl * per, b1 = min(nb, b0 + per);
+  float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
+  for (int b = b0; b < b1; ++b) {
+    const float4 v = part[int64_t(b) * e4n + e];
+    s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
+  }
+  tmp[int64_t(sl) * e4n + e] = s;
+}
+
+// [nsl][147][64] -> dW[co][c][kh][kw] (element strides) (+)=, one thread per (k, co)
+__global__ __launch_bounds__(256) void stem_f32_wgrad_final_kernel(const float* __restrict__ tmp, int nsl, int cin,
+                                                                   float* __restrict__ dw, int64_t s0, int64_t s1,
+                                                                   int64_t s2, int64_t s3, int accumulate) {
+  const int i = blockIdx.x * 256 + threadIdx.x;  // k * 64 + co
+  if (i >= kWK * kFCo) return;
+  const int k = i / kFCo, co = i - k * kFCo;
+  const int kh = k / (kFK * kFC), r = k - kh * (kFK * kFC);
+  const int kw = r / kFC, c = r - kw * kFC;
+  if (c >= cin) return;
+  float v = 0.f;
+  for (int sl = 0; sl < nsl; ++sl) v += tmp[int64_t(sl) * kWK * kFCo + i];
+  float* o = dw + co * s0 + c * s1 + kh * s2 + kw * s3;
+  *o = v + (accumulate ? *o : 0.f);
+}
+
 }  // namespace
+
+constexpr int kWMaxSlicesF32 = 64;
+
+int64_t stem_wgrad_f32_workspace_floats(int N, int Ho) {
+  return int64_t(stem_partial_rows(N, Ho) + kWMaxSlicesF32) * kWK * kFCo;
+}
+
+bool stem_wgrad_f32_supported(int Wo) { return Wo >= 1 && Wo <= kWMaxWo; }
+
+void stem_conv_wgrad_f32(uintptr_t x, int64_t sN, int64_t sC, int64_t sH, int64_t sW, int Cin, uintptr_t dy,
+                         uintptr_t dw, int64_t s0, int64_t s1, int64_t s2, int64_t s3, uintptr_t ws, int N, int H,
+                         int W, int Ho, int Wo, bool accumulate, uintptr_t stream) {
+  VODA_CHECK(Cin >= 1 && Cin <= kFC, "stem_wgrad_f32: 1..3 input channels");
+  VODA_CHECK(Ho == (H + 2 * kFP - kFK) / kFS + 1 && Wo == (W + 2 * kFP - kFK) / kFS + 1,
+             "stem_wgrad_f32: output size mismatch (7x7, stride 2, pad 3)");
+  VODA_CHECK(stem_wgrad_f32_supported(Wo), "stem_wgrad_f32: output width must be <= 112");
+  VODA_CHECK(x % 4 == 0 && dy % 16 == 0 && dw % 4 == 0 && ws % 16 == 0, "stem_wgrad_f32: misaligned operands");
+  VODA_CHECK(sN >= 0 && sC >= 0 && sH >= 0 && sW >= 0 &&
+                 (int64_t(N - 1) * sN + int64_t(Cin - 1) * sC + int64_t(H - 1) * sH + int64_t(W - 1) * sW + 1) * 4 <
+                     (int64_t(1) << 31),
+             "stem_wgrad_f32: image must span < 2 GB (32-bit buffer offsets)");
+  hipStream_t s = as_stream(stream);
+  const int nb = stem_partial_rows(N, Ho);
+  float* part = reinterpret_cast<float*>(ws);
+  float* tmp = part + int64_t(nb) * kWK * kFCo;
+  const int nsl = std::min(kWMaxSlicesF32, nb);
+  StemF32WArgs a{reinterpret_cast<const float*>(x), sN, sC, sH, sW, Cin, reinterpret_cast<const float*>(dy), part,
+                 N, H, W, Ho, Wo};
+  hipLaunchKernelGGL(stem_f32_wgrad_kernel, dim3(nb), dim3(kFThreads), 0, s, a);
+  hipLaunchKernelGGL(stem_f32_wgrad_slice_kernel, dim3((kWK * kFCo / 4 + 255) / 256, nsl), dim3(256), 0, s,
+                     reinterpret_cast<const float4*>(part), nb, reinterpret_cast<float4*>(tmp));
+  hipLaunchKernelGGL(stem_f32_wgrad_final_kernel, dim3((kWK * kFCo + 255) / 256), dim3(256), 0, s, tmp, nsl, Cin,
+                     reinterpret_cast<float*>(dw), s0, s1, s2, s3, int(accumulate));
+  check_launch();
+}
 
 void stem_conv_fwd_f32(uintptr_t x, int64_t sN, int64_t sC, int64_t sH, int64_t sW, int Cin, uintptr_t w,
                        int64_t sw0, int64_t sw1, int64_t sw2, int64_t sw3, uintptr_t y, uintptr_t part, int nb, int N,

@@ -246,3 +246,29 @@ def test_resnet50_fp32_uses_fused_stem_f32():
     m = resnet50().cuda().to(memory_format=torch.channels_last)
     x = _img(2, 224, 224, cl=True)
     assert m.stem._fast_f32_ok(x) and not m.stem._fast_ok(x)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n,h,w,cl,acc", [(2, 224, 224, True, False), (3, 97, 61, False, True),
+                                          (1, 30, 223, True, False), (4, 9, 1, False, False)])
+def test_stem_wgrad_f32_vs_fp64(n, h, w, cl, acc):
+    """Own fp32 filter gradient (pixel reduction on the f32 MFMA) against fp64, any image
+    strides, odd / ragged output widths, (+)= into an existing gradient."""
+    torch.manual_seed(5)
+    x = _img(n, h, w, cl=cl, seed=5)
+    ho, wo = S._out(h), S._out(w)
+    dy = torch.randn(n, 64, ho, wo, device="cuda").contiguous(memory_format=torch.channels_last)
+    wt = torch.randn(64, 3, 7, 7, device="cuda")
+    from vodascheduler_amd.ops import _native as N
+
+    hh = N.hip()
+    ws = torch.empty(hh.stem_wgrad_f32_workspace_floats(n, ho), device="cuda")
+    base = torch.randn_like(wt) if acc else torch.zeros_like(wt)
+    out = base.clone()
+    hh.stem_conv_wgrad_f32(x.data_ptr(), *x.stride(), 3, dy.data_ptr(), out.data_ptr(), *out.stride(),
+                           ws.data_ptr(), n, h, w, ho, wo, acc, N.stream_of(x))
+    torch.cuda.synchronize()
+    ref = torch.nn.grad.conv2d_weight(x.double(), wt.shape, dy.double(), stride=2, padding=3)
+    if acc:
+        ref = ref + base.double()
+    torch.testing.assert_close(out.double(), ref, rtol=1e-5, atol=1e-5 * ref.abs().max().item())

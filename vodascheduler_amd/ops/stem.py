@@ -142,10 +142,29 @@ def stem_conv_stats_f32(x: torch.Tensor, weight: torch.Tensor, ws: torch.Tensor 
     return y, ws, nb
 
 
+def stem_wgrad_f32(x: torch.Tensor, dyc: torch.Tensor, weight: torch.Tensor) -> torch.Tensor | None:
+    """fp32 filter gradient of the stem conv on the own MFMA kernel (csrc/hip/stem_f32.hip):
+    accumulated into the optimizer's flat gradient when it owns one (returns None), else
+    returned."""
+    n, cin, hh, ww = x.shape
+    ho, wo = dyc.shape[2], dyc.shape[3]
+    h = N.hip()
+    ws = torch.empty(h.stem_wgrad_f32_workspace_floats(n, ho), dtype=torch.float32, device=x.device)
+    gw = flat_grad(weight) if _direct(weight) else None
+    direct = gw is not None and gw.dtype == torch.float32
+    out = gw if direct else torch.empty(weight.shape, dtype=torch.float32, device=weight.device)
+    h.stem_conv_wgrad_f32(x.data_ptr(), *x.stride(), cin, dyc.data_ptr(), out.data_ptr(), *out.stride(),
+                          ws.data_ptr(), n, hh, ww, ho, wo, direct, N.stream_of(x))
+    if direct:
+        _ready(weight)
+        return None
+    return out
+
+
 class _StemF32Fn(torch.autograd.Function):
     """The reference-precision stem: own fp32 MFMA convolution with the BN statistics in its
-    epilogue (no zero-fill, no statistics pass), the fused BN + ReLU + max pool, and MIOpen's
-    weight gradient on the original image."""
+    epilogue (no zero-fill, no statistics pass), the fused BN + ReLU + max pool, and the own
+    fp32 MFMA weight gradient (MIOpen's for output widths > 112)."""
 
     @staticmethod
     def forward(ctx, x, weight, gamma, beta, running_mean, running_var, momentum, eps):
@@ -164,6 +183,10 @@ class _StemF32Fn(torch.autograd.Function):
                                                  need_g, ctx.needs_input_grad[3])
         mask = [bool(ctx.needs_input_grad[0]), bool(ctx.needs_input_grad[1]), False]
         dx = dw = None
+        if (mask[1] and USE_STEM_WGRAD and dyc.is_contiguous(memory_format=torch.channels_last)
+                and N.hip().stem_wgrad_f32_supported(dyc.shape[3])):
+            dw = stem_wgrad_f32(x, dyc, weight)
+            mask[1] = False
         if mask[0] or mask[1]:
             dx, dw, _ = torch.ops.aten.convolution_backward(dyc, x, weight, None, [2, 2], [3, 3], [1, 1], False,
                                                             [0, 0], 1, mask)
