@@ -303,9 +303,9 @@ __global__ __launch_bounds__(kFThreads, 2) void stem_f32_fwd_kernel(StemF32Args 
 //  * the A operand of lane (k, half h) at pixel pair p is ring[slot(kh)][k % 21 + 6 (p + h)]: one
 //    ds_read_b32 at a per-lane base plus a compile-time offset; B is dY[p + h][co], one
 //    ds_read_b32 (lanes read 32 consecutive channels);
-//  * waves = 2 channel tiles x 2 groups of k tiles (3 + 2 tiles; the groups swap in the second
-//    half of the grid, so co-resident workgroups tend to balance the SIMDs); one fp32 partial [147][64]
-//    per workgroup, summed by the slice / final kernels below.
+//  * waves = 2 channel tiles x 2 pixel halves (alternate pixel pairs), all 5 k tiles each (80
+//    accumulators): every SIMD does the same work (a 3 + 2 split of the k tiles ran 707 us);
+//    one fp32 partial [147][64] per wave pair, summed by the slice / final kernels below.
 constexpr int kWMaxWo = 112;
 constexpr int kWRowPx = 2 * kWMaxWo + 8;                        // 232
 constexpr int kWRowF = kWRowPx * kFC;                           // 696 floats
@@ -322,10 +322,11 @@ struct StemF32WArgs {
   int N, H, W, Ho, Wo;
 };
 
-// every wave runs the same code (barriers included); a wave of the 2-tile group skips its
-// third MFMA per k-step on a wave-uniform branch
-constexpr int NT = 3;
-__device__ __forceinline__ void sf_wgrad_rows(const StemF32WArgs& a, float* ring, float* dyl, int t0, int nt) {
+// wave (ct, ph): channel tile ct, all 5 k tiles, the pixel pairs p = 4 j + 2 ph of every row
+constexpr int NT = 5;
+__device__ __forceinline__ void sf_wgrad_rows(const StemF32WArgs& a, float* ring, float* dyl) {
+  constexpr int t0 = 0;
+  const int ph = threadIdx.x >> 7;
   const int tid = threadIdx.x;
   const int lane = tid & 63, lc = lane & 31, lh = lane >> 5;
   const int ct = (tid >> 6) & 1;
@@ -388,14 +389,13 @@ __device__ __forceinline__ void sf_wgrad_rows(const StemF32WArgs& a, float* ring
 #pragma unroll
     for (int i = 0; i < NT; ++i) ao[i] = ((kFS * ho - kFP + kh_[i]) & (kFSlots - 1)) * kWRowF + kr_[i];
     // ---- k-steps over pixel pairs (p, p + 1); dY rows past Wo are zero
-    for (int p = 0; p < a.Wo; p += 8) {
+    for (int p = 2 * ph; p < a.Wo; p += 16) {
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
-        const int pp = p + 2 * u;
+        const int pp = p + 4 * u;
         const float b = dyl[boff + pp * kFCo];
 #pragma unroll
-        for (int i = 0; i < NT; ++i)
-          if (i < 2 || nt == 3) acc[i] = sf_mfma(ring[ao[i] + 6 * pp], b, acc[i]);
+        for (int i = 0; i < NT; ++i) acc[i] = sf_mfma(ring[ao[i] + 6 * pp], b, acc[i]);
       }
     }
     __syncthreads();  // every wave is done with this row's window and dY row
@@ -425,26 +425,25 @@ __device__ __forceinline__ void sf_wgrad_rows(const StemF32WArgs& a, float* ring
     step(row, std::integral_constant<int, 0>{});
     if (row + 1 < r1) step(row + 1, std::integral_constant<int, 1>{});
   }
-  // ---- partial [147][64]: lane holds column co = 32 ct + lc of rows k = 32 (t0 + i) + crow
-  float* out = a.part + int64_t(blockIdx.x) * kWK * kFCo + 32 * ct + lc;
+  // ---- partial [147][64] of pixel half ph: lane holds column co = 32 ct + lc of rows
+  // k = 32 i + crow
+  float* out = a.part + (2 * int64_t(blockIdx.x) + ph) * kWK * kFCo + 32 * ct + lc;
 #pragma unroll
   for (int i = 0; i < NT; ++i)
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
       const int k = 32 * (t0 + i) + (r & 3) + 8 * (r >> 2) + 4 * lh;
-      if (i < nt && k < kWK) out[k * kFCo] = acc[i][r];
+      if (k < kWK) out[k * kFCo] = acc[i][r];
     }
 }
 
 __global__ __launch_bounds__(kFThreads, 2) void stem_f32_wgrad_kernel(StemF32WArgs a) {
   __shared__ __attribute__((aligned(16))) float ring[kFSlots * kWRowF];  // 44.5 KB
-  __shared__ __attribute__((aligned(16))) float dyl[(kWMaxWo + 1) * kFCo];  // 29 KB (+ a zero row)
-  // pixel rows Wo .. 112 of the dY tile stay zero (an odd Wo pairs its last pixel with row Wo)
-  for (int i = threadIdx.x; i < (kWMaxWo + 1 - a.Wo) * kFCo; i += kFThreads) dyl[a.Wo * kFCo + i] = 0.f;
-  // wave-uniform: waves 0, 1 take k tiles 0-2 and waves 2, 3 tiles 3-4, swapped in the second
-  // half of the grid
-  const int grp = __builtin_amdgcn_readfirstlane(((threadIdx.x >> 7) & 1) ^ (blockIdx.x >= gridDim.x / 2 ? 1 : 0));
-  sf_wgrad_rows(a, ring, dyl, grp == 0 ? 0 : 3, grp == 0 ? 3 : 2);
+  __shared__ __attribute__((aligned(16))) float dyl[kWMaxWo * kFCo];  // 28.7 KB
+  // pixel rows Wo .. 111 of the dY tile stay zero (the last 16-pixel block of a row reads past Wo;
+  // with p = 2 ph + 16 j < Wo <= 112, no pair starts past pixel 110)
+  for (int i = threadIdx.x; i < (kWMaxWo - a.Wo) * kFCo; i += kFThreads) dyl[a.Wo * kFCo + i] = 0.f;
+  sf_wgrad_rows(a, ring, dyl);
 }
 
 // partials [nb][147][64] -> [nsl][147][64] (each slice sums <= ceil(nb / nsl) rows)
@@ -485,7 +484,7 @@ __global__ __launch_bounds__(256) void stem_f32_wgrad_final_kernel(const float* 
 constexpr int kWMaxSlicesF32 = 64;
 
 int64_t stem_wgrad_f32_workspace_floats(int N, int Ho) {
-  return int64_t(stem_partial_rows(N, Ho) + kWMaxSlicesF32) * kWK * kFCo;
+  return int64_t(2 * stem_partial_rows(N, Ho) + kWMaxSlicesF32) * kWK * kFCo;
 }
 
 bool stem_wgrad_f32_supported(int Wo) { return Wo >= 1 && Wo <= kWMaxWo; }
@@ -505,13 +504,13 @@ void stem_conv_wgrad_f32(uintptr_t x, int64_t sN, int64_t sC, int64_t sH, int64_
   hipStream_t s = as_stream(stream);
   const int nb = stem_partial_rows(N, Ho);
   float* part = reinterpret_cast<float*>(ws);
-  float* tmp = part + int64_t(nb) * kWK * kFCo;
-  const int nsl = std::min(kWMaxSlicesF32, nb);
+  float* tmp = part + int64_t(2 * nb) * kWK * kFCo;  // partials: [nb][2 pixel halves][147][64]
+  const int nsl = std::min(kWMaxSlicesF32, 2 * nb);
   StemF32WArgs a{reinterpret_cast<const float*>(x), sN, sC, sH, sW, Cin, reinterpret_cast<const float*>(dy), part,
                  N, H, W, Ho, Wo};
   hipLaunchKernelGGL(stem_f32_wgrad_kernel, dim3(nb), dim3(kFThreads), 0, s, a);
   hipLaunchKernelGGL(stem_f32_wgrad_slice_kernel, dim3((kWK * kFCo / 4 + 255) / 256, nsl), dim3(256), 0, s,
-                     reinterpret_cast<const float4*>(part), nb, reinterpret_cast<float4*>(tmp));
+                     reinterpret_cast<const float4*>(part), 2 * nb, reinterpret_cast<float4*>(tmp));
   hipLaunchKernelGGL(stem_f32_wgrad_final_kernel, dim3((kWK * kFCo + 255) / 256), dim3(256), 0, s, tmp, nsl, Cin,
                      reinterpret_cast<float*>(dw), s0, s1, s2, s3, int(accumulate));
   check_launch();
