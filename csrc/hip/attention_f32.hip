@@ -465,6 +465,164 @@ __global__ __launch_bounds__(64 * W, (D < 64 || (D == 64 && W != 2)) ? 2 : 1) vo
   }
 }
 
+// ======================================================================== fused backward, T <= 128
+// BERT-base's shape (self-attention, Tq = Tk <= 128, D = 64): one workgroup per (batch, head)
+// computes dK, dV AND dQ, instead of the dQ pass and the dK/dV pass above, which both recompute
+// S = Q K^T and dP = dO V^T (7 T x T x D products per (batch, head); here 5):
+//   phase 0  Q and dO rows of the whole head in LDS, delta = rowsum(dO o O), lse;
+//   phase 1  lane = key (wave w: keys 32 w ..): per 32-query tile S, dP from the LDS rows,
+//            P and dS in registers, dV += dO^T P, dK += Q^T dS (as attn_f32_bwd_dkv), and dS
+//            stored into an LDS image [query][key] (pitch 132: conflict-free row writes by
+//            consecutive keys, 16-byte aligned reads);
+//   phase 2  lane = query (wave w: queries 32 w ..): K staged transposed (Kt [d][key], pitch
+//            132, in the Q rows' LDS) and dQ^T[d][q] = K^T[d][k] dS^T[k][q] with the permuted
+//            key order of conv1x1_f32.hip (key 8 j + 4 h + s for MFMA s): one 16-byte read of
+//            each operand feeds four MFMAs.
+// LDS: Q 33.8 KB + dO 33.8 KB + dS 67.6 KB + lse / delta = 136 KB (one workgroup per CU).
+constexpr int kFbT = 128, kFbP = 132;
+
+template <int D>
+__global__ __launch_bounds__(256, 1) void attn_f32_bwd_fused_t128(AttnArgsF a) {
+  constexpr int RS = D + 2, DT = D / 32;
+  static_assert(D == 64, "fused backward: head dim 64");
+  static_assert(kFbT * RS >= D * kFbP, "Kt must fit in the Q rows' LDS");
+  __shared__ __attribute__((aligned(16))) float Qs[kFbT * RS];
+  __shared__ __attribute__((aligned(16))) float Ds[kFbT * RS];
+  __shared__ __attribute__((aligned(16))) float dSs[kFbT * kFbP];
+  __shared__ __attribute__((aligned(16))) float lse_s[kFbT];
+  __shared__ __attribute__((aligned(16))) float del_s[kFbT];
+  const int T = a.Tq;  // == Tk
+  const int bh = blockIdx.y, b = bh / a.H, hh = bh % a.H;
+  const int lane = threadIdx.x & 63, r = lane & 31, h = lane >> 5, w = threadIdx.x >> 6;
+  const float* qb = a.q + b * a.q_sb + hh * a.q_sh;
+  const float* db = a.dout + b * a.do_sb + hh * a.do_sh;
+  const float* kb = a.k + b * a.k_sb + hh * a.k_sh;
+
+  // ---- phase 0: Q, dO rows (rows >= T zero), lse (+inf past T: P = 0), delta
+#pragma unroll
+  for (int t0 = 0; t0 < kFbT; t0 += kT) {
+    stage<D, RS>(qb, a.q_st, t0, T, Qs + t0 * RS);
+    stage<D, RS>(db, a.do_st, t0, T, Ds + t0 * RS);
+  }
+  for (int i = threadIdx.x; i < kFbT; i += blockDim.x)
+    lse_s[i] = i < T ? a.lse[int64_t(bh) * T + i] : __builtin_huge_valf();
+  __syncthreads();
+  {
+    const int q = 32 * w + r;
+    float dpart = 0.f;
+    if (q < T) {
+      const float* orow = a.o + b * a.o_sb + hh * a.o_sh + int64_t(q) * a.o_st + 2 * h;
+#pragma unroll
+      for (int t = 0; t < D / 4; ++t) {
+        const float2 ov = *reinterpret_cast<const float2*>(orow + 4 * t);
+        const float2 dv = *reinterpret_cast<const float2*>(Ds + q * RS + 2 * h + 4 * t);
+        dpart += dv.x * ov.x + dv.y * ov.y;
+      }
+    }
+    const float delta = dpart + __shfl_xor(dpart, 32, 64);
+    if (h == 0) del_s[q] = delta;  // rows >= T: 0
+  }
+  __syncthreads();
+
+  // ---- phase 1: lane = key
+  {
+    const int key = 32 * w + r;
+    const bool kv = key < T;
+    const int kc = min(key, T - 1);
+    RowFrag<D, true> kf, vf;
+    kf.init(kb + int64_t(kc) * a.k_st, kv, h);
+    vf.init(a.v + b * a.v_sb + hh * a.v_sh + int64_t(kc) * a.v_st, kv, h);
+    const uint8_t* mrow = a.mask != nullptr ? a.mask + b * a.mask_sb : nullptr;
+    const bool kmasked = kv && mrow != nullptr && mrow[key] == 0;
+    f32x16 dk[DT], dv[DT];
+#pragma unroll
+    for (int t = 0; t < DT; ++t) {
+      dk[t] = zero16();
+      dv[t] = zero16();
+    }
+    for (int qt = 0; qt < T; qt += kT) {
+      const float* qt_rows = Qs + qt * RS;
+      const float* dt_rows = Ds + qt * RS;
+      f32x16 s = zero16(), dp = zero16();
+      dot_hd<D, RS, true>(s, qt_rows + r * RS + 2 * h, kf);   // S[query r][key]: lane = key
+      dot_hd<D, RS, true>(dp, dt_rows + r * RS + 2 * h, vf);  // dP = dO V^T
+      float ls[16], ds[16];
+      rows16(lse_s + qt, h, ls);
+      rows16(del_s + qt, h, ds);
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const int ql = crow(i, h);
+        float add = 0.f;
+        if (!kv) add = kNegInf;
+        else if (kmasked || (a.causal && key > qt + ql)) add = kMaskNeg;
+        const float p = __expf(s[i] * a.scale + add - ls[i]);
+        s[i] = p;
+        dp[i] = p * (dp[i] - ds[i]);  // dS
+        dSs[(qt + ql) * kFbP + key] = dp[i];
+      }
+      // dV^T[d][key] += dO^T[d][q] P[q][key];  dK^T[d][key] += Q^T[d][q] dS[q][key]
+#pragma unroll
+      for (int t = 0; t < DT; ++t) {
+        float dc[16], qc[16];
+        col16(dt_rows, RS, 32 * t + r, h, dc);
+        col16(qt_rows, RS, 32 * t + r, h, qc);
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          dv[t] = mfma(dc[i], s[i], dv[t]);
+          dk[t] = mfma(qc[i], dp[i], dk[t]);
+        }
+      }
+    }
+    float* dkb = a.dk + b * a.dk_sb + hh * a.dk_sh;
+    float* dvb = a.dv + b * a.dv_sb + hh * a.dv_sh;
+#pragma unroll
+    for (int t = 0; t < DT; ++t) {
+      store_row(dkb, a.dk_st, key, T, 32 * t, dk[t], a.scale, h);
+      store_row(dvb, a.dv_st, key, T, 32 * t, dv[t], 1.f, h);
+    }
+  }
+  // dS rows / columns past T: keys >= T got P = 0 above, queries >= T have lse = +inf; rows of
+  // the image past T were never written -- zero them for the phase-2 reads
+  for (int i = threadIdx.x; i < (kFbT - T) * kFbP; i += blockDim.x) dSs[T * kFbP + i] = 0.f;
+  __syncthreads();  // phase 1 done: Q rows free, dS complete
+
+  // ---- phase 2: Kt[d][key] in the Q rows' LDS; lane = query
+  float* Kt = Qs;
+  for (int i = threadIdx.x; i < kFbT * (D / 4); i += blockDim.x) {
+    const int key = i % kFbT, c4 = i / kFbT;
+    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (key < T) v = *reinterpret_cast<const float4*>(kb + int64_t(key) * a.k_st + 4 * c4);
+    Kt[(4 * c4 + 0) * kFbP + key] = v.x;
+    Kt[(4 * c4 + 1) * kFbP + key] = v.y;
+    Kt[(4 * c4 + 2) * kFbP + key] = v.z;
+    Kt[(4 * c4 + 3) * kFbP + key] = v.w;
+  }
+  __syncthreads();
+  {
+    const int q = 32 * w + r;
+    f32x16 dq[DT];
+#pragma unroll
+    for (int t = 0; t < DT; ++t) dq[t] = zero16();
+    const float* brow = dSs + q * kFbP + 4 * h;
+#pragma unroll 4
+    for (int j = 0; j < kFbT / 8; ++j) {
+      const float4 bv = *reinterpret_cast<const float4*>(brow + 8 * j);
+#pragma unroll
+      for (int t = 0; t < DT; ++t) {
+        const float4 av = *reinterpret_cast<const float4*>(Kt + (32 * t + r) * kFbP + 8 * j + 4 * h);
+        dq[t] = mfma(av.x, bv.x, dq[t]);
+        dq[t] = mfma(av.y, bv.y, dq[t]);
+        dq[t] = mfma(av.z, bv.z, dq[t]);
+        dq[t] = mfma(av.w, bv.w, dq[t]);
+      }
+    }
+    float* base = a.out + b * a.out_sb + hh * a.out_sh;
+#pragma unroll
+    for (int t = 0; t < DT; ++t) store_row(base, a.out_st, q, T, 32 * t, dq[t], a.scale, h);
+  }
+}
+
 template <typename F>
 void dispatch_d32(int D, F&& f) {
   if (D == 32) f(std::integral_constant<int, 32>{});
@@ -505,6 +663,12 @@ AttnArgsF make_args_f(const std::vector<int64_t>& t, int B, int H, int Tq, int T
   return a;
 }
 
+bool g_fused_bwd_f32 = true;  // attn_f32_set_fused_bwd: tests reach the two-pass backward
+
+bool attn_f32_fused_bwd_ok(int D, int Tq, int Tk) {
+  return g_fused_bwd_f32 && D == 64 && Tq == Tk && Tq >= 1 && Tq <= kFbT;
+}
+
 bool f32_shape_ok(int D, int Tq, int Tk) {
   return (D == 32 || D == 64 || D == 128 || D == 256) && Tq >= 1 && Tk >= 1 && Tq <= kMaxT32 && Tk <= kMaxT32;
 }
@@ -527,6 +691,9 @@ void attention_fwd_f32(const std::vector<int64_t>& t, int B, int H, int Tq, int 
   check_launch();
 }
 
+// the fused T <= 128 backward (default on); false: the dQ + dK/dV passes (A/B and tests)
+void attn_f32_set_fused_bwd(bool on) { g_fused_bwd_f32 = on; }
+
 void attention_bwd_f32(const std::vector<int64_t>& t, int B, int H, int Tq, int Tk, int D, float scale, bool causal,
                        uintptr_t stream) {
   VODA_CHECK(t.size() == 36, "attention_bwd_f32: bad argument vector");
@@ -534,6 +701,11 @@ void attention_bwd_f32(const std::vector<int64_t>& t, int B, int H, int Tq, int 
   VODA_CHECK(int64_t(B) * H <= 65535, "attention_bwd_f32: B*H exceeds the grid's y dimension");
   const AttnArgsF a = make_args_f(t, B, H, Tq, Tk, scale, causal);
   hipStream_t s = as_stream(stream);
+  if (attn_f32_fused_bwd_ok(D, Tq, Tk)) {
+    hipLaunchKernelGGL((attn_f32_bwd_fused_t128<64>), dim3(1, unsigned(B * H)), dim3(256), 0, s, a);
+    check_launch();
+    return;
+  }
   dispatch_d32(D, [&](auto dc) {
     constexpr int DD = decltype(dc)::value;
     dispatch_w32(Tq, [&](auto wc) {

@@ -57,6 +57,7 @@ PYBIND11_MODULE(_vodahip, m) {
   m.def("gemm_f32_stats_supported", &gemm_f32_stats_supported);
   m.def("gemm_f32_dgrad_bn", &gemm_f32_dgrad_bn);
   m.def("stem_conv_fwd_f32", &stem_conv_fwd_f32);
+  m.def("attn_f32_set_fused_bwd", &attn_f32_set_fused_bwd);
   m.def("stem_wgrad_f32_workspace_floats", &stem_wgrad_f32_workspace_floats);
   m.def("stem_wgrad_f32_supported", &stem_wgrad_f32_supported);
   m.def("stem_conv_wgrad_f32", &stem_conv_wgrad_f32);

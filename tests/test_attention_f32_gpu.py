@@ -134,3 +134,36 @@ def test_bert_fp32_layer_runs_fp32_kernel(monkeypatch):
     loss.backward()
     assert calls["fwd"] == 2 and calls["bwd"] == 2, calls
     assert all(p.grad is None or torch.isfinite(p.grad).all() for p in m.parameters())
+
+
+@pytest.mark.parametrize("B,H,T", [(4, 12, 128), (3, 4, 77), (2, 3, 20), (2, 2, 1), (5, 2, 33)])
+@pytest.mark.parametrize("causal", [False, True])
+@pytest.mark.parametrize("masked", [False, True])
+def test_f32_fused_backward_t128_vs_two_pass_and_fp64(B, H, T, causal, masked):
+    """The one-workgroup-per-head fp32 backward (D = 64, T <= 128: dK, dV and dQ from one dS
+    image) against fp64 and against the dQ + dK/dV passes it replaces; NaN-filled gradient
+    buffer, so every element it owns must be written."""
+    h = _native.hip()
+    torch.manual_seed(7)
+    D = 64
+    qkv = torch.randn(B, T, 3, H, D, device="cuda")
+    km = _mask(B, T, "cuda") if masked else None
+    scale = D ** -0.5
+    do = torch.randn(B, T, H, D, device="cuda")
+    grads = []
+    try:
+        for fused in (True, False):
+            h.attn_f32_set_fused_bwd(fused)
+            x = qkv.clone().requires_grad_()
+            o = attention_qkvpacked(x, km, causal, scale)
+            o.backward(do)
+            grads.append(x.grad)
+    finally:
+        h.attn_f32_set_fused_bwd(True)
+    xd = qkv.double().requires_grad_()
+    q, k, v = (xd[:, :, i].transpose(1, 2) for i in range(3))
+    ref = ref_attn(q, k, v, km, causal, scale).transpose(1, 2)
+    ref.backward(do.double())
+    assert torch.isfinite(grads[0]).all()
+    torch.testing.assert_close(grads[0].double(), xd.grad, **TOL)
+    torch.testing.assert_close(grads[0], grads[1], atol=2e-5, rtol=2e-4)
