@@ -164,7 +164,7 @@ struct RowFrag {
 
 // acc += A_lds(row r) . frag over the head dim: ``lds_row`` = row r of a row-major LDS tile
 // [kT][RS], already offset by the lane half's 2h (k-step s reads d = 4 (s>>1) + 2h + (s&1))
-template <int D, int RS, bool REG>
+template <int D, int RS, bool REG, bool SB = true>
 __device__ __forceinline__ void dot_hd(f32x16& acc, const float* lds_row, const RowFrag<D, REG>& fr) {
   // LDS operand of step t + 1 read while the two MFMAs of step t issue (the scheduler would
   // otherwise put a wait on each read right before its MFMAs)
@@ -174,10 +174,10 @@ __device__ __forceinline__ void dot_hd(f32x16& acc, const float* lds_row, const 
     float2 xn = x;
     if (t + 1 < D / 4) xn = *reinterpret_cast<const float2*>(lds_row + 4 * (t + 1));
     const float2 y = fr.get(t);
-    __builtin_amdgcn_sched_barrier(0);
+    if constexpr (SB) __builtin_amdgcn_sched_barrier(0);
     acc = mfma(x.x, y.x, acc);
     acc = mfma(x.y, y.y, acc);
-    __builtin_amdgcn_sched_barrier(0);
+    if constexpr (SB) __builtin_amdgcn_sched_barrier(0);
     x = xn;
   }
 }
@@ -479,10 +479,16 @@ __global__ __launch_bounds__(64 * W, (D < 64 || (D == 64 && W != 2)) ? 2 : 1) vo
 //            key order of conv1x1_f32.hip (key 8 j + 4 h + s for MFMA s): one 16-byte read of
 //            each operand feeds four MFMAs.
 // LDS: Q 33.8 KB + dO 33.8 KB + dS 67.6 KB + lse / delta = 136 KB (one workgroup per CU).
+// BERT-base fp32 (B 64, H 12): 157.3 -> ~135 us per layer for the backward
+// (profiles/r5/rocprof_bert_fp32_fused_attn_bwd.md, profiles/r5/attn_fused_bwd_modes.json).
 constexpr int kFbT = 128, kFbP = 132;
 
+// The four query tiles of phase 1 are unrolled with no scheduling barriers, so the compiler
+// overlaps one tile's softmax VALU work with the previous tile's MFMAs (one wave per SIMD: the
+// barriered loop of the two-pass kernels measured ~10 us per layer slower here).
 template <int D>
 __global__ __launch_bounds__(256, 1) void attn_f32_bwd_fused_t128(AttnArgsF a) {
+  constexpr bool SB = false;
   constexpr int RS = D + 2, DT = D / 32;
   static_assert(D == 64, "fused backward: head dim 64");
   static_assert(kFbT * RS >= D * kFbP, "Kt must fit in the Q rows' LDS");
@@ -540,12 +546,15 @@ __global__ __launch_bounds__(256, 1) void attn_f32_bwd_fused_t128(AttnArgsF a) {
       dk[t] = zero16();
       dv[t] = zero16();
     }
-    for (int qt = 0; qt < T; qt += kT) {
+#pragma unroll
+    for (int it = 0; it < kFbT / kT; ++it) {
+      const int qt = it * kT;
+      if (qt >= T) break;
       const float* qt_rows = Qs + qt * RS;
       const float* dt_rows = Ds + qt * RS;
       f32x16 s = zero16(), dp = zero16();
-      dot_hd<D, RS, true>(s, qt_rows + r * RS + 2 * h, kf);   // S[query r][key]: lane = key
-      dot_hd<D, RS, true>(dp, dt_rows + r * RS + 2 * h, vf);  // dP = dO V^T
+      dot_hd<D, RS, true, SB>(s, qt_rows + r * RS + 2 * h, kf);   // S[query r][key]: lane = key
+      dot_hd<D, RS, true, SB>(dp, dt_rows + r * RS + 2 * h, vf);  // dP = dO V^T
       float ls[16], ds[16];
       rows16(lse_s + qt, h, ls);
       rows16(del_s + qt, h, ds);
@@ -566,7 +575,7 @@ __global__ __launch_bounds__(256, 1) void attn_f32_bwd_fused_t128(AttnArgsF a) {
         float dc[16], qc[16];
         col16(dt_rows, RS, 32 * t + r, h, dc);
         col16(qt_rows, RS, 32 * t + r, h, qc);
-        __builtin_amdgcn_sched_barrier(0);
+        if constexpr (SB) __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
         for (int i = 0; i < 16; ++i) {
           dv[t] = mfma(dc[i], s[i], dv[t]);
@@ -663,10 +672,10 @@ AttnArgsF make_args_f(const std::vector<int64_t>& t, int B, int H, int Tq, int T
   return a;
 }
 
-bool g_fused_bwd_f32 = true;  // attn_f32_set_fused_bwd: tests reach the two-pass backward
+int g_fused_bwd_f32 = 1;  // attn_f32_set_fused_bwd: 0 = the two-pass backward (tests, A/B)
 
 bool attn_f32_fused_bwd_ok(int D, int Tq, int Tk) {
-  return g_fused_bwd_f32 && D == 64 && Tq == Tk && Tq >= 1 && Tq <= kFbT;
+  return g_fused_bwd_f32 != 0 && D == 64 && Tq == Tk && Tq >= 1 && Tq <= kFbT;
 }
 
 bool f32_shape_ok(int D, int Tq, int Tk) {
@@ -692,7 +701,7 @@ void attention_fwd_f32(const std::vector<int64_t>& t, int B, int H, int Tq, int 
 }
 
 // the fused T <= 128 backward (default on); false: the dQ + dK/dV passes (A/B and tests)
-void attn_f32_set_fused_bwd(bool on) { g_fused_bwd_f32 = on; }
+void attn_f32_set_fused_bwd(int mode) { g_fused_bwd_f32 = mode; }
 
 void attention_bwd_f32(const std::vector<int64_t>& t, int B, int H, int Tq, int Tk, int D, float scale, bool causal,
                        uintptr_t stream) {

@@ -201,7 +201,7 @@ void attention_bwd(const std::vector<int64_t>& t, int B, int H, int Tq, int Tk, 
 // ---- fused attention at fp32 on v_mfma_f32_32x32x2_f32 (attention_f32.hip) ----
 void attention_fwd_f32(const std::vector<int64_t>& t, int B, int H, int Tq, int Tk, int D, float scale, bool causal,
                        uintptr_t stream);
-void attn_f32_set_fused_bwd(bool on);
+void attn_f32_set_fused_bwd(int mode);
 void attention_bwd_f32(const std::vector<int64_t>& t, int B, int H, int Tq, int Tk, int D, float scale, bool causal,
                        uintptr_t stream);
 

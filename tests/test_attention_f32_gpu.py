@@ -153,13 +153,13 @@ def test_f32_fused_backward_t128_vs_two_pass_and_fp64(B, H, T, causal, masked):
     grads = []
     try:
         for fused in (True, False):
-            h.attn_f32_set_fused_bwd(fused)
+            h.attn_f32_set_fused_bwd(1 if fused else 0)
             x = qkv.clone().requires_grad_()
             o = attention_qkvpacked(x, km, causal, scale)
             o.backward(do)
             grads.append(x.grad)
     finally:
-        h.attn_f32_set_fused_bwd(True)
+        h.attn_f32_set_fused_bwd(1)
     xd = qkv.double().requires_grad_()
     q, k, v = (xd[:, :, i].transpose(1, 2) for i in range(3))
     ref = ref_attn(q, k, v, km, causal, scale).transpose(1, 2)
