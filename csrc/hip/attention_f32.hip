@@ -32,6 +32,7 @@ namespace {
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 
 constexpr int kT = 32;                 // rows of the streamed operand per LDS tile
+constexpr int kFbT = 128, kFbP = 132;  // fused backward: rows, dS / Kt pitch
 constexpr int kMaxT32 = 4096;
 constexpr float kMaskNeg = -1e9f;
 constexpr float kNegInf = -__builtin_huge_valf();
@@ -481,8 +482,6 @@ __global__ __launch_bounds__(64 * W, (D < 64 || (D == 64 && W != 2)) ? 2 : 1) vo
 // LDS: Q 33.8 KB + dO 33.8 KB + dS 67.6 KB + lse / delta = 136 KB (one workgroup per CU).
 // BERT-base fp32 (B 64, H 12): 157.3 -> ~135 us per layer for the backward
 // (profiles/r5/rocprof_bert_fp32_fused_attn_bwd.md, profiles/r5/attn_fused_bwd_modes.json).
-constexpr int kFbT = 128, kFbP = 132;
-
 // The four query tiles of phase 1 are unrolled with no scheduling barriers, so the compiler
 // overlaps one tile's softmax VALU work with the previous tile's MFMAs (one wave per SIMD: the
 // barriered loop of the two-pass kernels measured ~10 us per layer slower here).
@@ -642,7 +641,9 @@ void dispatch_d32(int D, F&& f) {
 }
 
 // waves per workgroup (32 rows each): enough for the rows, at most 4.  Removed in round 5 after
-// their recorded losses: a register prefetch of the next K / V tile in the forward and dQ passes
+// their recorded losses: a resident-head T <= 128 forward (K / V staged once, 67.7 KB LDS, two
+// workgroups per CU, unrolled key tiles: 58.3 vs 48.3 us per BERT-base layer,
+// profiles/r5/attn_fused_bwd_modes.json); a register prefetch of the next K / V tile in the forward and dQ passes
 // (fwd 48.0 -> 51.2 us, dQ 75.9 -> 81.6 us per BERT-base layer) and an LDS-DMA ring for the D = 64
 // forward (53.5 vs 48.3 us: its swizzled addressing cost a wave per SIMD; profiles/r4/README.md,
 // r4ad)
