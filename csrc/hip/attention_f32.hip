@@ -480,14 +480,19 @@ __global__ __launch_bounds__(64 * W, (D < 64 || (D == 64 && W != 2)) ? 2 : 1) vo
 //            key order of conv1x1_f32.hip (key 8 j + 4 h + s for MFMA s): one 16-byte read of
 //            each operand feeds four MFMAs.
 // LDS: Q 33.8 KB + dO 33.8 KB + dS 67.6 KB + lse / delta = 136 KB (one workgroup per CU).
-// BERT-base fp32 (B 64, H 12): 157.3 -> ~135 us per layer for the backward
+// BERT-base fp32 (B 64, H 12): 157.3 -> ~127 us per layer for the backward
 // (profiles/r5/rocprof_bert_fp32_fused_attn_bwd.md, profiles/r5/attn_fused_bwd_modes.json).
 // The four query tiles of phase 1 are unrolled with no scheduling barriers, so the compiler
 // overlaps one tile's softmax VALU work with the previous tile's MFMAs (one wave per SIMD: the
 // barriered loop of the two-pass kernels measured ~10 us per layer slower here).
+// Eight waves, two per SIMD (four waves, one per SIMD, ran 212 vs 205 us per forward + backward
+// call, profiles/r5/attn_fused_bwd_modes.json): phase 1 splits each key tile's four query tiles
+// between two waves (dK / dV partials summed through the dO rows' LDS), phase 2 gives each wave
+// one (query tile, d tile) pair.
 template <int D>
-__global__ __launch_bounds__(256, 1) void attn_f32_bwd_fused_t128(AttnArgsF a) {
+__global__ __launch_bounds__(512, 1) void attn_f32_bwd_fused_t128(AttnArgsF a) {
   constexpr bool SB = false;
+  constexpr int NQ = 2;  // query tiles per wave in phase 1
   constexpr int RS = D + 2, DT = D / 32;
   static_assert(D == 64, "fused backward: head dim 64");
   static_assert(kFbT * RS >= D * kFbP, "Kt must fit in the Q rows' LDS");
@@ -512,7 +517,7 @@ __global__ __launch_bounds__(256, 1) void attn_f32_bwd_fused_t128(AttnArgsF a) {
   for (int i = threadIdx.x; i < kFbT; i += blockDim.x)
     lse_s[i] = i < T ? a.lse[int64_t(bh) * T + i] : __builtin_huge_valf();
   __syncthreads();
-  {
+  if (w < 4) {
     const int q = 32 * w + r;
     float dpart = 0.f;
     if (q < T) {
@@ -531,7 +536,8 @@ __global__ __launch_bounds__(256, 1) void attn_f32_bwd_fused_t128(AttnArgsF a) {
 
   // ---- phase 1: lane = key
   {
-    const int key = 32 * w + r;
+    const int kt = w & 3, qh = w >> 2;
+    const int key = 32 * kt + r;
     const bool kv = key < T;
     const int kc = min(key, T - 1);
     RowFrag<D, true> kf, vf;
@@ -546,8 +552,8 @@ __global__ __launch_bounds__(256, 1) void attn_f32_bwd_fused_t128(AttnArgsF a) {
       dv[t] = zero16();
     }
 #pragma unroll
-    for (int it = 0; it < kFbT / kT; ++it) {
-      const int qt = it * kT;
+    for (int it = 0; it < NQ; ++it) {
+      const int qt = (qh * NQ + it) * kT;
       if (qt >= T) break;
       const float* qt_rows = Qs + qt * RS;
       const float* dt_rows = Ds + qt * RS;
@@ -584,10 +590,43 @@ __global__ __launch_bounds__(256, 1) void attn_f32_bwd_fused_t128(AttnArgsF a) {
     }
     float* dkb = a.dk + b * a.dk_sb + hh * a.dk_sh;
     float* dvb = a.dv + b * a.dv_sb + hh * a.dv_sh;
+    {
+      // waves 4..7 hand their partial sums to waves 0..3 of the same key tile through the dO
+      // rows' LDS (4 key tiles x 2 d tiles x 16 registers x 64 lanes = 8192 floats <= 8448)
+      static_assert(4 * DT * 16 * 64 <= kFbT * RS, "partials must fit in the dO rows");
+      float* red = Ds + (kt * DT * 16) * 64 + lane;
+      __syncthreads();  // every wave is done reading the dO rows
+      if (qh == 1) {
 #pragma unroll
-    for (int t = 0; t < DT; ++t) {
-      store_row(dkb, a.dk_st, key, T, 32 * t, dk[t], a.scale, h);
-      store_row(dvb, a.dv_st, key, T, 32 * t, dv[t], 1.f, h);
+        for (int t = 0; t < DT; ++t)
+#pragma unroll
+          for (int i = 0; i < 16; ++i) red[(t * 16 + i) * 64] = dk[t][i];
+      }
+      __syncthreads();
+      if (qh == 0) {
+#pragma unroll
+        for (int t = 0; t < DT; ++t) {
+#pragma unroll
+          for (int i = 0; i < 16; ++i) dk[t][i] += red[(t * 16 + i) * 64];
+          store_row(dkb, a.dk_st, key, T, 32 * t, dk[t], a.scale, h);
+        }
+      }
+      __syncthreads();
+      if (qh == 1) {
+#pragma unroll
+        for (int t = 0; t < DT; ++t)
+#pragma unroll
+          for (int i = 0; i < 16; ++i) red[(t * 16 + i) * 64] = dv[t][i];
+      }
+      __syncthreads();
+      if (qh == 0) {
+#pragma unroll
+        for (int t = 0; t < DT; ++t) {
+#pragma unroll
+          for (int i = 0; i < 16; ++i) dv[t][i] += red[(t * 16 + i) * 64];
+          store_row(dvb, a.dv_st, key, T, 32 * t, dv[t], 1.f, h);
+        }
+      }
     }
   }
   // dS rows / columns past T: keys >= T got P = 0 above, queries >= T have lse = +inf; rows of
@@ -608,17 +647,20 @@ __global__ __launch_bounds__(256, 1) void attn_f32_bwd_fused_t128(AttnArgsF a) {
   }
   __syncthreads();
   {
-    const int q = 32 * w + r;
-    f32x16 dq[DT];
+    // wave w: queries 32 (w & 3).., d tile w >> 2
+    constexpr int TT = 1;
+    const int q = 32 * (w & 3) + r;
+    const int t0 = w >> 2;
+    f32x16 dq[TT];
 #pragma unroll
-    for (int t = 0; t < DT; ++t) dq[t] = zero16();
+    for (int t = 0; t < TT; ++t) dq[t] = zero16();
     const float* brow = dSs + q * kFbP + 4 * h;
 #pragma unroll 4
     for (int j = 0; j < kFbT / 8; ++j) {
       const float4 bv = *reinterpret_cast<const float4*>(brow + 8 * j);
 #pragma unroll
-      for (int t = 0; t < DT; ++t) {
-        const float4 av = *reinterpret_cast<const float4*>(Kt + (32 * t + r) * kFbP + 8 * j + 4 * h);
+      for (int t = 0; t < TT; ++t) {
+        const float4 av = *reinterpret_cast<const float4*>(Kt + (32 * (t0 + t) + r) * kFbP + 8 * j + 4 * h);
         dq[t] = mfma(av.x, bv.x, dq[t]);
         dq[t] = mfma(av.y, bv.y, dq[t]);
         dq[t] = mfma(av.z, bv.z, dq[t]);
@@ -627,7 +669,7 @@ __global__ __launch_bounds__(256, 1) void attn_f32_bwd_fused_t128(AttnArgsF a) {
     }
     float* base = a.out + b * a.out_sb + hh * a.out_sh;
 #pragma unroll
-    for (int t = 0; t < DT; ++t) store_row(base, a.out_st, q, T, 32 * t, dq[t], a.scale, h);
+    for (int t = 0; t < TT; ++t) store_row(base, a.out_st, q, T, 32 * (t0 + t), dq[t], a.scale, h);
   }
 }
 
@@ -712,7 +754,7 @@ void attention_bwd_f32(const std::vector<int64_t>& t, int B, int H, int Tq, int 
   const AttnArgsF a = make_args_f(t, B, H, Tq, Tk, scale, causal);
   hipStream_t s = as_stream(stream);
   if (attn_f32_fused_bwd_ok(D, Tq, Tk)) {
-    hipLaunchKernelGGL((attn_f32_bwd_fused_t128<64>), dim3(1, unsigned(B * H)), dim3(256), 0, s, a);
+    hipLaunchKernelGGL((attn_f32_bwd_fused_t128<64>), dim3(1, unsigned(B * H)), dim3(512), 0, s, a);
     check_launch();
     return;
   }

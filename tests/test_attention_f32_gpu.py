@@ -152,8 +152,8 @@ def test_f32_fused_backward_t128_vs_two_pass_and_fp64(B, H, T, causal, masked):
     do = torch.randn(B, T, H, D, device="cuda")
     grads = []
     try:
-        for fused in (True, False):
-            h.attn_f32_set_fused_bwd(1 if fused else 0)
+        for mode in (1, 0):  # fused, two-pass
+            h.attn_f32_set_fused_bwd(mode)
             x = qkv.clone().requires_grad_()
             o = attention_qkvpacked(x, km, causal, scale)
             o.backward(do)
