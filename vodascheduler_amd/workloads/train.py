@@ -69,12 +69,19 @@ class TrainConfig:
     # lock-step oracle (tests): every step appends "step:world:lr:sha1(optimizer state)" to the
     # committed extras (workloads/replay.py); one host sync per step, never in production
     step_digests: bool = False
+    # deterministic library kernels (MIOpen's deterministic solvers, no atomic split-K): a GPU
+    # trajectory then repeats bit for bit, so the elastic-equivalence tests can compare a run with
+    # its replay on real hardware; off in production (the atomic solvers are the fast ones)
+    deterministic: bool = False
 
 
 def build(cfg: TrainConfig, device: torch.device):
     w = get_workload(cfg.model)
     torch.manual_seed(cfg.seed)  # identical init everywhere (state is broadcast anyway)
     model = prepare_model(w, device, cfg.amp)
+    if cfg.deterministic:
+        torch.backends.cudnn.deterministic = True
+        torch.backends.cudnn.benchmark = False
     kw = dict(w.opt_kwargs)
     if cfg.lr is not None:
         kw["lr"] = cfg.lr
