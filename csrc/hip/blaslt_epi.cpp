@@ -2,10 +2,6 @@
 //
 //   forward   h = X W1^T + b1 (kept for backward),  y = gelu_tanh(h)     GELU_AUX_BIAS epilogue
 //   backward  dh = (dY2 W2) * gelu_tanh'(h)                              DGELU epilogue
-//             (+ db1 = sum_rows dh)                                      DGELU_BGRAD epilogue
-//
-// and, for any Linear layer, the weight gradient with the bias gradient in its epilogue:
-//             dW (+)= dY^T X,  db = sum_rows dY                          BGRADB epilogue
 //
 // Without them the FFN runs fc1 GEMM -> GELU kernel (reads h, writes y) and fc2 input-gradient
 // GEMM -> GELU-backward kernel (reads dY2 W2 and h, writes dh): at fp32 and BERT-base's 8192
@@ -21,10 +17,6 @@
 //                                        D = Y (ldd N); m = N, n = M
 //   dX[M][K] = dY[M][N] . W[N][K]   ==  A = W (op N, lda K), B = dY (op N, ldb N), D = dX
 //                                        (ldd K); m = K, n = M, k = N
-//   dW[N][K] = dY[M][N]^T . X[M][K] ==  column-major dW^T (K x N) = A . op(B) with A = X (K x M,
-//                                        op N, lda K), B = dY (N x M, op T, ldb N), D = dW
-//                                        (ldd K); m = K, n = N, k = M; BGRADB sums op(B) over k,
-//                                        i.e. dY over the tokens: the bias gradient (length N)
 // so the epilogue's per-row bias (length m) is the per-output-feature bias, and the aux
 // matrix has D's layout (row-major [M][features]).
 //
@@ -86,11 +78,10 @@ hipblasLtHandle_t lt_handle(int dev) {
 // (the heuristic finds the fp32 GELU_AUX_BIAS / DGELU kernels only when the bias / aux pointers
 // are already set: they are, to the call's operands; the probe passes a scratch allocation)
 void make_desc(hipblasLtMatmulDesc_t* op, hipblasLtMatrixLayout_t* la, hipblasLtMatrixLayout_t* lb,
-               hipblasLtMatrixLayout_t* ld, hipblasLtEpilogue_t epi, bool trans_a, bool trans_b, hipDataType t,
-               int64_t m, int64_t n, int64_t k, int64_t lda, int64_t ldb, int64_t ldd, const void* bias,
-               const void* aux) {
+               hipblasLtMatrixLayout_t* ld, hipblasLtEpilogue_t epi, bool trans_a, hipDataType t, int64_t m, int64_t n,
+               int64_t k, int64_t lda, int64_t ldb, int64_t ldd, const void* bias, const void* aux) {
   VODA_LT_CHECK(hipblasLtMatmulDescCreate(op, HIPBLAS_COMPUTE_32F, HIP_R_32F));
-  const hipblasOperation_t ta = trans_a ? HIPBLAS_OP_T : HIPBLAS_OP_N, tb = trans_b ? HIPBLAS_OP_T : HIPBLAS_OP_N;
+  const hipblasOperation_t ta = trans_a ? HIPBLAS_OP_T : HIPBLAS_OP_N, tb = HIPBLAS_OP_N;
   VODA_LT_CHECK(hipblasLtMatmulDescSetAttribute(*op, HIPBLASLT_MATMUL_DESC_TRANSA, &ta, sizeof(ta)));
   VODA_LT_CHECK(hipblasLtMatmulDescSetAttribute(*op, HIPBLASLT_MATMUL_DESC_TRANSB, &tb, sizeof(tb)));
   VODA_LT_CHECK(hipblasLtMatmulDescSetAttribute(*op, HIPBLASLT_MATMUL_DESC_EPILOGUE, &epi, sizeof(epi)));
@@ -102,31 +93,12 @@ void make_desc(hipblasLtMatmulDesc_t* op, hipblasLtMatrixLayout_t* la, hipblasLt
   VODA_LT_CHECK(hipblasLtMatmulDescSetAttribute(*op, HIPBLASLT_MATMUL_DESC_EPILOGUE_AUX_POINTER, &aux, sizeof(aux)));
   if (trans_a) VODA_LT_CHECK(hipblasLtMatrixLayoutCreate(la, t, k, m, lda));
   else VODA_LT_CHECK(hipblasLtMatrixLayoutCreate(la, t, m, k, lda));
-  if (trans_b) VODA_LT_CHECK(hipblasLtMatrixLayoutCreate(lb, t, n, k, ldb));
-  else VODA_LT_CHECK(hipblasLtMatrixLayoutCreate(lb, t, k, n, ldb));
+  VODA_LT_CHECK(hipblasLtMatrixLayoutCreate(lb, t, k, n, ldb));
   VODA_LT_CHECK(hipblasLtMatrixLayoutCreate(ld, t, m, n, ldd));
 }
 
-// The plan modes: epilogue and operand transposes
-//   0: D = gelu(A.B + bias), aux = A.B + bias        (A = W op T, B = X op N)
-//   1: D = (A.B) * gelu'(aux)                        (A = W op N, B = dY op N)
-//   2: mode 1 + bias = sum over n of D               (DGELU_BGRAD)
-//   3: D = A.op(B) + beta D, bias = sum over k of op(B)   (A = X op N, B = dY op T; BGRADB)
-struct ModeInfo {
-  hipblasLtEpilogue_t epi;
-  bool ta, tb;
-};
-ModeInfo mode_info(int mode) {
-  switch (mode) {
-    case 0: return {HIPBLASLT_EPILOGUE_GELU_AUX_BIAS, true, false};
-    case 1: return {HIPBLASLT_EPILOGUE_DGELU, false, false};
-    case 2: return {HIPBLASLT_EPILOGUE_DGELU_BGRAD, false, false};
-    case 3: return {HIPBLASLT_EPILOGUE_BGRADB, false, true};
-  }
-  VODA_CHECK(false, "hipBLASLt epilogue GEMM: unknown mode");
-  return {};
-}
-
+// mode 0: D = gelu(A.B + bias), aux = A.B + bias   (A = W op T, B = X op N)
+// mode 1: D = (A.B) * gelu'(aux)                   (A = W op N, B = dY op N)
 Plan& get_plan(hipblasLtHandle_t h, const PlanKey& key, const void* bias, const void* aux) {
   static std::map<PlanKey, Plan> plans;
   auto it = plans.find(key);
@@ -134,8 +106,8 @@ Plan& get_plan(hipblasLtHandle_t h, const PlanKey& key, const void* bias, const 
   const auto [mode, dt, m, n, k, lda, ldb, ldd, dev, ws_bytes] = key;
   (void)dev;
   Plan p;
-  const ModeInfo mi = mode_info(mode);
-  make_desc(&p.op, &p.la, &p.lb, &p.ld, mi.epi, mi.ta, mi.tb, lt_type(dt), m, n, k, lda, ldb, ldd, bias, aux);
+  make_desc(&p.op, &p.la, &p.lb, &p.ld, mode == 0 ? HIPBLASLT_EPILOGUE_GELU_AUX_BIAS : HIPBLASLT_EPILOGUE_DGELU,
+            mode == 0, lt_type(dt), m, n, k, lda, ldb, ldd, bias, aux);
   hipblasLtMatmulPreference_t pref;
   VODA_LT_CHECK(hipblasLtMatmulPreferenceCreate(&pref));
   const uint64_t wsb = ws_bytes;
@@ -145,36 +117,33 @@ Plan& get_plan(hipblasLtHandle_t h, const PlanKey& key, const void* bias, const 
   int ret = 0;
   VODA_LT_CHECK(hipblasLtMatmulAlgoGetHeuristic(h, p.op, p.la, p.lb, p.ld, p.ld, pref, 1, res, &ret));
   hipblasLtMatmulPreferenceDestroy(pref);
-  VODA_CHECK(ret > 0, "hipBLASLt: no algorithm for this epilogue GEMM (mode " + std::to_string(mode) + ")");
+  VODA_CHECK(ret > 0, "hipBLASLt: no algorithm for the GELU epilogue GEMM of this shape");
   p.algo = res[0].algo;
   p.ws_needed = res[0].workspaceSize;
   return plans.emplace(key, p).first->second;
 }
 
 void run(int mode, int dt, const void* A, int64_t lda, const void* B, int64_t ldb, void* D, int64_t ldd,
-         const void* bias, void* aux, int64_t m, int64_t n, int64_t k, void* ws, size_t ws_bytes, hipStream_t s,
-         float beta = 0.f) {
+         const void* bias, void* aux, int64_t m, int64_t n, int64_t k, void* ws, size_t ws_bytes, hipStream_t s) {
   int dev = 0;
   VODA_HIP_CHECK(hipGetDevice(&dev));
   std::lock_guard<std::mutex> g(lt_mutex());
   hipblasLtHandle_t h = lt_handle(dev);
   Plan& p = get_plan(h, PlanKey{mode, dt, m, n, k, lda, ldb, ldd, dev, ws_bytes}, bias, aux);
   VODA_CHECK(p.ws_needed <= ws_bytes, "hipBLASLt: workspace too small for the chosen algorithm");
-  if (mode != 1)
+  if (mode == 0)
     VODA_LT_CHECK(hipblasLtMatmulDescSetAttribute(p.op, HIPBLASLT_MATMUL_DESC_BIAS_POINTER, &bias, sizeof(bias)));
-  if (mode != 3)
-    VODA_LT_CHECK(hipblasLtMatmulDescSetAttribute(p.op, HIPBLASLT_MATMUL_DESC_EPILOGUE_AUX_POINTER, &aux, sizeof(aux)));
-  const float alpha = 1.f;
+  VODA_LT_CHECK(hipblasLtMatmulDescSetAttribute(p.op, HIPBLASLT_MATMUL_DESC_EPILOGUE_AUX_POINTER, &aux, sizeof(aux)));
+  const float alpha = 1.f, beta = 0.f;
   VODA_LT_CHECK(hipblasLtMatmul(h, p.op, &alpha, A, p.la, B, p.lb, &beta, D, p.ld, D, p.ld, &p.algo, ws, ws_bytes, s));
 }
 
 }  // namespace
 
 // Number of algorithms hipBLASLt's heuristic returns for epilogue ``epi`` on a GEMM of dtype
-// ``dt`` with op(A) = A^T if ``trans_a`` and op(B) = B^T if ``trans_b`` (m x n x k, tight
-// leading dimensions); aux / bias are declared when the epilogue takes them.  Capability probe
-// for tests and the FFN's / Linear's path choice.
-int gemm_epilogue_algos(int epi, int dt, bool trans_a, bool trans_b, int64_t m, int64_t n, int64_t k) {
+// ``dt`` with op(A) = A^T if ``trans_a`` (m x n x k, tight leading dimensions); aux / bias are
+// declared when the epilogue takes them.  Capability probe for tests and the FFN's path choice.
+int gemm_epilogue_algos(int epi, int dt, bool trans_a, int64_t m, int64_t n, int64_t k) {
   int dev = 0;
   VODA_HIP_CHECK(hipGetDevice(&dev));
   std::lock_guard<std::mutex> g(lt_mutex());
@@ -183,8 +152,8 @@ int gemm_epilogue_algos(int epi, int dt, bool trans_a, bool trans_b, int64_t m, 
   if (scratch == nullptr) VODA_HIP_CHECK(hipMalloc(&scratch, 256));
   hipblasLtMatmulDesc_t op;
   hipblasLtMatrixLayout_t la, lb, ld;
-  make_desc(&op, &la, &lb, &ld, hipblasLtEpilogue_t(epi), trans_a, trans_b, lt_type(dt), m, n, k, trans_a ? k : m,
-            trans_b ? n : k, m, scratch, scratch);
+  make_desc(&op, &la, &lb, &ld, hipblasLtEpilogue_t(epi), trans_a, lt_type(dt), m, n, k, trans_a ? k : m, k, m, scratch,
+            scratch);
   hipblasLtMatmulPreference_t pref;
   VODA_LT_CHECK(hipblasLtMatmulPreferenceCreate(&pref));
   const uint64_t wsb = 32ull << 20;
@@ -217,27 +186,6 @@ void gemm_dgelu(uintptr_t dy, uintptr_t w, uintptr_t h, uintptr_t dh, int64_t M,
   // dh[M][K] = (dY[M][N] . W[N][K]) * gelu'(h[M][K]); A = W (op N, lda K), B = dY (ldb N)
   run(1, dt, reinterpret_cast<const void*>(w), K, reinterpret_cast<const void*>(dy), N, reinterpret_cast<void*>(dh), K,
       nullptr, reinterpret_cast<void*>(h), K, M, N, reinterpret_cast<void*>(ws), size_t(ws_bytes), as_stream(stream));
-}
-
-void gemm_dgelu_bgrad(uintptr_t dy, uintptr_t w, uintptr_t h, uintptr_t dh, uintptr_t dbias, int64_t M, int64_t N,
-                      int64_t K, int dt, uintptr_t ws, int64_t ws_bytes, uintptr_t stream) {
-  VODA_CHECK(M > 0 && N > 0 && K > 0 && N % 8 == 0 && K % 8 == 0, "gemm_dgelu_bgrad: bad shape");
-  VODA_CHECK(dy % 16 == 0 && w % 16 == 0 && h % 16 == 0 && dh % 16 == 0 && dbias % 16 == 0,
-             "gemm_dgelu_bgrad: operands");
-  // gemm_dgelu + dbias[K] = sum over the M rows of dh (written, in the operands' dtype)
-  run(2, dt, reinterpret_cast<const void*>(w), K, reinterpret_cast<const void*>(dy), N, reinterpret_cast<void*>(dh), K,
-      reinterpret_cast<const void*>(dbias), reinterpret_cast<void*>(h), K, M, N, reinterpret_cast<void*>(ws),
-      size_t(ws_bytes), as_stream(stream));
-}
-
-void gemm_wgrad_bgrad(uintptr_t dy, uintptr_t x, uintptr_t dw, uintptr_t dbias, int64_t M, int64_t N, int64_t K,
-                      int dt, bool accumulate, uintptr_t ws, int64_t ws_bytes, uintptr_t stream) {
-  VODA_CHECK(M > 0 && N > 0 && K > 0 && N % 8 == 0 && K % 8 == 0, "gemm_wgrad_bgrad: bad shape");
-  VODA_CHECK(dy % 16 == 0 && x % 16 == 0 && dw % 16 == 0 && dbias % 16 == 0, "gemm_wgrad_bgrad: operands");
-  // dW[N][K] (+)= dY[M][N]^T . X[M][K]; dbias[N] = sum over the M rows of dY (written)
-  run(3, dt, reinterpret_cast<const void*>(x), K, reinterpret_cast<const void*>(dy), N, reinterpret_cast<void*>(dw), K,
-      reinterpret_cast<const void*>(dbias), nullptr, K, N, M, reinterpret_cast<void*>(ws), size_t(ws_bytes),
-      as_stream(stream), accumulate ? 1.f : 0.f);
 }
 
 }  // namespace voda

@@ -123,11 +123,7 @@ void gemm_f32_dgrad_bn(uintptr_t dy, uintptr_t w, uintptr_t y, uintptr_t cg, uin
 
 // ---- hipBLASLt GEMMs with GELU epilogues for the transformer FFN (blaslt_epi.cpp); dt: kF32 /
 // kBF16 ----
-int gemm_epilogue_algos(int epi, int dt, bool trans_a, bool trans_b, int64_t m, int64_t n, int64_t k);
-void gemm_dgelu_bgrad(uintptr_t dy, uintptr_t w, uintptr_t h, uintptr_t dh, uintptr_t dbias, int64_t M, int64_t N,
-                      int64_t K, int dt, uintptr_t ws, int64_t ws_bytes, uintptr_t stream);
-void gemm_wgrad_bgrad(uintptr_t dy, uintptr_t x, uintptr_t dw, uintptr_t dbias, int64_t M, int64_t N, int64_t K,
-                      int dt, bool accumulate, uintptr_t ws, int64_t ws_bytes, uintptr_t stream);
+int gemm_epilogue_algos(int epi, int dt, bool trans_a, int64_t m, int64_t n, int64_t k);
 void gemm_gelu_aux(uintptr_t x, uintptr_t w, uintptr_t bias, uintptr_t h, uintptr_t y, int64_t M, int64_t N,
                    int64_t K, int dt, uintptr_t ws, int64_t ws_bytes, uintptr_t stream);
 void gemm_dgelu(uintptr_t dy, uintptr_t w, uintptr_t h, uintptr_t dh, int64_t M, int64_t N, int64_t K, int dt,

@@ -16,10 +16,10 @@ def test_epilogue_probe_runs():
     from vodascheduler_amd.ops import _native
 
     h = _native.hip()
-    assert h.gemm_epilogue_algos(36, 0, True, False, 3072, 8192, 768) > 0
+    assert h.gemm_epilogue_algos(36, 0, True, 3072, 8192, 768) > 0
     for dt in (0, 1):
         for e in (ffn.EPI_GELU_AUX_BIAS, ffn.EPI_DGELU):
-            assert h.gemm_epilogue_algos(e, dt, False, False, 3072, 8192, 768) >= 0
+            assert h.gemm_epilogue_algos(e, dt, False, 3072, 8192, 768) >= 0
     assert ffn.epilogues_available(torch.device("cuda", 0), torch.float32)
     ffn.epilogues_available(torch.device("cuda", 0), torch.bfloat16)
 

@@ -32,7 +32,7 @@ from . import dense as D
 # VODA_GELU_EPILOGUE=0: the FFN runs FusedLinear -> GELU kernel -> FusedLinear (A/B switch)
 USE_GELU_EPILOGUE = os.environ.get("VODA_GELU_EPILOGUE", "1") != "0"
 
-EPI_GELU_AUX_BIAS, EPI_DGELU, EPI_DGELU_BGRAD, EPI_BGRADB = 164, 192, 208, 512  # hipblasLtEpilogue_t values
+EPI_GELU_AUX_BIAS, EPI_DGELU = 164, 192  # hipblasLtEpilogue_t values
 _WS_BYTES = 32 << 20
 _WS: dict[torch.device, torch.Tensor] = {}
 _EPI_OK: dict[tuple[int, torch.dtype], bool] = {}
@@ -90,44 +90,6 @@ def gemm_dgelu(dy2: torch.Tensor, w: torch.Tensor, h: torch.Tensor) -> torch.Ten
     N.hip().gemm_dgelu(dy2.data_ptr(), w.data_ptr(), h.data_ptr(), dh.data_ptr(), M, Nn, K, N.dtype_code(dy2.dtype),
                        ws.data_ptr(), ws.numel(), N.stream_of(dy2))
     return dh
-
-
-def gemm_dgelu_bgrad(dy2: torch.Tensor, w: torch.Tensor, h: torch.Tensor) -> tuple[torch.Tensor, torch.Tensor]:
-    """(dh, db) = ((dy2 W) * gelu_tanh'(h), dh.sum(0)): the DGELU GEMM with fc1's bias gradient
-    in its epilogue (DGELU_BGRAD)."""
-    if not dy2.is_cuda:
-        dh = gemm_dgelu(dy2, w, h)
-        return dh, dh.sum(0)
-    M, Nn = dy2.shape
-    K = w.shape[1]
-    for t, nm in ((dy2, "dy"), (w, "w"), (h, "h")):
-        N.check_gpu_tensor(t, nm, align=16)
-    dh = torch.empty(M, K, dtype=dy2.dtype, device=dy2.device)
-    db = torch.empty(K, dtype=dy2.dtype, device=dy2.device)
-    ws = _workspace(dy2.device)
-    N.hip().gemm_dgelu_bgrad(dy2.data_ptr(), w.data_ptr(), h.data_ptr(), dh.data_ptr(), db.data_ptr(), M, Nn, K,
-                             N.dtype_code(dy2.dtype), ws.data_ptr(), ws.numel(), N.stream_of(dy2))
-    return dh, db
-
-
-def gemm_wgrad_bgrad(dy2: torch.Tensor, x2: torch.Tensor, dw: torch.Tensor, accumulate: bool) -> torch.Tensor:
-    """dw (+)= dy2^T x2 in place (dw [N, K] contiguous, the operands' dtype) and returns
-    db = dy2.sum(0): the weight-gradient GEMM with the bias gradient in its epilogue (BGRADB)."""
-    if not dy2.is_cuda:
-        g = dy2.t() @ x2
-        dw.add_(g) if accumulate else dw.copy_(g)
-        return dy2.sum(0)
-    M, Nn = dy2.shape
-    K = x2.shape[1]
-    for t, nm in ((dy2, "dy"), (x2, "x"), (dw, "dw")):
-        N.check_gpu_tensor(t, nm, align=16)
-    if dw.shape != (Nn, K) or dw.dtype != dy2.dtype or x2.dtype != dy2.dtype:
-        raise ValueError(f"gemm_wgrad_bgrad: dw {tuple(dw.shape)}/{dw.dtype} for dY {tuple(dy2.shape)}/{dy2.dtype}")
-    db = torch.empty(Nn, dtype=dy2.dtype, device=dy2.device)
-    ws = _workspace(dy2.device)
-    N.hip().gemm_wgrad_bgrad(dy2.data_ptr(), x2.data_ptr(), dw.data_ptr(), db.data_ptr(), M, Nn, K,
-                             N.dtype_code(dy2.dtype), bool(accumulate), ws.data_ptr(), ws.numel(), N.stream_of(dy2))
-    return db
 
 
 class _FFNGeluFn(torch.autograd.Function):
@@ -202,8 +164,8 @@ def epilogues_available(device: torch.device, dtype: torch.dtype = torch.float32
         h = N.hip()
         dt = N.dtype_code(dtype)
         with torch.cuda.device(idx):
-            ok = (h.gemm_epilogue_algos(EPI_GELU_AUX_BIAS, dt, True, False, 3072, 8192, 768) > 0
-                  and h.gemm_epilogue_algos(EPI_DGELU, dt, False, False, 3072, 8192, 768) > 0)
+            ok = (h.gemm_epilogue_algos(EPI_GELU_AUX_BIAS, dt, True, 3072, 8192, 768) > 0
+                  and h.gemm_epilogue_algos(EPI_DGELU, dt, False, 3072, 8192, 768) > 0)
         _EPI_OK[(idx, dtype)] = ok
     return ok
 
