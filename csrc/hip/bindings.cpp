@@ -31,6 +31,7 @@ PYBIND11_MODULE(_vodahip, m) {
   m.def("layernorm_fwd", &layernorm_fwd);
   m.def("layernorm_bwd", &layernorm_bwd);
   m.def("layernorm_bwd_partial_rows", &layernorm_bwd_partial_rows);
+  m.def("layernorm_set_bwd_waves", &layernorm_set_bwd_waves);
   m.def("masked_softmax_fwd", &masked_softmax_fwd);
   m.def("masked_softmax_bwd", &masked_softmax_bwd);
   m.def("xent_fwd", &xent_fwd);

@@ -118,8 +118,10 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(const T* __restrict__ x, co
   }
 }
 
-template <typename T, typename WT, int MAXITER>
-__global__ __launch_bounds__(256) void ln_bwd_kernel(const T* __restrict__ dy, const T* __restrict__ x,
+// W waves per block (4 or 8): each block writes ONE partial row of dgamma / dbeta, so the grid
+// is capped (kLnBwdBlockCap) and more rows in flight per CU have to come from more waves per block
+template <typename T, typename WT, int MAXITER, int W = 4>
+__global__ __launch_bounds__(64 * W) void ln_bwd_kernel(const T* __restrict__ dy, const T* __restrict__ x,
                                                      const float* __restrict__ mean, const float* __restrict__ rstd,
                                                      const void* __restrict__ gamma, T* __restrict__ dx,
                                                      float* __restrict__ part_g, float* __restrict__ part_b,
@@ -127,7 +129,7 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const T* __restrict__ dy, c
   // part_x (optional): per-block column sums of dx -- the bias gradient of the Linear whose
   // output is this LayerNorm's input (a post-LN sublayer's last projection), folded in here
   // instead of a separate column-sum pass over dx (ops/dense.BiasHandoff)
-  extern __shared__ __attribute__((aligned(16))) float lds[];  // [4][N]
+  extern __shared__ __attribute__((aligned(16))) float lds[];  // [W][N]
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
   const int N4 = N >> 2;
@@ -141,14 +143,14 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const T* __restrict__ dy, c
     ab[it] = make_float4(0.f, 0.f, 0.f, 0.f);
     ax[it] = make_float4(0.f, 0.f, 0.f, 0.f);
   }
-  // A wave owns rows wave + 4*blockIdx.x + k * 4*gridDim.x.  The grid is capped (one fp32
+  // A wave owns rows wave + W*blockIdx.x + k * W*gridDim.x.  The grid is capped (one fp32
   // partial row per block for dgamma/dbeta), so a wave walks several rows; R of them are
   // loaded together before any is reduced, which keeps R row-loads in flight per wave
   // instead of one dependent HBM round trip per row (BERT-base 8192 x 768: 25 -> ~8 us).
   // (8 rows at N <= 768 measured slower in the BERT-base step: 10.36-10.41 vs 10.30-10.33 ms)
   constexpr int R = MAXITER <= 3 ? 4 : (MAXITER <= 4 ? 2 : 1);
-  const int64_t rstride = int64_t(gridDim.x) * 4;
-  for (int64_t row0 = int64_t(blockIdx.x) * 4 + wave; row0 < M; row0 += rstride * R) {
+  const int64_t rstride = int64_t(gridDim.x) * W;
+  for (int64_t row0 = int64_t(blockIdx.x) * W + wave; row0 < M; row0 += rstride * R) {
     // every load is unconditional (clamped row / column) and kept as raw bits until all R
     // rows are in flight; out-of-range lanes are zeroed after the conversion.  A branch or a
     // conversion right behind each load makes hipcc wait for it before issuing the next one.
@@ -221,20 +223,29 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const T* __restrict__ dy, c
     }
   }
   if (part_g == nullptr) return;  // gamma/beta gradients not requested
-  // combine the 4 waves' column partials through LDS, gamma, beta [, dx]: one partial row per
+  // combine the W waves' column partials through LDS, gamma, beta [, dx]: one partial row per
   // block (col_sum_kernel adds them up)
-  const int passes = part_x != nullptr ? 3 : 2;
-  for (int pass = 0; pass < passes; ++pass) {
+  // (one call per array with the array named statically: selecting ag / ab / ax by a loop index
+  // made hipcc keep all three in scratch for the whole kernel, 160 B per lane, and the row loop
+  // read-modify-wrote them there)
+  auto combine = [&](const float4 (&acc)[MAXITER], float* __restrict__ part) {
 #pragma unroll
     for (int it = 0; it < MAXITER; ++it) {
       const int c4 = it * 64 + lane;
-      if (c4 < N4) reinterpret_cast<float4*>(lds + wave * N)[c4] = pass == 0 ? ag[it] : (pass == 1 ? ab[it] : ax[it]);
+      if (c4 < N4) reinterpret_cast<float4*>(lds + wave * N)[c4] = acc[it];
     }
     __syncthreads();
-    float* out = (pass == 0 ? part_g : (pass == 1 ? part_b : part_x)) + int64_t(blockIdx.x) * N;
-    for (int c = threadIdx.x; c < N; c += 256) out[c] = (lds[c] + lds[N + c]) + (lds[2 * N + c] + lds[3 * N + c]);
+    float* out = part + int64_t(blockIdx.x) * N;
+    for (int c = threadIdx.x; c < N; c += 64 * W) {
+      float t = (lds[c] + lds[N + c]) + (lds[2 * N + c] + lds[3 * N + c]);
+      if constexpr (W == 8) t += (lds[4 * N + c] + lds[5 * N + c]) + (lds[6 * N + c] + lds[7 * N + c]);
+      out[c] = t;
+    }
     __syncthreads();
-  }
+  };
+  combine(ag, part_g);
+  combine(ab, part_b);
+  if (part_x != nullptr) combine(ax, part_x);
 }
 
 // Column sums of a [rows][N] fp32 partial matrix: out[c] = sum_r part[r][c] (cast to WT).
@@ -334,6 +345,13 @@ void layernorm_fwd(uintptr_t x, uintptr_t gamma, uintptr_t beta, uintptr_t y, ui
 // reproducible; removed in round 5.)
 constexpr int kLnBwdBlockCap = 256;
 int ln_bwd_block_cap() { return kLnBwdBlockCap; }
+// Waves per backward block for N <= 1024 (larger rows keep 4: LDS of W x N floats): 8 gives two
+// waves per SIMD at the same 256 partial rows.  Settable for the A/B (benchmarks/bench_layernorm.py).
+int g_ln_bwd_waves = 8;
+void layernorm_set_bwd_waves(int w) {
+  VODA_CHECK(w == 4 || w == 8, "layernorm: 4 or 8 waves per backward block");
+  g_ln_bwd_waves = w;
+}
 
 int layernorm_bwd_partial_rows(int64_t M) {
   int64_t g = (M + 3) / 4;
@@ -358,10 +376,20 @@ void layernorm_bwd(uintptr_t dy, uintptr_t x, uintptr_t mean, uintptr_t rstd, ui
   } else {
     VODA_CHECK(dbias_in == 0, "layernorm_bwd: the input bias sum rides with dgamma / dbeta");
   }
-  const size_t lds = size_t(4) * N * sizeof(float);
+  const int W = (g_ln_bwd_waves == 8 && N <= 1024) ? 8 : 4;
+  const size_t lds = size_t(W) * N * sizeof(float);
   LN_DISPATCH_T(dt, wdt, [&] {
     LN_DISPATCH_ITER(N, [&] {
-      hipLaunchKernelGGL((ln_bwd_kernel<T, WT, MI>), dim3(grid), dim3(256), pg ? lds : 0,
+      if constexpr (MI <= 4) {
+        if (W == 8) {
+          hipLaunchKernelGGL((ln_bwd_kernel<T, WT, MI, 8>), dim3(grid), dim3(512), pg ? lds : 0,
+                             as_stream(stream), reinterpret_cast<const T*>(dy), reinterpret_cast<const T*>(x),
+                             reinterpret_cast<const float*>(mean), reinterpret_cast<const float*>(rstd),
+                             reinterpret_cast<const void*>(gamma), reinterpret_cast<T*>(dx), pg, pb, M, N, px);
+          return;
+        }
+      }
+      hipLaunchKernelGGL((ln_bwd_kernel<T, WT, MI, 4>), dim3(grid), dim3(256), pg ? lds : 0,
                          as_stream(stream), reinterpret_cast<const T*>(dy), reinterpret_cast<const T*>(x),
                          reinterpret_cast<const float*>(mean), reinterpret_cast<const float*>(rstd),
                          reinterpret_cast<const void*>(gamma), reinterpret_cast<T*>(dx), pg, pb, M, N, px);

@@ -54,6 +54,7 @@ void gelu_tanh_bwd(uintptr_t h, uintptr_t dy, uintptr_t dh, int64_t n, int dt, u
 void layernorm_fwd(uintptr_t x, uintptr_t gamma, uintptr_t beta, uintptr_t y, uintptr_t mean, uintptr_t rstd,
                    int64_t M, int N, float eps, int dt, int wdt, uintptr_t residual, uintptr_t sum, uintptr_t stream);
 int layernorm_bwd_partial_rows(int64_t M);
+void layernorm_set_bwd_waves(int w);
 void layernorm_bwd(uintptr_t dy, uintptr_t x, uintptr_t mean, uintptr_t rstd, uintptr_t gamma, uintptr_t dx,
                    uintptr_t dgamma, uintptr_t dbeta, uintptr_t workspace, int64_t M, int N, int dt, int wdt,
                    bool accumulate, uintptr_t stream,
