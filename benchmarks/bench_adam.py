@@ -30,6 +30,19 @@ def main():
     v = torch.zeros(n, device="cuda")
     lp = torch.empty(n, device="cuda", dtype=torch.bfloat16)
     s = torch.cuda.current_stream().cuda_stream
+    # reference: a device copy of the same element count (read 4 B + write 4 B per element)
+    for _ in range(3):
+        m.copy_(p)
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(a.iters):
+        m.copy_(p)
+    e1.record()
+    torch.cuda.synchronize()
+    us = e0.elapsed_time(e1) / a.iters * 1e3
+    print(json.dumps({"n": n, "copy_us": round(us, 1), "copy_TBps": round(8 * n / us / 1e6, 2)}), flush=True)
+    m.zero_()
     for lowp in (True, False):
         def step(k):
             h.adam_step(p.data_ptr(), g.data_ptr(), N.dtype_code(g.dtype), m.data_ptr(), v.data_ptr(),

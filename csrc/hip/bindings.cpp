@@ -65,7 +65,6 @@ PYBIND11_MODULE(_vodahip, m) {
   m.def("gemm_epilogue_algos", &gemm_epilogue_algos);
   m.def("gemm_gelu_aux", &gemm_gelu_aux);
   m.def("gemm_dgelu", &gemm_dgelu);
-  m.def("gemm_wgrad_f32acc", &gemm_wgrad_f32acc);
   m.def("gemm_f32_dgrad_bn_supported", &gemm_f32_dgrad_bn_supported);
   m.def("gemm_f32_dgrad_bn_groups", &gemm_f32_dgrad_bn_groups);
   m.def("gemm_f32_stats_groups", &gemm_f32_stats_groups);

@@ -188,78 +188,4 @@ void gemm_dgelu(uintptr_t dy, uintptr_t w, uintptr_t h, uintptr_t dh, int64_t M,
       nullptr, reinterpret_cast<void*>(h), K, M, N, reinterpret_cast<void*>(ws), size_t(ws_bytes), as_stream(stream));
 }
 
-// ---- weight gradient into an fp32 gradient buffer: dW[N][K] (+)= dY[M][N]^T . X[M][K] with
-// 16-bit (or fp32) dY / X and fp32 dW (C = D, beta = 1 accumulates into the optimizer's flat
-// gradient), optionally db[N] = sum over the M rows of dY in the BGRADB epilogue (written).
-// Column-major view: dW^T (K x N) = A . op(B), A = X (K x M, op N, lda K), B = dY (N x M, op T,
-// ldb N); m = K, n = N, k = M; BGRADB sums op(B) over k.
-namespace {
-struct WPlan {
-  hipblasLtMatmulDesc_t op = nullptr;
-  hipblasLtMatrixLayout_t la = nullptr, lb = nullptr, lc = nullptr;
-  hipblasLtMatmulAlgo_t algo;
-  size_t ws_needed = 0;
-};
-using WPlanKey = std::tuple<int, bool, int64_t, int64_t, int64_t, int64_t, int64_t, int64_t, int, size_t>;
-
-WPlan& get_wplan(hipblasLtHandle_t h, const WPlanKey& key, const void* bias) {
-  static std::map<WPlanKey, WPlan> plans;
-  auto it = plans.find(key);
-  if (it != plans.end()) return it->second;
-  const auto [dt, with_bias, M, N, K, ldx, ldy, ldw, dev, ws_bytes] = key;
-  (void)dev;
-  WPlan p;
-  const hipDataType tin = lt_type(dt), tout = HIP_R_32F;
-  VODA_LT_CHECK(hipblasLtMatmulDescCreate(&p.op, HIPBLAS_COMPUTE_32F, HIP_R_32F));
-  const hipblasOperation_t ta = HIPBLAS_OP_N, tb = HIPBLAS_OP_T;
-  VODA_LT_CHECK(hipblasLtMatmulDescSetAttribute(p.op, HIPBLASLT_MATMUL_DESC_TRANSA, &ta, sizeof(ta)));
-  VODA_LT_CHECK(hipblasLtMatmulDescSetAttribute(p.op, HIPBLASLT_MATMUL_DESC_TRANSB, &tb, sizeof(tb)));
-  if (with_bias) {
-    const hipblasLtEpilogue_t epi = HIPBLASLT_EPILOGUE_BGRADB;
-    VODA_LT_CHECK(hipblasLtMatmulDescSetAttribute(p.op, HIPBLASLT_MATMUL_DESC_EPILOGUE, &epi, sizeof(epi)));
-    const hipDataType bt = HIP_R_32F;
-    VODA_LT_CHECK(hipblasLtMatmulDescSetAttribute(p.op, HIPBLASLT_MATMUL_DESC_BIAS_DATA_TYPE, &bt, sizeof(bt)));
-    VODA_LT_CHECK(hipblasLtMatmulDescSetAttribute(p.op, HIPBLASLT_MATMUL_DESC_BIAS_POINTER, &bias, sizeof(bias)));
-  }
-  VODA_LT_CHECK(hipblasLtMatrixLayoutCreate(&p.la, tin, K, M, ldx));
-  VODA_LT_CHECK(hipblasLtMatrixLayoutCreate(&p.lb, tin, N, M, ldy));
-  VODA_LT_CHECK(hipblasLtMatrixLayoutCreate(&p.lc, tout, K, N, ldw));
-  hipblasLtMatmulPreference_t pref;
-  VODA_LT_CHECK(hipblasLtMatmulPreferenceCreate(&pref));
-  const uint64_t wsb = ws_bytes;
-  VODA_LT_CHECK(hipblasLtMatmulPreferenceSetAttribute(pref, HIPBLASLT_MATMUL_PREF_MAX_WORKSPACE_BYTES, &wsb,
-                                                      sizeof(wsb)));
-  hipblasLtMatmulHeuristicResult_t res[1];
-  int ret = 0;
-  VODA_LT_CHECK(hipblasLtMatmulAlgoGetHeuristic(h, p.op, p.la, p.lb, p.lc, p.lc, pref, 1, res, &ret));
-  hipblasLtMatmulPreferenceDestroy(pref);
-  VODA_CHECK(ret > 0, "hipBLASLt: no algorithm for the fp32-accumulating weight-gradient GEMM");
-  p.algo = res[0].algo;
-  p.ws_needed = res[0].workspaceSize;
-  return plans.emplace(key, p).first->second;
-}
-}  // namespace
-
-void gemm_wgrad_f32acc(uintptr_t dy, int64_t ldy, uintptr_t x, int64_t ldx, uintptr_t dw, int64_t ldw,
-                       uintptr_t dbias, int64_t M, int64_t N, int64_t K, int dt, bool accumulate, uintptr_t ws,
-                       int64_t ws_bytes, uintptr_t stream) {
-  VODA_CHECK(M > 0 && N > 0 && K > 0 && N % 8 == 0 && K % 8 == 0, "gemm_wgrad_f32acc: bad shape");
-  VODA_CHECK(ldy >= N && ldx >= K && ldw >= K, "gemm_wgrad_f32acc: leading dimensions");
-  VODA_CHECK(dy % 16 == 0 && x % 16 == 0 && dw % 16 == 0 && dbias % 16 == 0, "gemm_wgrad_f32acc: operands");
-  int dev = 0;
-  VODA_HIP_CHECK(hipGetDevice(&dev));
-  std::lock_guard<std::mutex> g(lt_mutex());
-  hipblasLtHandle_t h = lt_handle(dev);
-  const void* bias = reinterpret_cast<const void*>(dbias);
-  WPlan& p = get_wplan(h, WPlanKey{dt, dbias != 0, M, N, K, ldx, ldy, ldw, dev, size_t(ws_bytes)}, bias);
-  VODA_CHECK(p.ws_needed <= size_t(ws_bytes), "hipBLASLt: workspace too small for the chosen algorithm");
-  if (dbias != 0)
-    VODA_LT_CHECK(hipblasLtMatmulDescSetAttribute(p.op, HIPBLASLT_MATMUL_DESC_BIAS_POINTER, &bias, sizeof(bias)));
-  const float alpha = 1.f, beta = accumulate ? 1.f : 0.f;
-  void* D = reinterpret_cast<void*>(dw);
-  VODA_LT_CHECK(hipblasLtMatmul(h, p.op, &alpha, reinterpret_cast<const void*>(x), p.la,
-                                reinterpret_cast<const void*>(dy), p.lb, &beta, D, p.lc, D, p.lc, &p.algo,
-                                reinterpret_cast<void*>(ws), size_t(ws_bytes), as_stream(stream)));
-}
-
 }  // namespace voda

@@ -127,9 +127,6 @@ void gemm_f32_dgrad_bn(uintptr_t dy, uintptr_t w, uintptr_t y, uintptr_t cg, uin
 int gemm_epilogue_algos(int epi, int dt, bool trans_a, int64_t m, int64_t n, int64_t k);
 void gemm_gelu_aux(uintptr_t x, uintptr_t w, uintptr_t bias, uintptr_t h, uintptr_t y, int64_t M, int64_t N,
                    int64_t K, int dt, uintptr_t ws, int64_t ws_bytes, uintptr_t stream);
-void gemm_wgrad_f32acc(uintptr_t dy, int64_t ldy, uintptr_t x, int64_t ldx, uintptr_t dw, int64_t ldw,
-                       uintptr_t dbias, int64_t M, int64_t N, int64_t K, int dt, bool accumulate, uintptr_t ws,
-                       int64_t ws_bytes, uintptr_t stream);
 void gemm_dgelu(uintptr_t dy, uintptr_t w, uintptr_t h, uintptr_t dh, int64_t M, int64_t N, int64_t K, int dt,
                 uintptr_t ws, int64_t ws_bytes, uintptr_t stream);
 

@@ -6,7 +6,8 @@
 // examples/py/pytorch/pytorch_mnist_elastic.py:112-113).  Here every
 // parameter of a job lives in ONE flat fp32 buffer, so a step is ONE HBM-streaming
 // launch: param/grad/state are read once and written once with 16-B (f32) or 8-B
-// (bf16/f16) accesses per lane, grid-stride over <= 2048 blocks of 256 threads.
+// (bf16/f16) accesses per lane, one float4 group per thread (opt_grid; the loops still
+// grid-stride, so any grid is correct).
 // Optionally the kernel also emits a low-precision copy of the updated weights
 // (bf16/f16 model weights + fp32 master), fusing the cast that would otherwise be a
 // second pass.  Semantics match torch.optim.{SGD,Adam,AdamW,RMSprop}.
@@ -99,7 +100,7 @@ __device__ __forceinline__ void adam1(float& p, float g, float& m, float& v, con
   p -= a.step_size * (m / denom);
 }
 
-// One float4 group of every array per thread and grid-stride iteration.  Two groups in flight
+// One float4 group of every array per thread.  Two groups in flight
 // were measured equal within noise (110 M-parameter AdamW step, benchmarks/bench_adam.py:
 // 708 / 690 us with a bf16 copy, 669 / 686 us without; profiles/r4/bench_adam_variants.log) and
 // were removed in round 5; non-temporal state stores did not help either.
@@ -229,6 +230,11 @@ __global__ __launch_bounds__(256) void rmsprop_kernel(float* __restrict__ p, con
     }                                                                                   \
   }()
 
+// One float4 group per thread, no grid-stride loop: the 110 M-parameter AdamW step takes 565 us
+// (5.45 TB/s, above a plain device copy's 5.28) against 678-734 us with the grid capped at
+// 1024-8192 blocks (benchmarks/bench_adam.py, profiles/r5/optim_grid_cap.jsonl).
+unsigned opt_grid(int64_t n) { return stream_grid((n + 3) / 4, 256, int64_t(1) << 30); }
+
 void sgd_step(uintptr_t p, uintptr_t g, int g_dtype, uintptr_t mom_buf, uintptr_t p_lp, int lp_dtype,
               int64_t n, float lr, float momentum, float dampening, float wd, bool nesterov,
               bool first_step, float grad_scale, uintptr_t stream) {
@@ -236,7 +242,7 @@ void sgd_step(uintptr_t p, uintptr_t g, int g_dtype, uintptr_t mom_buf, uintptr_
   VODA_CHECK(momentum == 0.f || mom_buf != 0, "momentum buffer required");
   if (n == 0) return;
   SgdArgs a{lr, momentum, dampening, wd, grad_scale, nesterov ? 1 : 0, first_step ? 1 : 0};
-  unsigned grid = stream_grid((n + 3) / 4);
+  unsigned grid = opt_grid(n);
   DISPATCH_GT_LP(g_dtype, lp_dtype, [&] {
     hipLaunchKernelGGL((sgd_kernel<GT, LP>), dim3(grid), dim3(256), 0, as_stream(stream),
                        reinterpret_cast<float*>(p), reinterpret_cast<const GT*>(g),
@@ -255,7 +261,7 @@ void adam_step(uintptr_t p, uintptr_t g, int g_dtype, uintptr_t m, uintptr_t v, 
   const double bc2 = 1.0 - std::pow(double(beta2), st);
   AdamArgs a{lr, beta1, beta2, eps, wd, grad_scale, float(lr / bc1), float(1.0 / std::sqrt(bc2)),
              adamw ? 1 : 0};
-  unsigned grid = stream_grid((n + 3) / 4);
+  unsigned grid = opt_grid(n);
   DISPATCH_GT_LP(g_dtype, lp_dtype, [&] {
     hipLaunchKernelGGL((adam_kernel<GT, LP>), dim3(grid), dim3(256), 0, as_stream(stream),
                        reinterpret_cast<float*>(p), reinterpret_cast<const GT*>(g),
@@ -272,7 +278,7 @@ void rmsprop_step(uintptr_t p, uintptr_t g, int g_dtype, uintptr_t sq, uintptr_t
   VODA_CHECK(!centered || gavg != 0, "grad-average buffer required for centered RMSprop");
   if (n == 0) return;
   RmsArgs a{lr, alpha, eps, wd, momentum, grad_scale, centered ? 1 : 0};
-  unsigned grid = stream_grid((n + 3) / 4);
+  unsigned grid = opt_grid(n);
   DISPATCH_GT_LP(g_dtype, lp_dtype, [&] {
     hipLaunchKernelGGL((rmsprop_kernel<GT, LP>), dim3(grid), dim3(256), 0, as_stream(stream),
                        reinterpret_cast<float*>(p), reinterpret_cast<const GT*>(g),
