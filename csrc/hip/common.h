@@ -89,7 +89,10 @@ __device__ __forceinline__ float wave_max(float v) {
 
 // Grid size for grid-stride memory-bound kernels: enough blocks to fill 256 CUs with
 // several resident blocks each, capped (guide §6 Guideline 11).
-inline unsigned stream_grid(int64_t work_items, int block = 256, int64_t cap = 2048) {
+// Grid of a streaming (elementwise) kernel: one work item per thread.  The kernels keep their
+// grid-stride loops, so a cap stays correct, but on MI355X the uncapped grid streams faster (a
+// 110 M-parameter AdamW step 709 -> 555 us vs 2048 grid-striding blocks, profiles/r5/optim_grid_cap.jsonl).
+inline unsigned stream_grid(int64_t work_items, int block = 256, int64_t cap = int64_t(1) << 30) {
   int64_t g = (work_items + block - 1) / block;
   if (g < 1) g = 1;
   if (g > cap) g = cap;

@@ -230,10 +230,10 @@ __global__ __launch_bounds__(256) void rmsprop_kernel(float* __restrict__ p, con
     }                                                                                   \
   }()
 
-// One float4 group per thread, no grid-stride loop: the 110 M-parameter AdamW step takes 565 us
-// (5.45 TB/s, above a plain device copy's 5.28) against 678-734 us with the grid capped at
-// 1024-8192 blocks (benchmarks/bench_adam.py, profiles/r5/optim_grid_cap.jsonl).
-unsigned opt_grid(int64_t n) { return stream_grid((n + 3) / 4, 256, int64_t(1) << 30); }
+// One float4 group per thread: the 110 M-parameter AdamW step takes 555 us (5.55 TB/s, above a
+// plain device copy's 5.32) against 678-734 us with the grid capped at 1024-8192 blocks
+// (benchmarks/bench_adam.py, profiles/r5/optim_grid_cap.jsonl).
+unsigned opt_grid(int64_t n) { return stream_grid((n + 3) / 4); }
 
 void sgd_step(uintptr_t p, uintptr_t g, int g_dtype, uintptr_t mom_buf, uintptr_t p_lp, int lp_dtype,
               int64_t n, float lr, float momentum, float dampening, float wd, bool nesterov,
