@@ -126,6 +126,34 @@ def test_layernorm_fwd_bwd(shape, dt):
     torch.testing.assert_close(b.grad, br.grad, **gt)
 
 
+@pytest.mark.parametrize("shape", [(8192, 768), (10240, 256), (1000, 1024), (5, 12)])
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+def test_layernorm_bwd_4_and_8_waves_agree(shape, dt):
+    """The 8-wave LayerNorm backward (the default for rows <= 1024) against the 4-wave one: dx
+    bitwise (same per-row arithmetic), dgamma / dbeta to fp32 summation order."""
+    from vodascheduler_amd.ops import _native
+
+    h = _native.hip()
+    torch.manual_seed(0)
+    n = shape[-1]
+    x = torch.randn(shape, device=DEV).mul(2).to(dt)
+    w = torch.randn(n, device=DEV)
+    b = torch.randn(n, device=DEV)
+    dy = torch.randn(shape, device=DEV).to(dt)
+    outs = []
+    try:
+        for waves in (4, 8):
+            h.layernorm_set_bwd_waves(waves)
+            xx, ww, bb = (t.clone().requires_grad_() for t in (x, w, b))
+            layer_norm(xx, ww, bb, 1e-5).backward(dy)
+            outs.append((xx.grad, ww.grad, bb.grad))
+    finally:
+        h.layernorm_set_bwd_waves(8)
+    assert torch.equal(outs[0][0], outs[1][0])
+    for a, c in zip(outs[0][1:], outs[1][1:]):
+        torch.testing.assert_close(a, c, rtol=1e-5, atol=1e-4)
+
+
 @pytest.mark.parametrize("shape", [(512, 768), (3, 5, 1024), (7, 12)])
 @pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
 def test_layernorm_fused_residual(shape, dt):
