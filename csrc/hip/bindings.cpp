@@ -74,6 +74,7 @@ PYBIND11_MODULE(_vodahip, m) {
   m.def("subsample2d", &subsample2d);
   m.def("conv3x3_c64_wgrad_workspace_floats", &conv3x3_c64_wgrad_workspace_floats);
   m.def("conv3x3_c64_wgrad", &conv3x3_c64_wgrad);
+  m.def("filter_flip_t", &filter_flip_t);
   m.def("stem_partial_rows", &stem_partial_rows);
   m.def("stem_pack", &stem_pack);
   m.def("stem_conv_fwd", &stem_conv_fwd);

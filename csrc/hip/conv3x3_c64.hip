@@ -483,4 +483,58 @@ void conv3x3_c64_wgrad(uintptr_t x, uintptr_t dy, uintptr_t dw, int64_t s0, int6
   check_launch();
 }
 
+// ---- flipped, channel-transposed filter for the input gradient as a forward convolution
+// (ops/conv3x3.dgrad_as_forward): wt[ci][co][kh][kw] = w[co][ci][K-1-kh][K-1-kw], written
+// channels_last ([ci][kh][kw][co] in memory) and in the activations' dtype -- one launch instead
+// of a flip, a layout copy and (under autocast) a cast.  The filter is at most a few MB (L2).
+namespace {
+// one 32 (co) x 32 (ci) tile of one filter tap per block, transposed through LDS: the reads run
+// along ci (contiguous in a channels_last filter), the writes along co (contiguous in the output)
+template <typename IT, typename OT>
+__global__ __launch_bounds__(256) void filter_flip_t_kernel(const IT* __restrict__ w, int64_t s0, int64_t s1,
+                                                            int64_t s2, int64_t s3, OT* __restrict__ out, int Cout,
+                                                            int Cin, int K) {
+  __shared__ float tile[32][33];
+  const int co0 = blockIdx.x * 32, ci0 = blockIdx.y * 32;
+  const int kh = int(blockIdx.z) / K, kw = int(blockIdx.z) - (int(blockIdx.z) / K) * K;  // source tap
+  const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int co = co0 + ty + 8 * j, ci = ci0 + tx;
+    tile[ty + 8 * j][tx] = (co < Cout && ci < Cin) ? Vec4<IT>::load1(w, co * s0 + ci * s1 + kh * s2 + kw * s3) : 0.f;
+  }
+  __syncthreads();
+  // destination tap (K-1-kh, K-1-kw); out memory order [ci][kh'][kw'][co]
+  const int64_t tap = int64_t(K - 1 - kh) * K + (K - 1 - kw);
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int ci = ci0 + ty + 8 * j, co = co0 + tx;
+    if (ci < Cin && co < Cout) Vec4<OT>::store1(out, (int64_t(ci) * K * K + tap) * Cout + co, tile[tx][ty + 8 * j]);
+  }
+}
+}  // namespace
+
+void filter_flip_t(uintptr_t w, int in_dt, int64_t s0, int64_t s1, int64_t s2, int64_t s3, uintptr_t out,
+                   int out_dt, int Cout, int Cin, int K, uintptr_t stream) {
+  VODA_CHECK(Cout > 0 && Cin > 0 && K > 0, "filter_flip_t: empty filter");
+  VODA_CHECK((in_dt == kF32 || in_dt == kBF16) && (out_dt == kF32 || out_dt == kBF16),
+             "filter_flip_t: fp32 or bf16");
+  const dim3 grid(unsigned((Cout + 31) / 32), unsigned((Cin + 31) / 32), unsigned(K * K));
+  hipStream_t s = as_stream(stream);
+  auto go = [&](auto it, auto ot) {
+    using IT = decltype(it);
+    using OT = decltype(ot);
+    hipLaunchKernelGGL((filter_flip_t_kernel<IT, OT>), grid, dim3(256), 0, s, reinterpret_cast<const IT*>(w), s0, s1,
+                       s2, s3, reinterpret_cast<OT*>(out), Cout, Cin, K);
+  };
+  if (in_dt == kF32) {
+    if (out_dt == kF32) go(float{}, float{});
+    else go(float{}, BF16{});
+  } else {
+    if (out_dt == kF32) go(BF16{}, float{});
+    else go(BF16{}, BF16{});
+  }
+  check_launch();
+}
+
 }  // namespace voda

@@ -138,6 +138,8 @@ void gemm_bnstats(uintptr_t x, uintptr_t w, uintptr_t y, uintptr_t part, int64_t
 
 // ---- 3x3 / stride-1 conv weight gradient at 64 -> 64 channels (conv3x3_c64.hip) ----
 int64_t conv3x3_c64_wgrad_workspace_floats(int N, int H);
+void filter_flip_t(uintptr_t w, int in_dt, int64_t s0, int64_t s1, int64_t s2, int64_t s3, uintptr_t out,
+                   int out_dt, int Cout, int Cin, int K, uintptr_t stream);
 void conv3x3_c64_wgrad(uintptr_t x, uintptr_t dy, uintptr_t dw, int64_t s0, int64_t s1, int64_t s2, int64_t s3,
                        uintptr_t ws, int N, int H, int W, bool accumulate, int out_dt, uintptr_t stream,
                        int in_dt);  // in_dt: bf16 or fp32 activations

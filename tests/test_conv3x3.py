@@ -120,6 +120,24 @@ def test_dgrad_as_forward_matches_conv2d_input(k, pad):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("k", [3, 1, 5])
+@pytest.mark.parametrize("wdt,odt", [(torch.float32, torch.float32), (torch.float32, torch.bfloat16),
+                                     (torch.bfloat16, torch.bfloat16)])
+@pytest.mark.parametrize("cl", [True, False])
+def test_flipped_filter_kernel_matches_torch(k, wdt, odt, cl):
+    """One-launch flipped, channel-transposed filter (filter_flip_t) == the torch composition,
+    bitwise, for channels_last and contiguous weights."""
+    torch.manual_seed(k)
+    w = torch.randn(48, 40, k, k, device="cuda").to(wdt)
+    if cl:
+        w = w.contiguous(memory_format=torch.channels_last)
+    got = C.flipped_filter(w, odt)
+    want = w.transpose(0, 1).flip(2, 3).to(odt)
+    assert got.shape == want.shape and got.is_contiguous(memory_format=torch.channels_last)
+    assert torch.equal(got, want)
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("cin,cout", [(64, 64), (128, 128)])
 def test_convkxk_dgrad_forward_path_matches_autograd(monkeypatch, cin, cout):
     """The ConvKxK layer with VODA_CONV_DGRAD_FWD on: bf16 input gradient == stock autograd's

@@ -92,8 +92,24 @@ def dgrad_as_forward(dy: torch.Tensor, weight: torch.Tensor, padding: int) -> to
     """Input gradient of a stride-1 KxK convolution as the forward convolution of ``dy`` with
     the flipped, channel-transposed filter (channels_last in, channels_last out)."""
     k = weight.shape[-1]
-    wt = weight.transpose(0, 1).flip(2, 3).contiguous(memory_format=torch.channels_last)
-    return F.conv2d(dy, wt, None, 1, k - 1 - padding)
+    return F.conv2d(dy, flipped_filter(weight, dy.dtype), None, 1, k - 1 - padding)
+
+
+def flipped_filter(weight: torch.Tensor, dtype: torch.dtype | None = None) -> torch.Tensor:
+    """``weight.transpose(0, 1).flip(2, 3)`` as a channels_last tensor of ``dtype`` (default the
+    weight's): on GPU one HIP launch (csrc/hip/conv3x3_c64.hip filter_flip_t) instead of a flip,
+    a layout copy and, under autocast, a cast."""
+    dtype = dtype or weight.dtype
+    co, ci, kh, kw = weight.shape
+    ok = (weight.is_cuda and kh == kw and weight.dtype in (torch.float32, torch.bfloat16)
+          and dtype in (torch.float32, torch.bfloat16))
+    if not ok:
+        return weight.transpose(0, 1).flip(2, 3).contiguous(memory_format=torch.channels_last).to(dtype)
+    out = torch.empty((ci, co, kh, kw), dtype=dtype, device=weight.device, memory_format=torch.channels_last)
+    s0, s1, s2, s3 = weight.stride()
+    N.hip().filter_flip_t(weight.data_ptr(), N.dtype_code(weight.dtype), s0, s1, s2, s3, out.data_ptr(),
+                          N.dtype_code(dtype), co, ci, kh, N.stream_of(weight))
+    return out
 
 
 def dgrad_fwd_ok(weight: torch.Tensor, stride: int, padding: int) -> bool:
