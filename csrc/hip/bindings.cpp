@@ -75,6 +75,9 @@ PYBIND11_MODULE(_vodahip, m) {
   m.def("conv3x3_c64_wgrad_workspace_floats", &conv3x3_c64_wgrad_workspace_floats);
   m.def("conv3x3_c64_wgrad", &conv3x3_c64_wgrad);
   m.def("filter_flip_t", &filter_flip_t);
+  m.def("wino_f23_supported", &wino_f23_supported);
+  m.def("wino_f23_filter", &wino_f23_filter);
+  m.def("wino_f23_fwd", &wino_f23_fwd);
   m.def("stem_partial_rows", &stem_partial_rows);
   m.def("stem_pack", &stem_pack);
   m.def("stem_conv_fwd", &stem_conv_fwd);

@@ -1,0 +1,237 @@
+// Winograd F(2x2, 3x3) forward convolution, fp32, on the f32-input MFMA of gfx950
+// (v_mfma_f32_32x32x2_f32), for ResNet-50's 3x3 stride-1 pad-1 layers in NHWC.
+//
+// A 2x2 output tile needs a 4x4 input patch d; per channel the patch is transformed to
+// V = B^T d B, the filter to U = G g G^T, and the 16 products M = sum_ci V[p] U[p] (one GEMM per
+// transform position p = 4r + c, over the input channels) are transformed back, Y = A^T M A.
+// The 16 GEMMs do 16 x 2 x tiles x Cin x Cout FLOPs: 2.25x fewer than the direct convolution
+// (the igemm MIOpen runs: 59.2 GF per ResNet-50 3x3 layer at batch 256).  Nothing transformed
+// goes to HBM (unfused, the 4x-expanded V and M tensors would cost more traffic than the FLOPs
+// save):
+//   * a workgroup (4 waves) owns 32 consecutive tiles x 32 output channels;
+//   * per 32-channel chunk every thread loads one tile's 4x4 patch of 4 channels (16 float4,
+//     zero outside the image), transforms it in registers and writes V[p][tile][ci] to LDS;
+//   * wave w owns positions 4w .. 4w+3: its MFMAs read V as 16-byte LDS rows (lane half h takes
+//     ci = 8q + 4h + s for MFMA s = 0..3, the permuted-k order of conv1x1_f32.hip) and U as
+//     16-byte global rows of the pre-transformed filter U[p][co][ci] (L2-resident, <= 16 MB);
+//   * after the last chunk the 16 accumulators of every (tile, channel) meet in LDS and each
+//     thread applies A^T M A to four of them and stores the 2x2 outputs.
+// The filter transform (wino_f23_filter) runs once per use; the weights change every step.
+#include "common.h"
+#include "ops.h"
+
+namespace voda {
+
+namespace {
+
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+__device__ __forceinline__ f32x16 wmfma(float a, float b, f32x16 c) {
+  return __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, c, 0, 0, 0);
+}
+
+constexpr int kWT = 32;           // tiles per workgroup
+constexpr int kWN = 32;           // output channels per workgroup
+constexpr int kWK = 32;           // input channels per chunk
+constexpr int kWP = kWK + 4;      // LDS row pitch of V (floats)
+constexpr int kWThreads = 256;
+
+struct WinoArgs {
+  const float* x;  // [N][H][W][C]
+  const float* u;  // [16][Co][C]
+  float* y;        // [N][H][W][Co]
+  int N, H, W, C, Co;
+  int th, tw;      // tiles per column / row
+  int64_t T;       // N * th * tw
+};
+
+__global__ __launch_bounds__(kWThreads, 2) void wino_f23_fwd_kernel(WinoArgs a) {
+  __shared__ __attribute__((aligned(16))) float lds[16 * kWT * kWP];  // V chunk, then M exchange
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, lc = lane & 31, lh = lane >> 5;
+  const int64_t t0 = int64_t(blockIdx.x) * kWT;
+  const int co0 = blockIdx.y * kWN;
+
+  // this thread's staging task: tile t0 + (tid & 31), channels 4 * (tid >> 5) .. + 3 of the chunk
+  const int st = tid & 31, sq = tid >> 5;
+  const int64_t tg = t0 + st;
+  const bool tok = tg < a.T;
+  const int64_t tt = tok ? tg : 0;
+  const int n = int(tt / (int64_t(a.th) * a.tw));
+  const int trem = int(tt - int64_t(n) * a.th * a.tw);
+  const int ty = trem / a.tw, tx = trem - (trem / a.tw) * a.tw;
+  const int h0 = 2 * ty - 1, w0 = 2 * tx - 1;
+  const float* xn = a.x + int64_t(n) * a.H * a.W * a.C;
+
+  f32x16 acc[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) acc[j] = f32x16{};
+
+  // 4x4 patch (4 channels) of this thread's tile, chunk c0 (zero outside the image)
+  float4 d[16];
+  auto load_patch = [&](int c0) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int hh = h0 + i, ww = w0 + j;
+        const bool ok = tok && hh >= 0 && hh < a.H && ww >= 0 && ww < a.W;
+        d[4 * i + j] = ok ? *reinterpret_cast<const float4*>(xn + (int64_t(hh) * a.W + ww) * a.C + c0 + 4 * sq)
+                          : make_float4(0.f, 0.f, 0.f, 0.f);
+      }
+  };
+  load_patch(0);
+  for (int c0 = 0; c0 < a.C; c0 += kWK) {
+    // U rows of this wave's first position for the chunk (issued before the barriers; the next
+    // position's rows load during the MFMAs of the current one)
+    const float* ub = a.u + (int64_t(4 * wave) * a.Co + co0 + lc) * a.C + c0 + 4 * lh;
+    const int64_t ups = int64_t(a.Co) * a.C;  // floats per position
+    float4 bc[kWK / 8], bn[kWK / 8];
+#pragma unroll
+    for (int q = 0; q < kWK / 8; ++q) bc[q] = *reinterpret_cast<const float4*>(ub + 8 * q);
+    // ---- V = B^T d B in registers, in place (rows, then columns)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const float4 a0 = d[j], a1 = d[4 + j], a2 = d[8 + j], a3 = d[12 + j];
+      d[j] = make_float4(a0.x - a2.x, a0.y - a2.y, a0.z - a2.z, a0.w - a2.w);
+      d[4 + j] = make_float4(a1.x + a2.x, a1.y + a2.y, a1.z + a2.z, a1.w + a2.w);
+      d[8 + j] = make_float4(a2.x - a1.x, a2.y - a1.y, a2.z - a1.z, a2.w - a1.w);
+      d[12 + j] = make_float4(a1.x - a3.x, a1.y - a3.y, a1.z - a3.z, a1.w - a3.w);
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const float4 a0 = d[4 * i], a1 = d[4 * i + 1], a2 = d[4 * i + 2], a3 = d[4 * i + 3];
+      d[4 * i] = make_float4(a0.x - a2.x, a0.y - a2.y, a0.z - a2.z, a0.w - a2.w);
+      d[4 * i + 1] = make_float4(a1.x + a2.x, a1.y + a2.y, a1.z + a2.z, a1.w + a2.w);
+      d[4 * i + 2] = make_float4(a2.x - a1.x, a2.y - a1.y, a2.z - a1.z, a2.w - a1.w);
+      d[4 * i + 3] = make_float4(a1.x - a3.x, a1.y - a3.y, a1.z - a3.z, a1.w - a3.w);
+    }
+    __syncthreads();  // the previous chunk's V reads are done
+#pragma unroll
+    for (int p = 0; p < 16; ++p) *reinterpret_cast<float4*>(lds + (p * kWT + st) * kWP + 4 * sq) = d[p];
+    __syncthreads();
+    if (c0 + kWK < a.C) load_patch(c0 + kWK);  // in flight during this chunk's MFMAs
+    // ---- 4 positions per wave: acc[j] (tiles x co) += V[p] (tiles x ci) . U[p] (ci x co)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int p = 4 * wave + j;
+      if (j < 3) {
+#pragma unroll
+        for (int q = 0; q < kWK / 8; ++q) bn[q] = *reinterpret_cast<const float4*>(ub + (j + 1) * ups + 8 * q);
+      }
+#pragma unroll
+      for (int q = 0; q < kWK / 8; ++q) {
+        const float4 av = *reinterpret_cast<const float4*>(lds + (p * kWT + lc) * kWP + 8 * q + 4 * lh);
+        acc[j] = wmfma(av.x, bc[q].x, acc[j]);
+        acc[j] = wmfma(av.y, bc[q].y, acc[j]);
+        acc[j] = wmfma(av.z, bc[q].z, acc[j]);
+        acc[j] = wmfma(av.w, bc[q].w, acc[j]);
+      }
+#pragma unroll
+      for (int q = 0; q < kWK / 8; ++q) bc[q] = bn[q];
+    }
+  }
+  __syncthreads();
+  // ---- exchange: M[p][tile][co] (pitch 32) in LDS
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int p = 4 * wave + j;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int row = (r & 3) + 8 * (r >> 2) + 4 * lh;
+      lds[(p * kWT + row) * kWN + lc] = acc[j][r];
+    }
+  }
+  __syncthreads();
+  // ---- inverse transform: Y = A^T M A, thread -> channel tid & 31, tiles tid >> 5 + 8k
+  const int co = tid & 31;
+#pragma unroll
+  for (int k = 0; k < kWT / 8; ++k) {
+    const int tl = (tid >> 5) + 8 * k;
+    const int64_t tgo = t0 + tl;
+    if (tgo >= a.T) continue;
+    float m[16];
+#pragma unroll
+    for (int p = 0; p < 16; ++p) m[p] = lds[(p * kWT + tl) * kWN + co];
+    float r0[4], r1[4];  // A^T M: rows
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      r0[c] = m[c] + m[4 + c] + m[8 + c];
+      r1[c] = m[4 + c] - m[8 + c] - m[12 + c];
+    }
+    const float y00 = r0[0] + r0[1] + r0[2], y01 = r0[1] - r0[2] - r0[3];
+    const float y10 = r1[0] + r1[1] + r1[2], y11 = r1[1] - r1[2] - r1[3];
+    const int no = int(tgo / (int64_t(a.th) * a.tw));
+    const int rem = int(tgo - int64_t(no) * a.th * a.tw);
+    const int oy = 2 * (rem / a.tw), ox = 2 * (rem - (rem / a.tw) * a.tw);
+    float* yb = a.y + (int64_t(no) * a.H * a.W) * a.Co + co0 + co;
+    yb[(int64_t(oy) * a.W + ox) * a.Co] = y00;
+    if (ox + 1 < a.W) yb[(int64_t(oy) * a.W + ox + 1) * a.Co] = y01;
+    if (oy + 1 < a.H) {
+      yb[(int64_t(oy + 1) * a.W + ox) * a.Co] = y10;
+      if (ox + 1 < a.W) yb[(int64_t(oy + 1) * a.W + ox + 1) * a.Co] = y11;
+    }
+  }
+}
+
+// U[p][co][ci] = (G g G^T)[p] for g = w[co][ci] (3x3, any strides); one thread per (co, ci).
+// flip: the filter of the input gradient as a forward convolution, g = w[ci][co] rotated by 180
+// degrees (w is the layer's [Cout][Cin] filter; here co runs over its Cin and ci over its Cout).
+__global__ __launch_bounds__(256) void wino_f23_filter_kernel(const float* __restrict__ w, int64_t s0, int64_t s1,
+                                                              int64_t s2, int64_t s3, float* __restrict__ u, int Co,
+                                                              int C, int flip) {
+  const int64_t i = int64_t(blockIdx.x) * 256 + threadIdx.x;
+  if (i >= int64_t(Co) * C) return;
+  const int co = int(i / C), ci = int(i - int64_t(co) * C);
+  float g[3][3];
+#pragma unroll
+  for (int r = 0; r < 3; ++r)
+#pragma unroll
+    for (int c = 0; c < 3; ++c)
+      g[r][c] = flip ? w[ci * s0 + co * s1 + (2 - r) * s2 + (2 - c) * s3] : w[co * s0 + ci * s1 + r * s2 + c * s3];
+  float t[4][3];  // G g: G = [[1,0,0],[.5,.5,.5],[.5,-.5,.5],[0,0,1]]
+#pragma unroll
+  for (int c = 0; c < 3; ++c) {
+    t[0][c] = g[0][c];
+    t[1][c] = 0.5f * (g[0][c] + g[1][c] + g[2][c]);
+    t[2][c] = 0.5f * (g[0][c] - g[1][c] + g[2][c]);
+    t[3][c] = g[2][c];
+  }
+  const int64_t pstride = int64_t(Co) * C;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {  // (G g) G^T
+    const float v0 = t[r][0], v1 = 0.5f * (t[r][0] + t[r][1] + t[r][2]), v2 = 0.5f * (t[r][0] - t[r][1] + t[r][2]),
+                v3 = t[r][2];
+    u[(4 * r + 0) * pstride + i] = v0;
+    u[(4 * r + 1) * pstride + i] = v1;
+    u[(4 * r + 2) * pstride + i] = v2;
+    u[(4 * r + 3) * pstride + i] = v3;
+  }
+}
+
+}  // namespace
+
+bool wino_f23_supported(int C, int Co) { return C > 0 && Co > 0 && C % kWK == 0 && Co % kWN == 0; }
+
+void wino_f23_filter(uintptr_t w, int64_t s0, int64_t s1, int64_t s2, int64_t s3, uintptr_t u, int Co, int C,
+                     bool flip, uintptr_t stream) {
+  VODA_CHECK(Co > 0 && C > 0, "wino_f23_filter: empty filter");
+  const int64_t n = int64_t(Co) * C;
+  hipLaunchKernelGGL(wino_f23_filter_kernel, dim3(unsigned((n + 255) / 256)), dim3(256), 0, as_stream(stream),
+                     reinterpret_cast<const float*>(w), s0, s1, s2, s3, reinterpret_cast<float*>(u), Co, C,
+                     int(flip));
+  check_launch();
+}
+
+void wino_f23_fwd(uintptr_t x, uintptr_t u, uintptr_t y, int N, int H, int W, int C, int Co, uintptr_t stream) {
+  VODA_CHECK(N > 0 && H > 0 && W > 0, "wino_f23_fwd: empty input");
+  VODA_CHECK(wino_f23_supported(C, Co), "wino_f23_fwd: channels must be multiples of 32");
+  VODA_CHECK(x % 16 == 0 && u % 16 == 0 && y % 4 == 0, "wino_f23_fwd: misaligned operands");
+  WinoArgs a{reinterpret_cast<const float*>(x), reinterpret_cast<const float*>(u), reinterpret_cast<float*>(y),
+             N, H, W, C, Co, (H + 1) / 2, (W + 1) / 2, 0};
+  a.T = int64_t(N) * a.th * a.tw;
+  const dim3 grid(unsigned((a.T + kWT - 1) / kWT), unsigned(Co / kWN));
+  hipLaunchKernelGGL(wino_f23_fwd_kernel, grid, dim3(kWThreads), 0, as_stream(stream), a);
+  check_launch();
+}
+
+}  // namespace voda

@@ -1,0 +1,40 @@
+"""Winograd F(2x2, 3x3) fp32 convolution (csrc/hip/winograd_f32.hip) against an fp64 PyTorch
+reference: ResNet-50 3x3 shapes, odd sizes (ragged last tile), tile counts off the 32-tile
+workgroup, channel counts that are multiples of 32, channels_last and contiguous filters."""
+import pytest
+import torch
+import torch.nn.functional as F
+
+from vodascheduler_amd.ops import winograd as Wg
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize("n,c,co,h,w", [(2, 64, 64, 56, 56), (3, 128, 96, 28, 28), (4, 256, 256, 14, 14),
+                                        (5, 512, 512, 7, 7), (1, 32, 32, 5, 9), (3, 64, 32, 1, 1)])
+@pytest.mark.parametrize("wcl", [True, False])
+def test_wino_f23_matches_fp64(n, c, co, h, w, wcl):
+    torch.manual_seed(c + h)
+    x = torch.randn(n, c, h, w, device="cuda").contiguous(memory_format=torch.channels_last)
+    wt = torch.randn(co, c, 3, 3, device="cuda") / (3 * c ** 0.5)
+    if wcl:
+        wt = wt.contiguous(memory_format=torch.channels_last)
+    assert Wg.supported(x, wt)
+    y = Wg.conv3x3_wino(x, wt)
+    ref = F.conv2d(x.double(), wt.double(), None, 1, 1)
+    rel = ((y.double() - ref).norm() / ref.norm()).item()
+    assert rel < 2e-6, rel
+    assert (y.double() - ref).abs().max().item() < 1e-4
+
+
+@pytest.mark.parametrize("n,c,co,h", [(2, 64, 64, 56), (3, 256, 128, 14), (2, 512, 512, 7), (1, 64, 32, 5)])
+def test_wino_f23_input_gradient_matches_fp64(n, c, co, h):
+    """flip mode: dX of a 3x3 stride-1 pad-1 layer with filter [co][c] from dY [n][co][h][h]."""
+    torch.manual_seed(c + h)
+    dy = torch.randn(n, co, h, h, device="cuda").contiguous(memory_format=torch.channels_last)
+    wt = (torch.randn(co, c, 3, 3, device="cuda") / (3 * c ** 0.5)).contiguous(memory_format=torch.channels_last)
+    assert Wg.supported(dy, wt, flip=True)
+    dx = Wg.conv3x3_wino(dy, wt, flip=True)
+    ref = torch.nn.grad.conv2d_input((n, c, h, h), wt.double(), dy.double(), stride=1, padding=1)
+    rel = ((dx.double() - ref).norm() / ref.norm()).item()
+    assert rel < 2e-6, rel

@@ -28,10 +28,14 @@ import torch.nn.functional as F
 
 from . import _native as N
 from . import wgrad as W
+from . import winograd as Wg
 from ..utils.flat import FOLD_CAST, flat_grad
 from .conv1x1 import _direct, _ready
 
 USE_CONV_WGRAD = True
+# USE_WINOGRAD (module switch): fp32 3x3 stride-1 pad-1 forwards and input gradients (as forward
+# convolutions) on the own Winograd F(2x2, 3x3) kernel (ops/winograd.py) instead of MIOpen
+USE_WINOGRAD = True
 # DGRAD_FWD (module switch, default on): the input gradient of a stride-1 KxK convolution runs as a
 # FORWARD convolution of dy with the transposed, spatially flipped filter
 #     dX[n, ci, h, w] = sum_{co, kh, kw} dY[n, co, h - kh + p, w - kw + p] * W[co, ci, kh, kw]
@@ -173,7 +177,10 @@ def supported(dy: torch.Tensor, x: torch.Tensor, gw: torch.Tensor) -> bool:
 class _ConvKxKFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, weight, stride: int, padding: int, kernel_wgrad: bool = True):
-        y = F.conv2d(x, weight, None, stride, padding)
+        if USE_WINOGRAD and Wg.supported(x, weight, stride, padding):
+            y = Wg.conv3x3_wino(x, weight)
+        else:
+            y = F.conv2d(x, weight, None, stride, padding)
         ctx.save_for_backward(x, weight)
         ctx.conf = (stride, padding, kernel_wgrad)
         return y
@@ -185,7 +192,9 @@ class _ConvKxKFn(torch.autograd.Function):
         if not dy.is_contiguous(memory_format=torch.channels_last):
             dy = dy.contiguous(memory_format=torch.channels_last)
         dx = None
-        if ctx.needs_input_grad[0] and dgrad_fwd_ok(weight, stride, padding):
+        if ctx.needs_input_grad[0] and USE_WINOGRAD and Wg.supported(dy, weight, stride, padding, flip=True):
+            dx = Wg.conv3x3_wino(dy, weight, flip=True)
+        elif ctx.needs_input_grad[0] and dgrad_fwd_ok(weight, stride, padding):
             dx = dgrad_as_forward(dy, weight, padding)
         elif ctx.needs_input_grad[0]:
             dx = torch.ops.aten.convolution_backward(dy, x, weight, None, [stride, stride], [padding, padding],

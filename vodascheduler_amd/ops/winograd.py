@@ -1,0 +1,48 @@
+"""fp32 3x3 stride-1 pad-1 convolution as Winograd F(2x2, 3x3) on the f32 MFMA
+(csrc/hip/winograd_f32.hip): 2.25x fewer multiply-adds than the direct / implicit-GEMM
+convolution, transforms fused into the kernel (nothing transformed goes to HBM).
+
+``conv3x3_wino(x, w)`` takes NHWC (channels_last) fp32 activations and any-layout fp32 filters;
+the filter transform U = G g G^T runs per call (the weights change every step).
+"""
+from __future__ import annotations
+
+import torch
+import torch.nn.functional as F
+
+from . import _native as N
+
+
+def supported(x: torch.Tensor, w: torch.Tensor, stride: int = 1, padding: int = 1, flip: bool = False) -> bool:
+    """fp32 NHWC x, fp32 3x3 filter, stride 1, pad 1, channels multiples of 32.  ``flip``: x is a
+    layer's output gradient and w that layer's filter (the input gradient as a forward conv)."""
+    cin, cout = (int(w.shape[0]), int(w.shape[1])) if flip else (int(w.shape[1]), int(w.shape[0]))
+    return (x.is_cuda and x.dtype == torch.float32 and w.dtype == torch.float32 and x.dim() == 4
+            and tuple(w.shape[2:]) == (3, 3) and stride == 1 and padding == 1 and x.shape[1] == cin
+            and x.is_contiguous(memory_format=torch.channels_last) and x.data_ptr() % 16 == 0
+            and N.hip().wino_f23_supported(cin, cout))
+
+
+def filter_transform(w: torch.Tensor, flip: bool = False) -> torch.Tensor:
+    """U [16][Cout][Cin] = G g G^T per (co, ci); ``flip``: of the 180-degree-rotated,
+    channel-transposed filter (Cout and Cin of the result are w's Cin and Cout)."""
+    co, ci = (int(w.shape[1]), int(w.shape[0])) if flip else (int(w.shape[0]), int(w.shape[1]))
+    u = torch.empty(16, co, ci, dtype=torch.float32, device=w.device)
+    s0, s1, s2, s3 = w.stride()
+    N.hip().wino_f23_filter(w.data_ptr(), s0, s1, s2, s3, u.data_ptr(), co, ci, bool(flip), N.stream_of(w))
+    return u
+
+
+def conv3x3_wino(x: torch.Tensor, w: torch.Tensor, u: torch.Tensor | None = None, flip: bool = False) -> torch.Tensor:
+    """y = conv2d(x, w, padding=1) for NHWC fp32 x; ``flip``: dX = conv2d(dY, w^T rotated 180,
+    padding=1), the input gradient of a 3x3 stride-1 pad-1 layer.  CPU / unsupported: F.conv2d."""
+    if not supported(x, w, flip=flip):
+        wf = w.transpose(0, 1).flip(2, 3) if flip else w
+        return F.conv2d(x, wf, None, 1, 1)
+    n, c, h, wd = x.shape
+    co = int(w.shape[1]) if flip else int(w.shape[0])
+    if u is None:
+        u = filter_transform(w, flip)
+    y = torch.empty((n, co, h, wd), dtype=torch.float32, device=x.device, memory_format=torch.channels_last)
+    N.hip().wino_f23_fwd(x.data_ptr(), u.data_ptr(), y.data_ptr(), n, h, wd, c, co, N.stream_of(x))
+    return y
