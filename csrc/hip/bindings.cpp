@@ -77,6 +77,7 @@ PYBIND11_MODULE(_vodahip, m) {
   m.def("filter_flip_t", &filter_flip_t);
   m.def("wino_f23_supported", &wino_f23_supported);
   m.def("wino_f23_filter", &wino_f23_filter);
+  m.def("wino_f23_groups", &wino_f23_groups);
   m.def("wino_f23_fwd", &wino_f23_fwd);
   m.def("stem_partial_rows", &stem_partial_rows);
   m.def("stem_pack", &stem_pack);

@@ -20,6 +20,8 @@
 #include "common.h"
 #include "ops.h"
 
+#include <algorithm>
+
 namespace voda {
 
 namespace {
@@ -40,32 +42,35 @@ struct WinoArgs {
   const float* x;  // [N][H][W][C]
   const float* u;  // [16][Co][C]
   float* y;        // [N][H][W][Co]
+  float* part;     // [2][G][Co] BN partial sums (sum, sum of squares) of y, or null
   int N, H, W, C, Co;
   int th, tw;      // tiles per column / row
   int64_t T;       // N * th * tw
+  int G;           // workgroups along the tiles (gridDim.x); each walks tile blocks x, x + G, ...
 };
 
 __global__ __launch_bounds__(kWThreads, 2) void wino_f23_fwd_kernel(WinoArgs a) {
   __shared__ __attribute__((aligned(16))) float lds[16 * kWT * kWP];  // V chunk, then M exchange
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, lc = lane & 31, lh = lane >> 5;
-  const int64_t t0 = int64_t(blockIdx.x) * kWT;
   const int co0 = blockIdx.y * kWN;
+  const int64_t nblk = (a.T + kWT - 1) / kWT;
 
-  // this thread's staging task: tile t0 + (tid & 31), channels 4 * (tid >> 5) .. + 3 of the chunk
+  // this thread's staging task: tile (tid & 31) of the block, channels 4 * (tid >> 5) .. + 3
   const int st = tid & 31, sq = tid >> 5;
-  const int64_t tg = t0 + st;
-  const bool tok = tg < a.T;
-  const int64_t tt = tok ? tg : 0;
-  const int n = int(tt / (int64_t(a.th) * a.tw));
-  const int trem = int(tt - int64_t(n) * a.th * a.tw);
-  const int ty = trem / a.tw, tx = trem - (trem / a.tw) * a.tw;
-  const int h0 = 2 * ty - 1, w0 = 2 * tx - 1;
-  const float* xn = a.x + int64_t(n) * a.H * a.W * a.C;
-
-  f32x16 acc[4];
-#pragma unroll
-  for (int j = 0; j < 4; ++j) acc[j] = f32x16{};
-
+  bool tok = false;
+  int h0 = 0, w0 = 0;
+  const float* xn = a.x;
+  auto tile_setup = [&](int64_t blk) {
+    const int64_t tg = blk * kWT + st;
+    tok = tg < a.T;
+    const int64_t tt = tok ? tg : 0;
+    const int n = int(tt / (int64_t(a.th) * a.tw));
+    const int trem = int(tt - int64_t(n) * a.th * a.tw);
+    const int ty = trem / a.tw, tx = trem - (trem / a.tw) * a.tw;
+    h0 = 2 * ty - 1;
+    w0 = 2 * tx - 1;
+    xn = a.x + int64_t(n) * a.H * a.W * a.C;
+  };
   // 4x4 patch (4 channels) of this thread's tile, chunk c0 (zero outside the image)
   float4 d[16];
   auto load_patch = [&](int c0) {
@@ -79,97 +84,145 @@ __global__ __launch_bounds__(kWThreads, 2) void wino_f23_fwd_kernel(WinoArgs a) 
                           : make_float4(0.f, 0.f, 0.f, 0.f);
       }
   };
-  load_patch(0);
-  for (int c0 = 0; c0 < a.C; c0 += kWK) {
-    // U rows of this wave's first position for the chunk (issued before the barriers; the next
-    // position's rows load during the MFMAs of the current one)
-    const float* ub = a.u + (int64_t(4 * wave) * a.Co + co0 + lc) * a.C + c0 + 4 * lh;
-    const int64_t ups = int64_t(a.Co) * a.C;  // floats per position
-    float4 bc[kWK / 8], bn[kWK / 8];
+  const int64_t ups = int64_t(a.Co) * a.C;  // floats per transform position of U
+  float s1 = 0.f, s2 = 0.f;                 // BN statistics of channel co0 + (tid & 31)
+
+  int64_t blk = blockIdx.x;
+  if (blk < nblk) {
+    tile_setup(blk);
+    load_patch(0);
+  }
+  for (; blk < nblk; blk += a.G) {
+    f32x16 acc[4];
 #pragma unroll
-    for (int q = 0; q < kWK / 8; ++q) bc[q] = *reinterpret_cast<const float4*>(ub + 8 * q);
-    // ---- V = B^T d B in registers, in place (rows, then columns)
+    for (int j = 0; j < 4; ++j) acc[j] = f32x16{};
+    for (int c0 = 0; c0 < a.C; c0 += kWK) {
+      // U rows of this wave's first position for the chunk (issued before the barriers; the next
+      // position's rows load during the MFMAs of the current one)
+      const float* ub = a.u + (int64_t(4 * wave) * a.Co + co0 + lc) * a.C + c0 + 4 * lh;
+      float4 bc[kWK / 8], bn[kWK / 8];
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const float4 a0 = d[j], a1 = d[4 + j], a2 = d[8 + j], a3 = d[12 + j];
-      d[j] = make_float4(a0.x - a2.x, a0.y - a2.y, a0.z - a2.z, a0.w - a2.w);
-      d[4 + j] = make_float4(a1.x + a2.x, a1.y + a2.y, a1.z + a2.z, a1.w + a2.w);
-      d[8 + j] = make_float4(a2.x - a1.x, a2.y - a1.y, a2.z - a1.z, a2.w - a1.w);
-      d[12 + j] = make_float4(a1.x - a3.x, a1.y - a3.y, a1.z - a3.z, a1.w - a3.w);
+      for (int q = 0; q < kWK / 8; ++q) bc[q] = *reinterpret_cast<const float4*>(ub + 8 * q);
+      // ---- V = B^T d B in registers, in place (rows, then columns)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const float4 a0 = d[j], a1 = d[4 + j], a2 = d[8 + j], a3 = d[12 + j];
+        d[j] = make_float4(a0.x - a2.x, a0.y - a2.y, a0.z - a2.z, a0.w - a2.w);
+        d[4 + j] = make_float4(a1.x + a2.x, a1.y + a2.y, a1.z + a2.z, a1.w + a2.w);
+        d[8 + j] = make_float4(a2.x - a1.x, a2.y - a1.y, a2.z - a1.z, a2.w - a1.w);
+        d[12 + j] = make_float4(a1.x - a3.x, a1.y - a3.y, a1.z - a3.z, a1.w - a3.w);
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const float4 a0 = d[4 * i], a1 = d[4 * i + 1], a2 = d[4 * i + 2], a3 = d[4 * i + 3];
+        d[4 * i] = make_float4(a0.x - a2.x, a0.y - a2.y, a0.z - a2.z, a0.w - a2.w);
+        d[4 * i + 1] = make_float4(a1.x + a2.x, a1.y + a2.y, a1.z + a2.z, a1.w + a2.w);
+        d[4 * i + 2] = make_float4(a2.x - a1.x, a2.y - a1.y, a2.z - a1.z, a2.w - a1.w);
+        d[4 * i + 3] = make_float4(a1.x - a3.x, a1.y - a3.y, a1.z - a3.z, a1.w - a3.w);
+      }
+      __syncthreads();  // the previous chunk's V reads (or the previous block's M reads) are done
+#pragma unroll
+      for (int p = 0; p < 16; ++p) *reinterpret_cast<float4*>(lds + (p * kWT + st) * kWP + 4 * sq) = d[p];
+      __syncthreads();
+      // in flight during this chunk's MFMAs: the next chunk, or the next block's first chunk
+      if (c0 + kWK < a.C) {
+        load_patch(c0 + kWK);
+      } else if (blk + a.G < nblk) {
+        tile_setup(blk + a.G);
+        load_patch(0);
+      }
+      // ---- 4 positions per wave: acc[j] (tiles x co) += V[p] (tiles x ci) . U[p] (ci x co)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int p = 4 * wave + j;
+        if (j < 3) {
+#pragma unroll
+          for (int q = 0; q < kWK / 8; ++q) bn[q] = *reinterpret_cast<const float4*>(ub + (j + 1) * ups + 8 * q);
+        }
+#pragma unroll
+        for (int q = 0; q < kWK / 8; ++q) {
+          const float4 av = *reinterpret_cast<const float4*>(lds + (p * kWT + lc) * kWP + 8 * q + 4 * lh);
+          acc[j] = wmfma(av.x, bc[q].x, acc[j]);
+          acc[j] = wmfma(av.y, bc[q].y, acc[j]);
+          acc[j] = wmfma(av.z, bc[q].z, acc[j]);
+          acc[j] = wmfma(av.w, bc[q].w, acc[j]);
+        }
+#pragma unroll
+        for (int q = 0; q < kWK / 8; ++q) bc[q] = bn[q];
+      }
     }
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const float4 a0 = d[4 * i], a1 = d[4 * i + 1], a2 = d[4 * i + 2], a3 = d[4 * i + 3];
-      d[4 * i] = make_float4(a0.x - a2.x, a0.y - a2.y, a0.z - a2.z, a0.w - a2.w);
-      d[4 * i + 1] = make_float4(a1.x + a2.x, a1.y + a2.y, a1.z + a2.z, a1.w + a2.w);
-      d[4 * i + 2] = make_float4(a2.x - a1.x, a2.y - a1.y, a2.z - a1.z, a2.w - a1.w);
-      d[4 * i + 3] = make_float4(a1.x - a3.x, a1.y - a3.y, a1.z - a3.z, a1.w - a3.w);
-    }
-    __syncthreads();  // the previous chunk's V reads are done
-#pragma unroll
-    for (int p = 0; p < 16; ++p) *reinterpret_cast<float4*>(lds + (p * kWT + st) * kWP + 4 * sq) = d[p];
     __syncthreads();
-    if (c0 + kWK < a.C) load_patch(c0 + kWK);  // in flight during this chunk's MFMAs
-    // ---- 4 positions per wave: acc[j] (tiles x co) += V[p] (tiles x ci) . U[p] (ci x co)
+    // ---- exchange: M[p][tile][co] (pitch 32) in LDS
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       const int p = 4 * wave + j;
-      if (j < 3) {
 #pragma unroll
-        for (int q = 0; q < kWK / 8; ++q) bn[q] = *reinterpret_cast<const float4*>(ub + (j + 1) * ups + 8 * q);
+      for (int r = 0; r < 16; ++r) {
+        const int row = (r & 3) + 8 * (r >> 2) + 4 * lh;
+        lds[(p * kWT + row) * kWN + lc] = acc[j][r];
       }
+    }
+    __syncthreads();
+    // ---- inverse transform: Y = A^T M A, thread -> channel tid & 31, tiles tid >> 5 + 8k
+    const int co = tid & 31;
+    const int64_t t0 = blk * kWT;
 #pragma unroll
-      for (int q = 0; q < kWK / 8; ++q) {
-        const float4 av = *reinterpret_cast<const float4*>(lds + (p * kWT + lc) * kWP + 8 * q + 4 * lh);
-        acc[j] = wmfma(av.x, bc[q].x, acc[j]);
-        acc[j] = wmfma(av.y, bc[q].y, acc[j]);
-        acc[j] = wmfma(av.z, bc[q].z, acc[j]);
-        acc[j] = wmfma(av.w, bc[q].w, acc[j]);
+    for (int k = 0; k < kWT / 8; ++k) {
+      const int tl = (tid >> 5) + 8 * k;
+      const int64_t tgo = t0 + tl;
+      if (tgo >= a.T) continue;
+      float m[16];
+#pragma unroll
+      for (int p = 0; p < 16; ++p) m[p] = lds[(p * kWT + tl) * kWN + co];
+      float r0[4], r1[4];  // A^T M: rows
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        r0[c] = m[c] + m[4 + c] + m[8 + c];
+        r1[c] = m[4 + c] - m[8 + c] - m[12 + c];
       }
-#pragma unroll
-      for (int q = 0; q < kWK / 8; ++q) bc[q] = bn[q];
+      const float y00 = r0[0] + r0[1] + r0[2], y01 = r0[1] - r0[2] - r0[3];
+      const float y10 = r1[0] + r1[1] + r1[2], y11 = r1[1] - r1[2] - r1[3];
+      const int no = int(tgo / (int64_t(a.th) * a.tw));
+      const int rem = int(tgo - int64_t(no) * a.th * a.tw);
+      const int oy = 2 * (rem / a.tw), ox = 2 * (rem - (rem / a.tw) * a.tw);
+      float* yb = a.y + (int64_t(no) * a.H * a.W) * a.Co + co0 + co;
+      const bool xr = ox + 1 < a.W, yr = oy + 1 < a.H;
+      yb[(int64_t(oy) * a.W + ox) * a.Co] = y00;
+      s1 += y00;
+      s2 = fmaf(y00, y00, s2);
+      if (xr) {
+        yb[(int64_t(oy) * a.W + ox + 1) * a.Co] = y01;
+        s1 += y01;
+        s2 = fmaf(y01, y01, s2);
+      }
+      if (yr) {
+        yb[(int64_t(oy + 1) * a.W + ox) * a.Co] = y10;
+        s1 += y10;
+        s2 = fmaf(y10, y10, s2);
+        if (xr) {
+          yb[(int64_t(oy + 1) * a.W + ox + 1) * a.Co] = y11;
+          s1 += y11;
+          s2 = fmaf(y11, y11, s2);
+        }
+      }
     }
   }
+  if (a.part == nullptr) return;
+  // BN partials of this workgroup: the 8 threads of each channel through LDS, one row per x block
   __syncthreads();
-  // ---- exchange: M[p][tile][co] (pitch 32) in LDS
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const int p = 4 * wave + j;
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const int row = (r & 3) + 8 * (r >> 2) + 4 * lh;
-      lds[(p * kWT + row) * kWN + lc] = acc[j][r];
-    }
-  }
+  float* red = lds;
+  red[tid] = s1;
+  red[kWThreads + tid] = s2;
   __syncthreads();
-  // ---- inverse transform: Y = A^T M A, thread -> channel tid & 31, tiles tid >> 5 + 8k
-  const int co = tid & 31;
+  if (tid < kWN) {
+    float t1 = 0.f, t2 = 0.f;
 #pragma unroll
-  for (int k = 0; k < kWT / 8; ++k) {
-    const int tl = (tid >> 5) + 8 * k;
-    const int64_t tgo = t0 + tl;
-    if (tgo >= a.T) continue;
-    float m[16];
-#pragma unroll
-    for (int p = 0; p < 16; ++p) m[p] = lds[(p * kWT + tl) * kWN + co];
-    float r0[4], r1[4];  // A^T M: rows
-#pragma unroll
-    for (int c = 0; c < 4; ++c) {
-      r0[c] = m[c] + m[4 + c] + m[8 + c];
-      r1[c] = m[4 + c] - m[8 + c] - m[12 + c];
+    for (int g = 0; g < kWThreads / kWN; ++g) {
+      t1 += red[g * kWN + tid];
+      t2 += red[kWThreads + g * kWN + tid];
     }
-    const float y00 = r0[0] + r0[1] + r0[2], y01 = r0[1] - r0[2] - r0[3];
-    const float y10 = r1[0] + r1[1] + r1[2], y11 = r1[1] - r1[2] - r1[3];
-    const int no = int(tgo / (int64_t(a.th) * a.tw));
-    const int rem = int(tgo - int64_t(no) * a.th * a.tw);
-    const int oy = 2 * (rem / a.tw), ox = 2 * (rem - (rem / a.tw) * a.tw);
-    float* yb = a.y + (int64_t(no) * a.H * a.W) * a.Co + co0 + co;
-    yb[(int64_t(oy) * a.W + ox) * a.Co] = y00;
-    if (ox + 1 < a.W) yb[(int64_t(oy) * a.W + ox + 1) * a.Co] = y01;
-    if (oy + 1 < a.H) {
-      yb[(int64_t(oy + 1) * a.W + ox) * a.Co] = y10;
-      if (ox + 1 < a.W) yb[(int64_t(oy + 1) * a.W + ox + 1) * a.Co] = y11;
-    }
+    a.part[int64_t(blockIdx.x) * a.Co + co0 + tid] = t1;
+    a.part[int64_t(a.G) * a.Co + int64_t(blockIdx.x) * a.Co + co0 + tid] = t2;
   }
 }
 
@@ -222,14 +275,41 @@ void wino_f23_filter(uintptr_t w, int64_t s0, int64_t s1, int64_t s2, int64_t s3
   check_launch();
 }
 
-void wino_f23_fwd(uintptr_t x, uintptr_t u, uintptr_t y, int N, int H, int W, int C, int Co, uintptr_t stream) {
+int wino_cus() {
+  static int g = [] {
+    int dev = 0, cus = 256;
+    if (hipGetDevice(&dev) == hipSuccess) {
+      hipDeviceProp_t pr;
+      if (hipGetDeviceProperties(&pr, dev) == hipSuccess && pr.multiProcessorCount > 0) cus = pr.multiProcessorCount;
+    }
+    return cus;
+  }();
+  return g;
+}
+
+// workgroups along the tiles; the BN partials have one row per such workgroup.  With 64 input
+// channels (two chunks) a workgroup's fixed costs -- the first patch load, the exchange and the
+// stores -- are as long as its MFMAs, so two workgroups per CU walk several 32-tile blocks each and
+// prefetch the next block during the epilogue (499 vs 508 us per ResNet-50 stage-1 layer).  From
+// 128 channels on one block per workgroup balances better: a persistent grid left a one-block tail
+// (C = 256: 433 vs 402 us, profiles/r5/winograd_f23_vs_miopen.jsonl).
+int wino_f23_groups(int N, int H, int W, int C, int Co) {
+  const int64_t nblk = (int64_t(N) * ((H + 1) / 2) * ((W + 1) / 2) + kWT - 1) / kWT;
+  if (C >= 128) return int(nblk);
+  const int ncol = std::max(1, Co / kWN);
+  return int(std::max<int64_t>(1, std::min<int64_t>(nblk, (2 * wino_cus() + ncol - 1) / ncol)));
+}
+
+void wino_f23_fwd(uintptr_t x, uintptr_t u, uintptr_t y, uintptr_t part, int N, int H, int W, int C, int Co, int G,
+                  uintptr_t stream) {
   VODA_CHECK(N > 0 && H > 0 && W > 0, "wino_f23_fwd: empty input");
   VODA_CHECK(wino_f23_supported(C, Co), "wino_f23_fwd: channels must be multiples of 32");
-  VODA_CHECK(x % 16 == 0 && u % 16 == 0 && y % 4 == 0, "wino_f23_fwd: misaligned operands");
+  VODA_CHECK(x % 16 == 0 && u % 16 == 0 && y % 4 == 0 && part % 4 == 0, "wino_f23_fwd: misaligned operands");
+  VODA_CHECK(G == wino_f23_groups(N, H, W, C, Co), "wino_f23_fwd: group count mismatch");
   WinoArgs a{reinterpret_cast<const float*>(x), reinterpret_cast<const float*>(u), reinterpret_cast<float*>(y),
-             N, H, W, C, Co, (H + 1) / 2, (W + 1) / 2, 0};
+             reinterpret_cast<float*>(part), N, H, W, C, Co, (H + 1) / 2, (W + 1) / 2, 0, G};
   a.T = int64_t(N) * a.th * a.tw;
-  const dim3 grid(unsigned((a.T + kWT - 1) / kWT), unsigned(Co / kWN));
+  const dim3 grid(unsigned(G), unsigned(Co / kWN));
   hipLaunchKernelGGL(wino_f23_fwd_kernel, grid, dim3(kWThreads), 0, as_stream(stream), a);
   check_launch();
 }

@@ -38,3 +38,44 @@ def test_wino_f23_input_gradient_matches_fp64(n, c, co, h):
     ref = torch.nn.grad.conv2d_input((n, c, h, h), wt.double(), dy.double(), stride=1, padding=1)
     rel = ((dx.double() - ref).norm() / ref.norm()).item()
     assert rel < 2e-6, rel
+
+
+@pytest.mark.parametrize("n,c,co,h", [(4, 64, 64, 56), (3, 256, 256, 14), (5, 512, 512, 7), (2, 32, 64, 9)])
+def test_wino_f23_bn_partials(n, c, co, h):
+    """The epilogue's per-workgroup BN partial sums add up to the column sums of y and y^2."""
+    from vodascheduler_amd.ops.conv1x1 import StatsHolder
+
+    torch.manual_seed(h)
+    x = torch.randn(n, c, h, h, device="cuda").contiguous(memory_format=torch.channels_last)
+    wt = (torch.randn(co, c, 3, 3, device="cuda") / (3 * c ** 0.5)).contiguous(memory_format=torch.channels_last)
+    hd = StatsHolder()
+    y = Wg.conv3x3_wino(x, wt, holder=hd)
+    ws, G = hd.stats
+    part = ws[: 2 * G * co].view(2, G, co).double().sum(1)
+    yd = y.double().permute(0, 2, 3, 1).reshape(-1, co)
+    torch.testing.assert_close(part[0], yd.sum(0), rtol=1e-4, atol=1e-3)
+    torch.testing.assert_close(part[1], (yd * yd).sum(0), rtol=1e-4, atol=1e-3)
+
+
+def test_resnet_fp32_step_with_winograd_matches_miopen(monkeypatch):
+    """A small fp32 ResNet-50 training step with the Winograd 3x3 layers (and their BN statistics)
+    vs the same step on MIOpen: loss and every gradient agree to fp32 rounding."""
+    from vodascheduler_amd.models.resnet import resnet50
+    from vodascheduler_amd.ops import conv3x3 as C3
+
+    torch.manual_seed(0)
+    m = resnet50(num_classes=10).cuda().to(memory_format=torch.channels_last)
+    x = torch.randn(4, 3, 64, 64, device="cuda").contiguous(memory_format=torch.channels_last)
+    tgt = torch.randint(0, 10, (4,), device="cuda")
+
+    def run(wino):
+        monkeypatch.setattr(C3, "USE_WINOGRAD", wino)
+        m.zero_grad(set_to_none=True)
+        loss = torch.nn.functional.cross_entropy(m(x), tgt)
+        loss.backward()
+        return [loss.detach()] + [p.grad.clone() for p in m.parameters()]
+
+    a, b = run(True), run(False)
+    for i, (u, v) in enumerate(zip(a, b)):
+        rel = ((u.double() - v.double()).norm() / (v.double().norm() + 1e-12)).item()
+        assert rel < 1e-3, f"tensor {i}: {rel}"

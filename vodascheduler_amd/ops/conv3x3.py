@@ -36,6 +36,7 @@ USE_CONV_WGRAD = True
 # USE_WINOGRAD (module switch): fp32 3x3 stride-1 pad-1 forwards and input gradients (as forward
 # convolutions) on the own Winograd F(2x2, 3x3) kernel (ops/winograd.py) instead of MIOpen
 USE_WINOGRAD = True
+WINO_BN_STATS = True  # the Winograd epilogue also hands the following BN its partial statistics
 # DGRAD_FWD (module switch, default on): the input gradient of a stride-1 KxK convolution runs as a
 # FORWARD convolution of dy with the transposed, spatially flipped filter
 #     dX[n, ci, h, w] = sum_{co, kh, kw} dY[n, co, h - kh + p, w - kw + p] * W[co, ci, kh, kw]
@@ -176,9 +177,11 @@ def supported(dy: torch.Tensor, x: torch.Tensor, gw: torch.Tensor) -> bool:
 
 class _ConvKxKFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, weight, stride: int, padding: int, kernel_wgrad: bool = True):
+    def forward(ctx, x, weight, stride: int, padding: int, kernel_wgrad: bool = True, holder=None):
+        """``holder`` (ops/conv1x1.StatsHolder): the Winograd epilogue's BN partial statistics
+        of y for the BN that follows (attached to the output by ConvKxK.forward)."""
         if USE_WINOGRAD and Wg.supported(x, weight, stride, padding):
-            y = Wg.conv3x3_wino(x, weight)
+            y = Wg.conv3x3_wino(x, weight, holder=holder)
         else:
             y = F.conv2d(x, weight, None, stride, padding)
         ctx.save_for_backward(x, weight)
@@ -214,7 +217,7 @@ class _ConvKxKFn(torch.autograd.Function):
                     gw.add_(dw.to(gw.dtype) if FOLD_CAST else dw)  # see utils/flat.FOLD_CAST
                     _ready(weight)
                     dw = None
-        return dx, dw, None, None, None
+        return dx, dw, None, None, None, None
 
 
 class ConvKxK(torch.nn.Conv2d):
@@ -241,17 +244,39 @@ class ConvKxK(torch.nn.Conv2d):
         return (USE_CONV_WGRAD and self._layout_ok(x)
                 and self.in_channels >= 128 and self.out_channels >= 128)
 
+    def _holder(self, x: torch.Tensor):
+        """A statistics side channel when the Winograd forward runs for a training-mode layer
+        (its output feeds a BN, ResNet's bn2)."""
+        if (USE_WINOGRAD and WINO_BN_STATS and self.training and torch.is_grad_enabled()
+                and Wg.supported(x, self.weight, self.stride[0], self.padding[0])):
+            from .conv1x1 import StatsHolder
+
+            return StatsHolder()
+        return None
+
     def forward(self, x):
         if x.is_cuda and x.dtype != self.weight.dtype and torch.is_autocast_enabled("cuda"):
             x = x.to(self.weight.dtype)
         if self._fast_ok(x):
+            holder = self._holder(x)
             with torch.autocast("cuda", enabled=False):
-                return _ConvKxKFn.apply(x, self.weight, self.stride[0], self.padding[0], True)
+                y = _ConvKxKFn.apply(x, self.weight, self.stride[0], self.padding[0], True, holder)
+            return self._attach(y, holder)
         c64 = (USE_C64_WGRAD and self.in_channels == 64 and self.out_channels == 64 and self.kernel_size == (3, 3)
                and self.stride[0] == 1 and self.padding[0] == 1)
         if self._layout_ok(x) and (c64 or dgrad_fwd_ok(self.weight, self.stride[0], self.padding[0])):
             # input gradient as a forward convolution (DGRAD_FWD); weight gradient on the
             # 64-channel kernel (conv3x3_c64.hip) or MIOpen
+            holder = self._holder(x)
             with torch.autocast("cuda", enabled=False):
-                return _ConvKxKFn.apply(x, self.weight, self.stride[0], self.padding[0], False)
+                y = _ConvKxKFn.apply(x, self.weight, self.stride[0], self.padding[0], False, holder)
+            return self._attach(y, holder)
         return super().forward(x)
+
+    @staticmethod
+    def _attach(y: torch.Tensor, holder) -> torch.Tensor:
+        if holder is not None and holder.stats is not None:
+            from .batchnorm import attach_stats
+
+            attach_stats(y, *holder.stats)
+        return y

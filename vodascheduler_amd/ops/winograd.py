@@ -33,9 +33,11 @@ def filter_transform(w: torch.Tensor, flip: bool = False) -> torch.Tensor:
     return u
 
 
-def conv3x3_wino(x: torch.Tensor, w: torch.Tensor, u: torch.Tensor | None = None, flip: bool = False) -> torch.Tensor:
+def conv3x3_wino(x: torch.Tensor, w: torch.Tensor, u: torch.Tensor | None = None, flip: bool = False,
+                 holder=None) -> torch.Tensor:
     """y = conv2d(x, w, padding=1) for NHWC fp32 x; ``flip``: dX = conv2d(dY, w^T rotated 180,
-    padding=1), the input gradient of a 3x3 stride-1 pad-1 layer.  CPU / unsupported: F.conv2d."""
+    padding=1), the input gradient of a 3x3 stride-1 pad-1 layer.  CPU / unsupported: F.conv2d.
+    ``holder`` (ops/conv1x1.StatsHolder): receives y's BN partial statistics from the epilogue."""
     if not supported(x, w, flip=flip):
         wf = w.transpose(0, 1).flip(2, 3) if flip else w
         return F.conv2d(x, wf, None, 1, 1)
@@ -43,6 +45,13 @@ def conv3x3_wino(x: torch.Tensor, w: torch.Tensor, u: torch.Tensor | None = None
     co = int(w.shape[1]) if flip else int(w.shape[0])
     if u is None:
         u = filter_transform(w, flip)
+    hip = N.hip()
+    G = hip.wino_f23_groups(n, h, wd, c, co)
+    ws = None
+    if holder is not None:
+        ws = torch.empty(max(2 * G * co + 3 * co, hip.bn_workspace_floats(n * h * wd, co)), dtype=torch.float32,
+                         device=x.device)
+        holder.stats = (ws, G)
     y = torch.empty((n, co, h, wd), dtype=torch.float32, device=x.device, memory_format=torch.channels_last)
-    N.hip().wino_f23_fwd(x.data_ptr(), u.data_ptr(), y.data_ptr(), n, h, wd, c, co, N.stream_of(x))
+    hip.wino_f23_fwd(x.data_ptr(), u.data_ptr(), y.data_ptr(), N.ptr(ws), n, h, wd, c, co, G, N.stream_of(x))
     return y
