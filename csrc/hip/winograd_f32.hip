@@ -13,7 +13,7 @@
 //     zero outside the image), transforms it in registers and writes V[p][tile][ci] to LDS;
 //   * wave w owns positions 4w .. 4w+3: its MFMAs read V as 16-byte LDS rows (lane half h takes
 //     ci = 8q + 4h + s for MFMA s = 0..3, the permuted-k order of conv1x1_f32.hip) and U as
-//     16-byte global rows of the pre-transformed filter U[p][co][ci] (L2-resident, <= 16 MB);
+//     16-byte global reads of the pre-transformed filter U[p][ci/8][co][ci%8] (L2-resident, <= 16 MB);
 //   * after the last chunk the 16 accumulators of every (tile, channel) meet in LDS and each
 //     thread applies A^T M A to four of them and stores the 2x2 outputs.
 // The filter transform (wino_f23_filter) runs once per use; the weights change every step.
@@ -40,7 +40,7 @@ constexpr int kWThreads = 256;
 
 struct WinoArgs {
   const float* x;  // [N][H][W][C]
-  const float* u;  // [16][Co][C]
+  const float* u;  // [16][C / 8][Co][8]
   float* y;        // [N][H][W][Co]
   float* part;     // [2][G][Co] BN partial sums (sum, sum of squares) of y, or null
   int N, H, W, C, Co;
@@ -55,8 +55,8 @@ __global__ __launch_bounds__(kWThreads, 2) void wino_f23_fwd_kernel(WinoArgs a) 
   const int co0 = blockIdx.y * kWN;
   const int64_t nblk = (a.T + kWT - 1) / kWT;
 
-  // this thread's staging task: tile (tid & 31) of the block, channels 4 * (tid >> 5) .. + 3
-  const int st = tid & 31, sq = tid >> 5;
+  // this thread's staging task: tile (tid >> 3) of the block, channels 4 * (tid & 7) .. + 3
+  const int st = tid >> 3, sq = tid & 7;  // 8 lanes read one pixel's 32 channels: 128 contiguous bytes
   bool tok = false;
   int h0 = 0, w0 = 0;
   const float* xn = a.x;
@@ -99,10 +99,11 @@ __global__ __launch_bounds__(kWThreads, 2) void wino_f23_fwd_kernel(WinoArgs a) 
     for (int c0 = 0; c0 < a.C; c0 += kWK) {
       // U rows of this wave's first position for the chunk (issued before the barriers; the next
       // position's rows load during the MFMAs of the current one)
-      const float* ub = a.u + (int64_t(4 * wave) * a.Co + co0 + lc) * a.C + c0 + 4 * lh;
+      const float* ub = a.u + ((int64_t(4 * wave) * (a.C / 8) + c0 / 8) * a.Co + co0 + lc) * 8 + 4 * lh;
+      const int64_t uq = int64_t(8) * a.Co;  // floats per 8-channel block of U
       float4 bc[kWK / 8], bn[kWK / 8];
 #pragma unroll
-      for (int q = 0; q < kWK / 8; ++q) bc[q] = *reinterpret_cast<const float4*>(ub + 8 * q);
+      for (int q = 0; q < kWK / 8; ++q) bc[q] = *reinterpret_cast<const float4*>(ub + q * uq);
       // ---- V = B^T d B in registers, in place (rows, then columns)
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
@@ -137,7 +138,7 @@ __global__ __launch_bounds__(kWThreads, 2) void wino_f23_fwd_kernel(WinoArgs a) 
         const int p = 4 * wave + j;
         if (j < 3) {
 #pragma unroll
-          for (int q = 0; q < kWK / 8; ++q) bn[q] = *reinterpret_cast<const float4*>(ub + (j + 1) * ups + 8 * q);
+          for (int q = 0; q < kWK / 8; ++q) bn[q] = *reinterpret_cast<const float4*>(ub + (j + 1) * ups + q * uq);
         }
 #pragma unroll
         for (int q = 0; q < kWK / 8; ++q) {
@@ -249,15 +250,18 @@ __global__ __launch_bounds__(256) void wino_f23_filter_kernel(const float* __res
     t[2][c] = 0.5f * (g[0][c] - g[1][c] + g[2][c]);
     t[3][c] = g[2][c];
   }
+  // layout [p][ci / 8][co][ci % 8]: a wave's U reads (32 channels co, one 8-channel block) are
+  // 1 KB contiguous instead of 32 rows of C floats
   const int64_t pstride = int64_t(Co) * C;
+  const int64_t o = (int64_t(ci >> 3) * Co + co) * 8 + (ci & 7);
 #pragma unroll
   for (int r = 0; r < 4; ++r) {  // (G g) G^T
     const float v0 = t[r][0], v1 = 0.5f * (t[r][0] + t[r][1] + t[r][2]), v2 = 0.5f * (t[r][0] - t[r][1] + t[r][2]),
                 v3 = t[r][2];
-    u[(4 * r + 0) * pstride + i] = v0;
-    u[(4 * r + 1) * pstride + i] = v1;
-    u[(4 * r + 2) * pstride + i] = v2;
-    u[(4 * r + 3) * pstride + i] = v3;
+    u[(4 * r + 0) * pstride + o] = v0;
+    u[(4 * r + 1) * pstride + o] = v1;
+    u[(4 * r + 2) * pstride + o] = v2;
+    u[(4 * r + 3) * pstride + o] = v3;
   }
 }
 

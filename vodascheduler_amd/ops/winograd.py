@@ -24,7 +24,7 @@ def supported(x: torch.Tensor, w: torch.Tensor, stride: int = 1, padding: int = 
 
 
 def filter_transform(w: torch.Tensor, flip: bool = False) -> torch.Tensor:
-    """U [16][Cout][Cin] = G g G^T per (co, ci); ``flip``: of the 180-degree-rotated,
+    """U = G g G^T per (co, ci), stored [16][Cin / 8][Cout][8]; ``flip``: of the 180-degree-rotated,
     channel-transposed filter (Cout and Cin of the result are w's Cin and Cout)."""
     co, ci = (int(w.shape[1]), int(w.shape[0])) if flip else (int(w.shape[0]), int(w.shape[1]))
     u = torch.empty(16, co, ci, dtype=torch.float32, device=w.device)
