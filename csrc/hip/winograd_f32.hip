@@ -101,9 +101,11 @@ __global__ __launch_bounds__(kWThreads, 2) void wino_f23_fwd_kernel(WinoArgs a) 
       // position's rows load during the MFMAs of the current one)
       const float* ub = a.u + ((int64_t(4 * wave) * (a.C / 8) + c0 / 8) * a.Co + co0 + lc) * 8 + 4 * lh;
       const int64_t uq = int64_t(8) * a.Co;  // floats per 8-channel block of U
-      float4 bc[kWK / 8], bn[kWK / 8];
+      float4 bp[2][kWK / 8], bq[2][kWK / 8];  // U of the current / next position pair
 #pragma unroll
-      for (int q = 0; q < kWK / 8; ++q) bc[q] = *reinterpret_cast<const float4*>(ub + q * uq);
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int q = 0; q < kWK / 8; ++q) bp[j][q] = *reinterpret_cast<const float4*>(ub + j * ups + q * uq);
       // ---- V = B^T d B in registers, in place (rows, then columns)
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
@@ -132,24 +134,37 @@ __global__ __launch_bounds__(kWThreads, 2) void wino_f23_fwd_kernel(WinoArgs a) 
         tile_setup(blk + a.G);
         load_patch(0);
       }
-      // ---- 4 positions per wave: acc[j] (tiles x co) += V[p] (tiles x ci) . U[p] (ci x co)
+      // ---- 4 positions per wave: acc[j] (tiles x co) += V[p] (tiles x ci) . U[p] (ci x co), in
+      // pairs of positions whose two MFMA chains interleave; the next pair's U loads meanwhile
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int p = 4 * wave + j;
-        if (j < 3) {
+      for (int pr = 0; pr < 2; ++pr) {
+        if (pr == 0) {
 #pragma unroll
-          for (int q = 0; q < kWK / 8; ++q) bn[q] = *reinterpret_cast<const float4*>(ub + (j + 1) * ups + q * uq);
+          for (int j = 0; j < 2; ++j)
+#pragma unroll
+            for (int q = 0; q < kWK / 8; ++q) bq[j][q] = *reinterpret_cast<const float4*>(ub + (2 + j) * ups + q * uq);
         }
 #pragma unroll
         for (int q = 0; q < kWK / 8; ++q) {
-          const float4 av = *reinterpret_cast<const float4*>(lds + (p * kWT + lc) * kWP + 8 * q + 4 * lh);
-          acc[j] = wmfma(av.x, bc[q].x, acc[j]);
-          acc[j] = wmfma(av.y, bc[q].y, acc[j]);
-          acc[j] = wmfma(av.z, bc[q].z, acc[j]);
-          acc[j] = wmfma(av.w, bc[q].w, acc[j]);
+          const float4 a0 = *reinterpret_cast<const float4*>(lds + ((4 * wave + 2 * pr) * kWT + lc) * kWP + 8 * q + 4 * lh);
+          const float4 a1 = *reinterpret_cast<const float4*>(lds + ((4 * wave + 2 * pr + 1) * kWT + lc) * kWP + 8 * q + 4 * lh);
+          f32x16& c0r = acc[2 * pr];
+          f32x16& c1r = acc[2 * pr + 1];
+          c0r = wmfma(a0.x, bp[0][q].x, c0r);
+          c1r = wmfma(a1.x, bp[1][q].x, c1r);
+          c0r = wmfma(a0.y, bp[0][q].y, c0r);
+          c1r = wmfma(a1.y, bp[1][q].y, c1r);
+          c0r = wmfma(a0.z, bp[0][q].z, c0r);
+          c1r = wmfma(a1.z, bp[1][q].z, c1r);
+          c0r = wmfma(a0.w, bp[0][q].w, c0r);
+          c1r = wmfma(a1.w, bp[1][q].w, c1r);
         }
+        if (pr == 0) {
 #pragma unroll
-        for (int q = 0; q < kWK / 8; ++q) bc[q] = bn[q];
+          for (int j = 0; j < 2; ++j)
+#pragma unroll
+            for (int q = 0; q < kWK / 8; ++q) bp[j][q] = bq[j][q];
+        }
       }
     }
     __syncthreads();
