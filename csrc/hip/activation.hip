@@ -16,32 +16,6 @@ namespace voda {
 namespace {
 
 constexpr int kBlock = 256;
-constexpr float kK = 0.7978845608028654f;
-constexpr float kC = 0.044715f;
-
-// The kernels are VALU-bound, not HBM-bound, with the textbook formula (an IEEE divide is
-// ~10 instructions): written as a logistic, 0.5 (1 + tanh(u)) = 1 / (1 + e^{-2u}), with
-// v_exp_f32 (exp2) and v_rcp_f32 (1 ulp) it is 7 VALU ops forward, ~13 backward.
-//   s = 1 / (1 + 2^{h (A + B h^2)}),  A = -2 k log2(e),  B = A c;   g = h s
-//   g' = s + 2 k h s (1 - s) (1 + 3 c h^2),  s (1 - s) = e s^2
-constexpr float kA = -2.f * kK * 1.4426950408889634f;
-constexpr float kB = kA * kC;
-
-// exponent clamped at 64 so that e stays finite (s = 2^-64 then; e s = 1 - s exactly enough)
-__device__ __forceinline__ float gelu_exp(float h, float h2) {
-  return __builtin_amdgcn_exp2f(fminf(h * __builtin_fmaf(kB, h2, kA), 64.f));
-}
-
-__device__ __forceinline__ float gelu_f(float h) { return h * __builtin_amdgcn_rcpf(1.f + gelu_exp(h, h * h)); }
-
-__device__ __forceinline__ float gelu_grad(float h) {
-  const float h2 = h * h;
-  const float e = gelu_exp(h, h2);
-  const float s = __builtin_amdgcn_rcpf(1.f + e);
-  // s (1 - s) = e s^2: no cancellation as s -> 1
-  return __builtin_fmaf(2.f * kK * h * e * s * s, __builtin_fmaf(3.f * kC, h2, 1.f), s);
-}
-
 // 8 elements per lane as ONE 16 B access for 16-bit types (two for fp32)
 template <typename T> struct Pack8;
 template <typename T> struct Pack8Half {  // bf16 / fp16: uint4 = 8 x 16 bit
@@ -90,11 +64,11 @@ __global__ __launch_bounds__(kBlock) void gelu_fwd_kernel(const T* __restrict__ 
   for (int k = 0; k < kItems; ++k) {
     if (base + k * kBlock >= n8) continue;
 #pragma unroll
-    for (int e = 0; e < 8; ++e) v[k][e] = gelu_f(v[k][e]);
+    for (int e = 0; e < 8; ++e) v[k][e] = gelu_tanh_f(v[k][e]);
     Pack8<T>::store(y, base + k * kBlock, v[k]);
   }
   if (blockIdx.x == gridDim.x - 1)  // < 8 tail elements
-    for (int64_t j = n8 * 8 + threadIdx.x; j < n; j += kBlock) Vec4<T>::store1(y, j, gelu_f(Vec4<T>::load1(h, j)));
+    for (int64_t j = n8 * 8 + threadIdx.x; j < n; j += kBlock) Vec4<T>::store1(y, j, gelu_tanh_f(Vec4<T>::load1(h, j)));
 }
 
 template <typename T>
@@ -113,12 +87,12 @@ __global__ __launch_bounds__(kBlock) void gelu_bwd_kernel(const T* __restrict__ 
   for (int k = 0; k < kItems; ++k) {
     if (base + k * kBlock >= n8) continue;
 #pragma unroll
-    for (int e = 0; e < 8; ++e) g[k][e] *= gelu_grad(v[k][e]);
+    for (int e = 0; e < 8; ++e) g[k][e] *= gelu_tanh_grad(v[k][e]);
     Pack8<T>::store(dh, base + k * kBlock, g[k]);
   }
   if (blockIdx.x == gridDim.x - 1)
     for (int64_t j = n8 * 8 + threadIdx.x; j < n; j += kBlock)
-      Vec4<T>::store1(dh, j, Vec4<T>::load1(dy, j) * gelu_grad(Vec4<T>::load1(h, j)));
+      Vec4<T>::store1(dh, j, Vec4<T>::load1(dy, j) * gelu_tanh_grad(Vec4<T>::load1(h, j)));
 }
 
 template <typename F>

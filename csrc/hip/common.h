@@ -100,6 +100,35 @@ inline unsigned stream_grid(int64_t work_items, int block = 256, int64_t cap = i
 }
 
 
+// tanh-approximated GELU (activation.hip, the fused-epilogue GEMMs of splitgemm.hip):
+//   g(h)  = 0.5 h (1 + tanh(u)),  u = k (h + c h^3);  g'(h) = 0.5 (1 + t) + 0.5 h (1 - t^2) k (1 + 3 c h^2)
+constexpr float kGeluK = 0.7978845608028654f;
+constexpr float kGeluC = 0.044715f;
+
+// The kernels are VALU-bound, not HBM-bound, with the textbook formula (an IEEE divide is
+// ~10 instructions): written as a logistic, 0.5 (1 + tanh(u)) = 1 / (1 + e^{-2u}), with
+// v_exp_f32 (exp2) and v_rcp_f32 (1 ulp) it is 7 VALU ops forward, ~13 backward.
+//   s = 1 / (1 + 2^{h (A + B h^2)}),  A = -2 k log2(e),  B = A c;   g = h s
+//   g' = s + 2 k h s (1 - s) (1 + 3 c h^2),  s (1 - s) = e s^2
+constexpr float kGeluA = -2.f * kGeluK * 1.4426950408889634f;
+constexpr float kGeluB = kGeluA * kGeluC;
+
+// exponent clamped at 64 so that e stays finite (s = 2^-64 then; e s = 1 - s exactly enough)
+__device__ __forceinline__ float gelu_exp(float h, float h2) {
+  return __builtin_amdgcn_exp2f(fminf(h * __builtin_fmaf(kGeluB, h2, kGeluA), 64.f));
+}
+
+__device__ __forceinline__ float gelu_tanh_f(float h) { return h * __builtin_amdgcn_rcpf(1.f + gelu_exp(h, h * h)); }
+
+__device__ __forceinline__ float gelu_tanh_grad(float h) {
+  const float h2 = h * h;
+  const float e = gelu_exp(h, h2);
+  const float s = __builtin_amdgcn_rcpf(1.f + e);
+  // s (1 - s) = e s^2: no cancellation as s -> 1
+  return __builtin_fmaf(2.f * kGeluK * h * e * s * s, __builtin_fmaf(3.f * kGeluC, h2, 1.f), s);
+}
+
+
 inline void check_launch() { VODA_HIP_CHECK(hipGetLastError()); }
 
 }  // namespace voda

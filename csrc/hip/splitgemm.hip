@@ -1,0 +1,437 @@
+// fp32 GEMM at fp32 accuracy on the bf16 matrix cores of gfx950: exact 3-way bf16 split.
+//
+//   C[m][n] (+)= sum_k A(m,k) B(n,k)  [+ bias[n]]  [GELU_AUX / DGELU epilogue]
+//
+// Why.  The reference trains every workload in fp32 (Keras Dense / Conv2D with no mixed
+// precision policy: examples/py/tensorflow2/neural_machine_translation_with_transformer.py:
+// 191-315, tensorflow2_keras_cifar_elastic.py:148-158).  gfx950 has no xf32: the f32-input
+// MFMA runs at the fp32 vector rate (157 TF), 1/16 of the bf16 MFMA, and hipBLASLt / MIOpen
+// already sit at ~130 TF on it (docs/PERFORMANCE.md, round 5).  Every fp32 operand x splits
+// EXACTLY into three bf16 values while it is staged,
+//     hi = bf16(x),  mid = bf16(x - hi),  lo = bf16(x - hi - mid),   x == hi + mid + lo
+// (round-to-nearest each time, so every residual is exact in fp32 and carries <= 8 more
+// significant bits).  a.b = sum of the nine cross products; each bf16 x bf16 product is exact
+// in fp32 and the MFMA accumulates in fp32.  The six products kept (hh, hm, mh, hl, lh, mm)
+// drop terms <= ~2^-24 |a||b| with random signs, below the rounding of an fp32 FMA chain.
+// Six 32x32x16 bf16 MFMAs cost 6/16 of the 32x32x2 f32 MFMAs for the same 16 k: the ceiling
+// is ~2.7x the fp32 MFMA rate.  DUAL keeps the hi.hi products and the five small corrections
+// in separate accumulators (the corrections' roundings are 2^-8 smaller), summed once at the
+// end; NPROD 9 adds the three smallest products (error study, profiles/r6/).
+//
+// Design (guide §3 fragment maps, §5 GEMM anatomy, T10 transposed reads):
+//  * operands are fp32 in HBM in either orientation: "K-contiguous" (rows of k, e.g. X and W
+//    of a forward Linear) or "K-major" (k-rows of contiguous m / n, e.g. dY^T / X^T of a
+//    weight gradient, W of an input gradient).  No transposed copies and no split copies are
+//    ever written: each thread loads 8 fp32 (two 16-B loads), splits them in registers
+//    (3 v_cvt_pk_bf16_f32 + 8 VALU per pair) and writes the three planes to LDS.
+//  * LDS images per stage (16 k): K-contiguous -> [row][h][plane][8] with a 112-B row pitch
+//    (7 x 16 B: the 16 rows of a ds_read_b128 lane group land on 16 distinct bank slots), read
+//    as 3 x ds_read_b128 per fragment; K-major -> [plane][k][row] with 256-B XOR-swizzled
+//    rows (guide T10 layout (b)), read as 2 x ds_read_b64_tr_b16 per fragment.
+//  * v_mfma_f32_32x32x16_bf16; each wave owns a 64 x 64 output sub-tile (2 x 2 MFMA tiles);
+//    workgroups of 128 x 128 (4 waves, two workgroups per CU) or 256 x 128 / 128 x 256
+//    (8 waves).  LDS double-buffered, register staging two stages deep (the loads of stage
+//    s+2 fly while stage s is multiplied and stage s+1 is split into LDS), one barrier per
+//    stage.
+//  * split-K over a grid of tiles x splits: fp32 slabs + a reduce kernel that applies the
+//    epilogue; XCD-aware bijective block remap, split-major logical order (guide T1).
+#include "common.h"
+#include "ops.h"
+
+namespace voda {
+
+namespace {
+
+typedef __bf16 sx_bf16x8 __attribute__((ext_vector_type(8)));
+typedef float sx_f32x16 __attribute__((ext_vector_type(16)));
+typedef __bf16 sx_bf16x4_v __attribute__((__vector_size__(4 * sizeof(__bf16))));
+typedef __attribute__((address_space(3))) sx_bf16x4_v sx_lds_bf16x4;
+
+constexpr int kSxBK = 16;        // k per LDS stage: one 32x32x16 MFMA step
+constexpr int kSxKcPitch = 112;  // K-contiguous image: [h][plane][8] bf16 = 96 B + 16 B pad per row
+
+enum : int { kSxEpiNone = 0, kSxEpiGelu = 1, kSxEpiDGelu = 2 };
+
+struct SxArgs {
+  const float* a; int64_t lda;  // A(m,k) = a[m*lda + k] (K-contiguous) or a[k*lda + m] (K-major)
+  const float* b; int64_t ldb;  // B(n,k) = b[n*ldb + k] (K-contiguous) or b[k*ldb + n] (K-major)
+  float* c; int64_t ldc;
+  const float* bias;            // [N] or null
+  float* aux; int64_t ldaux;    // GELU: h = acc + bias written here (C gets gelu(h)); DGELU: h read
+  float* ws;                    // split-K slabs [S][M][N]
+  int M, N, K, S, kps;          // kps: k per split (multiple of 16)
+  int tiles_n, tiles;
+  int beta, epi;
+};
+
+template <int R, bool KM> struct SxImg {
+  static constexpr int kBytes = KM ? 3 * kSxBK * R * 2 : R * kSxKcPitch;
+};
+
+// K-major image: byte offset of column ``col`` (a multiple of 4) of k-row ``k`` in one plane
+// ([16][R] bf16).  The 16-B chunk index is XORed within each 256-B group (guide T10 (b)), which
+// keeps the 8-B staging writes and the 32x32x16 transposed reads conflict-free.
+template <int R>
+__device__ __forceinline__ int sx_km_off(int k, int col) {
+  const int ch = col >> 3;
+  return k * (2 * R) + ((ch & ~15) << 4) + (((ch & 15) ^ (((k & 3) << 2) | ((k >> 2) & 3))) << 4) + ((col & 4) << 1);
+}
+
+// exact split of 8 fp32 values into three packed bf16 planes (x == hi + mid + lo)
+__device__ __forceinline__ uint32_t sx_pack2(float a, float b) {
+  return uint32_t(f2bf(a)) | (uint32_t(f2bf(b)) << 16);
+}
+__device__ __forceinline__ void sx_split2(float x0, float x1, uint32_t& h, uint32_t& m, uint32_t& l) {
+  h = sx_pack2(x0, x1);
+  const float r0 = x0 - __uint_as_float(h << 16), r1 = x1 - __uint_as_float(h & 0xffff0000u);
+  m = sx_pack2(r0, r1);
+  const float s0 = r0 - __uint_as_float(m << 16), s1 = r1 - __uint_as_float(m & 0xffff0000u);
+  l = sx_pack2(s0, s1);
+}
+__device__ __forceinline__ void sx_split4(const float4 v, uint2& h, uint2& m, uint2& l) {
+  sx_split2(v.x, v.y, h.x, m.x, l.x);
+  sx_split2(v.z, v.w, h.y, m.y, l.y);
+}
+
+__device__ __forceinline__ uint2 sx_tr_read(const uint8_t* p) {
+  const sx_bf16x4_v v = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((sx_lds_bf16x4*)(p));
+  return __builtin_bit_cast(uint2, v);
+}
+
+__device__ __forceinline__ sx_f32x16 sx_mfma(const sx_bf16x8& a, const sx_bf16x8& b, const sx_f32x16& c) {
+  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+}
+
+// ---- one operand's staging: 2R units of 8 fp32 per 16-k stage -------------------------------
+// K-contiguous unit u: row u>>1, k 8(u&1)..+7 of that row (two 16-B loads).
+// K-major unit u: rows 4cg..4cg+3 (cg = u % (R/4)) at k-rows kp and kp+8 (kp = u / (R/4)).
+template <int R, bool KM, int T>
+struct SxStage {
+  static constexpr int kUnits = 2 * R;
+  static constexpr int kPer = (kUnits + T - 1) / T;
+  float4 v[kPer][2];
+};
+
+template <int R, bool KM, int T>
+struct SxOperand {
+  static constexpr int kUnits = 2 * R;
+  static constexpr int kPer = (kUnits + T - 1) / T;
+  const float* g[kPer];  // this thread's unit addresses at the current stage
+  int64_t step;          // floats per 16-k stage
+  int64_t ld8;           // K-major: offset of the second k-row (8 rows down)
+  int woff[kPer];        // LDS byte offset of the unit (plane 0)
+  int woff8[kPer];       // K-major: LDS byte offset of its k + 8 half (the swizzle term differs)
+  bool on[kPer];
+
+  __device__ __forceinline__ void init(const float* base, int64_t ld, int row0, int rows, int k0, int t) {
+#pragma unroll
+    for (int i = 0; i < kPer; ++i) {
+      const int u = t + i * T;
+      on[i] = (kUnits % T == 0) || u < kUnits;
+      const int uu = on[i] ? u : 0;
+      if (!KM) {
+        const int r = uu >> 1, h = uu & 1;
+        const int gr = min(row0 + r, rows - 1);  // rows past the matrix: a valid duplicate
+        g[i] = base + int64_t(gr) * ld + k0 + 8 * h;
+        woff[i] = r * kSxKcPitch + 48 * h;
+        woff8[i] = 0;
+      } else {
+        const int cg = uu % (R / 4), kp = uu / (R / 4);
+        const int gc = min(row0 + 4 * cg, rows - 4);
+        g[i] = base + int64_t(k0 + kp) * ld + gc;
+        woff[i] = sx_km_off<R>(kp, 4 * cg);
+        woff8[i] = sx_km_off<R>(kp + 8, 4 * cg);
+      }
+    }
+    step = KM ? int64_t(kSxBK) * ld : kSxBK;
+    ld8 = KM ? int64_t(8) * ld : 4;
+  }
+
+  __device__ __forceinline__ void load(SxStage<R, KM, T>& s) {
+#pragma unroll
+    for (int i = 0; i < kPer; ++i) {
+      if (on[i]) {
+        s.v[i][0] = *reinterpret_cast<const float4*>(g[i]);
+        s.v[i][1] = *reinterpret_cast<const float4*>(g[i] + ld8);
+      }
+      g[i] += step;
+    }
+  }
+
+  __device__ __forceinline__ void write(const SxStage<R, KM, T>& s, uint8_t* img) const {
+#pragma unroll
+    for (int i = 0; i < kPer; ++i) {
+      if (!on[i]) continue;
+      uint2 h0, m0, l0, h1, m1, l1;
+      sx_split4(s.v[i][0], h0, m0, l0);
+      sx_split4(s.v[i][1], h1, m1, l1);
+      if (!KM) {  // 48 contiguous bytes: hi | mid | lo, 8 k each
+        uint8_t* p = img + woff[i];
+        *reinterpret_cast<uint4*>(p) = make_uint4(h0.x, h0.y, h1.x, h1.y);
+        *reinterpret_cast<uint4*>(p + 16) = make_uint4(m0.x, m0.y, m1.x, m1.y);
+        *reinterpret_cast<uint4*>(p + 32) = make_uint4(l0.x, l0.y, l1.x, l1.y);
+      } else {    // k-row kp and kp + 8 of each plane ([k][R] bf16, 32 R bytes per plane)
+        constexpr int kPlane = kSxBK * R * 2;
+        uint8_t* p = img + woff[i];
+        *reinterpret_cast<uint2*>(p) = h0;
+        *reinterpret_cast<uint2*>(p + kPlane) = m0;
+        *reinterpret_cast<uint2*>(p + 2 * kPlane) = l0;
+        uint8_t* q = img + woff8[i];
+        *reinterpret_cast<uint2*>(q) = h1;
+        *reinterpret_cast<uint2*>(q + kPlane) = m1;
+        *reinterpret_cast<uint2*>(q + 2 * kPlane) = l1;
+      }
+    }
+  }
+};
+
+// three fragments (hi, mid, lo) of the 32-row tile starting at image row r0 for this lane
+template <int R, bool KM>
+__device__ __forceinline__ void sx_frag(const uint8_t* img, int r0, int lane, sx_bf16x8 (&f)[3]) {
+  if (!KM) {
+    const uint8_t* p = img + (r0 + (lane & 31)) * kSxKcPitch + 48 * (lane >> 5);
+#pragma unroll
+    for (int pl = 0; pl < 3; ++pl) f[pl] = *reinterpret_cast<const sx_bf16x8*>(p + 16 * pl);
+  } else {
+    // guide T10: lane 4q+p of a 16-lane group g names k-row 8(g>>1) + 4j + q, columns
+    // 16(g&1) + 4p .. +3 of the tile; lane i of the group receives column i
+    const int g = lane >> 4, i = lane & 15, q = i >> 2, pp = i & 3;
+    const int k = 8 * (g >> 1) + q, col = r0 + 16 * (g & 1) + 4 * pp;
+    const int o0 = sx_km_off<R>(k, col), o1 = sx_km_off<R>(k + 4, col);
+    constexpr int kPlane = kSxBK * R * 2;
+#pragma unroll
+    for (int pl = 0; pl < 3; ++pl) {
+      const uint2 lo = sx_tr_read(img + pl * kPlane + o0);
+      const uint2 hi = sx_tr_read(img + pl * kPlane + o1);
+      f[pl] = __builtin_bit_cast(sx_bf16x8, make_uint4(lo.x, lo.y, hi.x, hi.y));
+    }
+  }
+}
+
+__device__ __forceinline__ float sx_finish(const SxArgs& p, int row, int col, float v) {
+  if (p.beta) v += p.c[int64_t(row) * p.ldc + col];
+  if (p.bias) v += p.bias[col];
+  if (p.epi == kSxEpiGelu) {
+    p.aux[int64_t(row) * p.ldaux + col] = v;
+    v = gelu_tanh_f(v);
+  } else if (p.epi == kSxEpiDGelu) {
+    v *= gelu_tanh_grad(p.aux[int64_t(row) * p.ldaux + col]);
+  }
+  return v;
+}
+
+template <int BM, int BN, bool AKM, bool BKM, int NPROD, bool DUAL>
+__global__ __launch_bounds__(BM * BN / 64, 2) void sgemm_bf16x3_kernel(SxArgs p) {
+  constexpr int T = BM * BN / 64;
+  constexpr int NWN = BN / 64;
+  constexpr int kImgA = SxImg<BM, AKM>::kBytes, kImgB = SxImg<BN, BKM>::kBytes;
+  constexpr int kBuf = kImgA + kImgB;
+  __shared__ __attribute__((aligned(16))) uint8_t smem[2 * kBuf];
+
+  // bijective XCD remap (guide §5 'XCD swizzle must be bijective'): the blocks one XCD runs
+  // are a contiguous range of logical ids; logical order is split-major, tiles row-major
+  const int nwg = gridDim.x, bid = blockIdx.x;
+  const int xcd = bid & 7, q8 = nwg >> 3, r8 = nwg & 7;
+  const int lid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
+  const int split = lid / p.tiles, tile = lid - split * p.tiles;
+  const int m0 = (tile / p.tiles_n) * BM, n0 = (tile % p.tiles_n) * BN;
+  const int kb = split * p.kps;
+  const int ke = min(p.K, kb + p.kps);
+  const int nst = ke > kb ? (ke - kb) / kSxBK : 0;
+
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const int wm = wave / NWN, wn = wave % NWN;
+
+  SxOperand<BM, AKM, T> opa;
+  SxOperand<BN, BKM, T> opb;
+  opa.init(p.a, p.lda, m0, p.M, kb, t);
+  opb.init(p.b, p.ldb, n0, p.N, kb, t);
+  SxStage<BM, AKM, T> sa0, sa1;
+  SxStage<BN, BKM, T> sb0, sb1;
+
+  sx_f32x16 acc[2][2], cor[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) { acc[i][j][r] = 0.f; cor[i][j][r] = 0.f; }
+
+  auto compute = [&](int buf) {
+    const uint8_t* A = smem + buf * kBuf;
+    const uint8_t* B = A + kImgA;
+    sx_bf16x8 fa[2][3], fb[2][3];
+    sx_frag<BM, AKM>(A, wm * 64, lane, fa[0]);
+    sx_frag<BM, AKM>(A, wm * 64 + 32, lane, fa[1]);
+    sx_frag<BN, BKM>(B, wn * 64, lane, fb[0]);
+    sx_frag<BN, BKM>(B, wn * 64 + 32, lane, fb[1]);
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        sx_f32x16& s = DUAL ? cor[i][j] : acc[i][j];
+        if (NPROD >= 9) {
+          s = sx_mfma(fa[i][2], fb[j][2], s);
+          s = sx_mfma(fa[i][1], fb[j][2], s);
+          s = sx_mfma(fa[i][2], fb[j][1], s);
+        }
+        if (NPROD >= 6) {
+          s = sx_mfma(fa[i][1], fb[j][1], s);
+          s = sx_mfma(fa[i][0], fb[j][2], s);
+          s = sx_mfma(fa[i][2], fb[j][0], s);
+        }
+        s = sx_mfma(fa[i][0], fb[j][1], s);
+        s = sx_mfma(fa[i][1], fb[j][0], s);
+        acc[i][j] = sx_mfma(fa[i][0], fb[j][0], acc[i][j]);
+      }
+  };
+  auto write = [&](const SxStage<BM, AKM, T>& sa, const SxStage<BN, BKM, T>& sb, int buf) {
+    uint8_t* A = smem + buf * kBuf;
+    opa.write(sa, A);
+    opb.write(sb, A + kImgA);
+  };
+
+  if (nst > 0) {
+    opa.load(sa0);
+    opb.load(sb0);
+    write(sa0, sb0, 0);
+    if (nst > 1) {
+      opa.load(sa1);
+      opb.load(sb1);
+    }
+  }
+  __syncthreads();
+  // unrolled by two so the register stage sets stay compile-time (guide §5.4 rule 20)
+  for (int st = 0; st < nst; st += 2) {
+    if (st + 2 < nst) { opa.load(sa0); opb.load(sb0); }
+    compute(st & 1);
+    if (st + 1 < nst) write(sa1, sb1, (st + 1) & 1);
+    __syncthreads();
+    if (st + 1 < nst) {
+      if (st + 3 < nst) { opa.load(sa1); opb.load(sb1); }
+      compute((st + 1) & 1);
+      if (st + 2 < nst) write(sa0, sb0, st & 1);
+      __syncthreads();
+    }
+  }
+
+  // epilogue: C/D lane map col = lane & 31, row = (reg&3) + 8 (reg>>2) + 4 (lane>>5)
+  const int h = lane >> 5;
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int col = n0 + wn * 64 + 32 * j + (lane & 31);
+      if (col >= p.N) continue;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int row = m0 + wm * 64 + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * h;
+        if (row >= p.M) continue;
+        const float v = DUAL ? acc[i][j][r] + cor[i][j][r] : acc[i][j][r];
+        if (p.S > 1) {
+          p.ws[(int64_t(split) * p.M + row) * p.N + col] = v;
+        } else {
+          p.c[int64_t(row) * p.ldc + col] = sx_finish(p, row, col, v);
+        }
+      }
+    }
+}
+
+// split-K: C = epilogue(sum over the S slabs), 4 columns per thread (N % 4 == 0)
+__global__ __launch_bounds__(256) void sgemm_reduce_kernel(SxArgs p) {
+  const int64_t n4 = p.N >> 2;
+  const int64_t i = int64_t(blockIdx.x) * 256 + threadIdx.x;
+  if (i >= int64_t(p.M) * n4) return;
+  const int row = int(i / n4), col = int(i - int64_t(row) * n4) * 4;
+  const int64_t slab = int64_t(p.M) * p.N;
+  const float* w = p.ws + int64_t(row) * p.N + col;
+  float4 s = *reinterpret_cast<const float4*>(w);
+  for (int k = 1; k < p.S; ++k) {
+    const float4 v = *reinterpret_cast<const float4*>(w + k * slab);
+    s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
+  }
+  float* c = p.c + int64_t(row) * p.ldc + col;
+  c[0] = sx_finish(p, row, col, s.x);
+  c[1] = sx_finish(p, row, col + 1, s.y);
+  c[2] = sx_finish(p, row, col + 2, s.z);
+  c[3] = sx_finish(p, row, col + 3, s.w);
+}
+
+template <int BM, int BN, int NPROD, bool DUAL>
+void sx_launch_tile(const SxArgs& a, bool akm, bool bkm, unsigned grid, hipStream_t st) {
+  const dim3 blk(BM * BN / 64);
+  if (!akm && !bkm) hipLaunchKernelGGL((sgemm_bf16x3_kernel<BM, BN, false, false, NPROD, DUAL>), grid, blk, 0, st, a);
+  else if (!akm && bkm) hipLaunchKernelGGL((sgemm_bf16x3_kernel<BM, BN, false, true, NPROD, DUAL>), grid, blk, 0, st, a);
+  else if (akm && !bkm) hipLaunchKernelGGL((sgemm_bf16x3_kernel<BM, BN, true, false, NPROD, DUAL>), grid, blk, 0, st, a);
+  else hipLaunchKernelGGL((sgemm_bf16x3_kernel<BM, BN, true, true, NPROD, DUAL>), grid, blk, 0, st, a);
+}
+
+constexpr int kSxTileM[3] = {128, 256, 128};
+constexpr int kSxTileN[3] = {128, 128, 256};
+
+}  // namespace
+
+int64_t sgemm_f32_workspace_floats(int M, int N, int splits) {
+  return splits > 1 ? int64_t(splits) * M * N : 0;
+}
+
+// variant: 0 = 6 products, dual accumulators (the shipped math); 1 = 6 products, one
+// accumulator; 2 = 9 products, dual; 3 = 3 products (hi.hi + hi.mid + mid.hi: ~16-bit, error
+// study only).  Variants 1-3 exist for the 128 x 128 tile only.
+void sgemm_f32(uintptr_t a, int64_t lda, bool a_kmajor, uintptr_t b, int64_t ldb, bool b_kmajor, uintptr_t c,
+               int64_t ldc, int M, int N, int K, bool beta, uintptr_t bias, int epi, uintptr_t aux, int64_t ldaux,
+               int tile, int splits, int variant, uintptr_t ws, int64_t ws_floats, uintptr_t stream) {
+  VODA_CHECK(M > 0 && N > 0 && K > 0, "sgemm_f32: empty GEMM");
+  VODA_CHECK(K % kSxBK == 0, "sgemm_f32: K must be a multiple of 16");
+  VODA_CHECK(M % 4 == 0 && N % 4 == 0, "sgemm_f32: M and N must be multiples of 4");
+  VODA_CHECK(tile >= 0 && tile < 3, "sgemm_f32: bad tile id");
+  VODA_CHECK(variant >= 0 && variant <= 3 && (variant == 0 || tile == 0), "sgemm_f32: bad math variant");
+  VODA_CHECK(epi >= kSxEpiNone && epi <= kSxEpiDGelu && (epi == kSxEpiNone || aux != 0), "sgemm_f32: bad epilogue");
+  VODA_CHECK(a % 16 == 0 && b % 16 == 0 && lda % 4 == 0 && ldb % 4 == 0, "sgemm_f32: operands need 16-B rows");
+  VODA_CHECK(lda >= (a_kmajor ? M : K) && ldb >= (b_kmajor ? N : K) && ldc >= N, "sgemm_f32: leading dims");
+  const int BM = kSxTileM[tile], BN = kSxTileN[tile];
+  SxArgs p{};
+  p.a = reinterpret_cast<const float*>(a); p.lda = lda;
+  p.b = reinterpret_cast<const float*>(b); p.ldb = ldb;
+  p.c = reinterpret_cast<float*>(c); p.ldc = ldc;
+  p.bias = reinterpret_cast<const float*>(bias);
+  p.aux = reinterpret_cast<float*>(aux); p.ldaux = ldaux;
+  p.M = M; p.N = N; p.K = K;
+  const int kst = K / kSxBK;
+  int S = splits < 1 ? 1 : splits;
+  if (S > kst) S = kst;
+  p.kps = ((kst + S - 1) / S) * kSxBK;
+  S = (K + p.kps - 1) / p.kps;  // no empty split
+  p.S = S;
+  p.tiles_n = (N + BN - 1) / BN;
+  p.tiles = ((M + BM - 1) / BM) * p.tiles_n;
+  p.beta = beta ? 1 : 0;
+  p.epi = epi;
+  if (S > 1) {
+    VODA_CHECK(ws != 0 && ws_floats >= sgemm_f32_workspace_floats(M, N, S), "sgemm_f32: split-K workspace too small");
+    VODA_CHECK(c % 16 == 0 && ldc % 4 == 0, "sgemm_f32: split-K output needs 16-B rows");
+    p.ws = reinterpret_cast<float*>(ws);
+  }
+  const int64_t nwg = int64_t(p.tiles) * S;
+  VODA_CHECK(nwg < (int64_t(1) << 31), "sgemm_f32: grid too large");
+  const unsigned grid = unsigned(nwg);
+  hipStream_t st = as_stream(stream);
+  if (tile == 0) {
+    if (variant == 0) sx_launch_tile<128, 128, 6, true>(p, a_kmajor, b_kmajor, grid, st);
+    else if (variant == 1) sx_launch_tile<128, 128, 6, false>(p, a_kmajor, b_kmajor, grid, st);
+    else if (variant == 2) sx_launch_tile<128, 128, 9, true>(p, a_kmajor, b_kmajor, grid, st);
+    else sx_launch_tile<128, 128, 3, true>(p, a_kmajor, b_kmajor, grid, st);
+  } else if (tile == 1) {
+    sx_launch_tile<256, 128, 6, true>(p, a_kmajor, b_kmajor, grid, st);
+  } else {
+    sx_launch_tile<128, 256, 6, true>(p, a_kmajor, b_kmajor, grid, st);
+  }
+  check_launch();
+  if (S > 1) {
+    const int64_t items = int64_t(M) * (N / 4);
+    hipLaunchKernelGGL(sgemm_reduce_kernel, dim3(unsigned((items + 255) / 256)), dim3(256), 0, st, p);
+    check_launch();
+  }
+}
+
+}  // namespace voda

@@ -22,6 +22,9 @@ def test_epilogue_probe_runs():
             assert h.gemm_epilogue_algos(e, dt, False, 3072, 8192, 768) >= 0
     assert ffn.epilogues_available(torch.device("cuda", 0), torch.float32)
     ffn.epilogues_available(torch.device("cuda", 0), torch.bfloat16)
+    # the per-shape check covers the backward's DGELU GEMM of the real token count
+    assert ffn.shape_available(torch.device("cuda", 0), torch.float32, 8192, 768, 3072)
+    assert isinstance(ffn.shape_available(torch.device("cuda", 0), torch.float32, 24, 768, 3072), bool)
 
 
 @pytest.mark.parametrize("M,N,K", [(8192, 3072, 768), (256, 64, 32), (1000, 136, 48)])

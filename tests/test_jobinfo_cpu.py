@@ -232,3 +232,19 @@ def test_measured_step_times_keyed_by_precision(tmp_path):
         assert model_profile("resnet50", "bf16").t1() == pytest.approx(0.023)
     finally:
         set_measured_step_times(None)
+
+
+def test_fp32_profile_fallback_uses_fp32_measurements():
+    """a model without an fp32 profile falls back to its bf16 numbers, labelled
+    fp32, so step times measured at fp32 apply to it (they used to be silently ignored)."""
+    from vodascheduler_amd.common.workload import PROFILES_FP32, model_profile, set_measured_step_times
+
+    assert "mnist" not in PROFILES_FP32
+    p = model_profile("mnist", "fp32")
+    assert p.precision == "fp32" and p.step_time_1gpu == PROFILES["mnist"].step_time_1gpu
+    try:
+        set_measured_step_times({"mnist": {1: 3.5}}, "fp32")
+        assert model_profile("mnist", "fp32").t1() == pytest.approx(3.5e-3)
+        assert model_profile("mnist", "bf16").t1() == PROFILES["mnist"].step_time_1gpu
+    finally:
+        set_measured_step_times(None)

@@ -78,15 +78,41 @@ def test_settle_timeout_hard_limit_for_live_progressing_members():
     b._publish_if_settled("k")
     assert b.live["k"][0] > e1 and b.forced_epochs == 1 and b.forced_log[0]["stale"] == []
     assert b.forced_log[0]["why"] == "hard limit"
-    # the hard limit is also capped in absolute seconds
+    # the hard limit is also capped in absolute seconds, but never below 2 x settle_timeout
     store, b = _backend(10.0)
     b.HARD_SETTLE_S = 0.2
     rd = JobRendezvous(store, "h")
     e1 = _start(b, "h")
     rd.heartbeat("node0:0", e1, 0)
-    b.pending["h"] = (["node0:1"], "migrate", time.time() - 10.5, {})
+    b.pending["h"] = (["node0:1"], "migrate", time.time() - 20.5, {})
     b._publish_if_settled("h")
     assert b.live["h"][0] > e1 and b.forced_log[0]["why"] == "hard limit"
+
+
+def test_settle_timeout_above_hard_cap_keeps_progressing_member():
+    """with settle_timeout >= HARD_SETTLE_S a healthy epoch whose member keeps
+    progressing (bootstrap phases: join, communicator build, state broadcast) is not aborted
+    the moment settle_timeout expires."""
+    store, b = _backend(0.3)
+    b.HARD_SETTLE_S = 0.1                # below settle_timeout: hard limit = 2 x 0.3 s
+    rd = JobRendezvous(store, "p")
+    e1 = _start(b, "p")
+    b.pending["p"] = (["node0:0", "node0:1"], "scale_out", time.time(), {})
+    t0 = time.monotonic()
+    phase = 0
+    while time.monotonic() - t0 < 0.5:   # past settle_timeout, below 2 x settle_timeout
+        phase += 1
+        rd.heartbeat("node0:0", e1, -1, phase)  # no committed step yet: bootstrap progress only
+        b._publish_if_settled("p")
+        time.sleep(0.02)
+    assert b.live["p"][0] == e1 and b.forced_epochs == 0
+    # once it stops progressing, the no-progress rule fires
+    t1 = time.monotonic()
+    while b.live["p"][0] == e1 and time.monotonic() - t1 < 3:
+        rd.heartbeat("node0:0", e1, -1, phase)
+        b._publish_if_settled("p")
+        time.sleep(0.05)
+    assert b.live["p"][0] > e1 and b.forced_log[0]["why"] in ("no progress", "hard limit")
 
 
 def test_left_member_is_tombstoned():
@@ -95,6 +121,8 @@ def test_left_member_is_tombstoned():
     assert rd.read_heartbeat("node0:0") is None
     rd.heartbeat("node0:0", 3, 11)
     rd.heartbeat("node0:0", 3, 12)
-    assert rd.read_heartbeat("node0:0") == (2, 3, 12)
+    assert rd.read_heartbeat("node0:0") == (2, 3, 12, 0)
+    rd.heartbeat("node0:0", 3, 12, 5)
+    assert rd.read_heartbeat("node0:0") == (3, 3, 12, 5)
     rd.clear_heartbeat("node0:0")
     assert rd.read_heartbeat("node0:0") is None

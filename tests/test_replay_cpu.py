@@ -60,3 +60,20 @@ def test_collective_replay_equals_single_process_replay_at_worlds_1_and_2():
     assert len(ref) == len(got) and all(torch.equal(a, b) for a, b in zip(ref, got))
     assert first_divergence(got_ex["steplog"], ref_ex["steplog"]) is None
     assert got_ex["epoch"] == ref_ex["epoch"] and got_ex["samples"] == ref_ex["samples"]
+
+
+def test_deterministic_kernels_scoped_to_one_job():
+    """ADVICE r5: cfg.deterministic switches MIOpen's deterministic solvers on for that job only;
+    a warm pool worker gets its previous process-global flags back afterwards."""
+    from vodascheduler_amd.workloads.train import deterministic_kernels
+
+    prev = (torch.backends.cudnn.deterministic, torch.backends.cudnn.benchmark)
+    torch.backends.cudnn.deterministic, torch.backends.cudnn.benchmark = False, True
+    try:
+        with deterministic_kernels(True):
+            assert torch.backends.cudnn.deterministic and not torch.backends.cudnn.benchmark
+        assert not torch.backends.cudnn.deterministic and torch.backends.cudnn.benchmark
+        with deterministic_kernels(False):
+            assert not torch.backends.cudnn.deterministic
+    finally:
+        torch.backends.cudnn.deterministic, torch.backends.cudnn.benchmark = prev

@@ -1,0 +1,108 @@
+"""GPU numerics of the split-bf16 fp32 GEMM (csrc/hip/splitgemm.hip) against fp64 references:
+all four operand orientations, ragged M / N tiles, split-K, the three tiles, the bias /
+accumulate / GELU / DGELU epilogues, and an error bound no worse than hipBLASLt fp32's."""
+import pytest
+import torch
+
+from vodascheduler_amd.ops import splitgemm as SG
+from vodascheduler_amd.ops.ffn import gelu_tanh_grad_ref
+
+pytestmark = pytest.mark.gpu
+
+DEV = torch.device("cuda", 0)
+
+
+def _orient(a, b, akm, bkm):
+    """Views of the same a [M, K] / b [K, N] values in the requested memory orientation."""
+    a_v = a.t().contiguous().t() if akm else a.contiguous()
+    b_v = b.contiguous() if bkm else b.t().contiguous().t()
+    return a_v, b_v
+
+
+def _bound(a, b):
+    return a.double().abs() @ b.double().abs()
+
+
+@pytest.mark.parametrize("akm", [False, True])
+@pytest.mark.parametrize("bkm", [False, True])
+@pytest.mark.parametrize("tile", [0, 1, 2])
+def test_orientations_ragged(akm, bkm, tile):
+    torch.manual_seed(tile * 4 + 2 * akm + bkm)
+    M, K, N = 388, 272, 196  # ragged in M and N for every tile
+    a = torch.randn(M, K, device=DEV)
+    b = torch.randn(K, N, device=DEV)
+    av, bv = _orient(a, b, akm, bkm)
+    assert SG.supported(av, bv)
+    c = SG.matmul(av, bv, tile=tile, splits=1)
+    ref = a.double() @ b.double()
+    err = ((c.double() - ref).abs() / _bound(a, b)).max().item()
+    assert err < 2e-7, err
+
+
+@pytest.mark.parametrize("splits", [2, 3, 7])
+def test_split_k_matches_reference(splits):
+    torch.manual_seed(splits)
+    M, K, N = 256, 1024, 384
+    a = torch.randn(K, M, device=DEV).t()  # K-major a, as in a weight gradient
+    b = torch.randn(K, N, device=DEV)
+    c = SG.matmul(a, b, tile=0, splits=splits)
+    ref = a.double() @ b.double()
+    assert ((c.double() - ref).abs() / _bound(a, b)).max().item() < 2e-7
+
+
+def test_no_worse_than_hipblaslt_wide_magnitudes():
+    torch.backends.cuda.matmul.allow_tf32 = False
+    torch.manual_seed(5)
+    M, K, N = 512, 768, 512
+    a = torch.randn(M, K, device=DEV) * torch.exp2(torch.randint(-30, 31, (M, K), device=DEV).float())
+    b = torch.randn(K, N, device=DEV) * torch.exp2(torch.randint(-30, 31, (K, N), device=DEV).float())
+    ref = a.double() @ b.double()
+    bd = _bound(a, b)
+    e_lib = ((torch.mm(a, b).double() - ref).abs() / bd).max().item()
+    e_sx = ((SG.matmul(a, b).double() - ref).abs() / bd).max().item()
+    assert e_sx <= 1.5 * e_lib, (e_sx, e_lib)
+
+
+def test_epilogues_bias_accumulate_gelu_dgelu():
+    torch.manual_seed(9)
+    M, K, N = 320, 160, 256
+    x = torch.randn(M, K, device=DEV)
+    w = torch.randn(N, K, device=DEV) * 0.1
+    bias = torch.randn(N, device=DEV)
+    ref = x.double() @ w.double().t()
+    bd = _bound(x, w.t())
+    # bias
+    y = SG.matmul(x, w.t(), bias=bias)
+    assert ((y.double() - ref - bias.double()).abs() / (bd + 1)).max().item() < 2e-7
+    # accumulate into an existing output (beta = 1), split-K path too
+    for s in (1, 4):
+        acc = torch.randn(M, N, device=DEV)
+        want = acc.double() + ref
+        SG.matmul(x, w.t(), out=acc, accumulate=True, splits=s)
+        assert ((acc.double() - want).abs() / (bd + 1)).max().item() < 2e-7
+    # GELU: aux = h = xW^T + b, out = gelu(h)
+    h = torch.empty(M, N, device=DEV)
+    g = SG.matmul(x, w.t(), bias=bias, epi=SG.EPI_GELU, aux=h)
+    href = ref + bias.double()
+    assert ((h.double() - href).abs() / (bd + 1)).max().item() < 2e-7
+    gref = torch.nn.functional.gelu(href, approximate="tanh")
+    assert (g.double() - gref).abs().max().item() < 1e-5
+    # DGELU: out = (dY W) * gelu'(h), h [M, K]
+    dy = torch.randn(M, N, device=DEV)
+    hh = torch.randn(M, K, device=DEV)
+    d = SG.matmul(dy, w, epi=SG.EPI_DGELU, aux=hh)
+    dref = (dy.double() @ w.double()) * gelu_tanh_grad_ref(hh.double())
+    assert ((d.double() - dref).abs() / (_bound(dy, w) + 1)).max().item() < 1e-5
+
+
+def test_variants_error_ordering():
+    """9 products <= 6 products (dual) ~ hipBLASLt << 3 products (16-bit)."""
+    torch.manual_seed(3)
+    a = torch.randn(256, 1024, device=DEV)
+    b = torch.randn(1024, 256, device=DEV)
+    ref = a.double() @ b.double()
+    bd = _bound(a, b)
+    e = {v: ((SG.matmul(a, b, tile=0, splits=1, variant=v).double() - ref).abs() / bd).max().item()
+         for v in SG.VARIANT_NAMES}
+    assert e[0] < 2e-7 and e[2] < 2e-7 and e[1] < 4e-7
+    assert e[3] > 10 * e[0]

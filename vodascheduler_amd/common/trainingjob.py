@@ -225,10 +225,12 @@ def new_training_job(spec: dict, category: str, submit_time: float | None = None
     if num == 0:
         num = mn
     cfg = JobConfig(num_proc=num, min_num_proc=mn, max_num_proc=mx, epochs=epochs)
-    cfg.validate()
-    gpu_type = worker_template_spec(spec).get("nodeSelector", {}).get(GPU_NAME_LABEL)
+    # the reference's one rejection of a spec without a scheduler nodeSelector (raw Horovod
+    # MPIJobs such as examples/test_yaml/*.yaml) comes first, with its message
+    gpu_type = (worker_template_spec(spec).get("nodeSelector") or {}).get(GPU_NAME_LABEL)
     if not gpu_type:
         raise ValueError("gpu type not specified")
+    cfg.validate()  # stricter than the reference (trainingjob.go:114 TODO): knobs must be consistent
     return TrainingJob(job_name=name, job_category=category, kind=spec.get("kind", JobKind.MPIJOB.value),
                        spec=spec, gpu_type=gpu_type, priority=prio, status=JobStatus.SUBMITTED.value,
                        submit_timestamp=time.time() if submit_time is None else submit_time,

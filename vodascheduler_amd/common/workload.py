@@ -21,6 +21,7 @@ import json
 import math
 import os
 import shlex
+import dataclasses
 from dataclasses import dataclass
 
 from .types import MAX_NUM_GPU
@@ -247,7 +248,12 @@ def model_profile(model: str, precision: str = "bf16") -> ModelProfile | None:
     fp32 master weights / gradients, ``fp32`` = the reference's precision)."""
     if precision == "fp32" and model in PROFILES_FP32:
         return PROFILES_FP32[model]
-    return PROFILES.get(model)
+    prof = PROFILES.get(model)
+    if prof is not None and precision == "fp32":
+        # no fp32 profile: the bf16 numbers stand in, but labelled fp32 so that step times
+        # measured at fp32 (set_measured_step_times(..., "fp32")) apply to this job
+        prof = dataclasses.replace(prof, precision="fp32")
+    return prof
 
 
 def profile_of(wl: dict) -> ModelProfile:

@@ -36,6 +36,7 @@ EPI_GELU_AUX_BIAS, EPI_DGELU = 164, 192  # hipblasLtEpilogue_t values
 _WS_BYTES = 32 << 20
 _WS: dict[torch.device, torch.Tensor] = {}
 _EPI_OK: dict[tuple[int, torch.dtype], bool] = {}
+_SHAPE_OK: dict[tuple[int, torch.dtype, int, int, int], bool] = {}
 
 
 def _workspace(device: torch.device) -> torch.Tensor:
@@ -128,7 +129,12 @@ class _FFNGeluFn(torch.autograd.Function):
             need_b2 = False  # summed into the flat gradient by the LayerNorm backward
             hb.done = False
         dw2, db2 = D.linear_weight_grads(do2, y, w2, b2, need[3], need_b2)
-        dh = gemm_dgelu(do2, w2, h)
+        try:
+            dh = gemm_dgelu(do2, w2, h)
+        except RuntimeError as e:  # no DGELU kernel after all: unfused, same math
+            disable_epilogue(str(e))
+            g = do2 @ w2
+            dh = (g.float() * gelu_tanh_grad_ref(h)).to(do2.dtype)
         dw1, db1 = D.linear_weight_grads(dh, x2, w1, b1, need[1], need[2])
         dx = None
         acc = ctx.sink_in.take() if ctx.sink_in is not None and need[0] else None
@@ -170,11 +176,32 @@ def epilogues_available(device: torch.device, dtype: torch.dtype = torch.float32
     return ok
 
 
+def shape_available(device: torch.device, dtype: torch.dtype, M: int, d_model: int, d_ff: int) -> bool:
+    """Does hipBLASLt have kernels for BOTH epilogue GEMMs of THIS token count?  The forward
+    (GELU_AUX_BIAS, h [M, d_ff] = X W1^T) and the backward's DGELU GEMM (dh [M, d_ff] = dOut W2)
+    are queried for the real (M, N, K) before the fused path is taken, so a shape with a forward
+    kernel but no DGELU kernel never reaches the backward (cached per shape, no launch)."""
+    idx = device.index if device.index is not None else torch.cuda.current_device()
+    key = (idx, dtype, M, d_model, d_ff)
+    ok = _SHAPE_OK.get(key)
+    if ok is None:
+        h = N.hip()
+        dt = N.dtype_code(dtype)
+        with torch.cuda.device(idx):
+            ok = (h.gemm_epilogue_algos(EPI_GELU_AUX_BIAS, dt, True, d_ff, M, d_model) > 0
+                  and h.gemm_epilogue_algos(EPI_DGELU, dt, False, d_ff, M, d_model) > 0)
+        _SHAPE_OK[key] = ok
+    return ok
+
+
 def supported(x: torch.Tensor, w1: torch.Tensor, b1, w2: torch.Tensor, b2) -> bool:
     dt = w1.dtype
-    return (USE_GELU_EPILOGUE and x.is_cuda and x.dtype == dt and w2.dtype == dt and b1 is not None
+    if not (USE_GELU_EPILOGUE and x.is_cuda and x.dtype == dt and w2.dtype == dt and b1 is not None
             and b2 is not None and w1.is_contiguous() and w2.is_contiguous() and x.shape[-1] % 8 == 0
-            and w1.shape[0] % 8 == 0 and w2.shape[0] % 8 == 0 and epilogues_available(x.device, dt))
+            and w1.shape[0] % 8 == 0 and w2.shape[0] % 8 == 0 and epilogues_available(x.device, dt)):
+        return False
+    M = x.numel() // x.shape[-1]
+    return M > 0 and shape_available(x.device, dt, M, x.shape[-1], w1.shape[0])
 
 
 def ffn_gelu(x: torch.Tensor, w1: torch.Tensor, b1: torch.Tensor, w2: torch.Tensor, b2: torch.Tensor,

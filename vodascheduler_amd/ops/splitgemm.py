@@ -1,0 +1,183 @@
+"""fp32 GEMM at fp32 accuracy on the bf16 matrix cores (csrc/hip/splitgemm.hip).
+
+gfx950 has no xf32 MFMA; its f32-input MFMA runs at the fp32 vector rate (157 TF), which is
+where hipBLASLt's fp32 GEMMs (and the round-5 own f32-MFMA kernels) stop.  The kernel here
+splits every fp32 operand exactly into three bf16 planes while staging it
+(``x == hi + mid + lo``), multiplies the six significant cross products on
+``v_mfma_f32_32x32x16_bf16`` and accumulates in fp32: fp32 accuracy at up to 16/6 of the fp32
+MFMA rate.  ``split3`` / ``emulate`` below are the bit-exact host model of that arithmetic
+(products of bf16 values are exact, so fp64 accumulation of the kept products reproduces the
+kernel up to fp32 accumulation order), used by the CPU numerics tests.
+
+    matmul(a, b)         a [M, K], b [K, N] fp32 (either may be a transposed view)
+    linear(x, w, bias)   x [..., K] . w[N, K]^T + bias      (F.linear)
+
+Reference: the fp32 Dense / EinsumDense projections of
+examples/py/tensorflow2/neural_machine_translation_with_transformer.py:191-315 and the
+fp32 Conv2D of tensorflow2_keras_cifar_elastic.py:148-158 (no mixed-precision policy).
+"""
+from __future__ import annotations
+
+import os
+
+import torch
+
+from . import _native as N
+
+EPI_NONE, EPI_GELU, EPI_DGELU = 0, 1, 2
+TILES = {0: (128, 128), 1: (256, 128), 2: (128, 256)}
+# 0 = 6 products with the hi.hi products in their own accumulator (shipped); 1 = 6 products,
+# one accumulator; 2 = 9 products; 3 = 3 products (~16-bit: error study only)
+VARIANT_NAMES = {0: "bf16x3-6p-dual", 1: "bf16x3-6p-single", 2: "bf16x3-9p-dual", 3: "bf16x2-3p-dual"}
+GEMM_MATH = VARIANT_NAMES[0]
+
+# VODA_SPLIT_GEMM=0 routes the fp32 projections back to hipBLASLt (A/B switch)
+ENABLED = os.environ.get("VODA_SPLIT_GEMM", "1") != "0"
+
+_WS: dict[torch.device, torch.Tensor] = {}
+
+
+def split3(x: torch.Tensor) -> tuple[torch.Tensor, torch.Tensor, torch.Tensor]:
+    """Exact 3-way bf16 split of an fp32 tensor (round-to-nearest each step), as fp32 tensors:
+    hi + mid + lo == x for every finite x whose residuals stay normal."""
+    x = x.float()
+    hi = x.to(torch.bfloat16).float()
+    r = x - hi
+    mid = r.to(torch.bfloat16).float()
+    lo = (r - mid).to(torch.bfloat16).float()
+    return hi, mid, lo
+
+
+_PRODUCTS = {6: ((0, 0), (0, 1), (1, 0), (0, 2), (2, 0), (1, 1)),
+             9: ((0, 0), (0, 1), (1, 0), (0, 2), (2, 0), (1, 1), (1, 2), (2, 1), (2, 2)),
+             3: ((0, 0), (0, 1), (1, 0))}
+
+
+def emulate(a: torch.Tensor, b: torch.Tensor, nprod: int = 6) -> torch.Tensor:
+    """Host model of the kernel's arithmetic: sum of the kept bf16 cross products of ``a @ b``,
+    accumulated in fp64 (each product is exact; only the accumulation order differs from the
+    GPU), returned in fp64."""
+    pa, pb = split3(a), split3(b)
+    out = None
+    for i, j in _PRODUCTS[nprod]:
+        t = pa[i].double() @ pb[j].double()
+        out = t if out is None else out + t
+    return out
+
+
+def _layout(t: torch.Tensor, rows_dim_first: bool) -> tuple[bool, int] | None:
+    """(kmajor, ld) of a 2-D operand, or None if neither orientation is dense in one dim.
+
+    For ``a`` [M, K]: K-contiguous when stride(1) == 1, K-major when stride(0) == 1.
+    For ``b`` [K, N]: K-contiguous (b = W^T of a [N, K] W) when stride(0) == 1, K-major when
+    stride(1) == 1."""
+    s0, s1 = t.stride()
+    if rows_dim_first:  # a [M, K]
+        if s1 == 1 and (t.shape[0] == 1 or s0 >= t.shape[1]):
+            return False, s0
+        if s0 == 1 and s1 >= t.shape[0]:
+            return True, s1
+    else:               # b [K, N]
+        if s0 == 1 and s1 >= t.shape[0]:
+            return False, s1
+        if s1 == 1 and s0 >= t.shape[1]:
+            return True, s0
+    return None
+
+
+def _aligned(t: torch.Tensor, ld: int) -> bool:
+    return t.data_ptr() % 16 == 0 and ld % 4 == 0
+
+
+def supported(a: torch.Tensor, b: torch.Tensor) -> bool:
+    """True when ``a @ b`` can run on the split kernel (fp32 CUDA operands, K % 16 == 0,
+    M, N % 4 == 0, one dense dimension with 16-byte rows per operand)."""
+    if not (ENABLED and a.is_cuda and b.is_cuda and a.dtype == torch.float32 and b.dtype == torch.float32):
+        return False
+    if a.dim() != 2 or b.dim() != 2 or a.shape[1] != b.shape[0]:
+        return False
+    M, K = a.shape
+    Nn = b.shape[1]
+    if M == 0 or Nn == 0 or K == 0 or K % 16 or M % 4 or Nn % 4:
+        return False
+    la, lb = _layout(a, True), _layout(b, False)
+    return la is not None and lb is not None and _aligned(a, la[1]) and _aligned(b, lb[1])
+
+
+def choose(M: int, Nn: int, K: int) -> tuple[int, int]:
+    """(tile, splits) for an M x N x K GEMM: the 128 x 128 tile (two workgroups per CU, 512
+    resident) unless the output is large, split-K when the tiles cannot fill the chip."""
+    tiles = -(-M // 128) * -(-Nn // 128)
+    if tiles >= 384:
+        return 0, 1
+    kst = K // 16
+    s = max(1, min(kst // 16, -(-512 // tiles)))  # >= 16 stages (256 k) per split
+    return 0, s
+
+
+def _workspace(device: torch.device, floats: int) -> torch.Tensor:
+    w = _WS.get(device)
+    if w is None or w.numel() < floats:
+        w = _WS[device] = torch.empty(max(floats, 1 << 20), dtype=torch.float32, device=device)
+    return w
+
+
+def matmul(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor | None = None, accumulate: bool = False,
+           bias: torch.Tensor | None = None, epi: int = EPI_NONE, aux: torch.Tensor | None = None,
+           tile: int | None = None, splits: int | None = None, variant: int = 0) -> torch.Tensor:
+    """``out (+)= a @ b (+ bias)`` on the split kernel; epi GELU writes the pre-activation
+    into ``aux`` and gelu of it into ``out``, epi DGELU multiplies by gelu'(aux).  Callers
+    check ``supported`` (CPU tensors get the PyTorch reference)."""
+    M, K = a.shape
+    Nn = b.shape[1]
+    if not a.is_cuda:
+        y = a.float() @ b.float()
+        if accumulate and out is not None:
+            y = y + out
+        if bias is not None:
+            y = y + bias.float()
+        if epi == EPI_GELU:
+            aux.copy_(y)
+            y = torch.nn.functional.gelu(y, approximate="tanh")
+        elif epi == EPI_DGELU:
+            from .ffn import gelu_tanh_grad_ref
+
+            y = y * gelu_tanh_grad_ref(aux)
+        if out is None:
+            return y
+        out.copy_(y)
+        return out
+    la, lb = _layout(a, True), _layout(b, False)
+    if la is None or lb is None:
+        raise ValueError("splitgemm.matmul: operands need one dense dimension")
+    if out is None:
+        if accumulate:
+            raise ValueError("splitgemm.matmul: accumulate needs out")
+        out = torch.empty(M, Nn, dtype=torch.float32, device=a.device)
+    if out.stride(1) != 1 or out.shape != (M, Nn):
+        raise ValueError("splitgemm.matmul: out must be [M, N] with unit column stride")
+    t0, s0 = choose(M, Nn, K)
+    tile = t0 if tile is None else tile
+    splits = s0 if splits is None else splits
+    h = N.hip()
+    ws_floats = h.sgemm_f32_workspace_floats(M, Nn, splits)
+    ws = _workspace(a.device, ws_floats) if ws_floats else None
+    if bias is not None:
+        bias = bias.float().contiguous()
+    ld_aux = 0
+    if aux is not None:
+        if aux.dtype != torch.float32 or aux.stride(1) != 1 or aux.shape != (M, Nn):
+            raise ValueError("splitgemm.matmul: aux must be fp32 [M, N] with unit column stride")
+        ld_aux = aux.stride(0)
+    h.sgemm_f32(a.data_ptr(), la[1], la[0], b.data_ptr(), lb[1], lb[0], out.data_ptr(), out.stride(0), M, Nn, K,
+                bool(accumulate), bias.data_ptr() if bias is not None else 0, int(epi),
+                aux.data_ptr() if aux is not None else 0, ld_aux, int(tile), int(splits), int(variant),
+                ws.data_ptr() if ws is not None else 0, ws.numel() if ws is not None else 0, N.stream_of(a))
+    return out
+
+
+def linear(x: torch.Tensor, w: torch.Tensor, bias: torch.Tensor | None = None) -> torch.Tensor:
+    """``F.linear(x, w, bias)`` in fp32 on the split kernel (x [..., K], w [N, K])."""
+    x2 = x.reshape(-1, x.shape[-1])
+    y = matmul(x2, w.t(), bias=bias)
+    return y.view(*x.shape[:-1], w.shape[0])

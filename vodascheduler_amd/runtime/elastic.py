@@ -84,6 +84,7 @@ class ElasticContext:
         self.size = 0
         self.holds_state = False
         self.committed_step = -1
+        self.sync_phase = 0      # bootstrap progress for the heartbeat: bumped by join / comm build / sync
         self._latest_seen = 0
         self._stop = threading.Event()
         self._watcher: threading.Thread | None = None
@@ -109,7 +110,8 @@ class ElasticContext:
                         # liveness + progress for the backend: a dead process stops beating; a
                         # member stuck in a collective keeps beating (the GIL is released there)
                         # but its progress -- joined epoch, committed step -- stops advancing
-                        self._watch_rdzv.heartbeat(self.worker_id, self.epoch, self.committed_step)
+                        self._watch_rdzv.heartbeat(self.worker_id, self.epoch, self.committed_step,
+                                                   self.sync_phase)
                         last_hb = now
                     e = self._watch_rdzv.latest_epoch()
                     if e > self._latest_seen:
@@ -163,6 +165,7 @@ class ElasticContext:
 
     def join(self, epoch: int) -> None:
         t0 = time.perf_counter()
+        self.sync_phase += 1
         self.destroy_comm()
         self.epoch = epoch
         self.members = self.rdzv.members(epoch)
@@ -180,6 +183,7 @@ class ElasticContext:
                                         cancel=lambda: (self.rdzv.latest_epoch() > epoch
                                                         or self.rdzv.outcome() is not None),
                                         members=self.members if self.cache_comms else None)
+        self.sync_phase += 1
         self.resize_log.append({"epoch": epoch, "world": self.size, "comm_init_s": time.perf_counter() - t0,
                                 "cached": COMM_CACHE.hits > hits0})
 
@@ -399,6 +403,7 @@ class State:
 
     def _sync_on(self, comm) -> None:
         ctx = self.ctx
+        ctx.sync_phase += 1
         held = ctx.committed_step if ctx.holds_state else -1
         if comm is not None and comm.size > 1:
             t = torch.tensor([held], dtype=torch.int64, device=comm.device)
@@ -418,6 +423,7 @@ class State:
             from ..parallel.ddp import broadcast_tensors
 
             broadcast_tensors(comm, self.tensors(), root)  # small tensors coalesced per dtype
+            ctx.sync_phase += 1
         extras = dict(self._extras, __step__=self.step)
         extras = broadcast_object(comm, extras, root)
         self.step = extras.pop("__step__")

@@ -149,10 +149,11 @@ class PoolBackend(Backend):
             # a slow but healthy epoch (members still training towards the commit that joins
             # it, a state sync in flight) is left alone.  Abort when a member is known to be
             # gone (its beat counter stopped advancing), when NO member made progress (joined
-            # epoch / committed step) for settle_timeout -- live processes deadlocked in a
-            # collective keep beating but stop progressing -- or at the hard limit
+            # epoch / committed step / bootstrap phase) for settle_timeout -- live processes
+            # deadlocked in a collective keep beating but stop progressing -- or at the hard
+            # limit, which never falls below 2 x settle_timeout
             stuck = not stale and self._no_progress(name, live_m)
-            hard = min(self.STUCK_FACTOR * self.settle_timeout, self.HARD_SETTLE_S)
+            hard = max(2.0 * self.settle_timeout, min(self.STUCK_FACTOR * self.settle_timeout, self.HARD_SETTLE_S))
             if not stale and not stuck and waited < hard:
                 return
             why = "stale" if stale else ("no progress" if stuck else "hard limit")
@@ -177,7 +178,8 @@ class PoolBackend(Backend):
                 self._mail(wid, {"job": name, "epoch": e, "cfg": cfg})
 
     STUCK_FACTOR = 5.0      # hard limit: abort a never-syncing epoch after this x settle_timeout ...
-    HARD_SETTLE_S = 150.0   # ... or this many seconds, whichever is first (bench deadline 540 s)
+    HARD_SETTLE_S = 150.0   # ... or this many seconds, whichever is first (bench deadline 540 s),
+    #                         but never before 2 x settle_timeout
     HEARTBEAT_STALE_S = 10.0
 
     def _observe(self, rdzv, job: str, m: str):
@@ -211,7 +213,7 @@ class PoolBackend(Backend):
         return out
 
     def _no_progress(self, job: str, members: list[str]) -> bool:
-        """True when no member's progress (joined epoch, committed step) changed during the
+        """True when no member's progress (joined epoch, committed step, bootstrap phase) changed during the
         last settle_timeout (records refreshed by the _stale_members call just before)."""
         now = time.monotonic()
         recs = [self._hb_seen.get((job, m)) for m in members]

@@ -99,16 +99,18 @@ class JobRendezvous:
             time.sleep(0.02)
 
     # ----------------------------------------------------------- liveness / progress beats
-    def heartbeat(self, worker: str, epoch: int, step: int) -> None:
+    def heartbeat(self, worker: str, epoch: int, step: int, phase: int = 0) -> None:
         """One beat of ``worker``: a store-side counter (liveness: the backend checks that it
         ADVANCES, on its own clock -- no wall-clock comparison across hosts) and the member's
-        progress, the epoch it joined and its last committed step."""
-        self.store.set(self.p + f"hb/{worker}/p", f"{int(epoch)}:{int(step)}")
+        progress: the epoch it joined, its last committed step and its bootstrap phase counter
+        (bumped by join, communicator build and state broadcast, so a slow first sync of a
+        healthy epoch counts as progress)."""
+        self.store.set(self.p + f"hb/{worker}/p", f"{int(epoch)}:{int(step)}:{int(phase)}")
         self.store.add(self.p + f"hb/{worker}/n", 1)
 
-    def read_heartbeat(self, worker: str) -> tuple[int, int, int] | None:
-        """(beat count, joined epoch, committed step), or None when the worker never beat or
-        left the job (its beat tombstoned by ElasticContext.stop)."""
+    def read_heartbeat(self, worker: str) -> tuple[int, int, int, int] | None:
+        """(beat count, joined epoch, committed step, bootstrap phase), or None when the worker
+        never beat or left the job (its beat tombstoned by ElasticContext.stop)."""
         kp = self.p + f"hb/{worker}/p"
         if not self.store.check([kp]):
             return None
@@ -116,8 +118,8 @@ class JobRendezvous:
         if v == "left":
             return None
         n = int(self.store.add(self.p + f"hb/{worker}/n", 0))
-        e, st = v.split(":")
-        return n, int(e), int(st)
+        f = v.split(":")
+        return n, int(f[0]), int(f[1]), int(f[2]) if len(f) > 2 else 0
 
     def clear_heartbeat(self, worker: str) -> None:
         """Tombstone: a worker that left the job no longer counts as a live member, even if

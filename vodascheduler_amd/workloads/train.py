@@ -16,6 +16,7 @@ Standalone (one process per GPU, launched by the local node agent):
 from __future__ import annotations
 
 import argparse
+import contextlib
 import collections
 import hashlib
 import json
@@ -79,9 +80,6 @@ def build(cfg: TrainConfig, device: torch.device):
     w = get_workload(cfg.model)
     torch.manual_seed(cfg.seed)  # identical init everywhere (state is broadcast anyway)
     model = prepare_model(w, device, cfg.amp)
-    if cfg.deterministic:
-        torch.backends.cudnn.deterministic = True
-        torch.backends.cudnn.benchmark = False
     kw = dict(w.opt_kwargs)
     if cfg.lr is not None:
         kw["lr"] = cfg.lr
@@ -90,6 +88,22 @@ def build(cfg: TrainConfig, device: torch.device):
 
 
 GRAD_DTYPES = {"fp32": torch.float32, "bf16": torch.bfloat16, "fp16": torch.float16}
+
+
+@contextlib.contextmanager
+def deterministic_kernels(enabled: bool):
+    """MIOpen's deterministic solvers for the duration of ONE job (cfg.deterministic), then the
+    previous process-global flags again: a warm pool worker that hosted a deterministic job
+    must not keep the slow solvers for every later job."""
+    if not enabled:
+        yield
+        return
+    prev = (torch.backends.cudnn.deterministic, torch.backends.cudnn.benchmark)
+    torch.backends.cudnn.deterministic, torch.backends.cudnn.benchmark = True, False
+    try:
+        yield
+    finally:
+        torch.backends.cudnn.deterministic, torch.backends.cudnn.benchmark = prev
 
 
 def synthetic_pool(w, cfg: TrainConfig, bs: int, device: torch.device) -> list:
@@ -242,6 +256,11 @@ def write_progress(metrics_dir: str, job: str, doc: dict) -> None:
 
 
 def train_elastic(ctx: ElasticContext, cfg: TrainConfig, use_cache: bool = True) -> dict | None:
+    with deterministic_kernels(cfg.deterministic):
+        return _train_elastic(ctx, cfg, use_cache)
+
+
+def _train_elastic(ctx: ElasticContext, cfg: TrainConfig, use_cache: bool = True) -> dict | None:
     device = ctx.device
     wm = get_warm(cfg, device, use_cache)
     w, model, opt, base_lr, bs, pool, ddp = wm.w, wm.model, wm.opt, wm.base_lr, wm.bs, wm.pool, wm.ddp
@@ -428,6 +447,11 @@ def train_elastic(ctx: ElasticContext, cfg: TrainConfig, use_cache: bool = True)
 
 
 def replay_reference(cfg: TrainConfig, world_log: list[int], total_steps: int, device: torch.device):
+    with deterministic_kernels(cfg.deterministic):
+        return _replay_reference(cfg, world_log, total_steps, device)
+
+
+def _replay_reference(cfg: TrainConfig, world_log: list[int], total_steps: int, device: torch.device):
     """Uninterrupted single-process replay of an elastic run: step ``s`` runs at the world
     size of the last ``world_log`` segment starting at or before ``s`` (LR = base x world,
     the same synthetic batch every rank of the elastic run used).  The elastic run's final
