@@ -325,6 +325,22 @@ def tunable_status(device: str) -> dict | None:
     return st
 
 
+
+def gemm_math(precision: str, device: str) -> str:
+    """How the fp32 matrix products are computed (label the split)."""
+    if precision != "fp32":
+        return "bf16 MFMA, fp32 accumulate (autocast)"
+    if device != "cuda":
+        return "fp32 (CPU)"
+    from vodascheduler_amd.ops import splitgemm
+
+    if not splitgemm.ENABLED:
+        return "fp32: f32 MFMA (own kernels, hipBLASLt, MIOpen)"
+    return ("fp32 accuracy: Linear / FFN GEMMs as an exact 3-way bf16 split of each fp32 operand, "
+            f"6 cross products on the bf16 MFMA, fp32 accumulate ({splitgemm.GEMM_MATH}, csrc/hip/splitgemm.hip); "
+            "convolutions on f32 MFMA (own Winograd / 1x1 kernels, hipBLASLt, MIOpen)")
+
+
 def main():
     if os.environ.get("VODA_STACKDUMP_S"):  # debugging aid: dump every thread's stack once
         import faulthandler
@@ -607,6 +623,7 @@ def main():
                                  "reference number exists (BASELINE.json published: {})"),
             "dtype": dtype,
             "precision": a.precision,
+            "gemm_math": gemm_math(a.precision, a.device),
             "grad_dtype": a.grad_dtype,
             "allreduce_dtype": a.compression or a.grad_dtype,
             "data": "synthetic (random-init weights, synthetic batches of the real shapes)"

@@ -74,6 +74,9 @@ def main() -> None:
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--out", default="")
     ap.add_argument("--quick", action="store_true", help="one linear, no tile sweep")
+    ap.add_argument("--variants", default="", help="comma list of math variants to time on tile 0 (A/B)")
+    ap.add_argument("--no-sweep", action="store_true", help="no tile / split sweep")
+    ap.add_argument("--stagger-ab", action="store_true", help="also time the default without the WG stagger")
     args = ap.parse_args()
     dev = torch.device("cuda", 0)
     sink = open(args.out, "a") if args.out else None
@@ -94,9 +97,13 @@ def main() -> None:
             flops = 2.0 * Mo * No * Ko
             t0, s0 = SG.choose(Mo, No, Ko)
             cands = {"hipblaslt": None, f"split_t{t0}_s{s0}": (t0, s0, 0)}
-            if not args.quick:
+            for v in [int(x) for x in args.variants.split(",") if x]:
+                cands[f"var{v}_t0_s{s0}"] = (0, s0, v)
+            if args.stagger_ab:
+                cands[f"nostag_t{t0}_s{s0}"] = (t0, s0, 0, 0)
+            if not args.quick and not args.no_sweep:
                 tiles = -(-Mo // 128) * -(-No // 128)
-                for tile in (0, 1, 2):
+                for tile in (0, 1, 2, 3, 4):
                     for s in (1, 2, 4, 8, 16):
                         if s > 1 and tiles * s > 2048:
                             continue
@@ -107,9 +114,15 @@ def main() -> None:
                 if cfg is None:
                     fns[key] = lambda: torch.mm(a, b, out=out)
                 else:
-                    tile, s, var = cfg
-                    fns[key] = (lambda tile=tile, s=s, var=var:
-                                SG.matmul(a, b, out=out, tile=tile, splits=s, variant=var))
+                    tile, s, var = cfg[:3]
+                    stag = cfg[3] if len(cfg) > 3 else 1
+
+                    def fn(tile=tile, s=s, var=var, stag=stag):
+                        h = SG.N.hip()
+                        h.sgemm_f32_set_stagger(stag)
+                        SG.matmul(a, b, out=out, tile=tile, splits=s, variant=var)
+                        h.sgemm_f32_set_stagger(1)
+                    fns[key] = fn
             for f in fns.values():  # warm-up / first-call costs
                 f()
             torch.cuda.synchronize()

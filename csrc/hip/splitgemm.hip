@@ -47,6 +47,10 @@ typedef float sx_f32x16 __attribute__((ext_vector_type(16)));
 typedef __bf16 sx_bf16x4_v __attribute__((__vector_size__(4 * sizeof(__bf16))));
 typedef __attribute__((address_space(3))) sx_bf16x4_v sx_lds_bf16x4;
 
+#ifndef SX_SCHED_GROUPS
+#define SX_SCHED_GROUPS 0
+#endif
+
 constexpr int kSxBK = 16;        // k per LDS stage: one 32x32x16 MFMA step
 constexpr int kSxKcPitch = 112;  // K-contiguous image: [h][plane][8] bf16 = 96 B + 16 B pad per row
 
@@ -62,7 +66,10 @@ struct SxArgs {
   int M, N, K, S, kps;          // kps: k per split (multiple of 16)
   int tiles_n, tiles;
   int beta, epi;
+  int stagger;                  // 1: odd workgroups at issue priority 1
 };
+
+int g_sx_stagger = 1;
 
 template <int R, bool KM> struct SxImg {
   static constexpr int kBytes = KM ? 3 * kSxBK * R * 2 : R * kSxKcPitch;
@@ -77,9 +84,12 @@ __device__ __forceinline__ int sx_km_off(int k, int col) {
   return k * (2 * R) + ((ch & ~15) << 4) + (((ch & 15) ^ (((k & 3) << 2) | ((k >> 2) & 3))) << 4) + ((col & 4) << 1);
 }
 
-// exact split of 8 fp32 values into three packed bf16 planes (x == hi + mid + lo)
-__device__ __forceinline__ uint32_t sx_pack2(float a, float b) {
-  return uint32_t(f2bf(a)) | (uint32_t(f2bf(b)) << 16);
+// exact split of fp32 values into three packed bf16 planes (x == hi + mid + lo)
+typedef float sx_f32x2 __attribute__((ext_vector_type(2)));
+typedef __bf16 sx_bf16x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ uint32_t sx_pack2(float a, float b) {  // one v_cvt_pk_bf16_f32 (RNE)
+  const sx_f32x2 f = {a, b};
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector(f, sx_bf16x2));
 }
 __device__ __forceinline__ void sx_split2(float x0, float x1, uint32_t& h, uint32_t& m, uint32_t& l) {
   h = sx_pack2(x0, x1);
@@ -103,7 +113,8 @@ __device__ __forceinline__ sx_f32x16 sx_mfma(const sx_bf16x8& a, const sx_bf16x8
 }
 
 // ---- one operand's staging: 2R units of 8 fp32 per 16-k stage -------------------------------
-// K-contiguous unit u: row u>>1, k 8(u&1)..+7 of that row (two 16-B loads).
+// K-contiguous unit u: k 4q..4q+3 (q = u & 3) of rows r and r + R/2 (r = u >> 2): four lanes read
+//   one row's 64 contiguous bytes, a wave-load covers 16 whole 64-B row pieces.
 // K-major unit u: rows 4cg..4cg+3 (cg = u % (R/4)) at k-rows kp and kp+8 (kp = u / (R/4)).
 template <int R, bool KM, int T>
 struct SxStage {
@@ -116,11 +127,11 @@ template <int R, bool KM, int T>
 struct SxOperand {
   static constexpr int kUnits = 2 * R;
   static constexpr int kPer = (kUnits + T - 1) / T;
-  const float* g[kPer];  // this thread's unit addresses at the current stage
-  int64_t step;          // floats per 16-k stage
-  int64_t ld8;           // K-major: offset of the second k-row (8 rows down)
-  int woff[kPer];        // LDS byte offset of the unit (plane 0)
-  int woff8[kPer];       // K-major: LDS byte offset of its k + 8 half (the swizzle term differs)
+  const float* g[kPer];   // this thread's unit addresses at the current stage (first float4)
+  const float* g2[kPer];  // second float4 (K-contiguous: row r + R/2; K-major: k-row + 8)
+  int64_t step;           // floats per 16-k stage
+  int woff[kPer];         // LDS byte offset of the first float4's split (plane 0)
+  int woff2[kPer];        // ... of the second
   bool on[kPer];
 
   __device__ __forceinline__ void init(const float* base, int64_t ld, int row0, int rows, int k0, int t) {
@@ -130,57 +141,58 @@ struct SxOperand {
       on[i] = (kUnits % T == 0) || u < kUnits;
       const int uu = on[i] ? u : 0;
       if (!KM) {
-        const int r = uu >> 1, h = uu & 1;
-        const int gr = min(row0 + r, rows - 1);  // rows past the matrix: a valid duplicate
-        g[i] = base + int64_t(gr) * ld + k0 + 8 * h;
-        woff[i] = r * kSxKcPitch + 48 * h;
-        woff8[i] = 0;
+        const int q = uu & 3, r = uu >> 2;
+        const int gr = min(row0 + r, rows - 1), gr2 = min(row0 + r + R / 2, rows - 1);  // rows past the matrix: valid duplicates
+        g[i] = base + int64_t(gr) * ld + k0 + 4 * q;
+        g2[i] = base + int64_t(gr2) * ld + k0 + 4 * q;
+        woff[i] = r * kSxKcPitch + 48 * (q >> 1) + 8 * (q & 1);
+        woff2[i] = (r + R / 2) * kSxKcPitch + 48 * (q >> 1) + 8 * (q & 1);
       } else {
         const int cg = uu % (R / 4), kp = uu / (R / 4);
         const int gc = min(row0 + 4 * cg, rows - 4);
         g[i] = base + int64_t(k0 + kp) * ld + gc;
+        g2[i] = g[i] + int64_t(8) * ld;
         woff[i] = sx_km_off<R>(kp, 4 * cg);
-        woff8[i] = sx_km_off<R>(kp + 8, 4 * cg);
+        woff2[i] = sx_km_off<R>(kp + 8, 4 * cg);
       }
     }
     step = KM ? int64_t(kSxBK) * ld : kSxBK;
-    ld8 = KM ? int64_t(8) * ld : 4;
   }
 
-  __device__ __forceinline__ void load(SxStage<R, KM, T>& s) {
+  // Loads are unconditional (a finished operand re-reads its last stage): a load under a
+  // runtime condition makes hipcc merge the register sets with copies right after the loads and
+  // wait for them there, exposing the whole memory latency every stage (guide §5 item 4(c)).
+  __device__ __forceinline__ void load(SxStage<R, KM, T>& s, bool advance) {
 #pragma unroll
-    for (int i = 0; i < kPer; ++i) {
-      if (on[i]) {
-        s.v[i][0] = *reinterpret_cast<const float4*>(g[i]);
-        s.v[i][1] = *reinterpret_cast<const float4*>(g[i] + ld8);
-      }
-      g[i] += step;
+    for (int i = 0; i < kPer; ++i) {  // idle units (on == false) read unit 0's valid address
+      s.v[i][0] = *reinterpret_cast<const float4*>(g[i]);
+      s.v[i][1] = *reinterpret_cast<const float4*>(g2[i]);
+      const int64_t d = advance ? step : 0;
+      g[i] += d;
+      g2[i] += d;
     }
   }
 
-  __device__ __forceinline__ void write(const SxStage<R, KM, T>& s, uint8_t* img) const {
+  // unconditional (no branch around the split: it interleaves with the MFMAs); idle units
+  // (on == false) write to a dummy slot instead of their duplicate unit's bytes.  Each float4
+  // becomes three 8-byte plane pieces: K-contiguous images keep a row's planes 16 B apart,
+  // K-major images a whole [16][R] plane apart.
+  __device__ __forceinline__ void write(const SxStage<R, KM, T>& s, uint8_t* img, uint8_t* dummy) const {
+    constexpr int kPl = KM ? kSxBK * R * 2 : 16;
 #pragma unroll
     for (int i = 0; i < kPer; ++i) {
-      if (!on[i]) continue;
       uint2 h0, m0, l0, h1, m1, l1;
       sx_split4(s.v[i][0], h0, m0, l0);
       sx_split4(s.v[i][1], h1, m1, l1);
-      if (!KM) {  // 48 contiguous bytes: hi | mid | lo, 8 k each
-        uint8_t* p = img + woff[i];
-        *reinterpret_cast<uint4*>(p) = make_uint4(h0.x, h0.y, h1.x, h1.y);
-        *reinterpret_cast<uint4*>(p + 16) = make_uint4(m0.x, m0.y, m1.x, m1.y);
-        *reinterpret_cast<uint4*>(p + 32) = make_uint4(l0.x, l0.y, l1.x, l1.y);
-      } else {    // k-row kp and kp + 8 of each plane ([k][R] bf16, 32 R bytes per plane)
-        constexpr int kPlane = kSxBK * R * 2;
-        uint8_t* p = img + woff[i];
-        *reinterpret_cast<uint2*>(p) = h0;
-        *reinterpret_cast<uint2*>(p + kPlane) = m0;
-        *reinterpret_cast<uint2*>(p + 2 * kPlane) = l0;
-        uint8_t* q = img + woff8[i];
-        *reinterpret_cast<uint2*>(q) = h1;
-        *reinterpret_cast<uint2*>(q + kPlane) = m1;
-        *reinterpret_cast<uint2*>(q + 2 * kPlane) = l1;
-      }
+      uint8_t* p = on[i] ? img + woff[i] : dummy;
+      uint8_t* q = on[i] ? img + woff2[i] : dummy + 8;
+      const int pl = on[i] ? kPl : 16;
+      *reinterpret_cast<uint2*>(p) = h0;
+      *reinterpret_cast<uint2*>(p + pl) = m0;
+      *reinterpret_cast<uint2*>(p + 2 * pl) = l0;
+      *reinterpret_cast<uint2*>(q) = h1;
+      *reinterpret_cast<uint2*>(q + pl) = m1;
+      *reinterpret_cast<uint2*>(q + 2 * pl) = l1;
     }
   }
 };
@@ -220,13 +232,16 @@ __device__ __forceinline__ float sx_finish(const SxArgs& p, int row, int col, fl
   return v;
 }
 
-template <int BM, int BN, bool AKM, bool BKM, int NPROD, bool DUAL>
-__global__ __launch_bounds__(BM * BN / 64, 2) void sgemm_bf16x3_kernel(SxArgs p) {
-  constexpr int T = BM * BN / 64;
+// WMT: 32-row MFMA tiles per wave along M (2: 64 x 64 per wave; 4: 128 x 64 per wave, one wave per
+// SIMD with its accumulators in AGPRs)
+template <int BM, int BN, bool AKM, bool BKM, int NPROD, bool DUAL, bool TWO_SETS, int MINW, int WMT>
+__global__ __launch_bounds__(BM * BN / (32 * WMT), MINW) void sgemm_bf16x3_kernel(SxArgs p) {
   constexpr int NWN = BN / 64;
+  constexpr int NWM = BM / (32 * WMT);
+  constexpr int T = 64 * NWM * NWN;
   constexpr int kImgA = SxImg<BM, AKM>::kBytes, kImgB = SxImg<BN, BKM>::kBytes;
   constexpr int kBuf = kImgA + kImgB;
-  __shared__ __attribute__((aligned(16))) uint8_t smem[2 * kBuf];
+  __shared__ __attribute__((aligned(16))) uint8_t smem[2 * kBuf + 64];  // + dummy slot (idle units)
 
   // bijective XCD remap (guide §5 'XCD swizzle must be bijective'): the blocks one XCD runs
   // are a contiguous range of logical ids; logical order is split-major, tiles row-major
@@ -241,6 +256,10 @@ __global__ __launch_bounds__(BM * BN / 64, 2) void sgemm_bf16x3_kernel(SxArgs p)
 
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
   const int wm = wave / NWN, wn = wave % NWN;
+  // two co-resident workgroups run the same program in lock step (MFMA phases together, VALU /
+  // LDS / barrier phases together); static priority for one of them staggers the pair
+  // (MI355X_MICROARCH.md 'Two waves per SIMD', items 4 and 9)
+  if (__builtin_amdgcn_readfirstlane(p.stagger & blockIdx.x) & 1) __builtin_amdgcn_s_setprio(1);
 
   SxOperand<BM, AKM, T> opa;
   SxOperand<BN, BKM, T> opb;
@@ -249,9 +268,9 @@ __global__ __launch_bounds__(BM * BN / 64, 2) void sgemm_bf16x3_kernel(SxArgs p)
   SxStage<BM, AKM, T> sa0, sa1;
   SxStage<BN, BKM, T> sb0, sb1;
 
-  sx_f32x16 acc[2][2], cor[2][2];
+  sx_f32x16 acc[WMT][2], cor[WMT][2];
 #pragma unroll
-  for (int i = 0; i < 2; ++i)
+  for (int i = 0; i < WMT; ++i)
 #pragma unroll
     for (int j = 0; j < 2; ++j)
 #pragma unroll
@@ -260,13 +279,13 @@ __global__ __launch_bounds__(BM * BN / 64, 2) void sgemm_bf16x3_kernel(SxArgs p)
   auto compute = [&](int buf) {
     const uint8_t* A = smem + buf * kBuf;
     const uint8_t* B = A + kImgA;
-    sx_bf16x8 fa[2][3], fb[2][3];
-    sx_frag<BM, AKM>(A, wm * 64, lane, fa[0]);
-    sx_frag<BM, AKM>(A, wm * 64 + 32, lane, fa[1]);
+    sx_bf16x8 fa[WMT][3], fb[2][3];
+#pragma unroll
+    for (int i = 0; i < WMT; ++i) sx_frag<BM, AKM>(A, wm * 32 * WMT + 32 * i, lane, fa[i]);
     sx_frag<BN, BKM>(B, wn * 64, lane, fb[0]);
     sx_frag<BN, BKM>(B, wn * 64 + 32, lane, fb[1]);
 #pragma unroll
-    for (int i = 0; i < 2; ++i)
+    for (int i = 0; i < WMT; ++i)
 #pragma unroll
       for (int j = 0; j < 2; ++j) {
         sx_f32x16& s = DUAL ? cor[i][j] : acc[i][j];
@@ -287,30 +306,63 @@ __global__ __launch_bounds__(BM * BN / 64, 2) void sgemm_bf16x3_kernel(SxArgs p)
   };
   auto write = [&](const SxStage<BM, AKM, T>& sa, const SxStage<BN, BKM, T>& sb, int buf) {
     uint8_t* A = smem + buf * kBuf;
-    opa.write(sa, A);
-    opb.write(sb, A + kImgA);
+    opa.write(sa, A, smem + 2 * kBuf);
+    opb.write(sb, A + kImgA, smem + 2 * kBuf);
   };
 
-  if (nst > 0) {
-    opa.load(sa0);
-    opb.load(sb0);
-    write(sa0, sb0, 0);
-    if (nst > 1) {
-      opa.load(sa1);
-      opb.load(sb1);
+  // stage k is read from global at load number k (clamped to the last stage), multiplied from
+  // LDS buffer k & 1; the loads of stage s+2 fly while stage s is multiplied
+  int nld = 0;
+  auto load = [&](SxStage<BM, AKM, T>& sa, SxStage<BN, BKM, T>& sb) {
+    const bool adv = ++nld < nst;
+    opa.load(sa, adv);
+    opb.load(sb, adv);
+    // keep the loads ahead of the MFMAs: hipcc otherwise sinks them below the MFMAs into the
+    // fragment registers and waits for them at once (no prefetch at all)
+    __builtin_amdgcn_sched_barrier(0);
+  };
+  if (TWO_SETS) {
+    // software pipeline: iteration s loads stage s+2, multiplies stage s and splits stage s+1
+    // (loaded one iteration earlier) into the other LDS buffer; the split's VALU and LDS writes
+    // are interleaved with the MFMAs (sched_group_barrier), not issued after them
+    auto pipe = [&](SxStage<BM, AKM, T>& la, SxStage<BN, BKM, T>& lb, const SxStage<BM, AKM, T>& wa,
+                    const SxStage<BN, BKM, T>& wb, int buf) {
+      load(la, lb);
+      compute(buf);
+      write(wa, wb, buf ^ 1);
+#if SX_SCHED_GROUPS
+      constexpr int kMf = 2 * WMT * (NPROD == 9 ? 9 : NPROD == 6 ? 6 : 3);
+#pragma unroll
+      for (int k = 0; k < kMf; ++k) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // 1 MFMA
+        __builtin_amdgcn_sched_group_barrier(0x002, 4, 0);  // then up to 4 VALU
+        if ((k & 3) == 3) __builtin_amdgcn_sched_group_barrier(0x200, 1, 0);  // then a DS write
+      }
+#endif
+      __syncthreads();
+    };
+    if (nst > 0) {
+      load(sa0, sb0);
+      write(sa0, sb0, 0);
+      load(sa1, sb1);
     }
-  }
-  __syncthreads();
-  // unrolled by two so the register stage sets stay compile-time (guide §5.4 rule 20)
-  for (int st = 0; st < nst; st += 2) {
-    if (st + 2 < nst) { opa.load(sa0); opb.load(sb0); }
-    compute(st & 1);
-    if (st + 1 < nst) write(sa1, sb1, (st + 1) & 1);
     __syncthreads();
-    if (st + 1 < nst) {
-      if (st + 3 < nst) { opa.load(sa1); opb.load(sb1); }
-      compute((st + 1) & 1);
-      if (st + 2 < nst) write(sa0, sb0, st & 1);
+    // unrolled by two so the register stage sets stay compile-time (guide §5.4 rule 20)
+    for (int st = 0; st < nst; st += 2) {
+      pipe(sa0, sb0, sa1, sb1, 0);
+      if (st + 1 >= nst) break;
+      pipe(sa1, sb1, sa0, sb0, 1);
+    }
+  } else {  // one register set: the loads of stage s+1 fly during the MFMAs of stage s
+    if (nst > 0) {
+      load(sa0, sb0);
+      write(sa0, sb0, 0);
+    }
+    __syncthreads();
+    for (int st = 0; st < nst; ++st) {
+      load(sa0, sb0);
+      compute(st & 1);
+      if (st + 1 < nst) write(sa0, sb0, (st + 1) & 1);
       __syncthreads();
     }
   }
@@ -318,14 +370,14 @@ __global__ __launch_bounds__(BM * BN / 64, 2) void sgemm_bf16x3_kernel(SxArgs p)
   // epilogue: C/D lane map col = lane & 31, row = (reg&3) + 8 (reg>>2) + 4 (lane>>5)
   const int h = lane >> 5;
 #pragma unroll
-  for (int i = 0; i < 2; ++i)
+  for (int i = 0; i < WMT; ++i)
 #pragma unroll
     for (int j = 0; j < 2; ++j) {
       const int col = n0 + wn * 64 + 32 * j + (lane & 31);
       if (col >= p.N) continue;
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
-        const int row = m0 + wm * 64 + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * h;
+        const int row = m0 + wm * 32 * WMT + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * h;
         if (row >= p.M) continue;
         const float v = DUAL ? acc[i][j][r] + cor[i][j][r] : acc[i][j][r];
         if (p.S > 1) {
@@ -357,35 +409,39 @@ __global__ __launch_bounds__(256) void sgemm_reduce_kernel(SxArgs p) {
   c[3] = sx_finish(p, row, col + 3, s.w);
 }
 
-template <int BM, int BN, int NPROD, bool DUAL>
+template <int BM, int BN, int NPROD, bool DUAL, bool TWO, int MINW = 2, int WMT = 2>
 void sx_launch_tile(const SxArgs& a, bool akm, bool bkm, unsigned grid, hipStream_t st) {
-  const dim3 blk(BM * BN / 64);
-  if (!akm && !bkm) hipLaunchKernelGGL((sgemm_bf16x3_kernel<BM, BN, false, false, NPROD, DUAL>), grid, blk, 0, st, a);
-  else if (!akm && bkm) hipLaunchKernelGGL((sgemm_bf16x3_kernel<BM, BN, false, true, NPROD, DUAL>), grid, blk, 0, st, a);
-  else if (akm && !bkm) hipLaunchKernelGGL((sgemm_bf16x3_kernel<BM, BN, true, false, NPROD, DUAL>), grid, blk, 0, st, a);
-  else hipLaunchKernelGGL((sgemm_bf16x3_kernel<BM, BN, true, true, NPROD, DUAL>), grid, blk, 0, st, a);
+  const dim3 blk(BM * BN / (32 * WMT));
+  if (!akm && !bkm) hipLaunchKernelGGL((sgemm_bf16x3_kernel<BM, BN, false, false, NPROD, DUAL, TWO, MINW, WMT>), grid, blk, 0, st, a);
+  else if (!akm && bkm) hipLaunchKernelGGL((sgemm_bf16x3_kernel<BM, BN, false, true, NPROD, DUAL, TWO, MINW, WMT>), grid, blk, 0, st, a);
+  else if (akm && !bkm) hipLaunchKernelGGL((sgemm_bf16x3_kernel<BM, BN, true, false, NPROD, DUAL, TWO, MINW, WMT>), grid, blk, 0, st, a);
+  else hipLaunchKernelGGL((sgemm_bf16x3_kernel<BM, BN, true, true, NPROD, DUAL, TWO, MINW, WMT>), grid, blk, 0, st, a);
 }
 
-constexpr int kSxTileM[3] = {128, 256, 128};
-constexpr int kSxTileN[3] = {128, 128, 256};
+constexpr int kSxTileM[5] = {128, 256, 128, 256, 256};
+constexpr int kSxTileN[5] = {128, 128, 256, 128, 128};
 
 }  // namespace
+
+void sgemm_f32_set_stagger(int on) { g_sx_stagger = on ? 1 : 0; }
 
 int64_t sgemm_f32_workspace_floats(int M, int N, int splits) {
   return splits > 1 ? int64_t(splits) * M * N : 0;
 }
 
-// variant: 0 = 6 products, dual accumulators (the shipped math); 1 = 6 products, one
-// accumulator; 2 = 9 products, dual; 3 = 3 products (hi.hi + hi.mid + mid.hi: ~16-bit, error
-// study only).  Variants 1-3 exist for the 128 x 128 tile only.
+// variant: 0 = 6 products, dual accumulators, one register stage set (the shipped math);
+// 1 = 6 products, one accumulator, software-pipelined split (two register sets); 2 = 9
+// products; 3 = 3 products (hi.hi + hi.mid + mid.hi: ~16-bit, error study only); 4 = variant 0
+// software-pipelined at one wave per SIMD (512 VGPRs; the dual accumulators do not fit the
+// pipeline at two waves per SIMD: 400+ bytes of spills).  Variants 1-4: 128 x 128 tile only.
 void sgemm_f32(uintptr_t a, int64_t lda, bool a_kmajor, uintptr_t b, int64_t ldb, bool b_kmajor, uintptr_t c,
                int64_t ldc, int M, int N, int K, bool beta, uintptr_t bias, int epi, uintptr_t aux, int64_t ldaux,
                int tile, int splits, int variant, uintptr_t ws, int64_t ws_floats, uintptr_t stream) {
   VODA_CHECK(M > 0 && N > 0 && K > 0, "sgemm_f32: empty GEMM");
   VODA_CHECK(K % kSxBK == 0, "sgemm_f32: K must be a multiple of 16");
   VODA_CHECK(M % 4 == 0 && N % 4 == 0, "sgemm_f32: M and N must be multiples of 4");
-  VODA_CHECK(tile >= 0 && tile < 3, "sgemm_f32: bad tile id");
-  VODA_CHECK(variant >= 0 && variant <= 3 && (variant == 0 || tile == 0), "sgemm_f32: bad math variant");
+  VODA_CHECK(tile >= 0 && tile < 5, "sgemm_f32: bad tile id");
+  VODA_CHECK(variant >= 0 && variant <= 4 && (variant == 0 || tile == 0), "sgemm_f32: bad math variant");
   VODA_CHECK(epi >= kSxEpiNone && epi <= kSxEpiDGelu && (epi == kSxEpiNone || aux != 0), "sgemm_f32: bad epilogue");
   VODA_CHECK(a % 16 == 0 && b % 16 == 0 && lda % 4 == 0 && ldb % 4 == 0, "sgemm_f32: operands need 16-B rows");
   VODA_CHECK(lda >= (a_kmajor ? M : K) && ldb >= (b_kmajor ? N : K) && ldc >= N, "sgemm_f32: leading dims");
@@ -407,6 +463,7 @@ void sgemm_f32(uintptr_t a, int64_t lda, bool a_kmajor, uintptr_t b, int64_t ldb
   p.tiles = ((M + BM - 1) / BM) * p.tiles_n;
   p.beta = beta ? 1 : 0;
   p.epi = epi;
+  p.stagger = g_sx_stagger;
   if (S > 1) {
     VODA_CHECK(ws != 0 && ws_floats >= sgemm_f32_workspace_floats(M, N, S), "sgemm_f32: split-K workspace too small");
     VODA_CHECK(c % 16 == 0 && ldc % 4 == 0, "sgemm_f32: split-K output needs 16-B rows");
@@ -417,14 +474,19 @@ void sgemm_f32(uintptr_t a, int64_t lda, bool a_kmajor, uintptr_t b, int64_t ldb
   const unsigned grid = unsigned(nwg);
   hipStream_t st = as_stream(stream);
   if (tile == 0) {
-    if (variant == 0) sx_launch_tile<128, 128, 6, true>(p, a_kmajor, b_kmajor, grid, st);
-    else if (variant == 1) sx_launch_tile<128, 128, 6, false>(p, a_kmajor, b_kmajor, grid, st);
-    else if (variant == 2) sx_launch_tile<128, 128, 9, true>(p, a_kmajor, b_kmajor, grid, st);
-    else sx_launch_tile<128, 128, 3, true>(p, a_kmajor, b_kmajor, grid, st);
+    if (variant == 0) sx_launch_tile<128, 128, 6, true, false>(p, a_kmajor, b_kmajor, grid, st);
+    else if (variant == 1) sx_launch_tile<128, 128, 6, false, true>(p, a_kmajor, b_kmajor, grid, st);
+    else if (variant == 2) sx_launch_tile<128, 128, 9, true, false>(p, a_kmajor, b_kmajor, grid, st);
+    else if (variant == 3) sx_launch_tile<128, 128, 3, true, false>(p, a_kmajor, b_kmajor, grid, st);
+    else sx_launch_tile<128, 128, 6, true, true, 1>(p, a_kmajor, b_kmajor, grid, st);
   } else if (tile == 1) {
-    sx_launch_tile<256, 128, 6, true>(p, a_kmajor, b_kmajor, grid, st);
-  } else {
-    sx_launch_tile<128, 256, 6, true>(p, a_kmajor, b_kmajor, grid, st);
+    sx_launch_tile<256, 128, 6, true, false>(p, a_kmajor, b_kmajor, grid, st);
+  } else if (tile == 2) {
+    sx_launch_tile<128, 256, 6, true, false>(p, a_kmajor, b_kmajor, grid, st);
+  } else if (tile == 3) {  // 4 waves of 128 x 64, one per SIMD, software-pipelined split
+    sx_launch_tile<256, 128, 6, true, true, 1, 4>(p, a_kmajor, b_kmajor, grid, st);
+  } else {                 // the same without the pipeline (A/B)
+    sx_launch_tile<256, 128, 6, true, false, 1, 4>(p, a_kmajor, b_kmajor, grid, st);
   }
   check_launch();
   if (S > 1) {

@@ -24,6 +24,7 @@ import torch.nn.functional as F
 
 from ..utils.flat import flat_grad
 from . import _native as N
+from . import splitgemm as SG
 from . import wgrad as W
 
 USE_WGRAD_KERNEL = True
@@ -49,8 +50,11 @@ def _split_count(M: int, n_out: int, K: int) -> int:
 
 
 def _dgrad(dy2: torch.Tensor, weight: torch.Tensor) -> torch.Tensor:
-    """dY [M, n_out] . W [n_out, K] -> [M, K] in dY's dtype (split-K for long reductions)."""
+    """dY [M, n_out] . W [n_out, K] -> [M, K] in dY's dtype (split-K for long reductions).
+    fp32 operands run on the split-bf16 MFMA kernel (ops/splitgemm.py) when it takes them."""
     global _BMM_F32
+    if SG.supported(dy2, weight):
+        return SG.matmul(dy2, weight)
     M, n_out = dy2.shape
     K = weight.shape[1]
     S = _split_count(M, n_out, K) if (USE_SPLIT_DGRAD and dy2.is_cuda and weight.is_contiguous()) else 1
@@ -114,7 +118,9 @@ def linear_weight_grads(dy2: torch.Tensor, x2: torch.Tensor, weight: torch.Tenso
     if need_w:
         if _direct(weight):
             gw = flat_grad(weight)
-            if gw.dtype == dy2.dtype:
+            if gw.dtype == torch.float32 and SG.supported(dy2.t(), x2):
+                SG.matmul(dy2.t(), x2, out=gw, accumulate=True)  # fp32: split-bf16 MFMA, beta = 1
+            elif gw.dtype == dy2.dtype:
                 gw.addmm_(dy2.t(), x2)
             else:  # fp32 flat gradient of a bf16 weight (cast first: see utils/flat.FOLD_CAST)
                 gw.add_((dy2.t() @ x2).to(gw.dtype))
@@ -161,7 +167,11 @@ class _DenseFn(torch.autograd.Function):
         if x.dtype != weight.dtype and torch.is_autocast_enabled(x.device.type):
             x = x.to(weight.dtype)
         with torch.autocast(x.device.type, enabled=False):
-            y = F.linear(x, weight, bias.to(weight.dtype) if bias is not None else None)
+            x2 = x.reshape(-1, x.shape[-1])
+            if x.dim() >= 1 and SG.supported(x2, weight.t()):  # fp32: split-bf16 MFMA kernel
+                y = SG.matmul(x2, weight.t(), bias=bias).view(*x.shape[:-1], weight.shape[0])
+            else:
+                y = F.linear(x, weight, bias.to(weight.dtype) if bias is not None else None)
         ctx.save_for_backward(x, weight)
         ctx.bias = bias
         ctx.sink_in = sink_in
@@ -184,7 +194,10 @@ class _DenseFn(torch.autograd.Function):
         if acc is not None:
             if acc.shape != x.shape or acc.dtype != dy2.dtype or not acc.is_contiguous():
                 acc = acc.to(dy2.dtype).contiguous()
-            acc.view(-1, K).addmm_(dy2, weight)  # dX = residual gradient + dY . W
+            if SG.supported(dy2, weight):
+                SG.matmul(dy2, weight, out=acc.view(-1, K), accumulate=True)
+            else:
+                acc.view(-1, K).addmm_(dy2, weight)  # dX = residual gradient + dY . W
             dx = acc
         elif ctx.needs_input_grad[0]:
             dx = _dgrad(dy2, weight).view(x.shape)

@@ -28,6 +28,7 @@ import torch.nn.functional as F
 
 from . import _native as N
 from . import dense as D
+from . import splitgemm as SG
 
 # VODA_GELU_EPILOGUE=0: the FFN runs FusedLinear -> GELU kernel -> FusedLinear (A/B switch)
 USE_GELU_EPILOGUE = os.environ.get("VODA_GELU_EPILOGUE", "1") != "0"
@@ -104,8 +105,14 @@ class _FFNGeluFn(torch.autograd.Function):
         if not x2.is_contiguous():
             x2 = x2.contiguous()
         with torch.autocast(x.device.type, enabled=False):
-            h, y = gemm_gelu_aux(x2, w1, b1)
-            out = F.linear(y, w2, b2.to(w2.dtype))
+            ctx.split = _split_ok(x2, w1, w2)
+            if ctx.split:  # fp32: split-bf16 MFMA GEMMs with the GELU in their epilogues
+                h = torch.empty(x2.shape[0], w1.shape[0], dtype=torch.float32, device=x2.device)
+                y = SG.matmul(x2, w1.t(), bias=b1, epi=SG.EPI_GELU, aux=h)
+                out = SG.matmul(y, w2.t(), bias=b2)
+            else:
+                h, y = gemm_gelu_aux(x2, w1, b1)
+                out = F.linear(y, w2, b2.to(w2.dtype))
         ctx.save_for_backward(x2, w1, w2, h, y)
         ctx.biases = (b1, b2)
         ctx.sink_in = sink_in
@@ -129,19 +136,25 @@ class _FFNGeluFn(torch.autograd.Function):
             need_b2 = False  # summed into the flat gradient by the LayerNorm backward
             hb.done = False
         dw2, db2 = D.linear_weight_grads(do2, y, w2, b2, need[3], need_b2)
-        try:
-            dh = gemm_dgelu(do2, w2, h)
-        except RuntimeError as e:  # no DGELU kernel after all: unfused, same math
-            disable_epilogue(str(e))
-            g = do2 @ w2
-            dh = (g.float() * gelu_tanh_grad_ref(h)).to(do2.dtype)
+        if ctx.split and SG.supported(do2, w2):
+            dh = SG.matmul(do2, w2, epi=SG.EPI_DGELU, aux=h)
+        else:
+            try:
+                dh = gemm_dgelu(do2, w2, h)
+            except RuntimeError as e:  # no DGELU kernel after all: unfused, same math
+                disable_epilogue(str(e))
+                g = do2 @ w2
+                dh = (g.float() * gelu_tanh_grad_ref(h)).to(do2.dtype)
         dw1, db1 = D.linear_weight_grads(dh, x2, w1, b1, need[1], need[2])
         dx = None
         acc = ctx.sink_in.take() if ctx.sink_in is not None and need[0] else None
         if acc is not None:
             if acc.shape != ctx.x_shape or acc.dtype != dh.dtype or not acc.is_contiguous():
                 acc = acc.to(dh.dtype).contiguous()
-            acc.view(-1, w1.shape[1]).addmm_(dh, w1)  # residual-stream gradient + dh . W1
+            if SG.supported(dh, w1):
+                SG.matmul(dh, w1, out=acc.view(-1, w1.shape[1]), accumulate=True)
+            else:
+                acc.view(-1, w1.shape[1]).addmm_(dh, w1)  # residual-stream gradient + dh . W1
             dx = acc
         elif need[0]:
             dx = D._dgrad(dh, w1).view(ctx.x_shape)
@@ -194,8 +207,19 @@ def shape_available(device: torch.device, dtype: torch.dtype, M: int, d_model: i
     return ok
 
 
+def _split_ok(x2: torch.Tensor, w1: torch.Tensor, w2: torch.Tensor) -> bool:
+    """Both FFN GEMMs on the split-bf16 kernel: fp32 operands of supported shapes."""
+    M, d = x2.shape
+    return (SG.supported(x2, w1.t()) and w2.shape[1] == w1.shape[0] and w1.shape[0] % 16 == 0
+            and w2.shape[0] % 4 == 0 and w2.dtype == torch.float32 and w2.is_contiguous())
+
+
 def supported(x: torch.Tensor, w1: torch.Tensor, b1, w2: torch.Tensor, b2) -> bool:
     dt = w1.dtype
+    if (USE_GELU_EPILOGUE and b1 is not None and b2 is not None and x.is_cuda and x.dtype == dt == w2.dtype == torch.float32
+            and w1.is_contiguous() and w2.is_contiguous() and x.shape[-1] % 16 == 0 and x.is_contiguous()
+            and _split_ok(x.reshape(-1, x.shape[-1]), w1, w2)):
+        return True  # split-bf16 path: needs no hipBLASLt epilogue kernels
     if not (USE_GELU_EPILOGUE and x.is_cuda and x.dtype == dt and w2.dtype == dt and b1 is not None
             and b2 is not None and w1.is_contiguous() and w2.is_contiguous() and x.shape[-1] % 8 == 0
             and w1.shape[0] % 8 == 0 and w2.shape[0] % 8 == 0 and epilogues_available(x.device, dt)):

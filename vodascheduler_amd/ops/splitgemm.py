@@ -26,9 +26,11 @@ from . import _native as N
 
 EPI_NONE, EPI_GELU, EPI_DGELU = 0, 1, 2
 TILES = {0: (128, 128), 1: (256, 128), 2: (128, 256)}
-# 0 = 6 products with the hi.hi products in their own accumulator (shipped); 1 = 6 products,
-# one accumulator; 2 = 9 products; 3 = 3 products (~16-bit: error study only)
-VARIANT_NAMES = {0: "bf16x3-6p-dual", 1: "bf16x3-6p-single", 2: "bf16x3-9p-dual", 3: "bf16x2-3p-dual"}
+# 0 = 6 products with the hi.hi products in their own accumulator (shipped); 1 = 6 products, one
+# accumulator, software-pipelined split; 2 = 9 products; 3 = 3 products (~16-bit: error study
+# only); 4 = 0 software-pipelined at one wave per SIMD (A/B)
+VARIANT_NAMES = {0: "bf16x3-6p-dual", 1: "bf16x3-6p-single-pipe", 2: "bf16x3-9p-dual", 3: "bf16x2-3p-dual",
+                 4: "bf16x3-6p-dual-pipe-1wave"}
 GEMM_MATH = VARIANT_NAMES[0]
 
 # VODA_SPLIT_GEMM=0 routes the fp32 projections back to hipBLASLt (A/B switch)
@@ -105,13 +107,17 @@ def supported(a: torch.Tensor, b: torch.Tensor) -> bool:
 
 
 def choose(M: int, Nn: int, K: int) -> tuple[int, int]:
-    """(tile, splits) for an M x N x K GEMM: the 128 x 128 tile (two workgroups per CU, 512
-    resident) unless the output is large, split-K when the tiles cannot fill the chip."""
+    """(tile, splits) for an M x N x K GEMM on the 128 x 128 tile (two workgroups per CU, 512
+    resident).  From the MI355X sweep over the BERT-base shapes (profiles/r6/splitgemm_probe.md):
+    >= 1024 output tiles run whole; 384-1023 tiles split K in two when K >= 2048 (the single
+    384-workgroup round leaves CUs with one workgroup idle half the time); small outputs (weight
+    gradients: 36-144 tiles) split K towards ~1152 workgroups with >= 256 k per split."""
     tiles = -(-M // 128) * -(-Nn // 128)
-    if tiles >= 384:
+    if tiles >= 1024:
         return 0, 1
-    kst = K // 16
-    s = max(1, min(kst // 16, -(-512 // tiles)))  # >= 16 stages (256 k) per split
+    if tiles >= 384:
+        return 0, 2 if K >= 2048 else 1
+    s = max(1, min(16, 1152 // tiles, K // 256))
     return 0, s
 
 
