@@ -265,6 +265,9 @@ class RcclComm {
 // 256x128 / 128x256; variant 0 = 6 products dual-accumulated (others: error study).
 int64_t sgemm_f32_workspace_floats(int M, int N, int splits);
 void sgemm_f32_set_stagger(int on);
+void sgemm_conv_wgrad_f32(uintptr_t dy, uintptr_t x, uintptr_t gw, int n, int H, int W, int Cin, int Ho, int Wo,
+                          int Cout, int KH, int KW, int stride, int pad, int splits, bool accumulate, uintptr_t ws,
+                          int64_t ws_floats, uintptr_t stream);
 void sgemm_f32(uintptr_t a, int64_t lda, bool a_kmajor, uintptr_t b, int64_t ldb, bool b_kmajor, uintptr_t c,
                int64_t ldc, int M, int N, int K, bool beta, uintptr_t bias, int epi, uintptr_t aux, int64_t ldaux,
                int tile, int splits, int variant, uintptr_t ws, int64_t ws_floats, uintptr_t stream);

@@ -38,6 +38,8 @@
 #include "common.h"
 #include "ops.h"
 
+#include <type_traits>
+
 namespace voda {
 
 namespace {
@@ -67,6 +69,10 @@ struct SxArgs {
   int tiles_n, tiles;
   int beta, epi;
   int stagger;                  // 1: odd workgroups at issue priority 1
+  // implicit-GEMM convolution weight gradient (B operand in CONV mode): B(n, k) = X[img][ho*cs +
+  // kh - cpad][wo*cs + kw - cpad][ci] for n = (kh*ckw + kw)*cin + ci and output pixel
+  // k = (img, ho, wo); zero outside the image.  X is NHWC [cn][ch][cw][cin].
+  int cn, ch, cw, cin, cho, cwo, cs, cpad, ckw;
 };
 
 int g_sx_stagger = 1;
@@ -125,6 +131,7 @@ struct SxStage {
 
 template <int R, bool KM, int T>
 struct SxOperand {
+  using Stage = SxStage<R, KM, T>;
   static constexpr int kUnits = 2 * R;
   static constexpr int kPer = (kUnits + T - 1) / T;
   const float* g[kPer];   // this thread's unit addresses at the current stage (first float4)
@@ -197,6 +204,106 @@ struct SxOperand {
   }
 };
 
+// K-major B operand of a convolution weight gradient, gathered from the NHWC input while it is
+// staged (no im2col buffer): unit u covers input channels ci..ci+3 of one filter tap (4 rows of
+// the B image) at output pixels kp and kp + 8 of the stage; each of the two pixels is tracked as
+// (img, ho, wo) and advanced 16 pixels per stage.  Taps falling outside the image read a valid
+// address and are zeroed at the LDS write (no branch around the load).
+template <int R, int T>
+struct SxConvStage {
+  static constexpr int kPer = (2 * R + T - 1) / T;
+  float4 v[kPer][2];
+  uint32_t keep;  // bit 2i + j: pixel j of unit i is inside the image
+};
+
+template <int R, int T>
+struct SxConvOperand {
+  using Stage = SxConvStage<R, T>;
+  static constexpr int kUnits = 2 * R;
+  static constexpr int kPer = (kUnits + T - 1) / T;
+  const float* x;
+  int img[kPer][2], ho[kPer][2], wo[kPer][2];
+  int dh[kPer], dw[kPer], ci[kPer];
+  int H, W, C, Ho, Wo, cs;
+  int woff[kPer], woff2[kPer];
+  bool on[kPer];
+
+  __device__ __forceinline__ void init(const SxArgs& p, int n0, int k0, int t) {
+    x = p.b;
+    H = p.ch; W = p.cw; C = p.cin; Ho = p.cho; Wo = p.cwo; cs = p.cs;
+#pragma unroll
+    for (int i = 0; i < kPer; ++i) {
+      const int u = t + i * T;
+      on[i] = (kUnits % T == 0) || u < kUnits;
+      const int uu = on[i] ? u : 0;
+      const int cg = uu % (R / 4), kp = uu / (R / 4);
+      const int n = min(n0 + 4 * cg, p.N - 4);
+      const int tap = n / C;
+      ci[i] = n - tap * C;
+      dh[i] = tap / p.ckw - p.cpad;
+      dw[i] = tap % p.ckw - p.cpad;
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int m = k0 + kp + 8 * j;
+        const int hw = Ho * Wo;
+        img[i][j] = m / hw;
+        const int r = m - img[i][j] * hw;
+        ho[i][j] = r / Wo;
+        wo[i][j] = r - ho[i][j] * Wo;
+      }
+      woff[i] = sx_km_off<R>(kp, 4 * cg);
+      woff2[i] = sx_km_off<R>(kp + 8, 4 * cg);
+    }
+  }
+
+  __device__ __forceinline__ void load(Stage& s, bool advance) {
+    s.keep = 0;
+#pragma unroll
+    for (int i = 0; i < kPer; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int hi = ho[i][j] * cs + dh[i], wi = wo[i][j] * cs + dw[i];
+        const bool ok = hi >= 0 && hi < H && wi >= 0 && wi < W;
+        const int64_t off = ok ? ((int64_t(img[i][j]) * H + hi) * W + wi) * C + ci[i] : 0;
+        s.v[i][j] = *reinterpret_cast<const float4*>(x + off);
+        s.keep |= uint32_t(ok) << (2 * i + j);
+        if (advance) {  // next stage: 16 output pixels on
+          int w2 = wo[i][j] + kSxBK, h2 = ho[i][j], n2 = img[i][j];
+          while (w2 >= Wo) {
+            w2 -= Wo;
+            if (++h2 == Ho) { h2 = 0; ++n2; }
+          }
+          wo[i][j] = w2; ho[i][j] = h2; img[i][j] = n2;
+        }
+      }
+  }
+
+  __device__ __forceinline__ void write(const Stage& s, uint8_t* img_, uint8_t* dummy) const {
+    constexpr int kPl = kSxBK * R * 2;
+#pragma unroll
+    for (int i = 0; i < kPer; ++i) {
+      const uint32_t m0 = (s.keep >> (2 * i)) & 1 ? 0xffffffffu : 0u, m1 = (s.keep >> (2 * i + 1)) & 1 ? 0xffffffffu : 0u;
+      const float4 a = s.v[i][0], b = s.v[i][1];
+      const float4 va = make_float4(__uint_as_float(__float_as_uint(a.x) & m0), __uint_as_float(__float_as_uint(a.y) & m0),
+                                    __uint_as_float(__float_as_uint(a.z) & m0), __uint_as_float(__float_as_uint(a.w) & m0));
+      const float4 vb = make_float4(__uint_as_float(__float_as_uint(b.x) & m1), __uint_as_float(__float_as_uint(b.y) & m1),
+                                    __uint_as_float(__float_as_uint(b.z) & m1), __uint_as_float(__float_as_uint(b.w) & m1));
+      uint2 h0, md0, l0, h1, md1, l1;
+      sx_split4(va, h0, md0, l0);
+      sx_split4(vb, h1, md1, l1);
+      uint8_t* p = on[i] ? img_ + woff[i] : dummy;
+      uint8_t* q = on[i] ? img_ + woff2[i] : dummy + 8;
+      const int pl = on[i] ? kPl : 16;
+      *reinterpret_cast<uint2*>(p) = h0;
+      *reinterpret_cast<uint2*>(p + pl) = md0;
+      *reinterpret_cast<uint2*>(p + 2 * pl) = l0;
+      *reinterpret_cast<uint2*>(q) = h1;
+      *reinterpret_cast<uint2*>(q + pl) = md1;
+      *reinterpret_cast<uint2*>(q + 2 * pl) = l1;
+    }
+  }
+};
+
 // three fragments (hi, mid, lo) of the 32-row tile starting at image row r0 for this lane
 template <int R, bool KM>
 __device__ __forceinline__ void sx_frag(const uint8_t* img, int r0, int lane, sx_bf16x8 (&f)[3]) {
@@ -234,7 +341,7 @@ __device__ __forceinline__ float sx_finish(const SxArgs& p, int row, int col, fl
 
 // WMT: 32-row MFMA tiles per wave along M (2: 64 x 64 per wave; 4: 128 x 64 per wave, one wave per
 // SIMD with its accumulators in AGPRs)
-template <int BM, int BN, bool AKM, bool BKM, int NPROD, bool DUAL, bool TWO_SETS, int MINW, int WMT>
+template <int BM, int BN, bool AKM, bool BKM, int NPROD, bool DUAL, bool TWO_SETS, int MINW, int WMT, bool CONV = false>
 __global__ __launch_bounds__(BM * BN / (32 * WMT), MINW) void sgemm_bf16x3_kernel(SxArgs p) {
   constexpr int NWN = BN / 64;
   constexpr int NWM = BM / (32 * WMT);
@@ -262,11 +369,14 @@ __global__ __launch_bounds__(BM * BN / (32 * WMT), MINW) void sgemm_bf16x3_kerne
   if (__builtin_amdgcn_readfirstlane(p.stagger & blockIdx.x) & 1) __builtin_amdgcn_s_setprio(1);
 
   SxOperand<BM, AKM, T> opa;
-  SxOperand<BN, BKM, T> opb;
+  using OpB = std::conditional_t<CONV, SxConvOperand<BN, T>, SxOperand<BN, BKM, T>>;
+  using StB = typename OpB::Stage;
+  OpB opb;
   opa.init(p.a, p.lda, m0, p.M, kb, t);
-  opb.init(p.b, p.ldb, n0, p.N, kb, t);
+  if constexpr (CONV) opb.init(p, n0, kb, t);
+  else opb.init(p.b, p.ldb, n0, p.N, kb, t);
   SxStage<BM, AKM, T> sa0, sa1;
-  SxStage<BN, BKM, T> sb0, sb1;
+  StB sb0, sb1;
 
   sx_f32x16 acc[WMT][2], cor[WMT][2];
 #pragma unroll
@@ -304,7 +414,7 @@ __global__ __launch_bounds__(BM * BN / (32 * WMT), MINW) void sgemm_bf16x3_kerne
         acc[i][j] = sx_mfma(fa[i][0], fb[j][0], acc[i][j]);
       }
   };
-  auto write = [&](const SxStage<BM, AKM, T>& sa, const SxStage<BN, BKM, T>& sb, int buf) {
+  auto write = [&](const SxStage<BM, AKM, T>& sa, const StB& sb, int buf) {
     uint8_t* A = smem + buf * kBuf;
     opa.write(sa, A, smem + 2 * kBuf);
     opb.write(sb, A + kImgA, smem + 2 * kBuf);
@@ -313,7 +423,7 @@ __global__ __launch_bounds__(BM * BN / (32 * WMT), MINW) void sgemm_bf16x3_kerne
   // stage k is read from global at load number k (clamped to the last stage), multiplied from
   // LDS buffer k & 1; the loads of stage s+2 fly while stage s is multiplied
   int nld = 0;
-  auto load = [&](SxStage<BM, AKM, T>& sa, SxStage<BN, BKM, T>& sb) {
+  auto load = [&](SxStage<BM, AKM, T>& sa, StB& sb) {
     const bool adv = ++nld < nst;
     opa.load(sa, adv);
     opb.load(sb, adv);
@@ -325,8 +435,8 @@ __global__ __launch_bounds__(BM * BN / (32 * WMT), MINW) void sgemm_bf16x3_kerne
     // software pipeline: iteration s loads stage s+2, multiplies stage s and splits stage s+1
     // (loaded one iteration earlier) into the other LDS buffer; the split's VALU and LDS writes
     // are interleaved with the MFMAs (sched_group_barrier), not issued after them
-    auto pipe = [&](SxStage<BM, AKM, T>& la, SxStage<BN, BKM, T>& lb, const SxStage<BM, AKM, T>& wa,
-                    const SxStage<BN, BKM, T>& wb, int buf) {
+    auto pipe = [&](SxStage<BM, AKM, T>& la, StB& lb, const SxStage<BM, AKM, T>& wa,
+                    const StB& wb, int buf) {
       load(la, lb);
       compute(buf);
       write(wa, wb, buf ^ 1);
@@ -389,7 +499,9 @@ __global__ __launch_bounds__(BM * BN / (32 * WMT), MINW) void sgemm_bf16x3_kerne
     }
 }
 
-// split-K: C = epilogue(sum over the S slabs), 4 columns per thread (N % 4 == 0)
+// split-K: C = epilogue(sum over the S slabs), 4 columns per thread (N % 4 == 0); four
+// independent partial sums keep several slab loads in flight per thread (S reaches the
+// hundreds for the convolution weight gradients)
 __global__ __launch_bounds__(256) void sgemm_reduce_kernel(SxArgs p) {
   const int64_t n4 = p.N >> 2;
   const int64_t i = int64_t(blockIdx.x) * 256 + threadIdx.x;
@@ -397,16 +509,28 @@ __global__ __launch_bounds__(256) void sgemm_reduce_kernel(SxArgs p) {
   const int row = int(i / n4), col = int(i - int64_t(row) * n4) * 4;
   const int64_t slab = int64_t(p.M) * p.N;
   const float* w = p.ws + int64_t(row) * p.N + col;
-  float4 s = *reinterpret_cast<const float4*>(w);
-  for (int k = 1; k < p.S; ++k) {
-    const float4 v = *reinterpret_cast<const float4*>(w + k * slab);
-    s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
+  float4 s[4];
+#pragma unroll
+  for (int u = 0; u < 4; ++u) s[u] = make_float4(0.f, 0.f, 0.f, 0.f);
+  int k = 0;
+  for (; k + 4 <= p.S; k += 4) {
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const float4 v = *reinterpret_cast<const float4*>(w + (k + u) * slab);
+      s[u].x += v.x; s[u].y += v.y; s[u].z += v.z; s[u].w += v.w;
+    }
   }
+  for (; k < p.S; ++k) {
+    const float4 v = *reinterpret_cast<const float4*>(w + k * slab);
+    s[0].x += v.x; s[0].y += v.y; s[0].z += v.z; s[0].w += v.w;
+  }
+  const float4 t = make_float4((s[0].x + s[1].x) + (s[2].x + s[3].x), (s[0].y + s[1].y) + (s[2].y + s[3].y),
+                               (s[0].z + s[1].z) + (s[2].z + s[3].z), (s[0].w + s[1].w) + (s[2].w + s[3].w));
   float* c = p.c + int64_t(row) * p.ldc + col;
-  c[0] = sx_finish(p, row, col, s.x);
-  c[1] = sx_finish(p, row, col + 1, s.y);
-  c[2] = sx_finish(p, row, col + 2, s.z);
-  c[3] = sx_finish(p, row, col + 3, s.w);
+  c[0] = sx_finish(p, row, col, t.x);
+  c[1] = sx_finish(p, row, col + 1, t.y);
+  c[2] = sx_finish(p, row, col + 2, t.z);
+  c[3] = sx_finish(p, row, col + 3, t.w);
 }
 
 template <int BM, int BN, int NPROD, bool DUAL, bool TWO, int MINW = 2, int WMT = 2>
@@ -491,6 +615,56 @@ void sgemm_f32(uintptr_t a, int64_t lda, bool a_kmajor, uintptr_t b, int64_t ldb
   check_launch();
   if (S > 1) {
     const int64_t items = int64_t(M) * (N / 4);
+    hipLaunchKernelGGL(sgemm_reduce_kernel, dim3(unsigned((items + 255) / 256)), dim3(256), 0, st, p);
+    check_launch();
+  }
+}
+
+// Convolution weight gradient dW[co][kh][kw][ci] (+)= sum over output pixels of dY[pix][co] *
+// X[pix shifted by the tap][ci] as ONE implicit GEMM on the split-bf16 MFMA kernel: A = dY^T
+// (K-major, [pixels][Cout]), B gathered from the NHWC input per tap (CONV operand), C = the
+// channels_last filter gradient viewed [Cout][KH*KW*Cin] (ResNet-50 fp32: replaces MIOpen's
+// igemm_wrw for the 3x3 layers with C >= 128, including the stride-2 ones).
+void sgemm_conv_wgrad_f32(uintptr_t dy, uintptr_t x, uintptr_t gw, int n, int H, int W, int Cin, int Ho, int Wo,
+                          int Cout, int KH, int KW, int stride, int pad, int splits, bool accumulate, uintptr_t ws,
+                          int64_t ws_floats, uintptr_t stream) {
+  const int64_t K = int64_t(n) * Ho * Wo;
+  const int N = KH * KW * Cin;
+  VODA_CHECK(n > 0 && Cout > 0 && Cin > 0 && K > 0 && K < (int64_t(1) << 31), "sgemm_conv_wgrad_f32: bad shape");
+  VODA_CHECK(K % kSxBK == 0, "sgemm_conv_wgrad_f32: output pixels must be a multiple of 16");
+  VODA_CHECK(Cout % 4 == 0 && Cin % 4 == 0, "sgemm_conv_wgrad_f32: channels must be multiples of 4");
+  VODA_CHECK(dy % 16 == 0 && x % 16 == 0, "sgemm_conv_wgrad_f32: operands need 16-B alignment");
+  VODA_CHECK(Ho == (H + 2 * pad - KH) / stride + 1 && Wo == (W + 2 * pad - KW) / stride + 1,
+             "sgemm_conv_wgrad_f32: output size mismatch");
+  SxArgs p{};
+  p.a = reinterpret_cast<const float*>(dy); p.lda = Cout;
+  p.b = reinterpret_cast<const float*>(x); p.ldb = Cin;
+  p.c = reinterpret_cast<float*>(gw); p.ldc = N;
+  p.M = Cout; p.N = N; p.K = int(K);
+  p.cn = n; p.ch = H; p.cw = W; p.cin = Cin; p.cho = Ho; p.cwo = Wo; p.cs = stride; p.cpad = pad; p.ckw = KW;
+  const int kst = int(K / kSxBK);
+  int S = splits < 1 ? 1 : splits;
+  if (S > kst) S = kst;
+  p.kps = ((kst + S - 1) / S) * kSxBK;
+  S = int((K + p.kps - 1) / p.kps);
+  p.S = S;
+  p.tiles_n = (N + 127) / 128;
+  p.tiles = ((Cout + 127) / 128) * p.tiles_n;
+  p.beta = accumulate ? 1 : 0;
+  p.stagger = g_sx_stagger;
+  if (S > 1) {
+    VODA_CHECK(ws != 0 && ws_floats >= sgemm_f32_workspace_floats(Cout, N, S), "sgemm_conv_wgrad_f32: workspace too small");
+    VODA_CHECK(gw % 16 == 0, "sgemm_conv_wgrad_f32: split-K output needs 16-B rows");
+    p.ws = reinterpret_cast<float*>(ws);
+  }
+  const int64_t nwg = int64_t(p.tiles) * S;
+  VODA_CHECK(nwg < (int64_t(1) << 31), "sgemm_conv_wgrad_f32: grid too large");
+  hipStream_t st = as_stream(stream);
+  hipLaunchKernelGGL((sgemm_bf16x3_kernel<128, 128, true, true, 6, true, false, 2, 2, true>), dim3(unsigned(nwg)),
+                     dim3(256), 0, st, p);
+  check_launch();
+  if (S > 1) {
+    const int64_t items = int64_t(Cout) * (N / 4);
     hipLaunchKernelGGL(sgemm_reduce_kernel, dim3(unsigned((items + 255) / 256)), dim3(256), 0, st, p);
     check_launch();
   }

@@ -106,3 +106,25 @@ def test_variants_error_ordering():
          for v in SG.VARIANT_NAMES}
     assert e[0] < 2e-7 and e[2] < 2e-7 and e[1] < 4e-7
     assert e[3] > 10 * e[0]
+
+
+@pytest.mark.parametrize("n,cin,cout,hw,stride", [(2, 128, 128, 16, 1), (3, 64, 132, 8, 1), (16, 128, 128, 7, 1),
+                                                  (2, 128, 256, 16, 2), (4, 256, 128, 7, 2)])
+def test_conv_wgrad_implicit_gemm_matches_fp64(n, cin, cout, hw, stride):
+    """dW (+)= conv weight gradient of a 3x3 pad-1 convolution (NHWC gather per tap in the
+    B-operand staging, zero padding, stride 1 / 2, ragged maps) against fp64."""
+    torch.manual_seed(cin + cout + hw + stride)
+    cl = torch.channels_last
+    x = torch.randn(n, cin, hw, hw, device=DEV).contiguous(memory_format=cl)
+    ho = (hw + 2 - 3) // stride + 1
+    if (n * ho * ho) % 16:
+        pytest.skip("pixel count not a multiple of 16")
+    dy = torch.randn(n, cout, ho, ho, device=DEV).contiguous(memory_format=cl)
+    gw = torch.randn(cout, cin, 3, 3, device=DEV).contiguous(memory_format=cl)
+    g0 = gw.clone()
+    assert SG.conv_wgrad_ok(dy, x, gw)
+    SG.conv_wgrad_(dy, x, gw, stride, 1, accumulate=True)
+    ref = torch.nn.grad.conv2d_weight(x.double(), gw.shape, dy.double(), stride=stride, padding=1)
+    bound = torch.nn.grad.conv2d_weight(x.double().abs(), gw.shape, dy.double().abs(), stride=stride, padding=1)
+    err = ((gw.double() - g0.double() - ref).abs() / (bound + 1)).max().item()
+    assert err < 1e-6, err

@@ -28,6 +28,7 @@ import torch.nn.functional as F
 
 from ..utils.flat import FOLD_CAST, flat_grad
 from . import _native as N
+from . import splitgemm as SG
 from . import wgrad as W
 
 # Kernel-path switches (module constants; tests monkeypatch them to reach the other branch):
@@ -65,6 +66,32 @@ USE_GEMM_F32 = True
 USE_BLAS_WGRAD_F32 = True
 BLAS_WGRAD_F32_MAX_M = 16384
 BLAS_WGRAD_F32_MIN_OUT = 1 << 20
+
+
+# fp32 1x1 GEMMs the f32-MFMA kernels above do not take (K >= 512 forwards, the input gradients
+# into a sink, all weight gradients) on the split-bf16 MFMA GEMM (ops/splitgemm.py: fp32 accuracy
+# on the bf16 matrix cores) instead of hipBLASLt / MIOpen.  Off: on ResNet-50's tall shapes the
+# split GEMM lost to the libraries in the step (same-box A/B 65.06 -> 68.95 ms with the weight
+# gradients, 66.75 ms without them; profiles/r6/ab_split_resnet50_fp32.jsonl)
+USE_SPLIT_GEMM_F32 = False
+USE_SPLIT_WGRAD_F32 = True   # ... including the weight gradients (else MIOpen / hipBLASLt as before)
+
+
+def _sx(a: torch.Tensor, b: torch.Tensor) -> bool:
+    return USE_SPLIT_GEMM_F32 and a.dtype == torch.float32 and SG.supported(a, b)
+
+
+def _mm(a: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
+    """a @ b on the split-bf16 GEMM when it takes the fp32 operands, else the library."""
+    return SG.matmul(a, b) if _sx(a, b) else a @ b
+
+
+def _addmm_(c: torch.Tensor, a: torch.Tensor, b: torch.Tensor) -> None:
+    """c += a @ b (c [M, N] with unit column stride)."""
+    if _sx(a, b) and c.dtype == torch.float32 and c.stride(1) == 1:
+        SG.matmul(a, b, out=c, accumulate=True)
+    else:
+        c.addmm_(a, b)
 
 
 def blas_wgrad_f32_ok(m: int, cout: int, cin: int) -> bool:
@@ -319,7 +346,7 @@ class _Conv1x1Fn(torch.autograd.Function):
         if y2 is None and x2.dtype == torch.float32:
             y2 = gemm_f32_2d(x2, w2)
         if y2 is None:
-            y2 = x2 @ w2.t()
+            y2 = _mm(x2, w2.t())
         ctx.save_for_backward(x2, weight)
         ctx.meta = (x.shape, stride, n, h, w)
         ctx.sink_in = sink_in if stride == 1 else None
@@ -364,17 +391,17 @@ class _Conv1x1Fn(torch.autograd.Function):
             acc = acc.to(dy2.dtype).contiguous(memory_format=torch.channels_last)  # still owned here
         if strided is not None:
             dx2 = mfma_dgrad(dy2, w2)
-            dx = (dx2 if dx2 is not None else dy2 @ w2).view(n, h, w, cin).permute(0, 3, 1, 2)
+            dx = (dx2 if dx2 is not None else _mm(dy2, w2)).view(n, h, w, cin).permute(0, 3, 1, 2)
             s_ = strided.stride
             subsample_add_(dx, strided.g, strided.stride)
         elif acc is not None:
-            _as_2d(acc).addmm_(dy2, w2)  # dX = shortcut gradient + dY . W (one hipBLASLt GEMM, beta = 1)
+            _addmm_(_as_2d(acc), dy2, w2)  # dX = shortcut gradient + dY . W (one GEMM, beta = 1)
             dx = acc
         elif dx is not None:
             pass  # the fused input gradient above
         elif ctx.needs_input_grad[0]:
             dx2 = mfma_dgrad(dy2, w2)
-            dxs = (dx2 if dx2 is not None else dy2 @ w2).view(n, h, w, cin).permute(0, 3, 1, 2)
+            dxs = (dx2 if dx2 is not None else _mm(dy2, w2)).view(n, h, w, cin).permute(0, 3, 1, 2)
             if stride > 1 and ctx.sink_out is not None and USE_STRIDED_SINK:
                 dx = _StridedGrad(dxs, stride, in_shape)  # the consumer adds it in place
             elif stride > 1:
@@ -387,6 +414,10 @@ class _Conv1x1Fn(torch.autograd.Function):
         if ctx.needs_input_grad[1]:
             g2 = flat_grad(weight).view(cout, cin) if _direct(weight) else None
             if (dy2.dtype == torch.float32 and g2 is not None and g2.dtype == torch.float32
+                    and USE_SPLIT_WGRAD_F32 and _sx(dy2.t(), x2)):
+                SG.matmul(dy2.t(), x2, out=g2, accumulate=True)  # split-K into the flat gradient
+                _ready(weight)
+            elif (dy2.dtype == torch.float32 and g2 is not None and g2.dtype == torch.float32
                     and blas_wgrad_f32_ok(dy2.shape[0], cout, cin)):
                 g2.addmm_(dy2.t(), x2)
                 _ready(weight)

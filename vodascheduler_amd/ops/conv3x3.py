@@ -27,12 +27,16 @@ import torch
 import torch.nn.functional as F
 
 from . import _native as N
+from . import splitgemm as SG
 from . import wgrad as W
 from . import winograd as Wg
 from ..utils.flat import FOLD_CAST, flat_grad
 from .conv1x1 import _direct, _ready
 
 USE_CONV_WGRAD = True
+# fp32 weight gradients of the C >= 128 layers (stride 1 and 2) as one implicit GEMM on the
+# split-bf16 MFMA kernel (ops/splitgemm.conv_wgrad_) instead of MIOpen's igemm_wrw (A/B switch)
+USE_SPLIT_WGRAD_F32 = True
 # USE_WINOGRAD (module switch): fp32 3x3 stride-1 pad-1 forwards and input gradients (as forward
 # convolutions) on the own Winograd F(2x2, 3x3) kernel (ops/winograd.py) instead of MIOpen
 USE_WINOGRAD = True
@@ -209,6 +213,9 @@ class _ConvKxKFn(torch.autograd.Function):
             gw = flat_grad(weight) if _direct(weight) else None
             if gw is not None and kernel_wgrad and supported(dy, x, gw):
                 conv_wgrad_accumulate_(dy, x, gw, stride, padding)
+                _ready(weight)
+            elif gw is not None and kernel_wgrad and USE_SPLIT_WGRAD_F32 and SG.conv_wgrad_ok(dy, x, gw):
+                SG.conv_wgrad_(dy, x, gw, stride, padding)  # fp32: implicit GEMM on the split-bf16 MFMA
                 _ready(weight)
             else:
                 dw = torch.ops.aten.convolution_backward(dy, x, weight, None, [stride, stride], [padding, padding],

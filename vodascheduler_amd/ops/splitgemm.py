@@ -117,7 +117,9 @@ def choose(M: int, Nn: int, K: int) -> tuple[int, int]:
         return 0, 1
     if tiles >= 384:
         return 0, 2 if K >= 2048 else 1
-    s = max(1, min(16, 1152 // tiles, K // 256))
+    # tiny outputs with huge reductions (ResNet 1x1 weight gradients: 64 x 256 over 800k pixels)
+    # split further: the slabs stay small
+    s = max(1, min(16 if tiles >= 16 else 1024, 1152 // tiles, K // 256))
     return 0, s
 
 
@@ -187,3 +189,51 @@ def linear(x: torch.Tensor, w: torch.Tensor, bias: torch.Tensor | None = None) -
     x2 = x.reshape(-1, x.shape[-1])
     y = matmul(x2, w.t(), bias=bias)
     return y.view(*x.shape[:-1], w.shape[0])
+
+
+def conv_wgrad_ok(dy: torch.Tensor, x: torch.Tensor, gw: torch.Tensor) -> bool:
+    """Does the implicit-GEMM convolution weight gradient take these fp32 operands?  dy
+    [N, Cout, Ho, Wo] and x [N, Cin, H, W] channels_last, gw the channels_last filter gradient
+    [Cout, Cin, KH, KW] (memory [Cout][KH][KW][Cin])."""
+    cl = torch.channels_last
+    if not (ENABLED and dy.is_cuda and x.is_cuda and gw.is_cuda):
+        return False
+    if not (dy.dtype == x.dtype == gw.dtype == torch.float32 and dy.dim() == x.dim() == gw.dim() == 4):
+        return False
+    if not (dy.is_contiguous(memory_format=cl) and x.is_contiguous(memory_format=cl)
+            and gw.is_contiguous(memory_format=cl)):
+        return False
+    n, cin = x.shape[:2]
+    cout = gw.shape[0]
+    if gw.shape[1] != cin or dy.shape[0] != n or dy.shape[1] != cout or cin % 4 or cout % 4:
+        return False
+    if (n * dy.shape[2] * dy.shape[3]) % 16:
+        return False
+    return dy.data_ptr() % 16 == 0 and x.data_ptr() % 16 == 0 and gw.data_ptr() % 16 == 0
+
+
+def conv_wgrad_splits(cout: int, n_cols: int, pixels: int) -> int:
+    """Split-K count of the convolution weight gradient: ~1024 workgroups (two rounds of the 512
+    resident 128 x 128 workgroups), >= 256 pixels per split."""
+    tiles = -(-cout // 128) * -(-n_cols // 128)
+    return max(1, min(1024 // tiles, pixels // 256))
+
+
+def conv_wgrad_(dy: torch.Tensor, x: torch.Tensor, gw: torch.Tensor, stride: int, padding: int,
+                accumulate: bool = True) -> None:
+    """``gw (+)= dW`` of a convolution on the split-bf16 MFMA kernel (callers check
+    ``conv_wgrad_ok``); CPU tensors get the fp32 reference."""
+    if not dy.is_cuda:
+        w = torch.nn.grad.conv2d_weight(x.float(), gw.shape, dy.float(), stride=stride, padding=padding)
+        gw.copy_(w + gw if accumulate else w)
+        return
+    n, cin, H, W = x.shape
+    cout, _, kh, kw = gw.shape
+    ho, wo = dy.shape[2], dy.shape[3]
+    s = conv_wgrad_splits(cout, kh * kw * cin, n * ho * wo)
+    h = N.hip()
+    ws_floats = h.sgemm_f32_workspace_floats(cout, kh * kw * cin, s)
+    ws = _workspace(dy.device, ws_floats) if ws_floats else None
+    h.sgemm_conv_wgrad_f32(dy.data_ptr(), x.data_ptr(), gw.data_ptr(), n, H, W, cin, ho, wo, cout, kh, kw,
+                           int(stride), int(padding), s, bool(accumulate), ws.data_ptr() if ws is not None else 0,
+                           ws.numel() if ws is not None else 0, N.stream_of(dy))
