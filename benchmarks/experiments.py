@@ -9,7 +9,7 @@ curves come from the MI355X-calibrated ``sim.trace.PROFILES``.
   5. FfDL Optimizer, 32-job Philly-style trace, 1/2/4/8 GPUs (all 8 policies side by side),
      and with autoscale: capacity ramping 1 -> 2 -> 4 -> 8 GPUs during the trace
 
-python benchmarks/experiments.py [--precision fp32] [--out profiles/r5_sim_experiments.md] [--bench-json SCALE.json]
+python benchmarks/experiments.py [--precision fp32] [--out profiles/r6_sim_experiments.md] [--bench-json SCALE.json]
 
 ``--precision`` (default fp32, the reference's and the driver bench's precision) is declared by
 every job of every trace: the same steps are priced at that precision's measured step time
@@ -120,7 +120,7 @@ def exp_info():
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--out", default="profiles/r5_sim_experiments.md")
+    ap.add_argument("--out", default="profiles/r6_sim_experiments.md")
     ap.add_argument("--precision", default="fp32", choices=["fp32", "bf16"],
                     help="compute precision every job declares (prices its steps)")
     ap.add_argument("--bench-json", default=None,
@@ -136,7 +136,7 @@ def main():
     rn, bb = model_profile("resnet50", PREC), model_profile("bert-base", PREC)
     what = ("fp32 compute, the reference's precision and the driver bench's" if PREC == "fp32"
             else "bf16 autocast compute, fp32 gradients")
-    lines = [f"# BASELINE.json configs in the discrete-event simulator (round 5, {PREC})", "",
+    lines = [f"# BASELINE.json configs in the discrete-event simulator (round 6, {PREC})", "",
              "Real training service / scheduler / allocator / placement code driven in virtual time "
              f"(`benchmarks/experiments.py --precision {PREC}`). Job speed model (`vodascheduler_amd/common/"
              f"workload.py`): single-GPU step times MEASURED on MI355X ({what}; "

@@ -6,11 +6,18 @@ all-reduce bus bandwidth (no multi-GPU box is available to this build).
 
     python benchmarks/predict_driver_timeline.py --step-ms resnet50=69.88,bert-base=37.12 \
         --out profiles/r5/driver_timeline_prediction.md
+    python benchmarks/predict_driver_timeline.py --bench-json profiles/r6/bench_n1_fp32_r6a.json \
+        --out profiles/r6/driver_timeline_prediction.md
+
+``--bench-json`` takes the step times from a measured N = 1 bench line
+(``warmup_single_gpu_step_ms``) and names that file in the output, so a CPU test
+(tests/test_timeline_prediction_cpu.py) can check the prediction is priced at the measured times.
 """
 from __future__ import annotations
 
 import argparse
 import copy
+import json
 import os
 import sys
 
@@ -51,16 +58,28 @@ def main() -> None:
     ap.add_argument("--step-ms", default="resnet50=69.88,bert-base=37.12",
                     help="measured fp32 single-GPU step ms (default: BENCH_r04 warm-up)")
     ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup-s", type=float, default=59.0,
-                    help="warm-up wall before the timed trace (BENCH_r04: 329 s command - 135 main - 135 control)")
+    ap.add_argument("--warmup-s", type=float, default=45.0,
+                    help="warm-up wall before the timed trace (BENCH_r05: 296.3 s command - 127.0 main - 127.0 "
+                         "control = 42.3 s, rounded up)")
     ap.add_argument("--comm-init-s", type=float, default=3.0, help="ASSUMED RCCL communicator build time")
     ap.add_argument("--deadline", type=float, default=540.0)
     ap.add_argument("--out", default=None)
+    ap.add_argument("--bench-json", default=None,
+                    help="measured bench.py JSON line: its warmup_single_gpu_step_ms replace --step-ms")
     a = ap.parse_args()
     step_ms = {k: float(v) for k, v in (kv.split("=") for kv in a.step_ms.split(","))}
+    source = "--step-ms"
+    if a.bench_json:
+        with open(a.bench_json) as f:
+            d = json.load(f)
+        d = d.get("line", d)  # bench.py --out detail file: the printed line is under "line"
+        step_ms = {k: float(v) for k, v in d["warmup_single_gpu_step_ms"].items()}
+        source = a.bench_json
     rows = [timeline(n, step_ms, a.steps, a.warmup_s, a.deadline, a.comm_init_s) for n in (1, 2, 4, 8)]
     lines = [
         "# Predicted driver timeline (`bench.py --gpus N --steps 20 --warmup 5`, fp32)",
+        "",
+        f"Step times source: `{source}`",
         "",
         f"SIMULATED (sim/simulator.py, the predictor bench.py itself uses), priced with fp32 step times {step_ms} ms "
         f"and an ASSUMED {ASSUMED_BUSBW_GBS:g} GB/s all-reduce busbw; warm-up {a.warmup_s:g} s and "

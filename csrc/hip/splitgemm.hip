@@ -341,7 +341,8 @@ __device__ __forceinline__ float sx_finish(const SxArgs& p, int row, int col, fl
 
 // WMT: 32-row MFMA tiles per wave along M (2: 64 x 64 per wave; 4: 128 x 64 per wave, one wave per
 // SIMD with its accumulators in AGPRs)
-template <int BM, int BN, bool AKM, bool BKM, int NPROD, bool DUAL, bool TWO_SETS, int MINW, int WMT, bool CONV = false>
+template <int BM, int BN, bool AKM, bool BKM, int NPROD, bool DUAL, bool TWO_SETS, int MINW, int WMT, bool CONV = false,
+          int ORDER = 0>
 __global__ __launch_bounds__(BM * BN / (32 * WMT), MINW) void sgemm_bf16x3_kernel(SxArgs p) {
   constexpr int NWN = BN / 64;
   constexpr int NWM = BM / (32 * WMT);
@@ -394,25 +395,43 @@ __global__ __launch_bounds__(BM * BN / (32 * WMT), MINW) void sgemm_bf16x3_kerne
     for (int i = 0; i < WMT; ++i) sx_frag<BM, AKM>(A, wm * 32 * WMT + 32 * i, lane, fa[i]);
     sx_frag<BN, BKM>(B, wn * 64, lane, fb[0]);
     sx_frag<BN, BKM>(B, wn * 64 + 32, lane, fb[1]);
+    if constexpr (ORDER == 0) {  // tile-outer: each accumulator's products back to back
 #pragma unroll
-    for (int i = 0; i < WMT; ++i)
+      for (int i = 0; i < WMT; ++i)
 #pragma unroll
-      for (int j = 0; j < 2; ++j) {
-        sx_f32x16& s = DUAL ? cor[i][j] : acc[i][j];
-        if (NPROD >= 9) {
-          s = sx_mfma(fa[i][2], fb[j][2], s);
-          s = sx_mfma(fa[i][1], fb[j][2], s);
-          s = sx_mfma(fa[i][2], fb[j][1], s);
+        for (int j = 0; j < 2; ++j) {
+          sx_f32x16& s = DUAL ? cor[i][j] : acc[i][j];
+          if (NPROD >= 9) {
+            s = sx_mfma(fa[i][2], fb[j][2], s);
+            s = sx_mfma(fa[i][1], fb[j][2], s);
+            s = sx_mfma(fa[i][2], fb[j][1], s);
+          }
+          if (NPROD >= 6) {
+            s = sx_mfma(fa[i][1], fb[j][1], s);
+            s = sx_mfma(fa[i][0], fb[j][2], s);
+            s = sx_mfma(fa[i][2], fb[j][0], s);
+          }
+          s = sx_mfma(fa[i][0], fb[j][1], s);
+          s = sx_mfma(fa[i][1], fb[j][0], s);
+          acc[i][j] = sx_mfma(fa[i][0], fb[j][0], acc[i][j]);
         }
-        if (NPROD >= 6) {
-          s = sx_mfma(fa[i][1], fb[j][1], s);
-          s = sx_mfma(fa[i][0], fb[j][2], s);
-          s = sx_mfma(fa[i][2], fb[j][0], s);
-        }
-        s = sx_mfma(fa[i][0], fb[j][1], s);
-        s = sx_mfma(fa[i][1], fb[j][0], s);
-        acc[i][j] = sx_mfma(fa[i][0], fb[j][0], acc[i][j]);
-      }
+    } else {  // product-outer: consecutive MFMAs write different accumulators
+      constexpr int kPa[8] = {2, 1, 2, 1, 0, 2, 0, 1}, kPb[8] = {2, 2, 1, 1, 2, 0, 1, 0};
+      constexpr int p0 = NPROD >= 9 ? 0 : NPROD >= 6 ? 3 : 6;
+#pragma unroll
+      for (int q = p0; q < 8; ++q)
+#pragma unroll
+        for (int i = 0; i < WMT; ++i)
+#pragma unroll
+          for (int j = 0; j < 2; ++j) {
+            sx_f32x16& s = DUAL ? cor[i][j] : acc[i][j];
+            s = sx_mfma(fa[i][kPa[q]], fb[j][kPb[q]], s);
+          }
+#pragma unroll
+      for (int i = 0; i < WMT; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[i][j] = sx_mfma(fa[i][0], fb[j][0], acc[i][j]);
+    }
   };
   auto write = [&](const SxStage<BM, AKM, T>& sa, const StB& sb, int buf) {
     uint8_t* A = smem + buf * kBuf;
@@ -533,13 +552,13 @@ __global__ __launch_bounds__(256) void sgemm_reduce_kernel(SxArgs p) {
   c[3] = sx_finish(p, row, col + 3, t.w);
 }
 
-template <int BM, int BN, int NPROD, bool DUAL, bool TWO, int MINW = 2, int WMT = 2>
+template <int BM, int BN, int NPROD, bool DUAL, bool TWO, int MINW = 2, int WMT = 2, int ORDER = 0>
 void sx_launch_tile(const SxArgs& a, bool akm, bool bkm, unsigned grid, hipStream_t st) {
   const dim3 blk(BM * BN / (32 * WMT));
-  if (!akm && !bkm) hipLaunchKernelGGL((sgemm_bf16x3_kernel<BM, BN, false, false, NPROD, DUAL, TWO, MINW, WMT>), grid, blk, 0, st, a);
-  else if (!akm && bkm) hipLaunchKernelGGL((sgemm_bf16x3_kernel<BM, BN, false, true, NPROD, DUAL, TWO, MINW, WMT>), grid, blk, 0, st, a);
-  else if (akm && !bkm) hipLaunchKernelGGL((sgemm_bf16x3_kernel<BM, BN, true, false, NPROD, DUAL, TWO, MINW, WMT>), grid, blk, 0, st, a);
-  else hipLaunchKernelGGL((sgemm_bf16x3_kernel<BM, BN, true, true, NPROD, DUAL, TWO, MINW, WMT>), grid, blk, 0, st, a);
+  if (!akm && !bkm) hipLaunchKernelGGL((sgemm_bf16x3_kernel<BM, BN, false, false, NPROD, DUAL, TWO, MINW, WMT, false, ORDER>), grid, blk, 0, st, a);
+  else if (!akm && bkm) hipLaunchKernelGGL((sgemm_bf16x3_kernel<BM, BN, false, true, NPROD, DUAL, TWO, MINW, WMT, false, ORDER>), grid, blk, 0, st, a);
+  else if (akm && !bkm) hipLaunchKernelGGL((sgemm_bf16x3_kernel<BM, BN, true, false, NPROD, DUAL, TWO, MINW, WMT, false, ORDER>), grid, blk, 0, st, a);
+  else hipLaunchKernelGGL((sgemm_bf16x3_kernel<BM, BN, true, true, NPROD, DUAL, TWO, MINW, WMT, false, ORDER>), grid, blk, 0, st, a);
 }
 
 constexpr int kSxTileM[5] = {128, 256, 128, 256, 256};
@@ -557,7 +576,8 @@ int64_t sgemm_f32_workspace_floats(int M, int N, int splits) {
 // 1 = 6 products, one accumulator, software-pipelined split (two register sets); 2 = 9
 // products; 3 = 3 products (hi.hi + hi.mid + mid.hi: ~16-bit, error study only); 4 = variant 0
 // software-pipelined at one wave per SIMD (512 VGPRs; the dual accumulators do not fit the
-// pipeline at two waves per SIMD: 400+ bytes of spills).  Variants 1-4: 128 x 128 tile only.
+// pipeline at two waves per SIMD: 400+ bytes of spills); 5 = variant 0 with the products issued
+// product-outer (consecutive MFMAs on different accumulators).  Variants 1-5: 128 x 128 only.
 void sgemm_f32(uintptr_t a, int64_t lda, bool a_kmajor, uintptr_t b, int64_t ldb, bool b_kmajor, uintptr_t c,
                int64_t ldc, int M, int N, int K, bool beta, uintptr_t bias, int epi, uintptr_t aux, int64_t ldaux,
                int tile, int splits, int variant, uintptr_t ws, int64_t ws_floats, uintptr_t stream) {
@@ -565,7 +585,7 @@ void sgemm_f32(uintptr_t a, int64_t lda, bool a_kmajor, uintptr_t b, int64_t ldb
   VODA_CHECK(K % kSxBK == 0, "sgemm_f32: K must be a multiple of 16");
   VODA_CHECK(M % 4 == 0 && N % 4 == 0, "sgemm_f32: M and N must be multiples of 4");
   VODA_CHECK(tile >= 0 && tile < 5, "sgemm_f32: bad tile id");
-  VODA_CHECK(variant >= 0 && variant <= 4 && (variant == 0 || tile == 0), "sgemm_f32: bad math variant");
+  VODA_CHECK(variant >= 0 && variant <= 5 && (variant == 0 || tile == 0), "sgemm_f32: bad math variant");
   VODA_CHECK(epi >= kSxEpiNone && epi <= kSxEpiDGelu && (epi == kSxEpiNone || aux != 0), "sgemm_f32: bad epilogue");
   VODA_CHECK(a % 16 == 0 && b % 16 == 0 && lda % 4 == 0 && ldb % 4 == 0, "sgemm_f32: operands need 16-B rows");
   VODA_CHECK(lda >= (a_kmajor ? M : K) && ldb >= (b_kmajor ? N : K) && ldc >= N, "sgemm_f32: leading dims");
@@ -602,7 +622,8 @@ void sgemm_f32(uintptr_t a, int64_t lda, bool a_kmajor, uintptr_t b, int64_t ldb
     else if (variant == 1) sx_launch_tile<128, 128, 6, false, true>(p, a_kmajor, b_kmajor, grid, st);
     else if (variant == 2) sx_launch_tile<128, 128, 9, true, false>(p, a_kmajor, b_kmajor, grid, st);
     else if (variant == 3) sx_launch_tile<128, 128, 3, true, false>(p, a_kmajor, b_kmajor, grid, st);
-    else sx_launch_tile<128, 128, 6, true, true, 1>(p, a_kmajor, b_kmajor, grid, st);
+    else if (variant == 4) sx_launch_tile<128, 128, 6, true, true, 1>(p, a_kmajor, b_kmajor, grid, st);
+    else sx_launch_tile<128, 128, 6, true, false, 2, 2, 1>(p, a_kmajor, b_kmajor, grid, st);
   } else if (tile == 1) {
     sx_launch_tile<256, 128, 6, true, false>(p, a_kmajor, b_kmajor, grid, st);
   } else if (tile == 2) {

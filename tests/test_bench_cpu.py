@@ -72,7 +72,7 @@ def test_bench_control_overrun_keeps_headline():
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2", "--master-addr",
            "127.0.0.1", "--master-port", str(free_port()), os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps",
            "4", "--warmup", "1", "--jobs", "6", "--device", "cpu", "--rate-limit", "0.5", "--interarrival", "0.3",
-           "--control-timeout", "1.5"]
+           "--control-timeout", "0.2"]  # far below the control's run time on any host (was 1.5 s: flaky on fast hosts)
     r = subprocess.run(cmd, cwd="/tmp", capture_output=True, text=True, timeout=180)
     assert r.returncode == 0, r.stderr[-3000:]
     lines = [l for l in r.stdout.splitlines() if l.startswith("{")]

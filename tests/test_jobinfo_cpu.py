@@ -205,9 +205,9 @@ def test_fp32_trace_priced_at_measured_fp32_step_times():
             assert info["estimated_remainning_time_sec"] == pytest.approx(
                 epochs * wl["steps_per_epoch"] * meas[wl["model"]])
             assert info["step_time_sec"]["1"] == pytest.approx(meas[wl["model"]])
-        # the fp32 profiles themselves are fp32-scale (3-4x the bf16 ones)
+        # the fp32 profiles themselves are fp32-scale (2.5-4x the bf16 ones)
         for m in meas:
-            assert model_profile(m, "fp32").step_time_1gpu > 3 * PROFILES[m].step_time_1gpu
+            assert model_profile(m, "fp32").step_time_1gpu > 2.5 * PROFILES[m].step_time_1gpu
             assert model_profile(m, "fp32").t1() == pytest.approx(meas[m])   # measured beats profile
             # ... and only the fp32 profile: the bf16 one keeps its own step time
             assert model_profile(m, "bf16").t1() == pytest.approx(PROFILES[m].step_time_1gpu)

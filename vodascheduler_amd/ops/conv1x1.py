@@ -74,7 +74,9 @@ BLAS_WGRAD_F32_MIN_OUT = 1 << 20
 # split GEMM lost to the libraries in the step (same-box A/B 65.06 -> 68.95 ms with the weight
 # gradients, 66.75 ms without them; profiles/r6/ab_split_resnet50_fp32.jsonl)
 USE_SPLIT_GEMM_F32 = False
-USE_SPLIT_WGRAD_F32 = True   # ... including the weight gradients (else MIOpen / hipBLASLt as before)
+# the fp32 1x1 weight gradients (reduction over the pixels) on the split-bf16 GEMM, split-K to
+# ~1024 workgroups (else MIOpen / hipBLASLt as before)
+USE_SPLIT_WGRAD_F32 = False  # pending a same-box A/B (docs/PERFORMANCE.md round 6)
 
 
 def _sx(a: torch.Tensor, b: torch.Tensor) -> bool:
@@ -414,8 +416,10 @@ class _Conv1x1Fn(torch.autograd.Function):
         if ctx.needs_input_grad[1]:
             g2 = flat_grad(weight).view(cout, cin) if _direct(weight) else None
             if (dy2.dtype == torch.float32 and g2 is not None and g2.dtype == torch.float32
-                    and USE_SPLIT_WGRAD_F32 and _sx(dy2.t(), x2)):
-                SG.matmul(dy2.t(), x2, out=g2, accumulate=True)  # split-K into the flat gradient
+                    and USE_SPLIT_WGRAD_F32 and SG.supported(dy2.t(), x2)):
+                # split-K into the flat gradient, ~1024 workgroups over the pixels
+                SG.matmul(dy2.t(), x2, out=g2, accumulate=True, tile=0,
+                          splits=SG.conv_wgrad_splits(cout, cin, dy2.shape[0]))
                 _ready(weight)
             elif (dy2.dtype == torch.float32 and g2 is not None and g2.dtype == torch.float32
                     and blas_wgrad_f32_ok(dy2.shape[0], cout, cin)):

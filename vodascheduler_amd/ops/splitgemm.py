@@ -30,7 +30,7 @@ TILES = {0: (128, 128), 1: (256, 128), 2: (128, 256)}
 # accumulator, software-pipelined split; 2 = 9 products; 3 = 3 products (~16-bit: error study
 # only); 4 = 0 software-pipelined at one wave per SIMD (A/B)
 VARIANT_NAMES = {0: "bf16x3-6p-dual", 1: "bf16x3-6p-single-pipe", 2: "bf16x3-9p-dual", 3: "bf16x2-3p-dual",
-                 4: "bf16x3-6p-dual-pipe-1wave"}
+                 4: "bf16x3-6p-dual-pipe-1wave", 5: "bf16x3-6p-dual-product-outer"}
 GEMM_MATH = VARIANT_NAMES[0]
 
 # VODA_SPLIT_GEMM=0 routes the fp32 projections back to hipBLASLt (A/B switch)
