@@ -43,14 +43,15 @@ def main():
         w = (torch.randn(c, c, 3, 3, device="cuda") / (3 * c ** 0.5)).contiguous(memory_format=torch.channels_last)
         gf = 2.0 * n * h * h * c * c * 9 / 1e9
         row = {"C": c, "H": h, "N": n, "gflop_direct": round(gf, 1)}
-        y = Wg.conv3x3_wino(x, w)
         ref = F.conv2d(x[:2].double(), w.double(), None, 1, 1)
-        row["relerr_vs_fp64"] = float(((y[:2].double() - ref).norm() / ref.norm()).item())
-        u = Wg.filter_transform(w)
-        row["wino_us"] = round(timeit(lambda: Wg.conv3x3_wino(x, w, u)), 1)
-        row["wino_filter_us"] = round(timeit(lambda: Wg.filter_transform(w)), 1)
+        for tag, sx in (("", False), ("_sx", True)):  # f32 MFMA / split-bf16 tile GEMMs
+            u = Wg.filter_transform(w, sx=sx)
+            y = Wg.conv3x3_wino(x, w, u)
+            row["relerr_vs_fp64" + tag] = float(((y[:2].double() - ref).norm() / ref.norm()).item())
+            row["wino_us" + tag] = round(timeit(lambda: Wg.conv3x3_wino(x, w, u)), 1)
+            row["wino_filter_us" + tag] = round(timeit(lambda: Wg.filter_transform(w, sx=sx)), 1)
+            row["wino_eff_tf" + tag] = round(gf / row["wino_us" + tag] * 1e3, 1)
         row["miopen_us"] = round(timeit(lambda: F.conv2d(x, w, None, 1, 1)), 1)
-        row["wino_eff_tf"] = round(gf / row["wino_us"] * 1e3, 1)
         row["miopen_tf"] = round(gf / row["miopen_us"] * 1e3, 1)
         print(json.dumps(row), flush=True)
 

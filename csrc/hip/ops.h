@@ -140,10 +140,10 @@ void gemm_bnstats(uintptr_t x, uintptr_t w, uintptr_t y, uintptr_t part, int64_t
 int64_t conv3x3_c64_wgrad_workspace_floats(int N, int H);
 bool wino_f23_supported(int C, int Co);
 void wino_f23_filter(uintptr_t w, int64_t s0, int64_t s1, int64_t s2, int64_t s3, uintptr_t u, int Co, int C,
-                     bool flip, uintptr_t stream);
+                     bool flip, bool sx, uintptr_t stream);
 int wino_f23_groups(int N, int H, int W, int C, int Co);
 void wino_f23_fwd(uintptr_t x, uintptr_t u, uintptr_t y, uintptr_t part, int N, int H, int W, int C, int Co, int G,
-                  uintptr_t stream);
+                  bool sx, uintptr_t stream);
 void filter_flip_t(uintptr_t w, int in_dt, int64_t s0, int64_t s1, int64_t s2, int64_t s3, uintptr_t out,
                    int out_dt, int Cout, int Cin, int K, uintptr_t stream);
 void conv3x3_c64_wgrad(uintptr_t x, uintptr_t dy, uintptr_t dw, int64_t s0, int64_t s1, int64_t s2, int64_t s3,

@@ -17,6 +17,14 @@
 //   * after the last chunk the 16 accumulators of every (tile, channel) meet in LDS and each
 //     thread applies A^T M A to four of them and stores the 2x2 outputs.
 // The filter transform (wino_f23_filter) runs once per use; the weights change every step.
+//
+// SX (round 6): the 16 tile GEMMs at fp32 accuracy on the bf16 matrix cores
+// (v_mfma_f32_32x32x16_bf16), the exact 3-way bf16 split of splitgemm.hip: the filter transform
+// writes U split into hi / mid / lo bf16 planes ([p][plane][C/8][Co][8]); each wave reads its V
+// fragment (8 consecutive channels of one tile, 2 x 16-B LDS reads) as fp32, splits it in registers
+// and accumulates the six significant cross products (hh, hm, mh, hl, lh, mm) into one fp32
+// accumulator per position: 6 x 32 cycles per 16 channels instead of 8 x 64 for the f32 MFMA.
+// Staging, V layout, exchange and inverse transform are the f32 kernel's.
 #include "common.h"
 #include "ops.h"
 
@@ -32,6 +40,39 @@ __device__ __forceinline__ f32x16 wmfma(float a, float b, f32x16 c) {
   return __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, c, 0, 0, 0);
 }
 
+typedef __bf16 wsx_bf16x8 __attribute__((ext_vector_type(8)));
+typedef float wsx_f32x2 __attribute__((ext_vector_type(2)));
+typedef __bf16 wsx_bf16x2 __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ uint32_t wsx_pack2(float a, float b) {  // one v_cvt_pk_bf16_f32 (RNE)
+  const wsx_f32x2 f = {a, b};
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector(f, wsx_bf16x2));
+}
+// exact split of 8 fp32 values into three bf16x8 planes (x == hi + mid + lo)
+__device__ __forceinline__ void wsx_split8(const float4 v0, const float4 v1, uint4& h, uint4& m, uint4& l) {
+  const float x[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
+  uint32_t hh[4], mm[4], ll[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    hh[i] = wsx_pack2(x[2 * i], x[2 * i + 1]);
+    const float r0 = x[2 * i] - __uint_as_float(hh[i] << 16), r1 = x[2 * i + 1] - __uint_as_float(hh[i] & 0xffff0000u);
+    mm[i] = wsx_pack2(r0, r1);
+    const float q0 = r0 - __uint_as_float(mm[i] << 16), q1 = r1 - __uint_as_float(mm[i] & 0xffff0000u);
+    ll[i] = wsx_pack2(q0, q1);
+  }
+  h = make_uint4(hh[0], hh[1], hh[2], hh[3]);
+  m = make_uint4(mm[0], mm[1], mm[2], mm[3]);
+  l = make_uint4(ll[0], ll[1], ll[2], ll[3]);
+}
+__device__ __forceinline__ f32x16 wsx_mfma(const uint4 a, const uint4 b, const f32x16 c) {
+  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(wsx_bf16x8, a), __builtin_bit_cast(wsx_bf16x8, b),
+                                                 c, 0, 0, 0);
+}
+
+#ifndef WSX_PREFETCH
+#define WSX_PREFETCH 1
+#endif
+
 constexpr int kWT = 32;           // tiles per workgroup
 constexpr int kWN = 32;           // output channels per workgroup
 constexpr int kWK = 32;           // input channels per chunk
@@ -40,7 +81,7 @@ constexpr int kWThreads = 256;
 
 struct WinoArgs {
   const float* x;  // [N][H][W][C]
-  const float* u;  // [16][C / 8][Co][8]
+  const float* u;  // [16][C / 8][Co][8]; SX: bf16 [16][3][C / 8][Co][8]
   float* y;        // [N][H][W][Co]
   float* part;     // [2][G][Co] BN partial sums (sum, sum of squares) of y, or null
   int N, H, W, C, Co;
@@ -49,6 +90,23 @@ struct WinoArgs {
   int G;           // workgroups along the tiles (gridDim.x); each walks tile blocks x, x + G, ...
 };
 
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t wino_patch_rsrc(const WinoArgs& a) {
+  const float* base = a.x - (int64_t(a.W) + 1) * a.C;
+  const int64_t bytes = (int64_t(a.N) * a.H * a.W * a.C + (int64_t(a.W) + 1) * a.C) * 4;
+  const uint64_t pb = reinterpret_cast<uint64_t>(base);
+  const uint32_t lo = __builtin_amdgcn_readfirstlane(uint32_t(pb)), hi = __builtin_amdgcn_readfirstlane(uint32_t(pb >> 32));
+  return __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void*>((uint64_t(hi) << 32) | lo), 0,
+                                           __builtin_amdgcn_readfirstlane(int(bytes)), 0x00020000);
+}
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t wino_u_rsrc(const WinoArgs& a) {
+  const uint64_t pb = reinterpret_cast<uint64_t>(a.u);
+  const uint32_t lo = __builtin_amdgcn_readfirstlane(uint32_t(pb)), hi = __builtin_amdgcn_readfirstlane(uint32_t(pb >> 32));
+  return __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void*>((uint64_t(hi) << 32) | lo), 0,
+                                           __builtin_amdgcn_readfirstlane(int(int64_t(96) * a.C * a.Co)), 0x00020000);
+}
+
+template <bool SX>
 __global__ __launch_bounds__(kWThreads, 2) void wino_f23_fwd_kernel(WinoArgs a) {
   __shared__ __attribute__((aligned(16))) float lds[16 * kWT * kWP];  // V chunk, then M exchange
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, lc = lane & 31, lh = lane >> 5;
@@ -60,6 +118,15 @@ __global__ __launch_bounds__(kWThreads, 2) void wino_f23_fwd_kernel(WinoArgs a) 
   bool tok = false;
   int h0 = 0, w0 = 0;
   const float* xn = a.x;
+  // SX: buffer loads of the patch (voffset + uniform soffset, zero-fill out of range) instead of
+  // 16 hoisted 64-bit pointers.  The resource starts at pixel (-1, -1) of image 0, so every offset
+  // of a (-1-padded) patch is >= 0; a pixel outside the image gets an out-of-range voffset.
+  const __amdgpu_buffer_rsrc_t xr = wino_patch_rsrc(a);
+  // SX: U fragments by buffer loads too: lane (lc, lh) reads 16 B at (lh * Co + lc) * 16 from a
+  // wave-uniform (position, plane, 8-channel block, co0) origin
+  const __amdgpu_buffer_rsrc_t ur = wino_u_rsrc(a);
+  const uint32_t uvo = uint32_t((lh * a.Co + lc) * 16);
+  uint32_t vb = 0, okm = 0;  // byte offset of the patch origin + 16 sq; validity bits 4i + j
   auto tile_setup = [&](int64_t blk) {
     const int64_t tg = blk * kWT + st;
     tok = tg < a.T;
@@ -70,10 +137,34 @@ __global__ __launch_bounds__(kWThreads, 2) void wino_f23_fwd_kernel(WinoArgs a) 
     h0 = 2 * ty - 1;
     w0 = 2 * tx - 1;
     xn = a.x + int64_t(n) * a.H * a.W * a.C;
+    if constexpr (SX) {
+      vb = uint32_t(((int64_t(n) * a.H + h0 + 1) * a.W + w0 + 1) * a.C * 4 + 16 * sq);
+      okm = 0;
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int hh = h0 + i, ww = w0 + j;
+          okm |= uint32_t(tok && hh >= 0 && hh < a.H && ww >= 0 && ww < a.W) << (4 * i + j);
+        }
+    }
   };
   // 4x4 patch (4 channels) of this thread's tile, chunk c0 (zero outside the image)
   float4 d[16];
   auto load_patch = [&](int c0) {
+    if constexpr (SX) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const uint32_t vo = (okm >> (4 * i + j)) & 1u ? vb : 0x80000000u;
+          const int so = __builtin_amdgcn_readfirstlane(((i * a.W + j) * a.C + c0) * 4);
+          const auto v = __builtin_amdgcn_raw_buffer_load_b128(xr, int(vo), so, 0);
+          d[4 * i + j] = make_float4(__uint_as_float(v[0]), __uint_as_float(v[1]), __uint_as_float(v[2]),
+                                     __uint_as_float(v[3]));
+        }
+      return;
+    }
 #pragma unroll
     for (int i = 0; i < 4; ++i)
 #pragma unroll
@@ -102,10 +193,29 @@ __global__ __launch_bounds__(kWThreads, 2) void wino_f23_fwd_kernel(WinoArgs a) 
       const float* ub = a.u + ((int64_t(4 * wave) * (a.C / 8) + c0 / 8) * a.Co + co0 + lc) * 8 + 4 * lh;
       const int64_t uq = int64_t(8) * a.Co;  // floats per 8-channel block of U
       float4 bp[2][kWK / 8], bq[2][kWK / 8];  // U of the current / next position pair
+      // SX: bf16 U fragments (hi / mid / lo) of one (16-channel step, position pair): step
+      // s = 2 kk + pair covers channels c0 + 16 kk .. + 15 of positions 4 wave + 2 pair + {0, 1}
+      uint4 sp[2][3], sn[2][3];
+      auto sx_uload = [&](int st, uint4 (&dst)[2][3]) {
 #pragma unroll
-      for (int j = 0; j < 2; ++j)
+        for (int j = 0; j < 2; ++j)
 #pragma unroll
-        for (int q = 0; q < kWK / 8; ++q) bp[j][q] = *reinterpret_cast<const float4*>(ub + j * ups + q * uq);
+          for (int pl = 0; pl < 3; ++pl) {
+            const int pos = 4 * wave + 2 * (st & 1) + j;
+            const int so = __builtin_amdgcn_readfirstlane(
+                int(((int64_t(pos * 3 + pl) * (a.C / 8) + c0 / 8 + 2 * (st >> 1)) * a.Co + co0) * 16));
+            const auto v = __builtin_amdgcn_raw_buffer_load_b128(ur, int(uvo), so, 0);
+            dst[j][pl] = make_uint4(v[0], v[1], v[2], v[3]);
+          }
+      };
+      if constexpr (SX) {
+        sx_uload(0, sp);
+      } else {
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+          for (int q = 0; q < kWK / 8; ++q) bp[j][q] = *reinterpret_cast<const float4*>(ub + j * ups + q * uq);
+      }
       // ---- V = B^T d B in registers, in place (rows, then columns)
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
@@ -133,6 +243,49 @@ __global__ __launch_bounds__(kWThreads, 2) void wino_f23_fwd_kernel(WinoArgs a) 
       } else if (blk + a.G < nblk) {
         tile_setup(blk + a.G);
         load_patch(0);
+      }
+      if constexpr (SX) {
+        // ---- 4 steps x 2 positions x 6 products of 32x32x16 bf16; the next step's U loads meanwhile
+#pragma unroll
+        for (int st = 0; st < 4; ++st) {
+#if WSX_PREFETCH
+          if (st < 3) sx_uload(st + 1, sn);
+#else
+          if (st > 0) sx_uload(st, sp);
+#endif
+          __builtin_amdgcn_sched_barrier(0);  // keep each step's V reads / splits with its MFMAs
+          uint4 vh[2], vm[2], vl[2];
+#pragma unroll
+          for (int j = 0; j < 2; ++j) {
+            const float* vr = lds + ((4 * wave + 2 * (st & 1) + j) * kWT + lc) * kWP + 16 * (st >> 1) + 8 * lh;
+            wsx_split8(*reinterpret_cast<const float4*>(vr), *reinterpret_cast<const float4*>(vr + 4), vh[j], vm[j],
+                       vl[j]);
+          }
+          f32x16& c0r = acc[2 * (st & 1)];
+          f32x16& c1r = acc[2 * (st & 1) + 1];
+          // small products first; the two positions' chains interleave
+          c0r = wsx_mfma(vm[0], sp[0][1], c0r);
+          c1r = wsx_mfma(vm[1], sp[1][1], c1r);
+          c0r = wsx_mfma(vh[0], sp[0][2], c0r);
+          c1r = wsx_mfma(vh[1], sp[1][2], c1r);
+          c0r = wsx_mfma(vl[0], sp[0][0], c0r);
+          c1r = wsx_mfma(vl[1], sp[1][0], c1r);
+          c0r = wsx_mfma(vh[0], sp[0][1], c0r);
+          c1r = wsx_mfma(vh[1], sp[1][1], c1r);
+          c0r = wsx_mfma(vm[0], sp[0][0], c0r);
+          c1r = wsx_mfma(vm[1], sp[1][0], c1r);
+          c0r = wsx_mfma(vh[0], sp[0][0], c0r);
+          c1r = wsx_mfma(vh[1], sp[1][0], c1r);
+#if WSX_PREFETCH
+          if (st < 3) {
+#pragma unroll
+            for (int j = 0; j < 2; ++j)
+#pragma unroll
+              for (int pl = 0; pl < 3; ++pl) sp[j][pl] = sn[j][pl];
+          }
+#endif
+        }
+        continue;
       }
       // ---- 4 positions per wave: acc[j] (tiles x co) += V[p] (tiles x ci) . U[p] (ci x co), in
       // pairs of positions whose two MFMA chains interleave; the next pair's U loads meanwhile
@@ -245,6 +398,8 @@ __global__ __launch_bounds__(kWThreads, 2) void wino_f23_fwd_kernel(WinoArgs a) 
 // U[p][co][ci] = (G g G^T)[p] for g = w[co][ci] (3x3, any strides); one thread per (co, ci).
 // flip: the filter of the input gradient as a forward convolution, g = w[ci][co] rotated by 180
 // degrees (w is the layer's [Cout][Cin] filter; here co runs over its Cin and ci over its Cout).
+// SX: u is bf16 [p][plane][ci / 8][co][ci % 8], the exact hi / mid / lo split of each value.
+template <bool SX>
 __global__ __launch_bounds__(256) void wino_f23_filter_kernel(const float* __restrict__ w, int64_t s0, int64_t s1,
                                                               int64_t s2, int64_t s3, float* __restrict__ u, int Co,
                                                               int C, int flip) {
@@ -271,12 +426,23 @@ __global__ __launch_bounds__(256) void wino_f23_filter_kernel(const float* __res
   const int64_t o = (int64_t(ci >> 3) * Co + co) * 8 + (ci & 7);
 #pragma unroll
   for (int r = 0; r < 4; ++r) {  // (G g) G^T
-    const float v0 = t[r][0], v1 = 0.5f * (t[r][0] + t[r][1] + t[r][2]), v2 = 0.5f * (t[r][0] - t[r][1] + t[r][2]),
-                v3 = t[r][2];
-    u[(4 * r + 0) * pstride + o] = v0;
-    u[(4 * r + 1) * pstride + o] = v1;
-    u[(4 * r + 2) * pstride + o] = v2;
-    u[(4 * r + 3) * pstride + o] = v3;
+    const float v[4] = {t[r][0], 0.5f * (t[r][0] + t[r][1] + t[r][2]), 0.5f * (t[r][0] - t[r][1] + t[r][2]), t[r][2]};
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      if constexpr (SX) {
+        uint16_t* ub = reinterpret_cast<uint16_t*>(u) + int64_t(4 * r + c) * 3 * pstride + o;
+        const uint32_t h = wsx_pack2(v[c], 0.f);
+        const float r1 = v[c] - __uint_as_float(h << 16);
+        const uint32_t m = wsx_pack2(r1, 0.f);
+        const float r2 = r1 - __uint_as_float(m << 16);
+        const uint32_t l = wsx_pack2(r2, 0.f);
+        ub[0] = uint16_t(h & 0xffffu);
+        ub[pstride] = uint16_t(m & 0xffffu);
+        ub[2 * pstride] = uint16_t(l & 0xffffu);
+      } else {
+        u[(4 * r + c) * pstride + o] = v[c];
+      }
+    }
   }
 }
 
@@ -285,10 +451,11 @@ __global__ __launch_bounds__(256) void wino_f23_filter_kernel(const float* __res
 bool wino_f23_supported(int C, int Co) { return C > 0 && Co > 0 && C % kWK == 0 && Co % kWN == 0; }
 
 void wino_f23_filter(uintptr_t w, int64_t s0, int64_t s1, int64_t s2, int64_t s3, uintptr_t u, int Co, int C,
-                     bool flip, uintptr_t stream) {
+                     bool flip, bool sx, uintptr_t stream) {
   VODA_CHECK(Co > 0 && C > 0, "wino_f23_filter: empty filter");
   const int64_t n = int64_t(Co) * C;
-  hipLaunchKernelGGL(wino_f23_filter_kernel, dim3(unsigned((n + 255) / 256)), dim3(256), 0, as_stream(stream),
+  auto kern = sx ? wino_f23_filter_kernel<true> : wino_f23_filter_kernel<false>;
+  hipLaunchKernelGGL(kern, dim3(unsigned((n + 255) / 256)), dim3(256), 0, as_stream(stream),
                      reinterpret_cast<const float*>(w), s0, s1, s2, s3, reinterpret_cast<float*>(u), Co, C,
                      int(flip));
   check_launch();
@@ -320,7 +487,7 @@ int wino_f23_groups(int N, int H, int W, int C, int Co) {
 }
 
 void wino_f23_fwd(uintptr_t x, uintptr_t u, uintptr_t y, uintptr_t part, int N, int H, int W, int C, int Co, int G,
-                  uintptr_t stream) {
+                  bool sx, uintptr_t stream) {
   VODA_CHECK(N > 0 && H > 0 && W > 0, "wino_f23_fwd: empty input");
   VODA_CHECK(wino_f23_supported(C, Co), "wino_f23_fwd: channels must be multiples of 32");
   VODA_CHECK(x % 16 == 0 && u % 16 == 0 && y % 4 == 0 && part % 4 == 0, "wino_f23_fwd: misaligned operands");
@@ -329,7 +496,8 @@ void wino_f23_fwd(uintptr_t x, uintptr_t u, uintptr_t y, uintptr_t part, int N, 
              reinterpret_cast<float*>(part), N, H, W, C, Co, (H + 1) / 2, (W + 1) / 2, 0, G};
   a.T = int64_t(N) * a.th * a.tw;
   const dim3 grid(unsigned(G), unsigned(Co / kWN));
-  hipLaunchKernelGGL(wino_f23_fwd_kernel, grid, dim3(kWThreads), 0, as_stream(stream), a);
+  hipLaunchKernelGGL(sx ? wino_f23_fwd_kernel<true> : wino_f23_fwd_kernel<false>, grid, dim3(kWThreads), 0,
+                     as_stream(stream), a);
   check_launch();
 }
 

@@ -10,10 +10,17 @@ from vodascheduler_amd.ops import winograd as Wg
 pytestmark = pytest.mark.gpu
 
 
+@pytest.fixture(params=[False, True], ids=["f32mfma", "bf16x3"])
+def sx(request, monkeypatch):
+    """Both tile-GEMM paths: the f32 MFMA and the exact 3-way bf16 split (Wg.USE_SX)."""
+    monkeypatch.setattr(Wg, "USE_SX", request.param)
+    return request.param
+
+
 @pytest.mark.parametrize("n,c,co,h,w", [(2, 64, 64, 56, 56), (3, 128, 96, 28, 28), (4, 256, 256, 14, 14),
                                         (5, 512, 512, 7, 7), (1, 32, 32, 5, 9), (3, 64, 32, 1, 1)])
 @pytest.mark.parametrize("wcl", [True, False])
-def test_wino_f23_matches_fp64(n, c, co, h, w, wcl):
+def test_wino_f23_matches_fp64(n, c, co, h, w, wcl, sx):
     torch.manual_seed(c + h)
     x = torch.randn(n, c, h, w, device="cuda").contiguous(memory_format=torch.channels_last)
     wt = torch.randn(co, c, 3, 3, device="cuda") / (3 * c ** 0.5)
@@ -28,7 +35,7 @@ def test_wino_f23_matches_fp64(n, c, co, h, w, wcl):
 
 
 @pytest.mark.parametrize("n,c,co,h", [(2, 64, 64, 56), (3, 256, 128, 14), (2, 512, 512, 7), (1, 64, 32, 5)])
-def test_wino_f23_input_gradient_matches_fp64(n, c, co, h):
+def test_wino_f23_input_gradient_matches_fp64(n, c, co, h, sx):
     """flip mode: dX of a 3x3 stride-1 pad-1 layer with filter [co][c] from dY [n][co][h][h]."""
     torch.manual_seed(c + h)
     dy = torch.randn(n, co, h, h, device="cuda").contiguous(memory_format=torch.channels_last)
@@ -41,7 +48,7 @@ def test_wino_f23_input_gradient_matches_fp64(n, c, co, h):
 
 
 @pytest.mark.parametrize("n,c,co,h", [(4, 64, 64, 56), (3, 256, 256, 14), (5, 512, 512, 7), (2, 32, 64, 9)])
-def test_wino_f23_bn_partials(n, c, co, h):
+def test_wino_f23_bn_partials(n, c, co, h, sx):
     """The epilogue's per-workgroup BN partial sums add up to the column sums of y and y^2."""
     from vodascheduler_amd.ops.conv1x1 import StatsHolder
 
@@ -55,6 +62,26 @@ def test_wino_f23_bn_partials(n, c, co, h):
     yd = y.double().permute(0, 2, 3, 1).reshape(-1, co)
     torch.testing.assert_close(part[0], yd.sum(0), rtol=1e-4, atol=1e-3)
     torch.testing.assert_close(part[1], (yd * yd).sum(0), rtol=1e-4, atol=1e-3)
+
+
+@pytest.mark.parametrize("n,c,h", [(2, 128, 28), (2, 512, 7)])
+def test_wino_sx_error_no_worse_than_f32_mfma(n, c, h):
+    """The split-bf16 tile GEMMs are as accurate as the f32 MFMA ones (both vs fp64), also for
+    operands whose magnitudes span 2^+-20."""
+    torch.manual_seed(c)
+    x = torch.randn(n, c, h, h, device="cuda")
+    x = (x * torch.exp2(torch.randint(-20, 21, x.shape, device="cuda").float())).contiguous(
+        memory_format=torch.channels_last)
+    wt = (torch.randn(c, c, 3, 3, device="cuda") / (3 * c ** 0.5)).contiguous(memory_format=torch.channels_last)
+    ref = F.conv2d(x.double(), wt.double(), None, 1, 1)
+    bound = F.conv2d(x.double().abs(), wt.double().abs(), None, 1, 1) + 1e-30
+    err = {}
+    for sxv in (False, True):
+        y = Wg.conv3x3_wino(x, wt, u=Wg.filter_transform(wt, sx=sxv))
+        err[sxv] = ((y.double() - ref).abs() / bound).max().item()
+    assert err[True] <= 1.5 * err[False] + 1e-7, err
+    u = Wg.filter_transform(wt, sx=True)
+    assert u.dtype == torch.bfloat16 and u.numel() == 48 * c * c
 
 
 def test_resnet_fp32_step_with_winograd_matches_miopen(monkeypatch):

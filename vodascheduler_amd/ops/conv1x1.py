@@ -75,8 +75,9 @@ BLAS_WGRAD_F32_MIN_OUT = 1 << 20
 # gradients, 66.75 ms without them; profiles/r6/ab_split_resnet50_fp32.jsonl)
 USE_SPLIT_GEMM_F32 = False
 # the fp32 1x1 weight gradients (reduction over the pixels) on the split-bf16 GEMM, split-K to
-# ~1024 workgroups (else MIOpen / hipBLASLt as before)
-USE_SPLIT_WGRAD_F32 = False  # pending a same-box A/B (docs/PERFORMANCE.md round 6)
+# ~1024 workgroups (else MIOpen / hipBLASLt as before): ResNet-50 fp32 60.49 -> 60.37 ms
+# (same-box A/B, profiles/r6/ab_split_1x1_wgrad_resnet50_fp32.jsonl)
+USE_SPLIT_WGRAD_F32 = True
 
 
 def _sx(a: torch.Tensor, b: torch.Tensor) -> bool:

@@ -4,6 +4,13 @@ convolution, transforms fused into the kernel (nothing transformed goes to HBM).
 
 ``conv3x3_wino(x, w)`` takes NHWC (channels_last) fp32 activations and any-layout fp32 filters;
 the filter transform U = G g G^T runs per call (the weights change every step).
+
+``USE_SX`` (round 6): the 16 tile GEMMs on the bf16 matrix cores at fp32 accuracy -- U and each
+V fragment split exactly into hi / mid / lo bf16 parts, six cross products per 16 channels
+(v_mfma_f32_32x32x16_bf16, the split of ops/splitgemm.py) -- instead of the f32 MFMA: 267-379 vs
+337-450 us per ResNet-50 3x3 layer at batch 256, with a lower error vs fp64
+(profiles/r6/winograd_sx_vs_f32.jsonl); ResNet-50 fp32 step 62.34 -> 60.43 ms (same-box A/B,
+profiles/r6/ab_winograd_sx_resnet50_fp32.jsonl).
 """
 from __future__ import annotations
 
@@ -11,6 +18,8 @@ import torch
 import torch.nn.functional as F
 
 from . import _native as N
+
+USE_SX = True
 
 
 def supported(x: torch.Tensor, w: torch.Tensor, stride: int = 1, padding: int = 1, flip: bool = False) -> bool:
@@ -23,13 +32,17 @@ def supported(x: torch.Tensor, w: torch.Tensor, stride: int = 1, padding: int = 
             and N.hip().wino_f23_supported(cin, cout))
 
 
-def filter_transform(w: torch.Tensor, flip: bool = False) -> torch.Tensor:
-    """U = G g G^T per (co, ci), stored [16][Cin / 8][Cout][8]; ``flip``: of the 180-degree-rotated,
-    channel-transposed filter (Cout and Cin of the result are w's Cin and Cout)."""
+def filter_transform(w: torch.Tensor, flip: bool = False, sx: bool | None = None) -> torch.Tensor:
+    """U = G g G^T per (co, ci), stored [16][Cin / 8][Cout][8] fp32, or (``sx``) as three exact bf16
+    planes [16][3][Cin / 8][Cout][8]; ``flip``: of the 180-degree-rotated, channel-transposed filter
+    (Cout and Cin of the result are w's Cin and Cout)."""
+    sx = USE_SX if sx is None else sx
     co, ci = (int(w.shape[1]), int(w.shape[0])) if flip else (int(w.shape[0]), int(w.shape[1]))
-    u = torch.empty(16, co, ci, dtype=torch.float32, device=w.device)
+    u = (torch.empty(16, 3, co, ci, dtype=torch.bfloat16, device=w.device) if sx
+         else torch.empty(16, co, ci, dtype=torch.float32, device=w.device))
     s0, s1, s2, s3 = w.stride()
-    N.hip().wino_f23_filter(w.data_ptr(), s0, s1, s2, s3, u.data_ptr(), co, ci, bool(flip), N.stream_of(w))
+    N.hip().wino_f23_filter(w.data_ptr(), s0, s1, s2, s3, u.data_ptr(), co, ci, bool(flip), bool(sx),
+                            N.stream_of(w))
     return u
 
 
@@ -45,6 +58,7 @@ def conv3x3_wino(x: torch.Tensor, w: torch.Tensor, u: torch.Tensor | None = None
     co = int(w.shape[1]) if flip else int(w.shape[0])
     if u is None:
         u = filter_transform(w, flip)
+    sx = u.dtype == torch.bfloat16
     hip = N.hip()
     G = hip.wino_f23_groups(n, h, wd, c, co)
     ws = None
@@ -53,5 +67,5 @@ def conv3x3_wino(x: torch.Tensor, w: torch.Tensor, u: torch.Tensor | None = None
                          device=x.device)
         holder.stats = (ws, G)
     y = torch.empty((n, co, h, wd), dtype=torch.float32, device=x.device, memory_format=torch.channels_last)
-    hip.wino_f23_fwd(x.data_ptr(), u.data_ptr(), y.data_ptr(), N.ptr(ws), n, h, wd, c, co, G, N.stream_of(x))
+    hip.wino_f23_fwd(x.data_ptr(), u.data_ptr(), y.data_ptr(), N.ptr(ws), n, h, wd, c, co, G, sx, N.stream_of(x))
     return y
