@@ -76,6 +76,8 @@ def main() -> None:
     ap.add_argument("--quick", action="store_true", help="one linear, no tile sweep")
     ap.add_argument("--variants", default="", help="comma list of math variants to time on tile 0 (A/B)")
     ap.add_argument("--no-sweep", action="store_true", help="no tile / split sweep")
+    ap.add_argument("--variant-splits", action="store_true", help="sweep split-K for the --variants too")
+    ap.add_argument("--no-err", action="store_true", help="timing only")
     ap.add_argument("--stagger-ab", action="store_true", help="also time the default without the WG stagger")
     args = ap.parse_args()
     dev = torch.device("cuda", 0)
@@ -99,6 +101,11 @@ def main() -> None:
             cands = {"hipblaslt": None, f"split_t{t0}_s{s0}": (t0, s0, 0)}
             for v in [int(x) for x in args.variants.split(",") if x]:
                 cands[f"var{v}_t0_s{s0}"] = (0, s0, v)
+                if args.variant_splits:
+                    tiles = -(-Mo // 128) * -(-No // 128)
+                    for s in (1, 2, 3, 4, 8, 16):
+                        if tiles * s <= 4096 and s * 64 <= Ko:
+                            cands.setdefault(f"var{v}_t0_s{s}", (0, s, v))
             if args.stagger_ab:
                 cands[f"nostag_t{t0}_s{s0}"] = (t0, s0, 0, 0)
             if not args.quick and not args.no_sweep:
@@ -136,7 +143,7 @@ def main() -> None:
                 emit({"linear": name, "op": op, "M": Mo, "N": No, "K": Ko, "cand": k, "us": round(us, 2),
                       "tflops": round(flops / us / 1e6, 1), "speedup_vs_hipblaslt": round(base / us, 3)})
             # accuracy: hipBLASLt vs the split variants, N(0,1) and 2^+-30 magnitudes
-            for wide in (False, True):
+            for wide in (() if args.no_err else (False, True)):
                 a2, b2 = operands(op, k_in, n_out, dev, wide, 2)
                 res = {"hipblaslt": err(torch.mm(a2, b2), a2, b2)}
                 for var, vn in SG.VARIANT_NAMES.items():

@@ -265,6 +265,7 @@ class RcclComm {
 // 256x128 / 128x256; variant 0 = 6 products dual-accumulated (others: error study).
 int64_t sgemm_f32_workspace_floats(int M, int N, int splits);
 void sgemm_f32_set_stagger(int on);
+void sgemm_conv_wgrad_set_ws(int mode);
 void sgemm_conv_wgrad_f32(uintptr_t dy, uintptr_t x, uintptr_t gw, int n, int H, int W, int Cin, int Ho, int Wo,
                           int Cout, int KH, int KW, int stride, int pad, int splits, bool accumulate, uintptr_t ws,
                           int64_t ws_floats, uintptr_t stream);

@@ -76,6 +76,7 @@ struct SxArgs {
 };
 
 int g_sx_stagger = 1;
+int g_sx_conv_ws = 0;  // convolution weight gradient kernel: 0 one-role, 1 / 2 wave-specialised (lead 1 / 2)
 
 template <int R, bool KM> struct SxImg {
   static constexpr int kBytes = KM ? 3 * kSxBK * R * 2 : R * kSxKcPitch;
@@ -518,6 +519,164 @@ __global__ __launch_bounds__(BM * BN / (32 * WMT), MINW) void sgemm_bf16x3_kerne
     }
 }
 
+// Wave-specialised form of the kernel above (round 6): a 512-thread workgroup per 128 x 128 tile,
+// waves 0-3 multiply (each a 64 x 64 sub-tile, dual accumulators, ds_read fragments + 24 MFMAs
+// per 16-k stage) and waves 4-7 stage (global loads DEPTH - 1 stages ahead in registers, the
+// exact split, ds_write of the three planes).  In the one-role kernel every wave alternates an
+// MFMA phase with a VALU / LDS-write phase, and the two co-resident workgroups fall into step, so
+// the phases add up (~3.9k cycles per stage per CU against 1.5k of MFMA, profiles/r6/); here a
+// SIMD holds one MFMA wave and one staging wave, whose VALU issues in the 24 of every 32 MFMA
+// cycles that the MFMA leaves free (MI355X_MICROARCH.md 'vector-instruction ISSUE cost').
+// One barrier per stage, every wave executes the same nst barriers.  LEAD 1: two LDS buffers,
+// barrier k publishes stage k.  LEAD 2: three buffers, the staging waves run two stages ahead and
+// barrier k publishes stage k + 1, so the MFMA waves read the next stage's fragments while they
+// multiply the current one (no LDS latency at the head of each stage); two fragment sets leave
+// no room for the dual accumulators, so LEAD 2 keeps one (corrections first, hi.hi last).
+template <bool AKM, bool BKM, bool CONV, int LEAD, int DEPTH, bool DUAL = (LEAD == 1)>
+__global__ __launch_bounds__(512, 1) void sgemm_ws_kernel(SxArgs p) {
+  static_assert(DEPTH % 2 == 0 && (LEAD == 1 || LEAD == 2), "stage sets / lead");
+  constexpr int BM = 128, BN = 128, T = 256;
+  constexpr int NB = LEAD + 1;  // LDS buffers
+  constexpr int kImgA = SxImg<BM, AKM>::kBytes, kImgB = SxImg<BN, BKM>::kBytes;
+  constexpr int kBuf = kImgA + kImgB;
+  __shared__ __attribute__((aligned(16))) uint8_t smem[NB * kBuf + 64];
+
+  const int nwg = gridDim.x, bid = blockIdx.x;
+  const int xcd = bid & 7, q8 = nwg >> 3, r8 = nwg & 7;
+  const int lid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
+  const int split = lid / p.tiles, tile = lid - split * p.tiles;
+  const int m0 = (tile / p.tiles_n) * BM, n0 = (tile % p.tiles_n) * BN;
+  const int kb = split * p.kps;
+  const int ke = min(p.K, kb + p.kps);
+  const int nst = ke > kb ? (ke - kb) / kSxBK : 0;
+  const int t = threadIdx.x, lane = t & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(t >> 6);
+
+  if (wave >= 4) {  // ---------------- staging waves
+    const int tp = t - T;
+    SxOperand<BM, AKM, T> opa;
+    using OpB = std::conditional_t<CONV, SxConvOperand<BN, T>, SxOperand<BN, BKM, T>>;
+    using StB = typename OpB::Stage;
+    OpB opb;
+    opa.init(p.a, p.lda, m0, p.M, kb, tp);
+    if constexpr (CONV) opb.init(p, n0, kb, tp);
+    else opb.init(p.b, p.ldb, n0, p.N, kb, tp);
+    SxStage<BM, AKM, T> sa[DEPTH];
+    StB sb[DEPTH];
+    int nld = 0;
+    auto load = [&](SxStage<BM, AKM, T>& a_, StB& b_) {
+      const bool adv = ++nld < nst;
+      opa.load(a_, adv);
+      opb.load(b_, adv);
+    };
+    auto write = [&](const SxStage<BM, AKM, T>& a_, const StB& b_, int stage) {
+      uint8_t* A = smem + (stage % NB) * kBuf;
+      opa.write(a_, A, smem + NB * kBuf);
+      opb.write(b_, A + kImgA, smem + NB * kBuf);
+    };
+    // register sets: stage s lives in set s % DEPTH; stages 0 .. LEAD - 1 are written before
+    // barrier 0, then each set is refilled right after its stage is written
+    if (nst > 0) {
+#pragma unroll
+      for (int j = 0; j < DEPTH; ++j) load(sa[j], sb[j]);
+#pragma unroll
+      for (int j = 0; j < LEAD; ++j) {
+        if (j < nst) {
+          write(sa[j], sb[j], j);
+          load(sa[j], sb[j]);  // stage DEPTH + j
+        }
+      }
+    }
+    // iteration k: barrier k, then stage k + LEAD into its buffer; unrolled by DEPTH so the
+    // register sets stay static
+    for (int k = 0; k < nst; k += DEPTH) {
+#pragma unroll
+      for (int u = 0; u < DEPTH; ++u) {
+        if (k + u < nst) {
+          __syncthreads();
+          if (k + u + LEAD < nst) {
+            write(sa[(u + LEAD) % DEPTH], sb[(u + LEAD) % DEPTH], k + u + LEAD);
+            load(sa[(u + LEAD) % DEPTH], sb[(u + LEAD) % DEPTH]);
+          }
+        }
+      }
+    }
+    return;
+  }
+
+  // ---------------- MFMA waves
+  const int wm = wave >> 1, wn = wave & 1;
+  sx_f32x16 acc[2][2], cor[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) { acc[i][j][r] = 0.f; cor[i][j][r] = 0.f; }
+  auto frags = [&](int stage, sx_bf16x8 (&fa)[2][3], sx_bf16x8 (&fb)[2][3]) {
+    const uint8_t* A = smem + (stage % NB) * kBuf;
+    const uint8_t* B = A + kImgA;
+    sx_frag<BM, AKM>(A, wm * 64, lane, fa[0]);
+    sx_frag<BM, AKM>(A, wm * 64 + 32, lane, fa[1]);
+    sx_frag<BN, BKM>(B, wn * 64, lane, fb[0]);
+    sx_frag<BN, BKM>(B, wn * 64 + 32, lane, fb[1]);
+  };
+  auto mfmas = [&](const sx_bf16x8 (&fa)[2][3], const sx_bf16x8 (&fb)[2][3]) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        sx_f32x16& s = DUAL ? cor[i][j] : acc[i][j];
+        s = sx_mfma(fa[i][1], fb[j][1], s);
+        s = sx_mfma(fa[i][0], fb[j][2], s);
+        s = sx_mfma(fa[i][2], fb[j][0], s);
+        s = sx_mfma(fa[i][0], fb[j][1], s);
+        s = sx_mfma(fa[i][1], fb[j][0], s);
+        acc[i][j] = sx_mfma(fa[i][0], fb[j][0], acc[i][j]);
+      }
+  };
+  if constexpr (LEAD == 1) {
+    for (int k = 0; k < nst; ++k) {
+      __syncthreads();
+      sx_bf16x8 fa[2][3], fb[2][3];
+      frags(k, fa, fb);
+      mfmas(fa, fb);
+    }
+  } else {
+    // unrolled by two: set 0 holds even stages, set 1 odd ones
+    sx_bf16x8 fa0[2][3], fb0[2][3], fa1[2][3], fb1[2][3];
+    for (int k = 0; k < nst; k += 2) {
+      __syncthreads();                    // barrier k: stages <= k + 1 published
+      if (k == 0) frags(0, fa0, fb0);
+      if (k + 1 < nst) frags(k + 1, fa1, fb1);
+      mfmas(fa0, fb0);
+      if (k + 1 >= nst) break;
+      __syncthreads();                    // barrier k + 1
+      if (k + 2 < nst) frags(k + 2, fa0, fb0);
+      mfmas(fa1, fb1);
+    }
+  }
+  const int h = lane >> 5;
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int col = n0 + wn * 64 + 32 * j + (lane & 31);
+      if (col >= p.N) continue;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int row = m0 + wm * 64 + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * h;
+        if (row >= p.M) continue;
+        const float v = DUAL ? acc[i][j][r] + cor[i][j][r] : acc[i][j][r];
+        if (p.S > 1) {
+          p.ws[(int64_t(split) * p.M + row) * p.N + col] = v;
+        } else {
+          p.c[int64_t(row) * p.ldc + col] = sx_finish(p, row, col, v);
+        }
+      }
+    }
+}
+
 // split-K: C = epilogue(sum over the S slabs), 4 columns per thread (N % 4 == 0); four
 // independent partial sums keep several slab loads in flight per thread (S reaches the
 // hundreds for the convolution weight gradients)
@@ -561,12 +720,22 @@ void sx_launch_tile(const SxArgs& a, bool akm, bool bkm, unsigned grid, hipStrea
   else hipLaunchKernelGGL((sgemm_bf16x3_kernel<BM, BN, true, true, NPROD, DUAL, TWO, MINW, WMT, false, ORDER>), grid, blk, 0, st, a);
 }
 
+template <int LEAD, int DEPTH>
+void sx_launch_ws(const SxArgs& a, bool akm, bool bkm, unsigned grid, hipStream_t st) {
+  const dim3 blk(512);
+  if (!akm && !bkm) hipLaunchKernelGGL((sgemm_ws_kernel<false, false, false, LEAD, DEPTH>), grid, blk, 0, st, a);
+  else if (!akm && bkm) hipLaunchKernelGGL((sgemm_ws_kernel<false, true, false, LEAD, DEPTH>), grid, blk, 0, st, a);
+  else if (akm && !bkm) hipLaunchKernelGGL((sgemm_ws_kernel<true, false, false, LEAD, DEPTH>), grid, blk, 0, st, a);
+  else hipLaunchKernelGGL((sgemm_ws_kernel<true, true, false, LEAD, DEPTH>), grid, blk, 0, st, a);
+}
+
 constexpr int kSxTileM[5] = {128, 256, 128, 256, 256};
 constexpr int kSxTileN[5] = {128, 128, 256, 128, 128};
 
 }  // namespace
 
 void sgemm_f32_set_stagger(int on) { g_sx_stagger = on ? 1 : 0; }
+void sgemm_conv_wgrad_set_ws(int mode) { g_sx_conv_ws = mode < 0 || mode > 2 ? 0 : mode; }
 
 int64_t sgemm_f32_workspace_floats(int M, int N, int splits) {
   return splits > 1 ? int64_t(splits) * M * N : 0;
@@ -577,7 +746,10 @@ int64_t sgemm_f32_workspace_floats(int M, int N, int splits) {
 // products; 3 = 3 products (hi.hi + hi.mid + mid.hi: ~16-bit, error study only); 4 = variant 0
 // software-pipelined at one wave per SIMD (512 VGPRs; the dual accumulators do not fit the
 // pipeline at two waves per SIMD: 400+ bytes of spills); 5 = variant 0 with the products issued
-// product-outer (consecutive MFMAs on different accumulators).  Variants 1-5: 128 x 128 only.
+// product-outer (consecutive MFMAs on different accumulators); 6 = variant 0's math in the
+// wave-specialised kernel (sgemm_ws_kernel: 4 MFMA + 4 staging waves, one workgroup per CU);
+// 7 = 6 with three LDS buffers, the staging waves two stages ahead and the MFMA waves reading
+// the next stage's fragments during the current stage's MFMAs (one accumulator).  Variants 1-7: 128 x 128 only.
 void sgemm_f32(uintptr_t a, int64_t lda, bool a_kmajor, uintptr_t b, int64_t ldb, bool b_kmajor, uintptr_t c,
                int64_t ldc, int M, int N, int K, bool beta, uintptr_t bias, int epi, uintptr_t aux, int64_t ldaux,
                int tile, int splits, int variant, uintptr_t ws, int64_t ws_floats, uintptr_t stream) {
@@ -585,7 +757,7 @@ void sgemm_f32(uintptr_t a, int64_t lda, bool a_kmajor, uintptr_t b, int64_t ldb
   VODA_CHECK(K % kSxBK == 0, "sgemm_f32: K must be a multiple of 16");
   VODA_CHECK(M % 4 == 0 && N % 4 == 0, "sgemm_f32: M and N must be multiples of 4");
   VODA_CHECK(tile >= 0 && tile < 5, "sgemm_f32: bad tile id");
-  VODA_CHECK(variant >= 0 && variant <= 5 && (variant == 0 || tile == 0), "sgemm_f32: bad math variant");
+  VODA_CHECK(variant >= 0 && variant <= 7 && (variant == 0 || tile == 0), "sgemm_f32: bad math variant");
   VODA_CHECK(epi >= kSxEpiNone && epi <= kSxEpiDGelu && (epi == kSxEpiNone || aux != 0), "sgemm_f32: bad epilogue");
   VODA_CHECK(a % 16 == 0 && b % 16 == 0 && lda % 4 == 0 && ldb % 4 == 0, "sgemm_f32: operands need 16-B rows");
   VODA_CHECK(lda >= (a_kmajor ? M : K) && ldb >= (b_kmajor ? N : K) && ldc >= N, "sgemm_f32: leading dims");
@@ -623,7 +795,9 @@ void sgemm_f32(uintptr_t a, int64_t lda, bool a_kmajor, uintptr_t b, int64_t ldb
     else if (variant == 2) sx_launch_tile<128, 128, 9, true, false>(p, a_kmajor, b_kmajor, grid, st);
     else if (variant == 3) sx_launch_tile<128, 128, 3, true, false>(p, a_kmajor, b_kmajor, grid, st);
     else if (variant == 4) sx_launch_tile<128, 128, 6, true, true, 1>(p, a_kmajor, b_kmajor, grid, st);
-    else sx_launch_tile<128, 128, 6, true, false, 2, 2, 1>(p, a_kmajor, b_kmajor, grid, st);
+    else if (variant == 5) sx_launch_tile<128, 128, 6, true, false, 2, 2, 1>(p, a_kmajor, b_kmajor, grid, st);
+    else if (variant == 6) sx_launch_ws<1, 2>(p, a_kmajor, b_kmajor, grid, st);
+    else sx_launch_ws<2, 2>(p, a_kmajor, b_kmajor, grid, st);
   } else if (tile == 1) {
     sx_launch_tile<256, 128, 6, true, false>(p, a_kmajor, b_kmajor, grid, st);
   } else if (tile == 2) {
@@ -681,8 +855,13 @@ void sgemm_conv_wgrad_f32(uintptr_t dy, uintptr_t x, uintptr_t gw, int n, int H,
   const int64_t nwg = int64_t(p.tiles) * S;
   VODA_CHECK(nwg < (int64_t(1) << 31), "sgemm_conv_wgrad_f32: grid too large");
   hipStream_t st = as_stream(stream);
-  hipLaunchKernelGGL((sgemm_bf16x3_kernel<128, 128, true, true, 6, true, false, 2, 2, true>), dim3(unsigned(nwg)),
-                     dim3(256), 0, st, p);
+  if (g_sx_conv_ws == 1)
+    hipLaunchKernelGGL((sgemm_ws_kernel<true, true, true, 1, 2>), dim3(unsigned(nwg)), dim3(512), 0, st, p);
+  else if (g_sx_conv_ws == 2)
+    hipLaunchKernelGGL((sgemm_ws_kernel<true, true, true, 2, 2>), dim3(unsigned(nwg)), dim3(512), 0, st, p);
+  else
+    hipLaunchKernelGGL((sgemm_bf16x3_kernel<128, 128, true, true, 6, true, false, 2, 2, true>), dim3(unsigned(nwg)),
+                       dim3(256), 0, st, p);
   check_launch();
   if (S > 1) {
     const int64_t items = int64_t(Cout) * (N / 4);

@@ -39,13 +39,30 @@ def test_orientations_ragged(akm, bkm, tile):
     assert err < 2e-7, err
 
 
-@pytest.mark.parametrize("splits", [2, 3, 7])
-def test_split_k_matches_reference(splits):
+@pytest.mark.parametrize("akm", [False, True])
+@pytest.mark.parametrize("bkm", [False, True])
+@pytest.mark.parametrize("variant", [6, 7])
+def test_wave_specialised_orientations_ragged(akm, bkm, variant):
+    """The wave-specialised kernel (4 MFMA + 4 staging waves) on every orientation, ragged tiles,
+    odd and even stage counts."""
+    torch.manual_seed(2 * akm + bkm + variant)
+    for M, K, N in ((388, 272, 196), (132, 16, 260), (256, 48, 128)):
+        a = torch.randn(M, K, device=DEV)
+        b = torch.randn(K, N, device=DEV)
+        av, bv = _orient(a, b, akm, bkm)
+        c = SG.matmul(av, bv, tile=0, splits=1, variant=variant)
+        ref = a.double() @ b.double()
+        err = ((c.double() - ref).abs() / _bound(a, b)).max().item()
+        assert err < (2e-7 if variant == 6 else 4e-7), (M, K, N, err)  # 7: one accumulator
+
+
+@pytest.mark.parametrize("splits,variant", [(2, 0), (3, 0), (7, 0), (3, 6), (7, 6)])
+def test_split_k_matches_reference(splits, variant):
     torch.manual_seed(splits)
     M, K, N = 256, 1024, 384
     a = torch.randn(K, M, device=DEV).t()  # K-major a, as in a weight gradient
     b = torch.randn(K, N, device=DEV)
-    c = SG.matmul(a, b, tile=0, splits=splits)
+    c = SG.matmul(a, b, tile=0, splits=splits, variant=variant)
     ref = a.double() @ b.double()
     assert ((c.double() - ref).abs() / _bound(a, b)).max().item() < 2e-7
 
@@ -110,10 +127,13 @@ def test_variants_error_ordering():
 
 @pytest.mark.parametrize("n,cin,cout,hw,stride", [(2, 128, 128, 16, 1), (3, 64, 132, 8, 1), (16, 128, 128, 7, 1),
                                                   (2, 128, 256, 16, 2), (4, 256, 128, 7, 2)])
-def test_conv_wgrad_implicit_gemm_matches_fp64(n, cin, cout, hw, stride):
+@pytest.mark.parametrize("ws", [0, 1])
+def test_conv_wgrad_implicit_gemm_matches_fp64(n, cin, cout, hw, stride, ws):
     """dW (+)= conv weight gradient of a 3x3 pad-1 convolution (NHWC gather per tap in the
-    B-operand staging, zero padding, stride 1 / 2, ragged maps) against fp64."""
+    B-operand staging, zero padding, stride 1 / 2, ragged maps) against fp64; one-role and
+    wave-specialised kernels."""
     torch.manual_seed(cin + cout + hw + stride)
+    SG.N.hip().sgemm_conv_wgrad_set_ws(ws)
     cl = torch.channels_last
     x = torch.randn(n, cin, hw, hw, device=DEV).contiguous(memory_format=cl)
     ho = (hw + 2 - 3) // stride + 1
@@ -123,7 +143,10 @@ def test_conv_wgrad_implicit_gemm_matches_fp64(n, cin, cout, hw, stride):
     gw = torch.randn(cout, cin, 3, 3, device=DEV).contiguous(memory_format=cl)
     g0 = gw.clone()
     assert SG.conv_wgrad_ok(dy, x, gw)
-    SG.conv_wgrad_(dy, x, gw, stride, 1, accumulate=True)
+    try:
+        SG.conv_wgrad_(dy, x, gw, stride, 1, accumulate=True)
+    finally:
+        SG.N.hip().sgemm_conv_wgrad_set_ws(SG.CONV_WGRAD_WS)
     ref = torch.nn.grad.conv2d_weight(x.double(), gw.shape, dy.double(), stride=stride, padding=1)
     bound = torch.nn.grad.conv2d_weight(x.double().abs(), gw.shape, dy.double().abs(), stride=stride, padding=1)
     err = ((gw.double() - g0.double() - ref).abs() / (bound + 1)).max().item()

@@ -30,11 +30,16 @@ TILES = {0: (128, 128), 1: (256, 128), 2: (128, 256)}
 # accumulator, software-pipelined split; 2 = 9 products; 3 = 3 products (~16-bit: error study
 # only); 4 = 0 software-pipelined at one wave per SIMD (A/B)
 VARIANT_NAMES = {0: "bf16x3-6p-dual", 1: "bf16x3-6p-single-pipe", 2: "bf16x3-9p-dual", 3: "bf16x2-3p-dual",
-                 4: "bf16x3-6p-dual-pipe-1wave", 5: "bf16x3-6p-dual-product-outer"}
+                 4: "bf16x3-6p-dual-pipe-1wave", 5: "bf16x3-6p-dual-product-outer",
+                 6: "bf16x3-6p-dual-wavespec", 7: "bf16x3-6p-single-wavespec-lead2"}
 GEMM_MATH = VARIANT_NAMES[0]
 
 # VODA_SPLIT_GEMM=0 routes the fp32 projections back to hipBLASLt (A/B switch)
 ENABLED = os.environ.get("VODA_SPLIT_GEMM", "1") != "0"
+# math / kernel variant of the Linear GEMMs (VARIANT_NAMES) and of the convolution weight
+# gradient (0 one-role kernel, 1 / 2 wave-specialised, staging one / two stages ahead)
+DEFAULT_VARIANT = 0
+CONV_WGRAD_WS = 0
 
 _WS: dict[torch.device, torch.Tensor] = {}
 
@@ -106,7 +111,7 @@ def supported(a: torch.Tensor, b: torch.Tensor) -> bool:
     return la is not None and lb is not None and _aligned(a, la[1]) and _aligned(b, lb[1])
 
 
-def choose(M: int, Nn: int, K: int) -> tuple[int, int]:
+def choose(M: int, Nn: int, K: int, variant: int = 0) -> tuple[int, int]:
     """(tile, splits) for an M x N x K GEMM on the 128 x 128 tile (two workgroups per CU, 512
     resident).  From the MI355X sweep over the BERT-base shapes (profiles/r6/splitgemm_probe.md):
     >= 1024 output tiles run whole; 384-1023 tiles split K in two when K >= 2048 (the single
@@ -132,7 +137,7 @@ def _workspace(device: torch.device, floats: int) -> torch.Tensor:
 
 def matmul(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor | None = None, accumulate: bool = False,
            bias: torch.Tensor | None = None, epi: int = EPI_NONE, aux: torch.Tensor | None = None,
-           tile: int | None = None, splits: int | None = None, variant: int = 0) -> torch.Tensor:
+           tile: int | None = None, splits: int | None = None, variant: int | None = None) -> torch.Tensor:
     """``out (+)= a @ b (+ bias)`` on the split kernel; epi GELU writes the pre-activation
     into ``aux`` and gelu of it into ``out``, epi DGELU multiplies by gelu'(aux).  Callers
     check ``supported`` (CPU tensors get the PyTorch reference)."""
@@ -164,7 +169,8 @@ def matmul(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor | None = None, ac
         out = torch.empty(M, Nn, dtype=torch.float32, device=a.device)
     if out.stride(1) != 1 or out.shape != (M, Nn):
         raise ValueError("splitgemm.matmul: out must be [M, N] with unit column stride")
-    t0, s0 = choose(M, Nn, K)
+    variant = DEFAULT_VARIANT if variant is None else variant
+    t0, s0 = choose(M, Nn, K, variant)
     tile = t0 if tile is None else tile
     splits = s0 if splits is None else splits
     h = N.hip()
@@ -232,6 +238,7 @@ def conv_wgrad_(dy: torch.Tensor, x: torch.Tensor, gw: torch.Tensor, stride: int
     ho, wo = dy.shape[2], dy.shape[3]
     s = conv_wgrad_splits(cout, kh * kw * cin, n * ho * wo)
     h = N.hip()
+    h.sgemm_conv_wgrad_set_ws(CONV_WGRAD_WS)
     ws_floats = h.sgemm_f32_workspace_floats(cout, kh * kw * cin, s)
     ws = _workspace(dy.device, ws_floats) if ws_floats else None
     h.sgemm_conv_wgrad_f32(dy.data_ptr(), x.data_ptr(), gw.data_ptr(), n, H, W, cin, ho, wo, cout, kh, kw,
