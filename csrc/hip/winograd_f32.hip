@@ -395,6 +395,228 @@ __global__ __launch_bounds__(kWThreads, 2) void wino_f23_fwd_kernel(WinoArgs a) 
   }
 }
 
+// ---------------------------------------------------------------------------------------------
+// SX2 (round 6): the split-bf16 kernel above at 64 output channels per workgroup.  With 32, each
+// wave splits a V fragment (8 fp32 -> 3 bf16 planes, ~44 VALU) for 6 MFMAs, ~7 VALU per MFMA:
+// VALU-bound, and every 32-channel column of the grid re-loads and re-transforms the same patches.
+// Here a workgroup is 8 waves over 32 tiles x 64 output channels: wave w owns positions 2w, 2w + 1
+// and both 32-channel column tiles, so one split feeds 12 MFMAs (2 column tiles x 6 products), and
+// the patch loads / transforms per output halve.  Staging: 16 lanes read one pixel's 32 channels
+// (two per lane, 8-byte buffer loads); the M exchange runs in two 32-channel halves through the V
+// buffer.  One workgroup per CU (8 waves, ~220 VGPRs each).
+// ---------------------------------------------------------------------------------------------
+constexpr int kW2N = 64;
+constexpr int kW2Threads = 512;
+
+__global__ __launch_bounds__(kW2Threads, 1) void wino_f23_fwd_sx2_kernel(WinoArgs a) {
+  __shared__ __attribute__((aligned(16))) float lds[16 * kWT * kWP];  // V chunk, then M exchange halves
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, lc = lane & 31, lh = lane >> 5;
+  const int co0 = blockIdx.y * kW2N;
+  const int64_t nblk = (a.T + kWT - 1) / kWT;
+
+  // staging task: tile (tid >> 4) of the block, channels 2 * (tid & 15) .. + 1 of the chunk
+  const int st = tid >> 4, sq = tid & 15;
+  const __amdgpu_buffer_rsrc_t xr = wino_patch_rsrc(a);
+  const __amdgpu_buffer_rsrc_t ur = wino_u_rsrc(a);
+  const uint32_t uvo = uint32_t((lh * a.Co + lc) * 16);
+  uint32_t vb = 0, okm = 0;
+  auto tile_setup = [&](int64_t blk) {
+    const int64_t tg = blk * kWT + st;
+    const bool tok = tg < a.T;
+    const int64_t tt = tok ? tg : 0;
+    const int n = int(tt / (int64_t(a.th) * a.tw));
+    const int trem = int(tt - int64_t(n) * a.th * a.tw);
+    const int ty = trem / a.tw, tx = trem - (trem / a.tw) * a.tw;
+    const int h0 = 2 * ty - 1, w0 = 2 * tx - 1;
+    vb = uint32_t(((int64_t(n) * a.H + h0 + 1) * a.W + w0 + 1) * a.C * 4 + 8 * sq);
+    okm = 0;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int hh = h0 + i, ww = w0 + j;
+        okm |= uint32_t(tok && hh >= 0 && hh < a.H && ww >= 0 && ww < a.W) << (4 * i + j);
+      }
+  };
+  float2 d[16];
+  auto load_patch = [&](int c0) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const uint32_t vo = (okm >> (4 * i + j)) & 1u ? vb : 0x80000000u;
+        const int so = __builtin_amdgcn_readfirstlane(((i * a.W + j) * a.C + c0) * 4);
+        const auto v = __builtin_amdgcn_raw_buffer_load_b64(xr, int(vo), so, 0);
+        d[4 * i + j] = make_float2(__uint_as_float(v[0]), __uint_as_float(v[1]));
+      }
+  };
+  // bf16 U fragments (hi / mid / lo) of one 16-channel step for this wave's two positions and
+  // both column tiles: dst[j][c][plane]
+  auto uload = [&](int c0, int s, uint4 (&dst)[2][2][3]) {
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int c = 0; c < 2; ++c)
+#pragma unroll
+        for (int pl = 0; pl < 3; ++pl) {
+          const int pos = 2 * wave + j;
+          const int so = __builtin_amdgcn_readfirstlane(
+              int(((int64_t(pos * 3 + pl) * (a.C / 8) + c0 / 8 + 2 * s) * a.Co + co0 + 32 * c) * 16));
+          const auto v = __builtin_amdgcn_raw_buffer_load_b128(ur, int(uvo), so, 0);
+          dst[j][c][pl] = make_uint4(v[0], v[1], v[2], v[3]);
+        }
+  };
+  float s1[2] = {0.f, 0.f}, s2[2] = {0.f, 0.f};  // BN statistics of channels co0 + 32 h + (tid & 31)
+
+  int64_t blk = blockIdx.x;
+  if (blk < nblk) {
+    tile_setup(blk);
+    load_patch(0);
+  }
+  for (; blk < nblk; blk += a.G) {
+    f32x16 acc[2][2];
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int c = 0; c < 2; ++c) acc[j][c] = f32x16{};
+    for (int c0 = 0; c0 < a.C; c0 += kWK) {
+      uint4 u0[2][2][3], u1[2][2][3];
+      uload(c0, 0, u0);  // in flight across the transform and the barriers
+      // ---- V = B^T d B in registers (rows, then columns)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const float2 a0 = d[j], a1 = d[4 + j], a2 = d[8 + j], a3 = d[12 + j];
+        d[j] = make_float2(a0.x - a2.x, a0.y - a2.y);
+        d[4 + j] = make_float2(a1.x + a2.x, a1.y + a2.y);
+        d[8 + j] = make_float2(a2.x - a1.x, a2.y - a1.y);
+        d[12 + j] = make_float2(a1.x - a3.x, a1.y - a3.y);
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const float2 a0 = d[4 * i], a1 = d[4 * i + 1], a2 = d[4 * i + 2], a3 = d[4 * i + 3];
+        d[4 * i] = make_float2(a0.x - a2.x, a0.y - a2.y);
+        d[4 * i + 1] = make_float2(a1.x + a2.x, a1.y + a2.y);
+        d[4 * i + 2] = make_float2(a2.x - a1.x, a2.y - a1.y);
+        d[4 * i + 3] = make_float2(a1.x - a3.x, a1.y - a3.y);
+      }
+      __syncthreads();  // the previous chunk's V reads (or the previous block's M reads) are done
+#pragma unroll
+      for (int p = 0; p < 16; ++p) *reinterpret_cast<float2*>(lds + (p * kWT + st) * kWP + 2 * sq) = d[p];
+      __syncthreads();
+      if (c0 + kWK < a.C) {
+        load_patch(c0 + kWK);
+      } else if (blk + a.G < nblk) {
+        tile_setup(blk + a.G);
+        load_patch(0);
+      }
+      // ---- 2 steps x 2 positions x 2 column tiles x 6 products of 32x32x16 bf16
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        if (s == 0) uload(c0, 1, u1);
+        __builtin_amdgcn_sched_barrier(0);
+        const uint4 (&u)[2][2][3] = s == 0 ? u0 : u1;
+        uint4 vh[2], vm[2], vl[2];
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          const float* vr = lds + ((2 * wave + j) * kWT + lc) * kWP + 16 * s + 8 * lh;
+          wsx_split8(*reinterpret_cast<const float4*>(vr), *reinterpret_cast<const float4*>(vr + 4), vh[j], vm[j],
+                     vl[j]);
+        }
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+          for (int c = 0; c < 2; ++c) {  // small products first
+            f32x16& r = acc[j][c];
+            r = wsx_mfma(vm[j], u[j][c][1], r);
+            r = wsx_mfma(vh[j], u[j][c][2], r);
+            r = wsx_mfma(vl[j], u[j][c][0], r);
+            r = wsx_mfma(vh[j], u[j][c][1], r);
+            r = wsx_mfma(vm[j], u[j][c][0], r);
+            r = wsx_mfma(vh[j], u[j][c][0], r);
+          }
+      }
+    }
+    // ---- exchange + inverse transform, one 32-channel half at a time through the V buffer
+    const int co = tid & 31;
+    const int64_t t0 = blk * kWT;
+#pragma unroll
+    for (int hf = 0; hf < 2; ++hf) {
+      __syncthreads();  // V reads (hf 0) / the previous half's M reads (hf 1) are done
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int p = 2 * wave + j;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int row = (r & 3) + 8 * (r >> 2) + 4 * lh;
+          lds[(p * kWT + row) * 32 + lc] = acc[j][hf][r];
+        }
+      }
+      __syncthreads();
+#pragma unroll
+      for (int k = 0; k < kWT / 16; ++k) {
+        const int tl = (tid >> 5) + 16 * k;
+        const int64_t tgo = t0 + tl;
+        if (tgo >= a.T) continue;
+        float m[16];
+#pragma unroll
+        for (int p = 0; p < 16; ++p) m[p] = lds[(p * kWT + tl) * 32 + co];
+        float r0[4], r1[4];
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+          r0[c] = m[c] + m[4 + c] + m[8 + c];
+          r1[c] = m[4 + c] - m[8 + c] - m[12 + c];
+        }
+        const float y00 = r0[0] + r0[1] + r0[2], y01 = r0[1] - r0[2] - r0[3];
+        const float y10 = r1[0] + r1[1] + r1[2], y11 = r1[1] - r1[2] - r1[3];
+        const int no = int(tgo / (int64_t(a.th) * a.tw));
+        const int rem = int(tgo - int64_t(no) * a.th * a.tw);
+        const int oy = 2 * (rem / a.tw), ox = 2 * (rem - (rem / a.tw) * a.tw);
+        float* yb = a.y + (int64_t(no) * a.H * a.W) * a.Co + co0 + 32 * hf + co;
+        const bool xr2 = ox + 1 < a.W, yr2 = oy + 1 < a.H;
+        yb[(int64_t(oy) * a.W + ox) * a.Co] = y00;
+        s1[hf] += y00;
+        s2[hf] = fmaf(y00, y00, s2[hf]);
+        if (xr2) {
+          yb[(int64_t(oy) * a.W + ox + 1) * a.Co] = y01;
+          s1[hf] += y01;
+          s2[hf] = fmaf(y01, y01, s2[hf]);
+        }
+        if (yr2) {
+          yb[(int64_t(oy + 1) * a.W + ox) * a.Co] = y10;
+          s1[hf] += y10;
+          s2[hf] = fmaf(y10, y10, s2[hf]);
+          if (xr2) {
+            yb[(int64_t(oy + 1) * a.W + ox + 1) * a.Co] = y11;
+            s1[hf] += y11;
+            s2[hf] = fmaf(y11, y11, s2[hf]);
+          }
+        }
+      }
+    }
+  }
+  if (a.part == nullptr) return;
+  // BN partials of this workgroup: the 16 threads of each channel through LDS
+  __syncthreads();
+  float* red = lds;
+#pragma unroll
+  for (int hf = 0; hf < 2; ++hf) {
+    red[(2 * hf) * kW2Threads + tid] = s1[hf];
+    red[(2 * hf + 1) * kW2Threads + tid] = s2[hf];
+  }
+  __syncthreads();
+  if (tid < kW2N) {
+    const int hf = tid >> 5, c = tid & 31;
+    float t1 = 0.f, t2 = 0.f;
+#pragma unroll
+    for (int g = 0; g < kW2Threads / 32; ++g) {
+      t1 += red[(2 * hf) * kW2Threads + g * 32 + c];
+      t2 += red[(2 * hf + 1) * kW2Threads + g * 32 + c];
+    }
+    a.part[int64_t(blockIdx.x) * a.Co + co0 + tid] = t1;
+    a.part[int64_t(a.G) * a.Co + int64_t(blockIdx.x) * a.Co + co0 + tid] = t2;
+  }
+}
+
 // U[p][co][ci] = (G g G^T)[p] for g = w[co][ci] (3x3, any strides); one thread per (co, ci).
 // flip: the filter of the input gradient as a forward convolution, g = w[ci][co] rotated by 180
 // degrees (w is the layer's [Cout][Cin] filter; here co runs over its Cin and ci over its Cout).
@@ -498,6 +720,31 @@ void wino_f23_fwd(uintptr_t x, uintptr_t u, uintptr_t y, uintptr_t part, int N, 
   const dim3 grid(unsigned(G), unsigned(Co / kWN));
   hipLaunchKernelGGL(sx ? wino_f23_fwd_kernel<true> : wino_f23_fwd_kernel<false>, grid, dim3(kWThreads), 0,
                      as_stream(stream), a);
+  check_launch();
+}
+
+// SX2: 64 output channels and one 8-wave workgroup per CU; with 64 input channels the persistent
+// walk keeps one workgroup per CU, from 128 on one block per workgroup (as wino_f23_groups)
+bool wino_f23_sx2_supported(int C, int Co) { return C > 0 && Co > 0 && C % kWK == 0 && Co % kW2N == 0; }
+
+int wino_f23_groups2(int N, int H, int W, int C, int Co) {
+  const int64_t nblk = (int64_t(N) * ((H + 1) / 2) * ((W + 1) / 2) + kWT - 1) / kWT;
+  if (C >= 128) return int(nblk);
+  const int ncol = std::max(1, Co / kW2N);
+  return int(std::max<int64_t>(1, std::min<int64_t>(nblk, (wino_cus() + ncol - 1) / ncol)));
+}
+
+void wino_f23_fwd2(uintptr_t x, uintptr_t u, uintptr_t y, uintptr_t part, int N, int H, int W, int C, int Co, int G,
+                   uintptr_t stream) {
+  VODA_CHECK(N > 0 && H > 0 && W > 0, "wino_f23_fwd2: empty input");
+  VODA_CHECK(wino_f23_sx2_supported(C, Co), "wino_f23_fwd2: channels must be multiples of 32 (in) / 64 (out)");
+  VODA_CHECK(x % 16 == 0 && u % 16 == 0 && y % 4 == 0 && part % 4 == 0, "wino_f23_fwd2: misaligned operands");
+  VODA_CHECK(G == wino_f23_groups2(N, H, W, C, Co), "wino_f23_fwd2: group count mismatch");
+  WinoArgs a{reinterpret_cast<const float*>(x), reinterpret_cast<const float*>(u), reinterpret_cast<float*>(y),
+             reinterpret_cast<float*>(part), N, H, W, C, Co, (H + 1) / 2, (W + 1) / 2, 0, G};
+  a.T = int64_t(N) * a.th * a.tw;
+  const dim3 grid(unsigned(G), unsigned(Co / kW2N));
+  hipLaunchKernelGGL(wino_f23_fwd_sx2_kernel, grid, dim3(kW2Threads), 0, as_stream(stream), a);
   check_launch();
 }
 

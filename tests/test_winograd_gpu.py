@@ -10,15 +10,18 @@ from vodascheduler_amd.ops import winograd as Wg
 pytestmark = pytest.mark.gpu
 
 
-@pytest.fixture(params=[False, True], ids=["f32mfma", "bf16x3"])
+@pytest.fixture(params=[(False, False), (True, False), (True, True)], ids=["f32mfma", "bf16x3", "bf16x3-wide"])
 def sx(request, monkeypatch):
-    """Both tile-GEMM paths: the f32 MFMA and the exact 3-way bf16 split (Wg.USE_SX)."""
-    monkeypatch.setattr(Wg, "USE_SX", request.param)
-    return request.param
+    """The tile-GEMM paths: the f32 MFMA, the exact 3-way bf16 split (Wg.USE_SX) at 32 output
+    channels per workgroup, and the split at 64 (Wg.USE_WIDE, Cout % 64 == 0)."""
+    monkeypatch.setattr(Wg, "USE_SX", request.param[0])
+    monkeypatch.setattr(Wg, "USE_WIDE", request.param[1])
+    return request.param[0]
 
 
 @pytest.mark.parametrize("n,c,co,h,w", [(2, 64, 64, 56, 56), (3, 128, 96, 28, 28), (4, 256, 256, 14, 14),
-                                        (5, 512, 512, 7, 7), (1, 32, 32, 5, 9), (3, 64, 32, 1, 1)])
+                                        (5, 512, 512, 7, 7), (1, 32, 32, 5, 9), (3, 64, 32, 1, 1),
+                                        (3, 96, 128, 9, 7), (1, 32, 64, 3, 3)])
 @pytest.mark.parametrize("wcl", [True, False])
 def test_wino_f23_matches_fp64(n, c, co, h, w, wcl, sx):
     torch.manual_seed(c + h)

@@ -20,6 +20,9 @@ import torch.nn.functional as F
 from . import _native as N
 
 USE_SX = True
+# SX2 (round 6): the split kernel at 64 output channels per 8-wave workgroup (one V split feeds 12
+# MFMAs instead of 6; half the patch loads / transforms per output), where Cout % 64 == 0
+USE_WIDE = True
 
 
 def supported(x: torch.Tensor, w: torch.Tensor, stride: int = 1, padding: int = 1, flip: bool = False) -> bool:
@@ -60,12 +63,17 @@ def conv3x3_wino(x: torch.Tensor, w: torch.Tensor, u: torch.Tensor | None = None
         u = filter_transform(w, flip)
     sx = u.dtype == torch.bfloat16
     hip = N.hip()
-    G = hip.wino_f23_groups(n, h, wd, c, co)
+    wide = sx and USE_WIDE and hip.wino_f23_sx2_supported(c, co)
+    G = hip.wino_f23_groups2(n, h, wd, c, co) if wide else hip.wino_f23_groups(n, h, wd, c, co)
     ws = None
     if holder is not None:
         ws = torch.empty(max(2 * G * co + 3 * co, hip.bn_workspace_floats(n * h * wd, co)), dtype=torch.float32,
                          device=x.device)
         holder.stats = (ws, G)
     y = torch.empty((n, co, h, wd), dtype=torch.float32, device=x.device, memory_format=torch.channels_last)
-    hip.wino_f23_fwd(x.data_ptr(), u.data_ptr(), y.data_ptr(), N.ptr(ws), n, h, wd, c, co, G, sx, N.stream_of(x))
+    if wide:
+        hip.wino_f23_fwd2(x.data_ptr(), u.data_ptr(), y.data_ptr(), N.ptr(ws), n, h, wd, c, co, G, N.stream_of(x))
+    else:
+        hip.wino_f23_fwd(x.data_ptr(), u.data_ptr(), y.data_ptr(), N.ptr(ws), n, h, wd, c, co, G, sx,
+                         N.stream_of(x))
     return y
