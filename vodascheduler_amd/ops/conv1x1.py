@@ -69,11 +69,16 @@ BLAS_WGRAD_F32_MIN_OUT = 1 << 20
 
 
 # fp32 1x1 GEMMs the f32-MFMA kernels above do not take (K >= 512 forwards, the input gradients
-# into a sink, all weight gradients) on the split-bf16 MFMA GEMM (ops/splitgemm.py: fp32 accuracy
-# on the bf16 matrix cores) instead of hipBLASLt / MIOpen.  Off: on ResNet-50's tall shapes the
-# split GEMM lost to the libraries in the step (same-box A/B 65.06 -> 68.95 ms with the weight
-# gradients, 66.75 ms without them; profiles/r6/ab_split_resnet50_fp32.jsonl)
+# with K = Cout >= 512, also into a sink) on the split-bf16 MFMA GEMM (ops/splitgemm.py: fp32
+# accuracy on the bf16 matrix cores) instead of hipBLASLt.  Early in round 6 (the dual-accumulator
+# variant 0) the split GEMM lost to the libraries in the step (same-box A/B 65.06 -> 66.75 ms,
+# profiles/r6/ab_split_resnet50_fp32.jsonl); SPLIT_VARIANT 1 (one accumulator, software-pipelined
+# split; error still <= hipBLASLt fp32's) runs the 13 library shapes 170-335 us vs 174-351 us for
+# variant 0 and 186-463 us for UNTUNED hipBLASLt (profiles/r6/resnet50_1x1_split_probe.jsonl), but
+# the step uses the shipped tuned hipBLASLt solutions and still loses: 60.85 -> 61.97 ms (same-box
+# A/B, profiles/r6/ab_split_1x1_v1_resnet50_fp32.jsonl).  Stays off.
 USE_SPLIT_GEMM_F32 = False
+SPLIT_VARIANT = 1
 # the fp32 1x1 weight gradients (reduction over the pixels) on the split-bf16 GEMM, split-K to
 # ~1024 workgroups (else MIOpen / hipBLASLt as before): ResNet-50 fp32 60.49 -> 60.37 ms
 # (same-box A/B, profiles/r6/ab_split_1x1_wgrad_resnet50_fp32.jsonl)
@@ -86,13 +91,13 @@ def _sx(a: torch.Tensor, b: torch.Tensor) -> bool:
 
 def _mm(a: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
     """a @ b on the split-bf16 GEMM when it takes the fp32 operands, else the library."""
-    return SG.matmul(a, b) if _sx(a, b) else a @ b
+    return SG.matmul(a, b, variant=SPLIT_VARIANT) if _sx(a, b) else a @ b
 
 
 def _addmm_(c: torch.Tensor, a: torch.Tensor, b: torch.Tensor) -> None:
     """c += a @ b (c [M, N] with unit column stride)."""
     if _sx(a, b) and c.dtype == torch.float32 and c.stride(1) == 1:
-        SG.matmul(a, b, out=c, accumulate=True)
+        SG.matmul(a, b, out=c, accumulate=True, variant=SPLIT_VARIANT)
     else:
         c.addmm_(a, b)
 

@@ -21,8 +21,14 @@ from . import _native as N
 
 USE_SX = True
 # SX2 (round 6): the split kernel at 64 output channels per 8-wave workgroup (one V split feeds 12
-# MFMAs instead of 6; half the patch loads / transforms per output), where Cout % 64 == 0
+# MFMAs instead of 6; half the patch loads / transforms per output), where Cout % 64 == 0 and
+# Cin <= WIDE_MAX_C: per ResNet-50 layer 335 vs 377 us at C = 64, 305 vs 310 at 128, but 294 vs 281
+# at 256 and 340 vs 322 at 512, where the per-workgroup U stream (64 output channels x all input
+# channels x 16 positions x 3 planes, re-read by every 32-tile block) and not the split's VALU sets
+# the pace (profiles/r6/winograd_sx2_layers.jsonl).  ResNet-50 fp32 step 60.90 -> 60.74 ms (same-box
+# A/B, profiles/r6/ab_winograd_wide_resnet50_fp32.jsonl).
 USE_WIDE = True
+WIDE_MAX_C = 128
 
 
 def supported(x: torch.Tensor, w: torch.Tensor, stride: int = 1, padding: int = 1, flip: bool = False) -> bool:
@@ -63,7 +69,7 @@ def conv3x3_wino(x: torch.Tensor, w: torch.Tensor, u: torch.Tensor | None = None
         u = filter_transform(w, flip)
     sx = u.dtype == torch.bfloat16
     hip = N.hip()
-    wide = sx and USE_WIDE and hip.wino_f23_sx2_supported(c, co)
+    wide = sx and USE_WIDE and c <= WIDE_MAX_C and hip.wino_f23_sx2_supported(c, co)
     G = hip.wino_f23_groups2(n, h, wd, c, co) if wide else hip.wino_f23_groups(n, h, wd, c, co)
     ws = None
     if holder is not None:
