@@ -677,38 +677,77 @@ __global__ __launch_bounds__(512, 1) void sgemm_ws_kernel(SxArgs p) {
     }
 }
 
-// split-K: C = epilogue(sum over the S slabs), 4 columns per thread (N % 4 == 0); four
-// independent partial sums keep several slab loads in flight per thread (S reaches the
-// hundreds for the convolution weight gradients)
-__global__ __launch_bounds__(256) void sgemm_reduce_kernel(SxArgs p) {
+// split-K: C = epilogue(sum over the S slabs), 4 columns per thread (N % 4 == 0).  A block is
+// 64 float4 columns x GR slab groups: thread (g, c) sums slabs g, g + GR, ... of its column with
+// four partial sums in flight, the GR partials meet in LDS and group 0 applies the epilogue.  With
+// one group per column (the round-5 form) a small output with hundreds of slabs (ResNet-50 1x1
+// weight gradients: 64 x 256 outputs over 256 slabs) ran as 16-64 blocks of long serial loops.
+template <int GR>
+__global__ __launch_bounds__(64 * GR) void sgemm_reduce_kernel(SxArgs p) {
+  __shared__ float4 red[GR > 1 ? GR - 1 : 1][64];
   const int64_t n4 = p.N >> 2;
-  const int64_t i = int64_t(blockIdx.x) * 256 + threadIdx.x;
-  if (i >= int64_t(p.M) * n4) return;
-  const int row = int(i / n4), col = int(i - int64_t(row) * n4) * 4;
+  const int c = threadIdx.x & 63, g = threadIdx.x >> 6;
+  const int64_t i = int64_t(blockIdx.x) * 64 + c;
+  const bool ok = i < int64_t(p.M) * n4;
+  const int64_t ii = ok ? i : 0;
+  const int row = int(ii / n4), col = int(ii - int64_t(row) * n4) * 4;
   const int64_t slab = int64_t(p.M) * p.N;
   const float* w = p.ws + int64_t(row) * p.N + col;
   float4 s[4];
 #pragma unroll
   for (int u = 0; u < 4; ++u) s[u] = make_float4(0.f, 0.f, 0.f, 0.f);
-  int k = 0;
-  for (; k + 4 <= p.S; k += 4) {
+  int k = g;
+  for (; k + 3 * GR < p.S; k += 4 * GR) {
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
-      const float4 v = *reinterpret_cast<const float4*>(w + (k + u) * slab);
+      const float4 v = *reinterpret_cast<const float4*>(w + (k + u * GR) * slab);
       s[u].x += v.x; s[u].y += v.y; s[u].z += v.z; s[u].w += v.w;
     }
   }
-  for (; k < p.S; ++k) {
+  for (; k < p.S; k += GR) {
     const float4 v = *reinterpret_cast<const float4*>(w + k * slab);
     s[0].x += v.x; s[0].y += v.y; s[0].z += v.z; s[0].w += v.w;
   }
-  const float4 t = make_float4((s[0].x + s[1].x) + (s[2].x + s[3].x), (s[0].y + s[1].y) + (s[2].y + s[3].y),
-                               (s[0].z + s[1].z) + (s[2].z + s[3].z), (s[0].w + s[1].w) + (s[2].w + s[3].w));
-  float* c = p.c + int64_t(row) * p.ldc + col;
-  c[0] = sx_finish(p, row, col, t.x);
-  c[1] = sx_finish(p, row, col + 1, t.y);
-  c[2] = sx_finish(p, row, col + 2, t.z);
-  c[3] = sx_finish(p, row, col + 3, t.w);
+  float4 t = make_float4((s[0].x + s[1].x) + (s[2].x + s[3].x), (s[0].y + s[1].y) + (s[2].y + s[3].y),
+                         (s[0].z + s[1].z) + (s[2].z + s[3].z), (s[0].w + s[1].w) + (s[2].w + s[3].w));
+  if constexpr (GR > 1) {
+    if (g > 0) red[g - 1][c] = t;
+    __syncthreads();
+    if (g > 0) return;
+#pragma unroll
+    for (int q = 0; q < GR - 1; ++q) {
+      const float4 v = red[q][c];
+      t.x += v.x; t.y += v.y; t.z += v.z; t.w += v.w;
+    }
+  }
+  if (!ok) return;
+  float* cp = p.c + int64_t(row) * p.ldc + col;
+  cp[0] = sx_finish(p, row, col, t.x);
+  cp[1] = sx_finish(p, row, col + 1, t.y);
+  cp[2] = sx_finish(p, row, col + 2, t.z);
+  cp[3] = sx_finish(p, row, col + 3, t.w);
+}
+
+// slab groups per float4 column: enough blocks for ~4 waves per SIMD chip-wide, >= 8 slabs per thread
+int g_sx_reduce_groups = -1;  // < 0: automatic; else fixed (A/B)
+
+void sx_reduce(const SxArgs& p, hipStream_t st) {
+  const int64_t items = int64_t(p.M) * (p.N / 4);
+  const int64_t blocks = (items + 63) / 64;
+  int gr = g_sx_reduce_groups;
+  if (gr < 0) {
+    gr = 1;
+    while (gr < 16 && blocks * gr < 4096 && p.S >= 16 * gr) gr *= 2;
+  }
+  const dim3 grid{unsigned(blocks)};
+  switch (gr) {
+    case 16: hipLaunchKernelGGL(sgemm_reduce_kernel<16>, grid, dim3(1024), 0, st, p); break;
+    case 8: hipLaunchKernelGGL(sgemm_reduce_kernel<8>, grid, dim3(512), 0, st, p); break;
+    case 4: hipLaunchKernelGGL(sgemm_reduce_kernel<4>, grid, dim3(256), 0, st, p); break;
+    case 2: hipLaunchKernelGGL(sgemm_reduce_kernel<2>, grid, dim3(128), 0, st, p); break;
+    default: hipLaunchKernelGGL(sgemm_reduce_kernel<1>, grid, dim3(64), 0, st, p); break;
+  }
+  check_launch();
 }
 
 template <int BM, int BN, int NPROD, bool DUAL, bool TWO, int MINW = 2, int WMT = 2, int ORDER = 0>
@@ -736,6 +775,7 @@ constexpr int kSxTileN[5] = {128, 128, 256, 128, 128};
 
 void sgemm_f32_set_stagger(int on) { g_sx_stagger = on ? 1 : 0; }
 void sgemm_conv_wgrad_set_ws(int mode) { g_sx_conv_ws = mode < 0 || mode > 2 ? 0 : mode; }
+void sgemm_set_reduce_groups(int g) { g_sx_reduce_groups = (g == 1 || g == 2 || g == 4 || g == 8 || g == 16) ? g : -1; }
 
 int64_t sgemm_f32_workspace_floats(int M, int N, int splits) {
   return splits > 1 ? int64_t(splits) * M * N : 0;
@@ -808,11 +848,7 @@ void sgemm_f32(uintptr_t a, int64_t lda, bool a_kmajor, uintptr_t b, int64_t ldb
     sx_launch_tile<256, 128, 6, true, false, 1, 4>(p, a_kmajor, b_kmajor, grid, st);
   }
   check_launch();
-  if (S > 1) {
-    const int64_t items = int64_t(M) * (N / 4);
-    hipLaunchKernelGGL(sgemm_reduce_kernel, dim3(unsigned((items + 255) / 256)), dim3(256), 0, st, p);
-    check_launch();
-  }
+  if (S > 1) sx_reduce(p, st);
 }
 
 // Convolution weight gradient dW[co][kh][kw][ci] (+)= sum over output pixels of dY[pix][co] *
@@ -863,11 +899,7 @@ void sgemm_conv_wgrad_f32(uintptr_t dy, uintptr_t x, uintptr_t gw, int n, int H,
     hipLaunchKernelGGL((sgemm_bf16x3_kernel<128, 128, true, true, 6, true, false, 2, 2, true>), dim3(unsigned(nwg)),
                        dim3(256), 0, st, p);
   check_launch();
-  if (S > 1) {
-    const int64_t items = int64_t(Cout) * (N / 4);
-    hipLaunchKernelGGL(sgemm_reduce_kernel, dim3(unsigned((items + 255) / 256)), dim3(256), 0, st, p);
-    check_launch();
-  }
+  if (S > 1) sx_reduce(p, st);
 }
 
 }  // namespace voda

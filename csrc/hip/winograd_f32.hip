@@ -450,21 +450,19 @@ __global__ __launch_bounds__(kW2Threads, 1) void wino_f23_fwd_sx2_kernel(WinoArg
         d[4 * i + j] = make_float2(__uint_as_float(v[0]), __uint_as_float(v[1]));
       }
   };
-  // bf16 U fragments (hi / mid / lo) of one 16-channel step for this wave's two positions and
-  // both column tiles: dst[j][c][plane]
-  auto uload = [&](int c0, int s, uint4 (&dst)[2][2][3]) {
+  // bf16 U fragments (hi / mid / lo) of one 16-channel step s and one column tile c for this
+  // wave's two positions: dst[j][plane]
+  auto uload = [&](int c0, int s, int c, uint4 (&dst)[2][3]) {
 #pragma unroll
     for (int j = 0; j < 2; ++j)
 #pragma unroll
-      for (int c = 0; c < 2; ++c)
-#pragma unroll
-        for (int pl = 0; pl < 3; ++pl) {
-          const int pos = 2 * wave + j;
-          const int so = __builtin_amdgcn_readfirstlane(
-              int(((int64_t(pos * 3 + pl) * (a.C / 8) + c0 / 8 + 2 * s) * a.Co + co0 + 32 * c) * 16));
-          const auto v = __builtin_amdgcn_raw_buffer_load_b128(ur, int(uvo), so, 0);
-          dst[j][c][pl] = make_uint4(v[0], v[1], v[2], v[3]);
-        }
+      for (int pl = 0; pl < 3; ++pl) {
+        const int pos = 2 * wave + j;
+        const int so = __builtin_amdgcn_readfirstlane(
+            int(((int64_t(pos * 3 + pl) * (a.C / 8) + c0 / 8 + 2 * s) * a.Co + co0 + 32 * c) * 16));
+        const auto v = __builtin_amdgcn_raw_buffer_load_b128(ur, int(uvo), so, 0);
+        dst[j][pl] = make_uint4(v[0], v[1], v[2], v[3]);
+      }
   };
   float s1[2] = {0.f, 0.f}, s2[2] = {0.f, 0.f};  // BN statistics of channels co0 + 32 h + (tid & 31)
 
@@ -480,8 +478,8 @@ __global__ __launch_bounds__(kW2Threads, 1) void wino_f23_fwd_sx2_kernel(WinoArg
 #pragma unroll
       for (int c = 0; c < 2; ++c) acc[j][c] = f32x16{};
     for (int c0 = 0; c0 < a.C; c0 += kWK) {
-      uint4 u0[2][2][3], u1[2][2][3];
-      uload(c0, 0, u0);  // in flight across the transform and the barriers
+      uint4 ua[2][3], ub[2][3];  // U of the current / next (step, column tile)
+      uload(c0, 0, 0, ua);       // in flight across the transform and the barriers
       // ---- V = B^T d B in registers (rows, then columns)
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
@@ -509,32 +507,39 @@ __global__ __launch_bounds__(kW2Threads, 1) void wino_f23_fwd_sx2_kernel(WinoArg
         tile_setup(blk + a.G);
         load_patch(0);
       }
-      // ---- 2 steps x 2 positions x 2 column tiles x 6 products of 32x32x16 bf16
-#pragma unroll
-      for (int s = 0; s < 2; ++s) {
-        if (s == 0) uload(c0, 1, u1);
-        __builtin_amdgcn_sched_barrier(0);
-        const uint4 (&u)[2][2][3] = s == 0 ? u0 : u1;
-        uint4 vh[2], vm[2], vl[2];
+      // ---- 2 steps x 2 column tiles x 2 positions x 6 products of 32x32x16 bf16; each V split
+      // (per step and position) feeds both column tiles; the U of the next (step, column tile)
+      // loads during the current one's MFMAs
+      uint4 vh[2], vm[2], vl[2];
+      auto split = [&](int s) {
 #pragma unroll
         for (int j = 0; j < 2; ++j) {
           const float* vr = lds + ((2 * wave + j) * kWT + lc) * kWP + 16 * s + 8 * lh;
           wsx_split8(*reinterpret_cast<const float4*>(vr), *reinterpret_cast<const float4*>(vr + 4), vh[j], vm[j],
                      vl[j]);
         }
+      };
+      auto mfmas = [&](int c, const uint4 (&u)[2][3]) {
 #pragma unroll
-        for (int j = 0; j < 2; ++j)
-#pragma unroll
-          for (int c = 0; c < 2; ++c) {  // small products first
-            f32x16& r = acc[j][c];
-            r = wsx_mfma(vm[j], u[j][c][1], r);
-            r = wsx_mfma(vh[j], u[j][c][2], r);
-            r = wsx_mfma(vl[j], u[j][c][0], r);
-            r = wsx_mfma(vh[j], u[j][c][1], r);
-            r = wsx_mfma(vm[j], u[j][c][0], r);
-            r = wsx_mfma(vh[j], u[j][c][0], r);
-          }
-      }
+        for (int j = 0; j < 2; ++j) {  // small products first
+          f32x16& r = acc[j][c];
+          r = wsx_mfma(vm[j], u[j][1], r);
+          r = wsx_mfma(vh[j], u[j][2], r);
+          r = wsx_mfma(vl[j], u[j][0], r);
+          r = wsx_mfma(vh[j], u[j][1], r);
+          r = wsx_mfma(vm[j], u[j][0], r);
+          r = wsx_mfma(vh[j], u[j][0], r);
+        }
+      };
+      split(0);
+      uload(c0, 0, 1, ub);
+      mfmas(0, ua);
+      uload(c0, 1, 0, ua);
+      mfmas(1, ub);
+      split(1);
+      uload(c0, 1, 1, ub);
+      mfmas(0, ua);
+      mfmas(1, ub);
     }
     // ---- exchange + inverse transform, one 32-channel half at a time through the V buffer
     const int co = tid & 31;

@@ -67,6 +67,24 @@ def test_split_k_matches_reference(splits, variant):
     assert ((c.double() - ref).abs() / _bound(a, b)).max().item() < 2e-7
 
 
+@pytest.mark.parametrize("groups", [-1, 1, 2, 4, 16])
+def test_split_k_reduce_slab_groups(groups, monkeypatch):
+    """The split-K reduce with 1-16 slab groups per column (LDS combine) on a small output with
+    many slabs (the ResNet 1x1 weight-gradient shape class), accumulating into C."""
+    monkeypatch.setattr(SG, "REDUCE_GROUPS", groups)
+    torch.manual_seed(groups + 3)
+    M, K, N = 64, 16 * 200, 260
+    a = torch.randn(K, M, device=DEV).t()
+    b = torch.randn(K, N, device=DEV)
+    c0 = torch.randn(M, N, device=DEV)
+    c = c0.clone()
+    SG.matmul(a, b, out=c, accumulate=True, tile=0, splits=100)
+    ref = a.double() @ b.double() + c0.double()
+    assert ((c.double() - ref).abs() / (_bound(a, b) + 1)).max().item() < 2e-7
+    monkeypatch.setattr(SG, "REDUCE_GROUPS", -1)
+    SG.matmul(a, b, out=c, tile=0, splits=2)  # back to the automatic setting
+
+
 def test_no_worse_than_hipblaslt_wide_magnitudes():
     torch.backends.cuda.matmul.allow_tf32 = False
     torch.manual_seed(5)

@@ -40,6 +40,18 @@ ENABLED = os.environ.get("VODA_SPLIT_GEMM", "1") != "0"
 # gradient (0 one-role kernel, 1 / 2 wave-specialised, staging one / two stages ahead)
 DEFAULT_VARIANT = 0
 CONV_WGRAD_WS = 0
+# split-K reduce: slab groups per float4 column (-1 automatic: ~4096 blocks-worth of groups, >= 16
+# slabs per group; 1 = one thread per column, the round-5 form)
+REDUCE_GROUPS = -1
+REDUCE_GROUPS_AUTO = True  # False: one group (A/B switch)
+_applied = {"reduce_groups": None}
+
+
+def _sync_knobs(h) -> None:
+    g = REDUCE_GROUPS if REDUCE_GROUPS_AUTO else 1
+    if _applied["reduce_groups"] != g:
+        h.sgemm_set_reduce_groups(int(g))
+        _applied["reduce_groups"] = g
 
 _WS: dict[torch.device, torch.Tensor] = {}
 
@@ -174,6 +186,7 @@ def matmul(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor | None = None, ac
     tile = t0 if tile is None else tile
     splits = s0 if splits is None else splits
     h = N.hip()
+    _sync_knobs(h)
     ws_floats = h.sgemm_f32_workspace_floats(M, Nn, splits)
     ws = _workspace(a.device, ws_floats) if ws_floats else None
     if bias is not None:
@@ -238,6 +251,7 @@ def conv_wgrad_(dy: torch.Tensor, x: torch.Tensor, gw: torch.Tensor, stride: int
     ho, wo = dy.shape[2], dy.shape[3]
     s = conv_wgrad_splits(cout, kh * kw * cin, n * ho * wo)
     h = N.hip()
+    _sync_knobs(h)
     h.sgemm_conv_wgrad_set_ws(CONV_WGRAD_WS)
     ws_floats = h.sgemm_f32_workspace_floats(cout, kh * kw * cin, s)
     ws = _workspace(dy.device, ws_floats) if ws_floats else None
