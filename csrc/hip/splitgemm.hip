@@ -87,8 +87,14 @@ template <int R, bool KM> struct SxImg {
 // keeps the 8-B staging writes and the 32x32x16 transposed reads conflict-free.
 template <int R>
 __device__ __forceinline__ int sx_km_off(int k, int col) {
-  const int ch = col >> 3;
-  return k * (2 * R) + ((ch & ~15) << 4) + (((ch & 15) ^ (((k & 3) << 2) | ((k >> 2) & 3))) << 4) + ((col & 4) << 1);
+  if constexpr (R == 64) {
+    // 128-B k-rows: k-rows 2j and 2j + 1 side by side form row j of a [8][128] image that takes
+    // the 256-B swizzle (a bijection, so staging writes and fragment reads agree)
+    return sx_km_off<128>(k >> 1, ((k & 1) << 6) + col);
+  } else {
+    const int ch = col >> 3;
+    return k * (2 * R) + ((ch & ~15) << 4) + (((ch & 15) ^ (((k & 3) << 2) | ((k >> 2) & 3))) << 4) + ((col & 4) << 1);
+  }
 }
 
 // exact split of fp32 values into three packed bf16 planes (x == hi + mid + lo)
@@ -768,8 +774,8 @@ void sx_launch_ws(const SxArgs& a, bool akm, bool bkm, unsigned grid, hipStream_
   else hipLaunchKernelGGL((sgemm_ws_kernel<true, true, false, LEAD, DEPTH>), grid, blk, 0, st, a);
 }
 
-constexpr int kSxTileM[5] = {128, 256, 128, 256, 256};
-constexpr int kSxTileN[5] = {128, 128, 256, 128, 128};
+constexpr int kSxTileM[7] = {128, 256, 128, 256, 256, 64, 256};
+constexpr int kSxTileN[7] = {128, 128, 256, 128, 128, 256, 64};
 
 }  // namespace
 
@@ -796,7 +802,7 @@ void sgemm_f32(uintptr_t a, int64_t lda, bool a_kmajor, uintptr_t b, int64_t ldb
   VODA_CHECK(M > 0 && N > 0 && K > 0, "sgemm_f32: empty GEMM");
   VODA_CHECK(K % kSxBK == 0, "sgemm_f32: K must be a multiple of 16");
   VODA_CHECK(M % 4 == 0 && N % 4 == 0, "sgemm_f32: M and N must be multiples of 4");
-  VODA_CHECK(tile >= 0 && tile < 5, "sgemm_f32: bad tile id");
+  VODA_CHECK(tile >= 0 && tile < 7, "sgemm_f32: bad tile id");
   VODA_CHECK(variant >= 0 && variant <= 7 && (variant == 0 || tile == 0), "sgemm_f32: bad math variant");
   VODA_CHECK(epi >= kSxEpiNone && epi <= kSxEpiDGelu && (epi == kSxEpiNone || aux != 0), "sgemm_f32: bad epilogue");
   VODA_CHECK(a % 16 == 0 && b % 16 == 0 && lda % 4 == 0 && ldb % 4 == 0, "sgemm_f32: operands need 16-B rows");
@@ -842,6 +848,10 @@ void sgemm_f32(uintptr_t a, int64_t lda, bool a_kmajor, uintptr_t b, int64_t ldb
     sx_launch_tile<256, 128, 6, true, false>(p, a_kmajor, b_kmajor, grid, st);
   } else if (tile == 2) {
     sx_launch_tile<128, 256, 6, true, false>(p, a_kmajor, b_kmajor, grid, st);
+  } else if (tile == 5) {  // 64 x 256 (4 waves along N): outputs with 64 rows (no half-empty tiles)
+    sx_launch_tile<64, 256, 6, true, false>(p, a_kmajor, b_kmajor, grid, st);
+  } else if (tile == 6) {  // 256 x 64 (4 waves along M): outputs with 64 columns
+    sx_launch_tile<256, 64, 6, true, false>(p, a_kmajor, b_kmajor, grid, st);
   } else if (tile == 3) {  // 4 waves of 128 x 64, one per SIMD, software-pipelined split
     sx_launch_tile<256, 128, 6, true, true, 1, 4>(p, a_kmajor, b_kmajor, grid, st);
   } else {                 // the same without the pipeline (A/B)

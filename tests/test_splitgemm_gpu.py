@@ -56,6 +56,26 @@ def test_wave_specialised_orientations_ragged(akm, bkm, variant):
         assert err < (2e-7 if variant == 6 else 4e-7), (M, K, N, err)  # 7: one accumulator
 
 
+@pytest.mark.parametrize("tile", [5, 6])
+@pytest.mark.parametrize("akm", [False, True])
+@pytest.mark.parametrize("bkm", [False, True])
+def test_thin_tiles(tile, akm, bkm):
+    """64 x 256 / 256 x 64 tiles (the 128-byte-row K-major image), every orientation, ragged and
+    exact outputs, split-K into an accumulated C."""
+    torch.manual_seed(tile + 2 * akm + bkm)
+    for M, K, N, s in ((64, 512, 256, 1), (64, 1024, 516, 4), (256, 512, 64, 1), (516, 1024, 64, 4),
+                       (100, 272, 196, 1)):
+        a = torch.randn(M, K, device=DEV)
+        b = torch.randn(K, N, device=DEV)
+        av, bv = _orient(a, b, akm, bkm)
+        c0 = torch.randn(M, N, device=DEV)
+        c = c0.clone()
+        SG.matmul(av, bv, out=c, accumulate=True, tile=tile, splits=s)
+        ref = a.double() @ b.double() + c0.double()
+        err = ((c.double() - ref).abs() / (_bound(a, b) + 1)).max().item()
+        assert err < 2e-7, (tile, M, K, N, err)
+
+
 @pytest.mark.parametrize("splits,variant", [(2, 0), (3, 0), (7, 0), (3, 6), (7, 6)])
 def test_split_k_matches_reference(splits, variant):
     torch.manual_seed(splits)

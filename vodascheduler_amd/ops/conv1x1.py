@@ -83,6 +83,9 @@ SPLIT_VARIANT = 1
 # ~1024 workgroups (else MIOpen / hipBLASLt as before): ResNet-50 fp32 60.49 -> 60.37 ms
 # (same-box A/B, profiles/r6/ab_split_1x1_wgrad_resnet50_fp32.jsonl)
 USE_SPLIT_WGRAD_F32 = True
+# ... with the 64 x 256 / 256 x 64 tiles where the output has a 64-wide side (stage 1: [64][256],
+# [256][64], [64][64]) instead of half-empty 128 x 128 tiles
+USE_THIN_TILES = True
 
 
 def _sx(a: torch.Tensor, b: torch.Tensor) -> bool:
@@ -424,8 +427,9 @@ class _Conv1x1Fn(torch.autograd.Function):
             if (dy2.dtype == torch.float32 and g2 is not None and g2.dtype == torch.float32
                     and USE_SPLIT_WGRAD_F32 and SG.supported(dy2.t(), x2)):
                 # split-K into the flat gradient, ~1024 workgroups over the pixels
-                SG.matmul(dy2.t(), x2, out=g2, accumulate=True, tile=0,
-                          splits=SG.conv_wgrad_splits(cout, cin, dy2.shape[0]))
+                tile = SG.thin_tile(cout, cin) if USE_THIN_TILES else 0
+                SG.matmul(dy2.t(), x2, out=g2, accumulate=True, tile=tile,
+                          splits=SG.conv_wgrad_splits(cout, cin, dy2.shape[0], tile))
                 _ready(weight)
             elif (dy2.dtype == torch.float32 and g2 is not None and g2.dtype == torch.float32
                     and blas_wgrad_f32_ok(dy2.shape[0], cout, cin)):

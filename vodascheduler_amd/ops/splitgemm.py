@@ -25,7 +25,17 @@ import torch
 from . import _native as N
 
 EPI_NONE, EPI_GELU, EPI_DGELU = 0, 1, 2
-TILES = {0: (128, 128), 1: (256, 128), 2: (128, 256)}
+TILES = {0: (128, 128), 1: (256, 128), 2: (128, 256), 5: (64, 256), 6: (256, 64)}
+
+
+def thin_tile(M: int, Nn: int) -> int:
+    """The tile for an M x N output with one 64-wide dimension (ResNet-50 stage-1 1x1 weight
+    gradients: [64][256] / [256][64]), so that no 128-wide tile runs half empty; else tile 0."""
+    if M == 64 and Nn % 256 == 0:
+        return 5
+    if Nn == 64 and M % 256 == 0:
+        return 6
+    return 0
 # 0 = 6 products with the hi.hi products in their own accumulator (shipped); 1 = 6 products, one
 # accumulator, software-pipelined split; 2 = 9 products; 3 = 3 products (~16-bit: error study
 # only); 4 = 0 software-pipelined at one wave per SIMD (A/B)
@@ -231,10 +241,11 @@ def conv_wgrad_ok(dy: torch.Tensor, x: torch.Tensor, gw: torch.Tensor) -> bool:
     return dy.data_ptr() % 16 == 0 and x.data_ptr() % 16 == 0 and gw.data_ptr() % 16 == 0
 
 
-def conv_wgrad_splits(cout: int, n_cols: int, pixels: int) -> int:
+def conv_wgrad_splits(cout: int, n_cols: int, pixels: int, tile: int = 0) -> int:
     """Split-K count of the convolution weight gradient: ~1024 workgroups (two rounds of the 512
     resident 128 x 128 workgroups), >= 256 pixels per split."""
-    tiles = -(-cout // 128) * -(-n_cols // 128)
+    bm, bn = TILES[tile]
+    tiles = -(-cout // bm) * -(-n_cols // bn)
     return max(1, min(1024 // tiles, pixels // 256))
 
 
