@@ -311,6 +311,99 @@ struct SxConvOperand {
   }
 };
 
+// K-contiguous A operand of a convolution FORWARD, gathered from the NHWC input while it is
+// staged (implicit GEMM, no im2col buffer): A(m, k) = X[img][ho*cs + kh - cpad][wo*cs + kw - cpad][ci]
+// for output pixel m = (img, ho, wo) and k = (kh*ckw + kw)*cin + ci.  cin % 16 == 0, so a 16-k stage
+// is 16 consecutive channels of one tap: unit u (as SxOperand K-contiguous: k 4q..4q+3 of rows r and
+// r + R/2) reads one float4 per row, zeroed outside the image; the tap / channel cursor advances
+// one stage per load.
+template <int R, int T>
+struct SxConvAOperand {
+  using Stage = SxConvStage<R, T>;
+  static constexpr int kUnits = 2 * R;
+  static constexpr int kPer = (kUnits + T - 1) / T;
+  const float* x;
+  int img[kPer][2], hb[kPer][2], wb[kPer][2];  // image, ho * cs - cpad, wo * cs - cpad of each row
+  int q4[kPer];
+  int ci0, kh, kw;                              // the next load's channel offset and tap
+  int H, W, C, KW;
+  int woff[kPer], woff2[kPer];
+  bool on[kPer];
+
+  __device__ __forceinline__ void init(const SxArgs& p, int m0, int k0, int t) {
+    x = p.a;
+    H = p.ch; W = p.cw; C = p.cin; KW = p.ckw;
+    const int tap = k0 / C;
+    ci0 = k0 - tap * C;
+    kh = tap / KW;
+    kw = tap - kh * KW;
+    const int hw = p.cho * p.cwo;
+#pragma unroll
+    for (int i = 0; i < kPer; ++i) {
+      const int u = t + i * T;
+      on[i] = (kUnits % T == 0) || u < kUnits;
+      const int uu = on[i] ? u : 0;
+      const int q = uu & 3, r = uu >> 2;
+      q4[i] = 4 * q;
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int m = min(m0 + r + j * (R / 2), p.M - 1);  // rows past the matrix: valid duplicates
+        img[i][j] = m / hw;
+        const int rem = m - img[i][j] * hw;
+        const int ho = rem / p.cwo, wo = rem - (rem / p.cwo) * p.cwo;
+        hb[i][j] = ho * p.cs - p.cpad;
+        wb[i][j] = wo * p.cs - p.cpad;
+      }
+      woff[i] = r * kSxKcPitch + 48 * (q >> 1) + 8 * (q & 1);
+      woff2[i] = (r + R / 2) * kSxKcPitch + 48 * (q >> 1) + 8 * (q & 1);
+    }
+  }
+
+  __device__ __forceinline__ void load(Stage& s, bool advance) {
+    s.keep = 0;
+#pragma unroll
+    for (int i = 0; i < kPer; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int hi = hb[i][j] + kh, wi = wb[i][j] + kw;
+        const bool ok = hi >= 0 && hi < H && wi >= 0 && wi < W;
+        const int64_t off = ok ? ((int64_t(img[i][j]) * H + hi) * W + wi) * C + ci0 + q4[i] : 0;
+        s.v[i][j] = *reinterpret_cast<const float4*>(x + off);
+        s.keep |= uint32_t(ok) << (2 * i + j);
+      }
+    if (advance) {
+      ci0 += kSxBK;
+      if (ci0 >= C) {
+        ci0 = 0;
+        if (++kw == KW) { kw = 0; ++kh; }
+      }
+    }
+  }
+
+  __device__ __forceinline__ void write(const Stage& s, uint8_t* img_, uint8_t* dummy) const {
+#pragma unroll
+    for (int i = 0; i < kPer; ++i) {
+      const uint32_t m0 = (s.keep >> (2 * i)) & 1 ? 0xffffffffu : 0u, m1 = (s.keep >> (2 * i + 1)) & 1 ? 0xffffffffu : 0u;
+      const float4 a = s.v[i][0], b = s.v[i][1];
+      const float4 va = make_float4(__uint_as_float(__float_as_uint(a.x) & m0), __uint_as_float(__float_as_uint(a.y) & m0),
+                                    __uint_as_float(__float_as_uint(a.z) & m0), __uint_as_float(__float_as_uint(a.w) & m0));
+      const float4 vb = make_float4(__uint_as_float(__float_as_uint(b.x) & m1), __uint_as_float(__float_as_uint(b.y) & m1),
+                                    __uint_as_float(__float_as_uint(b.z) & m1), __uint_as_float(__float_as_uint(b.w) & m1));
+      uint2 h0, md0, l0, h1, md1, l1;
+      sx_split4(va, h0, md0, l0);
+      sx_split4(vb, h1, md1, l1);
+      uint8_t* pp = on[i] ? img_ + woff[i] : dummy;
+      uint8_t* qq = on[i] ? img_ + woff2[i] : dummy + 8;
+      *reinterpret_cast<uint2*>(pp) = h0;
+      *reinterpret_cast<uint2*>(pp + 16) = md0;
+      *reinterpret_cast<uint2*>(pp + 32) = l0;
+      *reinterpret_cast<uint2*>(qq) = h1;
+      *reinterpret_cast<uint2*>(qq + 16) = md1;
+      *reinterpret_cast<uint2*>(qq + 32) = l1;
+    }
+  }
+};
+
 // three fragments (hi, mid, lo) of the 32-row tile starting at image row r0 for this lane
 template <int R, bool KM>
 __device__ __forceinline__ void sx_frag(const uint8_t* img, int r0, int lane, sx_bf16x8 (&f)[3]) {
@@ -349,7 +442,7 @@ __device__ __forceinline__ float sx_finish(const SxArgs& p, int row, int col, fl
 // WMT: 32-row MFMA tiles per wave along M (2: 64 x 64 per wave; 4: 128 x 64 per wave, one wave per
 // SIMD with its accumulators in AGPRs)
 template <int BM, int BN, bool AKM, bool BKM, int NPROD, bool DUAL, bool TWO_SETS, int MINW, int WMT, bool CONV = false,
-          int ORDER = 0>
+          int ORDER = 0, bool CONVA = false>
 __global__ __launch_bounds__(BM * BN / (32 * WMT), MINW) void sgemm_bf16x3_kernel(SxArgs p) {
   constexpr int NWN = BN / 64;
   constexpr int NWM = BM / (32 * WMT);
@@ -376,14 +469,17 @@ __global__ __launch_bounds__(BM * BN / (32 * WMT), MINW) void sgemm_bf16x3_kerne
   // (MI355X_MICROARCH.md 'Two waves per SIMD', items 4 and 9)
   if (__builtin_amdgcn_readfirstlane(p.stagger & blockIdx.x) & 1) __builtin_amdgcn_s_setprio(1);
 
-  SxOperand<BM, AKM, T> opa;
+  using OpA = std::conditional_t<CONVA, SxConvAOperand<BM, T>, SxOperand<BM, AKM, T>>;
+  using StA = typename OpA::Stage;
+  OpA opa;
   using OpB = std::conditional_t<CONV, SxConvOperand<BN, T>, SxOperand<BN, BKM, T>>;
   using StB = typename OpB::Stage;
   OpB opb;
-  opa.init(p.a, p.lda, m0, p.M, kb, t);
+  if constexpr (CONVA) opa.init(p, m0, kb, t);
+  else opa.init(p.a, p.lda, m0, p.M, kb, t);
   if constexpr (CONV) opb.init(p, n0, kb, t);
   else opb.init(p.b, p.ldb, n0, p.N, kb, t);
-  SxStage<BM, AKM, T> sa0, sa1;
+  StA sa0, sa1;
   StB sb0, sb1;
 
   sx_f32x16 acc[WMT][2], cor[WMT][2];
@@ -440,7 +536,7 @@ __global__ __launch_bounds__(BM * BN / (32 * WMT), MINW) void sgemm_bf16x3_kerne
         for (int j = 0; j < 2; ++j) acc[i][j] = sx_mfma(fa[i][0], fb[j][0], acc[i][j]);
     }
   };
-  auto write = [&](const SxStage<BM, AKM, T>& sa, const StB& sb, int buf) {
+  auto write = [&](const StA& sa, const StB& sb, int buf) {
     uint8_t* A = smem + buf * kBuf;
     opa.write(sa, A, smem + 2 * kBuf);
     opb.write(sb, A + kImgA, smem + 2 * kBuf);
@@ -449,7 +545,7 @@ __global__ __launch_bounds__(BM * BN / (32 * WMT), MINW) void sgemm_bf16x3_kerne
   // stage k is read from global at load number k (clamped to the last stage), multiplied from
   // LDS buffer k & 1; the loads of stage s+2 fly while stage s is multiplied
   int nld = 0;
-  auto load = [&](SxStage<BM, AKM, T>& sa, StB& sb) {
+  auto load = [&](StA& sa, StB& sb) {
     const bool adv = ++nld < nst;
     opa.load(sa, adv);
     opb.load(sb, adv);
@@ -461,8 +557,7 @@ __global__ __launch_bounds__(BM * BN / (32 * WMT), MINW) void sgemm_bf16x3_kerne
     // software pipeline: iteration s loads stage s+2, multiplies stage s and splits stage s+1
     // (loaded one iteration earlier) into the other LDS buffer; the split's VALU and LDS writes
     // are interleaved with the MFMAs (sched_group_barrier), not issued after them
-    auto pipe = [&](SxStage<BM, AKM, T>& la, StB& lb, const SxStage<BM, AKM, T>& wa,
-                    const StB& wb, int buf) {
+    auto pipe = [&](StA& la, StB& lb, const StA& wa, const StB& wb, int buf) {
       load(la, lb);
       compute(buf);
       write(wa, wb, buf ^ 1);
@@ -910,6 +1005,36 @@ void sgemm_conv_wgrad_f32(uintptr_t dy, uintptr_t x, uintptr_t gw, int n, int H,
                        dim3(256), 0, st, p);
   check_launch();
   if (S > 1) sx_reduce(p, st);
+}
+
+// Convolution forward Y[pix][Cout] = sum_{tap, ci} X[pix shifted by the tap][ci] W[co][tap][ci] as ONE
+// implicit GEMM on the split-bf16 MFMA kernel: A gathered per tap from the NHWC input (CONVA
+// operand), B = the channels_last filter [Cout][KH*KW*Cin] (K-contiguous), C = the NHWC output
+// (ResNet-50 fp32: the three stride-2 3x3 layers, which the Winograd kernel does not take).
+void sgemm_conv_fwd_f32(uintptr_t x, uintptr_t w, uintptr_t y, int n, int H, int W, int Cin, int Ho, int Wo, int Cout,
+                        int KH, int KW, int stride, int pad, uintptr_t stream) {
+  const int64_t M = int64_t(n) * Ho * Wo;
+  const int K = KH * KW * Cin;
+  VODA_CHECK(n > 0 && Cout > 0 && Cin > 0 && M > 0 && M < (int64_t(1) << 31), "sgemm_conv_fwd_f32: bad shape");
+  VODA_CHECK(Cin % kSxBK == 0, "sgemm_conv_fwd_f32: input channels must be a multiple of 16");
+  VODA_CHECK(Cout % 4 == 0, "sgemm_conv_fwd_f32: output channels must be a multiple of 4");
+  VODA_CHECK(x % 16 == 0 && w % 16 == 0 && y % 16 == 0, "sgemm_conv_fwd_f32: operands need 16-B alignment");
+  VODA_CHECK(Ho == (H + 2 * pad - KH) / stride + 1 && Wo == (W + 2 * pad - KW) / stride + 1,
+             "sgemm_conv_fwd_f32: output size mismatch");
+  SxArgs p{};
+  p.a = reinterpret_cast<const float*>(x); p.lda = Cin;
+  p.b = reinterpret_cast<const float*>(w); p.ldb = K;
+  p.c = reinterpret_cast<float*>(y); p.ldc = Cout;
+  p.M = int(M); p.N = Cout; p.K = K;
+  p.cn = n; p.ch = H; p.cw = W; p.cin = Cin; p.cho = Ho; p.cwo = Wo; p.cs = stride; p.cpad = pad; p.ckw = KW;
+  p.S = 1;
+  p.kps = K;
+  p.tiles_n = (Cout + 127) / 128;
+  p.tiles = int((M + 127) / 128) * p.tiles_n;
+  p.stagger = g_sx_stagger;
+  hipLaunchKernelGGL((sgemm_bf16x3_kernel<128, 128, false, false, 6, true, false, 2, 2, false, 0, true>),
+                     dim3(unsigned(p.tiles)), dim3(256), 0, as_stream(stream), p);
+  check_launch();
 }
 
 }  // namespace voda

@@ -189,3 +189,22 @@ def test_conv_wgrad_implicit_gemm_matches_fp64(n, cin, cout, hw, stride, ws):
     bound = torch.nn.grad.conv2d_weight(x.double().abs(), gw.shape, dy.double().abs(), stride=stride, padding=1)
     err = ((gw.double() - g0.double() - ref).abs() / (bound + 1)).max().item()
     assert err < 1e-6, err
+
+
+@pytest.mark.parametrize("n,cin,cout,hw,stride,k", [(2, 128, 128, 56, 2, 3), (3, 256, 256, 28, 2, 3), (2, 512, 512, 14, 2, 3),
+                                                    (3, 64, 132, 9, 1, 3), (2, 32, 64, 7, 2, 1), (1, 16, 8, 5, 1, 3)])
+def test_conv_fwd_implicit_gemm_matches_fp64(n, cin, cout, hw, stride, k):
+    """y = conv2d(x, w, stride, pad) as one implicit GEMM (NHWC gather per tap in the A staging,
+    zero padding, stride 1 / 2, ragged pixel counts) against fp64."""
+    torch.manual_seed(cin + cout + hw + stride)
+    cl = torch.channels_last
+    pad = k // 2
+    x = torch.randn(n, cin, hw, hw, device=DEV).contiguous(memory_format=cl)
+    w = (torch.randn(cout, cin, k, k, device=DEV) / (k * cin ** 0.5)).contiguous(memory_format=cl)
+    assert SG.conv_fwd_ok(x, w)
+    y = SG.conv_fwd(x, w, stride, pad)
+    ref = torch.nn.functional.conv2d(x.double(), w.double(), None, stride, pad)
+    bound = torch.nn.functional.conv2d(x.double().abs(), w.double().abs(), None, stride, pad)
+    assert y.shape == ref.shape and y.is_contiguous(memory_format=cl)
+    err = ((y.double() - ref).abs() / (bound + 1e-30)).max().item()
+    assert err < 2e-7, err

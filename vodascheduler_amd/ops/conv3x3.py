@@ -37,6 +37,10 @@ USE_CONV_WGRAD = True
 # fp32 weight gradients of the C >= 128 layers (stride 1 and 2) as one implicit GEMM on the
 # split-bf16 MFMA kernel (ops/splitgemm.conv_wgrad_) instead of MIOpen's igemm_wrw (A/B switch)
 USE_SPLIT_WGRAD_F32 = True
+# fp32 forwards the Winograd kernel does not take (ResNet-50's three stride-2 3x3 layers) as one
+# implicit GEMM on the split-bf16 MFMA kernel (ops/splitgemm.conv_fwd, input gathered per tap while
+# staged) instead of MIOpen's igemm_fwd (A/B switch)
+USE_SPLIT_CONV_FWD = True
 # USE_WINOGRAD (module switch): fp32 3x3 stride-1 pad-1 forwards and input gradients (as forward
 # convolutions) on the own Winograd F(2x2, 3x3) kernel (ops/winograd.py) instead of MIOpen
 USE_WINOGRAD = True
@@ -186,6 +190,8 @@ class _ConvKxKFn(torch.autograd.Function):
         of y for the BN that follows (attached to the output by ConvKxK.forward)."""
         if USE_WINOGRAD and Wg.supported(x, weight, stride, padding):
             y = Wg.conv3x3_wino(x, weight, holder=holder)
+        elif USE_SPLIT_CONV_FWD and SG.conv_fwd_ok(x, weight):
+            y = SG.conv_fwd(x, weight, stride, padding)  # fp32 stride-2: implicit GEMM, split-bf16 MFMA
         else:
             y = F.conv2d(x, weight, None, stride, padding)
         ctx.save_for_backward(x, weight)

@@ -269,3 +269,32 @@ def conv_wgrad_(dy: torch.Tensor, x: torch.Tensor, gw: torch.Tensor, stride: int
     h.sgemm_conv_wgrad_f32(dy.data_ptr(), x.data_ptr(), gw.data_ptr(), n, H, W, cin, ho, wo, cout, kh, kw,
                            int(stride), int(padding), s, bool(accumulate), ws.data_ptr() if ws is not None else 0,
                            ws.numel() if ws is not None else 0, N.stream_of(dy))
+
+
+def conv_fwd_ok(x: torch.Tensor, w: torch.Tensor) -> bool:
+    """Does the implicit-GEMM convolution forward take these fp32 operands?  x [N, Cin, H, W] and
+    w [Cout, Cin, KH, KW], both channels_last, Cin % 16 == 0, Cout % 4 == 0."""
+    cl = torch.channels_last
+    if not (ENABLED and x.is_cuda and w.is_cuda and x.dtype == w.dtype == torch.float32):
+        return False
+    if x.dim() != 4 or w.dim() != 4 or w.shape[1] != x.shape[1] or x.shape[1] % 16 or w.shape[0] % 4:
+        return False
+    if not (x.is_contiguous(memory_format=cl) and w.is_contiguous(memory_format=cl)):
+        return False
+    return x.data_ptr() % 16 == 0 and w.data_ptr() % 16 == 0
+
+
+def conv_fwd(x: torch.Tensor, w: torch.Tensor, stride: int, padding: int) -> torch.Tensor:
+    """``F.conv2d(x, w, None, stride, padding)`` for fp32 channels_last operands (callers check
+    ``conv_fwd_ok``) as one implicit GEMM on the split-bf16 MFMA kernel; channels_last output.
+    CPU tensors get the PyTorch reference."""
+    if not x.is_cuda:
+        return torch.nn.functional.conv2d(x, w, None, stride, padding)
+    n, cin, H, W = x.shape
+    cout, _, kh, kw = w.shape
+    ho = (H + 2 * padding - kh) // stride + 1
+    wo = (W + 2 * padding - kw) // stride + 1
+    y = torch.empty((n, cout, ho, wo), dtype=torch.float32, device=x.device, memory_format=torch.channels_last)
+    N.hip().sgemm_conv_fwd_f32(x.data_ptr(), w.data_ptr(), y.data_ptr(), n, H, W, cin, ho, wo, cout, kh, kw,
+                               int(stride), int(padding), N.stream_of(x))
+    return y
