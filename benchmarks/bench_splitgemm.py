@@ -109,8 +109,8 @@ def main() -> None:
             if args.stagger_ab:
                 cands[f"nostag_t{t0}_s{s0}"] = (t0, s0, 0, 0)
             if not args.quick and not args.no_sweep:
-                tiles = -(-Mo // 128) * -(-No // 128)
-                for tile in (0, 1, 2, 3, 4):
+                tiles = -(-Mo // 128) * -(-No // 96)
+                for tile in (0, 1, 2, 3, 4, 7):
                     for s in (1, 2, 4, 8, 16):
                         if s > 1 and tiles * s > 2048:
                             continue

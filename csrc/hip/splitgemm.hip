@@ -78,8 +78,11 @@ struct SxArgs {
 int g_sx_stagger = 1;
 int g_sx_conv_ws = 0;  // convolution weight gradient kernel: 0 one-role, 1 / 2 wave-specialised (lead 1 / 2)
 
+// K-major images of R = 96 columns use the R = 128 layout (192-byte k-rows padded to 256 B)
+template <int R> struct SxKmPitch { static constexpr int kR = R == 96 ? 128 : R; };
+
 template <int R, bool KM> struct SxImg {
-  static constexpr int kBytes = KM ? 3 * kSxBK * R * 2 : R * kSxKcPitch;
+  static constexpr int kBytes = KM ? 3 * kSxBK * SxKmPitch<R>::kR * 2 : R * kSxKcPitch;
 };
 
 // K-major image: byte offset of column ``col`` (a multiple of 4) of k-row ``k`` in one plane
@@ -87,7 +90,9 @@ template <int R, bool KM> struct SxImg {
 // keeps the 8-B staging writes and the 32x32x16 transposed reads conflict-free.
 template <int R>
 __device__ __forceinline__ int sx_km_off(int k, int col) {
-  if constexpr (R == 64) {
+  if constexpr (R == 96) {
+    return sx_km_off<128>(k, col);
+  } else if constexpr (R == 64) {
     // 128-B k-rows: k-rows 2j and 2j + 1 side by side form row j of a [8][128] image that takes
     // the 256-B swizzle (a bijection, so staging writes and fragment reads agree)
     return sx_km_off<128>(k >> 1, ((k & 1) << 6) + col);
@@ -192,7 +197,7 @@ struct SxOperand {
   // becomes three 8-byte plane pieces: K-contiguous images keep a row's planes 16 B apart,
   // K-major images a whole [16][R] plane apart.
   __device__ __forceinline__ void write(const SxStage<R, KM, T>& s, uint8_t* img, uint8_t* dummy) const {
-    constexpr int kPl = KM ? kSxBK * R * 2 : 16;
+    constexpr int kPl = KM ? kSxBK * SxKmPitch<R>::kR * 2 : 16;
 #pragma unroll
     for (int i = 0; i < kPer; ++i) {
       uint2 h0, m0, l0, h1, m1, l1;
@@ -286,7 +291,7 @@ struct SxConvOperand {
   }
 
   __device__ __forceinline__ void write(const Stage& s, uint8_t* img_, uint8_t* dummy) const {
-    constexpr int kPl = kSxBK * R * 2;
+    constexpr int kPl = kSxBK * SxKmPitch<R>::kR * 2;
 #pragma unroll
     for (int i = 0; i < kPer; ++i) {
       const uint32_t m0 = (s.keep >> (2 * i)) & 1 ? 0xffffffffu : 0u, m1 = (s.keep >> (2 * i + 1)) & 1 ? 0xffffffffu : 0u;
@@ -417,7 +422,7 @@ __device__ __forceinline__ void sx_frag(const uint8_t* img, int r0, int lane, sx
     const int g = lane >> 4, i = lane & 15, q = i >> 2, pp = i & 3;
     const int k = 8 * (g >> 1) + q, col = r0 + 16 * (g & 1) + 4 * pp;
     const int o0 = sx_km_off<R>(k, col), o1 = sx_km_off<R>(k + 4, col);
-    constexpr int kPlane = kSxBK * R * 2;
+    constexpr int kPlane = kSxBK * SxKmPitch<R>::kR * 2;
 #pragma unroll
     for (int pl = 0; pl < 3; ++pl) {
       const uint2 lo = sx_tr_read(img + pl * kPlane + o0);
@@ -439,12 +444,12 @@ __device__ __forceinline__ float sx_finish(const SxArgs& p, int row, int col, fl
   return v;
 }
 
-// WMT: 32-row MFMA tiles per wave along M (2: 64 x 64 per wave; 4: 128 x 64 per wave, one wave per
-// SIMD with its accumulators in AGPRs)
+// WMT / WNT: 32-row / 32-column MFMA tiles per wave (2 x 2: 64 x 64 per wave; 4 x 2: 128 x 64 per
+// wave, one wave per SIMD with its accumulators in AGPRs; 1 x 3: 32 x 96, the 128 x 96 tile)
 template <int BM, int BN, bool AKM, bool BKM, int NPROD, bool DUAL, bool TWO_SETS, int MINW, int WMT, bool CONV = false,
-          int ORDER = 0, bool CONVA = false>
-__global__ __launch_bounds__(BM * BN / (32 * WMT), MINW) void sgemm_bf16x3_kernel(SxArgs p) {
-  constexpr int NWN = BN / 64;
+          int ORDER = 0, bool CONVA = false, int WNT = 2>
+__global__ __launch_bounds__((BM / (32 * WMT)) * (BN / (32 * WNT)) * 64, MINW) void sgemm_bf16x3_kernel(SxArgs p) {
+  constexpr int NWN = BN / (32 * WNT);
   constexpr int NWM = BM / (32 * WMT);
   constexpr int T = 64 * NWM * NWN;
   constexpr int kImgA = SxImg<BM, AKM>::kBytes, kImgB = SxImg<BN, BKM>::kBytes;
@@ -482,27 +487,27 @@ __global__ __launch_bounds__(BM * BN / (32 * WMT), MINW) void sgemm_bf16x3_kerne
   StA sa0, sa1;
   StB sb0, sb1;
 
-  sx_f32x16 acc[WMT][2], cor[WMT][2];
+  sx_f32x16 acc[WMT][WNT], cor[WMT][WNT];
 #pragma unroll
   for (int i = 0; i < WMT; ++i)
 #pragma unroll
-    for (int j = 0; j < 2; ++j)
+    for (int j = 0; j < WNT; ++j)
 #pragma unroll
       for (int r = 0; r < 16; ++r) { acc[i][j][r] = 0.f; cor[i][j][r] = 0.f; }
 
   auto compute = [&](int buf) {
     const uint8_t* A = smem + buf * kBuf;
     const uint8_t* B = A + kImgA;
-    sx_bf16x8 fa[WMT][3], fb[2][3];
+    sx_bf16x8 fa[WMT][3], fb[WNT][3];
 #pragma unroll
     for (int i = 0; i < WMT; ++i) sx_frag<BM, AKM>(A, wm * 32 * WMT + 32 * i, lane, fa[i]);
-    sx_frag<BN, BKM>(B, wn * 64, lane, fb[0]);
-    sx_frag<BN, BKM>(B, wn * 64 + 32, lane, fb[1]);
+#pragma unroll
+    for (int j = 0; j < WNT; ++j) sx_frag<BN, BKM>(B, wn * 32 * WNT + 32 * j, lane, fb[j]);
     if constexpr (ORDER == 0) {  // tile-outer: each accumulator's products back to back
 #pragma unroll
       for (int i = 0; i < WMT; ++i)
 #pragma unroll
-        for (int j = 0; j < 2; ++j) {
+        for (int j = 0; j < WNT; ++j) {
           sx_f32x16& s = DUAL ? cor[i][j] : acc[i][j];
           if (NPROD >= 9) {
             s = sx_mfma(fa[i][2], fb[j][2], s);
@@ -526,14 +531,14 @@ __global__ __launch_bounds__(BM * BN / (32 * WMT), MINW) void sgemm_bf16x3_kerne
 #pragma unroll
         for (int i = 0; i < WMT; ++i)
 #pragma unroll
-          for (int j = 0; j < 2; ++j) {
+          for (int j = 0; j < WNT; ++j) {
             sx_f32x16& s = DUAL ? cor[i][j] : acc[i][j];
             s = sx_mfma(fa[i][kPa[q]], fb[j][kPb[q]], s);
           }
 #pragma unroll
       for (int i = 0; i < WMT; ++i)
 #pragma unroll
-        for (int j = 0; j < 2; ++j) acc[i][j] = sx_mfma(fa[i][0], fb[j][0], acc[i][j]);
+        for (int j = 0; j < WNT; ++j) acc[i][j] = sx_mfma(fa[i][0], fb[j][0], acc[i][j]);
     }
   };
   auto write = [&](const StA& sa, const StB& sb, int buf) {
@@ -603,8 +608,8 @@ __global__ __launch_bounds__(BM * BN / (32 * WMT), MINW) void sgemm_bf16x3_kerne
 #pragma unroll
   for (int i = 0; i < WMT; ++i)
 #pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      const int col = n0 + wn * 64 + 32 * j + (lane & 31);
+    for (int j = 0; j < WNT; ++j) {
+      const int col = n0 + wn * 32 * WNT + 32 * j + (lane & 31);
       if (col >= p.N) continue;
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
@@ -851,13 +856,13 @@ void sx_reduce(const SxArgs& p, hipStream_t st) {
   check_launch();
 }
 
-template <int BM, int BN, int NPROD, bool DUAL, bool TWO, int MINW = 2, int WMT = 2, int ORDER = 0>
+template <int BM, int BN, int NPROD, bool DUAL, bool TWO, int MINW = 2, int WMT = 2, int ORDER = 0, int WNT = 2>
 void sx_launch_tile(const SxArgs& a, bool akm, bool bkm, unsigned grid, hipStream_t st) {
-  const dim3 blk(BM * BN / (32 * WMT));
-  if (!akm && !bkm) hipLaunchKernelGGL((sgemm_bf16x3_kernel<BM, BN, false, false, NPROD, DUAL, TWO, MINW, WMT, false, ORDER>), grid, blk, 0, st, a);
-  else if (!akm && bkm) hipLaunchKernelGGL((sgemm_bf16x3_kernel<BM, BN, false, true, NPROD, DUAL, TWO, MINW, WMT, false, ORDER>), grid, blk, 0, st, a);
-  else if (akm && !bkm) hipLaunchKernelGGL((sgemm_bf16x3_kernel<BM, BN, true, false, NPROD, DUAL, TWO, MINW, WMT, false, ORDER>), grid, blk, 0, st, a);
-  else hipLaunchKernelGGL((sgemm_bf16x3_kernel<BM, BN, true, true, NPROD, DUAL, TWO, MINW, WMT, false, ORDER>), grid, blk, 0, st, a);
+  const dim3 blk((BM / (32 * WMT)) * (BN / (32 * WNT)) * 64);
+  if (!akm && !bkm) hipLaunchKernelGGL((sgemm_bf16x3_kernel<BM, BN, false, false, NPROD, DUAL, TWO, MINW, WMT, false, ORDER, false, WNT>), grid, blk, 0, st, a);
+  else if (!akm && bkm) hipLaunchKernelGGL((sgemm_bf16x3_kernel<BM, BN, false, true, NPROD, DUAL, TWO, MINW, WMT, false, ORDER, false, WNT>), grid, blk, 0, st, a);
+  else if (akm && !bkm) hipLaunchKernelGGL((sgemm_bf16x3_kernel<BM, BN, true, false, NPROD, DUAL, TWO, MINW, WMT, false, ORDER, false, WNT>), grid, blk, 0, st, a);
+  else hipLaunchKernelGGL((sgemm_bf16x3_kernel<BM, BN, true, true, NPROD, DUAL, TWO, MINW, WMT, false, ORDER, false, WNT>), grid, blk, 0, st, a);
 }
 
 template <int LEAD, int DEPTH>
@@ -869,8 +874,8 @@ void sx_launch_ws(const SxArgs& a, bool akm, bool bkm, unsigned grid, hipStream_
   else hipLaunchKernelGGL((sgemm_ws_kernel<true, true, false, LEAD, DEPTH>), grid, blk, 0, st, a);
 }
 
-constexpr int kSxTileM[7] = {128, 256, 128, 256, 256, 64, 256};
-constexpr int kSxTileN[7] = {128, 128, 256, 128, 128, 256, 64};
+constexpr int kSxTileM[8] = {128, 256, 128, 256, 256, 64, 256, 128};
+constexpr int kSxTileN[8] = {128, 128, 256, 128, 128, 256, 64, 96};
 
 }  // namespace
 
@@ -897,7 +902,7 @@ void sgemm_f32(uintptr_t a, int64_t lda, bool a_kmajor, uintptr_t b, int64_t ldb
   VODA_CHECK(M > 0 && N > 0 && K > 0, "sgemm_f32: empty GEMM");
   VODA_CHECK(K % kSxBK == 0, "sgemm_f32: K must be a multiple of 16");
   VODA_CHECK(M % 4 == 0 && N % 4 == 0, "sgemm_f32: M and N must be multiples of 4");
-  VODA_CHECK(tile >= 0 && tile < 7, "sgemm_f32: bad tile id");
+  VODA_CHECK(tile >= 0 && tile < 8, "sgemm_f32: bad tile id");
   VODA_CHECK(variant >= 0 && variant <= 7 && (variant == 0 || tile == 0), "sgemm_f32: bad math variant");
   VODA_CHECK(epi >= kSxEpiNone && epi <= kSxEpiDGelu && (epi == kSxEpiNone || aux != 0), "sgemm_f32: bad epilogue");
   VODA_CHECK(a % 16 == 0 && b % 16 == 0 && lda % 4 == 0 && ldb % 4 == 0, "sgemm_f32: operands need 16-B rows");
@@ -943,6 +948,9 @@ void sgemm_f32(uintptr_t a, int64_t lda, bool a_kmajor, uintptr_t b, int64_t ldb
     sx_launch_tile<256, 128, 6, true, false>(p, a_kmajor, b_kmajor, grid, st);
   } else if (tile == 2) {
     sx_launch_tile<128, 256, 6, true, false>(p, a_kmajor, b_kmajor, grid, st);
+  } else if (tile == 7) {  // 128 x 96 (4 waves of 32 x 96): N = 768 outputs as 8 column tiles, so
+                           // 8192 x 768 runs 512 workgroups (two per CU) instead of 384
+    sx_launch_tile<128, 96, 6, true, false, 2, 1, 0, 3>(p, a_kmajor, b_kmajor, grid, st);
   } else if (tile == 5) {  // 64 x 256 (4 waves along N): outputs with 64 rows (no half-empty tiles)
     sx_launch_tile<64, 256, 6, true, false>(p, a_kmajor, b_kmajor, grid, st);
   } else if (tile == 6) {  // 256 x 64 (4 waves along M): outputs with 64 columns

@@ -25,7 +25,7 @@ def _bound(a, b):
 
 @pytest.mark.parametrize("akm", [False, True])
 @pytest.mark.parametrize("bkm", [False, True])
-@pytest.mark.parametrize("tile", [0, 1, 2])
+@pytest.mark.parametrize("tile", [0, 1, 2, 7])
 def test_orientations_ragged(akm, bkm, tile):
     torch.manual_seed(tile * 4 + 2 * akm + bkm)
     M, K, N = 388, 272, 196  # ragged in M and N for every tile
@@ -118,9 +118,12 @@ def test_no_worse_than_hipblaslt_wide_magnitudes():
     assert e_sx <= 1.5 * e_lib, (e_sx, e_lib)
 
 
-def test_epilogues_bias_accumulate_gelu_dgelu():
+@pytest.mark.parametrize("tile", [None, 7])
+def test_epilogues_bias_accumulate_gelu_dgelu(tile, monkeypatch):
+    if tile is not None:  # route every call of this test to the given tile
+        monkeypatch.setattr(SG, "choose", lambda M, N, K, variant=0: (tile, 1))
     torch.manual_seed(9)
-    M, K, N = 320, 160, 256
+    M, K, N = 320, 160, 192
     x = torch.randn(M, K, device=DEV)
     w = torch.randn(N, K, device=DEV) * 0.1
     bias = torch.randn(N, device=DEV)

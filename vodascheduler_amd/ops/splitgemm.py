@@ -25,7 +25,7 @@ import torch
 from . import _native as N
 
 EPI_NONE, EPI_GELU, EPI_DGELU = 0, 1, 2
-TILES = {0: (128, 128), 1: (256, 128), 2: (128, 256), 5: (64, 256), 6: (256, 64)}
+TILES = {0: (128, 128), 1: (256, 128), 2: (128, 256), 5: (64, 256), 6: (256, 64), 7: (128, 96)}
 
 
 def thin_tile(M: int, Nn: int) -> int:
@@ -52,6 +52,7 @@ DEFAULT_VARIANT = 0
 CONV_WGRAD_WS = 0
 # split-K reduce: slab groups per float4 column (-1 automatic: ~4096 blocks-worth of groups, >= 16
 # slabs per group; 1 = one thread per column, the round-5 form)
+USE_T7 = True  # the 128 x 96 tile in ``choose`` (A/B switch)
 REDUCE_GROUPS = -1
 REDUCE_GROUPS_AUTO = True  # False: one group (A/B switch)
 _applied = {"reduce_groups": None}
@@ -140,6 +141,18 @@ def choose(M: int, Nn: int, K: int, variant: int = 0) -> tuple[int, int]:
     384-workgroup round leaves CUs with one workgroup idle half the time); small outputs (weight
     gradients: 36-144 tiles) split K towards ~1152 workgroups with >= 256 k per split."""
     tiles = -(-M // 128) * -(-Nn // 128)
+    # 128 x 96 tiles where they fill whole rounds of the 512 resident workgroups and 128 x 128
+    # tiles do not (BERT-base: 8192 x 2304 as 1536 tiles, 8192 x 768 as 512): qkv forward 200 ->
+    # 192 us, o forward 76 -> 71, o input gradient 78 -> 71 (profiles/r6/splitgemm_t7_sweep.jsonl);
+    # not for K > 2304, where 128 x 128 with split-K 2 stays ahead (fc1 / fc2 input gradient / fc2)
+    if USE_T7 and Nn % 96 == 0 and K <= 2304 and M >= 4096:
+        t7 = -(-M // 128) * (Nn // 96)
+
+        def fill(t: int) -> float:
+            return t / (-(-t // 512) * 512)
+
+        if t7 >= 384 and fill(t7) > 1.05 * fill(tiles):
+            return 7, 1
     if tiles >= 1024:
         return 0, 1
     if tiles >= 384:
