@@ -86,6 +86,9 @@ USE_SPLIT_WGRAD_F32 = True
 # ... with the 64 x 256 / 256 x 64 tiles where the output has a 64-wide side (stage 1: [64][256],
 # [256][64], [64][64]) instead of half-empty 128 x 128 tiles
 USE_THIN_TILES = True
+# ... split-K to ~this many workgroups (one round of the 512 resident ones; 1024 before round 6's
+# sweep, profiles/r6/resnet50_wgrad_splits_probe_b.jsonl)
+WGRAD_TARGET_WG = 512
 
 
 def _sx(a: torch.Tensor, b: torch.Tensor) -> bool:
@@ -429,7 +432,7 @@ class _Conv1x1Fn(torch.autograd.Function):
                 # split-K into the flat gradient, ~1024 workgroups over the pixels
                 tile = SG.thin_tile(cout, cin) if USE_THIN_TILES else 0
                 SG.matmul(dy2.t(), x2, out=g2, accumulate=True, tile=tile,
-                          splits=SG.conv_wgrad_splits(cout, cin, dy2.shape[0], tile))
+                          splits=SG.conv_wgrad_splits(cout, cin, dy2.shape[0], tile, WGRAD_TARGET_WG))
                 _ready(weight)
             elif (dy2.dtype == torch.float32 and g2 is not None and g2.dtype == torch.float32
                     and blas_wgrad_f32_ok(dy2.shape[0], cout, cin)):

@@ -157,6 +157,14 @@ def choose(M: int, Nn: int, K: int, variant: int = 0) -> tuple[int, int]:
         return 0, 1
     if tiles >= 384:
         return 0, 2 if K >= 2048 else 1
+    # small outputs with long reductions (weight gradients over the tokens): the split-K sweep of
+    # the BERT-base shapes (profiles/r6/splitgemm_wgrad_splits.jsonl) put the optimum at 7 splits
+    # for 108-144 output tiles (qkv 210 -> 183 us, fc1 / fc2 254 -> 237 us vs the ~1152-workgroup
+    # rule below) and 12 for 36 tiles (o: 89 -> 74 us)
+    if 96 <= tiles <= 160 and K >= 7 * 512:
+        return 0, 7
+    if 24 <= tiles <= 48 and K >= 12 * 512:
+        return 0, 12
     # tiny outputs with huge reductions (ResNet 1x1 weight gradients: 64 x 256 over 800k pixels)
     # split further: the slabs stay small
     s = max(1, min(16 if tiles >= 16 else 1024, 1152 // tiles, K // 256))
@@ -254,16 +262,18 @@ def conv_wgrad_ok(dy: torch.Tensor, x: torch.Tensor, gw: torch.Tensor) -> bool:
     return dy.data_ptr() % 16 == 0 and x.data_ptr() % 16 == 0 and gw.data_ptr() % 16 == 0
 
 
-def conv_wgrad_splits(cout: int, n_cols: int, pixels: int, tile: int = 0) -> int:
-    """Split-K count of the convolution weight gradient: ~1024 workgroups (two rounds of the 512
-    resident 128 x 128 workgroups), >= 256 pixels per split."""
+def conv_wgrad_splits(cout: int, n_cols: int, pixels: int, tile: int = 0, target: int = 1024) -> int:
+    """Split-K count of a convolution weight gradient: ~``target`` workgroups, >= 256 pixels per
+    split.  1024 (two rounds of the 512 resident 128 x 128 workgroups) for the 3x3 implicit GEMMs;
+    the 1x1 weight gradients pass 512: one round ran all nine ResNet-50 1x1 shapes 5-11 % faster
+    than two (profiles/r6/resnet50_wgrad_splits_probe_b.jsonl)."""
     bm, bn = TILES[tile]
     tiles = -(-cout // bm) * -(-n_cols // bn)
-    return max(1, min(1024 // tiles, pixels // 256))
+    return max(1, min(max(1, target // tiles), pixels // 256))
 
 
 def conv_wgrad_(dy: torch.Tensor, x: torch.Tensor, gw: torch.Tensor, stride: int, padding: int,
-                accumulate: bool = True) -> None:
+                accumulate: bool = True, splits: int | None = None) -> None:
     """``gw (+)= dW`` of a convolution on the split-bf16 MFMA kernel (callers check
     ``conv_wgrad_ok``); CPU tensors get the fp32 reference."""
     if not dy.is_cuda:
@@ -273,7 +283,7 @@ def conv_wgrad_(dy: torch.Tensor, x: torch.Tensor, gw: torch.Tensor, stride: int
     n, cin, H, W = x.shape
     cout, _, kh, kw = gw.shape
     ho, wo = dy.shape[2], dy.shape[3]
-    s = conv_wgrad_splits(cout, kh * kw * cin, n * ho * wo)
+    s = conv_wgrad_splits(cout, kh * kw * cin, n * ho * wo) if splits is None else splits
     h = N.hip()
     _sync_knobs(h)
     h.sgemm_conv_wgrad_set_ws(CONV_WGRAD_WS)
