@@ -30,6 +30,7 @@ PYBIND11_MODULE(_vodahip, m) {
   m.def("sgemm_conv_wgrad_set_ws", &sgemm_conv_wgrad_set_ws);
   m.def("sgemm_set_reduce_groups", &sgemm_set_reduce_groups);
   m.def("sgemm_conv_fwd_f32", &sgemm_conv_fwd_f32);
+  m.def("sgemm_conv_dgrad_s2_class", &sgemm_conv_dgrad_s2_class);
   m.def("sgemm_conv_wgrad_f32", &sgemm_conv_wgrad_f32);
   m.def("wgrad_conv_workspace_floats", &wgrad_conv_workspace_floats);
   m.def("wgrad_conv", &wgrad_conv);

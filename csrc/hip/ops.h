@@ -273,6 +273,8 @@ void sgemm_conv_wgrad_set_ws(int mode);
 void sgemm_set_reduce_groups(int g);
 void sgemm_conv_fwd_f32(uintptr_t x, uintptr_t w, uintptr_t y, int n, int H, int W, int Cin, int Ho, int Wo, int Cout,
                         int KH, int KW, int stride, int pad, uintptr_t stream);
+void sgemm_conv_dgrad_s2_class(uintptr_t dy, uintptr_t wc, uintptr_t dx, int n, int Ho, int Wo, int Cout, int H, int W,
+                               int Cin, int ph, int pw, uintptr_t stream);
 void sgemm_conv_wgrad_f32(uintptr_t dy, uintptr_t x, uintptr_t gw, int n, int H, int W, int Cin, int Ho, int Wo,
                           int Cout, int KH, int KW, int stride, int pad, int splits, bool accumulate, uintptr_t ws,
                           int64_t ws_floats, uintptr_t stream);

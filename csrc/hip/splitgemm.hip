@@ -73,6 +73,10 @@ struct SxArgs {
   // kh - cpad][wo*cs + kw - cpad][ci] for n = (kh*ckw + kw)*cin + ci and output pixel
   // k = (img, ho, wo); zero outside the image.  X is NHWC [cn][ch][cw][cin].
   int cn, ch, cw, cin, cho, cwo, cs, cpad, ckw;
+  // output row map (omap = 1, S == 1, beta == 0): GEMM row m = (img, i, j) of an ohc x owc grid is
+  // stored at pixel (2i + oph, 2j + opw) of an oH x oW NHWC map -- one parity class of a stride-2
+  // convolution's input gradient
+  int omap, oH, oW, oph, opw, ohc, owc;
 };
 
 int g_sx_stagger = 1;
@@ -432,6 +436,13 @@ __device__ __forceinline__ void sx_frag(const uint8_t* img, int r0, int lane, sx
   }
 }
 
+__device__ __forceinline__ int64_t sx_out_row(const SxArgs& p, int row) {
+  if (!p.omap) return row;
+  const int hw = p.ohc * p.owc;
+  const int img = row / hw, r = row - img * hw, i = r / p.owc, j = r - (r / p.owc) * p.owc;
+  return (int64_t(img) * p.oH + 2 * i + p.oph) * p.oW + 2 * j + p.opw;
+}
+
 __device__ __forceinline__ float sx_finish(const SxArgs& p, int row, int col, float v) {
   if (p.beta) v += p.c[int64_t(row) * p.ldc + col];
   if (p.bias) v += p.bias[col];
@@ -619,7 +630,7 @@ __global__ __launch_bounds__((BM / (32 * WMT)) * (BN / (32 * WNT)) * 64, MINW) v
         if (p.S > 1) {
           p.ws[(int64_t(split) * p.M + row) * p.N + col] = v;
         } else {
-          p.c[int64_t(row) * p.ldc + col] = sx_finish(p, row, col, v);
+          p.c[sx_out_row(p, row) * p.ldc + col] = sx_finish(p, row, col, v);
         }
       }
     }
@@ -1041,6 +1052,40 @@ void sgemm_conv_fwd_f32(uintptr_t x, uintptr_t w, uintptr_t y, int n, int H, int
   p.tiles = int((M + 127) / 128) * p.tiles_n;
   p.stagger = g_sx_stagger;
   hipLaunchKernelGGL((sgemm_bf16x3_kernel<128, 128, false, false, 6, true, false, 2, 2, false, 0, true>),
+                     dim3(unsigned(p.tiles)), dim3(256), 0, as_stream(stream), p);
+  check_launch();
+}
+
+// One parity class (ph, pw) of the input gradient of a stride-2, pad-1 3x3 convolution:
+//   dX[img][2i + ph][2j + pw][ci] = sum_{taps (th, tw) of the class} sum_co dY[img][i + th][j + tw][co] Wc[tap][co][ci]
+// the class's taps are 1 (even) or 2 (odd) per dimension: even rows take kh = 1, odd rows kh = 2
+// (th = 0) and kh = 0 (th = 1); Wc = [nth * ntw][Cout][Cin] holds W[:, :, kh, kw] of the class's taps
+// in that order (ops/splitgemm.conv_dgrad_s2).  A = dY gathered per tap (CONVA, stride 1, no pad,
+// zero past the map), B = Wc (K-major), C rows mapped onto the class's pixels of dX.
+void sgemm_conv_dgrad_s2_class(uintptr_t dy, uintptr_t wc, uintptr_t dx, int n, int Ho, int Wo, int Cout, int H, int W,
+                               int Cin, int ph, int pw, uintptr_t stream) {
+  const int nth = ph ? 2 : 1, ntw = pw ? 2 : 1;
+  const int hc = (H - ph + 1) / 2, wcn = (W - pw + 1) / 2;  // class rows / columns
+  const int64_t M = int64_t(n) * hc * wcn;
+  const int K = nth * ntw * Cout;
+  VODA_CHECK(n > 0 && Cin > 0 && Cout > 0 && M > 0 && M < (int64_t(1) << 31), "sgemm_conv_dgrad_s2: bad shape");
+  VODA_CHECK(Cout % kSxBK == 0 && Cin % 4 == 0, "sgemm_conv_dgrad_s2: Cout % 16 and Cin % 4 required");
+  VODA_CHECK(Ho == (H - 1) / 2 + 1 && Wo == (W - 1) / 2 + 1, "sgemm_conv_dgrad_s2: output size mismatch");
+  VODA_CHECK(hc <= Ho && wcn <= Wo && (ph == 0 || ph == 1) && (pw == 0 || pw == 1), "sgemm_conv_dgrad_s2: class");
+  VODA_CHECK(dy % 16 == 0 && wc % 16 == 0 && dx % 16 == 0, "sgemm_conv_dgrad_s2: operands need 16-B alignment");
+  SxArgs p{};
+  p.a = reinterpret_cast<const float*>(dy); p.lda = Cout;
+  p.b = reinterpret_cast<const float*>(wc); p.ldb = Cin;
+  p.c = reinterpret_cast<float*>(dx); p.ldc = Cin;
+  p.M = int(M); p.N = Cin; p.K = K;
+  p.cn = n; p.ch = Ho; p.cw = Wo; p.cin = Cout; p.cho = hc; p.cwo = wcn; p.cs = 1; p.cpad = 0; p.ckw = ntw;
+  p.omap = 1; p.oH = H; p.oW = W; p.oph = ph; p.opw = pw; p.ohc = hc; p.owc = wcn;
+  p.S = 1;
+  p.kps = K;
+  p.tiles_n = (Cin + 127) / 128;
+  p.tiles = int((M + 127) / 128) * p.tiles_n;
+  p.stagger = g_sx_stagger;
+  hipLaunchKernelGGL((sgemm_bf16x3_kernel<128, 128, false, true, 6, true, false, 2, 2, false, 0, true>),
                      dim3(unsigned(p.tiles)), dim3(256), 0, as_stream(stream), p);
   check_launch();
 }

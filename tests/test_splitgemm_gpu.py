@@ -211,3 +211,23 @@ def test_conv_fwd_implicit_gemm_matches_fp64(n, cin, cout, hw, stride, k):
     assert y.shape == ref.shape and y.is_contiguous(memory_format=cl)
     err = ((y.double() - ref).abs() / (bound + 1e-30)).max().item()
     assert err < 2e-7, err
+
+
+@pytest.mark.parametrize("n,cin,cout,hw", [(2, 128, 128, 56), (2, 256, 256, 28), (3, 512, 512, 14), (3, 64, 48, 7),
+                                           (2, 32, 16, 9), (1, 16, 32, 8)])
+def test_conv_dgrad_stride2_polyphase_matches_fp64(n, cin, cout, hw):
+    """dX of a stride-2 pad-1 3x3 convolution as four parity-class implicit GEMMs (odd and even
+    input sizes) against fp64."""
+    torch.manual_seed(cin + cout + hw)
+    cl = torch.channels_last
+    ho = (hw - 1) // 2 + 1
+    dy = torch.randn(n, cout, ho, ho, device=DEV).contiguous(memory_format=cl)
+    w = (torch.randn(cout, cin, 3, 3, device=DEV) / (3 * cout ** 0.5)).contiguous(memory_format=cl)
+    shape = (n, cin, hw, hw)
+    assert SG.conv_dgrad_s2_ok(dy, w, shape)
+    dx = SG.conv_dgrad_s2(dy, w, shape)
+    ref = torch.nn.grad.conv2d_input(shape, w.double(), dy.double(), stride=2, padding=1)
+    bound = torch.nn.grad.conv2d_input(shape, w.double().abs(), dy.double().abs(), stride=2, padding=1)
+    assert dx.is_contiguous(memory_format=cl)
+    err = ((dx.double() - ref).abs() / (bound + 1e-30)).max().item()
+    assert err < 2e-7, err

@@ -41,6 +41,11 @@ USE_SPLIT_WGRAD_F32 = True
 # implicit GEMM on the split-bf16 MFMA kernel (ops/splitgemm.conv_fwd, input gathered per tap while
 # staged) instead of MIOpen's igemm_fwd (A/B switch)
 USE_SPLIT_CONV_FWD = True
+# ... and their input gradients as four polyphase implicit GEMMs (ops/splitgemm.conv_dgrad_s2)
+# instead of MIOpen's igemm_bwd + zero fill.  Off: the parity classes with 1-2 taps reduce over
+# only 128-512 k (8-32 stages per tile), and the step lost 58.95 -> 59.12 ms (same-box A/B,
+# profiles/r6/ab_split_conv_dgrad_s2_resnet50_fp32.jsonl); kept tested (fp64) as the alternative
+USE_SPLIT_CONV_DGRAD = False
 # USE_WINOGRAD (module switch): fp32 3x3 stride-1 pad-1 forwards and input gradients (as forward
 # convolutions) on the own Winograd F(2x2, 3x3) kernel (ops/winograd.py) instead of MIOpen
 USE_WINOGRAD = True
@@ -207,6 +212,9 @@ class _ConvKxKFn(torch.autograd.Function):
         dx = None
         if ctx.needs_input_grad[0] and USE_WINOGRAD and Wg.supported(dy, weight, stride, padding, flip=True):
             dx = Wg.conv3x3_wino(dy, weight, flip=True)
+        elif (ctx.needs_input_grad[0] and USE_SPLIT_CONV_DGRAD and stride == 2 and padding == 1
+              and SG.conv_dgrad_s2_ok(dy, weight, x.shape)):
+            dx = SG.conv_dgrad_s2(dy, weight, x.shape)  # fp32: four polyphase implicit GEMMs
         elif ctx.needs_input_grad[0] and dgrad_fwd_ok(weight, stride, padding):
             dx = dgrad_as_forward(dy, weight, padding)
         elif ctx.needs_input_grad[0]:

@@ -321,3 +321,46 @@ def conv_fwd(x: torch.Tensor, w: torch.Tensor, stride: int, padding: int) -> tor
     N.hip().sgemm_conv_fwd_f32(x.data_ptr(), w.data_ptr(), y.data_ptr(), n, H, W, cin, ho, wo, cout, kh, kw,
                                int(stride), int(padding), N.stream_of(x))
     return y
+
+
+_S2_TAPS = {0: (1,), 1: (2, 0)}  # kernel rows (cols) of the taps that reach even / odd input rows
+
+
+def conv_dgrad_s2_ok(dy: torch.Tensor, w: torch.Tensor, in_shape) -> bool:
+    """Input gradient of a stride-2, pad-1 3x3 fp32 convolution on the polyphase implicit GEMMs?"""
+    cl = torch.channels_last
+    if not (ENABLED and dy.is_cuda and w.is_cuda and dy.dtype == w.dtype == torch.float32):
+        return False
+    if dy.dim() != 4 or w.dim() != 4 or tuple(w.shape[2:]) != (3, 3) or len(in_shape) != 4:
+        return False
+    n, cin, H, W = in_shape
+    cout = w.shape[0]
+    if w.shape[1] != cin or dy.shape[1] != cout or dy.shape[0] != n or cout % 16 or cin % 4:
+        return False
+    if dy.shape[2] != (H - 1) // 2 + 1 or dy.shape[3] != (W - 1) // 2 + 1:
+        return False
+    return dy.is_contiguous(memory_format=cl) and dy.data_ptr() % 16 == 0
+
+
+def conv_dgrad_s2(dy: torch.Tensor, w: torch.Tensor, in_shape) -> torch.Tensor:
+    """dX of ``conv2d(x, w, stride=2, padding=1)`` (3x3, fp32, channels_last) as four polyphase
+    implicit GEMMs on the split-bf16 MFMA kernel: the input pixels of one (row, column) parity
+    class receive 1, 2, 2 or 4 of the nine taps, each a stride-1 gather of dY (no zero-inserted
+    map, no wasted products).  CPU tensors get the PyTorch reference."""
+    n, cin, H, W = in_shape
+    if not dy.is_cuda:
+        return torch.nn.grad.conv2d_input(tuple(in_shape), w, dy, stride=2, padding=1)
+    cout = w.shape[0]
+    ho, wo = dy.shape[2], dy.shape[3]
+    dx = torch.empty((n, cin, H, W), dtype=torch.float32, device=dy.device, memory_format=torch.channels_last)
+    wt = w.permute(2, 3, 0, 1)  # [kh][kw][co][ci] view
+    h = N.hip()
+    st = N.stream_of(dy)
+    for ph in (0, 1):
+        for pw in (0, 1):
+            if (H - ph + 1) // 2 <= 0 or (W - pw + 1) // 2 <= 0:
+                continue
+            wc = torch.stack([wt[kh, kw] for kh in _S2_TAPS[ph] for kw in _S2_TAPS[pw]]).contiguous()
+            h.sgemm_conv_dgrad_s2_class(dy.data_ptr(), wc.data_ptr(), dx.data_ptr(), n, ho, wo, cout, H, W, cin,
+                                        ph, pw, st)
+    return dx
