@@ -45,8 +45,10 @@ def main():
         row = {"C": c, "H": h, "N": n, "gflop_direct": round(gf, 1)}
         ref = F.conv2d(x[:2].double(), w.double(), None, 1, 1)
         # f32 MFMA / split-bf16 tile GEMMs at 32 (sx) and 64 (sx2) output channels per workgroup
-        for tag, sx, wide in (("", False, False), ("_sx", True, False), ("_sx2", True, True)):
+        for tag, sx, wide, onepos in (("", False, False, True), ("_sx", True, False, False), ("_sx1p", True, False, True),
+                                      ("_sx2", True, True, True)):
             Wg.USE_WIDE = wide
+            Wg.ONEPOS = onepos
             u = Wg.filter_transform(w, sx=sx)
             y = Wg.conv3x3_wino(x, w, u)
             row["relerr_vs_fp64" + tag] = float(((y[:2].double() - ref).norm() / ref.norm()).item())

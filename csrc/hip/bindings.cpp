@@ -88,6 +88,7 @@ PYBIND11_MODULE(_vodahip, m) {
   m.def("wino_f23_groups", &wino_f23_groups);
   m.def("wino_f23_fwd", &wino_f23_fwd);
   m.def("wino_f23_sx2_supported", &wino_f23_sx2_supported);
+  m.def("wino_f23_set_onepos", &wino_f23_set_onepos);
   m.def("wino_f23_groups2", &wino_f23_groups2);
   m.def("wino_f23_fwd2", &wino_f23_fwd2);
   m.def("stem_partial_rows", &stem_partial_rows);

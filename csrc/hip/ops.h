@@ -143,6 +143,7 @@ void wino_f23_filter(uintptr_t w, int64_t s0, int64_t s1, int64_t s2, int64_t s3
                      bool flip, bool sx, uintptr_t stream);
 int wino_f23_groups(int N, int H, int W, int C, int Co);
 bool wino_f23_sx2_supported(int C, int Co);
+void wino_f23_set_onepos(int on);
 int wino_f23_groups2(int N, int H, int W, int C, int Co);
 void wino_f23_fwd2(uintptr_t x, uintptr_t u, uintptr_t y, uintptr_t part, int N, int H, int W, int C, int Co, int G,
                    uintptr_t stream);

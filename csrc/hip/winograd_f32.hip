@@ -106,7 +106,10 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t wino_u_rsrc(const WinoArgs& a)
                                            __builtin_amdgcn_readfirstlane(int(int64_t(96) * a.C * a.Co)), 0x00020000);
 }
 
-template <bool SX>
+// ONEPOS (SX only): the split tile GEMMs one position at a time (V split of one row, its 6 MFMAs,
+// the next position's U prefetched: 12 + 12 registers instead of 24 + 24) -- the position-pair form
+// runs at 256 VGPRs with 116 bytes of scratch per lane
+template <bool SX, bool ONEPOS = false>
 __global__ __launch_bounds__(kWThreads, 2) void wino_f23_fwd_kernel(WinoArgs a) {
   __shared__ __attribute__((aligned(16))) float lds[16 * kWT * kWP];  // V chunk, then M exchange
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, lc = lane & 31, lh = lane >> 5;
@@ -243,6 +246,42 @@ __global__ __launch_bounds__(kWThreads, 2) void wino_f23_fwd_kernel(WinoArgs a) 
       } else if (blk + a.G < nblk) {
         tile_setup(blk + a.G);
         load_patch(0);
+      }
+      if constexpr (SX && ONEPOS) {
+        // ---- 8 sub-steps (16-channel half h, position j of the wave's four) x 6 products; the next
+        // sub-step's U (3 planes) loads during the current one's MFMAs
+        auto uload1 = [&](int q, uint4 (&dst)[3]) {
+          const int pos = 4 * wave + (q & 3), hh = q >> 2;
+#pragma unroll
+          for (int pl = 0; pl < 3; ++pl) {
+            const int so = __builtin_amdgcn_readfirstlane(
+                int(((int64_t(pos * 3 + pl) * (a.C / 8) + c0 / 8 + 2 * hh) * a.Co + co0) * 16));
+            const auto v = __builtin_amdgcn_raw_buffer_load_b128(ur, int(uvo), so, 0);
+            dst[pl] = make_uint4(v[0], v[1], v[2], v[3]);
+          }
+        };
+        auto sub = [&](int q, const uint4 (&u)[3]) {
+          const float* vr = lds + ((4 * wave + (q & 3)) * kWT + lc) * kWP + 16 * (q >> 2) + 8 * lh;
+          uint4 vh, vm, vl;
+          wsx_split8(*reinterpret_cast<const float4*>(vr), *reinterpret_cast<const float4*>(vr + 4), vh, vm, vl);
+          f32x16& r = acc[q & 3];
+          r = wsx_mfma(vm, u[1], r);
+          r = wsx_mfma(vh, u[2], r);
+          r = wsx_mfma(vl, u[0], r);
+          r = wsx_mfma(vh, u[1], r);
+          r = wsx_mfma(vm, u[0], r);
+          r = wsx_mfma(vh, u[0], r);
+        };
+        uint4 ua[3], ub[3];
+        uload1(0, ua);
+#pragma unroll
+        for (int q = 0; q < 8; q += 2) {
+          uload1(q + 1, ub);
+          sub(q, ua);
+          if (q + 2 < 8) uload1(q + 2, ua);
+          sub(q + 1, ub);
+        }
+        continue;
       }
       if constexpr (SX) {
         // ---- 4 steps x 2 positions x 6 products of 32x32x16 bf16; the next step's U loads meanwhile
@@ -675,6 +714,9 @@ __global__ __launch_bounds__(256) void wino_f23_filter_kernel(const float* __res
 
 }  // namespace
 
+int g_wino_onepos = 1;
+void wino_f23_set_onepos(int on) { g_wino_onepos = on ? 1 : 0; }
+
 bool wino_f23_supported(int C, int Co) { return C > 0 && Co > 0 && C % kWK == 0 && Co % kWN == 0; }
 
 void wino_f23_filter(uintptr_t w, int64_t s0, int64_t s1, int64_t s2, int64_t s3, uintptr_t u, int Co, int C,
@@ -723,7 +765,9 @@ void wino_f23_fwd(uintptr_t x, uintptr_t u, uintptr_t y, uintptr_t part, int N, 
              reinterpret_cast<float*>(part), N, H, W, C, Co, (H + 1) / 2, (W + 1) / 2, 0, G};
   a.T = int64_t(N) * a.th * a.tw;
   const dim3 grid(unsigned(G), unsigned(Co / kWN));
-  hipLaunchKernelGGL(sx ? wino_f23_fwd_kernel<true> : wino_f23_fwd_kernel<false>, grid, dim3(kWThreads), 0,
+  void (*kern)(WinoArgs) = sx ? (g_wino_onepos ? wino_f23_fwd_kernel<true, true> : wino_f23_fwd_kernel<true, false>)
+                              : wino_f23_fwd_kernel<false, false>;
+  hipLaunchKernelGGL(kern, grid, dim3(kWThreads), 0,
                      as_stream(stream), a);
   check_launch();
 }

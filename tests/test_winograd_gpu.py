@@ -10,12 +10,16 @@ from vodascheduler_amd.ops import winograd as Wg
 pytestmark = pytest.mark.gpu
 
 
-@pytest.fixture(params=[(False, False), (True, False), (True, True)], ids=["f32mfma", "bf16x3", "bf16x3-wide"])
+@pytest.fixture(params=[(False, False, True), (True, False, False), (True, False, True), (True, True, True)],
+                ids=["f32mfma", "bf16x3-pairs", "bf16x3", "bf16x3-wide"])
 def sx(request, monkeypatch):
     """The tile-GEMM paths: the f32 MFMA, the exact 3-way bf16 split (Wg.USE_SX) at 32 output
-    channels per workgroup, and the split at 64 (Wg.USE_WIDE, Cout % 64 == 0)."""
+    channels per workgroup (position pairs or one position at a time, Wg.ONEPOS), and the split at
+    64 (Wg.USE_WIDE, Cout % 64 == 0)."""
     monkeypatch.setattr(Wg, "USE_SX", request.param[0])
     monkeypatch.setattr(Wg, "USE_WIDE", request.param[1])
+    monkeypatch.setattr(Wg, "ONEPOS", request.param[2])
+    monkeypatch.setattr(Wg, "WIDE_MAX_C", 1 << 20)  # the wide kernel on every covered shape
     return request.param[0]
 
 

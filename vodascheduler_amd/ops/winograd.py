@@ -29,6 +29,10 @@ USE_SX = True
 # A/B, profiles/r6/ab_winograd_wide_resnet50_fp32.jsonl).
 USE_WIDE = True
 WIDE_MAX_C = 128
+# the 32-channel split kernel one Winograd position at a time (no scratch spills; the position-
+# pair form spills 116 bytes per lane at 256 VGPRs)
+ONEPOS = True
+_applied = {"onepos": None}
 
 
 def supported(x: torch.Tensor, w: torch.Tensor, stride: int = 1, padding: int = 1, flip: bool = False) -> bool:
@@ -77,6 +81,9 @@ def conv3x3_wino(x: torch.Tensor, w: torch.Tensor, u: torch.Tensor | None = None
                          device=x.device)
         holder.stats = (ws, G)
     y = torch.empty((n, co, h, wd), dtype=torch.float32, device=x.device, memory_format=torch.channels_last)
+    if _applied["onepos"] != ONEPOS:
+        hip.wino_f23_set_onepos(int(bool(ONEPOS)))
+        _applied["onepos"] = ONEPOS
     if wide:
         hip.wino_f23_fwd2(x.data_ptr(), u.data_ptr(), y.data_ptr(), N.ptr(ws), n, h, wd, c, co, G, N.stream_of(x))
     else:
