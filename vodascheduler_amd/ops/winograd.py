@@ -28,9 +28,11 @@ USE_SX = True
 # the pace (profiles/r6/winograd_sx2_layers.jsonl).  ResNet-50 fp32 step 60.90 -> 60.74 ms (same-box
 # A/B, profiles/r6/ab_winograd_wide_resnet50_fp32.jsonl).
 USE_WIDE = True
-WIDE_MAX_C = 128
+WIDE_MAX_C = 64  # 128 until the one-position form below: 272 (one-position) vs 295 us (wide) at C = 128
 # the 32-channel split kernel one Winograd position at a time (no scratch spills; the position-
-# pair form spills 116 bytes per lane at 256 VGPRs)
+# pair form spills 116 bytes per lane at 256 VGPRs): per ResNet-50 layer 354 vs 378 us (C = 64),
+# 272 vs 301 (128), 255 vs 272 (256), 306 vs 315 (512) (profiles/r6/winograd_onepos_layers.jsonl);
+# ResNet-50 fp32 step 58.59 -> 58.54 ms with WIDE_MAX_C = 128 (ab_winograd_onepos_resnet50_fp32.jsonl)
 ONEPOS = True
 _applied = {"onepos": None}
 
