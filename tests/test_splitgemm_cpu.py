@@ -59,3 +59,67 @@ def test_cpu_matmul_reference_and_layouts():
     assert SG._layout(w.t(), False) == (False, 32)
     assert SG._layout(w, False) == (True, 32)
     assert not SG.supported(x, w.t())  # CPU tensors never take the GPU kernel
+
+
+def test_choose_tiles_and_splits():
+    """The launch-shape rules from the round-6 sweeps (profiles/r6/splitgemm_t7_sweep.jsonl,
+    splitgemm_wgrad_splits.jsonl): 128 x 96 where it fills whole rounds of the 512 resident
+    workgroups, 7 / 12 splits for the BERT-base weight gradients, 128 x 128 elsewhere."""
+    assert SG.choose(8192, 2304, 768) == (7, 1)     # qkv forward: 1536 tiles of 128 x 96
+    assert SG.choose(8192, 768, 768) == (7, 1)      # o forward / input gradient: 512 tiles
+    assert SG.choose(8192, 768, 2304) == (7, 1)     # qkv input gradient
+    assert SG.choose(8192, 3072, 768) == (0, 1)     # fc1 forward: 1536 tiles of 128 x 128 already
+    assert SG.choose(8192, 768, 3072) == (0, 2)     # long K: 128 x 128 with split-K 2
+    assert SG.choose(768, 2304, 8192) == (0, 7)     # weight gradients
+    assert SG.choose(3072, 768, 8192) == (0, 7)
+    assert SG.choose(768, 768, 8192) == (0, 12)
+    old = SG.USE_T7
+    try:
+        SG.USE_T7 = False
+        assert SG.choose(8192, 2304, 768) == (0, 1)
+    finally:
+        SG.USE_T7 = old
+
+
+def test_thin_tiles_and_wgrad_splits():
+    assert SG.thin_tile(64, 256) == 5 and SG.thin_tile(256, 64) == 6 and SG.thin_tile(128, 256) == 0
+    # ~target workgroups, >= 256 pixels per split
+    assert SG.conv_wgrad_splits(64, 256, 802816, 5, 512) == 512
+    assert SG.conv_wgrad_splits(512, 128, 200704, 0, 512) == 128
+    assert SG.conv_wgrad_splits(128, 1152, 200704) == 113      # 3x3: ~1024 workgroups
+    assert SG.conv_wgrad_splits(2048, 512, 12544, 0, 512) == 8
+
+
+def test_conv_cpu_references():
+    """CPU tensors take the PyTorch reference of the implicit-GEMM convolutions."""
+    torch.manual_seed(2)
+    x = torch.randn(2, 16, 9, 9)
+    w = torch.randn(8, 16, 3, 3)
+    torch.testing.assert_close(SG.conv_fwd(x, w, 2, 1), torch.nn.functional.conv2d(x, w, None, 2, 1))
+    dy = torch.randn(2, 8, 5, 5)
+    ref = torch.nn.grad.conv2d_input((2, 16, 9, 9), w, dy, stride=2, padding=1)
+    torch.testing.assert_close(SG.conv_dgrad_s2(dy, w, (2, 16, 9, 9)), ref)
+
+
+def test_polyphase_taps_cover_the_stride2_input_gradient():
+    """Host model of conv_dgrad_s2's decomposition: the four parity classes with their 1 / 2 / 2
+    / 4 taps (kh = 1 for even rows; kh = 2, 0 at dY rows i, i + 1 for odd rows) reproduce the
+    stride-2 pad-1 input gradient exactly in fp64."""
+    torch.manual_seed(3)
+    n, cin, cout, H = 2, 4, 3, 9
+    w = torch.randn(cout, cin, 3, 3, dtype=torch.float64)
+    ho = (H - 1) // 2 + 1
+    dy = torch.randn(n, cout, ho, ho, dtype=torch.float64)
+    ref = torch.nn.grad.conv2d_input((n, cin, H, H), w, dy, stride=2, padding=1)
+    dx = torch.zeros_like(ref)
+    dyp = torch.nn.functional.pad(dy, (0, 1, 0, 1))  # zero past the map
+    for ph in (0, 1):
+        for pw in (0, 1):
+            hc, wc = (H - ph + 1) // 2, (H - pw + 1) // 2
+            acc = torch.zeros(n, cin, hc, wc, dtype=torch.float64)
+            for th, kh in enumerate(SG._S2_TAPS[ph]):
+                for tw, kw in enumerate(SG._S2_TAPS[pw]):
+                    g = dyp[:, :, th:th + hc, tw:tw + wc]
+                    acc += torch.einsum("nohw,oi->nihw", g, w[:, :, kh, kw])
+            dx[:, :, ph::2, pw::2] = acc
+    torch.testing.assert_close(dx, ref)
