@@ -281,6 +281,7 @@ void sgemm_conv_wgrad_f32(uintptr_t dy, uintptr_t x, uintptr_t gw, int n, int H,
                           int64_t ws_floats, uintptr_t stream);
 void sgemm_f32(uintptr_t a, int64_t lda, bool a_kmajor, uintptr_t b, int64_t ldb, bool b_kmajor, uintptr_t c,
                int64_t ldc, int M, int N, int K, bool beta, uintptr_t bias, int epi, uintptr_t aux, int64_t ldaux,
-               int tile, int splits, int variant, uintptr_t ws, int64_t ws_floats, uintptr_t stream);
+               int tile, int splits, int variant, uintptr_t ws, int64_t ws_floats, uintptr_t stream,
+               uintptr_t bsum = 0);
 
 }  // namespace voda

@@ -64,7 +64,8 @@ struct SxArgs {
   float* c; int64_t ldc;
   const float* bias;            // [N] or null
   float* aux; int64_t ldaux;    // GELU: h = acc + bias written here (C gets gelu(h)); DGELU: h read
-  float* ws;                    // split-K slabs [S][M][N]
+  float* ws;                    // split-K slabs [S][M][N], then (bsum) the row-sum slabs [S][M]
+  float* bsum;                  // optional: bsum[m] += sum_k A(m, k) (a Linear's bias gradient from dY^T)
   int M, N, K, S, kps;          // kps: k per split (multiple of 16)
   int tiles_n, tiles;
   int beta, epi;
@@ -156,6 +157,7 @@ struct SxOperand {
   int woff[kPer];         // LDS byte offset of the first float4's split (plane 0)
   int woff2[kPer];        // ... of the second
   bool on[kPer];
+  bool rok[kPer];         // K-major: the unit's 4 rows are inside the matrix (not clamped duplicates)
 
   __device__ __forceinline__ void init(const float* base, int64_t ld, int row0, int rows, int k0, int t) {
 #pragma unroll
@@ -173,6 +175,7 @@ struct SxOperand {
       } else {
         const int cg = uu % (R / 4), kp = uu / (R / 4);
         const int gc = min(row0 + 4 * cg, rows - 4);
+        rok[i] = on[i] && row0 + 4 * cg < rows;
         g[i] = base + int64_t(k0 + kp) * ld + gc;
         g2[i] = g[i] + int64_t(8) * ld;
         woff[i] = sx_km_off<R>(kp, 4 * cg);
@@ -193,6 +196,17 @@ struct SxOperand {
       const int64_t d = advance ? step : 0;
       g[i] += d;
       g2[i] += d;
+    }
+  }
+
+  // K-major operands: this thread's 4 rows summed over the stage's two k-rows (kPer == 1)
+  __device__ __forceinline__ void rowsum(const SxStage<R, KM, T>& s, float4& acc) const {
+    static_assert(KM && kPer == 1, "row sums: K-major operand, one unit per thread");
+    if (rok[0]) {
+      acc.x += s.v[0][0].x + s.v[0][1].x;
+      acc.y += s.v[0][0].y + s.v[0][1].y;
+      acc.z += s.v[0][0].z + s.v[0][1].z;
+      acc.w += s.v[0][0].w + s.v[0][1].w;
     }
   }
 
@@ -552,8 +566,15 @@ __global__ __launch_bounds__((BM / (32 * WMT)) * (BN / (32 * WNT)) * 64, MINW) v
         for (int j = 0; j < WNT; ++j) acc[i][j] = sx_mfma(fa[i][0], fb[j][0], acc[i][j]);
     }
   };
+  // fused row sums of A (a Linear's bias gradient from dY^T): the workgroups of column tile 0
+  constexpr bool kRowSum = AKM && !CONVA && SxOperand<BM, AKM, T>::kPer == 1;
+  const bool do_rs = kRowSum && __builtin_amdgcn_readfirstlane(p.bsum != nullptr && n0 == 0);
+  float4 rs = make_float4(0.f, 0.f, 0.f, 0.f);
   auto write = [&](const StA& sa, const StB& sb, int buf) {
     uint8_t* A = smem + buf * kBuf;
+    if constexpr (kRowSum) {
+      if (do_rs) opa.rowsum(sa, rs);
+    }
     opa.write(sa, A, smem + 2 * kBuf);
     opb.write(sb, A + kImgA, smem + 2 * kBuf);
   };
@@ -611,6 +632,34 @@ __global__ __launch_bounds__((BM / (32 * WMT)) * (BN / (32 * WNT)) * 64, MINW) v
       compute(st & 1);
       if (st + 1 < nst) write(sa0, sb0, (st + 1) & 1);
       __syncthreads();
+    }
+  }
+
+  if constexpr (kRowSum) {
+    if (do_rs) {  // the R/4 row groups' partials over the k-row slots, through LDS (loop ended in a barrier)
+      constexpr int kGroups = BM / 4, kSlots = T / kGroups;
+      float4* red = reinterpret_cast<float4*>(smem);
+      red[t] = rs;
+      __syncthreads();
+      if (t < kGroups) {
+        float4 v = red[t];
+#pragma unroll
+        for (int q = 1; q < kSlots; ++q) {
+          const float4 w = red[q * kGroups + t];
+          v.x += w.x; v.y += w.y; v.z += w.z; v.w += w.w;
+        }
+        const int row = m0 + 4 * t;
+        if (row < p.M) {
+          if (p.S > 1) {
+            *reinterpret_cast<float4*>(p.ws + int64_t(p.S) * p.M * p.N + int64_t(split) * p.M + row) = v;
+          } else {
+            float4* b = reinterpret_cast<float4*>(p.bsum + row);
+            float4 o = *b;
+            o.x += v.x; o.y += v.y; o.z += v.z; o.w += v.w;
+            *b = o;
+          }
+        }
+      }
     }
   }
 
@@ -845,6 +894,21 @@ __global__ __launch_bounds__(64 * GR) void sgemm_reduce_kernel(SxArgs p) {
   cp[3] = sx_finish(p, row, col + 3, t.w);
 }
 
+// bsum[m] += sum over the S row-sum slabs (the fused bias gradient of a split-K weight gradient)
+__global__ __launch_bounds__(256) void sgemm_rowsum_reduce_kernel(SxArgs p) {
+  const int m = blockIdx.x * 256 + threadIdx.x;
+  if (m >= p.M) return;
+  const float* w = p.ws + int64_t(p.S) * p.M * p.N + m;
+  float s0 = 0.f, s1 = 0.f;
+  int k = 0;
+  for (; k + 1 < p.S; k += 2) {
+    s0 += w[int64_t(k) * p.M];
+    s1 += w[int64_t(k + 1) * p.M];
+  }
+  if (k < p.S) s0 += w[int64_t(k) * p.M];
+  p.bsum[m] += s0 + s1;
+}
+
 // slab groups per float4 column: enough blocks for ~4 waves per SIMD chip-wide, >= 8 slabs per thread
 int g_sx_reduce_groups = -1;  // < 0: automatic; else fixed (A/B)
 
@@ -895,7 +959,7 @@ void sgemm_conv_wgrad_set_ws(int mode) { g_sx_conv_ws = mode < 0 || mode > 2 ? 0
 void sgemm_set_reduce_groups(int g) { g_sx_reduce_groups = (g == 1 || g == 2 || g == 4 || g == 8 || g == 16) ? g : -1; }
 
 int64_t sgemm_f32_workspace_floats(int M, int N, int splits) {
-  return splits > 1 ? int64_t(splits) * M * N : 0;
+  return splits > 1 ? int64_t(splits) * M * N + int64_t(splits) * M : 0;  // + the row-sum slabs
 }
 
 // variant: 0 = 6 products, dual accumulators, one register stage set (the shipped math);
@@ -909,8 +973,10 @@ int64_t sgemm_f32_workspace_floats(int M, int N, int splits) {
 // the next stage's fragments during the current stage's MFMAs (one accumulator).  Variants 1-7: 128 x 128 only.
 void sgemm_f32(uintptr_t a, int64_t lda, bool a_kmajor, uintptr_t b, int64_t ldb, bool b_kmajor, uintptr_t c,
                int64_t ldc, int M, int N, int K, bool beta, uintptr_t bias, int epi, uintptr_t aux, int64_t ldaux,
-               int tile, int splits, int variant, uintptr_t ws, int64_t ws_floats, uintptr_t stream) {
+               int tile, int splits, int variant, uintptr_t ws, int64_t ws_floats, uintptr_t stream, uintptr_t bsum) {
   VODA_CHECK(M > 0 && N > 0 && K > 0, "sgemm_f32: empty GEMM");
+  VODA_CHECK(bsum == 0 || (a_kmajor && (tile == 0 || tile == 7) && variant == 0 && bsum % 16 == 0),
+             "sgemm_f32: fused row sums need a K-major A on tile 0 / 7, variant 0, 16-B aligned");
   VODA_CHECK(K % kSxBK == 0, "sgemm_f32: K must be a multiple of 16");
   VODA_CHECK(M % 4 == 0 && N % 4 == 0, "sgemm_f32: M and N must be multiples of 4");
   VODA_CHECK(tile >= 0 && tile < 8, "sgemm_f32: bad tile id");
@@ -937,6 +1003,7 @@ void sgemm_f32(uintptr_t a, int64_t lda, bool a_kmajor, uintptr_t b, int64_t ldb
   p.beta = beta ? 1 : 0;
   p.epi = epi;
   p.stagger = g_sx_stagger;
+  p.bsum = reinterpret_cast<float*>(bsum);
   if (S > 1) {
     VODA_CHECK(ws != 0 && ws_floats >= sgemm_f32_workspace_floats(M, N, S), "sgemm_f32: split-K workspace too small");
     VODA_CHECK(c % 16 == 0 && ldc % 4 == 0, "sgemm_f32: split-K output needs 16-B rows");
@@ -972,7 +1039,13 @@ void sgemm_f32(uintptr_t a, int64_t lda, bool a_kmajor, uintptr_t b, int64_t ldb
     sx_launch_tile<256, 128, 6, true, false, 1, 4>(p, a_kmajor, b_kmajor, grid, st);
   }
   check_launch();
-  if (S > 1) sx_reduce(p, st);
+  if (S > 1) {
+    sx_reduce(p, st);
+    if (bsum) {
+      hipLaunchKernelGGL(sgemm_rowsum_reduce_kernel, dim3(unsigned((M + 255) / 256)), dim3(256), 0, st, p);
+      check_launch();
+    }
+  }
 }
 
 // Convolution weight gradient dW[co][kh][kw][ci] (+)= sum over output pixels of dY[pix][co] *

@@ -231,3 +231,25 @@ def test_conv_dgrad_stride2_polyphase_matches_fp64(n, cin, cout, hw):
     assert dx.is_contiguous(memory_format=cl)
     err = ((dx.double() - ref).abs() / (bound + 1e-30)).max().item()
     assert err < 2e-7, err
+
+
+@pytest.mark.parametrize("M,K,N,splits,tile", [(768, 8192, 768, 12, 0), (2304, 8192, 768, 7, 0), (260, 1024, 196, 1, 0),
+                                               (256, 4096, 192, 3, 7), (128, 64, 128, 1, 0)])
+def test_fused_row_sums(M, K, N, splits, tile):
+    """row_sums += a.sum(1) from the A staging of a weight-gradient GEMM (K-major a = dY^T), with
+    and without split-K, ragged M, next to the accumulated product."""
+    torch.manual_seed(M + K)
+    dy = torch.randn(K, M, device=DEV)
+    x = torch.randn(K, N, device=DEV)
+    a = dy.t()
+    c0 = torch.randn(M, N, device=DEV)
+    c = c0.clone()
+    rs0 = torch.randn(M, device=DEV)
+    rs = rs0.clone()
+    assert SG.row_sums_ok(a, rs, tile, 0)
+    SG.matmul(a, x, out=c, accumulate=True, tile=tile, splits=splits, row_sums=rs)
+    ref = a.double() @ x.double() + c0.double()
+    assert ((c.double() - ref).abs() / (_bound(a, x) + 1)).max().item() < 2e-7
+    rref = dy.double().sum(0) + rs0.double()
+    rbound = dy.double().abs().sum(0) + 1
+    assert ((rs.double() - rref).abs() / rbound).max().item() < 1e-6

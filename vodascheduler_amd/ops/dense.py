@@ -119,7 +119,16 @@ def linear_weight_grads(dy2: torch.Tensor, x2: torch.Tensor, weight: torch.Tenso
         if _direct(weight):
             gw = flat_grad(weight)
             if gw.dtype == torch.float32 and SG.supported(dy2.t(), x2):
-                SG.matmul(dy2.t(), x2, out=gw, accumulate=True)  # fp32: split-bf16 MFMA, beta = 1
+                # fp32: split-bf16 MFMA, beta = 1; the bias gradient (column sums of dY) from the same
+                # launch's A staging when the layout allows
+                gb = flat_grad(bias) if need_b and _direct(bias) else None
+                tile = SG.choose(dy2.shape[1], x2.shape[1], dy2.shape[0])[0]
+                if gb is not None and SG.row_sums_ok(dy2.t(), gb, tile, SG.DEFAULT_VARIANT):
+                    SG.matmul(dy2.t(), x2, out=gw, accumulate=True, row_sums=gb)
+                    _ready(weight)
+                    _ready(bias)
+                    return None, None
+                SG.matmul(dy2.t(), x2, out=gw, accumulate=True)
             elif gw.dtype == dy2.dtype:
                 gw.addmm_(dy2.t(), x2)
             else:  # fp32 flat gradient of a bf16 weight (cast first: see utils/flat.FOLD_CAST)

@@ -53,6 +53,9 @@ CONV_WGRAD_WS = 0
 # split-K reduce: slab groups per float4 column (-1 automatic: ~4096 blocks-worth of groups, >= 16
 # slabs per group; 1 = one thread per column, the round-5 form)
 USE_T7 = True  # the 128 x 96 tile in ``choose`` (A/B switch)
+# a Linear's bias gradient summed in the weight-gradient GEMM's A staging (matmul(row_sums=...))
+# instead of a separate column-sum pass over dY (A/B switch)
+USE_FUSED_ROW_SUMS = True
 REDUCE_GROUPS = -1
 REDUCE_GROUPS_AUTO = True  # False: one group (A/B switch)
 _applied = {"reduce_groups": None}
@@ -180,13 +183,18 @@ def _workspace(device: torch.device, floats: int) -> torch.Tensor:
 
 def matmul(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor | None = None, accumulate: bool = False,
            bias: torch.Tensor | None = None, epi: int = EPI_NONE, aux: torch.Tensor | None = None,
-           tile: int | None = None, splits: int | None = None, variant: int | None = None) -> torch.Tensor:
+           tile: int | None = None, splits: int | None = None, variant: int | None = None,
+           row_sums: torch.Tensor | None = None) -> torch.Tensor:
     """``out (+)= a @ b (+ bias)`` on the split kernel; epi GELU writes the pre-activation
-    into ``aux`` and gelu of it into ``out``, epi DGELU multiplies by gelu'(aux).  Callers
-    check ``supported`` (CPU tensors get the PyTorch reference)."""
+    into ``aux`` and gelu of it into ``out``, epi DGELU multiplies by gelu'(aux).  ``row_sums``
+    (fp32 [M], 16-B aligned; K-major ``a`` only, see ``row_sums_ok``): ``row_sums += a.sum(1)``
+    from the A staging of the same launch (a Linear's bias gradient next to its weight gradient
+    dW = dY^T X).  Callers check ``supported`` (CPU tensors get the PyTorch reference)."""
     M, K = a.shape
     Nn = b.shape[1]
     if not a.is_cuda:
+        if row_sums is not None:
+            row_sums.add_(a.float().sum(1))
         y = a.float() @ b.float()
         if accumulate and out is not None:
             y = y + out
@@ -216,6 +224,8 @@ def matmul(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor | None = None, ac
     t0, s0 = choose(M, Nn, K, variant)
     tile = t0 if tile is None else tile
     splits = s0 if splits is None else splits
+    if row_sums is not None and not row_sums_ok(a, row_sums, tile, variant):
+        raise ValueError("splitgemm.matmul: row_sums need a K-major a, tile 0 / 7, variant 0 and an aligned fp32 [M]")
     h = N.hip()
     _sync_knobs(h)
     ws_floats = h.sgemm_f32_workspace_floats(M, Nn, splits)
@@ -230,8 +240,21 @@ def matmul(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor | None = None, ac
     h.sgemm_f32(a.data_ptr(), la[1], la[0], b.data_ptr(), lb[1], lb[0], out.data_ptr(), out.stride(0), M, Nn, K,
                 bool(accumulate), bias.data_ptr() if bias is not None else 0, int(epi),
                 aux.data_ptr() if aux is not None else 0, ld_aux, int(tile), int(splits), int(variant),
-                ws.data_ptr() if ws is not None else 0, ws.numel() if ws is not None else 0, N.stream_of(a))
+                ws.data_ptr() if ws is not None else 0, ws.numel() if ws is not None else 0, N.stream_of(a),
+                row_sums.data_ptr() if row_sums is not None else 0)
     return out
+
+
+def row_sums_ok(a: torch.Tensor, row_sums: torch.Tensor, tile: int, variant: int) -> bool:
+    """Can ``matmul`` fuse ``row_sums += a.sum(1)`` on this launch shape?  K-major a (a weight
+    gradient's dY^T), tile 0 or 7, math variant 0, a contiguous 16-byte-aligned fp32 [M] target."""
+    if not USE_FUSED_ROW_SUMS or not a.is_cuda:
+        return False
+    la = _layout(a, True)
+    M = a.shape[0]
+    return (la is not None and la[0] and tile in (0, 7) and variant == 0 and row_sums.dtype == torch.float32
+            and row_sums.is_cuda and row_sums.dim() == 1 and row_sums.numel() == M and row_sums.is_contiguous()
+            and row_sums.data_ptr() % 16 == 0)
 
 
 def linear(x: torch.Tensor, w: torch.Tensor, bias: torch.Tensor | None = None) -> torch.Tensor:
