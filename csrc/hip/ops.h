@@ -278,7 +278,7 @@ void sgemm_conv_dgrad_s2_class(uintptr_t dy, uintptr_t wc, uintptr_t dx, int n, 
                                int Cin, int ph, int pw, uintptr_t stream);
 void sgemm_conv_wgrad_f32(uintptr_t dy, uintptr_t x, uintptr_t gw, int n, int H, int W, int Cin, int Ho, int Wo,
                           int Cout, int KH, int KW, int stride, int pad, int splits, bool accumulate, uintptr_t ws,
-                          int64_t ws_floats, uintptr_t stream);
+                          int64_t ws_floats, uintptr_t stream, int tile);
 void sgemm_f32(uintptr_t a, int64_t lda, bool a_kmajor, uintptr_t b, int64_t ldb, bool b_kmajor, uintptr_t c,
                int64_t ldc, int M, int N, int K, bool beta, uintptr_t bias, int epi, uintptr_t aux, int64_t ldaux,
                int tile, int splits, int variant, uintptr_t ws, int64_t ws_floats, uintptr_t stream,

@@ -84,7 +84,7 @@ int g_sx_stagger = 1;
 int g_sx_conv_ws = 0;  // convolution weight gradient kernel: 0 one-role, 1 / 2 wave-specialised (lead 1 / 2)
 
 // K-major images of R = 96 columns use the R = 128 layout (192-byte k-rows padded to 256 B)
-template <int R> struct SxKmPitch { static constexpr int kR = R == 96 ? 128 : R; };
+template <int R> struct SxKmPitch { static constexpr int kR = R == 96 ? 128 : R == 192 ? 256 : R; };
 
 template <int R, bool KM> struct SxImg {
   static constexpr int kBytes = KM ? 3 * kSxBK * SxKmPitch<R>::kR * 2 : R * kSxKcPitch;
@@ -97,6 +97,8 @@ template <int R>
 __device__ __forceinline__ int sx_km_off(int k, int col) {
   if constexpr (R == 96) {
     return sx_km_off<128>(k, col);
+  } else if constexpr (R == 192) {
+    return sx_km_off<256>(k, col);
   } else if constexpr (R == 64) {
     // 128-B k-rows: k-rows 2j and 2j + 1 side by side form row j of a [8][128] image that takes
     // the 256-B swizzle (a bijection, so staging writes and fragment reads agree)
@@ -1055,7 +1057,9 @@ void sgemm_f32(uintptr_t a, int64_t lda, bool a_kmajor, uintptr_t b, int64_t ldb
 // igemm_wrw for the 3x3 layers with C >= 128, including the stride-2 ones).
 void sgemm_conv_wgrad_f32(uintptr_t dy, uintptr_t x, uintptr_t gw, int n, int H, int W, int Cin, int Ho, int Wo,
                           int Cout, int KH, int KW, int stride, int pad, int splits, bool accumulate, uintptr_t ws,
-                          int64_t ws_floats, uintptr_t stream) {
+                          int64_t ws_floats, uintptr_t stream, int tile) {
+  VODA_CHECK(tile == 0 || tile == 8, "sgemm_conv_wgrad_f32: tile 0 (128 x 128) or 8 (64 x 192)");
+  const int BM = tile == 8 ? 64 : 128, BN = tile == 8 ? 192 : 128;
   const int64_t K = int64_t(n) * Ho * Wo;
   const int N = KH * KW * Cin;
   VODA_CHECK(n > 0 && Cout > 0 && Cin > 0 && K > 0 && K < (int64_t(1) << 31), "sgemm_conv_wgrad_f32: bad shape");
@@ -1076,8 +1080,8 @@ void sgemm_conv_wgrad_f32(uintptr_t dy, uintptr_t x, uintptr_t gw, int n, int H,
   p.kps = ((kst + S - 1) / S) * kSxBK;
   S = int((K + p.kps - 1) / p.kps);
   p.S = S;
-  p.tiles_n = (N + 127) / 128;
-  p.tiles = ((Cout + 127) / 128) * p.tiles_n;
+  p.tiles_n = (N + BN - 1) / BN;
+  p.tiles = ((Cout + BM - 1) / BM) * p.tiles_n;
   p.beta = accumulate ? 1 : 0;
   p.stagger = g_sx_stagger;
   if (S > 1) {
@@ -1088,7 +1092,10 @@ void sgemm_conv_wgrad_f32(uintptr_t dy, uintptr_t x, uintptr_t gw, int n, int H,
   const int64_t nwg = int64_t(p.tiles) * S;
   VODA_CHECK(nwg < (int64_t(1) << 31), "sgemm_conv_wgrad_f32: grid too large");
   hipStream_t st = as_stream(stream);
-  if (g_sx_conv_ws == 1)
+  if (tile == 8)  // 64 x 192: 64-channel layers (N = 9 x 64 = 3 tiles exactly), 3 waves of 64 x 64
+    hipLaunchKernelGGL((sgemm_bf16x3_kernel<64, 192, true, true, 6, true, false, 2, 2, true>), dim3(unsigned(nwg)),
+                       dim3(192), 0, st, p);
+  else if (g_sx_conv_ws == 1)
     hipLaunchKernelGGL((sgemm_ws_kernel<true, true, true, 1, 2>), dim3(unsigned(nwg)), dim3(512), 0, st, p);
   else if (g_sx_conv_ws == 2)
     hipLaunchKernelGGL((sgemm_ws_kernel<true, true, true, 2, 2>), dim3(unsigned(nwg)), dim3(512), 0, st, p);

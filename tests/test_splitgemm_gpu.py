@@ -167,7 +167,8 @@ def test_variants_error_ordering():
 
 
 @pytest.mark.parametrize("n,cin,cout,hw,stride", [(2, 128, 128, 16, 1), (3, 64, 132, 8, 1), (16, 128, 128, 7, 1),
-                                                  (2, 128, 256, 16, 2), (4, 256, 128, 7, 2)])
+                                                  (2, 128, 256, 16, 2), (4, 256, 128, 7, 2), (2, 64, 64, 16, 1),
+                                                  (4, 128, 64, 8, 1), (3, 64, 64, 7, 2)])
 @pytest.mark.parametrize("ws", [0, 1])
 def test_conv_wgrad_implicit_gemm_matches_fp64(n, cin, cout, hw, stride, ws):
     """dW (+)= conv weight gradient of a 3x3 pad-1 convolution (NHWC gather per tap in the

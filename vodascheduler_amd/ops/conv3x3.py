@@ -41,6 +41,10 @@ USE_SPLIT_WGRAD_F32 = True
 # implicit GEMM on the split-bf16 MFMA kernel (ops/splitgemm.conv_fwd, input gathered per tap while
 # staged) instead of MIOpen's igemm_fwd (A/B switch)
 USE_SPLIT_CONV_FWD = True
+# fp32 weight gradients of the 64-channel 3x3 layers (ResNet stage 1) on the split GEMM with 64 x 192
+# tiles instead of the f32-MFMA c64 kernel.  Off: the step lost 60.94 -> 61.32 ms (same-box A/B,
+# profiles/r6/ab_split_wgrad_c64_resnet50_fp32.jsonl); kept tested as the alternative
+USE_SPLIT_WGRAD_C64 = False
 # ... and their input gradients as four polyphase implicit GEMMs (ops/splitgemm.conv_dgrad_s2)
 # instead of MIOpen's igemm_bwd + zero fill.  Off: the parity classes with 1-2 taps reduce over
 # only 128-512 k (8-32 stages per tile), and the step lost 58.95 -> 59.12 ms (same-box A/B,
@@ -221,7 +225,14 @@ class _ConvKxKFn(torch.autograd.Function):
             dx = torch.ops.aten.convolution_backward(dy, x, weight, None, [stride, stride], [padding, padding],
                                                      [1, 1], False, [0, 0], 1, [True, False, False])[0]
         dw = None
-        if ctx.needs_input_grad[1] and not kernel_wgrad and c64_ok(dy, x, weight, stride, padding):
+        gw64 = flat_grad(weight) if (ctx.needs_input_grad[1] and USE_SPLIT_WGRAD_C64 and x.dtype == torch.float32
+                                     and weight.shape[0] == 64 and _direct(weight)) else None
+        if gw64 is not None and SG.conv_wgrad_ok(dy, x, gw64):
+            # fp32 64-channel layers: the implicit GEMM on the split-bf16 MFMA, 64 x 192 tiles
+            SG.conv_wgrad_(dy, x, gw64, stride, padding)
+            _ready(weight)
+            dw = None
+        elif ctx.needs_input_grad[1] and not kernel_wgrad and c64_ok(dy, x, weight, stride, padding):
             dw = conv_c64_wgrad(dy, x, weight)
         elif ctx.needs_input_grad[1]:
             gw = flat_grad(weight) if _direct(weight) else None

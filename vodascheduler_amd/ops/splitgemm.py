@@ -25,7 +25,7 @@ import torch
 from . import _native as N
 
 EPI_NONE, EPI_GELU, EPI_DGELU = 0, 1, 2
-TILES = {0: (128, 128), 1: (256, 128), 2: (128, 256), 5: (64, 256), 6: (256, 64), 7: (128, 96)}
+TILES = {0: (128, 128), 1: (256, 128), 2: (128, 256), 5: (64, 256), 6: (256, 64), 7: (128, 96), 8: (64, 192)}
 
 
 def thin_tile(M: int, Nn: int) -> int:
@@ -295,8 +295,14 @@ def conv_wgrad_splits(cout: int, n_cols: int, pixels: int, tile: int = 0, target
     return max(1, min(max(1, target // tiles), pixels // 256))
 
 
+def conv_wgrad_tile(cout: int, n_cols: int) -> int:
+    """Tile of a convolution weight gradient [Cout][KH*KW*Cin]: 64 x 192 for the 64-channel 3x3
+    layers (576 columns = 3 tiles exactly), 128 x 128 otherwise."""
+    return 8 if cout == 64 and n_cols % 192 == 0 else 0
+
+
 def conv_wgrad_(dy: torch.Tensor, x: torch.Tensor, gw: torch.Tensor, stride: int, padding: int,
-                accumulate: bool = True, splits: int | None = None) -> None:
+                accumulate: bool = True, splits: int | None = None, tile: int | None = None) -> None:
     """``gw (+)= dW`` of a convolution on the split-bf16 MFMA kernel (callers check
     ``conv_wgrad_ok``); CPU tensors get the fp32 reference."""
     if not dy.is_cuda:
@@ -306,7 +312,8 @@ def conv_wgrad_(dy: torch.Tensor, x: torch.Tensor, gw: torch.Tensor, stride: int
     n, cin, H, W = x.shape
     cout, _, kh, kw = gw.shape
     ho, wo = dy.shape[2], dy.shape[3]
-    s = conv_wgrad_splits(cout, kh * kw * cin, n * ho * wo) if splits is None else splits
+    tile = conv_wgrad_tile(cout, kh * kw * cin) if tile is None else tile
+    s = conv_wgrad_splits(cout, kh * kw * cin, n * ho * wo, tile) if splits is None else splits
     h = N.hip()
     _sync_knobs(h)
     h.sgemm_conv_wgrad_set_ws(CONV_WGRAD_WS)
@@ -314,7 +321,7 @@ def conv_wgrad_(dy: torch.Tensor, x: torch.Tensor, gw: torch.Tensor, stride: int
     ws = _workspace(dy.device, ws_floats) if ws_floats else None
     h.sgemm_conv_wgrad_f32(dy.data_ptr(), x.data_ptr(), gw.data_ptr(), n, H, W, cin, ho, wo, cout, kh, kw,
                            int(stride), int(padding), s, bool(accumulate), ws.data_ptr() if ws is not None else 0,
-                           ws.numel() if ws is not None else 0, N.stream_of(dy))
+                           ws.numel() if ws is not None else 0, N.stream_of(dy), int(tile))
 
 
 def conv_fwd_ok(x: torch.Tensor, w: torch.Tensor) -> bool:
