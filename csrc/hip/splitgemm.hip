@@ -70,6 +70,7 @@ struct SxArgs {
   int tiles_n, tiles;
   int beta, epi;
   int stagger;                  // 1: odd workgroups at issue priority 1
+  int wmap;                     // K-contiguous staging unit -> row map (sx_kc_unit)
   // implicit-GEMM convolution weight gradient (B operand in CONV mode): B(n, k) = X[img][ho*cs +
   // kh - cpad][wo*cs + kw - cpad][ci] for n = (kh*ckw + kw)*cin + ci and output pixel
   // k = (img, ho, wo); zero outside the image.  X is NHWC [cn][ch][cw][cin].
@@ -81,6 +82,7 @@ struct SxArgs {
 };
 
 int g_sx_stagger = 1;
+int g_sx_wmap = 1;  // conflict-free K-contiguous staging writes (sx_kc_unit)
 int g_sx_conv_ws = 0;  // convolution weight gradient kernel: 0 one-role, 1 / 2 wave-specialised (lead 1 / 2)
 
 // K-major images of R = 96 columns use the R = 128 layout (192-byte k-rows padded to 256 B)
@@ -106,6 +108,22 @@ __device__ __forceinline__ int sx_km_off(int k, int col) {
   } else {
     const int ch = col >> 3;
     return k * (2 * R) + ((ch & ~15) << 4) + (((ch & 15) ^ (((k & 3) << 2) | ((k >> 2) & 3))) << 4) + ((col & 4) << 1);
+  }
+}
+
+// K-contiguous staging: unit u -> (row r, 4-float chunk q).  Lanes 4a..4a+3 of a wave read one
+// row's 64 contiguous bytes either way.  wmap 0: r = u >> 2 (16 consecutive rows per wave); the
+// three-plane 8-B LDS writes (ds_write_b64: 16-lane groups, bank = dword mod 32, row pitch 28
+// dwords) then collide 2-way inside every group (rows 0 and 3 of a group share banks 0-3).
+// wmap 1: a 16-lane group takes rows of one parity, 2 apart ({0, 2, 4, 6}, {1, 3, 5, 7}, ...),
+// whose bank shifts {0, 24, 16, 8} tile the 32 banks exactly: conflict-free writes.
+__device__ __forceinline__ void sx_kc_unit(int u, bool wmap, int& r, int& q) {
+  q = u & 3;
+  if (!wmap) {
+    r = u >> 2;
+  } else {
+    const int l = u & 63, g = l >> 4, a = (l >> 2) & 3;
+    r = 16 * (u >> 6) + 8 * (g >> 1) + 2 * a + (g & 1);
   }
 }
 
@@ -161,14 +179,16 @@ struct SxOperand {
   bool on[kPer];
   bool rok[kPer];         // K-major: the unit's 4 rows are inside the matrix (not clamped duplicates)
 
-  __device__ __forceinline__ void init(const float* base, int64_t ld, int row0, int rows, int k0, int t) {
+  __device__ __forceinline__ void init(const float* base, int64_t ld, int row0, int rows, int k0, int t,
+                                       bool wmap = false) {
 #pragma unroll
     for (int i = 0; i < kPer; ++i) {
       const int u = t + i * T;
       on[i] = (kUnits % T == 0) || u < kUnits;
       const int uu = on[i] ? u : 0;
       if (!KM) {
-        const int q = uu & 3, r = uu >> 2;
+        int q, r;
+        sx_kc_unit(uu, wmap && (R / 2) % 16 == 0, r, q);
         const int gr = min(row0 + r, rows - 1), gr2 = min(row0 + r + R / 2, rows - 1);  // rows past the matrix: valid duplicates
         g[i] = base + int64_t(gr) * ld + k0 + 4 * q;
         g2[i] = base + int64_t(gr2) * ld + k0 + 4 * q;
@@ -368,7 +388,8 @@ struct SxConvAOperand {
       const int u = t + i * T;
       on[i] = (kUnits % T == 0) || u < kUnits;
       const int uu = on[i] ? u : 0;
-      const int q = uu & 3, r = uu >> 2;
+      int q, r;
+      sx_kc_unit(uu, p.wmap && (R / 2) % 16 == 0, r, q);
       q4[i] = 4 * q;
 #pragma unroll
       for (int j = 0; j < 2; ++j) {
@@ -508,9 +529,9 @@ __global__ __launch_bounds__((BM / (32 * WMT)) * (BN / (32 * WNT)) * 64, MINW) v
   using StB = typename OpB::Stage;
   OpB opb;
   if constexpr (CONVA) opa.init(p, m0, kb, t);
-  else opa.init(p.a, p.lda, m0, p.M, kb, t);
+  else opa.init(p.a, p.lda, m0, p.M, kb, t, p.wmap);
   if constexpr (CONV) opb.init(p, n0, kb, t);
-  else opb.init(p.b, p.ldb, n0, p.N, kb, t);
+  else opb.init(p.b, p.ldb, n0, p.N, kb, t, p.wmap);
   StA sa0, sa1;
   StB sb0, sb1;
 
@@ -726,9 +747,9 @@ __global__ __launch_bounds__(512, 1) void sgemm_ws_kernel(SxArgs p) {
     using OpB = std::conditional_t<CONV, SxConvOperand<BN, T>, SxOperand<BN, BKM, T>>;
     using StB = typename OpB::Stage;
     OpB opb;
-    opa.init(p.a, p.lda, m0, p.M, kb, tp);
+    opa.init(p.a, p.lda, m0, p.M, kb, tp, p.wmap);
     if constexpr (CONV) opb.init(p, n0, kb, tp);
-    else opb.init(p.b, p.ldb, n0, p.N, kb, tp);
+    else opb.init(p.b, p.ldb, n0, p.N, kb, tp, p.wmap);
     SxStage<BM, AKM, T> sa[DEPTH];
     StB sb[DEPTH];
     int nld = 0;
@@ -957,6 +978,7 @@ constexpr int kSxTileN[8] = {128, 128, 256, 128, 128, 256, 64, 96};
 }  // namespace
 
 void sgemm_f32_set_stagger(int on) { g_sx_stagger = on ? 1 : 0; }
+void sgemm_set_write_map(int on) { g_sx_wmap = on ? 1 : 0; }
 void sgemm_conv_wgrad_set_ws(int mode) { g_sx_conv_ws = mode < 0 || mode > 2 ? 0 : mode; }
 void sgemm_set_reduce_groups(int g) { g_sx_reduce_groups = (g == 1 || g == 2 || g == 4 || g == 8 || g == 16) ? g : -1; }
 
@@ -1005,6 +1027,7 @@ void sgemm_f32(uintptr_t a, int64_t lda, bool a_kmajor, uintptr_t b, int64_t ldb
   p.beta = beta ? 1 : 0;
   p.epi = epi;
   p.stagger = g_sx_stagger;
+  p.wmap = g_sx_wmap;
   p.bsum = reinterpret_cast<float*>(bsum);
   if (S > 1) {
     VODA_CHECK(ws != 0 && ws_floats >= sgemm_f32_workspace_floats(M, N, S), "sgemm_f32: split-K workspace too small");
@@ -1084,6 +1107,7 @@ void sgemm_conv_wgrad_f32(uintptr_t dy, uintptr_t x, uintptr_t gw, int n, int H,
   p.tiles = ((Cout + BM - 1) / BM) * p.tiles_n;
   p.beta = accumulate ? 1 : 0;
   p.stagger = g_sx_stagger;
+  p.wmap = g_sx_wmap;
   if (S > 1) {
     VODA_CHECK(ws != 0 && ws_floats >= sgemm_f32_workspace_floats(Cout, N, S), "sgemm_conv_wgrad_f32: workspace too small");
     VODA_CHECK(gw % 16 == 0, "sgemm_conv_wgrad_f32: split-K output needs 16-B rows");
@@ -1131,6 +1155,7 @@ void sgemm_conv_fwd_f32(uintptr_t x, uintptr_t w, uintptr_t y, int n, int H, int
   p.tiles_n = (Cout + 127) / 128;
   p.tiles = int((M + 127) / 128) * p.tiles_n;
   p.stagger = g_sx_stagger;
+  p.wmap = g_sx_wmap;
   hipLaunchKernelGGL((sgemm_bf16x3_kernel<128, 128, false, false, 6, true, false, 2, 2, false, 0, true>),
                      dim3(unsigned(p.tiles)), dim3(256), 0, as_stream(stream), p);
   check_launch();
@@ -1165,6 +1190,7 @@ void sgemm_conv_dgrad_s2_class(uintptr_t dy, uintptr_t wc, uintptr_t dx, int n, 
   p.tiles_n = (Cin + 127) / 128;
   p.tiles = int((M + 127) / 128) * p.tiles_n;
   p.stagger = g_sx_stagger;
+  p.wmap = g_sx_wmap;
   hipLaunchKernelGGL((sgemm_bf16x3_kernel<128, 128, false, true, 6, true, false, 2, 2, false, 0, true>),
                      dim3(unsigned(p.tiles)), dim3(256), 0, as_stream(stream), p);
   check_launch();

@@ -58,7 +58,10 @@ USE_T7 = True  # the 128 x 96 tile in ``choose`` (A/B switch)
 USE_FUSED_ROW_SUMS = True
 REDUCE_GROUPS = -1
 REDUCE_GROUPS_AUTO = True  # False: one group (A/B switch)
-_applied = {"reduce_groups": None}
+# K-contiguous operands staged with a row map whose 8-byte LDS writes hit 32 distinct banks per
+# 16-lane group (csrc/hip/splitgemm.hip sx_kc_unit; False: consecutive rows, 2-way conflicts)
+WRITE_MAP = True
+_applied = {"reduce_groups": None, "write_map": None}
 
 
 def _sync_knobs(h) -> None:
@@ -66,6 +69,9 @@ def _sync_knobs(h) -> None:
     if _applied["reduce_groups"] != g:
         h.sgemm_set_reduce_groups(int(g))
         _applied["reduce_groups"] = g
+    if _applied["write_map"] != WRITE_MAP:
+        h.sgemm_set_write_map(int(bool(WRITE_MAP)))
+        _applied["write_map"] = WRITE_MAP
 
 _WS: dict[torch.device, torch.Tensor] = {}
 
@@ -348,6 +354,7 @@ def conv_fwd(x: torch.Tensor, w: torch.Tensor, stride: int, padding: int) -> tor
     ho = (H + 2 * padding - kh) // stride + 1
     wo = (W + 2 * padding - kw) // stride + 1
     y = torch.empty((n, cout, ho, wo), dtype=torch.float32, device=x.device, memory_format=torch.channels_last)
+    _sync_knobs(N.hip())
     N.hip().sgemm_conv_fwd_f32(x.data_ptr(), w.data_ptr(), y.data_ptr(), n, H, W, cin, ho, wo, cout, kh, kw,
                                int(stride), int(padding), N.stream_of(x))
     return y
@@ -385,6 +392,7 @@ def conv_dgrad_s2(dy: torch.Tensor, w: torch.Tensor, in_shape) -> torch.Tensor:
     dx = torch.empty((n, cin, H, W), dtype=torch.float32, device=dy.device, memory_format=torch.channels_last)
     wt = w.permute(2, 3, 0, 1)  # [kh][kw][co][ci] view
     h = N.hip()
+    _sync_knobs(h)
     st = N.stream_of(dy)
     for ph in (0, 1):
         for pw in (0, 1):
