@@ -12,6 +12,7 @@
 #   step-MODEL[-fp32]        benchmarks/model_step.py timing of one model (resnet50, bert-base, ...)
 #   prof-MODEL[-fp32]        rocprofv3 --kernel-trace --stats of 10 steps of one model
 #   pmc-MODEL:COUNTERS       one rocprofv3 --pmc pass (comma-separated counters)
+#   profset:MODULE:ATTR=VALUE:MODEL[-fp32]  prof-MODEL with one module switch set (model_step.py --set)
 #   py:SCRIPT[:ARGS]         python benchmarks/SCRIPT ARGS (comma-separated args)
 #   pytest:FILE[,ARGS]       pytest -m gpu of one test file (comma-separated extra args)
 #   env:NAME=VALUE           export for the following steps (their logs get a "+NAME=VALUE" suffix)
@@ -83,6 +84,24 @@ for step in "$@"; do
       python3 benchmarks/trace_dispatches.py "/tmp/$st/k_kernel_trace.csv" "$OUT/$st/sequence.csv" "" \
         >> "$OUT/$st.log" 2>&1 || exit 7
       python3 benchmarks/rocprof_summary.py "$OUT/$st/steady_kernel_stats.csv" "$m $prec steady state (10 steps)" 45 10 \
+        > "$OUT/$st.md" || exit 7
+      tail -n 3 "$OUT/$st.log" ;;
+    profset:*)  # profset:MODULE:ATTR=VALUE:MODEL[-fp32] -- prof-MODEL with one module switch set
+      spec=${step#profset:}
+      IFS=: read -r mod kv m <<< "$spec"
+      prec=bf16-amp
+      if [[ $m == *-fp32 ]]; then m=${m%-fp32}; prec=fp32; fi
+      R=$PWD
+      st="profset-$m-${kv//=/-}$SUFFIX"
+      ( cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "/tmp/$st" -o k -- \
+          python3 "$R/benchmarks/model_step.py" --model "$m" --steps 10 --warmup 6 --precision "$prec" \
+          --profile-marker --set "$mod:$kv" ) > "$OUT/$st.log" 2>&1 || { tail -20 "$OUT/$st.log"; exit 6; }
+      mkdir -p "$OUT/$st"
+      python3 benchmarks/trace_window_stats.py "/tmp/$st/k_kernel_trace.csv" "$OUT/$st/steady_kernel_stats.csv" \
+        >> "$OUT/$st.log" 2>&1 || exit 7
+      python3 benchmarks/trace_dispatches.py "/tmp/$st/k_kernel_trace.csv" "$OUT/$st/sequence.csv" "" \
+        >> "$OUT/$st.log" 2>&1 || exit 7
+      python3 benchmarks/rocprof_summary.py "$OUT/$st/steady_kernel_stats.csv" "$m $prec $mod:$kv (10 steps)" 60 10 \
         > "$OUT/$st.md" || exit 7
       tail -n 3 "$OUT/$st.log" ;;
     pmc-*)
