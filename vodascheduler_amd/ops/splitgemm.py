@@ -50,12 +50,12 @@ ENABLED = os.environ.get("VODA_SPLIT_GEMM", "1") != "0"
 # gradient (0 one-role kernel, 1 / 2 wave-specialised, staging one / two stages ahead)
 DEFAULT_VARIANT = 0
 CONV_WGRAD_WS = 0
-# split-K reduce: slab groups per float4 column (-1 automatic: ~4096 blocks-worth of groups, >= 16
-# slabs per group; 1 = one thread per column, the round-5 form)
 USE_T7 = True  # the 128 x 96 tile in ``choose`` (A/B switch)
 # a Linear's bias gradient summed in the weight-gradient GEMM's A staging (matmul(row_sums=...))
 # instead of a separate column-sum pass over dY (A/B switch)
 USE_FUSED_ROW_SUMS = True
+# split-K reduce: slab groups per float4 column (-1 automatic: ~4096 blocks-worth of groups, >= 16
+# slabs per group; 1 = one thread per column, the round-5 form)
 REDUCE_GROUPS = -1
 REDUCE_GROUPS_AUTO = True  # False: one group (A/B switch)
 # K-contiguous operands staged with a row map whose 8-byte LDS writes hit 32 distinct banks per
@@ -148,7 +148,8 @@ def choose(M: int, Nn: int, K: int, variant: int = 0) -> tuple[int, int]:
     resident).  From the MI355X sweep over the BERT-base shapes (profiles/r6/splitgemm_probe.md):
     >= 1024 output tiles run whole; 384-1023 tiles split K in two when K >= 2048 (the single
     384-workgroup round leaves CUs with one workgroup idle half the time); small outputs (weight
-    gradients: 36-144 tiles) split K towards ~1152 workgroups with >= 256 k per split."""
+    gradients: 36-144 tiles) split K towards ~1152 workgroups with >= 256 k per split.  The same
+    shapes serve every math variant (``variant`` is accepted for call-site symmetry)."""
     tiles = -(-M // 128) * -(-Nn // 128)
     # 128 x 96 tiles where they fill whole rounds of the 512 resident workgroups and 128 x 128
     # tiles do not (BERT-base: 8192 x 2304 as 1536 tiles, 8192 x 768 as 512): qkv forward 200 ->
