@@ -79,6 +79,12 @@ BLAS_WGRAD_F32_MIN_OUT = 1 << 20
 # A/B, profiles/r6/ab_split_1x1_v1_resnet50_fp32.jsonl).  Stays off.
 USE_SPLIT_GEMM_F32 = False
 SPLIT_VARIANT = 1
+# ... but the FORWARDS with K >= 512 input channels alone do win: a per-call rocprof of the step with
+# every library 1x1 GEMM on the split kernel (profiles/r6/rocprof_resnet50_fp32_split_1x1_calls.md)
+# has the ten K >= 512 forwards 0-10 % faster than the tuned hipBLASLt solutions (-160 us per
+# step), while the K = 64 forward lost 76 -> 221 us and the input gradients +1.4 ms
+USE_SPLIT_FWD_F32 = True
+SPLIT_FWD_MIN_K = 512
 # the fp32 1x1 weight gradients (reduction over the pixels) on the split-bf16 GEMM, split-K to
 # ~1024 workgroups (else MIOpen / hipBLASLt as before): ResNet-50 fp32 60.49 -> 60.37 ms
 # (same-box A/B, profiles/r6/ab_split_1x1_wgrad_resnet50_fp32.jsonl)
@@ -359,6 +365,9 @@ class _Conv1x1Fn(torch.autograd.Function):
         y2 = gemm_bnstats_2d(x2, w2, holder)
         if y2 is None and x2.dtype == torch.float32:
             y2 = gemm_f32_2d(x2, w2)
+        if y2 is None and (USE_SPLIT_FWD_F32 and not USE_SPLIT_GEMM_F32 and x2.dtype == torch.float32
+                           and x2.shape[1] >= SPLIT_FWD_MIN_K and SG.supported(x2, w2.t())):
+            y2 = SG.matmul(x2, w2.t(), variant=SPLIT_VARIANT)
         if y2 is None:
             y2 = _mm(x2, w2.t())
         ctx.save_for_backward(x2, weight)
