@@ -82,8 +82,10 @@ SPLIT_VARIANT = 1
 # ... but the FORWARDS with K >= 512 input channels alone do win: a per-call rocprof of the step with
 # every library 1x1 GEMM on the split kernel (profiles/r6/rocprof_resnet50_fp32_split_1x1_calls.md)
 # has the ten K >= 512 forwards 0-10 % faster than the tuned hipBLASLt solutions (-160 us per
-# step), while the K = 64 forward lost 76 -> 221 us and the input gradients +1.4 ms
-USE_SPLIT_FWD_F32 = True
+# step), while the K = 64 forward lost 76 -> 221 us and the input gradients +1.4 ms.  Routed
+# alone, the same-box step A/B still lost: 59.11 -> 59.67 ms (profiles/r6/
+# ab_split_fwd_1x1_resnet50_fp32.jsonl), so it stays off
+USE_SPLIT_FWD_F32 = False
 SPLIT_FWD_MIN_K = 512
 # the fp32 1x1 weight gradients (reduction over the pixels) on the split-bf16 GEMM, split-K to
 # ~1024 workgroups (else MIOpen / hipBLASLt as before): ResNet-50 fp32 60.49 -> 60.37 ms
