@@ -994,7 +994,8 @@ int64_t sgemm_f32_workspace_floats(int M, int N, int splits) {
 // product-outer (consecutive MFMAs on different accumulators); 6 = variant 0's math in the
 // wave-specialised kernel (sgemm_ws_kernel: 4 MFMA + 4 staging waves, one workgroup per CU);
 // 7 = 6 with three LDS buffers, the staging waves two stages ahead and the MFMA waves reading
-// the next stage's fragments during the current stage's MFMAs (one accumulator).  Variants 1-7: 128 x 128 only.
+// the next stage's fragments during the current stage's MFMAs (one accumulator); 8 = one
+// accumulator at three workgroups per CU (<= 168 VGPRs; K-major images fit 3 x 49 KB of LDS).  Variants 1-7: 128 x 128 only.
 void sgemm_f32(uintptr_t a, int64_t lda, bool a_kmajor, uintptr_t b, int64_t ldb, bool b_kmajor, uintptr_t c,
                int64_t ldc, int M, int N, int K, bool beta, uintptr_t bias, int epi, uintptr_t aux, int64_t ldaux,
                int tile, int splits, int variant, uintptr_t ws, int64_t ws_floats, uintptr_t stream, uintptr_t bsum) {
@@ -1004,7 +1005,7 @@ void sgemm_f32(uintptr_t a, int64_t lda, bool a_kmajor, uintptr_t b, int64_t ldb
   VODA_CHECK(K % kSxBK == 0, "sgemm_f32: K must be a multiple of 16");
   VODA_CHECK(M % 4 == 0 && N % 4 == 0, "sgemm_f32: M and N must be multiples of 4");
   VODA_CHECK(tile >= 0 && tile < 8, "sgemm_f32: bad tile id");
-  VODA_CHECK(variant >= 0 && variant <= 7 && (variant == 0 || tile == 0), "sgemm_f32: bad math variant");
+  VODA_CHECK(variant >= 0 && variant <= 8 && (variant == 0 || tile == 0), "sgemm_f32: bad math variant");
   VODA_CHECK(epi >= kSxEpiNone && epi <= kSxEpiDGelu && (epi == kSxEpiNone || aux != 0), "sgemm_f32: bad epilogue");
   VODA_CHECK(a % 16 == 0 && b % 16 == 0 && lda % 4 == 0 && ldb % 4 == 0, "sgemm_f32: operands need 16-B rows");
   VODA_CHECK(lda >= (a_kmajor ? M : K) && ldb >= (b_kmajor ? N : K) && ldc >= N, "sgemm_f32: leading dims");
@@ -1046,7 +1047,8 @@ void sgemm_f32(uintptr_t a, int64_t lda, bool a_kmajor, uintptr_t b, int64_t ldb
     else if (variant == 4) sx_launch_tile<128, 128, 6, true, true, 1>(p, a_kmajor, b_kmajor, grid, st);
     else if (variant == 5) sx_launch_tile<128, 128, 6, true, false, 2, 2, 1>(p, a_kmajor, b_kmajor, grid, st);
     else if (variant == 6) sx_launch_ws<1, 2>(p, a_kmajor, b_kmajor, grid, st);
-    else sx_launch_ws<2, 2>(p, a_kmajor, b_kmajor, grid, st);
+    else if (variant == 7) sx_launch_ws<2, 2>(p, a_kmajor, b_kmajor, grid, st);
+    else sx_launch_tile<128, 128, 6, false, false, 3>(p, a_kmajor, b_kmajor, grid, st);
   } else if (tile == 1) {
     sx_launch_tile<256, 128, 6, true, false>(p, a_kmajor, b_kmajor, grid, st);
   } else if (tile == 2) {

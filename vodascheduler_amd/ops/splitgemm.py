@@ -41,7 +41,7 @@ def thin_tile(M: int, Nn: int) -> int:
 # only); 4 = 0 software-pipelined at one wave per SIMD (A/B)
 VARIANT_NAMES = {0: "bf16x3-6p-dual", 1: "bf16x3-6p-single-pipe", 2: "bf16x3-9p-dual", 3: "bf16x2-3p-dual",
                  4: "bf16x3-6p-dual-pipe-1wave", 5: "bf16x3-6p-dual-product-outer",
-                 6: "bf16x3-6p-dual-wavespec", 7: "bf16x3-6p-single-wavespec-lead2"}
+                 6: "bf16x3-6p-dual-wavespec", 7: "bf16x3-6p-single-wavespec-lead2", 8: "bf16x3-6p-single-3wg"}
 GEMM_MATH = VARIANT_NAMES[0]
 
 # VODA_SPLIT_GEMM=0 routes the fp32 projections back to hipBLASLt (A/B switch)
