@@ -83,7 +83,9 @@ struct SxArgs {
 
 int g_sx_stagger = 1;
 int g_sx_wmap = 1;  // conflict-free K-contiguous staging writes (sx_kc_unit)
-int g_sx_conv_ws = 0;  // convolution weight gradient kernel: 0 one-role, 1 / 2 wave-specialised (lead 1 / 2)
+// convolution weight gradient kernel: 0 one-role, 1 / 2 wave-specialised (lead 1 / 2), 3 one-role
+// with one accumulator at three workgroups per CU
+int g_sx_conv_ws = 0;
 
 // K-major images of R = 96 columns use the R = 128 layout (192-byte k-rows padded to 256 B)
 template <int R> struct SxKmPitch { static constexpr int kR = R == 96 ? 128 : R == 192 ? 256 : R; };
@@ -979,7 +981,7 @@ constexpr int kSxTileN[8] = {128, 128, 256, 128, 128, 256, 64, 96};
 
 void sgemm_f32_set_stagger(int on) { g_sx_stagger = on ? 1 : 0; }
 void sgemm_set_write_map(int on) { g_sx_wmap = on ? 1 : 0; }
-void sgemm_conv_wgrad_set_ws(int mode) { g_sx_conv_ws = mode < 0 || mode > 2 ? 0 : mode; }
+void sgemm_conv_wgrad_set_ws(int mode) { g_sx_conv_ws = mode < 0 || mode > 3 ? 0 : mode; }
 void sgemm_set_reduce_groups(int g) { g_sx_reduce_groups = (g == 1 || g == 2 || g == 4 || g == 8 || g == 16) ? g : -1; }
 
 int64_t sgemm_f32_workspace_floats(int M, int N, int splits) {
@@ -1000,8 +1002,8 @@ void sgemm_f32(uintptr_t a, int64_t lda, bool a_kmajor, uintptr_t b, int64_t ldb
                int64_t ldc, int M, int N, int K, bool beta, uintptr_t bias, int epi, uintptr_t aux, int64_t ldaux,
                int tile, int splits, int variant, uintptr_t ws, int64_t ws_floats, uintptr_t stream, uintptr_t bsum) {
   VODA_CHECK(M > 0 && N > 0 && K > 0, "sgemm_f32: empty GEMM");
-  VODA_CHECK(bsum == 0 || (a_kmajor && (tile == 0 || tile == 7) && variant == 0 && bsum % 16 == 0),
-             "sgemm_f32: fused row sums need a K-major A on tile 0 / 7, variant 0, 16-B aligned");
+  VODA_CHECK(bsum == 0 || (a_kmajor && (tile == 0 || tile == 7) && (variant == 0 || variant == 8) && bsum % 16 == 0),
+             "sgemm_f32: fused row sums need a K-major A on tile 0 / 7, variant 0 / 8, 16-B aligned");
   VODA_CHECK(K % kSxBK == 0, "sgemm_f32: K must be a multiple of 16");
   VODA_CHECK(M % 4 == 0 && N % 4 == 0, "sgemm_f32: M and N must be multiples of 4");
   VODA_CHECK(tile >= 0 && tile < 8, "sgemm_f32: bad tile id");
@@ -1125,6 +1127,9 @@ void sgemm_conv_wgrad_f32(uintptr_t dy, uintptr_t x, uintptr_t gw, int n, int H,
     hipLaunchKernelGGL((sgemm_ws_kernel<true, true, true, 1, 2>), dim3(unsigned(nwg)), dim3(512), 0, st, p);
   else if (g_sx_conv_ws == 2)
     hipLaunchKernelGGL((sgemm_ws_kernel<true, true, true, 2, 2>), dim3(unsigned(nwg)), dim3(512), 0, st, p);
+  else if (g_sx_conv_ws == 3)  // one accumulator at three workgroups per CU (as GEMM variant 8)
+    hipLaunchKernelGGL((sgemm_bf16x3_kernel<128, 128, true, true, 6, false, false, 3, 2, true>), dim3(unsigned(nwg)),
+                       dim3(256), 0, st, p);
   else
     hipLaunchKernelGGL((sgemm_bf16x3_kernel<128, 128, true, true, 6, true, false, 2, 2, true>), dim3(unsigned(nwg)),
                        dim3(256), 0, st, p);

@@ -81,6 +81,30 @@ def test_choose_tiles_and_splits():
         SG.USE_T7 = old
 
 
+def test_plan_variant_8_for_kmajor_b():
+    """Input / weight gradients (K-major B) plan variant 8 on 128 x 128 tiles with the same
+    split-K rules; row-major B and pinned tiles keep the default (profiles/r6/splitgemm_v8_3wg_probe.jsonl)."""
+    x = torch.zeros(64, 32)
+    w = torch.zeros(32, 48)  # B [K, N] row-major: K-major (dX = dY W, dW = dY^T X)
+    assert SG.plan_variant(True) == (8 if SG.USE_V8_KMAJOR_B else 0)
+    assert SG.plan_variant(True, tile=7) == SG.DEFAULT_VARIANT
+    assert SG.plan_variant(False) == SG.DEFAULT_VARIANT
+    assert SG.plan(x, w)[2] == SG.plan_variant(True)
+    assert SG.plan(x, w.t().contiguous().t())[2] == SG.DEFAULT_VARIANT
+    assert SG.choose(8192, 768, 2304, 8) == (0, 2)     # qkv input gradient: 384 tiles, no 128 x 96
+    assert SG.choose(8192, 768, 3072, 8) == (0, 2)
+    assert SG.choose(768, 2304, 8192, 8) == (0, 7)
+    assert SG.choose(768, 768, 8192, 8) == (0, 12)
+    rs = torch.zeros(64)
+    assert not SG.row_sums_ok(x.t(), rs, 7, 8)        # CPU tensors never fuse anyway
+    old = SG.USE_V8_KMAJOR_B
+    try:
+        SG.USE_V8_KMAJOR_B = False
+        assert SG.plan_variant(True) == SG.DEFAULT_VARIANT
+    finally:
+        SG.USE_V8_KMAJOR_B = old
+
+
 def test_thin_tiles_and_wgrad_splits():
     assert SG.thin_tile(64, 256) == 5 and SG.thin_tile(256, 64) == 6 and SG.thin_tile(128, 256) == 0
     # ~target workgroups, >= 256 pixels per split

@@ -76,7 +76,7 @@ def test_thin_tiles(tile, akm, bkm):
         assert err < 2e-7, (tile, M, K, N, err)
 
 
-@pytest.mark.parametrize("splits,variant", [(2, 0), (3, 0), (7, 0), (3, 6), (7, 6)])
+@pytest.mark.parametrize("splits,variant", [(2, 0), (3, 0), (7, 0), (3, 6), (7, 6), (2, 8), (7, 8)])
 def test_split_k_matches_reference(splits, variant):
     torch.manual_seed(splits)
     M, K, N = 256, 1024, 384
@@ -84,7 +84,7 @@ def test_split_k_matches_reference(splits, variant):
     b = torch.randn(K, N, device=DEV)
     c = SG.matmul(a, b, tile=0, splits=splits, variant=variant)
     ref = a.double() @ b.double()
-    assert ((c.double() - ref).abs() / _bound(a, b)).max().item() < 2e-7
+    assert ((c.double() - ref).abs() / _bound(a, b)).max().item() < (4e-7 if variant == 8 else 2e-7)
 
 
 @pytest.mark.parametrize("groups", [-1, 1, 2, 4, 16])
@@ -120,6 +120,8 @@ def test_no_worse_than_hipblaslt_wide_magnitudes():
 
 @pytest.mark.parametrize("tile", [None, 7])
 def test_epilogues_bias_accumulate_gelu_dgelu(tile, monkeypatch):
+    """Epilogues on the planned launch (variant 8 for the K-major weights of x @ W^T) and on
+    tile 7 (variant 0)."""
     if tile is not None:  # route every call of this test to the given tile
         monkeypatch.setattr(SG, "choose", lambda M, N, K, variant=0: (tile, 1))
     torch.manual_seed(9)
@@ -130,19 +132,20 @@ def test_epilogues_bias_accumulate_gelu_dgelu(tile, monkeypatch):
     ref = x.double() @ w.double().t()
     bd = _bound(x, w.t())
     # bias
+    tol = 4e-7 if tile is None and SG.plan(x, w.t())[2] == 8 else 2e-7  # 8: one accumulator
     y = SG.matmul(x, w.t(), bias=bias)
-    assert ((y.double() - ref - bias.double()).abs() / (bd + 1)).max().item() < 2e-7
+    assert ((y.double() - ref - bias.double()).abs() / (bd + 1)).max().item() < tol
     # accumulate into an existing output (beta = 1), split-K path too
     for s in (1, 4):
         acc = torch.randn(M, N, device=DEV)
         want = acc.double() + ref
         SG.matmul(x, w.t(), out=acc, accumulate=True, splits=s)
-        assert ((acc.double() - want).abs() / (bd + 1)).max().item() < 2e-7
+        assert ((acc.double() - want).abs() / (bd + 1)).max().item() < tol
     # GELU: aux = h = xW^T + b, out = gelu(h)
     h = torch.empty(M, N, device=DEV)
     g = SG.matmul(x, w.t(), bias=bias, epi=SG.EPI_GELU, aux=h)
     href = ref + bias.double()
-    assert ((h.double() - href).abs() / (bd + 1)).max().item() < 2e-7
+    assert ((h.double() - href).abs() / (bd + 1)).max().item() < tol
     gref = torch.nn.functional.gelu(href, approximate="tanh")
     assert (g.double() - gref).abs().max().item() < 1e-5
     # DGELU: out = (dY W) * gelu'(h), h [M, K]
@@ -169,13 +172,14 @@ def test_variants_error_ordering():
 @pytest.mark.parametrize("n,cin,cout,hw,stride", [(2, 128, 128, 16, 1), (3, 64, 132, 8, 1), (16, 128, 128, 7, 1),
                                                   (2, 128, 256, 16, 2), (4, 256, 128, 7, 2), (2, 64, 64, 16, 1),
                                                   (4, 128, 64, 8, 1), (3, 64, 64, 7, 2)])
-@pytest.mark.parametrize("ws", [0, 1])
-def test_conv_wgrad_implicit_gemm_matches_fp64(n, cin, cout, hw, stride, ws):
+@pytest.mark.parametrize("ws", [0, 1, 3])
+def test_conv_wgrad_implicit_gemm_matches_fp64(n, cin, cout, hw, stride, ws, monkeypatch):
     """dW (+)= conv weight gradient of a 3x3 pad-1 convolution (NHWC gather per tap in the
-    B-operand staging, zero padding, stride 1 / 2, ragged maps) against fp64; one-role and
-    wave-specialised kernels."""
+    B-operand staging, zero padding, stride 1 / 2, ragged maps) against fp64; one-role (dual
+    accumulators), wave-specialised and one-role single-accumulator three-workgroup kernels."""
     torch.manual_seed(cin + cout + hw + stride)
-    SG.N.hip().sgemm_conv_wgrad_set_ws(ws)
+    monkeypatch.setattr(SG, "CONV_WGRAD_WS", 1 if ws == 1 else 0)
+    monkeypatch.setattr(SG, "CONV_WGRAD_V8", ws == 3)
     cl = torch.channels_last
     x = torch.randn(n, cin, hw, hw, device=DEV).contiguous(memory_format=cl)
     ho = (hw + 2 - 3) // stride + 1
@@ -185,10 +189,7 @@ def test_conv_wgrad_implicit_gemm_matches_fp64(n, cin, cout, hw, stride, ws):
     gw = torch.randn(cout, cin, 3, 3, device=DEV).contiguous(memory_format=cl)
     g0 = gw.clone()
     assert SG.conv_wgrad_ok(dy, x, gw)
-    try:
-        SG.conv_wgrad_(dy, x, gw, stride, 1, accumulate=True)
-    finally:
-        SG.N.hip().sgemm_conv_wgrad_set_ws(SG.CONV_WGRAD_WS)
+    SG.conv_wgrad_(dy, x, gw, stride, 1, accumulate=True)
     ref = torch.nn.grad.conv2d_weight(x.double(), gw.shape, dy.double(), stride=stride, padding=1)
     bound = torch.nn.grad.conv2d_weight(x.double().abs(), gw.shape, dy.double().abs(), stride=stride, padding=1)
     err = ((gw.double() - g0.double() - ref).abs() / (bound + 1)).max().item()
@@ -234,9 +235,11 @@ def test_conv_dgrad_stride2_polyphase_matches_fp64(n, cin, cout, hw):
     assert err < 2e-7, err
 
 
-@pytest.mark.parametrize("M,K,N,splits,tile", [(768, 8192, 768, 12, 0), (2304, 8192, 768, 7, 0), (260, 1024, 196, 1, 0),
-                                               (256, 4096, 192, 3, 7), (128, 64, 128, 1, 0)])
-def test_fused_row_sums(M, K, N, splits, tile):
+@pytest.mark.parametrize("M,K,N,splits,tile,variant", [(768, 8192, 768, 12, 0, 0), (2304, 8192, 768, 7, 0, 0),
+                                                       (260, 1024, 196, 1, 0, 0), (256, 4096, 192, 3, 7, 0),
+                                                       (128, 64, 128, 1, 0, 0), (2304, 8192, 768, 7, 0, 8),
+                                                       (260, 1024, 196, 1, 0, 8), (768, 4096, 260, 12, 0, 8)])
+def test_fused_row_sums(M, K, N, splits, tile, variant):
     """row_sums += a.sum(1) from the A staging of a weight-gradient GEMM (K-major a = dY^T), with
     and without split-K, ragged M, next to the accumulated product."""
     torch.manual_seed(M + K)
@@ -247,10 +250,10 @@ def test_fused_row_sums(M, K, N, splits, tile):
     c = c0.clone()
     rs0 = torch.randn(M, device=DEV)
     rs = rs0.clone()
-    assert SG.row_sums_ok(a, rs, tile, 0)
-    SG.matmul(a, x, out=c, accumulate=True, tile=tile, splits=splits, row_sums=rs)
+    assert SG.row_sums_ok(a, rs, tile, variant)
+    SG.matmul(a, x, out=c, accumulate=True, tile=tile, splits=splits, variant=variant, row_sums=rs)
     ref = a.double() @ x.double() + c0.double()
-    assert ((c.double() - ref).abs() / (_bound(a, x) + 1)).max().item() < 2e-7
+    assert ((c.double() - ref).abs() / (_bound(a, x) + 1)).max().item() < (4e-7 if variant == 8 else 2e-7)
     rref = dy.double().sum(0) + rs0.double()
     rbound = dy.double().abs().sum(0) + 1
     assert ((rs.double() - rref).abs() / rbound).max().item() < 1e-6

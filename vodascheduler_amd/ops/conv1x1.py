@@ -97,6 +97,8 @@ USE_THIN_TILES = True
 # ... split-K to ~this many workgroups (one round of the 512 resident ones; 1024 before round 6's
 # sweep, profiles/r6/resnet50_wgrad_splits_probe_b.jsonl)
 WGRAD_TARGET_WG = 512
+# ... and on the 128 x 128 tile as GEMM variant 8 (one accumulator, three workgroups per CU; A/B switch)
+WGRAD_V8 = True
 
 
 def _sx(a: torch.Tensor, b: torch.Tensor) -> bool:
@@ -443,7 +445,8 @@ class _Conv1x1Fn(torch.autograd.Function):
                 # split-K into the flat gradient, ~1024 workgroups over the pixels
                 tile = SG.thin_tile(cout, cin) if USE_THIN_TILES else 0
                 SG.matmul(dy2.t(), x2, out=g2, accumulate=True, tile=tile,
-                          splits=SG.conv_wgrad_splits(cout, cin, dy2.shape[0], tile, WGRAD_TARGET_WG))
+                          splits=SG.conv_wgrad_splits(cout, cin, dy2.shape[0], tile, WGRAD_TARGET_WG),
+                          variant=8 if WGRAD_V8 and tile == 0 else None)
                 _ready(weight)
             elif (dy2.dtype == torch.float32 and g2 is not None and g2.dtype == torch.float32
                     and blas_wgrad_f32_ok(dy2.shape[0], cout, cin)):

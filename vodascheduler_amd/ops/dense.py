@@ -122,8 +122,8 @@ def linear_weight_grads(dy2: torch.Tensor, x2: torch.Tensor, weight: torch.Tenso
                 # fp32: split-bf16 MFMA, beta = 1; the bias gradient (column sums of dY) from the same
                 # launch's A staging when the layout allows
                 gb = flat_grad(bias) if need_b and _direct(bias) else None
-                tile = SG.choose(dy2.shape[1], x2.shape[1], dy2.shape[0])[0]
-                if gb is not None and SG.row_sums_ok(dy2.t(), gb, tile, SG.DEFAULT_VARIANT):
+                tile, _, variant = SG.plan(dy2.t(), x2)
+                if gb is not None and SG.row_sums_ok(dy2.t(), gb, tile, variant):
                     SG.matmul(dy2.t(), x2, out=gw, accumulate=True, row_sums=gb)
                     _ready(weight)
                     _ready(bias)

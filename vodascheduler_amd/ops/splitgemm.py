@@ -50,7 +50,15 @@ ENABLED = os.environ.get("VODA_SPLIT_GEMM", "1") != "0"
 # gradient (0 one-role kernel, 1 / 2 wave-specialised, staging one / two stages ahead)
 DEFAULT_VARIANT = 0
 CONV_WGRAD_WS = 0
+# 3x3 convolution weight gradients on the 128 x 128 tile with one accumulator at three workgroups
+# per CU (the conv-gather image of variant 8; A/B switch)
+CONV_WGRAD_V8 = True
 USE_T7 = True  # the 128 x 96 tile in ``choose`` (A/B switch)
+# GEMMs whose B operand is K-major (input and weight gradients) on variant 8: one accumulator at
+# three workgroups per CU (K-major B images leave room for three in LDS); qkv / fc1 / fc2 input
+# gradients 184 -> 177, 239 -> 227, 246 -> 230 us, qkv weight gradient 183 -> 176 us
+# (profiles/r6/splitgemm_v8_3wg_probe.jsonl); error still below hipBLASLt fp32's (A/B switch)
+USE_V8_KMAJOR_B = True
 # a Linear's bias gradient summed in the weight-gradient GEMM's A staging (matmul(row_sums=...))
 # instead of a separate column-sum pass over dY (A/B switch)
 USE_FUSED_ROW_SUMS = True
@@ -151,6 +159,16 @@ def choose(M: int, Nn: int, K: int, variant: int = 0) -> tuple[int, int]:
     gradients: 36-144 tiles) split K towards ~1152 workgroups with >= 256 k per split.  The same
     shapes serve every math variant (``variant`` is accepted for call-site symmetry)."""
     tiles = -(-M // 128) * -(-Nn // 128)
+    if variant == 8:  # three workgroups per CU: 128 x 128 tiles, splits as below
+        if tiles >= 1024:
+            return 0, 1
+        if tiles >= 384:
+            return 0, 2 if K >= 2048 else 1
+        if 96 <= tiles <= 160 and K >= 7 * 512:
+            return 0, 7
+        if 24 <= tiles <= 48 and K >= 12 * 512:
+            return 0, 12
+        return 0, max(1, min(16 if tiles >= 16 else 1024, 1152 // tiles, K // 256))
     # 128 x 96 tiles where they fill whole rounds of the 512 resident workgroups and 128 x 128
     # tiles do not (BERT-base: 8192 x 2304 as 1536 tiles, 8192 x 768 as 512): qkv forward 200 ->
     # 192 us, o forward 76 -> 71, o input gradient 78 -> 71 (profiles/r6/splitgemm_t7_sweep.jsonl);
@@ -227,12 +245,15 @@ def matmul(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor | None = None, ac
         out = torch.empty(M, Nn, dtype=torch.float32, device=a.device)
     if out.stride(1) != 1 or out.shape != (M, Nn):
         raise ValueError("splitgemm.matmul: out must be [M, N] with unit column stride")
-    variant = DEFAULT_VARIANT if variant is None else variant
+    if variant is None:
+        variant = plan_variant(lb[0], tile)
     t0, s0 = choose(M, Nn, K, variant)
     tile = t0 if tile is None else tile
     splits = s0 if splits is None else splits
+    if variant == 8 and tile != 0:  # variant 8 exists on the 128 x 128 tile only
+        variant = DEFAULT_VARIANT
     if row_sums is not None and not row_sums_ok(a, row_sums, tile, variant):
-        raise ValueError("splitgemm.matmul: row_sums need a K-major a, tile 0 / 7, variant 0 and an aligned fp32 [M]")
+        raise ValueError("splitgemm.matmul: row_sums need a K-major a, tile 0 / 7, variant 0 / 8 and an aligned fp32 [M]")
     h = N.hip()
     _sync_knobs(h)
     ws_floats = h.sgemm_f32_workspace_floats(M, Nn, splits)
@@ -252,14 +273,32 @@ def matmul(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor | None = None, ac
     return out
 
 
+def plan_variant(b_kmajor: bool, tile: int | None = None) -> int:
+    """The math / kernel variant ``matmul`` runs when the caller does not pin one: variant 8 for a
+    K-major B on the default tiles (``USE_V8_KMAJOR_B``), else ``DEFAULT_VARIANT``."""
+    if USE_V8_KMAJOR_B and b_kmajor and tile is None and DEFAULT_VARIANT == 0:
+        return 8
+    return DEFAULT_VARIANT
+
+
+def plan(a: torch.Tensor, b: torch.Tensor) -> tuple[int, int, int]:
+    """(tile, splits, variant) ``matmul(a, b)`` picks for these operands."""
+    lb = _layout(b, False)
+    v = plan_variant(bool(lb and lb[0]))
+    t, sp = choose(a.shape[0], b.shape[1], a.shape[1], v)
+    return t, sp, v
+
+
 def row_sums_ok(a: torch.Tensor, row_sums: torch.Tensor, tile: int, variant: int) -> bool:
     """Can ``matmul`` fuse ``row_sums += a.sum(1)`` on this launch shape?  K-major a (a weight
-    gradient's dY^T), tile 0 or 7, math variant 0, a contiguous 16-byte-aligned fp32 [M] target."""
+    gradient's dY^T), tile 0 or 7 on math variant 0 or tile 0 on variant 8, a contiguous
+    16-byte-aligned fp32 [M] target."""
     if not USE_FUSED_ROW_SUMS or not a.is_cuda:
         return False
     la = _layout(a, True)
     M = a.shape[0]
-    return (la is not None and la[0] and tile in (0, 7) and variant == 0 and row_sums.dtype == torch.float32
+    shape_ok = tile in (0, 7) if variant == 0 else (variant == 8 and tile == 0)
+    return (la is not None and la[0] and shape_ok and row_sums.dtype == torch.float32
             and row_sums.is_cuda and row_sums.dim() == 1 and row_sums.numel() == M and row_sums.is_contiguous()
             and row_sums.data_ptr() % 16 == 0)
 
@@ -323,7 +362,7 @@ def conv_wgrad_(dy: torch.Tensor, x: torch.Tensor, gw: torch.Tensor, stride: int
     s = conv_wgrad_splits(cout, kh * kw * cin, n * ho * wo, tile) if splits is None else splits
     h = N.hip()
     _sync_knobs(h)
-    h.sgemm_conv_wgrad_set_ws(CONV_WGRAD_WS)
+    h.sgemm_conv_wgrad_set_ws(3 if CONV_WGRAD_V8 and CONV_WGRAD_WS == 0 and tile == 0 else CONV_WGRAD_WS)
     ws_floats = h.sgemm_f32_workspace_floats(cout, kh * kw * cin, s)
     ws = _workspace(dy.device, ws_floats) if ws_floats else None
     h.sgemm_conv_wgrad_f32(dy.data_ptr(), x.data_ptr(), gw.data_ptr(), n, H, W, cin, ho, wo, cout, kh, kw,
