@@ -24,8 +24,8 @@
 //    weight gradient, W of an input gradient).  No transposed copies and no split copies are
 //    ever written: each thread loads 8 fp32 (two 16-B loads), splits them in registers
 //    (3 v_cvt_pk_bf16_f32 + 8 VALU per pair) and writes the three planes to LDS.
-//  * LDS images per stage (16 k): K-contiguous -> [row][h][plane][8] with a 112-B row pitch
-//    (7 x 16 B: the 16 rows of a ds_read_b128 lane group land on 16 distinct bank slots), read
+//  * LDS images per stage (16 k): K-contiguous -> [row][h][plane][8] with a 96-B row pitch and
+//    the k-halves swapped in every other 8-row block (sx_kc_off: conflict-free), read
 //    as 3 x ds_read_b128 per fragment; K-major -> [plane][k][row] with 256-B XOR-swizzled
 //    rows (guide T10 layout (b)), read as 2 x ds_read_b64_tr_b16 per fragment.
 //  * v_mfma_f32_32x32x16_bf16; each wave owns a 64 x 64 output sub-tile (2 x 2 MFMA tiles);
@@ -54,7 +54,23 @@ typedef __attribute__((address_space(3))) sx_bf16x4_v sx_lds_bf16x4;
 #endif
 
 constexpr int kSxBK = 16;        // k per LDS stage: one 32x32x16 MFMA step
-constexpr int kSxKcPitch = 112;  // K-contiguous image: [h][plane][8] bf16 = 96 B + 16 B pad per row
+// K-contiguous image row: [h][plane][8] bf16 = 96 B.  Round 6 (SX_KC_PITCH 96): unpadded, the two
+// k-halves swapped in rows with bit 3 set (sx_kc_off), which keeps the 32x32x16 fragment reads
+// conflict-free (ds_read_b128 lane groups {0-3, 12-15, 20-27} / {4-11, 16-19, 28-31}: the rows of
+// a group pair up by row mod 8, and each pair differs in bit 3, so the 16 reads land on 8 even and
+// 8 odd 16-B bank slots) and, with 4 consecutive rows per 16-lane group (sx_kc_unit wmap 0), the
+// 8-B staging writes too.  At 96 B a 128 x 128 workgroup's double-buffered images take 48 KB for
+// every orientation, so three workgroups share a CU's LDS (variant 8).  112 (padded, no swap) is
+// the round-5 layout, kept buildable for A/Bs.
+#ifndef SX_KC_PITCH
+#define SX_KC_PITCH 96
+#endif
+constexpr int kSxKcPitch = SX_KC_PITCH;
+static_assert(kSxKcPitch == 96 || kSxKcPitch == 112, "K-contiguous pitch: 96 (swapped halves) or 112 (padded)");
+constexpr bool kSxKcWmap = kSxKcPitch == 112;  // the parity row map is for the padded layout only
+__device__ __forceinline__ int sx_kc_off(int r, int h) {
+  return r * kSxKcPitch + 48 * (kSxKcPitch == 96 ? h ^ ((r >> 3) & 1) : h);
+}
 
 enum : int { kSxEpiNone = 0, kSxEpiGelu = 1, kSxEpiDGelu = 2 };
 
@@ -190,12 +206,12 @@ struct SxOperand {
       const int uu = on[i] ? u : 0;
       if (!KM) {
         int q, r;
-        sx_kc_unit(uu, wmap && (R / 2) % 16 == 0, r, q);
+        sx_kc_unit(uu, kSxKcWmap && wmap && (R / 2) % 16 == 0, r, q);
         const int gr = min(row0 + r, rows - 1), gr2 = min(row0 + r + R / 2, rows - 1);  // rows past the matrix: valid duplicates
         g[i] = base + int64_t(gr) * ld + k0 + 4 * q;
         g2[i] = base + int64_t(gr2) * ld + k0 + 4 * q;
-        woff[i] = r * kSxKcPitch + 48 * (q >> 1) + 8 * (q & 1);
-        woff2[i] = (r + R / 2) * kSxKcPitch + 48 * (q >> 1) + 8 * (q & 1);
+        woff[i] = sx_kc_off(r, q >> 1) + 8 * (q & 1);
+        woff2[i] = sx_kc_off(r + R / 2, q >> 1) + 8 * (q & 1);
       } else {
         const int cg = uu % (R / 4), kp = uu / (R / 4);
         const int gc = min(row0 + 4 * cg, rows - 4);
@@ -391,7 +407,7 @@ struct SxConvAOperand {
       on[i] = (kUnits % T == 0) || u < kUnits;
       const int uu = on[i] ? u : 0;
       int q, r;
-      sx_kc_unit(uu, p.wmap && (R / 2) % 16 == 0, r, q);
+      sx_kc_unit(uu, kSxKcWmap && p.wmap && (R / 2) % 16 == 0, r, q);
       q4[i] = 4 * q;
 #pragma unroll
       for (int j = 0; j < 2; ++j) {
@@ -402,8 +418,8 @@ struct SxConvAOperand {
         hb[i][j] = ho * p.cs - p.cpad;
         wb[i][j] = wo * p.cs - p.cpad;
       }
-      woff[i] = r * kSxKcPitch + 48 * (q >> 1) + 8 * (q & 1);
-      woff2[i] = (r + R / 2) * kSxKcPitch + 48 * (q >> 1) + 8 * (q & 1);
+      woff[i] = sx_kc_off(r, q >> 1) + 8 * (q & 1);
+      woff2[i] = sx_kc_off(r + R / 2, q >> 1) + 8 * (q & 1);
     }
   }
 
@@ -456,7 +472,7 @@ struct SxConvAOperand {
 template <int R, bool KM>
 __device__ __forceinline__ void sx_frag(const uint8_t* img, int r0, int lane, sx_bf16x8 (&f)[3]) {
   if (!KM) {
-    const uint8_t* p = img + (r0 + (lane & 31)) * kSxKcPitch + 48 * (lane >> 5);
+    const uint8_t* p = img + sx_kc_off(r0 + (lane & 31), lane >> 5);
 #pragma unroll
     for (int pl = 0; pl < 3; ++pl) f[pl] = *reinterpret_cast<const sx_bf16x8*>(p + 16 * pl);
   } else {

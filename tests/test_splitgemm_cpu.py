@@ -82,15 +82,21 @@ def test_choose_tiles_and_splits():
 
 
 def test_plan_variant_8_for_kmajor_b():
-    """Input / weight gradients (K-major B) plan variant 8 on 128 x 128 tiles with the same
-    split-K rules; row-major B and pinned tiles keep the default (profiles/r6/splitgemm_v8_3wg_probe.jsonl)."""
+    """Input / weight gradients (K-major B) and forwards plan variant 8 on 128 x 128 tiles with
+    the same split-K rules, except where a whole 128 x 96 round wins; pinned tiles keep the default (profiles/r6/splitgemm_v8_3wg_probe.jsonl)."""
     x = torch.zeros(64, 32)
     w = torch.zeros(32, 48)  # B [K, N] row-major: K-major (dX = dY W, dW = dY^T X)
     assert SG.plan_variant(True) == (8 if SG.USE_V8_KMAJOR_B else 0)
     assert SG.plan_variant(True, tile=7) == SG.DEFAULT_VARIANT
-    assert SG.plan_variant(False) == SG.DEFAULT_VARIANT
+    assert SG.plan_variant(False) == (8 if SG.USE_V8_FWD else 0)
     assert SG.plan(x, w)[2] == SG.plan_variant(True)
-    assert SG.plan(x, w.t().contiguous().t())[2] == SG.DEFAULT_VARIANT
+    assert SG.plan(x, w.t().contiguous().t())[2] == SG.plan_variant(False)
+    if SG.USE_V8_KMAJOR_B and SG.USE_V8_FWD and SG.USE_T7:
+        assert SG.plan_variant(True, None, 8192, 768, 768) == 0     # o input gradient: a t7 round
+        assert SG.plan_variant(False, None, 8192, 768, 768) == 0    # o forward
+        assert SG.plan_variant(True, None, 8192, 768, 2304) == 8    # qkv input gradient (split-K 2)
+        assert SG.plan_variant(False, None, 8192, 2304, 768) == 8   # qkv forward: 1152 tiles
+        assert SG.plan_variant(False, None, 8192, 3072, 768) == 8   # fc1 forward
     assert SG.choose(8192, 768, 2304, 8) == (0, 2)     # qkv input gradient: 384 tiles, no 128 x 96
     assert SG.choose(8192, 768, 3072, 8) == (0, 2)
     assert SG.choose(768, 2304, 8192, 8) == (0, 7)
@@ -101,6 +107,7 @@ def test_plan_variant_8_for_kmajor_b():
     try:
         SG.USE_V8_KMAJOR_B = False
         assert SG.plan_variant(True) == SG.DEFAULT_VARIANT
+        assert SG.plan_variant(False) == (8 if SG.USE_V8_FWD else 0)
     finally:
         SG.USE_V8_KMAJOR_B = old
 

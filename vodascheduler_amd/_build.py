@@ -105,6 +105,8 @@ def hip_compile_flags() -> list[str]:
         "-munsafe-fp-atomics",
         "-fvisibility=hidden",
         "-Wno-unused-result",
+        # extra -D options for A/B builds of a layout constant (e.g. -DSX_KC_PITCH=112)
+        *os.environ.get("VODA_HIP_DEFINES", "").split(),
     ]
 
 

@@ -59,6 +59,9 @@ USE_T7 = True  # the 128 x 96 tile in ``choose`` (A/B switch)
 # gradients 184 -> 177, 239 -> 227, 246 -> 230 us, qkv weight gradient 183 -> 176 us
 # (profiles/r6/splitgemm_v8_3wg_probe.jsonl); error still below hipBLASLt fp32's (A/B switch)
 USE_V8_KMAJOR_B = True
+# ... and the forwards (K-contiguous B) once the 96-B K-contiguous images fit three workgroups:
+# qkv / fc1 / fc2 forwards 199 -> 192, 266 -> 250, 241 -> 235 us (profiles/r6/fwd_probe_kc96.jsonl)
+USE_V8_FWD = True
 # a Linear's bias gradient summed in the weight-gradient GEMM's A staging (matmul(row_sums=...))
 # instead of a separate column-sum pass over dY (A/B switch)
 USE_FUSED_ROW_SUMS = True
@@ -246,7 +249,7 @@ def matmul(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor | None = None, ac
     if out.stride(1) != 1 or out.shape != (M, Nn):
         raise ValueError("splitgemm.matmul: out must be [M, N] with unit column stride")
     if variant is None:
-        variant = plan_variant(lb[0], tile)
+        variant = plan_variant(lb[0], tile, M, Nn, K)
     t0, s0 = choose(M, Nn, K, variant)
     tile = t0 if tile is None else tile
     splits = s0 if splits is None else splits
@@ -273,19 +276,28 @@ def matmul(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor | None = None, ac
     return out
 
 
-def plan_variant(b_kmajor: bool, tile: int | None = None) -> int:
-    """The math / kernel variant ``matmul`` runs when the caller does not pin one: variant 8 for a
-    K-major B on the default tiles (``USE_V8_KMAJOR_B``), else ``DEFAULT_VARIANT``."""
-    if USE_V8_KMAJOR_B and b_kmajor and tile is None and DEFAULT_VARIANT == 0:
-        return 8
-    return DEFAULT_VARIANT
+def plan_variant(b_kmajor: bool, tile: int | None = None, M: int = 0, Nn: int = 0, K: int = 0) -> int:
+    """The math / kernel variant ``matmul`` runs when the caller does not pin one: variant 8 (one
+    accumulator, three workgroups per CU) for K-major B operands (``USE_V8_KMAJOR_B``) and, since
+    the 96-B K-contiguous LDS layout lets three workgroups fit, for K-contiguous ones too
+    (``USE_V8_FWD``); else ``DEFAULT_VARIANT``.  Shapes whose variant-0 plan is a whole round of
+    128 x 96 tiles stay there when variant 8 would leave its 768-workgroup round half empty
+    (BERT-base o forward / input gradient: 73 vs 78-81 us, profiles/r6/splitgemm_v8_3wg_probe.jsonl)."""
+    if tile is not None or DEFAULT_VARIANT != 0 or not (USE_V8_KMAJOR_B if b_kmajor else USE_V8_FWD):
+        return DEFAULT_VARIANT
+    if M and choose(M, Nn, K, 0)[0] == 7:
+        t, sp = choose(M, Nn, K, 8)
+        if -(-M // 128) * -(-Nn // 128) * sp < 768:
+            return DEFAULT_VARIANT
+    return 8
 
 
 def plan(a: torch.Tensor, b: torch.Tensor) -> tuple[int, int, int]:
     """(tile, splits, variant) ``matmul(a, b)`` picks for these operands."""
     lb = _layout(b, False)
-    v = plan_variant(bool(lb and lb[0]))
-    t, sp = choose(a.shape[0], b.shape[1], a.shape[1], v)
+    M, K, Nn = a.shape[0], a.shape[1], b.shape[1]
+    v = plan_variant(bool(lb and lb[0]), None, M, Nn, K)
+    t, sp = choose(M, Nn, K, v)
     return t, sp, v
 
 
