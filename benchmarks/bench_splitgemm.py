@@ -78,6 +78,7 @@ def main() -> None:
     ap.add_argument("--no-sweep", action="store_true", help="no tile / split sweep")
     ap.add_argument("--variant-splits", action="store_true", help="sweep split-K for the --variants too")
     ap.add_argument("--no-err", action="store_true", help="timing only")
+    ap.add_argument("--split-list", default="1,2,3,4,8,16", help="split-K counts of --variant-splits")
     ap.add_argument("--stagger-ab", action="store_true", help="also time the default without the WG stagger")
     args = ap.parse_args()
     dev = torch.device("cuda", 0)
@@ -97,13 +98,13 @@ def main() -> None:
             Mo, Ko = a.shape
             No = b.shape[1]
             flops = 2.0 * Mo * No * Ko
-            t0, s0 = SG.choose(Mo, No, Ko)
-            cands = {"hipblaslt": None, f"split_t{t0}_s{s0}": (t0, s0, 0)}
+            t0, s0, v0 = SG.plan(a, b)
+            cands = {"hipblaslt": None, f"plan_t{t0}_s{s0}_v{v0}": (t0, s0, v0)}
             for v in [int(x) for x in args.variants.split(",") if x]:
                 cands[f"var{v}_t0_s{s0}"] = (0, s0, v)
                 if args.variant_splits:
                     tiles = -(-Mo // 128) * -(-No // 128)
-                    for s in (1, 2, 3, 4, 8, 16):
+                    for s in [int(x) for x in args.split_list.split(",")]:
                         if tiles * s <= 4096 and s * 64 <= Ko:
                             cands.setdefault(f"var{v}_t0_s{s}", (0, s, v))
             if args.stagger_ab:
