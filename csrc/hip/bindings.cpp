@@ -28,6 +28,7 @@ PYBIND11_MODULE(_vodahip, m) {
   m.def("sgemm_f32", &sgemm_f32);
   m.def("sgemm_f32_set_stagger", &sgemm_f32_set_stagger);
   m.def("sgemm_conv_wgrad_set_ws", &sgemm_conv_wgrad_set_ws);
+  m.def("sgemm_conv_fwd_set_v8", &sgemm_conv_fwd_set_v8);
   m.def("sgemm_set_reduce_groups", &sgemm_set_reduce_groups);
   m.def("sgemm_set_write_map", &sgemm_set_write_map);
   m.def("sgemm_conv_fwd_f32", &sgemm_conv_fwd_f32);

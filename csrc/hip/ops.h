@@ -271,6 +271,7 @@ class RcclComm {
 int64_t sgemm_f32_workspace_floats(int M, int N, int splits);
 void sgemm_f32_set_stagger(int on);
 void sgemm_conv_wgrad_set_ws(int mode);
+void sgemm_conv_fwd_set_v8(int on);
 void sgemm_set_reduce_groups(int g);
 void sgemm_set_write_map(int on);
 void sgemm_conv_fwd_f32(uintptr_t x, uintptr_t w, uintptr_t y, int n, int H, int W, int Cin, int Ho, int Wo, int Cout,

@@ -102,6 +102,7 @@ int g_sx_wmap = 1;  // conflict-free K-contiguous staging writes (sx_kc_unit)
 // convolution weight gradient kernel: 0 one-role, 1 / 2 wave-specialised (lead 1 / 2), 3 one-role
 // with one accumulator at three workgroups per CU
 int g_sx_conv_ws = 0;
+int g_sx_conv_fwd_v8 = 0;  // convolution forward: 1 = one accumulator at three workgroups per CU
 
 // K-major images of R = 96 columns use the R = 128 layout (192-byte k-rows padded to 256 B)
 template <int R> struct SxKmPitch { static constexpr int kR = R == 96 ? 128 : R == 192 ? 256 : R; };
@@ -997,6 +998,7 @@ constexpr int kSxTileN[8] = {128, 128, 256, 128, 128, 256, 64, 96};
 
 void sgemm_f32_set_stagger(int on) { g_sx_stagger = on ? 1 : 0; }
 void sgemm_set_write_map(int on) { g_sx_wmap = on ? 1 : 0; }
+void sgemm_conv_fwd_set_v8(int on) { g_sx_conv_fwd_v8 = on ? 1 : 0; }
 void sgemm_conv_wgrad_set_ws(int mode) { g_sx_conv_ws = mode < 0 || mode > 3 ? 0 : mode; }
 void sgemm_set_reduce_groups(int g) { g_sx_reduce_groups = (g == 1 || g == 2 || g == 4 || g == 8 || g == 16) ? g : -1; }
 
@@ -1179,8 +1181,12 @@ void sgemm_conv_fwd_f32(uintptr_t x, uintptr_t w, uintptr_t y, int n, int H, int
   p.tiles = int((M + 127) / 128) * p.tiles_n;
   p.stagger = g_sx_stagger;
   p.wmap = g_sx_wmap;
-  hipLaunchKernelGGL((sgemm_bf16x3_kernel<128, 128, false, false, 6, true, false, 2, 2, false, 0, true>),
-                     dim3(unsigned(p.tiles)), dim3(256), 0, as_stream(stream), p);
+  if (g_sx_conv_fwd_v8)  // one accumulator at three workgroups per CU (as GEMM variant 8)
+    hipLaunchKernelGGL((sgemm_bf16x3_kernel<128, 128, false, false, 6, false, false, 3, 2, false, 0, true>),
+                       dim3(unsigned(p.tiles)), dim3(256), 0, as_stream(stream), p);
+  else
+    hipLaunchKernelGGL((sgemm_bf16x3_kernel<128, 128, false, false, 6, true, false, 2, 2, false, 0, true>),
+                       dim3(unsigned(p.tiles)), dim3(256), 0, as_stream(stream), p);
   check_launch();
 }
 

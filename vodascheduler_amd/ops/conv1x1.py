@@ -78,7 +78,9 @@ BLAS_WGRAD_F32_MIN_OUT = 1 << 20
 # the step uses the shipped tuned hipBLASLt solutions and still loses: 60.85 -> 61.97 ms (same-box
 # A/B, profiles/r6/ab_split_1x1_v1_resnet50_fp32.jsonl).  Stays off.
 USE_SPLIT_GEMM_F32 = False
-SPLIT_VARIANT = 1
+# None: the split GEMM's own plan (variant 8, three workgroups per CU, since the 96-B K-contiguous
+# layout; variant 1 before)
+SPLIT_VARIANT = None
 # ... but the FORWARDS with K >= 512 input channels alone do win: a per-call rocprof of the step with
 # every library 1x1 GEMM on the split kernel (profiles/r6/rocprof_resnet50_fp32_split_1x1_calls.md)
 # has the ten K >= 512 forwards 0-10 % faster than the tuned hipBLASLt solutions (-160 us per

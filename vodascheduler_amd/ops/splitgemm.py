@@ -53,6 +53,8 @@ CONV_WGRAD_WS = 0
 # 3x3 convolution weight gradients on the 128 x 128 tile with one accumulator at three workgroups
 # per CU (the conv-gather image of variant 8; A/B switch)
 CONV_WGRAD_V8 = True
+# the implicit-GEMM convolution forward (ResNet's stride-2 3x3 layers) in the same form (A/B switch)
+CONV_FWD_V8 = True
 USE_T7 = True  # the 128 x 96 tile in ``choose`` (A/B switch)
 # GEMMs whose B operand is K-major (input and weight gradients) on variant 8: one accumulator at
 # three workgroups per CU (K-major B images leave room for three in LDS); qkv / fc1 / fc2 input
@@ -407,6 +409,7 @@ def conv_fwd(x: torch.Tensor, w: torch.Tensor, stride: int, padding: int) -> tor
     wo = (W + 2 * padding - kw) // stride + 1
     y = torch.empty((n, cout, ho, wo), dtype=torch.float32, device=x.device, memory_format=torch.channels_last)
     _sync_knobs(N.hip())
+    N.hip().sgemm_conv_fwd_set_v8(int(CONV_FWD_V8))
     N.hip().sgemm_conv_fwd_f32(x.data_ptr(), w.data_ptr(), y.data_ptr(), n, H, W, cin, ho, wo, cout, kh, kw,
                                int(stride), int(padding), N.stream_of(x))
     return y
