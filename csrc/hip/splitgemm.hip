@@ -1220,7 +1220,11 @@ void sgemm_conv_dgrad_s2_class(uintptr_t dy, uintptr_t wc, uintptr_t dx, int n, 
   p.tiles = int((M + 127) / 128) * p.tiles_n;
   p.stagger = g_sx_stagger;
   p.wmap = g_sx_wmap;
-  hipLaunchKernelGGL((sgemm_bf16x3_kernel<128, 128, false, true, 6, true, false, 2, 2, false, 0, true>),
+  if (g_sx_conv_fwd_v8)  // as the forward: one accumulator at three workgroups per CU
+    hipLaunchKernelGGL((sgemm_bf16x3_kernel<128, 128, false, true, 6, false, false, 3, 2, false, 0, true>),
+                     dim3(unsigned(p.tiles)), dim3(256), 0, as_stream(stream), p);
+  else
+    hipLaunchKernelGGL((sgemm_bf16x3_kernel<128, 128, false, true, 6, true, false, 2, 2, false, 0, true>),
                      dim3(unsigned(p.tiles)), dim3(256), 0, as_stream(stream), p);
   check_launch();
 }

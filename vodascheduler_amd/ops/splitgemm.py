@@ -53,7 +53,8 @@ CONV_WGRAD_WS = 0
 # 3x3 convolution weight gradients on the 128 x 128 tile with one accumulator at three workgroups
 # per CU (the conv-gather image of variant 8; A/B switch)
 CONV_WGRAD_V8 = True
-# the implicit-GEMM convolution forward (ResNet's stride-2 3x3 layers) in the same form (A/B switch)
+# the implicit-GEMM convolution forward (ResNet's stride-2 3x3 layers) and the polyphase input
+# gradient's class GEMMs in the same form (A/B switch)
 CONV_FWD_V8 = True
 USE_T7 = True  # the 128 x 96 tile in ``choose`` (A/B switch)
 # GEMMs whose B operand is K-major (input and weight gradients) on variant 8: one accumulator at
@@ -448,6 +449,7 @@ def conv_dgrad_s2(dy: torch.Tensor, w: torch.Tensor, in_shape) -> torch.Tensor:
     wt = w.permute(2, 3, 0, 1)  # [kh][kw][co][ci] view
     h = N.hip()
     _sync_knobs(h)
+    h.sgemm_conv_fwd_set_v8(int(CONV_FWD_V8))  # the class GEMMs take the forward's kernel form
     st = N.stream_of(dy)
     for ph in (0, 1):
         for pw in (0, 1):
