@@ -1,6 +1,7 @@
 """Split-K count sweep of ResNet-50 bs256 fp32 weight gradients on the split-bf16 kernel: the 1x1
 layers (dW = dY^T X over the pixels, tiles as ops/conv1x1 picks them) and the 3x3 implicit-GEMM
-ones (C >= 128), at 0.25 / 0.375 / 0.5 / 0.75 / 1 x the round-6 split count (~1024 workgroups).  us per (shape, splits).
+ones (C >= 128), at 0.25 / 0.375 / 0.5 / 0.75 / 1 x (or --factors) the shipped split count, in the
+shipped kernel forms (variant 8 / conv mode 3 on 128 x 128 tiles).  us per (shape, splits).
 
     python benchmarks/probe_resnet_wgrad_splits.py [--out gpurun_out/rwsplits.jsonl]
 """
@@ -16,7 +17,10 @@ import torch
 
 sys.path.insert(0, os.path.join(os.path.dirname(__file__), ".."))
 from benchmarks.bench_splitgemm import timeit  # noqa: E402
+from vodascheduler_amd.ops import conv1x1 as C1  # noqa: E402
 from vodascheduler_amd.ops import splitgemm as SG  # noqa: E402
+
+FACTORS = (0.25, 0.375, 0.5, 0.75, 1.0)
 
 ONE = [(64, 256, 802816), (256, 64, 802816), (128, 256, 802816), (512, 128, 200704), (128, 512, 200704),
        (1024, 256, 50176), (256, 1024, 50176), (2048, 512, 12544), (512, 2048, 12544)]
@@ -27,7 +31,11 @@ THREE = [(128, 28, 1, 28), (256, 14, 1, 14), (512, 7, 1, 7), (128, 28, 2, 56), (
 def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--out", default="")
+    ap.add_argument("--factors", default="", help="comma list of multiples of the shipped split count")
     args = ap.parse_args()
+    global FACTORS
+    if args.factors:
+        FACTORS = tuple(float(f) for f in args.factors.split(","))
     dev = torch.device("cuda", 0)
     sink = open(args.out, "a") if args.out else None
 
@@ -41,9 +49,11 @@ def main() -> None:
         x = torch.randn(m, cin, device=dev)
         g = torch.zeros(cout, cin, device=dev)
         tile = SG.thin_tile(cout, cin)
-        s0 = SG.conv_wgrad_splits(cout, cin, m, tile)
-        ss = sorted({max(1, int(s0 * f)) for f in (0.25, 0.375, 0.5, 0.75, 1.0)})
-        fns = {s: (lambda s=s: SG.matmul(dy.t(), x, out=g, accumulate=True, tile=tile, splits=s)) for s in ss}
+        s0 = SG.conv_wgrad_splits(cout, cin, m, tile, C1.WGRAD_TARGET_WG)
+        ss = sorted({max(1, int(s0 * f)) for f in FACTORS})
+        v = 8 if C1.WGRAD_V8 and tile == 0 else None
+        fns = {s: (lambda s=s: SG.matmul(dy.t(), x, out=g, accumulate=True, tile=tile, splits=s, variant=v))
+               for s in ss}
         for f in fns.values():
             f()
         torch.cuda.synchronize()
@@ -59,7 +69,7 @@ def main() -> None:
         dy = torch.randn(256, c, ho, ho, device=dev).contiguous(memory_format=cl)
         gw = torch.zeros(c, c, 3, 3, device=dev).contiguous(memory_format=cl)
         s0 = SG.conv_wgrad_splits(c, 9 * c, 256 * ho * ho)
-        ss = sorted({max(1, int(s0 * f)) for f in (0.25, 0.375, 0.5, 0.75, 1.0)})
+        ss = sorted({max(1, int(s0 * f)) for f in FACTORS})
         fns = {s: (lambda s=s: SG.conv_wgrad_(dy, x, gw, stride, 1, splits=s)) for s in ss}
         for f in fns.values():
             f()

@@ -53,6 +53,9 @@ CONV_WGRAD_WS = 0
 # 3x3 convolution weight gradients on the 128 x 128 tile with one accumulator at three workgroups
 # per CU (the conv-gather image of variant 8; A/B switch)
 CONV_WGRAD_V8 = True
+# ... split-K towards two rounds of its 768 resident workgroups (1536) instead of 1024: C = 128 /
+# 256 / 512 layers 388 -> 374, 379 -> 372, 395 -> 393 us (profiles/r6/resnet50_wgrad_splits_v8_probe.jsonl)
+CONV_WGRAD_V8_ROUNDS = True
 # the implicit-GEMM convolution forward (ResNet's stride-2 3x3 layers) and the polyphase input
 # gradient's class GEMMs in the same form (A/B switch)
 CONV_FWD_V8 = True
@@ -374,10 +377,12 @@ def conv_wgrad_(dy: torch.Tensor, x: torch.Tensor, gw: torch.Tensor, stride: int
     cout, _, kh, kw = gw.shape
     ho, wo = dy.shape[2], dy.shape[3]
     tile = conv_wgrad_tile(cout, kh * kw * cin) if tile is None else tile
-    s = conv_wgrad_splits(cout, kh * kw * cin, n * ho * wo, tile) if splits is None else splits
+    v8 = CONV_WGRAD_V8 and CONV_WGRAD_WS == 0 and tile == 0
+    target = 1536 if v8 and CONV_WGRAD_V8_ROUNDS else 1024
+    s = conv_wgrad_splits(cout, kh * kw * cin, n * ho * wo, tile, target) if splits is None else splits
     h = N.hip()
     _sync_knobs(h)
-    h.sgemm_conv_wgrad_set_ws(3 if CONV_WGRAD_V8 and CONV_WGRAD_WS == 0 and tile == 0 else CONV_WGRAD_WS)
+    h.sgemm_conv_wgrad_set_ws(3 if v8 else CONV_WGRAD_WS)
     ws_floats = h.sgemm_f32_workspace_floats(cout, kh * kw * cin, s)
     ws = _workspace(dy.device, ws_floats) if ws_floats else None
     h.sgemm_conv_wgrad_f32(dy.data_ptr(), x.data_ptr(), gw.data_ptr(), n, H, W, cin, ho, wo, cout, kh, kw,
