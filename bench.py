@@ -336,9 +336,13 @@ def gemm_math(precision: str, device: str) -> str:
 
     if not splitgemm.ENABLED:
         return "fp32: f32 MFMA (own kernels, hipBLASLt, MIOpen)"
-    return ("fp32 accuracy: Linear / FFN GEMMs as an exact 3-way bf16 split of each fp32 operand, "
-            f"6 cross products on the bf16 MFMA, fp32 accumulate ({splitgemm.GEMM_MATH}, csrc/hip/splitgemm.hip); "
-            "convolutions on f32 MFMA (own Winograd / 1x1 kernels, hipBLASLt, MIOpen)")
+    names = sorted({splitgemm.GEMM_MATH} | ({splitgemm.VARIANT_NAMES[8]} if splitgemm.USE_V8_KMAJOR_B
+                                            or splitgemm.USE_V8_FWD else set()))
+    return ("fp32 accuracy: Linear / FFN GEMMs, 3x3 weight gradients, stride-2 3x3 forwards, 1x1 weight "
+            "gradients and the Winograd tile GEMMs as an exact 3-way bf16 split of each fp32 operand, "
+            f"6 cross products on the bf16 MFMA, fp32 accumulate ({' / '.join(names)}, csrc/hip/splitgemm.hip, "
+            "winograd_f32.hip); 1x1 forwards / input gradients on f32 MFMA (own kernels with BN epilogues, "
+            "hipBLASLt), stride-2 3x3 input gradients on MIOpen")
 
 
 def main():
