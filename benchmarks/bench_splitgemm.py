@@ -108,7 +108,7 @@ def main() -> None:
                         if tiles * s <= 4096 and s * 64 <= Ko:
                             cands.setdefault(f"var{v}_t0_s{s}", (0, s, v))
             if args.stagger_ab:
-                cands[f"nostag_t{t0}_s{s0}"] = (t0, s0, 0, 0)
+                cands[f"nostag_t{t0}_s{s0}_v{v0}"] = (t0, s0, v0, 0)
             if not args.quick and not args.no_sweep:
                 tiles = -(-Mo // 128) * -(-No // 96)
                 for tile in (0, 1, 2, 3, 4, 7):
