@@ -230,14 +230,15 @@ PROFILES = {
 
 # fp32 compute (the reference's precision: tensorflow2_keras_cifar_elastic.py:147-166 builds
 # the Keras model with no mixed-precision policy; pytorch_mnist_elastic.py is plain fp32):
-# MI355X single-GPU step times, same batches.  ResNet-50 58.75 ms / BERT-base 33.53 ms at the end of
-# round 6 (bench.py warm-up, ``warmup_single_gpu_step_ms`` of profiles/r6/bench_n1_fp32_r6i.json;
-# 63.18 / 35.59 early in round 6, r6a; round 4 ended at 69.96 / 37.1, BENCH_r04); the other models'
-# fp32 step times are unmeasured, so they fall back to the bf16 profile.
+# MI355X single-GPU step times, same batches.  ResNet-50 58.16 ms / BERT-base 31.68 ms at the end of
+# round 6 (bench.py warm-up, ``warmup_single_gpu_step_ms`` of profiles/r6/bench_n1_fp32_r6z.json;
+# 58.75 / 33.53 before the variant-8 split GEMM, r6i; 63.18 / 35.59 early in round 6, r6a; round 4
+# ended at 69.96 / 37.1, BENCH_r04); the other models' fp32 step times are unmeasured, so they fall
+# back to the bf16 profile.
 PROFILES_FP32 = {
-    "resnet50": ModelProfile("resnet50", alpha=0.01, step_time_1gpu=0.05875, grad_mb=102.2, measured=True,
+    "resnet50": ModelProfile("resnet50", alpha=0.01, step_time_1gpu=0.05816, grad_mb=102.2, measured=True,
                              precision="fp32"),
-    "bert-base": ModelProfile("bert-base", alpha=0.05, step_time_1gpu=0.03353, grad_mb=438.0, measured=True,
+    "bert-base": ModelProfile("bert-base", alpha=0.05, step_time_1gpu=0.03168, grad_mb=438.0, measured=True,
                               precision="fp32"),
 }
 PRECISIONS = ("bf16", "fp32")
