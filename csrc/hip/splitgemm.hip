@@ -1025,7 +1025,8 @@ void sgemm_f32(uintptr_t a, int64_t lda, bool a_kmajor, uintptr_t b, int64_t ldb
   VODA_CHECK(K % kSxBK == 0, "sgemm_f32: K must be a multiple of 16");
   VODA_CHECK(M % 4 == 0 && N % 4 == 0, "sgemm_f32: M and N must be multiples of 4");
   VODA_CHECK(tile >= 0 && tile < 8, "sgemm_f32: bad tile id");
-  VODA_CHECK(variant >= 0 && variant <= 8 && (variant == 0 || tile == 0), "sgemm_f32: bad math variant");
+  VODA_CHECK(variant >= 0 && variant <= 8 && (variant == 0 || tile == 0 || (variant == 8 && tile == 7)),
+             "sgemm_f32: bad math variant");
   VODA_CHECK(epi >= kSxEpiNone && epi <= kSxEpiDGelu && (epi == kSxEpiNone || aux != 0), "sgemm_f32: bad epilogue");
   VODA_CHECK(a % 16 == 0 && b % 16 == 0 && lda % 4 == 0 && ldb % 4 == 0, "sgemm_f32: operands need 16-B rows");
   VODA_CHECK(lda >= (a_kmajor ? M : K) && ldb >= (b_kmajor ? N : K) && ldc >= N, "sgemm_f32: leading dims");
@@ -1075,7 +1076,10 @@ void sgemm_f32(uintptr_t a, int64_t lda, bool a_kmajor, uintptr_t b, int64_t ldb
     sx_launch_tile<128, 256, 6, true, false>(p, a_kmajor, b_kmajor, grid, st);
   } else if (tile == 7) {  // 128 x 96 (4 waves of 32 x 96): N = 768 outputs as 8 column tiles, so
                            // 8192 x 768 runs 512 workgroups (two per CU) instead of 384
-    sx_launch_tile<128, 96, 6, true, false, 2, 1, 0, 3>(p, a_kmajor, b_kmajor, grid, st);
+    if (variant == 8)  // one accumulator at three workgroups per CU (43 KB of LDS each)
+      sx_launch_tile<128, 96, 6, false, false, 3, 1, 0, 3>(p, a_kmajor, b_kmajor, grid, st);
+    else
+      sx_launch_tile<128, 96, 6, true, false, 2, 1, 0, 3>(p, a_kmajor, b_kmajor, grid, st);
   } else if (tile == 5) {  // 64 x 256 (4 waves along N): outputs with 64 rows (no half-empty tiles)
     sx_launch_tile<64, 256, 6, true, false>(p, a_kmajor, b_kmajor, grid, st);
   } else if (tile == 6) {  // 256 x 64 (4 waves along M): outputs with 64 columns

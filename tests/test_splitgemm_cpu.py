@@ -98,6 +98,8 @@ def test_plan_variant_8_for_kmajor_b():
         assert SG.plan_variant(False, None, 8192, 2304, 768) == 8   # qkv forward: 1152 tiles
         assert SG.plan_variant(False, None, 8192, 3072, 768) == 8   # fc1 forward
     assert SG.choose(8192, 768, 2304, 8) == (0, 2)     # qkv input gradient: 384 tiles, no 128 x 96
+    assert SG.choose(8192, 2304, 768, 8) == ((7, 1) if SG.USE_T7_V8 else (0, 1))  # qkv forward: 2 rounds
+    assert SG.choose(8192, 3072, 768, 8) == (0, 1)     # fc1 forward: 1536 tiles fill 2 rounds already
     assert SG.choose(8192, 768, 3072, 8) == (0, 2)
     assert SG.choose(768, 2304, 8192, 8) == (0, 7)
     assert SG.choose(768, 768, 8192, 8) == (0, 12)

@@ -120,8 +120,8 @@ def test_no_worse_than_hipblaslt_wide_magnitudes():
 
 @pytest.mark.parametrize("tile", [None, 7])
 def test_epilogues_bias_accumulate_gelu_dgelu(tile, monkeypatch):
-    """Epilogues on the planned launch (variant 8 for the K-major weights of x @ W^T) and on
-    tile 7 (variant 0)."""
+    """Epilogues on the planned launch (variant 8) and on tile 7 (variant 8 where planned, the
+    dual form for the pinned-variant calls)."""
     if tile is not None:  # route every call of this test to the given tile
         monkeypatch.setattr(SG, "choose", lambda M, N, K, variant=0: (tile, 1))
     torch.manual_seed(9)
@@ -132,7 +132,7 @@ def test_epilogues_bias_accumulate_gelu_dgelu(tile, monkeypatch):
     ref = x.double() @ w.double().t()
     bd = _bound(x, w.t())
     # bias
-    tol = 4e-7 if tile is None and SG.plan(x, w.t())[2] == 8 else 2e-7  # 8: one accumulator
+    tol = 4e-7 if SG.plan(x, w.t())[2] == 8 else 2e-7  # 8: one accumulator
     y = SG.matmul(x, w.t(), bias=bias)
     assert ((y.double() - ref - bias.double()).abs() / (bd + 1)).max().item() < tol
     # accumulate into an existing output (beta = 1), split-K path too
@@ -154,6 +154,26 @@ def test_epilogues_bias_accumulate_gelu_dgelu(tile, monkeypatch):
     d = SG.matmul(dy, w, epi=SG.EPI_DGELU, aux=hh)
     dref = (dy.double() @ w.double()) * gelu_tanh_grad_ref(hh.double())
     assert ((d.double() - dref).abs() / (_bound(dy, w) + 1)).max().item() < 1e-5
+
+
+@pytest.mark.parametrize("akm", [False, True])
+@pytest.mark.parametrize("bkm", [False, True])
+def test_tile7_variant8_orientations_epilogue(akm, bkm):
+    """Variant 8 on 128 x 96 tiles (one accumulator, three workgroups per CU): every operand
+    orientation, ragged M / N, bias + GELU epilogue, against fp64."""
+    torch.manual_seed(11 + 2 * akm + bkm)
+    M, K, N = 324, 208, 196
+    a = torch.randn(M, K, device=DEV)
+    b = torch.randn(K, N, device=DEV) * 0.1
+    av = a.t().contiguous().t() if akm else a
+    bv = b if bkm else b.t().contiguous().t()
+    bias = torch.randn(N, device=DEV)
+    h = torch.empty(M, N, device=DEV)
+    g = SG.matmul(av, bv, bias=bias, epi=SG.EPI_GELU, aux=h, tile=7, splits=1, variant=8)
+    ref = a.double() @ b.double() + bias.double()
+    assert ((h.double() - ref).abs() / (_bound(a, b) + 1)).max().item() < 4e-7
+    gref = torch.nn.functional.gelu(ref, approximate="tanh")
+    assert (g.double() - gref).abs().max().item() < 1e-5
 
 
 def test_variants_error_ordering():
@@ -243,7 +263,8 @@ def test_conv_dgrad_stride2_polyphase_matches_fp64(n, cin, cout, hw, v8, monkeyp
 @pytest.mark.parametrize("M,K,N,splits,tile,variant", [(768, 8192, 768, 12, 0, 0), (2304, 8192, 768, 7, 0, 0),
                                                        (260, 1024, 196, 1, 0, 0), (256, 4096, 192, 3, 7, 0),
                                                        (128, 64, 128, 1, 0, 0), (2304, 8192, 768, 7, 0, 8),
-                                                       (260, 1024, 196, 1, 0, 8), (768, 4096, 260, 12, 0, 8)])
+                                                       (260, 1024, 196, 1, 0, 8), (768, 4096, 260, 12, 0, 8),
+                                                       (256, 4096, 192, 3, 7, 8)])
 def test_fused_row_sums(M, K, N, splits, tile, variant):
     """row_sums += a.sum(1) from the A staging of a weight-gradient GEMM (K-major a = dY^T), with
     and without split-K, ragged M, next to the accumulated product."""

@@ -68,6 +68,10 @@ USE_V8_KMAJOR_B = True
 # ... and the forwards (K-contiguous B) once the 96-B K-contiguous images fit three workgroups:
 # qkv / fc1 / fc2 forwards 199 -> 192, 266 -> 250, 241 -> 235 us (profiles/r6/fwd_probe_kc96.jsonl)
 USE_V8_FWD = True
+# ... with 128 x 96 tiles where those fill whole rounds of 768 and 128 x 128 ones do not: the
+# qkv forward ran 189.7 vs 188.9 us and the step tied (32.11 / 32.11 ms, profiles/r6/
+# ab_t7_v8_bert_fp32.jsonl), so off; the tile-7 variant-8 image stays tested (A/B switch)
+USE_T7_V8 = False
 # a Linear's bias gradient summed in the weight-gradient GEMM's A staging (matmul(row_sums=...))
 # instead of a separate column-sum pass over dY (A/B switch)
 USE_FUSED_ROW_SUMS = True
@@ -169,6 +173,16 @@ def choose(M: int, Nn: int, K: int, variant: int = 0) -> tuple[int, int]:
     shapes serve every math variant (``variant`` is accepted for call-site symmetry)."""
     tiles = -(-M // 128) * -(-Nn // 128)
     if variant == 8:  # three workgroups per CU: 128 x 128 tiles, splits as below
+        if USE_T7_V8 and Nn % 96 == 0 and K <= 2304 and M >= 4096 and tiles >= 1024:
+            # 128 x 96 where it fills whole rounds of the 768 resident workgroups and 128 x 128
+            # does not (BERT-base qkv forward: 1536 vs 1152 tiles)
+            t7 = -(-M // 128) * (Nn // 96)
+
+            def fill3(t: int) -> float:
+                return t / (-(-t // 768) * 768)
+
+            if fill3(t7) > 1.05 * fill3(tiles):
+                return 7, 1
         if tiles >= 1024:
             return 0, 1
         if tiles >= 384:
@@ -259,7 +273,7 @@ def matmul(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor | None = None, ac
     t0, s0 = choose(M, Nn, K, variant)
     tile = t0 if tile is None else tile
     splits = s0 if splits is None else splits
-    if variant == 8 and tile != 0:  # variant 8 exists on the 128 x 128 tile only
+    if variant == 8 and tile not in (0, 7):  # variant 8 exists on the 128 x 128 / 128 x 96 tiles
         variant = DEFAULT_VARIANT
     if row_sums is not None and not row_sums_ok(a, row_sums, tile, variant):
         raise ValueError("splitgemm.matmul: row_sums need a K-major a, tile 0 / 7, variant 0 / 8 and an aligned fp32 [M]")
@@ -309,13 +323,13 @@ def plan(a: torch.Tensor, b: torch.Tensor) -> tuple[int, int, int]:
 
 def row_sums_ok(a: torch.Tensor, row_sums: torch.Tensor, tile: int, variant: int) -> bool:
     """Can ``matmul`` fuse ``row_sums += a.sum(1)`` on this launch shape?  K-major a (a weight
-    gradient's dY^T), tile 0 or 7 on math variant 0 or tile 0 on variant 8, a contiguous
+    gradient's dY^T), tile 0 or 7, math variant 0 or 8, a contiguous
     16-byte-aligned fp32 [M] target."""
     if not USE_FUSED_ROW_SUMS or not a.is_cuda:
         return False
     la = _layout(a, True)
     M = a.shape[0]
-    shape_ok = tile in (0, 7) if variant == 0 else (variant == 8 and tile == 0)
+    shape_ok = tile in (0, 7) and variant in (0, 8)
     return (la is not None and la[0] and shape_ok and row_sums.dtype == torch.float32
             and row_sums.is_cuda and row_sums.dim() == 1 and row_sums.numel() == M and row_sums.is_contiguous()
             and row_sums.data_ptr() % 16 == 0)
