@@ -80,7 +80,9 @@ USE_FUSED_ROW_SUMS = True
 REDUCE_GROUPS = -1
 REDUCE_GROUPS_AUTO = True  # False: one group (A/B switch)
 # K-contiguous operands staged with a row map whose 8-byte LDS writes hit 32 distinct banks per
-# 16-lane group (csrc/hip/splitgemm.hip sx_kc_unit; False: consecutive rows, 2-way conflicts)
+# 16-lane group (csrc/hip/splitgemm.hip sx_kc_unit; False: consecutive rows, 2-way conflicts).
+# Applies to the padded 112-B layout only (-DSX_KC_PITCH=112); the shipped 96-B layout's
+# consecutive-row staging is the conflict-free one, and the kernel ignores this switch there.
 WRITE_MAP = True
 _applied = {"reduce_groups": None, "write_map": None}
 
